@@ -1,0 +1,22 @@
+"""SSIM on the HIP path (DSGAN/MS_SSIM.py:95-150 interface).
+
+``ssim(X, Y, data_range, size_average=True)`` with the default 11-tap sigma-1.5 gaussian runs
+the fused SSIM kernel (forward + analytic backward w.r.t. Y).  The multi-scale ``ms_ssim`` is
+not on the training path and is not provided by this round's build.
+"""
+from dsgan_hip import functional as HF
+
+
+def ssim(X, Y, data_range=255, size_average=True, win_size=11, win_sigma=1.5, win=None,
+         K=(0.01, 0.03), nonnegative_ssim=False):
+    if X.shape != Y.shape:
+        raise ValueError(f"Input images should have the same dimensions, but got {X.shape} and {Y.shape}.")
+    if X.dim() != 4:
+        raise ValueError("HIP ssim supports 4-d (N,C,H,W) tensors")
+    if win is not None or win_size != 11 or win_sigma != 1.5 or tuple(K) != (0.01, 0.03):
+        raise NotImplementedError("HIP ssim implements the default window (11, 1.5) and K=(0.01, 0.03)")
+    if not size_average or nonnegative_ssim:
+        raise NotImplementedError("HIP ssim implements size_average=True without relu")
+    if X.requires_grad:
+        raise NotImplementedError("HIP ssim differentiates w.r.t. Y only (the generated image)")
+    return HF.ssim_affine(X, Y, 1.0, 0.0, float(data_range))

@@ -1,0 +1,74 @@
+"""Build libdsgan_hip.so in-tree: hipcc --offload-arch=gfx950, one object per source, then link.
+
+    python ds-gan_amd/build_lib.py [-j N] [--force]
+
+The library lands at ds-gan_amd/dsgan_hip/libdsgan_hip.so (git-ignored, but it travels to the
+GPU box with the gpurun snapshot).  Objects are rebuilt only when a source or header is newer.
+"""
+import argparse
+import concurrent.futures as cf
+import glob
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(HERE, "csrc")
+OUT_DIR = os.path.join(HERE, "dsgan_hip")
+OBJ_DIR = os.path.join(HERE, "build", "obj")
+LIB = os.path.join(OUT_DIR, "libdsgan_hip.so")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = "gfx950"
+FLAGS = ["-O3", "-fPIC", "-std=c++17", "--offload-arch=" + ARCH, "-munsafe-fp-atomics",
+         "-Wno-unused-result", "-I" + CSRC]
+
+
+def _newer(src, obj, headers):
+    if not os.path.exists(obj):
+        return True
+    t = os.path.getmtime(obj)
+    return os.path.getmtime(src) > t or any(os.path.getmtime(h) > t for h in headers)
+
+
+def _compile(src, obj):
+    cmd = [HIPCC] + FLAGS + ["-c", src, "-o", obj]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError("compile failed: %s\n%s\n%s" % (" ".join(cmd), r.stdout, r.stderr))
+    return obj
+
+
+def build(jobs=8, force=False, verbose=True):
+    os.makedirs(OBJ_DIR, exist_ok=True)
+    os.makedirs(OUT_DIR, exist_ok=True)
+    headers = glob.glob(os.path.join(CSRC, "*.h"))
+    srcs = sorted(glob.glob(os.path.join(CSRC, "*.hip")) + glob.glob(os.path.join(CSRC, "*.cpp")))
+    objs, todo = [], []
+    for s in srcs:
+        o = os.path.join(OBJ_DIR, os.path.basename(s) + ".o")
+        objs.append(o)
+        if force or _newer(s, o, headers):
+            todo.append((s, o))
+    if todo:
+        with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
+            futs = [ex.submit(_compile, s, o) for s, o in todo]
+            for f in cf.as_completed(futs):
+                o = f.result()
+                if verbose:
+                    print("  built", os.path.relpath(o, HERE), flush=True)
+    if todo or not os.path.exists(LIB) or any(os.path.getmtime(o) > os.path.getmtime(LIB) for o in objs):
+        cmd = [HIPCC, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", LIB] + objs
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError("link failed:\n%s\n%s" % (r.stdout, r.stderr))
+        if verbose:
+            print("  linked", os.path.relpath(LIB, HERE), flush=True)
+    return LIB
+
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("-j", type=int, default=min(8, os.cpu_count() or 4))
+    ap.add_argument("--force", action="store_true")
+    a = ap.parse_args()
+    build(a.j, a.force)

@@ -1,0 +1,93 @@
+// Shared device helpers for libdsgan_hip.so (gfx950 / CDNA4 only).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace dsg {
+
+enum Act : int { ACT_NONE = 0, ACT_GELU = 1, ACT_RELU = 2, ACT_LRELU = 3, ACT_SIGMOID = 4 };
+
+constexpr float kInvSqrt2 = 0.70710678118654752440f;
+constexpr float kInvSqrt2Pi = 0.39894228040143267794f;
+
+// nn.GELU() (exact erf form) -- the activation of MixConvNeXtML (DSGAN/models/model/MixConvNeXtML.py:51,82,223)
+__device__ __forceinline__ float gelu_f(float x) { return 0.5f * x * (1.f + erff(x * kInvSqrt2)); }
+__device__ __forceinline__ float gelu_g(float x) {
+  float cdf = 0.5f * (1.f + erff(x * kInvSqrt2));
+  return cdf + x * (kInvSqrt2Pi * __expf(-0.5f * x * x));
+}
+
+__device__ __forceinline__ float act_f(int act, float x, float slope) {
+  switch (act) {
+    case ACT_GELU: return gelu_f(x);
+    case ACT_RELU: return x > 0.f ? x : 0.f;
+    case ACT_LRELU: return x > 0.f ? x : x * slope;
+    case ACT_SIGMOID: return 1.f / (1.f + __expf(-x));
+    default: return x;
+  }
+}
+// derivative of act at pre-activation x
+__device__ __forceinline__ float act_g(int act, float x, float slope) {
+  switch (act) {
+    case ACT_GELU: return gelu_g(x);
+    case ACT_RELU: return x > 0.f ? 1.f : 0.f;
+    case ACT_LRELU: return x > 0.f ? 1.f : slope;
+    case ACT_SIGMOID: { float s = 1.f / (1.f + __expf(-x)); return s * (1.f - s); }
+    default: return 1.f;
+  }
+}
+
+__device__ __forceinline__ float warp_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ double warp_sum_d(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float warp_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// Block-wide sum for blockDim.x == NT (multiple of 64).  `sh` needs NT/64 floats.
+template <int NT>
+__device__ __forceinline__ float block_sum(float v, float* sh) {
+  v = warp_sum(v);
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  __syncthreads();
+  if (l == 0) sh[w] = v;
+  __syncthreads();
+  float r = 0.f;
+#pragma unroll
+  for (int i = 0; i < NT / 64; ++i) r += sh[i];
+  return r;
+}
+
+}  // namespace dsg
+
+// ---- error plumbing for the C ABI -------------------------------------------------
+extern "C" const char* dsgan_last_error_string(void);
+void dsgan_set_error(const char* fmt, ...);
+
+#define DSG_CHECK_LAUNCH()                                                   \
+  do {                                                                       \
+    hipError_t e__ = hipGetLastError();                                      \
+    if (e__ != hipSuccess) {                                                 \
+      dsgan_set_error("%s: %s", __func__, hipGetErrorString(e__));           \
+      return (int)e__;                                                       \
+    }                                                                        \
+  } while (0)
+
+#define DSG_REQUIRE(cond, ...)                                               \
+  do {                                                                       \
+    if (!(cond)) {                                                           \
+      dsgan_set_error(__VA_ARGS__);                                          \
+      return -1;                                                             \
+    }                                                                        \
+  } while (0)
+
+static inline unsigned cdiv(long a, long b) { return (unsigned)((a + b - 1) / b); }

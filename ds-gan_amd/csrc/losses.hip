@@ -1,0 +1,292 @@
+// Loss kernels of backward_D / backward_G (DSGAN/models/pix2pix_model.py:141-199):
+//   BCE-with-logits vs a constant label (GANLoss, DSGAN/models/networks.py:143-163),
+//   L1 mean (:177, :182-186), TV sum (:189-191), and the fused gaussian SSIM
+//   (DSGAN/MS_SSIM.py:26-150) forward + analytic backward.
+// Scalar results are written to device memory; backward kernels read the upstream gradient
+// from device memory, so nothing here forces a host synchronisation.
+#include "common.h"
+
+namespace dsg {
+
+static inline unsigned red_grid(long n) {
+  long g = (n + 2047) / 2048;
+  if (g > 4096) g = 4096;
+  if (g < 1) g = 1;
+  return (unsigned)g;
+}
+
+// ---- BCE with logits, mean over n, target t -----------------------------------------
+__global__ __launch_bounds__(256) void bce_fwd_kernel(const float* x, long n, float t, float* out, float coef) {
+  __shared__ float sh[4];
+  float s = 0.f;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+    const float v = x[i];
+    s += fmaxf(v, 0.f) - v * t + log1pf(__expf(-fabsf(v)));
+  }
+  s = block_sum<256>(s, sh);
+  if (threadIdx.x == 0) atomicAdd(out, s * coef);
+}
+__global__ void bce_bwd_kernel(const float* x, long n, float t, const float* gout, float coef, float* dx, int accumulate) {
+  const float g = gout[0] * coef;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+    const float v = (1.f / (1.f + __expf(-x[i])) - t) * g;
+    dx[i] = accumulate ? dx[i] + v : v;
+  }
+}
+
+// ---- L1 mean ------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void l1_fwd_kernel(const float* a, const float* b, long n, float* out, float coef) {
+  __shared__ float sh[4];
+  float s = 0.f;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) s += fabsf(a[i] - b[i]);
+  s = block_sum<256>(s, sh);
+  if (threadIdx.x == 0) atomicAdd(out, s * coef);
+}
+__global__ void l1_bwd_kernel(const float* a, const float* b, long n, const float* gout, float coef, float* da, int accumulate) {
+  const float g = gout[0] * coef;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+    const float d = a[i] - b[i];
+    const float v = d > 0.f ? g : (d < 0.f ? -g : 0.f);
+    da[i] = accumulate ? da[i] + v : v;
+  }
+}
+
+// ---- TV: (sum |y[..,w+1]-y[..,w]| + sum |y[..,h+1,:]-y[..,h,:]|) * coef ----------------
+__global__ __launch_bounds__(256) void tv_fwd_kernel(const float* y, long planes, int H, int W, float* out, float coef) {
+  __shared__ float sh[4];
+  const long n = planes * H * W;
+  float s = 0.f;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+    const int w = i % W; const int h = (i / W) % H;
+    const float v = y[i];
+    if (w + 1 < W) s += fabsf(y[i + 1] - v);
+    if (h + 1 < H) s += fabsf(y[i + W] - v);
+  }
+  s = block_sum<256>(s, sh);
+  if (threadIdx.x == 0) atomicAdd(out, s * coef);
+}
+__device__ __forceinline__ float sgnf(float d) { return d > 0.f ? 1.f : (d < 0.f ? -1.f : 0.f); }
+__global__ void tv_bwd_kernel(const float* y, long planes, int H, int W, const float* gout, float coef, float* dy, int accumulate) {
+  const float g = gout[0] * coef;
+  const long n = planes * H * W;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+    const int w = i % W; const int h = (i / W) % H;
+    const float v = y[i];
+    float d = 0.f;
+    if (w + 1 < W) d -= sgnf(y[i + 1] - v);
+    if (w > 0) d += sgnf(v - y[i - 1]);
+    if (h + 1 < H) d -= sgnf(y[i + W] - v);
+    if (h > 0) d += sgnf(v - y[i - W]);
+    dy[i] = accumulate ? dy[i] + g * d : g * d;
+  }
+}
+
+// ---- SSIM ---------------------------------------------------------------------------
+// X = a*real + b, Y = a*fake + b (a=b=0.5 for (t+1)/2, :193-194).  11-tap gaussian (sigma 1.5),
+// valid filtering; per output pixel S = A1*A2/(B1*B2).  The forward also writes the three
+// per-pixel coefficient maps of dS/dY used by the backward:
+//   dS/dmu2 = S*(2mu1/A1 - 2mu1/A2 - 2mu2/B1 + 2mu2/B2), dS/dE[YY] = -S/B2, dS/dE[XY] = 2S/A2
+// and dL/dY = G^T*(c_mu) + 2Y*G^T*(c_yy) + X*G^T*(c_xy)   (G^T = adjoint "full" filtering).
+constexpr int SS_T = 32, SS_K = 11, SS_E = SS_T + SS_K - 1;
+
+struct SSIMArgs {
+  const float* real; const float* fake; float a, b;
+  int planes, H, W;
+  const float* win;   // 11 taps
+  float C1, C2;
+  float* coef;        // [3][planes][Ho][Wo]
+  float* out;         // sum of S
+};
+
+__global__ __launch_bounds__(256) void ssim_fwd_kernel(SSIMArgs s, int tiles_w) {
+  __shared__ float xs[SS_E][SS_E + 1], ys[SS_E][SS_E + 1];
+  __shared__ float hb[5][SS_E][SS_T + 1];  // blurred along H first (reference order: dim 2 then 3)
+  __shared__ float wsh[SS_K];
+  __shared__ float sh[4];
+  const int plane = blockIdx.y;
+  const int Ho = s.H - SS_K + 1, Wo = s.W - SS_K + 1;
+  const int oh0 = (blockIdx.x / tiles_w) * SS_T, ow0 = (blockIdx.x % tiles_w) * SS_T;
+  const float* rp = s.real + (long)plane * s.H * s.W;
+  const float* fp = s.fake + (long)plane * s.H * s.W;
+  if (threadIdx.x < SS_K) wsh[threadIdx.x] = s.win[threadIdx.x];
+  for (int i = threadIdx.x; i < SS_E * SS_E; i += 256) {
+    const int r = i / SS_E, q = i - r * SS_E;
+    const int h = oh0 + r, w = ow0 + q;
+    const bool ok = h < s.H && w < s.W;
+    xs[r][q] = ok ? rp[(long)h * s.W + w] * s.a + s.b : 0.f;
+    ys[r][q] = ok ? fp[(long)h * s.W + w] * s.a + s.b : 0.f;
+  }
+  __syncthreads();
+  // vertical (H) pass: hb[k][out_row r][col q] for r in [0,32), q in [0,42)
+  for (int i = threadIdx.x; i < SS_T * SS_E; i += 256) {
+    const int r = i / SS_E, q = i - r * SS_E;
+    float m1 = 0, m2 = 0, e11 = 0, e22 = 0, e12 = 0;
+#pragma unroll
+    for (int k = 0; k < SS_K; ++k) {
+      const float g = wsh[k], xv = xs[r + k][q], yv = ys[r + k][q];
+      m1 += g * xv; m2 += g * yv; e11 += g * (xv * xv); e22 += g * (yv * yv); e12 += g * (xv * yv);
+    }
+    hb[0][q][r] = m1; hb[1][q][r] = m2; hb[2][q][r] = e11; hb[3][q][r] = e22; hb[4][q][r] = e12;
+  }
+  __syncthreads();
+  float ssum = 0.f;
+  const long plane_out = (long)Ho * Wo;
+  for (int i = threadIdx.x; i < SS_T * SS_T; i += 256) {
+    const int r = i >> 5, q = i & 31;
+    const int oh = oh0 + r, ow = ow0 + q;
+    if (oh >= Ho || ow >= Wo) continue;
+    float v[5] = {0, 0, 0, 0, 0};
+#pragma unroll
+    for (int k = 0; k < SS_K; ++k) {
+      const float g = wsh[k];
+#pragma unroll
+      for (int j = 0; j < 5; ++j) v[j] += g * hb[j][q + k][r];
+    }
+    const float mu1 = v[0], mu2 = v[1];
+    const float s11 = v[2] - mu1 * mu1, s22 = v[3] - mu2 * mu2, s12 = v[4] - mu1 * mu2;
+    const float A1 = 2.f * mu1 * mu2 + s.C1, A2 = 2.f * s12 + s.C2;
+    const float B1 = mu1 * mu1 + mu2 * mu2 + s.C1, B2 = s11 + s22 + s.C2;
+    const float cs = A2 / B2;
+    const float S = (A1 / B1) * cs;
+    ssum += S;
+    const long o = (long)plane * plane_out + (long)oh * Wo + ow;
+    const long stride = (long)s.planes * plane_out;
+    s.coef[o] = S * (2.f * mu1 / A1 - 2.f * mu1 / A2 - 2.f * mu2 / B1 + 2.f * mu2 / B2);
+    s.coef[o + stride] = -S / B2;
+    s.coef[o + 2 * stride] = 2.f * S / A2;
+  }
+  ssum = block_sum<256>(ssum, sh);
+  if (threadIdx.x == 0) atomicAdd(s.out, ssum);
+}
+
+// dfake[h,w] = g * a * ( G^T c_mu + 2Y G^T c_yy + X G^T c_xy )  over input tile 32x32
+__global__ __launch_bounds__(256) void ssim_bwd_kernel(SSIMArgs s, const float* gout, float gcoef,
+                                                       float* dfake, int tiles_w, int accumulate) {
+  __shared__ float cs[3][SS_E][SS_E + 1];
+  __shared__ float vb[3][SS_T][SS_E + 1];
+  __shared__ float wsh[SS_K];
+  const int plane = blockIdx.y;
+  const int Ho = s.H - SS_K + 1, Wo = s.W - SS_K + 1;
+  const int h0 = (blockIdx.x / tiles_w) * SS_T, w0 = (blockIdx.x % tiles_w) * SS_T;
+  if (threadIdx.x < SS_K) wsh[threadIdx.x] = s.win[threadIdx.x];
+  const long plane_out = (long)Ho * Wo, stride = (long)s.planes * plane_out;
+  // coefficient window: output rows h0-10 .. h0+31
+  for (int i = threadIdx.x; i < SS_E * SS_E; i += 256) {
+    const int r = i / SS_E, q = i - r * SS_E;
+    const int oh = h0 - (SS_K - 1) + r, ow = w0 - (SS_K - 1) + q;
+    const bool ok = oh >= 0 && ow >= 0 && oh < Ho && ow < Wo;
+    const long o = (long)plane * plane_out + (long)oh * Wo + ow;
+#pragma unroll
+    for (int j = 0; j < 3; ++j) cs[j][r][q] = ok ? s.coef[o + j * stride] : 0.f;
+  }
+  __syncthreads();
+  // adjoint of the W pass: vb[j][r][c] = sum_k g[k] * cs[j][r][c + 10 - k]  (rows r of the window)
+  for (int i = threadIdx.x; i < SS_E * SS_T; i += 256) {
+    const int r = i / SS_T, c = i - r * SS_T;
+    float a0 = 0, a1 = 0, a2 = 0;
+#pragma unroll
+    for (int k = 0; k < SS_K; ++k) {
+      const float g = wsh[k];
+      a0 += g * cs[0][r][c + SS_K - 1 - k];
+      a1 += g * cs[1][r][c + SS_K - 1 - k];
+      a2 += g * cs[2][r][c + SS_K - 1 - k];
+    }
+    vb[0][c][r] = a0; vb[1][c][r] = a1; vb[2][c][r] = a2;
+  }
+  __syncthreads();
+  const float g = gout[0] * gcoef * s.a;
+  const float* rp = s.real + (long)plane * s.H * s.W;
+  const float* fp = s.fake + (long)plane * s.H * s.W;
+  float* dp = dfake + (long)plane * s.H * s.W;
+  for (int i = threadIdx.x; i < SS_T * SS_T; i += 256) {
+    const int r = i >> 5, c = i & 31;
+    const int h = h0 + r, w = w0 + c;
+    if (h >= s.H || w >= s.W) continue;
+    float a0 = 0, a1 = 0, a2 = 0;
+#pragma unroll
+    for (int k = 0; k < SS_K; ++k) {
+      const float gk = wsh[k];
+      a0 += gk * vb[0][c][r + SS_K - 1 - k];
+      a1 += gk * vb[1][c][r + SS_K - 1 - k];
+      a2 += gk * vb[2][c][r + SS_K - 1 - k];
+    }
+    const long e = (long)h * s.W + w;
+    const float X = rp[e] * s.a + s.b, Y = fp[e] * s.a + s.b;
+    const float v = g * (a0 + 2.f * Y * a1 + X * a2);
+    dp[e] = accumulate ? dp[e] + v : v;
+  }
+}
+
+}  // namespace dsg
+
+using namespace dsg;
+
+extern "C" {
+
+int dsgan_bce_logits_fwd(const float* x, long n, float target, float* out, hipStream_t st) {
+  DSG_REQUIRE(x && out && n > 0, "dsgan_bce_logits_fwd: bad args");
+  hipMemsetAsync(out, 0, sizeof(float), st);
+  hipLaunchKernelGGL(bce_fwd_kernel, dim3(red_grid(n)), dim3(256), 0, st, x, n, target, out, 1.f / (float)n);
+  DSG_CHECK_LAUNCH();
+  return 0;
+}
+int dsgan_bce_logits_bwd(const float* x, long n, float target, const float* gout, float* dx,
+                         int accumulate, hipStream_t st) {
+  hipLaunchKernelGGL(bce_bwd_kernel, dim3(red_grid(n) * 8), dim3(256), 0, st, x, n, target, gout, 1.f / (float)n, dx, accumulate);
+  DSG_CHECK_LAUNCH();
+  return 0;
+}
+int dsgan_l1_fwd(const float* a, const float* b, long n, float* out, hipStream_t st) {
+  DSG_REQUIRE(a && b && out && n > 0, "dsgan_l1_fwd: bad args");
+  hipMemsetAsync(out, 0, sizeof(float), st);
+  hipLaunchKernelGGL(l1_fwd_kernel, dim3(red_grid(n)), dim3(256), 0, st, a, b, n, out, 1.f / (float)n);
+  DSG_CHECK_LAUNCH();
+  return 0;
+}
+int dsgan_l1_bwd(const float* a, const float* b, long n, const float* gout, float* da,
+                 int accumulate, hipStream_t st) {
+  hipLaunchKernelGGL(l1_bwd_kernel, dim3(red_grid(n) * 8), dim3(256), 0, st, a, b, n, gout, 1.f / (float)n, da, accumulate);
+  DSG_CHECK_LAUNCH();
+  return 0;
+}
+int dsgan_tv_fwd(const float* y, long planes, int H, int W, float coef, float* out, hipStream_t st) {
+  DSG_REQUIRE(y && out && planes > 0, "dsgan_tv_fwd: bad args");
+  hipMemsetAsync(out, 0, sizeof(float), st);
+  hipLaunchKernelGGL(tv_fwd_kernel, dim3(red_grid(planes * H * W)), dim3(256), 0, st, y, planes, H, W, out, coef);
+  DSG_CHECK_LAUNCH();
+  return 0;
+}
+int dsgan_tv_bwd(const float* y, long planes, int H, int W, float coef, const float* gout, float* dy,
+                 int accumulate, hipStream_t st) {
+  hipLaunchKernelGGL(tv_bwd_kernel, dim3(red_grid(planes * H * W) * 8), dim3(256), 0, st, y, planes, H, W, gout, coef, dy, accumulate);
+  DSG_CHECK_LAUNCH();
+  return 0;
+}
+
+// out = sum of the SSIM map (caller divides by planes*Ho*Wo); coef: [3][planes][Ho][Wo] scratch
+int dsgan_ssim_fwd(const float* real, const float* fake, float a, float b, int planes, int H, int W,
+                   const float* win11, float C1, float C2, float* coef, float* out, hipStream_t st) {
+  DSG_REQUIRE(real && fake && win11 && coef && out && H >= SS_K && W >= SS_K && planes > 0 && planes <= 65535,
+              "dsgan_ssim_fwd: bad args (H,W >= 11 required)");
+  SSIMArgs s{real, fake, a, b, planes, H, W, win11, C1, C2, coef, out};
+  const int Ho = H - SS_K + 1, Wo = W - SS_K + 1;
+  const int tw = cdiv(Wo, SS_T), th = cdiv(Ho, SS_T);
+  hipMemsetAsync(out, 0, sizeof(float), st);
+  hipLaunchKernelGGL(ssim_fwd_kernel, dim3(tw * th, planes), dim3(256), 0, st, s, tw);
+  DSG_CHECK_LAUNCH();
+  return 0;
+}
+
+// dfake = gout[0] * gcoef * d(sum S)/d(fake)
+int dsgan_ssim_bwd(const float* real, const float* fake, float a, float b, int planes, int H, int W,
+                   const float* win11, const float* coef, const float* gout, float gcoef,
+                   float* dfake, int accumulate, hipStream_t st) {
+  DSG_REQUIRE(real && fake && win11 && coef && gout && dfake, "dsgan_ssim_bwd: bad args");
+  SSIMArgs s{real, fake, a, b, planes, H, W, win11, 0.f, 0.f, const_cast<float*>(coef), nullptr};
+  const int tw = cdiv(W, SS_T), th = cdiv(H, SS_T);
+  hipLaunchKernelGGL(ssim_bwd_kernel, dim3(tw * th, planes), dim3(256), 0, st, s, gout, gcoef, dfake, tw, accumulate);
+  DSG_CHECK_LAUNCH();
+  return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,565 @@
+// InstanceNorm (+per-plane scale, +residual, +activation), max-pooling with indices,
+// channel attention (CA), and the small elementwise/reduction kernels of the DS-GAN step.
+//
+// InstanceNorm2d(affine=False, eps=1e-5, biased variance) appears 35x in the generator and
+// 3x in the PatchGAN D (DSGAN/models/model/MixConvNeXtML.py:54,80,151,158,221,335-420;
+// DSGAN/models/networks.py:556,565).  One plane (n,c) is one workgroup (or one wave when the
+// plane is small); the activation that follows it (GELU / LeakyReLU(0.2)) and, for MidMLKA
+// (:113-116), the CA scaling before it and the residual add after it, are fused in.
+#include "common.h"
+
+namespace dsg {
+
+constexpr int IN_CACHE = 16;  // elements per thread held in registers (plane <= 256*16)
+
+struct INArgs {
+  const float* x; long x_bs;
+  const float* scale;           // per-plane multiplier [N*C] applied to x first (nullable)
+  const float* res; long res_bs;  // residual added after normalisation (nullable)
+  float* y; long y_bs;
+  float* mean; float* rstd;     // statistics of scale*x, [N*C]
+  int N, C, HW, act; float slope, eps;
+};
+
+// Plane reduction helper: NT threads per plane (NT = 64: one wave, NT = 256: whole block).
+template <int NT>
+__device__ __forceinline__ float plane_sum(float v, float* sh) {
+  if (NT == 64) return warp_sum(v);
+  return block_sum<NT>(v, sh);
+}
+
+template <int NT>
+__global__ __launch_bounds__(256) void instnorm_fwd_kernel(INArgs a) {
+  __shared__ float sh[4];
+  const int planes_per_block = 256 / NT;
+  const int plane = blockIdx.x * planes_per_block + (NT == 64 ? (threadIdx.x >> 6) : 0);
+  const int t = NT == 64 ? (threadIdx.x & 63) : threadIdx.x;
+  if (plane >= a.N * a.C) return;  // whole wave / block uniform
+  const int n = plane / a.C, c = plane - n * a.C;
+  const float* x = a.x + (long)n * a.x_bs + (long)c * a.HW;
+  const float s = a.scale ? a.scale[plane] : 1.f;
+  const bool cached = a.HW <= NT * IN_CACHE;
+  float rv[IN_CACHE];
+  float sum = 0.f;
+  if (cached) {
+#pragma unroll
+    for (int j = 0; j < IN_CACHE; ++j) {
+      const int i = t + j * NT;
+      rv[j] = i < a.HW ? x[i] * s : 0.f;
+      sum += rv[j];
+    }
+  } else {
+    for (int i = t; i < a.HW; i += NT) sum += x[i] * s;
+  }
+  const float mean = plane_sum<NT>(sum, sh) / (float)a.HW;
+  float sq = 0.f;
+  if (cached) {
+#pragma unroll
+    for (int j = 0; j < IN_CACHE; ++j) {
+      const int i = t + j * NT;
+      const float d = rv[j] - mean;
+      if (i < a.HW) sq += d * d;
+    }
+  } else {
+    for (int i = t; i < a.HW; i += NT) { const float d = x[i] * s - mean; sq += d * d; }
+  }
+  const float var = plane_sum<NT>(sq, sh) / (float)a.HW;
+  const float rs = 1.f / sqrtf(var + a.eps);
+  if (t == 0) { a.mean[plane] = mean; a.rstd[plane] = rs; }
+  float* y = a.y + (long)n * a.y_bs + (long)c * a.HW;
+  const float* r = a.res ? a.res + (long)n * a.res_bs + (long)c * a.HW : nullptr;
+  if (cached) {
+#pragma unroll
+    for (int j = 0; j < IN_CACHE; ++j) {
+      const int i = t + j * NT;
+      if (i < a.HW) {
+        float v = (rv[j] - mean) * rs;
+        if (r) v += r[i];
+        y[i] = act_f(a.act, v, a.slope);
+      }
+    }
+  } else {
+    for (int i = t; i < a.HW; i += NT) {
+      float v = (x[i] * s - mean) * rs;
+      if (r) v += r[i];
+      y[i] = act_f(a.act, v, a.slope);
+    }
+  }
+}
+
+struct INBwdArgs {
+  const float* dy; long dy_bs;
+  const float* x; long x_bs;
+  const float* scale;
+  const float* res; long res_bs;
+  const float* mean; const float* rstd;
+  float* dx; long dx_bs;
+  float* dres; long dres_bs;   // nullable
+  float* dscale;               // nullable, [N*C] (written)
+  int N, C, HW, act; float slope, eps;
+};
+
+// y = act(xhat + res), xhat = (s*x - mean) * rstd
+// g = dy * act'(xhat + res);  dres = g;  dxs = rstd * (g - mean(g) - xhat * mean(g * xhat))
+// dx = s * dxs;  dscale = sum_p dxs * x.  The sum cancels to O(eps) (IN is scale invariant up to
+// eps), so it is evaluated in closed form: sum dxs = 0 and sum xhat^2 = HW*var*rstd^2 give
+//   dscale = mean(g*xhat) * HW * eps * rstd^2 / s
+// which is what the fp64 reference converges to; the direct fp32 sum loses ~1e-3 relative.
+template <int NT>
+__global__ __launch_bounds__(256) void instnorm_bwd_kernel(INBwdArgs a) {
+  __shared__ float sh[4];
+  const int planes_per_block = 256 / NT;
+  const int plane = blockIdx.x * planes_per_block + (NT == 64 ? (threadIdx.x >> 6) : 0);
+  const int t = NT == 64 ? (threadIdx.x & 63) : threadIdx.x;
+  if (plane >= a.N * a.C) return;
+  const int n = plane / a.C, c = plane - n * a.C;
+  const long po = (long)c * a.HW;
+  const float* x = a.x + (long)n * a.x_bs + po;
+  const float* dy = a.dy + (long)n * a.dy_bs + po;
+  const float* r = a.res ? a.res + (long)n * a.res_bs + po : nullptr;
+  float* dres = a.dres ? a.dres + (long)n * a.dres_bs + po : nullptr;
+  const float s = a.scale ? a.scale[plane] : 1.f;
+  const float mean = a.mean[plane], rs = a.rstd[plane];
+  const bool cached = a.HW <= NT * IN_CACHE;
+  float gv[IN_CACHE], hv[IN_CACHE];
+  float sg = 0.f, sgh = 0.f;
+  auto grad_at = [&](int i, float& xh) -> float {
+    xh = (x[i] * s - mean) * rs;
+    float g = dy[i];
+    if (a.act != ACT_NONE) g *= act_g(a.act, r ? xh + r[i] : xh, a.slope);
+    if (dres) dres[i] = g;
+    return g;
+  };
+  if (cached) {
+#pragma unroll
+    for (int j = 0; j < IN_CACHE; ++j) {
+      const int i = t + j * NT;
+      gv[j] = 0.f; hv[j] = 0.f;
+      if (i < a.HW) { gv[j] = grad_at(i, hv[j]); sg += gv[j]; sgh += gv[j] * hv[j]; }
+    }
+  } else {
+    for (int i = t; i < a.HW; i += NT) { float xh; const float g = grad_at(i, xh); sg += g; sgh += g * xh; }
+  }
+  const float inv = 1.f / (float)a.HW;
+  const float mg = plane_sum<NT>(sg, sh) * inv;
+  const float mgh = plane_sum<NT>(sgh, sh) * inv;
+  float* dx = a.dx + (long)n * a.dx_bs + po;
+  if (cached) {
+#pragma unroll
+    for (int j = 0; j < IN_CACHE; ++j) {
+      const int i = t + j * NT;
+      if (i < a.HW) {
+        const float dxs = rs * (gv[j] - mg - hv[j] * mgh);
+        dx[i] = s * dxs;
+      }
+    }
+  } else {
+    for (int i = t; i < a.HW; i += NT) {
+      const float xh = (x[i] * s - mean) * rs;
+      float g = dy[i];
+      if (a.act != ACT_NONE) g *= act_g(a.act, r ? xh + r[i] : xh, a.slope);
+      const float dxs = rs * (g - mg - xh * mgh);
+      dx[i] = s * dxs;
+    }
+  }
+  if (a.dscale && t == 0) a.dscale[plane] = mgh * (float)a.HW * a.eps * rs * rs / s;
+}
+
+// ---------------------------------------------------------------------------------------
+// MaxPool2d(k) (stride k, no padding, floor): DSGAN/models/model/MixConvNeXtML.py:71,194,333-417
+// Indices are the plane-flat argmax ih*W+iw, first maximum in row-major window order, NaN wins
+// (the rule of PyTorch's CPU max_pool2d) -- bit-exact with the reference's int64 indices.
+// ---------------------------------------------------------------------------------------
+__global__ void maxpool_fwd_kernel(const float* __restrict__ x, long x_bs, float* __restrict__ y,
+                                   long y_bs, int* __restrict__ idx, int N, int C, int H, int W,
+                                   int k) {
+  const int Ho = H / k, Wo = W / k;
+  const long total = (long)N * C * Ho * Wo;
+  for (long o = blockIdx.x * (long)blockDim.x + threadIdx.x; o < total; o += (long)gridDim.x * blockDim.x) {
+    const int ow = o % Wo; long t = o / Wo;
+    const int oh = t % Ho; t /= Ho;
+    const int c = t % C; const int n = t / C;
+    const float* xp = x + (long)n * x_bs + (long)c * H * W;
+    float best = -INFINITY; int bi = oh * k * W + ow * k;
+    for (int i = 0; i < k; ++i)
+      for (int j = 0; j < k; ++j) {
+        const int q = (oh * k + i) * W + ow * k + j;
+        const float v = xp[q];
+        if (v > best || isnan(v)) { best = v; bi = q; }
+      }
+    y[(long)n * y_bs + ((long)c * Ho + oh) * Wo + ow] = best;
+    idx[((long)n * C + c) * Ho * Wo + (long)oh * Wo + ow] = bi;
+  }
+}
+
+// dx over the full input plane: dy at the argmax, 0 elsewhere (also rows/cols beyond floor).
+__global__ void maxpool_bwd_kernel(const float* __restrict__ dy, long dy_bs, const int* __restrict__ idx,
+                                   float* __restrict__ dx, long dx_bs, int N, int C, int H, int W,
+                                   int k, int accumulate) {
+  const int Ho = H / k, Wo = W / k;
+  const long total = (long)N * C * H * W;
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
+    const int iw = e % W; long t = e / W;
+    const int ih = t % H; t /= H;
+    const int c = t % C; const int n = t / C;
+    const int oh = ih / k, ow = iw / k;
+    float v = 0.f;
+    if (oh < Ho && ow < Wo) {
+      const long o = ((long)c * Ho + oh) * Wo + ow;
+      if (idx[(long)n * C * Ho * Wo + o] == ih * W + iw) v = dy[(long)n * dy_bs + o];
+    }
+    float* d = dx + (long)n * dx_bs + ((long)c * H + ih) * W + iw;
+    *d = accumulate ? *d + v : v;
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// CA (DSGAN/models/model/MixConvNeXtML.py:5-22): per-plane avg/max(+argmax), then the tiny
+// shared MLP fc2(prelu(fc1(.))) on both, summed, sigmoid.
+// ---------------------------------------------------------------------------------------
+template <int NT>
+__global__ __launch_bounds__(256) void plane_stats_kernel(const float* __restrict__ x, long x_bs,
+                                                          float* avg, float* mx, int* amax, int N,
+                                                          int C, int HW) {
+  __shared__ float shv[4];
+  __shared__ int shi[4];
+  __shared__ float shs[4];
+  const int ppb = 256 / NT;
+  const int plane = blockIdx.x * ppb + (NT == 64 ? (threadIdx.x >> 6) : 0);
+  const int t = NT == 64 ? (threadIdx.x & 63) : threadIdx.x;
+  if (plane >= N * C) return;
+  const int n = plane / C, c = plane - n * C;
+  const float* xp = x + (long)n * x_bs + (long)c * HW;
+  float s = 0.f, best = -INFINITY; int bi = 0x7fffffff;
+  for (int i = t; i < HW; i += NT) {
+    const float v = xp[i];
+    s += v;
+    if (v > best || (isnan(v) && !isnan(best))) { best = v; bi = i; }
+  }
+  // reduce max with smallest index among equal maxima (first occurrence)
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float ov = __shfl_xor(best, o, 64);
+    const int oi = __shfl_xor(bi, o, 64);
+    const bool take = (ov > best) || (ov == best && oi < bi) || (isnan(ov) && (!isnan(best) || oi < bi));
+    if (take) { best = ov; bi = oi; }
+  }
+  s = warp_sum(s);
+  if (NT == 256) {
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) { shv[w] = best; shi[w] = bi; shs[w] = s; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      best = shv[0]; bi = shi[0]; s = shs[0];
+      for (int i = 1; i < 4; ++i) {
+        const bool take = (shv[i] > best) || (shv[i] == best && shi[i] < bi) ||
+                          (isnan(shv[i]) && (!isnan(best) || shi[i] < bi));
+        if (take) { best = shv[i]; bi = shi[i]; }
+        s += shs[i];
+      }
+    }
+  }
+  if (t == 0) { avg[plane] = s / (float)HW; mx[plane] = best; amax[plane] = bi; }
+}
+
+// One block per sample n.  C <= 1024, R = C/8 <= 128.
+__global__ __launch_bounds__(256) void ca_fwd_kernel(const float* avg, const float* mx,
+                                                     const float* w1, const float* w2,
+                                                     const float* pa, float* att, float* hsave,
+                                                     int C, int R) {
+  extern __shared__ float sm[];
+  float* sa = sm;            // C
+  float* sx = sa + C;        // C
+  float* hp = sx + C;        // R : prelu(h_avg) + prelu(h_max)
+  const int n = blockIdx.x;
+  for (int c = threadIdx.x; c < C; c += blockDim.x) { sa[c] = avg[n * C + c]; sx[c] = mx[n * C + c]; }
+  __syncthreads();
+  const float a = pa[0];
+  const int wid = threadIdx.x >> 6, l = threadIdx.x & 63;
+  for (int j = wid; j < R; j += blockDim.x / 64) {
+    float ha = 0.f, hm = 0.f;
+    for (int c = l; c < C; c += 64) { const float w = w1[j * C + c]; ha += w * sa[c]; hm += w * sx[c]; }
+    ha = warp_sum(ha); hm = warp_sum(hm);
+    if (l == 0) {
+      hsave[(n * R + j) * 2 + 0] = ha;
+      hsave[(n * R + j) * 2 + 1] = hm;
+      hp[j] = (ha >= 0.f ? ha : a * ha) + (hm >= 0.f ? hm : a * hm);
+    }
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    float o = 0.f;
+    for (int j = 0; j < R; ++j) o += w2[c * R + j] * hp[j];
+    att[n * C + c] = 1.f / (1.f + __expf(-o));
+  }
+}
+
+// Backward of CA for one sample per block.  Weight grads accumulate (atomics) into dw1/dw2/dpa.
+__global__ __launch_bounds__(256) void ca_bwd_kernel(const float* datt, const float* att,
+                                                     const float* avg, const float* mx,
+                                                     const float* hsave, const float* w1,
+                                                     const float* w2, const float* pa, float* davg,
+                                                     float* dmx, float* dw1, float* dw2, float* dpa,
+                                                     int C, int R) {
+  extern __shared__ float sm[];
+  float* dO = sm;           // C
+  float* hp = dO + C;       // R
+  float* dha = hp + R;      // R
+  float* dhm = dha + R;     // R
+  const int n = blockIdx.x;
+  const float a = pa[0];
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    const float s = att[n * C + c];
+    dO[c] = datt[n * C + c] * s * (1.f - s);
+  }
+  for (int j = threadIdx.x; j < R; j += blockDim.x) {
+    const float ha = hsave[(n * R + j) * 2], hm = hsave[(n * R + j) * 2 + 1];
+    hp[j] = (ha >= 0.f ? ha : a * ha) + (hm >= 0.f ? hm : a * hm);
+  }
+  __syncthreads();
+  const int wid = threadIdx.x >> 6, l = threadIdx.x & 63;
+  float dal = 0.f;
+  for (int j = wid; j < R; j += blockDim.x / 64) {
+    float dp = 0.f;
+    for (int c = l; c < C; c += 64) dp += w2[c * R + j] * dO[c];
+    dp = warp_sum(dp);
+    if (l == 0) {
+      const float ha = hsave[(n * R + j) * 2], hm = hsave[(n * R + j) * 2 + 1];
+      dha[j] = ha > 0.f ? dp : a * dp;
+      dhm[j] = hm > 0.f ? dp : a * dp;
+      dal += (ha > 0.f ? 0.f : ha * dp) + (hm > 0.f ? 0.f : hm * dp);
+    }
+  }
+  if (dpa && l == 0 && dal != 0.f) atomicAdd(dpa, dal);
+  __syncthreads();
+  if (dw2)
+    for (int e = threadIdx.x; e < C * R; e += blockDim.x) atomicAdd(dw2 + e, dO[e / R] * hp[e % R]);
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    float ga = 0.f, gm = 0.f;
+    const float va = avg[n * C + c], vm = mx[n * C + c];
+    for (int j = 0; j < R; ++j) {
+      const float w = w1[j * C + c];
+      ga += w * dha[j]; gm += w * dhm[j];
+      if (dw1) atomicAdd(dw1 + j * C + c, dha[j] * va + dhm[j] * vm);
+    }
+    davg[n * C + c] = ga; dmx[n * C + c] = gm;
+  }
+}
+
+// dx[n,c,:] += davg/HW ; dx[n,c,argmax] += dmax
+__global__ void plane_stats_bwd_kernel(const float* davg, const float* dmx, const int* amax,
+                                       float* dx, long dx_bs, int N, int C, int HW) {
+  const long total = (long)N * C * HW;
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
+    const int i = e % HW; const long pl = e / HW;
+    const int c = pl % C, n = pl / C;
+    float v = davg[pl] / (float)HW;
+    if (amax[pl] == i) v += dmx[pl];
+    dx[(long)n * dx_bs + (long)c * HW + i] += v;
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// Elementwise helpers
+// ---------------------------------------------------------------------------------------
+struct PtrList { const float* p[8]; long bs[8]; };
+
+// out[n, e] = sum_i in_i[n, e]   (per-sample extent E, batch strides per operand)
+__global__ void add_n_kernel(PtrList in, int nin, float* out, long out_bs, int N, long E) {
+  const long total = (long)N * E;
+  for (long t = blockIdx.x * (long)blockDim.x + threadIdx.x; t < total; t += (long)gridDim.x * blockDim.x) {
+    const int n = t / E; const long e = t - (long)n * E;
+    float s = in.p[0][(long)n * in.bs[0] + e];
+    for (int i = 1; i < nin; ++i) s += in.p[i][(long)n * in.bs[i] + e];
+    out[(long)n * out_bs + e] = s;
+  }
+}
+
+__global__ void copy_strided_kernel(const float* src, long src_bs, float* dst, long dst_bs, int N, long E) {
+  const long total = (long)N * E;
+  for (long t = blockIdx.x * (long)blockDim.x + threadIdx.x; t < total; t += (long)gridDim.x * blockDim.x) {
+    const int n = t / E; const long e = t - (long)n * E;
+    dst[(long)n * dst_bs + e] = src[(long)n * src_bs + e];
+  }
+}
+
+__global__ void scale_kernel(float* p, float a, long n) {
+  for (long t = blockIdx.x * (long)blockDim.x + threadIdx.x; t < n; t += (long)gridDim.x * blockDim.x) p[t] *= a;
+}
+
+__global__ void fill_kernel(float* p, float v, long n) {
+  for (long t = blockIdx.x * (long)blockDim.x + threadIdx.x; t < n; t += (long)gridDim.x * blockDim.x) p[t] = v;
+}
+
+// dx = dy * act'(pre)  (+ dx if accumulate)
+__global__ void act_bwd_kernel(const float* dy, const float* pre, float* dx, long n, int act, float slope, int accumulate) {
+  for (long t = blockIdx.x * (long)blockDim.x + threadIdx.x; t < n; t += (long)gridDim.x * blockDim.x) {
+    float v = dy[t] * act_g(act, pre[t], slope);
+    dx[t] = accumulate ? dx[t] + v : v;
+  }
+}
+
+// out[c] += sum_{n,p} dy[n,c,p]   (bias gradient; one block per (n,c) plane, atomics over n)
+__global__ __launch_bounds__(256) void channel_sum_kernel(const float* dy, long dy_bs, float* out, int N, int C, int HW) {
+  __shared__ float sh[4];
+  const int plane = blockIdx.x;
+  const int n = plane / C, c = plane - n * C;
+  const float* p = dy + (long)n * dy_bs + (long)c * HW;
+  float s = 0.f;
+  for (int i = threadIdx.x; i < HW; i += 256) s += p[i];
+  s = block_sum<256>(s, sh);
+  if (threadIdx.x == 0) atomicAdd(out + c, s);
+}
+
+static inline unsigned grid_for(long n, int bs = 256) {
+  long g = (n + bs - 1) / bs;
+  if (g > 65535L * 8) g = 65535L * 8;
+  if (g < 1) g = 1;
+  return (unsigned)g;
+}
+
+}  // namespace dsg
+
+using namespace dsg;
+
+extern "C" {
+
+int dsgan_instnorm_fwd(const float* x, long x_bs, const float* scale, const float* res, long res_bs,
+                       float* y, long y_bs, float* mean, float* rstd, int N, int C, int HW, int act,
+                       float slope, float eps, hipStream_t st) {
+  DSG_REQUIRE(x && y && mean && rstd && N > 0 && C > 0 && HW > 0, "dsgan_instnorm_fwd: bad args");
+  INArgs a{x, x_bs, scale, res, res_bs, y, y_bs, mean, rstd, N, C, HW, act, slope, eps};
+  const int planes = N * C;
+  if (HW <= 64 * IN_CACHE)
+    hipLaunchKernelGGL(instnorm_fwd_kernel<64>, dim3(cdiv(planes, 4)), dim3(256), 0, st, a);
+  else
+    hipLaunchKernelGGL(instnorm_fwd_kernel<256>, dim3(planes), dim3(256), 0, st, a);
+  DSG_CHECK_LAUNCH();
+  return 0;
+}
+
+int dsgan_instnorm_bwd(const float* dy, long dy_bs, const float* x, long x_bs, const float* scale,
+                       const float* res, long res_bs, const float* mean, const float* rstd,
+                       float* dx, long dx_bs, float* dres, long dres_bs, float* dscale, int N,
+                       int C, int HW, int act, float slope, float eps, hipStream_t st) {
+  DSG_REQUIRE(dy && x && mean && rstd && dx && N > 0 && C > 0 && HW > 0, "dsgan_instnorm_bwd: bad args");
+  INBwdArgs a{dy, dy_bs, x, x_bs, scale, res, res_bs, mean, rstd, dx, dx_bs, dres, dres_bs, dscale,
+              N, C, HW, act, slope, eps};
+  const int planes = N * C;
+  if (HW <= 64 * IN_CACHE)
+    hipLaunchKernelGGL(instnorm_bwd_kernel<64>, dim3(cdiv(planes, 4)), dim3(256), 0, st, a);
+  else
+    hipLaunchKernelGGL(instnorm_bwd_kernel<256>, dim3(planes), dim3(256), 0, st, a);
+  DSG_CHECK_LAUNCH();
+  return 0;
+}
+
+int dsgan_maxpool_fwd(const float* x, long x_bs, float* y, long y_bs, int* idx, int N, int C, int H,
+                      int W, int k, hipStream_t st) {
+  DSG_REQUIRE(x && y && idx && k > 0 && H >= k && W >= k, "dsgan_maxpool_fwd: bad args");
+  const long total = (long)N * C * (H / k) * (W / k);
+  hipLaunchKernelGGL(maxpool_fwd_kernel, dim3(grid_for(total)), dim3(256), 0, st, x, x_bs, y, y_bs,
+                     idx, N, C, H, W, k);
+  DSG_CHECK_LAUNCH();
+  return 0;
+}
+
+int dsgan_maxpool_bwd(const float* dy, long dy_bs, const int* idx, float* dx, long dx_bs, int N,
+                      int C, int H, int W, int k, int accumulate, hipStream_t st) {
+  DSG_REQUIRE(dy && idx && dx && k > 0, "dsgan_maxpool_bwd: bad args");
+  const long total = (long)N * C * H * W;
+  hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(grid_for(total)), dim3(256), 0, st, dy, dy_bs, idx,
+                     dx, dx_bs, N, C, H, W, k, accumulate);
+  DSG_CHECK_LAUNCH();
+  return 0;
+}
+
+int dsgan_plane_stats(const float* x, long x_bs, float* avg, float* mx, int* amax, int N, int C,
+                      int HW, hipStream_t st) {
+  DSG_REQUIRE(x && avg && mx && amax && HW > 0, "dsgan_plane_stats: bad args");
+  const int planes = N * C;
+  if (HW <= 4096)
+    hipLaunchKernelGGL(plane_stats_kernel<64>, dim3(cdiv(planes, 4)), dim3(256), 0, st, x, x_bs, avg, mx, amax, N, C, HW);
+  else
+    hipLaunchKernelGGL(plane_stats_kernel<256>, dim3(planes), dim3(256), 0, st, x, x_bs, avg, mx, amax, N, C, HW);
+  DSG_CHECK_LAUNCH();
+  return 0;
+}
+
+int dsgan_plane_stats_bwd(const float* davg, const float* dmx, const int* amax, float* dx,
+                          long dx_bs, int N, int C, int HW, hipStream_t st) {
+  const long total = (long)N * C * HW;
+  hipLaunchKernelGGL(plane_stats_bwd_kernel, dim3(grid_for(total)), dim3(256), 0, st, davg, dmx,
+                     amax, dx, dx_bs, N, C, HW);
+  DSG_CHECK_LAUNCH();
+  return 0;
+}
+
+int dsgan_ca_fwd(const float* avg, const float* mx, const float* w1, const float* w2,
+                 const float* prelu_a, float* att, float* hsave, int N, int C, int R,
+                 hipStream_t st) {
+  DSG_REQUIRE(C > 0 && R > 0 && C <= 4096, "dsgan_ca_fwd: bad dims");
+  const size_t shm = (2 * C + R) * sizeof(float);
+  hipLaunchKernelGGL(ca_fwd_kernel, dim3(N), dim3(256), shm, st, avg, mx, w1, w2, prelu_a, att, hsave, C, R);
+  DSG_CHECK_LAUNCH();
+  return 0;
+}
+
+int dsgan_ca_bwd(const float* datt, const float* att, const float* avg, const float* mx,
+                 const float* hsave, const float* w1, const float* w2, const float* prelu_a,
+                 float* davg, float* dmx, float* dw1, float* dw2, float* dprelu_a, int N, int C,
+                 int R, hipStream_t st) {
+  DSG_REQUIRE(C > 0 && R > 0 && C <= 4096, "dsgan_ca_bwd: bad dims");
+  const size_t shm = (C + 3 * R) * sizeof(float);
+  hipLaunchKernelGGL(ca_bwd_kernel, dim3(N), dim3(256), shm, st, datt, att, avg, mx, hsave, w1, w2,
+                     prelu_a, davg, dmx, dw1, dw2, dprelu_a, C, R);
+  DSG_CHECK_LAUNCH();
+  return 0;
+}
+
+int dsgan_add_n(const float* const* ins, const long* in_bs, int nin, float* out, long out_bs, int N,
+                long E, hipStream_t st) {
+  DSG_REQUIRE(nin >= 1 && nin <= 8 && ins && out, "dsgan_add_n: 1..8 inputs");
+  PtrList pl{};
+  for (int i = 0; i < nin; ++i) { pl.p[i] = ins[i]; pl.bs[i] = in_bs[i]; }
+  hipLaunchKernelGGL(add_n_kernel, dim3(grid_for((long)N * E)), dim3(256), 0, st, pl, nin, out, out_bs, N, E);
+  DSG_CHECK_LAUNCH();
+  return 0;
+}
+
+int dsgan_copy_strided(const float* src, long src_bs, float* dst, long dst_bs, int N, long E,
+                       hipStream_t st) {
+  hipLaunchKernelGGL(copy_strided_kernel, dim3(grid_for((long)N * E)), dim3(256), 0, st, src, src_bs, dst, dst_bs, N, E);
+  DSG_CHECK_LAUNCH();
+  return 0;
+}
+
+int dsgan_fill(float* p, float v, long n, hipStream_t st) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(fill_kernel, dim3(grid_for(n)), dim3(256), 0, st, p, v, n);
+  DSG_CHECK_LAUNCH();
+  return 0;
+}
+
+int dsgan_scale(float* p, float a, long n, hipStream_t st) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(scale_kernel, dim3(grid_for(n)), dim3(256), 0, st, p, a, n);
+  DSG_CHECK_LAUNCH();
+  return 0;
+}
+
+int dsgan_act_bwd(const float* dy, const float* pre, float* dx, long n, int act, float slope,
+                  int accumulate, hipStream_t st) {
+  hipLaunchKernelGGL(act_bwd_kernel, dim3(grid_for(n)), dim3(256), 0, st, dy, pre, dx, n, act, slope, accumulate);
+  DSG_CHECK_LAUNCH();
+  return 0;
+}
+
+int dsgan_channel_sum(const float* dy, long dy_bs, float* out, int N, int C, int HW, hipStream_t st) {
+  DSG_REQUIRE(dy && out && N > 0 && C > 0 && HW > 0, "dsgan_channel_sum: bad args");
+  hipLaunchKernelGGL(channel_sum_kernel, dim3(N * C), dim3(256), 0, st, dy, dy_bs, out, N, C, HW);
+  DSG_CHECK_LAUNCH();
+  return 0;
+}
+
+}  // extern "C"

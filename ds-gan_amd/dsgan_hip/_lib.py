@@ -1,0 +1,98 @@
+"""ctypes binding of libdsgan_hip.so (the C-ABI declared in include/dsgan_hip.h).
+
+There is no fallback: if the library is missing or fails to load, every op raises.  The
+signature table below is the single source of truth on the Python side and is checked
+against include/dsgan_hip.h by tests/test_capi.py.
+"""
+import ctypes
+import os
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("DSGAN_HIP_LIB", os.path.join(_HERE, "libdsgan_hip.so"))
+
+P = ctypes.c_void_p
+L = ctypes.c_long
+I = ctypes.c_int
+F = ctypes.c_float
+S = ctypes.c_void_p  # hipStream_t
+
+SIGNATURES = {
+    "dsgan_abi_version": [],
+    "dsgan_last_error_string": [],
+    # igemm.hip
+    "dsgan_conv_fwd": [P, L, P, P, P, L, P, L, I, I, I, I, I, I, I, I, I, I, I, I, F, I, I, S],
+    "dsgan_conv_dgrad": [P, L, P, P, P, L, P, L, P, L, I, I, I, I, I, I, I, I, I, I, I, I, I, F, I, I, S],
+    "dsgan_conv_wgrad": [P, L, P, L, P] + [I] * 12 + [S],
+    # dwconv.hip
+    "dsgan_dwconv_fwd": [P, L, P, P, P, L, I, I, I, I, I, I, S],
+    "dsgan_dwconv_wgrad": [P, L, P, L, P, P, I, I, I, I, I, S],
+    # norm_pointwise.hip
+    "dsgan_instnorm_fwd": [P, L, P, P, L, P, L, P, P, I, I, I, I, F, F, S],
+    "dsgan_instnorm_bwd": [P, L, P, L, P, P, L, P, P, P, L, P, L, P, I, I, I, I, F, F, S],
+    "dsgan_maxpool_fwd": [P, L, P, L, P, I, I, I, I, I, S],
+    "dsgan_maxpool_bwd": [P, L, P, P, L, I, I, I, I, I, I, S],
+    "dsgan_plane_stats": [P, L, P, P, P, I, I, I, S],
+    "dsgan_plane_stats_bwd": [P, P, P, P, L, I, I, I, S],
+    "dsgan_ca_fwd": [P, P, P, P, P, P, P, I, I, I, S],
+    "dsgan_ca_bwd": [P, P, P, P, P, P, P, P, P, P, P, P, P, I, I, I, S],
+    "dsgan_add_n": [P, P, I, P, L, I, L, S],
+    "dsgan_copy_strided": [P, L, P, L, I, L, S],
+    "dsgan_fill": [P, F, L, S],
+    "dsgan_scale": [P, F, L, S],
+    "dsgan_act_bwd": [P, P, P, L, I, F, I, S],
+    "dsgan_channel_sum": [P, L, P, I, I, I, S],
+    # losses.hip
+    "dsgan_bce_logits_fwd": [P, L, F, P, S],
+    "dsgan_bce_logits_bwd": [P, L, F, P, P, I, S],
+    "dsgan_l1_fwd": [P, P, L, P, S],
+    "dsgan_l1_bwd": [P, P, L, P, P, I, S],
+    "dsgan_tv_fwd": [P, L, I, I, F, P, S],
+    "dsgan_tv_bwd": [P, L, I, I, F, P, P, I, S],
+    "dsgan_ssim_fwd": [P, P, F, F, I, I, I, P, F, F, P, P, S],
+    "dsgan_ssim_bwd": [P, P, F, F, I, I, I, P, P, P, F, P, I, S],
+    # adam.hip
+    "dsgan_adam": [P, P, P, P, L, F, F, F, F, I, S],
+}
+
+_lib = None
+
+
+def load():
+    """Load the library (idempotent).  Raises RuntimeError if it is absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(
+            "libdsgan_hip.so not found at %s -- build it with `python ds-gan_amd/build_lib.py` "
+            "(there is no CPU/PyTorch fallback for the DS-GAN hot path)" % LIB_PATH)
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, argtypes in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.argtypes = argtypes
+        fn.restype = ctypes.c_char_p if name == "dsgan_last_error_string" else ctypes.c_int
+    _lib = lib
+    return lib
+
+
+def call(name, *args):
+    lib = load()
+    rc = getattr(lib, name)(*args)
+    if rc != 0:
+        msg = lib.dsgan_last_error_string()
+        raise RuntimeError("%s failed (rc=%d): %s" % (name, rc, msg.decode() if msg else ""))
+
+
+def ptr(t):
+    """Device pointer of a tensor (None -> NULL).  Refuses CPU tensors: the product path is GPU-only."""
+    if t is None:
+        return None
+    if not t.is_cuda:
+        raise RuntimeError("dsgan_hip: expected a device tensor, got %s on %s" % (tuple(t.shape), t.device))
+    return t.data_ptr()
+
+
+def stream():
+    return torch.cuda.current_stream().cuda_stream

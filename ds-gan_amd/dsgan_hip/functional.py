@@ -1,0 +1,699 @@
+"""Autograd Functions over libdsgan_hip.so -- the fused ops the DS-GAN networks are built from.
+
+Every forward and backward here is one or more HIP kernels launched on torch's current stream.
+PyTorch provides allocation (caching allocator), stream handles and the autograd tape only.
+
+Weight/bias gradients are *accumulated* by the kernels straight into ``param.grad``, which
+``dsgan_hip.flat.FlatParams`` binds to a view of one flat fp32 buffer (zeroed once per step);
+the Functions therefore return ``None`` for parameters.  A parameter whose ``requires_grad`` is
+False (the frozen VGG16, or D during the G step, DSGAN/models/base_model.py:171-177) gets no
+weight-grad launch at all.
+"""
+import math
+
+import torch
+
+from . import _lib
+from ._lib import call, ptr, stream
+
+ACT = {None: 0, "none": 0, "gelu": 1, "relu": 2, "lrelu": 3, "sigmoid": 4}
+PREC = {"fp32": 0, "bf16": 1}
+_state = {"prec": "fp32"}
+IN_EPS = 1e-5
+LRELU_SLOPE = 0.2
+
+
+def set_precision(p):
+    """'fp32' (exact f32 MFMA, parity mode) or 'bf16' (bf16 MFMA operands, fp32 accumulate)."""
+    if p not in PREC:
+        raise ValueError(p)
+    _state["prec"] = p
+
+
+def get_precision():
+    return _state["prec"]
+
+
+def _prec():
+    return PREC[_state["prec"]]
+
+
+class KernelTimer:
+    """Brackets every implicit-GEMM launch with HIP events on the launch stream (bench.py's
+    roofline leg).  Off by default; when on, records (start, end, algorithmic_flops)."""
+
+    def __init__(self):
+        self.on = False
+        self.rec = []
+
+    def begin(self):
+        if not self.on:
+            return None
+        e0 = torch.cuda.Event(enable_timing=True)
+        e0.record()
+        return e0
+
+    def end(self, e0, flops):
+        if e0 is None:
+            return
+        e1 = torch.cuda.Event(enable_timing=True)
+        e1.record()
+        self.rec.append((e0, e1, flops))
+
+    def summary(self):
+        torch.cuda.synchronize()
+        ms = sum(a.elapsed_time(b) for a, b, _ in self.rec)
+        fl = sum(f for _, _, f in self.rec)
+        return dict(launches=len(self.rec), total_ms=ms, flops=fl)
+
+
+IGEMM_TIMER = KernelTimer()
+
+
+def _conv_flops(N, Cin, Cout, KH, KW, Ho, Wo):
+    # algorithmic MACs of the conv (also for its dgrad/wgrad): every output pixel x every tap
+    return 2.0 * N * Cout * Cin * KH * KW * Ho * Wo
+
+
+def nchw(t):
+    """Return (tensor, batch_stride) with the per-sample [C,H,W] block dense (channel slices of
+    a concat buffer qualify); otherwise make it contiguous."""
+    if t.dim() != 4:
+        raise ValueError("expected NCHW tensor, got %s" % (tuple(t.shape),))
+    N, C, H, W = t.shape
+    s = t.stride()
+    if (s[3] == 1 and s[2] == W and s[1] == H * W) or t.numel() == 0:
+        return t, (s[0] if N > 1 else C * H * W)
+    t = t.contiguous()
+    return t, C * H * W
+
+
+def _empty(N, C, H, W, like):
+    return torch.empty((N, C, H, W), device=like.device, dtype=torch.float32)
+
+
+def _grad_buf(p):
+    """Accumulation target for a parameter's gradient, or None when it is frozen."""
+    if p is None or not p.requires_grad:
+        return None
+    if p.grad is None:
+        # FlatParams binds .grad up front; a free-standing parameter gets a zeroed buffer here.
+        p.grad = torch.zeros_like(p)
+    return p.grad
+
+
+# ------------------------------------------------------------------------------------------
+# raw launchers (no autograd)
+# ------------------------------------------------------------------------------------------
+
+def conv_fwd_raw(x, w, b, stride, pad, act=None, out=None, pre=None, accumulate=False):
+    x, xbs = nchw(x)
+    N, Cin, H, W = x.shape
+    Cout, Cin_w, KH, KW = w.shape if w.dim() == 4 else (w.shape[0], w.shape[1], 1, 1)
+    if Cin_w != Cin:
+        raise ValueError("conv: input has %d channels, weight expects %d" % (Cin, Cin_w))
+    Ho = (H + 2 * pad - KH) // stride + 1
+    Wo = (W + 2 * pad - KW) // stride + 1
+    y = out if out is not None else _empty(N, Cout, Ho, Wo, x)
+    y, ybs = nchw(y)
+    pbs = 0
+    if pre is not None:
+        pre, pbs = nchw(pre)
+    e0 = IGEMM_TIMER.begin()
+    call("dsgan_conv_fwd", ptr(x), xbs, ptr(w), ptr(b), ptr(y), ybs, ptr(pre), pbs, N, Cin, H, W,
+         Cout, KH, KW, stride, pad, Ho, Wo, ACT[act], LRELU_SLOPE, int(accumulate), _prec(), stream())
+    IGEMM_TIMER.end(e0, _conv_flops(N, Cin, Cout, KH, KW, Ho, Wo))
+    return y
+
+
+def conv_dgrad_raw(dy, w, x_shape, stride, pad, bias=None, act=None, gpre=None, gact=None,
+                   out=None, accumulate=False):
+    """dx (N,Cin,H,W) of a conv with weight w [Cout,Cin,KH,KW]; also a ConvTranspose forward."""
+    dy, dybs = nchw(dy)
+    N, Cin, H, W = x_shape
+    Cout, _, KH, KW = w.shape if w.dim() == 4 else (w.shape[0], w.shape[1], 1, 1)
+    Ho, Wo = dy.shape[2], dy.shape[3]
+    dx = out if out is not None else torch.empty((N, Cin, H, W), device=dy.device, dtype=torch.float32)
+    dx, dxbs = nchw(dx)
+    gbs = 0
+    if gpre is not None:
+        gpre, gbs = nchw(gpre)
+    e0 = IGEMM_TIMER.begin()
+    call("dsgan_conv_dgrad", ptr(dy), dybs, ptr(w), ptr(bias), ptr(dx), dxbs, None, 0, ptr(gpre), gbs,
+         ACT[gact], N, Cin, H, W, Cout, KH, KW, stride, pad, Ho, Wo, ACT[act], LRELU_SLOPE,
+         int(accumulate), _prec(), stream())
+    IGEMM_TIMER.end(e0, _conv_flops(N, Cin, Cout, KH, KW, Ho, Wo))
+    return dx
+
+
+def conv_wgrad_raw(dy, x, dw, stride, pad):
+    dy, dybs = nchw(dy)
+    x, xbs = nchw(x)
+    N, Cin, H, W = x.shape
+    Cout = dy.shape[1]
+    KH, KW = (dw.shape[2], dw.shape[3]) if dw.dim() == 4 else (1, 1)
+    e0 = IGEMM_TIMER.begin()
+    call("dsgan_conv_wgrad", ptr(dy), dybs, ptr(x), xbs, ptr(dw), N, Cin, H, W, Cout, KH, KW,
+         stride, pad, dy.shape[2], dy.shape[3], _prec(), stream())
+    IGEMM_TIMER.end(e0, _conv_flops(N, Cin, Cout, KH, KW, dy.shape[2], dy.shape[3]))
+
+
+def channel_sum_raw(dy, out):
+    dy, dybs = nchw(dy)
+    N, C, H, W = dy.shape
+    call("dsgan_channel_sum", ptr(dy), dybs, ptr(out), N, C, H * W, stream())
+
+
+def act_bwd_raw(dy, pre, act, out=None):
+    dy = dy.contiguous()
+    pre = pre.contiguous()
+    out = out if out is not None else torch.empty_like(dy)
+    call("dsgan_act_bwd", ptr(dy), ptr(pre), ptr(out), dy.numel(), ACT[act], LRELU_SLOPE, 0, stream())
+    return out
+
+
+def fill_(t, v):
+    if not t.is_contiguous():
+        raise ValueError("fill_: contiguous tensor required")
+    call("dsgan_fill", ptr(t), float(v), t.numel(), stream())
+    return t
+
+
+def zeros(shape, like):
+    return fill_(torch.empty(shape, device=like.device, dtype=torch.float32), 0.0)
+
+
+def copy_into(dst, src):
+    """dst[n] <- src[n] for per-sample dense blocks (used for channel concatenation)."""
+    src, sbs = nchw(src)
+    dst4, dbs = nchw(dst)
+    if dst4.data_ptr() != dst.data_ptr():
+        raise ValueError("copy_into: destination must be per-sample dense")
+    N = src.shape[0]
+    E = src.shape[1] * src.shape[2] * src.shape[3]
+    call("dsgan_copy_strided", ptr(src), sbs, ptr(dst), dbs, N, E, stream())
+
+
+# ------------------------------------------------------------------------------------------
+# Conv2d (+bias, +relu/lrelu):  VGG 3x3, PatchGAN 4x4, G head 3x3, 1x1 convs
+# ------------------------------------------------------------------------------------------
+
+class Conv2dFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b, stride, pad, act):
+        y = conv_fwd_raw(x, w, b, stride, pad, act)
+        ctx.stride, ctx.pad, ctx.act = stride, pad, act
+        ctx.x_shape = tuple(x.shape)
+        ctx.save_for_backward(x, w, b, y if act in ("relu", "lrelu") else None)
+        ctx.w_ref, ctx.b_ref = w, b
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w, b, y = ctx.saved_tensors
+        if ctx.act in ("relu", "lrelu"):
+            dy = act_bwd_raw(dy, y, ctx.act)  # sign(y) == sign(pre) for relu/lrelu
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = conv_dgrad_raw(dy, w, ctx.x_shape, ctx.stride, ctx.pad)
+        gw = _grad_buf(ctx.w_ref) if ctx.needs_input_grad[1] else None
+        if gw is not None:
+            conv_wgrad_raw(dy, x, gw, ctx.stride, ctx.pad)
+        gb = _grad_buf(ctx.b_ref) if (b is not None and ctx.needs_input_grad[2]) else None
+        if gb is not None:
+            channel_sum_raw(dy, gb)
+        return dx, None, None, None, None, None
+
+
+def conv2d(x, w, b=None, stride=1, pad=0, act=None):
+    """w may be OIHW or a Linear [out, in] weight (== 1x1 conv); pass the Parameter itself so its
+    gradient lands in param.grad."""
+    return Conv2dFn.apply(x, w, b, stride, pad, act)
+
+
+# ------------------------------------------------------------------------------------------
+# ConvTranspose2d(k3, s2, p1, op1) (+bias): forward = conv data-grad, backward = conv forward
+# ------------------------------------------------------------------------------------------
+
+class ConvT3s2Fn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b):
+        N, Ci, Hi, Wi = x.shape
+        Co = w.shape[1]
+        y = conv_dgrad_raw(x, w, (N, Co, 2 * Hi, 2 * Wi), 2, 1, bias=b)
+        ctx.save_for_backward(x, w, b)
+        ctx.w_ref, ctx.b_ref = w, b
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w, b = ctx.saved_tensors
+        dx = conv_fwd_raw(dy, w, None, 2, 1) if ctx.needs_input_grad[0] else None
+        gw = _grad_buf(ctx.w_ref) if ctx.needs_input_grad[1] else None
+        if gw is not None:
+            conv_wgrad_raw(x, dy, gw, 2, 1)
+        gb = _grad_buf(ctx.b_ref) if (b is not None and ctx.needs_input_grad[2]) else None
+        if gb is not None:
+            channel_sum_raw(dy, gb)
+        return dx, None, None
+
+
+def conv_transpose3s2(x, w, b):
+    return ConvT3s2Fn.apply(x, w, b)
+
+
+# ------------------------------------------------------------------------------------------
+# ConvNeXt pointwise MLP + shortcut (Block.forward tail, MixConvNeXtML.py:236-242):
+#   out = Ws x + W2 gelu(W1 h + b1) + b2
+# backward: the dgrad of W2 multiplies by gelu'(z) in its epilogue (no standalone GELU pass).
+# ------------------------------------------------------------------------------------------
+
+class PwMlpFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, h, x, w1, b1, w2, b2, ws):
+        N, C, H, W = h.shape
+        P = w2.shape[0]
+        w1v = w1.view(w1.shape[0], w1.shape[1], 1, 1)
+        w2v = w2.view(w2.shape[0], w2.shape[1], 1, 1)
+        z = _empty(N, w1.shape[0], H, W, h)
+        g = conv_fwd_raw(h, w1v, b1, 1, 0, act="gelu", pre=z)
+        out = conv_fwd_raw(x, ws, None, 1, 0)
+        conv_fwd_raw(g, w2v, b2, 1, 0, out=out, accumulate=True)
+        ctx.save_for_backward(h, x, z, g, w1v, w2v, ws)
+        ctx.refs = (w1, b1, w2, b2, ws)
+        return out
+
+    @staticmethod
+    def backward(ctx, dy):
+        h, x, z, g, w1v, w2v, ws = ctx.saved_tensors
+        w1, b1, w2, b2, ws_ref = ctx.refs
+        dy = dy.contiguous()
+        # dz = (W2^T dy) * gelu'(z)
+        dz = conv_dgrad_raw(dy, w2v, tuple(z.shape), 1, 0, gpre=z, gact="gelu")
+        gw2, gb2, gws = _grad_buf(w2), _grad_buf(b2), _grad_buf(ws_ref)
+        if gw2 is not None:
+            conv_wgrad_raw(dy, g, gw2.view(w2v.shape), 1, 0)
+        if gb2 is not None:
+            channel_sum_raw(dy, gb2)
+        if gws is not None:
+            conv_wgrad_raw(dy, x, gws, 1, 0)
+        gw1, gb1 = _grad_buf(w1), _grad_buf(b1)
+        if gw1 is not None:
+            conv_wgrad_raw(dz, h, gw1.view(w1v.shape), 1, 0)
+        if gb1 is not None:
+            channel_sum_raw(dz, gb1)
+        dh = conv_dgrad_raw(dz, w1v, tuple(h.shape), 1, 0) if ctx.needs_input_grad[0] else None
+        dx = conv_dgrad_raw(dy, ws, tuple(x.shape), 1, 0) if ctx.needs_input_grad[1] else None
+        return dh, dx, None, None, None, None, None
+
+
+def pw_mlp(h, x, w1, b1, w2, b2, ws):
+    return PwMlpFn.apply(h, x, w1, b1, w2, b2, ws)
+
+
+# ------------------------------------------------------------------------------------------
+# Depthwise conv
+# ------------------------------------------------------------------------------------------
+
+def dwconv_raw(x, w, b, flip=False, out=None):
+    x, xbs = nchw(x)
+    N, C, H, W = x.shape
+    K = w.shape[-1]
+    y = out if out is not None else _empty(N, C, H, W, x)
+    y4, ybs = nchw(y)
+    call("dsgan_dwconv_fwd", ptr(x), xbs, ptr(w), ptr(b), ptr(y4), ybs, N, C, H, W, K, int(flip), stream())
+    return y4
+
+
+def _dw_wgrad(dy, x, gw, gb, K):
+    dy4, dybs = nchw(dy)
+    x4, xbs = nchw(x)
+    N, C, H, W = x4.shape
+    call("dsgan_dwconv_wgrad", ptr(dy4), dybs, ptr(x4), xbs, ptr(gw), ptr(gb), N, C, H, W, K, stream())
+
+
+class DwConvFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b):
+        y = dwconv_raw(x, w, b)
+        ctx.save_for_backward(x, w)
+        ctx.refs = (w, b)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        wr, br = ctx.refs
+        dx = dwconv_raw(dy, w, None, flip=True) if ctx.needs_input_grad[0] else None
+        gw, gb = _grad_buf(wr), _grad_buf(br)
+        if gw is not None:
+            _dw_wgrad(dy, x, gw, gb, w.shape[-1])
+        return dx, None, None
+
+
+def dwconv(x, w, b):
+    return DwConvFn.apply(x, w, b)
+
+
+class MultiDwConvFn(torch.autograd.Function):
+    """MidMLKA's chunk(4) -> X3/X5/X7/X9 depthwise -> cat (MixConvNeXtML.py:110-111), written
+    straight into one output buffer (no chunk/cat copies)."""
+
+    @staticmethod
+    def forward(ctx, x, *wb):
+        x4, _ = nchw(x)
+        N, C, H, W = x4.shape
+        q = C // 4
+        y = _empty(N, C, H, W, x4)
+        for i in range(4):
+            dwconv_raw(x4[:, i * q:(i + 1) * q], wb[2 * i], wb[2 * i + 1], out=y[:, i * q:(i + 1) * q])
+        ctx.save_for_backward(x4, *wb)
+        ctx.refs = wb
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, *wb = ctx.saved_tensors
+        N, C, H, W = x.shape
+        q = C // 4
+        dy4, _ = nchw(dy)
+        dx = _empty(N, C, H, W, x) if ctx.needs_input_grad[0] else None
+        for i in range(4):
+            sl = slice(i * q, (i + 1) * q)
+            w = wb[2 * i]
+            if dx is not None:
+                dwconv_raw(dy4[:, sl], w, None, flip=True, out=dx[:, sl])
+            gw, gb = _grad_buf(ctx.refs[2 * i]), _grad_buf(ctx.refs[2 * i + 1])
+            if gw is not None:
+                _dw_wgrad(dy4[:, sl], x[:, sl], gw, gb, w.shape[-1])
+        return (dx,) + (None,) * 8
+
+
+def multi_dwconv(x, w3, b3, w5, b5, w7, b7, w9, b9):
+    return MultiDwConvFn.apply(x, w3, b3, w5, b5, w7, b7, w9, b9)
+
+
+# ------------------------------------------------------------------------------------------
+# InstanceNorm (+scale, +residual, +act)
+# ------------------------------------------------------------------------------------------
+
+def instnorm_raw(x, scale=None, res=None, act=None, out=None):
+    x, xbs = nchw(x)
+    N, C, H, W = x.shape
+    rbs = 0
+    if res is not None:
+        res, rbs = nchw(res)
+    y = out if out is not None else _empty(N, C, H, W, x)
+    y4, ybs = nchw(y)
+    mean = torch.empty(N * C, device=x.device, dtype=torch.float32)
+    rstd = torch.empty(N * C, device=x.device, dtype=torch.float32)
+    call("dsgan_instnorm_fwd", ptr(x), xbs, ptr(scale), ptr(res), rbs, ptr(y4), ybs, ptr(mean),
+         ptr(rstd), N, C, H * W, ACT[act], LRELU_SLOPE, IN_EPS, stream())
+    return y4, mean, rstd
+
+
+def instnorm_bwd_raw(dy, x, scale, res, mean, rstd, act, want_dres, want_dscale):
+    dy, dybs = nchw(dy)
+    x, xbs = nchw(x)
+    N, C, H, W = x.shape
+    rbs = 0
+    if res is not None:
+        res, rbs = nchw(res)
+    dx = _empty(N, C, H, W, x)
+    dres = _empty(N, C, H, W, x) if want_dres else None
+    dscale = torch.empty(N * C, device=x.device, dtype=torch.float32) if want_dscale else None
+    call("dsgan_instnorm_bwd", ptr(dy), dybs, ptr(x), xbs, ptr(scale), ptr(res), rbs, ptr(mean),
+         ptr(rstd), ptr(dx), C * H * W, ptr(dres), C * H * W, ptr(dscale), N, C, H * W, ACT[act],
+         LRELU_SLOPE, IN_EPS, stream())
+    return dx, dres, dscale
+
+
+class InstanceNormFn(torch.autograd.Function):
+    """y = act(IN(x) + res) -- InstanceNorm2d(affine=False) fused with what follows it."""
+
+    @staticmethod
+    def forward(ctx, x, res, act):
+        y, mean, rstd = instnorm_raw(x, None, res, act)
+        ctx.act = act
+        ctx.save_for_backward(x, res, mean, rstd)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, res, mean, rstd = ctx.saved_tensors
+        dx, dres, _ = instnorm_bwd_raw(dy, x, None, res, mean, rstd, ctx.act,
+                                       res is not None and ctx.needs_input_grad[1], False)
+        return dx, dres, None
+
+
+def instance_norm(x, act=None, res=None):
+    return InstanceNormFn.apply(x, res, act)
+
+
+# ------------------------------------------------------------------------------------------
+# MaxPool2d(k) with int32 plane-flat argmax
+# ------------------------------------------------------------------------------------------
+
+class MaxPoolFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, k):
+        x4, xbs = nchw(x)
+        N, C, H, W = x4.shape
+        Ho, Wo = H // k, W // k
+        y = _empty(N, C, Ho, Wo, x4)
+        idx = torch.empty((N, C, Ho, Wo), device=x4.device, dtype=torch.int32)
+        call("dsgan_maxpool_fwd", ptr(x4), xbs, ptr(y), C * Ho * Wo, ptr(idx), N, C, H, W, k, stream())
+        ctx.k, ctx.shape = k, (N, C, H, W)
+        ctx.save_for_backward(idx)
+        ctx.mark_non_differentiable(idx)
+        return y, idx
+
+    @staticmethod
+    def backward(ctx, dy, _didx):
+        (idx,) = ctx.saved_tensors
+        N, C, H, W = ctx.shape
+        dy4, dybs = nchw(dy)
+        dx = torch.empty((N, C, H, W), device=dy.device, dtype=torch.float32)
+        call("dsgan_maxpool_bwd", ptr(dy4), dybs, ptr(idx), ptr(dx), C * H * W, N, C, H, W, ctx.k, 0, stream())
+        return dx, None
+
+
+def max_pool2d(x, k, return_indices=False):
+    y, idx = MaxPoolFn.apply(x, k)
+    return (y, idx) if return_indices else y
+
+
+# ------------------------------------------------------------------------------------------
+# MidMLKA tail (MixConvNeXtML.py:112-116):  out = GELU( IN( v * CA(v) ) + x )
+# ------------------------------------------------------------------------------------------
+
+class MidTailFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, v, x, w1, pa, w2):
+        v4, vbs = nchw(v)
+        N, C, H, W = v4.shape
+        R = w1.shape[0]
+        avg = torch.empty(N * C, device=v.device, dtype=torch.float32)
+        mx = torch.empty_like(avg)
+        amax = torch.empty(N * C, device=v.device, dtype=torch.int32)
+        call("dsgan_plane_stats", ptr(v4), vbs, ptr(avg), ptr(mx), ptr(amax), N, C, H * W, stream())
+        att = torch.empty(N * C, device=v.device, dtype=torch.float32)
+        hsave = torch.empty(N * R * 2, device=v.device, dtype=torch.float32)
+        call("dsgan_ca_fwd", ptr(avg), ptr(mx), ptr(w1), ptr(w2), ptr(pa), ptr(att), ptr(hsave), N, C, R, stream())
+        y, mean, rstd = instnorm_raw(v4, att, x, "gelu")
+        ctx.save_for_backward(v4, x, w1, pa, w2, avg, mx, amax, att, hsave, mean, rstd)
+        ctx.refs = (w1, pa, w2)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        v, x, w1, pa, w2, avg, mx, amax, att, hsave, mean, rstd = ctx.saved_tensors
+        N, C, H, W = v.shape
+        R = w1.shape[0]
+        dv, dx, datt = instnorm_bwd_raw(dy, v, att, x, mean, rstd, "gelu", ctx.needs_input_grad[1], True)
+        davg = torch.empty(N * C, device=v.device, dtype=torch.float32)
+        dmx = torch.empty_like(davg)
+        w1r, par, w2r = ctx.refs
+        call("dsgan_ca_bwd", ptr(datt), ptr(att), ptr(avg), ptr(mx), ptr(hsave), ptr(w1), ptr(w2), ptr(pa),
+             ptr(davg), ptr(dmx), ptr(_grad_buf(w1r)), ptr(_grad_buf(w2r)), ptr(_grad_buf(par)), N, C, R, stream())
+        call("dsgan_plane_stats_bwd", ptr(davg), ptr(dmx), ptr(amax), ptr(dv), C * H * W, N, C, H * W, stream())
+        return dv, dx, None, None, None
+
+
+def mid_tail(v, x, w1, pa, w2):
+    """w1: CA.fc1 weight [C/8, C, 1, 1], pa: PReLU weight [1], w2: CA.fc2 weight [C, C/8, 1, 1]."""
+    return MidTailFn.apply(v, x, w1, pa, w2)
+
+
+# ------------------------------------------------------------------------------------------
+# n-ary add and channel concat
+# ------------------------------------------------------------------------------------------
+
+class AddNFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, *xs):
+        ts = [nchw(t) for t in xs]
+        N, C, H, W = ts[0][0].shape
+        out = _empty(N, C, H, W, ts[0][0])
+        import ctypes
+        arr = (ctypes.c_void_p * len(ts))(*[t.data_ptr() for t, _ in ts])
+        bss = (ctypes.c_long * len(ts))(*[bs for _, bs in ts])
+        call("dsgan_add_n", ctypes.cast(arr, ctypes.c_void_p), ctypes.cast(bss, ctypes.c_void_p), len(ts),
+             ptr(out), C * H * W, N, C * H * W, stream())
+        ctx.n = len(xs)
+        return out
+
+    @staticmethod
+    def backward(ctx, dy):
+        return tuple(dy for _ in range(ctx.n))
+
+
+def add_n(*xs):
+    return AddNFn.apply(*xs)
+
+
+class CatFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, a, b):
+        N, Ca, H, W = a.shape
+        Cb = b.shape[1]
+        out = _empty(N, Ca + Cb, H, W, a)
+        copy_into(out[:, :Ca], a)
+        copy_into(out[:, Ca:], b)
+        ctx.Ca = Ca
+        return out
+
+    @staticmethod
+    def backward(ctx, dy):
+        return dy[:, :ctx.Ca], dy[:, ctx.Ca:]
+
+
+def cat_channels(a, b):
+    return CatFn.apply(a, b)
+
+
+# ------------------------------------------------------------------------------------------
+# Losses (0-d device tensors; backward reads the upstream grad from device memory)
+# ------------------------------------------------------------------------------------------
+
+class BCELogitsFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, target):
+        x = x.contiguous()
+        out = torch.empty((), device=x.device, dtype=torch.float32)
+        call("dsgan_bce_logits_fwd", ptr(x), x.numel(), float(target), ptr(out), stream())
+        ctx.target = float(target)
+        ctx.save_for_backward(x)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        (x,) = ctx.saved_tensors
+        dx = torch.empty_like(x)
+        g = g.contiguous()
+        call("dsgan_bce_logits_bwd", ptr(x), x.numel(), ctx.target, ptr(g), ptr(dx), 0, stream())
+        return dx, None
+
+
+def bce_with_logits(x, target):
+    return BCELogitsFn.apply(x, target)
+
+
+class L1Fn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, a, b):
+        a, b = a.contiguous(), b.contiguous()
+        out = torch.empty((), device=a.device, dtype=torch.float32)
+        call("dsgan_l1_fwd", ptr(a), ptr(b), a.numel(), ptr(out), stream())
+        ctx.save_for_backward(a, b)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        a, b = ctx.saved_tensors
+        g = g.contiguous()
+        da = db = None
+        if ctx.needs_input_grad[0]:
+            da = torch.empty_like(a)
+            call("dsgan_l1_bwd", ptr(a), ptr(b), a.numel(), ptr(g), ptr(da), 0, stream())
+        if ctx.needs_input_grad[1]:
+            db = torch.empty_like(b)
+            call("dsgan_l1_bwd", ptr(b), ptr(a), b.numel(), ptr(g), ptr(db), 0, stream())
+        return da, db
+
+
+def l1_loss(a, b):
+    return L1Fn.apply(a, b)
+
+
+class TVFn(torch.autograd.Function):
+    """(sum|dW| + sum|dH|) * coef over the whole batch (pix2pix_model.py:189-191, coef=1/(320*256))."""
+
+    @staticmethod
+    def forward(ctx, y, coef):
+        y = y.contiguous()
+        N, C, H, W = y.shape
+        out = torch.empty((), device=y.device, dtype=torch.float32)
+        call("dsgan_tv_fwd", ptr(y), N * C, H, W, float(coef), ptr(out), stream())
+        ctx.coef = float(coef)
+        ctx.save_for_backward(y)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        (y,) = ctx.saved_tensors
+        N, C, H, W = y.shape
+        dy = torch.empty_like(y)
+        call("dsgan_tv_bwd", ptr(y), N * C, H, W, ctx.coef, ptr(g.contiguous()), ptr(dy), 0, stream())
+        return dy, None
+
+
+def tv_loss(y, coef=1.0 / (320 * 256)):
+    return TVFn.apply(y, coef)
+
+
+_WIN_CACHE = {}
+
+
+def gauss_win(device, size=11, sigma=1.5):
+    """_fspecial_gauss_1d (DSGAN/MS_SSIM.py:9-23), built in fp32 on the host, cached on device."""
+    key = (str(device), size, sigma)
+    if key not in _WIN_CACHE:
+        c = torch.arange(size, dtype=torch.float) - size // 2
+        g = torch.exp(-(c ** 2) / (2 * sigma ** 2))
+        _WIN_CACHE[key] = (g / g.sum()).to(device)
+    return _WIN_CACHE[key]
+
+
+class SSIMFn(torch.autograd.Function):
+    """mean SSIM of (a*real+b, a*fake+b) with data_range 1 (MS_SSIM.py:95-150); grad w.r.t. fake."""
+
+    @staticmethod
+    def forward(ctx, real, fake, a, b, data_range):
+        real, fake = real.contiguous(), fake.contiguous()
+        N, C, H, W = real.shape
+        Ho, Wo = H - 10, W - 10
+        coef = torch.empty((3, N * C, Ho, Wo), device=real.device, dtype=torch.float32)
+        s = torch.empty((), device=real.device, dtype=torch.float32)
+        win = gauss_win(real.device)
+        C1 = (0.01 * data_range) ** 2
+        C2 = (0.03 * data_range) ** 2
+        call("dsgan_ssim_fwd", ptr(real), ptr(fake), float(a), float(b), N * C, H, W, ptr(win),
+             float(C1), float(C2), ptr(coef), ptr(s), stream())
+        cnt = float(N * C * Ho * Wo)
+        ctx.save_for_backward(real, fake, coef)
+        ctx.ab, ctx.cnt = (float(a), float(b)), cnt
+        return s / cnt
+
+    @staticmethod
+    def backward(ctx, g):
+        real, fake, coef = ctx.saved_tensors
+        N, C, H, W = real.shape
+        dfake = torch.empty_like(fake)
+        call("dsgan_ssim_bwd", ptr(real), ptr(fake), ctx.ab[0], ctx.ab[1], N * C, H, W,
+             ptr(gauss_win(real.device)), ptr(coef), ptr(g.contiguous()), 1.0 / ctx.cnt, ptr(dfake), 0, stream())
+        return None, dfake, None, None, None
+
+
+def ssim_affine(real, fake, a=0.5, b=0.5, data_range=1.0):
+    return SSIMFn.apply(real, fake, a, b, data_range)

@@ -1,0 +1,207 @@
+"""MixConvNeXtML generator on libdsgan_hip.so (DSGAN/models/model/MixConvNeXtML.py).
+
+Module tree, attribute names, parameter shapes and registration order are those of the
+reference, so ``state_dict()`` keys match key-for-key (188 tensors) and reference checkpoints
+load as-is.  The torch ``nn.Conv2d`` / ``nn.Linear`` / ``nn.ConvTranspose2d`` / ``nn.PReLU``
+children are parameter *holders* only (their torch forward is never called): every forward
+below is a chain of fused HIP kernels from ``dsgan_hip.functional``.
+"""
+import torch
+import torch.nn as nn
+
+from dsgan_hip import functional as HF
+
+
+class CA(nn.Module):
+    """Channel attention, MixConvNeXtML.py:5-22 (computed inside HF.mid_tail)."""
+
+    def __init__(self, in_planes, ratio=8):
+        super().__init__()
+        self.fc1 = nn.Conv2d(in_planes, in_planes // ratio, 1, bias=False)
+        self.relu1 = nn.PReLU()
+        self.fc2 = nn.Conv2d(in_planes // ratio, in_planes, 1, bias=False)
+
+
+class upSample(nn.Module):
+    """ConvT 3x3/s2 -> IN -> GELU, then cat(skip) (MixConvNeXtML.py:48-66)."""
+
+    def __init__(self, in_channel, out_channel):
+        super().__init__()
+        self.model = nn.Sequential(nn.ConvTranspose2d(in_channel, out_channel, kernel_size=3, stride=2,
+                                                      padding=1, output_padding=1))
+
+    def forward(self, x, feature_map):
+        t = self.model[0]
+        u = HF.instance_norm(HF.conv_transpose3s2(x, t.weight, t.bias), act="gelu")
+        return HF.cat_channels(u, feature_map)
+
+
+class MidMLKA(nn.Module):
+    """MixConvNeXtML.py:76-117: chunk4 -> dw3/5/7/9 -> 1x1(+b) -> *CA -> IN -> +x -> GELU."""
+
+    def __init__(self, dim):
+        super().__init__()
+        self.dim = dim
+        self.conv = nn.Conv2d(dim, dim, kernel_size=1)
+        self.attn = CA(dim)
+        q = dim // 4
+        self.X3 = nn.Conv2d(q, q, 3, 1, 1, groups=q)
+        self.X5 = nn.Conv2d(q, q, 5, 1, 2, groups=q)
+        self.X7 = nn.Conv2d(q, q, 7, 1, 3, groups=q)
+        self.X9 = nn.Conv2d(q, q, 9, 1, 4, groups=q)
+
+    def forward(self, x):
+        d = HF.multi_dwconv(x, self.X3.weight, self.X3.bias, self.X5.weight, self.X5.bias,
+                            self.X7.weight, self.X7.bias, self.X9.weight, self.X9.bias)
+        v = HF.conv2d(d, self.conv.weight, self.conv.bias)
+        return HF.mid_tail(v, x, self.attn.fc1.weight, self.attn.relu1.weight, self.attn.fc2.weight)
+
+
+class OriginMLKA(nn.Module):
+    """The local (MLKA U-Net) branch, MixConvNeXtML.py:119-189."""
+
+    def __init__(self):
+        super().__init__()
+        self.to32 = nn.Conv2d(3, 32, kernel_size=1, bias=False)
+        self.mid32 = MidMLKA(32)
+        self.to64 = nn.Conv2d(32, 64, kernel_size=1, bias=False)
+        self.mid64 = MidMLKA(64)
+        self.to128 = nn.Conv2d(64, 128, kernel_size=1, bias=False)
+        self.mid128 = MidMLKA(128)
+        self.to256 = nn.Conv2d(128, 256, kernel_size=1, bias=False)
+        self.mid256 = MidMLKA(256)
+        self.up1 = upSample(256, 128)
+        self.upc1 = nn.Sequential(nn.Conv2d(256, 128, kernel_size=1, bias=False), MidMLKA(128))
+        self.up2 = upSample(128, 64)
+        self.upc2 = MidMLKA(128)
+        self.up3 = upSample(128, 64)
+        self.upc3 = MidMLKA(128)
+        self.up4 = nn.Sequential(nn.ConvTranspose2d(128, 64, kernel_size=3, stride=2, padding=1,
+                                                    output_padding=1))
+        self.shortcut = nn.Sequential(nn.Conv2d(3, 64, 1, bias=False))
+
+    def forward(self, x):
+        mp = lambda t: HF.max_pool2d(t, 2)
+        d1 = HF.conv2d(x, self.to32.weight)
+        d2 = self.mid32(mp(d1))
+        d3 = HF.conv2d(d2, self.to64.weight)
+        d4 = self.mid64(mp(d3))
+        d5 = HF.conv2d(d4, self.to128.weight)
+        d6 = self.mid128(mp(d5))
+        d7 = HF.conv2d(d6, self.to256.weight)
+        d8 = self.mid256(mp(d7))
+        u1 = self.upc1[1](HF.conv2d(self.up1(d8, d6), self.upc1[0].weight))
+        u2 = self.upc2(self.up2(u1, d4))
+        u3 = self.upc3(self.up3(u2, d3))
+        sc = HF.instance_norm(HF.conv2d(x, self.shortcut[0].weight))
+        t = self.up4[0]
+        # GELU(IN(up4(u3)) + IN(shortcut(x))): the add and GELU are fused into the second IN
+        return HF.instance_norm(HF.conv_transpose3s2(u3, t.weight, t.bias), act="gelu", res=sc)
+
+
+class Block(nn.Module):
+    """ConvNeXt block, MixConvNeXtML.py:203-243:
+    dw7x7(+b) -> IN -> Linear(C,4C)+b -> GELU -> Linear(4C,P)+b, + 1x1 shortcut(x)."""
+
+    def __init__(self, dim, plans):
+        super().__init__()
+        self.shortcut = nn.Conv2d(dim, plans, kernel_size=1, bias=False)
+        self.dwconv = nn.Conv2d(dim, dim, kernel_size=7, padding=3, groups=dim)
+        self.pwconv1 = nn.Linear(dim, 4 * dim)
+        self.pwconv2 = nn.Linear(4 * dim, plans)
+
+    def forward(self, x):
+        h = HF.instance_norm(HF.dwconv(x, self.dwconv.weight, self.dwconv.bias))
+        return HF.pw_mlp(h, x, self.pwconv1.weight, self.pwconv1.bias, self.pwconv2.weight,
+                         self.pwconv2.bias, self.shortcut.weight)
+
+
+def _skip(cin, cout, k):
+    # nn.Sequential(MaxPool2d(k), Conv2d 1x1, InstanceNorm2d, GELU): only index 1 holds params
+    return nn.Sequential(nn.MaxPool2d(kernel_size=k), nn.Conv2d(cin, cout, 1, bias=False),
+                         nn.InstanceNorm2d(cout), nn.GELU())
+
+
+def _skip_fwd(seq, x):
+    k = seq[0].kernel_size
+    return HF.instance_norm(HF.conv2d(HF.max_pool2d(x, k), seq[1].weight), act="gelu")
+
+
+class downSkip(nn.Module):
+    def __init__(self):
+        super().__init__()
+        self.to2, self.to4, self.to8, self.to16 = _skip(64, 128, 2), _skip(64, 256, 4), _skip(64, 512, 8), _skip(64, 1024, 16)
+
+    def forward(self, x):
+        return [_skip_fwd(s, x) for s in (self.to2, self.to4, self.to8, self.to16)]
+
+
+class downSkip128(nn.Module):
+    def __init__(self):
+        super().__init__()
+        self.to4, self.to8, self.to16 = _skip(128, 256, 2), _skip(128, 512, 4), _skip(128, 1024, 8)
+
+    def forward(self, x):
+        return [_skip_fwd(s, x) for s in (self.to4, self.to8, self.to16)]
+
+
+class downSkip256(nn.Module):
+    def __init__(self):
+        super().__init__()
+        self.to8, self.to16 = _skip(256, 512, 2), _skip(256, 1024, 4)
+
+    def forward(self, x):
+        return [_skip_fwd(s, x) for s in (self.to8, self.to16)]
+
+
+class downSkip512(nn.Module):
+    def __init__(self):
+        super().__init__()
+        self.to16 = _skip(512, 1024, 2)
+
+    def forward(self, x):
+        return [_skip_fwd(self.to16, x)]
+
+
+class MixConvNeXtML(nn.Module):
+    """MixConvNeXtML.py:428-494 -- default generator (--which_model_netG MixConvNeXtML)."""
+
+    def __init__(self):
+        super().__init__()
+        self.c1 = Block(3, 64)
+        self.c2 = Block(64, 128)
+        self.c3 = Block(128, 256)
+        self.c4 = Block(256, 512)
+        self.c5 = Block(512, 1024)
+        self.u1 = upSample(1024, 512)
+        self.uc1 = Block(1024, 512)
+        self.u2 = upSample(512, 256)
+        self.uc2 = Block(512, 256)
+        self.u3 = upSample(256, 128)
+        self.uc3 = Block(256, 128)
+        self.u4 = upSample(128, 64)
+        self.uc4 = Block(128, 64)
+        self.down64 = downSkip()
+        self.down128 = downSkip128()
+        self.down256 = downSkip256()
+        self.down512 = downSkip512()
+        self.local = OriginMLKA()
+        self.res = nn.Conv2d(64, 3, kernel_size=3, padding=1)
+
+    def forward(self, x):
+        mp = lambda t: HF.max_pool2d(t, 2)
+        R1 = self.c1(x)
+        R2 = self.c2(mp(R1))
+        R3 = self.c3(mp(R2))
+        R4 = self.c4(mp(R3))
+        R5 = self.c5(mp(R4))
+        s64 = self.down64(R1)
+        s128 = self.down128(R2)
+        s256 = self.down256(R3)
+        s512 = self.down512(R4)
+        O1 = self.uc1(self.u1(HF.add_n(R5, s64[3], s128[2], s256[1], s512[0]), R4))
+        O2 = self.uc2(self.u2(HF.add_n(O1, s64[2], s128[1], s256[0]), R3))
+        O3 = self.uc3(self.u3(HF.add_n(O2, s64[1], s128[0]), R2))
+        O4 = self.uc4(self.u4(HF.add_n(O3, s64[0]), R1))
+        Loc = self.local(x)
+        return HF.conv2d(HF.add_n(O4, Loc), self.res.weight, self.res.bias, stride=1, pad=1)

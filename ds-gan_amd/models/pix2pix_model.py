@@ -1,0 +1,158 @@
+"""The DS-GAN train step (DSGAN/models/pix2pix_model.py), MI355X-native.
+
+``--model pix2pix`` resolves here through the same registry rule as the reference, and the
+class keeps the reference's API: ``initialize / set_input / forward / backward_D /
+backward_G / optimize_parameters / get_img_tir / get_img_gen / get_img_label`` plus the
+``loss_*`` / ``real_A`` / ``fake_B`` / ``real_B`` / ``netG`` / ``netD`` / ``optimizers``
+attributes that ``train.py`` reads.
+
+What runs underneath: every forward/backward op is a fused HIP kernel (``dsgan_hip``), params
+and grads of each network live in one flat buffer updated by one fused-Adam launch, and under
+``torchrun`` the two gradient exchanges are RCCL all-reduces (``dsgan_hip.dist``).
+
+Deliberate, documented deviations:
+  * q1: untyped loss-weight flags are cast to numbers (the reference crashes on CLI values);
+  * multi-GPU: per-rank ImagePool; the TV term (a batch *sum*, :189-191) is scaled by the world
+    size so averaged gradients equal the reference's global-batch gradient;
+  * the unused VGG relu5_3 block is not computed (the loss never reads it, :182-186).
+"""
+import torch
+
+from dsgan_hip import functional as HF
+from dsgan_hip import dist as hdist
+from dsgan_hip.flat import FlatParams, FlatAdam
+from util.image_pool import ImagePool
+from .base_model import BaseModel
+from . import networks
+from .vgg import Vgg16
+
+
+class Pix2PixModel(BaseModel):
+    def name(self):
+        return "Pix2PixModel"
+
+    @staticmethod
+    def modify_commandline_options(parser, is_train=True):
+        if is_train:
+            parser.add_argument("--lambda_L1", type=float, default=100.0, help="weight for L1 loss")
+        return parser
+
+    def initialize(self, opt):
+        BaseModel.initialize(self, opt)
+        if self.device.type != "cuda":
+            raise RuntimeError("Pix2PixModel (MI355X build) needs a ROCm GPU: set --gpu_ids; "
+                               "there is no CPU execution path")
+        HF.set_precision(getattr(opt, "precision", "fp32"))
+        self.isTrain = opt.isTrain
+        self.loss_names = ["G_GAN", "G_L1", "D_real", "D_fake"]
+        self.visual_names = ["real_A", "fake_B", "real_B"]
+        self.model_names = ["G", "D"] if self.isTrain else ["G"]
+        self.use_gan = int(opt.use_GAN)
+        self.w_vgg = float(opt.w_vgg)
+        self.w_tv = float(opt.w_tv)
+        self.w_gan = float(opt.w_gan)
+        self.w_ss = float(opt.w_ss)
+        self.use_condition = int(opt.use_condition)
+        self.netG = networks.define_G(opt.input_nc, opt.output_nc, opt.ngf, opt.which_model_netG,
+                                      opt.norm, not opt.no_dropout, opt.init_type, self.gpu_ids)
+        if self.isTrain:
+            use_sigmoid = opt.no_lsgan
+            d_in = opt.input_nc + opt.output_nc if self.use_condition == 1 else opt.input_nc
+            self.netD = networks.define_D(d_in, opt.ndf, opt.which_model_netD, opt.n_layers_D,
+                                          opt.norm, use_sigmoid, opt.init_type, self.gpu_ids)
+        if self.isTrain:
+            self.fake_AB_pool = ImagePool(opt.pool_size)
+            self.criterionGAN = networks.GANLoss(use_lsgan=opt.no_lsgan).to(self.device)
+            self.criterionL1 = HF.l1_loss
+            self.vgg = Vgg16(getattr(opt, "vgg_weights", "") or None).to(self.device)
+            # flat param/grad buffers + fused Adam (one launch per network per step)
+            self.flatG = FlatParams(self.netG, self.device)
+            self.flatD = FlatParams(self.netD, self.device)
+            hdist.broadcast_params(self.flatG)
+            hdist.broadcast_params(self.flatD)
+            self.optimizers = []
+            self.optimizer_G = FlatAdam(self.flatG, lr=opt.lr, betas=(opt.beta1, 0.999))
+            self.optimizer_D = FlatAdam(self.flatD, lr=opt.lr, betas=(opt.beta1, 0.999))
+            self.optimizers.append(self.optimizer_G)
+            self.optimizers.append(self.optimizer_D)
+            self.tv_scale = float(hdist.world_size())
+
+    def set_input(self, input):
+        AtoB = self.opt.which_direction == "AtoB"
+        self.real_A = input["A" if AtoB else "B"].to(self.device, non_blocking=True)
+        self.real_B = input["B" if AtoB else "A"].to(self.device, non_blocking=True)
+        self.image_paths = input["A_paths" if AtoB else "B_paths"]
+
+    def forward(self):
+        self.fake_B = self.netG(self.real_A)
+
+    def backward_D(self):
+        if self.use_condition == 1:
+            fake_AB = self.fake_AB_pool.query(HF.cat_channels(self.real_A, self.fake_B.detach()))
+        else:
+            fake_AB = self.fake_B
+        pred_fake = self.netD(fake_AB.detach())
+        self.loss_D_fake = self.criterionGAN(pred_fake, False)
+        real_AB = HF.cat_channels(self.real_A, self.real_B) if self.use_condition == 1 else self.real_B
+        pred_real = self.netD(real_AB)
+        self.loss_D_real = self.criterionGAN(pred_real, True)
+        self.loss_D = (self.loss_D_fake + self.loss_D_real) * 0.5
+        self.loss_D.backward()
+
+    def backward_G(self):
+        if self.use_gan == 1:
+            fake_AB = HF.cat_channels(self.real_A, self.fake_B) if self.use_condition == 1 else self.fake_B
+            self.loss_G_GAN = self.criterionGAN(self.netD(fake_AB), True)
+        else:
+            self.loss_G_GAN = 0
+        self.loss_G_L1 = self.criterionL1(self.fake_B, self.real_B)
+        with torch.no_grad():
+            self.real_B_features = self.vgg(self.real_B)
+        self.fake_B_features = self.vgg(self.fake_B)
+        f, r = self.fake_B_features, self.real_B_features
+        self.loss_vgg = (self.criterionL1(f[1], r[1]) + self.criterionL1(f[2], r[2])
+                         + self.criterionL1(f[3], r[3]) + self.criterionL1(f[0], r[0]))
+        self.tv_loss = HF.tv_loss(self.fake_B, self.tv_scale / (320 * 256))
+        # 1 - ssim((real_B+1)/2, (fake_B+1)/2, data_range=1): the affine map is fused in-kernel
+        self.loss_ssim = 1 - HF.ssim_affine(self.real_B, self.fake_B, 0.5, 0.5, 1.0)
+        self.loss_G = (self.loss_G_GAN * self.w_gan + self.loss_G_L1 + self.loss_vgg * self.w_vgg
+                       + self.tv_loss * self.w_tv + self.w_ss * self.loss_ssim)
+        self.loss_G.backward()
+
+    def optimize_parameters(self):
+        self.forward()
+        if self.use_gan == 1:
+            self.set_requires_grad(self.netD, True)
+            self.optimizer_D.zero_grad()
+            self.backward_D()
+            hdist.allreduce_mean_(self.flatD.grad)
+            self.optimizer_D.step()
+        else:
+            self.loss_D_fake = 0
+            self.loss_D_real = 0
+        self.set_requires_grad(self.netD, False)
+        self.optimizer_G.zero_grad()
+        self.backward_G()
+        hdist.allreduce_mean_(self.flatG.grad)
+        self.optimizer_G.step()
+
+    # ---- train.py helpers (DSGAN/models/pix2pix_model.py:292-310) ----
+    def get_img_tir(self, input):
+        self.real_A = input["A"].to(self.device)
+        return ((self.real_A + 1) / 2) * 255
+
+    def get_img_gen(self, input):
+        AtoB = self.opt.which_direction == "AtoB"
+        self.real_B = input["B" if AtoB else "A"].to(self.device)
+        self.fake_B = self.netG(self.real_A)
+        return ((self.fake_B + 1) / 2) * 255
+
+    def get_img_label(self, input):
+        AtoB = self.opt.which_direction == "AtoB"
+        self.real_B = input["B" if AtoB else "A"].to(self.device)
+        return ((self.real_B + 1) / 2) * 255
+
+    def get_img_nir(self, input):
+        AtoB = self.opt.which_direction == "AtoB"
+        self.real_A = input["A" if AtoB else "B"].to(self.device)
+        return ((self.real_A + 1) / 2) * 255

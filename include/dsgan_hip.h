@@ -1,0 +1,137 @@
+/*
+ * dsgan_hip.h -- C ABI of libdsgan_hip.so, the MI355X (gfx950) kernels of the DS-GAN
+ * G+D train step.
+ *
+ * The reference (yglbgyx/DS-GAN) has no native code: its hot path is PyTorch modules whose
+ * math runs in cuDNN/cuBLAS/ATen.  Each entry point below replaces the reference op(s) cited
+ * next to it (paths relative to the reference's DSGAN/ directory).  The binding the reference
+ * side would add is the ctypes table in ds-gan_amd/dsgan_hip/_lib.py.
+ *
+ * Conventions
+ *   - All tensors are caller-owned device pointers (fp32 unless stated), NCHW activations,
+ *     OIHW weights.  `*_bs` = batch stride in elements (lets a channel slice of a concat
+ *     buffer be read/written in place).  No allocation happens inside the library.
+ *   - Every call is asynchronous on `stream` and returns 0, or a hipError_t / -1 with a
+ *     message available from dsgan_last_error_string().
+ *   - Weight-gradient entry points ACCUMULATE (+=) into their outputs: the caller zeroes the
+ *     flat gradient buffer once per optimizer step, exactly like autograd's accumulation.
+ *   - act codes: 0 none, 1 GELU (erf), 2 ReLU, 3 LeakyReLU(slope), 4 sigmoid.
+ *   - prec: 0 = exact f32 MFMA (v_mfma_f32_32x32x2_f32), 1 = bf16 MFMA operands with fp32
+ *     accumulation (v_mfma_f32_32x32x16_bf16).
+ */
+#ifndef DSGAN_HIP_H
+#define DSGAN_HIP_H
+
+#include <hip/hip_runtime.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+int dsgan_abi_version(void);
+const char* dsgan_last_error_string(void);
+
+/* ---- implicit-GEMM convolution (igemm.hip) ------------------------------------------------
+ * Replaces nn.Conv2d / nn.Linear / nn.ConvTranspose2d forward+backward:
+ *   Block.pwconv1/2 + shortcut   models/model/MixConvNeXtML.py:218-242
+ *   1x1 convs (downSkip*, OriginMLKA, MidMLKA.conv)  :85,122-157,334-419
+ *   ConvTranspose2d 3x3 s2       :53,150   (fwd = dsgan_conv_dgrad, dgrad = dsgan_conv_fwd)
+ *   res 3x3 head                 :459
+ *   PatchGAN 4x4 s2/s1           models/networks.py:543-569
+ *   VGG16 3x3 + ReLU             models/vgg.py:15-24
+ * y = act(conv(x, w) + bias) [+ y if accumulate]; ypre (nullable) receives the pre-activation. */
+int dsgan_conv_fwd(const float* x, long x_bs, const float* w, const float* bias, float* y,
+                   long y_bs, float* ypre, long ypre_bs, int N, int Cin, int H, int W, int Cout,
+                   int KH, int KW, int stride, int pad, int Ho, int Wo, int act, float slope,
+                   int accumulate, int prec, hipStream_t stream);
+/* dx = conv^T(dy, w) (+bias) ; if gpre: dx *= act'(gpre) with act code gact (fuses the
+ * backward of the activation that produced the conv input). */
+int dsgan_conv_dgrad(const float* dy, long dy_bs, const float* w, const float* bias, float* dx,
+                     long dx_bs, float* ypre, long ypre_bs, const float* gpre, long gpre_bs,
+                     int gact, int N, int Cin, int H, int W, int Cout, int KH, int KW, int stride,
+                     int pad, int Ho, int Wo, int act, float slope, int accumulate, int prec,
+                     hipStream_t stream);
+/* dw[Cout][Cin][KH][KW] += sum_{n,oh,ow} dy * x  (split-K, fp32 atomics) */
+int dsgan_conv_wgrad(const float* dy, long dy_bs, const float* x, long x_bs, float* dw, int N,
+                     int Cin, int H, int W, int Cout, int KH, int KW, int stride, int pad, int Ho,
+                     int Wo, int prec, hipStream_t stream);
+
+/* ---- depthwise conv (dwconv.hip): Block.dwconv :220, MidMLKA.X3..X9 :94-97 ---------------- */
+int dsgan_dwconv_fwd(const float* x, long x_bs, const float* w, const float* bias, float* y,
+                     long y_bs, int N, int C, int H, int W, int K, int flip, hipStream_t stream);
+int dsgan_dwconv_wgrad(const float* dy, long dy_bs, const float* x, long x_bs, float* dw,
+                       float* db, int N, int C, int H, int W, int K, hipStream_t stream);
+
+/* ---- InstanceNorm2d(affine=False, eps) fused with per-plane scale, residual and activation
+ * (norm_pointwise.hip): nn.InstanceNorm2d at MixConvNeXtML.py:54,80,113-116,151,158,221,
+ * 335-420 and networks.py:556,565.  y = act(IN(scale*x) + res). */
+int dsgan_instnorm_fwd(const float* x, long x_bs, const float* scale, const float* res,
+                       long res_bs, float* y, long y_bs, float* mean, float* rstd, int N, int C,
+                       int HW, int act, float slope, float eps, hipStream_t stream);
+int dsgan_instnorm_bwd(const float* dy, long dy_bs, const float* x, long x_bs, const float* scale,
+                       const float* res, long res_bs, const float* mean, const float* rstd,
+                       float* dx, long dx_bs, float* dres, long dres_bs, float* dscale, int N,
+                       int C, int HW, int act, float slope, float eps, hipStream_t stream);
+
+/* ---- MaxPool2d(k) with int32 plane-flat argmax (bit-exact with torch's indices):
+ * downSample :68-74, downSkip* :333-417, OriginMLKA :123-136, VGG pools vgg.py. */
+int dsgan_maxpool_fwd(const float* x, long x_bs, float* y, long y_bs, int* idx, int N, int C,
+                      int H, int W, int k, hipStream_t stream);
+int dsgan_maxpool_bwd(const float* dy, long dy_bs, const int* idx, float* dx, long dx_bs, int N,
+                      int C, int H, int W, int k, int accumulate, hipStream_t stream);
+
+/* ---- channel attention CA (MixConvNeXtML.py:5-22) --------------------------------------- */
+int dsgan_plane_stats(const float* x, long x_bs, float* avg, float* mx, int* amax, int N, int C,
+                      int HW, hipStream_t stream);
+int dsgan_plane_stats_bwd(const float* davg, const float* dmx, const int* amax, float* dx,
+                          long dx_bs, int N, int C, int HW, hipStream_t stream);
+int dsgan_ca_fwd(const float* avg, const float* mx, const float* w1, const float* w2,
+                 const float* prelu_a, float* att, float* hsave, int N, int C, int R,
+                 hipStream_t stream);
+int dsgan_ca_bwd(const float* datt, const float* att, const float* avg, const float* mx,
+                 const float* hsave, const float* w1, const float* w2, const float* prelu_a,
+                 float* davg, float* dmx, float* dw1, float* dw2, float* dprelu_a, int N, int C,
+                 int R, hipStream_t stream);
+
+/* ---- elementwise / reductions ------------------------------------------------------------
+ * add_n: the decoder skip sums MixConvNeXtML.py:482-492; copy_strided: torch.cat :66;
+ * channel_sum: conv/linear bias gradients; act_bwd: ReLU/LeakyReLU/GELU backward. */
+int dsgan_add_n(const float* const* ins, const long* in_bs, int nin, float* out, long out_bs,
+                int N, long E, hipStream_t stream);
+int dsgan_copy_strided(const float* src, long src_bs, float* dst, long dst_bs, int N, long E,
+                       hipStream_t stream);
+int dsgan_fill(float* p, float v, long n, hipStream_t stream);
+int dsgan_scale(float* p, float a, long n, hipStream_t stream);
+int dsgan_act_bwd(const float* dy, const float* pre, float* dx, long n, int act, float slope,
+                  int accumulate, hipStream_t stream);
+int dsgan_channel_sum(const float* dy, long dy_bs, float* out, int N, int C, int HW,
+                      hipStream_t stream);
+
+/* ---- losses (losses.hip): scalars written to device memory, upstream grads read from it ----
+ * GANLoss/BCEWithLogits networks.py:143-163; L1 pix2pix_model.py:177,182-186;
+ * TV :189-191; ssim MS_SSIM.py:95-150 (coef: 3*planes*(H-10)*(W-10) floats of scratch). */
+int dsgan_bce_logits_fwd(const float* x, long n, float target, float* out, hipStream_t stream);
+int dsgan_bce_logits_bwd(const float* x, long n, float target, const float* gout, float* dx,
+                         int accumulate, hipStream_t stream);
+int dsgan_l1_fwd(const float* a, const float* b, long n, float* out, hipStream_t stream);
+int dsgan_l1_bwd(const float* a, const float* b, long n, const float* gout, float* da,
+                 int accumulate, hipStream_t stream);
+int dsgan_tv_fwd(const float* y, long planes, int H, int W, float coef, float* out,
+                 hipStream_t stream);
+int dsgan_tv_bwd(const float* y, long planes, int H, int W, float coef, const float* gout,
+                 float* dy, int accumulate, hipStream_t stream);
+int dsgan_ssim_fwd(const float* real, const float* fake, float a, float b, int planes, int H,
+                   int W, const float* win11, float C1, float C2, float* coef, float* out,
+                   hipStream_t stream);
+int dsgan_ssim_bwd(const float* real, const float* fake, float a, float b, int planes, int H,
+                   int W, const float* win11, const float* coef, const float* gout, float gcoef,
+                   float* dfake, int accumulate, hipStream_t stream);
+
+/* ---- fused Adam over a flat buffer (adam.hip): torch.optim.Adam pix2pix_model.py:122-125 -- */
+int dsgan_adam(float* p, const float* g, float* m, float* v, long n, float lr, float beta1,
+               float beta2, float eps, int step, hipStream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DSGAN_HIP_H */

@@ -1,0 +1,93 @@
+"""Host-side logic on CPU: the options/models plugin surface mirrors the reference (flag names,
+defaults, registry rule, state_dict keys), LR schedule, and the data-parallel gradient exchange
+(gloo, world_size 2)."""
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_option_defaults_match_reference():
+    from options.train_options import TrainOptions
+    ref = json.load(open(os.path.join(REPO, "tests", "golden", "train_option_defaults.json")))
+    opt = vars(TrainOptions().gather_options([]))
+    for k, v in ref.items():
+        assert k in opt, k
+        mine = opt[k]
+        if isinstance(v, str) and v == "inf":
+            assert mine == float("inf"), k
+        else:
+            assert mine == v, (k, mine, v)
+
+
+def test_registry_rule():
+    from models import find_model_using_name
+    from models.pix2pix_model import Pix2PixModel
+    assert find_model_using_name("pix2pix") is Pix2PixModel
+
+
+def test_state_dict_keys_match_reference(golden):
+    from models.networks import define_G, define_D
+    from models.vgg import Vgg16
+    g = define_G(3, 3, 32, "MixConvNeXtML", "instance", False, "normal", [])
+    d = define_D(6, 32, "basic", 3, "instance", False, "normal", [])
+    assert list(g.state_dict().keys()) == list(golden["g_keys"])
+    assert [json.dumps(list(v.shape)) for v in g.state_dict().values()] == list(golden["g_shapes"])
+    assert list(d.state_dict().keys()) == list(golden["d_keys"])
+    assert list(Vgg16().state_dict().keys()) == list(golden["vgg_keys"])
+    assert abs(sum(p.numel() for p in g.parameters()) / 1e6 - 22.425) < 1e-3
+    assert abs(sum(p.numel() for p in d.parameters()) / 1e6 - 0.696) < 1e-3
+
+
+def test_unknown_networks_raise():
+    from models.networks import define_G, define_D
+    with pytest.raises(NotImplementedError):
+        define_G(3, 3, 32, "unet_256")
+    with pytest.raises(NotImplementedError):
+        define_D(6, 32, "nope")
+
+
+def test_lambda_lr_schedule(golden):
+    from argparse import Namespace
+    from models.networks import get_scheduler
+    opt = Namespace(lr_policy="lambda", epoch_count=1, niter=10, niter_decay=10)
+    sgd = torch.optim.SGD([torch.zeros(1, requires_grad=True)], lr=1.0)
+    sch = get_scheduler(sgd, opt)
+    m = []
+    for _ in range(21):
+        m.append(sgd.param_groups[0]["lr"])
+        sgd.step()
+        sch.step()
+    assert np.allclose(m, golden["lr_mults"])
+
+
+def _ddp_worker(rank, world, port, q):
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from dsgan_hip import dist as hdist
+    buf = torch.arange(10, dtype=torch.float32) * (rank + 1)
+    hdist.allreduce_mean_(buf, bucket_mb=1e-5)   # many tiny buckets
+    q.put((rank, buf.tolist()))
+    dist.destroy_process_group()
+
+
+def test_allreduce_mean_gloo_world2():
+    import multiprocessing as mp
+    import random as _r
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29500 + _r.randint(0, 2000)
+    ps = [ctx.Process(target=_ddp_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    out = dict(q.get(timeout=120) for _ in ps)
+    for p in ps:
+        p.join(timeout=60)
+    expect = (torch.arange(10, dtype=torch.float32) * 1.5).tolist()
+    assert out[0] == expect and out[1] == expect

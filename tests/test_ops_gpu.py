@@ -1,0 +1,338 @@
+"""Per-kernel parity: every HIP op (through the C-ABI) vs the same op on PyTorch-CPU fp32/fp64,
+i.e. the exact CPU math the reference runs (DSGAN's modules are torch ops).
+
+fp32 mode (exact f32 MFMA) must match to ~1e-5 relative; bf16 mode (bf16 operands, fp32
+accumulation) to the bf16 rounding bar stated per test.  Index tensors are bit-exact.
+"""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _lib():
+    import dsgan_hip
+    dsgan_hip.require_gpu()
+    yield
+    dsgan_hip.set_precision("fp32")
+
+
+def rel(a, b):
+    a = a.detach().double().cpu()
+    b = b.detach().double().cpu()
+    return ((a - b).norm() / max(b.norm().item(), 1e-30)).item()
+
+
+def _leaf(t):
+    return t.detach().clone().to(DEV).requires_grad_(True)
+
+
+def _param(t):
+    p = torch.nn.Parameter(t.detach().clone().to(DEV))
+    p.grad = torch.zeros_like(p)
+    return p
+
+
+TOL = {"fp32": 2e-5, "bf16": 1.5e-2}
+
+
+def _q(t, prec):
+    """bf16 mode rounds MFMA operands to bf16: the reference sees the same rounded operands, so
+    activation masks agree and the bar measures accumulation/rounding only."""
+    return t.bfloat16().float() if prec == "bf16" else t
+
+
+@pytest.mark.parametrize("prec", ["fp32", "bf16"])
+@pytest.mark.parametrize("N,Cin,H,W,Cout,K,s,p", [
+    (2, 3, 16, 16, 12, 1, 1, 0),       # c1.pwconv1 shape class (K tiny)
+    (2, 64, 16, 16, 256, 1, 1, 0),
+    (3, 130, 9, 7, 70, 1, 1, 0),       # ragged M/N/K tails
+    (2, 3, 20, 20, 64, 3, 1, 1),       # VGG conv1_1 (K=27)
+    (2, 64, 18, 18, 128, 3, 1, 1),
+    (2, 64, 16, 16, 3, 3, 1, 1),       # G head 64->3
+    (2, 6, 32, 32, 32, 4, 2, 1),       # PatchGAN layer 0
+    (2, 64, 16, 16, 128, 4, 2, 1),
+    (2, 128, 9, 9, 256, 4, 1, 1),      # PatchGAN s1 layers
+    (2, 256, 8, 8, 1, 4, 1, 1),
+])
+def test_conv2d(prec, N, Cin, H, W, Cout, K, s, p):
+    from dsgan_hip import functional as HF
+    HF.set_precision(prec)
+    g = torch.Generator().manual_seed(N * 1000 + Cin + Cout + K)
+    x = torch.randn(N, Cin, H, W, generator=g)
+    w = torch.randn(Cout, Cin, K, K, generator=g) / math.sqrt(Cin * K * K)
+    b = torch.randn(Cout, generator=g) * 0.1
+    x, w = _q(x, prec), _q(w, prec)
+    for act in (None, "lrelu", "relu"):
+        xr, wr, br = x.clone().requires_grad_(), w.clone().requires_grad_(), b.clone().requires_grad_()
+        y_ref = F.conv2d(xr, wr, br, stride=s, padding=p)
+        if act == "lrelu":
+            y_ref = F.leaky_relu(y_ref, 0.2)
+        elif act == "relu":
+            y_ref = F.relu(y_ref)
+        gy = torch.randn(y_ref.shape, generator=g)
+        y_ref.backward(gy)
+        xd, wd, bd = _leaf(x), _param(w), _param(b)
+        y = HF.conv2d(xd, wd, bd, stride=s, pad=p, act=act)
+        y.backward(gy.to(DEV))
+        torch.cuda.synchronize()
+        tol = TOL[prec]
+        assert rel(y, y_ref) < tol, ("fwd", act)
+        assert rel(xd.grad, xr.grad) < tol * 2, ("dgrad", act)
+        assert rel(wd.grad, wr.grad) < tol * 2, ("wgrad", act)
+        assert rel(bd.grad, br.grad) < max(1e-5, tol), ("bgrad", act)
+
+
+@pytest.mark.parametrize("prec", ["fp32", "bf16"])
+@pytest.mark.parametrize("N,Ci,Co,H", [(2, 64, 32, 8), (2, 128, 64, 5), (1, 256, 128, 16)])
+def test_conv_transpose(prec, N, Ci, Co, H):
+    from dsgan_hip import functional as HF
+    HF.set_precision(prec)
+    g = torch.Generator().manual_seed(Ci + Co + H)
+    x = _q(torch.randn(N, Ci, H, H + 1, generator=g), prec)
+    w = _q(torch.randn(Ci, Co, 3, 3, generator=g) / math.sqrt(Ci * 9), prec)
+    b = torch.randn(Co, generator=g) * 0.1
+    xr, wr, br = x.clone().requires_grad_(), w.clone().requires_grad_(), b.clone().requires_grad_()
+    y_ref = F.conv_transpose2d(xr, wr, br, stride=2, padding=1, output_padding=1)
+    gy = torch.randn(y_ref.shape, generator=g)
+    y_ref.backward(gy)
+    xd, wd, bd = _leaf(x), _param(w), _param(b)
+    y = HF.conv_transpose3s2(xd, wd, bd)
+    y.backward(gy.to(DEV))
+    tol = TOL[prec]
+    assert y.shape == y_ref.shape
+    assert rel(y, y_ref) < tol
+    assert rel(xd.grad, xr.grad) < 2 * tol
+    assert rel(wd.grad, wr.grad) < 2 * tol
+    assert rel(bd.grad, br.grad) < 1e-5
+
+
+@pytest.mark.parametrize("prec", ["fp32", "bf16"])
+@pytest.mark.parametrize("N,C,H,P", [(2, 3, 16, 64), (2, 64, 8, 128), (2, 128, 12, 64)])
+def test_pw_mlp(prec, N, C, H, P):
+    """Block tail: shortcut(x) + W2 gelu(W1 h + b1) + b2 (MixConvNeXtML.py:236-242)."""
+    from dsgan_hip import functional as HF
+    HF.set_precision(prec)
+    g = torch.Generator().manual_seed(C + P)
+    h = _q(torch.randn(N, C, H, H, generator=g), prec)
+    x = _q(torch.randn(N, C, H, H, generator=g), prec)
+    w1 = _q(torch.randn(4 * C, C, generator=g) / math.sqrt(C), prec)
+    b1 = torch.randn(4 * C, generator=g) * 0.1
+    w2 = _q(torch.randn(P, 4 * C, generator=g) / math.sqrt(4 * C), prec)
+    b2 = torch.randn(P, generator=g) * 0.1
+    ws = _q(torch.randn(P, C, 1, 1, generator=g) / math.sqrt(C), prec)
+    R = [t.clone().requires_grad_() for t in (h, x, w1, b1, w2, b2, ws)]
+    t = F.linear(R[0].permute(0, 2, 3, 1), R[2], R[3])
+    t = F.linear(F.gelu(t), R[4], R[5]).permute(0, 3, 1, 2)
+    y_ref = F.conv2d(R[1], R[6]) + t
+    gy = torch.randn(y_ref.shape, generator=g)
+    y_ref.backward(gy)
+    hd, xd = _leaf(h), _leaf(x)
+    P_ = [_param(t) for t in (w1, b1, w2, b2, ws)]
+    y = HF.pw_mlp(hd, xd, *P_)
+    y.backward(gy.to(DEV))
+    tol = TOL[prec]
+    assert rel(y, y_ref) < tol
+    assert rel(hd.grad, R[0].grad) < 2 * tol
+    assert rel(xd.grad, R[1].grad) < 2 * tol
+    for pd, pr in zip(P_, R[2:]):
+        assert rel(pd.grad, pr.grad) < 2 * tol
+
+
+@pytest.mark.parametrize("K", [3, 5, 7, 9])
+@pytest.mark.parametrize("N,C,H,W", [(2, 4, 16, 16), (2, 3, 40, 37), (1, 2, 4, 4), (2, 8, 70, 65)])
+def test_dwconv(K, N, C, H, W):
+    from dsgan_hip import functional as HF
+    g = torch.Generator().manual_seed(K * 100 + C + H)
+    x = torch.randn(N, C, H, W, generator=g)
+    w = torch.randn(C, 1, K, K, generator=g) / K
+    b = torch.randn(C, generator=g)
+    xr, wr, br = x.clone().requires_grad_(), w.clone().requires_grad_(), b.clone().requires_grad_()
+    y_ref = F.conv2d(xr, wr, br, padding=K // 2, groups=C)
+    gy = torch.randn(y_ref.shape, generator=g)
+    y_ref.backward(gy)
+    xd, wd, bd = _leaf(x), _param(w), _param(b)
+    y = HF.dwconv(xd, wd, bd)
+    y.backward(gy.to(DEV))
+    assert rel(y, y_ref) < 1e-5
+    assert rel(xd.grad, xr.grad) < 1e-5
+    assert rel(wd.grad, wr.grad) < 1e-5
+    assert rel(bd.grad, br.grad) < 1e-5
+
+
+@pytest.mark.parametrize("act", [None, "gelu", "lrelu"])
+@pytest.mark.parametrize("res", [False, True])
+@pytest.mark.parametrize("N,C,H,W", [(2, 3, 4, 4), (2, 5, 33, 31), (1, 2, 80, 80), (2, 4, 16, 16)])
+def test_instance_norm(act, res, N, C, H, W):
+    from dsgan_hip import functional as HF
+    g = torch.Generator().manual_seed(C * H + W)
+    x = torch.randn(N, C, H, W, generator=g) * 3 + 1
+    r = torch.randn(N, C, H, W, generator=g)
+    xr = x.clone().requires_grad_()
+    rr = r.clone().requires_grad_()
+    y_ref = F.instance_norm(xr, eps=1e-5) + (rr if res else 0)
+    y_ref = {None: lambda t: t, "gelu": F.gelu, "lrelu": lambda t: F.leaky_relu(t, 0.2)}[act](y_ref)
+    gy = torch.randn(y_ref.shape, generator=g)
+    y_ref.backward(gy)
+    xd, rd = _leaf(x), _leaf(r)
+    y = HF.instance_norm(xd, act=act, res=rd if res else None)
+    y.backward(gy.to(DEV))
+    assert rel(y, y_ref) < 1e-5
+    assert rel(xd.grad, xr.grad) < 1e-4
+    if res:
+        assert rel(rd.grad, rr.grad) < 1e-5
+
+
+@pytest.mark.parametrize("k", [2, 4, 8, 16])
+def test_maxpool_indices_bit_exact(k):
+    from dsgan_hip import functional as HF
+    g = torch.Generator().manual_seed(k)
+    x = torch.randn(2, 3, 32, 48, generator=g)
+    x[0, 0, :4, :4] = 1.5  # ties: first max in row-major window order wins
+    xr = x.clone().requires_grad_()
+    y_ref, i_ref = F.max_pool2d(xr, k, return_indices=True)
+    gy = torch.randn(y_ref.shape, generator=g)
+    y_ref.backward(gy)
+    xd = _leaf(x)
+    y, idx = HF.max_pool2d(xd, k, return_indices=True)
+    y.backward(gy.to(DEV))
+    assert torch.equal(y.cpu(), y_ref.detach())
+    assert torch.equal(idx.cpu().long(), i_ref)
+    assert torch.equal(xd.grad.cpu(), xr.grad)
+
+
+@pytest.mark.parametrize("C,H", [(32, 16), (128, 8), (256, 4)])
+def test_mid_tail(C, H):
+    """GELU(IN(v * CA(v)) + x) (MixConvNeXtML.py:112-116, CA :18-22) fwd + all grads."""
+    from dsgan_hip import functional as HF
+    from oracle.dsgan_cpu import ca_fwd
+    g = torch.Generator().manual_seed(C)
+    N, R = 2, C // 8
+    v = torch.randn(N, C, H, H, generator=g)
+    x = torch.randn(N, C, H, H, generator=g)
+    w1 = torch.randn(R, C, 1, 1, generator=g) / math.sqrt(C)
+    w2 = torch.randn(C, R, 1, 1, generator=g) / math.sqrt(R)
+    pa = torch.tensor([0.25])
+    gy = torch.randn(N, C, H, H, generator=g)
+
+    def ref(dtype):
+        T = [t.clone().to(dtype).requires_grad_() for t in (v, x, w1, pa, w2)]
+        p = {"a.fc1.weight": T[2], "a.relu1.weight": T[3], "a.fc2.weight": T[4]}
+        yr = F.gelu(F.instance_norm(T[0] * ca_fwd(p, "a.", T[0]), eps=1e-5) + T[1])
+        yr.backward(gy.to(dtype))
+        return yr, T
+
+    y_ref, T = ref(torch.float64)
+    y32, T32 = ref(torch.float32)
+    vd, xd = _leaf(v), _leaf(x)
+    P_ = [_param(t) for t in (w1, pa, w2)]
+    y = HF.mid_tail(vd, xd, *P_)
+    y.backward(gy.to(DEV))
+    assert rel(y, y_ref) < 1e-5
+    assert rel(vd.grad, T[0].grad) < 1e-4
+    assert rel(xd.grad, T[1].grad) < 1e-5
+    # CA weight grads are sums of cancelling terms: bar = 2x torch-fp32's own error vs fp64
+    for pd, pr, p32 in zip(P_, T[2:], T32[2:]):
+        assert rel(pd.grad, pr.grad) <= max(2 * rel(p32.grad, pr.grad), 1e-5)
+
+
+def test_multi_dwconv():
+    from dsgan_hip import functional as HF
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(2, 16, 12, 12, generator=g)
+    ws = []
+    for k in (3, 5, 7, 9):
+        ws += [torch.randn(4, 1, k, k, generator=g) / k, torch.randn(4, generator=g)]
+    T = [t.clone().requires_grad_() for t in [x] + ws]
+    parts = torch.chunk(T[0], 4, 1)
+    y_ref = torch.cat([F.conv2d(parts[i], T[1 + 2 * i], T[2 + 2 * i], padding=k // 2, groups=4)
+                       for i, k in enumerate((3, 5, 7, 9))], 1)
+    gy = torch.randn(y_ref.shape, generator=g)
+    y_ref.backward(gy)
+    xd = _leaf(x)
+    P_ = [_param(t) for t in ws]
+    y = HF.multi_dwconv(xd, *P_)
+    y.backward(gy.to(DEV))
+    assert rel(y, y_ref) < 1e-5
+    assert rel(xd.grad, T[0].grad) < 1e-5
+    for pd, pr in zip(P_, T[1:]):
+        assert rel(pd.grad, pr.grad) < 1e-5
+
+
+def test_losses():
+    from dsgan_hip import functional as HF
+    from oracle import dsgan_cpu as O
+    g = torch.Generator().manual_seed(11)
+    x = torch.randn(2, 1, 30, 30, generator=g) * 3
+    for t in (0.0, 1.0):
+        xr = x.clone().requires_grad_()
+        l_ref = O.bce_logits(xr, t)
+        l_ref.backward()
+        xd = _leaf(x)
+        l = HF.bce_with_logits(xd, t)
+        l.backward()
+        assert abs(l.item() - l_ref.item()) < 1e-5 * abs(l_ref.item())
+        assert rel(xd.grad, xr.grad) < 1e-5
+    a = torch.randn(2, 3, 40, 40, generator=g)
+    b = torch.randn(2, 3, 40, 40, generator=g)
+    ar = a.clone().requires_grad_()
+    l_ref = torch.mean(torch.abs(ar - b))
+    l_ref.backward()
+    ad = _leaf(a)
+    l = HF.l1_loss(ad, b.to(DEV))
+    l.backward()
+    assert abs(l.item() - l_ref.item()) < 1e-5
+    assert rel(ad.grad, ar.grad) < 1e-6
+    ar = a.clone().requires_grad_()
+    l_ref = O.tv_loss(ar)
+    l_ref.backward()
+    ad = _leaf(a)
+    l = HF.tv_loss(ad)
+    l.backward()
+    assert abs(l.item() - l_ref.item()) < 1e-5 * l_ref.item()
+    assert rel(ad.grad, ar.grad) < 1e-6
+
+
+@pytest.mark.parametrize("shape", [(2, 3, 64, 64), (1, 3, 75, 41), (2, 3, 11, 11)])
+def test_ssim_fwd_bwd(shape):
+    from dsgan_hip import functional as HF
+    from oracle import dsgan_cpu as O
+    g = torch.Generator().manual_seed(sum(shape))
+    real = torch.rand(shape, generator=g) * 2 - 1
+    fake = (real + 0.3 * torch.randn(shape, generator=g)).clamp(-1.2, 1.2)
+    fr = fake.clone().requires_grad_()
+    s_ref = O.ssim((real.double() + 1) / 2, (fr.double() + 1) / 2)
+    s_ref.backward()
+    fd = _leaf(fake)
+    s = HF.ssim_affine(real.to(DEV), fd, 0.5, 0.5, 1.0)
+    s.backward()
+    assert abs(s.item() - s_ref.item()) < 2e-5
+    assert rel(fd.grad, fr.grad) < 1e-3
+
+
+def test_adam_matches_torch():
+    from dsgan_hip.flat import FlatParams, FlatAdam
+    torch.manual_seed(0)
+    net = torch.nn.Sequential(torch.nn.Linear(7, 5), torch.nn.Linear(5, 3))
+    ref = torch.nn.Sequential(torch.nn.Linear(7, 5), torch.nn.Linear(5, 3))
+    ref.load_state_dict(net.state_dict())
+    flat = FlatParams(net, torch.device(DEV))
+    opt = FlatAdam(flat, lr=2e-4, betas=(0.5, 0.999))
+    ropt = torch.optim.Adam(ref.parameters(), lr=2e-4, betas=(0.5, 0.999))
+    for it in range(5):
+        grads = [torch.randn(p.shape) * (10 ** (it - 2)) for p in ref.parameters()]
+        for p, gr in zip(ref.parameters(), grads):
+            p.grad = gr.clone()
+        ropt.step()
+        opt.zero_grad()
+        for p, gr in zip(net.parameters(), grads):
+            p.grad.copy_(gr)
+        opt.step()
+    for p, q in zip(net.parameters(), ref.parameters()):
+        assert torch.allclose(p.detach().cpu(), q.detach(), rtol=1e-6, atol=1e-7)
