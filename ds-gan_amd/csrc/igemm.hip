@@ -12,6 +12,11 @@
 //   FWD  : y[b,co,p]        M=Cout  N=B*P      K=Cin*KK   A=w (dense)      B=x  (im2col gather)
 //   DGRAD: dx[b,ci,q]       M=Cin   N=B*Q      K=Cout*KK  A=w^T (gather)   B=dy (col2im gather)
 //   WGRAD: dw[co,(ci,kk)]   M=Cout  N=Cin*KK   K=B*P      A=dy             B=x  (gather), split-K, atomics
+//   DGRAD2: stride-2 data-grad split into the 4 output parity classes (ph,pw).  Pixel
+//           ih = 2*ih'+ph only receives taps kh = kh0 + 2*th with kh0 = (ph+pad)&1, so each class
+//           is a dense stride-1 GEMM with K = Cout*ceil((KH-kh0)/2)*ceil((KW-kw0)/2): no MFMA
+//           work on the structural zeros of the strided transpose (ConvTranspose2d forward,
+//           PatchGAN s2 data-grad).  One launch per class.
 //
 // The M dimension runs over channels and N over pixels, so an MFMA 32x32 accumulator column
 // (lane & 31) walks 32 consecutive pixels of one channel plane: epilogue stores of NCHW
@@ -21,10 +26,11 @@
 // PREC_BF16 converts both operands to bf16 while staging to LDS and runs
 // v_mfma_f32_32x32x16_bf16 with fp32 accumulation.  HBM tensors stay fp32 in both modes.
 #include "common.h"
+#include <stdlib.h>
 
 namespace dsg {
 
-enum Mode : int { FWD = 0, DGRAD = 1, WGRAD = 2 };
+enum Mode : int { FWD = 0, DGRAD = 1, WGRAD = 2, DGRAD2 = 3 };
 enum Prec : int { PREC_F32 = 0, PREC_BF16 = 1 };
 
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
@@ -43,6 +49,10 @@ struct GemmArgs {
   float* ypre; long ypre_bs;
   const float* gpre; long gpre_bs; int gact;
   int act; float slope; int accumulate;
+  int bact;                     // FWD/WGRAD: apply act code to the B operand on load (gelu(z))
+  int dbg;                      // experiment switches (DSGAN_IGEMM_DBG): 1 skip stores, 2 skip loads
+  // DGRAD2 parity class
+  int ph, pw, kh0, kw0, nth, ntw, Hc, Wc;
 };
 
 template <int PREC> struct PT;
@@ -82,6 +92,13 @@ __device__ __forceinline__ RowB make_rowB(const GemmArgs& g, int n) {
       r.base = g.dy + (long)b * g.dy_bs;
       r.a0 = ih + g.pad; r.a1 = iw + g.pad;
     }
+  } else if (MODE == DGRAD2) {  // n = (b, ih', iw') of parity class (ph, pw)
+    const int Q = g.Hc * g.Wc;
+    const int b = n / Q, q = n - b * Q;
+    const int ihc = q / g.Wc, iwc = q - ihc * g.Wc;
+    r.base = g.dy + (long)b * g.dy_bs;
+    r.a0 = ihc + ((g.ph + g.pad - g.kh0) >> 1);
+    r.a1 = iwc + ((g.pw + g.pad - g.kw0) >> 1);
   } else {  // WGRAD: n = (ci, kh, kw)
     const int KK = g.KH * g.KW;
     const int ci = n / KK, kk = n - ci * KK;
@@ -90,6 +107,14 @@ __device__ __forceinline__ RowB make_rowB(const GemmArgs& g, int n) {
     r.a0 = kh - g.pad; r.a1 = kw - g.pad;
   }
   return r;
+}
+
+// Branch-free guarded load: always dereference an in-bounds address (offset 0 of a live row when
+// the element is outside the tensor), then select.  A `ok ? p[i] : 0` expression makes hipcc
+// branch around every load and drain vmcnt(0) per element, serialising the whole tile.
+__device__ __forceinline__ float ldsel(const float* base, long off, bool ok) {
+  const float t = base[ok ? off : 0];
+  return ok ? t : 0.f;
 }
 
 // Load CH consecutive-k elements of B row `r` starting at kbeg.
@@ -101,7 +126,7 @@ __device__ __forceinline__ void load_B(const GemmArgs& g, const RowB& r, int kbe
 #pragma unroll
       for (int j = 0; j < CH; ++j) {
         const int k = kbeg + j;
-        v[j] = (r.valid && k < g.K) ? r.base[(long)k * HW] : 0.f;
+        v[j] = ldsel(r.base, (long)k * HW, r.valid && k < g.K);
       }
     } else {
       const int KK = g.KH * g.KW;
@@ -112,7 +137,7 @@ __device__ __forceinline__ void load_B(const GemmArgs& g, const RowB& r, int kbe
         const int ih = r.a0 + kh, iw = r.a1 + kw;
         const bool ok = r.valid && (kbeg + j) < g.K && (unsigned)ih < (unsigned)g.H &&
                         (unsigned)iw < (unsigned)g.W;
-        v[j] = ok ? r.base[(long)ci * HW + ih * g.W + iw] : 0.f;
+        v[j] = ldsel(r.base, (long)ci * HW + ih * g.W + iw, ok);
         if (++kw == g.KW) { kw = 0; if (++kh == g.KH) { kh = 0; ++ci; } }
       }
     }
@@ -122,7 +147,7 @@ __device__ __forceinline__ void load_B(const GemmArgs& g, const RowB& r, int kbe
 #pragma unroll
       for (int j = 0; j < CH; ++j) {
         const int k = kbeg + j;
-        v[j] = (r.valid && k < g.K) ? r.base[(long)k * P] : 0.f;
+        v[j] = ldsel(r.base, (long)k * P, r.valid && k < g.K);
       }
     } else {
       const int KK = g.KH * g.KW;
@@ -136,9 +161,21 @@ __device__ __forceinline__ void load_B(const GemmArgs& g, const RowB& r, int kbe
         bool ok = r.valid && (kbeg + j) < g.K && th >= 0 && tw >= 0;
         if (s != 1) { ok = ok && (th % s == 0) && (tw % s == 0); oh = th / s; ow = tw / s; }
         ok = ok && oh < g.Ho && ow < g.Wo;
-        v[j] = ok ? r.base[(long)co * P + oh * g.Wo + ow] : 0.f;
+        v[j] = ldsel(r.base, (long)co * P + oh * g.Wo + ow, ok);
         if (++kw == g.KW) { kw = 0; if (++kh == g.KH) { kh = 0; ++co; } }
       }
+    }
+  } else if (MODE == DGRAD2) {  // k = (co, th, tw): oh = a0 - th, ow = a1 - tw
+    const int P = g.Ho * g.Wo, T = g.nth * g.ntw;
+    int co = kbeg / T, tt = kbeg - co * T;
+    int th = tt / g.ntw, tw = tt - th * g.ntw;
+#pragma unroll
+    for (int j = 0; j < CH; ++j) {
+      const int oh = r.a0 - th, ow = r.a1 - tw;
+      const bool ok = r.valid && (kbeg + j) < g.K && (unsigned)oh < (unsigned)g.Ho &&
+                      (unsigned)ow < (unsigned)g.Wo;
+      v[j] = ldsel(r.base, (long)co * P + oh * g.Wo + ow, ok);
+      if (++tw == g.ntw) { tw = 0; if (++th == g.nth) { th = 0; ++co; } }
     }
   } else {  // WGRAD, k = (b, oh, ow)
     const int P = g.Ho * g.Wo;
@@ -147,7 +184,7 @@ __device__ __forceinline__ void load_B(const GemmArgs& g, const RowB& r, int kbe
 #pragma unroll
       for (int j = 0; j < CH; ++j) {
         const bool ok = r.valid && (kbeg + j) < g.K;
-        v[j] = ok ? r.base[(long)b * g.x_bs + p] : 0.f;
+        v[j] = ldsel(r.base, (long)b * g.x_bs + p, ok);
         if (++p == P) { p = 0; ++b; }
       }
     } else {
@@ -157,7 +194,7 @@ __device__ __forceinline__ void load_B(const GemmArgs& g, const RowB& r, int kbe
         const int ih = oh * g.stride + r.a0, iw = ow * g.stride + r.a1;
         const bool ok = r.valid && (kbeg + j) < g.K && (unsigned)ih < (unsigned)g.H &&
                         (unsigned)iw < (unsigned)g.W;
-        v[j] = ok ? r.base[(long)b * g.x_bs + ih * g.W + iw] : 0.f;
+        v[j] = ldsel(r.base, (long)b * g.x_bs + ih * g.W + iw, ok);
         if (++ow == g.Wo) { ow = 0; if (++oh == g.Ho) { oh = 0; ++b; } }
       }
     }
@@ -178,7 +215,7 @@ __device__ __forceinline__ void load_A(const GemmArgs& g, int m, int kbeg, float
       }
     } else {
 #pragma unroll
-      for (int j = 0; j < CH; ++j) v[j] = (mv && kbeg + j < g.K) ? base[kbeg + j] : 0.f;
+      for (int j = 0; j < CH; ++j) v[j] = ldsel(base, kbeg + j, mv && kbeg + j < g.K);
     }
   } else if (MODE == DGRAD) {  // A[ci][(co,kk)] = w[co][ci][kk]
     const int KK = g.KH * g.KW;
@@ -186,8 +223,18 @@ __device__ __forceinline__ void load_A(const GemmArgs& g, int m, int kbeg, float
 #pragma unroll
     for (int j = 0; j < CH; ++j) {
       const bool ok = mv && (kbeg + j) < g.K;
-      v[j] = ok ? g.w[((long)co * g.Cin + m) * KK + kk] : 0.f;
+      v[j] = ldsel(g.w, ((long)co * g.Cin + m) * KK + kk, ok);
       if (++kk == KK) { kk = 0; ++co; }
+    }
+  } else if (MODE == DGRAD2) {  // A[ci][(co,th,tw)] = w[co][ci][kh0+2th][kw0+2tw]
+    const int T = g.nth * g.ntw;
+    int co = kbeg / T, tt = kbeg - co * T;
+    int th = tt / g.ntw, tw = tt - th * g.ntw;
+#pragma unroll
+    for (int j = 0; j < CH; ++j) {
+      const bool ok = mv && (kbeg + j) < g.K;
+      v[j] = ldsel(g.w, (((long)co * g.Cin + m) * g.KH + g.kh0 + 2 * th) * g.KW + g.kw0 + 2 * tw, ok);
+      if (++tw == g.ntw) { tw = 0; if (++th == g.nth) { th = 0; ++co; } }
     }
   } else {  // WGRAD: A[co][(b,p)] = dy[b][co][p]
     const int P = g.Ho * g.Wo;
@@ -196,7 +243,7 @@ __device__ __forceinline__ void load_A(const GemmArgs& g, int m, int kbeg, float
 #pragma unroll
     for (int j = 0; j < CH; ++j) {
       const bool ok = mv && (kbeg + j) < g.K;
-      v[j] = ok ? base[(long)b * g.dy_bs + p] : 0.f;
+      v[j] = ldsel(base, (long)b * g.dy_bs + p, ok);
       if (++p == P) { p = 0; ++b; }
     }
   }
@@ -238,10 +285,23 @@ __global__ __launch_bounds__(256) void igemm_kernel(GemmArgs g) {
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WN, wn = wave % WN;
-  const int n0 = blockIdx.x * BN, m0 = blockIdx.y * BM;
+  // 1-D grid, XCD-aware: blocks b, b+8, b+16, ... share an XCD (round-robin dispatch), so the
+  // bijective remap below gives each XCD a contiguous run of tile ids; tiles are numbered with
+  // the M (channel) tile fastest, so the M-tiles that read the same activation (B) columns run
+  // together on one XCD and the activation streams from HBM once instead of M/BM times.
+  const int mt = (g.M + BM - 1) / BM, nt = (g.NN + BN - 1) / BN;
+  int tile;
+  {
+    const int nwg = gridDim.x, id = blockIdx.x;
+    const int xcd = id & 7, q = nwg >> 3, r = nwg & 7;
+    tile = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (id >> 3);
+  }
+  const int m_t = tile % mt, rest = tile / mt;
+  const int n_t = rest % nt, split = rest / nt;
+  const int n0 = n_t * BN, m0 = m_t * BM;
 
   int kbeg = 0, kend = g.K;
-  if (MODE == WGRAD) { kbeg = blockIdx.z * g.k_split; kend = min(g.K, kbeg + g.k_split); }
+  if (MODE == WGRAD) { kbeg = split * g.k_split; kend = min(g.K, kbeg + g.k_split); }
   if (kbeg >= kend) return;
   const int nk = (kend - kbeg + BK - 1) / BK;
 
@@ -269,6 +329,17 @@ __global__ __launch_bounds__(256) void igemm_kernel(GemmArgs g) {
   float ra[A_ITEMS][CH], rbv[B_ITEMS][CH];
   auto gload = [&](int kt) {
     const int kb = kbeg + kt * BK;
+    if (g.dbg & 2) {
+#pragma unroll
+      for (int i = 0; i < A_ITEMS; ++i)
+#pragma unroll
+        for (int j = 0; j < CH; ++j) ra[i][j] = (float)(kt + j);
+#pragma unroll
+      for (int i = 0; i < B_ITEMS; ++i)
+#pragma unroll
+        for (int j = 0; j < CH; ++j) rbv[i][j] = (float)(kt - j);
+      return;
+    }
 #pragma unroll
     for (int i = 0; i < A_ITEMS; ++i)
       if (a_on[i]) {
@@ -287,8 +358,13 @@ __global__ __launch_bounds__(256) void igemm_kernel(GemmArgs g) {
     for (int i = 0; i < B_ITEMS; ++i)
       if (b_on[i]) {
         const int k0 = kb + b_ch[i] * CH;
-        if (k0 < kend) load_B<MODE, PW, CH>(g, rb[i], k0, rbv[i]);
-        else {
+        if (k0 < kend) {
+          load_B<MODE, PW, CH>(g, rb[i], k0, rbv[i]);
+          if ((MODE == FWD || MODE == WGRAD) && g.bact) {
+#pragma unroll
+            for (int j = 0; j < CH; ++j) rbv[i][j] = act_f(g.bact, rbv[i][j], g.slope);
+          }
+        } else {
 #pragma unroll
           for (int j = 0; j < CH; ++j) rbv[i][j] = 0.f;
         }
@@ -388,29 +464,87 @@ __global__ __launch_bounds__(256) void igemm_kernel(GemmArgs g) {
     return;
   }
   const int Pout = (MODE == FWD) ? g.Ho * g.Wo : g.H * g.W;
+  const bool has_bias = g.bias != nullptr, has_pre = g.ypre != nullptr, has_g = g.gpre != nullptr;
+  const int act = g.act, gact = g.gact;
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
-    const int n = n0 + wn * TN * 32 + j * 32 + lr;
-    if (n >= g.NN) continue;
-    const int b = n / Pout, p = n - b * Pout;
+    int n = n0 + wn * TN * 32 + j * 32 + lr;
+    const bool nv = n < g.NN;
+    if (!nv) n = 0;
+    int b, p;
+    if (MODE == DGRAD2) {
+      const int Q = g.Hc * g.Wc;
+      b = n / Q;
+      const int q = n - b * Q, ihc = q / g.Wc, iwc = q - ihc * g.Wc;
+      p = (2 * ihc + g.ph) * g.W + 2 * iwc + g.pw;
+    } else {
+      b = n / Pout; p = n - b * Pout;
+    }
     float* yb = g.y + (long)b * g.y_bs + p;
-    float* ypb = g.ypre ? g.ypre + (long)b * g.ypre_bs + p : nullptr;
-    const float* gpb = g.gpre ? g.gpre + (long)b * g.gpre_bs + p : nullptr;
+    float* ypb = has_pre ? g.ypre + (long)b * g.ypre_bs + p : nullptr;
+    const float* gpb = has_g ? g.gpre + (long)b * g.gpre_bs + p : nullptr;
 #pragma unroll
-    for (int i = 0; i < TM; ++i)
+    for (int i = 0; i < TM; ++i) {
+      float v[16];
+      long off[16];
+      bool ok[16];
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int m = m0 + wm * TM * 32 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-        if (m >= g.M) continue;
-        const long off = (long)m * Pout;
-        float v = acc[i][j][r];
-        if (g.bias) v += g.bias[m];
-        if (gpb) v *= act_g(g.gact, gpb[off], g.slope);
-        if (ypb) ypb[off] = v;
-        v = act_f(g.act, v, g.slope);
-        if (g.accumulate) v += yb[off];
-        yb[off] = v;
+        ok[r] = nv && m < g.M;
+        off[r] = ok[r] ? (long)m * Pout : 0;
+        v[r] = acc[i][j][r];
+        if (has_bias) v[r] += g.bias[ok[r] ? m : 0];
       }
+      if (has_g) {
+        float gv[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) gv[r] = gpb[off[r]];
+        switch (gact) {
+          case ACT_GELU:
+#pragma unroll
+            for (int r = 0; r < 16; ++r) v[r] *= gelu_g(gv[r]);
+            break;
+          default:
+#pragma unroll
+            for (int r = 0; r < 16; ++r) v[r] *= act_g(gact, gv[r], g.slope);
+        }
+      }
+      if (has_pre) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) if (ok[r]) ypb[off[r]] = v[r];
+      }
+      switch (act) {
+        case ACT_NONE: break;
+        case ACT_GELU:
+#pragma unroll
+          for (int r = 0; r < 16; ++r) v[r] = gelu_f(v[r]);
+          break;
+        case ACT_RELU:
+#pragma unroll
+          for (int r = 0; r < 16; ++r) v[r] = fmaxf(v[r], 0.f);
+          break;
+        default:
+#pragma unroll
+          for (int r = 0; r < 16; ++r) v[r] = act_f(act, v[r], g.slope);
+      }
+      if (g.accumulate) {
+        float o[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) o[r] = yb[off[r]];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) v[r] += o[r];
+      }
+      if (g.dbg & 1) {
+        float t = 0.f;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) t += v[r];
+        if (t == 12345.678f) yb[0] = t;
+        continue;
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) if (ok[r]) yb[off[r]] = v[r];
+    }
   }
 }
 
@@ -419,20 +553,20 @@ template <int MODE, int PREC, bool PW>
 static void launch_cfg(const GemmArgs& g, int splits, hipStream_t st) {
   const int M = g.M;
   if (M > 64) {
-    dim3 grid(cdiv(g.NN, 128), cdiv(M, 128), splits);
+    dim3 grid(cdiv(g.NN, 128) * cdiv(M, 128) * splits);
     hipLaunchKernelGGL((igemm_kernel<MODE, PREC, 128, 128, 2, 2, PW>), grid, dim3(256), 0, st, g);
   } else if (M > 32) {
-    dim3 grid(cdiv(g.NN, 128), cdiv(M, 64), splits);
+    dim3 grid(cdiv(g.NN, 128) * cdiv(M, 64) * splits);
     hipLaunchKernelGGL((igemm_kernel<MODE, PREC, 64, 128, 2, 2, PW>), grid, dim3(256), 0, st, g);
   } else {
-    dim3 grid(cdiv(g.NN, 128), cdiv(M, 32), splits);
+    dim3 grid(cdiv(g.NN, 128) * cdiv(M, 32) * splits);
     hipLaunchKernelGGL((igemm_kernel<MODE, PREC, 32, 128, 1, 4, PW>), grid, dim3(256), 0, st, g);
   }
 }
 
 template <int MODE>
 static void launch_mode(const GemmArgs& g, int prec, int splits, hipStream_t st) {
-  const bool pw = g.KH == 1 && g.KW == 1 && g.stride == 1 && g.pad == 0;
+  const bool pw = MODE != DGRAD2 && g.KH == 1 && g.KW == 1 && g.stride == 1 && g.pad == 0;
   if (prec == PREC_BF16) {
     if (pw) launch_cfg<MODE, PREC_BF16, true>(g, splits, st);
     else launch_cfg<MODE, PREC_BF16, false>(g, splits, st);
@@ -446,9 +580,16 @@ static void launch_mode(const GemmArgs& g, int prec, int splits, hipStream_t st)
 
 using namespace dsg;
 
+static int dbg_flags() {
+  static int f = -1;
+  if (f < 0) { const char* e = getenv("DSGAN_IGEMM_DBG"); f = e ? atoi(e) : 0; }
+  return f;
+}
+
 static GemmArgs base_args(int N, int Cin, int H, int W, int Cout, int KH, int KW, int stride,
                           int pad, int Ho, int Wo) {
   GemmArgs g{};
+  g.dbg = dbg_flags();
   g.N = N; g.Cin = Cin; g.H = H; g.W = W; g.Cout = Cout; g.KH = KH; g.KW = KW;
   g.stride = stride; g.pad = pad; g.Ho = Ho; g.Wo = Wo;
   g.slope = 0.2f;
@@ -473,12 +614,13 @@ extern "C" {
 int dsgan_conv_fwd(const float* x, long x_bs, const float* w, const float* bias, float* y,
                    long y_bs, float* ypre, long ypre_bs, int N, int Cin, int H, int W, int Cout,
                    int KH, int KW, int stride, int pad, int Ho, int Wo, int act, float slope,
-                   int accumulate, int prec, hipStream_t st) {
+                   int accumulate, int xact, int prec, hipStream_t st) {
   if (int e = check_geom(N, Cin, H, W, Cout, KH, KW, stride, pad, Ho, Wo, prec)) return e;
   DSG_REQUIRE(x && w && y, "dsgan_conv_fwd: null pointer");
   GemmArgs g = base_args(N, Cin, H, W, Cout, KH, KW, stride, pad, Ho, Wo);
   g.x = x; g.x_bs = x_bs; g.w = w; g.bias = bias; g.y = y; g.y_bs = y_bs;
   g.ypre = ypre; g.ypre_bs = ypre_bs; g.act = act; g.slope = slope; g.accumulate = accumulate;
+  g.bact = xact;
   g.M = Cout; g.NN = N * Ho * Wo; g.K = Cin * KH * KW;
   launch_mode<FWD>(g, prec, 1, st);
   DSG_CHECK_LAUNCH();
@@ -496,8 +638,28 @@ int dsgan_conv_dgrad(const float* dy, long dy_bs, const float* w, const float* b
   g.dy = dy; g.dy_bs = dy_bs; g.w = w; g.bias = bias; g.y = dx; g.y_bs = dx_bs;
   g.ypre = ypre; g.ypre_bs = ypre_bs; g.gpre = gpre; g.gpre_bs = gpre_bs; g.gact = gact;
   g.act = act; g.slope = slope; g.accumulate = accumulate;
-  g.M = Cin; g.NN = N * H * W; g.K = Cout * KH * KW;
-  launch_mode<DGRAD>(g, prec, 1, st);
+  g.M = Cin;
+  if (stride == 2) {
+    for (int ph = 0; ph < 2; ++ph)
+      for (int pw = 0; pw < 2; ++pw) {
+        GemmArgs c = g;
+        c.ph = ph; c.pw = pw;
+        c.kh0 = (ph + pad) & 1; c.kw0 = (pw + pad) & 1;
+        c.nth = (KH - c.kh0 + 1) / 2; c.ntw = (KW - c.kw0 + 1) / 2;
+        c.Hc = (H - ph + 1) / 2; c.Wc = (W - pw + 1) / 2;
+        if (c.Hc <= 0 || c.Wc <= 0) continue;
+        c.NN = N * c.Hc * c.Wc;
+        c.K = Cout * c.nth * c.ntw;
+        if (c.K == 0) {  // no tap reaches this class: bias/act only -- not needed on the DS-GAN path
+          dsgan_set_error("dsgan_conv_dgrad: empty parity class (K=%d, stride 2)", KH);
+          return -1;
+        }
+        launch_mode<DGRAD2>(c, prec, 1, st);
+      }
+  } else {
+    g.NN = N * H * W; g.K = Cout * KH * KW;
+    launch_mode<DGRAD>(g, prec, 1, st);
+  }
   DSG_CHECK_LAUNCH();
   return 0;
 }
@@ -506,11 +668,12 @@ int dsgan_conv_dgrad(const float* dy, long dy_bs, const float* w, const float* b
 // per step; concurrent uses of one weight accumulate, as autograd would).
 int dsgan_conv_wgrad(const float* dy, long dy_bs, const float* x, long x_bs, float* dw, int N,
                      int Cin, int H, int W, int Cout, int KH, int KW, int stride, int pad, int Ho,
-                     int Wo, int prec, hipStream_t st) {
+                     int Wo, int xact, int prec, hipStream_t st) {
   if (int e = check_geom(N, Cin, H, W, Cout, KH, KW, stride, pad, Ho, Wo, prec)) return e;
   DSG_REQUIRE(dy && x && dw, "dsgan_conv_wgrad: null pointer");
   GemmArgs g = base_args(N, Cin, H, W, Cout, KH, KW, stride, pad, Ho, Wo);
   g.dy = dy; g.dy_bs = dy_bs; g.x = x; g.x_bs = x_bs; g.y = dw;
+  g.bact = xact;
   g.M = Cout; g.NN = Cin * KH * KW; g.K = N * Ho * Wo;
   const int BK = prec == PREC_BF16 ? PT<PREC_BF16>::BK : PT<PREC_F32>::BK;
   const int BM = g.M > 64 ? 128 : (g.M > 32 ? 64 : 32);

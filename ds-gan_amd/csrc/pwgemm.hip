@@ -1,0 +1,386 @@
+// Pointwise (1x1, stride 1) convolution / nn.Linear-on-NCHW GEMMs on MFMA bf16 (gfx950).
+//
+// The 1x1 contractions are ~70% of the DS-GAN generator's FLOPs (Block.pwconv1/pwconv2 +
+// shortcut, DSGAN/models/model/MixConvNeXtML.py:218-242; downSkip* / OriginMLKA 1x1 convs
+// :122-157,334-419).  In NCHW they are plain GEMMs over contiguous pixel rows, so this kernel
+// drops the im2col machinery of igemm.hip and is built to keep VALU work per MFMA low:
+//   * operands are staged global->LDS as 16-byte float4 loads, converted to bf16 in registers,
+//     written as 8-byte LDS stores in the SAME layout they have in HBM (no register transpose);
+//   * operands whose contiguous axis is not the MFMA k-axis (pixel-major activations, the W^T
+//     of the data-grad) are read with the gfx950 hardware transpose ds_read_b64_tr_b16;
+//   * the epilogue uses buffer stores whose row offset is a per-(tile,register) scalar, so an
+//     output element costs a conversion-free store and no address VALU; rows past M are
+//     dropped by the buffer range check; the bias is folded into the accumulator init.
+//
+// Modes (P = H*W pixels per image, all tensors NCHW / [out,in] weights, fp32 in HBM):
+//   FWD  : Y[b][m][p]  = act( sum_k W[m][k] * xact(X[b][k][p]) + bias[m] ) (+Y)   (ypre = pre-act)
+//   DGRAD: DX[b][m][p] = ( sum_k W[k][m] * DY[b][k][p] ) * gact'(G[b][m][p])
+//   WGRAD: DW[m][n]   += sum_{b,p} DY[b][m][p] * xact(X[b][n][p])     (split over pixels, atomics)
+#include "common.h"
+
+namespace dsg {
+
+typedef __attribute__((ext_vector_type(8))) __bf16 pbf16x8;
+typedef __attribute__((ext_vector_type(4))) __bf16 pbf16x4;
+typedef __attribute__((ext_vector_type(16))) float pf32x16;
+typedef __attribute__((ext_vector_type(4))) short s16x4;
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+enum PwMode : int { PW_FWD = 0, PW_DGRAD = 1, PW_WGRAD = 2 };
+
+struct PwArgs {
+  const float* A; long a_bs;   // FWD: W[M][K]  DGRAD: W[K][M]  WGRAD: DY[b][M][P]
+  const float* B; long b_bs;   // FWD/DGRAD: X/DY [b][K][P]     WGRAD: X[b][N][P]
+  float* Y; long y_bs;         // FWD/DGRAD output [b][M][P];   WGRAD: DW[M][N] (+=)
+  const float* bias;
+  float* ypre; long ypre_bs;
+  const float* gpre; long gpre_bs;
+  int M, N, K, P;
+  int act, gact, bact, accumulate; float slope;
+  int k_split;
+};
+
+constexpr int PBK = 32;                 // K per main-loop step
+constexpr int RM_STR = PBK + 8;         // row-major [rows][k] tile stride (80 B: conflict-free b128)
+
+__device__ __forceinline__ pbf16x8 tr_frag(const __bf16* p0, int stride) {
+  // two ds_read_b64_tr_b16: rows k..k+3 then k+4..k+7 of a k-major tile
+#if defined(__HIP_DEVICE_COMPILE__)
+  s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p0));
+  s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p0 + 4 * stride));
+  typedef __attribute__((ext_vector_type(8))) short s16x8;
+  s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(pbf16x8, v);
+#else
+  return pbf16x8{};
+#endif
+}
+
+__device__ __forceinline__ float4 ld4(const float* p, bool ok, const float* safe) {
+  const float4 t = *reinterpret_cast<const float4*>(ok ? p : safe);
+  return ok ? t : make_float4(0.f, 0.f, 0.f, 0.f);
+}
+
+__device__ __forceinline__ pbf16x4 cvt4(float4 v, int bact, float slope) {
+  if (bact) { v.x = act_f(bact, v.x, slope); v.y = act_f(bact, v.y, slope); v.z = act_f(bact, v.z, slope); v.w = act_f(bact, v.w, slope); }
+  pbf16x4 r;
+  r[0] = (__bf16)v.x; r[1] = (__bf16)v.y; r[2] = (__bf16)v.z; r[3] = (__bf16)v.w;
+  return r;
+}
+
+template <int MODE, int BM>
+__global__ __launch_bounds__(256) void pwgemm_kernel(PwArgs g) {
+  constexpr int BN = 128;
+  constexpr int WM = 2, WN = 2;
+  constexpr int TM = BM / WM / 32, TN = BN / WN / 32;
+  // A tile: row-major [BM][RM_STR] (FWD, WGRAD) or k-major [PBK][BM+32] (DGRAD)
+  // B tile: k-major [PBK][BN+32] (FWD, DGRAD) or row-major [BN][RM_STR] (WGRAD)
+  constexpr bool A_KMAJ = (MODE == PW_DGRAD);
+  constexpr bool B_KMAJ = (MODE != PW_WGRAD);
+  constexpr int A_STR = A_KMAJ ? BM + 32 : RM_STR;
+  constexpr int B_STR = B_KMAJ ? BN + 32 : RM_STR;
+  constexpr int A_SZ = A_KMAJ ? PBK * A_STR : BM * A_STR;
+  constexpr int B_SZ = B_KMAJ ? PBK * B_STR : BN * B_STR;
+  __shared__ __attribute__((aligned(16))) __bf16 smem[2 * (A_SZ + B_SZ)];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  const int lr = lane & 31, lh = lane >> 5;
+
+  // ---- tile decode (1-D grid, XCD-aware, M-tile fastest; see igemm.hip) ----
+  const int mt = (g.M + BM - 1) / BM;
+  const int nt = (MODE == PW_WGRAD) ? (g.N + BN - 1) / BN : g.N / BN;
+  int tile;
+  {
+    const int nwg = gridDim.x, id = blockIdx.x;
+    const int xcd = id & 7, q = nwg >> 3, r = nwg & 7;
+    tile = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (id >> 3);
+  }
+  const int m_t = tile % mt, rest = tile / mt;
+  const int n_t = rest % nt, split = rest / nt;
+  const int m0 = m_t * BM, n0 = n_t * BN;
+
+  int kbeg = 0, kend = g.K;
+  if (MODE == PW_WGRAD) { kbeg = split * g.k_split; kend = min(g.K, kbeg + g.k_split); }
+  if (kbeg >= kend) return;
+  const int nk = (kend - kbeg + PBK - 1) / PBK;
+
+  // FWD/DGRAD: the N tile lies inside one image (P % BN == 0)
+  const int bimg = (MODE == PW_WGRAD) ? 0 : n0 / g.P;
+  const int p0 = (MODE == PW_WGRAD) ? 0 : n0 - bimg * g.P;
+  const float* Bimg = (MODE == PW_WGRAD) ? g.B : g.B + (long)bimg * g.b_bs + p0;
+
+  // ---- staging maps ----
+  // row-major tiles: item = (row, c4) with c4 in [0,8): 8 float4 per 32-k row
+  // k-major tiles  : item = (k, c4) with c4 in [0, C/4)
+  constexpr int A_ITEMS = (A_KMAJ ? PBK * BM / 4 : BM * 8) / 256;
+  constexpr int B_ITEMS = (B_KMAJ ? PBK * BN / 4 : BN * 8) / 256;
+  float4 ra[A_ITEMS], rb[B_ITEMS];
+
+  auto gload = [&](int kt) {
+    const int kb = kbeg + kt * PBK;
+#pragma unroll
+    for (int i = 0; i < A_ITEMS; ++i) {
+      const int it = tid + i * 256;
+      if (MODE == PW_FWD) {                      // W[M][K], row m, k = kb + c4*4
+        const int row = it >> 3, k = kb + (it & 7) * 4;
+        const int m = m0 + row;
+        ra[i] = ld4(g.A + (long)m * g.K + k, m < g.M && k < kend, g.A);
+      } else if (MODE == PW_DGRAD) {             // W[K][M], row k, m = m0 + c4*4
+        const int kr = it / (BM / 4), c4 = it % (BM / 4);
+        const int k = kb + kr, m = m0 + c4 * 4;
+        ra[i] = ld4(g.A + (long)k * g.M + m, k < kend && m < g.M, g.A);
+      } else {                                   // DY[b][M][P], row m, pixels of one image
+        const int row = it >> 3, k = kb + (it & 7) * 4;
+        const int m = m0 + row;
+        const int b = k / g.P, p = k - b * g.P;
+        ra[i] = ld4(g.A + (long)b * g.a_bs + (long)m * g.P + p, m < g.M && k < kend, g.A);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < B_ITEMS; ++i) {
+      const int it = tid + i * 256;
+      if (MODE != PW_WGRAD) {                    // [K][P] k-major, row k, pixels n0 + c4*4
+        const int kr = it / (BN / 4), c4 = it % (BN / 4);
+        const int k = kb + kr;
+        rb[i] = ld4(Bimg + (long)k * g.P + c4 * 4, k < kend, g.B);
+      } else {                                   // X[b][N][P], row n
+        const int row = it >> 3, k = kb + (it & 7) * 4;
+        const int n = n0 + row;
+        const int b = k / g.P, p = k - b * g.P;
+        rb[i] = ld4(g.B + (long)b * g.b_bs + (long)n * g.P + p, n < g.N && k < kend, g.B);
+      }
+    }
+  };
+  auto sstore = [&](int buf) {
+    __bf16* As = smem + buf * (A_SZ + B_SZ);
+    __bf16* Bs = As + A_SZ;
+#pragma unroll
+    for (int i = 0; i < A_ITEMS; ++i) {
+      const int it = tid + i * 256;
+      int off;
+      if (A_KMAJ) off = (it / (BM / 4)) * A_STR + (it % (BM / 4)) * 4;
+      else off = (it >> 3) * A_STR + (it & 7) * 4;
+      *reinterpret_cast<pbf16x4*>(As + off) = cvt4(ra[i], 0, 0.f);
+    }
+#pragma unroll
+    for (int i = 0; i < B_ITEMS; ++i) {
+      const int it = tid + i * 256;
+      int off;
+      if (B_KMAJ) off = (it / (BN / 4)) * B_STR + (it % (BN / 4)) * 4;
+      else off = (it >> 3) * B_STR + (it & 7) * 4;
+      *reinterpret_cast<pbf16x4*>(Bs + off) = cvt4(rb[i], g.bact, g.slope);
+    }
+  };
+
+  // ---- accumulators (bias folded into the init for FWD) ----
+  pf32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    float bv[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int m = m0 + wm * TM * 32 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+      bv[r] = (MODE == PW_FWD && g.bias && m < g.M) ? g.bias[m] : 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = bv[r];
+  }
+
+  gload(0);
+  sstore(0);
+  __syncthreads();
+
+  // per-lane fragment address parts for the transposed reads:
+  // lane = 32h + 16G + 4q + p supplies row (8h + q) and column 16G + 4p of its 16-column block
+  const int tq = (lane >> 2) & 3, tp = lane & 3, tG = (lane >> 4) & 1;
+
+  for (int kt = 0; kt < nk; ++kt) {
+    const int buf = kt & 1;
+    if (kt + 1 < nk) gload(kt + 1);
+    const __bf16* As = smem + buf * (A_SZ + B_SZ);
+    const __bf16* Bs = As + A_SZ;
+#pragma unroll
+    for (int ks = 0; ks < PBK / 16; ++ks) {
+      pbf16x8 af[TM], bfr[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int mb = wm * TM * 32 + i * 32;
+        if (A_KMAJ)
+          af[i] = tr_frag(As + (ks * 16 + 8 * lh + tq) * A_STR + mb + 16 * tG + 4 * tp, A_STR);
+        else
+          af[i] = *reinterpret_cast<const pbf16x8*>(As + (mb + lr) * A_STR + ks * 16 + lh * 8);
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int nbb = wn * TN * 32 + j * 32;
+        if (B_KMAJ)
+          bfr[j] = tr_frag(Bs + (ks * 16 + 8 * lh + tq) * B_STR + nbb + 16 * tG + 4 * tp, B_STR);
+        else
+          bfr[j] = *reinterpret_cast<const pbf16x8*>(Bs + (nbb + lr) * B_STR + ks * 16 + lh * 8);
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    if (kt + 1 < nk) sstore(buf ^ 1);
+    __syncthreads();
+  }
+
+  // ---- epilogue ----
+  if (MODE == PW_WGRAD) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int n = n0 + wn * TN * 32 + j * 32 + lr;
+      if (n >= g.N) continue;
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int m = m0 + wm * TM * 32 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+          if (m < g.M) atomicAdd(g.Y + (long)m * g.N + n, acc[i][j][r]);
+        }
+    }
+    return;
+  }
+  // FWD / DGRAD: element (m, n0+col) of image bimg lives at base + m*P + col; buffer resources
+  // are based at pixel p0 of row 0, their range ends at row M (rows >= M are dropped/read 0).
+  const unsigned range = (unsigned)(((long)g.M * g.P - p0) * 4);
+  const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(g.Y + (long)bimg * g.y_bs + p0), (short)0, range, 0x00020000);
+  __amdgpu_buffer_rsrc_t rp = ry, rg = ry;
+  if (g.ypre) rp = __builtin_amdgcn_make_buffer_rsrc((void*)(g.ypre + (long)bimg * g.ypre_bs + p0), (short)0, range, 0x00020000);
+  if (g.gpre) rg = __builtin_amdgcn_make_buffer_rsrc((void*)(g.gpre + (long)bimg * g.gpre_bs + p0), (short)0, range, 0x00020000);
+  const int P4 = g.P * 4;
+  const bool full = m0 + BM <= g.M;
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int col = wn * TN * 32 + j * 32 + lr;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int mrow = m0 + wm * TM * 32 + i * 32;   // uniform
+      // lane part of the offset: rows 4h, column col.  In a partial M tile, rows >= M get an
+      // offset past the resource range so the hardware drops the store / returns 0.
+      int vofs = (4 * lh * g.P + col) * 4;
+      int vrow[16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        vrow[r] = vofs;
+        if (!full && mrow + (r & 3) + 8 * (r >> 2) + 4 * lh >= g.M) vrow[r] = 0x7fffffff;
+      }
+      float v[16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) v[r] = acc[i][j][r];
+      if (g.gpre) {
+        float gv[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          gv[r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                      rg, vrow[r], (mrow + (r & 3) + 8 * (r >> 2)) * P4, 0));
+        if (g.gact == ACT_GELU) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) v[r] *= gelu_g(gv[r]);
+        } else {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) v[r] *= act_g(g.gact, gv[r], g.slope);
+        }
+      }
+      if (g.ypre) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v[r]), rp, vrow[r],
+                                                (mrow + (r & 3) + 8 * (r >> 2)) * P4, 0);
+      }
+      switch (g.act) {
+        case ACT_NONE: break;
+        case ACT_GELU:
+#pragma unroll
+          for (int r = 0; r < 16; ++r) v[r] = gelu_f(v[r]);
+          break;
+        default:
+#pragma unroll
+          for (int r = 0; r < 16; ++r) v[r] = act_f(g.act, v[r], g.slope);
+      }
+      if (g.accumulate) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          v[r] += __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                      ry, vrow[r], (mrow + (r & 3) + 8 * (r >> 2)) * P4, 0));
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v[r]), ry, vrow[r],
+                                              (mrow + (r & 3) + 8 * (r >> 2)) * P4, 0);
+    }
+  }
+}
+
+template <int MODE, int BM>
+static void pw_launch(const PwArgs& g, int splits, hipStream_t st) {
+  const int mt = (g.M + BM - 1) / BM;
+  const int nt = (MODE == PW_WGRAD) ? (g.N + 127) / 128 : g.N / 128;
+  hipLaunchKernelGGL((pwgemm_kernel<MODE, BM>), dim3((unsigned)((long)mt * nt * splits)), dim3(256), 0, st, g);
+}
+
+static bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
+}  // namespace dsg
+
+using namespace dsg;
+
+// Fast-path eligibility (else the caller uses the generic implicit-GEMM kernel):
+//   FWD/DGRAD: P % 128 == 0, K % 4 == 0 (and M % 4 == 0 for DGRAD), 16-byte aligned operands.
+//   WGRAD:     P % 32 == 0, 16-byte aligned operands.
+extern "C" int dsgan_pw_supported(int mode, int M, int K, int P, long a_bs, long b_bs, const void* a,
+                                  const void* b) {
+  if (!al16(a) || !al16(b) || (a_bs & 3) || (b_bs & 3) || M < 16) return 0;
+  if (mode == PW_WGRAD) return (P % 32) == 0;
+  if (P % 128 != 0 || (K & 3)) return 0;
+  if (mode == PW_DGRAD && (M & 3)) return 0;
+  return 1;
+}
+
+// mode FWD:   A=W[M][K], B=X[b][K][P] (b_bs), Y[b][M][P]
+// mode DGRAD: A=W[K][M], B=DY[b][K][P], Y=DX[b][M][P], gpre/gact epilogue
+// mode WGRAD: A=DY[b][M][P] (a_bs), B=X[b][N][P] (b_bs), Y=DW[M][N] (+=), nb images
+extern "C" int dsgan_pw_gemm(int mode, const float* A, long a_bs, const float* B, long b_bs,
+                             float* Y, long y_bs, const float* bias, float* ypre, long ypre_bs,
+                             const float* gpre, long gpre_bs, int M, int N, int K, int P, int nb,
+                             int act, int gact, int bact, int accumulate, float slope,
+                             hipStream_t st) {
+  DSG_REQUIRE(A && B && Y && M > 0 && N > 0 && K > 0 && P > 0 && nb > 0, "dsgan_pw_gemm: bad args");
+  PwArgs g{};
+  g.A = A; g.a_bs = a_bs; g.B = B; g.b_bs = b_bs; g.Y = Y; g.y_bs = y_bs; g.bias = bias;
+  g.ypre = ypre; g.ypre_bs = ypre_bs; g.gpre = gpre; g.gpre_bs = gpre_bs;
+  g.act = act; g.gact = gact; g.bact = bact; g.accumulate = accumulate; g.slope = slope;
+  g.P = P;
+  if (mode == PW_WGRAD) {
+    DSG_REQUIRE(dsgan_pw_supported(mode, M, K, P, a_bs, b_bs, A, B), "dsgan_pw_gemm: unsupported WGRAD shape");
+    g.M = M; g.N = N; g.K = nb * P;
+    const int BM = M > 64 ? 128 : 64;
+    const long tiles = (long)((M + BM - 1) / BM) * ((N + 127) / 128);
+    long splits = (2048 + tiles - 1) / tiles;
+    const long max_splits = (g.K + 8L * PBK - 1) / (8L * PBK);
+    if (splits > max_splits) splits = max_splits;
+    if (splits < 1) splits = 1;
+    long ks = (g.K + splits - 1) / splits;
+    ks = (ks + PBK - 1) / PBK * PBK;
+    splits = (g.K + ks - 1) / ks;
+    g.k_split = (int)ks;
+    if (BM == 128) pw_launch<PW_WGRAD, 128>(g, (int)splits, st);
+    else pw_launch<PW_WGRAD, 64>(g, (int)splits, st);
+  } else {
+    DSG_REQUIRE(dsgan_pw_supported(mode, M, K, P, a_bs, b_bs, A, B), "dsgan_pw_gemm: unsupported shape");
+    DSG_REQUIRE((long)M * P * 4 < (1L << 32), "dsgan_pw_gemm: M*P too large for a buffer resource");
+    g.M = M; g.N = nb * P; g.K = K;
+    const bool big = M > 64;
+    if (mode == PW_FWD) { if (big) pw_launch<PW_FWD, 128>(g, 1, st); else pw_launch<PW_FWD, 64>(g, 1, st); }
+    else { if (big) pw_launch<PW_DGRAD, 128>(g, 1, st); else pw_launch<PW_DGRAD, 64>(g, 1, st); }
+  }
+  DSG_CHECK_LAUNCH();
+  return 0;
+}

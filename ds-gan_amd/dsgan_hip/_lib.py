@@ -22,9 +22,12 @@ SIGNATURES = {
     "dsgan_abi_version": [],
     "dsgan_last_error_string": [],
     # igemm.hip
-    "dsgan_conv_fwd": [P, L, P, P, P, L, P, L, I, I, I, I, I, I, I, I, I, I, I, I, F, I, I, S],
+    "dsgan_conv_fwd": [P, L, P, P, P, L, P, L] + [I] * 12 + [F, I, I, I, S],
     "dsgan_conv_dgrad": [P, L, P, P, P, L, P, L, P, L, I, I, I, I, I, I, I, I, I, I, I, I, I, F, I, I, S],
-    "dsgan_conv_wgrad": [P, L, P, L, P] + [I] * 12 + [S],
+    "dsgan_conv_wgrad": [P, L, P, L, P] + [I] * 13 + [S],
+    # pwgemm.hip
+    "dsgan_pw_supported": [I, I, I, I, L, L, P, P],
+    "dsgan_pw_gemm": [I, P, L, P, L, P, L, P, P, L, P, L, I, I, I, I, I, I, I, I, I, F, S],
     # dwconv.hip
     "dsgan_dwconv_fwd": [P, L, P, P, P, L, I, I, I, I, I, I, S],
     "dsgan_dwconv_wgrad": [P, L, P, L, P, P, I, I, I, I, I, S],

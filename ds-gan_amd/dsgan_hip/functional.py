@@ -53,18 +53,22 @@ class KernelTimer:
         e0.record()
         return e0
 
-    def end(self, e0, flops):
+    def end(self, e0, flops, tag=None):
         if e0 is None:
             return
         e1 = torch.cuda.Event(enable_timing=True)
         e1.record()
-        self.rec.append((e0, e1, flops))
+        self.rec.append((e0, e1, flops, tag))
 
     def summary(self):
         torch.cuda.synchronize()
-        ms = sum(a.elapsed_time(b) for a, b, _ in self.rec)
-        fl = sum(f for _, _, f in self.rec)
+        ms = sum(r[0].elapsed_time(r[1]) for r in self.rec)
+        fl = sum(r[2] for r in self.rec)
         return dict(launches=len(self.rec), total_ms=ms, flops=fl)
+
+    def table(self):
+        torch.cuda.synchronize()
+        return [(r[0].elapsed_time(r[1]), r[2], r[3]) for r in self.rec]
 
 
 IGEMM_TIMER = KernelTimer()
@@ -106,7 +110,13 @@ def _grad_buf(p):
 # raw launchers (no autograd)
 # ------------------------------------------------------------------------------------------
 
-def conv_fwd_raw(x, w, b, stride, pad, act=None, out=None, pre=None, accumulate=False):
+def _pw_ok(mode, M, K, P, a_bs, b_bs, a, b):
+    if _state["prec"] != "bf16":
+        return False
+    return bool(_lib.load().dsgan_pw_supported(mode, M, K, P, a_bs, b_bs, a, b))
+
+
+def conv_fwd_raw(x, w, b, stride, pad, act=None, out=None, pre=None, accumulate=False, xact=None):
     x, xbs = nchw(x)
     N, Cin, H, W = x.shape
     Cout, Cin_w, KH, KW = w.shape if w.dim() == 4 else (w.shape[0], w.shape[1], 1, 1)
@@ -120,9 +130,14 @@ def conv_fwd_raw(x, w, b, stride, pad, act=None, out=None, pre=None, accumulate=
     if pre is not None:
         pre, pbs = nchw(pre)
     e0 = IGEMM_TIMER.begin()
-    call("dsgan_conv_fwd", ptr(x), xbs, ptr(w), ptr(b), ptr(y), ybs, ptr(pre), pbs, N, Cin, H, W,
-         Cout, KH, KW, stride, pad, Ho, Wo, ACT[act], LRELU_SLOPE, int(accumulate), _prec(), stream())
-    IGEMM_TIMER.end(e0, _conv_flops(N, Cin, Cout, KH, KW, Ho, Wo))
+    if KH == 1 and KW == 1 and stride == 1 and pad == 0 and _pw_ok(0, Cout, Cin, H * W, 0, xbs, w.data_ptr(), x.data_ptr()):
+        call("dsgan_pw_gemm", 0, ptr(w), 0, ptr(x), xbs, ptr(y), ybs, ptr(b), ptr(pre), pbs, None, 0,
+             Cout, N * H * W, Cin, H * W, N, ACT[act], 0, ACT[xact], int(accumulate), LRELU_SLOPE, stream())
+    else:
+        call("dsgan_conv_fwd", ptr(x), xbs, ptr(w), ptr(b), ptr(y), ybs, ptr(pre), pbs, N, Cin, H, W,
+             Cout, KH, KW, stride, pad, Ho, Wo, ACT[act], LRELU_SLOPE, int(accumulate), ACT[xact], _prec(),
+             stream())
+    IGEMM_TIMER.end(e0, _conv_flops(N, Cin, Cout, KH, KW, Ho, Wo), ("fwd", N, Cin, H, W, Cout, KH, stride))
     return y
 
 
@@ -139,23 +154,33 @@ def conv_dgrad_raw(dy, w, x_shape, stride, pad, bias=None, act=None, gpre=None, 
     if gpre is not None:
         gpre, gbs = nchw(gpre)
     e0 = IGEMM_TIMER.begin()
-    call("dsgan_conv_dgrad", ptr(dy), dybs, ptr(w), ptr(bias), ptr(dx), dxbs, None, 0, ptr(gpre), gbs,
-         ACT[gact], N, Cin, H, W, Cout, KH, KW, stride, pad, Ho, Wo, ACT[act], LRELU_SLOPE,
-         int(accumulate), _prec(), stream())
-    IGEMM_TIMER.end(e0, _conv_flops(N, Cin, Cout, KH, KW, Ho, Wo))
+    if (KH == 1 and KW == 1 and stride == 1 and pad == 0 and bias is None and act is None
+            and not accumulate and _pw_ok(1, Cin, Cout, H * W, 0, dybs, w.data_ptr(), dy.data_ptr())):
+        call("dsgan_pw_gemm", 1, ptr(w), 0, ptr(dy), dybs, ptr(dx), dxbs, None, None, 0, ptr(gpre), gbs,
+             Cin, N * H * W, Cout, H * W, N, 0, ACT[gact], 0, 0, LRELU_SLOPE, stream())
+    else:
+        call("dsgan_conv_dgrad", ptr(dy), dybs, ptr(w), ptr(bias), ptr(dx), dxbs, None, 0, ptr(gpre), gbs,
+             ACT[gact], N, Cin, H, W, Cout, KH, KW, stride, pad, Ho, Wo, ACT[act], LRELU_SLOPE,
+             int(accumulate), _prec(), stream())
+    IGEMM_TIMER.end(e0, _conv_flops(N, Cin, Cout, KH, KW, Ho, Wo), ("dgrad", N, Cin, H, W, Cout, KH, stride))
     return dx
 
 
-def conv_wgrad_raw(dy, x, dw, stride, pad):
+def conv_wgrad_raw(dy, x, dw, stride, pad, xact=None):
     dy, dybs = nchw(dy)
     x, xbs = nchw(x)
     N, Cin, H, W = x.shape
     Cout = dy.shape[1]
     KH, KW = (dw.shape[2], dw.shape[3]) if dw.dim() == 4 else (1, 1)
     e0 = IGEMM_TIMER.begin()
-    call("dsgan_conv_wgrad", ptr(dy), dybs, ptr(x), xbs, ptr(dw), N, Cin, H, W, Cout, KH, KW,
-         stride, pad, dy.shape[2], dy.shape[3], _prec(), stream())
-    IGEMM_TIMER.end(e0, _conv_flops(N, Cin, Cout, KH, KW, dy.shape[2], dy.shape[3]))
+    if KH == 1 and KW == 1 and stride == 1 and pad == 0 and _pw_ok(2, Cout, N * H * W, H * W, dybs, xbs, dy.data_ptr(), x.data_ptr()):
+        call("dsgan_pw_gemm", 2, ptr(dy), dybs, ptr(x), xbs, ptr(dw), 0, None, None, 0, None, 0,
+             Cout, Cin, N * H * W, H * W, N, 0, 0, ACT[xact], 0, LRELU_SLOPE, stream())
+    else:
+        call("dsgan_conv_wgrad", ptr(dy), dybs, ptr(x), xbs, ptr(dw), N, Cin, H, W, Cout, KH, KW,
+             stride, pad, dy.shape[2], dy.shape[3], ACT[xact], _prec(), stream())
+    IGEMM_TIMER.end(e0, _conv_flops(N, Cin, Cout, KH, KW, dy.shape[2], dy.shape[3]),
+                    ("wgrad", N, Cin, H, W, Cout, KH, stride))
 
 
 def channel_sum_raw(dy, out):
@@ -269,30 +294,32 @@ def conv_transpose3s2(x, w, b):
 # ------------------------------------------------------------------------------------------
 
 class PwMlpFn(torch.autograd.Function):
+    """Only the pre-GELU hidden z [N,4C,H,W] is materialised: pwconv2 and its weight-grad read
+    gelu(z) through the GEMM's activation-on-load, and the data-grad of pwconv2 multiplies by
+    gelu'(z) in its epilogue -- the 4C-channel g = gelu(z) never touches HBM."""
+
     @staticmethod
     def forward(ctx, h, x, w1, b1, w2, b2, ws):
         N, C, H, W = h.shape
-        P = w2.shape[0]
         w1v = w1.view(w1.shape[0], w1.shape[1], 1, 1)
         w2v = w2.view(w2.shape[0], w2.shape[1], 1, 1)
-        z = _empty(N, w1.shape[0], H, W, h)
-        g = conv_fwd_raw(h, w1v, b1, 1, 0, act="gelu", pre=z)
+        z = conv_fwd_raw(h, w1v, b1, 1, 0)
         out = conv_fwd_raw(x, ws, None, 1, 0)
-        conv_fwd_raw(g, w2v, b2, 1, 0, out=out, accumulate=True)
-        ctx.save_for_backward(h, x, z, g, w1v, w2v, ws)
+        conv_fwd_raw(z, w2v, b2, 1, 0, out=out, accumulate=True, xact="gelu")
+        ctx.save_for_backward(h, x, z, w1v, w2v, ws)
         ctx.refs = (w1, b1, w2, b2, ws)
         return out
 
     @staticmethod
     def backward(ctx, dy):
-        h, x, z, g, w1v, w2v, ws = ctx.saved_tensors
+        h, x, z, w1v, w2v, ws = ctx.saved_tensors
         w1, b1, w2, b2, ws_ref = ctx.refs
         dy = dy.contiguous()
         # dz = (W2^T dy) * gelu'(z)
         dz = conv_dgrad_raw(dy, w2v, tuple(z.shape), 1, 0, gpre=z, gact="gelu")
         gw2, gb2, gws = _grad_buf(w2), _grad_buf(b2), _grad_buf(ws_ref)
         if gw2 is not None:
-            conv_wgrad_raw(dy, g, gw2.view(w2v.shape), 1, 0)
+            conv_wgrad_raw(dy, z, gw2.view(w2v.shape), 1, 0, xact="gelu")
         if gb2 is not None:
             channel_sum_raw(dy, gb2)
         if gws is not None:

@@ -39,22 +39,37 @@ const char* dsgan_last_error_string(void);
  *   res 3x3 head                 :459
  *   PatchGAN 4x4 s2/s1           models/networks.py:543-569
  *   VGG16 3x3 + ReLU             models/vgg.py:15-24
- * y = act(conv(x, w) + bias) [+ y if accumulate]; ypre (nullable) receives the pre-activation. */
+ * y = act(conv(xact(x), w) + bias) [+ y if accumulate]; ypre (nullable) receives the
+ * pre-activation; xact (act code) is applied to x as it is loaded (the Block MLP stores only
+ * the pre-GELU hidden z and both of its consumers read gelu(z) this way). */
 int dsgan_conv_fwd(const float* x, long x_bs, const float* w, const float* bias, float* y,
                    long y_bs, float* ypre, long ypre_bs, int N, int Cin, int H, int W, int Cout,
                    int KH, int KW, int stride, int pad, int Ho, int Wo, int act, float slope,
-                   int accumulate, int prec, hipStream_t stream);
+                   int accumulate, int xact, int prec, hipStream_t stream);
 /* dx = conv^T(dy, w) (+bias) ; if gpre: dx *= act'(gpre) with act code gact (fuses the
- * backward of the activation that produced the conv input). */
+ * backward of the activation that produced the conv input).  stride 2 runs as four dense
+ * parity-class GEMMs (no MFMA work on the structural zeros of the strided transpose). */
 int dsgan_conv_dgrad(const float* dy, long dy_bs, const float* w, const float* bias, float* dx,
                      long dx_bs, float* ypre, long ypre_bs, const float* gpre, long gpre_bs,
                      int gact, int N, int Cin, int H, int W, int Cout, int KH, int KW, int stride,
                      int pad, int Ho, int Wo, int act, float slope, int accumulate, int prec,
                      hipStream_t stream);
-/* dw[Cout][Cin][KH][KW] += sum_{n,oh,ow} dy * x  (split-K, fp32 atomics) */
+/* dw[Cout][Cin][KH][KW] += sum_{n,oh,ow} dy * xact(x)  (split-K, fp32 atomics) */
 int dsgan_conv_wgrad(const float* dy, long dy_bs, const float* x, long x_bs, float* dw, int N,
                      int Cin, int H, int W, int Cout, int KH, int KW, int stride, int pad, int Ho,
-                     int Wo, int prec, hipStream_t stream);
+                     int Wo, int xact, int prec, hipStream_t stream);
+
+/* ---- pointwise (1x1 / Linear) GEMM fast path (pwgemm.hip): bf16 MFMA, fp32 in HBM ----------
+ * mode 0 FWD  : Y[b][M][P] = act(W[M][K] . xact(X[b][K][P]) + bias) (+Y), ypre = pre-act
+ * mode 1 DGRAD: DX[b][M][P] = (W[K][M]^T . DY[b][K][P]) * gact'(gpre)
+ * mode 2 WGRAD: DW[M][N] += sum_{b,p} DY[b][M][p] * xact(X[b][N][p])   (K = P, nb images)
+ * dsgan_pw_supported() reports whether a shape/alignment takes this path (else use igemm). */
+int dsgan_pw_supported(int mode, int M, int K, int P, long a_bs, long b_bs, const void* a,
+                       const void* b);
+int dsgan_pw_gemm(int mode, const float* A, long a_bs, const float* B, long b_bs, float* Y,
+                  long y_bs, const float* bias, float* ypre, long ypre_bs, const float* gpre,
+                  long gpre_bs, int M, int N, int K, int P, int nb, int act, int gact, int bact,
+                  int accumulate, float slope, hipStream_t stream);
 
 /* ---- depthwise conv (dwconv.hip): Block.dwconv :220, MidMLKA.X3..X9 :94-97 ---------------- */
 int dsgan_dwconv_fwd(const float* x, long x_bs, const float* w, const float* bias, float* y,
