@@ -10,8 +10,6 @@
 
 namespace dsg {
 
-constexpr int IN_CACHE = 16;  // elements per thread held in registers (plane <= 256*16)
-
 struct INArgs {
   const float* x; long x_bs;
   const float* scale;           // per-plane multiplier [N*C] applied to x first (nullable)
@@ -21,56 +19,49 @@ struct INArgs {
   int N, C, HW, act; float slope, eps;
 };
 
-// Plane reduction helper: NT threads per plane (NT = 64: one wave, NT = 256: whole block).
+// Plane reduction helper: NT threads per plane (NT = 64: one wave, else the whole block).
 template <int NT>
 __device__ __forceinline__ float plane_sum(float v, float* sh) {
   if (NT == 64) return warp_sum(v);
   return block_sum<NT>(v, sh);
 }
 
-template <int NT>
-__global__ __launch_bounds__(256) void instnorm_fwd_kernel(INArgs a) {
-  __shared__ float sh[4];
-  const int planes_per_block = 256 / NT;
+// One plane per workgroup (NT = 256 / 1024) or per wave (NT = 64, 4 planes per 256-thread
+// block).  Planes up to NT*CACHE elements are read ONCE into registers (two-pass mean/variance
+// from registers); larger planes stream three times.
+template <int NT, int CACHE>
+__global__ __launch_bounds__(NT == 64 ? 256 : NT) void instnorm_fwd_kernel(INArgs a) {
+  __shared__ float sh[16];
+  const int planes_per_block = NT == 64 ? 4 : 1;
   const int plane = blockIdx.x * planes_per_block + (NT == 64 ? (threadIdx.x >> 6) : 0);
   const int t = NT == 64 ? (threadIdx.x & 63) : threadIdx.x;
   if (plane >= a.N * a.C) return;  // whole wave / block uniform
   const int n = plane / a.C, c = plane - n * a.C;
   const float* x = a.x + (long)n * a.x_bs + (long)c * a.HW;
   const float s = a.scale ? a.scale[plane] : 1.f;
-  const bool cached = a.HW <= NT * IN_CACHE;
-  float rv[IN_CACHE];
-  float sum = 0.f;
-  if (cached) {
+  float* y = a.y + (long)n * a.y_bs + (long)c * a.HW;
+  const float* r = a.res ? a.res + (long)n * a.res_bs + (long)c * a.HW : nullptr;
+  const float inv = 1.f / (float)a.HW;
+  if (CACHE > 0) {
+    float rv[CACHE > 0 ? CACHE : 1];
+    float sum = 0.f;
 #pragma unroll
-    for (int j = 0; j < IN_CACHE; ++j) {
+    for (int j = 0; j < CACHE; ++j) {
       const int i = t + j * NT;
       rv[j] = i < a.HW ? x[i] * s : 0.f;
       sum += rv[j];
     }
-  } else {
-    for (int i = t; i < a.HW; i += NT) sum += x[i] * s;
-  }
-  const float mean = plane_sum<NT>(sum, sh) / (float)a.HW;
-  float sq = 0.f;
-  if (cached) {
+    const float mean = plane_sum<NT>(sum, sh) * inv;
+    float sq = 0.f;
 #pragma unroll
-    for (int j = 0; j < IN_CACHE; ++j) {
-      const int i = t + j * NT;
+    for (int j = 0; j < CACHE; ++j) {
       const float d = rv[j] - mean;
-      if (i < a.HW) sq += d * d;
+      if (t + j * NT < a.HW) sq += d * d;
     }
-  } else {
-    for (int i = t; i < a.HW; i += NT) { const float d = x[i] * s - mean; sq += d * d; }
-  }
-  const float var = plane_sum<NT>(sq, sh) / (float)a.HW;
-  const float rs = 1.f / sqrtf(var + a.eps);
-  if (t == 0) { a.mean[plane] = mean; a.rstd[plane] = rs; }
-  float* y = a.y + (long)n * a.y_bs + (long)c * a.HW;
-  const float* r = a.res ? a.res + (long)n * a.res_bs + (long)c * a.HW : nullptr;
-  if (cached) {
+    const float rs = 1.f / sqrtf(plane_sum<NT>(sq, sh) * inv + a.eps);
+    if (t == 0) { a.mean[plane] = mean; a.rstd[plane] = rs; }
 #pragma unroll
-    for (int j = 0; j < IN_CACHE; ++j) {
+    for (int j = 0; j < CACHE; ++j) {
       const int i = t + j * NT;
       if (i < a.HW) {
         float v = (rv[j] - mean) * rs;
@@ -79,6 +70,13 @@ __global__ __launch_bounds__(256) void instnorm_fwd_kernel(INArgs a) {
       }
     }
   } else {
+    float sum = 0.f;
+    for (int i = t; i < a.HW; i += NT) sum += x[i] * s;
+    const float mean = plane_sum<NT>(sum, sh) * inv;
+    float sq = 0.f;
+    for (int i = t; i < a.HW; i += NT) { const float d = x[i] * s - mean; sq += d * d; }
+    const float rs = 1.f / sqrtf(plane_sum<NT>(sq, sh) * inv + a.eps);
+    if (t == 0) { a.mean[plane] = mean; a.rstd[plane] = rs; }
     for (int i = t; i < a.HW; i += NT) {
       float v = (x[i] * s - mean) * rs;
       if (r) v += r[i];
@@ -105,10 +103,11 @@ struct INBwdArgs {
 // eps), so it is evaluated in closed form: sum dxs = 0 and sum xhat^2 = HW*var*rstd^2 give
 //   dscale = mean(g*xhat) * HW * eps * rstd^2 / s
 // which is what the fp64 reference converges to; the direct fp32 sum loses ~1e-3 relative.
-template <int NT>
-__global__ __launch_bounds__(256) void instnorm_bwd_kernel(INBwdArgs a) {
-  __shared__ float sh[4];
-  const int planes_per_block = 256 / NT;
+// g is cached in registers (planes <= NT*CACHE); xhat is recomputed from x in the final pass.
+template <int NT, int CACHE>
+__global__ __launch_bounds__(NT == 64 ? 256 : NT) void instnorm_bwd_kernel(INBwdArgs a) {
+  __shared__ float sh[16];
+  const int planes_per_block = NT == 64 ? 4 : 1;
   const int plane = blockIdx.x * planes_per_block + (NT == 64 ? (threadIdx.x >> 6) : 0);
   const int t = NT == 64 ? (threadIdx.x & 63) : threadIdx.x;
   if (plane >= a.N * a.C) return;
@@ -120,9 +119,7 @@ __global__ __launch_bounds__(256) void instnorm_bwd_kernel(INBwdArgs a) {
   float* dres = a.dres ? a.dres + (long)n * a.dres_bs + po : nullptr;
   const float s = a.scale ? a.scale[plane] : 1.f;
   const float mean = a.mean[plane], rs = a.rstd[plane];
-  const bool cached = a.HW <= NT * IN_CACHE;
-  float gv[IN_CACHE], hv[IN_CACHE];
-  float sg = 0.f, sgh = 0.f;
+  float* dx = a.dx + (long)n * a.dx_bs + po;
   auto grad_at = [&](int i, float& xh) -> float {
     xh = (x[i] * s - mean) * rs;
     float g = dy[i];
@@ -130,39 +127,39 @@ __global__ __launch_bounds__(256) void instnorm_bwd_kernel(INBwdArgs a) {
     if (dres) dres[i] = g;
     return g;
   };
-  if (cached) {
-#pragma unroll
-    for (int j = 0; j < IN_CACHE; ++j) {
-      const int i = t + j * NT;
-      gv[j] = 0.f; hv[j] = 0.f;
-      if (i < a.HW) { gv[j] = grad_at(i, hv[j]); sg += gv[j]; sgh += gv[j] * hv[j]; }
-    }
-  } else {
-    for (int i = t; i < a.HW; i += NT) { float xh; const float g = grad_at(i, xh); sg += g; sgh += g * xh; }
-  }
   const float inv = 1.f / (float)a.HW;
-  const float mg = plane_sum<NT>(sg, sh) * inv;
-  const float mgh = plane_sum<NT>(sgh, sh) * inv;
-  float* dx = a.dx + (long)n * a.dx_bs + po;
-  if (cached) {
+  float sg = 0.f, sgh = 0.f;
+  if (CACHE > 0) {
+    float gv[CACHE > 0 ? CACHE : 1];
 #pragma unroll
-    for (int j = 0; j < IN_CACHE; ++j) {
+    for (int j = 0; j < CACHE; ++j) {
+      const int i = t + j * NT;
+      gv[j] = 0.f;
+      if (i < a.HW) { float xh; gv[j] = grad_at(i, xh); sg += gv[j]; sgh += gv[j] * xh; }
+    }
+    const float mg = plane_sum<NT>(sg, sh) * inv;
+    const float mgh = plane_sum<NT>(sgh, sh) * inv;
+#pragma unroll
+    for (int j = 0; j < CACHE; ++j) {
       const int i = t + j * NT;
       if (i < a.HW) {
-        const float dxs = rs * (gv[j] - mg - hv[j] * mgh);
-        dx[i] = s * dxs;
+        const float xh = (x[i] * s - mean) * rs;
+        dx[i] = s * rs * (gv[j] - mg - xh * mgh);
       }
     }
+    if (a.dscale && t == 0) a.dscale[plane] = mgh * (float)a.HW * a.eps * rs * rs / s;
   } else {
+    for (int i = t; i < a.HW; i += NT) { float xh; const float g = grad_at(i, xh); sg += g; sgh += g * xh; }
+    const float mg = plane_sum<NT>(sg, sh) * inv;
+    const float mgh = plane_sum<NT>(sgh, sh) * inv;
     for (int i = t; i < a.HW; i += NT) {
       const float xh = (x[i] * s - mean) * rs;
       float g = dy[i];
       if (a.act != ACT_NONE) g *= act_g(a.act, r ? xh + r[i] : xh, a.slope);
-      const float dxs = rs * (g - mg - xh * mgh);
-      dx[i] = s * dxs;
+      dx[i] = s * rs * (g - mg - xh * mgh);
     }
+    if (a.dscale && t == 0) a.dscale[plane] = mgh * (float)a.HW * a.eps * rs * rs / s;
   }
-  if (a.dscale && t == 0) a.dscale[plane] = mgh * (float)a.HW * a.eps * rs * rs / s;
 }
 
 // ---------------------------------------------------------------------------------------
@@ -170,25 +167,28 @@ __global__ __launch_bounds__(256) void instnorm_bwd_kernel(INBwdArgs a) {
 // Indices are the plane-flat argmax ih*W+iw, first maximum in row-major window order, NaN wins
 // (the rule of PyTorch's CPU max_pool2d) -- bit-exact with the reference's int64 indices.
 // ---------------------------------------------------------------------------------------
+// 2-D grid: blockIdx.y walks planes (n,c), blockIdx.x chunks of the plane; 32-bit index math.
 __global__ void maxpool_fwd_kernel(const float* __restrict__ x, long x_bs, float* __restrict__ y,
                                    long y_bs, int* __restrict__ idx, int N, int C, int H, int W,
                                    int k) {
-  const int Ho = H / k, Wo = W / k;
-  const long total = (long)N * C * Ho * Wo;
-  for (long o = blockIdx.x * (long)blockDim.x + threadIdx.x; o < total; o += (long)gridDim.x * blockDim.x) {
-    const int ow = o % Wo; long t = o / Wo;
-    const int oh = t % Ho; t /= Ho;
-    const int c = t % C; const int n = t / C;
+  const int Ho = H / k, Wo = W / k, Po = Ho * Wo;
+  for (int plane = blockIdx.y; plane < N * C; plane += gridDim.y) {
+    const int n = plane / C, c = plane - n * C;
     const float* xp = x + (long)n * x_bs + (long)c * H * W;
-    float best = -INFINITY; int bi = oh * k * W + ow * k;
-    for (int i = 0; i < k; ++i)
-      for (int j = 0; j < k; ++j) {
-        const int q = (oh * k + i) * W + ow * k + j;
-        const float v = xp[q];
-        if (v > best || isnan(v)) { best = v; bi = q; }
-      }
-    y[(long)n * y_bs + ((long)c * Ho + oh) * Wo + ow] = best;
-    idx[((long)n * C + c) * Ho * Wo + (long)oh * Wo + ow] = bi;
+    float* yp = y + (long)n * y_bs + (long)c * Po;
+    int* ip = idx + (long)plane * Po;
+    for (int o = blockIdx.x * blockDim.x + threadIdx.x; o < Po; o += gridDim.x * blockDim.x) {
+      const int oh = o / Wo, ow = o - oh * Wo;
+      const float* wp = xp + (oh * k) * W + ow * k;
+      float best = -INFINITY; int bi = (oh * k) * W + ow * k;
+      for (int i = 0; i < k; ++i)
+        for (int j = 0; j < k; ++j) {
+          const float v = wp[i * W + j];
+          if (v > best || isnan(v)) { best = v; bi = (oh * k + i) * W + ow * k + j; }
+        }
+      yp[o] = best;
+      ip[o] = bi;
+    }
   }
 }
 
@@ -196,21 +196,30 @@ __global__ void maxpool_fwd_kernel(const float* __restrict__ x, long x_bs, float
 __global__ void maxpool_bwd_kernel(const float* __restrict__ dy, long dy_bs, const int* __restrict__ idx,
                                    float* __restrict__ dx, long dx_bs, int N, int C, int H, int W,
                                    int k, int accumulate) {
-  const int Ho = H / k, Wo = W / k;
-  const long total = (long)N * C * H * W;
-  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
-    const int iw = e % W; long t = e / W;
-    const int ih = t % H; t /= H;
-    const int c = t % C; const int n = t / C;
-    const int oh = ih / k, ow = iw / k;
-    float v = 0.f;
-    if (oh < Ho && ow < Wo) {
-      const long o = ((long)c * Ho + oh) * Wo + ow;
-      if (idx[(long)n * C * Ho * Wo + o] == ih * W + iw) v = dy[(long)n * dy_bs + o];
+  const int Ho = H / k, Wo = W / k, Po = Ho * Wo, HW = H * W;
+  for (int plane = blockIdx.y; plane < N * C; plane += gridDim.y) {
+    const int n = plane / C, c = plane - n * C;
+    const float* gp = dy + (long)n * dy_bs + (long)c * Po;
+    const int* ip = idx + (long)plane * Po;
+    float* dp = dx + (long)n * dx_bs + (long)c * HW;
+    for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < HW; e += gridDim.x * blockDim.x) {
+      const int ih = e / W, iw = e - ih * W;
+      const int oh = ih / k, ow = iw / k;
+      float v = 0.f;
+      if (oh < Ho && ow < Wo) {
+        const int o = oh * Wo + ow;
+        if (ip[o] == e) v = gp[o];
+      }
+      dp[e] = accumulate ? dp[e] + v : v;
     }
-    float* d = dx + (long)n * dx_bs + ((long)c * H + ih) * W + iw;
-    *d = accumulate ? *d + v : v;
   }
+}
+
+static inline dim3 plane_grid(long per_plane, long planes) {
+  long gx = (per_plane + 255) / 256;
+  if (gx > 1024) gx = 1024;
+  long gy = planes > 65535 ? 65535 : planes;
+  return dim3((unsigned)(gx < 1 ? 1 : gx), (unsigned)gy);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -399,16 +408,24 @@ __global__ void act_bwd_kernel(const float* dy, const float* pre, float* dx, lon
   }
 }
 
-// out[c] += sum_{n,p} dy[n,c,p]   (bias gradient; one block per (n,c) plane, atomics over n)
+// out[c] += sum_{n,p} dy[n,c,p]   (bias gradient; NT threads per (n,c) plane, atomics over n)
+template <int NT>
 __global__ __launch_bounds__(256) void channel_sum_kernel(const float* dy, long dy_bs, float* out, int N, int C, int HW) {
   __shared__ float sh[4];
-  const int plane = blockIdx.x;
+  const int plane = blockIdx.x * (256 / NT) + (NT == 64 ? (threadIdx.x >> 6) : 0);
+  const int t = NT == 64 ? (threadIdx.x & 63) : threadIdx.x;
+  if (plane >= N * C) return;
   const int n = plane / C, c = plane - n * C;
   const float* p = dy + (long)n * dy_bs + (long)c * HW;
   float s = 0.f;
-  for (int i = threadIdx.x; i < HW; i += 256) s += p[i];
-  s = block_sum<256>(s, sh);
-  if (threadIdx.x == 0) atomicAdd(out + c, s);
+  if ((HW & 3) == 0 && (((uintptr_t)p) & 15) == 0) {
+    const float4* p4 = reinterpret_cast<const float4*>(p);
+    for (int i = t; i < HW / 4; i += NT) { const float4 v = p4[i]; s += (v.x + v.y) + (v.z + v.w); }
+  } else {
+    for (int i = t; i < HW; i += NT) s += p[i];
+  }
+  s = NT == 64 ? warp_sum(s) : block_sum<NT>(s, sh);
+  if (t == 0) atomicAdd(out + c, s);
 }
 
 static inline unsigned grid_for(long n, int bs = 256) {
@@ -430,10 +447,16 @@ int dsgan_instnorm_fwd(const float* x, long x_bs, const float* scale, const floa
   DSG_REQUIRE(x && y && mean && rstd && N > 0 && C > 0 && HW > 0, "dsgan_instnorm_fwd: bad args");
   INArgs a{x, x_bs, scale, res, res_bs, y, y_bs, mean, rstd, N, C, HW, act, slope, eps};
   const int planes = N * C;
-  if (HW <= 64 * IN_CACHE)
-    hipLaunchKernelGGL(instnorm_fwd_kernel<64>, dim3(cdiv(planes, 4)), dim3(256), 0, st, a);
+  if (HW <= 64 * 16)
+    hipLaunchKernelGGL((instnorm_fwd_kernel<64, 16>), dim3(cdiv(planes, 4)), dim3(256), 0, st, a);
+  else if (HW <= 256 * 16)
+    hipLaunchKernelGGL((instnorm_fwd_kernel<256, 16>), dim3(planes), dim3(256), 0, st, a);
+  else if (HW <= 1024 * 16)
+    hipLaunchKernelGGL((instnorm_fwd_kernel<1024, 16>), dim3(planes), dim3(1024), 0, st, a);
+  else if (HW <= 1024 * 64)
+    hipLaunchKernelGGL((instnorm_fwd_kernel<1024, 64>), dim3(planes), dim3(1024), 0, st, a);
   else
-    hipLaunchKernelGGL(instnorm_fwd_kernel<256>, dim3(planes), dim3(256), 0, st, a);
+    hipLaunchKernelGGL((instnorm_fwd_kernel<1024, 0>), dim3(planes), dim3(1024), 0, st, a);
   DSG_CHECK_LAUNCH();
   return 0;
 }
@@ -446,10 +469,16 @@ int dsgan_instnorm_bwd(const float* dy, long dy_bs, const float* x, long x_bs, c
   INBwdArgs a{dy, dy_bs, x, x_bs, scale, res, res_bs, mean, rstd, dx, dx_bs, dres, dres_bs, dscale,
               N, C, HW, act, slope, eps};
   const int planes = N * C;
-  if (HW <= 64 * IN_CACHE)
-    hipLaunchKernelGGL(instnorm_bwd_kernel<64>, dim3(cdiv(planes, 4)), dim3(256), 0, st, a);
+  if (HW <= 64 * 16)
+    hipLaunchKernelGGL((instnorm_bwd_kernel<64, 16>), dim3(cdiv(planes, 4)), dim3(256), 0, st, a);
+  else if (HW <= 256 * 16)
+    hipLaunchKernelGGL((instnorm_bwd_kernel<256, 16>), dim3(planes), dim3(256), 0, st, a);
+  else if (HW <= 1024 * 16)
+    hipLaunchKernelGGL((instnorm_bwd_kernel<1024, 16>), dim3(planes), dim3(1024), 0, st, a);
+  else if (HW <= 1024 * 64)
+    hipLaunchKernelGGL((instnorm_bwd_kernel<1024, 64>), dim3(planes), dim3(1024), 0, st, a);
   else
-    hipLaunchKernelGGL(instnorm_bwd_kernel<256>, dim3(planes), dim3(256), 0, st, a);
+    hipLaunchKernelGGL((instnorm_bwd_kernel<1024, 0>), dim3(planes), dim3(1024), 0, st, a);
   DSG_CHECK_LAUNCH();
   return 0;
 }
@@ -457,9 +486,8 @@ int dsgan_instnorm_bwd(const float* dy, long dy_bs, const float* x, long x_bs, c
 int dsgan_maxpool_fwd(const float* x, long x_bs, float* y, long y_bs, int* idx, int N, int C, int H,
                       int W, int k, hipStream_t st) {
   DSG_REQUIRE(x && y && idx && k > 0 && H >= k && W >= k, "dsgan_maxpool_fwd: bad args");
-  const long total = (long)N * C * (H / k) * (W / k);
-  hipLaunchKernelGGL(maxpool_fwd_kernel, dim3(grid_for(total)), dim3(256), 0, st, x, x_bs, y, y_bs,
-                     idx, N, C, H, W, k);
+  hipLaunchKernelGGL(maxpool_fwd_kernel, plane_grid((long)(H / k) * (W / k), (long)N * C), dim3(256), 0, st,
+                     x, x_bs, y, y_bs, idx, N, C, H, W, k);
   DSG_CHECK_LAUNCH();
   return 0;
 }
@@ -467,9 +495,8 @@ int dsgan_maxpool_fwd(const float* x, long x_bs, float* y, long y_bs, int* idx, 
 int dsgan_maxpool_bwd(const float* dy, long dy_bs, const int* idx, float* dx, long dx_bs, int N,
                       int C, int H, int W, int k, int accumulate, hipStream_t st) {
   DSG_REQUIRE(dy && idx && dx && k > 0, "dsgan_maxpool_bwd: bad args");
-  const long total = (long)N * C * H * W;
-  hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(grid_for(total)), dim3(256), 0, st, dy, dy_bs, idx,
-                     dx, dx_bs, N, C, H, W, k, accumulate);
+  hipLaunchKernelGGL(maxpool_bwd_kernel, plane_grid((long)H * W, (long)N * C), dim3(256), 0, st, dy, dy_bs,
+                     idx, dx, dx_bs, N, C, H, W, k, accumulate);
   DSG_CHECK_LAUNCH();
   return 0;
 }
@@ -557,7 +584,10 @@ int dsgan_act_bwd(const float* dy, const float* pre, float* dx, long n, int act,
 
 int dsgan_channel_sum(const float* dy, long dy_bs, float* out, int N, int C, int HW, hipStream_t st) {
   DSG_REQUIRE(dy && out && N > 0 && C > 0 && HW > 0, "dsgan_channel_sum: bad args");
-  hipLaunchKernelGGL(channel_sum_kernel, dim3(N * C), dim3(256), 0, st, dy, dy_bs, out, N, C, HW);
+  if (HW <= 8192)
+    hipLaunchKernelGGL(channel_sum_kernel<64>, dim3(cdiv((long)N * C, 4)), dim3(256), 0, st, dy, dy_bs, out, N, C, HW);
+  else
+    hipLaunchKernelGGL(channel_sum_kernel<256>, dim3(N * C), dim3(256), 0, st, dy, dy_bs, out, N, C, HW);
   DSG_CHECK_LAUNCH();
   return 0;
 }

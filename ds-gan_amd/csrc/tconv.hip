@@ -1,0 +1,291 @@
+// Tap-major implicit-GEMM convolution for KxK convs with K-channel count % 32 == 0 (gfx950, bf16 MFMA).
+//
+// Covers the dense 3x3 / 4x4 contractions of the step: VGG16 3x3 convs forward and data-grad
+// (DSGAN/models/vgg.py:15-24), the PatchGAN 4x4 s2/s1 convs (DSGAN/models/networks.py:543-569),
+// the G head (MixConvNeXtML.py:459) and the ConvTranspose2d 3x3 s2 forward (its stride-2
+// parity classes, :53,150).
+//
+//   out[b][m][dst(o)] = act( sum_{tap, k} Wt[tap][m][k] * in[b][k][o*s + d(tap)] + bias[m] )
+//
+// * K is ordered tap-major (tap outer, channel inner): one 32-deep K step is 32 channels of ONE
+//   tap, so every B row of the step has the same spatial shift.  Each thread owns one output
+//   pixel (column) of the 128-pixel tile and 16 consecutive channels; the pixel's input offset
+//   for the tap is computed once per tap, and channels advance by a scalar plane stride.
+// * Loads are buffer loads; a tap that falls in the zero padding gets an offset past the
+//   buffer range, so the hardware returns 0 -- no per-element mask VALU.
+// * Weights are pre-transformed once per call into Wt[tap][m][k] (dsgan_conv_wtrans), so the A
+//   tile is a row-major float4 stream.  Data-grads are the same kernel: stride 1 with the
+//   flipped/transposed kernel, stride 2 as four parity classes each a stride-1 conv whose
+//   outputs land on a stride-2 lattice of the destination.
+#include "common.h"
+
+namespace dsg {
+
+typedef __attribute__((ext_vector_type(8))) __bf16 tbf16x8;
+typedef __attribute__((ext_vector_type(16))) float tf32x16;
+
+constexpr int TBK = 32;
+constexpr int T_STR = TBK + 8;  // [rows][k] bf16 tile stride, 80 B (conflict-free ds_read_b128)
+constexpr int T_MAXTAPS = 16;
+
+struct TcArgs {
+  const float* X; long x_bs;     // input  [nb][K][Hin][Win]
+  const float* Wt;               // [taps][M][K]
+  float* Y; long y_bs;           // output [nb][M][Hdst][Wdst]
+  const float* bias;
+  const float* gpre; long gpre_bs;  // dst-shaped, act' multiplier (data-grad of the producer's act)
+  int nb, K, M, Hin, Win, Hout, Wout, stride;
+  int ntaps;
+  int dh[T_MAXTAPS], dw[T_MAXTAPS];   // input offset of each tap: ih = oh*stride + dh
+  int Hdst, Wdst, os, ph, pw;          // dst pixel = (oh*os + ph, ow*os + pw)
+  int act, gact; float slope;
+};
+
+template <int BM>
+__global__ __launch_bounds__(256) void tconv_kernel(TcArgs g) {
+  constexpr int BN = 128;
+  constexpr int WM = 2, WN = 2;
+  constexpr int TM = BM / WM / 32, TN = BN / WN / 32;
+  constexpr int A_SZ = BM * T_STR, B_SZ = BN * T_STR;
+  constexpr int A_ITEMS = BM * 8 / 256;  // float4 items of the [BM][32] A tile
+  __shared__ __attribute__((aligned(16))) __bf16 smem[2 * (A_SZ + B_SZ)];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  const int lr = lane & 31, lh = lane >> 5;
+
+  const int Pout = g.Hout * g.Wout;
+  const int ntpi = (Pout + BN - 1) / BN;       // N tiles per image
+  const int mt = (g.M + BM - 1) / BM;
+  int tile;
+  {
+    const int nwg = gridDim.x, id = blockIdx.x;
+    const int xcd = id & 7, q = nwg >> 3, r = nwg & 7;
+    tile = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (id >> 3);
+  }
+  const int m_t = tile % mt, rest = tile / mt;
+  const int bimg = rest / ntpi, nt_i = rest - bimg * ntpi;
+  const int m0 = m_t * BM, q0 = nt_i * BN;
+
+  const int HWin = g.Hin * g.Win;
+  const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(g.X + (long)bimg * g.x_bs), (short)0, (unsigned)((long)g.K * HWin * 4), 0x00020000);
+
+  // B staging: thread -> column c = tid % 128, channels 16*(tid/128) .. +15 of the step
+  const int col = tid & 127, kc = tid >> 7;
+  const int q = q0 + col;
+  const bool qv = q < Pout;
+  const int oh = qv ? q / g.Wout : 0, ow = qv ? q - (q / g.Wout) * g.Wout : 0;
+  const int ih0 = oh * g.stride, iw0 = ow * g.stride;
+
+  const int ksteps_per_tap = g.K / TBK;
+  const int nk = g.ntaps * ksteps_per_tap;
+
+  float4 ra[A_ITEMS];
+  float rb[16];
+  auto gload = [&](int kt) {
+    const int tap = kt / ksteps_per_tap;
+    const int k0 = (kt - tap * ksteps_per_tap) * TBK;
+    const float* Wtap = g.Wt + (long)tap * g.M * g.K;
+#pragma unroll
+    for (int i = 0; i < A_ITEMS; ++i) {
+      const int it = tid + i * 256;
+      const int row = it >> 3, kk = k0 + (it & 7) * 4;
+      const int m = m0 + row;
+      const bool ok = m < g.M;
+      const float4 t = *reinterpret_cast<const float4*>(Wtap + (long)(ok ? m : 0) * g.K + kk);
+      ra[i] = ok ? t : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    const int ih = ih0 + g.dh[tap], iw = iw0 + g.dw[tap];
+    const bool in = qv && (unsigned)ih < (unsigned)g.Hin && (unsigned)iw < (unsigned)g.Win;
+    const int voff = in ? (ih * g.Win + iw) * 4 : 0x7fffffff;
+    const int kb = k0 + 16 * kc;
+#pragma unroll
+    for (int j = 0; j < 16; ++j)
+      rb[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rx, voff, (kb + j) * HWin * 4, 0));
+  };
+  auto sstore = [&](int buf) {
+    __bf16* As = smem + buf * (A_SZ + B_SZ);
+    __bf16* Bs = As + A_SZ;
+#pragma unroll
+    for (int i = 0; i < A_ITEMS; ++i) {
+      const int it = tid + i * 256;
+      typedef __attribute__((ext_vector_type(4))) __bf16 b4;
+      b4 v;
+      v[0] = (__bf16)ra[i].x; v[1] = (__bf16)ra[i].y; v[2] = (__bf16)ra[i].z; v[3] = (__bf16)ra[i].w;
+      *reinterpret_cast<b4*>(As + (it >> 3) * T_STR + (it & 7) * 4) = v;
+    }
+    tbf16x8 lo, hi;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { lo[j] = (__bf16)rb[j]; hi[j] = (__bf16)rb[8 + j]; }
+    tbf16x8* dst = reinterpret_cast<tbf16x8*>(Bs + col * T_STR + 16 * kc);
+    dst[0] = lo;
+    dst[1] = hi;
+  };
+
+  tf32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    float bv[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int m = m0 + wm * TM * 32 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+      bv[r] = (g.bias && m < g.M) ? g.bias[m] : 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = bv[r];
+  }
+
+  gload(0);
+  sstore(0);
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int buf = kt & 1;
+    if (kt + 1 < nk) gload(kt + 1);
+    const __bf16* As = smem + buf * (A_SZ + B_SZ);
+    const __bf16* Bs = As + A_SZ;
+#pragma unroll
+    for (int ks = 0; ks < TBK / 16; ++ks) {
+      tbf16x8 af[TM], bfr[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+        af[i] = *reinterpret_cast<const tbf16x8*>(As + (wm * TM * 32 + i * 32 + lr) * T_STR + ks * 16 + lh * 8);
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        bfr[j] = *reinterpret_cast<const tbf16x8*>(Bs + (wn * TN * 32 + j * 32 + lr) * T_STR + ks * 16 + lh * 8);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    if (kt + 1 < nk) sstore(buf ^ 1);
+    __syncthreads();
+  }
+
+  // ---- epilogue: dst pixel of this lane's column, channel rows via scalar offsets ----
+  const int HWd = g.Hdst * g.Wdst;
+  const unsigned range = (unsigned)((long)g.M * HWd * 4);
+  const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(g.Y + (long)bimg * g.y_bs), (short)0, range, 0x00020000);
+  __amdgpu_buffer_rsrc_t rg = ry;
+  if (g.gpre) rg = __builtin_amdgcn_make_buffer_rsrc((void*)(g.gpre + (long)bimg * g.gpre_bs), (short)0, range, 0x00020000);
+  const bool full = m0 + BM <= g.M;
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int c = wn * TN * 32 + j * 32 + lr;
+    const int qq = q0 + c;
+    int vbase = 0x7fffffff;
+    if (qq < Pout) {
+      const int ohh = qq / g.Wout, oww = qq - ohh * g.Wout;
+      vbase = (((ohh * g.os + g.ph) * g.Wdst + oww * g.os + g.pw) + 4 * lh * HWd) * 4;
+    }
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int mrow = m0 + wm * TM * 32 + i * 32;
+      int vrow[16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        vrow[r] = vbase;
+        if (!full && mrow + (r & 3) + 8 * (r >> 2) + 4 * lh >= g.M) vrow[r] = 0x7fffffff;
+      }
+      float v[16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) v[r] = acc[i][j][r];
+      if (g.gpre) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float gv = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+              rg, vrow[r], (mrow + (r & 3) + 8 * (r >> 2)) * HWd * 4, 0));
+          v[r] *= act_g(g.gact, gv, g.slope);
+        }
+      }
+      switch (g.act) {
+        case ACT_NONE: break;
+        case ACT_RELU:
+#pragma unroll
+          for (int r = 0; r < 16; ++r) v[r] = fmaxf(v[r], 0.f);
+          break;
+        default:
+#pragma unroll
+          for (int r = 0; r < 16; ++r) v[r] = act_f(g.act, v[r], g.slope);
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v[r]), ry, vrow[r],
+                                              (mrow + (r & 3) + 8 * (r >> 2)) * HWd * 4, 0);
+    }
+  }
+}
+
+// Wt[tap][m][k] from an OIHW weight W[Co][Ci][KH][KW].
+//   mode 0 (forward):      m = co, k = ci, tap = (kh, kw)
+//   mode 1 (data-grad s1): m = ci, k = co, tap = (kh', kw') with kh = KH-1-kh'
+//   mode 2 (data-grad s2 parity class): m = ci, k = co, tap = (th', tw'),
+//                          kh = kh0 + 2*(nth-1-th'), kw = kw0 + 2*(ntw-1-tw')
+__global__ void wtrans_kernel(const float* __restrict__ W, float* __restrict__ Wt, int Co, int Ci,
+                              int KH, int KW, int mode, int kh0, int kw0, int nth, int ntw) {
+  const int M = mode == 0 ? Co : Ci, K = mode == 0 ? Ci : Co;
+  const int taps = mode == 2 ? nth * ntw : KH * KW;
+  const long total = (long)taps * M * K;
+  for (long e = blockIdx.x * 256L + threadIdx.x; e < total; e += (long)gridDim.x * 256) {
+    const int k = e % K; const long t = e / K;
+    const int m = t % M; const int tap = t / M;
+    int kh, kw, co, ci;
+    if (mode == 0) { kh = tap / KW; kw = tap % KW; co = m; ci = k; }
+    else if (mode == 1) { kh = KH - 1 - tap / KW; kw = KW - 1 - tap % KW; co = k; ci = m; }
+    else { const int th = tap / ntw, tw = tap % ntw; kh = kh0 + 2 * (nth - 1 - th); kw = kw0 + 2 * (ntw - 1 - tw); co = k; ci = m; }
+    Wt[e] = W[(((long)co * Ci + ci) * KH + kh) * KW + kw];
+  }
+}
+
+}  // namespace dsg
+
+using namespace dsg;
+
+extern "C" {
+
+int dsgan_conv_wtrans(const float* W, float* Wt, int Co, int Ci, int KH, int KW, int mode, int kh0,
+                      int kw0, int nth, int ntw, hipStream_t st) {
+  DSG_REQUIRE(W && Wt && mode >= 0 && mode <= 2, "dsgan_conv_wtrans: bad args");
+  const long taps = mode == 2 ? (long)nth * ntw : (long)KH * KW;
+  const long total = taps * Co * Ci;
+  long blocks = (total + 255) / 256;
+  if (blocks > 8192) blocks = 8192;
+  hipLaunchKernelGGL(wtrans_kernel, dim3((unsigned)blocks), dim3(256), 0, st, W, Wt, Co, Ci, KH, KW,
+                     mode, kh0, kw0, nth, ntw);
+  DSG_CHECK_LAUNCH();
+  return 0;
+}
+
+// Generic launcher.  taps: ntaps pairs (dh, dw).  dst lattice: (oh*os+ph, ow*os+pw) in Hdst x Wdst.
+int dsgan_tconv(const float* X, long x_bs, const float* Wt, const float* bias, float* Y, long y_bs,
+                const float* gpre, long gpre_bs, int nb, int K, int M, int Hin, int Win, int Hout,
+                int Wout, int stride, int ntaps, const int* dh, const int* dw, int Hdst, int Wdst,
+                int os, int ph, int pw, int act, int gact, float slope, hipStream_t st) {
+  DSG_REQUIRE(X && Wt && Y && nb > 0 && M > 0 && Hout > 0 && Wout > 0, "dsgan_tconv: bad args");
+  DSG_REQUIRE(K % TBK == 0 && K > 0, "dsgan_tconv: K (input channels) must be a multiple of 32");
+  DSG_REQUIRE(ntaps >= 1 && ntaps <= T_MAXTAPS, "dsgan_tconv: 1..16 taps");
+  DSG_REQUIRE((long)K * Hin * Win * 4 < 0x7fffffffL && (long)M * Hdst * Wdst * 4 < 0x7fffffffL,
+              "dsgan_tconv: tensor exceeds a 2 GiB buffer resource");
+  DSG_REQUIRE(((uintptr_t)Wt & 15) == 0, "dsgan_tconv: Wt must be 16-byte aligned");
+  TcArgs g{};
+  g.X = X; g.x_bs = x_bs; g.Wt = Wt; g.Y = Y; g.y_bs = y_bs; g.bias = bias; g.gpre = gpre;
+  g.gpre_bs = gpre_bs; g.nb = nb; g.K = K; g.M = M; g.Hin = Hin; g.Win = Win; g.Hout = Hout;
+  g.Wout = Wout; g.stride = stride; g.ntaps = ntaps;
+  for (int t = 0; t < ntaps; ++t) { g.dh[t] = dh[t]; g.dw[t] = dw[t]; }
+  g.Hdst = Hdst; g.Wdst = Wdst; g.os = os; g.ph = ph; g.pw = pw;
+  g.act = act; g.gact = gact; g.slope = slope;
+  const long ntiles = (long)nb * ((Hout * Wout + 127) / 128);
+  if (M > 64) {
+    hipLaunchKernelGGL(tconv_kernel<128>, dim3((unsigned)(ntiles * ((M + 127) / 128))), dim3(256), 0, st, g);
+  } else {
+    hipLaunchKernelGGL(tconv_kernel<64>, dim3((unsigned)(ntiles * ((M + 63) / 64))), dim3(256), 0, st, g);
+  }
+  DSG_CHECK_LAUNCH();
+  return 0;
+}
+
+}  // extern "C"

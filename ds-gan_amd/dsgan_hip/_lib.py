@@ -28,6 +28,9 @@ SIGNATURES = {
     # pwgemm.hip
     "dsgan_pw_supported": [I, I, I, I, L, L, P, P],
     "dsgan_pw_gemm": [I, P, L, P, L, P, L, P, P, L, P, L, I, I, I, I, I, I, I, I, I, F, S],
+    # tconv.hip
+    "dsgan_conv_wtrans": [P, P, I, I, I, I, I, I, I, I, I, S],
+    "dsgan_tconv": [P, L, P, P, P, L, P, L] + [I] * 9 + [P, P] + [I] * 7 + [F, S],
     # dwconv.hip
     "dsgan_dwconv_fwd": [P, L, P, P, P, L, I, I, I, I, I, I, S],
     "dsgan_dwconv_wgrad": [P, L, P, L, P, P, I, I, I, I, I, S],

@@ -116,6 +116,25 @@ def _pw_ok(mode, M, K, P, a_bs, b_bs, a, b):
     return bool(_lib.load().dsgan_pw_supported(mode, M, K, P, a_bs, b_bs, a, b))
 
 
+def _tconv(X, xbs, Wt, bias, Y, ybs, gpre, gbs, nb, K, M, Hin, Win, Hout, Wout, stride, taps,
+           Hdst, Wdst, os_, ph, pw, act, gact):
+    import ctypes
+    dh = (ctypes.c_int * len(taps))(*[t[0] for t in taps])
+    dw = (ctypes.c_int * len(taps))(*[t[1] for t in taps])
+    call("dsgan_tconv", ptr(X), xbs, ptr(Wt), ptr(bias), ptr(Y), ybs, ptr(gpre), gbs, nb, K, M, Hin,
+         Win, Hout, Wout, stride, len(taps), ctypes.cast(dh, ctypes.c_void_p),
+         ctypes.cast(dw, ctypes.c_void_p), Hdst, Wdst, os_, ph, pw, ACT[act], ACT[gact],
+         LRELU_SLOPE, stream())
+
+
+def _wtrans(w, mode, kh0=0, kw0=0, nth=0, ntw=0):
+    Co, Ci, KH, KW = w.shape
+    taps = nth * ntw if mode == 2 else KH * KW
+    wt = torch.empty(taps * Co * Ci, device=w.device, dtype=torch.float32)
+    call("dsgan_conv_wtrans", ptr(w), ptr(wt), Co, Ci, KH, KW, mode, kh0, kw0, nth, ntw, stream())
+    return wt
+
+
 def conv_fwd_raw(x, w, b, stride, pad, act=None, out=None, pre=None, accumulate=False, xact=None):
     x, xbs = nchw(x)
     N, Cin, H, W = x.shape
@@ -133,6 +152,12 @@ def conv_fwd_raw(x, w, b, stride, pad, act=None, out=None, pre=None, accumulate=
     if KH == 1 and KW == 1 and stride == 1 and pad == 0 and _pw_ok(0, Cout, Cin, H * W, 0, xbs, w.data_ptr(), x.data_ptr()):
         call("dsgan_pw_gemm", 0, ptr(w), 0, ptr(x), xbs, ptr(y), ybs, ptr(b), ptr(pre), pbs, None, 0,
              Cout, N * H * W, Cin, H * W, N, ACT[act], 0, ACT[xact], int(accumulate), LRELU_SLOPE, stream())
+    elif (_state["prec"] == "bf16" and w.dim() == 4 and (KH > 1 or KW > 1) and Cin % 32 == 0
+          and pre is None and not accumulate and xact is None and KH * KW <= 16):
+        wt = _wtrans(w, 0)
+        taps = [(kh - pad, kw - pad) for kh in range(KH) for kw in range(KW)]
+        _tconv(x, xbs, wt, b, y, ybs, None, 0, N, Cin, Cout, H, W, Ho, Wo, stride, taps, Ho, Wo, 1, 0, 0,
+               act, None)
     else:
         call("dsgan_conv_fwd", ptr(x), xbs, ptr(w), ptr(b), ptr(y), ybs, ptr(pre), pbs, N, Cin, H, W,
              Cout, KH, KW, stride, pad, Ho, Wo, ACT[act], LRELU_SLOPE, int(accumulate), ACT[xact], _prec(),
@@ -158,6 +183,28 @@ def conv_dgrad_raw(dy, w, x_shape, stride, pad, bias=None, act=None, gpre=None, 
             and not accumulate and _pw_ok(1, Cin, Cout, H * W, 0, dybs, w.data_ptr(), dy.data_ptr())):
         call("dsgan_pw_gemm", 1, ptr(w), 0, ptr(dy), dybs, ptr(dx), dxbs, None, None, 0, ptr(gpre), gbs,
              Cin, N * H * W, Cout, H * W, N, 0, ACT[gact], 0, 0, LRELU_SLOPE, stream())
+    elif (_state["prec"] == "bf16" and w.dim() == 4 and (KH > 1 or KW > 1) and Cout % 32 == 0
+          and act is None and not accumulate and stride in (1, 2) and KH * KW <= 16):
+        if stride == 1:
+            wt = _wtrans(w, 1)
+            pp = KH - 1 - pad
+            qq = KW - 1 - pad
+            taps = [(kh - pp, kw - qq) for kh in range(KH) for kw in range(KW)]
+            _tconv(dy, dybs, wt, bias, dx, dxbs, gpre, gbs, N, Cout, Cin, Ho, Wo, H, W, 1, taps, H, W, 1,
+                   0, 0, None, gact)
+        else:
+            for ph in range(2):
+                for pw_ in range(2):
+                    kh0, kw0 = (ph + pad) & 1, (pw_ + pad) & 1
+                    nth, ntw = (KH - kh0 + 1) // 2, (KW - kw0 + 1) // 2
+                    Hc, Wc = (H - ph + 1) // 2, (W - pw_ + 1) // 2
+                    if Hc <= 0 or Wc <= 0:
+                        continue
+                    ch, cw = (ph + pad - kh0) // 2, (pw_ + pad - kw0) // 2
+                    wt = _wtrans(w, 2, kh0, kw0, nth, ntw)
+                    taps = [(ch - (nth - 1) + a, cw - (ntw - 1) + c) for a in range(nth) for c in range(ntw)]
+                    _tconv(dy, dybs, wt, bias, dx, dxbs, gpre, gbs, N, Cout, Cin, Ho, Wo, Hc, Wc, 1, taps,
+                           H, W, 2, ph, pw_, None, gact)
     else:
         call("dsgan_conv_dgrad", ptr(dy), dybs, ptr(w), ptr(bias), ptr(dx), dxbs, None, 0, ptr(gpre), gbs,
              ACT[gact], N, Cin, H, W, Cout, KH, KW, stride, pad, Ho, Wo, ACT[act], LRELU_SLOPE,

@@ -71,6 +71,18 @@ int dsgan_pw_gemm(int mode, const float* A, long a_bs, const float* B, long b_bs
                   long gpre_bs, int M, int N, int K, int P, int nb, int act, int gact, int bact,
                   int accumulate, float slope, hipStream_t stream);
 
+/* ---- tap-major implicit-GEMM conv for channel counts % 32 == 0 (tconv.hip, bf16 MFMA) -------
+ * out[b][m][dst(o)] = act(sum_{tap,k} Wt[tap][m][k] * X[b][k][o*stride + (dh,dw)[tap]] + bias[m])
+ *                     (* gact'(gpre) if gpre); dst(o) = (oh*os+ph, ow*os+pw) in Hdst x Wdst.
+ * dsgan_conv_wtrans builds Wt from an OIHW weight: mode 0 forward, 1 stride-1 data-grad (flipped,
+ * transposed), 2 one stride-2 data-grad parity class (kh0, kw0, nth, ntw). */
+int dsgan_conv_wtrans(const float* W, float* Wt, int Co, int Ci, int KH, int KW, int mode, int kh0,
+                      int kw0, int nth, int ntw, hipStream_t stream);
+int dsgan_tconv(const float* X, long x_bs, const float* Wt, const float* bias, float* Y, long y_bs,
+                const float* gpre, long gpre_bs, int nb, int K, int M, int Hin, int Win, int Hout,
+                int Wout, int stride, int ntaps, const int* dh, const int* dw, int Hdst, int Wdst,
+                int os, int ph, int pw, int act, int gact, float slope, hipStream_t stream);
+
 /* ---- depthwise conv (dwconv.hip): Block.dwconv :220, MidMLKA.X3..X9 :94-97 ---------------- */
 int dsgan_dwconv_fwd(const float* x, long x_bs, const float* w, const float* bias, float* y,
                      long y_bs, int N, int C, int H, int W, int K, int flip, hipStream_t stream);

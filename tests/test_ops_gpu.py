@@ -374,3 +374,33 @@ def test_pw_gemm_fast_path(N, Cin, H, Cout):
     ref = torch.einsum("bmhw,bkhw->mk", _q(dy, "bf16"), xq).view_as(w)
     assert rel(dw, ref) < 1e-2
     HF.set_precision("fp32")
+
+
+@pytest.mark.parametrize("N,Cin,H,W,Cout,K,s,p", [
+    (2, 64, 18, 18, 128, 3, 1, 1),     # VGG-like
+    (2, 32, 20, 13, 200, 3, 1, 1),     # ragged pixels, partial M tile
+    (2, 32, 32, 32, 64, 4, 2, 1),      # PatchGAN s2
+    (2, 128, 9, 9, 256, 4, 1, 1),      # PatchGAN s1 (31x31-like odd outputs)
+    (2, 64, 16, 16, 3, 3, 1, 1),       # G head (M = 3)
+])
+def test_tap_conv_bf16(N, Cin, H, W, Cout, K, s, p):
+    """Tap-major bf16 conv (tconv.hip): fwd, stride-1 dgrad (flipped kernel) and stride-2 dgrad
+    (parity classes) vs fp32 torch on bf16-rounded operands."""
+    from dsgan_hip import functional as HF
+    HF.set_precision("bf16")
+    g = torch.Generator().manual_seed(Cin + Cout + K + H)
+    x = _q(torch.randn(N, Cin, H, W, generator=g), "bf16")
+    w = _q(torch.randn(Cout, Cin, K, K, generator=g) / math.sqrt(Cin * K * K), "bf16")
+    b = torch.randn(Cout, generator=g) * 0.1
+    y = HF.conv_fwd_raw(x.to(DEV), w.to(DEV), b.to(DEV), s, p, act="relu")
+    assert rel(y, F.relu(F.conv2d(x, w, b, stride=s, padding=p))) < 1e-2
+    Ho, Wo = y.shape[2], y.shape[3]
+    dy = _q(torch.randn(N, Cout, Ho, Wo, generator=g), "bf16")
+    gp = torch.randn(N, Cin, H, W, generator=g)
+    if Cout % 32 == 0:
+        dx = HF.conv_dgrad_raw(dy.to(DEV), w.to(DEV), (N, Cin, H, W), s, p, gpre=gp.to(DEV), gact="lrelu")
+        xr = torch.zeros(N, Cin, H, W, requires_grad=True)
+        ref = torch.autograd.grad(F.conv2d(xr, w, None, stride=s, padding=p), xr, dy)[0]
+        ref = ref * torch.where(gp > 0, 1.0, 0.2)
+        assert rel(dx, ref) < 1e-2
+    HF.set_precision("fp32")
