@@ -7,6 +7,7 @@
 // plane is small); the activation that follows it (GELU / LeakyReLU(0.2)) and, for MidMLKA
 // (:113-116), the CA scaling before it and the residual add after it, are fused in.
 #include "common.h"
+#include <stdlib.h>
 
 namespace dsg {
 
@@ -168,6 +169,85 @@ __global__ __launch_bounds__(NT == 64 ? 256 : NT) void instnorm_bwd_kernel(INBwd
 // (the rule of PyTorch's CPU max_pool2d) -- bit-exact with the reference's int64 indices.
 // ---------------------------------------------------------------------------------------
 // 2-D grid: blockIdx.y walks planes (n,c), blockIdx.x chunks of the plane; 32-bit index math.
+// Fast path (H, W divisible by K, aligned rows): one thread per output window, the window rows
+// moved with 8/16-byte vector accesses (consecutive lanes = consecutive windows).
+template <int K>
+__device__ __forceinline__ void load_row(const float* p, float* v) {
+  if constexpr (K == 2) { const float2 t = *reinterpret_cast<const float2*>(p); v[0] = t.x; v[1] = t.y; }
+  else {
+#pragma unroll
+    for (int j = 0; j < K; j += 4) {
+      const float4 t = *reinterpret_cast<const float4*>(p + j);
+      v[j] = t.x; v[j + 1] = t.y; v[j + 2] = t.z; v[j + 3] = t.w;
+    }
+  }
+}
+template <int K>
+__device__ __forceinline__ void store_row(float* p, const float* v) {
+  if constexpr (K == 2) { *reinterpret_cast<float2*>(p) = make_float2(v[0], v[1]); }
+  else {
+#pragma unroll
+    for (int j = 0; j < K; j += 4) *reinterpret_cast<float4*>(p + j) = make_float4(v[j], v[j + 1], v[j + 2], v[j + 3]);
+  }
+}
+
+template <int K>
+__global__ void maxpool_fwd_win_kernel(const float* __restrict__ x, long x_bs, float* __restrict__ y,
+                                       long y_bs, int* __restrict__ idx, int N, int C, int H, int W) {
+  const int Ho = H / K, Wo = W / K, Po = Ho * Wo;
+  for (int plane = blockIdx.y; plane < N * C; plane += gridDim.y) {
+    const int n = plane / C, c = plane - n * C;
+    const float* xp = x + (long)n * x_bs + (long)c * H * W;
+    float* yp = y + (long)n * y_bs + (long)c * Po;
+    int* ip = idx + (long)plane * Po;
+    for (int o = blockIdx.x * blockDim.x + threadIdx.x; o < Po; o += gridDim.x * blockDim.x) {
+      const int oh = o / Wo, ow = o - oh * Wo;
+      float best = -INFINITY; int bi = (oh * K) * W + ow * K;
+#pragma unroll
+      for (int i = 0; i < K; ++i) {
+        float v[K];
+        load_row<K>(xp + (oh * K + i) * W + ow * K, v);
+#pragma unroll
+        for (int j = 0; j < K; ++j)
+          if (v[j] > best || isnan(v[j])) { best = v[j]; bi = (oh * K + i) * W + ow * K + j; }
+      }
+      yp[o] = best;
+      ip[o] = bi;
+    }
+  }
+}
+
+template <int K>
+__global__ void maxpool_bwd_win_kernel(const float* __restrict__ dy, long dy_bs, const int* __restrict__ idx,
+                                       float* __restrict__ dx, long dx_bs, int N, int C, int H, int W,
+                                       int accumulate) {
+  const int Ho = H / K, Wo = W / K, Po = Ho * Wo;
+  for (int plane = blockIdx.y; plane < N * C; plane += gridDim.y) {
+    const int n = plane / C, c = plane - n * C;
+    const float* gp = dy + (long)n * dy_bs + (long)c * Po;
+    const int* ip = idx + (long)plane * Po;
+    float* dp = dx + (long)n * dx_bs + (long)c * H * W;
+    for (int o = blockIdx.x * blockDim.x + threadIdx.x; o < Po; o += gridDim.x * blockDim.x) {
+      const int oh = o / Wo, ow = o - oh * Wo;
+      const int id = ip[o];
+      const float gv = gp[o];
+#pragma unroll
+      for (int i = 0; i < K; ++i) {
+        const int rb = (oh * K + i) * W + ow * K;
+        float v[K];
+        if (accumulate) load_row<K>(dp + rb, v);
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+          const float add = (rb + j == id) ? gv : 0.f;
+          v[j] = accumulate ? v[j] + add : add;
+        }
+        store_row<K>(dp + rb, v);
+      }
+    }
+  }
+}
+
+// Generic fallback (any H, W): element-parallel, zero fill beyond the floor windows.
 __global__ void maxpool_fwd_kernel(const float* __restrict__ x, long x_bs, float* __restrict__ y,
                                    long y_bs, int* __restrict__ idx, int N, int C, int H, int W,
                                    int k) {
@@ -192,7 +272,6 @@ __global__ void maxpool_fwd_kernel(const float* __restrict__ x, long x_bs, float
   }
 }
 
-// dx over the full input plane: dy at the argmax, 0 elsewhere (also rows/cols beyond floor).
 __global__ void maxpool_bwd_kernel(const float* __restrict__ dy, long dy_bs, const int* __restrict__ idx,
                                    float* __restrict__ dx, long dx_bs, int N, int C, int H, int W,
                                    int k, int accumulate) {
@@ -441,6 +520,12 @@ using namespace dsg;
 
 extern "C" {
 
+static int in_big_mode() {
+  static int m = -1;
+  if (m < 0) { const char* e = getenv("DSGAN_IN_BIG"); m = e ? atoi(e) : 0; }
+  return m;
+}
+
 int dsgan_instnorm_fwd(const float* x, long x_bs, const float* scale, const float* res, long res_bs,
                        float* y, long y_bs, float* mean, float* rstd, int N, int C, int HW, int act,
                        float slope, float eps, hipStream_t st) {
@@ -453,8 +538,10 @@ int dsgan_instnorm_fwd(const float* x, long x_bs, const float* scale, const floa
     hipLaunchKernelGGL((instnorm_fwd_kernel<256, 16>), dim3(planes), dim3(256), 0, st, a);
   else if (HW <= 1024 * 16)
     hipLaunchKernelGGL((instnorm_fwd_kernel<1024, 16>), dim3(planes), dim3(1024), 0, st, a);
-  else if (HW <= 1024 * 64)
+  else if (HW <= 1024 * 64 && in_big_mode() == 2)
     hipLaunchKernelGGL((instnorm_fwd_kernel<1024, 64>), dim3(planes), dim3(1024), 0, st, a);
+  else if (HW <= 512 * 128 && in_big_mode() == 1)
+    hipLaunchKernelGGL((instnorm_fwd_kernel<512, 128>), dim3(planes), dim3(512), 0, st, a);
   else
     hipLaunchKernelGGL((instnorm_fwd_kernel<1024, 0>), dim3(planes), dim3(1024), 0, st, a);
   DSG_CHECK_LAUNCH();
@@ -475,8 +562,10 @@ int dsgan_instnorm_bwd(const float* dy, long dy_bs, const float* x, long x_bs, c
     hipLaunchKernelGGL((instnorm_bwd_kernel<256, 16>), dim3(planes), dim3(256), 0, st, a);
   else if (HW <= 1024 * 16)
     hipLaunchKernelGGL((instnorm_bwd_kernel<1024, 16>), dim3(planes), dim3(1024), 0, st, a);
-  else if (HW <= 1024 * 64)
+  else if (HW <= 1024 * 64 && in_big_mode() == 2)
     hipLaunchKernelGGL((instnorm_bwd_kernel<1024, 64>), dim3(planes), dim3(1024), 0, st, a);
+  else if (HW <= 512 * 128 && in_big_mode() == 1)
+    hipLaunchKernelGGL((instnorm_bwd_kernel<512, 128>), dim3(planes), dim3(512), 0, st, a);
   else
     hipLaunchKernelGGL((instnorm_bwd_kernel<1024, 0>), dim3(planes), dim3(1024), 0, st, a);
   DSG_CHECK_LAUNCH();
@@ -486,8 +575,14 @@ int dsgan_instnorm_bwd(const float* dy, long dy_bs, const float* x, long x_bs, c
 int dsgan_maxpool_fwd(const float* x, long x_bs, float* y, long y_bs, int* idx, int N, int C, int H,
                       int W, int k, hipStream_t st) {
   DSG_REQUIRE(x && y && idx && k > 0 && H >= k && W >= k, "dsgan_maxpool_fwd: bad args");
-  hipLaunchKernelGGL(maxpool_fwd_kernel, plane_grid((long)(H / k) * (W / k), (long)N * C), dim3(256), 0, st,
-                     x, x_bs, y, y_bs, idx, N, C, H, W, k);
+  const dim3 grid = plane_grid((long)(H / k) * (W / k), (long)N * C);
+  const bool fast = (H % k == 0) && (W % k == 0) && (k == 2 ? ((W & 1) == 0 && (x_bs & 1) == 0 && ((uintptr_t)x & 7) == 0)
+                                                            : ((W & 3) == 0 && (x_bs & 3) == 0 && ((uintptr_t)x & 15) == 0));
+  if (fast && k == 2) hipLaunchKernelGGL(maxpool_fwd_win_kernel<2>, grid, dim3(256), 0, st, x, x_bs, y, y_bs, idx, N, C, H, W);
+  else if (fast && k == 4) hipLaunchKernelGGL(maxpool_fwd_win_kernel<4>, grid, dim3(256), 0, st, x, x_bs, y, y_bs, idx, N, C, H, W);
+  else if (fast && k == 8) hipLaunchKernelGGL(maxpool_fwd_win_kernel<8>, grid, dim3(256), 0, st, x, x_bs, y, y_bs, idx, N, C, H, W);
+  else if (fast && k == 16) hipLaunchKernelGGL(maxpool_fwd_win_kernel<16>, grid, dim3(256), 0, st, x, x_bs, y, y_bs, idx, N, C, H, W);
+  else hipLaunchKernelGGL(maxpool_fwd_kernel, grid, dim3(256), 0, st, x, x_bs, y, y_bs, idx, N, C, H, W, k);
   DSG_CHECK_LAUNCH();
   return 0;
 }
@@ -495,8 +590,15 @@ int dsgan_maxpool_fwd(const float* x, long x_bs, float* y, long y_bs, int* idx, 
 int dsgan_maxpool_bwd(const float* dy, long dy_bs, const int* idx, float* dx, long dx_bs, int N,
                       int C, int H, int W, int k, int accumulate, hipStream_t st) {
   DSG_REQUIRE(dy && idx && dx && k > 0, "dsgan_maxpool_bwd: bad args");
-  hipLaunchKernelGGL(maxpool_bwd_kernel, plane_grid((long)H * W, (long)N * C), dim3(256), 0, st, dy, dy_bs,
-                     idx, dx, dx_bs, N, C, H, W, k, accumulate);
+  const bool fast = (H % k == 0) && (W % k == 0) && (k == 2 ? ((W & 1) == 0 && (dx_bs & 1) == 0 && ((uintptr_t)dx & 7) == 0)
+                                                            : ((W & 3) == 0 && (dx_bs & 3) == 0 && ((uintptr_t)dx & 15) == 0));
+  const dim3 wgrid = plane_grid((long)(H / k) * (W / k), (long)N * C);
+  if (fast && k == 2) hipLaunchKernelGGL(maxpool_bwd_win_kernel<2>, wgrid, dim3(256), 0, st, dy, dy_bs, idx, dx, dx_bs, N, C, H, W, accumulate);
+  else if (fast && k == 4) hipLaunchKernelGGL(maxpool_bwd_win_kernel<4>, wgrid, dim3(256), 0, st, dy, dy_bs, idx, dx, dx_bs, N, C, H, W, accumulate);
+  else if (fast && k == 8) hipLaunchKernelGGL(maxpool_bwd_win_kernel<8>, wgrid, dim3(256), 0, st, dy, dy_bs, idx, dx, dx_bs, N, C, H, W, accumulate);
+  else if (fast && k == 16) hipLaunchKernelGGL(maxpool_bwd_win_kernel<16>, wgrid, dim3(256), 0, st, dy, dy_bs, idx, dx, dx_bs, N, C, H, W, accumulate);
+  else hipLaunchKernelGGL(maxpool_bwd_kernel, plane_grid((long)H * W, (long)N * C), dim3(256), 0, st, dy, dy_bs,
+                          idx, dx, dx_bs, N, C, H, W, k, accumulate);
   DSG_CHECK_LAUNCH();
   return 0;
 }

@@ -11,7 +11,7 @@ State-dict keys and shapes are untouched, so reference checkpoints load unchange
 import torch
 
 from ._lib import call, ptr, stream
-from .functional import fill_
+from .functional import fill_, bump_weight_generation
 
 
 class FlatParams:
@@ -63,4 +63,5 @@ class FlatAdam(torch.optim.Optimizer):
         call("dsgan_adam", ptr(self.flat.data), ptr(self.flat.grad), ptr(self.m), ptr(self.v),
              self.flat.numel, float(g["lr"]), float(b1), float(b2), float(g["eps"]),
              self.step_count, stream())
+        bump_weight_generation()
         return None

@@ -127,7 +127,31 @@ def _tconv(X, xbs, Wt, bias, Y, ybs, gpre, gbs, nb, K, M, Hin, Win, Hout, Wout, 
          LRELU_SLOPE, stream())
 
 
+# Transformed-weight cache: an entry is valid while the parameter's storage pointer and the
+# global weight generation are unchanged.  FlatAdam.step() bumps the generation (weights are
+# updated in place by the fused Adam kernel, invisible to torch's version counters).
+WEIGHT_GEN = [0]
+_WT_CACHE = {}
+
+
+def bump_weight_generation():
+    WEIGHT_GEN[0] += 1
+    if len(_WT_CACHE) > 512:
+        _WT_CACHE.clear()
+
+
 def _wtrans(w, mode, kh0=0, kw0=0, nth=0, ntw=0):
+    key = (id(w), w.data_ptr(), tuple(w.shape), mode, kh0, kw0, nth, ntw)
+    ent = _WT_CACHE.get(key)
+    gen = WEIGHT_GEN[0]
+    if ent is not None and ent[0] == gen and ent[1] == w._version and ent[2] is w:
+        return ent[3]
+    wt = _wtrans_build(w, mode, kh0, kw0, nth, ntw)
+    _WT_CACHE[key] = (gen, w._version, w, wt)
+    return wt
+
+
+def _wtrans_build(w, mode, kh0=0, kw0=0, nth=0, ntw=0):
     Co, Ci, KH, KW = w.shape
     taps = nth * ntw if mode == 2 else KH * KW
     wt = torch.empty(taps * Co * Ci, device=w.device, dtype=torch.float32)
