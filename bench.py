@@ -33,7 +33,8 @@ PEAK_F32_TFLOPS = 157.3
 
 
 def cpu_baseline(threads):
-    """Bounded sample of the same step on the CPU oracle: 1 warmup + 2 timed steps at 256^2, B=2."""
+    """Bounded sample of the same step on the CPU oracle: 1 warmup + 6 timed steps at 256^2, B=2
+    (~10-20 s of CPU work)."""
     from oracle import dsgan_cpu as O
     from oracle.recipe import make_params, synth_pair
     torch.set_num_threads(threads)
@@ -44,12 +45,12 @@ def cpu_baseline(threads):
     A, B = synth_pair(2, 256, seed=0)
     st.step(A, B)
     t0 = time.time()
-    steps = 2
+    steps = 6
     for _ in range(steps):
         st.step(A, B)
     dt = time.time() - t0
     return dict(value=round(2 * steps / dt, 4), unit="img/s", cores=threads, kind="port",
-                sample="oracle/dsgan_cpu.py OracleStep, fp32, 256x256, batch 2, 2 timed steps after 1 warmup (%.1f s)" % dt)
+                sample="oracle/dsgan_cpu.py OracleStep, fp32, 256x256, batch 2, %d timed steps after 1 warmup (%.1f s)" % (steps, dt))
 
 
 def main():
@@ -129,7 +130,7 @@ def main():
                        "global_batch": args.batch * world, "per_gpu_batch": args.batch,
                        "image": [args.size, args.size], "parallelism": "dp%d" % world,
                        "baseline_config": "configs[1]: 256x256, batch 16, bf16, 1xMI355X"},
-            "roofline": {"bound": "mfma", "kernel": "igemm_kernel (implicit-GEMM conv fwd/dgrad/wgrad)",
+            "roofline": {"bound": "mfma", "kernel": "conv contraction kernels (pwgemm_kernel + tconv_kernel + igemm_kernel: every 1x1/3x3/4x4/ConvT fwd, dgrad, wgrad launch)",
                          "achieved": round(ach, 2), "peak": peak, "unit": "TFLOP/s",
                          "frac": round(ach / peak, 4), "traffic": None,
                          "launches_per_step": ig["launches"] // max(1, args.steps),
