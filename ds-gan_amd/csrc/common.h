@@ -11,9 +11,31 @@ constexpr float kInvSqrt2 = 0.70710678118654752440f;
 constexpr float kInvSqrt2Pi = 0.39894228040143267794f;
 
 // nn.GELU() (exact erf form) -- the activation of MixConvNeXtML (DSGAN/models/model/MixConvNeXtML.py:51,82,223)
-__device__ __forceinline__ float gelu_f(float x) { return 0.5f * x * (1.f + erff(x * kInvSqrt2)); }
+// Branch-free erf: the two polynomial pieces of the device library's erff (|x| < 1 and
+// |x| >= 1), both evaluated and selected.  erff itself branches on |x| < 1, which diverges
+// inside a wavefront on real activations and costs exec-mask juggling per element.
+__device__ __forceinline__ float erf_nb(float x) {
+  const float a = fabsf(x);
+  const float p = a * a;
+  float r = fmaf(p, -0x1.268bc2p-11f, 0x1.420828p-8f);
+  r = fmaf(p, r, -0x1.b5937p-6f);
+  r = fmaf(p, r, 0x1.ce077cp-4f);
+  r = fmaf(p, r, -0x1.81266p-2f);
+  r = fmaf(p, r, 0x1.06eba0p-3f);
+  const float small = fmaf(a, r, a);
+  float q = fmaf(a, 0x1.1d3156p-16f, -0x1.8d129p-12f);
+  q = fmaf(a, q, 0x1.f9a6d2p-9f);
+  q = fmaf(a, q, -0x1.8c3164p-6f);
+  q = fmaf(a, q, 0x1.b4e9c8p-4f);
+  q = fmaf(a, q, 0x1.4515fap-1f);
+  q = fmaf(a, q, 0x1.078e50p-3f);
+  q = fmaf(a, q, a);
+  const float large = 1.f - expf(-q);
+  return copysignf(a < 1.f ? small : large, x);
+}
+__device__ __forceinline__ float gelu_f(float x) { return 0.5f * x * (1.f + erf_nb(x * kInvSqrt2)); }
 __device__ __forceinline__ float gelu_g(float x) {
-  float cdf = 0.5f * (1.f + erff(x * kInvSqrt2));
+  float cdf = 0.5f * (1.f + erf_nb(x * kInvSqrt2));
   return cdf + x * (kInvSqrt2Pi * __expf(-0.5f * x * x));
 }
 
@@ -34,6 +56,52 @@ __device__ __forceinline__ float act_g(int act, float x, float slope) {
     case ACT_LRELU: return x > 0.f ? 1.f : slope;
     case ACT_SIGMOID: { float s = 1.f / (1.f + __expf(-x)); return s * (1.f - s); }
     default: return 1.f;
+  }
+}
+
+// Array forms for GEMM epilogues: the (uniform) activation switch sits OUTSIDE the element
+// loop, so each case is a straight-line unrolled block (no per-element branches / waits).
+template <int N>
+__device__ __forceinline__ void act_f_arr(int act, float (&v)[N], float slope) {
+  switch (act) {
+    case ACT_NONE: break;
+    case ACT_GELU:
+#pragma unroll
+      for (int i = 0; i < N; ++i) v[i] = gelu_f(v[i]);
+      break;
+    case ACT_RELU:
+#pragma unroll
+      for (int i = 0; i < N; ++i) v[i] = fmaxf(v[i], 0.f);
+      break;
+    case ACT_LRELU:
+#pragma unroll
+      for (int i = 0; i < N; ++i) v[i] = v[i] > 0.f ? v[i] : v[i] * slope;
+      break;
+    default:
+#pragma unroll
+      for (int i = 0; i < N; ++i) v[i] = act_f(act, v[i], slope);
+  }
+}
+// v[i] *= act'(x[i])
+template <int N>
+__device__ __forceinline__ void act_g_mul_arr(int act, float (&v)[N], const float (&x)[N], float slope) {
+  switch (act) {
+    case ACT_NONE: break;
+    case ACT_GELU:
+#pragma unroll
+      for (int i = 0; i < N; ++i) v[i] *= gelu_g(x[i]);
+      break;
+    case ACT_RELU:
+#pragma unroll
+      for (int i = 0; i < N; ++i) v[i] = x[i] > 0.f ? v[i] : 0.f;
+      break;
+    case ACT_LRELU:
+#pragma unroll
+      for (int i = 0; i < N; ++i) v[i] = x[i] > 0.f ? v[i] : v[i] * slope;
+      break;
+    default:
+#pragma unroll
+      for (int i = 0; i < N; ++i) v[i] *= act_g(act, x[i], slope);
   }
 }
 

@@ -283,7 +283,9 @@ __global__ __launch_bounds__(256) void igemm_kernel(GemmArgs g) {
   T* As = smem;                      // [2][BM][PADK]
   T* Bs = smem + 2 * BM * PADK;      // [2][BN][PADK]
 
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // wave index through readfirstlane: the compiler then knows it is uniform (SGPR), so
+  // per-wave row offsets can be scalar soffsets instead of readfirstlane waterfall loops
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave / WN, wn = wave % WN;
   // 1-D grid, XCD-aware: blocks b, b+8, b+16, ... share an XCD (round-robin dispatch), so the
   // bijective remap below gives each XCD a contiguous run of tile ids; tiles are numbered with
@@ -494,40 +496,25 @@ __global__ __launch_bounds__(256) void igemm_kernel(GemmArgs g) {
         ok[r] = nv && m < g.M;
         off[r] = ok[r] ? (long)m * Pout : 0;
         v[r] = acc[i][j][r];
-        if (has_bias) v[r] += g.bias[ok[r] ? m : 0];
+      }
+      if (has_bias) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int m = m0 + wm * TM * 32 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+          v[r] += g.bias[m < g.M ? m : 0];
+        }
       }
       if (has_g) {
         float gv[16];
 #pragma unroll
         for (int r = 0; r < 16; ++r) gv[r] = gpb[off[r]];
-        switch (gact) {
-          case ACT_GELU:
-#pragma unroll
-            for (int r = 0; r < 16; ++r) v[r] *= gelu_g(gv[r]);
-            break;
-          default:
-#pragma unroll
-            for (int r = 0; r < 16; ++r) v[r] *= act_g(gact, gv[r], g.slope);
-        }
+        act_g_mul_arr(gact, v, gv, g.slope);
       }
       if (has_pre) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) if (ok[r]) ypb[off[r]] = v[r];
       }
-      switch (act) {
-        case ACT_NONE: break;
-        case ACT_GELU:
-#pragma unroll
-          for (int r = 0; r < 16; ++r) v[r] = gelu_f(v[r]);
-          break;
-        case ACT_RELU:
-#pragma unroll
-          for (int r = 0; r < 16; ++r) v[r] = fmaxf(v[r], 0.f);
-          break;
-        default:
-#pragma unroll
-          for (int r = 0; r < 16; ++r) v[r] = act_f(act, v[r], g.slope);
-      }
+      act_f_arr(act, v, g.slope);
       if (g.accumulate) {
         float o[16];
 #pragma unroll

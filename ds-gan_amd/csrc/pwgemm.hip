@@ -17,6 +17,7 @@
 //   DGRAD: DX[b][m][p] = ( sum_k W[k][m] * DY[b][k][p] ) * gact'(G[b][m][p])
 //   WGRAD: DW[m][n]   += sum_{b,p} DY[b][m][p] * xact(X[b][n][p])     (split over pixels, atomics)
 #include "common.h"
+#include <stdlib.h>
 
 namespace dsg {
 
@@ -38,6 +39,8 @@ struct PwArgs {
   int M, N, K, P;
   int act, gact, bact, accumulate; float slope;
   int k_split;
+  unsigned a_range, b_range;   // buffer-resource byte ranges of A and B (B: per image for FWD/DGRAD)
+  int dbg;   // DSGAN_PW_DBG experiment switches: 1 skip epilogue stores, 2 skip global loads
 };
 
 constexpr int PBK = 32;                 // K per main-loop step
@@ -56,10 +59,7 @@ __device__ __forceinline__ pbf16x8 tr_frag(const __bf16* p0, int stride) {
 #endif
 }
 
-__device__ __forceinline__ float4 ld4(const float* p, bool ok, const float* safe) {
-  const float4 t = *reinterpret_cast<const float4*>(ok ? p : safe);
-  return ok ? t : make_float4(0.f, 0.f, 0.f, 0.f);
-}
+constexpr unsigned PW_OOB = 0xFFFFFFF0u;   // voffset past every resource range (ranges < PW_OOB)
 
 __device__ __forceinline__ pbf16x4 cvt4(float4 v, int bact, float slope) {
   if (bact) { v.x = act_f(bact, v.x, slope); v.y = act_f(bact, v.y, slope); v.z = act_f(bact, v.z, slope); v.w = act_f(bact, v.w, slope); }
@@ -69,7 +69,7 @@ __device__ __forceinline__ pbf16x4 cvt4(float4 v, int bact, float slope) {
 }
 
 template <int MODE, int BM>
-__global__ __launch_bounds__(256) void pwgemm_kernel(PwArgs g) {
+__global__ __launch_bounds__(256, 2) void pwgemm_kernel(PwArgs g) {
   constexpr int BN = 128;
   constexpr int WM = 2, WN = 2;
   constexpr int TM = BM / WM / 32, TN = BN / WN / 32;
@@ -83,7 +83,9 @@ __global__ __launch_bounds__(256) void pwgemm_kernel(PwArgs g) {
   constexpr int B_SZ = B_KMAJ ? PBK * B_STR : BN * B_STR;
   __shared__ __attribute__((aligned(16))) __bf16 smem[2 * (A_SZ + B_SZ)];
 
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // wave index through readfirstlane: the compiler then knows it is uniform (SGPR), so
+  // per-wave row offsets can be scalar soffsets instead of readfirstlane waterfall loops
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave / WN, wn = wave % WN;
   const int lr = lane & 31, lh = lane >> 5;
 
@@ -108,7 +110,6 @@ __global__ __launch_bounds__(256) void pwgemm_kernel(PwArgs g) {
   // FWD/DGRAD: the N tile lies inside one image (P % BN == 0)
   const int bimg = (MODE == PW_WGRAD) ? 0 : n0 / g.P;
   const int p0 = (MODE == PW_WGRAD) ? 0 : n0 - bimg * g.P;
-  const float* Bimg = (MODE == PW_WGRAD) ? g.B : g.B + (long)bimg * g.b_bs + p0;
 
   // ---- staging maps ----
   // row-major tiles: item = (row, c4) with c4 in [0,8): 8 float4 per 32-k row
@@ -117,39 +118,59 @@ __global__ __launch_bounds__(256) void pwgemm_kernel(PwArgs g) {
   constexpr int B_ITEMS = (B_KMAJ ? PBK * BN / 4 : BN * 8) / 256;
   float4 ra[A_ITEMS], rb[B_ITEMS];
 
+  // Operand loads are 16-byte buffer loads: an element outside its tensor gets the offset
+  // PW_OOB, past every resource range, and reads 0 in hardware -- no branch, no mask VALU.
+  // (A select of the address followed by a select of the value is turned back into a branch
+  // around the load by the compiler; see igemm.hip ldsel.)
+  const int b_fix = (MODE == PW_WGRAD) ? 0 : bimg;
+  const __amdgpu_buffer_rsrc_t rA = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)g.A, (short)0, g.a_range, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rB = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(g.B + (long)b_fix * g.b_bs), (short)0, g.b_range, 0x00020000);
+  auto bld4 = [](__amdgpu_buffer_rsrc_t r, unsigned voff) {
+    return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)voff, 0, 0));
+  };
+
   auto gload = [&](int kt) {
     const int kb = kbeg + kt * PBK;
+    if (g.dbg & 2) {
+#pragma unroll
+      for (int i = 0; i < A_ITEMS; ++i) ra[i] = make_float4(kt, 1.f, 2.f, 3.f);
+#pragma unroll
+      for (int i = 0; i < B_ITEMS; ++i) rb[i] = make_float4(1.f, kt, 2.f, 3.f);
+      return;
+    }
+    // WGRAD: a 32-pixel K step lies inside one image (P % 32 == 0): image index is uniform
+    const unsigned bw = (MODE == PW_WGRAD) ? (unsigned)(kb / g.P) : 0u;
+    const unsigned pw = (MODE == PW_WGRAD) ? (unsigned)(kb - (int)bw * g.P) : 0u;
 #pragma unroll
     for (int i = 0; i < A_ITEMS; ++i) {
       const int it = tid + i * 256;
+      unsigned off;
       if (MODE == PW_FWD) {                      // W[M][K], row m, k = kb + c4*4
-        const int row = it >> 3, k = kb + (it & 7) * 4;
-        const int m = m0 + row;
-        ra[i] = ld4(g.A + (long)m * g.K + k, m < g.M && k < kend, g.A);
-      } else if (MODE == PW_DGRAD) {             // W[K][M], row k, m = m0 + c4*4
-        const int kr = it / (BM / 4), c4 = it % (BM / 4);
-        const int k = kb + kr, m = m0 + c4 * 4;
-        ra[i] = ld4(g.A + (long)k * g.M + m, k < kend && m < g.M, g.A);
-      } else {                                   // DY[b][M][P], row m, pixels of one image
-        const int row = it >> 3, k = kb + (it & 7) * 4;
-        const int m = m0 + row;
-        const int b = k / g.P, p = k - b * g.P;
-        ra[i] = ld4(g.A + (long)b * g.a_bs + (long)m * g.P + p, m < g.M && k < kend, g.A);
+        const int m = m0 + (it >> 3), k = kb + (it & 7) * 4;
+        off = ((m < g.M) & (k < kend)) ? ((unsigned)m * g.K + k) * 4u : PW_OOB;
+      } else if (MODE == PW_DGRAD) {             // W[K][M], row k (k >= K is past the range)
+        const int k = kb + it / (BM / 4), m = m0 + (it % (BM / 4)) * 4;
+        off = (m < g.M) ? ((unsigned)k * g.M + m) * 4u : PW_OOB;
+      } else {                                   // DY[b][M][P], row m
+        const int m = m0 + (it >> 3);
+        off = (m < g.M) ? (bw * (unsigned)g.a_bs + (unsigned)m * g.P + pw + (it & 7) * 4) * 4u : PW_OOB;
       }
+      ra[i] = bld4(rA, off);
     }
 #pragma unroll
     for (int i = 0; i < B_ITEMS; ++i) {
       const int it = tid + i * 256;
-      if (MODE != PW_WGRAD) {                    // [K][P] k-major, row k, pixels n0 + c4*4
-        const int kr = it / (BN / 4), c4 = it % (BN / 4);
-        const int k = kb + kr;
-        rb[i] = ld4(Bimg + (long)k * g.P + c4 * 4, k < kend, g.B);
+      unsigned off;
+      if (MODE != PW_WGRAD) {                    // [K][P] k-major (k >= K is past the range)
+        const int k = kb + it / (BN / 4);
+        off = ((unsigned)k * g.P + p0 + (it % (BN / 4)) * 4) * 4u;
       } else {                                   // X[b][N][P], row n
-        const int row = it >> 3, k = kb + (it & 7) * 4;
-        const int n = n0 + row;
-        const int b = k / g.P, p = k - b * g.P;
-        rb[i] = ld4(g.B + (long)b * g.b_bs + (long)n * g.P + p, n < g.N && k < kend, g.B);
+        const int n = n0 + (it >> 3);
+        off = (n < g.N) ? (bw * (unsigned)g.b_bs + (unsigned)n * g.P + pw + (it & 7) * 4) * 4u : PW_OOB;
       }
+      rb[i] = bld4(rB, off);
     }
   };
   auto sstore = [&](int buf) {
@@ -163,25 +184,40 @@ __global__ __launch_bounds__(256) void pwgemm_kernel(PwArgs g) {
       else off = (it >> 3) * A_STR + (it & 7) * 4;
       *reinterpret_cast<pbf16x4*>(As + off) = cvt4(ra[i], 0, 0.f);
     }
+    auto bstore = [&](auto cv) {
 #pragma unroll
-    for (int i = 0; i < B_ITEMS; ++i) {
-      const int it = tid + i * 256;
-      int off;
-      if (B_KMAJ) off = (it / (BN / 4)) * B_STR + (it % (BN / 4)) * 4;
-      else off = (it >> 3) * B_STR + (it & 7) * 4;
-      *reinterpret_cast<pbf16x4*>(Bs + off) = cvt4(rb[i], g.bact, g.slope);
-    }
+      for (int i = 0; i < B_ITEMS; ++i) {
+        const int it = tid + i * 256;
+        int off;
+        if (B_KMAJ) off = (it / (BN / 4)) * B_STR + (it % (BN / 4)) * 4;
+        else off = (it >> 3) * B_STR + (it & 7) * 4;
+        *reinterpret_cast<pbf16x4*>(Bs + off) = cv(rb[i]);
+      }
+    };
+    // activation-on-load switch hoisted out of the element loop (uniform)
+    if (g.bact == ACT_NONE) bstore([](float4 v) { return cvt4(v, 0, 0.f); });
+    else if (g.bact == ACT_GELU)
+      bstore([](float4 v) {
+        return cvt4(make_float4(gelu_f(v.x), gelu_f(v.y), gelu_f(v.z), gelu_f(v.w)), 0, 0.f);
+      });
+    else bstore([&](float4 v) { return cvt4(v, g.bact, g.slope); });
   };
 
   // ---- accumulators (bias folded into the init for FWD) ----
   pf32x16 acc[TM][TN];
+  const bool has_bias = MODE == PW_FWD && g.bias != nullptr;
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
     float bv[16];
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int m = m0 + wm * TM * 32 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-      bv[r] = (MODE == PW_FWD && g.bias && m < g.M) ? g.bias[m] : 0.f;
+    for (int r = 0; r < 16; ++r) bv[r] = 0.f;
+    if (has_bias) {   // one uniform branch; guarded loads are clamp + select (see igemm.hip ldsel)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = m0 + wm * TM * 32 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+        const float t = g.bias[m < g.M ? m : 0];
+        bv[r] = m < g.M ? t : 0.f;
+      }
     }
 #pragma unroll
     for (int j = 0; j < TN; ++j)
@@ -265,13 +301,11 @@ __global__ __launch_bounds__(256) void pwgemm_kernel(PwArgs g) {
       const int mrow = m0 + wm * TM * 32 + i * 32;   // uniform
       // lane part of the offset: rows 4h, column col.  In a partial M tile, rows >= M get an
       // offset past the resource range so the hardware drops the store / returns 0.
-      int vofs = (4 * lh * g.P + col) * 4;
+      const int vofs = (4 * lh * g.P + col) * 4;
+      const int mlim = full ? BM : g.M - mrow - 4 * lh;   // rows (r&3)+8(r>>2) < mlim are valid
       int vrow[16];
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        vrow[r] = vofs;
-        if (!full && mrow + (r & 3) + 8 * (r >> 2) + 4 * lh >= g.M) vrow[r] = 0x7fffffff;
-      }
+      for (int r = 0; r < 16; ++r) vrow[r] = ((r & 3) + 8 * (r >> 2) < mlim) ? vofs : (int)PW_OOB;
       float v[16];
 #pragma unroll
       for (int r = 0; r < 16; ++r) v[r] = acc[i][j][r];
@@ -281,13 +315,7 @@ __global__ __launch_bounds__(256) void pwgemm_kernel(PwArgs g) {
         for (int r = 0; r < 16; ++r)
           gv[r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
                       rg, vrow[r], (mrow + (r & 3) + 8 * (r >> 2)) * P4, 0));
-        if (g.gact == ACT_GELU) {
-#pragma unroll
-          for (int r = 0; r < 16; ++r) v[r] *= gelu_g(gv[r]);
-        } else {
-#pragma unroll
-          for (int r = 0; r < 16; ++r) v[r] *= act_g(g.gact, gv[r], g.slope);
-        }
+        act_g_mul_arr(g.gact, v, gv, g.slope);
       }
       if (g.ypre) {
 #pragma unroll
@@ -295,21 +323,19 @@ __global__ __launch_bounds__(256) void pwgemm_kernel(PwArgs g) {
           __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v[r]), rp, vrow[r],
                                                 (mrow + (r & 3) + 8 * (r >> 2)) * P4, 0);
       }
-      switch (g.act) {
-        case ACT_NONE: break;
-        case ACT_GELU:
-#pragma unroll
-          for (int r = 0; r < 16; ++r) v[r] = gelu_f(v[r]);
-          break;
-        default:
-#pragma unroll
-          for (int r = 0; r < 16; ++r) v[r] = act_f(g.act, v[r], g.slope);
-      }
+      act_f_arr(g.act, v, g.slope);
       if (g.accumulate) {
 #pragma unroll
         for (int r = 0; r < 16; ++r)
           v[r] += __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
                       ry, vrow[r], (mrow + (r & 3) + 8 * (r >> 2)) * P4, 0));
+      }
+      if (g.dbg & 1) {
+        float t = 0.f;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) t += v[r];
+        if (t == 1234.5678f) g.Y[0] = t;
+        continue;
       }
 #pragma unroll
       for (int r = 0; r < 16; ++r)
@@ -354,11 +380,20 @@ extern "C" int dsgan_pw_gemm(int mode, const float* A, long a_bs, const float* B
                              hipStream_t st) {
   DSG_REQUIRE(A && B && Y && M > 0 && N > 0 && K > 0 && P > 0 && nb > 0, "dsgan_pw_gemm: bad args");
   PwArgs g{};
+  {
+    static int dbg = -1;
+    if (dbg < 0) { const char* e = getenv("DSGAN_PW_DBG"); dbg = e ? atoi(e) : 0; }
+    g.dbg = dbg;
+  }
   g.A = A; g.a_bs = a_bs; g.B = B; g.b_bs = b_bs; g.Y = Y; g.y_bs = y_bs; g.bias = bias;
   g.ypre = ypre; g.ypre_bs = ypre_bs; g.gpre = gpre; g.gpre_bs = gpre_bs;
   g.act = act; g.gact = gact; g.bact = bact; g.accumulate = accumulate; g.slope = slope;
   g.P = P;
+  const long lim = (long)PW_OOB;
   if (mode == PW_WGRAD) {
+    const long ar = ((long)(nb - 1) * a_bs + (long)M * P) * 4, br = ((long)(nb - 1) * b_bs + (long)N * P) * 4;
+    DSG_REQUIRE(ar < lim && br < lim, "dsgan_pw_gemm: WGRAD operands exceed 4 GiB buffer range");
+    g.a_range = (unsigned)ar; g.b_range = (unsigned)br;
     DSG_REQUIRE(dsgan_pw_supported(mode, M, K, P, a_bs, b_bs, A, B), "dsgan_pw_gemm: unsupported WGRAD shape");
     g.M = M; g.N = N; g.K = nb * P;
     const int BM = M > 64 ? 128 : 64;
@@ -377,6 +412,9 @@ extern "C" int dsgan_pw_gemm(int mode, const float* A, long a_bs, const float* B
     DSG_REQUIRE(dsgan_pw_supported(mode, M, K, P, a_bs, b_bs, A, B), "dsgan_pw_gemm: unsupported shape");
     DSG_REQUIRE((long)M * P * 4 < (1L << 32), "dsgan_pw_gemm: M*P too large for a buffer resource");
     g.M = M; g.N = nb * P; g.K = K;
+    DSG_REQUIRE((long)K * P * 4 < lim && (long)M * K * 4 < lim, "dsgan_pw_gemm: operand exceeds 4 GiB buffer range");
+    g.a_range = (unsigned)((long)M * K * 4);
+    g.b_range = (unsigned)((long)K * P * 4);
     const bool big = M > 64;
     if (mode == PW_FWD) { if (big) pw_launch<PW_FWD, 128>(g, 1, st); else pw_launch<PW_FWD, 64>(g, 1, st); }
     else { if (big) pw_launch<PW_DGRAD, 128>(g, 1, st); else pw_launch<PW_DGRAD, 64>(g, 1, st); }

@@ -42,7 +42,7 @@ struct TcArgs {
 };
 
 template <int BM>
-__global__ __launch_bounds__(256) void tconv_kernel(TcArgs g) {
+__global__ __launch_bounds__(256, 2) void tconv_kernel(TcArgs g) {
   constexpr int BN = 128;
   constexpr int WM = 2, WN = 2;
   constexpr int TM = BM / WM / 32, TN = BN / WN / 32;
@@ -50,7 +50,9 @@ __global__ __launch_bounds__(256) void tconv_kernel(TcArgs g) {
   constexpr int A_ITEMS = BM * 8 / 256;  // float4 items of the [BM][32] A tile
   __shared__ __attribute__((aligned(16))) __bf16 smem[2 * (A_SZ + B_SZ)];
 
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // wave index through readfirstlane: the compiler then knows it is uniform (SGPR), so
+  // per-wave row offsets can be scalar soffsets instead of readfirstlane waterfall loops
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave / WN, wn = wave % WN;
   const int lr = lane & 31, lh = lane >> 5;
 
@@ -68,11 +70,13 @@ __global__ __launch_bounds__(256) void tconv_kernel(TcArgs g) {
   const int m0 = m_t * BM, q0 = nt_i * BN;
 
   const int HWin = g.Hin * g.Win;
+  const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)g.Wt, (short)0, (unsigned)((long)g.ntaps * g.M * g.K * 4), 0x00020000);
   const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(g.X + (long)bimg * g.x_bs), (short)0, (unsigned)((long)g.K * HWin * 4), 0x00020000);
 
   // B staging: thread -> column c = tid % 128, channels 16*(tid/128) .. +15 of the step
-  const int col = tid & 127, kc = tid >> 7;
+  const int col = tid & 127, kc = wave >> 1;   // kc uniform per wave: channel rows are soffsets
   const int q = q0 + col;
   const bool qv = q < Pout;
   const int oh = qv ? q / g.Wout : 0, ow = qv ? q - (q / g.Wout) * g.Wout : 0;
@@ -86,15 +90,14 @@ __global__ __launch_bounds__(256) void tconv_kernel(TcArgs g) {
   auto gload = [&](int kt) {
     const int tap = kt / ksteps_per_tap;
     const int k0 = (kt - tap * ksteps_per_tap) * TBK;
-    const float* Wtap = g.Wt + (long)tap * g.M * g.K;
+    // A rows past M get an offset past the resource range (reads 0, no branch)
+    const unsigned wtap = (unsigned)tap * g.M * g.K * 4u;
 #pragma unroll
     for (int i = 0; i < A_ITEMS; ++i) {
       const int it = tid + i * 256;
-      const int row = it >> 3, kk = k0 + (it & 7) * 4;
-      const int m = m0 + row;
-      const bool ok = m < g.M;
-      const float4 t = *reinterpret_cast<const float4*>(Wtap + (long)(ok ? m : 0) * g.K + kk);
-      ra[i] = ok ? t : make_float4(0.f, 0.f, 0.f, 0.f);
+      const int m = m0 + (it >> 3), kk = k0 + (it & 7) * 4;
+      const unsigned off = m < g.M ? ((unsigned)m * g.K + kk) * 4u : 0xFFFFFFF0u;
+      ra[i] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rw, (int)off, wtap, 0));
     }
     const int ih = ih0 + g.dh[tap], iw = iw0 + g.dw[tap];
     const bool in = qv && (unsigned)ih < (unsigned)g.Hin && (unsigned)iw < (unsigned)g.Win;
@@ -124,13 +127,19 @@ __global__ __launch_bounds__(256) void tconv_kernel(TcArgs g) {
   };
 
   tf32x16 acc[TM][TN];
+  const bool has_bias = g.bias != nullptr;
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
     float bv[16];
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int m = m0 + wm * TM * 32 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-      bv[r] = (g.bias && m < g.M) ? g.bias[m] : 0.f;
+    for (int r = 0; r < 16; ++r) bv[r] = 0.f;
+    if (has_bias) {   // one uniform branch; guarded loads are clamp + select (see igemm.hip ldsel)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = m0 + wm * TM * 32 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+        const float t = g.bias[m < g.M ? m : 0];
+        bv[r] = m < g.M ? t : 0.f;
+      }
     }
 #pragma unroll
     for (int j = 0; j < TN; ++j)
@@ -185,33 +194,22 @@ __global__ __launch_bounds__(256) void tconv_kernel(TcArgs g) {
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
       const int mrow = m0 + wm * TM * 32 + i * 32;
+      const int mlim = full ? BM : g.M - mrow - 4 * lh;   // rows (r&3)+8(r>>2) < mlim are valid
       int vrow[16];
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        vrow[r] = vbase;
-        if (!full && mrow + (r & 3) + 8 * (r >> 2) + 4 * lh >= g.M) vrow[r] = 0x7fffffff;
-      }
+      for (int r = 0; r < 16; ++r) vrow[r] = ((r & 3) + 8 * (r >> 2) < mlim) ? vbase : 0x7fffffff;
       float v[16];
 #pragma unroll
       for (int r = 0; r < 16; ++r) v[r] = acc[i][j][r];
       if (g.gpre) {
+        float gv[16];
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const float gv = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+        for (int r = 0; r < 16; ++r)
+          gv[r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
               rg, vrow[r], (mrow + (r & 3) + 8 * (r >> 2)) * HWd * 4, 0));
-          v[r] *= act_g(g.gact, gv, g.slope);
-        }
+        act_g_mul_arr(g.gact, v, gv, g.slope);
       }
-      switch (g.act) {
-        case ACT_NONE: break;
-        case ACT_RELU:
-#pragma unroll
-          for (int r = 0; r < 16; ++r) v[r] = fmaxf(v[r], 0.f);
-          break;
-        default:
-#pragma unroll
-          for (int r = 0; r < 16; ++r) v[r] = act_f(g.act, v[r], g.slope);
-      }
+      act_f_arr(g.act, v, g.slope);
 #pragma unroll
       for (int r = 0; r < 16; ++r)
         __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v[r]), ry, vrow[r],
@@ -271,6 +269,7 @@ int dsgan_tconv(const float* X, long x_bs, const float* Wt, const float* bias, f
   DSG_REQUIRE((long)K * Hin * Win * 4 < 0x7fffffffL && (long)M * Hdst * Wdst * 4 < 0x7fffffffL,
               "dsgan_tconv: tensor exceeds a 2 GiB buffer resource");
   DSG_REQUIRE(((uintptr_t)Wt & 15) == 0, "dsgan_tconv: Wt must be 16-byte aligned");
+  DSG_REQUIRE((long)ntaps * M * K * 4 < 0xFFFFFFF0L, "dsgan_tconv: Wt exceeds a 4 GiB buffer resource");
   TcArgs g{};
   g.X = X; g.x_bs = x_bs; g.Wt = Wt; g.Y = Y; g.y_bs = y_bs; g.bias = bias; g.gpre = gpre;
   g.gpre_bs = gpre_bs; g.nb = nb; g.K = K; g.M = M; g.Hin = Hin; g.Win = Win; g.Hout = Hout;
