@@ -1,0 +1,298 @@
+// Direct convolutions for contractions with a handful of channels on one side (gfx950).
+//
+// A 128x128 MFMA tile wastes >95% of its work when one GEMM dimension is 1..8, and these
+// layers sit at the full 256x256 resolution, so they are HBM/L2-bound streaming kernels here:
+//   * small_out: outputs with M <= 8 channels -- the G head conv 64->3 (MixConvNeXtML.py:459),
+//     the PatchGAN last conv 256->1 (networks.py:567), and the data-grads INTO a 3/6-channel
+//     tensor (VGG16 conv1_1, vgg.py:17; PatchGAN conv 0, networks.py:543) as transposed convs.
+//     Thread = output pixel, all M accumulators in registers, weights via scalar loads, the
+//     input through branch-free buffer loads (zero padding = out-of-range offset).
+//   * wgrad_small: weight-grads with <= 8 channels on one side -- the G head (Cout 3), the
+//     first 1x1 convs from the 3-channel input (to32 / shortcut, MixConvNeXtML.py:124,145) and
+//     the PatchGAN ends.  Workgroup = (big-side channel, pixel chunk); the small side x taps are
+//     register accumulators, reduced once per workgroup and added atomically.
+#include "common.h"
+
+namespace dsg {
+
+constexpr unsigned SK_OOB = 0xFFFFFFF0u;
+
+struct SkArgs {
+  const float* x; long x_bs;        // input [nb][K][Hin][Win]
+  const float* w;                   // element (m, k, kh, kw) at w[m*wm + k*wk + kh*wh + kw*ww]
+  long wm, wk, wh, ww;
+  const float* bias;
+  float* y; long y_bs;              // output [nb][M][Ho][Wo]
+  int nb, K, M, Hin, Win, Ho, Wo, KH, KW, stride, pad, transposed;
+  int accumulate;
+  unsigned x_range;
+};
+
+__device__ __forceinline__ float bld(__amdgpu_buffer_rsrc_t r, unsigned off) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, (int)off, 0, 0));
+}
+
+// out[b][m][oh][ow] (+)= bias[m] + sum_{k,kh,kw} w(m,k,kh,kw) * in(b, k, tap)
+//   conv:        in = x[b][k][oh*s - pad + kh][ow*s - pad + kw]
+//   transposed:  in = x[b][k][(oh + pad - kh)/s][(ow + pad - kw)/s]  (when divisible)
+// Workgroup = 64 output pixels x 4 waves; wave w sums channels k = w, w+4, ...; the four partial
+// sums are combined through LDS in a fixed order (deterministic, no atomics).  The weights are
+// staged once per workgroup into LDS as [k][tap][MS] (broadcast reads in the loop); KH/KW are
+// template constants for the common 1x1/3x3/4x4 cases so every tap load of a channel is issued
+// back to back (KH_ = 0: runtime taps).
+template <int MS, int KH_, int KW_>
+__global__ __launch_bounds__(256) void small_out_kernel(SkArgs a) {
+  extern __shared__ float wsm[];                 // [K][KH*KW][MS]
+  __shared__ float part[3][MS][64];
+  const int KH = KH_ ? KH_ : a.KH, KW = KW_ ? KW_ : a.KW, T = KH * KW;
+  for (int i = threadIdx.x; i < a.K * T * MS; i += 256) {
+    const int m = i % MS, kt = i / MS, k = kt / T, t = kt - k * T;
+    wsm[i] = m < a.M ? a.w[m * a.wm + k * a.wk + (t / KW) * a.wh + (t % KW) * a.ww] : 0.f;
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int HWo = a.Ho * a.Wo;
+  const long total = (long)a.nb * HWo;
+  long q = (long)blockIdx.x * 64 + lane;
+  const bool qv = q < total;
+  if (!qv) q = 0;
+  const int b = (int)(q / HWo), r = (int)(q - (long)b * HWo);
+  const int oh = r / a.Wo, ow = r - (r / a.Wo) * a.Wo;
+  const int HWi = a.Hin * a.Win;
+  const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc((void*)a.x, (short)0, a.x_range, 0x00020000);
+  const unsigned xb = (unsigned)((long)b * a.x_bs);
+
+  // per-tap in-plane offsets (or OOB), independent of k
+  constexpr int TMAX = KH_ ? KH_ * KW_ : 1;
+  unsigned toff[TMAX];
+  auto tap_off = [&](int kh, int kw) -> unsigned {
+    int ih, iw; bool ok;
+    if (!a.transposed) {
+      ih = oh * a.stride - a.pad + kh; iw = ow * a.stride - a.pad + kw;
+      ok = ((unsigned)ih < (unsigned)a.Hin) & ((unsigned)iw < (unsigned)a.Win);
+    } else {
+      const int th = oh + a.pad - kh, tw = ow + a.pad - kw;
+      ih = a.stride == 1 ? th : (th >> 1); iw = a.stride == 1 ? tw : (tw >> 1);
+      ok = (th >= 0) & (tw >= 0) & ((a.stride == 1) | !((th | tw) & 1)) & (ih < a.Hin) & (iw < a.Win);
+    }
+    return ok ? (unsigned)(ih * a.Win + iw) : 0x3FFFFFF0u;
+  };
+  if (KH_) {
+#pragma unroll
+    for (int t = 0; t < TMAX; ++t) toff[t] = tap_off(t / KW_, t % KW_);
+  }
+
+  float acc[MS];
+#pragma unroll
+  for (int m = 0; m < MS; ++m) acc[m] = 0.f;
+  for (int k = wave; k < a.K; k += 4) {
+    const unsigned xk = xb + (unsigned)k * HWi;
+    const float* wk = wsm + k * T * MS;
+    if (KH_) {
+      float xv[TMAX];
+#pragma unroll
+      for (int t = 0; t < TMAX; ++t) xv[t] = bld(rx, toff[t] >= 0x3FFFFFF0u ? SK_OOB : (xk + toff[t]) * 4u);
+#pragma unroll
+      for (int t = 0; t < TMAX; ++t)
+#pragma unroll
+        for (int m = 0; m < MS; ++m) acc[m] = fmaf(wk[t * MS + m], xv[t], acc[m]);
+    } else {
+      for (int t = 0; t < T; ++t) {
+        const unsigned o = tap_off(t / KW, t % KW);
+        const float xv = bld(rx, o >= 0x3FFFFFF0u ? SK_OOB : (xk + o) * 4u);
+#pragma unroll
+        for (int m = 0; m < MS; ++m) acc[m] = fmaf(wk[t * MS + m], xv, acc[m]);
+      }
+    }
+  }
+  if (wave > 0) {
+#pragma unroll
+    for (int m = 0; m < MS; ++m) part[wave - 1][m][lane] = acc[m];
+  }
+  __syncthreads();
+  if (wave > 0 || !qv) return;
+  float* yp = a.y + (long)b * a.y_bs + r;
+#pragma unroll
+  for (int m = 0; m < MS; ++m) {
+    if (m >= a.M) break;
+    float v = ((acc[m] + part[0][m][lane]) + part[1][m][lane]) + part[2][m][lane];
+    if (a.bias) v += a.bias[m];
+    if (a.accumulate) v += yp[(long)m * HWo];
+    yp[(long)m * HWo] = v;
+  }
+}
+
+// dw[co][ci][kh][kw] += sum_{b,oh,ow} dy[b][co][oh][ow] * x[b][ci][oh*s-pad+kh][ow*s-pad+kw]
+// SMALL_OUT: Cout <= S (block = ci); else Cin <= S (block = co).  T = KH*KW taps.
+struct WsArgs {
+  const float* dy; long dy_bs;
+  const float* x; long x_bs;
+  float* dw;
+  int nb, Cin, Hin, Win, Cout, Ho, Wo, KW, stride, pad, nsmall;
+  long pix_per_block;
+  unsigned x_range, dy_range;
+};
+
+template <int S, int T, bool SMALL_OUT>
+__global__ __launch_bounds__(256) void wgrad_small_kernel(WsArgs a) {
+  __shared__ float red[4][S * T];
+  const int c = blockIdx.x;                      // ci (SMALL_OUT) or co
+  const int HWo = a.Ho * a.Wo, HWi = a.Hin * a.Win;
+  const long total = (long)a.nb * HWo;
+  const long p0 = (long)blockIdx.y * a.pix_per_block;
+  const long p1 = min(total, p0 + a.pix_per_block);
+  const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc((void*)a.x, (short)0, a.x_range, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rg = __builtin_amdgcn_make_buffer_rsrc((void*)a.dy, (short)0, a.dy_range, 0x00020000);
+
+  float acc[S][T];
+#pragma unroll
+  for (int s = 0; s < S; ++s)
+#pragma unroll
+    for (int t = 0; t < T; ++t) acc[s][t] = 0.f;
+
+  for (long p = p0 + threadIdx.x; p < p1; p += 256) {
+    const int b = (int)(p / HWo), r = (int)(p - (long)b * HWo);
+    const int oh = r / a.Wo, ow = r - (r / a.Wo) * a.Wo;
+    const int ih0 = oh * a.stride - a.pad, iw0 = ow * a.stride - a.pad;
+    unsigned toff[T];                            // tap offsets inside one input plane (or OOB)
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+      const int ih = ih0 + t / a.KW, iw = iw0 + t % a.KW;
+      const bool ok = ((unsigned)ih < (unsigned)a.Hin) & ((unsigned)iw < (unsigned)a.Win);
+      toff[t] = ok ? (unsigned)(ih * a.Win + iw) : 0x3FFFFFF0u;
+    }
+    const unsigned xb = (unsigned)((long)b * a.x_bs), gb = (unsigned)((long)b * a.dy_bs) + r;
+    if (SMALL_OUT) {
+      float g[S];
+#pragma unroll
+      for (int s = 0; s < S; ++s)
+        g[s] = s < a.nsmall ? bld(rg, (gb + (unsigned)s * HWo) * 4u) : 0.f;
+      const unsigned xc = xb + (unsigned)c * HWi;
+#pragma unroll
+      for (int t = 0; t < T; ++t) {
+        const float xv = bld(rx, toff[t] >= 0x3FFFFFF0u ? SK_OOB : (xc + toff[t]) * 4u);
+#pragma unroll
+        for (int s = 0; s < S; ++s) acc[s][t] = fmaf(g[s], xv, acc[s][t]);
+      }
+    } else {
+      const float g = bld(rg, (gb + (unsigned)c * HWo) * 4u);
+#pragma unroll
+      for (int s = 0; s < S; ++s) {
+        if (s >= a.nsmall) break;
+        const unsigned xc = xb + (unsigned)s * HWi;
+#pragma unroll
+        for (int t = 0; t < T; ++t) {
+          const float xv = bld(rx, toff[t] >= 0x3FFFFFF0u ? SK_OOB : (xc + toff[t]) * 4u);
+          acc[s][t] = fmaf(g, xv, acc[s][t]);
+        }
+      }
+    }
+  }
+  const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
+#pragma unroll
+  for (int s = 0; s < S; ++s) {
+    if (s >= a.nsmall) break;
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+      const float v = warp_sum(acc[s][t]);
+      if (ln == 0) red[wv][s * T + t] = v;
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < a.nsmall * T; i += 256) {
+    const float v = red[0][i] + red[1][i] + red[2][i] + red[3][i];
+    const int s = i / T, t = i - s * T;
+    const long o = SMALL_OUT ? ((long)s * a.Cin + c) * T + t : ((long)c * a.Cin + s) * T + t;
+    atomicAdd(a.dw + o, v);
+  }
+}
+
+template <int S, int T, bool SO>
+static void ws_launch(const WsArgs& a, int big, int chunks, hipStream_t st) {
+  hipLaunchKernelGGL((wgrad_small_kernel<S, T, SO>), dim3(big, chunks), dim3(256), 0, st, a);
+}
+
+}  // namespace dsg
+
+using namespace dsg;
+
+extern "C" {
+
+// Small-output direct conv / transposed conv (see small_out_kernel).  Weight strides are in
+// elements and may be negative (flipped kernels).  accumulate=0 overwrites y.
+int dsgan_conv_small_out(const float* x, long x_bs, const float* w, long wm, long wk, long wh, long ww,
+                         const float* bias, float* y, long y_bs, int nb, int K, int M, int Hin, int Win,
+                         int Ho, int Wo, int KH, int KW, int stride, int pad, int transposed,
+                         int accumulate, hipStream_t st) {
+  DSG_REQUIRE(x && w && y && nb > 0 && K > 0 && M >= 1 && M <= 8 && Ho > 0 && Wo > 0 && KH > 0 && KW > 0,
+              "dsgan_conv_small_out: bad args");
+  DSG_REQUIRE(!transposed || stride == 1 || stride == 2, "dsgan_conv_small_out: transposed stride must be 1 or 2");
+  const long xr = ((long)(nb - 1) * x_bs + (long)K * Hin * Win) * 4;
+  DSG_REQUIRE(xr < (long)SK_OOB && (long)nb * x_bs * 4 < (long)SK_OOB, "dsgan_conv_small_out: input exceeds 4 GiB");
+  SkArgs a{};
+  a.x = x; a.x_bs = x_bs; a.w = w; a.wm = wm; a.wk = wk; a.wh = wh; a.ww = ww; a.bias = bias;
+  a.y = y; a.y_bs = y_bs; a.nb = nb; a.K = K; a.M = M; a.Hin = Hin; a.Win = Win; a.Ho = Ho; a.Wo = Wo;
+  a.KH = KH; a.KW = KW; a.stride = stride; a.pad = pad; a.transposed = transposed;
+  a.x_range = (unsigned)xr;
+  a.accumulate = accumulate;
+  const long pblocks = ((long)nb * Ho * Wo + 63) / 64;
+  DSG_REQUIRE(pblocks < (1L << 31), "dsgan_conv_small_out: too many pixels");
+  const dim3 grid((unsigned)pblocks);
+  const int MSr = M == 1 ? 1 : (M <= 4 ? 4 : 8);
+  const size_t lds = (size_t)K * KH * KW * MSr * 4;
+  DSG_REQUIRE(lds <= 64 * 1024, "dsgan_conv_small_out: K*KH*KW*M too large for the LDS weight stage");
+#define SO_LAUNCH(MS_, KH__, KW__) hipLaunchKernelGGL((small_out_kernel<MS_, KH__, KW__>), grid, dim3(256), lds, st, a)
+#define SO_SHAPES(MS_)                                                      \
+  if (KH == 1 && KW == 1) SO_LAUNCH(MS_, 1, 1);                             \
+  else if (KH == 3 && KW == 3) SO_LAUNCH(MS_, 3, 3);                        \
+  else if (KH == 4 && KW == 4) SO_LAUNCH(MS_, 4, 4);                        \
+  else SO_LAUNCH(MS_, 0, 0);
+  if (MSr == 1) { SO_SHAPES(1) } else if (MSr == 4) { SO_SHAPES(4) } else { SO_SHAPES(8) }
+#undef SO_SHAPES
+#undef SO_LAUNCH
+  DSG_CHECK_LAUNCH();
+  return 0;
+}
+
+// Weight-grad with Cout <= 8 or Cin <= 8 and KH*KW in {1, 9, 16}; dw += (OIHW).
+int dsgan_conv_wgrad_small(const float* dy, long dy_bs, const float* x, long x_bs, float* dw, int N,
+                           int Cin, int H, int W, int Cout, int KH, int KW, int stride, int pad, int Ho,
+                           int Wo, hipStream_t st) {
+  DSG_REQUIRE(dy && x && dw && N > 0 && Cin > 0 && Cout > 0 && Ho > 0 && Wo > 0, "dsgan_conv_wgrad_small: bad args");
+  const int T = KH * KW;
+  DSG_REQUIRE(T == 1 || T == 9 || T == 16, "dsgan_conv_wgrad_small: KH*KW must be 1, 9 or 16");
+  const bool so = Cout <= 8;
+  DSG_REQUIRE(so || Cin <= 8, "dsgan_conv_wgrad_small: needs Cout <= 8 or Cin <= 8");
+  const long xr = ((long)(N - 1) * x_bs + (long)Cin * H * W) * 4;
+  const long gr = ((long)(N - 1) * dy_bs + (long)Cout * Ho * Wo) * 4;
+  DSG_REQUIRE(xr < 0x3FFFFFF0L && gr < (long)SK_OOB, "dsgan_conv_wgrad_small: operand exceeds buffer range");
+  DSG_REQUIRE((long)H * W < 0x3FFFFFF0L, "dsgan_conv_wgrad_small: plane too large");
+  WsArgs a{};
+  a.dy = dy; a.dy_bs = dy_bs; a.x = x; a.x_bs = x_bs; a.dw = dw; a.nb = N; a.Cin = Cin; a.Hin = H;
+  a.Win = W; a.Cout = Cout; a.Ho = Ho; a.Wo = Wo; a.KW = KW; a.stride = stride; a.pad = pad;
+  a.nsmall = so ? Cout : Cin;
+  a.x_range = (unsigned)xr; a.dy_range = (unsigned)gr;
+  const int big = so ? Cin : Cout;
+  const long total = (long)N * Ho * Wo;
+  long chunks = (2048 + big - 1) / big;
+  const long max_chunks = (total + 4095) / 4096;      // >= 16 pixels per thread
+  if (chunks > max_chunks) chunks = max_chunks;
+  if (chunks < 1) chunks = 1;
+  long ppb = (total + chunks - 1) / chunks;
+  ppb = (ppb + 255) / 256 * 256;
+  chunks = (total + ppb - 1) / ppb;
+  a.pix_per_block = ppb;
+  DSG_REQUIRE(chunks <= 65535, "dsgan_conv_wgrad_small: grid too large");
+  const bool s4 = a.nsmall <= 4;
+#define WS_CASE(TT)                                                                    \
+  if (T == TT) {                                                                       \
+    if (so) { if (s4) ws_launch<4, TT, true>(a, big, (int)chunks, st); else ws_launch<8, TT, true>(a, big, (int)chunks, st); } \
+    else { if (s4) ws_launch<4, TT, false>(a, big, (int)chunks, st); else ws_launch<8, TT, false>(a, big, (int)chunks, st); } \
+  }
+  WS_CASE(1) else WS_CASE(9) else WS_CASE(16)
+#undef WS_CASE
+  DSG_CHECK_LAUNCH();
+  return 0;
+}
+
+}  // extern "C"

@@ -31,6 +31,9 @@ SIGNATURES = {
     # tconv.hip
     "dsgan_conv_wtrans": [P, P, I, I, I, I, I, I, I, I, I, S],
     "dsgan_tconv": [P, L, P, P, P, L, P, L] + [I] * 9 + [P, P] + [I] * 7 + [F, S],
+    # skinny.hip
+    "dsgan_conv_small_out": [P, L, P, L, L, L, L, P, P, L] + [I] * 13 + [S],
+    "dsgan_conv_wgrad_small": [P, L, P, L, P] + [I] * 11 + [S],
     # dwconv.hip
     "dsgan_dwconv_fwd": [P, L, P, P, P, L, I, I, I, I, I, I, S],
     "dsgan_dwconv_wgrad": [P, L, P, L, P, P, I, I, I, I, I, S],

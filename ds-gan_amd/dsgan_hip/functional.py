@@ -173,7 +173,11 @@ def conv_fwd_raw(x, w, b, stride, pad, act=None, out=None, pre=None, accumulate=
     if pre is not None:
         pre, pbs = nchw(pre)
     e0 = IGEMM_TIMER.begin()
-    if KH == 1 and KW == 1 and stride == 1 and pad == 0 and _pw_ok(0, Cout, Cin, H * W, 0, xbs, w.data_ptr(), x.data_ptr()):
+    if Cout <= 8 and act is None and pre is None and xact is None:
+        # few output channels (G head, PatchGAN last layer): direct conv, not a GEMM tile
+        call("dsgan_conv_small_out", ptr(x), xbs, ptr(w), Cin * KH * KW, KH * KW, KW, 1, ptr(b), ptr(y), ybs,
+             N, Cin, Cout, H, W, Ho, Wo, KH, KW, stride, pad, 0, int(accumulate), stream())
+    elif KH == 1 and KW == 1 and stride == 1 and pad == 0 and _pw_ok(0, Cout, Cin, H * W, 0, xbs, w.data_ptr(), x.data_ptr()):
         call("dsgan_pw_gemm", 0, ptr(w), 0, ptr(x), xbs, ptr(y), ybs, ptr(b), ptr(pre), pbs, None, 0,
              Cout, N * H * W, Cin, H * W, N, ACT[act], 0, ACT[xact], int(accumulate), LRELU_SLOPE, stream())
     elif (_state["prec"] == "bf16" and w.dim() == 4 and (KH > 1 or KW > 1) and Cin % 32 == 0
@@ -203,7 +207,11 @@ def conv_dgrad_raw(dy, w, x_shape, stride, pad, bias=None, act=None, gpre=None, 
     if gpre is not None:
         gpre, gbs = nchw(gpre)
     e0 = IGEMM_TIMER.begin()
-    if (KH == 1 and KW == 1 and stride == 1 and pad == 0 and bias is None and act is None
+    if Cin <= 8 and act is None and gpre is None and stride in (1, 2):
+        # data-grad into a 3/6-channel tensor: direct transposed gather, w(m=ci, k=co, kh, kw)
+        call("dsgan_conv_small_out", ptr(dy), dybs, ptr(w), KH * KW, Cin * KH * KW, KW, 1, ptr(bias),
+             ptr(dx), dxbs, N, Cout, Cin, Ho, Wo, H, W, KH, KW, stride, pad, 1, int(accumulate), stream())
+    elif (KH == 1 and KW == 1 and stride == 1 and pad == 0 and bias is None and act is None
             and not accumulate and _pw_ok(1, Cin, Cout, H * W, 0, dybs, w.data_ptr(), dy.data_ptr())):
         call("dsgan_pw_gemm", 1, ptr(w), 0, ptr(dy), dybs, ptr(dx), dxbs, None, None, 0, ptr(gpre), gbs,
              Cin, N * H * W, Cout, H * W, N, 0, ACT[gact], 0, 0, LRELU_SLOPE, stream())
@@ -244,7 +252,10 @@ def conv_wgrad_raw(dy, x, dw, stride, pad, xact=None):
     Cout = dy.shape[1]
     KH, KW = (dw.shape[2], dw.shape[3]) if dw.dim() == 4 else (1, 1)
     e0 = IGEMM_TIMER.begin()
-    if KH == 1 and KW == 1 and stride == 1 and pad == 0 and _pw_ok(2, Cout, N * H * W, H * W, dybs, xbs, dy.data_ptr(), x.data_ptr()):
+    if xact is None and KH * KW in (1, 9, 16) and (Cout <= 8 or (Cin <= 8 and KH * KW == 1)):
+        call("dsgan_conv_wgrad_small", ptr(dy), dybs, ptr(x), xbs, ptr(dw), N, Cin, H, W, Cout, KH, KW,
+             stride, pad, dy.shape[2], dy.shape[3], stream())
+    elif KH == 1 and KW == 1 and stride == 1 and pad == 0 and _pw_ok(2, Cout, N * H * W, H * W, dybs, xbs, dy.data_ptr(), x.data_ptr()):
         call("dsgan_pw_gemm", 2, ptr(dy), dybs, ptr(x), xbs, ptr(dw), 0, None, None, 0, None, 0,
              Cout, Cin, N * H * W, H * W, N, 0, 0, ACT[xact], 0, LRELU_SLOPE, stream())
     else:

@@ -71,6 +71,24 @@ int dsgan_pw_gemm(int mode, const float* A, long a_bs, const float* B, long b_bs
                   long gpre_bs, int M, int N, int K, int P, int nb, int act, int gact, int bact,
                   int accumulate, float slope, hipStream_t stream);
 
+/* ---- direct convs for <= 8 channels on one side (skinny.hip) -----------------------------------
+ * dsgan_conv_small_out: out[b][m][oh][ow] (+)= bias[m] + sum_{k,kh,kw} w(m,k,kh,kw) * in(b,k,tap),
+ *   M <= 8; w(m,k,kh,kw) = w[m*wm + k*wk + kh*wh + kw*ww] (element strides, may be negative).
+ *   transposed=0: conv (in = x[oh*s-pad+kh][ow*s-pad+kw]); transposed=1: the data-grad/ConvTranspose
+ *   gather (in = x[(oh+pad-kh)/s][(ow+pad-kw)/s] where divisible, s in {1,2}).
+ *   Replaces: G head Conv2d(64,3,3) (DSGAN/models/model/MixConvNeXtML.py:459), PatchGAN last Conv2d
+ *   (DSGAN/models/networks.py:567), data-grads into 3/6-channel tensors (VGG conv1_1
+ *   DSGAN/models/vgg.py:17, PatchGAN conv 0 networks.py:543) -- torch.nn.Conv2d forward/backward.
+ * dsgan_conv_wgrad_small: dw[Cout][Cin][KH][KW] += conv weight-grad, Cout <= 8 or Cin <= 8,
+ *   KH*KW in {1, 9, 16}. */
+int dsgan_conv_small_out(const float* x, long x_bs, const float* w, long wm, long wk, long wh, long ww,
+                         const float* bias, float* y, long y_bs, int nb, int K, int M, int Hin, int Win,
+                         int Ho, int Wo, int KH, int KW, int stride, int pad, int transposed,
+                         int accumulate, hipStream_t stream);
+int dsgan_conv_wgrad_small(const float* dy, long dy_bs, const float* x, long x_bs, float* dw, int N,
+                           int Cin, int H, int W, int Cout, int KH, int KW, int stride, int pad, int Ho,
+                           int Wo, hipStream_t stream);
+
 /* ---- tap-major implicit-GEMM conv for channel counts % 32 == 0 (tconv.hip, bf16 MFMA) -------
  * out[b][m][dst(o)] = act(sum_{tap,k} Wt[tap][m][k] * X[b][k][o*stride + (dh,dw)[tap]] + bias[m])
  *                     (* gact'(gpre) if gpre); dst(o) = (oh*os+ph, ow*os+pw) in Hdst x Wdst.

@@ -60,6 +60,10 @@ def _q(t, prec):
     (2, 64, 16, 16, 128, 4, 2, 1),
     (2, 128, 9, 9, 256, 4, 1, 1),      # PatchGAN s1 layers
     (2, 256, 8, 8, 1, 4, 1, 1),
+    (3, 64, 40, 36, 3, 3, 1, 1),       # skinny direct kernels at larger planes
+    (4, 256, 31, 31, 1, 4, 1, 1),      # PatchGAN last layer shape (K-split atomics)
+    (2, 3, 64, 64, 32, 1, 1, 0),       # to32 (wgrad with Cin = 3)
+    (2, 6, 66, 66, 64, 4, 2, 1),       # PatchGAN layer 0 (stride-2 data-grad into 6 channels)
 ])
 def test_conv2d(prec, N, Cin, H, W, Cout, K, s, p):
     from dsgan_hip import functional as HF

@@ -27,7 +27,7 @@ for ms, fl, tag in rows:
 tot = sum(a[1] for a in agg.values())
 print("total igemm ms %.2f over %d launches" % (tot, len(rows)))
 print("%-8s %3s %5s %4s %4s %5s %2s %2s | %4s %8s %7s %7s" % ("mode", "N", "Cin", "H", "W", "Cout", "K", "s", "cnt", "ms", "TF/s", "GB/s*"))
-for tag, (c, ms, fl) in sorted(agg.items(), key=lambda kv: -kv[1][1])[:45]:
+for tag, (c, ms, fl) in sorted(agg.items(), key=lambda kv: -kv[1][1])[:80]:
     mode, N, Cin, H, W, Cout, K, s = tag
     Ho = (H + 2 * (K // 2 if K != 4 else 1) - K) // s + 1
     # fp32 bytes of the three operands at minimum
