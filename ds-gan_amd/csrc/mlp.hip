@@ -1,0 +1,587 @@
+// Fused ConvNeXt pointwise MLP (Block.pwconv1 -> GELU -> pwconv2, DSGAN/models/model/MixConvNeXtML.py:
+// 221-223,236-240) on bf16 MFMA (gfx950).  The 4C-channel hidden activation never touches HBM.
+//
+//   forward : out[b][p][n] (+)= b2[p] + sum_m W2[p][m] * gelu( b1[m] + sum_c W1[m][c] h[b][c][n] )
+//   backward: z = W1 h + b1 (recomputed), t = W2^T dy, dz = t * gelu'(z), g = gelu(z)
+//             dh = W1^T dz                           (fp32, to the InstanceNorm backward)
+//             g, dz -> HBM as bf16                   (operands of the two weight-grads)
+//             bsum[tile][m] = sum_n dz[m][n]         (per-tile partials of the b1 grad)
+//
+// One workgroup owns BN pixels of one image.  Its activation tile(s) are staged once into LDS
+// (bf16, k-major, read with ds_read_b64_tr_b16); the hidden dimension is walked in chunks of HC:
+// per chunk the W1 rows and W2 columns are staged into LDS (register-prefetched one chunk
+// ahead), GEMM1 produces the chunk of z in accumulators, the GELU epilogue writes it to LDS,
+// and GEMM2 (forward) / GEMM-dh (backward) consumes it from there.  Per-pixel HBM traffic is
+// C + P fp32 values forward (vs 2*(4C) + C + 2P unfused) -- the kernel is HBM/LDS bound, not
+// MFMA bound, for every DS-GAN shape.
+//
+// Weights are bf16 copies (w1 [4C][C] as nn.Linear stores it, w2 [P][4C]); the same two LDS
+// chunk layouts serve the transposed products of the backward through the transposing LDS read.
+#include "common.h"
+
+namespace dsg {
+
+typedef __attribute__((ext_vector_type(8))) __bf16 mbf16x8;
+typedef __attribute__((ext_vector_type(4))) __bf16 mbf16x4;
+typedef __attribute__((ext_vector_type(16))) float mf32x16;
+typedef __attribute__((ext_vector_type(4))) short ms16x4;
+typedef __attribute__((address_space(3))) ms16x4 lds_ms16x4;
+typedef __attribute__((ext_vector_type(4))) unsigned int mu32x4;   // raw 16 bytes
+
+// Fragment of a k-major LDS tile T[k][col] (row stride STR elements) for a 32x32x16 MFMA
+// operand: lane (h = lane>>5, c = lane&31) receives T[8h + i][c], i = 0..7, via two
+// ds_read_b64_tr_b16 (see pwgemm.hip).  `p` = T + (ks*16 + 8h + q)*STR + colbase + 16G + 4p.
+__device__ __forceinline__ mbf16x8 mtr_frag(const __bf16* p0, int stride) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  ms16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_ms16x4*)(p0));
+  ms16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_ms16x4*)(p0 + 4 * stride));
+  typedef __attribute__((ext_vector_type(8))) short s16x8;
+  s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(mbf16x8, v);
+#else
+  return mbf16x8{};
+#endif
+}
+
+__device__ __forceinline__ mbf16x4 mcvt4(float4 v) {
+  mbf16x4 r;
+  r[0] = (__bf16)v.x; r[1] = (__bf16)v.y; r[2] = (__bf16)v.z; r[3] = (__bf16)v.w;
+  return r;
+}
+
+// GELU for the bf16 path: erfc by Abramowitz & Stegun 7.1.26 (|err| <= 1.5e-7, far below the
+// bf16 rounding of the result), t = 1/(1 + p*u).  Its exp(-u^2) = exp(-z^2/2) is the same factor
+// GELU's derivative needs, so the pair costs one rcp + one exp + ~14 FMA-class ops (the exact
+// branch-free erf of common.h costs ~40).
+__device__ __forceinline__ float half_erfc_e(float z, float& e) {
+  const float u = fabsf(z) * kInvSqrt2;
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, u, 1.f));
+  float p = fmaf(t, 1.061405429f, -1.453152027f);
+  p = fmaf(t, p, 1.421413741f);
+  p = fmaf(t, p, -0.284496736f);
+  p = fmaf(t, p, 0.254829592f);
+  e = __expf(-u * u);
+  return 0.5f * t * p * e;
+}
+__device__ __forceinline__ float gelu_fast(float z) {
+  float e;
+  const float he = half_erfc_e(z, e);
+  return z * (z >= 0.f ? 1.f - he : he);
+}
+__device__ __forceinline__ void gelu_and_grad(float z, float& g, float& gp) {
+  float e;
+  const float he = half_erfc_e(z, e);
+  const float cdf = z >= 0.f ? 1.f - he : he;
+  g = z * cdf;
+  gp = fmaf(z * kInvSqrt2Pi, e, cdf);
+}
+
+struct MlpArgs {
+  const float* h; long h_bs;        // [nb][C][HW]   block activation after InstanceNorm
+  const float* dy; long dy_bs;      // [nb][P][HW]   (backward) upstream grad of the block output
+  const __bf16* w1;                 // [4C][C]
+  const float* b1;                  // [4C]
+  const __bf16* w2;                 // [P][4C]
+  const float* b2;                  // [P]           (forward; may be null)
+  float* out; long out_bs;          // forward: out [nb][P][HW] (+= when accumulate); backward: dh [nb][C][HW]
+  __bf16* g_out;                    // (backward) gelu(z)  [nb][4C][HW]
+  __bf16* dz_out;                   // (backward) dz       [nb][4C][HW]
+  float* bsum;                      // (backward) [ntiles][4C] per-tile sums of dz
+  int HW, nb, accumulate;
+};
+
+__device__ __forceinline__ int xcd_tile(int id, int nwg) {
+  // consecutive tiles on one XCD (dispatch round-robins workgroups over the 8 XCDs)
+  const int xcd = id & 7, q = nwg >> 3, r = nwg & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (id >> 3);
+}
+
+// Stage a [K][BN] fp32 tile (rows strided by HW) into a k-major bf16 LDS tile [K][STR].
+template <int K, int BN, int STR, int NT>
+__device__ __forceinline__ void stage_rows(__bf16* dst, const float* __restrict__ src, int HW, int tid) {
+  constexpr int ITEMS = K * BN / 4;
+  static_assert(ITEMS % NT == 0, "tile must split evenly over the workgroup");
+  constexpr int PER = ITEMS / NT;
+  constexpr int BATCH = PER < 8 ? PER : 8;
+#pragma unroll
+  for (int i0 = 0; i0 < PER; i0 += BATCH) {
+    float4 v[BATCH];
+#pragma unroll
+    for (int i = 0; i < BATCH; ++i) {
+      const int it = tid + (i0 + i) * NT;
+      const int k = it / (BN / 4), c4 = it % (BN / 4);
+      v[i] = *reinterpret_cast<const float4*>(src + (long)k * HW + c4 * 4);
+    }
+#pragma unroll
+    for (int i = 0; i < BATCH; ++i) {
+      const int it = tid + (i0 + i) * NT;
+      const int k = it / (BN / 4), c4 = it % (BN / 4);
+      *reinterpret_cast<mbf16x4*>(dst + k * STR + c4 * 4) = mcvt4(v[i]);
+    }
+  }
+}
+
+// Register-staged weight chunk j: W1 rows [j*HC, +HC) (all C columns) and W2 columns
+// [j*HC, +HC) (all P rows), 16-byte items.  (Plain native-vector register arrays: a struct of
+// HIP uint4 arrays is demoted to scratch/LDS by the compiler.)
+template <int C, int P, int HC, int NT>
+struct WCh {
+  static constexpr int N1 = HC * C / 8 / NT, N2 = P * HC / 8 / NT;
+  static_assert((HC * C / 8) % NT == 0 && (P * HC / 8) % NT == 0, "weight chunk split");
+};
+
+template <int C, int P, int HC, int NT, int N1, int N2>
+__device__ __forceinline__ void wch_load(mu32x4 (&r1)[N1], mu32x4 (&r2)[N2], const __bf16* __restrict__ w1,
+                                         const __bf16* __restrict__ w2, int j, int tid) {
+  const mu32x4* s1 = reinterpret_cast<const mu32x4*>(w1 + (long)j * HC * C);
+#pragma unroll
+  for (int i = 0; i < N1; ++i) r1[i] = s1[tid + i * NT];
+#pragma unroll
+  for (int i = 0; i < N2; ++i) {
+    const int it = tid + i * NT, row = it / (HC / 8), c8 = it % (HC / 8);
+    r2[i] = *reinterpret_cast<const mu32x4*>(w2 + (long)row * (4 * C) + j * HC + c8 * 8);
+  }
+}
+
+template <int C, int P, int HC, int NT, int W1STR, int W2STR, int N1, int N2>
+__device__ __forceinline__ void wch_store(const mu32x4 (&r1)[N1], const mu32x4 (&r2)[N2], __bf16* W1s, __bf16* W2s,
+                                          int tid) {
+#pragma unroll
+  for (int i = 0; i < N1; ++i) {
+    const int it = tid + i * NT, row = it / (C / 8), c8 = it % (C / 8);
+    *reinterpret_cast<mu32x4*>(W1s + row * W1STR + c8 * 8) = r1[i];
+  }
+#pragma unroll
+  for (int i = 0; i < N2; ++i) {
+    const int it = tid + i * NT, row = it / (HC / 8), c8 = it % (HC / 8);
+    *reinterpret_cast<mu32x4*>(W2s + row * W2STR + c8 * 8) = r2[i];
+  }
+}
+
+// Wave grid of a [M x N] product over NW waves: 2 waves along M, NW/2 along N, each wave
+// TM x TN tiles of 32x32.
+template <int M, int N, int NW>
+struct WGrid {
+  static constexpr int WN = NW / 2, TM = M / 64, TN = N / 32 / WN;
+  static_assert(M % 64 == 0 && N % (32 * WN) == 0 && TM >= 1 && TN >= 1, "wave grid");
+};
+
+// ------------------------------------------------------------------------------------------
+// forward
+// ------------------------------------------------------------------------------------------
+template <int C, int P, int BN, int HC, int NW, int MINB>
+__global__ __launch_bounds__(NW * 64, MINB) void mlp_fwd_kernel(MlpArgs g) {
+  constexpr int NT = NW * 64;
+  constexpr int C4 = 4 * C, NCH = C4 / HC;
+  constexpr int HSTR = BN + 32, GSTR = HC + 8, W1STR = C + 8, W2STR = HC + 8;
+  constexpr int H_SZ = C * HSTR, G_SZ = BN * GSTR, W1_SZ = HC * W1STR, W2_SZ = P * W2STR;
+  // the g chunk overwrites the W1 chunk once GEMM1 is done with it
+  constexpr int GW_SZ = G_SZ > W1_SZ ? G_SZ : W1_SZ;
+  __shared__ __attribute__((aligned(16))) __bf16 smem[H_SZ + GW_SZ + W2_SZ];
+  __bf16* Hs = smem;
+  __bf16* Gs = Hs + H_SZ;
+  __bf16* W1s = Gs;
+  __bf16* W2s = Gs + GW_SZ;
+
+  using ZG = WGrid<HC, BN, NW>;   // z chunk [HC x BN]
+  using OG = WGrid<P, BN, NW>;    // out tile [P x BN]
+  static_assert(C % 32 == 0, "C");
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int lr = lane & 31, lh = lane >> 5;
+  const int tq = (lane >> 2) & 3, tp = lane & 3, tG = (lane >> 4) & 1;
+  const int wm = wave / ZG::WN, wn = wave % ZG::WN;   // same split for both grids (2 x NW/2)
+
+  const int tpi = g.HW / BN;
+  const int tile = xcd_tile(blockIdx.x, gridDim.x);
+  const int img = tile / tpi, p0 = (tile - img * tpi) * BN;
+
+  using WC = WCh<C, P, HC, NT>;
+  mu32x4 wr1[WC::N1], wr2[WC::N2];
+  wch_load<C, P, HC, NT>(wr1, wr2, g.w1, g.w2, 0, tid);
+  stage_rows<C, BN, HSTR, NT>(Hs, g.h + (long)img * g.h_bs + p0, g.HW, tid);
+  wch_store<C, P, HC, NT, W1STR, W2STR>(wr1, wr2, W1s, W2s, tid);
+
+  mf32x16 oacc[OG::TM][OG::TN];
+#pragma unroll
+  for (int i = 0; i < OG::TM; ++i) {
+    float bv[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r)
+      bv[r] = g.b2 ? g.b2[wm * (P / 2) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh] : 0.f;
+#pragma unroll
+    for (int t = 0; t < OG::TN; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) oacc[i][t][r] = bv[r];
+  }
+  __syncthreads();
+
+  for (int j = 0; j < NCH; ++j) {
+    if (j + 1 < NCH) wch_load<C, P, HC, NT>(wr1, wr2, g.w1, g.w2, j + 1, tid);
+    // ---- GEMM1: z = W1[chunk] h + b1 ----
+    mf32x16 zacc[ZG::TM][ZG::TN];
+#pragma unroll
+    for (int i = 0; i < ZG::TM; ++i) {
+      float bv[16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) bv[r] = g.b1[j * HC + wm * (HC / 2) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh];
+#pragma unroll
+      for (int t = 0; t < ZG::TN; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) zacc[i][t][r] = bv[r];
+    }
+#pragma unroll 4
+    for (int ks = 0; ks < C / 16; ++ks) {
+      mbf16x8 af[ZG::TM], bf[ZG::TN];
+#pragma unroll
+      for (int i = 0; i < ZG::TM; ++i)
+        af[i] = *reinterpret_cast<const mbf16x8*>(W1s + (wm * (HC / 2) + i * 32 + lr) * W1STR + ks * 16 + lh * 8);
+#pragma unroll
+      for (int t = 0; t < ZG::TN; ++t)
+        bf[t] = mtr_frag(Hs + (ks * 16 + 8 * lh + tq) * HSTR + wn * (BN / ZG::WN) + t * 32 + 16 * tG + 4 * tp, HSTR);
+#pragma unroll
+      for (int i = 0; i < ZG::TM; ++i)
+#pragma unroll
+        for (int t = 0; t < ZG::TN; ++t)
+          zacc[i][t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bf[t], zacc[i][t], 0, 0, 0);
+    }
+    __syncthreads();   // every wave is done reading W1s (Gs aliases it)
+    // ---- GELU -> Gs (pixel-major [BN][GSTR]) ----
+#pragma unroll
+    for (int i = 0; i < ZG::TM; ++i)
+#pragma unroll
+      for (int t = 0; t < ZG::TN; ++t) {
+        const int n = wn * (BN / ZG::WN) + t * 32 + lr;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          mbf16x4 v;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = (__bf16)gelu_fast(zacc[i][t][4 * q + e]);
+          *reinterpret_cast<mbf16x4*>(Gs + n * GSTR + wm * (HC / 2) + i * 32 + 8 * q + 4 * lh) = v;
+        }
+      }
+    __syncthreads();
+    // ---- GEMM2: out += W2[:, chunk] g ----
+#pragma unroll
+    for (int ks = 0; ks < HC / 16; ++ks) {
+      mbf16x8 af[OG::TM], bf[OG::TN];
+#pragma unroll
+      for (int i = 0; i < OG::TM; ++i)
+        af[i] = *reinterpret_cast<const mbf16x8*>(W2s + (wm * (P / 2) + i * 32 + lr) * W2STR + ks * 16 + lh * 8);
+#pragma unroll
+      for (int t = 0; t < OG::TN; ++t)
+        bf[t] = *reinterpret_cast<const mbf16x8*>(Gs + (wn * (BN / OG::WN) + t * 32 + lr) * GSTR + ks * 16 + lh * 8);
+#pragma unroll
+      for (int i = 0; i < OG::TM; ++i)
+#pragma unroll
+        for (int t = 0; t < OG::TN; ++t)
+          oacc[i][t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bf[t], oacc[i][t], 0, 0, 0);
+    }
+    __syncthreads();
+    if (j + 1 < NCH) {
+      wch_store<C, P, HC, NT, W1STR, W2STR>(wr1, wr2, W1s, W2s, tid);
+      __syncthreads();
+    }
+  }
+
+  // ---- epilogue ----
+  float* ob = g.out + (long)img * g.out_bs + p0;
+#pragma unroll
+  for (int i = 0; i < OG::TM; ++i)
+#pragma unroll
+    for (int t = 0; t < OG::TN; ++t) {
+      const int n = wn * (BN / OG::WN) + t * 32 + lr;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = wm * (P / 2) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+        float* o = ob + (long)m * g.HW + n;
+        *o = g.accumulate ? *o + oacc[i][t][r] : oacc[i][t][r];
+      }
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// backward (data path): dh, g, dz, per-(tile, quarter) sums of dz
+// ------------------------------------------------------------------------------------------
+template <int C, int P, int BN, int HC, int NW>
+__global__ __launch_bounds__(NW * 64, 1) void mlp_bwd_kernel(MlpArgs g) {
+  constexpr int NT = NW * 64;
+  constexpr int C4 = 4 * C, NCH = C4 / HC;
+  constexpr int HSTR = BN + 32, NSTR = HC + 8, W1STR = C + 8, W2STR = HC + 8;
+  constexpr int H_SZ = C * HSTR, D_SZ = P * HSTR, N_SZ = BN * NSTR, W1_SZ = HC * W1STR, W2_SZ = P * W2STR;
+  __shared__ __attribute__((aligned(16))) __bf16 smem[H_SZ + D_SZ + 2 * N_SZ + W1_SZ + W2_SZ];
+  __bf16* Hs = smem;
+  __bf16* Ds = Hs + H_SZ;
+  __bf16* Zn = Ds + D_SZ;     // dz chunk, pixel-major [BN][NSTR]
+  __bf16* Gn = Zn + N_SZ;     // g chunk,  pixel-major [BN][NSTR]
+  __bf16* W1s = Gn + N_SZ;
+  __bf16* W2s = W1s + W1_SZ;
+
+  using ZG = WGrid<HC, BN, NW>;   // z / t chunk [HC x BN]
+  using HG = WGrid<C, BN, NW>;    // dh tile [C x BN]
+  static_assert(P % 16 == 0 && HC == 64 && BN % 16 == 0, "tile shape");
+  // copy-out: blocks of 16 pixels x 32 hidden (one transposing read per lane)
+  constexpr int CB = (BN / 16) * (HC / 32);
+  static_assert(CB % NW == 0, "copy-out split");
+  constexpr int CPW = CB / NW;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int lr = lane & 31, lh = lane >> 5;
+  const int tq = (lane >> 2) & 3, tp = lane & 3, tG = (lane >> 4) & 1;
+  const int wm = wave / ZG::WN, wn = wave % ZG::WN;
+
+  const int tpi = g.HW / BN;
+  const int tile = xcd_tile(blockIdx.x, gridDim.x);
+  const int img = tile / tpi, p0 = (tile - img * tpi) * BN;
+
+  using WC = WCh<C, P, HC, NT>;
+  mu32x4 wr1[WC::N1], wr2[WC::N2];
+  wch_load<C, P, HC, NT>(wr1, wr2, g.w1, g.w2, 0, tid);
+  stage_rows<C, BN, HSTR, NT>(Hs, g.h + (long)img * g.h_bs + p0, g.HW, tid);
+  stage_rows<P, BN, HSTR, NT>(Ds, g.dy + (long)img * g.dy_bs + p0, g.HW, tid);
+  wch_store<C, P, HC, NT, W1STR, W2STR>(wr1, wr2, W1s, W2s, tid);
+
+  mf32x16 hacc[HG::TM][HG::TN];
+#pragma unroll
+  for (int i = 0; i < HG::TM; ++i)
+#pragma unroll
+    for (int t = 0; t < HG::TN; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) hacc[i][t][r] = 0.f;
+  __syncthreads();
+
+  // copy-out block of this wave: hidden half (wave & 1), pixel blocks (wave >> 1) * CPW + c
+  const int chh = (wave & 1) * 32;
+  const long gbase = (long)img * C4 * g.HW + p0;
+  for (int j = 0; j < NCH; ++j) {
+    if (j + 1 < NCH) wch_load<C, P, HC, NT>(wr1, wr2, g.w1, g.w2, j + 1, tid);
+    // ---- z = W1[chunk] h + b1 ;  t = W2[:, chunk]^T dy ----
+    mf32x16 zacc[ZG::TM][ZG::TN], tacc[ZG::TM][ZG::TN];
+#pragma unroll
+    for (int i = 0; i < ZG::TM; ++i) {
+      float bv[16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) bv[r] = g.b1[j * HC + wm * (HC / 2) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh];
+#pragma unroll
+      for (int t = 0; t < ZG::TN; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) { zacc[i][t][r] = bv[r]; tacc[i][t][r] = 0.f; }
+    }
+#pragma unroll 4
+    for (int ks = 0; ks < C / 16; ++ks) {
+      mbf16x8 af[ZG::TM], bf[ZG::TN];
+#pragma unroll
+      for (int i = 0; i < ZG::TM; ++i)
+        af[i] = *reinterpret_cast<const mbf16x8*>(W1s + (wm * (HC / 2) + i * 32 + lr) * W1STR + ks * 16 + lh * 8);
+#pragma unroll
+      for (int t = 0; t < ZG::TN; ++t)
+        bf[t] = mtr_frag(Hs + (ks * 16 + 8 * lh + tq) * HSTR + wn * (BN / ZG::WN) + t * 32 + 16 * tG + 4 * tp, HSTR);
+#pragma unroll
+      for (int i = 0; i < ZG::TM; ++i)
+#pragma unroll
+        for (int t = 0; t < ZG::TN; ++t)
+          zacc[i][t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bf[t], zacc[i][t], 0, 0, 0);
+    }
+#pragma unroll 4
+    for (int ks = 0; ks < P / 16; ++ks) {
+      mbf16x8 af[ZG::TM], bf[ZG::TN];
+#pragma unroll
+      for (int i = 0; i < ZG::TM; ++i)   // A[m][p] = W2[p][m]: W2s [P][W2STR] is k-major for this product
+        af[i] = mtr_frag(W2s + (ks * 16 + 8 * lh + tq) * W2STR + wm * (HC / 2) + i * 32 + 16 * tG + 4 * tp, W2STR);
+#pragma unroll
+      for (int t = 0; t < ZG::TN; ++t)
+        bf[t] = mtr_frag(Ds + (ks * 16 + 8 * lh + tq) * HSTR + wn * (BN / ZG::WN) + t * 32 + 16 * tG + 4 * tp, HSTR);
+#pragma unroll
+      for (int i = 0; i < ZG::TM; ++i)
+#pragma unroll
+        for (int t = 0; t < ZG::TN; ++t)
+          tacc[i][t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bf[t], tacc[i][t], 0, 0, 0);
+    }
+    // ---- epilogue: g = gelu(z), dz = t * gelu'(z) -> LDS, pixel-major, 4 hidden per write ----
+#pragma unroll
+    for (int i = 0; i < ZG::TM; ++i)
+#pragma unroll
+      for (int t = 0; t < ZG::TN; ++t) {
+        const int n = wn * (BN / ZG::WN) + t * 32 + lr;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          mbf16x4 gv4, dv4;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            float gv, gp;
+            gelu_and_grad(zacc[i][t][4 * q + e], gv, gp);
+            gv4[e] = (__bf16)gv;
+            dv4[e] = (__bf16)(tacc[i][t][4 * q + e] * gp);
+          }
+          const int m = wm * (HC / 2) + i * 32 + 8 * q + 4 * lh;
+          *reinterpret_cast<mbf16x4*>(Gn + n * NSTR + m) = gv4;
+          *reinterpret_cast<mbf16x4*>(Zn + n * NSTR + m) = dv4;
+        }
+      }
+    __syncthreads();
+    // ---- copy-out: 8 pixels of one hidden row per lane (transposing read) -> 16-byte stores;
+    //      per-(tile, wave>>1) sums of dz for the b1 grad ----
+    {
+      float bacc = 0.f;
+#pragma unroll
+      for (int c = 0; c < CPW; ++c) {
+        const int pb = ((wave >> 1) * CPW + c) * 16;
+        const int off = (pb + 8 * lh + tq) * NSTR + chh + 16 * tG + 4 * tp;
+        const mbf16x8 gv = mtr_frag(Gn + off, NSTR);
+        const mbf16x8 dv = mtr_frag(Zn + off, NSTR);
+        const long o = gbase + (long)(j * HC + chh + lr) * g.HW + pb + 8 * lh;
+        *reinterpret_cast<mbf16x8*>(g.g_out + o) = gv;
+        *reinterpret_cast<mbf16x8*>(g.dz_out + o) = dv;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) bacc += (float)dv[e];
+      }
+      bacc += __shfl_xor(bacc, 32, 64);
+      if (lh == 0) g.bsum[((long)tile * (NW / 2) + (wave >> 1)) * C4 + j * HC + chh + lr] = bacc;
+    }
+    // ---- dh += W1[chunk]^T dz ----
+#pragma unroll
+    for (int ks = 0; ks < HC / 16; ++ks) {
+      mbf16x8 af[HG::TM], bf[HG::TN];
+#pragma unroll
+      for (int i = 0; i < HG::TM; ++i)   // A[c][m] = W1[m][c]: W1s [HC][W1STR] is k-major here
+        af[i] = mtr_frag(W1s + (ks * 16 + 8 * lh + tq) * W1STR + wm * (C / 2) + i * 32 + 16 * tG + 4 * tp, W1STR);
+#pragma unroll
+      for (int t = 0; t < HG::TN; ++t)
+        bf[t] = *reinterpret_cast<const mbf16x8*>(Zn + (wn * (BN / HG::WN) + t * 32 + lr) * NSTR + ks * 16 + lh * 8);
+#pragma unroll
+      for (int i = 0; i < HG::TM; ++i)
+#pragma unroll
+        for (int t = 0; t < HG::TN; ++t)
+          hacc[i][t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bf[t], hacc[i][t], 0, 0, 0);
+    }
+    __syncthreads();
+    if (j + 1 < NCH) {
+      wch_store<C, P, HC, NT, W1STR, W2STR>(wr1, wr2, W1s, W2s, tid);
+      __syncthreads();
+    }
+  }
+
+  float* ob = g.out + (long)img * g.out_bs + p0;
+#pragma unroll
+  for (int i = 0; i < HG::TM; ++i)
+#pragma unroll
+    for (int t = 0; t < HG::TN; ++t) {
+      const int n = wn * (BN / HG::WN) + t * 32 + lr;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int c = wm * (C / 2) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+        ob[(long)c * g.HW + n] = hacc[i][t][r];
+      }
+    }
+}
+
+// out[c] += sum_r part[r][c]: block (column group of 64, row group of 64 * 4)
+__global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ part, int rows, int cols,
+                                                     float* __restrict__ out) {
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int q = threadIdx.x >> 6;
+  const int r0 = blockIdx.y * 256, r1 = min(rows, r0 + 256);
+  __shared__ float sh[4][64];
+  float acc = 0.f;
+  if (c < cols)
+    for (int r = r0 + q; r < r1; r += 4) acc += part[(long)r * cols + c];
+  sh[q][threadIdx.x & 63] = acc;
+  __syncthreads();
+  if (q == 0 && c < cols)
+    atomicAdd(out + c, sh[0][threadIdx.x] + sh[1][threadIdx.x] + sh[2][threadIdx.x] + sh[3][threadIdx.x]);
+}
+
+__global__ __launch_bounds__(256) void f32_to_bf16_kernel(const float* __restrict__ s, __bf16* __restrict__ d, long n) {
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) d[i] = (__bf16)s[i];
+}
+
+// Supported (C, P) -> pixel tile (forward and backward use the same BN); HC = 64, 8 waves.
+static int mlp_bn(int C, int P) {
+  if ((C == 64 && P == 128) || (C == 128 && P == 64) || (C == 128 && P == 256) || (C == 256 && P == 128)) return 128;
+  return 0;
+}
+constexpr int MLP_NW = 8;
+
+template <int C, int P, int BN, int MINB>
+static void fwd_launch(const MlpArgs& g, hipStream_t st) {
+  const unsigned tiles = (unsigned)((long)g.nb * (g.HW / BN));
+  hipLaunchKernelGGL((mlp_fwd_kernel<C, P, BN, 64, MLP_NW, MINB>), dim3(tiles), dim3(MLP_NW * 64), 0, st, g);
+}
+// backward: 8 waves x 128 pixels where the LDS tiles fit, else 4 waves x 64 pixels (same bsum
+// granularity: one partial row per 32 pixels)
+template <int C, int P, int BN, int NW>
+static void bwd_launch(const MlpArgs& g, hipStream_t st) {
+  static_assert(BN / (NW / 2) == 32, "bsum granularity");
+  const unsigned tiles = (unsigned)((long)g.nb * (g.HW / BN));
+  hipLaunchKernelGGL((mlp_bwd_kernel<C, P, BN, 64, NW>), dim3(tiles), dim3(NW * 64), 0, st, g);
+}
+
+}  // namespace dsg
+
+using namespace dsg;
+
+extern "C" {
+
+// 0 if the fused kernels do not take (C, P, HW), else the number of bsum partial rows per
+// image pixel: bsum has nb * HW / return rows (one per 32-pixel group of a tile x wave pair).
+int dsgan_mlp_supported(int C, int P, int HW) {
+  const int bn = mlp_bn(C, P);
+  if (bn == 0 || HW % bn != 0) return 0;
+  return 32;
+}
+
+int dsgan_mlp_fwd(const float* h, long h_bs, const void* w1, const float* b1, const void* w2,
+                  const float* b2, float* out, long out_bs, int nb, int C, int P, int HW,
+                  int accumulate, hipStream_t st) {
+  DSG_REQUIRE(h && w1 && b1 && w2 && out && nb > 0, "dsgan_mlp_fwd: bad args");
+  DSG_REQUIRE(dsgan_mlp_supported(C, P, HW), "dsgan_mlp_fwd: unsupported shape C=%d P=%d HW=%d", C, P, HW);
+  DSG_REQUIRE(((uintptr_t)h & 15) == 0 && (h_bs & 3) == 0 && ((uintptr_t)w1 & 15) == 0 && ((uintptr_t)w2 & 15) == 0,
+              "dsgan_mlp_fwd: operands must be 16-byte aligned");
+  MlpArgs g{};
+  g.h = h; g.h_bs = h_bs; g.w1 = (const __bf16*)w1; g.b1 = b1; g.w2 = (const __bf16*)w2; g.b2 = b2;
+  g.out = out; g.out_bs = out_bs; g.HW = HW; g.nb = nb; g.accumulate = accumulate;
+  if (C == 64) fwd_launch<64, 128, 128, 2>(g, st);
+  else if (C == 128 && P == 64) fwd_launch<128, 64, 128, 2>(g, st);
+  else if (C == 128) fwd_launch<128, 256, 128, 1>(g, st);
+  else fwd_launch<256, 128, 128, 1>(g, st);
+  DSG_CHECK_LAUNCH();
+  return 0;
+}
+
+int dsgan_mlp_bwd(const float* h, long h_bs, const float* dy, long dy_bs, const void* w1, const float* b1,
+                  const void* w2, float* dh, long dh_bs, void* g_out, void* dz_out, float* bsum, int nb,
+                  int C, int P, int HW, hipStream_t st) {
+  DSG_REQUIRE(h && dy && w1 && b1 && w2 && dh && g_out && dz_out && bsum && nb > 0, "dsgan_mlp_bwd: bad args");
+  DSG_REQUIRE(dsgan_mlp_supported(C, P, HW), "dsgan_mlp_bwd: unsupported shape C=%d P=%d HW=%d", C, P, HW);
+  DSG_REQUIRE(((uintptr_t)h & 15) == 0 && ((uintptr_t)dy & 15) == 0 && (h_bs & 3) == 0 && (dy_bs & 3) == 0 &&
+              ((uintptr_t)g_out & 15) == 0 && ((uintptr_t)dz_out & 15) == 0,
+              "dsgan_mlp_bwd: operands must be 16-byte aligned");
+  MlpArgs g{};
+  g.h = h; g.h_bs = h_bs; g.dy = dy; g.dy_bs = dy_bs; g.w1 = (const __bf16*)w1; g.b1 = b1;
+  g.w2 = (const __bf16*)w2; g.out = dh; g.out_bs = dh_bs; g.g_out = (__bf16*)g_out;
+  g.dz_out = (__bf16*)dz_out; g.bsum = bsum; g.HW = HW; g.nb = nb;
+  if (C == 64) bwd_launch<64, 128, 128, 8>(g, st);
+  else if (C == 128 && P == 64) bwd_launch<128, 64, 128, 8>(g, st);
+  else if (C == 128) bwd_launch<128, 256, 64, 4>(g, st);
+  else bwd_launch<256, 128, 64, 4>(g, st);
+  DSG_CHECK_LAUNCH();
+  return 0;
+}
+
+int dsgan_colsum(const float* part, int rows, int cols, float* out, hipStream_t st) {
+  DSG_REQUIRE(part && out && rows > 0 && cols > 0, "dsgan_colsum: bad args");
+  hipLaunchKernelGGL(colsum_kernel, dim3(cdiv(cols, 64), cdiv(rows, 256)), dim3(256), 0, st, part, rows, cols, out);
+  DSG_CHECK_LAUNCH();
+  return 0;
+}
+
+int dsgan_f32_to_bf16(const float* src, void* dst, long n, hipStream_t st) {
+  DSG_REQUIRE(src && dst && n > 0, "dsgan_f32_to_bf16: bad args");
+  long blocks = (n + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(f32_to_bf16_kernel, dim3((unsigned)blocks), dim3(256), 0, st, src, (__bf16*)dst, n);
+  DSG_CHECK_LAUNCH();
+  return 0;
+}
+
+}  // extern "C"

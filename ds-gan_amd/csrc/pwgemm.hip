@@ -26,6 +26,7 @@ typedef __attribute__((ext_vector_type(4))) __bf16 pbf16x4;
 typedef __attribute__((ext_vector_type(16))) float pf32x16;
 typedef __attribute__((ext_vector_type(4))) short s16x4;
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+typedef __attribute__((ext_vector_type(4))) unsigned int pu32x4;   // 16 raw bytes (8 bf16)
 
 enum PwMode : int { PW_FWD = 0, PW_DGRAD = 1, PW_WGRAD = 2 };
 
@@ -68,8 +69,11 @@ __device__ __forceinline__ pbf16x4 cvt4(float4 v, int bact, float slope) {
   return r;
 }
 
-template <int MODE, int BM>
+// ABF / BBF (WGRAD only): the A (dy) / B (x) operand is bf16 in HBM -- the gelu(z) and dz
+// tensors written by the fused MLP backward (mlp.hip) -- and is copied to LDS unconverted.
+template <int MODE, int BM, int ABF = 0, int BBF = 0>
 __global__ __launch_bounds__(256, 2) void pwgemm_kernel(PwArgs g) {
+  static_assert(MODE == PW_WGRAD || (ABF == 0 && BBF == 0), "bf16 operands: WGRAD only");
   constexpr int BN = 128;
   constexpr int WM = 2, WN = 2;
   constexpr int TM = BM / WM / 32, TN = BN / WN / 32;
@@ -114,9 +118,10 @@ __global__ __launch_bounds__(256, 2) void pwgemm_kernel(PwArgs g) {
   // ---- staging maps ----
   // row-major tiles: item = (row, c4) with c4 in [0,8): 8 float4 per 32-k row
   // k-major tiles  : item = (k, c4) with c4 in [0, C/4)
-  constexpr int A_ITEMS = (A_KMAJ ? PBK * BM / 4 : BM * 8) / 256;
-  constexpr int B_ITEMS = (B_KMAJ ? PBK * BN / 4 : BN * 8) / 256;
-  float4 ra[A_ITEMS], rb[B_ITEMS];
+  constexpr int A_ITEMS = ABF ? BM * 4 / 256 : (A_KMAJ ? PBK * BM / 4 : BM * 8) / 256;
+  constexpr int B_ITEMS = BBF ? BN * 4 / 256 : (B_KMAJ ? PBK * BN / 4 : BN * 8) / 256;
+  float4 ra[ABF ? 1 : A_ITEMS], rb[BBF ? 1 : B_ITEMS];
+  pu32x4 rha[ABF ? A_ITEMS : 1], rhb[BBF ? B_ITEMS : 1];
 
   // Operand loads are 16-byte buffer loads: an element outside its tensor gets the offset
   // PW_OOB, past every resource range, and reads 0 in hardware -- no branch, no mask VALU.
@@ -129,6 +134,9 @@ __global__ __launch_bounds__(256, 2) void pwgemm_kernel(PwArgs g) {
       (void*)(g.B + (long)b_fix * g.b_bs), (short)0, g.b_range, 0x00020000);
   auto bld4 = [](__amdgpu_buffer_rsrc_t r, unsigned voff) {
     return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)voff, 0, 0));
+  };
+  auto bldh = [](__amdgpu_buffer_rsrc_t r, unsigned voff) {
+    return __builtin_bit_cast(pu32x4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)voff, 0, 0));
   };
 
   auto gload = [&](int kt) {
@@ -143,6 +151,15 @@ __global__ __launch_bounds__(256, 2) void pwgemm_kernel(PwArgs g) {
     // WGRAD: a 32-pixel K step lies inside one image (P % 32 == 0): image index is uniform
     const unsigned bw = (MODE == PW_WGRAD) ? (unsigned)(kb / g.P) : 0u;
     const unsigned pw = (MODE == PW_WGRAD) ? (unsigned)(kb - (int)bw * g.P) : 0u;
+    if constexpr (ABF) {                         // DY[b][M][P] bf16, row m, 8 pixels per item
+#pragma unroll
+      for (int i = 0; i < A_ITEMS; ++i) {
+        const int it = tid + i * 256;
+        const int m = m0 + (it >> 2);
+        const unsigned off = (m < g.M) ? (bw * (unsigned)g.a_bs + (unsigned)m * g.P + pw + (it & 3) * 8) * 2u : PW_OOB;
+        rha[i] = bldh(rA, off);
+      }
+    } else
 #pragma unroll
     for (int i = 0; i < A_ITEMS; ++i) {
       const int it = tid + i * 256;
@@ -159,6 +176,15 @@ __global__ __launch_bounds__(256, 2) void pwgemm_kernel(PwArgs g) {
       }
       ra[i] = bld4(rA, off);
     }
+    if constexpr (BBF) {                         // X[b][N][P] bf16, row n
+#pragma unroll
+      for (int i = 0; i < B_ITEMS; ++i) {
+        const int it = tid + i * 256;
+        const int n = n0 + (it >> 2);
+        const unsigned off = (n < g.N) ? (bw * (unsigned)g.b_bs + (unsigned)n * g.P + pw + (it & 3) * 8) * 2u : PW_OOB;
+        rhb[i] = bldh(rB, off);
+      }
+    } else
 #pragma unroll
     for (int i = 0; i < B_ITEMS; ++i) {
       const int it = tid + i * 256;
@@ -176,6 +202,13 @@ __global__ __launch_bounds__(256, 2) void pwgemm_kernel(PwArgs g) {
   auto sstore = [&](int buf) {
     __bf16* As = smem + buf * (A_SZ + B_SZ);
     __bf16* Bs = As + A_SZ;
+    if constexpr (ABF) {
+#pragma unroll
+      for (int i = 0; i < A_ITEMS; ++i) {
+        const int it = tid + i * 256;
+        *reinterpret_cast<pu32x4*>(As + (it >> 2) * A_STR + (it & 3) * 8) = rha[i];
+      }
+    } else
 #pragma unroll
     for (int i = 0; i < A_ITEMS; ++i) {
       const int it = tid + i * 256;
@@ -194,6 +227,14 @@ __global__ __launch_bounds__(256, 2) void pwgemm_kernel(PwArgs g) {
         *reinterpret_cast<pbf16x4*>(Bs + off) = cv(rb[i]);
       }
     };
+    if constexpr (BBF) {
+#pragma unroll
+      for (int i = 0; i < B_ITEMS; ++i) {
+        const int it = tid + i * 256;
+        *reinterpret_cast<pu32x4*>(Bs + (it >> 2) * B_STR + (it & 3) * 8) = rhb[i];
+      }
+      return;
+    }
     // activation-on-load switch hoisted out of the element loop (uniform)
     if (g.bact == ACT_NONE) bstore([](float4 v) { return cvt4(v, 0, 0.f); });
     else if (g.bact == ACT_GELU)
@@ -345,11 +386,25 @@ __global__ __launch_bounds__(256, 2) void pwgemm_kernel(PwArgs g) {
   }
 }
 
-template <int MODE, int BM>
+template <int MODE, int BM, int ABF = 0, int BBF = 0>
 static void pw_launch(const PwArgs& g, int splits, hipStream_t st) {
   const int mt = (g.M + BM - 1) / BM;
   const int nt = (MODE == PW_WGRAD) ? (g.N + 127) / 128 : g.N / 128;
-  hipLaunchKernelGGL((pwgemm_kernel<MODE, BM>), dim3((unsigned)((long)mt * nt * splits)), dim3(256), 0, st, g);
+  hipLaunchKernelGGL((pwgemm_kernel<MODE, BM, ABF, BBF>), dim3((unsigned)((long)mt * nt * splits)), dim3(256), 0, st, g);
+}
+
+// K split of a weight-grad launch: enough workgroups to fill the chip, >= 8 K steps each.
+static int wgrad_split(PwArgs& g, int BM) {
+  const long tiles = (long)((g.M + BM - 1) / BM) * ((g.N + 127) / 128);
+  long splits = (2048 + tiles - 1) / tiles;
+  const long max_splits = (g.K + 8L * PBK - 1) / (8L * PBK);
+  if (splits > max_splits) splits = max_splits;
+  if (splits < 1) splits = 1;
+  long ks = (g.K + splits - 1) / splits;
+  ks = (ks + PBK - 1) / PBK * PBK;
+  splits = (g.K + ks - 1) / ks;
+  g.k_split = (int)ks;
+  return (int)splits;
 }
 
 static bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
@@ -397,17 +452,9 @@ extern "C" int dsgan_pw_gemm(int mode, const float* A, long a_bs, const float* B
     DSG_REQUIRE(dsgan_pw_supported(mode, M, K, P, a_bs, b_bs, A, B), "dsgan_pw_gemm: unsupported WGRAD shape");
     g.M = M; g.N = N; g.K = nb * P;
     const int BM = M > 64 ? 128 : 64;
-    const long tiles = (long)((M + BM - 1) / BM) * ((N + 127) / 128);
-    long splits = (2048 + tiles - 1) / tiles;
-    const long max_splits = (g.K + 8L * PBK - 1) / (8L * PBK);
-    if (splits > max_splits) splits = max_splits;
-    if (splits < 1) splits = 1;
-    long ks = (g.K + splits - 1) / splits;
-    ks = (ks + PBK - 1) / PBK * PBK;
-    splits = (g.K + ks - 1) / ks;
-    g.k_split = (int)ks;
-    if (BM == 128) pw_launch<PW_WGRAD, 128>(g, (int)splits, st);
-    else pw_launch<PW_WGRAD, 64>(g, (int)splits, st);
+    const int splits = wgrad_split(g, BM);
+    if (BM == 128) pw_launch<PW_WGRAD, 128>(g, splits, st);
+    else pw_launch<PW_WGRAD, 64>(g, splits, st);
   } else {
     DSG_REQUIRE(dsgan_pw_supported(mode, M, K, P, a_bs, b_bs, A, B), "dsgan_pw_gemm: unsupported shape");
     DSG_REQUIRE((long)M * P * 4 < (1L << 32), "dsgan_pw_gemm: M*P too large for a buffer resource");
@@ -418,6 +465,37 @@ extern "C" int dsgan_pw_gemm(int mode, const float* A, long a_bs, const float* B
     const bool big = M > 64;
     if (mode == PW_FWD) { if (big) pw_launch<PW_FWD, 128>(g, 1, st); else pw_launch<PW_FWD, 64>(g, 1, st); }
     else { if (big) pw_launch<PW_DGRAD, 128>(g, 1, st); else pw_launch<PW_DGRAD, 64>(g, 1, st); }
+  }
+  DSG_CHECK_LAUNCH();
+  return 0;
+}
+
+// Weight-grad with bf16 operand(s): DW[M][N] += sum_{b,p} A[b][M][P] * B[b][N][P], A/B fp32 or
+// bf16 (a_bf16 / b_bf16).  P % 32 == 0, 16-byte aligned operands.
+extern "C" int dsgan_pw_wgrad_mixed(const void* A, long a_bs, int a_bf16, const void* B, long b_bs,
+                                    int b_bf16, float* DW, int M, int N, int P, int nb, hipStream_t st) {
+  DSG_REQUIRE(A && B && DW && M >= 16 && N > 0 && P > 0 && nb > 0, "dsgan_pw_wgrad_mixed: bad args");
+  DSG_REQUIRE(P % 32 == 0 && al16(A) && al16(B) && (a_bs & 7) == 0 && (b_bs & 7) == 0,
+              "dsgan_pw_wgrad_mixed: P %% 32 and 16-byte alignment required");
+  PwArgs g{};
+  g.A = (const float*)A; g.a_bs = a_bs; g.B = (const float*)B; g.b_bs = b_bs; g.Y = DW; g.P = P;
+  const long ar = ((long)(nb - 1) * a_bs + (long)M * P) * (a_bf16 ? 2 : 4);
+  const long br = ((long)(nb - 1) * b_bs + (long)N * P) * (b_bf16 ? 2 : 4);
+  DSG_REQUIRE(ar < (long)PW_OOB && br < (long)PW_OOB, "dsgan_pw_wgrad_mixed: operands exceed 4 GiB buffer range");
+  g.a_range = (unsigned)ar; g.b_range = (unsigned)br;
+  g.M = M; g.N = N; g.K = nb * P;
+  const int BM = M > 64 ? 128 : 64;
+  const int splits = wgrad_split(g, BM);
+  const int sel = (a_bf16 ? 2 : 0) + (b_bf16 ? 1 : 0) + (BM == 128 ? 4 : 0);
+  switch (sel) {
+    case 0: pw_launch<PW_WGRAD, 64, 0, 0>(g, splits, st); break;
+    case 1: pw_launch<PW_WGRAD, 64, 0, 1>(g, splits, st); break;
+    case 2: pw_launch<PW_WGRAD, 64, 1, 0>(g, splits, st); break;
+    case 3: pw_launch<PW_WGRAD, 64, 1, 1>(g, splits, st); break;
+    case 4: pw_launch<PW_WGRAD, 128, 0, 0>(g, splits, st); break;
+    case 5: pw_launch<PW_WGRAD, 128, 0, 1>(g, splits, st); break;
+    case 6: pw_launch<PW_WGRAD, 128, 1, 0>(g, splits, st); break;
+    default: pw_launch<PW_WGRAD, 128, 1, 1>(g, splits, st); break;
   }
   DSG_CHECK_LAUNCH();
   return 0;

@@ -28,6 +28,13 @@ SIGNATURES = {
     # pwgemm.hip
     "dsgan_pw_supported": [I, I, I, I, L, L, P, P],
     "dsgan_pw_gemm": [I, P, L, P, L, P, L, P, P, L, P, L, I, I, I, I, I, I, I, I, I, F, S],
+    "dsgan_pw_wgrad_mixed": [P, L, I, P, L, I, P, I, I, I, I, S],
+    # mlp.hip
+    "dsgan_mlp_supported": [I, I, I],
+    "dsgan_mlp_fwd": [P, L, P, P, P, P, P, L, I, I, I, I, I, S],
+    "dsgan_mlp_bwd": [P, L, P, L, P, P, P, P, L, P, P, P, I, I, I, I, S],
+    "dsgan_colsum": [P, I, I, P, S],
+    "dsgan_f32_to_bf16": [P, P, L, S],
     # tconv.hip
     "dsgan_conv_wtrans": [P, P, I, I, I, I, I, I, I, I, I, S],
     "dsgan_tconv": [P, L, P, P, P, L, P, L] + [I] * 9 + [P, P] + [I] * 7 + [F, S],

@@ -375,25 +375,75 @@ def conv_transpose3s2(x, w, b):
 # backward: the dgrad of W2 multiplies by gelu'(z) in its epilogue (no standalone GELU pass).
 # ------------------------------------------------------------------------------------------
 
+_BF16_CACHE = {}
+
+
+def bf16_weight(w):
+    """bf16 copy of a parameter for the fused kernels, cached like _wtrans (same invalidation)."""
+    key = (id(w), w.data_ptr(), tuple(w.shape))
+    ent = _BF16_CACHE.get(key)
+    gen = WEIGHT_GEN[0]
+    if ent is not None and ent[0] == gen and ent[1] == w._version and ent[2] is w:
+        return ent[3]
+    out = torch.empty(w.shape, device=w.device, dtype=torch.bfloat16)
+    call("dsgan_f32_to_bf16", ptr(w), ptr(out), w.numel(), stream())
+    if len(_BF16_CACHE) > 512:
+        _BF16_CACHE.clear()
+    _BF16_CACHE[key] = (gen, w._version, w, out)
+    return out
+
+
+def _mlp_tile(h, x, P):
+    """Pixels per b1-grad partial row of the fused MLP kernels (mlp.hip), 0 if unsupported."""
+    if _state["prec"] != "bf16":
+        return 0
+    N, C, H, W = h.shape
+    if h.data_ptr() % 16 or x.data_ptr() % 16:
+        return 0
+    return int(_lib.load().dsgan_mlp_supported(C, P, H * W))
+
+
+def _mlp_flops(N, C, P, HW):
+    # algorithmic MACs of the two Linear layers (fwd; each of dgrad/wgrad is the same count)
+    return 2.0 * N * HW * (4 * C * C + 4 * C * P)
+
+
 class PwMlpFn(torch.autograd.Function):
-    """Only the pre-GELU hidden z [N,4C,H,W] is materialised: pwconv2 and its weight-grad read
-    gelu(z) through the GEMM's activation-on-load, and the data-grad of pwconv2 multiplies by
-    gelu'(z) in its epilogue -- the 4C-channel g = gelu(z) never touches HBM."""
+    """Block tail.  bf16 mode on the fused shapes (mlp.hip): forward out = Ws x (pwgemm) then
+    out += W2 gelu(W1 h + b1) + b2 in one kernel -- z is never stored; backward recomputes z
+    and writes only bf16 gelu(z) and dz for the two weight-grads.  Otherwise (fp32 parity mode,
+    other shapes) only the pre-GELU hidden z [N,4C,H,W] is materialised: pwconv2 and its
+    weight-grad read gelu(z) through the GEMM's activation-on-load, and the data-grad of pwconv2
+    multiplies by gelu'(z) in its epilogue."""
 
     @staticmethod
     def forward(ctx, h, x, w1, b1, w2, b2, ws):
         N, C, H, W = h.shape
+        P = w2.shape[0]
+        h, hbs = nchw(h)
+        tile = _mlp_tile(h, x, P)
+        ctx.refs = (w1, b1, w2, b2, ws)
+        ctx.tile = tile
+        if tile:
+            out = conv_fwd_raw(x, ws, None, 1, 0)
+            e0 = IGEMM_TIMER.begin()
+            call("dsgan_mlp_fwd", ptr(h), hbs, ptr(bf16_weight(w1)), ptr(b1), ptr(bf16_weight(w2)), ptr(b2),
+                 ptr(out), P * H * W, N, C, P, H * W, 1, stream())
+            IGEMM_TIMER.end(e0, _mlp_flops(N, C, P, H * W), ("mlp_fwd", N, C, H, W, P, 1, 1))
+            ctx.save_for_backward(h, x, ws)
+            return out
         w1v = w1.view(w1.shape[0], w1.shape[1], 1, 1)
         w2v = w2.view(w2.shape[0], w2.shape[1], 1, 1)
         z = conv_fwd_raw(h, w1v, b1, 1, 0)
         out = conv_fwd_raw(x, ws, None, 1, 0)
         conv_fwd_raw(z, w2v, b2, 1, 0, out=out, accumulate=True, xact="gelu")
         ctx.save_for_backward(h, x, z, w1v, w2v, ws)
-        ctx.refs = (w1, b1, w2, b2, ws)
         return out
 
     @staticmethod
     def backward(ctx, dy):
+        if ctx.tile:
+            return PwMlpFn._backward_fused(ctx, dy)
         h, x, z, w1v, w2v, ws = ctx.saved_tensors
         w1, b1, w2, b2, ws_ref = ctx.refs
         dy = dy.contiguous()
@@ -412,6 +462,42 @@ class PwMlpFn(torch.autograd.Function):
         if gb1 is not None:
             channel_sum_raw(dz, gb1)
         dh = conv_dgrad_raw(dz, w1v, tuple(h.shape), 1, 0) if ctx.needs_input_grad[0] else None
+        dx = conv_dgrad_raw(dy, ws, tuple(x.shape), 1, 0) if ctx.needs_input_grad[1] else None
+        return dh, dx, None, None, None, None, None
+
+    @staticmethod
+    def _backward_fused(ctx, dy):
+        h, x, ws = ctx.saved_tensors
+        w1, b1, w2, b2, ws_ref = ctx.refs
+        N, C, H, W = h.shape
+        HW, C4, P = H * W, 4 * h.shape[1], w2.shape[0]
+        dy, dybs = nchw(dy)
+        if dy.data_ptr() % 16:
+            dy, dybs = dy.contiguous(), P * HW
+        ntiles = N * HW // ctx.tile
+        g = torch.empty((N, C4, H, W), device=h.device, dtype=torch.bfloat16)
+        dz = torch.empty_like(g)
+        bsum = torch.empty((ntiles, C4), device=h.device, dtype=torch.float32)
+        dh = _empty(N, C, H, W, h)
+        e0 = IGEMM_TIMER.begin()
+        call("dsgan_mlp_bwd", ptr(h), C * HW, ptr(dy), dybs, ptr(bf16_weight(w1)), ptr(b1), ptr(bf16_weight(w2)),
+             ptr(dh), C * HW, ptr(g), ptr(dz), ptr(bsum), N, C, P, HW, stream())
+        IGEMM_TIMER.end(e0, _mlp_flops(N, C, P, HW), ("mlp_bwd", N, C, H, W, P, 1, 1))
+        gw2, gb2, gws, gw1, gb1 = (_grad_buf(t) for t in (w2, b2, ws_ref, w1, b1))
+        if gw2 is not None:
+            e0 = IGEMM_TIMER.begin()
+            call("dsgan_pw_wgrad_mixed", ptr(dy), dybs, 0, ptr(g), C4 * HW, 1, ptr(gw2), P, C4, HW, N, stream())
+            IGEMM_TIMER.end(e0, 2.0 * N * HW * C4 * P, ("wgrad", N, C4, H, W, P, 1, 1))
+        if gb2 is not None:
+            channel_sum_raw(dy, gb2)
+        if gws is not None:
+            conv_wgrad_raw(dy, x, gws, 1, 0)
+        if gw1 is not None:
+            e0 = IGEMM_TIMER.begin()
+            call("dsgan_pw_wgrad_mixed", ptr(dz), C4 * HW, 1, ptr(h), C * HW, 0, ptr(gw1), C4, C, HW, N, stream())
+            IGEMM_TIMER.end(e0, 2.0 * N * HW * C4 * C, ("wgrad", N, C, H, W, C4, 1, 1))
+        if gb1 is not None:
+            call("dsgan_colsum", ptr(bsum), ntiles, C4, ptr(gb1), stream())
         dx = conv_dgrad_raw(dy, ws, tuple(x.shape), 1, 0) if ctx.needs_input_grad[1] else None
         return dh, dx, None, None, None, None, None
 

@@ -71,6 +71,32 @@ int dsgan_pw_gemm(int mode, const float* A, long a_bs, const float* B, long b_bs
                   long gpre_bs, int M, int N, int K, int P, int nb, int act, int gact, int bact,
                   int accumulate, float slope, hipStream_t stream);
 
+/* Weight-grad with bf16 operand(s) (pwgemm.hip): DW[M][N] += sum_{b,p} A[b][M][p] * B[b][N][p];
+ * a_bf16 / b_bf16 select bf16 storage (the fused MLP backward's gelu(z) and dz).  P % 32 == 0. */
+int dsgan_pw_wgrad_mixed(const void* A, long a_bs, int a_bf16, const void* B, long b_bs, int b_bf16,
+                         float* dw, int M, int N, int P, int nb, hipStream_t stream);
+
+/* ---- fused ConvNeXt MLP (mlp.hip), replaces Block.pwconv1 -> GELU -> pwconv2 -------------------
+ * DSGAN/models/model/MixConvNeXtML.py:221-223,236-240 (nn.Linear(C,4C) + GELU + nn.Linear(4C,P) on
+ * the NHWC permute of the InstanceNorm output).  bf16 MFMA, fp32 accumulation, hidden kept on chip.
+ * dsgan_mlp_supported: 0 if (C, P, HW) has no fused kernel, else the backward pixel tile BN
+ *   (the bsum partials buffer has nb*HW/BN rows of 4C floats).
+ * dsgan_mlp_fwd: out[b][p][n] (+)= b2[p] + sum_m w2[p][m] gelu(b1[m] + sum_c w1[m][c] h[b][c][n]);
+ *   w1 [4C][C], w2 [P][4C] bf16 copies of the Linear weights.
+ * dsgan_mlp_bwd: recomputes z, writes dh (fp32), gelu(z) and dz (bf16 [nb][4C][HW]), and per-tile
+ *   row sums of dz (bsum) for the pwconv1 bias grad (reduce with dsgan_colsum). */
+int dsgan_mlp_supported(int C, int P, int HW);
+int dsgan_mlp_fwd(const float* h, long h_bs, const void* w1, const float* b1, const void* w2,
+                  const float* b2, float* out, long out_bs, int nb, int C, int P, int HW,
+                  int accumulate, hipStream_t stream);
+int dsgan_mlp_bwd(const float* h, long h_bs, const float* dy, long dy_bs, const void* w1,
+                  const float* b1, const void* w2, float* dh, long dh_bs, void* g_out, void* dz_out,
+                  float* bsum, int nb, int C, int P, int HW, hipStream_t stream);
+/* out[c] += sum_r part[r][c] */
+int dsgan_colsum(const float* part, int rows, int cols, float* out, hipStream_t stream);
+/* dst (bf16) = src (fp32), round to nearest even */
+int dsgan_f32_to_bf16(const float* src, void* dst, long n, hipStream_t stream);
+
 /* ---- direct convs for <= 8 channels on one side (skinny.hip) -----------------------------------
  * dsgan_conv_small_out: out[b][m][oh][ow] (+)= bias[m] + sum_{k,kh,kw} w(m,k,kh,kw) * in(b,k,tap),
  *   M <= 8; w(m,k,kh,kw) = w[m*wm + k*wk + kh*wh + kw*ww] (element strides, may be negative).

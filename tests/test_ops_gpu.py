@@ -149,6 +149,40 @@ def test_pw_mlp(prec, N, C, H, P):
         assert rel(pd.grad, pr.grad) < 2 * tol
 
 
+@pytest.mark.parametrize("N,C,H,P", [(2, 64, 16, 128), (2, 128, 16, 64), (3, 128, 16, 256), (2, 256, 16, 128),
+                                     (1, 128, 32, 64)])
+def test_pw_mlp_fused(N, C, H, P):
+    """bf16 fused MLP kernels (mlp.hip) at every (C, P) they take: forward without the hidden z,
+    backward recomputing z and feeding bf16 gelu(z)/dz to the weight-grads."""
+    from dsgan_hip import functional as HF, _lib
+    HF.set_precision("bf16")
+    assert _lib.load().dsgan_mlp_supported(C, P, H * H) > 0
+    g = torch.Generator().manual_seed(7 * C + P)
+    h = _q(torch.randn(N, C, H, H, generator=g), "bf16")
+    x = _q(torch.randn(N, C, H, H, generator=g), "bf16")
+    w1 = _q(torch.randn(4 * C, C, generator=g) / math.sqrt(C), "bf16")
+    b1 = torch.randn(4 * C, generator=g) * 0.1
+    w2 = _q(torch.randn(P, 4 * C, generator=g) / math.sqrt(4 * C), "bf16")
+    b2 = torch.randn(P, generator=g) * 0.1
+    ws = _q(torch.randn(P, C, 1, 1, generator=g) / math.sqrt(C), "bf16")
+    R = [t.clone().requires_grad_() for t in (h, x, w1, b1, w2, b2, ws)]
+    t = F.linear(R[0].permute(0, 2, 3, 1), R[2], R[3])
+    t = F.linear(F.gelu(t), R[4], R[5]).permute(0, 3, 1, 2)
+    y_ref = F.conv2d(R[1], R[6]) + t
+    gy = torch.randn(y_ref.shape, generator=g)
+    y_ref.backward(gy)
+    hd, xd = _leaf(h), _leaf(x)
+    P_ = [_param(t) for t in (w1, b1, w2, b2, ws)]
+    y = HF.pw_mlp(hd, xd, *P_)
+    y.backward(gy.to(DEV))
+    tol = TOL["bf16"]
+    assert rel(y, y_ref) < tol
+    assert rel(hd.grad, R[0].grad) < 2 * tol
+    assert rel(xd.grad, R[1].grad) < 2 * tol
+    for name, pd, pr in zip(("w1", "b1", "w2", "b2", "ws"), P_, R[2:]):
+        assert rel(pd.grad, pr.grad) < 2 * tol, name
+
+
 @pytest.mark.parametrize("K", [3, 5, 7, 9])
 @pytest.mark.parametrize("N,C,H,W", [(2, 4, 16, 16), (2, 3, 40, 37), (1, 2, 4, 4), (2, 8, 70, 65)])
 def test_dwconv(K, N, C, H, W):

@@ -1,0 +1,11 @@
+# Parity tests (optionally filtered: $1 = -k expression), then one bench line.
+set -o pipefail
+mkdir -p gpurun_out
+K=${1:-}
+if [ -n "$K" ]; then
+  timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -k "$K" > gpurun_out/t.log 2>&1; rc=$?
+else
+  timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/t.log 2>&1; rc=$?
+fi
+tail -15 gpurun_out/t.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python bench.py --steps 10 --warmup 3 --no-cpu-baseline > gpurun_out/bench.log 2>&1; rc=$?; tail -1 gpurun_out/bench.log; [ $rc -eq 0 ] || exit $rc
