@@ -23,6 +23,10 @@ FLAGS = ["-O3", "-fPIC", "-std=c++17", "--offload-arch=" + ARCH, "-munsafe-fp-at
          "-Wno-unused-result", "-I" + CSRC]
 
 
+# per-source extra flags
+EXTRA = {"dwconv.hip": ["-fno-slp-vectorize"]}
+
+
 def _newer(src, obj, headers):
     if not os.path.exists(obj):
         return True
@@ -31,7 +35,7 @@ def _newer(src, obj, headers):
 
 
 def _compile(src, obj):
-    cmd = [HIPCC] + FLAGS + ["-c", src, "-o", obj]
+    cmd = [HIPCC] + FLAGS + EXTRA.get(os.path.basename(src), []) + ["-c", src, "-o", obj]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError("compile failed: %s\n%s\n%s" % (" ".join(cmd), r.stdout, r.stderr))

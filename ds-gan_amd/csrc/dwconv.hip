@@ -150,19 +150,249 @@ __global__ __launch_bounds__(256) void dwconv_wgrad_kernel(const float* __restri
   }
 }
 
+// ------------------------------------------------------------------------------------------
+// Register-blocked variants for W % 4 == 0 planes of width >= 32 (every DS-GAN plane but the
+// 16x16 bottleneck).  Thread (tx, ty) owns a 4-column x R-row output block; the workgroup tile
+// (4*TWT) x (R*THT) plus halo is staged as float4 rows with the LDS column origin 4 to the left
+// of the tile, so each input row of a thread's window is three ds_read_b128 and serves
+// up to R*4*K FMAs.  The per-plane weights are wave-uniform (scalar loads).
+// ------------------------------------------------------------------------------------------
+template <int K, int TWT, int THT, int R>
+struct DwTile {
+  static constexpr int TW = 4 * TWT, TH = R * THT, P = K / 2;
+  static constexpr int LW = TW + 8, LH = TH + K - 1, F4 = LW / 4;
+  static constexpr int OFF = 4 - P;      // LDS column of input (out col - P) for i = kw = 0
+  static_assert(TWT * THT == 256, "256 threads");
+};
+
+template <int K, int TWT, int THT, int R>
+__device__ __forceinline__ void dw_stage(float* tile, const float* __restrict__ xp, int H, int W, int th0, int tw0) {
+  using T = DwTile<K, TWT, THT, R>;
+  for (int i = threadIdx.x; i < T::LH * T::F4; i += 256) {
+    const int r = i / T::F4, q = i - r * T::F4;
+    const int ih = th0 - T::P + r, iw = tw0 - 4 + 4 * q;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if ((unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W)
+      v = *reinterpret_cast<const float4*>(xp + (long)ih * W + iw);
+    *reinterpret_cast<float4*>(tile + r * T::LW + 4 * q) = v;
+  }
+}
+
+__device__ __forceinline__ void dw_row(float (&v)[12], const float* row) {
+  *reinterpret_cast<float4*>(v) = *reinterpret_cast<const float4*>(row);
+  *reinterpret_cast<float4*>(v + 4) = *reinterpret_cast<const float4*>(row + 4);
+  *reinterpret_cast<float4*>(v + 8) = *reinterpret_cast<const float4*>(row + 8);
+}
+
+template <int K, int TWT, int THT, int R>
+__global__ __launch_bounds__(256, 4) void dwconv_fwd_v2(const float* __restrict__ x, long x_bs,
+                                                     const float* __restrict__ w,
+                                                     const float* __restrict__ bias,
+                                                     float* __restrict__ y, long y_bs, int C, int H,
+                                                     int W, int flip, int accumulate, int tiles_w) {
+  using T = DwTile<K, TWT, THT, R>;
+  __shared__ __attribute__((aligned(16))) float tile[T::LH][T::LW];
+  const int plane = blockIdx.y;
+  const int n = plane / C, c = plane - n * C;
+  const int th0 = (blockIdx.x / tiles_w) * T::TH, tw0 = (blockIdx.x % tiles_w) * T::TW;
+  dw_stage<K, TWT, THT, R>(&tile[0][0], x + (long)n * x_bs + (long)c * H * W, H, W, th0, tw0);
+  float wv[K * K];
+#pragma unroll
+  for (int i = 0; i < K * K; ++i) wv[i] = w[c * K * K + (flip ? K * K - 1 - i : i)];
+  const float b = bias ? bias[c] : 0.f;
+  const int tx = threadIdx.x % TWT, ty = threadIdx.x / TWT;
+  float acc[R][4];
+#pragma unroll
+  for (int s = 0; s < R; ++s)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) acc[s][i] = b;
+  __syncthreads();
+  // one input row in flight ahead of the FMAs; the scheduling barrier keeps the compiler from
+  // hoisting every row load of the unrolled loop (which costs occupancy or spills)
+  float cur[12], nxt[12];
+  dw_row(cur, &tile[R * ty][4 * tx]);
+#pragma unroll
+  for (int r = 0; r < R + K - 1; ++r) {
+    if (r + 1 < R + K - 1) dw_row(nxt, &tile[R * ty + r + 1][4 * tx]);
+#pragma unroll
+    for (int s = 0; s < R; ++s) {
+      const int kh = r - s;
+      if (kh < 0 || kh >= K) continue;
+#pragma unroll
+      for (int kw = 0; kw < K; ++kw)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc[s][i] = fmaf(wv[kh * K + kw], cur[i + kw + T::OFF], acc[s][i]);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int i = 0; i < 12; ++i) cur[i] = nxt[i];
+  }
+  float* yp = y + (long)n * y_bs + (long)c * H * W + tw0 + 4 * tx;
+#pragma unroll
+  for (int s = 0; s < R; ++s) {
+    const int oh = th0 + R * ty + s;
+    if (oh >= H) continue;
+    float4* o = reinterpret_cast<float4*>(yp + (long)oh * W);
+    float4 v = make_float4(acc[s][0], acc[s][1], acc[s][2], acc[s][3]);
+    if (accumulate) {
+      const float4 u = *o;
+      v.x += u.x; v.y += u.y; v.z += u.z; v.w += u.w;
+    }
+    *o = v;
+  }
+}
+
+// dw[c] += sum over (images [n0, n0+nper), tile) of the 7x7 (KxK) correlation of dy with x;
+// db[c] += sum dy.  The dy block of a thread stays in registers; partial sums are reduced over
+// the workgroup once, after all of its images.
+template <int K, int TWT, int THT, int R>
+__global__ __launch_bounds__(256, 4) void dwconv_wgrad_v2(const float* __restrict__ dy, long dy_bs,
+                                                       const float* __restrict__ x, long x_bs,
+                                                       float* __restrict__ dw, float* __restrict__ db,
+                                                       int N, int C, int H, int W, int tiles_w, int nper) {
+  using T = DwTile<K, TWT, THT, R>;
+  __shared__ __attribute__((aligned(16))) float tile[T::LH][T::LW];
+  __shared__ float red[4][K * K + 1];
+  const int c = blockIdx.y;
+  const int th0 = (blockIdx.x / tiles_w) * T::TH, tw0 = (blockIdx.x % tiles_w) * T::TW;
+  const int n0 = blockIdx.z * nper, n1 = min(N, n0 + nper);
+  const int tx = threadIdx.x % TWT, ty = threadIdx.x / TWT;
+  float acc[K * K];
+#pragma unroll
+  for (int i = 0; i < K * K; ++i) acc[i] = 0.f;
+  float bacc = 0.f;
+  for (int n = n0; n < n1; ++n) {
+    __syncthreads();
+    dw_stage<K, TWT, THT, R>(&tile[0][0], x + (long)n * x_bs + (long)c * H * W, H, W, th0, tw0);
+    float g[R][4];
+    const float* gp = dy + (long)n * dy_bs + (long)c * H * W + tw0 + 4 * tx;
+#pragma unroll
+    for (int s = 0; s < R; ++s) {
+      const int oh = th0 + R * ty + s;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (oh < H) v = *reinterpret_cast<const float4*>(gp + (long)oh * W);
+      g[s][0] = v.x; g[s][1] = v.y; g[s][2] = v.z; g[s][3] = v.w;
+      bacc += (v.x + v.y) + (v.z + v.w);
+    }
+    __syncthreads();
+    float cur[12], nxt[12];
+    dw_row(cur, &tile[R * ty][4 * tx]);
+#pragma unroll
+    for (int r = 0; r < R + K - 1; ++r) {
+      if (r + 1 < R + K - 1) dw_row(nxt, &tile[R * ty + r + 1][4 * tx]);
+#pragma unroll
+      for (int s = 0; s < R; ++s) {
+        const int kh = r - s;
+        if (kh < 0 || kh >= K) continue;
+#pragma unroll
+        for (int kw = 0; kw < K; ++kw)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) acc[kh * K + kw] = fmaf(g[s][i], cur[i + kw + T::OFF], acc[kh * K + kw]);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int i = 0; i < 12; ++i) cur[i] = nxt[i];
+    }
+  }
+  // workgroup reduction of the K*K + 1 partials
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+  for (int i = 0; i < K * K; ++i) {
+    const float v = warp_sum(acc[i]);
+    if (lane == 0) red[wv][i] = v;
+  }
+  {
+    const float v = warp_sum(bacc);
+    if (lane == 0) red[wv][K * K] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x < K * K + 1) {
+    const float v = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
+    if (threadIdx.x < K * K) atomicAdd(dw + c * K * K + threadIdx.x, v);
+    else if (db) atomicAdd(db + c, v);
+  }
+}
+
+// tile configuration by plane width: 0 = generic kernel
+static int dw_cfg(int H, int W) {
+  if ((W & 3) || H < 8) return 0;
+  // (built with -fno-slp-vectorize: packed-f32 FMAs would need even-aligned register pairs of
+  // the shifted input window and spill)
+  if (W % 128 == 0) return 1;   // 128 x 64 tile, 4x8 per thread
+  if (W == 64) return 2;        // 64 x 64, 4x4
+  if (W == 32) return 3;        // 32 x 32, 4x1
+  return 0;
+}
+
+template <int K, int TWT, int THT, int R>
+static void dw_fwd_v2(const float* x, long x_bs, const float* w, const float* bias, float* y, long y_bs,
+                      int N, int C, int H, int W, int flip, int accumulate, hipStream_t st) {
+  using T = DwTile<K, TWT, THT, R>;
+  const int tw = W / T::TW, th = (H + T::TH - 1) / T::TH;
+  hipLaunchKernelGGL((dwconv_fwd_v2<K, TWT, THT, R>), dim3(tw * th, N * C), dim3(256), 0, st, x, x_bs, w, bias, y,
+                     y_bs, C, H, W, flip, accumulate, tw);
+}
+
+template <int K, int TWT, int THT, int R>
+static void dw_wgrad_v2(const float* dy, long dy_bs, const float* x, long x_bs, float* dw, float* db, int N, int C,
+                        int H, int W, hipStream_t st) {
+  using T = DwTile<K, TWT, THT, R>;
+  const int tw = W / T::TW, th = (H + T::TH - 1) / T::TH;
+  // images per workgroup: enough workgroups to fill the chip, as many images each as that allows
+  const long base = (long)tw * th * C;
+  int nsplit = (int)((2048 + base - 1) / base);
+  if (nsplit > N) nsplit = N;
+  const int nper = (N + nsplit - 1) / nsplit;
+  nsplit = (N + nper - 1) / nper;
+  hipLaunchKernelGGL((dwconv_wgrad_v2<K, TWT, THT, R>), dim3(tw * th, C, nsplit), dim3(256), 0, st, dy, dy_bs, x,
+                     x_bs, dw, db, N, C, H, W, tw, nper);
+}
+
+// rows per thread: as many as the registers allow without spilling (K = 7, 9 windows are big)
+template <int K>
+static void dw_fwd_dispatch(int cfg, const float* x, long x_bs, const float* w, const float* bias, float* y,
+                            long y_bs, int N, int C, int H, int W, int flip, int accumulate, hipStream_t st) {
+  constexpr int R1 = K >= 7 ? 4 : 8, R2 = K >= 9 ? 2 : 4;
+  if (cfg == 1) dw_fwd_v2<K, 32, 8, R1>(x, x_bs, w, bias, y, y_bs, N, C, H, W, flip, accumulate, st);
+  else if (cfg == 2) dw_fwd_v2<K, 16, 16, R2>(x, x_bs, w, bias, y, y_bs, N, C, H, W, flip, accumulate, st);
+  else dw_fwd_v2<K, 8, 32, 1>(x, x_bs, w, bias, y, y_bs, N, C, H, W, flip, accumulate, st);
+}
+
+template <int K>
+static void dw_wgrad_dispatch(int cfg, const float* dy, long dy_bs, const float* x, long x_bs, float* dw, float* db,
+                              int N, int C, int H, int W, hipStream_t st) {
+  constexpr int R1 = K >= 9 ? 4 : 8, R2 = K >= 9 ? 2 : 4;
+  if (cfg == 1) dw_wgrad_v2<K, 32, 8, R1>(dy, dy_bs, x, x_bs, dw, db, N, C, H, W, st);
+  else if (cfg == 2) dw_wgrad_v2<K, 16, 16, R2>(dy, dy_bs, x, x_bs, dw, db, N, C, H, W, st);
+  else dw_wgrad_v2<K, 8, 32, 1>(dy, dy_bs, x, x_bs, dw, db, N, C, H, W, st);
+}
+
 }  // namespace dsg
 
 using namespace dsg;
 
 extern "C" {
 
-// y = dwconv(x, w) + bias   (flip=1, bias=NULL gives the data-grad of dy)
+// y (+)= dwconv(x, w) + bias   (flip=1, bias=NULL gives the data-grad of dy; accumulate adds
+// into y -- the data-grad of a tensor that has another consumer)
 int dsgan_dwconv_fwd(const float* x, long x_bs, const float* w, const float* bias, float* y,
-                     long y_bs, int N, int C, int H, int W, int K, int flip, hipStream_t st) {
+                     long y_bs, int N, int C, int H, int W, int K, int flip, int accumulate, hipStream_t st) {
   DSG_REQUIRE(x && w && y && N > 0 && C > 0 && H > 0 && W > 0, "dsgan_dwconv_fwd: bad args");
   DSG_REQUIRE(K == 3 || K == 5 || K == 7 || K == 9, "dsgan_dwconv_fwd: K must be odd and <= 9");
-  const int tw = cdiv(W, DW_T), th = cdiv(H, DW_T);
   DSG_REQUIRE((long)N * C <= 65535, "dsgan_dwconv_fwd: N*C > 65535");
+  const int cfg = dw_cfg(H, W);
+  if (cfg && ((uintptr_t)x & 15) == 0 && ((uintptr_t)y & 15) == 0 && (x_bs & 3) == 0 && (y_bs & 3) == 0) {
+    switch (K) {
+      case 3: dw_fwd_dispatch<3>(cfg, x, x_bs, w, bias, y, y_bs, N, C, H, W, flip, accumulate, st); break;
+      case 5: dw_fwd_dispatch<5>(cfg, x, x_bs, w, bias, y, y_bs, N, C, H, W, flip, accumulate, st); break;
+      case 7: dw_fwd_dispatch<7>(cfg, x, x_bs, w, bias, y, y_bs, N, C, H, W, flip, accumulate, st); break;
+      default: dw_fwd_dispatch<9>(cfg, x, x_bs, w, bias, y, y_bs, N, C, H, W, flip, accumulate, st); break;
+    }
+    DSG_CHECK_LAUNCH();
+    return 0;
+  }
+  DSG_REQUIRE(!accumulate, "dsgan_dwconv_fwd: accumulate needs a 16-byte aligned plane of width %% 4 == 0");
+  const int tw = cdiv(W, DW_T), th = cdiv(H, DW_T);
   const dim3 grid(tw * th, N * C);
   switch (K) {
     case 3: hipLaunchKernelGGL(dwconv_fwd_kernel<3>, grid, dim3(256), 0, st, x, x_bs, w, bias, y, y_bs, C, H, W, flip, tw); break;
@@ -178,6 +408,17 @@ int dsgan_dwconv_fwd(const float* x, long x_bs, const float* w, const float* bia
 int dsgan_dwconv_wgrad(const float* dy, long dy_bs, const float* x, long x_bs, float* dw, float* db,
                        int N, int C, int H, int W, int K, hipStream_t st) {
   DSG_REQUIRE(dy && x && dw && K >= 1 && K <= DW_MAXK && (K & 1), "dsgan_dwconv_wgrad: bad args");
+  const int cfg = dw_cfg(H, W);
+  if (cfg && K >= 3 && ((uintptr_t)x & 15) == 0 && ((uintptr_t)dy & 15) == 0 && (x_bs & 3) == 0 && (dy_bs & 3) == 0) {
+    switch (K) {
+      case 3: dw_wgrad_dispatch<3>(cfg, dy, dy_bs, x, x_bs, dw, db, N, C, H, W, st); break;
+      case 5: dw_wgrad_dispatch<5>(cfg, dy, dy_bs, x, x_bs, dw, db, N, C, H, W, st); break;
+      case 7: dw_wgrad_dispatch<7>(cfg, dy, dy_bs, x, x_bs, dw, db, N, C, H, W, st); break;
+      default: dw_wgrad_dispatch<9>(cfg, dy, dy_bs, x, x_bs, dw, db, N, C, H, W, st); break;
+    }
+    DSG_CHECK_LAUNCH();
+    return 0;
+  }
   const int ntiles = cdiv(W, DW_T) * cdiv(H, DW_T);
   // spread a plane's tiles over several workgroups when there are few planes
   int groups = (int)((2048 + (long)N * C - 1) / ((long)N * C));

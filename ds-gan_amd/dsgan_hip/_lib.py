@@ -42,7 +42,7 @@ SIGNATURES = {
     "dsgan_conv_small_out": [P, L, P, L, L, L, L, P, P, L] + [I] * 13 + [S],
     "dsgan_conv_wgrad_small": [P, L, P, L, P] + [I] * 11 + [S],
     # dwconv.hip
-    "dsgan_dwconv_fwd": [P, L, P, P, P, L, I, I, I, I, I, I, S],
+    "dsgan_dwconv_fwd": [P, L, P, P, P, L, I, I, I, I, I, I, I, S],
     "dsgan_dwconv_wgrad": [P, L, P, L, P, P, I, I, I, I, I, S],
     # norm_pointwise.hip
     "dsgan_instnorm_fwd": [P, L, P, P, L, P, L, P, P, I, I, I, I, F, F, S],

@@ -510,13 +510,14 @@ def pw_mlp(h, x, w1, b1, w2, b2, ws):
 # Depthwise conv
 # ------------------------------------------------------------------------------------------
 
-def dwconv_raw(x, w, b, flip=False, out=None):
+def dwconv_raw(x, w, b, flip=False, out=None, accumulate=False):
     x, xbs = nchw(x)
     N, C, H, W = x.shape
     K = w.shape[-1]
     y = out if out is not None else _empty(N, C, H, W, x)
     y4, ybs = nchw(y)
-    call("dsgan_dwconv_fwd", ptr(x), xbs, ptr(w), ptr(b), ptr(y4), ybs, N, C, H, W, K, int(flip), stream())
+    call("dsgan_dwconv_fwd", ptr(x), xbs, ptr(w), ptr(b), ptr(y4), ybs, N, C, H, W, K, int(flip), int(accumulate),
+         stream())
     return y4
 
 

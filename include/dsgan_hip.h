@@ -127,9 +127,12 @@ int dsgan_tconv(const float* X, long x_bs, const float* Wt, const float* bias, f
                 int Wout, int stride, int ntaps, const int* dh, const int* dw, int Hdst, int Wdst,
                 int os, int ph, int pw, int act, int gact, float slope, hipStream_t stream);
 
-/* ---- depthwise conv (dwconv.hip): Block.dwconv :220, MidMLKA.X3..X9 :94-97 ---------------- */
+/* ---- depthwise conv (dwconv.hip): Block.dwconv :220, MidMLKA.X3..X9 :94-97 ----------------
+ * y (+)= dwconv_KxK(x, w) + bias; flip = 1 with bias = NULL is the data-grad; accumulate adds into
+ * y (data-grad of a tensor with a second consumer; needs 16-byte aligned rows, W % 4 == 0). */
 int dsgan_dwconv_fwd(const float* x, long x_bs, const float* w, const float* bias, float* y,
-                     long y_bs, int N, int C, int H, int W, int K, int flip, hipStream_t stream);
+                     long y_bs, int N, int C, int H, int W, int K, int flip, int accumulate,
+                     hipStream_t stream);
 int dsgan_dwconv_wgrad(const float* dy, long dy_bs, const float* x, long x_bs, float* dw,
                        float* db, int N, int C, int H, int W, int K, hipStream_t stream);
 

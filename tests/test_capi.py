@@ -50,7 +50,7 @@ def test_bad_args_fail_loudly_without_gpu_work():
         _lib.call("dsgan_conv_fwd", None, 0, None, None, None, 0, None, 0, 0, 3, 8, 8, 4, 1, 1, 1, 0,
                   8, 8, 0, 0.2, 0, 0, 0, None)
     with pytest.raises(RuntimeError, match="K must be odd"):
-        _lib.call("dsgan_dwconv_fwd", 1, 0, 1, None, 1, 0, 1, 1, 8, 8, 4, 0, None)
+        _lib.call("dsgan_dwconv_fwd", 1, 0, 1, None, 1, 0, 1, 1, 8, 8, 4, 0, 0, None)
 
 
 def test_ptr_refuses_cpu_tensors():

@@ -184,7 +184,8 @@ def test_pw_mlp_fused(N, C, H, P):
 
 
 @pytest.mark.parametrize("K", [3, 5, 7, 9])
-@pytest.mark.parametrize("N,C,H,W", [(2, 4, 16, 16), (2, 3, 40, 37), (1, 2, 4, 4), (2, 8, 70, 65)])
+@pytest.mark.parametrize("N,C,H,W", [(2, 4, 16, 16), (2, 3, 40, 37), (1, 2, 4, 4), (2, 8, 70, 65),
+                                     (2, 4, 64, 64), (1, 3, 70, 128), (2, 2, 32, 32), (3, 2, 100, 256)])
 def test_dwconv(K, N, C, H, W):
     from dsgan_hip import functional as HF
     g = torch.Generator().manual_seed(K * 100 + C + H)
@@ -202,6 +203,21 @@ def test_dwconv(K, N, C, H, W):
     assert rel(xd.grad, xr.grad) < 1e-5
     assert rel(wd.grad, wr.grad) < 1e-5
     assert rel(bd.grad, br.grad) < 1e-5
+
+
+@pytest.mark.parametrize("K", [3, 7, 9])
+@pytest.mark.parametrize("H,W", [(64, 64), (40, 128), (32, 32)])
+def test_dwconv_accumulate(K, H, W):
+    """Data-grad accumulated into an existing buffer (the Block input's second consumer)."""
+    from dsgan_hip import functional as HF
+    g = torch.Generator().manual_seed(K + H)
+    dy = torch.randn(2, 6, H, W, generator=g)
+    w = torch.randn(6, 1, K, K, generator=g) / K
+    base = torch.randn(2, 6, H, W, generator=g)
+    ref = base + F.conv_transpose2d(dy, w, padding=K // 2, groups=6)
+    out = base.to(DEV)
+    HF.dwconv_raw(dy.to(DEV), w.to(DEV), None, flip=True, out=out, accumulate=True)
+    assert rel(out, ref) < 1e-5
 
 
 @pytest.mark.parametrize("act", [None, "gelu", "lrelu"])
