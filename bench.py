@@ -53,6 +53,49 @@ def cpu_baseline(threads):
                 sample="oracle/dsgan_cpu.py OracleStep, fp32, 256x256, batch 2, %d timed steps after 1 warmup (%.1f s)" % (steps, dt))
 
 
+def quality(steps=10, batch=2, size=256, threads=16):
+    """'MS-SSIM Δ vs ref' of the BASELINE metric.  The GPU model (bench precision) and the CPU
+    oracle (oracle/dsgan_cpu.py, the reference step restated in fp32 -- the checker, never the
+    thing measured) train `steps` steps from identical weights (the reference's own N(0, 0.02)
+    init recipe) on identical synthetic 256^2 pairs (pool_size 0).  Δ = |MS-SSIM(fake_gpu, real_B)
+    - MS-SSIM(fake_ref, real_B)| on the last step's fake_B, DSGAN/MS_SSIM.py:153 with data_range 1."""
+    import random
+    from oracle import dsgan_cpu as O
+    from oracle.recipe import make_params, synth_pair
+    from options.train_options import default_train_opt
+    from models import create_model
+    from dsgan_hip import functional as HF
+    torch.set_num_threads(threads)
+    prec = HF.get_precision()
+    random.seed(20)
+    torch.manual_seed(20)
+    model = create_model(default_train_opt(gpu_ids=[torch.cuda.current_device()], pool_size=0, precision=prec,
+                                           batchSize=batch))
+    gp = make_params(O.g_param_spec(), "ref", 1000)
+    dp = make_params(O.d_param_spec(), "ref", 5000)
+    with torch.no_grad():
+        for net, pr in ((model.netG, gp), (model.netD, dp), (model.vgg, make_params(O.vgg_param_spec(True), "vgg", 7000))):
+            for k, v in net.state_dict().items():
+                v.copy_(pr[k])
+    ref = O.OracleStep(gp, dp, make_params(O.vgg_param_spec(False), "vgg", 7000), pool_size=0)
+    t0 = time.time()
+    for i in range(steps):
+        A, B = synth_pair(batch, size, seed=100 + i)
+        model.set_input({"A": A.cuda(), "B": B.cuda(), "A_paths": [""] * batch, "B_paths": [""] * batch})
+        model.optimize_parameters()
+        ref.step(A, B)
+    fg = model.fake_B.detach().float().cpu()
+    fo = ref.fake_B
+    tgt = (B + 1) / 2
+    m_gpu = O.ms_ssim((fg + 1) / 2, tgt).item()
+    m_ref = O.ms_ssim((fo + 1) / 2, tgt).item()
+    HF.set_precision(prec)
+    return {"msssim_delta": round(abs(m_gpu - m_ref), 6), "msssim_gpu": round(m_gpu, 6), "msssim_ref": round(m_ref, 6),
+            "msssim_gpu_vs_ref": round(O.ms_ssim(((fg + 1) / 2).clamp(0, 1), ((fo + 1) / 2).clamp(0, 1)).item(), 6),
+            "steps": steps, "batch": batch, "size": size, "init": "reference N(0,0.02) recipe", "precision": prec,
+            "ref": "oracle/dsgan_cpu.py fp32 (%d threads)" % threads, "seconds": round(time.time() - t0, 1)}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -62,6 +105,7 @@ def main():
     ap.add_argument("--size", type=int, default=256)
     ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-quality", action="store_true", help="skip the MS-SSIM delta leg")
     ap.add_argument("--cpu-threads", type=int, default=16)
     args = ap.parse_args()
 
@@ -109,10 +153,14 @@ def main():
         dt = t.item()
     ig = HF.IGEMM_TIMER.summary()
 
+    fams = HF.IGEMM_TIMER.families()
     if rank == 0:
         imgs = args.batch * args.steps * world
         peak = PEAK_BF16_TFLOPS if args.precision == "bf16" else PEAK_F32_TFLOPS
         ach = ig["flops"] / (ig["total_ms"] * 1e-3) / 1e12 if ig["total_ms"] > 0 else 0.0
+        # dominant kernel: the contraction family with the most time in the timed steps
+        dom, (dn, dms, dfl) = max(fams.items(), key=lambda kv: kv[1][1])
+        dach = dfl / (dms * 1e-3) / 1e12 if dms > 0 else 0.0
         out = {
             "metric": METRIC,
             "value": round(imgs / dt, 3),
@@ -130,18 +178,31 @@ def main():
                        "global_batch": args.batch * world, "per_gpu_batch": args.batch,
                        "image": [args.size, args.size], "parallelism": "dp%d" % world,
                        "baseline_config": "configs[1]: 256x256, batch 16, bf16, 1xMI355X"},
-            "roofline": {"bound": "mfma", "kernel": "conv contraction kernels (pwgemm_kernel + tconv_kernel + igemm_kernel: every 1x1/3x3/4x4/ConvT fwd, dgrad, wgrad launch)",
-                         "achieved": round(ach, 2), "peak": peak, "unit": "TFLOP/s",
-                         "frac": round(ach / peak, 4), "traffic": None,
-                         "launches_per_step": ig["launches"] // max(1, args.steps),
-                         "igemm_ms_per_step": round(ig["total_ms"] / args.steps, 3),
-                         "gflop_per_step": round(ig["flops"] / args.steps / 1e9, 1)},
+            "roofline": {"bound": "mfma", "kernel": dom,
+                         "achieved": round(dach, 2), "peak": peak, "unit": "TFLOP/s",
+                         "frac": round(dach / peak, 4), "traffic": None,
+                         "launches_per_step": round(dn / args.steps, 2),
+                         "kernel_ms_per_step": round(dms / args.steps, 3),
+                         "avg_launch_us": round(dms / max(1, dn) * 1e3, 1),
+                         "gflop_per_launch": round(dfl / max(1, dn) / 1e9, 3),
+                         "all_contractions": {"achieved": round(ach, 2), "frac": round(ach / peak, 4),
+                                              "ms_per_step": round(ig["total_ms"] / args.steps, 3),
+                                              "gflop_per_step": round(ig["flops"] / args.steps / 1e9, 1),
+                                              "launches_per_step": ig["launches"] // max(1, args.steps)},
+                         "families": {k: {"ms_per_step": round(v[1] / args.steps, 3),
+                                          "tflops": round(v[2] / (v[1] * 1e-3) / 1e12, 1) if v[1] > 0 else 0.0}
+                                      for k, v in sorted(fams.items(), key=lambda kv: -kv[1][1])}},
         }
         if not args.no_cpu_baseline and world == 1:
             try:
                 out["cpu_baseline"] = cpu_baseline(args.cpu_threads)
             except Exception as e:  # reported, never fatal to the GPU measurement
                 out["cpu_baseline"] = {"error": repr(e)}
+        if not args.no_quality and world == 1:
+            try:
+                out["quality"] = quality(threads=args.cpu_threads)
+            except Exception as e:
+                out["quality"] = {"error": repr(e)}
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

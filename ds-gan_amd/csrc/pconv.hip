@@ -1,0 +1,283 @@
+// Patch-staged implicit-GEMM convolution (gfx950, bf16 MFMA): KxK, stride 1 or 2, Cin % 32 == 0.
+//
+// Covers the dense contractions of VGG16 (3x3 s1, forward and data-grad; DSGAN/models/vgg.py:15-24)
+// and the PatchGAN 4x4 convs (s2 and s1; DSGAN/models/networks.py:543-569).
+//
+//   out[b][m][oh][ow] = act( bias[m] + sum_{c, kh, kw} W[tap][m][c] * in[b][c][oh*S - pad + kh][ow*S - pad + kw] )
+//
+// A workgroup owns BM output channels x one TH x TW block of output pixels (128 pixels) of one
+// image.  The K loop walks 32-channel blocks; per block the input patch that ALL taps of the
+// block need ((TH-1)*S + KH) x ((TW-1)*S + KW) pixels) is staged once into LDS as bf16,
+// pixel-major with the 32 channels contiguous, so the B fragment of any tap is one 16-byte LDS
+// read at a shifted pixel -- the input is read from L2 ~1.4x instead of KH*KW times (tconv.hip).
+// Per tap the bf16 weight slice [BM][32] is register-prefetched one tap ahead into a double
+// buffer.  Weights are a bf16 tap-major copy (dsgan_conv_wtrans_bf16).
+#include "common.h"
+
+namespace dsg {
+
+typedef __attribute__((ext_vector_type(8))) __bf16 cbf16x8;
+typedef __attribute__((ext_vector_type(16))) float cf32x16;
+typedef __attribute__((ext_vector_type(4))) unsigned int cu32x4;
+
+struct PcArgs {
+  const float* X; long x_bs;          // [nb][K][H][W]
+  const __bf16* Wb;                   // [taps][M][K] bf16
+  float* Y; long y_bs;                // [nb][M][Hdst][Wdst]
+  const float* bias;
+  const float* gpre; long gpre_bs;    // dst-shaped act' multiplier (data-grad of the producer's act)
+  int nb, K, M, H, W, Ho, Wo, pad;
+  int tiles_w, tiles_h;
+  int act, gact; float slope;
+  int accumulate;
+};
+
+constexpr int PC_STR = 40;   // bf16 per staged pixel / weight row (32 + 8: conflict-free b128 reads)
+
+template <int BM, int TH, int TW, int S, int KH, int KW>
+__global__ __launch_bounds__(256, 2) void pconv_kernel(PcArgs g) {
+  constexpr int BN = TH * TW;
+  static_assert(BN == 128, "128 output pixels per tile");
+  constexpr int WM = 2, WN = 2, TM = BM / WM / 32, TN = BN / WN / 32;
+  constexpr int PH = (TH - 1) * S + KH, PW = (TW - 1) * S + KW, PPIX = PH * PW;
+  constexpr int TAPS = KH * KW;
+  constexpr int A_SZ = BM * PC_STR, P_SZ = PPIX * PC_STR;
+  constexpr int A_ITEMS = BM * 4 / 256;           // 16-byte items of a [BM][32] bf16 slice
+  constexpr int P_ITEMS = (PPIX * 4 + 255) / 256; // (pixel, 8-channel group) items of the patch
+  __shared__ __attribute__((aligned(16))) __bf16 smem[2 * A_SZ + P_SZ];
+  __bf16* Ps = smem + 2 * A_SZ;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / WN, wn = wave % WN;
+  const int lr = lane & 31, lh = lane >> 5;
+
+  // tile decode: M tile fastest (the tiles of one pixel block share its patch in L2)
+  const int mt = (g.M + BM - 1) / BM;
+  int tile;
+  {
+    const int nwg = gridDim.x, id = blockIdx.x;
+    const int xcd = id & 7, q = nwg >> 3, r = nwg & 7;
+    tile = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (id >> 3);
+  }
+  const int m_t = tile % mt, rest = tile / mt;
+  const int tpi = g.tiles_w * g.tiles_h;
+  const int bimg = rest / tpi, t_i = rest - bimg * tpi;
+  const int m0 = m_t * BM;
+  const int oh0 = (t_i / g.tiles_w) * TH, ow0 = (t_i % g.tiles_w) * TW;
+  const int ih0 = oh0 * S - g.pad, iw0 = ow0 * S - g.pad;   // patch origin in the input
+  const int HW = g.H * g.W;
+  const float* xb = g.X + (long)bimg * g.x_bs;
+
+  // B fragment base (patch pixel of this lane's output column, tap (0,0)) per n-tile
+  int pbase[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int n = wn * (BN / WN) + j * 32 + lr;
+    pbase[j] = ((n / TW) * S * PW + (n % TW) * S) * PC_STR + lh * 8;
+  }
+
+  cu32x4 ra[A_ITEMS];
+  auto aload = [&](int tap, int k0) {
+#pragma unroll
+    for (int i = 0; i < A_ITEMS; ++i) {
+      const int it = tid + i * 256, row = it >> 2, c8 = it & 3;
+      const int m = m0 + row;
+      ra[i] = m < g.M ? *reinterpret_cast<const cu32x4*>(g.Wb + ((long)tap * g.M + m) * g.K + k0 + c8 * 8)
+                      : cu32x4{0u, 0u, 0u, 0u};
+    }
+  };
+  auto astore = [&](int buf) {
+    __bf16* As = smem + buf * A_SZ;
+#pragma unroll
+    for (int i = 0; i < A_ITEMS; ++i) {
+      const int it = tid + i * 256;
+      *reinterpret_cast<cu32x4*>(As + (it >> 2) * PC_STR + (it & 3) * 8) = ra[i];
+    }
+  };
+  // patch of channel block k0: item = (pixel, 8-channel group); lanes run along the pixels of
+  // a patch row, so each of the 8 channel loads is coalesced across the wave
+  auto pstage = [&](int k0) {
+#pragma unroll
+    for (int i = 0; i < P_ITEMS; ++i) {
+      const int it = tid + i * 256;
+      if (it < PPIX * 4) {
+        const int cg = it / PPIX, pix = it - cg * PPIX;
+        const int pr = pix / PW, pc = pix - pr * PW;
+        const int ih = ih0 + pr, iw = iw0 + pc;
+        const bool in = (unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W;
+        const float* src = xb + (long)(k0 + cg * 8) * HW + (in ? ih * g.W + iw : 0);
+        cbf16x8 v;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = (__bf16)(in ? src[(long)e * HW] : 0.f);
+        *reinterpret_cast<cbf16x8*>(Ps + pix * PC_STR + cg * 8) = v;
+      }
+    }
+  };
+
+  cf32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    float bv[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int m = m0 + wm * TM * 32 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+      bv[r] = (g.bias && m < g.M) ? g.bias[m] : 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = bv[r];
+  }
+
+  const int nkb = g.K / 32;
+  int buf = 0;
+  for (int kb = 0; kb < nkb; ++kb) {
+    const int k0 = kb * 32;
+    __syncthreads();                 // previous block's patch and A buffers are free
+    aload(0, k0);
+    pstage(k0);
+    astore(buf);
+    __syncthreads();
+#pragma unroll 1
+    for (int tap = 0; tap < TAPS; ++tap) {
+      if (tap + 1 < TAPS) aload(tap + 1, k0);
+      const __bf16* As = smem + buf * A_SZ;
+      const int kh = tap / KW, kw = tap - (tap / KW) * KW;
+      const int toff = (kh * PW + kw) * PC_STR;
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        cbf16x8 af[TM], bfr[TN];
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+          af[i] = *reinterpret_cast<const cbf16x8*>(As + (wm * TM * 32 + i * 32 + lr) * PC_STR + ks * 16 + lh * 8);
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          bfr[j] = *reinterpret_cast<const cbf16x8*>(Ps + pbase[j] + toff + ks * 16);
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      }
+      if (tap + 1 < TAPS) {
+        astore(buf ^ 1);
+        __syncthreads();
+        buf ^= 1;
+      }
+    }
+  }
+
+  // ---- epilogue ----
+  const int HWo = g.Ho * g.Wo;
+  float* yb = g.Y + (long)bimg * g.y_bs;
+  const float* gb = g.gpre ? g.gpre + (long)bimg * g.gpre_bs : nullptr;
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int n = wn * (BN / WN) + j * 32 + lr;
+    const int oh = oh0 + n / TW, ow = ow0 + n % TW;
+    const bool nv = oh < g.Ho && ow < g.Wo;
+    const long pofs = (long)oh * g.Wo + ow;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      float v[16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) v[r] = acc[i][j][r];
+      if (gb) {
+        float gv[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int m = m0 + wm * TM * 32 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+          gv[r] = (nv && m < g.M) ? gb[(long)m * HWo + pofs] : 0.f;
+        }
+        act_g_mul_arr(g.gact, v, gv, g.slope);
+      }
+      act_f_arr(g.act, v, g.slope);
+      if (nv) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int m = m0 + wm * TM * 32 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+          if (m < g.M) {
+            float* o = yb + (long)m * HWo + pofs;
+            *o = g.accumulate ? *o + v[r] : v[r];
+          }
+        }
+      }
+    }
+  }
+}
+
+// bf16 tap-major weights (same modes as dsgan_conv_wtrans):
+//   mode 0 (forward):      Wb[tap][co][ci], tap = (kh, kw)
+//   mode 1 (data-grad s1): Wb[tap][ci][co], tap = (kh', kw') with kh = KH-1-kh', kw = KW-1-kw'
+__global__ void wtrans_bf16_kernel(const float* __restrict__ W, __bf16* __restrict__ Wb, int Co, int Ci, int KH,
+                                   int KW, int mode) {
+  const int M = mode == 0 ? Co : Ci, K = mode == 0 ? Ci : Co;
+  const long total = (long)KH * KW * M * K;
+  for (long e = blockIdx.x * 256L + threadIdx.x; e < total; e += (long)gridDim.x * 256) {
+    const int k = e % K;
+    const long t = e / K;
+    const int m = t % M, tap = t / M;
+    int kh = tap / KW, kw = tap % KW, co = m, ci = k;
+    if (mode == 1) { kh = KH - 1 - kh; kw = KW - 1 - kw; co = k; ci = m; }
+    Wb[e] = (__bf16)W[(((long)co * Ci + ci) * KH + kh) * KW + kw];
+  }
+}
+
+template <int BM, int TH, int TW, int S, int KH, int KW>
+static void pc_launch(PcArgs& g, hipStream_t st) {
+  g.tiles_w = (g.Wo + TW - 1) / TW;
+  g.tiles_h = (g.Ho + TH - 1) / TH;
+  const long tiles = (long)g.nb * g.tiles_w * g.tiles_h * ((g.M + BM - 1) / BM);
+  hipLaunchKernelGGL((pconv_kernel<BM, TH, TW, S, KH, KW>), dim3((unsigned)tiles), dim3(256), 0, st, g);
+}
+
+template <int BM>
+static int pc_dispatch(PcArgs& g, int KH, int S, hipStream_t st) {
+  if (KH == 3 && S == 1) { pc_launch<BM, 8, 16, 1, 3, 3>(g, st); return 0; }
+  if (KH == 4 && S == 1) { pc_launch<BM, 8, 16, 1, 4, 4>(g, st); return 0; }
+  if (KH == 4 && S == 2) { pc_launch<BM, 8, 16, 2, 4, 4>(g, st); return 0; }
+  return -1;
+}
+
+}  // namespace dsg
+
+using namespace dsg;
+
+extern "C" {
+
+int dsgan_pconv_supported(int K, int KH, int KW, int stride) {
+  if (K % 32 != 0 || K <= 0 || KH != KW) return 0;
+  return (KH == 3 && stride == 1) || (KH == 4 && (stride == 1 || stride == 2));
+}
+
+int dsgan_conv_wtrans_bf16(const float* W, void* Wb, int Co, int Ci, int KH, int KW, int mode, hipStream_t st) {
+  DSG_REQUIRE(W && Wb && (mode == 0 || mode == 1), "dsgan_conv_wtrans_bf16: bad args");
+  const long total = (long)KH * KW * Co * Ci;
+  long blocks = (total + 255) / 256;
+  if (blocks > 8192) blocks = 8192;
+  hipLaunchKernelGGL(wtrans_bf16_kernel, dim3((unsigned)blocks), dim3(256), 0, st, W, (__bf16*)Wb, Co, Ci, KH, KW, mode);
+  DSG_CHECK_LAUNCH();
+  return 0;
+}
+
+// y[b][m][oh][ow] (+)= act(bias[m] + sum W * x) (* gact'(gpre)); Wb from dsgan_conv_wtrans_bf16.
+int dsgan_pconv(const float* X, long x_bs, const void* Wb, const float* bias, float* Y, long y_bs,
+                const float* gpre, long gpre_bs, int nb, int K, int M, int H, int W, int Ho, int Wo,
+                int KH, int KW, int stride, int pad, int act, int gact, float slope, int accumulate,
+                hipStream_t st) {
+  DSG_REQUIRE(X && Wb && Y && nb > 0 && M > 0 && Ho > 0 && Wo > 0, "dsgan_pconv: bad args");
+  DSG_REQUIRE(dsgan_pconv_supported(K, KH, KW, stride), "dsgan_pconv: unsupported K=%d KH=%d KW=%d stride=%d", K, KH, KW, stride);
+  DSG_REQUIRE(((uintptr_t)Wb & 15) == 0, "dsgan_pconv: Wb must be 16-byte aligned");
+  DSG_REQUIRE((Ho - 1) * stride - pad + KH <= H + pad && (Wo - 1) * stride - pad + KW <= W + pad,
+              "dsgan_pconv: output size inconsistent with input/pad");
+  PcArgs g{};
+  g.X = X; g.x_bs = x_bs; g.Wb = (const __bf16*)Wb; g.Y = Y; g.y_bs = y_bs; g.bias = bias;
+  g.gpre = gpre; g.gpre_bs = gpre_bs; g.nb = nb; g.K = K; g.M = M; g.H = H; g.W = W; g.Ho = Ho;
+  g.Wo = Wo; g.pad = pad; g.act = act; g.gact = gact; g.slope = slope; g.accumulate = accumulate;
+  const int rc = M > 64 ? pc_dispatch<128>(g, KH, stride, st) : pc_dispatch<64>(g, KH, stride, st);
+  DSG_REQUIRE(rc == 0, "dsgan_pconv: no kernel for KH=%d stride=%d", KH, stride);
+  DSG_CHECK_LAUNCH();
+  return 0;
+}
+
+}  // extern "C"

@@ -35,6 +35,10 @@ SIGNATURES = {
     "dsgan_mlp_bwd": [P, L, P, L, P, P, P, P, L, P, P, P, I, I, I, I, S],
     "dsgan_colsum": [P, I, I, P, S],
     "dsgan_f32_to_bf16": [P, P, L, S],
+    # pconv.hip
+    "dsgan_pconv_supported": [I, I, I, I],
+    "dsgan_conv_wtrans_bf16": [P, P, I, I, I, I, I, S],
+    "dsgan_pconv": [P, L, P, P, P, L, P, L] + [I] * 13 + [F, I, S],
     # tconv.hip
     "dsgan_conv_wtrans": [P, P, I, I, I, I, I, I, I, I, I, S],
     "dsgan_tconv": [P, L, P, P, P, L, P, L] + [I] * 9 + [P, P] + [I] * 7 + [F, S],

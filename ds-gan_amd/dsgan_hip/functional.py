@@ -34,6 +34,19 @@ def get_precision():
     return _state["prec"]
 
 
+@contextlib.contextmanager
+def precision(p):
+    """Scoped precision: ops created inside run (forward AND backward -- the contraction
+    Functions record it in ctx) at precision ``p``.  ``None`` keeps the current one."""
+    old = _state["prec"]
+    if p is not None:
+        set_precision(p)
+    try:
+        yield
+    finally:
+        _state["prec"] = old
+
+
 def _prec():
     return PREC[_state["prec"]]
 
@@ -53,12 +66,12 @@ class KernelTimer:
         e0.record()
         return e0
 
-    def end(self, e0, flops, tag=None):
+    def end(self, e0, flops, tag=None, fam="other"):
         if e0 is None:
             return
         e1 = torch.cuda.Event(enable_timing=True)
         e1.record()
-        self.rec.append((e0, e1, flops, tag))
+        self.rec.append((e0, e1, flops, tag, fam))
 
     def summary(self):
         torch.cuda.synchronize()
@@ -66,9 +79,20 @@ class KernelTimer:
         fl = sum(r[2] for r in self.rec)
         return dict(launches=len(self.rec), total_ms=ms, flops=fl)
 
+    def families(self):
+        """{kernel family: [launches, ms, algorithmic flops]} over the recorded launches."""
+        torch.cuda.synchronize()
+        out = {}
+        for r in self.rec:
+            a = out.setdefault(r[4], [0, 0.0, 0.0])
+            a[0] += 1
+            a[1] += r[0].elapsed_time(r[1])
+            a[2] += r[2]
+        return out
+
     def table(self):
         torch.cuda.synchronize()
-        return [(r[0].elapsed_time(r[1]), r[2], r[3]) for r in self.rec]
+        return [(r[0].elapsed_time(r[1]), r[2], r[3] + (r[4],)) for r in self.rec]
 
 
 IGEMM_TIMER = KernelTimer()
@@ -159,6 +183,29 @@ def _wtrans_build(w, mode, kh0=0, kw0=0, nth=0, ntw=0):
     return wt
 
 
+def _wtrans_bf16(w, mode):
+    """bf16 tap-major weights for pconv.hip (mode 0 forward, 1 stride-1 data-grad), cached."""
+    key = (id(w), w.data_ptr(), tuple(w.shape), "bf16", mode)
+    ent = _WT_CACHE.get(key)
+    gen = WEIGHT_GEN[0]
+    if ent is not None and ent[0] == gen and ent[1] == w._version and ent[2] is w:
+        return ent[3]
+    Co, Ci, KH, KW = w.shape
+    wb = torch.empty(KH * KW * Co * Ci, device=w.device, dtype=torch.bfloat16)
+    call("dsgan_conv_wtrans_bf16", ptr(w), ptr(wb), Co, Ci, KH, KW, mode, stream())
+    _WT_CACHE[key] = (gen, w._version, w, wb)
+    return wb
+
+
+def _pconv_ok(K, KH, KW, stride):
+    return _state["prec"] == "bf16" and bool(_lib.load().dsgan_pconv_supported(K, KH, KW, stride))
+
+
+def _pconv(x, xbs, wb, b, y, ybs, N, K, M, H, W, Ho, Wo, KH, KW, stride, pad, act, gpre, gbs, gact, accumulate):
+    call("dsgan_pconv", ptr(x), xbs, ptr(wb), ptr(b), ptr(y), ybs, ptr(gpre), gbs, N, K, M, H, W, Ho, Wo, KH, KW,
+         stride, pad, ACT[act], ACT[gact], LRELU_SLOPE, int(accumulate), stream())
+
+
 def conv_fwd_raw(x, w, b, stride, pad, act=None, out=None, pre=None, accumulate=False, xact=None):
     x, xbs = nchw(x)
     N, Cin, H, W = x.shape
@@ -173,15 +220,23 @@ def conv_fwd_raw(x, w, b, stride, pad, act=None, out=None, pre=None, accumulate=
     if pre is not None:
         pre, pbs = nchw(pre)
     e0 = IGEMM_TIMER.begin()
+    fam = "igemm_kernel"
     if Cout <= 8 and act is None and pre is None and xact is None:
         # few output channels (G head, PatchGAN last layer): direct conv, not a GEMM tile
+        fam = "small_out_kernel"
         call("dsgan_conv_small_out", ptr(x), xbs, ptr(w), Cin * KH * KW, KH * KW, KW, 1, ptr(b), ptr(y), ybs,
              N, Cin, Cout, H, W, Ho, Wo, KH, KW, stride, pad, 0, int(accumulate), stream())
     elif KH == 1 and KW == 1 and stride == 1 and pad == 0 and _pw_ok(0, Cout, Cin, H * W, 0, xbs, w.data_ptr(), x.data_ptr()):
+        fam = "pwgemm_kernel"
         call("dsgan_pw_gemm", 0, ptr(w), 0, ptr(x), xbs, ptr(y), ybs, ptr(b), ptr(pre), pbs, None, 0,
              Cout, N * H * W, Cin, H * W, N, ACT[act], 0, ACT[xact], int(accumulate), LRELU_SLOPE, stream())
+    elif w.dim() == 4 and pre is None and xact is None and _pconv_ok(Cin, KH, KW, stride):
+        fam = "pconv_kernel"
+        _pconv(x, xbs, _wtrans_bf16(w, 0), b, y, ybs, N, Cin, Cout, H, W, Ho, Wo, KH, KW, stride, pad, act,
+               None, 0, None, accumulate)
     elif (_state["prec"] == "bf16" and w.dim() == 4 and (KH > 1 or KW > 1) and Cin % 32 == 0
           and pre is None and not accumulate and xact is None and KH * KW <= 16):
+        fam = "tconv_kernel"
         wt = _wtrans(w, 0)
         taps = [(kh - pad, kw - pad) for kh in range(KH) for kw in range(KW)]
         _tconv(x, xbs, wt, b, y, ybs, None, 0, N, Cin, Cout, H, W, Ho, Wo, stride, taps, Ho, Wo, 1, 0, 0,
@@ -190,7 +245,7 @@ def conv_fwd_raw(x, w, b, stride, pad, act=None, out=None, pre=None, accumulate=
         call("dsgan_conv_fwd", ptr(x), xbs, ptr(w), ptr(b), ptr(y), ybs, ptr(pre), pbs, N, Cin, H, W,
              Cout, KH, KW, stride, pad, Ho, Wo, ACT[act], LRELU_SLOPE, int(accumulate), ACT[xact], _prec(),
              stream())
-    IGEMM_TIMER.end(e0, _conv_flops(N, Cin, Cout, KH, KW, Ho, Wo), ("fwd", N, Cin, H, W, Cout, KH, stride))
+    IGEMM_TIMER.end(e0, _conv_flops(N, Cin, Cout, KH, KW, Ho, Wo), ("fwd", N, Cin, H, W, Cout, KH, stride), fam)
     return y
 
 
@@ -207,16 +262,26 @@ def conv_dgrad_raw(dy, w, x_shape, stride, pad, bias=None, act=None, gpre=None, 
     if gpre is not None:
         gpre, gbs = nchw(gpre)
     e0 = IGEMM_TIMER.begin()
+    fam = "igemm_kernel"
     if Cin <= 8 and act is None and gpre is None and stride in (1, 2):
+        fam = "small_out_kernel"
         # data-grad into a 3/6-channel tensor: direct transposed gather, w(m=ci, k=co, kh, kw)
         call("dsgan_conv_small_out", ptr(dy), dybs, ptr(w), KH * KW, Cin * KH * KW, KW, 1, ptr(bias),
              ptr(dx), dxbs, N, Cout, Cin, Ho, Wo, H, W, KH, KW, stride, pad, 1, int(accumulate), stream())
     elif (KH == 1 and KW == 1 and stride == 1 and pad == 0 and bias is None and act is None
             and not accumulate and _pw_ok(1, Cin, Cout, H * W, 0, dybs, w.data_ptr(), dy.data_ptr())):
+        fam = "pwgemm_kernel"
         call("dsgan_pw_gemm", 1, ptr(w), 0, ptr(dy), dybs, ptr(dx), dxbs, None, None, 0, ptr(gpre), gbs,
              Cin, N * H * W, Cout, H * W, N, 0, ACT[gact], 0, 0, LRELU_SLOPE, stream())
+    elif (w.dim() == 4 and stride == 1 and act is None and bias is None and KH == KW
+          and _pconv_ok(Cout, KH, KW, 1)):
+        # stride-1 data-grad = forward conv of dy with the flipped, transposed kernel
+        fam = "pconv_kernel"
+        _pconv(dy, dybs, _wtrans_bf16(w, 1), None, dx, dxbs, N, Cout, Cin, Ho, Wo, H, W, KH, KW, 1,
+               KH - 1 - pad, None, gpre, gbs, gact, accumulate)
     elif (_state["prec"] == "bf16" and w.dim() == 4 and (KH > 1 or KW > 1) and Cout % 32 == 0
           and act is None and not accumulate and stride in (1, 2) and KH * KW <= 16):
+        fam = "tconv_kernel"
         if stride == 1:
             wt = _wtrans(w, 1)
             pp = KH - 1 - pad
@@ -241,7 +306,7 @@ def conv_dgrad_raw(dy, w, x_shape, stride, pad, bias=None, act=None, gpre=None, 
         call("dsgan_conv_dgrad", ptr(dy), dybs, ptr(w), ptr(bias), ptr(dx), dxbs, None, 0, ptr(gpre), gbs,
              ACT[gact], N, Cin, H, W, Cout, KH, KW, stride, pad, Ho, Wo, ACT[act], LRELU_SLOPE,
              int(accumulate), _prec(), stream())
-    IGEMM_TIMER.end(e0, _conv_flops(N, Cin, Cout, KH, KW, Ho, Wo), ("dgrad", N, Cin, H, W, Cout, KH, stride))
+    IGEMM_TIMER.end(e0, _conv_flops(N, Cin, Cout, KH, KW, Ho, Wo), ("dgrad", N, Cin, H, W, Cout, KH, stride), fam)
     return dx
 
 
@@ -252,17 +317,20 @@ def conv_wgrad_raw(dy, x, dw, stride, pad, xact=None):
     Cout = dy.shape[1]
     KH, KW = (dw.shape[2], dw.shape[3]) if dw.dim() == 4 else (1, 1)
     e0 = IGEMM_TIMER.begin()
+    fam = "igemm_kernel"
     if xact is None and KH * KW in (1, 9, 16) and (Cout <= 8 or (Cin <= 8 and KH * KW == 1)):
+        fam = "wgrad_small_kernel"
         call("dsgan_conv_wgrad_small", ptr(dy), dybs, ptr(x), xbs, ptr(dw), N, Cin, H, W, Cout, KH, KW,
              stride, pad, dy.shape[2], dy.shape[3], stream())
     elif KH == 1 and KW == 1 and stride == 1 and pad == 0 and _pw_ok(2, Cout, N * H * W, H * W, dybs, xbs, dy.data_ptr(), x.data_ptr()):
+        fam = "pwgemm_kernel"
         call("dsgan_pw_gemm", 2, ptr(dy), dybs, ptr(x), xbs, ptr(dw), 0, None, None, 0, None, 0,
              Cout, Cin, N * H * W, H * W, N, 0, 0, ACT[xact], 0, LRELU_SLOPE, stream())
     else:
         call("dsgan_conv_wgrad", ptr(dy), dybs, ptr(x), xbs, ptr(dw), N, Cin, H, W, Cout, KH, KW,
              stride, pad, dy.shape[2], dy.shape[3], ACT[xact], _prec(), stream())
     IGEMM_TIMER.end(e0, _conv_flops(N, Cin, Cout, KH, KW, dy.shape[2], dy.shape[3]),
-                    ("wgrad", N, Cin, H, W, Cout, KH, stride))
+                    ("wgrad", N, Cin, H, W, Cout, KH, stride), fam)
 
 
 def channel_sum_raw(dy, out):
@@ -429,7 +497,7 @@ class PwMlpFn(torch.autograd.Function):
             e0 = IGEMM_TIMER.begin()
             call("dsgan_mlp_fwd", ptr(h), hbs, ptr(bf16_weight(w1)), ptr(b1), ptr(bf16_weight(w2)), ptr(b2),
                  ptr(out), P * H * W, N, C, P, H * W, 1, stream())
-            IGEMM_TIMER.end(e0, _mlp_flops(N, C, P, H * W), ("mlp_fwd", N, C, H, W, P, 1, 1))
+            IGEMM_TIMER.end(e0, _mlp_flops(N, C, P, H * W), ("mlp_fwd", N, C, H, W, P, 1, 1), "mlp_fwd_kernel")
             ctx.save_for_backward(h, x, ws)
             return out
         w1v = w1.view(w1.shape[0], w1.shape[1], 1, 1)
@@ -482,12 +550,12 @@ class PwMlpFn(torch.autograd.Function):
         e0 = IGEMM_TIMER.begin()
         call("dsgan_mlp_bwd", ptr(h), C * HW, ptr(dy), dybs, ptr(bf16_weight(w1)), ptr(b1), ptr(bf16_weight(w2)),
              ptr(dh), C * HW, ptr(g), ptr(dz), ptr(bsum), N, C, P, HW, stream())
-        IGEMM_TIMER.end(e0, _mlp_flops(N, C, P, HW), ("mlp_bwd", N, C, H, W, P, 1, 1))
+        IGEMM_TIMER.end(e0, _mlp_flops(N, C, P, HW), ("mlp_bwd", N, C, H, W, P, 1, 1), "mlp_bwd_kernel")
         gw2, gb2, gws, gw1, gb1 = (_grad_buf(t) for t in (w2, b2, ws_ref, w1, b1))
         if gw2 is not None:
             e0 = IGEMM_TIMER.begin()
             call("dsgan_pw_wgrad_mixed", ptr(dy), dybs, 0, ptr(g), C4 * HW, 1, ptr(gw2), P, C4, HW, N, stream())
-            IGEMM_TIMER.end(e0, 2.0 * N * HW * C4 * P, ("wgrad", N, C4, H, W, P, 1, 1))
+            IGEMM_TIMER.end(e0, 2.0 * N * HW * C4 * P, ("wgrad", N, C4, H, W, P, 1, 1), "pwgemm_kernel")
         if gb2 is not None:
             channel_sum_raw(dy, gb2)
         if gws is not None:
@@ -495,7 +563,7 @@ class PwMlpFn(torch.autograd.Function):
         if gw1 is not None:
             e0 = IGEMM_TIMER.begin()
             call("dsgan_pw_wgrad_mixed", ptr(dz), C4 * HW, 1, ptr(h), C * HW, 0, ptr(gw1), C4, C, HW, N, stream())
-            IGEMM_TIMER.end(e0, 2.0 * N * HW * C4 * C, ("wgrad", N, C, H, W, C4, 1, 1))
+            IGEMM_TIMER.end(e0, 2.0 * N * HW * C4 * C, ("wgrad", N, C, H, W, C4, 1, 1), "pwgemm_kernel")
         if gb1 is not None:
             call("dsgan_colsum", ptr(bsum), ntiles, C4, ptr(gb1), stream())
         dx = conv_dgrad_raw(dy, ws, tuple(x.shape), 1, 0) if ctx.needs_input_grad[1] else None

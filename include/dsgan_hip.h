@@ -127,6 +127,20 @@ int dsgan_tconv(const float* X, long x_bs, const float* Wt, const float* bias, f
                 int Wout, int stride, int ntaps, const int* dh, const int* dw, int Hdst, int Wdst,
                 int os, int ph, int pw, int act, int gact, float slope, hipStream_t stream);
 
+/* ---- patch-staged implicit-GEMM conv (pconv.hip): VGG16 3x3 s1 (DSGAN/models/vgg.py:15-24) fwd
+ * and data-grad, PatchGAN 4x4 s2/s1 (DSGAN/models/networks.py:543-569) fwd and s1 data-grad ------
+ * y[b][m][oh][ow] (+)= act(bias[m] + sum_{c,kh,kw} Wb[tap][m][c] x[b][c][oh*s-pad+kh][ow*s-pad+kw])
+ *                     (* gact'(gpre[b][m][oh][ow]) when gpre != NULL).  bf16 MFMA, Cin % 32 == 0.
+ * dsgan_conv_wtrans_bf16 builds Wb from an OIHW weight: mode 0 forward, mode 1 the flipped
+ * transposed kernel of the stride-1 data-grad (then call with pad' = KH-1-pad). */
+int dsgan_pconv_supported(int K, int KH, int KW, int stride);
+int dsgan_conv_wtrans_bf16(const float* W, void* Wb, int Co, int Ci, int KH, int KW, int mode,
+                           hipStream_t stream);
+int dsgan_pconv(const float* X, long x_bs, const void* Wb, const float* bias, float* Y, long y_bs,
+                const float* gpre, long gpre_bs, int nb, int K, int M, int H, int W, int Ho, int Wo,
+                int KH, int KW, int stride, int pad, int act, int gact, float slope, int accumulate,
+                hipStream_t stream);
+
 /* ---- depthwise conv (dwconv.hip): Block.dwconv :220, MidMLKA.X3..X9 :94-97 ----------------
  * y (+)= dwconv_KxK(x, w) + bias; flip = 1 with bias = NULL is the data-grad; accumulate adds into
  * y (data-grad of a tensor with a second consumer; needs 16-byte aligned rows, W % 4 == 0). */

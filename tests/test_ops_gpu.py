@@ -149,6 +149,39 @@ def test_pw_mlp(prec, N, C, H, P):
         assert rel(pd.grad, pr.grad) < 2 * tol
 
 
+@pytest.mark.parametrize("N,Cin,H,W,Cout,K,s,p,act", [
+    (2, 64, 18, 18, 128, 3, 1, 1, "relu"),       # VGG block (ragged 18x18 vs 8x16 tiles)
+    (1, 128, 32, 40, 64, 3, 1, 1, None),
+    (2, 32, 34, 30, 64, 4, 2, 1, "lrelu"),       # PatchGAN s2
+    (2, 128, 9, 11, 256, 4, 1, 1, None),         # PatchGAN s1 (output 8x10)
+    (1, 256, 16, 16, 3 * 32, 3, 1, 1, "relu"),   # M not a multiple of the 128 tile
+])
+def test_pconv_bf16(N, Cin, H, W, Cout, K, s, p, act):
+    """Patch-staged conv (pconv.hip): forward and stride-1 data-grad vs the bf16-rounded fp32 conv."""
+    from dsgan_hip import functional as HF
+    HF.set_precision("bf16")
+    g = torch.Generator().manual_seed(Cin + Cout + K)
+    x = _q(torch.randn(N, Cin, H, W, generator=g), "bf16")
+    w = _q(torch.randn(Cout, Cin, K, K, generator=g) / math.sqrt(Cin * K * K), "bf16")
+    b = torch.randn(Cout, generator=g) * 0.1
+    y_ref = F.conv2d(x, w, b, stride=s, padding=p)
+    if act == "relu":
+        y_ref = F.relu(y_ref)
+    elif act == "lrelu":
+        y_ref = F.leaky_relu(y_ref, 0.2)
+    y = HF.conv_fwd_raw(x.to(DEV), w.to(DEV), b.to(DEV), s, p, act=act)
+    assert y.shape == y_ref.shape
+    assert rel(y, y_ref) < TOL["bf16"]
+    if s == 1:
+        gy = _q(torch.randn(y_ref.shape, generator=g), "bf16")
+        dx_ref = torch.nn.grad.conv2d_input(x.shape, w, gy, stride=1, padding=p)
+        dx = HF.conv_dgrad_raw(gy.to(DEV), w.to(DEV), tuple(x.shape), 1, p)
+        assert rel(dx, dx_ref) < TOL["bf16"]
+        # fused act' epilogue: dx * relu'(x)
+        dxg = HF.conv_dgrad_raw(gy.to(DEV), w.to(DEV), tuple(x.shape), 1, p, gpre=x.to(DEV), gact="relu")
+        assert rel(dxg, dx_ref * (x > 0)) < TOL["bf16"]
+
+
 @pytest.mark.parametrize("N,C,H,P", [(2, 64, 16, 128), (2, 128, 16, 64), (3, 128, 16, 256), (2, 256, 16, 128),
                                      (1, 128, 32, 64)])
 def test_pw_mlp_fused(N, C, H, P):

@@ -28,6 +28,7 @@ for it in range(reps):
     if s64 is None:
         s32 = T._oracle_step(gp, dp, A, B, torch.float32)
         s64 = T._oracle_step(gp, dp, A, B, torch.float64)
+        sens, _ = T.fp32_sensitivity(gp, dp, A, B)
     for net, o32, o64 in ((m.netG, s32.gp, s64.gp), (m.netD, s32.dp, s64.dp)):
         for (k, p), g32, g64 in zip(net.named_parameters(), o32.values(), o64.values()):
             n64 = g64.grad.norm().item()
@@ -39,6 +40,8 @@ for net, o64 in ((m.netG, s64.gp), (m.netD, s64.dp)):
     for (k, _), g64 in zip(net.named_parameters(), o64.values()):
         norms[k] = g64.grad.norm().item()
 ratios = {k: v for k, v in ratios.items() if norms[k] > 1e-5}   # bias-before-IN grads are ~0
+sensr = {k: v / max(norms[k], 1e-30) for (_, k), v in sens.items()}
 worst = sorted(ratios.items(), key=lambda kv: -max(r[0] for r in kv[1]))[:20]
 for k, rs in worst:
-    print("%-45s ours %s  oracle32 %.2e" % (k, " ".join("%.2e" % r[0] for r in rs), rs[0][1]))
+    print("%-45s ours %s  oracle32 %.2e  fp32-ulp-spread %.2e" % (k, " ".join("%.2e" % r[0] for r in rs), rs[0][1],
+                                                                 sensr.get(k, 0.0)))

@@ -22,13 +22,14 @@ m.optimize_parameters()
 HF.IGEMM_TIMER.on = False
 rows = HF.IGEMM_TIMER.table()
 agg = collections.defaultdict(lambda: [0, 0.0, 0.0])
+fams = HF.IGEMM_TIMER.families()
 for ms, fl, tag in rows:
     a = agg[tag]; a[0] += 1; a[1] += ms; a[2] += fl
 tot = sum(a[1] for a in agg.values())
 print("total igemm ms %.2f over %d launches" % (tot, len(rows)))
-print("%-8s %3s %5s %4s %4s %5s %2s %2s | %4s %8s %7s %7s" % ("mode", "N", "Cin", "H", "W", "Cout", "K", "s", "cnt", "ms", "TF/s", "GB/s*"))
+print("%-8s %3s %5s %4s %4s %5s %2s %2s | %4s %8s %7s %7s  %s" % ("mode", "N", "Cin", "H", "W", "Cout", "K", "s", "cnt", "ms", "TF/s", "GB/s*", "kernel"))
 for tag, (c, ms, fl) in sorted(agg.items(), key=lambda kv: -kv[1][1])[:80]:
-    mode, N, Cin, H, W, Cout, K, s = tag
+    mode, N, Cin, H, W, Cout, K, s, fam = tag
     Ho = (H + 2 * (K // 2 if K != 4 else 1) - K) // s + 1
     # fp32 bytes of the three operands at minimum
     if mode == "fwd":
@@ -37,4 +38,4 @@ for tag, (c, ms, fl) in sorted(agg.items(), key=lambda kv: -kv[1][1])[:80]:
         by = 4 * (N * Cin * H * W + N * Cout * Ho * Ho + Cout * Cin * K * K)
     else:
         by = 4 * (N * Cin * H * W + N * Cout * Ho * Ho)
-    print("%-8s %3d %5d %4d %4d %5d %2d %2d | %4d %8.3f %7.1f %7.0f" % (mode, N, Cin, H, W, Cout, K, s, c, ms, fl / (ms * 1e-3) / 1e12, by * c / (ms * 1e-3) / 1e9))
+    print("%-8s %3d %5d %4d %4d %5d %2d %2d | %4d %8.3f %7.1f %7.0f  %s" % (mode, N, Cin, H, W, Cout, K, s, c, ms, fl / (ms * 1e-3) / 1e12, by * c / (ms * 1e-3) / 1e9, fam))
