@@ -1,0 +1,357 @@
+// Patch-staged weight-gradient of KxK, pad-1 convolutions (gfx950, bf16 MFMA, fp32 accumulate).
+//
+//   dW[m][c][kh][kw] += sum_{b, oh, ow} D[b][m][oh][ow] * X[b][c][oh*S - 1 + kh][ow*S - 1 + kw]
+//
+// Covers the weight-grads of the ConvTranspose2d 3x3/s2 layers (as the equivalent stride-2
+// conv with D = ConvT input, X = ConvT output grad; DSGAN/models/model/MixConvNeXtML.py:53,149-152)
+// and of the PatchGAN 4x4 s2/s1 convs (DSGAN/models/networks.py:543-569).  The reduction runs
+// over N*Ho*Wo pixels into a small output; with fp32 activations these contractions are
+// HBM-bound, so the kernel streams D and X once per (M, C) tile pair (the tiles of one pixel
+// range are adjacent workgroups on one XCD and share the reads in L2).
+//
+// Workgroup = 64 m x 32 c x all T taps, over a run of pixel blocks (4 output rows x 16 columns).
+// Per block:
+//   * D[64 m][64 px] -> LDS bf16, row per m (float4 global loads);
+//   * the 32-channel input patch -> LDS bf16 as S column-parity planes per patch row, plane p
+//     holding X[c][ih0 + r][iw0 + S*j + p] (float4 global loads, paired dword LDS writes;
+//     plane p is stored at element offset OFF_p so every staging write is aligned);
+// MFMA 32x32x16: A = D (m x 16 px of one output row), B = X patch (16 px x c) for one tap.  Tap
+// (kh, kw) of output row r reads plane kw % S of patch row S*r + kh at element shift
+// kw / S + OFF: shift 0 is one aligned 16-byte LDS read, other shifts two reads and a
+// v_alignbit funnel (shifts are compile-time: wave w owns taps w, w+4, ...).
+// Partial sums per split -> workspace [splits][T][M][C]; wconv_reduce sums the splits in a
+// fixed order and accumulates into dW (deterministic, no atomics).
+#include "common.h"
+#include <type_traits>
+
+namespace dsg {
+
+typedef __attribute__((ext_vector_type(8))) __bf16 wbf16x8;
+typedef __attribute__((ext_vector_type(4))) __bf16 wbf16x4;
+typedef __attribute__((ext_vector_type(2))) __bf16 wbf16x2;
+typedef __attribute__((ext_vector_type(16))) float wf32x16;
+typedef __attribute__((ext_vector_type(4))) unsigned int wu32x4;
+
+struct WcArgs {
+  const float* D; long d_bs;   // conv output grad  [nb][M][Ho][Wo]
+  const float* X; long x_bs;   // conv input        [nb][C][H][W]
+  float* P;                    // partials          [splits][T][M][C]
+  int nb, M, C, H, W, Ho, Wo;
+  int nbw, nbh, nblk, bps;     // pixel blocks per row / per column / total, blocks per split
+  int mt, ct;                  // M tiles (64), C tiles (32)
+  int vec_d;                   // D rows float4-loadable
+};
+
+constexpr int WC_TW = 16, WC_TH = 4;
+constexpr int WC_BM = 64, WC_BC = 32;
+constexpr int WC_JW = 24;      // stored elements per plane row (48 B)
+
+template <int S> struct WcGeo;
+// S = 2, pad 1: float4 q of a patch row covers t = col - iw0 = 4q-3 .. 4q; its two odd-t
+// elements are plane 1, j = 2q-2, 2q-1 (stored at j); its even-t elements plane 0,
+// j = 2q-1, 2q (stored at j+1).  Planes hold j = 0..16.
+template <> struct WcGeo<2> {
+  static constexpr int NQ = 10;
+  static constexpr int OFF0 = 1, OFF1 = 0;
+  __device__ static constexpr int shift(int kw) { return (kw >> 1) + ((kw & 1) ? OFF1 : OFF0); }
+};
+// S = 1, pad 1: one plane, t = 4q-3+e stored at t+3 = 4q+e; holds t = 0..18.
+template <> struct WcGeo<1> {
+  static constexpr int NQ = 6;
+  __device__ static constexpr int shift(int kw) { return kw + 3; }
+};
+
+// 8 consecutive bf16 starting SH elements after the 16-byte aligned p.
+template <int SH>
+__device__ __forceinline__ wbf16x8 frag_at(const __bf16* p) {
+  if constexpr (SH == 0) {
+    return *reinterpret_cast<const wbf16x8*>(p);
+  } else {
+    const wu32x4 a = *reinterpret_cast<const wu32x4*>(p);
+    const wu32x4 b = *reinterpret_cast<const wu32x4*>(p + 8);
+    const unsigned d[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+    constexpr int q = SH >> 1;
+    wu32x4 r;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      r[i] = (SH & 1) ? __builtin_amdgcn_alignbit(d[q + i + 1], d[q + i], 16) : d[q + i];
+    return __builtin_bit_cast(wbf16x8, r);
+  }
+}
+
+template <int KH, int KW, int S>
+__global__ __launch_bounds__(256, 1) void wconv_kernel(WcArgs g) {
+  constexpr int T = KH * KW, NT4 = (T + 3) / 4;
+  constexpr int PX = WC_TH * WC_TW;
+  constexpr int PH = (WC_TH - 1) * S + KH;
+  constexpr int NQ = WcGeo<S>::NQ;
+  constexpr int A_STR = PX + 8;                           // bf16 per m row; /8 odd -> conflict-free b128
+  static_assert(((A_STR / 8) & 1) == 1, "A row stride");
+  constexpr int C_DW0 = PH * S * (WC_JW / 2);             // dwords per channel
+  constexpr int C_DW = ((C_DW0 / 4) & 1) ? C_DW0 : C_DW0 + 4;
+  constexpr int C_STR = C_DW * 2;                         // bf16 per channel
+  constexpr int A_IT = WC_BM * PX / 4 / 256;              // float4 items per thread
+  constexpr int B_ITEMS = WC_BC * PH * NQ;                // (c, patch row, float4) items
+  constexpr int B_IT = (B_ITEMS + 255) / 256;
+  static_assert(A_IT * 256 * 4 == WC_BM * PX, "A items");
+  __shared__ __attribute__((aligned(16))) __bf16 As[WC_BM * A_STR];
+  __shared__ __attribute__((aligned(16))) __bf16 Bs[WC_BC * C_STR];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int lr = lane & 31, lh = lane >> 5;
+
+  int tile;
+  {
+    const int nwg = gridDim.x, id = blockIdx.x;
+    const int xcd = id & 7, q = nwg >> 3, r = nwg & 7;
+    tile = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (id >> 3);
+  }
+  const int ntile = g.mt * g.ct;
+  const int split = tile / ntile, tmc = tile - split * ntile;
+  const int m_t = tmc % g.mt, c_t = tmc / g.mt;
+  const int m0 = m_t * WC_BM, c0 = c_t * WC_BC;
+  const int qbeg = split * g.bps;
+  const int qend = min(g.nblk, qbeg + g.bps);
+  const int HWo = g.Ho * g.Wo, HW = g.H * g.W;
+  const int per_img = g.nbh * g.nbw;
+
+  float4 ra[A_IT], rb[B_IT];
+
+  auto load = [&](int q) __attribute__((always_inline)) {
+    const int b = q / per_img, rem = q - b * per_img;
+    const int oh0 = (rem / g.nbw) * WC_TH, ow0 = (rem % g.nbw) * WC_TW;
+    const float* db = g.D + (long)b * g.d_bs;
+#pragma unroll
+    for (int i = 0; i < A_IT; ++i) {
+      const int it = tid + i * 256, mm = it / (PX / 4), qq = it % (PX / 4);
+      const int oh = oh0 + (qq >> 2), ow = ow0 + (qq & 3) * 4;
+      float4 v = {0.f, 0.f, 0.f, 0.f};
+      if (m0 + mm < g.M && oh < g.Ho) {
+        const float* src = db + (long)(m0 + mm) * HWo + (long)oh * g.Wo + ow;
+        if (g.vec_d && ow + 3 < g.Wo) {
+          v = *reinterpret_cast<const float4*>(src);
+        } else {
+          if (ow < g.Wo) v.x = src[0];
+          if (ow + 1 < g.Wo) v.y = src[1];
+          if (ow + 2 < g.Wo) v.z = src[2];
+          if (ow + 3 < g.Wo) v.w = src[3];
+        }
+      }
+      ra[i] = v;
+    }
+    // input patch rows: float4 q covers cols a0 + 4q .. a0 + 4q + 3, a0 = iw0 - 3 (16-byte aligned)
+    const float* xb = g.X + (long)b * g.x_bs;
+    const int ih0 = oh0 * S - 1, a0 = ow0 * S - 4;
+#pragma unroll
+    for (int i = 0; i < B_IT; ++i) {
+      const int it = tid + i * 256;
+      const int q4 = it % NQ, rest = it / NQ;
+      const int pr = rest % PH, c = rest / PH;
+      const int ih = ih0 + pr, col = a0 + 4 * q4;
+      float4 v = {0.f, 0.f, 0.f, 0.f};
+      if (it < B_ITEMS && (unsigned)ih < (unsigned)g.H && (unsigned)col < (unsigned)g.W)
+        v = *reinterpret_cast<const float4*>(xb + (long)(c0 + c) * HW + (long)ih * g.W + col);
+      rb[i] = v;
+    }
+  };
+  auto store = [&]() __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < A_IT; ++i) {
+      const int it = tid + i * 256, mm = it / (PX / 4), qq = it % (PX / 4);
+      const wbf16x4 v = {(__bf16)ra[i].x, (__bf16)ra[i].y, (__bf16)ra[i].z, (__bf16)ra[i].w};
+      *reinterpret_cast<wbf16x4*>(As + mm * A_STR + qq * 4) = v;
+    }
+#pragma unroll
+    for (int i = 0; i < B_IT; ++i) {
+      const int it = tid + i * 256;
+      if (it < B_ITEMS) {
+        const int q4 = it % NQ, rest = it / NQ;
+        const int pr = rest % PH, c = rest / PH;
+        __bf16* row = Bs + c * C_STR + pr * (S * WC_JW);
+        if constexpr (S == 2) {
+          // plane 1 <- (x, z) at j = 2q-2 (skip q = 0: j < 0); plane 0 <- (y, w) stored at 2q
+          if (q4 > 0) *reinterpret_cast<wbf16x2*>(row + WC_JW + 2 * q4 - 2) = wbf16x2{(__bf16)rb[i].x, (__bf16)rb[i].z};
+          *reinterpret_cast<wbf16x2*>(row + 2 * q4) = wbf16x2{(__bf16)rb[i].y, (__bf16)rb[i].w};
+        } else {
+          *reinterpret_cast<wbf16x4*>(row + 4 * q4) =
+              wbf16x4{(__bf16)rb[i].x, (__bf16)rb[i].y, (__bf16)rb[i].z, (__bf16)rb[i].w};
+        }
+      }
+    }
+  };
+
+  // Each wave runs its own instantiation of the block loop: wave WV owns taps WV, WV+4, ...,
+  // so every tap's plane and shift are compile-time (the barriers are reached by all four
+  // waves once per block in every instantiation).
+  auto run = [&](auto wtag) __attribute__((always_inline)) {
+    constexpr int WV = decltype(wtag)::value;
+    wf32x16 acc[2][NT4];
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int i = 0; i < NT4; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[s][i][r] = 0.f;
+
+    if (qbeg < qend) load(qbeg);
+    for (int q = qbeg; q < qend; ++q) {
+      __syncthreads();   // LDS free (previous block consumed)
+      store();
+      __syncthreads();
+      if (q + 1 < qend) load(q + 1);
+#pragma unroll
+      for (int r = 0; r < WC_TH; ++r) {
+        const wbf16x8 a0 = *reinterpret_cast<const wbf16x8*>(As + lr * A_STR + r * 16 + lh * 8);
+        const wbf16x8 a1 = *reinterpret_cast<const wbf16x8*>(As + (32 + lr) * A_STR + r * 16 + lh * 8);
+#pragma unroll
+        for (int i = 0; i < NT4; ++i) {
+          if (WV + 4 * i < T) {
+            const int t = WV + 4 * i, kh = t / KW, kw = t % KW;
+            const __bf16* row = Bs + lr * C_STR + (S * r + kh) * (S * WC_JW) + (kw % S) * WC_JW + lh * 8;
+            wbf16x8 bf;
+            switch (WcGeo<S>::shift(kw)) {   // folds: t, kw are compile-time after unrolling
+              case 0: bf = frag_at<0>(row); break;
+              case 1: bf = frag_at<1>(row); break;
+              case 2: bf = frag_at<2>(row); break;
+              case 3: bf = frag_at<3>(row); break;
+              case 4: bf = frag_at<4>(row); break;
+              case 5: bf = frag_at<5>(row); break;
+              default: bf = frag_at<6>(row); break;
+            }
+            acc[0][i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, bf, acc[0][i], 0, 0, 0);
+            acc[1][i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, bf, acc[1][i], 0, 0, 0);
+          }
+        }
+      }
+    }
+
+    // partials: P[split][t][m][c], lanes along c (coalesced)
+    const int c = c0 + lr;
+#pragma unroll
+    for (int i = 0; i < NT4; ++i) {
+      const int t = WV + 4 * i;
+      if (t < T) {
+        float* pt = g.P + ((long)split * T + t) * g.M * g.C;
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int m = m0 + s * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+            if (m < g.M) pt[(long)m * g.C + c] = acc[s][i][r];
+          }
+      }
+    }
+  };
+  switch (wave) {
+    case 0: run(std::integral_constant<int, 0>{}); break;
+    case 1: run(std::integral_constant<int, 1>{}); break;
+    case 2: run(std::integral_constant<int, 2>{}); break;
+    default: run(std::integral_constant<int, 3>{}); break;
+  }
+}
+
+// dW[m][c][t] += sum_s P[s][t][m][c] for 4 consecutive c per thread (fixed split order:
+// deterministic); 4 independent partial sums keep several loads in flight.
+__global__ void wconv_reduce_kernel(const float* __restrict__ P, int splits, int T, int M, int C,
+                                    float* __restrict__ dw) {
+  const long total = (long)T * M * C, total4 = total / 4;
+  for (long e4 = blockIdx.x * 256L + threadIdx.x; e4 < total4; e4 += (long)gridDim.x * 256) {
+    const float4* p = reinterpret_cast<const float4*>(P) + e4;
+    float4 s[4] = {};
+    int sp = 0;
+    for (; sp + 4 <= splits; sp += 4) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const float4 v = p[(long)(sp + u) * total4];
+        s[u].x += v.x; s[u].y += v.y; s[u].z += v.z; s[u].w += v.w;
+      }
+    }
+    for (; sp < splits; ++sp) {
+      const float4 v = p[(long)sp * total4];
+      s[0].x += v.x; s[0].y += v.y; s[0].z += v.z; s[0].w += v.w;
+    }
+    const float r[4] = {(s[0].x + s[1].x) + (s[2].x + s[3].x), (s[0].y + s[1].y) + (s[2].y + s[3].y),
+                        (s[0].z + s[1].z) + (s[2].z + s[3].z), (s[0].w + s[1].w) + (s[2].w + s[3].w)};
+    const long e = e4 * 4;
+    const int c = e % C;
+    const long rr = e / C;
+    const int m = rr % M, t = rr / M;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) dw[((long)m * C + c + u) * T + t] += r[u];
+  }
+}
+
+constexpr int WC_TARGET_WG = 256;   // one resident workgroup per CU (next block prefetched into registers)
+
+struct WcPlan { int nbw, nbh, nblk, mt, ct, splits, bps; };
+
+static WcPlan wc_plan(int nb, int C, int M, int Ho, int Wo) {
+  WcPlan p;
+  p.nbw = (Wo + WC_TW - 1) / WC_TW;
+  p.nbh = (Ho + WC_TH - 1) / WC_TH;
+  p.nblk = nb * p.nbw * p.nbh;
+  p.mt = (M + WC_BM - 1) / WC_BM;
+  p.ct = C / WC_BC;
+  const int tiles = p.mt * p.ct;
+  int splits = (WC_TARGET_WG + tiles - 1) / tiles;
+  if (splits > p.nblk) splits = p.nblk;
+  if (splits < 1) splits = 1;
+  p.bps = (p.nblk + splits - 1) / splits;
+  p.splits = (p.nblk + p.bps - 1) / p.bps;   // no empty splits
+  return p;
+}
+
+template <int K, int S>
+static void wc_launch(WcArgs& g, int grid, hipStream_t st) {
+  hipLaunchKernelGGL((wconv_kernel<K, K, S>), dim3((unsigned)grid), dim3(256), 0, st, g);
+}
+
+}  // namespace dsg
+
+using namespace dsg;
+
+extern "C" {
+
+int dsgan_wconv_supported(int C, int KH, int KW, int stride) {
+  if (C <= 0 || C % WC_BC != 0 || KH != KW) return 0;
+  return (KH == 3 || KH == 4) && (stride == 1 || stride == 2);
+}
+
+// fp32 workspace elements dsgan_wconv needs for this problem
+long dsgan_wconv_workspace(int nb, int C, int M, int Ho, int Wo, int KH, int KW) {
+  const WcPlan p = wc_plan(nb, C, M, Ho, Wo);
+  return (long)p.splits * KH * KW * M * C;
+}
+
+// dw[M][C][KH][KW] += weight-grad of y = conv(x, w, stride, pad = 1): D = dy [nb][M][Ho][Wo],
+// X = x [nb][C][H][W] (batch strides d_bs / x_bs; X 16-byte aligned rows: W % 4 == 0);
+// ws: dsgan_wconv_workspace() floats.
+int dsgan_wconv(const float* D, long d_bs, const float* X, long x_bs, float* dw, float* ws, int nb, int C, int M,
+                int H, int W, int Ho, int Wo, int KH, int KW, int stride, int pad, hipStream_t st) {
+  DSG_REQUIRE(D && X && dw && ws && nb > 0 && M > 0 && Ho > 0 && Wo > 0, "dsgan_wconv: bad args");
+  DSG_REQUIRE(dsgan_wconv_supported(C, KH, KW, stride) && pad == 1, "dsgan_wconv: unsupported C=%d K=%dx%d stride=%d pad=%d",
+              C, KH, KW, stride, pad);
+  DSG_REQUIRE(W % 4 == 0 && x_bs % 4 == 0 && ((uintptr_t)X & 15) == 0, "dsgan_wconv: X rows must be 16-byte aligned");
+  DSG_REQUIRE((Ho - 1) * stride - pad + KH <= H + pad && (Wo - 1) * stride - pad + KW <= W + pad,
+              "dsgan_wconv: output size inconsistent with input/pad");
+  const WcPlan p = wc_plan(nb, C, M, Ho, Wo);
+  WcArgs g{};
+  g.D = D; g.d_bs = d_bs; g.X = X; g.x_bs = x_bs; g.P = ws;
+  g.nb = nb; g.M = M; g.C = C; g.H = H; g.W = W; g.Ho = Ho; g.Wo = Wo;
+  g.nbw = p.nbw; g.nbh = p.nbh; g.nblk = p.nblk; g.bps = p.bps; g.mt = p.mt; g.ct = p.ct;
+  g.vec_d = ((uintptr_t)D % 16 == 0) && (d_bs % 4 == 0) && (Wo % 4 == 0);
+  const int grid = p.splits * p.mt * p.ct;
+  if (KH == 3 && stride == 2) wc_launch<3, 2>(g, grid, st);
+  else if (KH == 3 && stride == 1) wc_launch<3, 1>(g, grid, st);
+  else if (KH == 4 && stride == 2) wc_launch<4, 2>(g, grid, st);
+  else wc_launch<4, 1>(g, grid, st);
+  DSG_CHECK_LAUNCH();
+  const long total4 = (long)KH * KW * M * C / 4;
+  long blocks = (total4 + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(wconv_reduce_kernel, dim3((unsigned)blocks), dim3(256), 0, st, ws, p.splits, KH * KW, M, C, dw);
+  DSG_CHECK_LAUNCH();
+  return 0;
+}
+
+}  // extern "C"

@@ -39,6 +39,10 @@ SIGNATURES = {
     "dsgan_pconv_supported": [I, I, I, I],
     "dsgan_conv_wtrans_bf16": [P, P, I, I, I, I, I, S],
     "dsgan_pconv": [P, L, P, P, P, L, P, L] + [I] * 13 + [F, I, S],
+    # wconv.hip
+    "dsgan_wconv_supported": [I, I, I, I],
+    "dsgan_wconv_workspace": [I, I, I, I, I, I, I],
+    "dsgan_wconv": [P, L, P, L, P, P] + [I] * 11 + [S],
     # tconv.hip
     "dsgan_conv_wtrans": [P, P, I, I, I, I, I, I, I, I, I, S],
     "dsgan_tconv": [P, L, P, P, P, L, P, L] + [I] * 9 + [P, P] + [I] * 7 + [F, S],
@@ -92,7 +96,8 @@ def load():
     for name, argtypes in SIGNATURES.items():
         fn = getattr(lib, name)
         fn.argtypes = argtypes
-        fn.restype = ctypes.c_char_p if name == "dsgan_last_error_string" else ctypes.c_int
+        fn.restype = (ctypes.c_char_p if name == "dsgan_last_error_string"
+                      else ctypes.c_long if name.endswith("_workspace") else ctypes.c_int)
     _lib = lib
     return lib
 

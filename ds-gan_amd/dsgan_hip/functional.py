@@ -9,6 +9,7 @@ the Functions therefore return ``None`` for parameters.  A parameter whose ``req
 False (the frozen VGG16, or D during the G step, DSGAN/models/base_model.py:171-177) gets no
 weight-grad launch at all.
 """
+import contextlib
 import math
 
 import torch
@@ -326,6 +327,14 @@ def conv_wgrad_raw(dy, x, dw, stride, pad, xact=None):
         fam = "pwgemm_kernel"
         call("dsgan_pw_gemm", 2, ptr(dy), dybs, ptr(x), xbs, ptr(dw), 0, None, None, 0, None, 0,
              Cout, Cin, N * H * W, H * W, N, 0, 0, ACT[xact], 0, LRELU_SLOPE, stream())
+    elif (xact is None and _state["prec"] == "bf16" and dw.is_contiguous() and pad == 1 and W % 4 == 0
+          and xbs % 4 == 0 and x.data_ptr() % 16 == 0 and _lib.load().dsgan_wconv_supported(Cin, KH, KW, stride)):
+        fam = "wconv_kernel"
+        Ho, Wo = dy.shape[2], dy.shape[3]
+        ws = torch.empty(_lib.load().dsgan_wconv_workspace(N, Cin, Cout, Ho, Wo, KH, KW), device=dy.device,
+                         dtype=torch.float32)
+        call("dsgan_wconv", ptr(dy), dybs, ptr(x), xbs, ptr(dw), ptr(ws), N, Cin, Cout, H, W, Ho, Wo, KH, KW,
+             stride, pad, stream())
     else:
         call("dsgan_conv_wgrad", ptr(dy), dybs, ptr(x), xbs, ptr(dw), N, Cin, H, W, Cout, KH, KW,
              stride, pad, dy.shape[2], dy.shape[3], ACT[xact], _prec(), stream())
@@ -377,6 +386,7 @@ class Conv2dFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, b, stride, pad, act):
         y = conv_fwd_raw(x, w, b, stride, pad, act)
+        ctx.prec = _state["prec"]
         ctx.stride, ctx.pad, ctx.act = stride, pad, act
         ctx.x_shape = tuple(x.shape)
         ctx.save_for_backward(x, w, b, y if act in ("relu", "lrelu") else None)
@@ -385,6 +395,11 @@ class Conv2dFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy):
+        with precision(ctx.prec):
+            return Conv2dFn._backward(ctx, dy)
+
+    @staticmethod
+    def _backward(ctx, dy):
         x, w, b, y = ctx.saved_tensors
         if ctx.act in ("relu", "lrelu"):
             dy = act_bwd_raw(dy, y, ctx.act)  # sign(y) == sign(pre) for relu/lrelu
@@ -416,12 +431,18 @@ class ConvT3s2Fn(torch.autograd.Function):
         N, Ci, Hi, Wi = x.shape
         Co = w.shape[1]
         y = conv_dgrad_raw(x, w, (N, Co, 2 * Hi, 2 * Wi), 2, 1, bias=b)
+        ctx.prec = _state["prec"]
         ctx.save_for_backward(x, w, b)
         ctx.w_ref, ctx.b_ref = w, b
         return y
 
     @staticmethod
     def backward(ctx, dy):
+        with precision(ctx.prec):
+            return ConvT3s2Fn._backward(ctx, dy)
+
+    @staticmethod
+    def _backward(ctx, dy):
         x, w, b = ctx.saved_tensors
         dx = conv_fwd_raw(dy, w, None, 2, 1) if ctx.needs_input_grad[0] else None
         gw = _grad_buf(ctx.w_ref) if ctx.needs_input_grad[1] else None
@@ -492,6 +513,7 @@ class PwMlpFn(torch.autograd.Function):
         tile = _mlp_tile(h, x, P)
         ctx.refs = (w1, b1, w2, b2, ws)
         ctx.tile = tile
+        ctx.prec = _state["prec"]
         if tile:
             out = conv_fwd_raw(x, ws, None, 1, 0)
             e0 = IGEMM_TIMER.begin()
@@ -510,8 +532,13 @@ class PwMlpFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy):
-        if ctx.tile:
-            return PwMlpFn._backward_fused(ctx, dy)
+        with precision(ctx.prec):
+            if ctx.tile:
+                return PwMlpFn._backward_fused(ctx, dy)
+            return PwMlpFn._backward_unfused(ctx, dy)
+
+    @staticmethod
+    def _backward_unfused(ctx, dy):
         h, x, z, w1v, w2v, ws = ctx.saved_tensors
         w1, b1, w2, b2, ws_ref = ctx.refs
         dy = dy.contiguous()

@@ -141,6 +141,19 @@ int dsgan_pconv(const float* X, long x_bs, const void* Wb, const float* bias, fl
                 int KH, int KW, int stride, int pad, int act, int gact, float slope, int accumulate,
                 hipStream_t stream);
 
+/* ---- patch-staged conv weight-grad (wconv.hip): ConvTranspose2d 3x3/s2 weight-grads
+ * (MixConvNeXtML.py:53,149-152, as the equivalent stride-2 conv) and PatchGAN 4x4 s2/s1
+ * (DSGAN/models/networks.py:543-569) -- replaces the weight-grad half of torch's
+ * convolution_backward for these layers.
+ * dw[M][C][KH][KW] += sum_{b,oh,ow} D[b][m][oh][ow] * X[b][c][oh*s-pad+kh][ow*s-pad+kw], bf16 MFMA,
+ * C % 32 == 0.  ws: dsgan_wconv_workspace() fp32 elements (per-split partials, reduced in fixed
+ * order: deterministic). */
+int dsgan_wconv_supported(int C, int KH, int KW, int stride);
+long dsgan_wconv_workspace(int nb, int C, int M, int Ho, int Wo, int KH, int KW);
+int dsgan_wconv(const float* D, long d_bs, const float* X, long x_bs, float* dw, float* ws, int nb,
+                int C, int M, int H, int W, int Ho, int Wo, int KH, int KW, int stride, int pad,
+                hipStream_t stream);
+
 /* ---- depthwise conv (dwconv.hip): Block.dwconv :220, MidMLKA.X3..X9 :94-97 ----------------
  * y (+)= dwconv_KxK(x, w) + bias; flip = 1 with bias = NULL is the data-grad; accumulate adds into
  * y (data-grad of a tensor with a second consumer; needs 16-byte aligned rows, W % 4 == 0). */

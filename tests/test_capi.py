@@ -13,7 +13,7 @@ def _header_decls():
     txt = open(HEADER).read()
     txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
     decls = {}
-    for m in re.finditer(r"\b(?:int|const char\*)\s+(dsgan_\w+)\s*\(([^)]*)\)\s*;", txt):
+    for m in re.finditer(r"\b(?:int|long|const char\*)\s+(dsgan_\w+)\s*\(([^)]*)\)\s*;", txt):
         args = [a.strip() for a in m.group(2).split(",") if a.strip() and a.strip() != "void"]
         decls[m.group(1)] = len(args)
     return decls

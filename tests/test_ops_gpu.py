@@ -182,6 +182,40 @@ def test_pconv_bf16(N, Cin, H, W, Cout, K, s, p, act):
         assert rel(dxg, dx_ref * (x > 0)) < TOL["bf16"]
 
 
+@pytest.mark.parametrize("N,C,H,W,M,K,s,p", [
+    (2, 64, 32, 32, 128, 3, 2, 1),      # ConvT u4 / local.up4 weight-grad class (as the s2 conv)
+    (1, 128, 20, 36, 256, 3, 2, 1),     # ragged: 10x18 output pixels vs 4x16 blocks
+    (3, 32, 16, 16, 96, 3, 2, 1),       # M not a multiple of the 64 tile
+    (2, 32, 34, 36, 64, 4, 2, 1),       # PatchGAN 4x4 s2 (17x18 output)
+    (2, 128, 9, 12, 256, 4, 1, 1),      # PatchGAN 4x4 s1 (output 8x11)
+    (2, 64, 12, 16, 64, 3, 1, 1),       # 3x3 s1
+])
+def test_wconv_bf16(N, C, H, W, M, K, s, p):
+    """Patch-staged weight-grad (wconv.hip) vs torch's conv2d_weight on the bf16-rounded operands;
+    accumulates into the existing gradient; deterministic (fixed-order split reduction)."""
+    from dsgan_hip import functional as HF
+    HF.set_precision("bf16")
+    g = torch.Generator().manual_seed(C + M + K + H)
+    x = _q(torch.randn(N, C, H, W, generator=g), "bf16")
+    Ho, Wo = (H + 2 * p - K) // s + 1, (W + 2 * p - K) // s + 1
+    dy = _q(torch.randn(N, M, Ho, Wo, generator=g), "bf16")
+    dw_ref = torch.nn.grad.conv2d_weight(x.double(), (M, C, K, K), dy.double(), stride=s, padding=p)
+    w0 = torch.randn(M, C, K, K, generator=g)
+    dw = w0.to(DEV)
+    HF.IGEMM_TIMER.rec, HF.IGEMM_TIMER.on = [], True
+    try:
+        HF.conv_wgrad_raw(dy.to(DEV), x.to(DEV), dw, s, p)
+    finally:
+        HF.IGEMM_TIMER.on = False
+    assert HF.IGEMM_TIMER.rec[-1][4] == "wconv_kernel"
+    assert rel(dw - w0.to(DEV), dw_ref) < 1e-5
+    # channel-slice inputs (batch stride != C*H*W) and determinism
+    xb = torch.cat([x, torch.randn(N, 32, H, W, generator=g)], 1).to(DEV)[:, :C]
+    dw2 = w0.to(DEV)
+    HF.conv_wgrad_raw(dy.to(DEV), xb, dw2, s, p)
+    assert torch.equal(dw, dw2)
+
+
 @pytest.mark.parametrize("N,C,H,P", [(2, 64, 16, 128), (2, 128, 16, 64), (3, 128, 16, 256), (2, 256, 16, 128),
                                      (1, 128, 32, 64)])
 def test_pw_mlp_fused(N, C, H, P):
