@@ -19,7 +19,7 @@ __global__ __launch_bounds__(256) void dwconv_fwd_kernel(const float* __restrict
                                                          const float* __restrict__ w,
                                                          const float* __restrict__ bias,
                                                          float* __restrict__ y, long y_bs, int C,
-                                                         int H, int W, int flip, int tiles_w) {
+                                                         int H, int W, int flip, int tiles_w, int accumulate) {
   __shared__ float tile[DW_HALO][DW_HALO + 1];
   __shared__ float wk[DW_MAXK * DW_MAXK];
   const int plane = blockIdx.y;                 // n * C + c
@@ -56,7 +56,7 @@ __global__ __launch_bounds__(256) void dwconv_fwd_kernel(const float* __restrict
 #pragma unroll
   for (int s = 0; s < 4; ++s) {
     const int oh = th0 + r0 + s;
-    if (oh < H && ow < W) yp[(long)oh * W + ow] = acc[s];
+    if (oh < H && ow < W) yp[(long)oh * W + ow] = accumulate ? yp[(long)oh * W + ow] + acc[s] : acc[s];
   }
 }
 
@@ -394,14 +394,13 @@ int dsgan_dwconv_fwd(const float* x, long x_bs, const float* w, const float* bia
     DSG_CHECK_LAUNCH();
     return 0;
   }
-  DSG_REQUIRE(!accumulate, "dsgan_dwconv_fwd: accumulate needs a 16-byte aligned plane of width %% 4 == 0");
   const int tw = cdiv(W, DW_T), th = cdiv(H, DW_T);
   const dim3 grid(tw * th, N * C);
   switch (K) {
-    case 3: hipLaunchKernelGGL(dwconv_fwd_kernel<3>, grid, dim3(256), 0, st, x, x_bs, w, bias, y, y_bs, C, H, W, flip, tw); break;
-    case 5: hipLaunchKernelGGL(dwconv_fwd_kernel<5>, grid, dim3(256), 0, st, x, x_bs, w, bias, y, y_bs, C, H, W, flip, tw); break;
-    case 7: hipLaunchKernelGGL(dwconv_fwd_kernel<7>, grid, dim3(256), 0, st, x, x_bs, w, bias, y, y_bs, C, H, W, flip, tw); break;
-    case 9: hipLaunchKernelGGL(dwconv_fwd_kernel<9>, grid, dim3(256), 0, st, x, x_bs, w, bias, y, y_bs, C, H, W, flip, tw); break;
+    case 3: hipLaunchKernelGGL(dwconv_fwd_kernel<3>, grid, dim3(256), 0, st, x, x_bs, w, bias, y, y_bs, C, H, W, flip, tw, accumulate); break;
+    case 5: hipLaunchKernelGGL(dwconv_fwd_kernel<5>, grid, dim3(256), 0, st, x, x_bs, w, bias, y, y_bs, C, H, W, flip, tw, accumulate); break;
+    case 7: hipLaunchKernelGGL(dwconv_fwd_kernel<7>, grid, dim3(256), 0, st, x, x_bs, w, bias, y, y_bs, C, H, W, flip, tw, accumulate); break;
+    case 9: hipLaunchKernelGGL(dwconv_fwd_kernel<9>, grid, dim3(256), 0, st, x, x_bs, w, bias, y, y_bs, C, H, W, flip, tw, accumulate); break;
     default: DSG_REQUIRE(false, "dsgan_dwconv_fwd: K must be 3, 5, 7 or 9");
   }
   DSG_CHECK_LAUNCH();

@@ -66,6 +66,54 @@ __global__ __launch_bounds__(256) void tv_fwd_kernel(const float* y, long planes
   if (threadIdx.x == 0) atomicAdd(out, s * coef);
 }
 __device__ __forceinline__ float sgnf(float d) { return d > 0.f ? 1.f : (d < 0.f ? -1.f : 0.f); }
+
+// ---- VGG perceptual tap backward (DSGAN/models/vgg.py:30-42 + pix2pix_model.py:182-186) -----
+// Gradient w.r.t. the pre-ReLU activation of a tapped VGG conv whose post-ReLU output y is both
+// an L1 feature (vs the real-image feature r) and the input of a 2x2 MaxPool (or the top):
+//   dx = (maxpool_bwd(dpool, idx) + g*coef*sign(y - r)) * (y > 0)
+// fusing the L1 backward, the autograd sum of the two consumers' grads and the ReLU backward.
+// y, r, dx: contiguous [planes][H][W]; dpool/idx: [planes][H/2][W/2] (plane-flat argmax).
+__global__ void vgg_tap_bwd_pool_kernel(const float* __restrict__ dpool, const int* __restrict__ idx,
+                                        const float* __restrict__ y, const float* __restrict__ r, long npool,
+                                        int H, int W, const float* __restrict__ gout, float coef,
+                                        float* __restrict__ dx) {
+  const float g = gout[0] * coef;
+  const int Wo = W / 2, Po = (H / 2) * Wo;
+  for (long o = blockIdx.x * 256L + threadIdx.x; o < npool; o += (long)gridDim.x * 256) {
+    const long plane = o / Po;
+    const int p = (int)(o - plane * Po), oh = p / Wo, ow = p - oh * Wo;
+    const int id = idx[o];
+    const float gp = dpool[o];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int rb = (2 * oh + i) * W + 2 * ow;
+      const long e = plane * H * W + rb;
+      const float2 yv = *reinterpret_cast<const float2*>(y + e);
+      const float2 rv = *reinterpret_cast<const float2*>(r + e);
+      float2 v;
+      v.x = (rb == id ? gp : 0.f) + g * sgnf(yv.x - rv.x);
+      v.y = (rb + 1 == id ? gp : 0.f) + g * sgnf(yv.y - rv.y);
+      v.x = yv.x > 0.f ? v.x : 0.f;
+      v.y = yv.y > 0.f ? v.y : 0.f;
+      *reinterpret_cast<float2*>(dx + e) = v;
+    }
+  }
+}
+// top tap (no pool above): dx = g*coef*sign(y - r) * (y > 0)
+__global__ void vgg_tap_bwd_top_kernel(const float* __restrict__ y, const float* __restrict__ r, long n4,
+                                       const float* __restrict__ gout, float coef, float* __restrict__ dx) {
+  const float g = gout[0] * coef;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n4; i += (long)gridDim.x * 256) {
+    const float4 yv = reinterpret_cast<const float4*>(y)[i];
+    const float4 rv = reinterpret_cast<const float4*>(r)[i];
+    float4 v;
+    v.x = yv.x > 0.f ? g * sgnf(yv.x - rv.x) : 0.f;
+    v.y = yv.y > 0.f ? g * sgnf(yv.y - rv.y) : 0.f;
+    v.z = yv.z > 0.f ? g * sgnf(yv.z - rv.z) : 0.f;
+    v.w = yv.w > 0.f ? g * sgnf(yv.w - rv.w) : 0.f;
+    reinterpret_cast<float4*>(dx)[i] = v;
+  }
+}
 __global__ void tv_bwd_kernel(const float* y, long planes, int H, int W, const float* gout, float coef, float* dy, int accumulate) {
   const float g = gout[0] * coef;
   const long n = planes * H * W;
@@ -246,6 +294,28 @@ int dsgan_l1_fwd(const float* a, const float* b, long n, float* out, hipStream_t
 int dsgan_l1_bwd(const float* a, const float* b, long n, const float* gout, float* da,
                  int accumulate, hipStream_t st) {
   hipLaunchKernelGGL(l1_bwd_kernel, dim3(red_grid(n) * 8), dim3(256), 0, st, a, b, n, gout, 1.f / (float)n, da, accumulate);
+  DSG_CHECK_LAUNCH();
+  return 0;
+}
+// dx = (maxpool_bwd(dpool, idx) [dpool != NULL] + gout*sign(y - r)/n) * (y > 0), n = planes*H*W
+int dsgan_vgg_tap_bwd(const float* dpool, const int* idx, const float* y, const float* r, float* dx, long planes,
+                      int H, int W, const float* gout, hipStream_t st) {
+  DSG_REQUIRE(y && r && dx && gout && planes > 0 && H > 0 && W > 0, "dsgan_vgg_tap_bwd: bad args");
+  const long n = planes * H * W;
+  const float coef = 1.f / (float)n;
+  if (dpool) {
+    DSG_REQUIRE(idx && H % 2 == 0 && W % 2 == 0, "dsgan_vgg_tap_bwd: pool needs idx and even H, W");
+    const long np = n / 4;
+    long blocks = (np + 255) / 256;
+    if (blocks > 16384) blocks = 16384;
+    hipLaunchKernelGGL(vgg_tap_bwd_pool_kernel, dim3((unsigned)blocks), dim3(256), 0, st, dpool, idx, y, r, np, H, W,
+                       gout, coef, dx);
+  } else {
+    DSG_REQUIRE(n % 4 == 0, "dsgan_vgg_tap_bwd: top tap needs numel % 4 == 0");
+    long blocks = (n / 4 + 255) / 256;
+    if (blocks > 16384) blocks = 16384;
+    hipLaunchKernelGGL(vgg_tap_bwd_top_kernel, dim3((unsigned)blocks), dim3(256), 0, st, y, r, n / 4, gout, coef, dx);
+  }
   DSG_CHECK_LAUNCH();
   return 0;
 }

@@ -72,6 +72,7 @@ SIGNATURES = {
     "dsgan_bce_logits_bwd": [P, L, F, P, P, I, S],
     "dsgan_l1_fwd": [P, P, L, P, S],
     "dsgan_l1_bwd": [P, P, L, P, P, I, S],
+    "dsgan_vgg_tap_bwd": [P, P, P, P, P, L, I, I, P, S],
     "dsgan_tv_fwd": [P, L, I, I, F, P, S],
     "dsgan_tv_bwd": [P, L, I, I, F, P, P, I, S],
     "dsgan_ssim_fwd": [P, P, F, F, I, I, I, P, F, F, P, P, S],

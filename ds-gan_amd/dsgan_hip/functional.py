@@ -270,10 +270,10 @@ def conv_dgrad_raw(dy, w, x_shape, stride, pad, bias=None, act=None, gpre=None, 
         call("dsgan_conv_small_out", ptr(dy), dybs, ptr(w), KH * KW, Cin * KH * KW, KW, 1, ptr(bias),
              ptr(dx), dxbs, N, Cout, Cin, Ho, Wo, H, W, KH, KW, stride, pad, 1, int(accumulate), stream())
     elif (KH == 1 and KW == 1 and stride == 1 and pad == 0 and bias is None and act is None
-            and not accumulate and _pw_ok(1, Cin, Cout, H * W, 0, dybs, w.data_ptr(), dy.data_ptr())):
+            and _pw_ok(1, Cin, Cout, H * W, 0, dybs, w.data_ptr(), dy.data_ptr())):
         fam = "pwgemm_kernel"
         call("dsgan_pw_gemm", 1, ptr(w), 0, ptr(dy), dybs, ptr(dx), dxbs, None, None, 0, ptr(gpre), gbs,
-             Cin, N * H * W, Cout, H * W, N, 0, ACT[gact], 0, 0, LRELU_SLOPE, stream())
+             Cin, N * H * W, Cout, H * W, N, 0, ACT[gact], 0, int(accumulate), LRELU_SLOPE, stream())
     elif (w.dim() == 4 and stride == 1 and act is None and bias is None and KH == KW
           and _pconv_ok(Cout, KH, KW, 1)):
         # stride-1 data-grad = forward conv of dy with the flipped, transposed kernel
@@ -379,6 +379,98 @@ def copy_into(dst, src):
 
 
 # ------------------------------------------------------------------------------------------
+# Shared activations: one gradient buffer per tensor with several consumers.
+#
+# autograd sums the input-grads of a tensor's consumers with one torch add per extra consumer
+# (2 reads + 1 write of the whole tensor each).  ``share(x)`` returns an alias of x carrying a
+# _GradBox; consumer Functions see the box on their input and, in backward, either hand their
+# freshly computed grad to the box (the first one is adopted as the buffer, no copy) or let the
+# kernel accumulate straight into the buffer (maxpool / depthwise / GEMM data-grads have an
+# accumulate epilogue).  ShareFn's backward -- run by autograd after every consumer -- returns
+# the buffer.  A tensor that may also be referenced elsewhere (a grad autograd handed us) is
+# only borrowed, never accumulated into in place.
+# ------------------------------------------------------------------------------------------
+
+class _GradBox:
+    __slots__ = ("buf", "owned")
+
+    def __init__(self):
+        self.buf, self.owned = None, False
+
+
+def _box(t):
+    return getattr(t, "_dsg_box", None)
+
+
+def _add_n_raw(out, ts):
+    import ctypes
+    ts4 = [nchw(t) for t in ts]
+    o4, obs = nchw(out)
+    N, C, H, W = o4.shape
+    arr = (ctypes.c_void_p * len(ts4))(*[t.data_ptr() for t, _ in ts4])
+    bss = (ctypes.c_long * len(ts4))(*[bs for _, bs in ts4])
+    call("dsgan_add_n", ctypes.cast(arr, ctypes.c_void_p), ctypes.cast(bss, ctypes.c_void_p), len(ts4), ptr(o4),
+         obs, N, C * H * W, stream())
+
+
+def _acc_target(box):
+    """(buffer, True) when a kernel may accumulate its grad straight into the box."""
+    if box is not None and box.buf is not None and box.owned:
+        return box.buf, True
+    return None, False
+
+
+def _give(box, t, adopt=True):
+    """Route a consumer's input-grad t: returns t itself when the input is not shared."""
+    if box is None or t is None:
+        return t
+    if box.buf is None:
+        box.buf, box.owned = t, adopt
+    elif box.owned:
+        _add_n_raw(box.buf, [box.buf, t])
+    else:
+        nb = _empty(*t.shape, t)
+        _add_n_raw(nb, [box.buf, t])
+        box.buf, box.owned = nb, True
+    return None
+
+
+class ShareFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, box):
+        ctx.set_materialize_grads(False)
+        ctx.box, ctx.outer = box, _box(x)
+        return x.view_as(x)
+
+    @staticmethod
+    def backward(ctx, g):
+        box = ctx.box
+        buf, own = box.buf, box.owned
+        box.buf = None
+        if g is not None:
+            if buf is None:
+                buf, own = g, False
+            elif own:
+                _add_n_raw(buf, [buf, g])
+            else:
+                nb = _empty(*g.shape, g)
+                _add_n_raw(nb, [buf, g])
+                buf, own = nb, True
+        if ctx.outer is not None:
+            _give(ctx.outer, buf, adopt=own)
+            return None, None
+        return buf, None
+
+
+def share(x):
+    """Alias of x whose consumers accumulate into one gradient buffer (see above)."""
+    box = _GradBox()
+    y = ShareFn.apply(x, box)
+    y._dsg_box = box
+    return y
+
+
+# ------------------------------------------------------------------------------------------
 # Conv2d (+bias, +relu/lrelu):  VGG 3x3, PatchGAN 4x4, G head 3x3, 1x1 convs
 # ------------------------------------------------------------------------------------------
 
@@ -391,6 +483,7 @@ class Conv2dFn(torch.autograd.Function):
         ctx.x_shape = tuple(x.shape)
         ctx.save_for_backward(x, w, b, y if act in ("relu", "lrelu") else None)
         ctx.w_ref, ctx.b_ref = w, b
+        ctx.box = _box(x)
         return y
 
     @staticmethod
@@ -405,7 +498,9 @@ class Conv2dFn(torch.autograd.Function):
             dy = act_bwd_raw(dy, y, ctx.act)  # sign(y) == sign(pre) for relu/lrelu
         dx = None
         if ctx.needs_input_grad[0]:
-            dx = conv_dgrad_raw(dy, w, ctx.x_shape, ctx.stride, ctx.pad)
+            out, acc = _acc_target(ctx.box)
+            dx = conv_dgrad_raw(dy, w, ctx.x_shape, ctx.stride, ctx.pad, out=out, accumulate=acc)
+            dx = None if acc else _give(ctx.box, dx)
         gw = _grad_buf(ctx.w_ref) if ctx.needs_input_grad[1] else None
         if gw is not None:
             conv_wgrad_raw(dy, x, gw, ctx.stride, ctx.pad)
@@ -434,6 +529,7 @@ class ConvT3s2Fn(torch.autograd.Function):
         ctx.prec = _state["prec"]
         ctx.save_for_backward(x, w, b)
         ctx.w_ref, ctx.b_ref = w, b
+        ctx.box = _box(x)
         return y
 
     @staticmethod
@@ -451,7 +547,7 @@ class ConvT3s2Fn(torch.autograd.Function):
         gb = _grad_buf(ctx.b_ref) if (b is not None and ctx.needs_input_grad[2]) else None
         if gb is not None:
             channel_sum_raw(dy, gb)
-        return dx, None, None
+        return _give(ctx.box, dx), None, None
 
 
 def conv_transpose3s2(x, w, b):
@@ -514,6 +610,7 @@ class PwMlpFn(torch.autograd.Function):
         ctx.refs = (w1, b1, w2, b2, ws)
         ctx.tile = tile
         ctx.prec = _state["prec"]
+        ctx.box_h, ctx.box_x = _box(h), _box(x)
         if tile:
             out = conv_fwd_raw(x, ws, None, 1, 0)
             e0 = IGEMM_TIMER.begin()
@@ -557,8 +654,16 @@ class PwMlpFn(torch.autograd.Function):
         if gb1 is not None:
             channel_sum_raw(dz, gb1)
         dh = conv_dgrad_raw(dz, w1v, tuple(h.shape), 1, 0) if ctx.needs_input_grad[0] else None
-        dx = conv_dgrad_raw(dy, ws, tuple(x.shape), 1, 0) if ctx.needs_input_grad[1] else None
-        return dh, dx, None, None, None, None, None
+        return _give(ctx.box_h, dh), PwMlpFn._dx(ctx, dy, ws, x), None, None, None, None, None
+
+    @staticmethod
+    def _dx(ctx, dy, ws, x):
+        """shortcut data-grad, accumulated into the shared buffer of x when there is one"""
+        if not ctx.needs_input_grad[1]:
+            return None
+        out, acc = _acc_target(ctx.box_x)
+        dx = conv_dgrad_raw(dy, ws, tuple(x.shape), 1, 0, out=out, accumulate=acc)
+        return None if acc else _give(ctx.box_x, dx)
 
     @staticmethod
     def _backward_fused(ctx, dy):
@@ -593,8 +698,7 @@ class PwMlpFn(torch.autograd.Function):
             IGEMM_TIMER.end(e0, 2.0 * N * HW * C4 * C, ("wgrad", N, C, H, W, C4, 1, 1), "pwgemm_kernel")
         if gb1 is not None:
             call("dsgan_colsum", ptr(bsum), ntiles, C4, ptr(gb1), stream())
-        dx = conv_dgrad_raw(dy, ws, tuple(x.shape), 1, 0) if ctx.needs_input_grad[1] else None
-        return dh, dx, None, None, None, None, None
+        return _give(ctx.box_h, dh), PwMlpFn._dx(ctx, dy, ws, x), None, None, None, None, None
 
 
 def pw_mlp(h, x, w1, b1, w2, b2, ws):
@@ -629,13 +733,18 @@ class DwConvFn(torch.autograd.Function):
         y = dwconv_raw(x, w, b)
         ctx.save_for_backward(x, w)
         ctx.refs = (w, b)
+        ctx.box = _box(x)
         return y
 
     @staticmethod
     def backward(ctx, dy):
         x, w = ctx.saved_tensors
         wr, br = ctx.refs
-        dx = dwconv_raw(dy, w, None, flip=True) if ctx.needs_input_grad[0] else None
+        dx = None
+        if ctx.needs_input_grad[0]:
+            out, acc = _acc_target(ctx.box)
+            dx = dwconv_raw(dy, w, None, flip=True, out=out, accumulate=acc)
+            dx = None if acc else _give(ctx.box, dx)
         gw, gb = _grad_buf(wr), _grad_buf(br)
         if gw is not None:
             _dw_wgrad(dy, x, gw, gb, w.shape[-1])
@@ -660,6 +769,7 @@ class MultiDwConvFn(torch.autograd.Function):
             dwconv_raw(x4[:, i * q:(i + 1) * q], wb[2 * i], wb[2 * i + 1], out=y[:, i * q:(i + 1) * q])
         ctx.save_for_backward(x4, *wb)
         ctx.refs = wb
+        ctx.box = _box(x)
         return y
 
     @staticmethod
@@ -668,15 +778,19 @@ class MultiDwConvFn(torch.autograd.Function):
         N, C, H, W = x.shape
         q = C // 4
         dy4, _ = nchw(dy)
-        dx = _empty(N, C, H, W, x) if ctx.needs_input_grad[0] else None
+        out, acc = _acc_target(ctx.box)
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = out if acc else _empty(N, C, H, W, x)
         for i in range(4):
             sl = slice(i * q, (i + 1) * q)
             w = wb[2 * i]
             if dx is not None:
-                dwconv_raw(dy4[:, sl], w, None, flip=True, out=dx[:, sl])
+                dwconv_raw(dy4[:, sl], w, None, flip=True, out=dx[:, sl], accumulate=acc)
             gw, gb = _grad_buf(ctx.refs[2 * i]), _grad_buf(ctx.refs[2 * i + 1])
             if gw is not None:
                 _dw_wgrad(dy4[:, sl], x[:, sl], gw, gb, w.shape[-1])
+        dx = None if acc else _give(ctx.box, dx)
         return (dx,) + (None,) * 8
 
 
@@ -727,6 +841,7 @@ class InstanceNormFn(torch.autograd.Function):
         y, mean, rstd = instnorm_raw(x, None, res, act)
         ctx.act = act
         ctx.save_for_backward(x, res, mean, rstd)
+        ctx.box_x, ctx.box_r = _box(x), (_box(res) if res is not None else None)
         return y
 
     @staticmethod
@@ -734,7 +849,7 @@ class InstanceNormFn(torch.autograd.Function):
         x, res, mean, rstd = ctx.saved_tensors
         dx, dres, _ = instnorm_bwd_raw(dy, x, None, res, mean, rstd, ctx.act,
                                        res is not None and ctx.needs_input_grad[1], False)
-        return dx, dres, None
+        return _give(ctx.box_x, dx), _give(ctx.box_r, dres), None
 
 
 def instance_norm(x, act=None, res=None):
@@ -757,6 +872,7 @@ class MaxPoolFn(torch.autograd.Function):
         ctx.k, ctx.shape = k, (N, C, H, W)
         ctx.save_for_backward(idx)
         ctx.mark_non_differentiable(idx)
+        ctx.box = _box(x)
         return y, idx
 
     @staticmethod
@@ -764,14 +880,102 @@ class MaxPoolFn(torch.autograd.Function):
         (idx,) = ctx.saved_tensors
         N, C, H, W = ctx.shape
         dy4, dybs = nchw(dy)
-        dx = torch.empty((N, C, H, W), device=dy.device, dtype=torch.float32)
-        call("dsgan_maxpool_bwd", ptr(dy4), dybs, ptr(idx), ptr(dx), C * H * W, N, C, H, W, ctx.k, 0, stream())
-        return dx, None
+        out, acc = _acc_target(ctx.box)
+        dx = out if acc else torch.empty((N, C, H, W), device=dy.device, dtype=torch.float32)
+        dx4, dxbs = nchw(dx)
+        if dx4.data_ptr() != dx.data_ptr():
+            raise RuntimeError("maxpool backward: gradient buffer must be per-sample dense")
+        call("dsgan_maxpool_bwd", ptr(dy4), dybs, ptr(idx), ptr(dx4), dxbs, N, C, H, W, ctx.k, int(acc), stream())
+        return (None if acc else _give(ctx.box, dx)), None
 
 
 def max_pool2d(x, k, return_indices=False):
     y, idx = MaxPoolFn.apply(x, k)
     return (y, idx) if return_indices else y
+
+
+def maxpool_raw(x, k):
+    """MaxPool2d(k) forward without autograd: (y, int32 plane-flat argmax)."""
+    x4, xbs = nchw(x)
+    N, C, H, W = x4.shape
+    Ho, Wo = H // k, W // k
+    y = _empty(N, C, Ho, Wo, x4)
+    idx = torch.empty((N, C, Ho, Wo), device=x4.device, dtype=torch.int32)
+    call("dsgan_maxpool_fwd", ptr(x4), xbs, ptr(y), C * Ho * Wo, ptr(idx), N, C, H, W, k, stream())
+    return y, idx
+
+
+# ------------------------------------------------------------------------------------------
+# VGG16 perceptual term (DSGAN/models/vgg.py:30-42, pix2pix_model.py:180-186) as ONE autograd
+# node: loss = L1(f1,r1) + L1(f2,r2) + L1(f3,r3) + L1(f0,r0), f = VGG16(fake), r = VGG16(real).
+# Its backward walks the frozen VGG by hand (no weight-grads): each conv data-grad applies the
+# ReLU mask of the layer below in its epilogue, and at each tapped layer one kernel forms
+# (maxpool backward + L1 backward) * ReLU'  -- no standalone ReLU/L1 passes, no autograd adds.
+# ------------------------------------------------------------------------------------------
+
+def vgg_features_raw(x, blocks):
+    """blocks = [(pool, [(w, b), ...]), ...] -> (feats, saved): feats = post-ReLU output of each
+    block, saved = per block (pool argmax or None, input shape of the pool, [conv outputs])."""
+    h = x
+    feats, saved = [], []
+    for pool, convs in blocks:
+        idx, pin = None, None
+        if pool:
+            pin = tuple(h.shape)
+            h, idx = maxpool_raw(h, 2)
+        ys = []
+        for w, b in convs:
+            h = conv_fwd_raw(h, w, b, 1, 1, act="relu")
+            ys.append(h)
+        feats.append(h)
+        saved.append((idx, pin, ys))
+    return feats, saved
+
+
+class PerceptualL1Fn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, fake, blocks, real_feats):
+        fake, _ = nchw(fake)
+        feats, saved = vgg_features_raw(fake, blocks)
+        outs = torch.empty(4, device=fake.device, dtype=torch.float32)
+        for i, (f, r) in enumerate(zip(feats, real_feats)):
+            call("dsgan_l1_fwd", ptr(f), ptr(r.contiguous()), f.numel(), ptr(outs[i:]), stream())
+        ctx.blocks, ctx.saved, ctx.real = blocks, saved, real_feats
+        ctx.fake_shape = tuple(fake.shape)
+        ctx.prec = _state["prec"]
+        # reference order: L1(f1) + L1(f2) + L1(f3) + L1(f0)
+        return ((outs[1] + outs[2]) + outs[3]) + outs[0]
+
+    @staticmethod
+    def backward(ctx, g):
+        with precision(ctx.prec):
+            g = g.contiguous()
+            d, d_idx = None, None   # grad at the pool output of the block above, and that pool's argmax
+            for bi in range(len(ctx.blocks) - 1, -1, -1):
+                pool, convs = ctx.blocks[bi]
+                idx, pin, ys = ctx.saved[bi]
+                y_top = ys[-1]
+                N, C, H, W = y_top.shape
+                dpre = torch.empty_like(y_top)
+                # tapped layer: (pool backward of the block above + L1 backward) * ReLU'
+                call("dsgan_vgg_tap_bwd", ptr(d), ptr(d_idx), ptr(y_top), ptr(ctx.real[bi].contiguous()), ptr(dpre),
+                     N * C, H, W, ptr(g), stream())
+                for li in range(len(convs) - 1, -1, -1):
+                    w = convs[li][0]
+                    if li > 0:
+                        # data-grad into the conv below, masked by that conv's ReLU in the epilogue
+                        below = ys[li - 1]
+                        dpre = conv_dgrad_raw(dpre, w, tuple(below.shape), 1, 1, gpre=below, gact="relu")
+                    else:
+                        in_shape = (pin[0], pin[1], pin[2] // 2, pin[3] // 2) if pool else ctx.fake_shape
+                        dpre = conv_dgrad_raw(dpre, w, in_shape, 1, 1)
+                d, d_idx = dpre, idx
+            ctx.saved = ctx.real = None
+            return d, None, None
+
+
+def perceptual_l1(fake, blocks, real_feats):
+    return PerceptualL1Fn.apply(fake, blocks, real_feats)
 
 
 # ------------------------------------------------------------------------------------------
@@ -794,6 +998,7 @@ class MidTailFn(torch.autograd.Function):
         y, mean, rstd = instnorm_raw(v4, att, x, "gelu")
         ctx.save_for_backward(v4, x, w1, pa, w2, avg, mx, amax, att, hsave, mean, rstd)
         ctx.refs = (w1, pa, w2)
+        ctx.box_v, ctx.box_x = _box(v), _box(x)
         return y
 
     @staticmethod
@@ -808,7 +1013,7 @@ class MidTailFn(torch.autograd.Function):
         call("dsgan_ca_bwd", ptr(datt), ptr(att), ptr(avg), ptr(mx), ptr(hsave), ptr(w1), ptr(w2), ptr(pa),
              ptr(davg), ptr(dmx), ptr(_grad_buf(w1r)), ptr(_grad_buf(w2r)), ptr(_grad_buf(par)), N, C, R, stream())
         call("dsgan_plane_stats_bwd", ptr(davg), ptr(dmx), ptr(amax), ptr(dv), C * H * W, N, C, H * W, stream())
-        return dv, dx, None, None, None
+        return _give(ctx.box_v, dv), _give(ctx.box_x, dx), None, None, None
 
 
 def mid_tail(v, x, w1, pa, w2):
@@ -832,11 +1037,13 @@ class AddNFn(torch.autograd.Function):
         call("dsgan_add_n", ctypes.cast(arr, ctypes.c_void_p), ctypes.cast(bss, ctypes.c_void_p), len(ts),
              ptr(out), C * H * W, N, C * H * W, stream())
         ctx.n = len(xs)
+        ctx.boxes = [_box(t) for t in xs]
         return out
 
     @staticmethod
     def backward(ctx, dy):
-        return tuple(dy for _ in range(ctx.n))
+        # the same dy goes to every input: a shared input may only borrow it
+        return tuple(_give(b, dy, adopt=False) for b in ctx.boxes)
 
 
 def add_n(*xs):
@@ -852,11 +1059,13 @@ class CatFn(torch.autograd.Function):
         copy_into(out[:, :Ca], a)
         copy_into(out[:, Ca:], b)
         ctx.Ca = Ca
+        ctx.box_a, ctx.box_b = _box(a), _box(b)
         return out
 
     @staticmethod
     def backward(ctx, dy):
-        return dy[:, :ctx.Ca], dy[:, ctx.Ca:]
+        # disjoint channel slices of dy: a shared input may adopt its slice as its buffer
+        return _give(ctx.box_a, dy[:, :ctx.Ca]), _give(ctx.box_b, dy[:, ctx.Ca:])
 
 
 def cat_channels(a, b):

@@ -53,6 +53,7 @@ class MidMLKA(nn.Module):
         self.X9 = nn.Conv2d(q, q, 9, 1, 4, groups=q)
 
     def forward(self, x):
+        x = HF.share(x)   # read by the depthwise convs and by the residual of the tail
         d = HF.multi_dwconv(x, self.X3.weight, self.X3.bias, self.X5.weight, self.X5.bias,
                             self.X7.weight, self.X7.bias, self.X9.weight, self.X9.bias)
         # The 1x1 conv feeds an InstanceNorm whose input variance is far below eps at the
@@ -91,10 +92,10 @@ class OriginMLKA(nn.Module):
         mp = lambda t: HF.max_pool2d(t, 2)
         d1 = HF.conv2d(x, self.to32.weight)
         d2 = self.mid32(mp(d1))
-        d3 = HF.conv2d(d2, self.to64.weight)
-        d4 = self.mid64(mp(d3))
+        d3 = HF.share(HF.conv2d(d2, self.to64.weight))     # also the skip of up3
+        d4 = HF.share(self.mid64(mp(d3)))                   # also the skip of up2
         d5 = HF.conv2d(d4, self.to128.weight)
-        d6 = self.mid128(mp(d5))
+        d6 = HF.share(self.mid128(mp(d5)))                  # also the skip of up1
         d7 = HF.conv2d(d6, self.to256.weight)
         d8 = self.mid256(mp(d7))
         u1 = self.upc1[1](HF.conv2d(self.up1(d8, d6), self.upc1[0].weight))
@@ -118,6 +119,7 @@ class Block(nn.Module):
         self.pwconv2 = nn.Linear(4 * dim, plans)
 
     def forward(self, x):
+        x = HF.share(x)   # read by the depthwise conv and by the 1x1 shortcut
         h = HF.instance_norm(HF.dwconv(x, self.dwconv.weight, self.dwconv.bias))
         return HF.pw_mlp(h, x, self.pwconv1.weight, self.pwconv1.bias, self.pwconv2.weight,
                          self.pwconv2.bias, self.shortcut.weight)
@@ -129,9 +131,11 @@ def _skip(cin, cout, k):
                          nn.InstanceNorm2d(cout), nn.GELU())
 
 
-def _skip_fwd(seq, x):
+def _skip_fwd(seq, x, pooled=None):
+    """MaxPool(k) -> 1x1 -> IN -> GELU; ``pooled`` = MaxPool(k)(x) when already computed."""
     k = seq[0].kernel_size
-    return HF.instance_norm(HF.conv2d(HF.max_pool2d(x, k), seq[1].weight), act="gelu")
+    p = pooled if pooled is not None else HF.max_pool2d(x, k)
+    return HF.instance_norm(HF.conv2d(p, seq[1].weight), act="gelu")
 
 
 class downSkip(nn.Module):
@@ -139,8 +143,8 @@ class downSkip(nn.Module):
         super().__init__()
         self.to2, self.to4, self.to8, self.to16 = _skip(64, 128, 2), _skip(64, 256, 4), _skip(64, 512, 8), _skip(64, 1024, 16)
 
-    def forward(self, x):
-        return [_skip_fwd(s, x) for s in (self.to2, self.to4, self.to8, self.to16)]
+    def forward(self, x, pool2=None):
+        return [_skip_fwd(self.to2, x, pool2)] + [_skip_fwd(s, x) for s in (self.to4, self.to8, self.to16)]
 
 
 class downSkip128(nn.Module):
@@ -148,8 +152,8 @@ class downSkip128(nn.Module):
         super().__init__()
         self.to4, self.to8, self.to16 = _skip(128, 256, 2), _skip(128, 512, 4), _skip(128, 1024, 8)
 
-    def forward(self, x):
-        return [_skip_fwd(s, x) for s in (self.to4, self.to8, self.to16)]
+    def forward(self, x, pool2=None):
+        return [_skip_fwd(self.to4, x, pool2)] + [_skip_fwd(s, x) for s in (self.to8, self.to16)]
 
 
 class downSkip256(nn.Module):
@@ -157,8 +161,8 @@ class downSkip256(nn.Module):
         super().__init__()
         self.to8, self.to16 = _skip(256, 512, 2), _skip(256, 1024, 4)
 
-    def forward(self, x):
-        return [_skip_fwd(s, x) for s in (self.to8, self.to16)]
+    def forward(self, x, pool2=None):
+        return [_skip_fwd(self.to8, x, pool2), _skip_fwd(self.to16, x)]
 
 
 class downSkip512(nn.Module):
@@ -166,8 +170,8 @@ class downSkip512(nn.Module):
         super().__init__()
         self.to16 = _skip(512, 1024, 2)
 
-    def forward(self, x):
-        return [_skip_fwd(self.to16, x)]
+    def forward(self, x, pool2=None):
+        return [_skip_fwd(self.to16, x, pool2)]
 
 
 class MixConvNeXtML(nn.Module):
@@ -196,16 +200,24 @@ class MixConvNeXtML(nn.Module):
         self.res = nn.Conv2d(64, 3, kernel_size=3, padding=1)
 
     def forward(self, x):
-        mp = lambda t: HF.max_pool2d(t, 2)
-        R1 = self.c1(x)
-        R2 = self.c2(mp(R1))
-        R3 = self.c3(mp(R2))
-        R4 = self.c4(mp(R3))
-        R5 = self.c5(mp(R4))
-        s64 = self.down64(R1)
-        s128 = self.down128(R2)
-        s256 = self.down256(R3)
-        s512 = self.down512(R4)
+        # R1..R4 feed the next stage's MaxPool(2), their skip pyramid and a decoder concat; the
+        # MaxPool(2) of R_i is computed once for the encoder and the pyramid's k=2 branch
+        # (both are MaxPool2d(2) of the same tensor).  Shared tensors accumulate their grads in
+        # one buffer (HF.share) instead of through autograd adds.
+        sh, mp = HF.share, lambda t: HF.share(HF.max_pool2d(t, 2))
+        R1 = sh(self.c1(x))
+        P1 = mp(R1)
+        R2 = sh(self.c2(P1))
+        P2 = mp(R2)
+        R3 = sh(self.c3(P2))
+        P3 = mp(R3)
+        R4 = sh(self.c4(P3))
+        P4 = mp(R4)
+        R5 = self.c5(P4)
+        s64 = self.down64(R1, P1)
+        s128 = self.down128(R2, P2)
+        s256 = self.down256(R3, P3)
+        s512 = self.down512(R4, P4)
         O1 = self.uc1(self.u1(HF.add_n(R5, s64[3], s128[2], s256[1], s512[0]), R4))
         O2 = self.uc2(self.u2(HF.add_n(O1, s64[2], s128[1], s256[0]), R3))
         O3 = self.uc3(self.u3(HF.add_n(O2, s64[1], s128[0]), R2))

@@ -16,6 +16,8 @@ Deliberate, documented deviations:
     size so averaged gradients equal the reference's global-batch gradient;
   * the unused VGG relu5_3 block is not computed (the loss never reads it, :182-186).
 """
+import os
+
 import torch
 
 from dsgan_hip import functional as HF
@@ -25,6 +27,8 @@ from util.image_pool import ImagePool
 from .base_model import BaseModel
 from . import networks
 from .vgg import Vgg16
+
+_SERIAL_VGG = os.environ.get("DSGAN_SERIAL_VGG") == "1"   # A/B switch: vgg(real_B) on the main stream
 
 
 class Pix2PixModel(BaseModel):
@@ -76,6 +80,8 @@ class Pix2PixModel(BaseModel):
             self.optimizers.append(self.optimizer_G)
             self.optimizers.append(self.optimizer_D)
             self.tv_scale = float(hdist.world_size())
+            self._vgg_stream = torch.cuda.Stream(self.device)
+            self._real_feats = None
 
     def set_input(self, input):
         AtoB = self.opt.which_direction == "AtoB"
@@ -106,12 +112,10 @@ class Pix2PixModel(BaseModel):
         else:
             self.loss_G_GAN = 0
         self.loss_G_L1 = self.criterionL1(self.fake_B, self.real_B)
-        with torch.no_grad():
-            self.real_B_features = self.vgg(self.real_B)
-        self.fake_B_features = self.vgg(self.fake_B)
-        f, r = self.fake_B_features, self.real_B_features
-        self.loss_vgg = (self.criterionL1(f[1], r[1]) + self.criterionL1(f[2], r[2])
-                         + self.criterionL1(f[3], r[3]) + self.criterionL1(f[0], r[0]))
+        self.real_B_features = self._take_real_features()
+        # L1(f1,r1) + L1(f2,r2) + L1(f3,r3) + L1(f0,r0) over vgg(fake_B): one fused node whose
+        # backward is the hand-written VGG data-grad chain (vgg.py / functional.PerceptualL1Fn)
+        self.loss_vgg = self.vgg.perceptual_l1(self.fake_B, self.real_B_features)
         self.tv_loss = HF.tv_loss(self.fake_B, self.tv_scale / (320 * 256))
         # 1 - ssim((real_B+1)/2, (fake_B+1)/2, data_range=1): the affine map is fused in-kernel
         self.loss_ssim = 1 - HF.ssim_affine(self.real_B, self.fake_B, 0.5, 0.5, 1.0)
@@ -119,7 +123,29 @@ class Pix2PixModel(BaseModel):
                        + self.tv_loss * self.w_tv + self.w_ss * self.loss_ssim)
         self.loss_G.backward()
 
+    def _launch_real_features(self):
+        """vgg(real_B) (frozen, no grad) depends only on the input: run it on a side stream so it
+        overlaps the generator forward and the D step; backward_G joins the stream."""
+        main = torch.cuda.current_stream(self.device)
+        side = self._vgg_stream
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            self.real_B.record_stream(side)
+            feats = self.vgg.loss_features(self.real_B)
+        for f in feats:
+            f.record_stream(main)
+        self._real_feats = feats
+
+    def _take_real_features(self):
+        if self._real_feats is None:
+            self._launch_real_features()
+        torch.cuda.current_stream(self.device).wait_stream(self._vgg_stream)
+        feats, self._real_feats = self._real_feats, None
+        return feats
+
     def optimize_parameters(self):
+        if not _SERIAL_VGG:
+            self._launch_real_features()
         self.forward()
         if self.use_gan == 1:
             self.set_requires_grad(self.netD, True)

@@ -78,3 +78,22 @@ class Vgg16(nn.Module):
                 h = HF.conv2d(h, c.weight, c.bias, stride=1, pad=1, act="relu")
             feats.append(h)
         return tuple(feats)
+
+    def loss_blocks(self):
+        """[(pool, [(w, b), ...])] of the four blocks the perceptual loss reads (relu1_2..relu4_3)."""
+        out = []
+        for name, convs, pool in _CFG[:4]:
+            seq = getattr(self, name)
+            out.append((pool, [(seq._modules[str(i)].weight, seq._modules[str(i)].bias) for i, _, _ in convs]))
+        return out
+
+    @torch.no_grad()
+    def loss_features(self, x):
+        """relu1_2..relu4_3 of x without autograd (the real-image side of the perceptual loss)."""
+        return HF.vgg_features_raw(x, self.loss_blocks())[0]
+
+    def perceptual_l1(self, fake, real_feats):
+        """L1(f1,r1) + L1(f2,r2) + L1(f3,r3) + L1(f0,r0) of f = self(fake), r = real_feats
+        (DSGAN/models/pix2pix_model.py:180-186) as one fused autograd node."""
+        return HF.perceptual_l1(fake, self.loss_blocks(), list(real_feats))
+

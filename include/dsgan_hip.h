@@ -156,7 +156,7 @@ int dsgan_wconv(const float* D, long d_bs, const float* X, long x_bs, float* dw,
 
 /* ---- depthwise conv (dwconv.hip): Block.dwconv :220, MidMLKA.X3..X9 :94-97 ----------------
  * y (+)= dwconv_KxK(x, w) + bias; flip = 1 with bias = NULL is the data-grad; accumulate adds into
- * y (data-grad of a tensor with a second consumer; needs 16-byte aligned rows, W % 4 == 0). */
+ * y (data-grad of a tensor with a second consumer). */
 int dsgan_dwconv_fwd(const float* x, long x_bs, const float* w, const float* bias, float* y,
                      long y_bs, int N, int C, int H, int W, int K, int flip, int accumulate,
                      hipStream_t stream);
@@ -217,6 +217,11 @@ int dsgan_bce_logits_bwd(const float* x, long n, float target, const float* gout
 int dsgan_l1_fwd(const float* a, const float* b, long n, float* out, hipStream_t stream);
 int dsgan_l1_bwd(const float* a, const float* b, long n, const float* gout, float* da,
                  int accumulate, hipStream_t stream);
+/* VGG perceptual tap backward (DSGAN/models/vgg.py:30-42, pix2pix_model.py:182-186): the grad at
+ * the pre-ReLU output of a tapped conv, dx = (maxpool_bwd(dpool, idx) [dpool != NULL]
+ * + gout*sign(y - r)/numel) * (y > 0) -- L1 backward + the two consumers' sum + ReLU backward. */
+int dsgan_vgg_tap_bwd(const float* dpool, const int* idx, const float* y, const float* r, float* dx,
+                      long planes, int H, int W, const float* gout, hipStream_t stream);
 int dsgan_tv_fwd(const float* y, long planes, int H, int W, float coef, float* out,
                  hipStream_t stream);
 int dsgan_tv_bwd(const float* y, long planes, int H, int W, float coef, const float* gout,

@@ -525,3 +525,53 @@ def test_tap_conv_bf16(N, Cin, H, W, Cout, K, s, p):
         ref = ref * torch.where(gp > 0, 1.0, 0.2)
         assert rel(dx, ref) < 1e-2
     HF.set_precision("fp32")
+
+
+@pytest.mark.parametrize("prec", ["fp32", "bf16"])
+def test_perceptual_l1_fused(prec):
+    """VGG16 perceptual term as one node (PerceptualL1Fn): loss and d(loss)/d(fake) vs torch's
+    conv2d/relu/max_pool2d/l1_loss chain (DSGAN/models/vgg.py:30-42, pix2pix_model.py:182-186)."""
+    import sys, os
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "ds-gan_amd"))
+    from dsgan_hip import functional as HF
+    from models.vgg import Vgg16
+    HF.set_precision(prec)
+    torch.manual_seed(3)
+    vgg = Vgg16(seed=11).to(DEV)
+    g = torch.Generator().manual_seed(5)
+    fake = _q(torch.randn(2, 3, 32, 48, generator=g), prec)
+    real = _q(torch.randn(2, 3, 32, 48, generator=g), prec)
+    blocks = [(pool, [(w.detach().cpu(), b.detach().cpu()) for w, b in convs]) for pool, convs in vgg.loss_blocks()]
+
+    def ref_feats(x):
+        feats, h = [], x
+        for pool, convs in blocks:
+            if pool:
+                h = F.max_pool2d(h, 2)
+            for w, b in convs:
+                h = F.relu(F.conv2d(h, _q(w, prec), b, padding=1))
+            feats.append(h)
+        return feats
+    fr = fake.clone().requires_grad_()
+    f, r = ref_feats(fr), [t.detach() for t in ref_feats(real)]
+    loss_ref = F.l1_loss(f[1], r[1]) + F.l1_loss(f[2], r[2]) + F.l1_loss(f[3], r[3]) + F.l1_loss(f[0], r[0])
+    loss_ref.backward()
+    fd = _leaf(fake)
+    rfe = vgg.loss_features(real.to(DEV))
+    loss = vgg.perceptual_l1(fd, rfe)
+    loss.backward()
+    if prec == "fp32":
+        assert abs(loss.item() - loss_ref.item()) <= 1e-5 * abs(loss_ref.item())
+        assert rel(fd.grad, fr.grad) < 2e-5
+    else:
+        # bf16 activations move sign(f - r) and the ReLU masks against an fp32 chain, so the
+        # bf16 node is checked against the unfused HIP chain on the same kernels/rounding
+        # (Conv2dFn + MaxPoolFn + L1Fn autograd), and its loss against fp32 at the bf16 bar.
+        assert abs(loss.item() - loss_ref.item()) <= 2e-2 * abs(loss_ref.item())
+        fu = _leaf(fake)
+        f = vgg(fu)
+        rr = list(rfe)
+        lu = HF.l1_loss(f[1], rr[1]) + HF.l1_loss(f[2], rr[2]) + HF.l1_loss(f[3], rr[3]) + HF.l1_loss(f[0], rr[0])
+        lu.backward()
+        assert abs(loss.item() - lu.item()) <= 1e-5 * abs(lu.item())
+        assert rel(fd.grad, fu.grad) < 1e-3
