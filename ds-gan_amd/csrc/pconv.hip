@@ -43,7 +43,7 @@ __global__ __launch_bounds__(256, 2) void pconv_kernel(PcArgs g) {
   constexpr int TAPS = KH * KW;
   constexpr int A_SZ = BM * PC_STR, P_SZ = PPIX * PC_STR;
   constexpr int A_ITEMS = BM * 4 / 256;           // 16-byte items of a [BM][32] bf16 slice
-  constexpr int P_ITEMS = (PPIX * 4 + 255) / 256; // (pixel, 8-channel group) items of the patch
+  constexpr int P_ITEMS = (PPIX * 4 + 255) / 256; // (pixel, 8-channel group) items of the patch per thread
   __shared__ __attribute__((aligned(16))) __bf16 smem[2 * A_SZ + P_SZ];
   __bf16* Ps = smem + 2 * A_SZ;
 
@@ -95,20 +95,31 @@ __global__ __launch_bounds__(256, 2) void pconv_kernel(PcArgs g) {
     }
   };
   // patch of channel block k0: item = (pixel, 8-channel group); lanes run along the pixels of
-  // a patch row, so each of the 8 channel loads is coalesced across the wave
-  auto pstage = [&](int k0) {
+  // a patch row, so each of the 8 channel loads is coalesced across the wave.  The loads of
+  // block k0+32 are issued before the taps of block k0 run (registers), written to LDS after.
+  float rp[P_ITEMS][8];
+  auto pload = [&](int k0) {
+#pragma unroll
+    for (int i = 0; i < P_ITEMS; ++i) {
+      const int it = tid + i * 256;
+      const int cg = it / PPIX, pix = it - cg * PPIX;
+      const int pr = pix / PW, pc = pix - pr * PW;
+      const int ih = ih0 + pr, iw = iw0 + pc;
+      const bool in = it < PPIX * 4 && (unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W;
+      const float* src = xb + (long)(k0 + (in ? cg : 0) * 8) * HW + (in ? ih * g.W + iw : 0);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) rp[i][e] = in ? src[(long)e * HW] : 0.f;
+    }
+  };
+  auto pwrite = [&]() {
 #pragma unroll
     for (int i = 0; i < P_ITEMS; ++i) {
       const int it = tid + i * 256;
       if (it < PPIX * 4) {
         const int cg = it / PPIX, pix = it - cg * PPIX;
-        const int pr = pix / PW, pc = pix - pr * PW;
-        const int ih = ih0 + pr, iw = iw0 + pc;
-        const bool in = (unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W;
-        const float* src = xb + (long)(k0 + cg * 8) * HW + (in ? ih * g.W + iw : 0);
         cbf16x8 v;
 #pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] = (__bf16)(in ? src[(long)e * HW] : 0.f);
+        for (int e = 0; e < 8; ++e) v[e] = (__bf16)rp[i][e];
         *reinterpret_cast<cbf16x8*>(Ps + pix * PC_STR + cg * 8) = v;
       }
     }
@@ -131,16 +142,19 @@ __global__ __launch_bounds__(256, 2) void pconv_kernel(PcArgs g) {
 
   const int nkb = g.K / 32;
   int buf = 0;
+  aload(0, 0);
+  pload(0);
   for (int kb = 0; kb < nkb; ++kb) {
     const int k0 = kb * 32;
     __syncthreads();                 // previous block's patch and A buffers are free
-    aload(0, k0);
-    pstage(k0);
+    pwrite();
     astore(buf);
     __syncthreads();
+    if (kb + 1 < nkb) pload(k0 + 32);
 #pragma unroll 1
     for (int tap = 0; tap < TAPS; ++tap) {
       if (tap + 1 < TAPS) aload(tap + 1, k0);
+      else if (kb + 1 < nkb) aload(0, k0 + 32);
       const __bf16* As = smem + buf * A_SZ;
       const int kh = tap / KW, kw = tap - (tap / KW) * KW;
       const int toff = (kh * PW + kw) * PC_STR;
@@ -209,6 +223,7 @@ __global__ __launch_bounds__(256, 2) void pconv_kernel(PcArgs g) {
 // bf16 tap-major weights (same modes as dsgan_conv_wtrans):
 //   mode 0 (forward):      Wb[tap][co][ci], tap = (kh, kw)
 //   mode 1 (data-grad s1): Wb[tap][ci][co], tap = (kh', kw') with kh = KH-1-kh', kw = KW-1-kw'
+//   mode 2 (stride-2 data-grad / ConvTranspose, pconvt.hip): Wb[tap][ci][co], tap = (kh, kw)
 __global__ void wtrans_bf16_kernel(const float* __restrict__ W, __bf16* __restrict__ Wb, int Co, int Ci, int KH,
                                    int KW, int mode) {
   const int M = mode == 0 ? Co : Ci, K = mode == 0 ? Ci : Co;
@@ -219,6 +234,7 @@ __global__ void wtrans_bf16_kernel(const float* __restrict__ W, __bf16* __restri
     const int m = t % M, tap = t / M;
     int kh = tap / KW, kw = tap % KW, co = m, ci = k;
     if (mode == 1) { kh = KH - 1 - kh; kw = KW - 1 - kw; co = k; ci = m; }
+    if (mode == 2) { co = k; ci = m; }
     Wb[e] = (__bf16)W[(((long)co * Ci + ci) * KH + kh) * KW + kw];
   }
 }
@@ -251,7 +267,7 @@ int dsgan_pconv_supported(int K, int KH, int KW, int stride) {
 }
 
 int dsgan_conv_wtrans_bf16(const float* W, void* Wb, int Co, int Ci, int KH, int KW, int mode, hipStream_t st) {
-  DSG_REQUIRE(W && Wb && (mode == 0 || mode == 1), "dsgan_conv_wtrans_bf16: bad args");
+  DSG_REQUIRE(W && Wb && mode >= 0 && mode <= 2, "dsgan_conv_wtrans_bf16: bad args");
   const long total = (long)KH * KW * Co * Ci;
   long blocks = (total + 255) / 256;
   if (blocks > 8192) blocks = 8192;

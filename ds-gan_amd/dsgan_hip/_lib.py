@@ -39,6 +39,9 @@ SIGNATURES = {
     "dsgan_pconv_supported": [I, I, I, I],
     "dsgan_conv_wtrans_bf16": [P, P, I, I, I, I, I, S],
     "dsgan_pconv": [P, L, P, P, P, L, P, L] + [I] * 13 + [F, I, S],
+    # pconvt.hip
+    "dsgan_pconvt_supported": [I, I, I, I],
+    "dsgan_pconvt": [P, L, P, P, P, L, P, L] + [I] * 11 + [F, I, S],
     # wconv.hip
     "dsgan_wconv_supported": [I, I, I, I],
     "dsgan_wconv_workspace": [I, I, I, I, I, I, I],

@@ -185,7 +185,8 @@ def _wtrans_build(w, mode, kh0=0, kw0=0, nth=0, ntw=0):
 
 
 def _wtrans_bf16(w, mode):
-    """bf16 tap-major weights for pconv.hip (mode 0 forward, 1 stride-1 data-grad), cached."""
+    """bf16 tap-major weights for pconv.hip / pconvt.hip (mode 0 forward, 1 stride-1 data-grad,
+    2 stride-2 data-grad / ConvTranspose), cached."""
     key = (id(w), w.data_ptr(), tuple(w.shape), "bf16", mode)
     ent = _WT_CACHE.get(key)
     gen = WEIGHT_GEN[0]
@@ -280,6 +281,13 @@ def conv_dgrad_raw(dy, w, x_shape, stride, pad, bias=None, act=None, gpre=None, 
         fam = "pconv_kernel"
         _pconv(dy, dybs, _wtrans_bf16(w, 1), None, dx, dxbs, N, Cout, Cin, Ho, Wo, H, W, KH, KW, 1,
                KH - 1 - pad, None, gpre, gbs, gact, accumulate)
+    elif (_state["prec"] == "bf16" and w.dim() == 4 and stride == 2 and pad == 1 and KH == KW and act is None
+          and H <= 2 * Ho and H > 2 * Ho - 2 and W <= 2 * Wo and W > 2 * Wo - 2 and W % 2 == 0 and dxbs % 2 == 0
+          and (gpre is None or gbs % 2 == 0) and _lib.load().dsgan_pconvt_supported(Cout, KH, stride, pad)):
+        # stride-2 data-grad / ConvTranspose: all four output parities in one launch
+        fam = "pconvt_kernel"
+        call("dsgan_pconvt", ptr(dy), dybs, ptr(_wtrans_bf16(w, 2)), ptr(bias), ptr(dx), dxbs, ptr(gpre), gbs, N,
+             Cout, Cin, Ho, Wo, H, W, KH, stride, pad, ACT[gact], LRELU_SLOPE, int(accumulate), stream())
     elif (_state["prec"] == "bf16" and w.dim() == 4 and (KH > 1 or KW > 1) and Cout % 32 == 0
           and act is None and not accumulate and stride in (1, 2) and KH * KW <= 16):
         fam = "tconv_kernel"

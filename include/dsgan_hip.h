@@ -132,7 +132,8 @@ int dsgan_tconv(const float* X, long x_bs, const float* Wt, const float* bias, f
  * y[b][m][oh][ow] (+)= act(bias[m] + sum_{c,kh,kw} Wb[tap][m][c] x[b][c][oh*s-pad+kh][ow*s-pad+kw])
  *                     (* gact'(gpre[b][m][oh][ow]) when gpre != NULL).  bf16 MFMA, Cin % 32 == 0.
  * dsgan_conv_wtrans_bf16 builds Wb from an OIHW weight: mode 0 forward, mode 1 the flipped
- * transposed kernel of the stride-1 data-grad (then call with pad' = KH-1-pad). */
+ * transposed kernel of the stride-1 data-grad (then call with pad' = KH-1-pad), mode 2 the
+ * unflipped transposed kernel for dsgan_pconvt. */
 int dsgan_pconv_supported(int K, int KH, int KW, int stride);
 int dsgan_conv_wtrans_bf16(const float* W, void* Wb, int Co, int Ci, int KH, int KW, int mode,
                            hipStream_t stream);
@@ -140,6 +141,16 @@ int dsgan_pconv(const float* X, long x_bs, const void* Wb, const float* bias, fl
                 const float* gpre, long gpre_bs, int nb, int K, int M, int H, int W, int Ho, int Wo,
                 int KH, int KW, int stride, int pad, int act, int gact, float slope, int accumulate,
                 hipStream_t stream);
+
+/* ---- patch-staged stride-2 transposed conv (pconvt.hip): ConvTranspose2d(3, s2, p1, op1) forward
+ * (MixConvNeXtML.py:53,149-152) and the data-grad of the PatchGAN Conv2d(4, s2, p1)
+ * (DSGAN/models/networks.py:545-563) -- all four output parities from one staged input patch.
+ * y[b][m][2i+ph][2j+pw] (+)= (bias[m] + sum Wb[kh][kw][m][c] x[b][c][i+(ph+1-kh)/2][j+(pw+1-kw)/2])
+ *                          (* gact'(gpre)), bf16 MFMA, K % 32 == 0; Wb: dsgan_conv_wtrans_bf16 mode 2. */
+int dsgan_pconvt_supported(int K, int KS, int stride, int pad);
+int dsgan_pconvt(const float* X, long x_bs, const void* Wb, const float* bias, float* Y, long y_bs,
+                 const float* gpre, long gpre_bs, int nb, int K, int M, int Hi, int Wi, int Ho, int Wo,
+                 int KS, int stride, int pad, int gact, float slope, int accumulate, hipStream_t stream);
 
 /* ---- patch-staged conv weight-grad (wconv.hip): ConvTranspose2d 3x3/s2 weight-grads
  * (MixConvNeXtML.py:53,149-152, as the equivalent stride-2 conv) and PatchGAN 4x4 s2/s1

@@ -575,3 +575,35 @@ def test_perceptual_l1_fused(prec):
         lu.backward()
         assert abs(loss.item() - lu.item()) <= 1e-5 * abs(lu.item())
         assert rel(fd.grad, fu.grad) < 1e-3
+
+
+@pytest.mark.parametrize("N,Cout,Cin,Hi,Wi,K,H,W", [
+    (2, 64, 32, 8, 9, 3, 16, 18),        # ConvT 3x3/s2/op1 (ragged 8x9 grid vs 8x16 tiles)
+    (1, 128, 96, 16, 16, 3, 32, 32),     # M not a multiple of the 64 tile
+    (2, 64, 32, 17, 18, 4, 34, 36),      # data-grad of the PatchGAN 4x4/s2 conv
+    (2, 128, 64, 16, 16, 4, 32, 32),
+])
+def test_pconvt_bf16(N, Cout, Cin, Hi, Wi, K, H, W):
+    """pconvt.hip: the stride-2 data-grad / ConvTranspose with all four output parities in one
+    launch, vs torch's conv2d_input on bf16-rounded operands; bias, act'(gpre) and accumulate."""
+    from dsgan_hip import functional as HF
+    HF.set_precision("bf16")
+    g = torch.Generator().manual_seed(Cout + Cin + K + Hi)
+    dy = _q(torch.randn(N, Cout, Hi, Wi, generator=g), "bf16")
+    w = _q(torch.randn(Cout, Cin, K, K, generator=g) / math.sqrt(Cout * K * K / 4), "bf16")
+    b = torch.randn(Cin, generator=g) * 0.1
+    dx_ref = torch.nn.grad.conv2d_input((N, Cin, H, W), w.double(), dy.double(), stride=2, padding=1)
+    HF.IGEMM_TIMER.rec, HF.IGEMM_TIMER.on = [], True
+    try:
+        dx = HF.conv_dgrad_raw(dy.to(DEV), w.to(DEV), (N, Cin, H, W), 2, 1, bias=b.to(DEV))
+    finally:
+        HF.IGEMM_TIMER.on = False
+    assert HF.IGEMM_TIMER.rec[-1][4] == "pconvt_kernel"
+    assert rel(dx, dx_ref + b.double().view(1, -1, 1, 1)) < 1e-5
+    pre = torch.randn(N, Cin, H, W, generator=g)
+    y0 = torch.randn(N, Cin, H, W, generator=g)
+    out = y0.to(DEV)
+    HF.conv_dgrad_raw(dy.to(DEV), w.to(DEV), (N, Cin, H, W), 2, 1, gpre=pre.to(DEV), gact="lrelu", out=out,
+                      accumulate=True)
+    want = y0.double() + dx_ref * torch.where(pre > 0, 1.0, 0.2).double()
+    assert rel(out, want) < 1e-5
