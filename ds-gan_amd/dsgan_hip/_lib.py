@@ -39,6 +39,10 @@ SIGNATURES = {
     "dsgan_pconv_supported": [I, I, I, I],
     "dsgan_conv_wtrans_bf16": [P, P, I, I, I, I, I, S],
     "dsgan_pconv": [P, L, P, P, P, L, P, L] + [I] * 13 + [F, I, S],
+    # pwsmall.hip
+    "dsgan_pw_small_supported": [I, I, I, L, L],
+    "dsgan_pw_small": [P, L, P, I, I, P, P, L, P, L] + [I] * 8 + [F, S],
+    "dsgan_pw_small2": [P, L, P, I, I, P, L, P, I, P, P, L, P, L] + [I] * 8 + [F, S],
     # pconvt.hip
     "dsgan_pconvt_supported": [I, I, I, I],
     "dsgan_pconvt": [P, L, P, P, P, L, P, L] + [I] * 11 + [F, I, S],

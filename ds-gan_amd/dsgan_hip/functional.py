@@ -199,6 +199,12 @@ def _wtrans_bf16(w, mode):
     return wb
 
 
+def _pws_ok(K, M, P, xbs, ybs, x, y):
+    """1x1 contraction with <= 16 channels on one side for pwsmall.hip (16-byte rows)."""
+    return ((K <= 16 or M <= 16) and x.data_ptr() % 16 == 0 and y.data_ptr() % 16 == 0
+            and bool(_lib.load().dsgan_pw_small_supported(K, M, P, xbs, ybs)))
+
+
 def _pconv_ok(K, KH, KW, stride):
     return _state["prec"] == "bf16" and bool(_lib.load().dsgan_pconv_supported(K, KH, KW, stride))
 
@@ -223,7 +229,12 @@ def conv_fwd_raw(x, w, b, stride, pad, act=None, out=None, pre=None, accumulate=
         pre, pbs = nchw(pre)
     e0 = IGEMM_TIMER.begin()
     fam = "igemm_kernel"
-    if Cout <= 8 and act is None and pre is None and xact is None:
+    if KH == 1 and KW == 1 and stride == 1 and pad == 0 and pre is None and _pws_ok(Cin, Cout, H * W, xbs, ybs, x, y):
+        # 1x1 with <= 16 channels on one side (the 3/12-channel layers at 256^2): VALU stream
+        fam = "pw_small_kernel"
+        call("dsgan_pw_small", ptr(x), xbs, ptr(w), Cin, 1, ptr(b), ptr(y), ybs, None, 0, N, Cin, Cout, H * W,
+             ACT[act], ACT[xact], 0, int(accumulate), LRELU_SLOPE, stream())
+    elif Cout <= 8 and act is None and pre is None and xact is None:
         # few output channels (G head, PatchGAN last layer): direct conv, not a GEMM tile
         fam = "small_out_kernel"
         call("dsgan_conv_small_out", ptr(x), xbs, ptr(w), Cin * KH * KW, KH * KW, KW, 1, ptr(b), ptr(y), ybs,
@@ -265,7 +276,12 @@ def conv_dgrad_raw(dy, w, x_shape, stride, pad, bias=None, act=None, gpre=None, 
         gpre, gbs = nchw(gpre)
     e0 = IGEMM_TIMER.begin()
     fam = "igemm_kernel"
-    if Cin <= 8 and act is None and gpre is None and stride in (1, 2):
+    if (KH == 1 and KW == 1 and stride == 1 and pad == 0 and act is None and bias is None
+            and _pws_ok(Cout, Cin, H * W, dybs, dxbs, dy, dx) and (gpre is None or (gbs % 4 == 0 and gpre.data_ptr() % 16 == 0))):
+        fam = "pw_small_kernel"
+        call("dsgan_pw_small", ptr(dy), dybs, ptr(w), 1, Cin, None, ptr(dx), dxbs, ptr(gpre), gbs, N, Cout, Cin, H * W,
+             0, 0, ACT[gact], int(accumulate), LRELU_SLOPE, stream())
+    elif Cin <= 8 and act is None and gpre is None and stride in (1, 2):
         fam = "small_out_kernel"
         # data-grad into a 3/6-channel tensor: direct transposed gather, w(m=ci, k=co, kh, kw)
         call("dsgan_conv_small_out", ptr(dy), dybs, ptr(w), KH * KW, Cin * KH * KW, KW, 1, ptr(bias),
@@ -630,8 +646,17 @@ class PwMlpFn(torch.autograd.Function):
         w1v = w1.view(w1.shape[0], w1.shape[1], 1, 1)
         w2v = w2.view(w2.shape[0], w2.shape[1], 1, 1)
         z = conv_fwd_raw(h, w1v, b1, 1, 0)
-        out = conv_fwd_raw(x, ws, None, 1, 0)
-        conv_fwd_raw(z, w2v, b2, 1, 0, out=out, accumulate=True, xact="gelu")
+        x4, xbs = nchw(x)
+        if 5 * C <= 16 and _pws_ok(5 * C, P, H * W, xbs, P * H * W, x4, z) and z.data_ptr() % 16 == 0:
+            # tiny blocks (c1: 3 -> 12 -> 64 at 256^2): shortcut + pwconv2 in one streaming pass
+            out = _empty(N, P, H, W, h)
+            e0 = IGEMM_TIMER.begin()
+            call("dsgan_pw_small2", ptr(x4), xbs, ptr(ws), C, 1, ptr(z), 4 * C * H * W, ptr(w2), 4 * C, ptr(b2),
+                 ptr(out), P * H * W, None, 0, N, C, P, H * W, 0, ACT["gelu"], 0, 0, LRELU_SLOPE, stream())
+            IGEMM_TIMER.end(e0, 2.0 * N * H * W * P * 5 * C, ("fwd", N, 5 * C, H, W, P, 1, 1), "pw_small_kernel")
+        else:
+            out = conv_fwd_raw(x, ws, None, 1, 0)
+            conv_fwd_raw(z, w2v, b2, 1, 0, out=out, accumulate=True, xact="gelu")
         ctx.save_for_backward(h, x, z, w1v, w2v, ws)
         return out
 

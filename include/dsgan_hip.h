@@ -142,6 +142,21 @@ int dsgan_pconv(const float* X, long x_bs, const void* Wb, const float* bias, fl
                 int KH, int KW, int stride, int pad, int act, int gact, float slope, int accumulate,
                 hipStream_t stream);
 
+/* ---- 1x1 contractions with <= 16 channels on one side (pwsmall.hip): the 3/12-channel layers
+ * at 256^2 -- c1 pwconv1/pwconv2/shortcut, OriginMLKA.to32/shortcut (MixConvNeXtML.py:122,145,
+ * 218-224) and the data-grads into the 12-channel hidden.  Exact fp32 VALU (both modes):
+ * Y[b][m][p] (+)= act(bias[m] + sum_k W[m*wm + k*wk] * xact(X[b][k][p])) (* gact'(G[b][m][p])). */
+int dsgan_pw_small_supported(int K, int M, int P, long x_bs, long y_bs);
+int dsgan_pw_small(const float* X, long x_bs, const float* W, int wm, int wk, const float* bias, float* Y,
+                   long y_bs, const float* G, long g_bs, int nb, int K, int M, int P, int act, int xact,
+                   int gact, int accumulate, float slope, hipStream_t stream);
+/* two-input form (K + K2 <= 16): Y = act(bias + W X + W2 xact(X2)), W2 [M][K2] -- the c1 Block
+ * tail shortcut(x) + pwconv2(gelu(z)) (MixConvNeXtML.py:236-242) in one pass */
+int dsgan_pw_small2(const float* X, long x_bs, const float* W, int wm, int wk, const float* X2,
+                    long x2_bs, const float* W2, int K2, const float* bias, float* Y, long y_bs,
+                    const float* G, long g_bs, int nb, int K, int M, int P, int act, int xact, int gact,
+                    int accumulate, float slope, hipStream_t stream);
+
 /* ---- patch-staged stride-2 transposed conv (pconvt.hip): ConvTranspose2d(3, s2, p1, op1) forward
  * (MixConvNeXtML.py:53,149-152) and the data-grad of the PatchGAN Conv2d(4, s2, p1)
  * (DSGAN/models/networks.py:545-563) -- all four output parities from one staged input patch.
