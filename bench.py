@@ -53,6 +53,21 @@ def cpu_baseline(threads):
                 sample="oracle/dsgan_cpu.py OracleStep, fp32, 256x256, batch 2, %d timed steps after 1 warmup (%.1f s)" % (steps, dt))
 
 
+PMC_TRAFFIC = os.path.join(REPO, "profiles", "r01", "pmc_traffic.json")
+
+
+def pmc_traffic(family):
+    """HBM bytes per launch of a kernel family, from the committed rocprofv3 --pmc passes over
+    this same bench command (tools/gpu_pmc.sh -> tools/pmc_traffic.py; FETCH_SIZE doubled per
+    the gfx950 correction, + WRITE_SIZE).  None when that family was not profiled."""
+    try:
+        with open(PMC_TRAFFIC) as f:
+            fams = json.load(f)["families"]
+        return fams[family]["traffic_bytes_per_launch"] if family in fams else None
+    except (OSError, ValueError, KeyError):
+        return None
+
+
 def quality(steps=10, batch=2, size=256, threads=16):
     """'MS-SSIM Δ vs ref' of the BASELINE metric.  The GPU model (bench precision) and the CPU
     oracle (oracle/dsgan_cpu.py, the reference step restated in fp32 -- the checker, never the
@@ -180,7 +195,10 @@ def main():
                        "baseline_config": "configs[1]: 256x256, batch 16, bf16, 1xMI355X"},
             "roofline": {"bound": "mfma", "kernel": dom,
                          "achieved": round(dach, 2), "peak": peak, "unit": "TFLOP/s",
-                         "frac": round(dach / peak, 4), "traffic": None,
+                         "frac": round(dach / peak, 4), "traffic": pmc_traffic(dom),
+                         "traffic_unit": "HBM bytes per launch (rocprofv3 PMC, profiles/r01/pmc_traffic.json)",
+                         "traffic_gbs": (round(pmc_traffic(dom) / (dms / max(1, dn) * 1e-3) / 1e9, 1)
+                                         if pmc_traffic(dom) and dms > 0 else None),
                          "launches_per_step": round(dn / args.steps, 2),
                          "kernel_ms_per_step": round(dms / args.steps, 3),
                          "avg_launch_us": round(dms / max(1, dn) * 1e3, 1),

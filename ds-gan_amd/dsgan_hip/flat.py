@@ -63,5 +63,5 @@ class FlatAdam(torch.optim.Optimizer):
         call("dsgan_adam", ptr(self.flat.data), ptr(self.flat.grad), ptr(self.m), ptr(self.v),
              self.flat.numel, float(g["lr"]), float(b1), float(b2), float(g["eps"]),
              self.step_count, stream())
-        bump_weight_generation()
+        bump_weight_generation(self.flat.params)
         return None

@@ -159,16 +159,29 @@ WEIGHT_GEN = [0]
 _WT_CACHE = {}
 
 
-def bump_weight_generation():
-    WEIGHT_GEN[0] += 1
-    if len(_WT_CACHE) > 512:
+_PARAM_GEN = {}
+
+
+def bump_weight_generation(params=None):
+    """Invalidate cached weight transforms: of ``params`` (the ones an optimizer just updated),
+    or of every weight.  Frozen weights (VGG16) keep their bf16 / tap-major copies across steps."""
+    if params is None:
+        WEIGHT_GEN[0] += 1
+    else:
+        for p in params:
+            _PARAM_GEN[id(p)] = _PARAM_GEN.get(id(p), 0) + 1
+    if len(_WT_CACHE) > 8192:
         _WT_CACHE.clear()
+
+
+def _wgen(w):
+    return (WEIGHT_GEN[0], _PARAM_GEN.get(id(w), 0))
 
 
 def _wtrans(w, mode, kh0=0, kw0=0, nth=0, ntw=0):
     key = (id(w), w.data_ptr(), tuple(w.shape), mode, kh0, kw0, nth, ntw)
     ent = _WT_CACHE.get(key)
-    gen = WEIGHT_GEN[0]
+    gen = _wgen(w)
     if ent is not None and ent[0] == gen and ent[1] == w._version and ent[2] is w:
         return ent[3]
     wt = _wtrans_build(w, mode, kh0, kw0, nth, ntw)
@@ -189,7 +202,7 @@ def _wtrans_bf16(w, mode):
     2 stride-2 data-grad / ConvTranspose), cached."""
     key = (id(w), w.data_ptr(), tuple(w.shape), "bf16", mode)
     ent = _WT_CACHE.get(key)
-    gen = WEIGHT_GEN[0]
+    gen = _wgen(w)
     if ent is not None and ent[0] == gen and ent[1] == w._version and ent[2] is w:
         return ent[3]
     Co, Ci, KH, KW = w.shape
@@ -591,12 +604,12 @@ def bf16_weight(w):
     """bf16 copy of a parameter for the fused kernels, cached like _wtrans (same invalidation)."""
     key = (id(w), w.data_ptr(), tuple(w.shape))
     ent = _BF16_CACHE.get(key)
-    gen = WEIGHT_GEN[0]
+    gen = _wgen(w)
     if ent is not None and ent[0] == gen and ent[1] == w._version and ent[2] is w:
         return ent[3]
     out = torch.empty(w.shape, device=w.device, dtype=torch.bfloat16)
     call("dsgan_f32_to_bf16", ptr(w), ptr(out), w.numel(), stream())
-    if len(_BF16_CACHE) > 512:
+    if len(_BF16_CACHE) > 8192:
         _BF16_CACHE.clear()
     _BF16_CACHE[key] = (gen, w._version, w, out)
     return out
