@@ -42,6 +42,7 @@ struct PwArgs {
   int k_split;
   unsigned a_range, b_range;   // buffer-resource byte ranges of A and B (B: per image for FWD/DGRAD)
   int dbg;   // DSGAN_PW_DBG experiment switches: 1 skip epilogue stores, 2 skip global loads
+  int y_bf16;  // FWD: Y is bf16 [b][M][P] (y_bs in elements)
 };
 
 constexpr int PBK = 32;                 // K per main-loop step
@@ -69,11 +70,12 @@ __device__ __forceinline__ pbf16x4 cvt4(float4 v, int bact, float slope) {
   return r;
 }
 
-// ABF / BBF (WGRAD only): the A (dy) / B (x) operand is bf16 in HBM -- the gelu(z) and dz
+// ABF (WGRAD only) / BBF (WGRAD, FWD): the A (dy) / B (x) operand is bf16 in HBM -- the gelu(z)
+// and dz tensors of the MLPs (mlp.hip, and the unfused blocks' pwconv1 bf16 output g = gelu(z))
 // tensors written by the fused MLP backward (mlp.hip) -- and is copied to LDS unconverted.
 template <int MODE, int BM, int ABF = 0, int BBF = 0>
 __global__ __launch_bounds__(256, 2) void pwgemm_kernel(PwArgs g) {
-  static_assert(MODE == PW_WGRAD || (ABF == 0 && BBF == 0), "bf16 operands: WGRAD only");
+  static_assert((MODE == PW_WGRAD || ABF == 0) && (MODE != PW_DGRAD || BBF == 0), "bf16 operand modes");
   constexpr int BN = 128;
   constexpr int WM = 2, WN = 2;
   constexpr int TM = BM / WM / 32, TN = BN / WN / 32;
@@ -131,7 +133,7 @@ __global__ __launch_bounds__(256, 2) void pwgemm_kernel(PwArgs g) {
   const __amdgpu_buffer_rsrc_t rA = __builtin_amdgcn_make_buffer_rsrc(
       (void*)g.A, (short)0, g.a_range, 0x00020000);
   const __amdgpu_buffer_rsrc_t rB = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(g.B + (long)b_fix * g.b_bs), (short)0, g.b_range, 0x00020000);
+      (void*)((const char*)g.B + (long)b_fix * g.b_bs * (BBF ? 2 : 4)), (short)0, g.b_range, 0x00020000);
   auto bld4 = [](__amdgpu_buffer_rsrc_t r, unsigned voff) {
     return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)voff, 0, 0));
   };
@@ -176,7 +178,14 @@ __global__ __launch_bounds__(256, 2) void pwgemm_kernel(PwArgs g) {
       }
       ra[i] = bld4(rA, off);
     }
-    if constexpr (BBF) {                         // X[b][N][P] bf16, row n
+    if constexpr (BBF && MODE == PW_FWD) {       // X[b][K][P] bf16, k-major: row k, 8 pixels per item
+#pragma unroll
+      for (int i = 0; i < B_ITEMS; ++i) {
+        const int it = tid + i * 256;
+        const int k = kb + it / (BN / 8);
+        rhb[i] = bldh(rB, ((unsigned)k * g.P + p0 + (it % (BN / 8)) * 8) * 2u);
+      }
+    } else if constexpr (BBF) {                  // X[b][N][P] bf16, row n
 #pragma unroll
       for (int i = 0; i < B_ITEMS; ++i) {
         const int it = tid + i * 256;
@@ -227,7 +236,14 @@ __global__ __launch_bounds__(256, 2) void pwgemm_kernel(PwArgs g) {
         *reinterpret_cast<pbf16x4*>(Bs + off) = cv(rb[i]);
       }
     };
-    if constexpr (BBF) {
+    if constexpr (BBF && MODE == PW_FWD) {
+#pragma unroll
+      for (int i = 0; i < B_ITEMS; ++i) {
+        const int it = tid + i * 256;
+        *reinterpret_cast<pu32x4*>(Bs + (it / (BN / 8)) * B_STR + (it % (BN / 8)) * 8) = rhb[i];
+      }
+      return;
+    } else if constexpr (BBF) {
 #pragma unroll
       for (int i = 0; i < B_ITEMS; ++i) {
         const int it = tid + i * 256;
@@ -329,6 +345,8 @@ __global__ __launch_bounds__(256, 2) void pwgemm_kernel(PwArgs g) {
   const unsigned range = (unsigned)(((long)g.M * g.P - p0) * 4);
   const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(g.Y + (long)bimg * g.y_bs + p0), (short)0, range, 0x00020000);
+  const __amdgpu_buffer_rsrc_t ryh = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)((__bf16*)g.Y + (long)bimg * g.y_bs + p0), (short)0, range / 2, 0x00020000);
   __amdgpu_buffer_rsrc_t rp = ry, rg = ry;
   if (g.ypre) rp = __builtin_amdgcn_make_buffer_rsrc((void*)(g.ypre + (long)bimg * g.ypre_bs + p0), (short)0, range, 0x00020000);
   if (g.gpre) rg = __builtin_amdgcn_make_buffer_rsrc((void*)(g.gpre + (long)bimg * g.gpre_bs + p0), (short)0, range, 0x00020000);
@@ -376,6 +394,15 @@ __global__ __launch_bounds__(256, 2) void pwgemm_kernel(PwArgs g) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) t += v[r];
         if (t == 1234.5678f) g.Y[0] = t;
+        continue;
+      }
+      if (g.y_bf16) {   // bf16 output: same rows, half the byte offsets
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const unsigned short hb = __builtin_bit_cast(unsigned short, (__bf16)v[r]);
+          __builtin_amdgcn_raw_buffer_store_b16(hb, ryh, vrow[r] == (int)PW_OOB ? (int)PW_OOB : vrow[r] / 2,
+                                                (mrow + (r & 3) + 8 * (r >> 2)) * (P4 / 2), 0);
+        }
         continue;
       }
 #pragma unroll
@@ -466,6 +493,31 @@ extern "C" int dsgan_pw_gemm(int mode, const float* A, long a_bs, const float* B
     if (mode == PW_FWD) { if (big) pw_launch<PW_FWD, 128>(g, 1, st); else pw_launch<PW_FWD, 64>(g, 1, st); }
     else { if (big) pw_launch<PW_DGRAD, 128>(g, 1, st); else pw_launch<PW_DGRAD, 64>(g, 1, st); }
   }
+  DSG_CHECK_LAUNCH();
+  return 0;
+}
+
+// Forward with bf16 activations in and/or out (the unfused MLP blocks): Y[b][M][P] (+)=
+// act(W X + bias), X fp32 or bf16 (x_bf16), Y fp32 or bf16 (y_bf16; accumulate needs fp32 Y),
+// ypre (fp32, nullable) = the pre-activation.  P % 128 == 0, K % 8 == 0, 16-byte aligned.
+extern "C" int dsgan_pw_fwd_io(const float* W, const void* X, long x_bs, int x_bf16, void* Y, long y_bs, int y_bf16,
+                               const float* bias, float* ypre, long ypre_bs, int M, int K, int P, int nb, int act,
+                               int accumulate, float slope, hipStream_t st) {
+  DSG_REQUIRE(W && X && Y && M >= 16 && K > 0 && P > 0 && nb > 0, "dsgan_pw_fwd_io: bad args");
+  DSG_REQUIRE(P % 128 == 0 && K % 8 == 0 && al16(W) && al16(X) && al16(Y) && (x_bs & 7) == 0 && (y_bs & 7) == 0 &&
+                  !(y_bf16 && accumulate),
+              "dsgan_pw_fwd_io: unsupported shape/alignment");
+  DSG_REQUIRE((long)M * P * 4 < (1L << 32) && (long)K * P * 4 < (long)PW_OOB && (long)M * K * 4 < (long)PW_OOB,
+              "dsgan_pw_fwd_io: operand exceeds the 4 GiB buffer range");
+  PwArgs g{};
+  g.A = W; g.a_bs = 0; g.B = (const float*)X; g.b_bs = x_bs; g.Y = (float*)Y; g.y_bs = y_bs; g.bias = bias;
+  g.ypre = ypre; g.ypre_bs = ypre_bs; g.act = act; g.accumulate = accumulate; g.slope = slope; g.y_bf16 = y_bf16;
+  g.P = P; g.M = M; g.N = nb * P; g.K = K;
+  g.a_range = (unsigned)((long)M * K * 4);
+  g.b_range = (unsigned)((long)K * P * (x_bf16 ? 2 : 4));
+  const bool big = M > 64;
+  if (x_bf16) { if (big) pw_launch<PW_FWD, 128, 0, 1>(g, 1, st); else pw_launch<PW_FWD, 64, 0, 1>(g, 1, st); }
+  else { if (big) pw_launch<PW_FWD, 128>(g, 1, st); else pw_launch<PW_FWD, 64>(g, 1, st); }
   DSG_CHECK_LAUNCH();
   return 0;
 }

@@ -658,6 +658,25 @@ class PwMlpFn(torch.autograd.Function):
             return out
         w1v = w1.view(w1.shape[0], w1.shape[1], 1, 1)
         w2v = w2.view(w2.shape[0], w2.shape[1], 1, 1)
+        ctx.g = None
+        if _state["prec"] == "bf16" and H * W % 128 == 0 and C % 8 == 0 and h.data_ptr() % 16 == 0:
+            # large blocks: pwconv1 writes z (fp32, for gelu'(z)) AND g = gelu(z) in bf16 once;
+            # pwconv2 and the W2 weight-grad stream the bf16 g (no GELU recomputed per tile)
+            C4, HW = 4 * C, H * W
+            z = _empty(N, C4, H, W, h)
+            g = torch.empty((N, C4, H, W), device=h.device, dtype=torch.bfloat16)
+            e0 = IGEMM_TIMER.begin()
+            call("dsgan_pw_fwd_io", ptr(w1), ptr(h), hbs, 0, ptr(g), C4 * HW, 1, ptr(b1), ptr(z), C4 * HW, C4, C, HW,
+                 N, ACT["gelu"], 0, LRELU_SLOPE, stream())
+            IGEMM_TIMER.end(e0, 2.0 * N * HW * C4 * C, ("fwd", N, C, H, W, C4, 1, 1), "pwgemm_kernel")
+            out = conv_fwd_raw(x, ws, None, 1, 0)
+            e0 = IGEMM_TIMER.begin()
+            call("dsgan_pw_fwd_io", ptr(w2), ptr(g), C4 * HW, 1, ptr(out), P * HW, 0, ptr(b2), None, 0, P, C4, HW,
+                 N, 0, 1, LRELU_SLOPE, stream())
+            IGEMM_TIMER.end(e0, 2.0 * N * HW * C4 * P, ("fwd", N, C4, H, W, P, 1, 1), "pwgemm_kernel")
+            ctx.g = g
+            ctx.save_for_backward(h, x, z, w1v, w2v, ws)
+            return out
         z = conv_fwd_raw(h, w1v, b1, 1, 0)
         x4, xbs = nchw(x)
         if 5 * C <= 16 and _pws_ok(5 * C, P, H * W, xbs, P * H * W, x4, z) and z.data_ptr() % 16 == 0:
@@ -688,7 +707,15 @@ class PwMlpFn(torch.autograd.Function):
         # dz = (W2^T dy) * gelu'(z)
         dz = conv_dgrad_raw(dy, w2v, tuple(z.shape), 1, 0, gpre=z, gact="gelu")
         gw2, gb2, gws = _grad_buf(w2), _grad_buf(b2), _grad_buf(ws_ref)
-        if gw2 is not None:
+        if gw2 is not None and ctx.g is not None:
+            N, C4, H, W = z.shape
+            dy4, dybs = nchw(dy)
+            e0 = IGEMM_TIMER.begin()
+            call("dsgan_pw_wgrad_mixed", ptr(dy4), dybs, 0, ptr(ctx.g), C4 * H * W, 1, ptr(gw2), w2.shape[0], C4,
+                 H * W, N, stream())
+            IGEMM_TIMER.end(e0, 2.0 * N * H * W * C4 * w2.shape[0], ("wgrad", N, C4, H, W, w2.shape[0], 1, 1),
+                            "pwgemm_kernel")
+        elif gw2 is not None:
             conv_wgrad_raw(dy, z, gw2.view(w2v.shape), 1, 0, xact="gelu")
         if gb2 is not None:
             channel_sum_raw(dy, gb2)

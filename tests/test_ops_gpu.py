@@ -118,7 +118,8 @@ def test_conv_transpose(prec, N, Ci, Co, H):
 
 
 @pytest.mark.parametrize("prec", ["fp32", "bf16"])
-@pytest.mark.parametrize("N,C,H,P", [(2, 3, 16, 64), (2, 64, 8, 128), (2, 128, 12, 64)])
+@pytest.mark.parametrize("N,C,H,P", [(2, 3, 16, 64), (2, 64, 8, 128), (2, 128, 12, 64),
+                                     (2, 256, 16, 512)])   # unfused large block: bf16 g = gelu(z) path
 def test_pw_mlp(prec, N, C, H, P):
     """Block tail: shortcut(x) + W2 gelu(W1 h + b1) + b2 (MixConvNeXtML.py:236-242)."""
     from dsgan_hip import functional as HF

@@ -21,6 +21,26 @@ elif which == "vgg3":     # conv1_2 64->64 at 256^2
     b = torch.randn(64, device="cuda")
     f = lambda: HF.conv_fwd_raw(x, w, b, 1, 1, act="relu")
     fl = 2.0 * N * 64 * 64 * 9 * 256 * 256
+elif which == "pwfwd":     # uc1 pwconv2: gelu(z) 4096 -> 512 at 32^2
+    x = torch.randn(N, 4096, 32, 32, device="cuda"); w = torch.randn(512, 4096, 1, 1, device="cuda") * 0.02
+    y = torch.empty(N, 512, 32, 32, device="cuda")
+    f = lambda: HF.conv_fwd_raw(x, w, None, 1, 0, out=y, xact="gelu")
+    fl = 2.0 * N * 512 * 4096 * 1024
+elif which == "pwfwd2":    # uc2 pwconv1: 512 -> 2048 at 64^2
+    x = torch.randn(N, 512, 64, 64, device="cuda"); w = torch.randn(2048, 512, 1, 1, device="cuda") * 0.02
+    b = torch.randn(2048, device="cuda")
+    f = lambda: HF.conv_fwd_raw(x, w, b, 1, 0)
+    fl = 2.0 * N * 2048 * 512 * 4096
+elif which == "pwdgrad":   # uc2 pwconv2 data-grad: 256 -> 2048 at 64^2 (* gelu'(z))
+    dy = torch.randn(N, 256, 64, 64, device="cuda"); w = torch.randn(256, 2048, 1, 1, device="cuda") * 0.02
+    z = torch.randn(N, 2048, 64, 64, device="cuda")
+    f = lambda: HF.conv_dgrad_raw(dy, w, (N, 2048, 64, 64), 1, 0, gpre=z, gact="gelu")
+    fl = 2.0 * N * 2048 * 256 * 4096
+elif which == "pwwgrad":   # uc2 pwconv1 weight-grad: dz 2048 x h 512 over 16*64^2 pixels
+    dz = torch.randn(N, 2048, 64, 64, device="cuda"); x = torch.randn(N, 512, 64, 64, device="cuda")
+    dw = torch.zeros(2048, 512, 1, 1, device="cuda")
+    f = lambda: HF.conv_wgrad_raw(dz, x, dw, 1, 0)
+    fl = 2.0 * N * 2048 * 512 * 4096
 else:
     raise SystemExit("unknown op")
 f(); torch.cuda.synchronize()
