@@ -39,6 +39,22 @@ __device__ __forceinline__ float gelu_g(float x) {
   return cdf + x * (kInvSqrt2Pi * __expf(-0.5f * x * x));
 }
 
+// gelu(z) and gelu'(z) together for bf16 outputs: erfc by Abramowitz & Stegun 7.1.26
+// (|err| <= 1.5e-7, far below bf16 rounding); exp(-z^2/2) is shared by both.
+__device__ __forceinline__ void gelu_pair_fast(float z, float& g, float& gp) {
+  const float u = fabsf(z) * kInvSqrt2;
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, u, 1.f));
+  float p = fmaf(t, 1.061405429f, -1.453152027f);
+  p = fmaf(t, p, 1.421413741f);
+  p = fmaf(t, p, -0.284496736f);
+  p = fmaf(t, p, 0.254829592f);
+  const float e = __expf(-u * u);
+  const float he = 0.5f * t * p * e;
+  const float cdf = z >= 0.f ? 1.f - he : he;
+  g = z * cdf;
+  gp = fmaf(z * kInvSqrt2Pi, e, cdf);
+}
+
 __device__ __forceinline__ float act_f(int act, float x, float slope) {
   switch (act) {
     case ACT_GELU: return gelu_f(x);

@@ -43,6 +43,7 @@ struct PwArgs {
   unsigned a_range, b_range;   // buffer-resource byte ranges of A and B (B: per image for FWD/DGRAD)
   int dbg;   // DSGAN_PW_DBG experiment switches: 1 skip epilogue stores, 2 skip global loads
   int y_bf16;  // FWD: Y is bf16 [b][M][P] (y_bs in elements)
+  int gbf;     // FWD: ypre is bf16 and receives act'(pre);  DGRAD: gpre is a bf16 multiplier (no act')
 };
 
 constexpr int PBK = 32;                 // K per main-loop step
@@ -348,8 +349,12 @@ __global__ __launch_bounds__(256, 2) void pwgemm_kernel(PwArgs g) {
   const __amdgpu_buffer_rsrc_t ryh = __builtin_amdgcn_make_buffer_rsrc(
       (void*)((__bf16*)g.Y + (long)bimg * g.y_bs + p0), (short)0, range / 2, 0x00020000);
   __amdgpu_buffer_rsrc_t rp = ry, rg = ry;
-  if (g.ypre) rp = __builtin_amdgcn_make_buffer_rsrc((void*)(g.ypre + (long)bimg * g.ypre_bs + p0), (short)0, range, 0x00020000);
-  if (g.gpre) rg = __builtin_amdgcn_make_buffer_rsrc((void*)(g.gpre + (long)bimg * g.gpre_bs + p0), (short)0, range, 0x00020000);
+  // bf16 side tensors (gbf): same element offsets, byte offsets halved
+  const int esz = g.gbf ? 2 : 4;
+  if (g.ypre) rp = __builtin_amdgcn_make_buffer_rsrc((void*)((char*)g.ypre + ((long)bimg * g.ypre_bs + p0) * esz), (short)0,
+                                                     g.gbf ? range / 2 : range, 0x00020000);
+  if (g.gpre) rg = __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)g.gpre + ((long)bimg * g.gpre_bs + p0) * esz),
+                                                     (short)0, g.gbf ? range / 2 : range, 0x00020000);
   const int P4 = g.P * 4;
   const bool full = m0 + BM <= g.M;
 #pragma unroll
@@ -368,7 +373,14 @@ __global__ __launch_bounds__(256, 2) void pwgemm_kernel(PwArgs g) {
       float v[16];
 #pragma unroll
       for (int r = 0; r < 16; ++r) v[r] = acc[i][j][r];
-      if (g.gpre) {
+      if (g.gpre && g.gbf) {          // DGRAD: v *= gp, gp = act'(pre) stored bf16 by the forward
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const unsigned short hb = __builtin_amdgcn_raw_buffer_load_b16(
+              rg, vrow[r] == (int)PW_OOB ? (int)PW_OOB : vrow[r] / 2, (mrow + (r & 3) + 8 * (r >> 2)) * (P4 / 2), 0);
+          v[r] *= (float)__builtin_bit_cast(__bf16, hb);
+        }
+      } else if (g.gpre) {
         float gv[16];
 #pragma unroll
         for (int r = 0; r < 16; ++r)
@@ -376,13 +388,26 @@ __global__ __launch_bounds__(256, 2) void pwgemm_kernel(PwArgs g) {
                       rg, vrow[r], (mrow + (r & 3) + 8 * (r >> 2)) * P4, 0));
         act_g_mul_arr(g.gact, v, gv, g.slope);
       }
-      if (g.ypre) {
+      bool acted = false;
+      if (g.ypre && g.gbf) {          // FWD: ypre <- bf16 act'(pre), v <- act(pre) (one GELU evaluation)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          float a, ap;
+          if (g.act == ACT_GELU) gelu_pair_fast(v[r], a, ap);
+          else { a = act_f(g.act, v[r], g.slope); ap = act_g(g.act, v[r], g.slope); }
+          v[r] = a;
+          __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(unsigned short, (__bf16)ap), rp,
+                                                vrow[r] == (int)PW_OOB ? (int)PW_OOB : vrow[r] / 2,
+                                                (mrow + (r & 3) + 8 * (r >> 2)) * (P4 / 2), 0);
+        }
+        acted = true;
+      } else if (g.ypre) {
 #pragma unroll
         for (int r = 0; r < 16; ++r)
           __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v[r]), rp, vrow[r],
                                                 (mrow + (r & 3) + 8 * (r >> 2)) * P4, 0);
       }
-      act_f_arr(g.act, v, g.slope);
+      if (!acted) act_f_arr(g.act, v, g.slope);
       if (g.accumulate) {
 #pragma unroll
         for (int r = 0; r < 16; ++r)
@@ -498,11 +523,12 @@ extern "C" int dsgan_pw_gemm(int mode, const float* A, long a_bs, const float* B
 }
 
 // Forward with bf16 activations in and/or out (the unfused MLP blocks): Y[b][M][P] (+)=
-// act(W X + bias), X fp32 or bf16 (x_bf16), Y fp32 or bf16 (y_bf16; accumulate needs fp32 Y),
-// ypre (fp32, nullable) = the pre-activation.  P % 128 == 0, K % 8 == 0, 16-byte aligned.
+// act(W X + bias), X fp32 or bf16 (x_bf16), Y fp32 or bf16 (y_bf16; accumulate needs fp32 Y);
+// ypre (nullable): fp32 pre-activation, or (ypre_grad_bf16) bf16 act'(pre) for the backward.
+// P % 128 == 0, K % 8 == 0, 16-byte aligned.
 extern "C" int dsgan_pw_fwd_io(const float* W, const void* X, long x_bs, int x_bf16, void* Y, long y_bs, int y_bf16,
-                               const float* bias, float* ypre, long ypre_bs, int M, int K, int P, int nb, int act,
-                               int accumulate, float slope, hipStream_t st) {
+                               const void* ypre, long ypre_bs, int ypre_grad_bf16, const float* bias, int M, int K,
+                               int P, int nb, int act, int accumulate, float slope, hipStream_t st) {
   DSG_REQUIRE(W && X && Y && M >= 16 && K > 0 && P > 0 && nb > 0, "dsgan_pw_fwd_io: bad args");
   DSG_REQUIRE(P % 128 == 0 && K % 8 == 0 && al16(W) && al16(X) && al16(Y) && (x_bs & 7) == 0 && (y_bs & 7) == 0 &&
                   !(y_bf16 && accumulate),
@@ -511,13 +537,32 @@ extern "C" int dsgan_pw_fwd_io(const float* W, const void* X, long x_bs, int x_b
               "dsgan_pw_fwd_io: operand exceeds the 4 GiB buffer range");
   PwArgs g{};
   g.A = W; g.a_bs = 0; g.B = (const float*)X; g.b_bs = x_bs; g.Y = (float*)Y; g.y_bs = y_bs; g.bias = bias;
-  g.ypre = ypre; g.ypre_bs = ypre_bs; g.act = act; g.accumulate = accumulate; g.slope = slope; g.y_bf16 = y_bf16;
+  g.ypre = (float*)ypre; g.ypre_bs = ypre_bs; g.gbf = ypre_grad_bf16; g.act = act; g.accumulate = accumulate;
+  g.slope = slope; g.y_bf16 = y_bf16;
   g.P = P; g.M = M; g.N = nb * P; g.K = K;
   g.a_range = (unsigned)((long)M * K * 4);
   g.b_range = (unsigned)((long)K * P * (x_bf16 ? 2 : 4));
   const bool big = M > 64;
   if (x_bf16) { if (big) pw_launch<PW_FWD, 128, 0, 1>(g, 1, st); else pw_launch<PW_FWD, 64, 0, 1>(g, 1, st); }
   else { if (big) pw_launch<PW_FWD, 128>(g, 1, st); else pw_launch<PW_FWD, 64>(g, 1, st); }
+  DSG_CHECK_LAUNCH();
+  return 0;
+}
+
+// Data-grad with a bf16 multiplier: DX[b][M][p] (+)= (sum_k W[k][M] DY[b][k][p]) * GP[b][M][p],
+// GP = act'(pre) written by dsgan_pw_fwd_io (ypre_grad_bf16).  P % 128 == 0, 16-byte aligned.
+extern "C" int dsgan_pw_dgrad_gbf(const float* W, const float* DY, long dy_bs, float* DX, long dx_bs, const void* GP,
+                                  long gp_bs, int M, int K, int P, int nb, int accumulate, hipStream_t st) {
+  DSG_REQUIRE(W && DY && DX && GP && M > 0 && K > 0 && nb > 0, "dsgan_pw_dgrad_gbf: bad args");
+  DSG_REQUIRE(dsgan_pw_supported(PW_DGRAD, M, K, P, 0, dy_bs, W, DY) && al16(GP) && (gp_bs & 7) == 0,
+              "dsgan_pw_dgrad_gbf: unsupported shape/alignment");
+  DSG_REQUIRE((long)M * P * 4 < (1L << 32) && (long)K * P * 4 < (long)PW_OOB, "dsgan_pw_dgrad_gbf: operand too large");
+  PwArgs g{};
+  g.A = W; g.B = DY; g.b_bs = dy_bs; g.Y = DX; g.y_bs = dx_bs; g.gpre = (const float*)GP; g.gpre_bs = gp_bs; g.gbf = 1;
+  g.accumulate = accumulate; g.P = P; g.M = M; g.N = nb * P; g.K = K;
+  g.a_range = (unsigned)((long)M * K * 4);
+  g.b_range = (unsigned)((long)K * P * 4);
+  if (M > 64) pw_launch<PW_DGRAD, 128>(g, 1, st); else pw_launch<PW_DGRAD, 64>(g, 1, st);
   DSG_CHECK_LAUNCH();
   return 0;
 }

@@ -660,22 +660,22 @@ class PwMlpFn(torch.autograd.Function):
         w2v = w2.view(w2.shape[0], w2.shape[1], 1, 1)
         ctx.g = None
         if _state["prec"] == "bf16" and H * W % 128 == 0 and C % 8 == 0 and h.data_ptr() % 16 == 0:
-            # large blocks: pwconv1 writes z (fp32, for gelu'(z)) AND g = gelu(z) in bf16 once;
-            # pwconv2 and the W2 weight-grad stream the bf16 g (no GELU recomputed per tile)
+            # large blocks: pwconv1 evaluates GELU once and writes g = gelu(z) and gp = gelu'(z), both
+            # bf16; pwconv2 and the W2 weight-grad stream g, the pwconv2 data-grad multiplies by gp
             C4, HW = 4 * C, H * W
-            z = _empty(N, C4, H, W, h)
-            g = torch.empty((N, C4, H, W), device=h.device, dtype=torch.bfloat16)
+            gp = torch.empty((N, C4, H, W), device=h.device, dtype=torch.bfloat16)   # gelu'(z), for dz
+            g = torch.empty((N, C4, H, W), device=h.device, dtype=torch.bfloat16)    # gelu(z)
             e0 = IGEMM_TIMER.begin()
-            call("dsgan_pw_fwd_io", ptr(w1), ptr(h), hbs, 0, ptr(g), C4 * HW, 1, ptr(b1), ptr(z), C4 * HW, C4, C, HW,
-                 N, ACT["gelu"], 0, LRELU_SLOPE, stream())
+            call("dsgan_pw_fwd_io", ptr(w1), ptr(h), hbs, 0, ptr(g), C4 * HW, 1, ptr(gp), C4 * HW, 1, ptr(b1), C4, C,
+                 HW, N, ACT["gelu"], 0, LRELU_SLOPE, stream())
             IGEMM_TIMER.end(e0, 2.0 * N * HW * C4 * C, ("fwd", N, C, H, W, C4, 1, 1), "pwgemm_kernel")
             out = conv_fwd_raw(x, ws, None, 1, 0)
             e0 = IGEMM_TIMER.begin()
-            call("dsgan_pw_fwd_io", ptr(w2), ptr(g), C4 * HW, 1, ptr(out), P * HW, 0, ptr(b2), None, 0, P, C4, HW,
-                 N, 0, 1, LRELU_SLOPE, stream())
+            call("dsgan_pw_fwd_io", ptr(w2), ptr(g), C4 * HW, 1, ptr(out), P * HW, 0, None, 0, 0, ptr(b2), P, C4,
+                 HW, N, 0, 1, LRELU_SLOPE, stream())
             IGEMM_TIMER.end(e0, 2.0 * N * HW * C4 * P, ("fwd", N, C4, H, W, P, 1, 1), "pwgemm_kernel")
             ctx.g = g
-            ctx.save_for_backward(h, x, z, w1v, w2v, ws)
+            ctx.save_for_backward(h, x, gp, w1v, w2v, ws)
             return out
         z = conv_fwd_raw(h, w1v, b1, 1, 0)
         x4, xbs = nchw(x)
@@ -704,8 +704,17 @@ class PwMlpFn(torch.autograd.Function):
         h, x, z, w1v, w2v, ws = ctx.saved_tensors
         w1, b1, w2, b2, ws_ref = ctx.refs
         dy = dy.contiguous()
-        # dz = (W2^T dy) * gelu'(z)
-        dz = conv_dgrad_raw(dy, w2v, tuple(z.shape), 1, 0, gpre=z, gact="gelu")
+        # dz = (W2^T dy) * gelu'(z)   (z slot holds the bf16 gelu'(z) on the bf16-g path)
+        if ctx.g is not None:
+            N, C4, H, W = z.shape
+            dz = _empty(N, C4, H, W, dy)
+            e0 = IGEMM_TIMER.begin()
+            call("dsgan_pw_dgrad_gbf", ptr(w2), ptr(dy), w2.shape[0] * H * W, ptr(dz), C4 * H * W, ptr(z), C4 * H * W,
+                 C4, w2.shape[0], H * W, N, 0, stream())
+            IGEMM_TIMER.end(e0, 2.0 * N * H * W * C4 * w2.shape[0], ("dgrad", N, C4, H, W, w2.shape[0], 1, 1),
+                            "pwgemm_kernel")
+        else:
+            dz = conv_dgrad_raw(dy, w2v, tuple(z.shape), 1, 0, gpre=z, gact="gelu")
         gw2, gb2, gws = _grad_buf(w2), _grad_buf(b2), _grad_buf(ws_ref)
         if gw2 is not None and ctx.g is not None:
             N, C4, H, W = z.shape
