@@ -163,6 +163,218 @@ __global__ __launch_bounds__(NT == 64 ? 256 : NT) void instnorm_bwd_kernel(INBwd
   }
 }
 
+// ---- float4 forms (HW % 4 == 0, 16-byte aligned planes: every G/D plane but PatchGAN's 31x31) ----
+// Same math as above with 16-byte accesses: the scalar forms issue 256-byte wave loads and
+// reach only 2-4 TB/s on 64K/16K-pixel planes.  C4 float4s per thread are cached in registers
+// (C4 == 0: the plane streams, three passes fwd / five bwd); the bwd caches g and, with CX,
+// xhat too (x is then read once).
+template <int NT>
+__device__ __forceinline__ float2 plane_sum2(float u, float v, float* sh) {
+  u = warp_sum(u);
+  v = warp_sum(v);
+  if (NT == 64) return make_float2(u, v);
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  __syncthreads();
+  if (l == 0) { sh[w] = u; sh[NT / 64 + w] = v; }
+  __syncthreads();
+  float2 r = make_float2(0.f, 0.f);
+#pragma unroll
+  for (int i = 0; i < NT / 64; ++i) { r.x += sh[i]; r.y += sh[NT / 64 + i]; }
+  return r;
+}
+
+__device__ __forceinline__ float hsum4(float4 v) { return (v.x + v.y) + (v.z + v.w); }
+
+template <int NT, int C4>
+__global__ __launch_bounds__(NT == 64 ? 256 : NT) void instnorm_fwd_v4(INArgs a) {
+  __shared__ float sh[32];
+  const int plane = blockIdx.x * (NT == 64 ? 4 : 1) + (NT == 64 ? (threadIdx.x >> 6) : 0);
+  const int t = NT == 64 ? (threadIdx.x & 63) : threadIdx.x;
+  if (plane >= a.N * a.C) return;
+  const int n = plane / a.C, c = plane - n * a.C;
+  const int HW4 = a.HW >> 2;
+  const float4* x = reinterpret_cast<const float4*>(a.x + (long)n * a.x_bs + (long)c * a.HW);
+  float4* y = reinterpret_cast<float4*>(a.y + (long)n * a.y_bs + (long)c * a.HW);
+  const float4* r = a.res ? reinterpret_cast<const float4*>(a.res + (long)n * a.res_bs + (long)c * a.HW) : nullptr;
+  const float s = a.scale ? a.scale[plane] : 1.f;
+  const float inv = 1.f / (float)a.HW;
+  auto out = [&](int i, float4 v, float mean, float rs) {
+    v.x = (v.x - mean) * rs; v.y = (v.y - mean) * rs; v.z = (v.z - mean) * rs; v.w = (v.w - mean) * rs;
+    if (r) { const float4 q = r[i]; v.x += q.x; v.y += q.y; v.z += q.z; v.w += q.w; }
+    v.x = act_f(a.act, v.x, a.slope); v.y = act_f(a.act, v.y, a.slope);
+    v.z = act_f(a.act, v.z, a.slope); v.w = act_f(a.act, v.w, a.slope);
+    y[i] = v;
+  };
+  auto ld = [&](int i) -> float4 {
+    float4 v = x[i];
+    v.x *= s; v.y *= s; v.z *= s; v.w *= s;
+    return v;
+  };
+  if constexpr (C4 > 0) {
+    float4 rv[C4];
+    float sum = 0.f;
+#pragma unroll
+    for (int j = 0; j < C4; ++j) {
+      const int i = t + j * NT;
+      rv[j] = i < HW4 ? ld(i) : make_float4(0.f, 0.f, 0.f, 0.f);
+      sum += hsum4(rv[j]);
+    }
+    const float mean = plane_sum<NT>(sum, sh) * inv;
+    float sq = 0.f;
+#pragma unroll
+    for (int j = 0; j < C4; ++j) {
+      if (t + j * NT < HW4) {
+        const float dx = rv[j].x - mean, dy = rv[j].y - mean, dz = rv[j].z - mean, dw = rv[j].w - mean;
+        sq += (dx * dx + dy * dy) + (dz * dz + dw * dw);
+      }
+    }
+    const float rs = 1.f / sqrtf(plane_sum<NT>(sq, sh) * inv + a.eps);
+    if (t == 0) { a.mean[plane] = mean; a.rstd[plane] = rs; }
+#pragma unroll
+    for (int j = 0; j < C4; ++j) {
+      const int i = t + j * NT;
+      if (i < HW4) out(i, rv[j], mean, rs);
+    }
+  } else {
+    float sum = 0.f;
+    for (int i0 = t; i0 < HW4; i0 += 4 * NT) {
+      float4 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = i0 + u * NT < HW4 ? ld(i0 + u * NT) : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) sum += hsum4(v[u]);
+    }
+    const float mean = plane_sum<NT>(sum, sh) * inv;
+    float sq = 0.f;
+    for (int i0 = t; i0 < HW4; i0 += 4 * NT) {
+      float4 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = i0 + u * NT < HW4 ? ld(i0 + u * NT) : make_float4(mean, mean, mean, mean);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const float dx = v[u].x - mean, dy = v[u].y - mean, dz = v[u].z - mean, dw = v[u].w - mean;
+        sq += (dx * dx + dy * dy) + (dz * dz + dw * dw);
+      }
+    }
+    const float rs = 1.f / sqrtf(plane_sum<NT>(sq, sh) * inv + a.eps);
+    if (t == 0) { a.mean[plane] = mean; a.rstd[plane] = rs; }
+    for (int i0 = t; i0 < HW4; i0 += 4 * NT) {
+      float4 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) if (i0 + u * NT < HW4) v[u] = ld(i0 + u * NT);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) if (i0 + u * NT < HW4) out(i0 + u * NT, v[u], mean, rs);
+    }
+  }
+}
+
+template <int NT, int C4, bool CX>
+__global__ __launch_bounds__(NT == 64 ? 256 : NT) void instnorm_bwd_v4(INBwdArgs a) {
+  __shared__ float sh[32];
+  const int plane = blockIdx.x * (NT == 64 ? 4 : 1) + (NT == 64 ? (threadIdx.x >> 6) : 0);
+  const int t = NT == 64 ? (threadIdx.x & 63) : threadIdx.x;
+  if (plane >= a.N * a.C) return;
+  const int n = plane / a.C, c = plane - n * a.C;
+  const long po = (long)c * a.HW;
+  const int HW4 = a.HW >> 2;
+  const float4* x = reinterpret_cast<const float4*>(a.x + (long)n * a.x_bs + po);
+  const float4* dy = reinterpret_cast<const float4*>(a.dy + (long)n * a.dy_bs + po);
+  const float4* r = a.res ? reinterpret_cast<const float4*>(a.res + (long)n * a.res_bs + po) : nullptr;
+  float4* dres = a.dres ? reinterpret_cast<float4*>(a.dres + (long)n * a.dres_bs + po) : nullptr;
+  float4* dx = reinterpret_cast<float4*>(a.dx + (long)n * a.dx_bs + po);
+  const float s = a.scale ? a.scale[plane] : 1.f;
+  const float mean = a.mean[plane], rs = a.rstd[plane];
+  const float inv = 1.f / (float)a.HW;
+  auto xhat = [&](int i) -> float4 {
+    float4 v = x[i];
+    v.x = (v.x * s - mean) * rs; v.y = (v.y * s - mean) * rs; v.z = (v.z * s - mean) * rs; v.w = (v.w * s - mean) * rs;
+    return v;
+  };
+  auto grad = [&](int i, float4 xh) -> float4 {
+    float4 g = dy[i];
+    if (a.act != ACT_NONE) {
+      float4 z = xh;
+      if (r) { const float4 q = r[i]; z.x += q.x; z.y += q.y; z.z += q.z; z.w += q.w; }
+      g.x *= act_g(a.act, z.x, a.slope); g.y *= act_g(a.act, z.y, a.slope);
+      g.z *= act_g(a.act, z.z, a.slope); g.w *= act_g(a.act, z.w, a.slope);
+    }
+    if (dres) dres[i] = g;
+    return g;
+  };
+  auto fin = [&](int i, float4 g, float4 xh, float mg, float mgh) {
+    const float k = s * rs;
+    dx[i] = make_float4(k * (g.x - mg - xh.x * mgh), k * (g.y - mg - xh.y * mgh), k * (g.z - mg - xh.z * mgh),
+                        k * (g.w - mg - xh.w * mgh));
+  };
+  float sg = 0.f, sgh = 0.f;
+  float2 m;
+  if constexpr (C4 > 0) {
+    float4 gv[C4];
+    float4 xv[CX ? C4 : 1];
+#pragma unroll
+    for (int j = 0; j < C4; ++j) {
+      const int i = t + j * NT;
+      gv[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (i < HW4) {
+        const float4 xh = xhat(i);
+        if constexpr (CX) xv[j] = xh;
+        gv[j] = grad(i, xh);
+        sg += hsum4(gv[j]);
+        sgh += (gv[j].x * xh.x + gv[j].y * xh.y) + (gv[j].z * xh.z + gv[j].w * xh.w);
+      }
+    }
+    m = plane_sum2<NT>(sg, sgh, sh);
+    m.x *= inv; m.y *= inv;
+#pragma unroll
+    for (int j = 0; j < C4; ++j) {
+      const int i = t + j * NT;
+      if (i < HW4) {
+        if constexpr (CX) fin(i, gv[j], xv[j], m.x, m.y);
+        else fin(i, gv[j], xhat(i), m.x, m.y);
+      }
+    }
+  } else {
+    for (int i0 = t; i0 < HW4; i0 += 2 * NT) {
+      float4 xh[2], g[2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) if (i0 + u * NT < HW4) xh[u] = xhat(i0 + u * NT);
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        if (i0 + u * NT < HW4) {
+          g[u] = grad(i0 + u * NT, xh[u]);
+          sg += hsum4(g[u]);
+          sgh += (g[u].x * xh[u].x + g[u].y * xh[u].y) + (g[u].z * xh[u].z + g[u].w * xh[u].w);
+        }
+      }
+    }
+    m = plane_sum2<NT>(sg, sgh, sh);
+    m.x *= inv; m.y *= inv;
+    for (int i0 = t; i0 < HW4; i0 += 2 * NT) {
+      float4 xh[2], g[2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        if (i0 + u * NT < HW4) {
+          xh[u] = xhat(i0 + u * NT);
+          g[u] = dy[i0 + u * NT];
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        if (i0 + u * NT < HW4) {
+          if (a.act != ACT_NONE) {
+            float4 z = xh[u];
+            if (r) { const float4 q = r[i0 + u * NT]; z.x += q.x; z.y += q.y; z.z += q.z; z.w += q.w; }
+            g[u].x *= act_g(a.act, z.x, a.slope); g[u].y *= act_g(a.act, z.y, a.slope);
+            g[u].z *= act_g(a.act, z.z, a.slope); g[u].w *= act_g(a.act, z.w, a.slope);
+          }
+          fin(i0 + u * NT, g[u], xh[u], m.x, m.y);
+        }
+      }
+    }
+  }
+  if (a.dscale && t == 0) a.dscale[plane] = m.y * (float)a.HW * a.eps * rs * rs / s;
+}
+
 // ---------------------------------------------------------------------------------------
 // MaxPool2d(k) (stride k, no padding, floor): DSGAN/models/model/MixConvNeXtML.py:71,194,333-417
 // Indices are the plane-flat argmax ih*W+iw, first maximum in row-major window order, NaN wins
@@ -520,6 +732,17 @@ using namespace dsg;
 
 extern "C" {
 
+// float4 InstanceNorm kernels: DSGAN_IN_V4 = 0 (scalar kernels), 1 (64K-pixel planes stream),
+// 2 (default: 64K-pixel planes cached in registers; measured 1.45x faster fwd and bwd).
+static int in_v4_mode() {
+  static int m = -1;
+  if (m < 0) { const char* e = getenv("DSGAN_IN_V4"); m = e ? atoi(e) : 2; }
+  return m;
+}
+static inline bool in_v4_ok(int HW, const void* p, long bs) {
+  return (HW & 3) == 0 && (bs & 3) == 0 && (((uintptr_t)p) & 15) == 0;
+}
+
 static int in_big_mode() {
   static int m = -1;
   if (m < 0) { const char* e = getenv("DSGAN_IN_BIG"); m = e ? atoi(e) : 0; }
@@ -532,6 +755,21 @@ int dsgan_instnorm_fwd(const float* x, long x_bs, const float* scale, const floa
   DSG_REQUIRE(x && y && mean && rstd && N > 0 && C > 0 && HW > 0, "dsgan_instnorm_fwd: bad args");
   INArgs a{x, x_bs, scale, res, res_bs, y, y_bs, mean, rstd, N, C, HW, act, slope, eps};
   const int planes = N * C;
+  const int v4 = in_v4_ok(HW, x, x_bs) && in_v4_ok(HW, y, y_bs) && (!res || in_v4_ok(HW, res, res_bs));
+  if (v4 && in_v4_mode() > 0) {
+    if (HW <= 64 * 16)
+      hipLaunchKernelGGL((instnorm_fwd_v4<64, 4>), dim3(cdiv(planes, 4)), dim3(256), 0, st, a);
+    else if (HW <= 256 * 16)
+      hipLaunchKernelGGL((instnorm_fwd_v4<256, 4>), dim3(planes), dim3(256), 0, st, a);
+    else if (HW <= 256 * 64)
+      hipLaunchKernelGGL((instnorm_fwd_v4<256, 16>), dim3(planes), dim3(256), 0, st, a);
+    else if (HW <= 1024 * 64 && in_v4_mode() == 2)
+      hipLaunchKernelGGL((instnorm_fwd_v4<1024, 16>), dim3(planes), dim3(1024), 0, st, a);
+    else
+      hipLaunchKernelGGL((instnorm_fwd_v4<1024, 0>), dim3(planes), dim3(1024), 0, st, a);
+    DSG_CHECK_LAUNCH();
+    return 0;
+  }
   if (HW <= 64 * 16)
     hipLaunchKernelGGL((instnorm_fwd_kernel<64, 16>), dim3(cdiv(planes, 4)), dim3(256), 0, st, a);
   else if (HW <= 256 * 16)
@@ -556,6 +794,22 @@ int dsgan_instnorm_bwd(const float* dy, long dy_bs, const float* x, long x_bs, c
   INBwdArgs a{dy, dy_bs, x, x_bs, scale, res, res_bs, mean, rstd, dx, dx_bs, dres, dres_bs, dscale,
               N, C, HW, act, slope, eps};
   const int planes = N * C;
+  const int v4 = in_v4_ok(HW, dy, dy_bs) && in_v4_ok(HW, x, x_bs) && in_v4_ok(HW, dx, dx_bs) &&
+                 (!res || in_v4_ok(HW, res, res_bs)) && (!dres || in_v4_ok(HW, dres, dres_bs));
+  if (v4 && in_v4_mode() > 0) {
+    if (HW <= 64 * 16)
+      hipLaunchKernelGGL((instnorm_bwd_v4<64, 4, true>), dim3(cdiv(planes, 4)), dim3(256), 0, st, a);
+    else if (HW <= 256 * 16)
+      hipLaunchKernelGGL((instnorm_bwd_v4<256, 4, true>), dim3(planes), dim3(256), 0, st, a);
+    else if (HW <= 256 * 64)
+      hipLaunchKernelGGL((instnorm_bwd_v4<256, 16, true>), dim3(planes), dim3(256), 0, st, a);
+    else if (HW <= 1024 * 64 && in_v4_mode() == 2)
+      hipLaunchKernelGGL((instnorm_bwd_v4<1024, 16, false>), dim3(planes), dim3(1024), 0, st, a);
+    else
+      hipLaunchKernelGGL((instnorm_bwd_v4<1024, 0, false>), dim3(planes), dim3(1024), 0, st, a);
+    DSG_CHECK_LAUNCH();
+    return 0;
+  }
   if (HW <= 64 * 16)
     hipLaunchKernelGGL((instnorm_bwd_kernel<64, 16>), dim3(cdiv(planes, 4)), dim3(256), 0, st, a);
   else if (HW <= 256 * 16)

@@ -290,7 +290,10 @@ def test_dwconv_accumulate(K, H, W):
 
 @pytest.mark.parametrize("act", [None, "gelu", "lrelu"])
 @pytest.mark.parametrize("res", [False, True])
-@pytest.mark.parametrize("N,C,H,W", [(2, 3, 4, 4), (2, 5, 33, 31), (1, 2, 80, 80), (2, 4, 16, 16)])
+# sizes cover every kernel variant: scalar (HW % 4 != 0), float4 wave-per-plane (<= 1K, ragged
+# tail), 256-thread cached (<= 4K, <= 16K), 1024-thread cached 64K planes, streaming (> 64K)
+@pytest.mark.parametrize("N,C,H,W", [(2, 3, 4, 4), (2, 5, 33, 31), (1, 2, 80, 80), (2, 4, 16, 16), (2, 3, 36, 20),
+                                     (1, 2, 128, 128), (1, 2, 256, 256), (1, 1, 256, 260)])
 def test_instance_norm(act, res, N, C, H, W):
     from dsgan_hip import functional as HF
     g = torch.Generator().manual_seed(C * H + W)
