@@ -683,6 +683,35 @@ __global__ void copy_strided_kernel(const float* src, long src_bs, float* dst, l
   }
 }
 
+// float4 forms (E, batch strides multiples of 4, 16-byte aligned): blockIdx.y is the sample, so
+// no 64-bit division per element (the scalar forms above spend more time in it than in memory).
+__global__ __launch_bounds__(256) void add_n4_kernel(PtrList in, int nin, float* out, long out_bs, long E4) {
+  const int n = blockIdx.y;
+  float4* o = reinterpret_cast<float4*>(out + (long)n * out_bs);
+  for (long e = blockIdx.x * 256L + threadIdx.x; e < E4; e += (long)gridDim.x * 256) {
+    float4 s = reinterpret_cast<const float4*>(in.p[0] + (long)n * in.bs[0])[e];
+    for (int i = 1; i < nin; ++i) {
+      const float4 v = reinterpret_cast<const float4*>(in.p[i] + (long)n * in.bs[i])[e];
+      s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+    }
+    o[e] = s;
+  }
+}
+
+__global__ __launch_bounds__(256) void copy4_kernel(const float* src, long src_bs, float* dst, long dst_bs, long E4) {
+  const int n = blockIdx.y;
+  const float4* s = reinterpret_cast<const float4*>(src + (long)n * src_bs);
+  float4* d = reinterpret_cast<float4*>(dst + (long)n * dst_bs);
+  for (long e = blockIdx.x * 256L + threadIdx.x; e < E4; e += (long)gridDim.x * 256) d[e] = s[e];
+}
+
+static inline bool v4_ok(const void* p, long bs) { return (bs & 3) == 0 && (((uintptr_t)p) & 15) == 0; }
+static inline dim3 grid4(int N, long E4) {
+  long gx = (E4 + 255) / 256;
+  if (gx > 4096) gx = 4096;
+  return dim3((unsigned)(gx < 1 ? 1 : gx), (unsigned)N);
+}
+
 __global__ void scale_kernel(float* p, float a, long n) {
   for (long t = blockIdx.x * (long)blockDim.x + threadIdx.x; t < n; t += (long)gridDim.x * blockDim.x) p[t] *= a;
 }
@@ -904,7 +933,13 @@ int dsgan_add_n(const float* const* ins, const long* in_bs, int nin, float* out,
                 long E, hipStream_t st) {
   DSG_REQUIRE(nin >= 1 && nin <= 8 && ins && out, "dsgan_add_n: 1..8 inputs");
   PtrList pl{};
-  for (int i = 0; i < nin; ++i) { pl.p[i] = ins[i]; pl.bs[i] = in_bs[i]; }
+  bool v4 = (E & 3) == 0 && v4_ok(out, out_bs) && N <= 65535;
+  for (int i = 0; i < nin; ++i) { pl.p[i] = ins[i]; pl.bs[i] = in_bs[i]; v4 = v4 && v4_ok(ins[i], in_bs[i]); }
+  if (v4) {
+    hipLaunchKernelGGL(add_n4_kernel, grid4(N, E / 4), dim3(256), 0, st, pl, nin, out, out_bs, E / 4);
+    DSG_CHECK_LAUNCH();
+    return 0;
+  }
   hipLaunchKernelGGL(add_n_kernel, dim3(grid_for((long)N * E)), dim3(256), 0, st, pl, nin, out, out_bs, N, E);
   DSG_CHECK_LAUNCH();
   return 0;
@@ -912,6 +947,11 @@ int dsgan_add_n(const float* const* ins, const long* in_bs, int nin, float* out,
 
 int dsgan_copy_strided(const float* src, long src_bs, float* dst, long dst_bs, int N, long E,
                        hipStream_t st) {
+  if ((E & 3) == 0 && v4_ok(src, src_bs) && v4_ok(dst, dst_bs) && N <= 65535) {
+    hipLaunchKernelGGL(copy4_kernel, grid4(N, E / 4), dim3(256), 0, st, src, src_bs, dst, dst_bs, E / 4);
+    DSG_CHECK_LAUNCH();
+    return 0;
+  }
   hipLaunchKernelGGL(copy_strided_kernel, dim3(grid_for((long)N * E)), dim3(256), 0, st, src, src_bs, dst, dst_bs, N, E);
   DSG_CHECK_LAUNCH();
   return 0;

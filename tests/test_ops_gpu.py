@@ -611,3 +611,20 @@ def test_pconvt_bf16(N, Cout, Cin, Hi, Wi, K, H, W):
                       accumulate=True)
     want = y0.double() + dx_ref * torch.where(pre > 0, 1.0, 0.2).double()
     assert rel(out, want) < 1e-5
+
+
+@pytest.mark.parametrize("shape", [(2, 3, 5, 7), (3, 4, 16, 16), (2, 8, 64, 64)])
+def test_add_n_and_cat(shape):
+    """AddNFn / CatFn (float4 and scalar forms): exact sums and channel concatenation."""
+    from dsgan_hip import functional as HF
+    g = torch.Generator().manual_seed(shape[1] * shape[2])
+    xs = [torch.randn(shape, generator=g) for _ in range(3)]
+    y = HF.add_n(*[t.to(DEV) for t in xs])
+    assert torch.equal(y.cpu(), (xs[0] + xs[1]) + xs[2])
+    b = torch.randn(shape[0], 2, shape[2], shape[3], generator=g)
+    ad, bd = _leaf(xs[0]), _leaf(b)
+    c = HF.cat_channels(ad, bd)
+    assert torch.equal(c.detach().cpu(), torch.cat([xs[0], b], 1))
+    gy = torch.randn(c.shape, generator=g)
+    c.backward(gy.to(DEV))
+    assert torch.equal(ad.grad.cpu(), gy[:, :shape[1]]) and torch.equal(bd.grad.cpu(), gy[:, shape[1]:])
