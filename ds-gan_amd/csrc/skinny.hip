@@ -40,7 +40,10 @@ __device__ __forceinline__ float bld(__amdgpu_buffer_rsrc_t r, unsigned off) {
 // staged once per workgroup into LDS as [k][tap][MS] (broadcast reads in the loop); KH/KW are
 // template constants for the common 1x1/3x3/4x4 cases so every tap load of a channel is issued
 // back to back (KH_ = 0: runtime taps).
-template <int MS, int KH_, int KW_>
+// PAR (transposed, stride 2, KH_ x KW_ = 4x4): only the 2x2 taps whose parity matches the output
+// pixel can land on an input pixel, so each lane walks its own four taps (kh = (oh+pad)&1 + 2i,
+// kw = (ow+pad)&1 + 2j) instead of issuing 16 loads of which 12 are out of range.
+template <int MS, int KH_, int KW_, bool PAR = false>
 __global__ __launch_bounds__(256) void small_out_kernel(SkArgs a) {
   extern __shared__ float wsm[];                 // [K][KH*KW][MS]
   __shared__ float part[3][MS][64];
@@ -63,8 +66,9 @@ __global__ __launch_bounds__(256) void small_out_kernel(SkArgs a) {
   const unsigned xb = (unsigned)((long)b * a.x_bs);
 
   // per-tap in-plane offsets (or OOB), independent of k
-  constexpr int TMAX = KH_ ? KH_ * KW_ : 1;
+  constexpr int TMAX = PAR ? 4 : (KH_ ? KH_ * KW_ : 1);
   unsigned toff[TMAX];
+  int tsel[TMAX];                               // weight tap of each slot (PAR: per lane)
   auto tap_off = [&](int kh, int kw) -> unsigned {
     int ih, iw; bool ok;
     if (!a.transposed) {
@@ -77,9 +81,17 @@ __global__ __launch_bounds__(256) void small_out_kernel(SkArgs a) {
     }
     return ok ? (unsigned)(ih * a.Win + iw) : 0x3FFFFFF0u;
   };
-  if (KH_) {
+  if (PAR) {
+    const int kh0 = (oh + a.pad) & 1, kw0 = (ow + a.pad) & 1;
 #pragma unroll
-    for (int t = 0; t < TMAX; ++t) toff[t] = tap_off(t / KW_, t % KW_);
+    for (int t = 0; t < 4; ++t) {
+      const int kh = kh0 + 2 * (t >> 1), kw = kw0 + 2 * (t & 1);
+      toff[t] = tap_off(kh, kw);
+      tsel[t] = kh * KW_ + kw;
+    }
+  } else if (KH_) {
+#pragma unroll
+    for (int t = 0; t < TMAX; ++t) { toff[t] = tap_off(t / KW_, t % KW_); tsel[t] = t; }
   }
 
   float acc[MS];
@@ -95,7 +107,7 @@ __global__ __launch_bounds__(256) void small_out_kernel(SkArgs a) {
 #pragma unroll
       for (int t = 0; t < TMAX; ++t)
 #pragma unroll
-        for (int m = 0; m < MS; ++m) acc[m] = fmaf(wk[t * MS + m], xv[t], acc[m]);
+        for (int m = 0; m < MS; ++m) acc[m] = fmaf(wk[tsel[t] * MS + m], xv[t], acc[m]);
     } else {
       for (int t = 0; t < T; ++t) {
         const unsigned o = tap_off(t / KW, t % KW);
@@ -150,9 +162,19 @@ __global__ __launch_bounds__(256) void wgrad_small_kernel(WsArgs a) {
 #pragma unroll
     for (int t = 0; t < T; ++t) acc[s][t] = 0.f;
 
-  for (long p = p0 + threadIdx.x; p < p1; p += 256) {
-    const int b = (int)(p / HWo), r = (int)(p - (long)b * HWo);
-    const int oh = r / a.Wo, ow = r - (r / a.Wo) * a.Wo;
+  // pixel walk without a 64-bit division per pixel (it used to cost more than the loads):
+  // (b, oh, ow) of p = p0 + tid once, then advanced by 256 pixels per iteration
+  int b, oh, ow;
+  {
+    const int q = (int)(p0 + threadIdx.x);   // nb*Ho*Wo < 2^31 (host check)
+    b = q / HWo;
+    const int r = q - b * HWo;
+    oh = r / a.Wo;
+    ow = r - oh * a.Wo;
+  }
+  const int dq = 256 / a.Wo, dw = 256 - dq * a.Wo;
+  for (int p = (int)p0 + threadIdx.x; p < (int)p1; p += 256) {
+    const int r = oh * a.Wo + ow;
     const int ih0 = oh * a.stride - a.pad, iw0 = ow * a.stride - a.pad;
     unsigned toff[T];                            // tap offsets inside one input plane (or OOB)
 #pragma unroll
@@ -187,6 +209,9 @@ __global__ __launch_bounds__(256) void wgrad_small_kernel(WsArgs a) {
         }
       }
     }
+    ow += dw; oh += dq;
+    if (ow >= a.Wo) { ow -= a.Wo; ++oh; }
+    while (oh >= a.Ho) { oh -= a.Ho; ++b; }
   }
   const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
 #pragma unroll
@@ -245,6 +270,8 @@ int dsgan_conv_small_out(const float* x, long x_bs, const float* w, long wm, lon
 #define SO_SHAPES(MS_)                                                      \
   if (KH == 1 && KW == 1) SO_LAUNCH(MS_, 1, 1);                             \
   else if (KH == 3 && KW == 3) SO_LAUNCH(MS_, 3, 3);                        \
+  else if (KH == 4 && KW == 4 && transposed && stride == 2)                 \
+    hipLaunchKernelGGL((small_out_kernel<MS_, 4, 4, true>), grid, dim3(256), lds, st, a); \
   else if (KH == 4 && KW == 4) SO_LAUNCH(MS_, 4, 4);                        \
   else SO_LAUNCH(MS_, 0, 0);
   if (MSr == 1) { SO_SHAPES(1) } else if (MSr == 4) { SO_SHAPES(4) } else { SO_SHAPES(8) }
@@ -266,7 +293,7 @@ int dsgan_conv_wgrad_small(const float* dy, long dy_bs, const float* x, long x_b
   const long xr = ((long)(N - 1) * x_bs + (long)Cin * H * W) * 4;
   const long gr = ((long)(N - 1) * dy_bs + (long)Cout * Ho * Wo) * 4;
   DSG_REQUIRE(xr < 0x3FFFFFF0L && gr < (long)SK_OOB, "dsgan_conv_wgrad_small: operand exceeds buffer range");
-  DSG_REQUIRE((long)H * W < 0x3FFFFFF0L, "dsgan_conv_wgrad_small: plane too large");
+  DSG_REQUIRE((long)H * W < 0x3FFFFFF0L && (long)N * Ho * Wo + 256 < (1L << 31), "dsgan_conv_wgrad_small: plane too large");
   WsArgs a{};
   a.dy = dy; a.dy_bs = dy_bs; a.x = x; a.x_bs = x_bs; a.dw = dw; a.nb = N; a.Cin = Cin; a.Hin = H;
   a.Win = W; a.Cout = Cout; a.Ho = Ho; a.Wo = Wo; a.KW = KW; a.stride = stride; a.pad = pad;

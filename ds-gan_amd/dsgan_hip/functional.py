@@ -938,6 +938,33 @@ def instance_norm(x, act=None, res=None):
     return InstanceNormFn.apply(x, res, act)
 
 
+class InstanceNormCatFn(torch.autograd.Function):
+    """cat(act(IN(x)), skip) along channels: the IN kernel writes its plane straight into the
+    first Ca channels of the concatenation (upSample, MixConvNeXtML.py:61-66), so only the skip
+    is copied; the backward reads its slice of dy in place."""
+
+    @staticmethod
+    def forward(ctx, x, skip, act):
+        N, Ca, H, W = x.shape
+        out = _empty(N, Ca + skip.shape[1], H, W, x)
+        _, mean, rstd = instnorm_raw(x, None, None, act, out=out[:, :Ca])
+        copy_into(out[:, Ca:], skip)
+        ctx.act, ctx.Ca = act, Ca
+        ctx.save_for_backward(x, mean, rstd)
+        ctx.box_x, ctx.box_s = _box(x), _box(skip)
+        return out
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, mean, rstd = ctx.saved_tensors
+        dx, _, _ = instnorm_bwd_raw(dy[:, :ctx.Ca], x, None, None, mean, rstd, ctx.act, False, False)
+        return _give(ctx.box_x, dx), _give(ctx.box_s, dy[:, ctx.Ca:]), None
+
+
+def instance_norm_cat(x, skip, act=None):
+    return InstanceNormCatFn.apply(x, skip, act)
+
+
 # ------------------------------------------------------------------------------------------
 # MaxPool2d(k) with int32 plane-flat argmax
 # ------------------------------------------------------------------------------------------

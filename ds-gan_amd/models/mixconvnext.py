@@ -32,8 +32,7 @@ class upSample(nn.Module):
 
     def forward(self, x, feature_map):
         t = self.model[0]
-        u = HF.instance_norm(HF.conv_transpose3s2(x, t.weight, t.bias), act="gelu")
-        return HF.cat_channels(u, feature_map)
+        return HF.instance_norm_cat(HF.conv_transpose3s2(x, t.weight, t.bias), feature_map, act="gelu")
 
 
 class MidMLKA(nn.Module):

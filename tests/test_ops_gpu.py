@@ -628,3 +628,22 @@ def test_add_n_and_cat(shape):
     gy = torch.randn(c.shape, generator=g)
     c.backward(gy.to(DEV))
     assert torch.equal(ad.grad.cpu(), gy[:, :shape[1]]) and torch.equal(bd.grad.cpu(), gy[:, shape[1]:])
+
+
+@pytest.mark.parametrize("shape", [(2, 3, 8, 8), (2, 4, 32, 32)])
+def test_instance_norm_cat(shape):
+    """upSample tail: cat(GELU(IN(x)), skip) with the IN writing into the concatenation."""
+    from dsgan_hip import functional as HF
+    g = torch.Generator().manual_seed(shape[1])
+    x = torch.randn(shape, generator=g) * 2 + 0.5
+    sk = torch.randn(shape[0], 5, shape[2], shape[3], generator=g)
+    xr, sr = x.clone().requires_grad_(), sk.clone().requires_grad_()
+    y_ref = torch.cat([F.gelu(F.instance_norm(xr, eps=1e-5)), sr], 1)
+    gy = torch.randn(y_ref.shape, generator=g)
+    y_ref.backward(gy)
+    xd, sd = _leaf(x), _leaf(sk)
+    y = HF.instance_norm_cat(xd, sd, act="gelu")
+    y.backward(gy.to(DEV))
+    assert rel(y, y_ref) < 1e-5
+    assert rel(xd.grad, xr.grad) < 1e-4
+    assert torch.equal(sd.grad.cpu(), sr.grad)
