@@ -26,6 +26,7 @@ struct SkArgs {
   int nb, K, M, Hin, Win, Ho, Wo, KH, KW, stride, pad, transposed;
   int accumulate;
   unsigned x_range;
+  int act; float slope;   // small_in only
 };
 
 __device__ __forceinline__ float bld(__amdgpu_buffer_rsrc_t r, unsigned off) {
@@ -131,6 +132,97 @@ __global__ __launch_bounds__(256) void small_out_kernel(SkArgs a) {
     if (a.bias) v += a.bias[m];
     if (a.accumulate) v += yp[(long)m * HWo];
     yp[(long)m * HWo] = v;
+  }
+}
+
+// small_in: few INPUT taps (K*KH*KW <= 36) into many output channels -- VGG16 conv1_1 (3 -> 64,
+// vgg.py:17) and the data-grad of the G head (3 -> 64 transposed, MixConvNeXtML.py:459).  The
+// GEMM view (M = 64, K = 27) starves an MFMA tile on its im2col gather; here a thread owns PX
+// consecutive output pixels of a row: their K*T inputs are loaded once into registers, then
+// every output channel is an exact fp32 dot product with weights broadcast from LDS (one
+// float4 read serves 4 channels x PX pixels -- the LDS return path, not the FMAs, bounds this
+// kernel), written as one 16-byte store per channel (PX = 4).  blockIdx.y = 64-channel chunk.
+template <int KT, int PX>
+__global__ __launch_bounds__(256) void small_in_kernel(SkArgs a) {
+  __shared__ __attribute__((aligned(16))) float wsm[KT][64];   // [k*T + t][m - m0]
+  __shared__ __attribute__((aligned(16))) float bsm[64];
+  const int T = a.KH * a.KW, KTr = a.K * T;
+  const int m0 = blockIdx.y * 64;
+  for (int i = threadIdx.x; i < KT * 64; i += 256) {
+    const int j = i / 64, mm = i - j * 64, m = m0 + mm;
+    float v = 0.f;
+    if (j < KTr && m < a.M) {
+      const int k = j / T, t = j - k * T;
+      v = a.w[m * a.wm + k * a.wk + (t / a.KW) * a.wh + (t % a.KW) * a.ww];
+    }
+    wsm[j][mm] = v;
+  }
+  if (threadIdx.x < 64) bsm[threadIdx.x] = a.bias && m0 + (int)threadIdx.x < a.M ? a.bias[m0 + threadIdx.x] : 0.f;
+  __syncthreads();
+  const int HWo = a.Ho * a.Wo;
+  const int total = a.nb * HWo / PX;            // PX | Wo (host check)
+  int q = blockIdx.x * 256 + threadIdx.x;
+  const bool qv = q < total;
+  if (!qv) q = 0;
+  q *= PX;
+  const int b = q / HWo, r = q - b * HWo;
+  const int oh = r / a.Wo, ow0 = r - oh * a.Wo;
+  const int HWi = a.Hin * a.Win;
+  const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc((void*)a.x, (short)0, a.x_range, 0x00020000);
+  const unsigned xb = (unsigned)((long)b * a.x_bs);
+  float xv[KT][PX];
+#pragma unroll
+  for (int j = 0; j < KT; ++j) {
+#pragma unroll
+    for (int p = 0; p < PX; ++p) {
+      if (j < KTr) {
+        const int k = j / T, t = j - k * T, kh = t / a.KW, kw = t - kh * a.KW, ow = ow0 + p;
+        int ih, iw;
+        if (!a.transposed) { ih = oh * a.stride - a.pad + kh; iw = ow * a.stride - a.pad + kw; }
+        else { ih = oh + a.pad - kh; iw = ow + a.pad - kw; }
+        const bool ok = ((unsigned)ih < (unsigned)a.Hin) & ((unsigned)iw < (unsigned)a.Win);
+        xv[j][p] = bld(rx, ok ? (xb + (unsigned)k * HWi + (unsigned)(ih * a.Win + iw)) * 4u : SK_OOB);
+      } else {
+        xv[j][p] = 0.f;
+      }
+    }
+  }
+  if (!qv) return;
+  float* yp = a.y + (long)b * a.y_bs + (long)m0 * HWo + r;
+  const int mn = min(64, a.M - m0);
+  for (int mm = 0; mm < mn; mm += 4) {
+    float acc[4][PX];
+    const float4 bv = *reinterpret_cast<const float4*>(&bsm[mm]);
+#pragma unroll
+    for (int p = 0; p < PX; ++p) { acc[0][p] = bv.x; acc[1][p] = bv.y; acc[2][p] = bv.z; acc[3][p] = bv.w; }
+#pragma unroll
+    for (int j = 0; j < KT; ++j) {
+      const float4 wv = *reinterpret_cast<const float4*>(&wsm[j][mm]);
+#pragma unroll
+      for (int p = 0; p < PX; ++p) {
+        acc[0][p] = fmaf(wv.x, xv[j][p], acc[0][p]); acc[1][p] = fmaf(wv.y, xv[j][p], acc[1][p]);
+        acc[2][p] = fmaf(wv.z, xv[j][p], acc[2][p]); acc[3][p] = fmaf(wv.w, xv[j][p], acc[3][p]);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (mm + u < mn) {
+        float* dst = yp + (long)(mm + u) * HWo;
+        if constexpr (PX == 4) {
+          float4 v = make_float4(act_f(a.act, acc[u][0], a.slope), act_f(a.act, acc[u][1], a.slope),
+                                 act_f(a.act, acc[u][2], a.slope), act_f(a.act, acc[u][3], a.slope));
+          if (a.accumulate) { const float4 o = *reinterpret_cast<const float4*>(dst); v.x += o.x; v.y += o.y; v.z += o.z; v.w += o.w; }
+          *reinterpret_cast<float4*>(dst) = v;
+        } else {
+#pragma unroll
+          for (int p = 0; p < PX; ++p) {
+            float v = act_f(a.act, acc[u][p], a.slope);
+            if (a.accumulate) v += dst[p];
+            dst[p] = v;
+          }
+        }
+      }
+    }
   }
 }
 
@@ -277,6 +369,35 @@ int dsgan_conv_small_out(const float* x, long x_bs, const float* w, long wm, lon
   if (MSr == 1) { SO_SHAPES(1) } else if (MSr == 4) { SO_SHAPES(4) } else { SO_SHAPES(8) }
 #undef SO_SHAPES
 #undef SO_LAUNCH
+  DSG_CHECK_LAUNCH();
+  return 0;
+}
+
+// Few-input-tap direct conv / stride-1 transposed conv (see small_in_kernel): K*KH*KW <= 36,
+// y (+)= act(bias + conv).  Weight strides in elements, as dsgan_conv_small_out.
+int dsgan_conv_small_in(const float* x, long x_bs, const float* w, long wm, long wk, long wh, long ww,
+                        const float* bias, float* y, long y_bs, int nb, int K, int M, int Hin, int Win,
+                        int Ho, int Wo, int KH, int KW, int stride, int pad, int transposed, int act,
+                        float slope, int accumulate, hipStream_t st) {
+  DSG_REQUIRE(x && w && y && nb > 0 && K > 0 && M > 0 && Ho > 0 && Wo > 0 && KH > 0 && KW > 0,
+              "dsgan_conv_small_in: bad args");
+  DSG_REQUIRE(K * KH * KW <= 36 && (!transposed || stride == 1), "dsgan_conv_small_in: K*KH*KW <= 36, transposed stride 1");
+  const long xr = ((long)(nb - 1) * x_bs + (long)K * Hin * Win) * 4;
+  DSG_REQUIRE(xr < (long)SK_OOB && (long)nb * Ho * Wo < (1L << 31), "dsgan_conv_small_in: operand too large");
+  SkArgs a{};
+  a.x = x; a.x_bs = x_bs; a.w = w; a.wm = wm; a.wk = wk; a.wh = wh; a.ww = ww; a.bias = bias;
+  a.y = y; a.y_bs = y_bs; a.nb = nb; a.K = K; a.M = M; a.Hin = Hin; a.Win = Win; a.Ho = Ho; a.Wo = Wo;
+  a.KH = KH; a.KW = KW; a.stride = stride; a.pad = pad; a.transposed = transposed;
+  a.x_range = (unsigned)xr; a.accumulate = accumulate; a.act = act; a.slope = slope;
+  const int kt = K * KH * KW;
+  const bool v4 = Wo % 4 == 0 && (y_bs & 3) == 0 && (((uintptr_t)y) & 15) == 0;
+  const int px = v4 ? 4 : 1;
+  const dim3 grid((unsigned)(((long)nb * Ho * Wo / px + 255) / 256), (unsigned)((M + 63) / 64));
+#define SI_LAUNCH(KT_)                                                                        \
+  if (v4) hipLaunchKernelGGL((small_in_kernel<KT_, 4>), grid, dim3(256), 0, st, a);          \
+  else hipLaunchKernelGGL((small_in_kernel<KT_, 1>), grid, dim3(256), 0, st, a);
+  if (kt <= 12) { SI_LAUNCH(12) } else if (kt <= 27) { SI_LAUNCH(27) } else { SI_LAUNCH(36) }
+#undef SI_LAUNCH
   DSG_CHECK_LAUNCH();
   return 0;
 }

@@ -57,6 +57,7 @@ SIGNATURES = {
     "dsgan_tconv": [P, L, P, P, P, L, P, L] + [I] * 9 + [P, P] + [I] * 7 + [F, S],
     # skinny.hip
     "dsgan_conv_small_out": [P, L, P, L, L, L, L, P, P, L] + [I] * 13 + [S],
+    "dsgan_conv_small_in": [P, L, P, L, L, L, L, P, P, L] + [I] * 13 + [F, I, S],
     "dsgan_conv_wgrad_small": [P, L, P, L, P] + [I] * 11 + [S],
     # dwconv.hip
     "dsgan_dwconv_fwd": [P, L, P, P, P, L, I, I, I, I, I, I, I, S],

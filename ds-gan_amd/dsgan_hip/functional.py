@@ -252,6 +252,11 @@ def conv_fwd_raw(x, w, b, stride, pad, act=None, out=None, pre=None, accumulate=
         fam = "small_out_kernel"
         call("dsgan_conv_small_out", ptr(x), xbs, ptr(w), Cin * KH * KW, KH * KW, KW, 1, ptr(b), ptr(y), ybs,
              N, Cin, Cout, H, W, Ho, Wo, KH, KW, stride, pad, 0, int(accumulate), stream())
+    elif Cin * KH * KW <= 36 and Cout >= 16 and pre is None and xact is None and act in (None, "relu", "lrelu"):
+        # few input taps into many channels (VGG conv1_1): thread-per-pixel exact fp32 dot products
+        fam = "small_in_kernel"
+        call("dsgan_conv_small_in", ptr(x), xbs, ptr(w), Cin * KH * KW, KH * KW, KW, 1, ptr(b), ptr(y), ybs,
+             N, Cin, Cout, H, W, Ho, Wo, KH, KW, stride, pad, 0, ACT[act], LRELU_SLOPE, int(accumulate), stream())
     elif KH == 1 and KW == 1 and stride == 1 and pad == 0 and _pw_ok(0, Cout, Cin, H * W, 0, xbs, w.data_ptr(), x.data_ptr()):
         fam = "pwgemm_kernel"
         call("dsgan_pw_gemm", 0, ptr(w), 0, ptr(x), xbs, ptr(y), ybs, ptr(b), ptr(pre), pbs, None, 0,
@@ -299,6 +304,11 @@ def conv_dgrad_raw(dy, w, x_shape, stride, pad, bias=None, act=None, gpre=None, 
         # data-grad into a 3/6-channel tensor: direct transposed gather, w(m=ci, k=co, kh, kw)
         call("dsgan_conv_small_out", ptr(dy), dybs, ptr(w), KH * KW, Cin * KH * KW, KW, 1, ptr(bias),
              ptr(dx), dxbs, N, Cout, Cin, Ho, Wo, H, W, KH, KW, stride, pad, 1, int(accumulate), stream())
+    elif Cout * KH * KW <= 27 and KH * KW <= 9 and Cin >= 16 and act is None and gpre is None and stride == 1 and bias is None:
+        # data-grad out of a 3-channel conv (G head): stride-1 transposed gather, w(m=ci, k=co, kh, kw)
+        fam = "small_in_kernel"
+        call("dsgan_conv_small_in", ptr(dy), dybs, ptr(w), KH * KW, Cin * KH * KW, KW, 1, None, ptr(dx), dxbs,
+             N, Cout, Cin, Ho, Wo, H, W, KH, KW, 1, pad, 1, 0, LRELU_SLOPE, int(accumulate), stream())
     elif (KH == 1 and KW == 1 and stride == 1 and pad == 0 and bias is None and act is None
             and _pw_ok(1, Cin, Cout, H * W, 0, dybs, w.data_ptr(), dy.data_ptr())):
         fam = "pwgemm_kernel"

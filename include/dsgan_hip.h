@@ -120,6 +120,14 @@ int dsgan_conv_small_out(const float* x, long x_bs, const float* w, long wm, lon
                          const float* bias, float* y, long y_bs, int nb, int K, int M, int Hin, int Win,
                          int Ho, int Wo, int KH, int KW, int stride, int pad, int transposed,
                          int accumulate, hipStream_t stream);
+/* dsgan_conv_small_in: y (+)= act(bias + conv) with K*KH*KW <= 36 input taps and any M (exact
+ *   fp32, thread per output pixel); transposed=1 is the stride-1 data-grad gather.  Replaces:
+ *   VGG16 conv1_1 forward (DSGAN/models/vgg.py:17) and the G head data-grad 3 -> 64
+ *   (DSGAN/models/model/MixConvNeXtML.py:459, backward of the final nn.Conv2d(64, 3, 3, 1, 1)). */
+int dsgan_conv_small_in(const float* x, long x_bs, const float* w, long wm, long wk, long wh, long ww,
+                        const float* bias, float* y, long y_bs, int nb, int K, int M, int Hin, int Win,
+                        int Ho, int Wo, int KH, int KW, int stride, int pad, int transposed, int act,
+                        float slope, int accumulate, hipStream_t stream);
 int dsgan_conv_wgrad_small(const float* dy, long dy_bs, const float* x, long x_bs, float* dw, int N,
                            int Cin, int H, int W, int Cout, int KH, int KW, int stride, int pad, int Ho,
                            int Wo, hipStream_t stream);
