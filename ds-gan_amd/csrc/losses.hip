@@ -207,6 +207,107 @@ __global__ __launch_bounds__(256) void ssim_fwd_kernel(SSIMArgs s, int tiles_w) 
   if (threadIdx.x == 0) atomicAdd(s.out, ssum);
 }
 
+// ---- MS-SSIM evaluation (DSGAN/MS_SSIM.py:153-225; no gradient) ---------------------------
+// One scale: per plane the sums of the SSIM map and of the contrast-structure map cs
+// (_ssim, :55-92) -- same tiling and filter order as ssim_fwd_kernel, no backward coefficients.
+__global__ __launch_bounds__(256) void ssim_eval_kernel(SSIMArgs s, int tiles_w, float* stats) {
+  __shared__ float xs[SS_E][SS_E + 1], ys[SS_E][SS_E + 1];
+  __shared__ float hb[5][SS_E][SS_T + 1];
+  __shared__ float wsh[SS_K];
+  __shared__ float sh[8];
+  const int plane = blockIdx.y;
+  const int Ho = s.H - SS_K + 1, Wo = s.W - SS_K + 1;
+  const int oh0 = (blockIdx.x / tiles_w) * SS_T, ow0 = (blockIdx.x % tiles_w) * SS_T;
+  const float* rp = s.real + (long)plane * s.H * s.W;
+  const float* fp = s.fake + (long)plane * s.H * s.W;
+  if (threadIdx.x < SS_K) wsh[threadIdx.x] = s.win[threadIdx.x];
+  for (int i = threadIdx.x; i < SS_E * SS_E; i += 256) {
+    const int r = i / SS_E, q = i - r * SS_E;
+    const int h = oh0 + r, w = ow0 + q;
+    const bool ok = h < s.H && w < s.W;
+    xs[r][q] = ok ? rp[(long)h * s.W + w] * s.a + s.b : 0.f;
+    ys[r][q] = ok ? fp[(long)h * s.W + w] * s.a + s.b : 0.f;
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < SS_T * SS_E; i += 256) {
+    const int r = i / SS_E, q = i - r * SS_E;
+    float m1 = 0, m2 = 0, e11 = 0, e22 = 0, e12 = 0;
+#pragma unroll
+    for (int k = 0; k < SS_K; ++k) {
+      const float g = wsh[k], xv = xs[r + k][q], yv = ys[r + k][q];
+      m1 += g * xv; m2 += g * yv; e11 += g * (xv * xv); e22 += g * (yv * yv); e12 += g * (xv * yv);
+    }
+    hb[0][q][r] = m1; hb[1][q][r] = m2; hb[2][q][r] = e11; hb[3][q][r] = e22; hb[4][q][r] = e12;
+  }
+  __syncthreads();
+  float ssum = 0.f, csum = 0.f;
+  for (int i = threadIdx.x; i < SS_T * SS_T; i += 256) {
+    const int r = i >> 5, q = i & 31;
+    if (oh0 + r >= Ho || ow0 + q >= Wo) continue;
+    float v[5] = {0, 0, 0, 0, 0};
+#pragma unroll
+    for (int k = 0; k < SS_K; ++k) {
+      const float g = wsh[k];
+#pragma unroll
+      for (int j = 0; j < 5; ++j) v[j] += g * hb[j][q + k][r];
+    }
+    const float mu1 = v[0], mu2 = v[1];
+    const float s11 = v[2] - mu1 * mu1, s22 = v[3] - mu2 * mu2, s12 = v[4] - mu1 * mu2;
+    const float cs = (2.f * s12 + s.C2) / (s11 + s22 + s.C2);
+    ssum += ((2.f * mu1 * mu2 + s.C1) / (mu1 * mu1 + mu2 * mu2 + s.C1)) * cs;
+    csum += cs;
+  }
+  ssum = block_sum<256>(ssum, sh);
+  csum = block_sum<256>(csum, sh + 4);
+  if (threadIdx.x == 0) { atomicAdd(stats + 2 * plane, ssum); atomicAdd(stats + 2 * plane + 1, csum); }
+}
+
+// F.avg_pool2d(a*x+b, 2, padding=(H%2, W%2)) with count_include_pad (divisor 4), :213-215
+__global__ void avgpool2_pad_kernel(const float* __restrict__ x, float* __restrict__ y, int planes, int H, int W,
+                                    int Ho, int Wo, int ph, int pw, float a, float b) {
+  const long total = (long)planes * Ho * Wo;
+  for (long t = blockIdx.x * 256L + threadIdx.x; t < total; t += (long)gridDim.x * 256) {
+    const int p = (int)(t / ((long)Ho * Wo));
+    const int r = (int)(t - (long)p * Ho * Wo), oh = r / Wo, ow = r - oh * Wo;
+    const float* xp = x + (long)p * H * W;
+    float acc = 0.f;
+#pragma unroll
+    for (int dh = 0; dh < 2; ++dh)
+#pragma unroll
+      for (int dw = 0; dw < 2; ++dw) {
+        const int h = 2 * oh - ph + dh, w = 2 * ow - pw + dw;
+        if ((unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W) acc += xp[(long)h * W + w] * a + b;
+      }
+    y[t] = 0.25f * acc;
+  }
+}
+
+struct MsArgs { float inv_cnt[8]; float wt[8]; };
+
+// out[n] = mean_c prod_l relu(v_l[n][c])^w_l, v_l = cs (l < L-1) or ssim (l = L-1) -- :218-225;
+// out[N] = mean over n.  One workgroup.
+__global__ __launch_bounds__(256) void ms_ssim_combine_kernel(const float* stats, int levels, int N, int C,
+                                                              MsArgs m, float* out) {
+  __shared__ float sh[4];
+  float tot = 0.f;
+  for (int n = 0; n < N; ++n) {
+    float acc = 0.f;
+    for (int c = threadIdx.x; c < C; c += 256) {
+      float prod = 1.f;
+      for (int l = 0; l < levels; ++l) {
+        const float* st = stats + ((long)l * N * C + (long)n * C + c) * 2;
+        const float v = fmaxf((l < levels - 1 ? st[1] : st[0]) * m.inv_cnt[l], 0.f);
+        prod *= powf(v, m.wt[l]);
+      }
+      acc += prod;
+    }
+    acc = block_sum<256>(acc, sh) / (float)C;
+    if (threadIdx.x == 0) out[n] = acc;
+    tot += acc;
+  }
+  if (threadIdx.x == 0) out[N] = tot / (float)N;
+}
+
 // dfake[h,w] = g * a * ( G^T c_mu + 2Y G^T c_yy + X G^T c_xy )  over input tile 32x32
 __global__ __launch_bounds__(256) void ssim_bwd_kernel(SSIMArgs s, const float* gout, float gcoef,
                                                        float* dfake, int tiles_w, int accumulate) {
@@ -329,6 +430,60 @@ int dsgan_tv_fwd(const float* y, long planes, int H, int W, float coef, float* o
 int dsgan_tv_bwd(const float* y, long planes, int H, int W, float coef, const float* gout, float* dy,
                  int accumulate, hipStream_t st) {
   hipLaunchKernelGGL(tv_bwd_kernel, dim3(red_grid(planes * H * W) * 8), dim3(256), 0, st, y, planes, H, W, gout, coef, dy, accumulate);
+  DSG_CHECK_LAUNCH();
+  return 0;
+}
+
+static inline int ms_half(int h) { return (h + 2 * (h % 2) - 2) / 2 + 1; }
+
+// floats of `work` dsgan_ms_ssim needs: the two largest pyramid levels of X and Y (ping-pong)
+long dsgan_ms_ssim_workspace(int N, int C, int H, int W) {
+  const long p = (long)N * C;
+  const int h1 = ms_half(H), w1 = ms_half(W), h2 = ms_half(h1), w2 = ms_half(w1);
+  return 2 * p * ((long)h1 * w1 + (long)h2 * w2);
+}
+
+// MS-SSIM of (a*real+b, a*fake+b): levels = number of weights (host array, <= 8), each scale
+// but the last followed by the padded 2x2 average pool (the affine map is applied inside the
+// first pool, before the zero padding, as the reference maps before calling ms_ssim).
+// out[n] per image (size_average=False), out[N] the batch mean (size_average=True).
+int dsgan_ms_ssim(const float* real, const float* fake, float a, float b, int N, int C, int H, int W,
+                  const float* win11, float C1, float C2, const float* weights_host, int levels, float* work,
+                  float* stats, float* out, hipStream_t st) {
+  DSG_REQUIRE(real && fake && win11 && weights_host && work && stats && out && N > 0 && C > 0 && levels >= 1 &&
+                  levels <= 8 && N * C <= 65535,
+              "dsgan_ms_ssim: bad args");
+  DSG_REQUIRE(((H < W ? H : W) > (SS_K - 1) * (1 << (levels - 1))),
+              "dsgan_ms_ssim: image smaller than the (win_size-1)*2^(levels-1) ms-ssim minimum");
+  const int planes = N * C;
+  hipMemsetAsync(stats, 0, sizeof(float) * 2 * planes * levels, st);
+  MsArgs m{};
+  const float* xr = real;
+  const float* yr = fake;
+  float ca = a, cb = b;
+  const long big = 2L * planes * ms_half(H) * ms_half(W);
+  float* bufs[2] = {work, work + big};
+  int h = H, w = W;
+  for (int l = 0; l < levels; ++l) {
+    const int Ho = h - SS_K + 1, Wo = w - SS_K + 1;
+    SSIMArgs s{xr, yr, ca, cb, planes, h, w, win11, C1, C2, nullptr, nullptr};
+    const int tw = cdiv(Wo, SS_T), th = cdiv(Ho, SS_T);
+    hipLaunchKernelGGL(ssim_eval_kernel, dim3(tw * th, planes), dim3(256), 0, st, s, tw, stats + (long)l * planes * 2);
+    m.inv_cnt[l] = 1.f / ((float)Ho * (float)Wo);
+    m.wt[l] = weights_host[l];
+    if (l < levels - 1) {
+      const int h2 = ms_half(h), w2 = ms_half(w);
+      float* nx = bufs[l & 1];
+      float* ny = nx + (long)planes * h2 * w2;
+      const long n2 = (long)planes * h2 * w2;
+      hipLaunchKernelGGL(avgpool2_pad_kernel, dim3(red_grid(n2)), dim3(256), 0, st, xr, nx, planes, h, w, h2, w2,
+                         h % 2, w % 2, ca, cb);
+      hipLaunchKernelGGL(avgpool2_pad_kernel, dim3(red_grid(n2)), dim3(256), 0, st, yr, ny, planes, h, w, h2, w2,
+                         h % 2, w % 2, ca, cb);
+      xr = nx; yr = ny; h = h2; w = w2; ca = 1.f; cb = 0.f;
+    }
+  }
+  hipLaunchKernelGGL(ms_ssim_combine_kernel, dim3(1), dim3(256), 0, st, stats, levels, N, C, m, out);
   DSG_CHECK_LAUNCH();
   return 0;
 }

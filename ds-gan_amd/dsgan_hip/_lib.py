@@ -86,6 +86,8 @@ SIGNATURES = {
     "dsgan_tv_fwd": [P, L, I, I, F, P, S],
     "dsgan_tv_bwd": [P, L, I, I, F, P, P, I, S],
     "dsgan_ssim_fwd": [P, P, F, F, I, I, I, P, F, F, P, P, S],
+    "dsgan_ms_ssim_workspace": [I, I, I, I],
+    "dsgan_ms_ssim": [P, P, F, F, I, I, I, I, P, F, F, P, I, P, P, P, S],
     "dsgan_ssim_bwd": [P, P, F, F, I, I, I, P, P, P, F, P, I, S],
     # adam.hip
     "dsgan_adam": [P, P, P, P, L, F, F, F, F, I, S],

@@ -1316,3 +1316,27 @@ class SSIMFn(torch.autograd.Function):
 
 def ssim_affine(real, fake, a=0.5, b=0.5, data_range=1.0):
     return SSIMFn.apply(real, fake, a, b, data_range)
+
+
+MS_SSIM_WEIGHTS = (0.0448, 0.2856, 0.3001, 0.2363, 0.1333)
+
+
+def ms_ssim_affine(real, fake, a=1.0, b=0.0, data_range=1.0, weights=MS_SSIM_WEIGHTS, size_average=True):
+    """MS-SSIM of (a*real+b, a*fake+b) (DSGAN/MS_SSIM.py:153-225), evaluation only (no autograd):
+    a 0-d tensor (size_average) or the per-image values [N]."""
+    import ctypes
+    real, fake = real.detach().contiguous(), fake.detach().contiguous()
+    if real.shape != fake.shape or real.dim() != 4:
+        raise ValueError("ms_ssim: two (N,C,H,W) tensors of the same shape required")
+    N, C, H, W = real.shape
+    lib = _lib.load()
+    work = torch.empty(lib.dsgan_ms_ssim_workspace(N, C, H, W), device=real.device, dtype=torch.float32)
+    stats = torch.empty(2 * len(weights) * N * C, device=real.device, dtype=torch.float32)
+    out = torch.empty(N + 1, device=real.device, dtype=torch.float32)
+    wh = (ctypes.c_float * len(weights))(*[float(w) for w in weights])
+    C1 = (0.01 * data_range) ** 2
+    C2 = (0.03 * data_range) ** 2
+    call("dsgan_ms_ssim", ptr(real), ptr(fake), float(a), float(b), N, C, H, W, ptr(gauss_win(real.device)),
+         float(C1), float(C2), ctypes.cast(wh, ctypes.c_void_p), len(weights), ptr(work), ptr(stats), ptr(out),
+         stream())
+    return out[N] if size_average else out[:N]

@@ -13,3 +13,17 @@ class TestOptions(BaseOptions):
         parser.add_argument("--how_many", type=int, default=1000, help="how many test images to run")
         self.isTrain = False
         return parser
+
+
+def default_test_opt(args=None, **overrides):
+    """Programmatic TestOptions (``--model test`` unless overridden): the reference defaults
+    plus ``overrides``; used by the inference tests."""
+    import os
+    o = TestOptions()
+    opt = o.gather_options(["--model", "test"] + list(args or []))
+    opt.isTrain = False
+    opt.gpu_ids = [int(s) for s in str(opt.gpu_ids).split(",") if int(s) >= 0]
+    opt.checkpoints_dir = os.path.join(os.environ.get("TMPDIR", "/tmp"), "dsgan_checkpoints")
+    for k, v in overrides.items():
+        setattr(opt, k, v)
+    return opt

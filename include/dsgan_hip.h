@@ -275,6 +275,14 @@ int dsgan_ssim_fwd(const float* real, const float* fake, float a, float b, int p
 int dsgan_ssim_bwd(const float* real, const float* fake, float a, float b, int planes, int H,
                    int W, const float* win11, const float* coef, const float* gout, float gcoef,
                    float* dfake, int accumulate, hipStream_t stream);
+/* MS-SSIM evaluation of (a*real+b, a*fake+b), DSGAN/MS_SSIM.py:153-225 (ms_ssim; no gradient):
+ * per scale the SSIM / contrast-structure plane means, then the padded 2x2 average pool;
+ * weights_host = the level weights (host array, levels <= 8).  work: dsgan_ms_ssim_workspace
+ * floats, stats: 2*levels*N*C floats, out: N+1 floats (per image, then the batch mean). */
+long dsgan_ms_ssim_workspace(int N, int C, int H, int W);
+int dsgan_ms_ssim(const float* real, const float* fake, float a, float b, int N, int C, int H, int W,
+                  const float* win11, float C1, float C2, const float* weights_host, int levels,
+                  float* work, float* stats, float* out, hipStream_t stream);
 
 /* ---- fused Adam over a flat buffer (adam.hip): torch.optim.Adam pix2pix_model.py:122-125 -- */
 int dsgan_adam(float* p, const float* g, float* m, float* v, long n, float lr, float beta1,

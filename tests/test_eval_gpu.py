@@ -1,0 +1,91 @@
+"""Evaluation / inference path: the HIP ms_ssim (DSGAN/MS_SSIM.py:153-225)
+against the golden vector and the CPU oracle, and the ``--model test`` generator-only model
+loading a checkpoint written by the training model.
+
+Tolerance: ms_ssim is a product of five fp32 plane means; |HIP - oracle| <= 2e-5 absolute
+(the oracle itself matches the reference to 1e-6, tests/test_oracle.py)."""
+import os
+import tempfile
+
+import pytest
+import torch
+
+from oracle import dsgan_cpu as O
+from oracle.recipe import make_params, synth_pair
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _f3_pair():
+    # the exact generator sequence of tests/test_oracle.py::test_ssim_msssim
+    g = torch.Generator().manual_seed(3)
+    X = torch.rand(2, 3, 64, 64, generator=g)
+    _ = (X + 0.2 * torch.randn(2, 3, 64, 64, generator=g)).clamp(0, 1)
+    X2 = torch.rand(1, 3, 176, 176, generator=g)
+    Y2 = (X2 + 0.2 * torch.randn(1, 3, 176, 176, generator=g)).clamp(0, 1)
+    return X2, Y2
+
+
+def test_ms_ssim_golden(golden):
+    import MS_SSIM as M
+    X2, Y2 = _f3_pair()
+    v = M.ms_ssim(X2.to(DEV), Y2.to(DEV), data_range=1.0).item()
+    assert abs(v - float(golden["F3_msssim"])) < 2e-5, (v, float(golden["F3_msssim"]))
+
+
+@pytest.mark.parametrize("shape", [(2, 3, 176, 176), (2, 3, 181, 199), (1, 1, 256, 256)])
+def test_ms_ssim_vs_oracle(shape):
+    import MS_SSIM as M
+    g = torch.Generator().manual_seed(shape[2] + shape[3])
+    X = torch.rand(shape, generator=g)
+    Y = (X + 0.15 * torch.randn(shape, generator=g)).clamp(0, 1)
+    got = M.ms_ssim(X.to(DEV), Y.to(DEV), data_range=1.0, size_average=False).cpu()
+    for n in range(shape[0]):
+        ref = float(O.ms_ssim(X[n:n + 1], Y[n:n + 1]))
+        assert abs(got[n].item() - ref) < 2e-5, (n, got[n].item(), ref)
+    mean = M.ms_ssim(X.to(DEV), Y.to(DEV), data_range=1.0).item()
+    assert abs(mean - float(O.ms_ssim(X, Y))) < 2e-5
+    # the (t+1)/2 affine form the quality metric uses on generator outputs in [-1, 1]
+    from dsgan_hip import functional as HF
+    v = HF.ms_ssim_affine((2 * X - 1).to(DEV), (2 * Y - 1).to(DEV), 0.5, 0.5).item()
+    assert abs(v - mean) < 2e-5
+
+
+def test_ms_ssim_rejects_small_images():
+    import MS_SSIM as M
+    x = torch.rand(1, 3, 150, 150, device=DEV)
+    with pytest.raises(AssertionError):
+        M.ms_ssim(x, x, data_range=1.0)
+
+
+def test_test_model_loads_training_checkpoint():
+    """save_networks of the training model -> ``--model test`` -> identical generator output."""
+    import dsgan_hip
+    from models import create_model
+    from options.test_options import default_test_opt
+    from options.train_options import default_train_opt
+    dsgan_hip.require_gpu()
+    with tempfile.TemporaryDirectory() as d:
+        opt = default_train_opt(gpu_ids=[0], pool_size=0, precision="fp32", checkpoints_dir=d)
+        m = create_model(opt)
+        gp = make_params(O.g_param_spec(), "fanin", 1000)
+        with torch.no_grad():
+            for k, v in m.netG.state_dict().items():
+                v.copy_(gp[k])
+        A, _ = synth_pair(2, 64, seed=11)
+        with torch.no_grad():
+            ref = m.netG(A.to(DEV)).cpu()
+        m.save_networks("7")
+        # a reference-style DataParallel checkpoint name/prefix loads too
+        sd = torch.load(os.path.join(d, opt.name, "7_useSE_net_G.pth"), weights_only=True)
+        torch.save({"module." + k: v for k, v in sd.items()}, os.path.join(d, opt.name, "8_net_G.pth"))
+        for epoch in ("7", "8"):
+            topt = default_test_opt(gpu_ids=[0], precision="fp32", checkpoints_dir=d, which_epoch=epoch,
+                                    name=opt.name)
+            t = create_model(topt)
+            assert type(t).__name__ == "TestModel"
+            t.setup(topt)
+            t.set_input({"A": A, "A_paths": ["a", "b"]})
+            t.test()
+            assert torch.equal(t.fake_B.cpu(), ref), epoch

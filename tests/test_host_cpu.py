@@ -28,6 +28,16 @@ def test_registry_rule():
     from models import find_model_using_name
     from models.pix2pix_model import Pix2PixModel
     assert find_model_using_name("pix2pix") is Pix2PixModel
+    from models.test_model import TestModel
+    assert find_model_using_name("test") is TestModel
+
+
+def test_test_options_defaults():
+    """TestOptions (DSGAN/options/test_options.py:5-14) + TestModel's option setter."""
+    from options.test_options import default_test_opt
+    o = default_test_opt()
+    assert (o.model, o.phase, o.dataset_mode, o.which_epoch, o.isTrain) == ("test", "test", "single", "1", False)
+    assert o.model_suffix == ""
 
 
 def test_state_dict_keys_match_reference(golden):
