@@ -712,6 +712,31 @@ static inline dim3 grid4(int N, long E4) {
   return dim3((unsigned)(gx < 1 ? 1 : gx), (unsigned)N);
 }
 
+// Input pipeline (DSGAN/data/aligned_dataset.py:38-86): uint8 HWC crops -> ToTensor (/255) ->
+// Normalize(0.5, 0.5) -> horizontal flip (per-sample flag) -> optional RGB->gray
+// (0.299/0.587/0.114, evaluated in the reference's order without FMA contraction), NCHW fp32.
+// One thread per output pixel, all channels; bit-exact with the torchvision/torch CPU ops.
+__global__ void u8_to_image_kernel(const unsigned char* __restrict__ src, const int* __restrict__ flip,
+                                   float* __restrict__ dst, int N, int H, int W, int gray) {
+#pragma clang fp contract(off)   // hipcc contracts mul+add into FMA by default; torch CPU does not
+  const long total = (long)N * H * W;
+  for (long t = blockIdx.x * 256L + threadIdx.x; t < total; t += (long)gridDim.x * 256) {
+    const int n = (int)(t / ((long)H * W));
+    const int r = (int)(t - (long)n * H * W), h = r / W, w = r - h * W;
+    const int ws = flip[n] ? W - 1 - w : w;
+    const unsigned char* px = src + (((long)n * H + h) * W + ws) * 3;
+    float c[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) c[k] = ((float)px[k] / 255.f - 0.5f) / 0.5f;
+    if (gray) {
+      dst[(long)n * H * W + r] = (c[0] * 0.299f + c[1] * 0.587f) + c[2] * 0.114f;
+    } else {
+#pragma unroll
+      for (int k = 0; k < 3; ++k) dst[((long)n * 3 + k) * H * W + r] = c[k];
+    }
+  }
+}
+
 __global__ void scale_kernel(float* p, float a, long n) {
   for (long t = blockIdx.x * (long)blockDim.x + threadIdx.x; t < n; t += (long)gridDim.x * blockDim.x) p[t] *= a;
 }
@@ -953,6 +978,15 @@ int dsgan_copy_strided(const float* src, long src_bs, float* dst, long dst_bs, i
     return 0;
   }
   hipLaunchKernelGGL(copy_strided_kernel, dim3(grid_for((long)N * E)), dim3(256), 0, st, src, src_bs, dst, dst_bs, N, E);
+  DSG_CHECK_LAUNCH();
+  return 0;
+}
+
+int dsgan_u8_to_image(const unsigned char* src, const int* flip, float* dst, int N, int H, int W, int gray,
+                      hipStream_t st) {
+  DSG_REQUIRE(src && flip && dst && N > 0 && H > 0 && W > 0, "dsgan_u8_to_image: bad args");
+  hipLaunchKernelGGL(u8_to_image_kernel, dim3(grid_for((long)N * H * W)), dim3(256), 0, st, src, flip, dst, N, H, W,
+                     gray);
   DSG_CHECK_LAUNCH();
   return 0;
 }

@@ -275,6 +275,11 @@ int dsgan_ssim_fwd(const float* real, const float* fake, float a, float b, int p
 int dsgan_ssim_bwd(const float* real, const float* fake, float a, float b, int planes, int H,
                    int W, const float* win11, const float* coef, const float* gout, float gcoef,
                    float* dfake, int accumulate, hipStream_t stream);
+/* input pipeline, DSGAN/data/aligned_dataset.py:38-86 (ToTensor, crop, Normalize(0.5,0.5), flip,
+ * optional gray): src uint8 [N][H][W][3] (already cropped), flip int [N] (device), dst fp32
+ * [N][3 or 1][H][W]; bit-exact with the reference's torch CPU transforms. */
+int dsgan_u8_to_image(const unsigned char* src, const int* flip, float* dst, int N, int H, int W, int gray,
+                      hipStream_t stream);
 /* MS-SSIM evaluation of (a*real+b, a*fake+b), DSGAN/MS_SSIM.py:153-225 (ms_ssim; no gradient):
  * per scale the SSIM / contrast-structure plane means, then the padded 2x2 average pool;
  * weights_host = the level weights (host array, levels <= 8).  work: dsgan_ms_ssim_workspace

@@ -89,3 +89,45 @@ def test_test_model_loads_training_checkpoint():
             t.set_input({"A": A, "A_paths": ["a", "b"]})
             t.test()
             assert torch.equal(t.fake_B.cpu(), ref), epoch
+
+
+@pytest.mark.parametrize("gray", [False, True])
+def test_data_loader_gpu_transforms_bit_exact(tmp_path, gray):
+    """CreateDataLoader batches (uint8 upload + dsgan_u8_to_image) == the reference's torch CPU
+    transforms: ToTensor (/255), crop, Normalize(0.5, 0.5), flip, RGB->gray (aligned_dataset.py:52-82)."""
+    import random
+    import numpy as np
+    from PIL import Image
+    from data import CreateDataLoader
+    from options.train_options import default_train_opt
+    rng = np.random.default_rng(1)
+    d = tmp_path / "train_all"
+    d.mkdir()
+    for i in range(4):
+        for side in ("a", "b"):
+            Image.fromarray(rng.integers(0, 256, (40, 48, 3), dtype=np.uint8)).save(str(d / ("%s_%d.png" % (side, i))))
+    opt = default_train_opt(gpu_ids=[0], dataroot=str(tmp_path), phase="train_all", loadSize_w=48, fineSize_w=32,
+                            loadSize_h=40, fineSize_h=24, batchSize=2, nThreads=0, serial_batches=True,
+                            input_nc=1 if gray else 3)
+    loader = CreateDataLoader(opt, "train").load_data()
+    random.seed(9)
+    batches = list(loader)
+    assert len(batches) == 2
+    random.seed(9)
+    for bi, data in enumerate(batches):
+        for j in range(2):
+            k = 2 * bi + j
+            wo, ho = random.randint(0, 48 - 32 - 1), random.randint(0, 40 - 24 - 1)
+            flip = random.random() < 0.5
+            for side, key, g in (("a", "A", gray), ("b", "B", False)):
+                img = np.asarray(Image.open(str(d / ("%s_%d.png" % (side, k)))).convert("RGB"))
+                t = torch.from_numpy(img.copy()).permute(2, 0, 1).contiguous().float().div(255)
+                t = t[:, ho:ho + 24, wo:wo + 32]
+                m = torch.tensor([0.5, 0.5, 0.5])[:, None, None]
+                t = t.sub(m).div(m)
+                if flip:
+                    t = t.index_select(2, torch.arange(31, -1, -1))
+                if g:
+                    t = (t[0] * 0.299 + t[1] * 0.587 + t[2] * 0.114).unsqueeze(0)
+                got = data[key][j].cpu()
+                assert got.shape == t.shape and torch.equal(got, t), (k, key)

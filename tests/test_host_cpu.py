@@ -101,3 +101,44 @@ def test_allreduce_mean_gloo_world2():
         p.join(timeout=60)
     expect = (torch.arange(10, dtype=torch.float32) * 1.5).tolist()
     assert out[0] == expect and out[1] == expect
+
+
+def _write_pairs(d, n, H, W, seed=0):
+    import numpy as np
+    from PIL import Image
+    rng = np.random.default_rng(seed)
+    os.makedirs(d, exist_ok=True)
+    imgs = {}
+    for i in range(n):
+        for side in ("a", "b"):
+            arr = rng.integers(0, 256, (H, W, 3), dtype=np.uint8)
+            p = os.path.join(d, "%s_%03d.png" % (side, i))
+            Image.fromarray(arr).save(p)
+            imgs[p] = arr
+    return imgs
+
+
+def test_aligned_dataset_host_side(tmp_path):
+    """make_dataset halves (sorted), the reference's RNG order (w_offset, h_offset, flip) and
+    the uint8 crop (DSGAN/data/aligned_dataset.py:31-74, image_folder.py:24-34)."""
+    import random
+    from types import SimpleNamespace
+    import numpy as np
+    from data.aligned_dataset import AlignedDataset
+    from data.image_folder import make_dataset
+    imgs = _write_pairs(str(tmp_path / "train_all"), 3, 40, 48)
+    A, B = make_dataset(str(tmp_path / "train_all"))
+    assert [os.path.basename(p) for p in A] == ["a_000.png", "a_001.png", "a_002.png"]
+    assert [os.path.basename(p) for p in B] == ["b_000.png", "b_001.png", "b_002.png"]
+    opt = SimpleNamespace(dataroot=str(tmp_path), phase="train_all", resize_or_crop="resize_and_crop",
+                          loadSize_w=48, fineSize_w=32, loadSize_h=40, fineSize_h=24, no_flip=False)
+    ds = AlignedDataset()
+    ds.initialize(opt)
+    random.seed(5)
+    item = ds[1]
+    random.seed(5)
+    wo, ho = random.randint(0, 48 - 32 - 1), random.randint(0, 40 - 24 - 1)
+    fl = random.random() < 0.5
+    assert item["flip"] == int(fl)
+    assert np.array_equal(item["A_u8"].numpy(), imgs[A[1]][ho:ho + 24, wo:wo + 32])
+    assert np.array_equal(item["B_u8"].numpy(), imgs[B[1]][ho:ho + 24, wo:wo + 32])
