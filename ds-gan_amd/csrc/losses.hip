@@ -207,6 +207,64 @@ __global__ __launch_bounds__(256) void ssim_fwd_kernel(SSIMArgs s, int tiles_w) 
   if (threadIdx.x == 0) atomicAdd(s.out, ssum);
 }
 
+// ---- train.py per-iteration metrics (DSGAN/train.py:27-44, 110-124) ----------------------------
+// The reference converts image 0 of fake_B / real_B to uint8 HWC on the host ((t+1)/2*255, clip,
+// truncate) and calls skimage's structural_similarity (uniform 7x7 window, sample covariance,
+// data_range 255, border-cropped mean, channel mean) and PSNR.  Here both run on the device on
+// the same uint8 values; the per-call results are accumulated in device memory so the loop
+// needs no host sync per iteration.  acc[0] += ssim, acc[1] += psnr, acc[2] += 1.
+__device__ __forceinline__ float to_u8f(float t) {
+  const float v = ((t + 1.f) / 2.f) * 255.f;
+  return truncf(fminf(fmaxf(v, 0.f), 255.f));
+}
+
+__global__ __launch_bounds__(256) void img_metrics_kernel(const float* __restrict__ fake, const float* __restrict__ real,
+                                                          int C, int H, int W, double* part) {
+  __shared__ double sh[2][4];
+  const int Hc = H - 6, Wc = W - 6;
+  const long tot = (long)C * Hc * Wc;
+  double ssum = 0.0, se = 0.0;
+  const double NP = 49.0, cov = NP / (NP - 1.0), C1 = (0.01 * 255.0) * (0.01 * 255.0), C2 = (0.03 * 255.0) * (0.03 * 255.0);
+  for (long t = blockIdx.x * 256L + threadIdx.x; t < tot; t += (long)gridDim.x * 256) {
+    const int c = (int)(t / ((long)Hc * Wc));
+    const int r = (int)(t - (long)c * Hc * Wc), h = r / Wc + 3, w = r - (r / Wc) * Wc + 3;
+    const float* fp = fake + (long)c * H * W;
+    const float* rp = real + (long)c * H * W;
+    double sx = 0, sy = 0, sxx = 0, syy = 0, sxy = 0;
+    for (int dh = -3; dh <= 3; ++dh)
+      for (int dw = -3; dw <= 3; ++dw) {
+        const long o = (long)(h + dh) * W + (w + dw);
+        const double x = to_u8f(rp[o]), y = to_u8f(fp[o]);   // img1 = label, img2 = result
+        sx += x; sy += y; sxx += x * x; syy += y * y; sxy += x * y;
+      }
+    const double ux = sx / NP, uy = sy / NP;
+    const double vx = cov * (sxx / NP - ux * ux), vy = cov * (syy / NP - uy * uy), vxy = cov * (sxy / NP - ux * uy);
+    ssum += ((2 * ux * uy + C1) * (2 * vxy + C2)) / ((ux * ux + uy * uy + C1) * (vx + vy + C2));
+  }
+  for (long t = blockIdx.x * 256L + threadIdx.x; t < (long)C * H * W; t += (long)gridDim.x * 256) {
+    const double d = (double)to_u8f(real[t]) - (double)to_u8f(fake[t]);
+    se += d * d;
+  }
+  for (int o = 32; o > 0; o >>= 1) { ssum += __shfl_xor(ssum, o, 64); se += __shfl_xor(se, o, 64); }
+  const int wv = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) { sh[0][wv] = ssum; sh[1][wv] = se; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    part[2 * blockIdx.x] = (sh[0][0] + sh[0][1]) + (sh[0][2] + sh[0][3]);
+    part[2 * blockIdx.x + 1] = (sh[1][0] + sh[1][1]) + (sh[1][2] + sh[1][3]);
+  }
+}
+
+__global__ void img_metrics_final_kernel(const double* part, int nblk, int C, int H, int W, float* acc) {
+  if (threadIdx.x != 0) return;
+  double s = 0, e = 0;
+  for (int i = 0; i < nblk; ++i) { s += part[2 * i]; e += part[2 * i + 1]; }
+  const double ssim = s / ((double)C * (H - 6) * (W - 6));
+  const double mse = e / ((double)C * H * W);
+  const double psnr = mse / (255.0 * 255.0) < 1e-10 ? 100.0 : 10.0 * log10(255.0 * 255.0 / mse);
+  acc[0] += (float)ssim; acc[1] += (float)psnr; acc[2] += 1.f;
+}
+
 // ---- MS-SSIM evaluation (DSGAN/MS_SSIM.py:153-225; no gradient) ---------------------------
 // One scale: per plane the sums of the SSIM map and of the contrast-structure map cs
 // (_ssim, :55-92) -- same tiling and filter order as ssim_fwd_kernel, no backward coefficients.
@@ -430,6 +488,17 @@ int dsgan_tv_fwd(const float* y, long planes, int H, int W, float coef, float* o
 int dsgan_tv_bwd(const float* y, long planes, int H, int W, float coef, const float* gout, float* dy,
                  int accumulate, hipStream_t st) {
   hipLaunchKernelGGL(tv_bwd_kernel, dim3(red_grid(planes * H * W) * 8), dim3(256), 0, st, y, planes, H, W, gout, coef, dy, accumulate);
+  DSG_CHECK_LAUNCH();
+  return 0;
+}
+
+// acc[3] (device, float) += {ssim, psnr, 1} of one [C][H][W] image pair in [-1, 1] (see
+// img_metrics_kernel); part: 2*64 doubles of scratch.
+int dsgan_img_metrics(const float* fake, const float* real, int C, int H, int W, double* part, float* acc,
+                      hipStream_t st) {
+  DSG_REQUIRE(fake && real && part && acc && C > 0 && H > 6 && W > 6, "dsgan_img_metrics: bad args (H, W > 6)");
+  hipLaunchKernelGGL(img_metrics_kernel, dim3(64), dim3(256), 0, st, fake, real, C, H, W, part);
+  hipLaunchKernelGGL(img_metrics_final_kernel, dim3(1), dim3(64), 0, st, part, 64, C, H, W, acc);
   DSG_CHECK_LAUNCH();
   return 0;
 }

@@ -26,7 +26,7 @@ class AlignedDataset(torch.utils.data.Dataset):
     def _crop(self, path, h_off, w_off):
         img = np.asarray(Image.open(path).convert("RGB"), dtype=np.uint8)
         fh, fw = self.opt.fineSize_h, self.opt.fineSize_w
-        return np.ascontiguousarray(img[h_off:h_off + fh, w_off:w_off + fw])
+        return img[h_off:h_off + fh, w_off:w_off + fw].copy()
 
     def __getitem__(self, index):
         opt = self.opt

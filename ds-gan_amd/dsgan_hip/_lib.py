@@ -88,6 +88,7 @@ SIGNATURES = {
     "dsgan_ssim_fwd": [P, P, F, F, I, I, I, P, F, F, P, P, S],
     "dsgan_ms_ssim_workspace": [I, I, I, I],
     "dsgan_u8_to_image": [P, P, P, I, I, I, I, S],
+    "dsgan_img_metrics": [P, P, I, I, I, P, P, S],
     "dsgan_ms_ssim": [P, P, F, F, I, I, I, I, P, F, F, P, I, P, P, P, S],
     "dsgan_ssim_bwd": [P, P, F, F, I, I, I, P, P, P, F, P, I, S],
     # adam.hip

@@ -1,0 +1,91 @@
+"""Training loop with the reference's semantics (DSGAN/train.py:47-185) on the MI355X build.
+
+Same order of work per iteration: set_input -> optimize_parameters -> get_img_tir / get_img_gen
+/ get_img_label -> SSIM + PSNR of image 0 (device-side, util/metrics.py) -> every
+``output_freq`` iterations the loss line and ``result.csv``; per epoch ``each_epoch.csv``,
+``save_networks(epoch)`` and ``update_learning_rate()``.  The seed is 20 (:48).  Image dumps
+(cv2) and the visualizer/HTML are out of scope (SURVEY.md §8 out-of-scope list).
+
+    python ds-gan_amd/train.py --dataroot DATA --out RESULTS [reference TrainOptions flags...]
+"""
+import argparse
+import csv
+import math
+import os
+import random
+import sys
+import time
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+if HERE not in sys.path:
+    sys.path.insert(0, HERE)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+
+def setup_seed(seed):
+    torch.manual_seed(seed)
+    torch.cuda.manual_seed_all(seed)
+    np.random.seed(seed)
+    random.seed(seed)
+
+
+def main(argv=None, output_freq=100):
+    from data import CreateDataLoader
+    from models import create_model
+    from options.train_options import TrainOptions
+    from util.metrics import TrainMetrics
+
+    ap = argparse.ArgumentParser(add_help=False)
+    ap.add_argument("--out", default=os.path.abspath(os.path.join("..", "resext50_vision1")))
+    ap.add_argument("--dataroot", default="/root/dataset/256x256")
+    known, rest = ap.parse_known_args(argv)
+    setup_seed(20)
+    out = known.out
+    os.makedirs(out, exist_ok=True)
+    opt = TrainOptions().parse(known.dataroot, out, rest)   # parse() sets checkpoints_dir = out/checkpoints
+    dataset = CreateDataLoader(opt, "train").load_data()
+    print("#training images = %d" % len(dataset))
+    model = create_model(opt)
+    model.setup(opt)
+    metrics = TrainMetrics(model.device)
+    history = []
+    for epoch in range(opt.epoch_count, opt.niter + opt.niter_decay + 1):
+        metrics.reset()
+        epoch_start_time = time.time()
+        epoch_iter, i = 0, -1
+        for i, data in enumerate(dataset):
+            iter_start_time = time.time()
+            epoch_iter += opt.batchSize
+            model.set_input(data)
+            model.optimize_parameters()
+            model.get_img_tir(data)
+            with torch.no_grad():   # the reference runs this forward with autograd on; output is identical
+                model.get_img_gen(data)
+            model.get_img_label(data)
+            metrics.update(model.fake_B[0], model.real_B[0])
+            if (i + 1) % output_freq == 0:
+                losses = model.get_current_losses()
+                ssim_avg, psnr_avg = metrics.averages()
+                t = (time.time() - iter_start_time) / opt.batchSize
+                message = "(epoch: %d, iters: %d, time: %.3f) " % (epoch, epoch_iter, t)
+                message += "".join("%s: %.3f " % (k, v) for k, v in losses.items())
+                print(message + "ssim: %.4f psnr: %.3f" % (ssim_avg, psnr_avg))
+                with open(os.path.join(out, "result.csv"), "a", newline="") as f:
+                    csv.writer(f).writerow([epoch, "".join("%s: %.3f " % (k, v) for k, v in losses.items()) + "  ",
+                                            ssim_avg, psnr_avg])
+        ssim_avg, psnr_avg = metrics.averages()
+        history.append((epoch, ssim_avg, psnr_avg))
+        with open(os.path.join(out, "each_epoch.csv"), "a", newline="") as f:
+            csv.writer(f).writerow([epoch, "train", ssim_avg, psnr_avg])
+        print("saving the model at the end of epoch %d, iters %d" % (epoch, i + 1))
+        model.save_networks(epoch)
+        print("End of epoch %d / %d \t Time Taken: %d sec" % (epoch, opt.niter + opt.niter_decay,
+                                                                time.time() - epoch_start_time))
+        model.update_learning_rate()
+    return model, history
+
+
+if __name__ == "__main__":
+    main()

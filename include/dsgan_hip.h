@@ -280,6 +280,11 @@ int dsgan_ssim_bwd(const float* real, const float* fake, float a, float b, int p
  * [N][3 or 1][H][W]; bit-exact with the reference's torch CPU transforms. */
 int dsgan_u8_to_image(const unsigned char* src, const int* flip, float* dst, int N, int H, int W, int gray,
                       hipStream_t stream);
+/* train.py per-iteration metrics (DSGAN/train.py:27-44,110-124): acc[0..2] (device float) +=
+ * {skimage-SSIM, PSNR, 1} of one [C][H][W] pair in [-1,1] after the reference's uint8
+ * conversion; part = 128 doubles of scratch.  No host sync. */
+int dsgan_img_metrics(const float* fake, const float* real, int C, int H, int W, double* part, float* acc,
+                      hipStream_t stream);
 /* MS-SSIM evaluation of (a*real+b, a*fake+b), DSGAN/MS_SSIM.py:153-225 (ms_ssim; no gradient):
  * per scale the SSIM / contrast-structure plane means, then the padded 2x2 average pool;
  * weights_host = the level weights (host array, levels <= 8).  work: dsgan_ms_ssim_workspace
