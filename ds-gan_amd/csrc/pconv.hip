@@ -13,6 +13,7 @@
 // Per tap the bf16 weight slice [BM][32] is register-prefetched one tap ahead into a double
 // buffer.  Weights are a bf16 tap-major copy (dsgan_conv_wtrans_bf16).
 #include "common.h"
+#include <stdlib.h>
 
 namespace dsg {
 
@@ -290,7 +291,16 @@ int dsgan_pconv(const float* X, long x_bs, const void* Wb, const float* bias, fl
   g.X = X; g.x_bs = x_bs; g.Wb = (const __bf16*)Wb; g.Y = Y; g.y_bs = y_bs; g.bias = bias;
   g.gpre = gpre; g.gpre_bs = gpre_bs; g.nb = nb; g.K = K; g.M = M; g.H = H; g.W = W; g.Ho = Ho;
   g.Wo = Wo; g.pad = pad; g.act = act; g.gact = gact; g.slope = slope; g.accumulate = accumulate;
-  const int rc = M > 64 ? pc_dispatch<128>(g, KH, stride, st) : pc_dispatch<64>(g, KH, stride, st);
+  // BM = 256 for the wide layers (VGG conv3/conv4, 256/512 output channels): per tap twice the
+  // MFMAs between barriers and half the patch traffic per MAC (DSGAN_PC_BM256=0 disables)
+  static int bm256 = -1;
+  if (bm256 < 0) { const char* e = getenv("DSGAN_PC_BM256"); bm256 = e ? atoi(e) : 1; }
+  // ... only while the launch still has >= 2 workgroups per CU (at 32x32 it would have one)
+  const long ptiles = (long)nb * ((Ho + 7) / 8) * ((Wo + 15) / 16);
+  const bool use256 = bm256 && M >= 256 && ptiles * ((M + 255) / 256) >= 512;
+  const int rc = use256 ? pc_dispatch<256>(g, KH, stride, st)
+                 : M > 64            ? pc_dispatch<128>(g, KH, stride, st)
+                                     : pc_dispatch<64>(g, KH, stride, st);
   DSG_REQUIRE(rc == 0, "dsgan_pconv: no kernel for KH=%d stride=%d", KH, stride);
   DSG_CHECK_LAUNCH();
   return 0;
