@@ -459,6 +459,98 @@ __global__ void maxpool_bwd_win_kernel(const float* __restrict__ dy, long dy_bs,
   }
 }
 
+// 2x2 windows, two adjacent outputs per thread: one 16-byte load from each input row, 8-byte
+// value/index stores (W % 4 == 0, 16-byte aligned input planes, 8-byte aligned outputs).  The
+// window is scanned in the same row-major order as maxpool_fwd_win_kernel (NaN / tie rules
+// of torch's max_pool2d_with_indices are unchanged).
+__device__ __forceinline__ void mp_pick(float v, int pos, float& best, int& bi) {
+  if (v > best || isnan(v)) { best = v; bi = pos; }
+}
+__global__ void maxpool2_fwd_x2_kernel(const float* __restrict__ x, long x_bs, float* __restrict__ y, long y_bs,
+                                       int* __restrict__ idx, int N, int C, int H, int W) {
+  const int Wo = W / 2, Po = (H / 2) * Wo, Wq = Wo / 2, Q = Po / 2;
+  for (int plane = blockIdx.y; plane < N * C; plane += gridDim.y) {
+    const int n = plane / C, c = plane - n * C;
+    const float* xp = x + (long)n * x_bs + (long)c * H * W;
+    float* yp = y + (long)n * y_bs + (long)c * Po;
+    int* ip = idx + (long)plane * Po;
+    for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < Q; q += gridDim.x * blockDim.x) {
+      const int oh = q / Wq, qw = q - oh * Wq;
+      const int r0 = 2 * oh * W + 4 * qw;
+      const float4 a = *reinterpret_cast<const float4*>(xp + r0);
+      const float4 b = *reinterpret_cast<const float4*>(xp + r0 + W);
+      float b0 = -INFINITY, b1 = -INFINITY; int i0 = r0, i1 = r0 + 2;
+      mp_pick(a.x, r0, b0, i0);     mp_pick(a.y, r0 + 1, b0, i0);
+      mp_pick(b.x, r0 + W, b0, i0); mp_pick(b.y, r0 + W + 1, b0, i0);
+      mp_pick(a.z, r0 + 2, b1, i1);     mp_pick(a.w, r0 + 3, b1, i1);
+      mp_pick(b.z, r0 + W + 2, b1, i1); mp_pick(b.w, r0 + W + 3, b1, i1);
+      *reinterpret_cast<float2*>(yp + 2 * q) = make_float2(b0, b1);
+      *reinterpret_cast<int2*>(ip + 2 * q) = make_int2(i0, i1);
+    }
+  }
+}
+__global__ void maxpool2_bwd_x2_kernel(const float* __restrict__ dy, long dy_bs, const int* __restrict__ idx,
+                                       float* __restrict__ dx, long dx_bs, int N, int C, int H, int W,
+                                       int accumulate) {
+  const int Wo = W / 2, Po = (H / 2) * Wo, Wq = Wo / 2, Q = Po / 2;
+  for (int plane = blockIdx.y; plane < N * C; plane += gridDim.y) {
+    const int n = plane / C, c = plane - n * C;
+    const float* gp = dy + (long)n * dy_bs + (long)c * Po;
+    const int* ip = idx + (long)plane * Po;
+    float* dp = dx + (long)n * dx_bs + (long)c * H * W;
+    for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < Q; q += gridDim.x * blockDim.x) {
+      const int oh = q / Wq, qw = q - oh * Wq;
+      const int r0 = 2 * oh * W + 4 * qw;
+      const int2 id = *reinterpret_cast<const int2*>(ip + 2 * q);
+      const float2 gv = *reinterpret_cast<const float2*>(gp + 2 * q);
+      float4 a = make_float4((r0 == id.x) ? gv.x : 0.f, (r0 + 1 == id.x) ? gv.x : 0.f,
+                             (r0 + 2 == id.y) ? gv.y : 0.f, (r0 + 3 == id.y) ? gv.y : 0.f);
+      float4 b = make_float4((r0 + W == id.x) ? gv.x : 0.f, (r0 + W + 1 == id.x) ? gv.x : 0.f,
+                             (r0 + W + 2 == id.y) ? gv.y : 0.f, (r0 + W + 3 == id.y) ? gv.y : 0.f);
+      float4* pa = reinterpret_cast<float4*>(dp + r0);
+      float4* pb = reinterpret_cast<float4*>(dp + r0 + W);
+      if (accumulate) {
+        const float4 oa = *pa, ob = *pb;
+        a.x += oa.x; a.y += oa.y; a.z += oa.z; a.w += oa.w;
+        b.x += ob.x; b.y += ob.y; b.z += ob.z; b.w += ob.w;
+      }
+      *pa = a;
+      *pb = b;
+    }
+  }
+}
+
+// KxK windows with K % 4 == 0: one 16-byte dx chunk per thread (a chunk lies in one window), so
+// a wave writes 1 KB of one input row contiguously instead of K/4 strided 16-byte pieces.
+// Used for K = 8, 16 (84/65 us vs 107/77 us at 16x64x256x256); at K = 4 the window kernel's
+// one index load per 16 outputs wins (52 vs 56 us).
+template <int K>
+__global__ void maxpool_bwd_row_kernel(const float* __restrict__ dy, long dy_bs, const int* __restrict__ idx,
+                                       float* __restrict__ dx, long dx_bs, int N, int C, int H, int W,
+                                       int accumulate) {
+  static_assert(K % 4 == 0, "16-byte chunks must not straddle windows");
+  const int Wo = W / K, Po = (H / K) * Wo, W4 = W / 4, n4 = H * W4;
+  for (int plane = blockIdx.y; plane < N * C; plane += gridDim.y) {
+    const int n = plane / C, c = plane - n * C;
+    const float* gp = dy + (long)n * dy_bs + (long)c * Po;
+    const int* ip = idx + (long)plane * Po;
+    float* dp = dx + (long)n * dx_bs + (long)c * H * W;
+    for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < n4; q += gridDim.x * blockDim.x) {
+      const int h = q / W4, c4 = q - h * W4;
+      const int o = (h / K) * Wo + (c4 * 4) / K;
+      const int id = ip[o] - (h * W + c4 * 4);
+      const float gv = gp[o];
+      float4 v = make_float4(id == 0 ? gv : 0.f, id == 1 ? gv : 0.f, id == 2 ? gv : 0.f, id == 3 ? gv : 0.f);
+      float4* d = reinterpret_cast<float4*>(dp) + q;
+      if (accumulate) {
+        const float4 u = *d;
+        v.x += u.x; v.y += u.y; v.z += u.z; v.w += u.w;
+      }
+      *d = v;
+    }
+  }
+}
+
 // Generic fallback (any H, W): element-parallel, zero fill beyond the floor windows.
 __global__ void maxpool_fwd_kernel(const float* __restrict__ x, long x_bs, float* __restrict__ y,
                                    long y_bs, int* __restrict__ idx, int N, int C, int H, int W,
@@ -765,7 +857,18 @@ __global__ __launch_bounds__(256) void channel_sum_kernel(const float* dy, long 
   float s = 0.f;
   if ((HW & 3) == 0 && (((uintptr_t)p) & 15) == 0) {
     const float4* p4 = reinterpret_cast<const float4*>(p);
-    for (int i = t; i < HW / 4; i += NT) { const float4 v = p4[i]; s += (v.x + v.y) + (v.z + v.w); }
+    const int n4 = HW / 4;
+    float s1 = 0.f, s2 = 0.f, s3 = 0.f;
+    int i = t;
+    for (; i + 3 * NT < n4; i += 4 * NT) {   // four independent 16-byte loads in flight
+      const float4 v0 = p4[i], v1 = p4[i + NT], v2 = p4[i + 2 * NT], v3 = p4[i + 3 * NT];
+      s += (v0.x + v0.y) + (v0.z + v0.w);
+      s1 += (v1.x + v1.y) + (v1.z + v1.w);
+      s2 += (v2.x + v2.y) + (v2.z + v2.w);
+      s3 += (v3.x + v3.y) + (v3.z + v3.w);
+    }
+    for (; i < n4; i += NT) { const float4 v = p4[i]; s += (v.x + v.y) + (v.z + v.w); }
+    s = (s + s1) + (s2 + s3);
   } else {
     for (int i = t; i < HW; i += NT) s += p[i];
   }
@@ -886,7 +989,11 @@ int dsgan_maxpool_fwd(const float* x, long x_bs, float* y, long y_bs, int* idx, 
   const dim3 grid = plane_grid((long)(H / k) * (W / k), (long)N * C);
   const bool fast = (H % k == 0) && (W % k == 0) && (k == 2 ? ((W & 1) == 0 && (x_bs & 1) == 0 && ((uintptr_t)x & 7) == 0)
                                                             : ((W & 3) == 0 && (x_bs & 3) == 0 && ((uintptr_t)x & 15) == 0));
-  if (fast && k == 2) hipLaunchKernelGGL(maxpool_fwd_win_kernel<2>, grid, dim3(256), 0, st, x, x_bs, y, y_bs, idx, N, C, H, W);
+  const bool x2 = fast && k == 2 && (W & 3) == 0 && (x_bs & 3) == 0 && ((uintptr_t)x & 15) == 0 &&
+                  (y_bs & 1) == 0 && (((uintptr_t)y | (uintptr_t)idx) & 7) == 0;
+  if (x2) hipLaunchKernelGGL(maxpool2_fwd_x2_kernel, plane_grid((long)(H / 2) * (W / 4), (long)N * C), dim3(256), 0, st,
+                             x, x_bs, y, y_bs, idx, N, C, H, W);
+  else if (fast && k == 2) hipLaunchKernelGGL(maxpool_fwd_win_kernel<2>, grid, dim3(256), 0, st, x, x_bs, y, y_bs, idx, N, C, H, W);
   else if (fast && k == 4) hipLaunchKernelGGL(maxpool_fwd_win_kernel<4>, grid, dim3(256), 0, st, x, x_bs, y, y_bs, idx, N, C, H, W);
   else if (fast && k == 8) hipLaunchKernelGGL(maxpool_fwd_win_kernel<8>, grid, dim3(256), 0, st, x, x_bs, y, y_bs, idx, N, C, H, W);
   else if (fast && k == 16) hipLaunchKernelGGL(maxpool_fwd_win_kernel<16>, grid, dim3(256), 0, st, x, x_bs, y, y_bs, idx, N, C, H, W);
@@ -901,10 +1008,14 @@ int dsgan_maxpool_bwd(const float* dy, long dy_bs, const int* idx, float* dx, lo
   const bool fast = (H % k == 0) && (W % k == 0) && (k == 2 ? ((W & 1) == 0 && (dx_bs & 1) == 0 && ((uintptr_t)dx & 7) == 0)
                                                             : ((W & 3) == 0 && (dx_bs & 3) == 0 && ((uintptr_t)dx & 15) == 0));
   const dim3 wgrid = plane_grid((long)(H / k) * (W / k), (long)N * C);
-  if (fast && k == 2) hipLaunchKernelGGL(maxpool_bwd_win_kernel<2>, wgrid, dim3(256), 0, st, dy, dy_bs, idx, dx, dx_bs, N, C, H, W, accumulate);
+  const bool x2 = fast && k == 2 && (W & 3) == 0 && (dx_bs & 3) == 0 && ((uintptr_t)dx & 15) == 0 &&
+                  (dy_bs & 1) == 0 && (((uintptr_t)dy | (uintptr_t)idx) & 7) == 0;
+  if (x2) hipLaunchKernelGGL(maxpool2_bwd_x2_kernel, plane_grid((long)(H / 2) * (W / 4), (long)N * C), dim3(256), 0, st,
+                             dy, dy_bs, idx, dx, dx_bs, N, C, H, W, accumulate);
+  else if (fast && k == 2) hipLaunchKernelGGL(maxpool_bwd_win_kernel<2>, wgrid, dim3(256), 0, st, dy, dy_bs, idx, dx, dx_bs, N, C, H, W, accumulate);
   else if (fast && k == 4) hipLaunchKernelGGL(maxpool_bwd_win_kernel<4>, wgrid, dim3(256), 0, st, dy, dy_bs, idx, dx, dx_bs, N, C, H, W, accumulate);
-  else if (fast && k == 8) hipLaunchKernelGGL(maxpool_bwd_win_kernel<8>, wgrid, dim3(256), 0, st, dy, dy_bs, idx, dx, dx_bs, N, C, H, W, accumulate);
-  else if (fast && k == 16) hipLaunchKernelGGL(maxpool_bwd_win_kernel<16>, wgrid, dim3(256), 0, st, dy, dy_bs, idx, dx, dx_bs, N, C, H, W, accumulate);
+  else if (fast && k == 8) hipLaunchKernelGGL(maxpool_bwd_row_kernel<8>, plane_grid((long)H * W / 4, (long)N * C), dim3(256), 0, st, dy, dy_bs, idx, dx, dx_bs, N, C, H, W, accumulate);
+  else if (fast && k == 16) hipLaunchKernelGGL(maxpool_bwd_row_kernel<16>, plane_grid((long)H * W / 4, (long)N * C), dim3(256), 0, st, dy, dy_bs, idx, dx, dx_bs, N, C, H, W, accumulate);
   else hipLaunchKernelGGL(maxpool_bwd_kernel, plane_grid((long)H * W, (long)N * C), dim3(256), 0, st, dy, dy_bs,
                           idx, dx, dx_bs, N, C, H, W, k, accumulate);
   DSG_CHECK_LAUNCH();

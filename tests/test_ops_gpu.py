@@ -314,12 +314,14 @@ def test_instance_norm(act, res, N, C, H, W):
         assert rel(rd.grad, rr.grad) < 1e-5
 
 
-@pytest.mark.parametrize("k", [2, 4, 8, 16])
-def test_maxpool_indices_bit_exact(k):
+@pytest.mark.parametrize("k,W", [(2, 48), (2, 50), (4, 48), (8, 48), (16, 48)])
+def test_maxpool_indices_bit_exact(k, W):
+    """W=48 at k=2 takes the two-outputs-per-thread 16-byte kernel, W=50 the 8-byte one."""
     from dsgan_hip import functional as HF
     g = torch.Generator().manual_seed(k)
-    x = torch.randn(2, 3, 32, 48, generator=g)
+    x = torch.randn(2, 3, 32, W, generator=g)
     x[0, 0, :4, :4] = 1.5  # ties: first max in row-major window order wins
+    x[1, 2, 5, 7] = float("nan")  # NaN wins its window, as in torch's max_pool2d
     xr = x.clone().requires_grad_()
     y_ref, i_ref = F.max_pool2d(xr, k, return_indices=True)
     gy = torch.randn(y_ref.shape, generator=g)
@@ -327,9 +329,18 @@ def test_maxpool_indices_bit_exact(k):
     xd = _leaf(x)
     y, idx = HF.max_pool2d(xd, k, return_indices=True)
     y.backward(gy.to(DEV))
-    assert torch.equal(y.cpu(), y_ref.detach())
+    assert torch.allclose(y.cpu(), y_ref.detach(), rtol=0, atol=0, equal_nan=True)  # bit-exact, NaN == NaN
     assert torch.equal(idx.cpu().long(), i_ref)
     assert torch.equal(xd.grad.cpu(), xr.grad)
+    # accumulate form (shared gradient buffers): dx += scatter(dy, idx), through the C-ABI
+    from dsgan_hip._lib import call, ptr, stream
+    N, C, H, _ = x.shape
+    base = torch.randn(x.shape, generator=g)
+    dxa = base.to(DEV)
+    gyd = gy.to(DEV).contiguous()
+    call("dsgan_maxpool_bwd", ptr(gyd), C * (H // k) * (W // k), ptr(idx), ptr(dxa), C * H * W, N, C, H, W, k, 1,
+         stream())
+    assert torch.equal(dxa.cpu(), base + xr.grad)
 
 
 @pytest.mark.parametrize("C,H", [(32, 16), (128, 8), (256, 4)])
@@ -414,6 +425,13 @@ def test_losses():
     l.backward()
     assert abs(l.item() - l_ref.item()) < 1e-5
     assert rel(ad.grad, ar.grad) < 1e-6
+    # 16-byte path with an n % 4 tail, a large multi-block case, and the unaligned fallback
+    for n, off in ((1003, 0), (1 << 22, 0), (1003, 1)):
+        u = torch.randn(n + off, generator=g)
+        v = torch.randn(n + off, generator=g)
+        want = torch.mean(torch.abs(u[off:].double() - v[off:].double())).item()
+        got = HF.l1_loss(u.to(DEV)[off:], v.to(DEV)[off:]).item()
+        assert abs(got - want) < 1e-5 * want, (n, off, got, want)
     ar = a.clone().requires_grad_()
     l_ref = O.tv_loss(ar)
     l_ref.backward()
