@@ -192,7 +192,11 @@ def main():
             "config": {"workload": "DS-GAN optimize_parameters, MixConvNeXtML G + PatchGAN D + VGG16 perceptual + SSIM/L1/TV",
                        "global_batch": args.batch * world, "per_gpu_batch": args.batch,
                        "image": [args.size, args.size], "parallelism": "dp%d" % world,
-                       "baseline_config": "configs[1]: 256x256, batch 16, bf16, 1xMI355X"},
+                       "baseline_config": ("configs[1]: 256x256, batch 16, bf16, 1xMI355X"
+                                           if (args.size, args.batch) == (256, 16) else
+                                           "configs[4] shape: 512x512, batch 8/GPU (bf16 for the named fp16)"
+                                           if (args.size, args.batch) == (512, 8) else
+                                           "off-baseline shape %dx%d, batch %d" % (args.size, args.size, args.batch))},
             "roofline": {"bound": "mfma", "kernel": dom,
                          "achieved": round(dach, 2), "peak": peak, "unit": "TFLOP/s",
                          "frac": round(dach / peak, 4), "traffic": pmc_traffic(dom),
