@@ -461,6 +461,17 @@ static int wgrad_split(PwArgs& g, int BM) {
 
 static bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
+// 256-row M tiles for the wide, deep FWD / DGRAD GEMMs: each staged pixel tile feeds twice the
+// MFMAs, as long as the grid still keeps >= 2 workgroups per CU.  Isolated A/B at the step's
+// shapes (tools/gpu_pw256_micro.sh, B=16): K=4096 dgrad into 1024 ch 0.356 -> 0.264 ms, K=1024
+// fwd to 4096 ch 0.380 -> 0.342 ms; with K <= 512 the halved occupancy loses (K=256: +10 %),
+// hence K >= 1024.  DSGAN_PW_BM256=0 turns it off.
+static bool use_bm256(const PwArgs& g) {
+  static int e = -1;
+  if (e < 0) { const char* v = getenv("DSGAN_PW_BM256"); e = v ? atoi(v) : 1; }
+  return e && g.M >= 1024 && g.M % 256 == 0 && g.K >= 1024 && (long)(g.M / 256) * (g.N / 128) >= 512;
+}
+
 }  // namespace dsg
 
 using namespace dsg;
@@ -515,8 +526,15 @@ extern "C" int dsgan_pw_gemm(int mode, const float* A, long a_bs, const float* B
     g.a_range = (unsigned)((long)M * K * 4);
     g.b_range = (unsigned)((long)K * P * 4);
     const bool big = M > 64;
-    if (mode == PW_FWD) { if (big) pw_launch<PW_FWD, 128>(g, 1, st); else pw_launch<PW_FWD, 64>(g, 1, st); }
-    else { if (big) pw_launch<PW_DGRAD, 128>(g, 1, st); else pw_launch<PW_DGRAD, 64>(g, 1, st); }
+    if (mode == PW_FWD) {
+      if (use_bm256(g)) pw_launch<PW_FWD, 256>(g, 1, st);
+      else if (big) pw_launch<PW_FWD, 128>(g, 1, st);
+      else pw_launch<PW_FWD, 64>(g, 1, st);
+    } else {
+      if (use_bm256(g)) pw_launch<PW_DGRAD, 256>(g, 1, st);
+      else if (big) pw_launch<PW_DGRAD, 128>(g, 1, st);
+      else pw_launch<PW_DGRAD, 64>(g, 1, st);
+    }
   }
   DSG_CHECK_LAUNCH();
   return 0;
@@ -543,8 +561,16 @@ extern "C" int dsgan_pw_fwd_io(const float* W, const void* X, long x_bs, int x_b
   g.a_range = (unsigned)((long)M * K * 4);
   g.b_range = (unsigned)((long)K * P * (x_bf16 ? 2 : 4));
   const bool big = M > 64;
-  if (x_bf16) { if (big) pw_launch<PW_FWD, 128, 0, 1>(g, 1, st); else pw_launch<PW_FWD, 64, 0, 1>(g, 1, st); }
-  else { if (big) pw_launch<PW_FWD, 128>(g, 1, st); else pw_launch<PW_FWD, 64>(g, 1, st); }
+  const bool b256 = use_bm256(g);
+  if (x_bf16) {
+    if (b256) pw_launch<PW_FWD, 256, 0, 1>(g, 1, st);
+    else if (big) pw_launch<PW_FWD, 128, 0, 1>(g, 1, st);
+    else pw_launch<PW_FWD, 64, 0, 1>(g, 1, st);
+  } else {
+    if (b256) pw_launch<PW_FWD, 256>(g, 1, st);
+    else if (big) pw_launch<PW_FWD, 128>(g, 1, st);
+    else pw_launch<PW_FWD, 64>(g, 1, st);
+  }
   DSG_CHECK_LAUNCH();
   return 0;
 }
@@ -562,7 +588,9 @@ extern "C" int dsgan_pw_dgrad_gbf(const float* W, const float* DY, long dy_bs, f
   g.accumulate = accumulate; g.P = P; g.M = M; g.N = nb * P; g.K = K;
   g.a_range = (unsigned)((long)M * K * 4);
   g.b_range = (unsigned)((long)K * P * 4);
-  if (M > 64) pw_launch<PW_DGRAD, 128>(g, 1, st); else pw_launch<PW_DGRAD, 64>(g, 1, st);
+  if (use_bm256(g)) pw_launch<PW_DGRAD, 256>(g, 1, st);
+  else if (M > 64) pw_launch<PW_DGRAD, 128>(g, 1, st);
+  else pw_launch<PW_DGRAD, 64>(g, 1, st);
   DSG_CHECK_LAUNCH();
   return 0;
 }

@@ -64,9 +64,12 @@ def _q(t, prec):
     (4, 256, 31, 31, 1, 4, 1, 1),      # PatchGAN last layer shape (K-split atomics)
     (2, 3, 64, 64, 32, 1, 1, 0),       # to32 (wgrad with Cin = 3)
     (2, 6, 66, 66, 64, 4, 2, 1),       # PatchGAN layer 0 (stride-2 data-grad into 6 channels)
+    (2, 1024, 96, 96, 1024, 1, 1, 0),  # wide, deep 1x1 fwd + data-grad: 256-row M tiles (K >= 1024)
 ])
 def test_conv2d(prec, N, Cin, H, W, Cout, K, s, p):
     from dsgan_hip import functional as HF
+    if prec == "fp32" and Cin * Cout >= 256 * 1024:
+        pytest.skip("wide 1x1 shapes target the bf16 pwgemm 256-row tiles (fp32 mode runs igemm)")
     HF.set_precision(prec)
     g = torch.Generator().manual_seed(N * 1000 + Cin + Cout + K)
     x = torch.randn(N, Cin, H, W, generator=g)
@@ -119,7 +122,8 @@ def test_conv_transpose(prec, N, Ci, Co, H):
 
 @pytest.mark.parametrize("prec", ["fp32", "bf16"])
 @pytest.mark.parametrize("N,C,H,P", [(2, 3, 16, 64), (2, 64, 8, 128), (2, 128, 12, 64),
-                                     (2, 256, 16, 512)])   # unfused large block: bf16 g = gelu(z) path
+                                     (2, 256, 16, 512),    # unfused large block: bf16 g = gelu(z) path
+                                     (2, 256, 96, 1024)])  # 4C = 1024 = K of the data-grad: 256-row M tiles
 def test_pw_mlp(prec, N, C, H, P):
     """Block tail: shortcut(x) + W2 gelu(W1 h + b1) + b2 (MixConvNeXtML.py:236-242)."""
     from dsgan_hip import functional as HF
