@@ -471,6 +471,15 @@ static bool use_bm256(const PwArgs& g) {
   if (e < 0) { const char* v = getenv("DSGAN_PW_BM256"); e = v ? atoi(v) : 1; }
   return e && g.M >= 1024 && g.M % 256 == 0 && g.K >= 1024 && (long)(g.M / 256) * (g.N / 128) >= 512;
 }
+// WGRAD (M = dy channels, N = x channels, K = pixels, split over pixels): experiment switch
+// DSGAN_PW_BM256_WG=1, off by default -- measured 4-7 % slower on the step's wide weight-grads
+// (tools/gpu_pw256wg_micro.sh: 0.345 -> 0.369 ms at 1024x4096, 0.350 -> 0.364 at 512x2048):
+// the pixel-split weight-grads already stream at ~5 TB/s, and 2 waves/SIMD hide less latency.
+static bool use_bm256_wg(const PwArgs& g) {
+  static int e = -1;
+  if (e < 0) { const char* v = getenv("DSGAN_PW_BM256_WG"); e = v ? atoi(v) : 0; }
+  return e && g.M >= 1024;
+}
 
 }  // namespace dsg
 
@@ -514,9 +523,10 @@ extern "C" int dsgan_pw_gemm(int mode, const float* A, long a_bs, const float* B
     g.a_range = (unsigned)ar; g.b_range = (unsigned)br;
     DSG_REQUIRE(dsgan_pw_supported(mode, M, K, P, a_bs, b_bs, A, B), "dsgan_pw_gemm: unsupported WGRAD shape");
     g.M = M; g.N = N; g.K = nb * P;
-    const int BM = M > 64 ? 128 : 64;
+    const int BM = use_bm256_wg(g) ? 256 : M > 64 ? 128 : 64;
     const int splits = wgrad_split(g, BM);
-    if (BM == 128) pw_launch<PW_WGRAD, 128>(g, splits, st);
+    if (BM == 256) pw_launch<PW_WGRAD, 256>(g, splits, st);
+    else if (BM == 128) pw_launch<PW_WGRAD, 128>(g, splits, st);
     else pw_launch<PW_WGRAD, 64>(g, splits, st);
   } else {
     DSG_REQUIRE(dsgan_pw_supported(mode, M, K, P, a_bs, b_bs, A, B), "dsgan_pw_gemm: unsupported shape");
@@ -609,10 +619,13 @@ extern "C" int dsgan_pw_wgrad_mixed(const void* A, long a_bs, int a_bf16, const 
   DSG_REQUIRE(ar < (long)PW_OOB && br < (long)PW_OOB, "dsgan_pw_wgrad_mixed: operands exceed 4 GiB buffer range");
   g.a_range = (unsigned)ar; g.b_range = (unsigned)br;
   g.M = M; g.N = N; g.K = nb * P;
-  const int BM = M > 64 ? 128 : 64;
+  const bool b256 = !a_bf16 && use_bm256_wg(g);
+  const int BM = b256 ? 256 : M > 64 ? 128 : 64;
   const int splits = wgrad_split(g, BM);
-  const int sel = (a_bf16 ? 2 : 0) + (b_bf16 ? 1 : 0) + (BM == 128 ? 4 : 0);
+  const int sel = (a_bf16 ? 2 : 0) + (b_bf16 ? 1 : 0) + (BM == 128 ? 4 : 0) + (b256 ? 8 : 0);
   switch (sel) {
+    case 8: pw_launch<PW_WGRAD, 256, 0, 0>(g, splits, st); break;
+    case 9: pw_launch<PW_WGRAD, 256, 0, 1>(g, splits, st); break;
     case 0: pw_launch<PW_WGRAD, 64, 0, 0>(g, splits, st); break;
     case 1: pw_launch<PW_WGRAD, 64, 0, 1>(g, splits, st); break;
     case 2: pw_launch<PW_WGRAD, 64, 1, 0>(g, splits, st); break;
