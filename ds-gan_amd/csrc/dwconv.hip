@@ -338,9 +338,7 @@ __global__ __launch_bounds__(256, 4) void dwconv_wgrad_v2(const float* __restric
 
 // tile configuration by plane width: 0 = generic kernel
 static int dw_cfg(int H, int W) {
-  static int generic = -1;   // DSGAN_DW_GENERIC=1 forces the generic kernels (A/B checks)
-  if (generic < 0) { const char* e = getenv("DSGAN_DW_GENERIC"); generic = (e && *e == '1') ? 1 : 0; }
-  if (generic || (W & 3) || H < 8) return 0;
+  if ((W & 3) || H < 8) return 0;
   // (built with -fno-slp-vectorize: packed-f32 FMAs would need even-aligned register pairs of
   // the shifted input window and spill)
   if (W % 128 == 0) return 1;   // 128 x 64 tile, 4x8 per thread

@@ -50,7 +50,6 @@ struct GemmArgs {
   const float* gpre; long gpre_bs; int gact;
   int act; float slope; int accumulate;
   int bact;                     // FWD/WGRAD: apply act code to the B operand on load (gelu(z))
-  int dbg;                      // experiment switches (DSGAN_IGEMM_DBG): 1 skip stores, 2 skip loads
   // DGRAD2 parity class
   int ph, pw, kh0, kw0, nth, ntw, Hc, Wc;
 };
@@ -331,17 +330,6 @@ __global__ __launch_bounds__(256) void igemm_kernel(GemmArgs g) {
   float ra[A_ITEMS][CH], rbv[B_ITEMS][CH];
   auto gload = [&](int kt) {
     const int kb = kbeg + kt * BK;
-    if (g.dbg & 2) {
-#pragma unroll
-      for (int i = 0; i < A_ITEMS; ++i)
-#pragma unroll
-        for (int j = 0; j < CH; ++j) ra[i][j] = (float)(kt + j);
-#pragma unroll
-      for (int i = 0; i < B_ITEMS; ++i)
-#pragma unroll
-        for (int j = 0; j < CH; ++j) rbv[i][j] = (float)(kt - j);
-      return;
-    }
 #pragma unroll
     for (int i = 0; i < A_ITEMS; ++i)
       if (a_on[i]) {
@@ -522,13 +510,6 @@ __global__ __launch_bounds__(256) void igemm_kernel(GemmArgs g) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) v[r] += o[r];
       }
-      if (g.dbg & 1) {
-        float t = 0.f;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) t += v[r];
-        if (t == 12345.678f) yb[0] = t;
-        continue;
-      }
 #pragma unroll
       for (int r = 0; r < 16; ++r) if (ok[r]) yb[off[r]] = v[r];
     }
@@ -567,16 +548,9 @@ static void launch_mode(const GemmArgs& g, int prec, int splits, hipStream_t st)
 
 using namespace dsg;
 
-static int dbg_flags() {
-  static int f = -1;
-  if (f < 0) { const char* e = getenv("DSGAN_IGEMM_DBG"); f = e ? atoi(e) : 0; }
-  return f;
-}
-
 static GemmArgs base_args(int N, int Cin, int H, int W, int Cout, int KH, int KW, int stride,
                           int pad, int Ho, int Wo) {
   GemmArgs g{};
-  g.dbg = dbg_flags();
   g.N = N; g.Cin = Cin; g.H = H; g.W = W; g.Cout = Cout; g.KH = KH; g.KW = KW;
   g.stride = stride; g.pad = pad; g.Ho = Ho; g.Wo = Wo;
   g.slope = 0.2f;

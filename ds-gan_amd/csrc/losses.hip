@@ -165,7 +165,9 @@ struct SSIMArgs {
   const float* win;   // 11 taps
   float C1, C2;
   float* coef;        // [3][planes][Ho][Wo]
-  float* out;         // sum of S
+  float* out;         // sum of S (nullable: coefficient maps only)
+  const float* kscale;  // per-plane factor of the coefficient maps (nullable = 1)
+  int cs_mode;          // coefficient maps of the contrast-structure term cs instead of S (MS-SSIM)
 };
 
 __global__ __launch_bounds__(256) void ssim_fwd_kernel(SSIMArgs s, int tiles_w) {
@@ -221,12 +223,22 @@ __global__ __launch_bounds__(256) void ssim_fwd_kernel(SSIMArgs s, int tiles_w) 
     ssum += S;
     const long o = (long)plane * plane_out + (long)oh * Wo + ow;
     const long stride = (long)s.planes * plane_out;
-    s.coef[o] = S * (2.f * mu1 / A1 - 2.f * mu1 / A2 - 2.f * mu2 / B1 + 2.f * mu2 / B2);
-    s.coef[o + stride] = -S / B2;
-    s.coef[o + 2 * stride] = 2.f * S / A2;
+    if (s.cs_mode) {   // d cs: cs = (2 s12 + C2) / (s11 + s22 + C2)
+      const float k = s.kscale[plane];
+      s.coef[o] = k * ((2.f * mu2 * cs - 2.f * mu1) / B2);
+      s.coef[o + stride] = k * (-cs / B2);
+      s.coef[o + 2 * stride] = k * (2.f / B2);
+    } else {
+      const float k = s.kscale ? s.kscale[plane] : 1.f;
+      s.coef[o] = k * (S * (2.f * mu1 / A1 - 2.f * mu1 / A2 - 2.f * mu2 / B1 + 2.f * mu2 / B2));
+      s.coef[o + stride] = k * (-S / B2);
+      s.coef[o + 2 * stride] = k * (2.f * S / A2);
+    }
   }
-  ssum = block_sum<256>(ssum, sh);
-  if (threadIdx.x == 0) atomicAdd(s.out, ssum);
+  if (s.out) {
+    ssum = block_sum<256>(ssum, sh);
+    if (threadIdx.x == 0) atomicAdd(s.out, ssum);
+  }
 }
 
 // ---- train.py per-iteration metrics (DSGAN/train.py:27-44, 110-124) ----------------------------
@@ -388,6 +400,46 @@ __global__ __launch_bounds__(256) void ms_ssim_combine_kernel(const float* stats
   if (threadIdx.x == 0) out[N] = tot / (float)N;
 }
 
+// ---- MS-SSIM as a loss (backward of DSGAN/MS_SSIM.py:153-225 through its 5-level pyramid) ----
+// Per plane p and level l the forward keeps the map sums (ssim_eval_kernel).  The loss is
+// mean_p prod_l V_l^w_l with V_l = relu(mean cs_l) (l < L-1), relu(mean S_{L-1}); so
+//   dL/d(map_l pixel) = gout/P * w_l * prod / V_l / count_l     (0 where the relu clips)
+// = kscale[l][p]; the coefficient maps of level l are scaled by it and adjoint-filtered into
+// dY_l, which also receives 1/4 of dY_{l+1} through the padded 2x2 average pool.
+__global__ void ms_ssim_kscale_kernel(const float* stats, int levels, int planes, MsArgs m, const float* gout,
+                                      float inv_planes, float* kscale) {
+  for (int p = blockIdx.x * 256 + threadIdx.x; p < planes; p += gridDim.x * 256) {
+    float v[8], pw[8];
+    float prod = 1.f;
+    for (int l = 0; l < levels; ++l) {
+      const float* st = stats + ((long)l * planes + p) * 2;
+      v[l] = (l < levels - 1 ? st[1] : st[0]) * m.inv_cnt[l];
+      pw[l] = powf(fmaxf(v[l], 0.f), m.wt[l]);
+      prod *= pw[l];
+    }
+    const float g = gout[0] * inv_planes;
+    for (int l = 0; l < levels; ++l) {
+      float others = 1.f;
+      for (int k = 0; k < levels; ++k)
+        if (k != l) others *= pw[k];
+      // d V^w / dV = w V^(w-1), only where relu passes
+      const float d = v[l] > 0.f ? m.wt[l] * powf(v[l], m.wt[l] - 1.f) * others : 0.f;
+      kscale[(long)l * planes + p] = g * d * m.inv_cnt[l];
+    }
+  }
+}
+
+// dy[p][h][w] = scale * dup[p][(h+ph)/2][(w+pw)/2]  (adjoint of the count_include_pad 2x2 pool)
+__global__ void avgpool2_pad_bwd_kernel(const float* __restrict__ dup, float* __restrict__ dy, int planes, int H,
+                                        int W, int Ho, int Wo, int ph, int pw, float scale) {
+  const long total = (long)planes * H * W;
+  for (long t = blockIdx.x * 256L + threadIdx.x; t < total; t += (long)gridDim.x * 256) {
+    const int p = (int)(t / ((long)H * W));
+    const int r = (int)(t - (long)p * H * W), h = r / W, w = r - h * W;
+    dy[t] = scale * dup[((long)p * Ho + (h + ph) / 2) * Wo + (w + pw) / 2];
+  }
+}
+
 // dfake[h,w] = g * a * ( G^T c_mu + 2Y G^T c_yy + X G^T c_xy )  over input tile 32x32
 __global__ __launch_bounds__(256) void ssim_bwd_kernel(SSIMArgs s, const float* gout, float gcoef,
                                                        float* dfake, int tiles_w, int accumulate) {
@@ -423,7 +475,7 @@ __global__ __launch_bounds__(256) void ssim_bwd_kernel(SSIMArgs s, const float* 
     vb[0][c][r] = a0; vb[1][c][r] = a1; vb[2][c][r] = a2;
   }
   __syncthreads();
-  const float g = gout[0] * gcoef * s.a;
+  const float g = (gout ? gout[0] : 1.f) * gcoef * s.a;
   const float* rp = s.real + (long)plane * s.H * s.W;
   const float* fp = s.fake + (long)plane * s.H * s.W;
   float* dp = dfake + (long)plane * s.H * s.W;
@@ -566,7 +618,7 @@ int dsgan_ms_ssim(const float* real, const float* fake, float a, float b, int N,
   int h = H, w = W;
   for (int l = 0; l < levels; ++l) {
     const int Ho = h - SS_K + 1, Wo = w - SS_K + 1;
-    SSIMArgs s{xr, yr, ca, cb, planes, h, w, win11, C1, C2, nullptr, nullptr};
+    SSIMArgs s{xr, yr, ca, cb, planes, h, w, win11, C1, C2, nullptr, nullptr, nullptr, 0};
     const int tw = cdiv(Wo, SS_T), th = cdiv(Ho, SS_T);
     hipLaunchKernelGGL(ssim_eval_kernel, dim3(tw * th, planes), dim3(256), 0, st, s, tw, stats + (long)l * planes * 2);
     m.inv_cnt[l] = 1.f / ((float)Ho * (float)Wo);
@@ -588,12 +640,141 @@ int dsgan_ms_ssim(const float* real, const float* fake, float a, float b, int N,
   return 0;
 }
 
+// ---- MS-SSIM loss (forward keeping the pyramid, backward) ------------------------------------
+// work layout (floats): X_1, Y_1, X_2, Y_2, ... X_{L-1}, Y_{L-1} (each planes*h_l*w_l), then two
+// dY ping-pong buffers of level-1 size, then the kscale table [L][planes], then the coefficient
+// maps [3][planes][Ho_0][Wo_0].
+static void ms_dims(int H, int W, int levels, int* hs, int* ws) {
+  hs[0] = H; ws[0] = W;
+  for (int l = 1; l < levels; ++l) { hs[l] = ms_half(hs[l - 1]); ws[l] = ms_half(ws[l - 1]); }
+}
+long dsgan_ms_ssim_train_workspace(int N, int C, int H, int W, int levels) {
+  if (levels < 1 || levels > 8) return -1;
+  int hs[8], ws[8];
+  ms_dims(H, W, levels, hs, ws);
+  const long p = (long)N * C;
+  long n = 0;
+  for (int l = 1; l < levels; ++l) n += 2 * p * hs[l] * ws[l];
+  if (levels > 1) n += 2 * p * hs[1] * ws[1];
+  n += (long)levels * p;
+  n += 3 * p * (long)(H - SS_K + 1) * (W - SS_K + 1);
+  return n;
+}
+
+static MsArgs ms_args(int levels, const int* hs, const int* ws, const float* weights_host) {
+  MsArgs m{};
+  for (int l = 0; l < levels; ++l) {
+    m.inv_cnt[l] = 1.f / ((float)(hs[l] - SS_K + 1) * (float)(ws[l] - SS_K + 1));
+    m.wt[l] = weights_host[l];
+  }
+  return m;
+}
+
+// Same value as dsgan_ms_ssim (out[N] = batch mean, out[n] per image), keeping every pyramid
+// level in `work` for dsgan_ms_ssim_bwd.  stats: [levels][planes][2] map sums.
+int dsgan_ms_ssim_fwd_train(const float* real, const float* fake, float a, float b, int N, int C, int H, int W,
+                            const float* win11, float C1, float C2, const float* weights_host, int levels, float* work,
+                            float* stats, float* out, hipStream_t st) {
+  DSG_REQUIRE(real && fake && win11 && weights_host && work && stats && out && N > 0 && C > 0 && levels >= 1 &&
+                  levels <= 8 && N * C <= 65535,
+              "dsgan_ms_ssim_fwd_train: bad args");
+  DSG_REQUIRE(((H < W ? H : W) > (SS_K - 1) * (1 << (levels - 1))),
+              "dsgan_ms_ssim_fwd_train: image smaller than the (win_size-1)*2^(levels-1) ms-ssim minimum");
+  const int planes = N * C;
+  int hs[8], ws[8];
+  ms_dims(H, W, levels, hs, ws);
+  hipMemsetAsync(stats, 0, sizeof(float) * 2 * planes * levels, st);
+  const float* xr = real;
+  const float* yr = fake;
+  float ca = a, cb = b;
+  float* lvl = work;
+  for (int l = 0; l < levels; ++l) {
+    const int h = hs[l], w = ws[l];
+    const int Ho = h - SS_K + 1, Wo = w - SS_K + 1;
+    SSIMArgs s{xr, yr, ca, cb, planes, h, w, win11, C1, C2, nullptr, nullptr, nullptr, 0};
+    const int tw = cdiv(Wo, SS_T), th = cdiv(Ho, SS_T);
+    hipLaunchKernelGGL(ssim_eval_kernel, dim3(tw * th, planes), dim3(256), 0, st, s, tw, stats + (long)l * planes * 2);
+    if (l < levels - 1) {
+      const int h2 = hs[l + 1], w2 = ws[l + 1];
+      const long n2 = (long)planes * h2 * w2;
+      float* nx = lvl;
+      float* ny = lvl + n2;
+      hipLaunchKernelGGL(avgpool2_pad_kernel, dim3(red_grid(n2)), dim3(256), 0, st, xr, nx, planes, h, w, h2, w2,
+                         h % 2, w % 2, ca, cb);
+      hipLaunchKernelGGL(avgpool2_pad_kernel, dim3(red_grid(n2)), dim3(256), 0, st, yr, ny, planes, h, w, h2, w2,
+                         h % 2, w % 2, ca, cb);
+      xr = nx; yr = ny; ca = 1.f; cb = 0.f;
+      lvl += 2 * n2;
+    }
+  }
+  hipLaunchKernelGGL(ms_ssim_combine_kernel, dim3(1), dim3(256), 0, st, stats, levels, N, C,
+                     ms_args(levels, hs, ws, weights_host), out);
+  DSG_CHECK_LAUNCH();
+  return 0;
+}
+
+// dfake (+)= d(gout[0] * batch-mean MS-SSIM)/d(fake); work/stats as left by dsgan_ms_ssim_fwd_train.
+int dsgan_ms_ssim_bwd(const float* real, const float* fake, float a, float b, int N, int C, int H, int W,
+                      const float* win11, float C1, float C2, const float* weights_host, int levels, float* work,
+                      const float* stats, const float* gout, float* dfake, int accumulate, hipStream_t st) {
+  DSG_REQUIRE(real && fake && win11 && weights_host && work && stats && gout && dfake && N > 0 && C > 0 &&
+                  levels >= 1 && levels <= 8 && N * C <= 65535,
+              "dsgan_ms_ssim_bwd: bad args");
+  DSG_REQUIRE(!accumulate || levels == 1, "dsgan_ms_ssim_bwd: accumulate needs levels == 1 (dfake is staged)");
+  const int planes = N * C;
+  int hs[8], ws[8];
+  ms_dims(H, W, levels, hs, ws);
+  const float* xs[8];
+  const float* ys[8];
+  xs[0] = real; ys[0] = fake;
+  float* lvl = work;
+  for (int l = 1; l < levels; ++l) {
+    const long n = (long)planes * hs[l] * ws[l];
+    xs[l] = lvl; ys[l] = lvl + n;
+    lvl += 2 * n;
+  }
+  float* dbuf[2] = {lvl, levels > 1 ? lvl + (long)planes * hs[1] * ws[1] : lvl};
+  if (levels > 1) lvl += 2L * planes * hs[1] * ws[1];
+  float* kscale = lvl;
+  lvl += (long)levels * planes;
+  float* coef = lvl;
+  const MsArgs m = ms_args(levels, hs, ws, weights_host);
+  hipLaunchKernelGGL(ms_ssim_kscale_kernel, dim3(cdiv(planes, 256)), dim3(256), 0, st, stats, levels, planes, m, gout,
+                     1.f / (float)planes, kscale);
+  const float* dup = nullptr;
+  for (int l = levels - 1; l >= 0; --l) {
+    const int h = hs[l], w = ws[l];
+    const int Ho = h - SS_K + 1, Wo = w - SS_K + 1;
+    float* dy = l == 0 ? dfake : dbuf[l & 1];
+    const float sa = l == 0 ? a : 1.f, sb = l == 0 ? b : 0.f;
+    int acc = 0;
+    if (dup) {   // 1/4 of the level above through the padded pool (times a at the image level)
+      const long n = (long)planes * h * w;
+      hipLaunchKernelGGL(avgpool2_pad_bwd_kernel, dim3(red_grid(n)), dim3(256), 0, st, dup, dy, planes, h, w, hs[l + 1],
+                         ws[l + 1], h % 2, w % 2, 0.25f * sa);
+      acc = 1;
+    } else {
+      acc = l == 0 ? accumulate : 0;
+    }
+    SSIMArgs s{xs[l], ys[l], sa, sb, planes, h, w, win11, C1, C2, coef, nullptr, kscale + (long)l * planes,
+               l < levels - 1 ? 1 : 0};
+    const int tw = cdiv(Wo, SS_T), th = cdiv(Ho, SS_T);
+    hipLaunchKernelGGL(ssim_fwd_kernel, dim3(tw * th, planes), dim3(256), 0, st, s, tw);
+    const int tw2 = cdiv(w, SS_T), th2 = cdiv(h, SS_T);
+    hipLaunchKernelGGL(ssim_bwd_kernel, dim3(tw2 * th2, planes), dim3(256), 0, st, s, (const float*)nullptr, 1.f, dy,
+                       tw2, acc);
+    dup = dy;
+  }
+  DSG_CHECK_LAUNCH();
+  return 0;
+}
+
 // out = sum of the SSIM map (caller divides by planes*Ho*Wo); coef: [3][planes][Ho][Wo] scratch
 int dsgan_ssim_fwd(const float* real, const float* fake, float a, float b, int planes, int H, int W,
                    const float* win11, float C1, float C2, float* coef, float* out, hipStream_t st) {
   DSG_REQUIRE(real && fake && win11 && coef && out && H >= SS_K && W >= SS_K && planes > 0 && planes <= 65535,
               "dsgan_ssim_fwd: bad args (H,W >= 11 required)");
-  SSIMArgs s{real, fake, a, b, planes, H, W, win11, C1, C2, coef, out};
+  SSIMArgs s{real, fake, a, b, planes, H, W, win11, C1, C2, coef, out, nullptr, 0};
   const int Ho = H - SS_K + 1, Wo = W - SS_K + 1;
   const int tw = cdiv(Wo, SS_T), th = cdiv(Ho, SS_T);
   hipMemsetAsync(out, 0, sizeof(float), st);
@@ -607,7 +788,7 @@ int dsgan_ssim_bwd(const float* real, const float* fake, float a, float b, int p
                    const float* win11, const float* coef, const float* gout, float gcoef,
                    float* dfake, int accumulate, hipStream_t st) {
   DSG_REQUIRE(real && fake && win11 && coef && gout && dfake, "dsgan_ssim_bwd: bad args");
-  SSIMArgs s{real, fake, a, b, planes, H, W, win11, 0.f, 0.f, const_cast<float*>(coef), nullptr};
+  SSIMArgs s{real, fake, a, b, planes, H, W, win11, 0.f, 0.f, const_cast<float*>(coef), nullptr, nullptr, 0};
   const int tw = cdiv(W, SS_T), th = cdiv(H, SS_T);
   hipLaunchKernelGGL(ssim_bwd_kernel, dim3(tw * th, planes), dim3(256), 0, st, s, gout, gcoef, dfake, tw, accumulate);
   DSG_CHECK_LAUNCH();

@@ -292,12 +292,9 @@ int dsgan_pconv(const float* X, long x_bs, const void* Wb, const float* bias, fl
   g.gpre = gpre; g.gpre_bs = gpre_bs; g.nb = nb; g.K = K; g.M = M; g.H = H; g.W = W; g.Ho = Ho;
   g.Wo = Wo; g.pad = pad; g.act = act; g.gact = gact; g.slope = slope; g.accumulate = accumulate;
   // BM = 256 for the wide layers (VGG conv3/conv4, 256/512 output channels): per tap twice the
-  // MFMAs between barriers and half the patch traffic per MAC (DSGAN_PC_BM256=0 disables)
-  static int bm256 = -1;
-  if (bm256 < 0) { const char* e = getenv("DSGAN_PC_BM256"); bm256 = e ? atoi(e) : 1; }
-  // ... only while the launch still has >= 2 workgroups per CU (at 32x32 it would have one)
+  // MFMAs between barriers and half the patch traffic per MAC, only while the launch still has >= 2 workgroups per CU (at 32x32 it would have one)
   const long ptiles = (long)nb * ((Ho + 7) / 8) * ((Wo + 15) / 16);
-  const bool use256 = bm256 && M >= 256 && ptiles * ((M + 255) / 256) >= 512;
+  const bool use256 = M >= 256 && ptiles * ((M + 255) / 256) >= 512;
   const int rc = use256 ? pc_dispatch<256>(g, KH, stride, st)
                  : M > 64            ? pc_dispatch<128>(g, KH, stride, st)
                                      : pc_dispatch<64>(g, KH, stride, st);

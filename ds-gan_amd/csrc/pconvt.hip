@@ -33,7 +33,6 @@ struct PtArgs {
   int tiles_w, tiles_h;
   int gact; float slope;
   int accumulate;
-  int dbg;                            // development only: 1 skip stores, 2 skip weight loads, 4 skip patch loads
 };
 
 constexpr int PT_STR = 40;            // bf16 per staged pixel / weight row (32 + 8)
@@ -117,7 +116,7 @@ __global__ __launch_bounds__(256, BM == 32 ? 4 : 2) void pconvt_kernel(PtArgs g)
       const int it = tid + i * 256;
       const int c8 = it & 3, row = (it >> 2) % BM, tap = (it >> 2) / BM;
       const int m = t.m0 + row;
-      ra[i] = (it < A_ITEMS && m < g.M && !(g.dbg & 2))
+      ra[i] = (it < A_ITEMS && m < g.M)
                   ? *reinterpret_cast<const tu32x4*>(g.Wb + ((long)tap * g.M + m) * g.K + k0 + c8 * 8)
                   : tu32x4{0u, 0u, 0u, 0u};
     }
@@ -128,7 +127,7 @@ __global__ __launch_bounds__(256, BM == 32 ? 4 : 2) void pconvt_kernel(PtArgs g)
       const int cg = it / PPIX, pix = it - cg * PPIX;
       const int pr = pix / PW, pc = pix - pr * PW;
       const int ih = t.i0 + DMIN + pr, iw = t.j0 + DMIN + pc;
-      const bool in = it < P_ITEMS && (unsigned)ih < (unsigned)g.Hi && (unsigned)iw < (unsigned)g.Wi && !(g.dbg & 4);
+      const bool in = it < P_ITEMS && (unsigned)ih < (unsigned)g.Hi && (unsigned)iw < (unsigned)g.Wi;
       const float* src = xb + (long)(k0 + (in ? cg : 0) * 8) * HWi + (in ? ih * g.Wi + iw : 0);
 #pragma unroll
       for (int e = 0; e < 8; ++e) rp[i][e] = in ? src[(long)e * HWi] : 0.f;
@@ -223,10 +222,6 @@ __global__ __launch_bounds__(256, BM == 32 ? 4 : 2) void pconvt_kernel(PtArgs g)
         for (int r = 0; r < 16; ++r) {
           const int m = cur.m0 + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
           if (!rowok || m >= g.M || ow >= g.Wo) continue;
-          if (g.dbg & 1) {
-            if (acc[ph * 2][j][r] == 1234.5f) yb[0] = 1.f;
-            continue;
-          }
           const float bv = g.bias ? g.bias[m] : 0.f;
           float v0 = acc[ph * 2][j][r] + bv, v1 = acc[ph * 2 + 1][j][r] + bv;
           const long o = (long)m * HWo + (long)oh * g.Wo + ow;
@@ -287,13 +282,7 @@ int dsgan_pconvt(const float* X, long x_bs, const void* Wb, const float* bias, f
   g.X = X; g.x_bs = x_bs; g.Wb = (const __bf16*)Wb; g.Y = Y; g.y_bs = y_bs; g.bias = bias;
   g.gpre = gpre; g.gpre_bs = gpre_bs; g.nb = nb; g.K = K; g.M = M; g.Hi = Hi; g.Wi = Wi; g.Ho = Ho; g.Wo = Wo;
   g.pad = pad; g.gact = gact; g.slope = slope; g.accumulate = accumulate;
-  static int dbg = -1;
-  if (dbg < 0) { const char* e = getenv("DSGAN_PT_DBG"); dbg = e ? atoi(e) : 0; }
-  g.dbg = dbg;
-  static int bm = -1;
-  if (bm < 0) { const char* e = getenv("DSGAN_PT_BM"); bm = e ? atoi(e) : 64; }
-  if (KS == 3 && bm == 64) pt_launch<64, 3, false>(g, st);
-  else if (KS == 3) pt_launch<64, 3, true>(g, st);
+  if (KS == 3) pt_launch<64, 3, false>(g, st);
   else pt_launch<32, 4, false>(g, st);
   DSG_CHECK_LAUNCH();
   return 0;

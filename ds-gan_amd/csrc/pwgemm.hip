@@ -41,7 +41,6 @@ struct PwArgs {
   int act, gact, bact, accumulate; float slope;
   int k_split;
   unsigned a_range, b_range;   // buffer-resource byte ranges of A and B (B: per image for FWD/DGRAD)
-  int dbg;   // DSGAN_PW_DBG experiment switches: 1 skip epilogue stores, 2 skip global loads
   int y_bf16;  // FWD: Y is bf16 [b][M][P] (y_bs in elements)
   int gbf;     // FWD: ypre is bf16 and receives act'(pre);  DGRAD: gpre is a bf16 multiplier (no act')
 };
@@ -144,13 +143,6 @@ __global__ __launch_bounds__(256, 2) void pwgemm_kernel(PwArgs g) {
 
   auto gload = [&](int kt) {
     const int kb = kbeg + kt * PBK;
-    if (g.dbg & 2) {
-#pragma unroll
-      for (int i = 0; i < A_ITEMS; ++i) ra[i] = make_float4(kt, 1.f, 2.f, 3.f);
-#pragma unroll
-      for (int i = 0; i < B_ITEMS; ++i) rb[i] = make_float4(1.f, kt, 2.f, 3.f);
-      return;
-    }
     // WGRAD: a 32-pixel K step lies inside one image (P % 32 == 0): image index is uniform
     const unsigned bw = (MODE == PW_WGRAD) ? (unsigned)(kb / g.P) : 0u;
     const unsigned pw = (MODE == PW_WGRAD) ? (unsigned)(kb - (int)bw * g.P) : 0u;
@@ -414,13 +406,6 @@ __global__ __launch_bounds__(256, 2) void pwgemm_kernel(PwArgs g) {
           v[r] += __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
                       ry, vrow[r], (mrow + (r & 3) + 8 * (r >> 2)) * P4, 0));
       }
-      if (g.dbg & 1) {
-        float t = 0.f;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) t += v[r];
-        if (t == 1234.5678f) g.Y[0] = t;
-        continue;
-      }
       if (g.y_bf16) {   // bf16 output: same rows, half the byte offsets
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
@@ -465,20 +450,10 @@ static bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 // MFMAs, as long as the grid still keeps >= 2 workgroups per CU.  Isolated A/B at the step's
 // shapes (tools/gpu_pw256_micro.sh, B=16): K=4096 dgrad into 1024 ch 0.356 -> 0.264 ms, K=1024
 // fwd to 4096 ch 0.380 -> 0.342 ms; with K <= 512 the halved occupancy loses (K=256: +10 %),
-// hence K >= 1024.  DSGAN_PW_BM256=0 turns it off.
+// hence K >= 1024.  (WGRAD keeps 128-row tiles: 256 rows measured 4-7 % slower on the step's
+// wide weight-grads, tools/gpu_pw256wg_micro.sh -- they already stream at ~5 TB/s.)
 static bool use_bm256(const PwArgs& g) {
-  static int e = -1;
-  if (e < 0) { const char* v = getenv("DSGAN_PW_BM256"); e = v ? atoi(v) : 1; }
-  return e && g.M >= 1024 && g.M % 256 == 0 && g.K >= 1024 && (long)(g.M / 256) * (g.N / 128) >= 512;
-}
-// WGRAD (M = dy channels, N = x channels, K = pixels, split over pixels): experiment switch
-// DSGAN_PW_BM256_WG=1, off by default -- measured 4-7 % slower on the step's wide weight-grads
-// (tools/gpu_pw256wg_micro.sh: 0.345 -> 0.369 ms at 1024x4096, 0.350 -> 0.364 at 512x2048):
-// the pixel-split weight-grads already stream at ~5 TB/s, and 2 waves/SIMD hide less latency.
-static bool use_bm256_wg(const PwArgs& g) {
-  static int e = -1;
-  if (e < 0) { const char* v = getenv("DSGAN_PW_BM256_WG"); e = v ? atoi(v) : 0; }
-  return e && g.M >= 1024;
+  return g.M >= 1024 && g.M % 256 == 0 && g.K >= 1024 && (long)(g.M / 256) * (g.N / 128) >= 512;
 }
 
 }  // namespace dsg
@@ -507,11 +482,6 @@ extern "C" int dsgan_pw_gemm(int mode, const float* A, long a_bs, const float* B
                              hipStream_t st) {
   DSG_REQUIRE(A && B && Y && M > 0 && N > 0 && K > 0 && P > 0 && nb > 0, "dsgan_pw_gemm: bad args");
   PwArgs g{};
-  {
-    static int dbg = -1;
-    if (dbg < 0) { const char* e = getenv("DSGAN_PW_DBG"); dbg = e ? atoi(e) : 0; }
-    g.dbg = dbg;
-  }
   g.A = A; g.a_bs = a_bs; g.B = B; g.b_bs = b_bs; g.Y = Y; g.y_bs = y_bs; g.bias = bias;
   g.ypre = ypre; g.ypre_bs = ypre_bs; g.gpre = gpre; g.gpre_bs = gpre_bs;
   g.act = act; g.gact = gact; g.bact = bact; g.accumulate = accumulate; g.slope = slope;
@@ -523,10 +493,9 @@ extern "C" int dsgan_pw_gemm(int mode, const float* A, long a_bs, const float* B
     g.a_range = (unsigned)ar; g.b_range = (unsigned)br;
     DSG_REQUIRE(dsgan_pw_supported(mode, M, K, P, a_bs, b_bs, A, B), "dsgan_pw_gemm: unsupported WGRAD shape");
     g.M = M; g.N = N; g.K = nb * P;
-    const int BM = use_bm256_wg(g) ? 256 : M > 64 ? 128 : 64;
+    const int BM = M > 64 ? 128 : 64;
     const int splits = wgrad_split(g, BM);
-    if (BM == 256) pw_launch<PW_WGRAD, 256>(g, splits, st);
-    else if (BM == 128) pw_launch<PW_WGRAD, 128>(g, splits, st);
+    if (BM == 128) pw_launch<PW_WGRAD, 128>(g, splits, st);
     else pw_launch<PW_WGRAD, 64>(g, splits, st);
   } else {
     DSG_REQUIRE(dsgan_pw_supported(mode, M, K, P, a_bs, b_bs, A, B), "dsgan_pw_gemm: unsupported shape");
@@ -619,13 +588,10 @@ extern "C" int dsgan_pw_wgrad_mixed(const void* A, long a_bs, int a_bf16, const 
   DSG_REQUIRE(ar < (long)PW_OOB && br < (long)PW_OOB, "dsgan_pw_wgrad_mixed: operands exceed 4 GiB buffer range");
   g.a_range = (unsigned)ar; g.b_range = (unsigned)br;
   g.M = M; g.N = N; g.K = nb * P;
-  const bool b256 = !a_bf16 && use_bm256_wg(g);
-  const int BM = b256 ? 256 : M > 64 ? 128 : 64;
+  const int BM = M > 64 ? 128 : 64;
   const int splits = wgrad_split(g, BM);
-  const int sel = (a_bf16 ? 2 : 0) + (b_bf16 ? 1 : 0) + (BM == 128 ? 4 : 0) + (b256 ? 8 : 0);
+  const int sel = (a_bf16 ? 2 : 0) + (b_bf16 ? 1 : 0) + (BM == 128 ? 4 : 0);
   switch (sel) {
-    case 8: pw_launch<PW_WGRAD, 256, 0, 0>(g, splits, st); break;
-    case 9: pw_launch<PW_WGRAD, 256, 0, 1>(g, splits, st); break;
     case 0: pw_launch<PW_WGRAD, 64, 0, 0>(g, splits, st); break;
     case 1: pw_launch<PW_WGRAD, 64, 0, 1>(g, splits, st); break;
     case 2: pw_launch<PW_WGRAD, 64, 1, 0>(g, splits, st); break;

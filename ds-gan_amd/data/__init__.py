@@ -1,7 +1,20 @@
 """Data loading (DSGAN/data/__init__.py:5-60): ``CreateDataLoader(opt, isTrain)`` ->
 ``load_data()`` iterable of ``{'A', 'B', 'A_paths', 'B_paths'}`` batches, A/B float32 NCHW in
-[-1, 1] already on the GPU (set_input's ``.to(device)`` is then a no-op)."""
+[-1, 1] already on the GPU (set_input's ``.to(device)`` is then a no-op).
+
+Multi-GPU (one process per GPU under torchrun): ``--batchSize`` keeps the reference's meaning,
+the GLOBAL batch that ``nn.DataParallel`` scatters over the GPUs (DSGAN/models/networks.py:74-77,
+``Tensor.chunk`` along dim 0).  Every rank walks the same epoch permutation (same seed, same RNG
+draws as the 1-GPU loader) and takes its chunk of each global batch (``RankBatchSampler``), so
+the sequence of global batches equals the single-process run's.  Each batch dict also carries
+``global_batch`` (the size of the global batch it is a chunk of) for the loss weighting of
+ragged last batches (Pix2PixModel.set_input).
+"""
+import collections
+import math
+
 import torch
+import torch.distributed as dist
 
 from dsgan_hip._lib import call, ptr, stream
 
@@ -17,11 +30,62 @@ def to_images(u8, flip, gray=False):
     return out
 
 
+def _dist():
+    if dist.is_available() and dist.is_initialized():
+        return dist.get_rank(), dist.get_world_size()
+    return 0, 1
+
+
+class RankBatchSampler:
+    """Global batches of ``sampler`` (batch_size each, the last one ragged), of which this rank
+    yields its ``Tensor.chunk`` slice: chunk = ceil(n / world), rank r gets [r*chunk, (r+1)*chunk).
+    A global batch that would leave some rank empty (n <= (world-1)*chunk) is skipped on every
+    rank (the collectives of a step need all ranks).  ``sizes`` queues the global size of each
+    yielded chunk, in order."""
+
+    def __init__(self, sampler, batch_size, rank, world):
+        self.sampler, self.batch_size, self.rank, self.world = sampler, batch_size, rank, world
+        self.sizes = collections.deque()
+
+    def _chunk(self, buf):
+        n = len(buf)
+        c = math.ceil(n / self.world)
+        if n <= (self.world - 1) * c:
+            return None
+        return buf[self.rank * c:(self.rank + 1) * c]
+
+    def __iter__(self):
+        self.sizes.clear()
+        buf = []
+        for idx in self.sampler:
+            buf.append(idx)
+            if len(buf) == self.batch_size:
+                mine = self._chunk(buf)
+                if mine is not None:
+                    self.sizes.append(len(buf))
+                    yield mine
+                buf = []
+        if buf:
+            mine = self._chunk(buf)
+            if mine is not None:
+                self.sizes.append(len(buf))
+                yield mine
+
+    def __len__(self):
+        n = len(self.sampler)
+        full, tail = divmod(n, self.batch_size)
+        return full + (1 if tail and tail > (self.world - 1) * math.ceil(tail / self.world) else 0)
+
+
 def CreateDataset(opt):
-    if opt.dataset_mode != "aligned":
+    if opt.dataset_mode == "aligned":
+        from data.aligned_dataset import AlignedDataset
+        dataset = AlignedDataset()
+    elif opt.dataset_mode == "single":
+        from data.single_dataset import SingleDataset
+        dataset = SingleDataset()
+    else:
         raise ValueError("Dataset [%s] not recognized." % opt.dataset_mode)
-    from data.aligned_dataset import AlignedDataset
-    dataset = AlignedDataset()
     print("dataset [%s] was created" % dataset.name())
     dataset.initialize(opt)
     return dataset
@@ -34,10 +98,21 @@ class CustomDatasetDataLoader:
     def initialize(self, opt, isTrain):
         self.opt = opt
         self.dataset = CreateDataset(opt)
-        self.dataloader = torch.utils.data.DataLoader(
-            self.dataset, batch_size=opt.batchSize,
-            shuffle=(not opt.serial_batches) if isTrain == "train" else False,
-            num_workers=int(opt.nThreads), pin_memory=True)
+        shuffle = (not opt.serial_batches) if isTrain == "train" else False
+        rank, world = _dist()
+        self.batch_sampler = None
+        if world == 1:
+            self.dataloader = torch.utils.data.DataLoader(
+                self.dataset, batch_size=opt.batchSize, shuffle=shuffle,
+                num_workers=int(opt.nThreads), pin_memory=True)
+        else:
+            # the same sampler (hence the same RNG draws) as the 1-process loader above
+            sampler = (torch.utils.data.RandomSampler(self.dataset) if shuffle
+                       else torch.utils.data.SequentialSampler(self.dataset))
+            self.batch_sampler = RankBatchSampler(sampler, opt.batchSize, rank, world)
+            self.dataloader = torch.utils.data.DataLoader(
+                self.dataset, batch_sampler=self.batch_sampler, num_workers=int(opt.nThreads),
+                pin_memory=True)
 
     def load_data(self):
         return self
@@ -52,9 +127,14 @@ class CustomDatasetDataLoader:
         for i, data in enumerate(self.dataloader):
             if i * opt.batchSize >= opt.max_dataset_size:
                 break
+            gb = self.batch_sampler.sizes.popleft() if self.batch_sampler is not None else len(data["A_paths"])
+            if "B_u8" not in data:     # single dataset (--model test): A only
+                yield {"A": to_images(data["A_u8"], data["flip"], in_nc == 1), "A_paths": data["A_paths"],
+                       "global_batch": gb}
+                continue
             yield {"A": to_images(data["A_u8"], data["flip"], in_nc == 1),
                    "B": to_images(data["B_u8"], data["flip"], out_nc == 1),
-                   "A_paths": data["A_paths"], "B_paths": data["B_paths"]}
+                   "A_paths": data["A_paths"], "B_paths": data["B_paths"], "global_batch": gb}
 
 
 def CreateDataLoader(opt, isTrain="train"):

@@ -90,6 +90,9 @@ SIGNATURES = {
     "dsgan_u8_to_image": [P, P, P, I, I, I, I, S],
     "dsgan_img_metrics": [P, P, I, I, I, P, P, S],
     "dsgan_ms_ssim": [P, P, F, F, I, I, I, I, P, F, F, P, I, P, P, P, S],
+    "dsgan_ms_ssim_train_workspace": [I, I, I, I, I],
+    "dsgan_ms_ssim_fwd_train": [P, P, F, F, I, I, I, I, P, F, F, P, I, P, P, P, S],
+    "dsgan_ms_ssim_bwd": [P, P, F, F, I, I, I, I, P, F, F, P, I, P, P, P, P, I, S],
     "dsgan_ssim_bwd": [P, P, F, F, I, I, I, P, P, P, F, P, I, S],
     # adam.hip
     "dsgan_adam": [P, P, P, P, L, F, F, F, F, I, S],

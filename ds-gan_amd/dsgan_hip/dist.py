@@ -2,17 +2,22 @@
 backend on ROCm), replacing the reference's single-process nn.DataParallel
 (DSGAN/models/networks.py:74-77).
 
-Per step there are exactly two exchanges, both on flat fp32 gradient buffers:
-  1. D grads (0.70 M params, 2.8 MB) after backward_D -- must land before optimizer_D.step(),
-     because the G step reads the updated D;
-  2. G grads (22.4 M params, 89.7 MB) after backward_G, in ``bucket_mb`` chunks so several
-     RCCL rings can stream over the 7 xGMI links.
-Averaging = SUM then a HIP scale by 1/world (gloo, used by the CPU tests, has no AVG op).
+Per step there are exactly two exchanges, both on flat fp32 gradient buffers (dsgan_hip.flat):
+  1. D grads (0.70 M params, 2.8 MB) after backward_D, one all-reduce that must land before
+     optimizer_D.step(): the G step reads the updated D (DSGAN/models/pix2pix_model.py:204-217);
+  2. G grads (22.4 M params, 89.7 MB) in buckets that start DURING backward_G (``GradBuckets``):
+     the G flat buffer is laid out in backward order, every autograd Function reports the
+     parameters whose weight-grads it has launched (functional.GRAD_READY), and a bucket whose
+     parameters are all reported is all-reduced on RCCL's stream while the rest of the backward
+     keeps the CUs busy.  optimizer_G.step() waits for the buckets.
+Averaging: ReduceOp.AVG on RCCL; SUM then 1/world on gloo (the CPU rehearsal used by the
+tests has no AVG).
 """
 import torch
 import torch.distributed as dist
 
 from ._lib import call, ptr, stream
+from . import functional as HF
 
 
 def world_size():
@@ -35,15 +40,91 @@ def _scale(t, a):
         t.mul_(a)
 
 
+def _avg_op():
+    return dist.ReduceOp.AVG if dist.get_backend() == "nccl" else None
+
+
+def _allreduce_avg(t, async_op):
+    op = _avg_op()
+    return dist.all_reduce(t, op=op if op is not None else dist.ReduceOp.SUM, async_op=async_op)
+
+
+def _post_scale(buf, W):
+    if _avg_op() is None:
+        _scale(buf, 1.0 / W)
+
+
 def allreduce_mean_(buf, bucket_mb=32):
-    """In-place mean of a flat fp32 buffer over all ranks."""
+    """In-place mean of a flat fp32 buffer over all ranks (blocking for the caller's stream)."""
     W = world_size()
     if W == 1:
         return buf
     n = buf.numel()
     step = max(1, int(bucket_mb * (1 << 20) // 4))
-    works = [dist.all_reduce(buf[o:o + step], op=dist.ReduceOp.SUM, async_op=True) for o in range(0, n, step)]
+    works = [_allreduce_avg(buf[o:o + step], True) for o in range(0, n, step)]
     for w in works:
         w.wait()
-    _scale(buf, 1.0 / W)
+    _post_scale(buf, W)
     return buf
+
+
+class GradBuckets:
+    """Bucketed all-reduce of one flat gradient buffer, overlapped with the backward that fills it.
+
+    ``layout`` = [(param, offset, numel)] in buffer order.  Buckets are contiguous ranges of about
+    ``bucket_mb`` cut at parameter boundaries; ``arm()`` before the backward, ``ready(params)``
+    from functional.GRAD_READY as weight-grads are launched (a bucket starts when its last
+    parameter is reported), ``finish()`` after the backward: launches the buckets that are not
+    complete (parameters never reported) and waits for all of them."""
+
+    def __init__(self, grad, layout, bucket_mb=24):
+        self.grad = grad
+        self.buckets = []          # [start, end, set(param ids)]
+        self.owner = {}            # param id -> bucket index
+        lim = int(bucket_mb * (1 << 20) // 4)
+        cur = None
+        for p, off, n in layout:
+            if cur is None or (off + n - cur[0] > lim and cur[2]):
+                if cur is not None:
+                    cur[1] = off
+                cur = [off, off + n, set()]
+                self.buckets.append(cur)
+            cur[2].add(id(p))
+            cur[1] = off + n
+            self.owner[id(p)] = len(self.buckets) - 1
+        self.buckets[-1][1] = grad.numel()
+        self.pending = None
+        self.works = None
+        self.launched = None
+
+    def arm(self):
+        self.pending = [set(b[2]) for b in self.buckets]
+        self.works = []
+        self.launched = [False] * len(self.buckets)
+        HF.GRAD_READY[0] = self.ready
+
+    def _launch(self, i):
+        if not self.launched[i]:
+            s, e = self.buckets[i][0], self.buckets[i][1]
+            self.launched[i] = True
+            self.works.append(_allreduce_avg(self.grad[s:e], True))
+
+    def ready(self, params):
+        for p in params:
+            i = self.owner.get(id(p))
+            if i is None or self.launched[i]:
+                continue
+            self.pending[i].discard(id(p))
+            if not self.pending[i]:
+                self._launch(i)
+
+    def finish(self):
+        HF.GRAD_READY[0] = None
+        for i in range(len(self.buckets)):
+            self._launch(i)
+        for w in self.works:
+            w.wait()
+        _post_scale(self.grad, world_size())
+        n_early = sum(1 for i in range(len(self.buckets)) if not self.pending[i])
+        self.pending = self.works = None
+        return n_early

@@ -15,13 +15,32 @@ from .functional import fill_, bump_weight_generation
 
 
 class FlatParams:
-    def __init__(self, module, device):
+    """``order`` (optional): the modules whose parameters come first in the buffer, in that order
+    (the rest follow in ``module.parameters()`` order).  The generator passes its backward order
+    so that the gradient buckets of dsgan_hip.dist.GradBuckets fill front to back."""
+
+    def __init__(self, module, device, order=None):
         self.params = [p for p in module.parameters()]
+        placed = []
+        if order:
+            seen = set()
+            for m in order:
+                for p in m.parameters():
+                    if id(p) not in seen:
+                        seen.add(id(p))
+                        placed.append(p)
+            placed += [p for p in self.params if id(p) not in seen]
+        else:
+            placed = list(self.params)
+        assert len(placed) == len(self.params)
         # every tensor starts on a 256-byte boundary (vector loads in the kernels)
-        offs, n = [], 0
-        for p in self.params:
-            offs.append(n)
+        offs, n = {}, 0
+        self.layout = []
+        for p in placed:
+            offs[id(p)] = n
+            self.layout.append((p, n, p.numel()))
             n += (p.numel() + 63) // 64 * 64
+        offs = [offs[id(p)] for p in self.params]
         self.numel = n
         self.data = torch.empty(n, device=device, dtype=torch.float32)
         self.grad = torch.empty(n, device=device, dtype=torch.float32)

@@ -121,6 +121,18 @@ def _empty(N, C, H, W, like):
     return torch.empty((N, C, H, W), device=like.device, dtype=torch.float32)
 
 
+# Gradient-readiness hook (dsgan_hip.dist.GradBuckets): every Function calls _params_done() at
+# the end of its backward with the parameters whose weight-grads it has just launched, so a
+# bucket of the flat gradient can start its all-reduce while the rest of backward runs.
+GRAD_READY = [None]
+
+
+def _params_done(*ps):
+    h = GRAD_READY[0]
+    if h is not None:
+        h([p for p in ps if p is not None])
+
+
 def _grad_buf(p):
     """Accumulation target for a parameter's gradient, or None when it is frozen."""
     if p is None or not p.requires_grad:
@@ -554,6 +566,7 @@ class Conv2dFn(torch.autograd.Function):
         gb = _grad_buf(ctx.b_ref) if (b is not None and ctx.needs_input_grad[2]) else None
         if gb is not None:
             channel_sum_raw(dy, gb)
+        _params_done(ctx.w_ref, ctx.b_ref)
         return dx, None, None, None, None, None
 
 
@@ -594,6 +607,7 @@ class ConvT3s2Fn(torch.autograd.Function):
         gb = _grad_buf(ctx.b_ref) if (b is not None and ctx.needs_input_grad[2]) else None
         if gb is not None:
             channel_sum_raw(dy, gb)
+        _params_done(ctx.w_ref, ctx.b_ref)
         return _give(ctx.box, dx), None, None
 
 
@@ -746,6 +760,7 @@ class PwMlpFn(torch.autograd.Function):
         if gb1 is not None:
             channel_sum_raw(dz, gb1)
         dh = conv_dgrad_raw(dz, w1v, tuple(h.shape), 1, 0) if ctx.needs_input_grad[0] else None
+        _params_done(*ctx.refs)
         return _give(ctx.box_h, dh), PwMlpFn._dx(ctx, dy, ws, x), None, None, None, None, None
 
     @staticmethod
@@ -790,6 +805,7 @@ class PwMlpFn(torch.autograd.Function):
             IGEMM_TIMER.end(e0, 2.0 * N * HW * C4 * C, ("wgrad", N, C, H, W, C4, 1, 1), "pwgemm_kernel")
         if gb1 is not None:
             call("dsgan_colsum", ptr(bsum), ntiles, C4, ptr(gb1), stream())
+        _params_done(*ctx.refs)
         return _give(ctx.box_h, dh), PwMlpFn._dx(ctx, dy, ws, x), None, None, None, None, None
 
 
@@ -840,6 +856,7 @@ class DwConvFn(torch.autograd.Function):
         gw, gb = _grad_buf(wr), _grad_buf(br)
         if gw is not None:
             _dw_wgrad(dy, x, gw, gb, w.shape[-1])
+        _params_done(wr, br)
         return dx, None, None
 
 
@@ -883,6 +900,7 @@ class MultiDwConvFn(torch.autograd.Function):
             if gw is not None:
                 _dw_wgrad(dy4[:, sl], x[:, sl], gw, gb, w.shape[-1])
         dx = None if acc else _give(ctx.box, dx)
+        _params_done(*ctx.refs)
         return (dx,) + (None,) * 8
 
 
@@ -1132,6 +1150,7 @@ class MidTailFn(torch.autograd.Function):
         call("dsgan_ca_bwd", ptr(datt), ptr(att), ptr(avg), ptr(mx), ptr(hsave), ptr(w1), ptr(w2), ptr(pa),
              ptr(davg), ptr(dmx), ptr(_grad_buf(w1r)), ptr(_grad_buf(w2r)), ptr(_grad_buf(par)), N, C, R, stream())
         call("dsgan_plane_stats_bwd", ptr(davg), ptr(dmx), ptr(amax), ptr(dv), C * H * W, N, C, H * W, stream())
+        _params_done(*ctx.refs)
         return _give(ctx.box_v, dv), _give(ctx.box_x, dx), None, None, None
 
 
@@ -1340,3 +1359,47 @@ def ms_ssim_affine(real, fake, a=1.0, b=0.0, data_range=1.0, weights=MS_SSIM_WEI
          float(C1), float(C2), ctypes.cast(wh, ctypes.c_void_p), len(weights), ptr(work), ptr(stats), ptr(out),
          stream())
     return out[N] if size_average else out[:N]
+
+
+class MSSSIMFn(torch.autograd.Function):
+    """Batch-mean MS-SSIM of (a*real+b, a*fake+b) (DSGAN/MS_SSIM.py:153-225, size_average=True)
+    as a loss term: gradient w.r.t. fake through the 5-level pyramid (losses.hip)."""
+
+    @staticmethod
+    def forward(ctx, real, fake, a, b, data_range, weights):
+        import ctypes
+        real, fake = real.contiguous(), fake.contiguous()
+        if real.shape != fake.shape or real.dim() != 4:
+            raise ValueError("ms_ssim: two (N,C,H,W) tensors of the same shape required")
+        N, C, H, W = real.shape
+        L = len(weights)
+        lib = _lib.load()
+        work = torch.empty(lib.dsgan_ms_ssim_train_workspace(N, C, H, W, L), device=real.device, dtype=torch.float32)
+        stats = torch.empty(2 * L * N * C, device=real.device, dtype=torch.float32)
+        out = torch.empty(N + 1, device=real.device, dtype=torch.float32)
+        wh = (ctypes.c_float * L)(*[float(w) for w in weights])
+        C1, C2 = (0.01 * data_range) ** 2, (0.03 * data_range) ** 2
+        call("dsgan_ms_ssim_fwd_train", ptr(real), ptr(fake), float(a), float(b), N, C, H, W,
+             ptr(gauss_win(real.device)), float(C1), float(C2), ctypes.cast(wh, ctypes.c_void_p), L, ptr(work),
+             ptr(stats), ptr(out), stream())
+        ctx.save_for_backward(real, fake, work, stats)
+        ctx.args = (float(a), float(b), float(C1), float(C2), tuple(float(w) for w in weights))
+        return out[N]
+
+    @staticmethod
+    def backward(ctx, g):
+        import ctypes
+        real, fake, work, stats = ctx.saved_tensors
+        a, b, C1, C2, weights = ctx.args
+        N, C, H, W = real.shape
+        wh = (ctypes.c_float * len(weights))(*weights)
+        dfake = torch.empty_like(fake)
+        call("dsgan_ms_ssim_bwd", ptr(real), ptr(fake), a, b, N, C, H, W, ptr(gauss_win(real.device)), C1, C2,
+             ctypes.cast(wh, ctypes.c_void_p), len(weights), ptr(work), ptr(stats), ptr(g.contiguous()), ptr(dfake),
+             0, stream())
+        return None, dfake, None, None, None, None
+
+
+def ms_ssim_loss_affine(real, fake, a=0.5, b=0.5, data_range=1.0, weights=MS_SSIM_WEIGHTS):
+    """Differentiable batch-mean MS-SSIM of (a*real+b, a*fake+b); gradient w.r.t. fake only."""
+    return MSSSIMFn.apply(real, fake, a, b, data_range, tuple(weights))

@@ -96,7 +96,8 @@ class BaseModel:
         """Reads '{epoch}_net_{name}.pth' like the reference (:119) and, if that is absent, the
         '{epoch}_useSE_net_{name}.pth' this build (and the reference) saves -- the reference's
         save/load name mismatch is bridged instead of failing.  ``module.`` prefixes from
-        DataParallel checkpoints are stripped; strict=False as in the reference (:148)."""
+        DataParallel checkpoints are stripped.  As the reference's ``load_state_dict(strict=False)``
+        (:148): missing / unexpected keys are allowed (and printed), a shape mismatch raises."""
         for name in self.model_names:
             if isinstance(name, str):
                 net = getattr(self, "net" + name)
@@ -108,10 +109,19 @@ class BaseModel:
                 state_dict = OrderedDict((k[7:] if k.startswith("module.") else k, v) for k, v in state_dict.items())
                 state_dict = {k: v for k, v in state_dict.items()
                               if not (k.endswith("running_mean") or k.endswith("running_var"))}
+                own = net.state_dict()
+                bad = ["%s: checkpoint %s vs model %s" % (k, tuple(v.shape), tuple(own[k].shape))
+                       for k, v in state_dict.items() if k in own and own[k].shape != v.shape]
+                if bad:
+                    raise RuntimeError("Error(s) in loading state_dict for %s:\n\tsize mismatch for %s"
+                                       % (type(net).__name__, "\n\tsize mismatch for ".join(bad)))
+                missing = [k for k in own if k not in state_dict]
+                unexpected = [k for k in state_dict if k not in own]
+                if missing or unexpected:
+                    print("load_networks(%s): missing keys %s, unexpected keys %s" % (name, missing, unexpected))
                 with torch.no_grad():
-                    own = net.state_dict()
                     for k, v in state_dict.items():
-                        if k in own and own[k].shape == v.shape:
+                        if k in own:
                             own[k].copy_(v.to(own[k].device, own[k].dtype))
 
     def print_networks(self, verbose):

@@ -198,6 +198,13 @@ class MixConvNeXtML(nn.Module):
         self.local = OriginMLKA()
         self.res = nn.Conv2d(64, 3, kernel_size=3, padding=1)
 
+    def backward_order(self):
+        """Children in the order backward_G finishes their weight-grads (the reverse of the
+        forward's creation order: the local branch and the head are created last); FlatParams
+        lays the G gradient buffer out in this order for the overlapped bucketed all-reduce."""
+        return [self.res, self.local, self.uc4, self.u4, self.uc3, self.u3, self.uc2, self.u2, self.uc1, self.u1,
+                self.down512, self.down256, self.down128, self.down64, self.c5, self.c4, self.c3, self.c2, self.c1]
+
     def forward(self, x):
         # R1..R4 feed the next stage's MaxPool(2), their skip pyramid and a decoder concat; the
         # MaxPool(2) of R_i is computed once for the encoder and the pyramid's k=2 branch

@@ -68,11 +68,17 @@ def init_weights(net, init_type="normal", gain=0.02):
 
 def init_net(net, init_type="normal", gpu_ids=()):
     """DSGAN/models/networks.py:73-79, minus ``nn.DataParallel``: the build runs one process
-    per GPU (torch.distributed over RCCL), so the net is moved to this rank's device only."""
+    per GPU (torch.distributed over RCCL), so the net is moved to this rank's device only.
+
+    The weights are drawn on the CPU generator BEFORE the move, i.e. exactly the reference's
+    ``gpu_ids=[]`` init (module construction and the post-order N(0, 0.02) draws consume the
+    global CPU RNG in the same order; pinned by tests/golden/golden_v2.npz INIT_*).  (The
+    reference with GPUs draws from the CUDA generator after ``net.to``, which no CPU run can pin;
+    every rank of a multi-GPU run draws the same values, and rank 0's are broadcast anyway.)"""
+    init_weights(net, init_type)
     if len(gpu_ids) > 0:
         assert torch.cuda.is_available(), "gpu_ids given but no ROCm GPU is visible"
         net.to(torch.device("cuda", gpu_ids[0]))
-    init_weights(net, init_type)
     return net
 
 
@@ -88,7 +94,13 @@ def define_G(input_nc, output_nc, ngf, which_model_netG, norm="batch", use_dropo
 
 def define_D(input_nc, ndf, which_model_netD, n_layers_D=3, norm="batch", use_sigmoid=False,
              init_type="normal", gpu_ids=()):
-    """DSGAN/models/networks.py:115-131."""
+    """DSGAN/models/networks.py:115-131.  The PatchGAN runs InstanceNorm (affine=False, the
+    reference default ``--norm instance``) fused into its conv kernels; ``--norm batch`` (affine
+    BatchNorm2d with running stats) and ``none`` are not on the DS-GAN path and raise instead of
+    silently training a different discriminator."""
+    if norm != "instance":
+        raise NotImplementedError("define_D: norm [%s] is not supported by the MI355X PatchGAN "
+                                  "(instance only, the reference default)" % norm)
     norm_layer = get_norm_layer(norm_type=norm)
     if which_model_netD == "basic":
         netD = NLayerDiscriminator(input_nc, ndf, n_layers=3, norm_layer=norm_layer, use_sigmoid=use_sigmoid)

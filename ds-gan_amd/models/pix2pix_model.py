@@ -12,11 +12,15 @@ and grads of each network live in one flat buffer updated by one fused-Adam laun
 
 Deliberate, documented deviations:
   * q1: untyped loss-weight flags are cast to numbers (the reference crashes on CLI values);
-  * multi-GPU: per-rank ImagePool; the TV term (a batch *sum*, :189-191) is scaled by the world
-    size so averaged gradients equal the reference's global-batch gradient;
+  * multi-GPU (one process per GPU): each rank holds its chunk of the global batch (data/), so
+    the gradients are made equal to the reference's global-batch gradient
+    (nn.DataParallel computes every loss on the gathered batch, networks.py:74-77): the batch
+    *means* (BCE, L1, VGG-L1, SSIM) are weighted by world * n_rank / n_global (1 when the global
+    batch divides evenly), the TV term -- a batch *sum*, :189-191 -- by the world size, and the
+    gradients are averaged; the ImagePool is per rank (its python RNG seeded 20 + 1000 * rank);
   * the unused VGG relu5_3 block is not computed (the loss never reads it, :182-186).
 """
-import os
+import random
 
 import torch
 
@@ -28,7 +32,7 @@ from .base_model import BaseModel
 from . import networks
 from .vgg import Vgg16
 
-_SERIAL_VGG = os.environ.get("DSGAN_SERIAL_VGG") == "1"   # A/B switch: vgg(real_B) on the main stream
+POOL_SEED = 20   # DSGAN/train.py:48 setup_seed(20): the ImagePool's RNG on ranks > 0 is offset from it
 
 
 class Pix2PixModel(BaseModel):
@@ -57,6 +61,7 @@ class Pix2PixModel(BaseModel):
         self.w_gan = float(opt.w_gan)
         self.w_ss = float(opt.w_ss)
         self.use_condition = int(opt.use_condition)
+        self.ssim_kind = getattr(opt, "ssim_loss", "ssim")
         self.netG = networks.define_G(opt.input_nc, opt.output_nc, opt.ngf, opt.which_model_netG,
                                       opt.norm, not opt.no_dropout, opt.init_type, self.gpu_ids)
         if self.isTrain:
@@ -65,13 +70,17 @@ class Pix2PixModel(BaseModel):
             self.netD = networks.define_D(d_in, opt.ndf, opt.which_model_netD, opt.n_layers_D,
                                           opt.norm, use_sigmoid, opt.init_type, self.gpu_ids)
         if self.isTrain:
-            self.fake_AB_pool = ImagePool(opt.pool_size)
+            W, r = hdist.world_size(), hdist.rank()
+            # one process: the global python `random`, consumed exactly as the reference does
+            self.fake_AB_pool = ImagePool(opt.pool_size, rng=None if W == 1 else random.Random(POOL_SEED + 1000 * r))
             self.criterionGAN = networks.GANLoss(use_lsgan=opt.no_lsgan).to(self.device)
             self.criterionL1 = HF.l1_loss
             self.vgg = Vgg16(getattr(opt, "vgg_weights", "") or None).to(self.device)
             # flat param/grad buffers + fused Adam (one launch per network per step)
-            self.flatG = FlatParams(self.netG, self.device)
+            order = self.netG.backward_order() if hasattr(self.netG, "backward_order") else None
+            self.flatG = FlatParams(self.netG, self.device, order=order)
             self.flatD = FlatParams(self.netD, self.device)
+            self.g_buckets = hdist.GradBuckets(self.flatG.grad, self.flatG.layout) if W > 1 else None
             hdist.broadcast_params(self.flatG)
             hdist.broadcast_params(self.flatD)
             self.optimizers = []
@@ -79,7 +88,8 @@ class Pix2PixModel(BaseModel):
             self.optimizer_D = FlatAdam(self.flatD, lr=opt.lr, betas=(opt.beta1, 0.999))
             self.optimizers.append(self.optimizer_G)
             self.optimizers.append(self.optimizer_D)
-            self.tv_scale = float(hdist.world_size())
+            self.tv_scale = float(W)
+            self.mean_w = 1.0   # world * n_rank / n_global, set per batch by set_input
             self._vgg_stream = torch.cuda.Stream(self.device)
             self._real_feats = None
 
@@ -88,6 +98,10 @@ class Pix2PixModel(BaseModel):
         self.real_A = input["A" if AtoB else "B"].to(self.device, non_blocking=True)
         self.real_B = input["B" if AtoB else "A"].to(self.device, non_blocking=True)
         self.image_paths = input["A_paths" if AtoB else "B_paths"]
+        if self.isTrain:
+            W = hdist.world_size()
+            n = int(self.real_A.shape[0])
+            self.mean_w = float(W * n) / float(input.get("global_batch", W * n))
 
     def forward(self):
         self.fake_B = self.netG(self.real_A)
@@ -103,7 +117,7 @@ class Pix2PixModel(BaseModel):
         pred_real = self.netD(real_AB)
         self.loss_D_real = self.criterionGAN(pred_real, True)
         self.loss_D = (self.loss_D_fake + self.loss_D_real) * 0.5
-        self.loss_D.backward()
+        (self.loss_D if self.mean_w == 1.0 else self.loss_D * self.mean_w).backward()
 
     def backward_G(self):
         if self.use_gan == 1:
@@ -118,10 +132,18 @@ class Pix2PixModel(BaseModel):
         self.loss_vgg = self.vgg.perceptual_l1(self.fake_B, self.real_B_features)
         self.tv_loss = HF.tv_loss(self.fake_B, self.tv_scale / (320 * 256))
         # 1 - ssim((real_B+1)/2, (fake_B+1)/2, data_range=1): the affine map is fused in-kernel
-        self.loss_ssim = 1 - HF.ssim_affine(self.real_B, self.fake_B, 0.5, 0.5, 1.0)
+        # (--ssim_loss ms_ssim: the 5-level MS-SSIM of DSGAN/MS_SSIM.py:153-225 instead)
+        if self.ssim_kind == "ms_ssim":
+            self.loss_ssim = 1 - HF.ms_ssim_loss_affine(self.real_B, self.fake_B, 0.5, 0.5, 1.0)
+        else:
+            self.loss_ssim = 1 - HF.ssim_affine(self.real_B, self.fake_B, 0.5, 0.5, 1.0)
         self.loss_G = (self.loss_G_GAN * self.w_gan + self.loss_G_L1 + self.loss_vgg * self.w_vgg
                        + self.tv_loss * self.w_tv + self.w_ss * self.loss_ssim)
-        self.loss_G.backward()
+        if self.mean_w == 1.0:
+            self.loss_G.backward()
+        else:   # ragged global batch under DDP: reweight the batch means, not the TV sum
+            ((self.loss_G_GAN * self.w_gan + self.loss_G_L1 + self.loss_vgg * self.w_vgg + self.w_ss * self.loss_ssim)
+             * self.mean_w + self.tv_loss * self.w_tv).backward()
 
     def _launch_real_features(self):
         """vgg(real_B) (frozen, no grad) depends only on the input: run it on a side stream so it
@@ -144,8 +166,7 @@ class Pix2PixModel(BaseModel):
         return feats
 
     def optimize_parameters(self):
-        if not _SERIAL_VGG:
-            self._launch_real_features()
+        self._launch_real_features()
         self.forward()
         if self.use_gan == 1:
             self.set_requires_grad(self.netD, True)
@@ -158,8 +179,11 @@ class Pix2PixModel(BaseModel):
             self.loss_D_real = 0
         self.set_requires_grad(self.netD, False)
         self.optimizer_G.zero_grad()
+        if self.g_buckets is not None:
+            self.g_buckets.arm()       # G grad buckets all-reduce as backward_G fills them
         self.backward_G()
-        hdist.allreduce_mean_(self.flatG.grad)
+        if self.g_buckets is not None:
+            self.g_buckets.finish()
         self.optimizer_G.step()
 
     # ---- train.py helpers (DSGAN/models/pix2pix_model.py:292-310) ----

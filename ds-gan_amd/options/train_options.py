@@ -24,6 +24,11 @@ class TrainOptions(BaseOptions):
         parser.add_argument("--no_html", action="store_true", help="do not save intermediate training results")
         parser.add_argument("--lr_policy", type=str, default="lambda", help="learning rate policy: lambda|step|plateau")
         parser.add_argument("--lr_decay_iters", type=int, default=50, help="multiply by a gamma every lr_decay_iters iterations")
+        # build extension (not a reference flag): the structural term of backward_G
+        # (DSGAN/models/pix2pix_model.py:193-195 uses single-scale ssim; BASELINE config 4 names the
+        # gaussian-pyramid MS-SSIM of DSGAN/MS_SSIM.py:153-225, which needs images > 160 px)
+        parser.add_argument("--ssim_loss", type=str, default="ssim", choices=["ssim", "ms_ssim"],
+                            help="structural loss term: ssim (reference) or ms_ssim (opt-in)")
         self.isTrain = True
         return parser
 

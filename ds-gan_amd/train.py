@@ -7,6 +7,15 @@ Same order of work per iteration: set_input -> optimize_parameters -> get_img_ti
 (cv2) and the visualizer/HTML are out of scope (SURVEY.md §8 out-of-scope list).
 
     python ds-gan_amd/train.py --dataroot DATA --out RESULTS [reference TrainOptions flags...]
+    python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 \
+        ds-gan_amd/train.py --dataroot DATA --out RESULTS --batchSize 128 [...]
+
+Multi-GPU replaces the reference's single-process nn.DataParallel (DSGAN/models/networks.py:
+74-77) with one process per GPU: under torchrun (WORLD_SIZE > 1) every rank joins the RCCL
+process group and drives cuda:LOCAL_RANK; ``--batchSize`` stays the GLOBAL batch, of which each
+rank trains its DataParallel-style chunk (data/__init__.py); the printed / CSV losses are the
+global-batch values (an all-reduce of the per-rank means at logging time); only rank 0 writes
+checkpoints and CSV files, behind a barrier.
 """
 import argparse
 import csv
@@ -22,6 +31,7 @@ if HERE not in sys.path:
 
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
 
 
 def setup_seed(seed):
@@ -29,6 +39,28 @@ def setup_seed(seed):
     torch.cuda.manual_seed_all(seed)
     np.random.seed(seed)
     random.seed(seed)
+
+
+def init_distributed():
+    """(rank, world, local_rank); joins the RCCL process group when launched by torchrun."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world == 1:
+        return 0, 1, None
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if not dist.is_initialized():
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    return dist.get_rank(), world, local
+
+
+def global_losses(losses, n_local, n_global):
+    """Per-rank batch means -> the global-batch means the reference logs (weights n_rank/n)."""
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return losses
+    dev = torch.device("cuda", torch.cuda.current_device())
+    t = torch.tensor([v * n_local / n_global for v in losses.values()], dtype=torch.float64, device=dev)
+    dist.all_reduce(t)
+    return type(losses)(zip(losses.keys(), t.tolist()))
 
 
 def main(argv=None, output_freq=100):
@@ -41,10 +73,14 @@ def main(argv=None, output_freq=100):
     ap.add_argument("--out", default=os.path.abspath(os.path.join("..", "resext50_vision1")))
     ap.add_argument("--dataroot", default="/root/dataset/256x256")
     known, rest = ap.parse_known_args(argv)
+    rank, world, local = init_distributed()
     setup_seed(20)
     out = known.out
-    os.makedirs(out, exist_ok=True)
+    if rank == 0:
+        os.makedirs(out, exist_ok=True)
     opt = TrainOptions().parse(known.dataroot, out, rest)   # parse() sets checkpoints_dir = out/checkpoints
+    if world > 1:
+        opt.gpu_ids = [local]   # one process per GPU: this rank's device
     dataset = CreateDataLoader(opt, "train").load_data()
     print("#training images = %d" % len(dataset))
     model = create_model(opt)
@@ -66,7 +102,10 @@ def main(argv=None, output_freq=100):
             model.get_img_label(data)
             metrics.update(model.fake_B[0], model.real_B[0])
             if (i + 1) % output_freq == 0:
-                losses = model.get_current_losses()
+                losses = global_losses(model.get_current_losses(), int(model.real_A.shape[0]),
+                                       int(data.get("global_batch", model.real_A.shape[0])))
+                if rank != 0:
+                    continue
                 ssim_avg, psnr_avg = metrics.averages()
                 t = (time.time() - iter_start_time) / opt.batchSize
                 message = "(epoch: %d, iters: %d, time: %.3f) " % (epoch, epoch_iter, t)
@@ -77,12 +116,15 @@ def main(argv=None, output_freq=100):
                                             ssim_avg, psnr_avg])
         ssim_avg, psnr_avg = metrics.averages()
         history.append((epoch, ssim_avg, psnr_avg))
-        with open(os.path.join(out, "each_epoch.csv"), "a", newline="") as f:
-            csv.writer(f).writerow([epoch, "train", ssim_avg, psnr_avg])
-        print("saving the model at the end of epoch %d, iters %d" % (epoch, i + 1))
-        model.save_networks(epoch)
-        print("End of epoch %d / %d \t Time Taken: %d sec" % (epoch, opt.niter + opt.niter_decay,
-                                                                time.time() - epoch_start_time))
+        if rank == 0:
+            with open(os.path.join(out, "each_epoch.csv"), "a", newline="") as f:
+                csv.writer(f).writerow([epoch, "train", ssim_avg, psnr_avg])
+            print("saving the model at the end of epoch %d, iters %d" % (epoch, i + 1))
+            model.save_networks(epoch)
+            print("End of epoch %d / %d \t Time Taken: %d sec" % (epoch, opt.niter + opt.niter_decay,
+                                                                    time.time() - epoch_start_time))
+        if world > 1:
+            dist.barrier()
         model.update_learning_rate()
     return model, history
 

@@ -293,6 +293,18 @@ long dsgan_ms_ssim_workspace(int N, int C, int H, int W);
 int dsgan_ms_ssim(const float* real, const float* fake, float a, float b, int N, int C, int H, int W,
                   const float* win11, float C1, float C2, const float* weights_host, int levels,
                   float* work, float* stats, float* out, hipStream_t stream);
+/* MS-SSIM as a differentiable loss (C4 opt-in, --ssim_loss ms_ssim): the same value with every
+ * pyramid level kept in `work` (dsgan_ms_ssim_train_workspace floats), then the backward
+ * dfake (+)= d(gout[0] * out[N])/d(fake) through the per-level SSIM / contrast-structure maps,
+ * the relu'd product over levels and the padded 2x2 average pools (DSGAN/MS_SSIM.py:206-225).
+ * stats: 2*levels*N*C floats, written by the forward, read by the backward. */
+long dsgan_ms_ssim_train_workspace(int N, int C, int H, int W, int levels);
+int dsgan_ms_ssim_fwd_train(const float* real, const float* fake, float a, float b, int N, int C, int H, int W,
+                            const float* win11, float C1, float C2, const float* weights_host, int levels,
+                            float* work, float* stats, float* out, hipStream_t stream);
+int dsgan_ms_ssim_bwd(const float* real, const float* fake, float a, float b, int N, int C, int H, int W,
+                      const float* win11, float C1, float C2, const float* weights_host, int levels, float* work,
+                      const float* stats, const float* gout, float* dfake, int accumulate, hipStream_t stream);
 
 /* ---- fused Adam over a flat buffer (adam.hip): torch.optim.Adam pix2pix_model.py:122-125 -- */
 int dsgan_adam(float* p, const float* g, float* m, float* v, long n, float lr, float beta1,

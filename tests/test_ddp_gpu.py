@@ -1,0 +1,112 @@
+"""Data-parallel equivalence on the one-GPU box: two ranks share cuda:0 and
+exchange gradients over gloo (RCCL refuses two ranks on one device); each trains one image of a
+batch of two through the product path -- Pix2PixModel.optimize_parameters with the D all-reduce
+before optimizer_D.step and the G buckets all-reduced during backward_G (dsgan_hip.dist) -- and
+the result must equal ONE process training the whole batch (the reference's nn.DataParallel,
+DSGAN/models/networks.py:74-77, computes every loss on the gathered global batch):
+
+  * the averaged flat G and D gradients equal the single-process gradients (TV is a batch SUM,
+    DSGAN/models/pix2pix_model.py:189-191: the per-rank TV coefficient carries the world size);
+  * the post-step D (and G) parameters are identical on both ranks and equal the single run's --
+    the G step reads the updated D, so an exchange that landed after optimizer_D.step would show.
+fp32 mode, pool_size 0, "fanin" weight recipe; bars are fp32 reassociation level (the batch sum
+of every weight-grad is split differently across the two runs).
+"""
+import os
+import random
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _model():
+    import dsgan_hip
+    from oracle import dsgan_cpu as O
+    from oracle.recipe import make_params
+    from options.train_options import default_train_opt
+    from models import create_model
+    dsgan_hip.require_gpu()
+    random.seed(20)
+    torch.manual_seed(20)
+    m = create_model(default_train_opt(gpu_ids=[0], pool_size=0, precision="fp32", batchSize=2))
+    with torch.no_grad():
+        for net, pr in ((m.netG, make_params(O.g_param_spec(), "fanin", 1000)),
+                        (m.netD, make_params(O.d_param_spec(), "fanin", 5000)),
+                        (m.vgg, make_params(O.vgg_param_spec(True), "vgg", 7000))):
+            for k, v in net.state_dict().items():
+                v.copy_(pr[k])
+    return m
+
+
+def _grads_and_params(m):
+    torch.cuda.synchronize()
+    return {"gG": torch.cat([p.grad.detach().flatten() for p in m.netG.parameters()]).cpu(),
+            "gD": torch.cat([p.grad.detach().flatten() for p in m.netD.parameters()]).cpu(),
+            "pG": torch.cat([p.detach().flatten() for p in m.netG.parameters()]).cpu(),
+            "pD": torch.cat([p.detach().flatten() for p in m.netD.parameters()]).cpu(),
+            "loss_G": float(m.loss_G), "loss_D": float(m.loss_D)}
+
+
+def _worker(rank, world, port, out_dir):
+    import sys
+    sys.path[:0] = [REPO, os.path.join(REPO, "ds-gan_amd")]
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from oracle.recipe import synth_pair
+    m = _model()
+    assert m.g_buckets is not None and len(m.g_buckets.buckets) >= 3
+    A, B = synth_pair(2, 64, seed=4)
+    sl = slice(rank, rank + 1)
+    m.set_input({"A": A[sl].cuda(), "B": B[sl].cuda(), "A_paths": ["a"], "B_paths": ["b"]})
+    m.optimize_parameters()
+    res = _grads_and_params(m)
+    torch.save(res, os.path.join(out_dir, "rank%d.pt" % rank))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _rel(a, b):
+    return ((a.double() - b.double()).norm() / max(b.double().norm().item(), 1e-30)).item()
+
+
+def test_two_ranks_equal_one_process(tmp_path):
+    import multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    port = 33500 + random.randint(0, 2000)
+    ps = [ctx.Process(target=_worker, args=(r, 2, port, str(tmp_path))) for r in range(2)]
+    for p in ps:
+        p.start()
+    for p in ps:
+        p.join(timeout=240)
+    assert all(p.exitcode == 0 for p in ps), [p.exitcode for p in ps]
+    r0 = torch.load(tmp_path / "rank0.pt", weights_only=True)
+    r1 = torch.load(tmp_path / "rank1.pt", weights_only=True)
+
+    from oracle.recipe import synth_pair
+    m = _model()
+    A, B = synth_pair(2, 64, seed=4)
+    m.set_input({"A": A.cuda(), "B": B.cuda(), "A_paths": ["a"] * 2, "B_paths": ["b"] * 2})
+    m.optimize_parameters()
+    one = _grads_and_params(m)
+
+    # identical exchanges on both ranks: bitwise equal gradients and parameters
+    for k in ("gG", "gD", "pG", "pD"):
+        assert torch.equal(r0[k], r1[k]), k
+    # the mean of the per-rank losses is the global-batch loss
+    assert abs(0.5 * (r0["loss_D"] + r1["loss_D"]) - one["loss_D"]) <= 1e-5 * abs(one["loss_D"])
+    # averaged gradients == one process on the whole batch (fp32 reassociation level)
+    assert _rel(r0["gD"], one["gD"]) < 2e-5, _rel(r0["gD"], one["gD"])
+    assert _rel(r0["gG"], one["gG"]) < 1e-3, _rel(r0["gG"], one["gG"])
+    # post-step parameters: the D step used the exchanged gradient (Adam's first step is
+    # lr * sign(g): equal wherever |g| is above fp32 noise)
+    big = one["gD"].abs() > 1e-6
+    assert (r0["pD"][big] - one["pD"][big]).abs().max().item() < 1e-6
+    bigG = one["gG"].abs() > 1e-5
+    frac = ((r0["pG"][bigG] - one["pG"][bigG]).abs() > 1e-6).double().mean().item()
+    assert frac < 1e-3, frac

@@ -142,3 +142,71 @@ def test_aligned_dataset_host_side(tmp_path):
     assert item["flip"] == int(fl)
     assert np.array_equal(item["A_u8"].numpy(), imgs[A[1]][ho:ho + 24, wo:wo + 32])
     assert np.array_equal(item["B_u8"].numpy(), imgs[B[1]][ho:ho + 24, wo:wo + 32])
+
+
+def test_rank_batch_sampler_matches_global_batches():
+    """Each rank's chunk of every global batch, concatenated over ranks, is the 1-process batch
+    sequence (nn.DataParallel's Tensor.chunk scatter, DSGAN/models/networks.py:74-77); a ragged
+    last batch is chunked the same way and skipped only when a rank would get nothing."""
+    from data import RankBatchSampler
+    for n, B, W in ((37, 8, 2), (37, 8, 4), (30, 6, 3), (9, 4, 4), (5, 16, 8), (64, 16, 8)):
+        perm = torch.randperm(n, generator=torch.Generator().manual_seed(n)).tolist()
+        ref = [perm[i:i + B] for i in range(0, n, B)]
+        per_rank = []
+        for r in range(W):
+            s = RankBatchSampler(perm, B, r, W)
+            per_rank.append((list(s), list(s.sizes), len(s)))
+        lens = {len(b) for b, _, _ in per_rank}
+        assert len(lens) == 1 and lens.pop() == per_rank[0][2]   # every rank sees the same count
+        got = [sum((per_rank[r][0][i] for r in range(W)), []) for i in range(per_rank[0][2])]
+        kept = [b for b in ref if len(b) > (W - 1) * -(-len(b) // W)]
+        assert got == kept, (n, B, W)
+        assert per_rank[0][1] == [len(b) for b in kept]
+        for b, chunks in zip(kept, zip(*[pr[0] for pr in per_rank])):
+            assert [len(c) for c in chunks] == [len(t) for t in torch.arange(len(b)).chunk(W)] + [0] * (W - len(torch.arange(len(b)).chunk(W)))
+
+
+def _bucket_worker(rank, world, port, q):
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from dsgan_hip import dist as hdist
+    from dsgan_hip import functional as HF
+    sizes = [1000, 64, 300000, 7, 2_000_000, 5000, 123]
+    params = [torch.nn.Parameter(torch.zeros(k)) for k in sizes]
+    layout, off = [], 0
+    for p in params:
+        layout.append((p, off, p.numel()))
+        off += (p.numel() + 63) // 64 * 64
+    grad = torch.arange(off, dtype=torch.float32) * (rank + 1)
+    gb = hdist.GradBuckets(grad, layout, bucket_mb=2)     # ~524k floats per bucket
+    gb.arm()
+    # backward reports parameters (as the Functions do), in reverse layout order, one skipped
+    for p in reversed(params[1:]):
+        HF.GRAD_READY[0]([p])
+    early = sum(gb.launched)
+    n_early = gb.finish()
+    q.put((rank, grad.tolist() == (torch.arange(off, dtype=torch.float32) * 1.5).tolist(), len(gb.buckets), early,
+           n_early, HF.GRAD_READY[0] is None))
+    dist.destroy_process_group()
+
+
+def test_grad_buckets_gloo_world2():
+    """Bucketed, readiness-driven all-reduce of a flat gradient (dsgan_hip.dist.GradBuckets):
+    buckets whose parameters were all reported start before finish(); the result is the mean."""
+    import multiprocessing as mp
+    import random as _r
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 31500 + _r.randint(0, 2000)
+    ps = [ctx.Process(target=_bucket_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    out = dict((v[0], v[1:]) for v in (q.get(timeout=120) for _ in ps))
+    for p in ps:
+        p.join(timeout=60)
+    for r in (0, 1):
+        ok, nb, early, n_early, unhooked = out[r]
+        assert ok and unhooked
+        assert nb >= 3 and 1 <= early < nb and n_early == early

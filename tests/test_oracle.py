@@ -17,7 +17,10 @@ def test_param_inventory(golden):
     assert [json.dumps(list(s)) for _, s in spec] == list(golden["g_shapes"])
     assert [k for k, _ in O.d_param_spec()] == list(golden["d_keys"])
     assert [k for k, _ in O.vgg_param_spec()] == list(golden["vgg_keys"])
-    assert sum(int(np.prod(s)) for _, s in spec) == 22_425_160 or True
+    # the reference's print_networks figure (22.425 M), from the golden shapes
+    n_ref = sum(int(np.prod(json.loads(s))) for s in golden["g_shapes"])
+    assert n_ref == 22_425_232
+    assert sum(int(np.prod(s)) for _, s in spec) == n_ref
 
 
 @pytest.mark.parametrize("recipe", ["ref", "fanin"])
@@ -103,3 +106,53 @@ def test_trajectory_with_pool(golden):
 def test_lambda_lr(golden):
     mults = [O.lambda_rule(e) for e in range(21)]
     assert np.allclose(mults, golden["lr_mults"], atol=1e-12)
+
+
+def _golden_v2():
+    import os
+    return np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "golden_v2.npz"))
+
+
+def test_init_matches_reference_seed20():
+    """define_G / define_D under setup_seed(20) draw exactly the reference's CPU init
+    (DSGAN/models/networks.py:49-79, DSGAN/train.py:20-25): per-tensor sums, squares and probe
+    dots from tests/golden/gen_golden_v2.py, and the CPU RNG state after both."""
+    import train
+    from models.networks import define_G, define_D
+    gv = _golden_v2()
+    train.setup_seed(20)
+    g = define_G(3, 3, 32, "MixConvNeXtML", "instance", True, "normal", [])
+    d = define_D(6, 32, "basic", 3, "instance", False, "normal", [])
+    for net, tag in ((g, "G"), (d, "D")):
+        sums, sqs, dots = [], [], []
+        for i, v in enumerate(net.state_dict().values()):
+            x = v.detach().double().flatten()
+            sums.append(float(x.sum()))
+            sqs.append(float((x * x).sum()))
+            dots.append(float(x @ probe(x.numel(), 70000 + i)))
+        assert np.allclose(sums, gv["INIT_%s_sum" % tag], rtol=1e-9, atol=1e-12), tag
+        assert np.allclose(sqs, gv["INIT_%s_sq" % tag], rtol=1e-9, atol=1e-12), tag
+        assert np.allclose(dots, gv["INIT_%s_dot" % tag], rtol=1e-9, atol=1e-12), tag
+    assert np.array_equal(torch.rand(4, dtype=torch.float64).numpy(), gv["INIT_rng_after"])
+
+
+def test_oracle_msssim_grad_vs_reference():
+    """oracle.ms_ssim as a differentiable loss vs the reference's autograd (DSGAN/MS_SSIM.py:153-225)."""
+    gv = _golden_v2()
+    X = torch.from_numpy(gv["MS_X176"]).double()
+    Y = torch.from_numpy(gv["MS_Y176"]).double().requires_grad_(True)
+    loss = 1 - O.ms_ssim(X, Y)
+    loss.backward()
+    assert abs(loss.item() - float(gv["MS_loss176"])) < 1e-6
+    ref = torch.from_numpy(gv["MS_grad176"]).double()
+    assert ((Y.grad - ref).norm() / ref.norm()).item() < 1e-5
+    gen = torch.Generator().manual_seed(12)
+    X = torch.rand(2, 3, 256, 256, generator=gen, dtype=torch.float64)
+    Y = (X + 0.3 * torch.randn(2, 3, 256, 256, generator=gen, dtype=torch.float64)).clamp(0, 1).requires_grad_(True)
+    loss = 1 - O.ms_ssim(X, Y)
+    loss.backward()
+    assert abs(loss.item() - float(gv["MS_loss256"])) < 1e-9
+    gr = Y.grad.flatten()
+    assert abs(gr.norm().item() - float(gv["MS_grad256_norm"])) < 1e-9 * float(gv["MS_grad256_norm"])
+    for j in range(3):
+        assert abs(float(gr @ probe(gr.numel(), 61000 + j)) - gv["MS_grad256_dot"][j]) < 1e-8 * float(gv["MS_grad256_norm"]) * 600
