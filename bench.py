@@ -11,9 +11,13 @@ config 2 per GPU: 256x256 pairs, batch 16 per GPU, bf16 MFMA operands (fp32 accu
 fp32 master weights/activations), synthetic inputs resident in HBM, weak scaling.
 
 Printed JSON (rank 0): value = image-pairs/s over all ranks; "roofline" for the dominant kernel
-family (the implicit-GEMM MFMA kernel: algorithmic conv FLOPs / HIP-event time of its
-launches in the timed region, vs the dense bf16 MFMA peak); "cpu_baseline" = the CPU oracle
-(oracle/dsgan_cpu.py, a port of the reference step) timed on this host's cores.
+family: its algorithmic FLOPs and bytes per launch (every operand read / written once, in its
+stored dtype) over the HIP-event time of its launches in the timed region, bound = the resource
+that work needs longest at peak (dense bf16 MFMA 2.5 PF/s, HBM 8 TB/s), plus the PMC traffic
+and MFMA-busy of the same command from the committed rocprofv3 summaries under profiles/;
+"quality" (MS-SSIM Δ vs the fp32 oracle after 10 steps at the bench batch) and "cpu_baseline"
+(the oracle, a port of the reference step, timed on this host's cores over steps 3-7 of that
+same 10-step run) at N=1 only.
 """
 import argparse
 import json
@@ -32,48 +36,20 @@ PEAK_BF16_TFLOPS = 2500.0   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
 PEAK_F32_TFLOPS = 157.3
 
 
-def cpu_baseline(threads):
-    """Bounded sample of the same step on the CPU oracle: 1 warmup + 6 timed steps at 256^2, B=2
-    (~10-20 s of CPU work)."""
-    from oracle import dsgan_cpu as O
-    from oracle.recipe import make_params, synth_pair
-    torch.set_num_threads(threads)
-    gp = make_params(O.g_param_spec(), "ref", 1000)
-    dp = make_params(O.d_param_spec(), "ref", 5000)
-    vp = make_params(O.vgg_param_spec(False), "vgg", 7000)
-    st = O.OracleStep(gp, dp, vp, pool_size=50)
-    A, B = synth_pair(2, 256, seed=0)
-    st.step(A, B)
-    t0 = time.time()
-    steps = 6
-    for _ in range(steps):
-        st.step(A, B)
-    dt = time.time() - t0
-    return dict(value=round(2 * steps / dt, 4), unit="img/s", cores=threads, kind="port",
-                sample="oracle/dsgan_cpu.py OracleStep, fp32, 256x256, batch 2, %d timed steps after 1 warmup (%.1f s)" % (steps, dt))
+PEAK_HBM_GBS = 8000.0       # MI355X HBM3E (MI355X_MICROARCH.md)
 
 
-PMC_TRAFFIC = os.path.join(REPO, "profiles", "r01", "pmc_traffic.json")
+def reference_legs(steps=10, batch=16, size=256, threads=16, timed=(2, 7)):
+    """The two legs of the metric that need the reference's arithmetic, on ONE shared run:
 
-
-def pmc_traffic(family):
-    """HBM bytes per launch of a kernel family, from the committed rocprofv3 --pmc passes over
-    this same bench command (tools/gpu_pmc.sh -> tools/pmc_traffic.py; FETCH_SIZE doubled per
-    the gfx950 correction, + WRITE_SIZE).  None when that family was not profiled."""
-    try:
-        with open(PMC_TRAFFIC) as f:
-            fams = json.load(f)["families"]
-        return fams[family]["traffic_bytes_per_launch"] if family in fams else None
-    except (OSError, ValueError, KeyError):
-        return None
-
-
-def quality(steps=10, batch=2, size=256, threads=16):
-    """'MS-SSIM Δ vs ref' of the BASELINE metric.  The GPU model (bench precision) and the CPU
-    oracle (oracle/dsgan_cpu.py, the reference step restated in fp32 -- the checker, never the
-    thing measured) train `steps` steps from identical weights (the reference's own N(0, 0.02)
-    init recipe) on identical synthetic 256^2 pairs (pool_size 0).  Δ = |MS-SSIM(fake_gpu, real_B)
-    - MS-SSIM(fake_ref, real_B)| on the last step's fake_B, DSGAN/MS_SSIM.py:153 with data_range 1."""
+    * quality -- 'MS-SSIM Δ vs ref': the GPU model (bench precision) and the CPU oracle
+      (oracle/dsgan_cpu.py, the reference step restated in fp32 -- the checker, never the thing
+      measured) train `steps` steps from identical weights (the reference's own N(0, 0.02) init
+      recipe) on identical synthetic 256^2 pairs at the bench batch (pool_size 0).  Δ =
+      |MS-SSIM(fake_gpu, real_B) - MS-SSIM(fake_ref, real_B)| on the last step's fake_B,
+      DSGAN/MS_SSIM.py:153 with data_range 1.
+    * cpu_baseline -- the oracle's steps [timed[0], timed[1]) of that same run (BASELINE.md §3:
+      2 warm-up + 5 timed steps at B=16, 256^2, fp32) on `threads` host threads."""
     import random
     from oracle import dsgan_cpu as O
     from oracle.recipe import make_params, synth_pair
@@ -94,21 +70,44 @@ def quality(steps=10, batch=2, size=256, threads=16):
                 v.copy_(pr[k])
     ref = O.OracleStep(gp, dp, make_params(O.vgg_param_spec(False), "vgg", 7000), pool_size=0)
     t0 = time.time()
+    cpu_s = []
     for i in range(steps):
         A, B = synth_pair(batch, size, seed=100 + i)
         model.set_input({"A": A.cuda(), "B": B.cuda(), "A_paths": [""] * batch, "B_paths": [""] * batch})
         model.optimize_parameters()
+        tc = time.perf_counter()
         ref.step(A, B)
+        cpu_s.append(time.perf_counter() - tc)
+        print("[bench] reference leg step %d/%d: oracle %.1f s" % (i + 1, steps, cpu_s[-1]), file=sys.stderr, flush=True)
     fg = model.fake_B.detach().float().cpu()
     fo = ref.fake_B
     tgt = (B + 1) / 2
     m_gpu = O.ms_ssim((fg + 1) / 2, tgt).item()
     m_ref = O.ms_ssim((fo + 1) / 2, tgt).item()
     HF.set_precision(prec)
-    return {"msssim_delta": round(abs(m_gpu - m_ref), 6), "msssim_gpu": round(m_gpu, 6), "msssim_ref": round(m_ref, 6),
-            "msssim_gpu_vs_ref": round(O.ms_ssim(((fg + 1) / 2).clamp(0, 1), ((fo + 1) / 2).clamp(0, 1)).item(), 6),
-            "steps": steps, "batch": batch, "size": size, "init": "reference N(0,0.02) recipe", "precision": prec,
-            "ref": "oracle/dsgan_cpu.py fp32 (%d threads)" % threads, "seconds": round(time.time() - t0, 1)}
+    quality = {"msssim_delta": round(abs(m_gpu - m_ref), 6), "msssim_gpu": round(m_gpu, 6), "msssim_ref": round(m_ref, 6),
+               "msssim_gpu_vs_ref": round(O.ms_ssim(((fg + 1) / 2).clamp(0, 1), ((fo + 1) / 2).clamp(0, 1)).item(), 6),
+               "steps": steps, "batch": batch, "size": size, "init": "reference N(0,0.02) recipe", "precision": prec,
+               "ref": "oracle/dsgan_cpu.py fp32 (%d threads)" % threads, "seconds": round(time.time() - t0, 1)}
+    a, b = timed
+    ts = sum(cpu_s[a:b])
+    cpu = dict(value=round(batch * (b - a) / ts, 4), unit="img/s", cores=threads, kind="port",
+               sample="oracle/dsgan_cpu.py OracleStep (a port of the reference step), fp32, %dx%d, batch %d: "
+                      "steps %d-%d of the quality leg's %d (%d warm-up + %d timed, %.1f s), %d host threads"
+                      % (size, size, batch, a + 1, b, steps, a, b - a, ts, threads))
+    return quality, cpu
+
+
+def _profile_json(name):
+    """A committed rocprofv3 summary over this same bench command (profiles/r02, else r01)."""
+    for rnd in ("r02", "r01"):
+        path = os.path.join(REPO, "profiles", rnd, name)
+        try:
+            with open(path) as f:
+                return json.load(f)["families"], "profiles/%s/%s" % (rnd, name)
+        except (OSError, ValueError, KeyError):
+            continue
+    return {}, None
 
 
 def main():
@@ -122,6 +121,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-quality", action="store_true", help="skip the MS-SSIM delta leg")
     ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--quality-steps", type=int, default=10, help="steps of the shared quality / cpu_baseline leg")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -173,9 +173,37 @@ def main():
         imgs = args.batch * args.steps * world
         peak = PEAK_BF16_TFLOPS if args.precision == "bf16" else PEAK_F32_TFLOPS
         ach = ig["flops"] / (ig["total_ms"] * 1e-3) / 1e12 if ig["total_ms"] > 0 else 0.0
-        # dominant kernel: the contraction family with the most time in the timed steps
-        dom, (dn, dms, dfl) = max(fams.items(), key=lambda kv: kv[1][1])
-        dach = dfl / (dms * 1e-3) / 1e12 if dms > 0 else 0.0
+        # dominant kernel: the contraction family with the most time in the timed steps; its
+        # roofline bound is whichever resource its algorithmic work needs longest at peak
+        dom, (dn, dms, dfl, dby) = max(fams.items(), key=lambda kv: kv[1][1])
+        t_avg = dms / max(1, dn) * 1e-3
+        fl_l, by_l = dfl / max(1, dn), dby / max(1, dn)
+        mfma_ach, hbm_ach = fl_l / t_avg / 1e12, by_l / t_avg / 1e9
+        hbm_bound = by_l / (PEAK_HBM_GBS * 1e9) > fl_l / (peak * 1e12)
+        pmc_t, pmc_t_src = _profile_json("pmc_traffic.json")
+        pmc_m, pmc_m_src = _profile_json("mfma_pmc.json")
+        traffic = pmc_t.get(dom, {}).get("traffic_bytes_per_launch")
+        roof = {"bound": "hbm" if hbm_bound else "mfma", "kernel": dom,
+                "achieved": round(hbm_ach if hbm_bound else mfma_ach, 2), "peak": PEAK_HBM_GBS if hbm_bound else peak,
+                "unit": "GB/s" if hbm_bound else "TFLOP/s",
+                "frac": round(hbm_ach / PEAK_HBM_GBS if hbm_bound else mfma_ach / peak, 4),
+                "traffic": traffic,
+                "traffic_unit": "HBM bytes per launch, rocprofv3 PMC (FETCH_SIZE x2 + WRITE_SIZE) over this command: %s" % pmc_t_src,
+                "algorithmic_bytes_per_launch": round(by_l), "algorithmic_gflop_per_launch": round(fl_l / 1e9, 3),
+                "waste_ratio": round(traffic / by_l, 3) if traffic and by_l else None,
+                "mfma": {"achieved_tflops": round(mfma_ach, 2), "frac": round(mfma_ach / peak, 4),
+                         "pmc_mfma_busy": pmc_m.get(dom, {}).get("mfma_busy"), "pmc_source": pmc_m_src},
+                "hbm": {"achieved_gbs": round(hbm_ach, 1), "frac": round(hbm_ach / PEAK_HBM_GBS, 4)},
+                "launches_per_step": round(dn / args.steps, 2), "kernel_ms_per_step": round(dms / args.steps, 3),
+                "avg_launch_us": round(dms / max(1, dn) * 1e3, 1),
+                "all_contractions": {"achieved": round(ach, 2), "frac": round(ach / peak, 4),
+                                     "ms_per_step": round(ig["total_ms"] / args.steps, 3),
+                                     "gflop_per_step": round(ig["flops"] / args.steps / 1e9, 1),
+                                     "launches_per_step": ig["launches"] // max(1, args.steps)},
+                "families": {k: {"ms_per_step": round(v[1] / args.steps, 3),
+                                 "tflops": round(v[2] / (v[1] * 1e-3) / 1e12, 1) if v[1] > 0 else 0.0,
+                                 "gbs": round(v[3] / (v[1] * 1e-3) / 1e9, 1) if v[1] > 0 else 0.0}
+                             for k, v in sorted(fams.items(), key=lambda kv: -kv[1][1])}}
         out = {
             "metric": METRIC,
             "value": round(imgs / dt, 3),
@@ -193,38 +221,27 @@ def main():
                        "global_batch": args.batch * world, "per_gpu_batch": args.batch,
                        "image": [args.size, args.size], "parallelism": "dp%d" % world,
                        "baseline_config": ("configs[1]: 256x256, batch 16, bf16, 1xMI355X"
+                                           if (args.size, args.batch, world) == (256, 16, 1) else
+                                           "configs[2]: 256x256, batch 16/GPU, %dxMI355X, grad all-reduce over RCCL" % world
                                            if (args.size, args.batch) == (256, 16) else
-                                           "configs[4] shape: 512x512, batch 8/GPU (bf16 for the named fp16)"
+                                           "configs[3] shape: 256x256, batch 32/GPU (VGG16 perceptual + SSIM; "
+                                           "--ssim_loss ms_ssim is the MS-SSIM opt-in)"
+                                           if (args.size, args.batch) == (256, 32) else
+                                           "configs[4] shape (512x512, batch 8/GPU) in bf16 -- NOT configs[4] as named (fp16 is not implemented)"
                                            if (args.size, args.batch) == (512, 8) else
                                            "off-baseline shape %dx%d, batch %d" % (args.size, args.size, args.batch))},
-            "roofline": {"bound": "mfma", "kernel": dom,
-                         "achieved": round(dach, 2), "peak": peak, "unit": "TFLOP/s",
-                         "frac": round(dach / peak, 4), "traffic": pmc_traffic(dom),
-                         "traffic_unit": "HBM bytes per launch (rocprofv3 PMC, profiles/r01/pmc_traffic.json)",
-                         "traffic_gbs": (round(pmc_traffic(dom) / (dms / max(1, dn) * 1e-3) / 1e9, 1)
-                                         if pmc_traffic(dom) and dms > 0 else None),
-                         "launches_per_step": round(dn / args.steps, 2),
-                         "kernel_ms_per_step": round(dms / args.steps, 3),
-                         "avg_launch_us": round(dms / max(1, dn) * 1e3, 1),
-                         "gflop_per_launch": round(dfl / max(1, dn) / 1e9, 3),
-                         "all_contractions": {"achieved": round(ach, 2), "frac": round(ach / peak, 4),
-                                              "ms_per_step": round(ig["total_ms"] / args.steps, 3),
-                                              "gflop_per_step": round(ig["flops"] / args.steps / 1e9, 1),
-                                              "launches_per_step": ig["launches"] // max(1, args.steps)},
-                         "families": {k: {"ms_per_step": round(v[1] / args.steps, 3),
-                                          "tflops": round(v[2] / (v[1] * 1e-3) / 1e12, 1) if v[1] > 0 else 0.0}
-                                      for k, v in sorted(fams.items(), key=lambda kv: -kv[1][1])}},
+            "roofline": roof,
         }
-        if not args.no_cpu_baseline and world == 1:
+        if world == 1 and not (args.no_cpu_baseline and args.no_quality):
             try:
-                out["cpu_baseline"] = cpu_baseline(args.cpu_threads)
+                q, cpu = reference_legs(steps=args.quality_steps, batch=args.batch, size=args.size,
+                                        threads=args.cpu_threads)
+                if not args.no_quality:
+                    out["quality"] = q
+                if not args.no_cpu_baseline:
+                    out["cpu_baseline"] = cpu
             except Exception as e:  # reported, never fatal to the GPU measurement
-                out["cpu_baseline"] = {"error": repr(e)}
-        if not args.no_quality and world == 1:
-            try:
-                out["quality"] = quality(threads=args.cpu_threads)
-            except Exception as e:
-                out["quality"] = {"error": repr(e)}
+                out["cpu_baseline" if not args.no_cpu_baseline else "quality"] = {"error": repr(e)}
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -67,12 +67,12 @@ class KernelTimer:
         e0.record()
         return e0
 
-    def end(self, e0, flops, tag=None, fam="other"):
+    def end(self, e0, flops, tag=None, fam="other", nbytes=0):
         if e0 is None:
             return
         e1 = torch.cuda.Event(enable_timing=True)
         e1.record()
-        self.rec.append((e0, e1, flops, tag, fam))
+        self.rec.append((e0, e1, flops, tag, fam, nbytes))
 
     def summary(self):
         torch.cuda.synchronize()
@@ -81,14 +81,16 @@ class KernelTimer:
         return dict(launches=len(self.rec), total_ms=ms, flops=fl)
 
     def families(self):
-        """{kernel family: [launches, ms, algorithmic flops]} over the recorded launches."""
+        """{kernel family: [launches, ms, algorithmic flops, algorithmic bytes]} over the recorded
+        launches (bytes: every operand the launch must read or write once, in its stored dtype)."""
         torch.cuda.synchronize()
         out = {}
         for r in self.rec:
-            a = out.setdefault(r[4], [0, 0.0, 0.0])
+            a = out.setdefault(r[4], [0, 0.0, 0.0, 0.0])
             a[0] += 1
             a[1] += r[0].elapsed_time(r[1])
             a[2] += r[2]
+            a[3] += r[5]
         return out
 
     def table(self):
@@ -97,6 +99,11 @@ class KernelTimer:
 
 
 IGEMM_TIMER = KernelTimer()
+
+
+def _nb(*ts):
+    """HBM bytes of the given operands (None skipped): the algorithmic traffic of a launch."""
+    return float(sum(t.numel() * t.element_size() for t in ts if t is not None))
 
 
 def _conv_flops(N, Cin, Cout, KH, KW, Ho, Wo):
@@ -288,7 +295,8 @@ def conv_fwd_raw(x, w, b, stride, pad, act=None, out=None, pre=None, accumulate=
         call("dsgan_conv_fwd", ptr(x), xbs, ptr(w), ptr(b), ptr(y), ybs, ptr(pre), pbs, N, Cin, H, W,
              Cout, KH, KW, stride, pad, Ho, Wo, ACT[act], LRELU_SLOPE, int(accumulate), ACT[xact], _prec(),
              stream())
-    IGEMM_TIMER.end(e0, _conv_flops(N, Cin, Cout, KH, KW, Ho, Wo), ("fwd", N, Cin, H, W, Cout, KH, stride), fam)
+    IGEMM_TIMER.end(e0, _conv_flops(N, Cin, Cout, KH, KW, Ho, Wo), ("fwd", N, Cin, H, W, Cout, KH, stride), fam,
+                    _nb(x, w, b, y, pre) + (_nb(y) if accumulate else 0.0))
     return y
 
 
@@ -366,7 +374,8 @@ def conv_dgrad_raw(dy, w, x_shape, stride, pad, bias=None, act=None, gpre=None, 
         call("dsgan_conv_dgrad", ptr(dy), dybs, ptr(w), ptr(bias), ptr(dx), dxbs, None, 0, ptr(gpre), gbs,
              ACT[gact], N, Cin, H, W, Cout, KH, KW, stride, pad, Ho, Wo, ACT[act], LRELU_SLOPE,
              int(accumulate), _prec(), stream())
-    IGEMM_TIMER.end(e0, _conv_flops(N, Cin, Cout, KH, KW, Ho, Wo), ("dgrad", N, Cin, H, W, Cout, KH, stride), fam)
+    IGEMM_TIMER.end(e0, _conv_flops(N, Cin, Cout, KH, KW, Ho, Wo), ("dgrad", N, Cin, H, W, Cout, KH, stride), fam,
+                    _nb(dy, w, bias, dx, gpre) + (_nb(dx) if accumulate else 0.0))
     return dx
 
 
@@ -398,7 +407,7 @@ def conv_wgrad_raw(dy, x, dw, stride, pad, xact=None):
         call("dsgan_conv_wgrad", ptr(dy), dybs, ptr(x), xbs, ptr(dw), N, Cin, H, W, Cout, KH, KW,
              stride, pad, dy.shape[2], dy.shape[3], ACT[xact], _prec(), stream())
     IGEMM_TIMER.end(e0, _conv_flops(N, Cin, Cout, KH, KW, dy.shape[2], dy.shape[3]),
-                    ("wgrad", N, Cin, H, W, Cout, KH, stride), fam)
+                    ("wgrad", N, Cin, H, W, Cout, KH, stride), fam, _nb(dy, x, dw))
 
 
 def channel_sum_raw(dy, out):
@@ -677,7 +686,8 @@ class PwMlpFn(torch.autograd.Function):
             e0 = IGEMM_TIMER.begin()
             call("dsgan_mlp_fwd", ptr(h), hbs, ptr(bf16_weight(w1)), ptr(b1), ptr(bf16_weight(w2)), ptr(b2),
                  ptr(out), P * H * W, N, C, P, H * W, 1, stream())
-            IGEMM_TIMER.end(e0, _mlp_flops(N, C, P, H * W), ("mlp_fwd", N, C, H, W, P, 1, 1), "mlp_fwd_kernel")
+            IGEMM_TIMER.end(e0, _mlp_flops(N, C, P, H * W), ("mlp_fwd", N, C, H, W, P, 1, 1), "mlp_fwd_kernel",
+                            _nb(h, w1, b1, w2, b2) + 2 * _nb(out))
             ctx.save_for_backward(h, x, ws)
             return out
         w1v = w1.view(w1.shape[0], w1.shape[1], 1, 1)
@@ -692,12 +702,14 @@ class PwMlpFn(torch.autograd.Function):
             e0 = IGEMM_TIMER.begin()
             call("dsgan_pw_fwd_io", ptr(w1), ptr(h), hbs, 0, ptr(g), C4 * HW, 1, ptr(gp), C4 * HW, 1, ptr(b1), C4, C,
                  HW, N, ACT["gelu"], 0, LRELU_SLOPE, stream())
-            IGEMM_TIMER.end(e0, 2.0 * N * HW * C4 * C, ("fwd", N, C, H, W, C4, 1, 1), "pwgemm_kernel")
+            IGEMM_TIMER.end(e0, 2.0 * N * HW * C4 * C, ("fwd", N, C, H, W, C4, 1, 1), "pwgemm_kernel",
+                            _nb(h, w1, b1, g, gp))
             out = conv_fwd_raw(x, ws, None, 1, 0)
             e0 = IGEMM_TIMER.begin()
             call("dsgan_pw_fwd_io", ptr(w2), ptr(g), C4 * HW, 1, ptr(out), P * HW, 0, None, 0, 0, ptr(b2), P, C4,
                  HW, N, 0, 1, LRELU_SLOPE, stream())
-            IGEMM_TIMER.end(e0, 2.0 * N * HW * C4 * P, ("fwd", N, C4, H, W, P, 1, 1), "pwgemm_kernel")
+            IGEMM_TIMER.end(e0, 2.0 * N * HW * C4 * P, ("fwd", N, C4, H, W, P, 1, 1), "pwgemm_kernel",
+                            _nb(g, w2, b2) + 2 * _nb(out))
             ctx.g = g
             ctx.save_for_backward(h, x, gp, w1v, w2v, ws)
             return out
@@ -709,7 +721,8 @@ class PwMlpFn(torch.autograd.Function):
             e0 = IGEMM_TIMER.begin()
             call("dsgan_pw_small2", ptr(x4), xbs, ptr(ws), C, 1, ptr(z), 4 * C * H * W, ptr(w2), 4 * C, ptr(b2),
                  ptr(out), P * H * W, None, 0, N, C, P, H * W, 0, ACT["gelu"], 0, 0, LRELU_SLOPE, stream())
-            IGEMM_TIMER.end(e0, 2.0 * N * H * W * P * 5 * C, ("fwd", N, 5 * C, H, W, P, 1, 1), "pw_small_kernel")
+            IGEMM_TIMER.end(e0, 2.0 * N * H * W * P * 5 * C, ("fwd", N, 5 * C, H, W, P, 1, 1), "pw_small_kernel",
+                            _nb(x4, z, out, ws, w2, b2))
         else:
             out = conv_fwd_raw(x, ws, None, 1, 0)
             conv_fwd_raw(z, w2v, b2, 1, 0, out=out, accumulate=True, xact="gelu")
@@ -736,7 +749,7 @@ class PwMlpFn(torch.autograd.Function):
             call("dsgan_pw_dgrad_gbf", ptr(w2), ptr(dy), w2.shape[0] * H * W, ptr(dz), C4 * H * W, ptr(z), C4 * H * W,
                  C4, w2.shape[0], H * W, N, 0, stream())
             IGEMM_TIMER.end(e0, 2.0 * N * H * W * C4 * w2.shape[0], ("dgrad", N, C4, H, W, w2.shape[0], 1, 1),
-                            "pwgemm_kernel")
+                            "pwgemm_kernel", _nb(dy, w2, dz, z))
         else:
             dz = conv_dgrad_raw(dy, w2v, tuple(z.shape), 1, 0, gpre=z, gact="gelu")
         gw2, gb2, gws = _grad_buf(w2), _grad_buf(b2), _grad_buf(ws_ref)
@@ -747,7 +760,7 @@ class PwMlpFn(torch.autograd.Function):
             call("dsgan_pw_wgrad_mixed", ptr(dy4), dybs, 0, ptr(ctx.g), C4 * H * W, 1, ptr(gw2), w2.shape[0], C4,
                  H * W, N, stream())
             IGEMM_TIMER.end(e0, 2.0 * N * H * W * C4 * w2.shape[0], ("wgrad", N, C4, H, W, w2.shape[0], 1, 1),
-                            "pwgemm_kernel")
+                            "pwgemm_kernel", _nb(dy4, ctx.g, gw2))
         elif gw2 is not None:
             conv_wgrad_raw(dy, z, gw2.view(w2v.shape), 1, 0, xact="gelu")
         if gb2 is not None:
@@ -789,12 +802,14 @@ class PwMlpFn(torch.autograd.Function):
         e0 = IGEMM_TIMER.begin()
         call("dsgan_mlp_bwd", ptr(h), C * HW, ptr(dy), dybs, ptr(bf16_weight(w1)), ptr(b1), ptr(bf16_weight(w2)),
              ptr(dh), C * HW, ptr(g), ptr(dz), ptr(bsum), N, C, P, HW, stream())
-        IGEMM_TIMER.end(e0, _mlp_flops(N, C, P, HW), ("mlp_bwd", N, C, H, W, P, 1, 1), "mlp_bwd_kernel")
+        IGEMM_TIMER.end(e0, _mlp_flops(N, C, P, HW), ("mlp_bwd", N, C, H, W, P, 1, 1), "mlp_bwd_kernel",
+                        _nb(h, dy, w1, b1, w2, dh, g, dz, bsum))
         gw2, gb2, gws, gw1, gb1 = (_grad_buf(t) for t in (w2, b2, ws_ref, w1, b1))
         if gw2 is not None:
             e0 = IGEMM_TIMER.begin()
             call("dsgan_pw_wgrad_mixed", ptr(dy), dybs, 0, ptr(g), C4 * HW, 1, ptr(gw2), P, C4, HW, N, stream())
-            IGEMM_TIMER.end(e0, 2.0 * N * HW * C4 * P, ("wgrad", N, C4, H, W, P, 1, 1), "pwgemm_kernel")
+            IGEMM_TIMER.end(e0, 2.0 * N * HW * C4 * P, ("wgrad", N, C4, H, W, P, 1, 1), "pwgemm_kernel",
+                            _nb(dy, g, gw2))
         if gb2 is not None:
             channel_sum_raw(dy, gb2)
         if gws is not None:
@@ -802,7 +817,8 @@ class PwMlpFn(torch.autograd.Function):
         if gw1 is not None:
             e0 = IGEMM_TIMER.begin()
             call("dsgan_pw_wgrad_mixed", ptr(dz), C4 * HW, 1, ptr(h), C * HW, 0, ptr(gw1), C4, C, HW, N, stream())
-            IGEMM_TIMER.end(e0, 2.0 * N * HW * C4 * C, ("wgrad", N, C, H, W, C4, 1, 1), "pwgemm_kernel")
+            IGEMM_TIMER.end(e0, 2.0 * N * HW * C4 * C, ("wgrad", N, C, H, W, C4, 1, 1), "pwgemm_kernel",
+                            _nb(dz, h, gw1))
         if gb1 is not None:
             call("dsgan_colsum", ptr(bsum), ntiles, C4, ptr(gb1), stream())
         _params_done(*ctx.refs)
