@@ -67,12 +67,11 @@ __global__ __launch_bounds__(256) void dwconv_fwd_kernel(const float* __restrict
 template <int K>
 __global__ __launch_bounds__(256) void dwconv_wgrad_kernel(const float* __restrict__ dy, long dy_bs,
                                                            const float* __restrict__ x, long x_bs,
-                                                           float* __restrict__ dw,
-                                                           float* __restrict__ db, int C, int H,
+                                                           float* __restrict__ ws, int C, int H,
                                                            int W, int tiles_per_block) {
   __shared__ float xt[DW_HALO][DW_HALO + 1];
   __shared__ float gt[DW_T][DW_T + 1];
-  __shared__ float red[DW_MAXK * DW_MAXK];
+  __shared__ float part[(K * DW_T * 2 <= 256 ? 2 : 1) * K * DW_T][K];
   __shared__ float sh[4];
   const int plane = blockIdx.x;
   const int n = plane / C, c = plane - n * C;
@@ -130,25 +129,39 @@ __global__ __launch_bounds__(256) void dwconv_wgrad_kernel(const float* __restri
       }
     }
   }
-  // reduce: for each (kh, kw) sum over rows / column halves
-  __syncthreads();
-  for (int i = threadIdx.x; i < K * K; i += 256) red[i] = 0.f;
+  // reduce: for each (kh, kw) the sum over rows / column halves in a fixed order; this
+  // workgroup's K*K + 1 partials go to its slot of ws (dsgan_dwconv_wgrad sums the slots)
   __syncthreads();
 #pragma unroll
   for (int a = 0; a < 2; ++a) {
     const int it = threadIdx.x + a * 256;
     if (it < items) {
-      const int kh = it / (DW_T * QS);
 #pragma unroll
-      for (int kw = 0; kw < K; ++kw) atomicAdd(&red[kh * K + kw], acc[a][kw]);
+      for (int kw = 0; kw < K; ++kw) part[it][kw] = acc[a][kw];
     }
   }
-  __syncthreads();
-  for (int i = threadIdx.x; i < K * K; i += 256) atomicAdd(dw + c * K * K + i, red[i]);
-  if (db) {
-    const float bs = block_sum<256>(bacc, sh);
-    if (threadIdx.x == 0) atomicAdd(db + c, bs);
+  const float bs = block_sum<256>(bacc, sh);   // (its barrier also publishes part[])
+  float* slot = ws + ((long)c * (gridDim.y * (long)(gridDim.x / C)) + (long)n * gridDim.y + blockIdx.y) * (K * K + 1);
+  for (int i = threadIdx.x; i < K * K; i += 256) {
+    const int kh = i / K, kw = i - kh * K;
+    float v = 0.f;
+    for (int j = 0; j < DW_T * QS; ++j) v += part[kh * DW_T * QS + j][kw];
+    slot[i] = v;
   }
+  if (threadIdx.x == 0) slot[K * K] = bs;
+}
+
+// dw[c][i] += sum_g ws[c][g][i] (i < K*K), db[c] += sum_g ws[c][g][K*K]; g in order
+__global__ void dw_partial_reduce_kernel(const float* __restrict__ ws, int C, int G, int KK, float* __restrict__ dw,
+                                         float* __restrict__ db) {
+  const int t = blockIdx.x * 256 + threadIdx.x;
+  if (t >= C * (KK + 1)) return;
+  const int c = t / (KK + 1), i = t - c * (KK + 1);
+  const float* p = ws + (long)c * G * (KK + 1) + i;
+  float v = 0.f;
+  for (int g = 0; g < G; ++g) v += p[(long)g * (KK + 1)];
+  if (i < KK) dw[c * KK + i] += v;
+  else if (db) db[c] += v;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -271,7 +284,7 @@ __global__ __launch_bounds__(256, 4) void dwconv_fwd_v2(const float* __restrict_
 template <int K, int TWT, int THT, int R>
 __global__ __launch_bounds__(256, 4) void dwconv_wgrad_v2(const float* __restrict__ dy, long dy_bs,
                                                        const float* __restrict__ x, long x_bs,
-                                                       float* __restrict__ dw, float* __restrict__ db,
+                                                       float* __restrict__ ws,
                                                        int N, int C, int H, int W, int tiles_w, int nper) {
   using T = DwTile<K, TWT, THT, R>;
   __shared__ __attribute__((aligned(16))) float tile[T::LH][T::LW];
@@ -329,10 +342,10 @@ __global__ __launch_bounds__(256, 4) void dwconv_wgrad_v2(const float* __restric
     if (lane == 0) red[wv][K * K] = v;
   }
   __syncthreads();
-  if (threadIdx.x < K * K + 1) {
+  if (threadIdx.x < K * K + 1) {   // this workgroup's slot of ws (summed in order by dw_partial_reduce)
     const float v = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
-    if (threadIdx.x < K * K) atomicAdd(dw + c * K * K + threadIdx.x, v);
-    else if (db) atomicAdd(db + c, v);
+    const long g = (long)blockIdx.z * gridDim.x + blockIdx.x, G = (long)gridDim.z * gridDim.x;
+    ws[((long)c * G + g) * (K * K + 1) + threadIdx.x] = v;
   }
 }
 
@@ -356,19 +369,33 @@ static void dw_fwd_v2(const float* x, long x_bs, const float* w, const float* bi
                      y_bs, C, H, W, flip, accumulate, tw);
 }
 
+// images per workgroup of the tiled weight-grad: enough workgroups to fill the chip, as many
+// images each as that allows.  Returns the workgroups per channel (= partial slots).
 template <int K, int TWT, int THT, int R>
-static void dw_wgrad_v2(const float* dy, long dy_bs, const float* x, long x_bs, float* dw, float* db, int N, int C,
-                        int H, int W, hipStream_t st) {
+static long dw_wgrad_v2_plan(int N, int C, int H, int W, int* nsplit_out, int* nper_out) {
   using T = DwTile<K, TWT, THT, R>;
   const int tw = W / T::TW, th = (H + T::TH - 1) / T::TH;
-  // images per workgroup: enough workgroups to fill the chip, as many images each as that allows
   const long base = (long)tw * th * C;
   int nsplit = (int)((2048 + base - 1) / base);
   if (nsplit > N) nsplit = N;
   const int nper = (N + nsplit - 1) / nsplit;
   nsplit = (N + nper - 1) / nper;
-  hipLaunchKernelGGL((dwconv_wgrad_v2<K, TWT, THT, R>), dim3(tw * th, C, nsplit), dim3(256), 0, st, dy, dy_bs, x,
-                     x_bs, dw, db, N, C, H, W, tw, nper);
+  *nsplit_out = nsplit;
+  *nper_out = nper;
+  return (long)tw * th * nsplit;
+}
+
+template <int K, int TWT, int THT, int R>
+static long dw_wgrad_v2(const float* dy, long dy_bs, const float* x, long x_bs, float* ws, int N, int C, int H, int W,
+                        hipStream_t st) {
+  using T = DwTile<K, TWT, THT, R>;
+  const int tw = W / T::TW, th = (H + T::TH - 1) / T::TH;
+  int nsplit, nper;
+  const long G = dw_wgrad_v2_plan<K, TWT, THT, R>(N, C, H, W, &nsplit, &nper);
+  if (ws)
+    hipLaunchKernelGGL((dwconv_wgrad_v2<K, TWT, THT, R>), dim3(tw * th, C, nsplit), dim3(256), 0, st, dy, dy_bs, x,
+                       x_bs, ws, N, C, H, W, tw, nper);
+  return G;
 }
 
 // rows per thread: as many as the registers allow without spilling (K = 7, 9 windows are big)
@@ -381,13 +408,39 @@ static void dw_fwd_dispatch(int cfg, const float* x, long x_bs, const float* w, 
   else dw_fwd_v2<K, 8, 32, 1>(x, x_bs, w, bias, y, y_bs, N, C, H, W, flip, accumulate, st);
 }
 
+// ws == NULL: only the partial-slot count per channel is returned (workspace query)
 template <int K>
-static void dw_wgrad_dispatch(int cfg, const float* dy, long dy_bs, const float* x, long x_bs, float* dw, float* db,
+static long dw_wgrad_dispatch(int cfg, const float* dy, long dy_bs, const float* x, long x_bs, float* ws,
                               int N, int C, int H, int W, hipStream_t st) {
   constexpr int R1 = K >= 9 ? 4 : 8, R2 = K >= 9 ? 2 : 4;
-  if (cfg == 1) dw_wgrad_v2<K, 32, 8, R1>(dy, dy_bs, x, x_bs, dw, db, N, C, H, W, st);
-  else if (cfg == 2) dw_wgrad_v2<K, 16, 16, R2>(dy, dy_bs, x, x_bs, dw, db, N, C, H, W, st);
-  else dw_wgrad_v2<K, 8, 32, 1>(dy, dy_bs, x, x_bs, dw, db, N, C, H, W, st);
+  if (cfg == 1) return dw_wgrad_v2<K, 32, 8, R1>(dy, dy_bs, x, x_bs, ws, N, C, H, W, st);
+  if (cfg == 2) return dw_wgrad_v2<K, 16, 16, R2>(dy, dy_bs, x, x_bs, ws, N, C, H, W, st);
+  return dw_wgrad_v2<K, 8, 32, 1>(dy, dy_bs, x, x_bs, ws, N, C, H, W, st);
+}
+
+static long dw_wgrad_any(int K, int cfg, const float* dy, long dy_bs, const float* x, long x_bs, float* ws, int N,
+                         int C, int H, int W, hipStream_t st) {
+  switch (K) {
+    case 3: return dw_wgrad_dispatch<3>(cfg, dy, dy_bs, x, x_bs, ws, N, C, H, W, st);
+    case 5: return dw_wgrad_dispatch<5>(cfg, dy, dy_bs, x, x_bs, ws, N, C, H, W, st);
+    case 7: return dw_wgrad_dispatch<7>(cfg, dy, dy_bs, x, x_bs, ws, N, C, H, W, st);
+    default: return dw_wgrad_dispatch<9>(cfg, dy, dy_bs, x, x_bs, ws, N, C, H, W, st);
+  }
+}
+
+// generic kernel: (tiles per workgroup, workgroups per plane)
+static int dw_generic_groups(int N, int C, int H, int W, int* tpb_out) {
+  const int ntiles = cdiv(W, DW_T) * cdiv(H, DW_T);
+  int groups = (int)((2048 + (long)N * C - 1) / ((long)N * C));   // spread a plane's tiles when planes are few
+  if (groups > ntiles) groups = ntiles;
+  if (groups < 1) groups = 1;
+  const int tpb = (ntiles + groups - 1) / groups;
+  *tpb_out = tpb;
+  return (ntiles + tpb - 1) / tpb;
+}
+
+static bool dw_tiled_ok(int K, int cfg, const void* x, const void* dy, long x_bs, long dy_bs) {
+  return cfg && K >= 3 && ((uintptr_t)x & 15) == 0 && ((uintptr_t)dy & 15) == 0 && (x_bs & 3) == 0 && (dy_bs & 3) == 0;
 }
 
 }  // namespace dsg
@@ -427,36 +480,45 @@ int dsgan_dwconv_fwd(const float* x, long x_bs, const float* w, const float* bia
   return 0;
 }
 
-int dsgan_dwconv_wgrad(const float* dy, long dy_bs, const float* x, long x_bs, float* dw, float* db,
-                       int N, int C, int H, int W, int K, hipStream_t st) {
-  DSG_REQUIRE(dy && x && dw && K >= 1 && K <= DW_MAXK && (K & 1), "dsgan_dwconv_wgrad: bad args");
+// floats of partial-sum scratch dsgan_dwconv_wgrad needs (alignment as the call will see it)
+long dsgan_dwconv_wgrad_workspace(int N, int C, int H, int W, int K, int aligned16) {
   const int cfg = dw_cfg(H, W);
-  if (cfg && K >= 3 && ((uintptr_t)x & 15) == 0 && ((uintptr_t)dy & 15) == 0 && (x_bs & 3) == 0 && (dy_bs & 3) == 0) {
+  long G;
+  if (cfg && K >= 3 && aligned16) {
+    G = dw_wgrad_any(K, cfg, nullptr, 0, nullptr, 0, nullptr, N, C, H, W, 0);
+  } else {
+    int tpb;
+    G = (long)N * dw_generic_groups(N, C, H, W, &tpb);
+  }
+  return G * C * (K * K + 1);
+}
+
+// dw[c] += sum dy * x (KxK correlation), db[c] += sum dy: every workgroup writes its partial
+// sums to ws, dw_partial_reduce_kernel adds them in a fixed order (deterministic).
+int dsgan_dwconv_wgrad(const float* dy, long dy_bs, const float* x, long x_bs, float* dw, float* db,
+                       int N, int C, int H, int W, int K, float* ws, hipStream_t st) {
+  DSG_REQUIRE(dy && x && dw && ws && K >= 1 && K <= DW_MAXK && (K & 1), "dsgan_dwconv_wgrad: bad args");
+  const int cfg = dw_cfg(H, W);
+  long G;
+  if (dw_tiled_ok(K, cfg, x, dy, x_bs, dy_bs)) {
+    G = dw_wgrad_any(K, cfg, dy, dy_bs, x, x_bs, ws, N, C, H, W, st);
+  } else {
+    int tpb;
+    const int groups = dw_generic_groups(N, C, H, W, &tpb);
+    DSG_REQUIRE((long)N * C < (1L << 31) && groups <= 65535, "dsgan_dwconv_wgrad: grid too large");
+    const dim3 grid(N * C, groups);
     switch (K) {
-      case 3: dw_wgrad_dispatch<3>(cfg, dy, dy_bs, x, x_bs, dw, db, N, C, H, W, st); break;
-      case 5: dw_wgrad_dispatch<5>(cfg, dy, dy_bs, x, x_bs, dw, db, N, C, H, W, st); break;
-      case 7: dw_wgrad_dispatch<7>(cfg, dy, dy_bs, x, x_bs, dw, db, N, C, H, W, st); break;
-      default: dw_wgrad_dispatch<9>(cfg, dy, dy_bs, x, x_bs, dw, db, N, C, H, W, st); break;
+      case 3: hipLaunchKernelGGL(dwconv_wgrad_kernel<3>, grid, dim3(256), 0, st, dy, dy_bs, x, x_bs, ws, C, H, W, tpb); break;
+      case 5: hipLaunchKernelGGL(dwconv_wgrad_kernel<5>, grid, dim3(256), 0, st, dy, dy_bs, x, x_bs, ws, C, H, W, tpb); break;
+      case 7: hipLaunchKernelGGL(dwconv_wgrad_kernel<7>, grid, dim3(256), 0, st, dy, dy_bs, x, x_bs, ws, C, H, W, tpb); break;
+      case 9: hipLaunchKernelGGL(dwconv_wgrad_kernel<9>, grid, dim3(256), 0, st, dy, dy_bs, x, x_bs, ws, C, H, W, tpb); break;
+      default: DSG_REQUIRE(false, "dsgan_dwconv_wgrad: K must be 3, 5, 7 or 9");
     }
-    DSG_CHECK_LAUNCH();
-    return 0;
+    G = (long)N * groups;
   }
-  const int ntiles = cdiv(W, DW_T) * cdiv(H, DW_T);
-  // spread a plane's tiles over several workgroups when there are few planes
-  int groups = (int)((2048 + (long)N * C - 1) / ((long)N * C));
-  if (groups > ntiles) groups = ntiles;
-  if (groups < 1) groups = 1;
-  const int tpb = (ntiles + groups - 1) / groups;
-  groups = (ntiles + tpb - 1) / tpb;
-  DSG_REQUIRE((long)N * C < (1L << 31) && groups <= 65535, "dsgan_dwconv_wgrad: grid too large");
-  const dim3 grid(N * C, groups);
-  switch (K) {
-    case 3: hipLaunchKernelGGL(dwconv_wgrad_kernel<3>, grid, dim3(256), 0, st, dy, dy_bs, x, x_bs, dw, db, C, H, W, tpb); break;
-    case 5: hipLaunchKernelGGL(dwconv_wgrad_kernel<5>, grid, dim3(256), 0, st, dy, dy_bs, x, x_bs, dw, db, C, H, W, tpb); break;
-    case 7: hipLaunchKernelGGL(dwconv_wgrad_kernel<7>, grid, dim3(256), 0, st, dy, dy_bs, x, x_bs, dw, db, C, H, W, tpb); break;
-    case 9: hipLaunchKernelGGL(dwconv_wgrad_kernel<9>, grid, dim3(256), 0, st, dy, dy_bs, x, x_bs, dw, db, C, H, W, tpb); break;
-    default: DSG_REQUIRE(false, "dsgan_dwconv_wgrad: K must be 3, 5, 7 or 9");
-  }
+  const int KK = K * K;
+  hipLaunchKernelGGL(dw_partial_reduce_kernel, dim3(cdiv(C * (KK + 1), 256)), dim3(256), 0, st, ws, C, (int)G, KK, dw,
+                     db);
   DSG_CHECK_LAUNCH();
   return 0;
 }

@@ -11,7 +11,8 @@
 // GEMM views (NCHW activations, OIHW weights, P = Ho*Wo, Q = H*W, KK = KH*KW):
 //   FWD  : y[b,co,p]        M=Cout  N=B*P      K=Cin*KK   A=w (dense)      B=x  (im2col gather)
 //   DGRAD: dx[b,ci,q]       M=Cin   N=B*Q      K=Cout*KK  A=w^T (gather)   B=dy (col2im gather)
-//   WGRAD: dw[co,(ci,kk)]   M=Cout  N=Cin*KK   K=B*P      A=dy             B=x  (gather), split-K, atomics
+//   WGRAD: dw[co,(ci,kk)]   M=Cout  N=Cin*KK   K=B*P      A=dy             B=x  (gather), split-K into
+//          per-split partials reduced in a fixed order (pwgemm.hip launch_split_reduce): deterministic
 //   DGRAD2: stride-2 data-grad split into the 4 output parity classes (ph,pw).  Pixel
 //           ih = 2*ih'+ph only receives taps kh = kh0 + 2*th with kh0 = (ph+pad)&1, so each class
 //           is a dense stride-1 GEMM with K = Cout*ceil((KH-kh0)/2)*ceil((KW-kw0)/2): no MFMA
@@ -43,6 +44,7 @@ struct GemmArgs {
   const float* w;               // OIHW weights (FWD, DGRAD)
   int M, NN, K;
   int k_split;                  // WGRAD: K elements per split (multiple of BK)
+  float* ws;                    // WGRAD with splits > 1: partials [split][M][NN]
   // epilogue
   const float* bias;
   float* y;    long y_bs;
@@ -439,6 +441,7 @@ __global__ __launch_bounds__(256) void igemm_kernel(GemmArgs g) {
   // ---- epilogue ----
   // C/D layout (32x32): col = lane & 31, row = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)
   if (MODE == WGRAD) {
+    float* dst = g.ws ? g.ws + (long)split * g.M * g.NN : g.y;   // one split: the only writer, +=
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
       const int n = n0 + wn * TN * 32 + j * 32 + lr;
@@ -448,7 +451,10 @@ __global__ __launch_bounds__(256) void igemm_kernel(GemmArgs g) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int m = m0 + wm * TM * 32 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-          if (m < g.M) atomicAdd(g.y + (long)m * g.NN + n, acc[i][j][r]);
+          if (m < g.M) {
+            float* o = dst + (long)m * g.NN + n;
+            *o = g.ws ? acc[i][j][r] : *o + acc[i][j][r];
+          }
         }
     }
     return;
@@ -544,6 +550,25 @@ static void launch_mode(const GemmArgs& g, int prec, int splits, hipStream_t st)
   }
 }
 
+// K split of a weight-grad: about 640 workgroups, >= 8 K steps each, partials of at most a
+// quarter of the operand bytes (see pwgemm.hip wgrad_plan).
+static int igemm_wgrad_plan(int M, int NN, long K, int BK, int* k_split) {
+  const int BM = M > 64 ? 128 : (M > 32 ? 64 : 32);
+  const long tiles = (long)cdiv(NN, 128) * cdiv(M, BM);
+  long splits = (640 + tiles - 1) / tiles;
+  const long max_splits = (K + 8L * BK - 1) / (8L * BK);
+  const long byte_cap = ((long)(M + NN) * K) / (4L * M * NN);
+  if (splits > max_splits) splits = max_splits;
+  if (splits > byte_cap) splits = byte_cap;
+  if (splits < 1) splits = 1;
+  if (splits > 65535) splits = 65535;
+  long ks = (K + splits - 1) / splits;
+  ks = (ks + BK - 1) / BK * BK;
+  splits = (K + ks - 1) / ks;
+  *k_split = (int)ks;
+  return (int)splits;
+}
+
 }  // namespace dsg
 
 using namespace dsg;
@@ -625,11 +650,19 @@ int dsgan_conv_dgrad(const float* dy, long dy_bs, const float* w, const float* b
   return 0;
 }
 
+// floats of split-K scratch dsgan_conv_wgrad needs for this shape (0: no split)
+long dsgan_conv_wgrad_workspace(int N, int Cin, int Cout, int KH, int KW, int Ho, int Wo, int prec) {
+  int ks;
+  const int BK = prec == PREC_BF16 ? PT<PREC_BF16>::BK : PT<PREC_F32>::BK;
+  const int splits = igemm_wgrad_plan(Cout, Cin * KH * KW, (long)N * Ho * Wo, BK, &ks);
+  return splits > 1 ? (long)splits * Cout * Cin * KH * KW : 0;
+}
+
 // dw[Cout][Cin][KH][KW] += sum_b,p dy[b,co,p] * x[b,ci,p*stride-pad+k]   (caller zeroes dw once
 // per step; concurrent uses of one weight accumulate, as autograd would).
 int dsgan_conv_wgrad(const float* dy, long dy_bs, const float* x, long x_bs, float* dw, int N,
                      int Cin, int H, int W, int Cout, int KH, int KW, int stride, int pad, int Ho,
-                     int Wo, int xact, int prec, hipStream_t st) {
+                     int Wo, int xact, int prec, float* ws, hipStream_t st) {
   if (int e = check_geom(N, Cin, H, W, Cout, KH, KW, stride, pad, Ho, Wo, prec)) return e;
   DSG_REQUIRE(dy && x && dw, "dsgan_conv_wgrad: null pointer");
   GemmArgs g = base_args(N, Cin, H, W, Cout, KH, KW, stride, pad, Ho, Wo);
@@ -637,19 +670,11 @@ int dsgan_conv_wgrad(const float* dy, long dy_bs, const float* x, long x_bs, flo
   g.bact = xact;
   g.M = Cout; g.NN = Cin * KH * KW; g.K = N * Ho * Wo;
   const int BK = prec == PREC_BF16 ? PT<PREC_BF16>::BK : PT<PREC_F32>::BK;
-  const int BM = g.M > 64 ? 128 : (g.M > 32 ? 64 : 32);
-  const long tiles = (long)cdiv(g.NN, 128) * cdiv(g.M, BM);
-  // enough blocks to fill 256 CUs ~4 deep, but at least 8 K-steps per split
-  long splits = (1024 + tiles - 1) / tiles;
-  const long max_splits = (g.K + 8L * BK - 1) / (8L * BK);
-  if (splits > max_splits) splits = max_splits;
-  if (splits < 1) splits = 1;
-  if (splits > 65535) splits = 65535;
-  long ks = (g.K + splits - 1) / splits;
-  ks = (ks + BK - 1) / BK * BK;
-  splits = (g.K + ks - 1) / ks;
-  g.k_split = (int)ks;
-  launch_mode<WGRAD>(g, prec, (int)splits, st);
+  const int splits = igemm_wgrad_plan(g.M, g.NN, g.K, BK, &g.k_split);
+  DSG_REQUIRE(splits == 1 || ws, "dsgan_conv_wgrad: needs dsgan_conv_wgrad_workspace floats of scratch");
+  g.ws = splits > 1 ? ws : nullptr;
+  launch_mode<WGRAD>(g, prec, splits, st);
+  if (splits > 1) launch_split_reduce(ws, splits, (long)g.M * g.NN, dw, st);
   DSG_CHECK_LAUNCH();
   return 0;
 }

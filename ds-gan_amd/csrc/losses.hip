@@ -24,7 +24,7 @@ __global__ __launch_bounds__(256) void bce_fwd_kernel(const float* x, long n, fl
     s += fmaxf(v, 0.f) - v * t + log1pf(__expf(-fabsf(v)));
   }
   s = block_sum<256>(s, sh);
-  if (threadIdx.x == 0) atomicAdd(out, s * coef);
+  if (threadIdx.x == 0) out[blockIdx.x] = s;   // block partial (final_sum_kernel adds them in order)
 }
 __global__ void bce_bwd_kernel(const float* x, long n, float t, const float* gout, float coef, float* dx, int accumulate) {
   const float g = gout[0] * coef;
@@ -40,7 +40,7 @@ __global__ __launch_bounds__(256) void l1_fwd_kernel(const float* a, const float
   float s = 0.f;
   for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) s += fabsf(a[i] - b[i]);
   s = block_sum<256>(s, sh);
-  if (threadIdx.x == 0) atomicAdd(out, s * coef);
+  if (threadIdx.x == 0) out[blockIdx.x] = s;
 }
 // 16-byte form (both operands 16-byte aligned): float4 pairs, two in flight per thread; the
 // n % 4 tail is summed by block 0.
@@ -62,7 +62,7 @@ __global__ __launch_bounds__(256) void l1_fwd_v4_kernel(const float4* __restrict
   }
   if (blockIdx.x == 0 && (int)threadIdx.x < tail) s1 += fabsf(ta[threadIdx.x] - tb[threadIdx.x]);
   float s = block_sum<256>(s0 + s1, sh);
-  if (threadIdx.x == 0) atomicAdd(out, s * coef);
+  if (threadIdx.x == 0) out[blockIdx.x] = s;
 }
 __global__ void l1_bwd_kernel(const float* a, const float* b, long n, const float* gout, float coef, float* da, int accumulate) {
   const float g = gout[0] * coef;
@@ -85,7 +85,28 @@ __global__ __launch_bounds__(256) void tv_fwd_kernel(const float* y, long planes
     if (h + 1 < H) s += fabsf(y[i + W] - v);
   }
   s = block_sum<256>(s, sh);
-  if (threadIdx.x == 0) atomicAdd(out, s * coef);
+  if (threadIdx.x == 0) out[blockIdx.x] = s;
+}
+
+// out[0] = coef * sum_i part[i], i in a fixed order (deterministic loss values)
+__global__ __launch_bounds__(256) void final_sum_kernel(const float* __restrict__ part, int n, float coef,
+                                                        float* __restrict__ out) {
+  __shared__ float sh[4];
+  float s = 0.f;
+  for (int i = threadIdx.x; i < n; i += 256) s += part[i];
+  s = block_sum<256>(s, sh);
+  if (threadIdx.x == 0) out[0] = s * coef;
+}
+
+// stats[p][j] = sum over the tiles t of part[p][t][j], j in {0, 1} (fixed order)
+__global__ void plane_tile_sum_kernel(const float* __restrict__ part, int planes, int tiles, float* __restrict__ stats) {
+  const int t = blockIdx.x * 256 + threadIdx.x;
+  if (t >= planes * 2) return;
+  const int p = t >> 1, j = t & 1;
+  const float* q = part + (long)p * tiles * 2 + j;
+  float s = 0.f;
+  for (int i = 0; i < tiles; ++i) s += q[2L * i];
+  stats[t] = s;
 }
 __device__ __forceinline__ float sgnf(float d) { return d > 0.f ? 1.f : (d < 0.f ? -1.f : 0.f); }
 
@@ -235,9 +256,9 @@ __global__ __launch_bounds__(256) void ssim_fwd_kernel(SSIMArgs s, int tiles_w) 
       s.coef[o + 2 * stride] = k * (2.f * S / A2);
     }
   }
-  if (s.out) {
+  if (s.out) {   // per-tile partial sum of S (final_sum_kernel)
     ssum = block_sum<256>(ssum, sh);
-    if (threadIdx.x == 0) atomicAdd(s.out, ssum);
+    if (threadIdx.x == 0) s.out[(long)blockIdx.y * gridDim.x + blockIdx.x] = ssum;
   }
 }
 
@@ -351,7 +372,10 @@ __global__ __launch_bounds__(256) void ssim_eval_kernel(SSIMArgs s, int tiles_w,
   }
   ssum = block_sum<256>(ssum, sh);
   csum = block_sum<256>(csum, sh + 4);
-  if (threadIdx.x == 0) { atomicAdd(stats + 2 * plane, ssum); atomicAdd(stats + 2 * plane + 1, csum); }
+  if (threadIdx.x == 0) {   // per-(plane, tile) partials, summed over tiles by plane_tile_sum_kernel
+    float* q = stats + ((long)plane * gridDim.x + blockIdx.x) * 2;
+    q[0] = ssum; q[1] = csum;
+  }
 }
 
 // F.avg_pool2d(a*x+b, 2, padding=(H%2, W%2)) with count_include_pad (divisor 4), :213-215
@@ -504,10 +528,14 @@ using namespace dsg;
 
 extern "C" {
 
-int dsgan_bce_logits_fwd(const float* x, long n, float target, float* out, hipStream_t st) {
-  DSG_REQUIRE(x && out && n > 0, "dsgan_bce_logits_fwd: bad args");
-  hipMemsetAsync(out, 0, sizeof(float), st);
-  hipLaunchKernelGGL(bce_fwd_kernel, dim3(red_grid(n)), dim3(256), 0, st, x, n, target, out, 1.f / (float)n);
+// scratch floats the loss reductions below need for their block partials
+long dsgan_loss_parts(void) { return 4096; }
+
+int dsgan_bce_logits_fwd(const float* x, long n, float target, float* out, float* part, hipStream_t st) {
+  DSG_REQUIRE(x && out && part && n > 0, "dsgan_bce_logits_fwd: bad args");
+  const unsigned g = red_grid(n);
+  hipLaunchKernelGGL(bce_fwd_kernel, dim3(g), dim3(256), 0, st, x, n, target, part, 1.f);
+  hipLaunchKernelGGL(final_sum_kernel, dim3(1), dim3(256), 0, st, part, (int)g, 1.f / (float)n, out);
   DSG_CHECK_LAUNCH();
   return 0;
 }
@@ -517,19 +545,21 @@ int dsgan_bce_logits_bwd(const float* x, long n, float target, const float* gout
   DSG_CHECK_LAUNCH();
   return 0;
 }
-int dsgan_l1_fwd(const float* a, const float* b, long n, float* out, hipStream_t st) {
-  DSG_REQUIRE(a && b && out && n > 0, "dsgan_l1_fwd: bad args");
-  hipMemsetAsync(out, 0, sizeof(float), st);
+int dsgan_l1_fwd(const float* a, const float* b, long n, float* out, float* part, hipStream_t st) {
+  DSG_REQUIRE(a && b && out && part && n > 0, "dsgan_l1_fwd: bad args");
+  long g;
   if ((((uintptr_t)a | (uintptr_t)b) & 15) == 0) {
     const long n4 = n / 4;
-    long g = (n4 + 511) / 512;
+    g = (n4 + 511) / 512;
     if (g > 2048) g = 2048;
     if (g < 1) g = 1;
     hipLaunchKernelGGL(l1_fwd_v4_kernel, dim3((unsigned)g), dim3(256), 0, st, (const float4*)a, (const float4*)b, n4,
-                       a + n4 * 4, b + n4 * 4, (int)(n - n4 * 4), out, 1.f / (float)n);
+                       a + n4 * 4, b + n4 * 4, (int)(n - n4 * 4), part, 1.f);
   } else {
-    hipLaunchKernelGGL(l1_fwd_kernel, dim3(red_grid(n)), dim3(256), 0, st, a, b, n, out, 1.f / (float)n);
+    g = red_grid(n);
+    hipLaunchKernelGGL(l1_fwd_kernel, dim3((unsigned)g), dim3(256), 0, st, a, b, n, part, 1.f);
   }
+  hipLaunchKernelGGL(final_sum_kernel, dim3(1), dim3(256), 0, st, part, (int)g, 1.f / (float)n, out);
   DSG_CHECK_LAUNCH();
   return 0;
 }
@@ -561,10 +591,11 @@ int dsgan_vgg_tap_bwd(const float* dpool, const int* idx, const float* y, const 
   DSG_CHECK_LAUNCH();
   return 0;
 }
-int dsgan_tv_fwd(const float* y, long planes, int H, int W, float coef, float* out, hipStream_t st) {
-  DSG_REQUIRE(y && out && planes > 0, "dsgan_tv_fwd: bad args");
-  hipMemsetAsync(out, 0, sizeof(float), st);
-  hipLaunchKernelGGL(tv_fwd_kernel, dim3(red_grid(planes * H * W)), dim3(256), 0, st, y, planes, H, W, out, coef);
+int dsgan_tv_fwd(const float* y, long planes, int H, int W, float coef, float* out, float* part, hipStream_t st) {
+  DSG_REQUIRE(y && out && part && planes > 0, "dsgan_tv_fwd: bad args");
+  const unsigned g = red_grid(planes * H * W);
+  hipLaunchKernelGGL(tv_fwd_kernel, dim3(g), dim3(256), 0, st, y, planes, H, W, part, 1.f);
+  hipLaunchKernelGGL(final_sum_kernel, dim3(1), dim3(256), 0, st, part, (int)g, coef, out);
   DSG_CHECK_LAUNCH();
   return 0;
 }
@@ -588,11 +619,17 @@ int dsgan_img_metrics(const float* fake, const float* real, int C, int H, int W,
 
 static inline int ms_half(int h) { return (h + 2 * (h % 2) - 2) / 2 + 1; }
 
-// floats of `work` dsgan_ms_ssim needs: the two largest pyramid levels of X and Y (ping-pong)
+// per-(plane, tile) partials of the first (largest) scale: the fixed-order plane sums
+static long ms_tile_parts(long planes, int H, int W) {
+  return planes * cdiv(H - SS_K + 1, SS_T) * cdiv(W - SS_K + 1, SS_T) * 2;
+}
+
+// floats of `work` dsgan_ms_ssim needs: the two largest pyramid levels of X and Y (ping-pong),
+// then the tile partials
 long dsgan_ms_ssim_workspace(int N, int C, int H, int W) {
   const long p = (long)N * C;
   const int h1 = ms_half(H), w1 = ms_half(W), h2 = ms_half(h1), w2 = ms_half(w1);
-  return 2 * p * ((long)h1 * w1 + (long)h2 * w2);
+  return 2 * p * ((long)h1 * w1 + (long)h2 * w2) + ms_tile_parts(p, H, W);
 }
 
 // MS-SSIM of (a*real+b, a*fake+b): levels = number of weights (host array, <= 8), each scale
@@ -608,19 +645,22 @@ int dsgan_ms_ssim(const float* real, const float* fake, float a, float b, int N,
   DSG_REQUIRE(((H < W ? H : W) > (SS_K - 1) * (1 << (levels - 1))),
               "dsgan_ms_ssim: image smaller than the (win_size-1)*2^(levels-1) ms-ssim minimum");
   const int planes = N * C;
-  hipMemsetAsync(stats, 0, sizeof(float) * 2 * planes * levels, st);
   MsArgs m{};
   const float* xr = real;
   const float* yr = fake;
   float ca = a, cb = b;
   const long big = 2L * planes * ms_half(H) * ms_half(W);
   float* bufs[2] = {work, work + big};
+  const int h1 = ms_half(H), w1 = ms_half(W);
+  float* tparts = work + 2L * planes * ((long)h1 * w1 + (long)ms_half(h1) * ms_half(w1));
   int h = H, w = W;
   for (int l = 0; l < levels; ++l) {
     const int Ho = h - SS_K + 1, Wo = w - SS_K + 1;
     SSIMArgs s{xr, yr, ca, cb, planes, h, w, win11, C1, C2, nullptr, nullptr, nullptr, 0};
     const int tw = cdiv(Wo, SS_T), th = cdiv(Ho, SS_T);
-    hipLaunchKernelGGL(ssim_eval_kernel, dim3(tw * th, planes), dim3(256), 0, st, s, tw, stats + (long)l * planes * 2);
+    hipLaunchKernelGGL(ssim_eval_kernel, dim3(tw * th, planes), dim3(256), 0, st, s, tw, tparts);
+    hipLaunchKernelGGL(plane_tile_sum_kernel, dim3(cdiv(2 * planes, 256)), dim3(256), 0, st, tparts, planes, tw * th,
+                       stats + (long)l * planes * 2);
     m.inv_cnt[l] = 1.f / ((float)Ho * (float)Wo);
     m.wt[l] = weights_host[l];
     if (l < levels - 1) {
@@ -658,6 +698,7 @@ long dsgan_ms_ssim_train_workspace(int N, int C, int H, int W, int levels) {
   if (levels > 1) n += 2 * p * hs[1] * ws[1];
   n += (long)levels * p;
   n += 3 * p * (long)(H - SS_K + 1) * (W - SS_K + 1);
+  n += ms_tile_parts(p, H, W);
   return n;
 }
 
@@ -683,17 +724,20 @@ int dsgan_ms_ssim_fwd_train(const float* real, const float* fake, float a, float
   const int planes = N * C;
   int hs[8], ws[8];
   ms_dims(H, W, levels, hs, ws);
-  hipMemsetAsync(stats, 0, sizeof(float) * 2 * planes * levels, st);
   const float* xr = real;
   const float* yr = fake;
   float ca = a, cb = b;
   float* lvl = work;
+  // tile partials live at the end of the workspace (layout of dsgan_ms_ssim_train_workspace)
+  float* tparts = work + dsgan_ms_ssim_train_workspace(N, C, H, W, levels) - ms_tile_parts(planes, H, W);
   for (int l = 0; l < levels; ++l) {
     const int h = hs[l], w = ws[l];
     const int Ho = h - SS_K + 1, Wo = w - SS_K + 1;
     SSIMArgs s{xr, yr, ca, cb, planes, h, w, win11, C1, C2, nullptr, nullptr, nullptr, 0};
     const int tw = cdiv(Wo, SS_T), th = cdiv(Ho, SS_T);
-    hipLaunchKernelGGL(ssim_eval_kernel, dim3(tw * th, planes), dim3(256), 0, st, s, tw, stats + (long)l * planes * 2);
+    hipLaunchKernelGGL(ssim_eval_kernel, dim3(tw * th, planes), dim3(256), 0, st, s, tw, tparts);
+    hipLaunchKernelGGL(plane_tile_sum_kernel, dim3(cdiv(2 * planes, 256)), dim3(256), 0, st, tparts, planes, tw * th,
+                       stats + (long)l * planes * 2);
     if (l < levels - 1) {
       const int h2 = hs[l + 1], w2 = ws[l + 1];
       const long n2 = (long)planes * h2 * w2;
@@ -770,15 +814,20 @@ int dsgan_ms_ssim_bwd(const float* real, const float* fake, float a, float b, in
 }
 
 // out = sum of the SSIM map (caller divides by planes*Ho*Wo); coef: [3][planes][Ho][Wo] scratch
+// tile partials dsgan_ssim_fwd needs (one per 32x32 output tile and plane)
+long dsgan_ssim_parts(int planes, int H, int W) {
+  return (long)planes * cdiv(H - SS_K + 1, SS_T) * cdiv(W - SS_K + 1, SS_T);
+}
+
 int dsgan_ssim_fwd(const float* real, const float* fake, float a, float b, int planes, int H, int W,
-                   const float* win11, float C1, float C2, float* coef, float* out, hipStream_t st) {
-  DSG_REQUIRE(real && fake && win11 && coef && out && H >= SS_K && W >= SS_K && planes > 0 && planes <= 65535,
+                   const float* win11, float C1, float C2, float* coef, float* out, float* part, hipStream_t st) {
+  DSG_REQUIRE(real && fake && win11 && coef && out && part && H >= SS_K && W >= SS_K && planes > 0 && planes <= 65535,
               "dsgan_ssim_fwd: bad args (H,W >= 11 required)");
-  SSIMArgs s{real, fake, a, b, planes, H, W, win11, C1, C2, coef, out, nullptr, 0};
+  SSIMArgs s{real, fake, a, b, planes, H, W, win11, C1, C2, coef, part, nullptr, 0};
   const int Ho = H - SS_K + 1, Wo = W - SS_K + 1;
   const int tw = cdiv(Wo, SS_T), th = cdiv(Ho, SS_T);
-  hipMemsetAsync(out, 0, sizeof(float), st);
   hipLaunchKernelGGL(ssim_fwd_kernel, dim3(tw * th, planes), dim3(256), 0, st, s, tw);
+  hipLaunchKernelGGL(final_sum_kernel, dim3(1), dim3(256), 0, st, part, tw * th * planes, 1.f, out);
   DSG_CHECK_LAUNCH();
   return 0;
 }

@@ -475,22 +475,6 @@ __global__ __launch_bounds__(NW * 64, 1) void mlp_bwd_kernel(MlpArgs g) {
     }
 }
 
-// out[c] += sum_r part[r][c]: block (column group of 64, row group of 64 * 4)
-__global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ part, int rows, int cols,
-                                                     float* __restrict__ out) {
-  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
-  const int q = threadIdx.x >> 6;
-  const int r0 = blockIdx.y * 256, r1 = min(rows, r0 + 256);
-  __shared__ float sh[4][64];
-  float acc = 0.f;
-  if (c < cols)
-    for (int r = r0 + q; r < r1; r += 4) acc += part[(long)r * cols + c];
-  sh[q][threadIdx.x & 63] = acc;
-  __syncthreads();
-  if (q == 0 && c < cols)
-    atomicAdd(out + c, sh[0][threadIdx.x] + sh[1][threadIdx.x] + sh[2][threadIdx.x] + sh[3][threadIdx.x]);
-}
-
 __global__ __launch_bounds__(256) void f32_to_bf16_kernel(const float* __restrict__ s, __bf16* __restrict__ d, long n) {
   for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) d[i] = (__bf16)s[i];
 }
@@ -570,7 +554,7 @@ int dsgan_mlp_bwd(const float* h, long h_bs, const float* dy, long dy_bs, const 
 
 int dsgan_colsum(const float* part, int rows, int cols, float* out, hipStream_t st) {
   DSG_REQUIRE(part && out && rows > 0 && cols > 0, "dsgan_colsum: bad args");
-  hipLaunchKernelGGL(colsum_kernel, dim3(cdiv(cols, 64), cdiv(rows, 256)), dim3(256), 0, st, part, rows, cols, out);
+  launch_split_reduce(part, rows, cols, out, st);   // rows summed in a fixed order (deterministic)
   DSG_CHECK_LAUNCH();
   return 0;
 }

@@ -691,9 +691,12 @@ __global__ __launch_bounds__(256) void ca_bwd_kernel(const float* datt, const fl
                                                      const float* avg, const float* mx,
                                                      const float* hsave, const float* w1,
                                                      const float* w2, const float* pa, float* davg,
-                                                     float* dmx, float* dw1, float* dw2, float* dpa,
-                                                     int C, int R) {
+                                                     float* dmx, float* ws, int want_w1, int want_w2,
+                                                     int want_pa, int C, int R) {
+  // per-image partials (summed over images in a fixed order by launch_split_reduce):
+  // ws = [N][R*C] dw1 | [N][C*R] dw2 | [N] dpa
   extern __shared__ float sm[];
+  __shared__ float dal_w[16];
   float* dO = sm;           // C
   float* hp = dO + C;       // R
   float* dha = hp + R;      // R
@@ -722,17 +725,25 @@ __global__ __launch_bounds__(256) void ca_bwd_kernel(const float* datt, const fl
       dal += (ha > 0.f ? 0.f : ha * dp) + (hm > 0.f ? 0.f : hm * dp);
     }
   }
-  if (dpa && l == 0 && dal != 0.f) atomicAdd(dpa, dal);
+  if (l == 0) dal_w[wid] = dal;
   __syncthreads();
-  if (dw2)
-    for (int e = threadIdx.x; e < C * R; e += blockDim.x) atomicAdd(dw2 + e, dO[e / R] * hp[e % R]);
+  const int N = gridDim.x;
+  float* ws_w1 = ws + (long)n * R * C;
+  float* ws_w2 = ws + (long)N * R * C + (long)n * C * R;
+  if (want_pa && threadIdx.x == 0) {
+    float t = 0.f;
+    for (int w = 0; w < (int)(blockDim.x / 64); ++w) t += dal_w[w];
+    ws[2L * N * R * C + n] = t;
+  }
+  if (want_w2)
+    for (int e = threadIdx.x; e < C * R; e += blockDim.x) ws_w2[e] = dO[e / R] * hp[e % R];
   for (int c = threadIdx.x; c < C; c += blockDim.x) {
     float ga = 0.f, gm = 0.f;
     const float va = avg[n * C + c], vm = mx[n * C + c];
     for (int j = 0; j < R; ++j) {
       const float w = w1[j * C + c];
       ga += w * dha[j]; gm += w * dhm[j];
-      if (dw1) atomicAdd(dw1 + j * C + c, dha[j] * va + dhm[j] * vm);
+      if (want_w1) ws_w1[j * C + c] = dha[j] * va + dhm[j] * vm;
     }
     davg[n * C + c] = ga; dmx[n * C + c] = gm;
   }
@@ -845,7 +856,8 @@ __global__ void act_bwd_kernel(const float* dy, const float* pre, float* dx, lon
   }
 }
 
-// out[c] += sum_{n,p} dy[n,c,p]   (bias gradient; NT threads per (n,c) plane, atomics over n)
+// part[n*C + c] = sum_p dy[n,c,p]   (bias gradient, one plane per NT threads; the sum over n is
+// launch_split_reduce's fixed-order pass -- deterministic)
 template <int NT>
 __global__ __launch_bounds__(256) void channel_sum_kernel(const float* dy, long dy_bs, float* out, int N, int C, int HW) {
   __shared__ float sh[4];
@@ -873,7 +885,7 @@ __global__ __launch_bounds__(256) void channel_sum_kernel(const float* dy, long 
     for (int i = t; i < HW; i += NT) s += p[i];
   }
   s = NT == 64 ? warp_sum(s) : block_sum<NT>(s, sh);
-  if (t == 0) atomicAdd(out + c, s);
+  if (t == 0) out[plane] = s;
 }
 
 static inline unsigned grid_for(long n, int bs = 256) {
@@ -1038,11 +1050,14 @@ int dsgan_ca_fwd(const float* avg, const float* mx, const float* w1, const float
 int dsgan_ca_bwd(const float* datt, const float* att, const float* avg, const float* mx,
                  const float* hsave, const float* w1, const float* w2, const float* prelu_a,
                  float* davg, float* dmx, float* dw1, float* dw2, float* dprelu_a, int N, int C,
-                 int R, hipStream_t st) {
-  DSG_REQUIRE(C > 0 && R > 0 && C <= 4096, "dsgan_ca_bwd: bad dims");
+                 int R, float* ws, hipStream_t st) {
+  DSG_REQUIRE(C > 0 && R > 0 && C <= 4096 && ws, "dsgan_ca_bwd: bad dims / ws (N*(2*R*C+1) floats)");
   const size_t shm = (C + 3 * R) * sizeof(float);
   hipLaunchKernelGGL(ca_bwd_kernel, dim3(N), dim3(256), shm, st, datt, att, avg, mx, hsave, w1, w2,
-                     prelu_a, davg, dmx, dw1, dw2, dprelu_a, C, R);
+                     prelu_a, davg, dmx, ws, dw1 != nullptr, dw2 != nullptr, dprelu_a != nullptr, C, R);
+  if (dw1) launch_split_reduce(ws, N, (long)R * C, dw1, st);
+  if (dw2) launch_split_reduce(ws + (long)N * R * C, N, (long)C * R, dw2, st);
+  if (dprelu_a) launch_split_reduce(ws + 2L * N * R * C, N, 1, dprelu_a, st);
   DSG_CHECK_LAUNCH();
   return 0;
 }
@@ -1105,12 +1120,13 @@ int dsgan_act_bwd(const float* dy, const float* pre, float* dx, long n, int act,
   return 0;
 }
 
-int dsgan_channel_sum(const float* dy, long dy_bs, float* out, int N, int C, int HW, hipStream_t st) {
-  DSG_REQUIRE(dy && out && N > 0 && C > 0 && HW > 0, "dsgan_channel_sum: bad args");
+int dsgan_channel_sum(const float* dy, long dy_bs, float* out, int N, int C, int HW, float* ws, hipStream_t st) {
+  DSG_REQUIRE(dy && out && ws && N > 0 && C > 0 && HW > 0, "dsgan_channel_sum: bad args (ws: N*C floats)");
   if (HW <= 8192)
-    hipLaunchKernelGGL(channel_sum_kernel<64>, dim3(cdiv((long)N * C, 4)), dim3(256), 0, st, dy, dy_bs, out, N, C, HW);
+    hipLaunchKernelGGL(channel_sum_kernel<64>, dim3(cdiv((long)N * C, 4)), dim3(256), 0, st, dy, dy_bs, ws, N, C, HW);
   else
-    hipLaunchKernelGGL(channel_sum_kernel<256>, dim3(N * C), dim3(256), 0, st, dy, dy_bs, out, N, C, HW);
+    hipLaunchKernelGGL(channel_sum_kernel<256>, dim3(N * C), dim3(256), 0, st, dy, dy_bs, ws, N, C, HW);
+  launch_split_reduce(ws, N, C, out, st);
   DSG_CHECK_LAUNCH();
   return 0;
 }

@@ -15,7 +15,9 @@
 // Modes (P = H*W pixels per image, all tensors NCHW / [out,in] weights, fp32 in HBM):
 //   FWD  : Y[b][m][p]  = act( sum_k W[m][k] * xact(X[b][k][p]) + bias[m] ) (+Y)   (ypre = pre-act)
 //   DGRAD: DX[b][m][p] = ( sum_k W[k][m] * DY[b][k][p] ) * gact'(G[b][m][p])
-//   WGRAD: DW[m][n]   += sum_{b,p} DY[b][m][p] * xact(X[b][n][p])     (split over pixels, atomics)
+//   WGRAD: DW[m][n]   += sum_{b,p} DY[b][m][p] * xact(X[b][n][p])     (split over pixels: each split
+//          writes its partial tile to a workspace, pw_wgrad_reduce_kernel adds the splits in a fixed
+//          order -- deterministic, and plain stores stream faster than float atomics)
 #include "common.h"
 #include <stdlib.h>
 
@@ -40,6 +42,7 @@ struct PwArgs {
   int M, N, K, P;
   int act, gact, bact, accumulate; float slope;
   int k_split;
+  float* ws;                   // WGRAD with splits > 1: partials [split][M][N]
   unsigned a_range, b_range;   // buffer-resource byte ranges of A and B (B: per image for FWD/DGRAD)
   int y_bf16;  // FWD: Y is bf16 [b][M][P] (y_bs in elements)
   int gbf;     // FWD: ypre is bf16 and receives act'(pre);  DGRAD: gpre is a bf16 multiplier (no act')
@@ -319,6 +322,8 @@ __global__ __launch_bounds__(256, 2) void pwgemm_kernel(PwArgs g) {
 
   // ---- epilogue ----
   if (MODE == PW_WGRAD) {
+    // splits > 1: this split's partial tile (plain stores); one split: the only writer, +=
+    float* dst = g.ws ? g.ws + (long)split * g.M * g.N : g.Y;
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
       const int n = n0 + wn * TN * 32 + j * 32 + lr;
@@ -328,7 +333,10 @@ __global__ __launch_bounds__(256, 2) void pwgemm_kernel(PwArgs g) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int m = m0 + wm * TM * 32 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-          if (m < g.M) atomicAdd(g.Y + (long)m * g.N + n, acc[i][j][r]);
+          if (m < g.M) {
+            float* o = dst + (long)m * g.N + n;
+            *o = g.ws ? acc[i][j][r] : *o + acc[i][j][r];
+          }
         }
     }
     return;
@@ -430,18 +438,54 @@ static void pw_launch(const PwArgs& g, int splits, hipStream_t st) {
   hipLaunchKernelGGL((pwgemm_kernel<MODE, BM, ABF, BBF>), dim3((unsigned)((long)mt * nt * splits)), dim3(256), 0, st, g);
 }
 
-// K split of a weight-grad launch: enough workgroups to fill the chip, >= 8 K steps each.
-static int wgrad_split(PwArgs& g, int BM) {
-  const long tiles = (long)((g.M + BM - 1) / BM) * ((g.N + 127) / 128);
-  long splits = (2048 + tiles - 1) / tiles;
-  const long max_splits = (g.K + 8L * PBK - 1) / (8L * PBK);
+// dw[e] += sum_s ws[s][e], s in a fixed order: thread (e, j) sums s = j, j+4, ... in order, then
+// the four partial sums are added j = 0..3 -- the same tree on every run.
+__global__ __launch_bounds__(256) void pw_wgrad_reduce_kernel(const float* __restrict__ ws, int S, long MN,
+                                                              float* __restrict__ dw) {
+  __shared__ float sh[4][64];
+  const int el = threadIdx.x & 63, j = threadIdx.x >> 6;
+  const long e = (long)blockIdx.x * 64 + el;
+  float a = 0.f;
+  if (e < MN) {
+    int s = j;
+    for (; s + 12 < S; s += 16) {
+      const float v0 = ws[(long)s * MN + e], v1 = ws[(long)(s + 4) * MN + e];
+      const float v2 = ws[(long)(s + 8) * MN + e], v3 = ws[(long)(s + 12) * MN + e];
+      a += v0; a += v1; a += v2; a += v3;
+    }
+    for (; s < S; s += 4) a += ws[(long)s * MN + e];
+  }
+  sh[j][el] = a;
+  __syncthreads();
+  if (j == 0 && e < MN) dw[e] += ((sh[0][el] + sh[1][el]) + sh[2][el]) + sh[3][el];
+}
+
+// K (pixel) split of a weight-grad launch: about 640 workgroups (2.5 per CU: enough bytes in
+// flight to stream HBM), >= 8 K steps each, and partials of at most a quarter of the operand
+// bytes (each split writes, and the reduce reads, an M x N fp32 tile).
+static int wgrad_plan(int M, int N, long K, int BM, int* k_split) {
+  const long tiles = (long)((M + BM - 1) / BM) * ((N + 127) / 128);
+  long splits = (640 + tiles - 1) / tiles;
+  const long max_splits = (K + 8L * PBK - 1) / (8L * PBK);
+  const long byte_cap = ((long)(M + N) * K) / (4L * M * N);
   if (splits > max_splits) splits = max_splits;
+  if (splits > byte_cap) splits = byte_cap;
   if (splits < 1) splits = 1;
-  long ks = (g.K + splits - 1) / splits;
+  long ks = (K + splits - 1) / splits;
   ks = (ks + PBK - 1) / PBK * PBK;
-  splits = (g.K + ks - 1) / ks;
-  g.k_split = (int)ks;
+  splits = (K + ks - 1) / ks;
+  *k_split = (int)ks;
   return (int)splits;
+}
+static int wgrad_split(PwArgs& g, int BM) { return wgrad_plan(g.M, g.N, g.K, BM, &g.k_split); }
+
+// dw[e] += sum_s ws[s][e] (fixed order); shared with the implicit-GEMM weight-grad (igemm.hip)
+void launch_split_reduce(const float* ws, int splits, long MN, float* dw, hipStream_t st) {
+  hipLaunchKernelGGL(pw_wgrad_reduce_kernel, dim3((unsigned)((MN + 63) / 64)), dim3(256), 0, st, ws, splits, MN, dw);
+}
+
+static void wgrad_finish(const PwArgs& g, int splits, hipStream_t st) {
+  if (splits > 1) launch_split_reduce(g.ws, splits, (long)g.M * g.N, g.Y, st);
 }
 
 static bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
@@ -478,7 +522,7 @@ extern "C" int dsgan_pw_supported(int mode, int M, int K, int P, long a_bs, long
 extern "C" int dsgan_pw_gemm(int mode, const float* A, long a_bs, const float* B, long b_bs,
                              float* Y, long y_bs, const float* bias, float* ypre, long ypre_bs,
                              const float* gpre, long gpre_bs, int M, int N, int K, int P, int nb,
-                             int act, int gact, int bact, int accumulate, float slope,
+                             int act, int gact, int bact, int accumulate, float slope, float* ws,
                              hipStream_t st) {
   DSG_REQUIRE(A && B && Y && M > 0 && N > 0 && K > 0 && P > 0 && nb > 0, "dsgan_pw_gemm: bad args");
   PwArgs g{};
@@ -495,8 +539,11 @@ extern "C" int dsgan_pw_gemm(int mode, const float* A, long a_bs, const float* B
     g.M = M; g.N = N; g.K = nb * P;
     const int BM = M > 64 ? 128 : 64;
     const int splits = wgrad_split(g, BM);
+    DSG_REQUIRE(splits == 1 || ws, "dsgan_pw_gemm: WGRAD needs the dsgan_pw_wgrad_workspace scratch");
+    g.ws = splits > 1 ? ws : nullptr;
     if (BM == 128) pw_launch<PW_WGRAD, 128>(g, splits, st);
     else pw_launch<PW_WGRAD, 64>(g, splits, st);
+    wgrad_finish(g, splits, st);
   } else {
     DSG_REQUIRE(dsgan_pw_supported(mode, M, K, P, a_bs, b_bs, A, B), "dsgan_pw_gemm: unsupported shape");
     DSG_REQUIRE((long)M * P * 4 < (1L << 32), "dsgan_pw_gemm: M*P too large for a buffer resource");
@@ -576,8 +623,15 @@ extern "C" int dsgan_pw_dgrad_gbf(const float* W, const float* DY, long dy_bs, f
 
 // Weight-grad with bf16 operand(s): DW[M][N] += sum_{b,p} A[b][M][P] * B[b][N][P], A/B fp32 or
 // bf16 (a_bf16 / b_bf16).  P % 32 == 0, 16-byte aligned operands.
+// Scratch (floats) a weight-grad of M x N over nb*P pixels needs (0: no split).
+extern "C" long dsgan_pw_wgrad_workspace(int M, int N, int P, int nb) {
+  int ks;
+  const int splits = wgrad_plan(M, N, (long)nb * P, M > 64 ? 128 : 64, &ks);
+  return splits > 1 ? (long)splits * M * N : 0;
+}
+
 extern "C" int dsgan_pw_wgrad_mixed(const void* A, long a_bs, int a_bf16, const void* B, long b_bs,
-                                    int b_bf16, float* DW, int M, int N, int P, int nb, hipStream_t st) {
+                                    int b_bf16, float* DW, int M, int N, int P, int nb, float* ws, hipStream_t st) {
   DSG_REQUIRE(A && B && DW && M >= 16 && N > 0 && P > 0 && nb > 0, "dsgan_pw_wgrad_mixed: bad args");
   DSG_REQUIRE(P % 32 == 0 && al16(A) && al16(B) && (a_bs & 7) == 0 && (b_bs & 7) == 0,
               "dsgan_pw_wgrad_mixed: P %% 32 and 16-byte alignment required");
@@ -590,6 +644,8 @@ extern "C" int dsgan_pw_wgrad_mixed(const void* A, long a_bs, int a_bf16, const 
   g.M = M; g.N = N; g.K = nb * P;
   const int BM = M > 64 ? 128 : 64;
   const int splits = wgrad_split(g, BM);
+  DSG_REQUIRE(splits == 1 || ws, "dsgan_pw_wgrad_mixed: needs the dsgan_pw_wgrad_workspace scratch");
+  g.ws = splits > 1 ? ws : nullptr;
   const int sel = (a_bf16 ? 2 : 0) + (b_bf16 ? 1 : 0) + (BM == 128 ? 4 : 0);
   switch (sel) {
     case 0: pw_launch<PW_WGRAD, 64, 0, 0>(g, splits, st); break;
@@ -601,6 +657,7 @@ extern "C" int dsgan_pw_wgrad_mixed(const void* A, long a_bs, int a_bf16, const 
     case 6: pw_launch<PW_WGRAD, 128, 1, 0>(g, splits, st); break;
     default: pw_launch<PW_WGRAD, 128, 1, 1>(g, splits, st); break;
   }
+  wgrad_finish(g, splits, st);
   DSG_CHECK_LAUNCH();
   return 0;
 }

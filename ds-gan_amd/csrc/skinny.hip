@@ -235,6 +235,7 @@ struct WsArgs {
   int nb, Cin, Hin, Win, Cout, Ho, Wo, KW, stride, pad, nsmall;
   long pix_per_block;
   unsigned x_range, dy_range;
+  float* ws;   // chunk partials [gridDim.y][Cout*Cin*T] (NULL: one chunk, += into dw)
 };
 
 template <int S, int T, bool SMALL_OUT>
@@ -320,8 +321,21 @@ __global__ __launch_bounds__(256) void wgrad_small_kernel(WsArgs a) {
     const float v = red[0][i] + red[1][i] + red[2][i] + red[3][i];
     const int s = i / T, t = i - s * T;
     const long o = SMALL_OUT ? ((long)s * a.Cin + c) * T + t : ((long)c * a.Cin + s) * T + t;
-    atomicAdd(a.dw + o, v);
+    if (a.ws) a.ws[(long)blockIdx.y * a.Cout * a.Cin * T + o] = v;   // this chunk's partial
+    else a.dw[o] += v;                                               // one chunk: the only writer
   }
+}
+
+// pixel chunks of a small weight-grad (gridDim.y): ~2048 workgroups, >= 16 pixels per thread
+static long ws_chunks(int big, long total, long* ppb_out) {
+  long chunks = (2048 + big - 1) / big;
+  const long max_chunks = (total + 4095) / 4096;
+  if (chunks > max_chunks) chunks = max_chunks;
+  if (chunks < 1) chunks = 1;
+  long ppb = (total + chunks - 1) / chunks;
+  ppb = (ppb + 255) / 256 * 256;
+  *ppb_out = ppb;
+  return (total + ppb - 1) / ppb;
 }
 
 template <int S, int T, bool SO>
@@ -403,9 +417,15 @@ int dsgan_conv_small_in(const float* x, long x_bs, const float* w, long wm, long
 }
 
 // Weight-grad with Cout <= 8 or Cin <= 8 and KH*KW in {1, 9, 16}; dw += (OIHW).
+long dsgan_conv_wgrad_small_workspace(int N, int Cin, int Cout, int KH, int KW, int Ho, int Wo) {
+  long ppb;
+  const long chunks = ws_chunks(Cout <= 8 ? Cin : Cout, (long)N * Ho * Wo, &ppb);
+  return chunks > 1 ? chunks * Cout * Cin * KH * KW : 0;
+}
+
 int dsgan_conv_wgrad_small(const float* dy, long dy_bs, const float* x, long x_bs, float* dw, int N,
                            int Cin, int H, int W, int Cout, int KH, int KW, int stride, int pad, int Ho,
-                           int Wo, hipStream_t st) {
+                           int Wo, float* ws, hipStream_t st) {
   DSG_REQUIRE(dy && x && dw && N > 0 && Cin > 0 && Cout > 0 && Ho > 0 && Wo > 0, "dsgan_conv_wgrad_small: bad args");
   const int T = KH * KW;
   DSG_REQUIRE(T == 1 || T == 9 || T == 16, "dsgan_conv_wgrad_small: KH*KW must be 1, 9 or 16");
@@ -421,16 +441,12 @@ int dsgan_conv_wgrad_small(const float* dy, long dy_bs, const float* x, long x_b
   a.nsmall = so ? Cout : Cin;
   a.x_range = (unsigned)xr; a.dy_range = (unsigned)gr;
   const int big = so ? Cin : Cout;
-  const long total = (long)N * Ho * Wo;
-  long chunks = (2048 + big - 1) / big;
-  const long max_chunks = (total + 4095) / 4096;      // >= 16 pixels per thread
-  if (chunks > max_chunks) chunks = max_chunks;
-  if (chunks < 1) chunks = 1;
-  long ppb = (total + chunks - 1) / chunks;
-  ppb = (ppb + 255) / 256 * 256;
-  chunks = (total + ppb - 1) / ppb;
+  long ppb;
+  const long chunks = ws_chunks(big, (long)N * Ho * Wo, &ppb);
   a.pix_per_block = ppb;
   DSG_REQUIRE(chunks <= 65535, "dsgan_conv_wgrad_small: grid too large");
+  DSG_REQUIRE(chunks == 1 || ws, "dsgan_conv_wgrad_small: needs dsgan_conv_wgrad_small_workspace floats of scratch");
+  a.ws = chunks > 1 ? ws : nullptr;
   const bool s4 = a.nsmall <= 4;
 #define WS_CASE(TT)                                                                    \
   if (T == TT) {                                                                       \
@@ -439,6 +455,7 @@ int dsgan_conv_wgrad_small(const float* dy, long dy_bs, const float* x, long x_b
   }
   WS_CASE(1) else WS_CASE(9) else WS_CASE(16)
 #undef WS_CASE
+  if (chunks > 1) launch_split_reduce(ws, (int)chunks, (long)Cout * Cin * T, dw, st);
   DSG_CHECK_LAUNCH();
   return 0;
 }

@@ -24,11 +24,13 @@ SIGNATURES = {
     # igemm.hip
     "dsgan_conv_fwd": [P, L, P, P, P, L, P, L] + [I] * 12 + [F, I, I, I, S],
     "dsgan_conv_dgrad": [P, L, P, P, P, L, P, L, P, L, I, I, I, I, I, I, I, I, I, I, I, I, I, F, I, I, S],
-    "dsgan_conv_wgrad": [P, L, P, L, P] + [I] * 13 + [S],
+    "dsgan_conv_wgrad": [P, L, P, L, P] + [I] * 13 + [P, S],
+    "dsgan_conv_wgrad_workspace": [I] * 8,
     # pwgemm.hip
     "dsgan_pw_supported": [I, I, I, I, L, L, P, P],
-    "dsgan_pw_gemm": [I, P, L, P, L, P, L, P, P, L, P, L, I, I, I, I, I, I, I, I, I, F, S],
-    "dsgan_pw_wgrad_mixed": [P, L, I, P, L, I, P, I, I, I, I, S],
+    "dsgan_pw_gemm": [I, P, L, P, L, P, L, P, P, L, P, L, I, I, I, I, I, I, I, I, I, F, P, S],
+    "dsgan_pw_wgrad_workspace": [I, I, I, I],
+    "dsgan_pw_wgrad_mixed": [P, L, I, P, L, I, P, I, I, I, I, P, S],
     "dsgan_pw_fwd_io": [P, P, L, I, P, L, I, P, L, I, P, I, I, I, I, I, I, F, S],
     "dsgan_pw_dgrad_gbf": [P, P, L, P, L, P, L, I, I, I, I, I, S],
     # mlp.hip
@@ -58,10 +60,12 @@ SIGNATURES = {
     # skinny.hip
     "dsgan_conv_small_out": [P, L, P, L, L, L, L, P, P, L] + [I] * 13 + [S],
     "dsgan_conv_small_in": [P, L, P, L, L, L, L, P, P, L] + [I] * 13 + [F, I, S],
-    "dsgan_conv_wgrad_small": [P, L, P, L, P] + [I] * 11 + [S],
+    "dsgan_conv_wgrad_small_workspace": [I] * 7,
+    "dsgan_conv_wgrad_small": [P, L, P, L, P] + [I] * 11 + [P, S],
     # dwconv.hip
     "dsgan_dwconv_fwd": [P, L, P, P, P, L, I, I, I, I, I, I, I, S],
-    "dsgan_dwconv_wgrad": [P, L, P, L, P, P, I, I, I, I, I, S],
+    "dsgan_dwconv_wgrad_workspace": [I, I, I, I, I, I],
+    "dsgan_dwconv_wgrad": [P, L, P, L, P, P, I, I, I, I, I, P, S],
     # norm_pointwise.hip
     "dsgan_instnorm_fwd": [P, L, P, P, L, P, L, P, P, I, I, I, I, F, F, S],
     "dsgan_instnorm_bwd": [P, L, P, L, P, P, L, P, P, P, L, P, L, P, I, I, I, I, F, F, S],
@@ -70,22 +74,24 @@ SIGNATURES = {
     "dsgan_plane_stats": [P, L, P, P, P, I, I, I, S],
     "dsgan_plane_stats_bwd": [P, P, P, P, L, I, I, I, S],
     "dsgan_ca_fwd": [P, P, P, P, P, P, P, I, I, I, S],
-    "dsgan_ca_bwd": [P, P, P, P, P, P, P, P, P, P, P, P, P, I, I, I, S],
+    "dsgan_ca_bwd": [P, P, P, P, P, P, P, P, P, P, P, P, P, I, I, I, P, S],
     "dsgan_add_n": [P, P, I, P, L, I, L, S],
     "dsgan_copy_strided": [P, L, P, L, I, L, S],
     "dsgan_fill": [P, F, L, S],
     "dsgan_scale": [P, F, L, S],
     "dsgan_act_bwd": [P, P, P, L, I, F, I, S],
-    "dsgan_channel_sum": [P, L, P, I, I, I, S],
+    "dsgan_channel_sum": [P, L, P, I, I, I, P, S],
     # losses.hip
-    "dsgan_bce_logits_fwd": [P, L, F, P, S],
+    "dsgan_loss_parts": [],
+    "dsgan_ssim_parts": [I, I, I],
+    "dsgan_bce_logits_fwd": [P, L, F, P, P, S],
     "dsgan_bce_logits_bwd": [P, L, F, P, P, I, S],
-    "dsgan_l1_fwd": [P, P, L, P, S],
+    "dsgan_l1_fwd": [P, P, L, P, P, S],
     "dsgan_l1_bwd": [P, P, L, P, P, I, S],
     "dsgan_vgg_tap_bwd": [P, P, P, P, P, L, I, I, P, S],
-    "dsgan_tv_fwd": [P, L, I, I, F, P, S],
+    "dsgan_tv_fwd": [P, L, I, I, F, P, P, S],
     "dsgan_tv_bwd": [P, L, I, I, F, P, P, I, S],
-    "dsgan_ssim_fwd": [P, P, F, F, I, I, I, P, F, F, P, P, S],
+    "dsgan_ssim_fwd": [P, P, F, F, I, I, I, P, F, F, P, P, P, S],
     "dsgan_ms_ssim_workspace": [I, I, I, I],
     "dsgan_u8_to_image": [P, P, P, I, I, I, I, S],
     "dsgan_img_metrics": [P, P, I, I, I, P, P, S],
@@ -115,7 +121,7 @@ def load():
         fn = getattr(lib, name)
         fn.argtypes = argtypes
         fn.restype = (ctypes.c_char_p if name == "dsgan_last_error_string"
-                      else ctypes.c_long if name.endswith("_workspace") else ctypes.c_int)
+                      else ctypes.c_long if name.endswith(("_workspace", "_parts")) else ctypes.c_int)
     _lib = lib
     return lib
 

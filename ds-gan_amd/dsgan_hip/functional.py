@@ -231,6 +231,12 @@ def _wtrans_bf16(w, mode):
     return wb
 
 
+def _pw_ws(M, N, P, nb, like):
+    """Split-K scratch of a pointwise weight-grad (dsgan_pw_wgrad_workspace), or None."""
+    n = _lib.load().dsgan_pw_wgrad_workspace(M, N, P, nb)
+    return torch.empty(n, device=like.device, dtype=torch.float32) if n > 0 else None
+
+
 def _pws_ok(K, M, P, xbs, ybs, x, y):
     """1x1 contraction with <= 16 channels on one side for pwsmall.hip (16-byte rows)."""
     return ((K <= 16 or M <= 16) and x.data_ptr() % 16 == 0 and y.data_ptr() % 16 == 0
@@ -279,7 +285,7 @@ def conv_fwd_raw(x, w, b, stride, pad, act=None, out=None, pre=None, accumulate=
     elif KH == 1 and KW == 1 and stride == 1 and pad == 0 and _pw_ok(0, Cout, Cin, H * W, 0, xbs, w.data_ptr(), x.data_ptr()):
         fam = "pwgemm_kernel"
         call("dsgan_pw_gemm", 0, ptr(w), 0, ptr(x), xbs, ptr(y), ybs, ptr(b), ptr(pre), pbs, None, 0,
-             Cout, N * H * W, Cin, H * W, N, ACT[act], 0, ACT[xact], int(accumulate), LRELU_SLOPE, stream())
+             Cout, N * H * W, Cin, H * W, N, ACT[act], 0, ACT[xact], int(accumulate), LRELU_SLOPE, None, stream())
     elif w.dim() == 4 and pre is None and xact is None and _pconv_ok(Cin, KH, KW, stride):
         fam = "pconv_kernel"
         _pconv(x, xbs, _wtrans_bf16(w, 0), b, y, ybs, N, Cin, Cout, H, W, Ho, Wo, KH, KW, stride, pad, act,
@@ -333,7 +339,7 @@ def conv_dgrad_raw(dy, w, x_shape, stride, pad, bias=None, act=None, gpre=None, 
             and _pw_ok(1, Cin, Cout, H * W, 0, dybs, w.data_ptr(), dy.data_ptr())):
         fam = "pwgemm_kernel"
         call("dsgan_pw_gemm", 1, ptr(w), 0, ptr(dy), dybs, ptr(dx), dxbs, None, None, 0, ptr(gpre), gbs,
-             Cin, N * H * W, Cout, H * W, N, 0, ACT[gact], 0, int(accumulate), LRELU_SLOPE, stream())
+             Cin, N * H * W, Cout, H * W, N, 0, ACT[gact], 0, int(accumulate), LRELU_SLOPE, None, stream())
     elif (w.dim() == 4 and stride == 1 and act is None and bias is None and KH == KW
           and _pconv_ok(Cout, KH, KW, 1)):
         # stride-1 data-grad = forward conv of dy with the flipped, transposed kernel
@@ -389,12 +395,15 @@ def conv_wgrad_raw(dy, x, dw, stride, pad, xact=None):
     fam = "igemm_kernel"
     if xact is None and KH * KW in (1, 9, 16) and (Cout <= 8 or (Cin <= 8 and KH * KW == 1)):
         fam = "wgrad_small_kernel"
+        nws = _lib.load().dsgan_conv_wgrad_small_workspace(N, Cin, Cout, KH, KW, dy.shape[2], dy.shape[3])
+        ws = torch.empty(nws, device=dy.device, dtype=torch.float32) if nws > 0 else None
         call("dsgan_conv_wgrad_small", ptr(dy), dybs, ptr(x), xbs, ptr(dw), N, Cin, H, W, Cout, KH, KW,
-             stride, pad, dy.shape[2], dy.shape[3], stream())
+             stride, pad, dy.shape[2], dy.shape[3], ptr(ws), stream())
     elif KH == 1 and KW == 1 and stride == 1 and pad == 0 and _pw_ok(2, Cout, N * H * W, H * W, dybs, xbs, dy.data_ptr(), x.data_ptr()):
         fam = "pwgemm_kernel"
         call("dsgan_pw_gemm", 2, ptr(dy), dybs, ptr(x), xbs, ptr(dw), 0, None, None, 0, None, 0,
-             Cout, Cin, N * H * W, H * W, N, 0, 0, ACT[xact], 0, LRELU_SLOPE, stream())
+             Cout, Cin, N * H * W, H * W, N, 0, 0, ACT[xact], 0, LRELU_SLOPE, ptr(_pw_ws(Cout, Cin, H * W, N, dy)),
+             stream())
     elif (xact is None and _state["prec"] == "bf16" and dw.is_contiguous() and pad == 1 and W % 4 == 0
           and xbs % 4 == 0 and x.data_ptr() % 16 == 0 and _lib.load().dsgan_wconv_supported(Cin, KH, KW, stride)):
         fam = "wconv_kernel"
@@ -404,8 +413,10 @@ def conv_wgrad_raw(dy, x, dw, stride, pad, xact=None):
         call("dsgan_wconv", ptr(dy), dybs, ptr(x), xbs, ptr(dw), ptr(ws), N, Cin, Cout, H, W, Ho, Wo, KH, KW,
              stride, pad, stream())
     else:
+        nws = _lib.load().dsgan_conv_wgrad_workspace(N, Cin, Cout, KH, KW, dy.shape[2], dy.shape[3], _prec())
+        ws = torch.empty(nws, device=dy.device, dtype=torch.float32) if nws > 0 else None
         call("dsgan_conv_wgrad", ptr(dy), dybs, ptr(x), xbs, ptr(dw), N, Cin, H, W, Cout, KH, KW,
-             stride, pad, dy.shape[2], dy.shape[3], ACT[xact], _prec(), stream())
+             stride, pad, dy.shape[2], dy.shape[3], ACT[xact], _prec(), ptr(ws), stream())
     IGEMM_TIMER.end(e0, _conv_flops(N, Cin, Cout, KH, KW, dy.shape[2], dy.shape[3]),
                     ("wgrad", N, Cin, H, W, Cout, KH, stride), fam, _nb(dy, x, dw))
 
@@ -413,7 +424,8 @@ def conv_wgrad_raw(dy, x, dw, stride, pad, xact=None):
 def channel_sum_raw(dy, out):
     dy, dybs = nchw(dy)
     N, C, H, W = dy.shape
-    call("dsgan_channel_sum", ptr(dy), dybs, ptr(out), N, C, H * W, stream())
+    ws = torch.empty(N * C, device=dy.device, dtype=torch.float32)
+    call("dsgan_channel_sum", ptr(dy), dybs, ptr(out), N, C, H * W, ptr(ws), stream())
 
 
 def act_bwd_raw(dy, pre, act, out=None):
@@ -758,7 +770,7 @@ class PwMlpFn(torch.autograd.Function):
             dy4, dybs = nchw(dy)
             e0 = IGEMM_TIMER.begin()
             call("dsgan_pw_wgrad_mixed", ptr(dy4), dybs, 0, ptr(ctx.g), C4 * H * W, 1, ptr(gw2), w2.shape[0], C4,
-                 H * W, N, stream())
+                 H * W, N, ptr(_pw_ws(w2.shape[0], C4, H * W, N, dy)), stream())
             IGEMM_TIMER.end(e0, 2.0 * N * H * W * C4 * w2.shape[0], ("wgrad", N, C4, H, W, w2.shape[0], 1, 1),
                             "pwgemm_kernel", _nb(dy4, ctx.g, gw2))
         elif gw2 is not None:
@@ -807,7 +819,8 @@ class PwMlpFn(torch.autograd.Function):
         gw2, gb2, gws, gw1, gb1 = (_grad_buf(t) for t in (w2, b2, ws_ref, w1, b1))
         if gw2 is not None:
             e0 = IGEMM_TIMER.begin()
-            call("dsgan_pw_wgrad_mixed", ptr(dy), dybs, 0, ptr(g), C4 * HW, 1, ptr(gw2), P, C4, HW, N, stream())
+            call("dsgan_pw_wgrad_mixed", ptr(dy), dybs, 0, ptr(g), C4 * HW, 1, ptr(gw2), P, C4, HW, N,
+                 ptr(_pw_ws(P, C4, HW, N, dy)), stream())
             IGEMM_TIMER.end(e0, 2.0 * N * HW * C4 * P, ("wgrad", N, C4, H, W, P, 1, 1), "pwgemm_kernel",
                             _nb(dy, g, gw2))
         if gb2 is not None:
@@ -816,7 +829,8 @@ class PwMlpFn(torch.autograd.Function):
             conv_wgrad_raw(dy, x, gws, 1, 0)
         if gw1 is not None:
             e0 = IGEMM_TIMER.begin()
-            call("dsgan_pw_wgrad_mixed", ptr(dz), C4 * HW, 1, ptr(h), C * HW, 0, ptr(gw1), C4, C, HW, N, stream())
+            call("dsgan_pw_wgrad_mixed", ptr(dz), C4 * HW, 1, ptr(h), C * HW, 0, ptr(gw1), C4, C, HW, N,
+                 ptr(_pw_ws(C4, C, HW, N, dz)), stream())
             IGEMM_TIMER.end(e0, 2.0 * N * HW * C4 * C, ("wgrad", N, C, H, W, C4, 1, 1), "pwgemm_kernel",
                             _nb(dz, h, gw1))
         if gb1 is not None:
@@ -848,7 +862,9 @@ def _dw_wgrad(dy, x, gw, gb, K):
     dy4, dybs = nchw(dy)
     x4, xbs = nchw(x)
     N, C, H, W = x4.shape
-    call("dsgan_dwconv_wgrad", ptr(dy4), dybs, ptr(x4), xbs, ptr(gw), ptr(gb), N, C, H, W, K, stream())
+    al = int(x4.data_ptr() % 16 == 0 and dy4.data_ptr() % 16 == 0 and xbs % 4 == 0 and dybs % 4 == 0)
+    ws = torch.empty(_lib.load().dsgan_dwconv_wgrad_workspace(N, C, H, W, K, al), device=x4.device, dtype=torch.float32)
+    call("dsgan_dwconv_wgrad", ptr(dy4), dybs, ptr(x4), xbs, ptr(gw), ptr(gb), N, C, H, W, K, ptr(ws), stream())
 
 
 class DwConvFn(torch.autograd.Function):
@@ -1092,7 +1108,7 @@ class PerceptualL1Fn(torch.autograd.Function):
         feats, saved = vgg_features_raw(fake, blocks)
         outs = torch.empty(4, device=fake.device, dtype=torch.float32)
         for i, (f, r) in enumerate(zip(feats, real_feats)):
-            call("dsgan_l1_fwd", ptr(f), ptr(r.contiguous()), f.numel(), ptr(outs[i:]), stream())
+            call("dsgan_l1_fwd", ptr(f), ptr(r.contiguous()), f.numel(), ptr(outs[i:]), ptr(_loss_part(f)), stream())
         ctx.blocks, ctx.saved, ctx.real = blocks, saved, real_feats
         ctx.fake_shape = tuple(fake.shape)
         ctx.prec = _state["prec"]
@@ -1164,7 +1180,8 @@ class MidTailFn(torch.autograd.Function):
         dmx = torch.empty_like(davg)
         w1r, par, w2r = ctx.refs
         call("dsgan_ca_bwd", ptr(datt), ptr(att), ptr(avg), ptr(mx), ptr(hsave), ptr(w1), ptr(w2), ptr(pa),
-             ptr(davg), ptr(dmx), ptr(_grad_buf(w1r)), ptr(_grad_buf(w2r)), ptr(_grad_buf(par)), N, C, R, stream())
+             ptr(davg), ptr(dmx), ptr(_grad_buf(w1r)), ptr(_grad_buf(w2r)), ptr(_grad_buf(par)), N, C, R,
+             ptr(torch.empty(N * (2 * R * C + 1), device=v.device, dtype=torch.float32)), stream())
         call("dsgan_plane_stats_bwd", ptr(davg), ptr(dmx), ptr(amax), ptr(dv), C * H * W, N, C, H * W, stream())
         _params_done(*ctx.refs)
         return _give(ctx.box_v, dv), _give(ctx.box_x, dx), None, None, None
@@ -1230,12 +1247,17 @@ def cat_channels(a, b):
 # Losses (0-d device tensors; backward reads the upstream grad from device memory)
 # ------------------------------------------------------------------------------------------
 
+def _loss_part(like):
+    """Block-partial scratch of the deterministic loss reductions (dsgan_loss_parts floats)."""
+    return torch.empty(_lib.load().dsgan_loss_parts(), device=like.device, dtype=torch.float32)
+
+
 class BCELogitsFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, target):
         x = x.contiguous()
         out = torch.empty((), device=x.device, dtype=torch.float32)
-        call("dsgan_bce_logits_fwd", ptr(x), x.numel(), float(target), ptr(out), stream())
+        call("dsgan_bce_logits_fwd", ptr(x), x.numel(), float(target), ptr(out), ptr(_loss_part(x)), stream())
         ctx.target = float(target)
         ctx.save_for_backward(x)
         return out
@@ -1258,7 +1280,7 @@ class L1Fn(torch.autograd.Function):
     def forward(ctx, a, b):
         a, b = a.contiguous(), b.contiguous()
         out = torch.empty((), device=a.device, dtype=torch.float32)
-        call("dsgan_l1_fwd", ptr(a), ptr(b), a.numel(), ptr(out), stream())
+        call("dsgan_l1_fwd", ptr(a), ptr(b), a.numel(), ptr(out), ptr(_loss_part(a)), stream())
         ctx.save_for_backward(a, b)
         return out
 
@@ -1288,7 +1310,7 @@ class TVFn(torch.autograd.Function):
         y = y.contiguous()
         N, C, H, W = y.shape
         out = torch.empty((), device=y.device, dtype=torch.float32)
-        call("dsgan_tv_fwd", ptr(y), N * C, H, W, float(coef), ptr(out), stream())
+        call("dsgan_tv_fwd", ptr(y), N * C, H, W, float(coef), ptr(out), ptr(_loss_part(y)), stream())
         ctx.coef = float(coef)
         ctx.save_for_backward(y)
         return out
@@ -1332,8 +1354,9 @@ class SSIMFn(torch.autograd.Function):
         win = gauss_win(real.device)
         C1 = (0.01 * data_range) ** 2
         C2 = (0.03 * data_range) ** 2
+        part = torch.empty(_lib.load().dsgan_ssim_parts(N * C, H, W), device=real.device, dtype=torch.float32)
         call("dsgan_ssim_fwd", ptr(real), ptr(fake), float(a), float(b), N * C, H, W, ptr(win),
-             float(C1), float(C2), ptr(coef), ptr(s), stream())
+             float(C1), float(C2), ptr(coef), ptr(s), ptr(part), stream())
         cnt = float(N * C * Ho * Wo)
         ctx.save_for_backward(real, fake, coef)
         ctx.ab, ctx.cnt = (float(a), float(b)), cnt

@@ -54,27 +54,33 @@ int dsgan_conv_dgrad(const float* dy, long dy_bs, const float* w, const float* b
                      int gact, int N, int Cin, int H, int W, int Cout, int KH, int KW, int stride,
                      int pad, int Ho, int Wo, int act, float slope, int accumulate, int prec,
                      hipStream_t stream);
-/* dw[Cout][Cin][KH][KW] += sum_{n,oh,ow} dy * xact(x)  (split-K, fp32 atomics) */
+/* dw[Cout][Cin][KH][KW] += sum_{n,oh,ow} dy * xact(x)  (split-K partials in ws, summed in a fixed
+ * order: deterministic; ws = dsgan_conv_wgrad_workspace(...) floats, NULL when that is 0) */
+long dsgan_conv_wgrad_workspace(int N, int Cin, int Cout, int KH, int KW, int Ho, int Wo, int prec);
 int dsgan_conv_wgrad(const float* dy, long dy_bs, const float* x, long x_bs, float* dw, int N,
                      int Cin, int H, int W, int Cout, int KH, int KW, int stride, int pad, int Ho,
-                     int Wo, int xact, int prec, hipStream_t stream);
+                     int Wo, int xact, int prec, float* ws, hipStream_t stream);
 
 /* ---- pointwise (1x1 / Linear) GEMM fast path (pwgemm.hip): bf16 MFMA, fp32 in HBM ----------
  * mode 0 FWD  : Y[b][M][P] = act(W[M][K] . xact(X[b][K][P]) + bias) (+Y), ypre = pre-act
  * mode 1 DGRAD: DX[b][M][P] = (W[K][M]^T . DY[b][K][P]) * gact'(gpre)
  * mode 2 WGRAD: DW[M][N] += sum_{b,p} DY[b][M][p] * xact(X[b][N][p])   (K = P, nb images)
+ *              split over pixels into partials in `ws` (dsgan_pw_wgrad_workspace(M, N, P, nb)
+ *              floats; NULL allowed when that is 0), summed in a fixed order: deterministic.
  * dsgan_pw_supported() reports whether a shape/alignment takes this path (else use igemm). */
 int dsgan_pw_supported(int mode, int M, int K, int P, long a_bs, long b_bs, const void* a,
                        const void* b);
 int dsgan_pw_gemm(int mode, const float* A, long a_bs, const float* B, long b_bs, float* Y,
                   long y_bs, const float* bias, float* ypre, long ypre_bs, const float* gpre,
                   long gpre_bs, int M, int N, int K, int P, int nb, int act, int gact, int bact,
-                  int accumulate, float slope, hipStream_t stream);
+                  int accumulate, float slope, float* ws, hipStream_t stream);
+long dsgan_pw_wgrad_workspace(int M, int N, int P, int nb);
 
 /* Weight-grad with bf16 operand(s) (pwgemm.hip): DW[M][N] += sum_{b,p} A[b][M][p] * B[b][N][p];
- * a_bf16 / b_bf16 select bf16 storage (the fused MLP backward's gelu(z) and dz).  P % 32 == 0. */
+ * a_bf16 / b_bf16 select bf16 storage (the fused MLP backward's gelu(z) and dz).  P % 32 == 0.
+ * ws: dsgan_pw_wgrad_workspace(M, N, P, nb) floats (deterministic split reduction). */
 int dsgan_pw_wgrad_mixed(const void* A, long a_bs, int a_bf16, const void* B, long b_bs, int b_bf16,
-                         float* dw, int M, int N, int P, int nb, hipStream_t stream);
+                         float* dw, int M, int N, int P, int nb, float* ws, hipStream_t stream);
 /* forward with bf16 activations in and/or out (unfused ConvNeXt MLP blocks c4/c5/uc1/uc2,
  * MixConvNeXtML.py:221-240): Y (+)= act(W X + bias), X/Y fp32 or bf16; ypre (nullable) = fp32
  * pre-activation, or with ypre_grad_bf16 the bf16 act'(pre) the backward multiplies by */
@@ -115,7 +121,8 @@ int dsgan_f32_to_bf16(const float* src, void* dst, long n, hipStream_t stream);
  *   (DSGAN/models/networks.py:567), data-grads into 3/6-channel tensors (VGG conv1_1
  *   DSGAN/models/vgg.py:17, PatchGAN conv 0 networks.py:543) -- torch.nn.Conv2d forward/backward.
  * dsgan_conv_wgrad_small: dw[Cout][Cin][KH][KW] += conv weight-grad, Cout <= 8 or Cin <= 8,
- *   KH*KW in {1, 9, 16}. */
+ *   KH*KW in {1, 9, 16}; per-pixel-chunk partials in ws (dsgan_conv_wgrad_small_workspace floats,
+ *   NULL when that is 0) summed in a fixed order: deterministic. */
 int dsgan_conv_small_out(const float* x, long x_bs, const float* w, long wm, long wk, long wh, long ww,
                          const float* bias, float* y, long y_bs, int nb, int K, int M, int Hin, int Win,
                          int Ho, int Wo, int KH, int KW, int stride, int pad, int transposed,
@@ -128,9 +135,10 @@ int dsgan_conv_small_in(const float* x, long x_bs, const float* w, long wm, long
                         const float* bias, float* y, long y_bs, int nb, int K, int M, int Hin, int Win,
                         int Ho, int Wo, int KH, int KW, int stride, int pad, int transposed, int act,
                         float slope, int accumulate, hipStream_t stream);
+long dsgan_conv_wgrad_small_workspace(int N, int Cin, int Cout, int KH, int KW, int Ho, int Wo);
 int dsgan_conv_wgrad_small(const float* dy, long dy_bs, const float* x, long x_bs, float* dw, int N,
                            int Cin, int H, int W, int Cout, int KH, int KW, int stride, int pad, int Ho,
-                           int Wo, hipStream_t stream);
+                           int Wo, float* ws, hipStream_t stream);
 
 /* ---- tap-major implicit-GEMM conv for channel counts % 32 == 0 (tconv.hip, bf16 MFMA) -------
  * out[b][m][dst(o)] = act(sum_{tap,k} Wt[tap][m][k] * X[b][k][o*stride + (dh,dw)[tap]] + bias[m])
@@ -203,8 +211,11 @@ int dsgan_wconv(const float* D, long d_bs, const float* X, long x_bs, float* dw,
 int dsgan_dwconv_fwd(const float* x, long x_bs, const float* w, const float* bias, float* y,
                      long y_bs, int N, int C, int H, int W, int K, int flip, int accumulate,
                      hipStream_t stream);
+/* dw += sum dy*x (KxK), db += sum dy; per-workgroup partials in ws (dsgan_dwconv_wgrad_workspace
+ * floats; aligned16 = x, dy 16-byte aligned with batch strides % 4 == 0) summed in a fixed order. */
+long dsgan_dwconv_wgrad_workspace(int N, int C, int H, int W, int K, int aligned16);
 int dsgan_dwconv_wgrad(const float* dy, long dy_bs, const float* x, long x_bs, float* dw,
-                       float* db, int N, int C, int H, int W, int K, hipStream_t stream);
+                       float* db, int N, int C, int H, int W, int K, float* ws, hipStream_t stream);
 
 /* ---- InstanceNorm2d(affine=False, eps) fused with per-plane scale, residual and activation
  * (norm_pointwise.hip): nn.InstanceNorm2d at MixConvNeXtML.py:54,80,113-116,151,158,221,
@@ -235,11 +246,11 @@ int dsgan_ca_fwd(const float* avg, const float* mx, const float* w1, const float
 int dsgan_ca_bwd(const float* datt, const float* att, const float* avg, const float* mx,
                  const float* hsave, const float* w1, const float* w2, const float* prelu_a,
                  float* davg, float* dmx, float* dw1, float* dw2, float* dprelu_a, int N, int C,
-                 int R, hipStream_t stream);
+                 int R, float* ws, hipStream_t stream);   /* ws: N*(2*R*C+1) floats (per-image partials) */
 
 /* ---- elementwise / reductions ------------------------------------------------------------
  * add_n: the decoder skip sums MixConvNeXtML.py:482-492; copy_strided: torch.cat :66;
- * channel_sum: conv/linear bias gradients; act_bwd: ReLU/LeakyReLU/GELU backward. */
+ * channel_sum: conv/linear bias gradients (deterministic); act_bwd: ReLU/LeakyReLU/GELU backward. */
 int dsgan_add_n(const float* const* ins, const long* in_bs, int nin, float* out, long out_bs,
                 int N, long E, hipStream_t stream);
 int dsgan_copy_strided(const float* src, long src_bs, float* dst, long dst_bs, int N, long E,
@@ -248,16 +259,21 @@ int dsgan_fill(float* p, float v, long n, hipStream_t stream);
 int dsgan_scale(float* p, float a, long n, hipStream_t stream);
 int dsgan_act_bwd(const float* dy, const float* pre, float* dx, long n, int act, float slope,
                   int accumulate, hipStream_t stream);
-int dsgan_channel_sum(const float* dy, long dy_bs, float* out, int N, int C, int HW,
+/* out[c] += sum_{n,p} dy[n][c][p]; ws: N*C floats (per-plane sums, added over n in a fixed order) */
+int dsgan_channel_sum(const float* dy, long dy_bs, float* out, int N, int C, int HW, float* ws,
                       hipStream_t stream);
 
 /* ---- losses (losses.hip): scalars written to device memory, upstream grads read from it ----
  * GANLoss/BCEWithLogits networks.py:143-163; L1 pix2pix_model.py:177,182-186;
- * TV :189-191; ssim MS_SSIM.py:95-150 (coef: 3*planes*(H-10)*(W-10) floats of scratch). */
-int dsgan_bce_logits_fwd(const float* x, long n, float target, float* out, hipStream_t stream);
+ * TV :189-191; ssim MS_SSIM.py:95-150 (coef: 3*planes*(H-10)*(W-10) floats of scratch).
+ * Reductions are deterministic: block partials in `part` (dsgan_loss_parts() floats; ssim:
+ * dsgan_ssim_parts(planes, H, W)) summed in a fixed order by one final workgroup. */
+long dsgan_loss_parts(void);
+long dsgan_ssim_parts(int planes, int H, int W);
+int dsgan_bce_logits_fwd(const float* x, long n, float target, float* out, float* part, hipStream_t stream);
 int dsgan_bce_logits_bwd(const float* x, long n, float target, const float* gout, float* dx,
                          int accumulate, hipStream_t stream);
-int dsgan_l1_fwd(const float* a, const float* b, long n, float* out, hipStream_t stream);
+int dsgan_l1_fwd(const float* a, const float* b, long n, float* out, float* part, hipStream_t stream);
 int dsgan_l1_bwd(const float* a, const float* b, long n, const float* gout, float* da,
                  int accumulate, hipStream_t stream);
 /* VGG perceptual tap backward (DSGAN/models/vgg.py:30-42, pix2pix_model.py:182-186): the grad at
@@ -265,13 +281,13 @@ int dsgan_l1_bwd(const float* a, const float* b, long n, const float* gout, floa
  * + gout*sign(y - r)/numel) * (y > 0) -- L1 backward + the two consumers' sum + ReLU backward. */
 int dsgan_vgg_tap_bwd(const float* dpool, const int* idx, const float* y, const float* r, float* dx,
                       long planes, int H, int W, const float* gout, hipStream_t stream);
-int dsgan_tv_fwd(const float* y, long planes, int H, int W, float coef, float* out,
+int dsgan_tv_fwd(const float* y, long planes, int H, int W, float coef, float* out, float* part,
                  hipStream_t stream);
 int dsgan_tv_bwd(const float* y, long planes, int H, int W, float coef, const float* gout,
                  float* dy, int accumulate, hipStream_t stream);
 int dsgan_ssim_fwd(const float* real, const float* fake, float a, float b, int planes, int H,
                    int W, const float* win11, float C1, float C2, float* coef, float* out,
-                   hipStream_t stream);
+                   float* part, hipStream_t stream);
 int dsgan_ssim_bwd(const float* real, const float* fake, float a, float b, int planes, int H,
                    int W, const float* win11, const float* coef, const float* gout, float gcoef,
                    float* dfake, int accumulate, hipStream_t stream);

@@ -5,6 +5,7 @@ sys.path[:0] = [REPO, os.path.join(REPO, "ds-gan_amd")]
 import torch
 from dsgan_hip._lib import call, ptr, stream
 import dsgan_hip
+from dsgan_hip import functional as HF
 
 dsgan_hip.require_gpu()
 N = 16
@@ -41,8 +42,8 @@ for name, C, P, H in SHAPES:
     f = lambda: call("dsgan_mlp_fwd", ptr(h), C * HW, ptr(w1), ptr(b1), ptr(w2), ptr(b2), ptr(out), P * HW, N, C, P, HW, 1, stream())
     b = lambda: call("dsgan_mlp_bwd", ptr(h), C * HW, ptr(dy), P * HW, ptr(w1), ptr(b1), ptr(w2), ptr(dh), C * HW,
                      ptr(g), ptr(dz), ptr(bsum), N, C, P, HW, stream())
-    w2g = lambda: call("dsgan_pw_wgrad_mixed", ptr(dy), P * HW, 0, ptr(g), C4 * HW, 1, ptr(gw2), P, C4, HW, N, stream())
-    w1g = lambda: call("dsgan_pw_wgrad_mixed", ptr(dz), C4 * HW, 1, ptr(h), C * HW, 0, ptr(gw1), C4, C, HW, N, stream())
+    w2g = lambda: call("dsgan_pw_wgrad_mixed", ptr(dy), P * HW, 0, ptr(g), C4 * HW, 1, ptr(gw2), P, C4, HW, N, ptr(HF._pw_ws(P, C4, HW, N, dy)), stream())
+    w1g = lambda: call("dsgan_pw_wgrad_mixed", ptr(dz), C4 * HW, 1, ptr(h), C * HW, 0, ptr(gw1), C4, C, HW, N, ptr(HF._pw_ws(C4, C, HW, N, dz)), stream())
     tf, tb, t2, t1 = timeit(f), timeit(b), timeit(w2g), timeit(w1g)
     fl = 2.0 * N * HW * (C4 * C + C4 * P)
     byf = N * HW * (C + 2 * P) * 4
