@@ -8,6 +8,8 @@ namespace dsg {
 // dw[e] += sum_s ws[s * MN + e] for s = 0..splits-1 in a fixed order (pwgemm.hip): the
 // deterministic reduction every split weight-grad (pwgemm, igemm, skinny) finishes with.
 void launch_split_reduce(const float* ws, int splits, long MN, float* dw, hipStream_t st);
+// ... with elements e = (c, i), i < KK1: i < KK1-1 -> dw[c*(KK1-1)+i], i == KK1-1 -> db[c]
+void launch_split_reduce_kk(const float* ws, int splits, long MN, float* dw, float* db, int KK1, hipStream_t st);
 
 
 enum Act : int { ACT_NONE = 0, ACT_GELU = 1, ACT_RELU = 2, ACT_LRELU = 3, ACT_SIGMOID = 4 };

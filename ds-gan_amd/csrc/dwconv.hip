@@ -141,7 +141,8 @@ __global__ __launch_bounds__(256) void dwconv_wgrad_kernel(const float* __restri
     }
   }
   const float bs = block_sum<256>(bacc, sh);   // (its barrier also publishes part[])
-  float* slot = ws + ((long)c * (gridDim.y * (long)(gridDim.x / C)) + (long)n * gridDim.y + blockIdx.y) * (K * K + 1);
+  const long g = (long)n * gridDim.y + blockIdx.y;              // slot of this workgroup ([g][c][i])
+  float* slot = ws + (g * C + c) * (K * K + 1);
   for (int i = threadIdx.x; i < K * K; i += 256) {
     const int kh = i / K, kw = i - kh * K;
     float v = 0.f;
@@ -151,18 +152,6 @@ __global__ __launch_bounds__(256) void dwconv_wgrad_kernel(const float* __restri
   if (threadIdx.x == 0) slot[K * K] = bs;
 }
 
-// dw[c][i] += sum_g ws[c][g][i] (i < K*K), db[c] += sum_g ws[c][g][K*K]; g in order
-__global__ void dw_partial_reduce_kernel(const float* __restrict__ ws, int C, int G, int KK, float* __restrict__ dw,
-                                         float* __restrict__ db) {
-  const int t = blockIdx.x * 256 + threadIdx.x;
-  if (t >= C * (KK + 1)) return;
-  const int c = t / (KK + 1), i = t - c * (KK + 1);
-  const float* p = ws + (long)c * G * (KK + 1) + i;
-  float v = 0.f;
-  for (int g = 0; g < G; ++g) v += p[(long)g * (KK + 1)];
-  if (i < KK) dw[c * KK + i] += v;
-  else if (db) db[c] += v;
-}
 
 // ------------------------------------------------------------------------------------------
 // Register-blocked variants for W % 4 == 0 planes of width >= 32 (every DS-GAN plane but the
@@ -344,8 +333,8 @@ __global__ __launch_bounds__(256, 4) void dwconv_wgrad_v2(const float* __restric
   __syncthreads();
   if (threadIdx.x < K * K + 1) {   // this workgroup's slot of ws (summed in order by dw_partial_reduce)
     const float v = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
-    const long g = (long)blockIdx.z * gridDim.x + blockIdx.x, G = (long)gridDim.z * gridDim.x;
-    ws[((long)c * G + g) * (K * K + 1) + threadIdx.x] = v;
+    const long g = (long)blockIdx.z * gridDim.x + blockIdx.x;   // slot layout [g][c][i]
+    ws[(g * C + c) * (K * K + 1) + threadIdx.x] = v;
   }
 }
 
@@ -516,9 +505,8 @@ int dsgan_dwconv_wgrad(const float* dy, long dy_bs, const float* x, long x_bs, f
     }
     G = (long)N * groups;
   }
-  const int KK = K * K;
-  hipLaunchKernelGGL(dw_partial_reduce_kernel, dim3(cdiv(C * (KK + 1), 256)), dim3(256), 0, st, ws, C, (int)G, KK, dw,
-                     db);
+  // dw[c][i] += sum_g ws[g][c][i] (i < K*K), db[c] += sum_g ws[g][c][K*K]; g in a fixed order
+  launch_split_reduce_kk(ws, (int)G, (long)C * (K * K + 1), dw, db, K * K + 1, st);
   DSG_CHECK_LAUNCH();
   return 0;
 }

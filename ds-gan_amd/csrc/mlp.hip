@@ -552,7 +552,7 @@ int dsgan_mlp_bwd(const float* h, long h_bs, const float* dy, long dy_bs, const 
   return 0;
 }
 
-int dsgan_colsum(const float* part, int rows, int cols, float* out, hipStream_t st) {
+int dsgan_colsum(float* part, int rows, int cols, float* out, hipStream_t st) {
   DSG_REQUIRE(part && out && rows > 0 && cols > 0, "dsgan_colsum: bad args");
   launch_split_reduce(part, rows, cols, out, st);   // rows summed in a fixed order (deterministic)
   DSG_CHECK_LAUNCH();

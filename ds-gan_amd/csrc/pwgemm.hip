@@ -438,26 +438,43 @@ static void pw_launch(const PwArgs& g, int splits, hipStream_t st) {
   hipLaunchKernelGGL((pwgemm_kernel<MODE, BM, ABF, BBF>), dim3((unsigned)((long)mt * nt * splits)), dim3(256), 0, st, g);
 }
 
-// dw[e] += sum_s ws[s][e], s in a fixed order: thread (e, j) sums s = j, j+4, ... in order, then
-// the four partial sums are added j = 0..3 -- the same tree on every run.
-__global__ __launch_bounds__(256) void pw_wgrad_reduce_kernel(const float* __restrict__ ws, int S, long MN,
-                                                              float* __restrict__ dw) {
-  __shared__ float sh[4][64];
-  const int el = threadIdx.x & 63, j = threadIdx.x >> 6;
-  const long e = (long)blockIdx.x * 64 + el;
+// dw[e] += sum_s ws[s][e], s in a fixed order: thread (e, j) of a workgroup of EL elements x J
+// s-lanes sums s = j, j+J, j+2J, ... in order, then the J partial sums of an element are added
+// j = 0..J-1 -- the same tree on every run.  J grows with the split count so that a reduction of
+// many splits over few elements still spreads over many workgroups.  KK1 > 0: element e is
+// (c, i) = (e / KK1, e % KK1) and goes to dw[c*(KK1-1) + i] (i < KK1-1) or db[c] (depthwise
+// weight + bias partial vectors, dwconv.hip).
+template <int J>
+__global__ __launch_bounds__(256) void split_reduce_kernel(const float* __restrict__ ws, int S, long MN, long rs,
+                                                           float* __restrict__ dw, float* __restrict__ db, int KK1) {
+  constexpr int EL = 256 / J;
+  __shared__ float sh[J][EL + 1];
+  const int el = threadIdx.x % EL, j = threadIdx.x / EL;
+  const long e = (long)blockIdx.x * EL + el;
   float a = 0.f;
   if (e < MN) {
     int s = j;
-    for (; s + 12 < S; s += 16) {
-      const float v0 = ws[(long)s * MN + e], v1 = ws[(long)(s + 4) * MN + e];
-      const float v2 = ws[(long)(s + 8) * MN + e], v3 = ws[(long)(s + 12) * MN + e];
+    for (; s + 3 * J < S; s += 4 * J) {
+      const float v0 = ws[(long)s * rs + e], v1 = ws[(long)(s + J) * rs + e];
+      const float v2 = ws[(long)(s + 2 * J) * rs + e], v3 = ws[(long)(s + 3 * J) * rs + e];
       a += v0; a += v1; a += v2; a += v3;
     }
-    for (; s < S; s += 4) a += ws[(long)s * MN + e];
+    for (; s < S; s += J) a += ws[(long)s * rs + e];
   }
   sh[j][el] = a;
   __syncthreads();
-  if (j == 0 && e < MN) dw[e] += ((sh[0][el] + sh[1][el]) + sh[2][el]) + sh[3][el];
+  if (j == 0 && e < MN) {
+    float t = 0.f;
+#pragma unroll
+    for (int q = 0; q < J; ++q) t += sh[q][el];
+    if (KK1 == 0) dw[e] += t;
+    else {
+      const long c = e / KK1;
+      const int i = (int)(e - c * KK1);
+      if (i < KK1 - 1) dw[c * (KK1 - 1) + i] += t;
+      else if (db) db[c] += t;
+    }
+  }
 }
 
 // K (pixel) split of a weight-grad launch: about 640 workgroups (2.5 per CU: enough bytes in
@@ -479,9 +496,41 @@ static int wgrad_plan(int M, int N, long K, int BM, int* k_split) {
 }
 static int wgrad_split(PwArgs& g, int BM) { return wgrad_plan(g.M, g.N, g.K, BM, &g.k_split); }
 
-// dw[e] += sum_s ws[s][e] (fixed order); shared with the implicit-GEMM weight-grad (igemm.hip)
+// Pre-pass for many splits over few elements: workgroup (element block, row group g) adds rows
+// [g*SC, (g+1)*SC) (64 elements x 4 row lanes, coalesced 256-B row reads, fixed order) and writes
+// the sum over its own first row, which no other workgroup reads -- in place, no scratch.
+constexpr int SPLIT_SC = 16;
+__global__ __launch_bounds__(256) void split_prereduce_kernel(float* __restrict__ ws, int S, long MN) {
+  __shared__ float sh[4][65];
+  const int el = threadIdx.x & 63, j = threadIdx.x >> 6;
+  const long e = (long)blockIdx.x * 64 + el;
+  const int s0 = blockIdx.y * SPLIT_SC, s1 = min(S, s0 + SPLIT_SC);
+  float a = 0.f;
+  if (e < MN)
+    for (int s = s0 + j; s < s1; s += 4) a += ws[(long)s * MN + e];
+  sh[j][el] = a;
+  __syncthreads();
+  if (j == 0 && e < MN) ws[(long)s0 * MN + e] = ((sh[0][el] + sh[1][el]) + sh[2][el]) + sh[3][el];
+}
+
+// dw[e] += sum_s ws[s][e] (fixed order); every split reduction of the library goes through here.
+// (ws is consumed: the pre-pass overwrites some of its rows.)
+void launch_split_reduce_kk(const float* ws, int splits, long MN, float* dw, float* db, int KK1, hipStream_t st) {
+  long rs = MN;
+  if (splits > 64 && MN < 65536) {
+    const int groups = (splits + SPLIT_SC - 1) / SPLIT_SC;
+    hipLaunchKernelGGL(split_prereduce_kernel, dim3((unsigned)((MN + 63) / 64), (unsigned)groups), dim3(256), 0, st,
+                       (float*)ws, splits, MN);
+    splits = groups;
+    rs = MN * SPLIT_SC;
+  }
+  if (splits <= 8)
+    hipLaunchKernelGGL(split_reduce_kernel<4>, dim3((unsigned)((MN + 63) / 64)), dim3(256), 0, st, ws, splits, MN, rs, dw, db, KK1);
+  else
+    hipLaunchKernelGGL(split_reduce_kernel<16>, dim3((unsigned)((MN + 15) / 16)), dim3(256), 0, st, ws, splits, MN, rs, dw, db, KK1);
+}
 void launch_split_reduce(const float* ws, int splits, long MN, float* dw, hipStream_t st) {
-  hipLaunchKernelGGL(pw_wgrad_reduce_kernel, dim3((unsigned)((MN + 63) / 64)), dim3(256), 0, st, ws, splits, MN, dw);
+  launch_split_reduce_kk(ws, splits, MN, dw, nullptr, 0, st);
 }
 
 static void wgrad_finish(const PwArgs& g, int splits, hipStream_t st) {

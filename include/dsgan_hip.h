@@ -107,8 +107,9 @@ int dsgan_mlp_fwd(const float* h, long h_bs, const void* w1, const float* b1, co
 int dsgan_mlp_bwd(const float* h, long h_bs, const float* dy, long dy_bs, const void* w1,
                   const float* b1, const void* w2, float* dh, long dh_bs, void* g_out, void* dz_out,
                   float* bsum, int nb, int C, int P, int HW, hipStream_t stream);
-/* out[c] += sum_r part[r][c] */
-int dsgan_colsum(const float* part, int rows, int cols, float* out, hipStream_t stream);
+/* out[c] += sum_r part[r][c], rows added in a fixed order (deterministic); part is scratch and
+ * is overwritten (in-place pre-reduction of many rows). */
+int dsgan_colsum(float* part, int rows, int cols, float* out, hipStream_t stream);
 /* dst (bf16) = src (fp32), round to nearest even */
 int dsgan_f32_to_bf16(const float* src, void* dst, long n, hipStream_t stream);
 
