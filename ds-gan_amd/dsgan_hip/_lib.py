@@ -100,6 +100,15 @@ SIGNATURES = {
     "dsgan_ms_ssim_fwd_train": [P, P, F, F, I, I, I, I, P, F, F, P, I, P, P, P, S],
     "dsgan_ms_ssim_bwd": [P, P, F, F, I, I, I, I, P, F, F, P, I, P, P, P, P, I, S],
     "dsgan_ssim_bwd": [P, P, F, F, I, I, I, P, P, P, F, P, I, S],
+    # vggconv.hip
+    "dsgan_vconv_supported": [I, I, I, I],
+    "dsgan_vconv_wtrans_size": [I, I],
+    "dsgan_vconv_wtrans": [P, P, I, I, I, S],
+    "dsgan_vconv3x3": [P, P, P, P, P, I, I, I, I, I, I, I, S],
+    "dsgan_vgg_conv1_fwd": [P, L, P, P, P, I, I, I, S],
+    "dsgan_vgg_conv1_dgrad": [P, P, P, L, I, I, I, S],
+    "dsgan_cb16_maxpool": [P, P, P, I, I, I, I, S],
+    "dsgan_cb16_tap_bwd": [P, P, P, P, P, I, I, I, I, P, S],
     # adam.hip
     "dsgan_adam": [P, P, P, P, L, F, F, F, F, I, S],
 }
@@ -121,7 +130,7 @@ def load():
         fn = getattr(lib, name)
         fn.argtypes = argtypes
         fn.restype = (ctypes.c_char_p if name == "dsgan_last_error_string"
-                      else ctypes.c_long if name.endswith(("_workspace", "_parts")) else ctypes.c_int)
+                      else ctypes.c_long if name.endswith(("_workspace", "_parts", "_size")) else ctypes.c_int)
     _lib = lib
     return lib
 

@@ -1101,10 +1101,116 @@ def vgg_features_raw(x, blocks):
     return feats, saved
 
 
+# ---- the same pass in channel-blocked bf16 (vggconv.hip, bf16 mode at image sizes % 256) ----
+# Activations live as CB16 [N][C/16][H][W][16]: bf16 wherever the only consumers are bf16-operand
+# MFMAs / ReLU signs / max (exact w.r.t. the bf16 arithmetic), fp32 for the four tapped features
+# the L1 loss reads.  The backward's data-grads are stored as the bf16 the next conv consumes.
+
+def vgg_cb16_ok(x):
+    """bf16 mode and every VGG block resolution a multiple of 32 pixels wide (W % 256, H % 32)."""
+    return _state["prec"] == "bf16" and x.dim() == 4 and x.shape[3] % 256 == 0 and x.shape[2] % 32 == 0
+
+
+def _cb16_empty(N, C, H, W, like, dtype):
+    return torch.empty((N, C // 16, H, W, 16), device=like.device, dtype=dtype)
+
+
+def _vgg_wt(w, dgrad):
+    """bf16 weights of a VGG conv swizzled into vconv3x3's LDS image (dsgan_vconv_wtrans), cached."""
+    key = (id(w), w.data_ptr(), tuple(w.shape), "vconv", dgrad)
+    ent = _WT_CACHE.get(key)
+    gen = _wgen(w)
+    if ent is not None and ent[0] == gen and ent[1] == w._version and ent[2] is w:
+        return ent[3]
+    Co, Ci = w.shape[0], w.shape[1]
+    wt = torch.empty(_lib.load().dsgan_vconv_wtrans_size(Co, Ci), device=w.device, dtype=torch.bfloat16)
+    call("dsgan_vconv_wtrans", ptr(w), ptr(wt), Co, Ci, int(dgrad), stream())
+    _WT_CACHE[key] = (gen, w._version, w, wt)
+    return wt
+
+
+def _vconv(x, wt, bias, mask, y, N, K, M, H, W, relu, tag):
+    e0 = IGEMM_TIMER.begin()
+    call("dsgan_vconv3x3", ptr(x), ptr(wt), ptr(bias), ptr(mask), ptr(y), int(y.dtype == torch.float32), int(relu),
+         N, K, M, H, W, stream())
+    IGEMM_TIMER.end(e0, _conv_flops(N, K, M, 3, 3, H, W), (tag, N, K, H, W, M, 3, 1), "vconv_kernel",
+                    _nb(x, wt, bias, mask, y))
+    return y
+
+
+def vgg_features_cb16(x, blocks, keep=False):
+    """relu1_2..relu4_3 of x (NCHW fp32) as fp32 CB16 tensors; with keep, also per block (pool
+    argmax or None, [bf16 CB16 outputs of the block's convs below the tapped one]) for the backward."""
+    x, xbs = nchw(x)
+    N, _, H, W = x.shape
+    feats, saved = [], []
+    h = None
+    for bi, (pool, convs) in enumerate(blocks):
+        idx = None
+        if pool:
+            f = feats[-1]
+            C = f.shape[1] * 16
+            H, W = H // 2, W // 2
+            h = _cb16_empty(N, C, H, W, x, torch.bfloat16)
+            idx = torch.empty(h.shape, device=x.device, dtype=torch.uint8)
+            call("dsgan_cb16_maxpool", ptr(f), ptr(h), ptr(idx), N, C, 2 * H, 2 * W, stream())
+        acts = []
+        for li, (w, b) in enumerate(convs):
+            last = li == len(convs) - 1
+            Co, Ci = w.shape[0], w.shape[1]
+            y = _cb16_empty(N, Co, H, W, x, torch.float32 if last else torch.bfloat16)
+            if bi == 0 and li == 0:   # conv1_1, 3 -> 64: exact fp32 FMAs from the NCHW image
+                call("dsgan_vgg_conv1_fwd", ptr(x), xbs, ptr(w), ptr(b), ptr(y), N, H, W, stream())
+            else:
+                _vconv(h, _vgg_wt(w, 0), b, None, y, N, Ci, Co, H, W, True, "fwd")
+            if keep and not last:
+                acts.append(y)
+            h = y
+        feats.append(h)
+        saved.append((idx, acts))
+    return feats, saved
+
+
+def _perceptual_bwd_cb16(ctx, g):
+    """Backward of PerceptualL1Fn over the CB16 pass: tap (L1 + pool backward) x ReLU', then each
+    conv's data-grad x the ReLU' of the conv below in its epilogue, down to conv1_1's data-grad."""
+    d, d_idx = None, None
+    dx = None
+    for bi in range(len(ctx.blocks) - 1, -1, -1):
+        pool, convs = ctx.blocks[bi]
+        idx, acts = ctx.saved[bi]
+        f, r = ctx.feats[bi], ctx.real[bi]
+        N, Cb, H, W, _ = f.shape
+        dpre = _cb16_empty(N, Cb * 16, H, W, f, torch.bfloat16)
+        call("dsgan_cb16_tap_bwd", ptr(d), ptr(d_idx), ptr(f), ptr(r), ptr(dpre), N, Cb * 16, H, W, ptr(g), stream())
+        for li in range(len(convs) - 1, -1, -1):
+            w = convs[li][0]
+            Co, Ci = w.shape[0], w.shape[1]
+            if bi == 0 and li == 0:
+                dx = torch.empty(ctx.fake_shape, device=f.device, dtype=torch.float32)
+                call("dsgan_vgg_conv1_dgrad", ptr(dpre), ptr(w), ptr(dx), Ci * H * W, N, H, W, stream())
+            else:
+                out = _cb16_empty(N, Ci, H, W, f, torch.bfloat16)
+                _vconv(dpre, _vgg_wt(w, 1), None, acts[li - 1] if li > 0 else None, out, N, Co, Ci, H, W, False, "dgrad")
+                dpre = out
+        d, d_idx = dpre, idx
+    return dx
+
+
 class PerceptualL1Fn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, fake, blocks, real_feats):
         fake, _ = nchw(fake)
+        ctx.cb16 = real_feats[0].dim() == 5
+        if ctx.cb16:
+            feats, saved = vgg_features_cb16(fake, blocks, keep=True)
+            outs = torch.empty(4, device=fake.device, dtype=torch.float32)
+            for i, (f, r) in enumerate(zip(feats, real_feats)):
+                call("dsgan_l1_fwd", ptr(f), ptr(r), f.numel(), ptr(outs[i:]), ptr(_loss_part(f)), stream())
+            ctx.blocks, ctx.saved, ctx.real, ctx.feats = blocks, saved, real_feats, feats
+            ctx.fake_shape = tuple(fake.shape)
+            ctx.prec = _state["prec"]
+            return ((outs[1] + outs[2]) + outs[3]) + outs[0]
         feats, saved = vgg_features_raw(fake, blocks)
         outs = torch.empty(4, device=fake.device, dtype=torch.float32)
         for i, (f, r) in enumerate(zip(feats, real_feats)):
@@ -1117,6 +1223,11 @@ class PerceptualL1Fn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, g):
+        if ctx.cb16:
+            with precision(ctx.prec):
+                dx = _perceptual_bwd_cb16(ctx, g.contiguous())
+            ctx.saved = ctx.real = ctx.feats = None
+            return dx, None, None
         with precision(ctx.prec):
             g = g.contiguous()
             d, d_idx = None, None   # grad at the pool output of the block above, and that pool's argmax

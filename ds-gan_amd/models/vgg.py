@@ -89,7 +89,11 @@ class Vgg16(nn.Module):
 
     @torch.no_grad()
     def loss_features(self, x):
-        """relu1_2..relu4_3 of x without autograd (the real-image side of the perceptual loss)."""
+        """relu1_2..relu4_3 of x without autograd (the real-image side of the perceptual loss):
+        fp32 CB16 tensors from the channel-blocked bf16 pass (vggconv.hip) when the precision and
+        image size allow it, NCHW fp32 otherwise -- perceptual_l1 follows the same choice."""
+        if HF.vgg_cb16_ok(x):
+            return HF.vgg_features_cb16(x, self.loss_blocks())[0]
         return HF.vgg_features_raw(x, self.loss_blocks())[0]
 
     def perceptual_l1(self, fake, real_feats):

@@ -323,6 +323,27 @@ int dsgan_ms_ssim_bwd(const float* real, const float* fake, float a, float b, in
                       const float* win11, float C1, float C2, const float* weights_host, int levels, float* work,
                       const float* stats, const float* gout, float* dfake, int accumulate, hipStream_t stream);
 
+/* ---- VGG16 perceptual pass in channel-blocked bf16 (vggconv.hip): DSGAN/models/vgg.py:15-42 ----
+ * Layout CB16 = [n][c/16][h][w][c%16].  vconv3x3: 3x3/pad 1/stride 1 implicit GEMM on bf16 MFMA,
+ * Y = [relu](conv(X, W) + bias) [* (mask > 0)], Y bf16 or fp32 (y_f32); Wt = dsgan_vconv_wtrans
+ * (dgrad = 0: forward weights; dgrad = 1: flipped/transposed, the data-grad of that conv, M = Ci).
+ * Supported when K % 16 == 0, M % 64 == 0, W % 32 == 0, H % 4 == 0.
+ * vgg_conv1_fwd / _dgrad: conv1_1 (3 -> 64) between the NCHW fp32 image and CB16 bf16.
+ * cb16_maxpool: MaxPool2d(2) fp32 -> bf16 + u8 window argmax; cb16_tap_bwd: (maxpool backward +
+ * L1 backward of the tapped feature) * ReLU' -> bf16 (pix2pix_model.py:182-186). */
+int dsgan_vconv_supported(int K, int M, int H, int W);
+long dsgan_vconv_wtrans_size(int Co, int Ci);
+int dsgan_vconv_wtrans(const float* W, void* Wt, int Co, int Ci, int dgrad, hipStream_t stream);
+int dsgan_vconv3x3(const void* X, const void* Wt, const float* bias, const void* mask, void* Y, int y_f32, int relu,
+                   int N, int K, int M, int H, int W, hipStream_t stream);
+int dsgan_vgg_conv1_fwd(const float* x, long x_bs, const float* w, const float* b, void* y, int N, int H, int W,
+                        hipStream_t stream);
+int dsgan_vgg_conv1_dgrad(const void* d, const float* w, float* dx, long dx_bs, int N, int H, int W,
+                          hipStream_t stream);
+int dsgan_cb16_maxpool(const float* x, void* y, void* idx, int N, int C, int H, int W, hipStream_t stream);
+int dsgan_cb16_tap_bwd(const void* dpool, const void* idx, const float* f, const float* r, void* d, int N, int C,
+                       int H, int W, const float* gout, hipStream_t stream);
+
 /* ---- fused Adam over a flat buffer (adam.hip): torch.optim.Adam pix2pix_model.py:122-125 -- */
 int dsgan_adam(float* p, const float* g, float* m, float* v, long n, float lr, float beta1,
                float beta2, float eps, int step, hipStream_t stream);
