@@ -33,6 +33,10 @@ SIGNATURES = {
     "dsgan_pw_wgrad_mixed": [P, L, I, P, L, I, P, I, I, I, I, P, S],
     "dsgan_pw_fwd_io": [P, P, L, I, P, L, I, P, L, I, P, I, I, I, I, I, I, F, S],
     "dsgan_pw_dgrad_gbf": [P, P, L, P, L, P, L, I, I, I, I, I, S],
+    # pwf32.hip
+    "dsgan_pw_f32_supported": [I, I, I, I, L, L, P, P],
+    "dsgan_pw_f32_wgrad_workspace": [I, I, I, I],
+    "dsgan_pw_gemm_f32": [I, P, L, P, L, P, L, P, P, L, I, I, I, I, I, I, I, I, F, P, S],
     # mlp.hip
     "dsgan_mlp_supported": [I, I, I],
     "dsgan_mlp_fwd": [P, L, P, P, P, P, P, L, I, I, I, I, I, S],

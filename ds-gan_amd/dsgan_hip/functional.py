@@ -237,6 +237,11 @@ def _pw_ws(M, N, P, nb, like):
     return torch.empty(n, device=like.device, dtype=torch.float32) if n > 0 else None
 
 
+def _pwf_ok(mode, M, K, P, a_bs, b_bs, a, b):
+    """fp32 operands (the MidMLKA 1x1 conv, or every 1x1 in the fp32 parity mode): pwf32.hip."""
+    return _state["prec"] == "fp32" and bool(_lib.load().dsgan_pw_f32_supported(mode, M, K, P, a_bs, b_bs, a, b))
+
+
 def _pws_ok(K, M, P, xbs, ybs, x, y):
     """1x1 contraction with <= 16 channels on one side for pwsmall.hip (16-byte rows)."""
     return ((K <= 16 or M <= 16) and x.data_ptr() % 16 == 0 and y.data_ptr() % 16 == 0
@@ -286,6 +291,11 @@ def conv_fwd_raw(x, w, b, stride, pad, act=None, out=None, pre=None, accumulate=
         fam = "pwgemm_kernel"
         call("dsgan_pw_gemm", 0, ptr(w), 0, ptr(x), xbs, ptr(y), ybs, ptr(b), ptr(pre), pbs, None, 0,
              Cout, N * H * W, Cin, H * W, N, ACT[act], 0, ACT[xact], int(accumulate), LRELU_SLOPE, None, stream())
+    elif (KH == 1 and KW == 1 and stride == 1 and pad == 0 and pre is None and xact is None
+          and _pwf_ok(0, Cout, Cin, H * W, 0, xbs, w.data_ptr(), x.data_ptr())):
+        fam = "pwf32_kernel"
+        call("dsgan_pw_gemm_f32", 0, ptr(w), 0, ptr(x), xbs, ptr(y), ybs, ptr(b), None, 0, Cout, N * H * W, Cin,
+             H * W, N, ACT[act], 0, int(accumulate), LRELU_SLOPE, None, stream())
     elif w.dim() == 4 and pre is None and xact is None and _pconv_ok(Cin, KH, KW, stride):
         fam = "pconv_kernel"
         _pconv(x, xbs, _wtrans_bf16(w, 0), b, y, ybs, N, Cin, Cout, H, W, Ho, Wo, KH, KW, stride, pad, act,
@@ -340,6 +350,11 @@ def conv_dgrad_raw(dy, w, x_shape, stride, pad, bias=None, act=None, gpre=None, 
         fam = "pwgemm_kernel"
         call("dsgan_pw_gemm", 1, ptr(w), 0, ptr(dy), dybs, ptr(dx), dxbs, None, None, 0, ptr(gpre), gbs,
              Cin, N * H * W, Cout, H * W, N, 0, ACT[gact], 0, int(accumulate), LRELU_SLOPE, None, stream())
+    elif (KH == 1 and KW == 1 and stride == 1 and pad == 0 and bias is None and act is None
+            and _pwf_ok(1, Cin, Cout, H * W, 0, dybs, w.data_ptr(), dy.data_ptr())):
+        fam = "pwf32_kernel"
+        call("dsgan_pw_gemm_f32", 1, ptr(w), 0, ptr(dy), dybs, ptr(dx), dxbs, None, ptr(gpre), gbs, Cin, N * H * W,
+             Cout, H * W, N, 0, ACT[gact], int(accumulate), LRELU_SLOPE, None, stream())
     elif (w.dim() == 4 and stride == 1 and act is None and bias is None and KH == KW
           and _pconv_ok(Cout, KH, KW, 1)):
         # stride-1 data-grad = forward conv of dy with the flipped, transposed kernel
@@ -404,6 +419,13 @@ def conv_wgrad_raw(dy, x, dw, stride, pad, xact=None):
         call("dsgan_pw_gemm", 2, ptr(dy), dybs, ptr(x), xbs, ptr(dw), 0, None, None, 0, None, 0,
              Cout, Cin, N * H * W, H * W, N, 0, 0, ACT[xact], 0, LRELU_SLOPE, ptr(_pw_ws(Cout, Cin, H * W, N, dy)),
              stream())
+    elif (KH == 1 and KW == 1 and stride == 1 and pad == 0 and xact is None
+          and _pwf_ok(2, Cout, N * H * W, H * W, dybs, xbs, dy.data_ptr(), x.data_ptr())):
+        fam = "pwf32_kernel"
+        nws = _lib.load().dsgan_pw_f32_wgrad_workspace(Cout, Cin, H * W, N)
+        ws = torch.empty(nws, device=dy.device, dtype=torch.float32) if nws > 0 else None
+        call("dsgan_pw_gemm_f32", 2, ptr(dy), dybs, ptr(x), xbs, ptr(dw), 0, None, None, 0, Cout, Cin, N * H * W,
+             H * W, N, 0, 0, 0, LRELU_SLOPE, ptr(ws), stream())
     elif (xact is None and _state["prec"] == "bf16" and dw.is_contiguous() and pad == 1 and W % 4 == 0
           and xbs % 4 == 0 and x.data_ptr() % 16 == 0 and _lib.load().dsgan_wconv_supported(Cin, KH, KW, stride)):
         fam = "wconv_kernel"

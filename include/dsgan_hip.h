@@ -76,6 +76,16 @@ int dsgan_pw_gemm(int mode, const float* A, long a_bs, const float* B, long b_bs
                   int accumulate, float slope, float* ws, hipStream_t stream);
 long dsgan_pw_wgrad_workspace(int M, int N, int P, int nb);
 
+/* ---- exact-fp32 pointwise GEMMs (pwf32.hip): v_mfma_f32_32x32x2_f32, same modes and argument
+ * meaning as dsgan_pw_gemm (no ypre / activation-on-load); the MidMLKA 1x1 conv (fp32 by policy,
+ * MixConvNeXtML.py:85,112) and every 1x1 conv in the fp32 parity mode.  WGRAD: ws =
+ * dsgan_pw_f32_wgrad_workspace(M, N, P, nb) floats (deterministic split reduction). */
+int dsgan_pw_f32_supported(int mode, int M, int K, int P, long a_bs, long b_bs, const void* a, const void* b);
+long dsgan_pw_f32_wgrad_workspace(int M, int N, int P, int nb);
+int dsgan_pw_gemm_f32(int mode, const float* A, long a_bs, const float* B, long b_bs, float* Y, long y_bs,
+                      const float* bias, const float* gpre, long gpre_bs, int M, int N, int K, int P, int nb, int act,
+                      int gact, int accumulate, float slope, float* ws, hipStream_t stream);
+
 /* Weight-grad with bf16 operand(s) (pwgemm.hip): DW[M][N] += sum_{b,p} A[b][M][p] * B[b][N][p];
  * a_bf16 / b_bf16 select bf16 storage (the fused MLP backward's gelu(z) and dz).  P % 32 == 0.
  * ws: dsgan_pw_wgrad_workspace(M, N, P, nb) floats (deterministic split reduction). */
