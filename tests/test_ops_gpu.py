@@ -669,3 +669,30 @@ def test_instance_norm_cat(shape):
     assert rel(y, y_ref) < 1e-5
     assert rel(xd.grad, xr.grad) < 1e-4
     assert torch.equal(sd.grad.cpu(), sr.grad)
+
+
+@pytest.mark.parametrize("M,K,P,nb", [(2048, 512, 4096, 2), (1024, 256, 1024, 3), (256, 64, 256, 2), (4096, 1024, 1024, 1)])
+def test_pw_fwd_io_bf16_outputs(M, K, P, nb):
+    """pwconv1 of the unfused MLP blocks (MixConvNeXtML.py:221-223): g = gelu(W x + b) and
+    gp = gelu'(W x + b) written bf16 through the LDS-staged epilogue, vs torch on the same bf16
+    operands (one bf16 ulp)."""
+    import dsgan_hip
+    from dsgan_hip._lib import call, ptr, stream
+    from dsgan_hip import functional as HF
+    dsgan_hip.require_gpu()
+    g = torch.Generator().manual_seed(M + K)
+    x = torch.randn(nb, K, P, generator=g).cuda()
+    w = (torch.randn(M, K, generator=g) / K ** 0.5).cuda()
+    b = torch.randn(M, generator=g).cuda()
+    y = torch.empty(nb, M, P, device="cuda", dtype=torch.bfloat16)
+    gp = torch.empty_like(y)
+    call("dsgan_pw_fwd_io", ptr(w), ptr(x), K * P, 0, ptr(y), M * P, 1, ptr(gp), M * P, 1, ptr(b), M, K, P, nb,
+         HF.ACT["gelu"], 0, 0.2, stream())
+    z = torch.einsum("mk,bkp->bmp", w.bfloat16().double(), x.bfloat16().double()) + b.double().view(1, M, 1)
+    zz = z.clone().requires_grad_(True)
+    torch.nn.functional.gelu(zz).sum().backward()
+    ref_g, ref_gp = torch.nn.functional.gelu(z), zz.grad
+    torch.cuda.synchronize()
+    for got, ref in ((y, ref_g), (gp, ref_gp)):
+        got = got.double()
+        assert ((got - ref.cuda()).abs() <= ref.cuda().abs() * 2 ** -7 + 1e-3).all()
