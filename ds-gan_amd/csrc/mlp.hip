@@ -77,7 +77,7 @@ __device__ __forceinline__ void gelu_and_grad(float z, float& g, float& gp) {
 }
 
 struct MlpArgs {
-  const float* h; long h_bs;        // [nb][C][HW]   block activation after InstanceNorm
+  const void* h; long h_bs;         // [nb][C][HW]   block activation after InstanceNorm (fp32, or bf16 if h_bf16)
   const float* dy; long dy_bs;      // [nb][P][HW]   (backward) upstream grad of the block output
   const __bf16* w1;                 // [4C][C]
   const float* b1;                  // [4C]
@@ -88,6 +88,9 @@ struct MlpArgs {
   __bf16* dz_out;                   // (backward) dz       [nb][4C][HW]
   float* bsum;                      // (backward) [ntiles][4C] per-tile sums of dz
   int HW, nb, accumulate;
+  int h_bf16;
+  float* ws;                        // (weight-grad kernel) per-split partials, see mlp_wgrad_kernel
+  int splits;
 };
 
 __device__ __forceinline__ int xcd_tile(int id, int nwg) {
@@ -119,6 +122,37 @@ __device__ __forceinline__ void stage_rows(__bf16* dst, const float* __restrict_
       *reinterpret_cast<mbf16x4*>(dst + k * STR + c4 * 4) = mcvt4(v[i]);
     }
   }
+}
+
+// Same, from a bf16 source (the InstanceNorm's bf16 output): 16-byte items copied unconverted.
+template <int K, int BN, int STR, int NT>
+__device__ __forceinline__ void stage_rows_h16(__bf16* dst, const __bf16* __restrict__ src, int HW, int tid) {
+  constexpr int ITEMS = K * BN / 8;
+  static_assert(ITEMS % NT == 0, "tile must split evenly over the workgroup");
+  constexpr int PER = ITEMS / NT;
+  constexpr int BATCH = PER < 8 ? PER : 8;
+#pragma unroll
+  for (int i0 = 0; i0 < PER; i0 += BATCH) {
+    mu32x4 v[BATCH];
+#pragma unroll
+    for (int i = 0; i < BATCH; ++i) {
+      const int it = tid + (i0 + i) * NT;
+      const int k = it / (BN / 8), c8 = it % (BN / 8);
+      v[i] = *reinterpret_cast<const mu32x4*>(src + (long)k * HW + c8 * 8);
+    }
+#pragma unroll
+    for (int i = 0; i < BATCH; ++i) {
+      const int it = tid + (i0 + i) * NT;
+      const int k = it / (BN / 8), c8 = it % (BN / 8);
+      *reinterpret_cast<mu32x4*>(dst + k * STR + c8 * 8) = v[i];
+    }
+  }
+}
+
+template <int K, int BN, int STR, int NT>
+__device__ __forceinline__ void stage_h(__bf16* dst, const MlpArgs& g, int img, int p0, int tid) {
+  if (g.h_bf16) stage_rows_h16<K, BN, STR, NT>(dst, (const __bf16*)g.h + (long)img * g.h_bs + p0, g.HW, tid);
+  else stage_rows<K, BN, STR, NT>(dst, (const float*)g.h + (long)img * g.h_bs + p0, g.HW, tid);
 }
 
 // Register-staged weight chunk j: W1 rows [j*HC, +HC) (all C columns) and W2 columns
@@ -199,7 +233,7 @@ __global__ __launch_bounds__(NW * 64, MINB) void mlp_fwd_kernel(MlpArgs g) {
   using WC = WCh<C, P, HC, NT>;
   mu32x4 wr1[WC::N1], wr2[WC::N2];
   wch_load<C, P, HC, NT>(wr1, wr2, g.w1, g.w2, 0, tid);
-  stage_rows<C, BN, HSTR, NT>(Hs, g.h + (long)img * g.h_bs + p0, g.HW, tid);
+  stage_h<C, BN, HSTR, NT>(Hs, g, img, p0, tid);
   wch_store<C, P, HC, NT, W1STR, W2STR>(wr1, wr2, W1s, W2s, tid);
 
   mf32x16 oacc[OG::TM][OG::TN];
@@ -337,7 +371,7 @@ __global__ __launch_bounds__(NW * 64, 1) void mlp_bwd_kernel(MlpArgs g) {
   using WC = WCh<C, P, HC, NT>;
   mu32x4 wr1[WC::N1], wr2[WC::N2];
   wch_load<C, P, HC, NT>(wr1, wr2, g.w1, g.w2, 0, tid);
-  stage_rows<C, BN, HSTR, NT>(Hs, g.h + (long)img * g.h_bs + p0, g.HW, tid);
+  stage_h<C, BN, HSTR, NT>(Hs, g, img, p0, tid);
   stage_rows<P, BN, HSTR, NT>(Ds, g.dy + (long)img * g.dy_bs + p0, g.HW, tid);
   wch_store<C, P, HC, NT, W1STR, W2STR>(wr1, wr2, W1s, W2s, tid);
 
@@ -420,8 +454,9 @@ __global__ __launch_bounds__(NW * 64, 1) void mlp_bwd_kernel(MlpArgs g) {
       }
     __syncthreads();
     // ---- copy-out: 8 pixels of one hidden row per lane (transposing read) -> 16-byte stores;
-    //      per-(tile, wave>>1) sums of dz for the b1 grad ----
-    {
+    //      per-(tile, wave>>1) sums of dz for the b1 grad.  Skipped (g_out == NULL) when the
+    //      weight-grads come from mlp_wgrad_kernel instead. ----
+    if (g.g_out) {
       float bacc = 0.f;
 #pragma unroll
       for (int c = 0; c < CPW; ++c) {
@@ -475,6 +510,286 @@ __global__ __launch_bounds__(NW * 64, 1) void mlp_bwd_kernel(MlpArgs g) {
     }
 }
 
+// ------------------------------------------------------------------------------------------
+// backward (weight path): dW1 = dz h^T, dW2 = dy g^T, db1 = sum dz -- without g / dz in HBM.
+// Workgroup (hidden chunk j, pixel split s) holds chunk j's W1 rows / W2 columns in LDS for its
+// whole life and walks pixel tiles s, s+S, ...: per tile it recomputes z = W1[j] h + b1 and
+// t = W2[:, j]^T dy, forms g = gelu(z), dz = t gelu'(z) (bf16, LDS only) and accumulates
+// dW1[j] (HC x C) and dW2[:, j] (P x HC) in registers, K = the tile's pixels.  The NCH chunk
+// workgroups of one split run on the same XCD (xcd_tile, chunk index fastest) and read the same
+// h / dy tiles, so HBM sees them about once.  The next tile is prefetched into registers while
+// the current one computes.  Each split writes its partial dW1 / dW2 / db1 to ws (plain stores);
+// a fixed-order split reduction adds them (deterministic).
+// ------------------------------------------------------------------------------------------
+template <int K, int BN, int NT, bool BF>
+struct TileLd {   // a [K][BN] activation tile (rows strided by HW), fp32 or bf16 in HBM, via registers
+  static constexpr int E = BF ? 8 : 4;                 // elements per 16-byte item
+  static constexpr int N = K * BN / E / NT;
+  static_assert((K * BN / E) % NT == 0, "tile split");
+  mu32x4 v[N];
+  __device__ __forceinline__ void load(const void* src, int HW, int tid) {
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      const int it = tid + i * NT, k = it / (BN / E), c = it % (BN / E);
+      const char* p = (const char*)src + ((long)k * HW + c * E) * (BF ? 2 : 4);
+      v[i] = *reinterpret_cast<const mu32x4*>(p);
+    }
+  }
+  template <int STR>
+  __device__ __forceinline__ void store(__bf16* dst, int tid) const {
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      const int it = tid + i * NT, k = it / (BN / E), c = it % (BN / E);
+      if constexpr (BF) *reinterpret_cast<mu32x4*>(dst + k * STR + c * E) = v[i];
+      else *reinterpret_cast<mbf16x4*>(dst + k * STR + c * E) = mcvt4(__builtin_bit_cast(float4, v[i]));
+    }
+  }
+};
+
+// wave -> (tile, k-part) split of an [M x N] weight-grad product over NW waves: TPW tiles per wave,
+// or KS waves per tile each taking 1/KS of the K (pixel) range when there are fewer tiles than waves
+template <int M, int N, int NW>
+struct WTiles {
+  static constexpr int MT = M / 32, T = MT * (N / 32);
+  static constexpr int TPW = T >= NW ? T / NW : 1, KS = T >= NW ? 1 : NW / T;
+  static_assert(T % NW == 0 || NW % T == 0, "weight-grad tile split");
+};
+
+template <int C, int P, int BN, int NW, bool HBF>
+__global__ __launch_bounds__(NW * 64, 1) void mlp_wgrad_kernel(MlpArgs g) {
+  constexpr int HC = 64;
+  constexpr int NT = NW * 64;
+  constexpr int C4 = 4 * C, NCH = C4 / HC;
+  // Hs / Ds are read transposed (z, t: k = channel) and row-wise (dW: k = pixel): a row stride of
+  // 20 (mod 64) dwords keeps the row-wise 16-byte reads conflict-free
+  constexpr int HSTR = BN + 40, NSTR = HC + 8, W1STR = C + 8, W2STR = HC + 8;
+  constexpr int H_SZ = C * HSTR, D_SZ = P * HSTR, N_SZ = BN * NSTR, W1_SZ = HC * W1STR, W2_SZ = P * W2STR;
+  __shared__ __attribute__((aligned(16))) __bf16 smem[H_SZ + D_SZ + 2 * N_SZ + W1_SZ + W2_SZ];
+  __bf16* Hs = smem;
+  __bf16* Ds = Hs + H_SZ;
+  __bf16* Zn = Ds + D_SZ;     // dz, pixel-major [BN][NSTR]
+  __bf16* Gn = Zn + N_SZ;     // g,  pixel-major [BN][NSTR]
+  __bf16* W1s = Gn + N_SZ;
+  __bf16* W2s = W1s + W1_SZ;
+
+  using ZG = WGrid<HC, BN, NW>;    // z / t tile [HC x BN]
+  using T1 = WTiles<HC, C, NW>;    // dW1[j]    [HC x C]
+  using T2 = WTiles<P, HC, NW>;    // dW2[:, j] [P x HC]
+  static_assert(BN % (16 * T1::KS) == 0 && BN % (16 * T2::KS) == 0, "k split");
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int lr = lane & 31, lh = lane >> 5;
+  const int tq = (lane >> 2) & 3, tp = lane & 3, tG = (lane >> 4) & 1;
+  const int wm = wave / ZG::WN, wn = wave % ZG::WN;
+
+  const int id = xcd_tile(blockIdx.x, gridDim.x);
+  const int j = id % NCH, s = id / NCH;
+  const int S = g.splits, tpi = g.HW / BN, ntiles = g.nb * tpi;
+
+  {   // chunk j of the weights, once
+    using WC = WCh<C, P, HC, NT>;
+    mu32x4 wr1[WC::N1], wr2[WC::N2];
+    wch_load<C, P, HC, NT>(wr1, wr2, g.w1, g.w2, j, tid);
+    wch_store<C, P, HC, NT, W1STR, W2STR>(wr1, wr2, W1s, W2s, tid);
+  }
+  float bias[ZG::TM][16];
+#pragma unroll
+  for (int i = 0; i < ZG::TM; ++i)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) bias[i][r] = g.b1[j * HC + wm * (HC / 2) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh];
+
+  mf32x16 a1[T1::TPW], a2[T2::TPW];
+  float bacc[ZG::TM][16];
+#pragma unroll
+  for (int q = 0; q < T1::TPW; ++q)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) a1[q][r] = 0.f;
+#pragma unroll
+  for (int q = 0; q < T2::TPW; ++q)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) a2[q][r] = 0.f;
+#pragma unroll
+  for (int i = 0; i < ZG::TM; ++i)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) bacc[i][r] = 0.f;
+
+  TileLd<C, BN, NT, HBF> hreg;
+  TileLd<P, BN, NT, false> dreg;
+  auto tile_src = [&](int tt, const void*& hp, const float*& dp) {
+    const int img = tt / tpi, p0 = (tt - img * tpi) * BN;
+    hp = HBF ? (const void*)((const __bf16*)g.h + (long)img * g.h_bs + p0)
+             : (const void*)((const float*)g.h + (long)img * g.h_bs + p0);
+    dp = g.dy + (long)img * g.dy_bs + p0;
+  };
+  if (s < ntiles) {
+    const void* hp; const float* dp;
+    tile_src(s, hp, dp);
+    hreg.load(hp, g.HW, tid);
+    dreg.load(dp, g.HW, tid);
+  }
+
+  for (int tt = s; tt < ntiles; tt += S) {
+    __syncthreads();   // every wave is done with the previous tile's Hs / Ds / Zn / Gn
+    hreg.template store<HSTR>(Hs, tid);
+    dreg.template store<HSTR>(Ds, tid);
+    __syncthreads();
+    if (tt + S < ntiles) {   // prefetch the next tile while this one computes
+      const void* hp; const float* dp;
+      tile_src(tt + S, hp, dp);
+      hreg.load(hp, g.HW, tid);
+      dreg.load(dp, g.HW, tid);
+    }
+    // ---- z = W1[j] h + b1 ;  t = W2[:, j]^T dy ----
+    mf32x16 zacc[ZG::TM][ZG::TN], tacc[ZG::TM][ZG::TN];
+#pragma unroll
+    for (int i = 0; i < ZG::TM; ++i)
+#pragma unroll
+      for (int t = 0; t < ZG::TN; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) { zacc[i][t][r] = bias[i][r]; tacc[i][t][r] = 0.f; }
+#pragma unroll 4
+    for (int ks = 0; ks < C / 16; ++ks) {
+      mbf16x8 af[ZG::TM], bf[ZG::TN];
+#pragma unroll
+      for (int i = 0; i < ZG::TM; ++i)
+        af[i] = *reinterpret_cast<const mbf16x8*>(W1s + (wm * (HC / 2) + i * 32 + lr) * W1STR + ks * 16 + lh * 8);
+#pragma unroll
+      for (int t = 0; t < ZG::TN; ++t)
+        bf[t] = mtr_frag(Hs + (ks * 16 + 8 * lh + tq) * HSTR + wn * (BN / ZG::WN) + t * 32 + 16 * tG + 4 * tp, HSTR);
+#pragma unroll
+      for (int i = 0; i < ZG::TM; ++i)
+#pragma unroll
+        for (int t = 0; t < ZG::TN; ++t)
+          zacc[i][t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bf[t], zacc[i][t], 0, 0, 0);
+    }
+#pragma unroll 4
+    for (int ks = 0; ks < P / 16; ++ks) {
+      mbf16x8 af[ZG::TM], bf[ZG::TN];
+#pragma unroll
+      for (int i = 0; i < ZG::TM; ++i)
+        af[i] = mtr_frag(W2s + (ks * 16 + 8 * lh + tq) * W2STR + wm * (HC / 2) + i * 32 + 16 * tG + 4 * tp, W2STR);
+#pragma unroll
+      for (int t = 0; t < ZG::TN; ++t)
+        bf[t] = mtr_frag(Ds + (ks * 16 + 8 * lh + tq) * HSTR + wn * (BN / ZG::WN) + t * 32 + 16 * tG + 4 * tp, HSTR);
+#pragma unroll
+      for (int i = 0; i < ZG::TM; ++i)
+#pragma unroll
+        for (int t = 0; t < ZG::TN; ++t)
+          tacc[i][t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bf[t], tacc[i][t], 0, 0, 0);
+    }
+    // ---- g = gelu(z), dz = t gelu'(z) -> LDS (bf16, pixel-major); b1 sums of the rounded dz ----
+#pragma unroll
+    for (int i = 0; i < ZG::TM; ++i)
+#pragma unroll
+      for (int t = 0; t < ZG::TN; ++t) {
+        const int n = wn * (BN / ZG::WN) + t * 32 + lr;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          mbf16x4 gv4, dv4;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            float gv, gp;
+            gelu_and_grad(zacc[i][t][4 * q + e], gv, gp);
+            gv4[e] = (__bf16)gv;
+            dv4[e] = (__bf16)(tacc[i][t][4 * q + e] * gp);
+            bacc[i][4 * q + e] += (float)dv4[e];
+          }
+          const int m = wm * (HC / 2) + i * 32 + 8 * q + 4 * lh;
+          *reinterpret_cast<mbf16x4*>(Gn + n * NSTR + m) = gv4;
+          *reinterpret_cast<mbf16x4*>(Zn + n * NSTR + m) = dv4;
+        }
+      }
+    __syncthreads();
+    // ---- dW1[j] += dz h^T  (A = dz [hidden][px] transposed from Zn, B = h^T row-wise from Hs) ----
+#pragma unroll
+    for (int q = 0; q < T1::TPW; ++q) {
+      const int ti = T1::KS == 1 ? wave + NW * q : wave % T1::T;
+      const int kp = T1::KS == 1 ? 0 : wave / T1::T;
+      const int mt = ti % T1::MT, nt = ti / T1::MT;
+#pragma unroll
+      for (int ks = kp * (BN / 16 / T1::KS); ks < (kp + 1) * (BN / 16 / T1::KS); ++ks) {
+        const mbf16x8 af = mtr_frag(Zn + (ks * 16 + 8 * lh + tq) * NSTR + mt * 32 + 16 * tG + 4 * tp, NSTR);
+        const mbf16x8 bf = *reinterpret_cast<const mbf16x8*>(Hs + (nt * 32 + lr) * HSTR + ks * 16 + lh * 8);
+        a1[q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bf, a1[q], 0, 0, 0);
+      }
+    }
+    // ---- dW2[:, j] += dy g^T  (A = dy row-wise from Ds, B = g^T transposed from Gn) ----
+#pragma unroll
+    for (int q = 0; q < T2::TPW; ++q) {
+      const int ti = T2::KS == 1 ? wave + NW * q : wave % T2::T;
+      const int kp = T2::KS == 1 ? 0 : wave / T2::T;
+      const int mt = ti % T2::MT, nt = ti / T2::MT;
+#pragma unroll
+      for (int ks = kp * (BN / 16 / T2::KS); ks < (kp + 1) * (BN / 16 / T2::KS); ++ks) {
+        const mbf16x8 af = *reinterpret_cast<const mbf16x8*>(Ds + (mt * 32 + lr) * HSTR + ks * 16 + lh * 8);
+        const mbf16x8 bf = mtr_frag(Gn + (ks * 16 + 8 * lh + tq) * NSTR + nt * 32 + 16 * tG + 4 * tp, NSTR);
+        a2[q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bf, a2[q], 0, 0, 0);
+      }
+    }
+  }
+
+  // ---- partials: k-part sums through LDS (fixed order), then plain stores to this split's rows ----
+  __syncthreads();
+  float* red = reinterpret_cast<float*>(smem);   // [NW][64 lanes][16]
+  auto kreduce = [&](mf32x16& acc, int kp, int ks_n) {
+    // waves kp > 0 park their partial, wave kp == 0 of the same tile adds them in kp order
+    if (kp > 0) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) red[(wave * 64 + lane) * 16 + r] = acc[r];
+    }
+    __syncthreads();
+    if (kp == 0)
+      for (int k = 1; k < ks_n; ++k)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[r] += red[((wave + k * (NW / ks_n)) * 64 + lane) * 16 + r];
+    __syncthreads();
+  };
+  float* ws1 = g.ws + (long)s * C4 * C;                                   // [S][4C][C]
+  float* ws2 = g.ws + (long)S * C4 * C + (long)s * P * C4;                // [S][P][4C]
+  float* ws3 = g.ws + (long)S * (C4 * C + P * C4) + (long)s * C4;         // [S][4C]
+  if constexpr (T1::KS > 1) kreduce(a1[0], wave / T1::T, T1::KS);
+#pragma unroll
+  for (int q = 0; q < T1::TPW; ++q) {
+    const int ti = T1::KS == 1 ? wave + NW * q : wave % T1::T;
+    const int kp = T1::KS == 1 ? 0 : wave / T1::T;
+    const int mt = ti % T1::MT, nt = ti / T1::MT;
+    if (kp == 0)
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        ws1[(long)(j * HC + mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh) * C + nt * 32 + lr] = a1[q][r];
+  }
+  if constexpr (T2::KS > 1) kreduce(a2[0], wave / T2::T, T2::KS);
+#pragma unroll
+  for (int q = 0; q < T2::TPW; ++q) {
+    const int ti = T2::KS == 1 ? wave + NW * q : wave % T2::T;
+    const int kp = T2::KS == 1 ? 0 : wave / T2::T;
+    const int mt = ti % T2::MT, nt = ti / T2::MT;
+    if (kp == 0)
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        ws2[(long)(mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh) * C4 + j * HC + nt * 32 + lr] = a2[q][r];
+  }
+  // b1: lanes lr of a half hold the same hidden rows -> butterfly, then the WN waves of a row
+  // group in wn order
+  float* bred = red;   // [NW][HC]
+#pragma unroll
+  for (int i = 0; i < ZG::TM; ++i)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      float t = bacc[i][r];
+      t += __shfl_xor(t, 1, 64); t += __shfl_xor(t, 2, 64); t += __shfl_xor(t, 4, 64);
+      t += __shfl_xor(t, 8, 64); t += __shfl_xor(t, 16, 64);
+      if (lr == 0) bred[wave * HC + wm * (HC / 2) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh] = t;
+    }
+  __syncthreads();
+  if (tid < HC) {
+    const int wmr = tid / (HC / 2);
+    float t = 0.f;
+    for (int w = 0; w < ZG::WN; ++w) t += bred[(wmr * ZG::WN + w) * HC + tid];
+    ws3[j * HC + tid] = t;
+  }
+}
+
 __global__ __launch_bounds__(256) void f32_to_bf16_kernel(const float* __restrict__ s, __bf16* __restrict__ d, long n) {
   for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) d[i] = (__bf16)s[i];
 }
@@ -500,6 +815,26 @@ static void bwd_launch(const MlpArgs& g, hipStream_t st) {
   hipLaunchKernelGGL((mlp_bwd_kernel<C, P, BN, 64, NW>), dim3(tiles), dim3(NW * 64), 0, st, g);
 }
 
+// weight-grad kernel: same pixel tile as the backward; splits so that NCH * S ~ 512 workgroups
+// (2 per CU), a multiple of 8 (whole split groups per XCD), at most one tile per split
+static int mlp_wgrad_splits(int C, int P, int HW, int nb) {
+  const int bn = (C == 64 || (C == 128 && P == 64)) ? 128 : 64;
+  const int nch = 4 * C / 64;
+  const long ntiles = (long)nb * (HW / bn);
+  long S = 512 / nch;
+  S = S / 8 * 8;
+  if (S < 8) S = 8;
+  if (S > ntiles) S = ntiles;
+  return (int)S;
+}
+
+template <int C, int P, int BN, int NW>
+static void wgrad_launch(const MlpArgs& g, hipStream_t st) {
+  const unsigned wgs = (unsigned)((4 * C / 64) * g.splits);
+  if (g.h_bf16) hipLaunchKernelGGL((mlp_wgrad_kernel<C, P, BN, NW, true>), dim3(wgs), dim3(NW * 64), 0, st, g);
+  else hipLaunchKernelGGL((mlp_wgrad_kernel<C, P, BN, NW, false>), dim3(wgs), dim3(NW * 64), 0, st, g);
+}
+
 }  // namespace dsg
 
 using namespace dsg;
@@ -514,16 +849,16 @@ int dsgan_mlp_supported(int C, int P, int HW) {
   return 32;
 }
 
-int dsgan_mlp_fwd(const float* h, long h_bs, const void* w1, const float* b1, const void* w2,
+int dsgan_mlp_fwd(const void* h, long h_bs, int h_bf16, const void* w1, const float* b1, const void* w2,
                   const float* b2, float* out, long out_bs, int nb, int C, int P, int HW,
                   int accumulate, hipStream_t st) {
   DSG_REQUIRE(h && w1 && b1 && w2 && out && nb > 0, "dsgan_mlp_fwd: bad args");
   DSG_REQUIRE(dsgan_mlp_supported(C, P, HW), "dsgan_mlp_fwd: unsupported shape C=%d P=%d HW=%d", C, P, HW);
-  DSG_REQUIRE(((uintptr_t)h & 15) == 0 && (h_bs & 3) == 0 && ((uintptr_t)w1 & 15) == 0 && ((uintptr_t)w2 & 15) == 0,
+  DSG_REQUIRE(((uintptr_t)h & 15) == 0 && (h_bs & 7) == 0 && ((uintptr_t)w1 & 15) == 0 && ((uintptr_t)w2 & 15) == 0,
               "dsgan_mlp_fwd: operands must be 16-byte aligned");
   MlpArgs g{};
   g.h = h; g.h_bs = h_bs; g.w1 = (const __bf16*)w1; g.b1 = b1; g.w2 = (const __bf16*)w2; g.b2 = b2;
-  g.out = out; g.out_bs = out_bs; g.HW = HW; g.nb = nb; g.accumulate = accumulate;
+  g.out = out; g.out_bs = out_bs; g.HW = HW; g.nb = nb; g.accumulate = accumulate; g.h_bf16 = h_bf16;
   if (C == 64) fwd_launch<64, 128, 128, 2>(g, st);
   else if (C == 128 && P == 64) fwd_launch<128, 64, 128, 2>(g, st);
   else if (C == 128) fwd_launch<128, 256, 128, 1>(g, st);
@@ -532,22 +867,55 @@ int dsgan_mlp_fwd(const float* h, long h_bs, const void* w1, const float* b1, co
   return 0;
 }
 
-int dsgan_mlp_bwd(const float* h, long h_bs, const float* dy, long dy_bs, const void* w1, const float* b1,
+int dsgan_mlp_bwd(const void* h, long h_bs, int h_bf16, const float* dy, long dy_bs, const void* w1, const float* b1,
                   const void* w2, float* dh, long dh_bs, void* g_out, void* dz_out, float* bsum, int nb,
                   int C, int P, int HW, hipStream_t st) {
-  DSG_REQUIRE(h && dy && w1 && b1 && w2 && dh && g_out && dz_out && bsum && nb > 0, "dsgan_mlp_bwd: bad args");
+  DSG_REQUIRE(h && dy && w1 && b1 && w2 && dh && nb > 0 && ((g_out && dz_out && bsum) || (!g_out && !dz_out && !bsum)),
+              "dsgan_mlp_bwd: bad args (g_out, dz_out, bsum: all or none)");
   DSG_REQUIRE(dsgan_mlp_supported(C, P, HW), "dsgan_mlp_bwd: unsupported shape C=%d P=%d HW=%d", C, P, HW);
-  DSG_REQUIRE(((uintptr_t)h & 15) == 0 && ((uintptr_t)dy & 15) == 0 && (h_bs & 3) == 0 && (dy_bs & 3) == 0 &&
+  DSG_REQUIRE(((uintptr_t)h & 15) == 0 && ((uintptr_t)dy & 15) == 0 && (h_bs & 7) == 0 && (dy_bs & 3) == 0 &&
               ((uintptr_t)g_out & 15) == 0 && ((uintptr_t)dz_out & 15) == 0,
               "dsgan_mlp_bwd: operands must be 16-byte aligned");
   MlpArgs g{};
   g.h = h; g.h_bs = h_bs; g.dy = dy; g.dy_bs = dy_bs; g.w1 = (const __bf16*)w1; g.b1 = b1;
   g.w2 = (const __bf16*)w2; g.out = dh; g.out_bs = dh_bs; g.g_out = (__bf16*)g_out;
-  g.dz_out = (__bf16*)dz_out; g.bsum = bsum; g.HW = HW; g.nb = nb;
+  g.dz_out = (__bf16*)dz_out; g.bsum = bsum; g.HW = HW; g.nb = nb; g.h_bf16 = h_bf16;
   if (C == 64) bwd_launch<64, 128, 128, 8>(g, st);
   else if (C == 128 && P == 64) bwd_launch<128, 64, 128, 8>(g, st);
   else if (C == 128) bwd_launch<128, 256, 64, 4>(g, st);
   else bwd_launch<256, 128, 64, 4>(g, st);
+  DSG_CHECK_LAUNCH();
+  return 0;
+}
+
+// fp32 scratch (elements) of dsgan_mlp_wgrad
+long dsgan_mlp_wgrad_workspace(int C, int P, int HW, int nb) {
+  if (!dsgan_mlp_supported(C, P, HW)) return 0;
+  const long S = mlp_wgrad_splits(C, P, HW, nb);
+  return S * (4L * C * C + (long)P * 4 * C + 4L * C);
+}
+
+int dsgan_mlp_wgrad(const void* h, long h_bs, int h_bf16, const float* dy, long dy_bs, const void* w1,
+                    const float* b1, const void* w2, float* dw1, float* db1, float* dw2, float* ws, int nb, int C,
+                    int P, int HW, hipStream_t st) {
+  DSG_REQUIRE(h && dy && w1 && b1 && w2 && dw1 && db1 && dw2 && ws && nb > 0, "dsgan_mlp_wgrad: bad args");
+  DSG_REQUIRE(dsgan_mlp_supported(C, P, HW), "dsgan_mlp_wgrad: unsupported shape C=%d P=%d HW=%d", C, P, HW);
+  DSG_REQUIRE(((uintptr_t)h & 15) == 0 && ((uintptr_t)dy & 15) == 0 && (h_bs & 7) == 0 && (dy_bs & 3) == 0,
+              "dsgan_mlp_wgrad: operands must be 16-byte aligned");
+  MlpArgs g{};
+  g.h = h; g.h_bs = h_bs; g.h_bf16 = h_bf16; g.dy = dy; g.dy_bs = dy_bs; g.w1 = (const __bf16*)w1; g.b1 = b1;
+  g.w2 = (const __bf16*)w2; g.HW = HW; g.nb = nb; g.ws = ws;
+  const int S = mlp_wgrad_splits(C, P, HW, nb);
+  g.splits = S;
+  if (C == 64) wgrad_launch<64, 128, 128, 8>(g, st);
+  else if (C == 128 && P == 64) wgrad_launch<128, 64, 128, 8>(g, st);
+  else if (C == 128) wgrad_launch<128, 256, 64, 4>(g, st);
+  else wgrad_launch<256, 128, 64, 4>(g, st);
+  DSG_CHECK_LAUNCH();
+  const long n1 = 4L * C * C, n2 = (long)P * 4 * C;
+  launch_split_reduce(ws, S, n1, dw1, st);
+  launch_split_reduce(ws + S * n1, S, n2, dw2, st);
+  launch_split_reduce(ws + S * (n1 + n2), S, 4L * C, db1, st);
   DSG_CHECK_LAUNCH();
   return 0;
 }

@@ -18,6 +18,8 @@ struct INArgs {
   float* y; long y_bs;
   float* mean; float* rstd;     // statistics of scale*x, [N*C]
   int N, C, HW, act; float slope, eps;
+  int y_bf16;                   // y is bf16 (y_bs in elements): the block activation h whose only
+                                // consumers are bf16-operand MFMA GEMMs (v4 kernels only)
 };
 
 // Plane reduction helper: NT threads per plane (NT = 64: one wave, else the whole block).
@@ -203,7 +205,14 @@ __global__ __launch_bounds__(NT == 64 ? 256 : NT) void instnorm_fwd_v4(INArgs a)
     if (r) { const float4 q = r[i]; v.x += q.x; v.y += q.y; v.z += q.z; v.w += q.w; }
     v.x = act_f(a.act, v.x, a.slope); v.y = act_f(a.act, v.y, a.slope);
     v.z = act_f(a.act, v.z, a.slope); v.w = act_f(a.act, v.w, a.slope);
-    y[i] = v;
+    if (a.y_bf16) {   // round-to-nearest-even, the same rounding the GEMMs apply to fp32 operands
+      typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4_t;
+      bf16x4_t hv;
+      hv[0] = (__bf16)v.x; hv[1] = (__bf16)v.y; hv[2] = (__bf16)v.z; hv[3] = (__bf16)v.w;
+      reinterpret_cast<bf16x4_t*>(reinterpret_cast<__bf16*>(a.y) + (long)n * a.y_bs + (long)c * a.HW)[i] = hv;
+    } else {
+      y[i] = v;
+    }
   };
   auto ld = [&](int i) -> float4 {
     float4 v = x[i];
@@ -912,7 +921,7 @@ int dsgan_instnorm_fwd(const float* x, long x_bs, const float* scale, const floa
                        float* y, long y_bs, float* mean, float* rstd, int N, int C, int HW, int act,
                        float slope, float eps, hipStream_t st) {
   DSG_REQUIRE(x && y && mean && rstd && N > 0 && C > 0 && HW > 0, "dsgan_instnorm_fwd: bad args");
-  INArgs a{x, x_bs, scale, res, res_bs, y, y_bs, mean, rstd, N, C, HW, act, slope, eps};
+  INArgs a{x, x_bs, scale, res, res_bs, y, y_bs, mean, rstd, N, C, HW, act, slope, eps, 0};
   const int planes = N * C;
   const int v4 = in_v4_ok(HW, x, x_bs) && in_v4_ok(HW, y, y_bs) && (!res || in_v4_ok(HW, res, res_bs));
   if (v4) {
@@ -937,6 +946,28 @@ int dsgan_instnorm_fwd(const float* x, long x_bs, const float* scale, const floa
     hipLaunchKernelGGL((instnorm_fwd_kernel<1024, 16>), dim3(planes), dim3(1024), 0, st, a);
   else
     hipLaunchKernelGGL((instnorm_fwd_kernel<1024, 0>), dim3(planes), dim3(1024), 0, st, a);
+  DSG_CHECK_LAUNCH();
+  return 0;
+}
+
+// y (bf16) = IN(x): the plain InstanceNorm2d(affine=False) of a ConvNeXt block
+// (DSGAN/models/model/MixConvNeXtML.py:233), stored bf16 for the block's MLP GEMMs.
+int dsgan_instnorm_fwd_bf16(const float* x, long x_bs, void* y, long y_bs, float* mean, float* rstd, int N, int C,
+                            int HW, float eps, hipStream_t st) {
+  DSG_REQUIRE(x && y && mean && rstd && N > 0 && C > 0 && HW > 0, "dsgan_instnorm_fwd_bf16: bad args");
+  DSG_REQUIRE(in_v4_ok(HW, x, x_bs) && in_v4_ok(HW, y, y_bs), "dsgan_instnorm_fwd_bf16: HW %% 4 and 16-byte alignment");
+  INArgs a{x, x_bs, nullptr, nullptr, 0, (float*)y, y_bs, mean, rstd, N, C, HW, ACT_NONE, 0.f, eps, 1};
+  const int planes = N * C;
+  if (HW <= 64 * 16)
+    hipLaunchKernelGGL((instnorm_fwd_v4<64, 4>), dim3(cdiv(planes, 4)), dim3(256), 0, st, a);
+  else if (HW <= 256 * 16)
+    hipLaunchKernelGGL((instnorm_fwd_v4<256, 4>), dim3(planes), dim3(256), 0, st, a);
+  else if (HW <= 256 * 64)
+    hipLaunchKernelGGL((instnorm_fwd_v4<256, 16>), dim3(planes), dim3(256), 0, st, a);
+  else if (HW <= 1024 * 64)
+    hipLaunchKernelGGL((instnorm_fwd_v4<1024, 16>), dim3(planes), dim3(1024), 0, st, a);
+  else
+    hipLaunchKernelGGL((instnorm_fwd_v4<1024, 0>), dim3(planes), dim3(1024), 0, st, a);
   DSG_CHECK_LAUNCH();
   return 0;
 }

@@ -46,6 +46,8 @@ struct PwArgs {
   unsigned a_range, b_range;   // buffer-resource byte ranges of A and B (B: per image for FWD/DGRAD)
   int y_bf16;  // FWD: Y is bf16 [b][M][P] (y_bs in elements)
   int gbf;     // FWD: ypre is bf16 and receives act'(pre);  DGRAD: gpre is a bf16 multiplier (no act')
+  float* asum; // WGRAD (nullable): db[m] += sum_k A[m][k] -- the bias grad of the layer whose output
+               // grad is A, from the staged A tiles (split partials after the S*M*N weight partials)
 };
 
 constexpr int PBK = 32;                 // K per main-loop step
@@ -73,12 +75,12 @@ __device__ __forceinline__ pbf16x4 cvt4(float4 v, int bact, float slope) {
   return r;
 }
 
-// ABF (WGRAD only) / BBF (WGRAD, FWD): the A (dy) / B (x) operand is bf16 in HBM -- the gelu(z)
-// and dz tensors of the MLPs (mlp.hip, and the unfused blocks' pwconv1 bf16 output g = gelu(z))
-// tensors written by the fused MLP backward (mlp.hip) -- and is copied to LDS unconverted.
+// ABF (WGRAD only) / BBF: the A (dy) / B (x, dy) operand is bf16 in HBM -- the block activation h
+// (InstanceNorm bf16 output), gelu(z) and dz of the MLPs (mlp.hip and the unfused blocks) -- and
+// is copied to LDS unconverted.
 template <int MODE, int BM, int ABF = 0, int BBF = 0>
 __global__ __launch_bounds__(256, 2) void pwgemm_kernel(PwArgs g) {
-  static_assert((MODE == PW_WGRAD || ABF == 0) && (MODE != PW_DGRAD || BBF == 0), "bf16 operand modes");
+  static_assert(MODE == PW_WGRAD || ABF == 0, "bf16 operand modes");
   constexpr int BN = 128;
   constexpr int WM = 2, WN = 2;
   constexpr int TM = BM / WM / 32, TN = BN / WN / 32;
@@ -127,6 +129,9 @@ __global__ __launch_bounds__(256, 2) void pwgemm_kernel(PwArgs g) {
   constexpr int B_ITEMS = BBF ? BN * 4 / 256 : (B_KMAJ ? PBK * BN / 4 : BN * 8) / 256;
   float4 ra[ABF ? 1 : A_ITEMS], rb[BBF ? 1 : B_ITEMS];
   pu32x4 rha[ABF ? A_ITEMS : 1], rhb[BBF ? B_ITEMS : 1];
+  float asr[A_ITEMS];   // WGRAD asum: this thread's running row sums of its A items (fixed order)
+#pragma unroll
+  for (int i = 0; i < A_ITEMS; ++i) asr[i] = 0.f;
 
   // Operand loads are 16-byte buffer loads: an element outside its tensor gets the offset
   // PW_OOB, past every resource range, and reads 0 in hardware -- no branch, no mask VALU.
@@ -174,7 +179,7 @@ __global__ __launch_bounds__(256, 2) void pwgemm_kernel(PwArgs g) {
       }
       ra[i] = bld4(rA, off);
     }
-    if constexpr (BBF && MODE == PW_FWD) {       // X[b][K][P] bf16, k-major: row k, 8 pixels per item
+    if constexpr (BBF && MODE != PW_WGRAD) {     // X/DY[b][K][P] bf16, k-major: row k, 8 pixels per item
 #pragma unroll
       for (int i = 0; i < B_ITEMS; ++i) {
         const int it = tid + i * 256;
@@ -212,6 +217,11 @@ __global__ __launch_bounds__(256, 2) void pwgemm_kernel(PwArgs g) {
       for (int i = 0; i < A_ITEMS; ++i) {
         const int it = tid + i * 256;
         *reinterpret_cast<pu32x4*>(As + (it >> 2) * A_STR + (it & 3) * 8) = rha[i];
+        if (MODE == PW_WGRAD && g.asum) {
+          const pbf16x8 hv = __builtin_bit_cast(pbf16x8, rha[i]);
+          asr[i] += (((float)hv[0] + (float)hv[1]) + ((float)hv[2] + (float)hv[3])) +
+                    (((float)hv[4] + (float)hv[5]) + ((float)hv[6] + (float)hv[7]));
+        }
       }
     } else
 #pragma unroll
@@ -221,6 +231,7 @@ __global__ __launch_bounds__(256, 2) void pwgemm_kernel(PwArgs g) {
       if (A_KMAJ) off = (it / (BM / 4)) * A_STR + (it % (BM / 4)) * 4;
       else off = (it >> 3) * A_STR + (it & 7) * 4;
       *reinterpret_cast<pbf16x4*>(As + off) = cvt4(ra[i], 0, 0.f);
+      if (MODE == PW_WGRAD && g.asum) asr[i] += (ra[i].x + ra[i].y) + (ra[i].z + ra[i].w);
     }
     auto bstore = [&](auto cv) {
 #pragma unroll
@@ -232,7 +243,7 @@ __global__ __launch_bounds__(256, 2) void pwgemm_kernel(PwArgs g) {
         *reinterpret_cast<pbf16x4*>(Bs + off) = cv(rb[i]);
       }
     };
-    if constexpr (BBF && MODE == PW_FWD) {
+    if constexpr (BBF && MODE != PW_WGRAD) {
 #pragma unroll
       for (int i = 0; i < B_ITEMS; ++i) {
         const int it = tid + i * 256;
@@ -322,6 +333,22 @@ __global__ __launch_bounds__(256, 2) void pwgemm_kernel(PwArgs g) {
 
   // ---- epilogue ----
   if (MODE == PW_WGRAD) {
+    if (g.asum) {
+      // the threads of one A row (4 bf16 / 8 fp32 items per 32-pixel row) are adjacent lanes:
+      // butterfly over them; the n-tile-0 workgroup writes (its split's partial, or db += when unsplit)
+      constexpr int RT = ABF ? 4 : 8;
+#pragma unroll
+      for (int i = 0; i < A_ITEMS; ++i) {
+        float t = asr[i];
+        t += __shfl_xor(t, 1, 64); t += __shfl_xor(t, 2, 64);
+        if (RT == 8) t += __shfl_xor(t, 4, 64);
+        const int it = tid + i * 256, m = m0 + it / RT;
+        if (n_t == 0 && it % RT == 0 && m < g.M) {
+          if (g.ws) g.ws[(long)gridDim.x / mt / nt * g.M * g.N + (long)split * g.M + m] = t;
+          else g.asum[m] += t;
+        }
+      }
+    }
     // splits > 1: this split's partial tile (plain stores); one split: the only writer, +=
     float* dst = g.ws ? g.ws + (long)split * g.M * g.N : g.Y;
 #pragma unroll
@@ -534,7 +561,10 @@ void launch_split_reduce(const float* ws, int splits, long MN, float* dw, hipStr
 }
 
 static void wgrad_finish(const PwArgs& g, int splits, hipStream_t st) {
-  if (splits > 1) launch_split_reduce(g.ws, splits, (long)g.M * g.N, g.Y, st);
+  if (splits > 1) {
+    launch_split_reduce(g.ws, splits, (long)g.M * g.N, g.Y, st);
+    if (g.asum) launch_split_reduce(g.ws + (long)splits * g.M * g.N, splits, g.M, g.asum, st);
+  }
 }
 
 static bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
@@ -590,6 +620,8 @@ extern "C" int dsgan_pw_gemm(int mode, const float* A, long a_bs, const float* B
     const int splits = wgrad_split(g, BM);
     DSG_REQUIRE(splits == 1 || ws, "dsgan_pw_gemm: WGRAD needs the dsgan_pw_wgrad_workspace scratch");
     g.ws = splits > 1 ? ws : nullptr;
+    g.asum = const_cast<float*>(bias);   // WGRAD: bias (nullable) receives the bias grad += sum_k A
+    g.bias = nullptr;
     if (BM == 128) pw_launch<PW_WGRAD, 128>(g, splits, st);
     else pw_launch<PW_WGRAD, 64>(g, splits, st);
     wgrad_finish(g, splits, st);
@@ -650,42 +682,56 @@ extern "C" int dsgan_pw_fwd_io(const float* W, const void* X, long x_bs, int x_b
   return 0;
 }
 
-// Data-grad with a bf16 multiplier: DX[b][M][p] (+)= (sum_k W[k][M] DY[b][k][p]) * GP[b][M][p],
-// GP = act'(pre) written by dsgan_pw_fwd_io (ypre_grad_bf16).  P % 128 == 0, 16-byte aligned.
-extern "C" int dsgan_pw_dgrad_gbf(const float* W, const float* DY, long dy_bs, float* DX, long dx_bs, const void* GP,
-                                  long gp_bs, int M, int K, int P, int nb, int accumulate, hipStream_t st) {
-  DSG_REQUIRE(W && DY && DX && GP && M > 0 && K > 0 && nb > 0, "dsgan_pw_dgrad_gbf: bad args");
-  DSG_REQUIRE(dsgan_pw_supported(PW_DGRAD, M, K, P, 0, dy_bs, W, DY) && al16(GP) && (gp_bs & 7) == 0,
-              "dsgan_pw_dgrad_gbf: unsupported shape/alignment");
-  DSG_REQUIRE((long)M * P * 4 < (1L << 32) && (long)K * P * 4 < (long)PW_OOB, "dsgan_pw_dgrad_gbf: operand too large");
+// Data-grad with bf16 operands/outputs (the unfused MLP blocks' backward):
+//   DX[b][M][p] (+)= (sum_k W[k][M] DY[b][k][p]) (* GP[b][M][p])
+// DY fp32 or bf16 (dy_bf16), DX fp32 or bf16 (dx_bf16; accumulate needs fp32), GP (nullable) the bf16
+// act'(pre) written by dsgan_pw_fwd_io (ypre_grad_bf16).  P % 128 == 0, 16-byte aligned.
+extern "C" int dsgan_pw_dgrad_io(const float* W, const void* DY, long dy_bs, int dy_bf16, void* DX, long dx_bs,
+                                 int dx_bf16, const void* GP, long gp_bs, int M, int K, int P, int nb,
+                                 int accumulate, hipStream_t st) {
+  DSG_REQUIRE(W && DY && DX && M > 0 && K > 0 && nb > 0, "dsgan_pw_dgrad_io: bad args");
+  DSG_REQUIRE(dsgan_pw_supported(PW_DGRAD, M, K, P, 0, dy_bs, W, DY) && al16(DX) && (dy_bs & 7) == 0 &&
+                  (dx_bs & 7) == 0 && (!GP || (al16(GP) && (gp_bs & 7) == 0)) && !(dx_bf16 && accumulate),
+              "dsgan_pw_dgrad_io: unsupported shape/alignment");
+  DSG_REQUIRE((long)M * P * 4 < (1L << 32) && (long)K * P * 4 < (long)PW_OOB, "dsgan_pw_dgrad_io: operand too large");
   PwArgs g{};
-  g.A = W; g.B = DY; g.b_bs = dy_bs; g.Y = DX; g.y_bs = dx_bs; g.gpre = (const float*)GP; g.gpre_bs = gp_bs; g.gbf = 1;
+  g.A = W; g.B = (const float*)DY; g.b_bs = dy_bs; g.Y = (float*)DX; g.y_bs = dx_bs; g.y_bf16 = dx_bf16;
+  g.gpre = (const float*)GP; g.gpre_bs = gp_bs; g.gbf = GP ? 1 : 0;
   g.accumulate = accumulate; g.P = P; g.M = M; g.N = nb * P; g.K = K;
   g.a_range = (unsigned)((long)M * K * 4);
-  g.b_range = (unsigned)((long)K * P * 4);
-  if (use_bm256(g)) pw_launch<PW_DGRAD, 256>(g, 1, st);
-  else if (M > 64) pw_launch<PW_DGRAD, 128>(g, 1, st);
-  else pw_launch<PW_DGRAD, 64>(g, 1, st);
+  g.b_range = (unsigned)((long)K * P * (dy_bf16 ? 2 : 4));
+  const bool b256 = use_bm256(g);
+  if (dy_bf16) {
+    if (b256) pw_launch<PW_DGRAD, 256, 0, 1>(g, 1, st);
+    else if (M > 64) pw_launch<PW_DGRAD, 128, 0, 1>(g, 1, st);
+    else pw_launch<PW_DGRAD, 64, 0, 1>(g, 1, st);
+  } else {
+    if (b256) pw_launch<PW_DGRAD, 256>(g, 1, st);
+    else if (M > 64) pw_launch<PW_DGRAD, 128>(g, 1, st);
+    else pw_launch<PW_DGRAD, 64>(g, 1, st);
+  }
   DSG_CHECK_LAUNCH();
   return 0;
 }
 
 // Weight-grad with bf16 operand(s): DW[M][N] += sum_{b,p} A[b][M][P] * B[b][N][P], A/B fp32 or
-// bf16 (a_bf16 / b_bf16).  P % 32 == 0, 16-byte aligned operands.
+// bf16 (a_bf16 / b_bf16); db (nullable) += sum_{b,p} A[b][M][P] -- the bias grad, summed from the
+// staged A tiles (the bf16 values when A is bf16).  P % 32 == 0, 16-byte aligned operands.
 // Scratch (floats) a weight-grad of M x N over nb*P pixels needs (0: no split).
 extern "C" long dsgan_pw_wgrad_workspace(int M, int N, int P, int nb) {
   int ks;
   const int splits = wgrad_plan(M, N, (long)nb * P, M > 64 ? 128 : 64, &ks);
-  return splits > 1 ? (long)splits * M * N : 0;
+  return splits > 1 ? (long)splits * ((long)M * N + M) : 0;   // weight partials, then bias-sum partials
 }
 
 extern "C" int dsgan_pw_wgrad_mixed(const void* A, long a_bs, int a_bf16, const void* B, long b_bs,
-                                    int b_bf16, float* DW, int M, int N, int P, int nb, float* ws, hipStream_t st) {
+                                    int b_bf16, float* DW, float* db, int M, int N, int P, int nb, float* ws,
+                                    hipStream_t st) {
   DSG_REQUIRE(A && B && DW && M >= 16 && N > 0 && P > 0 && nb > 0, "dsgan_pw_wgrad_mixed: bad args");
   DSG_REQUIRE(P % 32 == 0 && al16(A) && al16(B) && (a_bs & 7) == 0 && (b_bs & 7) == 0,
               "dsgan_pw_wgrad_mixed: P %% 32 and 16-byte alignment required");
   PwArgs g{};
-  g.A = (const float*)A; g.a_bs = a_bs; g.B = (const float*)B; g.b_bs = b_bs; g.Y = DW; g.P = P;
+  g.A = (const float*)A; g.a_bs = a_bs; g.B = (const float*)B; g.b_bs = b_bs; g.Y = DW; g.asum = db; g.P = P;
   const long ar = ((long)(nb - 1) * a_bs + (long)M * P) * (a_bf16 ? 2 : 4);
   const long br = ((long)(nb - 1) * b_bs + (long)N * P) * (b_bf16 ? 2 : 4);
   DSG_REQUIRE(ar < (long)PW_OOB && br < (long)PW_OOB, "dsgan_pw_wgrad_mixed: operands exceed 4 GiB buffer range");

@@ -30,17 +30,19 @@ SIGNATURES = {
     "dsgan_pw_supported": [I, I, I, I, L, L, P, P],
     "dsgan_pw_gemm": [I, P, L, P, L, P, L, P, P, L, P, L, I, I, I, I, I, I, I, I, I, F, P, S],
     "dsgan_pw_wgrad_workspace": [I, I, I, I],
-    "dsgan_pw_wgrad_mixed": [P, L, I, P, L, I, P, I, I, I, I, P, S],
+    "dsgan_pw_wgrad_mixed": [P, L, I, P, L, I, P, P, I, I, I, I, P, S],
     "dsgan_pw_fwd_io": [P, P, L, I, P, L, I, P, L, I, P, I, I, I, I, I, I, F, S],
-    "dsgan_pw_dgrad_gbf": [P, P, L, P, L, P, L, I, I, I, I, I, S],
+    "dsgan_pw_dgrad_io": [P, P, L, I, P, L, I, P, L, I, I, I, I, I, S],
     # pwf32.hip
     "dsgan_pw_f32_supported": [I, I, I, I, L, L, P, P],
     "dsgan_pw_f32_wgrad_workspace": [I, I, I, I],
     "dsgan_pw_gemm_f32": [I, P, L, P, L, P, L, P, P, L, I, I, I, I, I, I, I, I, F, P, S],
     # mlp.hip
     "dsgan_mlp_supported": [I, I, I],
-    "dsgan_mlp_fwd": [P, L, P, P, P, P, P, L, I, I, I, I, I, S],
-    "dsgan_mlp_bwd": [P, L, P, L, P, P, P, P, L, P, P, P, I, I, I, I, S],
+    "dsgan_mlp_fwd": [P, L, I, P, P, P, P, P, L, I, I, I, I, I, S],
+    "dsgan_mlp_bwd": [P, L, I, P, L, P, P, P, P, L, P, P, P, I, I, I, I, S],
+    "dsgan_mlp_wgrad_workspace": [I, I, I, I],
+    "dsgan_mlp_wgrad": [P, L, I, P, L, P, P, P, P, P, P, P, I, I, I, I, S],
     "dsgan_colsum": [P, I, I, P, S],
     "dsgan_f32_to_bf16": [P, P, L, S],
     # pconv.hip
@@ -72,6 +74,7 @@ SIGNATURES = {
     "dsgan_dwconv_wgrad": [P, L, P, L, P, P, I, I, I, I, I, P, S],
     # norm_pointwise.hip
     "dsgan_instnorm_fwd": [P, L, P, P, L, P, L, P, P, I, I, I, I, F, F, S],
+    "dsgan_instnorm_fwd_bf16": [P, L, P, L, P, P, I, I, I, F, S],
     "dsgan_instnorm_bwd": [P, L, P, L, P, P, L, P, P, P, L, P, L, P, I, I, I, I, F, F, S],
     "dsgan_maxpool_fwd": [P, L, P, L, P, I, I, I, I, I, S],
     "dsgan_maxpool_bwd": [P, L, P, P, L, I, I, I, I, I, I, S],

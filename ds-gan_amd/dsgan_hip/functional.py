@@ -400,7 +400,10 @@ def conv_dgrad_raw(dy, w, x_shape, stride, pad, bias=None, act=None, gpre=None, 
     return dx
 
 
-def conv_wgrad_raw(dy, x, dw, stride, pad, xact=None):
+def conv_wgrad_raw(dy, x, dw, stride, pad, xact=None, db=None):
+    """dw += conv weight-grad; db (optional) += the bias grad sum(dy) when the kernel taken can fold
+    it into the weight-grad (the bf16 pointwise path).  Returns True when db was accumulated."""
+    did_db = False
     dy, dybs = nchw(dy)
     x, xbs = nchw(x)
     N, Cin, H, W = x.shape
@@ -416,7 +419,8 @@ def conv_wgrad_raw(dy, x, dw, stride, pad, xact=None):
              stride, pad, dy.shape[2], dy.shape[3], ptr(ws), stream())
     elif KH == 1 and KW == 1 and stride == 1 and pad == 0 and _pw_ok(2, Cout, N * H * W, H * W, dybs, xbs, dy.data_ptr(), x.data_ptr()):
         fam = "pwgemm_kernel"
-        call("dsgan_pw_gemm", 2, ptr(dy), dybs, ptr(x), xbs, ptr(dw), 0, None, None, 0, None, 0,
+        did_db = db is not None
+        call("dsgan_pw_gemm", 2, ptr(dy), dybs, ptr(x), xbs, ptr(dw), 0, ptr(db), None, 0, None, 0,
              Cout, Cin, N * H * W, H * W, N, 0, 0, ACT[xact], 0, LRELU_SLOPE, ptr(_pw_ws(Cout, Cin, H * W, N, dy)),
              stream())
     elif (KH == 1 and KW == 1 and stride == 1 and pad == 0 and xact is None
@@ -441,6 +445,7 @@ def conv_wgrad_raw(dy, x, dw, stride, pad, xact=None):
              stride, pad, dy.shape[2], dy.shape[3], ACT[xact], _prec(), ptr(ws), stream())
     IGEMM_TIMER.end(e0, _conv_flops(N, Cin, Cout, KH, KW, dy.shape[2], dy.shape[3]),
                     ("wgrad", N, Cin, H, W, Cout, KH, stride), fam, _nb(dy, x, dw))
+    return did_db
 
 
 def channel_sum_raw(dy, out):
@@ -604,9 +609,9 @@ class Conv2dFn(torch.autograd.Function):
             dx = conv_dgrad_raw(dy, w, ctx.x_shape, ctx.stride, ctx.pad, out=out, accumulate=acc)
             dx = None if acc else _give(ctx.box, dx)
         gw = _grad_buf(ctx.w_ref) if ctx.needs_input_grad[1] else None
-        if gw is not None:
-            conv_wgrad_raw(dy, x, gw, ctx.stride, ctx.pad)
         gb = _grad_buf(ctx.b_ref) if (b is not None and ctx.needs_input_grad[2]) else None
+        if gw is not None and conv_wgrad_raw(dy, x, gw, ctx.stride, ctx.pad, db=gb):
+            gb = None
         if gb is not None:
             channel_sum_raw(dy, gb)
         _params_done(ctx.w_ref, ctx.b_ref)
@@ -682,14 +687,11 @@ def bf16_weight(w):
     return out
 
 
-def _mlp_tile(h, x, P):
+def _mlp_tile(C, P, HW, x):
     """Pixels per b1-grad partial row of the fused MLP kernels (mlp.hip), 0 if unsupported."""
-    if _state["prec"] != "bf16":
+    if _state["prec"] != "bf16" or x.data_ptr() % 16:
         return 0
-    N, C, H, W = h.shape
-    if h.data_ptr() % 16 or x.data_ptr() % 16:
-        return 0
-    return int(_lib.load().dsgan_mlp_supported(C, P, H * W))
+    return int(_lib.load().dsgan_mlp_supported(C, P, HW))
 
 
 def _mlp_flops(N, C, P, HW):
@@ -698,43 +700,71 @@ def _mlp_flops(N, C, P, HW):
 
 
 class PwMlpFn(torch.autograd.Function):
-    """Block tail.  bf16 mode on the fused shapes (mlp.hip): forward out = Ws x (pwgemm) then
-    out += W2 gelu(W1 h + b1) + b2 in one kernel -- z is never stored; backward recomputes z
-    and writes only bf16 gelu(z) and dz for the two weight-grads.  Otherwise (fp32 parity mode,
-    other shapes) only the pre-GELU hidden z [N,4C,H,W] is materialised: pwconv2 and its
-    weight-grad read gelu(z) through the GEMM's activation-on-load, and the data-grad of pwconv2
-    multiplies by gelu'(z) in its epilogue."""
+    """Block tail: out = Ws x + W2 gelu(W1 h + b1) + b2, h = IN(d) when ``norm`` (the block's
+    InstanceNorm, MixConvNeXtML.py:221, folded into this node so that h never needs an fp32 copy).
+
+    In bf16 mode h is stored bf16 (dsgan_instnorm_fwd_bf16): its only readers are bf16-operand
+    MFMA GEMMs that round it to bf16 on load anyway, so this halves its bytes and changes no bit.
+      * fused shapes (mlp.hip): forward out = Ws x (pwgemm), then out += W2 gelu(W1 h + b1) + b2 in
+        one kernel -- z is never stored; backward recomputes z and writes only bf16 gelu(z) and dz
+        for the two weight-grads.
+      * other bf16 shapes with HW % 128 == 0: pwconv1 evaluates GELU once and writes g = gelu(z) and
+        gp = gelu'(z), both bf16; backward writes dz = (W2^T dy) * gp in bf16 (again exactly what
+        its two GEMM readers would round to) with the b1 grad summed from the fp32 values in the
+        same epilogue.
+      * otherwise (fp32 parity mode, tiny shapes) only the pre-GELU hidden z [N,4C,H,W] (fp32) is
+        materialised: pwconv2 and its weight-grad read gelu(z) through the GEMM's
+        activation-on-load, and the data-grad of pwconv2 multiplies by gelu'(z) in its epilogue."""
 
     @staticmethod
-    def forward(ctx, h, x, w1, b1, w2, b2, ws):
+    def forward(ctx, h, x, w1, b1, w2, b2, ws, norm=False):
         N, C, H, W = h.shape
-        P = w2.shape[0]
-        h, hbs = nchw(h)
-        tile = _mlp_tile(h, x, P)
+        P, HW, C4 = w2.shape[0], H * W, 4 * C
         ctx.refs = (w1, b1, w2, b2, ws)
-        ctx.tile = tile
         ctx.prec = _state["prec"]
         ctx.box_h, ctx.box_x = _box(h), _box(x)
+        h, hbs = nchw(h)
+        tile = _mlp_tile(C, P, HW, x)
+        bigg = (not tile and _state["prec"] == "bf16" and HW % 128 == 0 and C % 8 == 0
+                and (norm or h.data_ptr() % 16 == 0))
+        ctx.nrm = None
+        if norm:
+            d, dbs = h, hbs
+            if (tile or bigg) and d.data_ptr() % 16 == 0 and dbs % 4 == 0 and HW % 4 == 0:
+                mean = torch.empty(N * C, device=d.device, dtype=torch.float32)
+                rstd = torch.empty(N * C, device=d.device, dtype=torch.float32)
+                h = torch.empty((N, C, H, W), device=d.device, dtype=torch.bfloat16)
+                call("dsgan_instnorm_fwd_bf16", ptr(d), dbs, ptr(h), C * HW, ptr(mean), ptr(rstd), N, C, HW, IN_EPS,
+                     stream())
+            else:
+                h, mean, rstd = instnorm_raw(d)
+                tile = tile if h.data_ptr() % 16 == 0 else 0
+            hbs = C * HW
+            ctx.nrm = (d, mean, rstd)
+        elif h.data_ptr() % 16:
+            tile = 0
+        hb = int(h.dtype == torch.bfloat16)
+        ctx.hb = hb
+        ctx.tile = tile
         if tile:
             out = conv_fwd_raw(x, ws, None, 1, 0)
             e0 = IGEMM_TIMER.begin()
-            call("dsgan_mlp_fwd", ptr(h), hbs, ptr(bf16_weight(w1)), ptr(b1), ptr(bf16_weight(w2)), ptr(b2),
-                 ptr(out), P * H * W, N, C, P, H * W, 1, stream())
-            IGEMM_TIMER.end(e0, _mlp_flops(N, C, P, H * W), ("mlp_fwd", N, C, H, W, P, 1, 1), "mlp_fwd_kernel",
+            call("dsgan_mlp_fwd", ptr(h), hbs, hb, ptr(bf16_weight(w1)), ptr(b1), ptr(bf16_weight(w2)), ptr(b2),
+                 ptr(out), P * HW, N, C, P, HW, 1, stream())
+            IGEMM_TIMER.end(e0, _mlp_flops(N, C, P, HW), ("mlp_fwd", N, C, H, W, P, 1, 1), "mlp_fwd_kernel",
                             _nb(h, w1, b1, w2, b2) + 2 * _nb(out))
             ctx.save_for_backward(h, x, ws)
             return out
         w1v = w1.view(w1.shape[0], w1.shape[1], 1, 1)
         w2v = w2.view(w2.shape[0], w2.shape[1], 1, 1)
         ctx.g = None
-        if _state["prec"] == "bf16" and H * W % 128 == 0 and C % 8 == 0 and h.data_ptr() % 16 == 0:
+        if bigg:
             # large blocks: pwconv1 evaluates GELU once and writes g = gelu(z) and gp = gelu'(z), both
             # bf16; pwconv2 and the W2 weight-grad stream g, the pwconv2 data-grad multiplies by gp
-            C4, HW = 4 * C, H * W
             gp = torch.empty((N, C4, H, W), device=h.device, dtype=torch.bfloat16)   # gelu'(z), for dz
             g = torch.empty((N, C4, H, W), device=h.device, dtype=torch.bfloat16)    # gelu(z)
             e0 = IGEMM_TIMER.begin()
-            call("dsgan_pw_fwd_io", ptr(w1), ptr(h), hbs, 0, ptr(g), C4 * HW, 1, ptr(gp), C4 * HW, 1, ptr(b1), C4, C,
+            call("dsgan_pw_fwd_io", ptr(w1), ptr(h), hbs, hb, ptr(g), C4 * HW, 1, ptr(gp), C4 * HW, 1, ptr(b1), C4, C,
                  HW, N, ACT["gelu"], 0, LRELU_SLOPE, stream())
             IGEMM_TIMER.end(e0, 2.0 * N * HW * C4 * C, ("fwd", N, C, H, W, C4, 1, 1), "pwgemm_kernel",
                             _nb(h, w1, b1, g, gp))
@@ -749,13 +779,13 @@ class PwMlpFn(torch.autograd.Function):
             return out
         z = conv_fwd_raw(h, w1v, b1, 1, 0)
         x4, xbs = nchw(x)
-        if 5 * C <= 16 and _pws_ok(5 * C, P, H * W, xbs, P * H * W, x4, z) and z.data_ptr() % 16 == 0:
+        if 5 * C <= 16 and _pws_ok(5 * C, P, HW, xbs, P * HW, x4, z) and z.data_ptr() % 16 == 0:
             # tiny blocks (c1: 3 -> 12 -> 64 at 256^2): shortcut + pwconv2 in one streaming pass
             out = _empty(N, P, H, W, h)
             e0 = IGEMM_TIMER.begin()
-            call("dsgan_pw_small2", ptr(x4), xbs, ptr(ws), C, 1, ptr(z), 4 * C * H * W, ptr(w2), 4 * C, ptr(b2),
-                 ptr(out), P * H * W, None, 0, N, C, P, H * W, 0, ACT["gelu"], 0, 0, LRELU_SLOPE, stream())
-            IGEMM_TIMER.end(e0, 2.0 * N * H * W * P * 5 * C, ("fwd", N, 5 * C, H, W, P, 1, 1), "pw_small_kernel",
+            call("dsgan_pw_small2", ptr(x4), xbs, ptr(ws), C, 1, ptr(z), 4 * C * HW, ptr(w2), 4 * C, ptr(b2),
+                 ptr(out), P * HW, None, 0, N, C, P, HW, 0, ACT["gelu"], 0, 0, LRELU_SLOPE, stream())
+            IGEMM_TIMER.end(e0, 2.0 * N * HW * P * 5 * C, ("fwd", N, 5 * C, H, W, P, 1, 1), "pw_small_kernel",
                             _nb(x4, z, out, ws, w2, b2))
         else:
             out = conv_fwd_raw(x, ws, None, 1, 0)
@@ -767,48 +797,78 @@ class PwMlpFn(torch.autograd.Function):
     def backward(ctx, dy):
         with precision(ctx.prec):
             if ctx.tile:
-                return PwMlpFn._backward_fused(ctx, dy)
-            return PwMlpFn._backward_unfused(ctx, dy)
+                dh, dx = PwMlpFn._backward_fused(ctx, dy)
+            else:
+                dh, dx = PwMlpFn._backward_unfused(ctx, dy)
+            if dh is not None and ctx.nrm is not None:
+                d, mean, rstd = ctx.nrm
+                dh = instnorm_bwd_raw(dh, d, None, None, mean, rstd, None, False, False)[0]
+            ctx.nrm = None
+        return _give(ctx.box_h, dh), dx, None, None, None, None, None, None
 
     @staticmethod
     def _backward_unfused(ctx, dy):
         h, x, z, w1v, w2v, ws = ctx.saved_tensors
         w1, b1, w2, b2, ws_ref = ctx.refs
         dy = dy.contiguous()
-        # dz = (W2^T dy) * gelu'(z)   (z slot holds the bf16 gelu'(z) on the bf16-g path)
+        gw2, gb2, gws, gw1, gb1 = (_grad_buf(t) for t in (w2, b2, ws_ref, w1, b1))
+        want_dh = ctx.needs_input_grad[0]
         if ctx.g is not None:
+            # bf16 g/gp path (z slot holds gp = gelu'(z)): dz = (W2^T dy) * gp stored bf16, the b1
+            # grad as fp32 partial row sums of the same epilogue
             N, C4, H, W = z.shape
-            dz = _empty(N, C4, H, W, dy)
+            HW, P, C = H * W, w2.shape[0], h.shape[1]
+            dz = torch.empty((N, C4, H, W), device=dy.device, dtype=torch.bfloat16)
             e0 = IGEMM_TIMER.begin()
-            call("dsgan_pw_dgrad_gbf", ptr(w2), ptr(dy), w2.shape[0] * H * W, ptr(dz), C4 * H * W, ptr(z), C4 * H * W,
-                 C4, w2.shape[0], H * W, N, 0, stream())
-            IGEMM_TIMER.end(e0, 2.0 * N * H * W * C4 * w2.shape[0], ("dgrad", N, C4, H, W, w2.shape[0], 1, 1),
-                            "pwgemm_kernel", _nb(dy, w2, dz, z))
-        else:
-            dz = conv_dgrad_raw(dy, w2v, tuple(z.shape), 1, 0, gpre=z, gact="gelu")
-        gw2, gb2, gws = _grad_buf(w2), _grad_buf(b2), _grad_buf(ws_ref)
-        if gw2 is not None and ctx.g is not None:
-            N, C4, H, W = z.shape
-            dy4, dybs = nchw(dy)
-            e0 = IGEMM_TIMER.begin()
-            call("dsgan_pw_wgrad_mixed", ptr(dy4), dybs, 0, ptr(ctx.g), C4 * H * W, 1, ptr(gw2), w2.shape[0], C4,
-                 H * W, N, ptr(_pw_ws(w2.shape[0], C4, H * W, N, dy)), stream())
-            IGEMM_TIMER.end(e0, 2.0 * N * H * W * C4 * w2.shape[0], ("wgrad", N, C4, H, W, w2.shape[0], 1, 1),
-                            "pwgemm_kernel", _nb(dy4, ctx.g, gw2))
-        elif gw2 is not None:
-            conv_wgrad_raw(dy, z, gw2.view(w2v.shape), 1, 0, xact="gelu")
+            call("dsgan_pw_dgrad_io", ptr(w2), ptr(dy), P * HW, 0, ptr(dz), C4 * HW, 1, ptr(z), C4 * HW,
+                 C4, P, HW, N, 0, stream())
+            IGEMM_TIMER.end(e0, 2.0 * N * HW * C4 * P, ("dgrad", N, C4, H, W, P, 1, 1), "pwgemm_kernel",
+                            _nb(dy, w2, dz, z))
+            # bias grads ride on the weight-grads' staged A tiles (db += sum_k A): b2 from dy, b1 from
+            # the bf16 dz (as the fused kernels sum it)
+            if gw2 is not None:
+                e0 = IGEMM_TIMER.begin()
+                call("dsgan_pw_wgrad_mixed", ptr(dy), P * HW, 0, ptr(ctx.g), C4 * HW, 1, ptr(gw2), ptr(gb2), P, C4,
+                     HW, N, ptr(_pw_ws(P, C4, HW, N, dy)), stream())
+                IGEMM_TIMER.end(e0, 2.0 * N * HW * C4 * P, ("wgrad", N, C4, H, W, P, 1, 1), "pwgemm_kernel",
+                                _nb(dy, ctx.g, gw2))
+            elif gb2 is not None:
+                channel_sum_raw(dy, gb2)
+            if gws is not None:
+                conv_wgrad_raw(dy, x, gws, 1, 0)
+            if gw1 is not None:
+                e0 = IGEMM_TIMER.begin()
+                call("dsgan_pw_wgrad_mixed", ptr(dz), C4 * HW, 1, ptr(h), C * HW, ctx.hb, ptr(gw1), ptr(gb1), C4, C,
+                     HW, N, ptr(_pw_ws(C4, C, HW, N, dz)), stream())
+                IGEMM_TIMER.end(e0, 2.0 * N * HW * C4 * C, ("wgrad", N, C, H, W, C4, 1, 1), "pwgemm_kernel",
+                                _nb(dz, h, gw1))
+            elif gb1 is not None:   # frozen pwconv1 weight, trainable bias (not on the train path)
+                channel_sum_raw(dz.float(), gb1)
+            dh = None
+            if want_dh:
+                dh = _empty(N, C, H, W, dy)
+                e0 = IGEMM_TIMER.begin()
+                call("dsgan_pw_dgrad_io", ptr(w1), ptr(dz), C4 * HW, 1, ptr(dh), C * HW, 0, None, 0, C, C4, HW,
+                     N, 0, stream())
+                IGEMM_TIMER.end(e0, 2.0 * N * HW * C4 * C, ("dgrad", N, C4, H, W, C, 1, 1), "pwgemm_kernel",
+                                _nb(dz, w1, dh))
+            _params_done(*ctx.refs)
+            return dh, PwMlpFn._dx(ctx, dy, ws, x)
+        # fp32 z path: dz = (W2^T dy) * gelu'(z)
+        dz = conv_dgrad_raw(dy, w2v, tuple(z.shape), 1, 0, gpre=z, gact="gelu")
+        if gw2 is not None and conv_wgrad_raw(dy, z, gw2.view(w2v.shape), 1, 0, xact="gelu", db=gb2):
+            gb2 = None
         if gb2 is not None:
             channel_sum_raw(dy, gb2)
         if gws is not None:
             conv_wgrad_raw(dy, x, gws, 1, 0)
-        gw1, gb1 = _grad_buf(w1), _grad_buf(b1)
-        if gw1 is not None:
-            conv_wgrad_raw(dz, h, gw1.view(w1v.shape), 1, 0)
+        if gw1 is not None and conv_wgrad_raw(dz, h, gw1.view(w1v.shape), 1, 0, db=gb1):
+            gb1 = None
         if gb1 is not None:
             channel_sum_raw(dz, gb1)
-        dh = conv_dgrad_raw(dz, w1v, tuple(h.shape), 1, 0) if ctx.needs_input_grad[0] else None
+        dh = conv_dgrad_raw(dz, w1v, tuple(h.shape), 1, 0) if want_dh else None
         _params_done(*ctx.refs)
-        return _give(ctx.box_h, dh), PwMlpFn._dx(ctx, dy, ws, x), None, None, None, None, None
+        return dh, PwMlpFn._dx(ctx, dy, ws, x)
 
     @staticmethod
     def _dx(ctx, dy, ws, x):
@@ -828,20 +888,41 @@ class PwMlpFn(torch.autograd.Function):
         dy, dybs = nchw(dy)
         if dy.data_ptr() % 16:
             dy, dybs = dy.contiguous(), P * HW
+        gw2, gb2, gws, gw1, gb1 = (_grad_buf(t) for t in (w2, b2, ws_ref, w1, b1))
+        dh = _empty(N, C, H, W, h)
+        if gw1 is not None and gb1 is not None and gw2 is not None:
+            # dh from the data-path kernel; dW1 / db1 / dW2 from the weight-path kernel, which
+            # recomputes z and dz per hidden chunk -- gelu(z) and dz never reach HBM
+            w1b, w2b = bf16_weight(w1), bf16_weight(w2)
+            e0 = IGEMM_TIMER.begin()
+            call("dsgan_mlp_bwd", ptr(h), C * HW, ctx.hb, ptr(dy), dybs, ptr(w1b), ptr(b1), ptr(w2b), ptr(dh), C * HW,
+                 None, None, None, N, C, P, HW, stream())
+            IGEMM_TIMER.end(e0, 2.0 * N * HW * C4 * (2 * C + P), ("mlp_bwd", N, C, H, W, P, 1, 1), "mlp_bwd_kernel",
+                            _nb(h, dy, w1, b1, w2, dh))
+            wsp = torch.empty(_lib.load().dsgan_mlp_wgrad_workspace(C, P, HW, N), device=h.device, dtype=torch.float32)
+            e0 = IGEMM_TIMER.begin()
+            call("dsgan_mlp_wgrad", ptr(h), C * HW, ctx.hb, ptr(dy), dybs, ptr(w1b), ptr(b1), ptr(w2b), ptr(gw1),
+                 ptr(gb1), ptr(gw2), ptr(wsp), N, C, P, HW, stream())
+            IGEMM_TIMER.end(e0, 2.0 * N * HW * C4 * (2 * C + 2 * P), ("mlp_wgrad", N, C, H, W, P, 1, 1),
+                            "mlp_wgrad_kernel", _nb(h, dy, w1, b1, w2, gw1, gb1, gw2))
+            if gb2 is not None:
+                channel_sum_raw(dy, gb2)
+            if gws is not None:
+                conv_wgrad_raw(dy, x, gws, 1, 0)
+            _params_done(*ctx.refs)
+            return dh, PwMlpFn._dx(ctx, dy, ws, x)
         ntiles = N * HW // ctx.tile
         g = torch.empty((N, C4, H, W), device=h.device, dtype=torch.bfloat16)
         dz = torch.empty_like(g)
         bsum = torch.empty((ntiles, C4), device=h.device, dtype=torch.float32)
-        dh = _empty(N, C, H, W, h)
         e0 = IGEMM_TIMER.begin()
-        call("dsgan_mlp_bwd", ptr(h), C * HW, ptr(dy), dybs, ptr(bf16_weight(w1)), ptr(b1), ptr(bf16_weight(w2)),
-             ptr(dh), C * HW, ptr(g), ptr(dz), ptr(bsum), N, C, P, HW, stream())
+        call("dsgan_mlp_bwd", ptr(h), C * HW, ctx.hb, ptr(dy), dybs, ptr(bf16_weight(w1)), ptr(b1),
+             ptr(bf16_weight(w2)), ptr(dh), C * HW, ptr(g), ptr(dz), ptr(bsum), N, C, P, HW, stream())
         IGEMM_TIMER.end(e0, _mlp_flops(N, C, P, HW), ("mlp_bwd", N, C, H, W, P, 1, 1), "mlp_bwd_kernel",
                         _nb(h, dy, w1, b1, w2, dh, g, dz, bsum))
-        gw2, gb2, gws, gw1, gb1 = (_grad_buf(t) for t in (w2, b2, ws_ref, w1, b1))
         if gw2 is not None:
             e0 = IGEMM_TIMER.begin()
-            call("dsgan_pw_wgrad_mixed", ptr(dy), dybs, 0, ptr(g), C4 * HW, 1, ptr(gw2), P, C4, HW, N,
+            call("dsgan_pw_wgrad_mixed", ptr(dy), dybs, 0, ptr(g), C4 * HW, 1, ptr(gw2), None, P, C4, HW, N,
                  ptr(_pw_ws(P, C4, HW, N, dy)), stream())
             IGEMM_TIMER.end(e0, 2.0 * N * HW * C4 * P, ("wgrad", N, C4, H, W, P, 1, 1), "pwgemm_kernel",
                             _nb(dy, g, gw2))
@@ -851,18 +932,20 @@ class PwMlpFn(torch.autograd.Function):
             conv_wgrad_raw(dy, x, gws, 1, 0)
         if gw1 is not None:
             e0 = IGEMM_TIMER.begin()
-            call("dsgan_pw_wgrad_mixed", ptr(dz), C4 * HW, 1, ptr(h), C * HW, 0, ptr(gw1), C4, C, HW, N,
+            call("dsgan_pw_wgrad_mixed", ptr(dz), C4 * HW, 1, ptr(h), C * HW, ctx.hb, ptr(gw1), None, C4, C, HW, N,
                  ptr(_pw_ws(C4, C, HW, N, dz)), stream())
             IGEMM_TIMER.end(e0, 2.0 * N * HW * C4 * C, ("wgrad", N, C, H, W, C4, 1, 1), "pwgemm_kernel",
                             _nb(dz, h, gw1))
         if gb1 is not None:
             call("dsgan_colsum", ptr(bsum), ntiles, C4, ptr(gb1), stream())
         _params_done(*ctx.refs)
-        return _give(ctx.box_h, dh), PwMlpFn._dx(ctx, dy, ws, x), None, None, None, None, None
+        return dh, PwMlpFn._dx(ctx, dy, ws, x)
 
 
-def pw_mlp(h, x, w1, b1, w2, b2, ws):
-    return PwMlpFn.apply(h, x, w1, b1, w2, b2, ws)
+def pw_mlp(h, x, w1, b1, w2, b2, ws, norm=False):
+    """ConvNeXt block tail; with norm=True the first argument is the depthwise-conv output d and
+    the block's InstanceNorm h = IN(d) is applied inside (MixConvNeXtML.py:219-224)."""
+    return PwMlpFn.apply(h, x, w1, b1, w2, b2, ws, norm)
 
 
 # ------------------------------------------------------------------------------------------

@@ -119,9 +119,10 @@ class Block(nn.Module):
 
     def forward(self, x):
         x = HF.share(x)   # read by the depthwise conv and by the 1x1 shortcut
-        h = HF.instance_norm(HF.dwconv(x, self.dwconv.weight, self.dwconv.bias))
-        return HF.pw_mlp(h, x, self.pwconv1.weight, self.pwconv1.bias, self.pwconv2.weight,
-                         self.pwconv2.bias, self.shortcut.weight)
+        # norm=True: the block's InstanceNorm runs inside the MLP node (bf16 h, see PwMlpFn)
+        d = HF.dwconv(x, self.dwconv.weight, self.dwconv.bias)
+        return HF.pw_mlp(d, x, self.pwconv1.weight, self.pwconv1.bias, self.pwconv2.weight,
+                         self.pwconv2.bias, self.shortcut.weight, norm=True)
 
 
 def _skip(cin, cout, k):

@@ -67,6 +67,8 @@ int dsgan_conv_wgrad(const float* dy, long dy_bs, const float* x, long x_bs, flo
  * mode 2 WGRAD: DW[M][N] += sum_{b,p} DY[b][M][p] * xact(X[b][N][p])   (K = P, nb images)
  *              split over pixels into partials in `ws` (dsgan_pw_wgrad_workspace(M, N, P, nb)
  *              floats; NULL allowed when that is 0), summed in a fixed order: deterministic.
+ *              `bias` (nullable) is an OUTPUT here: bias[m] += sum_{b,p} DY[b][m][p] (the layer's
+ *              bias grad, from the same staged tiles -- no separate channel-sum pass).
  * dsgan_pw_supported() reports whether a shape/alignment takes this path (else use igemm). */
 int dsgan_pw_supported(int mode, int M, int K, int P, long a_bs, long b_bs, const void* a,
                        const void* b);
@@ -87,19 +89,21 @@ int dsgan_pw_gemm_f32(int mode, const float* A, long a_bs, const float* B, long 
                       int gact, int accumulate, float slope, float* ws, hipStream_t stream);
 
 /* Weight-grad with bf16 operand(s) (pwgemm.hip): DW[M][N] += sum_{b,p} A[b][M][p] * B[b][N][p];
- * a_bf16 / b_bf16 select bf16 storage (the fused MLP backward's gelu(z) and dz).  P % 32 == 0.
+ * a_bf16 / b_bf16 select bf16 storage (h, gelu(z), dz of the MLP blocks).  P % 32 == 0.
+ * db (nullable): db[m] += sum_{b,p} A[b][m][p], the bias grad (of the bf16 values when A is bf16).
  * ws: dsgan_pw_wgrad_workspace(M, N, P, nb) floats (deterministic split reduction). */
 int dsgan_pw_wgrad_mixed(const void* A, long a_bs, int a_bf16, const void* B, long b_bs, int b_bf16,
-                         float* dw, int M, int N, int P, int nb, float* ws, hipStream_t stream);
+                         float* dw, float* db, int M, int N, int P, int nb, float* ws, hipStream_t stream);
 /* forward with bf16 activations in and/or out (unfused ConvNeXt MLP blocks c4/c5/uc1/uc2,
  * MixConvNeXtML.py:221-240): Y (+)= act(W X + bias), X/Y fp32 or bf16; ypre (nullable) = fp32
  * pre-activation, or with ypre_grad_bf16 the bf16 act'(pre) the backward multiplies by */
 int dsgan_pw_fwd_io(const float* W, const void* X, long x_bs, int x_bf16, void* Y, long y_bs, int y_bf16,
                     const void* ypre, long ypre_bs, int ypre_grad_bf16, const float* bias, int M, int K,
                     int P, int nb, int act, int accumulate, float slope, hipStream_t stream);
-/* DX (+)= (W^T DY) * GP with GP the bf16 act'(pre) of dsgan_pw_fwd_io (pwconv2 data-grad) */
-int dsgan_pw_dgrad_gbf(const float* W, const float* DY, long dy_bs, float* DX, long dx_bs, const void* GP,
-                       long gp_bs, int M, int K, int P, int nb, int accumulate, hipStream_t stream);
+/* DX (+)= (W^T DY) (* GP): DY fp32 or bf16, DX fp32 or bf16, GP (nullable) the bf16 act'(pre) of
+ * dsgan_pw_fwd_io.  Unfused-block pwconv2 / pwconv1 data-grads. */
+int dsgan_pw_dgrad_io(const float* W, const void* DY, long dy_bs, int dy_bf16, void* DX, long dx_bs, int dx_bf16,
+                      const void* GP, long gp_bs, int M, int K, int P, int nb, int accumulate, hipStream_t stream);
 
 /* ---- fused ConvNeXt MLP (mlp.hip), replaces Block.pwconv1 -> GELU -> pwconv2 -------------------
  * DSGAN/models/model/MixConvNeXtML.py:221-223,236-240 (nn.Linear(C,4C) + GELU + nn.Linear(4C,P) on
@@ -109,14 +113,24 @@ int dsgan_pw_dgrad_gbf(const float* W, const float* DY, long dy_bs, float* DX, l
  * dsgan_mlp_fwd: out[b][p][n] (+)= b2[p] + sum_m w2[p][m] gelu(b1[m] + sum_c w1[m][c] h[b][c][n]);
  *   w1 [4C][C], w2 [P][4C] bf16 copies of the Linear weights.
  * dsgan_mlp_bwd: recomputes z, writes dh (fp32), gelu(z) and dz (bf16 [nb][4C][HW]), and per-tile
- *   row sums of dz (bsum) for the pwconv1 bias grad (reduce with dsgan_colsum). */
+ *   row sums of dz (bsum) for the pwconv1 bias grad (reduce with dsgan_colsum).
+ * h is fp32, or bf16 when h_bf16 (dsgan_instnorm_fwd_bf16's output: the kernels round h to bf16
+ *   on load either way, so the two forms give identical results). */
 int dsgan_mlp_supported(int C, int P, int HW);
-int dsgan_mlp_fwd(const float* h, long h_bs, const void* w1, const float* b1, const void* w2,
+int dsgan_mlp_fwd(const void* h, long h_bs, int h_bf16, const void* w1, const float* b1, const void* w2,
                   const float* b2, float* out, long out_bs, int nb, int C, int P, int HW,
                   int accumulate, hipStream_t stream);
-int dsgan_mlp_bwd(const float* h, long h_bs, const float* dy, long dy_bs, const void* w1,
+int dsgan_mlp_bwd(const void* h, long h_bs, int h_bf16, const float* dy, long dy_bs, const void* w1,
                   const float* b1, const void* w2, float* dh, long dh_bs, void* g_out, void* dz_out,
                   float* bsum, int nb, int C, int P, int HW, hipStream_t stream);
+/* dsgan_mlp_bwd with g_out = dz_out = bsum = NULL writes dh only; the weight-grads then come from
+ * dsgan_mlp_wgrad: dw1 [4C][C] += dz h^T, dw2 [P][4C] += dy gelu(z)^T, db1 [4C] += sum dz, with z and
+ * dz recomputed per (hidden chunk, pixel split) workgroup so neither reaches HBM.  ws:
+ * dsgan_mlp_wgrad_workspace() floats of per-split partials, summed in a fixed order. */
+long dsgan_mlp_wgrad_workspace(int C, int P, int HW, int nb);
+int dsgan_mlp_wgrad(const void* h, long h_bs, int h_bf16, const float* dy, long dy_bs, const void* w1,
+                    const float* b1, const void* w2, float* dw1, float* db1, float* dw2, float* ws, int nb, int C,
+                    int P, int HW, hipStream_t stream);
 /* out[c] += sum_r part[r][c], rows added in a fixed order (deterministic); part is scratch and
  * is overwritten (in-place pre-reduction of many rows). */
 int dsgan_colsum(float* part, int rows, int cols, float* out, hipStream_t stream);
@@ -238,6 +252,10 @@ int dsgan_instnorm_bwd(const float* dy, long dy_bs, const float* x, long x_bs, c
                        const float* res, long res_bs, const float* mean, const float* rstd,
                        float* dx, long dx_bs, float* dres, long dres_bs, float* dscale, int N,
                        int C, int HW, int act, float slope, float eps, hipStream_t stream);
+/* y (bf16, round-to-nearest-even) = IN(x): Block.norm (MixConvNeXtML.py:221) whose only consumers
+ * are the block's bf16-operand MLP GEMMs.  HW % 4 == 0, 16-byte aligned. */
+int dsgan_instnorm_fwd_bf16(const float* x, long x_bs, void* y, long y_bs, float* mean, float* rstd, int N,
+                            int C, int HW, float eps, hipStream_t stream);
 
 /* ---- MaxPool2d(k) with int32 plane-flat argmax (bit-exact with torch's indices):
  * downSample :68-74, downSkip* :333-417, OriginMLKA :123-136, VGG pools vgg.py. */

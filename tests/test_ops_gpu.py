@@ -154,6 +154,119 @@ def test_pw_mlp(prec, N, C, H, P):
         assert rel(pd.grad, pr.grad) < 2 * tol
 
 
+@pytest.mark.parametrize("prec", ["fp32", "bf16"])
+@pytest.mark.parametrize("N,C,H,P", [(2, 64, 16, 128),     # fused MLP kernels (mlp.hip)
+                                     (2, 256, 16, 512),    # unfused bf16 g / gp / dz path
+                                     (2, 3, 16, 64)])      # fp32-z path (tiny block)
+def test_block_tail_norm(prec, N, C, H, P):
+    """pw_mlp(norm=True): the block's InstanceNorm folded into the MLP node (bf16 h in bf16 mode)
+    vs a torch fp32 reference of IN -> Linear -> GELU -> Linear (+ shortcut), and BITWISE equal to
+    the unfolded pair instance_norm(d) -> pw_mlp(h): storing h in bf16 changes no bit because its
+    only readers round it to bf16 on load."""
+    from dsgan_hip import functional as HF
+    HF.set_precision(prec)
+    g = torch.Generator().manual_seed(3 * C + P)
+    d = torch.randn(N, C, H, H, generator=g) * 2 + 0.5
+    x = _q(torch.randn(N, C, H, H, generator=g), prec)
+    w1 = _q(torch.randn(4 * C, C, generator=g) / math.sqrt(C), prec)
+    b1 = torch.randn(4 * C, generator=g) * 0.1
+    w2 = _q(torch.randn(P, 4 * C, generator=g) / math.sqrt(4 * C), prec)
+    b2 = torch.randn(P, generator=g) * 0.1
+    ws = _q(torch.randn(P, C, 1, 1, generator=g) / math.sqrt(C), prec)
+    R = [t.clone().requires_grad_() for t in (d, x, w1, b1, w2, b2, ws)]
+    hr = F.instance_norm(R[0], eps=1e-5)
+    t = F.linear(hr.permute(0, 2, 3, 1), R[2], R[3])
+    t = F.linear(F.gelu(t), R[4], R[5]).permute(0, 3, 1, 2)
+    y_ref = F.conv2d(R[1], R[6]) + t
+    gy = torch.randn(y_ref.shape, generator=g)
+    y_ref.backward(gy)
+    runs = []
+    for folded in (True, False):
+        dd, xd = _leaf(d), _leaf(x)
+        P_ = [_param(t) for t in (w1, b1, w2, b2, ws)]
+        if folded:
+            y = HF.pw_mlp(dd, xd, *P_, norm=True)
+        else:
+            y = HF.pw_mlp(HF.instance_norm(dd), xd, *P_)
+        y.backward(gy.to(DEV))
+        runs.append([y.detach(), dd.grad, xd.grad] + [p.grad for p in P_])
+    tol = TOL[prec]
+    names = ("y", "d", "x", "w1", "b1", "w2", "b2", "ws")
+    for name, a, r in zip(names, runs[0], [y_ref, R[0].grad, R[1].grad] + [t.grad for t in R[2:]]):
+        assert rel(a, r) < (tol if name == "y" else 2 * tol), (name, rel(a, r))
+    for name, a, b in zip(names, runs[0], runs[1]):
+        assert torch.equal(a, b), (name, rel(a, b))
+
+
+@pytest.mark.parametrize("N,C,HW", [(2, 64, 256), (3, 128, 4096), (2, 256, 1024), (1, 32, 65536 + 1024)])
+def test_instnorm_bf16_output(N, C, HW):
+    """dsgan_instnorm_fwd_bf16 writes exactly the RNE bf16 rounding of the fp32 InstanceNorm output
+    (same statistics, every plane-size kernel variant)."""
+    from dsgan_hip import functional as HF
+    from dsgan_hip._lib import call, ptr, stream
+    g = torch.Generator().manual_seed(C + HW)
+    d = (torch.randn(N, C, 1, HW, generator=g) * 3 - 1).to(DEV)
+    y32, m32, r32 = HF.instnorm_raw(d)
+    yb = torch.empty((N, C, 1, HW), device=DEV, dtype=torch.bfloat16)
+    m, r = torch.empty(N * C, device=DEV), torch.empty(N * C, device=DEV)
+    call("dsgan_instnorm_fwd_bf16", ptr(d), C * HW, ptr(yb), C * HW, ptr(m), ptr(r), N, C, HW, 1e-5, stream())
+    torch.cuda.synchronize()
+    assert torch.equal(yb, y32.to(torch.bfloat16))
+    assert torch.equal(m, m32) and torch.equal(r, r32)
+
+
+@pytest.mark.parametrize("dy_bf16,dx_bf16,gp", [(0, 1, True), (1, 0, False), (1, 1, True), (0, 0, False)])
+@pytest.mark.parametrize("N,M,K,P", [(2, 512, 128, 256), (1, 2048, 256, 128), (2, 96, 64, 384), (1, 1024, 1024, 256)])
+def test_pw_dgrad_io(dy_bf16, dx_bf16, gp, N, M, K, P):
+    """dsgan_pw_dgrad_io: DX = (W^T DY) (* GP) with bf16 DY/DX options vs float64 torch on the
+    bf16-rounded operands (the last shape takes the 256-row M tiles)."""
+    from dsgan_hip._lib import call, ptr, stream
+    g = torch.Generator().manual_seed(M + K + P)
+    w = torch.randn(K, M, generator=g) / math.sqrt(K)
+    dy = torch.randn(N, K, P, generator=g)
+    gpv = torch.rand(N, M, P, generator=g).to(torch.bfloat16)
+    ref = torch.einsum("km,nkp->nmp", _q(w, "bf16").double(), _q(dy, "bf16").double())
+    if gp:
+        ref = ref * gpv.double()
+    dyd = dy.to(DEV).to(torch.bfloat16) if dy_bf16 else dy.to(DEV)
+    dx = torch.empty((N, M, P), device=DEV, dtype=torch.bfloat16 if dx_bf16 else torch.float32)
+    call("dsgan_pw_dgrad_io", ptr(w.to(DEV)), ptr(dyd), K * P, dy_bf16, ptr(dx), M * P, dx_bf16,
+         ptr(gpv.to(DEV)) if gp else None, M * P, M, K, P, N, 0, stream())
+    torch.cuda.synchronize()
+    got = dx.double().cpu()
+    if dx_bf16:
+        assert ((got - ref).abs() <= ref.abs() * 2 ** -8 + 1e-6).all()
+    else:
+        assert rel(got, ref) < 1e-5
+
+
+@pytest.mark.parametrize("a_bf16,b_bf16", [(0, 0), (1, 1), (1, 0), (0, 1)])
+@pytest.mark.parametrize("N,M,C,P", [(2, 512, 128, 4096), (16, 64, 512, 1024), (1, 96, 40, 256), (2, 2048, 512, 256)])
+def test_pw_wgrad_bias_sums(a_bf16, b_bf16, N, M, C, P):
+    """dsgan_pw_wgrad_mixed with db: dW += A B^T and db += row sums of A from the staged tiles, split or
+    unsplit, fp32 or bf16 A; deterministic (two runs bitwise equal)."""
+    from dsgan_hip import functional as HF
+    from dsgan_hip._lib import call, ptr, stream
+    g = torch.Generator().manual_seed(M + C + P)
+    a = torch.randn(N, M, P, generator=g)
+    b = torch.randn(N, C, P, generator=g)
+    aq, bq = (_q(a, "bf16") if a_bf16 else a), (_q(b, "bf16") if b_bf16 else b)
+    ref_w = torch.einsum("nmp,ncp->mc", _q(a, "bf16").double(), _q(b, "bf16").double())
+    ref_b = aq.double().sum(dim=(0, 2))
+    outs = []
+    for _ in range(2):
+        w0, b0 = torch.ones(M, C, device=DEV), torch.full((M,), 2.0, device=DEV)
+        ad = a.to(DEV).to(torch.bfloat16) if a_bf16 else a.to(DEV)
+        bd = b.to(DEV).to(torch.bfloat16) if b_bf16 else b.to(DEV)
+        call("dsgan_pw_wgrad_mixed", ptr(ad), M * P, a_bf16, ptr(bd), C * P, b_bf16, ptr(w0), ptr(b0), M, C, P, N,
+             ptr(HF._pw_ws(M, C, P, N, ad)), stream())
+        torch.cuda.synchronize()
+        outs.append((w0.cpu(), b0.cpu()))
+    assert rel(outs[0][0] - 1.0, ref_w) < 1e-5
+    assert rel(outs[0][1] - 2.0, ref_b) < 1e-5
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+
+
 @pytest.mark.parametrize("N,Cin,H,W,Cout,K,s,p,act", [
     (2, 64, 18, 18, 128, 3, 1, 1, "relu"),       # VGG block (ragged 18x18 vs 8x16 tiles)
     (1, 128, 32, 40, 64, 3, 1, 1, None),

@@ -42,6 +42,12 @@ def main():
     rows.sort(key=lambda t: -t[0])
     tot = sum(t[0] for t in rows)
     print("%d launches, %.3f ms" % (len(rows), tot))
+    fam = {}
+    for ms, f, _, fl, by in rows:
+        e = fam.setdefault(f, [0, 0.0, 0.0, 0.0])
+        e[0] += 1; e[1] += ms; e[2] += fl; e[3] += by
+    for f, (n, ms, fl, by) in sorted(fam.items(), key=lambda kv: -kv[1][1]):
+        print("  %-20s %4d launches %8.3f ms %7.1f TF/s %7.1f GB/s" % (f, n, ms, fl / ms / 1e9, by / ms / 1e6))
     for ms, fam, tag, fl, by in rows:
         print("%8.1f us  %-18s %-42s %7.1f TF/s %7.1f GB/s %8.1f MB" % (ms * 1e3, fam, str(tag), fl / ms / 1e9,
                                                                         by / ms / 1e6, by / 1e6))

@@ -39,8 +39,8 @@ for name, C, P, H in SHAPES:
     dh = torch.empty_like(h)
     gw2 = torch.zeros(P, C4, device="cuda")
     gw1 = torch.zeros(C4, C, device="cuda")
-    f = lambda: call("dsgan_mlp_fwd", ptr(h), C * HW, ptr(w1), ptr(b1), ptr(w2), ptr(b2), ptr(out), P * HW, N, C, P, HW, 1, stream())
-    b = lambda: call("dsgan_mlp_bwd", ptr(h), C * HW, ptr(dy), P * HW, ptr(w1), ptr(b1), ptr(w2), ptr(dh), C * HW,
+    f = lambda: call("dsgan_mlp_fwd", ptr(h), C * HW, 0, ptr(w1), ptr(b1), ptr(w2), ptr(b2), ptr(out), P * HW, N, C, P, HW, 1, stream())
+    b = lambda: call("dsgan_mlp_bwd", ptr(h), C * HW, 0, ptr(dy), P * HW, ptr(w1), ptr(b1), ptr(w2), ptr(dh), C * HW,
                      ptr(g), ptr(dz), ptr(bsum), N, C, P, HW, stream())
     w2g = lambda: call("dsgan_pw_wgrad_mixed", ptr(dy), P * HW, 0, ptr(g), C4 * HW, 1, ptr(gw2), P, C4, HW, N, ptr(HF._pw_ws(P, C4, HW, N, dy)), stream())
     w1g = lambda: call("dsgan_pw_wgrad_mixed", ptr(dz), C4 * HW, 1, ptr(h), C * HW, 0, ptr(gw1), C4, C, HW, N, ptr(HF._pw_ws(C4, C, HW, N, dz)), stream())
