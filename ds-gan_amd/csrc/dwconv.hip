@@ -203,10 +203,19 @@ __device__ __forceinline__ void dw_stage(float* tile, const float* __restrict__ 
   }
 }
 
+// One window row as three ds_read_b128.  The empty asm pins every component: without it the
+// compiler drops the window elements a K < 9 kernel never touches and splits the rest into
+// ds_read2_b32 pairs, whose 32-bank lane groups see the 16-B lane stride as a 4-way conflict
+// (SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE = 0.70 measured); b128 lane groups are conflict-free here.
+typedef __attribute__((ext_vector_type(4))) float dwf4;
+template <int K>   // (K = 9 uses the whole window: already b128, and the pin would spill it)
 __device__ __forceinline__ void dw_row(float (&v)[12], const float* row) {
-  *reinterpret_cast<float4*>(v) = *reinterpret_cast<const float4*>(row);
-  *reinterpret_cast<float4*>(v + 4) = *reinterpret_cast<const float4*>(row + 4);
-  *reinterpret_cast<float4*>(v + 8) = *reinterpret_cast<const float4*>(row + 8);
+  dwf4 a = *reinterpret_cast<const dwf4*>(row);
+  dwf4 b = *reinterpret_cast<const dwf4*>(row + 4);
+  dwf4 c = *reinterpret_cast<const dwf4*>(row + 8);
+  if constexpr (K < 9) asm volatile("" ::"v"(a), "v"(b), "v"(c));
+#pragma unroll
+  for (int i = 0; i < 4; ++i) { v[i] = a[i]; v[4 + i] = b[i]; v[8 + i] = c[i]; }
 }
 
 template <int K, int TWT, int THT, int R>
@@ -235,10 +244,10 @@ __global__ __launch_bounds__(256, 4) void dwconv_fwd_v2(const float* __restrict_
   // one input row in flight ahead of the FMAs; the scheduling barrier keeps the compiler from
   // hoisting every row load of the unrolled loop (which costs occupancy or spills)
   float cur[12], nxt[12];
-  dw_row(cur, &tile[R * ty][4 * tx]);
+  dw_row<K>(cur, &tile[R * ty][4 * tx]);
 #pragma unroll
   for (int r = 0; r < R + K - 1; ++r) {
-    if (r + 1 < R + K - 1) dw_row(nxt, &tile[R * ty + r + 1][4 * tx]);
+    if (r + 1 < R + K - 1) dw_row<K>(nxt, &tile[R * ty + r + 1][4 * tx]);
 #pragma unroll
     for (int s = 0; s < R; ++s) {
       const int kh = r - s;
@@ -301,10 +310,10 @@ __global__ __launch_bounds__(256, 4) void dwconv_wgrad_v2(const float* __restric
     }
     __syncthreads();
     float cur[12], nxt[12];
-    dw_row(cur, &tile[R * ty][4 * tx]);
+    dw_row<K>(cur, &tile[R * ty][4 * tx]);
 #pragma unroll
     for (int r = 0; r < R + K - 1; ++r) {
-      if (r + 1 < R + K - 1) dw_row(nxt, &tile[R * ty + r + 1][4 * tx]);
+      if (r + 1 < R + K - 1) dw_row<K>(nxt, &tile[R * ty + r + 1][4 * tx]);
 #pragma unroll
       for (int s = 0; s < R; ++s) {
         const int kh = r - s;
@@ -391,7 +400,7 @@ static long dw_wgrad_v2(const float* dy, long dy_bs, const float* x, long x_bs, 
 template <int K>
 static void dw_fwd_dispatch(int cfg, const float* x, long x_bs, const float* w, const float* bias, float* y,
                             long y_bs, int N, int C, int H, int W, int flip, int accumulate, hipStream_t st) {
-  constexpr int R1 = K >= 7 ? 4 : 8, R2 = K >= 9 ? 2 : 4;
+  constexpr int R1 = K >= 9 ? 2 : K >= 7 ? 4 : 8, R2 = K >= 9 ? 2 : 4;
   if (cfg == 1) dw_fwd_v2<K, 32, 8, R1>(x, x_bs, w, bias, y, y_bs, N, C, H, W, flip, accumulate, st);
   else if (cfg == 2) dw_fwd_v2<K, 16, 16, R2>(x, x_bs, w, bias, y, y_bs, N, C, H, W, flip, accumulate, st);
   else dw_fwd_v2<K, 8, 32, 1>(x, x_bs, w, bias, y, y_bs, N, C, H, W, flip, accumulate, st);
@@ -401,7 +410,7 @@ static void dw_fwd_dispatch(int cfg, const float* x, long x_bs, const float* w, 
 template <int K>
 static long dw_wgrad_dispatch(int cfg, const float* dy, long dy_bs, const float* x, long x_bs, float* ws,
                               int N, int C, int H, int W, hipStream_t st) {
-  constexpr int R1 = K >= 9 ? 4 : 8, R2 = K >= 9 ? 2 : 4;
+  constexpr int R1 = K >= 9 ? 2 : 8, R2 = K >= 9 ? 2 : 4;
   if (cfg == 1) return dw_wgrad_v2<K, 32, 8, R1>(dy, dy_bs, x, x_bs, ws, N, C, H, W, st);
   if (cfg == 2) return dw_wgrad_v2<K, 16, 16, R2>(dy, dy_bs, x, x_bs, ws, N, C, H, W, st);
   return dw_wgrad_v2<K, 8, 32, 1>(dy, dy_bs, x, x_bs, ws, N, C, H, W, st);

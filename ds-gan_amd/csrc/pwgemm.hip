@@ -80,7 +80,6 @@ __device__ __forceinline__ pbf16x4 cvt4(float4 v, int bact, float slope) {
 // is copied to LDS unconverted.
 template <int MODE, int BM, int ABF = 0, int BBF = 0>
 __global__ __launch_bounds__(256, 2) void pwgemm_kernel(PwArgs g) {
-  static_assert(MODE == PW_WGRAD || ABF == 0, "bf16 operand modes");
   constexpr int BN = 128;
   constexpr int WM = 2, WN = 2;
   constexpr int TM = BM / WM / 32, TN = BN / WN / 32;
@@ -125,7 +124,7 @@ __global__ __launch_bounds__(256, 2) void pwgemm_kernel(PwArgs g) {
   // ---- staging maps ----
   // row-major tiles: item = (row, c4) with c4 in [0,8): 8 float4 per 32-k row
   // k-major tiles  : item = (k, c4) with c4 in [0, C/4)
-  constexpr int A_ITEMS = ABF ? BM * 4 / 256 : (A_KMAJ ? PBK * BM / 4 : BM * 8) / 256;
+  constexpr int A_ITEMS = ABF ? (A_KMAJ ? PBK * BM / 8 : BM * 4) / 256 : (A_KMAJ ? PBK * BM / 4 : BM * 8) / 256;
   constexpr int B_ITEMS = BBF ? BN * 4 / 256 : (B_KMAJ ? PBK * BN / 4 : BN * 8) / 256;
   float4 ra[ABF ? 1 : A_ITEMS], rb[BBF ? 1 : B_ITEMS];
   pu32x4 rha[ABF ? A_ITEMS : 1], rhb[BBF ? B_ITEMS : 1];
@@ -154,12 +153,21 @@ __global__ __launch_bounds__(256, 2) void pwgemm_kernel(PwArgs g) {
     // WGRAD: a 32-pixel K step lies inside one image (P % 32 == 0): image index is uniform
     const unsigned bw = (MODE == PW_WGRAD) ? (unsigned)(kb / g.P) : 0u;
     const unsigned pw = (MODE == PW_WGRAD) ? (unsigned)(kb - (int)bw * g.P) : 0u;
-    if constexpr (ABF) {                         // DY[b][M][P] bf16, row m, 8 pixels per item
+    if constexpr (ABF) {   // bf16 A, 8 elements per item
 #pragma unroll
       for (int i = 0; i < A_ITEMS; ++i) {
         const int it = tid + i * 256;
-        const int m = m0 + (it >> 2);
-        const unsigned off = (m < g.M) ? (bw * (unsigned)g.a_bs + (unsigned)m * g.P + pw + (it & 3) * 8) * 2u : PW_OOB;
+        unsigned off;
+        if (MODE == PW_FWD) {                    // W[M][K] bf16, row m, k = kb + c8*8
+          const int m = m0 + (it >> 2), k = kb + (it & 3) * 8;
+          off = ((m < g.M) & (k < kend)) ? ((unsigned)m * g.K + k) * 2u : PW_OOB;
+        } else if (MODE == PW_DGRAD) {           // W[K][M] bf16, row k (k >= K is past the range)
+          const int k = kb + it / (BM / 8), m = m0 + (it % (BM / 8)) * 8;
+          off = (m < g.M) ? ((unsigned)k * g.M + m) * 2u : PW_OOB;
+        } else {                                 // DY[b][M][P] bf16, row m, 8 pixels per item
+          const int m = m0 + (it >> 2);
+          off = (m < g.M) ? (bw * (unsigned)g.a_bs + (unsigned)m * g.P + pw + (it & 3) * 8) * 2u : PW_OOB;
+        }
         rha[i] = bldh(rA, off);
       }
     } else
@@ -216,7 +224,8 @@ __global__ __launch_bounds__(256, 2) void pwgemm_kernel(PwArgs g) {
 #pragma unroll
       for (int i = 0; i < A_ITEMS; ++i) {
         const int it = tid + i * 256;
-        *reinterpret_cast<pu32x4*>(As + (it >> 2) * A_STR + (it & 3) * 8) = rha[i];
+        const int off = A_KMAJ ? (it / (BM / 8)) * A_STR + (it % (BM / 8)) * 8 : (it >> 2) * A_STR + (it & 3) * 8;
+        *reinterpret_cast<pu32x4*>(As + off) = rha[i];
         if (MODE == PW_WGRAD && g.asum) {
           const pbf16x8 hv = __builtin_bit_cast(pbf16x8, rha[i]);
           asr[i] += (((float)hv[0] + (float)hv[1]) + ((float)hv[2] + (float)hv[3])) +
@@ -465,6 +474,21 @@ static void pw_launch(const PwArgs& g, int splits, hipStream_t st) {
   hipLaunchKernelGGL((pwgemm_kernel<MODE, BM, ABF, BBF>), dim3((unsigned)((long)mt * nt * splits)), dim3(256), 0, st, g);
 }
 
+// FWD / DGRAD launch over (tile rows, bf16 weight, bf16 activation)
+template <int MODE>
+static void pw_launch_ab(const PwArgs& g, int bm, int abf, int bbf, hipStream_t st) {
+  const int sel = (abf ? 2 : 0) + (bbf ? 1 : 0);
+#define PW_AB(BM)                                                      \
+  switch (sel) {                                                       \
+    case 0: pw_launch<MODE, BM, 0, 0>(g, 1, st); break;                \
+    case 1: pw_launch<MODE, BM, 0, 1>(g, 1, st); break;                \
+    case 2: pw_launch<MODE, BM, 1, 0>(g, 1, st); break;                \
+    default: pw_launch<MODE, BM, 1, 1>(g, 1, st); break;               \
+  }
+  if (bm == 256) { PW_AB(256) } else if (bm == 128) { PW_AB(128) } else { PW_AB(64) }
+#undef PW_AB
+}
+
 // dw[e] += sum_s ws[s][e], s in a fixed order: thread (e, j) of a workgroup of EL elements x J
 // s-lanes sums s = j, j+J, j+2J, ... in order, then the J partial sums of an element are added
 // j = 0..J-1 -- the same tree on every run.  J grows with the split count so that a reduction of
@@ -651,9 +675,9 @@ extern "C" int dsgan_pw_gemm(int mode, const float* A, long a_bs, const float* B
 // act(W X + bias), X fp32 or bf16 (x_bf16), Y fp32 or bf16 (y_bf16; accumulate needs fp32 Y);
 // ypre (nullable): fp32 pre-activation, or (ypre_grad_bf16) bf16 act'(pre) for the backward.
 // P % 128 == 0, K % 8 == 0, 16-byte aligned.
-extern "C" int dsgan_pw_fwd_io(const float* W, const void* X, long x_bs, int x_bf16, void* Y, long y_bs, int y_bf16,
-                               const void* ypre, long ypre_bs, int ypre_grad_bf16, const float* bias, int M, int K,
-                               int P, int nb, int act, int accumulate, float slope, hipStream_t st) {
+extern "C" int dsgan_pw_fwd_io(const void* W, int w_bf16, const void* X, long x_bs, int x_bf16, void* Y, long y_bs,
+                               int y_bf16, const void* ypre, long ypre_bs, int ypre_grad_bf16, const float* bias, int M,
+                               int K, int P, int nb, int act, int accumulate, float slope, hipStream_t st) {
   DSG_REQUIRE(W && X && Y && M >= 16 && K > 0 && P > 0 && nb > 0, "dsgan_pw_fwd_io: bad args");
   DSG_REQUIRE(P % 128 == 0 && K % 8 == 0 && al16(W) && al16(X) && al16(Y) && (x_bs & 7) == 0 && (y_bs & 7) == 0 &&
                   !(y_bf16 && accumulate),
@@ -661,23 +685,14 @@ extern "C" int dsgan_pw_fwd_io(const float* W, const void* X, long x_bs, int x_b
   DSG_REQUIRE((long)M * P * 4 < (1L << 32) && (long)K * P * 4 < (long)PW_OOB && (long)M * K * 4 < (long)PW_OOB,
               "dsgan_pw_fwd_io: operand exceeds the 4 GiB buffer range");
   PwArgs g{};
-  g.A = W; g.a_bs = 0; g.B = (const float*)X; g.b_bs = x_bs; g.Y = (float*)Y; g.y_bs = y_bs; g.bias = bias;
+  g.A = (const float*)W; g.a_bs = 0; g.B = (const float*)X; g.b_bs = x_bs; g.Y = (float*)Y; g.y_bs = y_bs; g.bias = bias;
   g.ypre = (float*)ypre; g.ypre_bs = ypre_bs; g.gbf = ypre_grad_bf16; g.act = act; g.accumulate = accumulate;
   g.slope = slope; g.y_bf16 = y_bf16;
   g.P = P; g.M = M; g.N = nb * P; g.K = K;
-  g.a_range = (unsigned)((long)M * K * 4);
+  g.a_range = (unsigned)((long)M * K * (w_bf16 ? 2 : 4));
   g.b_range = (unsigned)((long)K * P * (x_bf16 ? 2 : 4));
-  const bool big = M > 64;
-  const bool b256 = use_bm256(g);
-  if (x_bf16) {
-    if (b256) pw_launch<PW_FWD, 256, 0, 1>(g, 1, st);
-    else if (big) pw_launch<PW_FWD, 128, 0, 1>(g, 1, st);
-    else pw_launch<PW_FWD, 64, 0, 1>(g, 1, st);
-  } else {
-    if (b256) pw_launch<PW_FWD, 256>(g, 1, st);
-    else if (big) pw_launch<PW_FWD, 128>(g, 1, st);
-    else pw_launch<PW_FWD, 64>(g, 1, st);
-  }
+  const int bm = use_bm256(g) ? 256 : M > 64 ? 128 : 64;
+  pw_launch_ab<PW_FWD>(g, bm, w_bf16, x_bf16, st);
   DSG_CHECK_LAUNCH();
   return 0;
 }
@@ -686,7 +701,7 @@ extern "C" int dsgan_pw_fwd_io(const float* W, const void* X, long x_bs, int x_b
 //   DX[b][M][p] (+)= (sum_k W[k][M] DY[b][k][p]) (* GP[b][M][p])
 // DY fp32 or bf16 (dy_bf16), DX fp32 or bf16 (dx_bf16; accumulate needs fp32), GP (nullable) the bf16
 // act'(pre) written by dsgan_pw_fwd_io (ypre_grad_bf16).  P % 128 == 0, 16-byte aligned.
-extern "C" int dsgan_pw_dgrad_io(const float* W, const void* DY, long dy_bs, int dy_bf16, void* DX, long dx_bs,
+extern "C" int dsgan_pw_dgrad_io(const void* W, int w_bf16, const void* DY, long dy_bs, int dy_bf16, void* DX, long dx_bs,
                                  int dx_bf16, const void* GP, long gp_bs, int M, int K, int P, int nb,
                                  int accumulate, hipStream_t st) {
   DSG_REQUIRE(W && DY && DX && M > 0 && K > 0 && nb > 0, "dsgan_pw_dgrad_io: bad args");
@@ -694,22 +709,15 @@ extern "C" int dsgan_pw_dgrad_io(const float* W, const void* DY, long dy_bs, int
                   (dx_bs & 7) == 0 && (!GP || (al16(GP) && (gp_bs & 7) == 0)) && !(dx_bf16 && accumulate),
               "dsgan_pw_dgrad_io: unsupported shape/alignment");
   DSG_REQUIRE((long)M * P * 4 < (1L << 32) && (long)K * P * 4 < (long)PW_OOB, "dsgan_pw_dgrad_io: operand too large");
+  DSG_REQUIRE(!w_bf16 || (M % 8) == 0, "dsgan_pw_dgrad_io: bf16 W needs M %% 8 == 0");
   PwArgs g{};
-  g.A = W; g.B = (const float*)DY; g.b_bs = dy_bs; g.Y = (float*)DX; g.y_bs = dx_bs; g.y_bf16 = dx_bf16;
+  g.A = (const float*)W; g.B = (const float*)DY; g.b_bs = dy_bs; g.Y = (float*)DX; g.y_bs = dx_bs; g.y_bf16 = dx_bf16;
   g.gpre = (const float*)GP; g.gpre_bs = gp_bs; g.gbf = GP ? 1 : 0;
   g.accumulate = accumulate; g.P = P; g.M = M; g.N = nb * P; g.K = K;
-  g.a_range = (unsigned)((long)M * K * 4);
+  g.a_range = (unsigned)((long)M * K * (w_bf16 ? 2 : 4));
   g.b_range = (unsigned)((long)K * P * (dy_bf16 ? 2 : 4));
-  const bool b256 = use_bm256(g);
-  if (dy_bf16) {
-    if (b256) pw_launch<PW_DGRAD, 256, 0, 1>(g, 1, st);
-    else if (M > 64) pw_launch<PW_DGRAD, 128, 0, 1>(g, 1, st);
-    else pw_launch<PW_DGRAD, 64, 0, 1>(g, 1, st);
-  } else {
-    if (b256) pw_launch<PW_DGRAD, 256>(g, 1, st);
-    else if (M > 64) pw_launch<PW_DGRAD, 128>(g, 1, st);
-    else pw_launch<PW_DGRAD, 64>(g, 1, st);
-  }
+  const int bm = use_bm256(g) ? 256 : M > 64 ? 128 : 64;
+  pw_launch_ab<PW_DGRAD>(g, bm, w_bf16, dy_bf16, st);
   DSG_CHECK_LAUNCH();
   return 0;
 }

@@ -764,13 +764,13 @@ class PwMlpFn(torch.autograd.Function):
             gp = torch.empty((N, C4, H, W), device=h.device, dtype=torch.bfloat16)   # gelu'(z), for dz
             g = torch.empty((N, C4, H, W), device=h.device, dtype=torch.bfloat16)    # gelu(z)
             e0 = IGEMM_TIMER.begin()
-            call("dsgan_pw_fwd_io", ptr(w1), ptr(h), hbs, hb, ptr(g), C4 * HW, 1, ptr(gp), C4 * HW, 1, ptr(b1), C4, C,
+            call("dsgan_pw_fwd_io", ptr(bf16_weight(w1)), 1, ptr(h), hbs, hb, ptr(g), C4 * HW, 1, ptr(gp), C4 * HW, 1, ptr(b1), C4, C,
                  HW, N, ACT["gelu"], 0, LRELU_SLOPE, stream())
             IGEMM_TIMER.end(e0, 2.0 * N * HW * C4 * C, ("fwd", N, C, H, W, C4, 1, 1), "pwgemm_kernel",
                             _nb(h, w1, b1, g, gp))
             out = conv_fwd_raw(x, ws, None, 1, 0)
             e0 = IGEMM_TIMER.begin()
-            call("dsgan_pw_fwd_io", ptr(w2), ptr(g), C4 * HW, 1, ptr(out), P * HW, 0, None, 0, 0, ptr(b2), P, C4,
+            call("dsgan_pw_fwd_io", ptr(bf16_weight(w2)), 1, ptr(g), C4 * HW, 1, ptr(out), P * HW, 0, None, 0, 0, ptr(b2), P, C4,
                  HW, N, 0, 1, LRELU_SLOPE, stream())
             IGEMM_TIMER.end(e0, 2.0 * N * HW * C4 * P, ("fwd", N, C4, H, W, P, 1, 1), "pwgemm_kernel",
                             _nb(g, w2, b2) + 2 * _nb(out))
@@ -820,7 +820,7 @@ class PwMlpFn(torch.autograd.Function):
             HW, P, C = H * W, w2.shape[0], h.shape[1]
             dz = torch.empty((N, C4, H, W), device=dy.device, dtype=torch.bfloat16)
             e0 = IGEMM_TIMER.begin()
-            call("dsgan_pw_dgrad_io", ptr(w2), ptr(dy), P * HW, 0, ptr(dz), C4 * HW, 1, ptr(z), C4 * HW,
+            call("dsgan_pw_dgrad_io", ptr(bf16_weight(w2)), 1, ptr(dy), P * HW, 0, ptr(dz), C4 * HW, 1, ptr(z), C4 * HW,
                  C4, P, HW, N, 0, stream())
             IGEMM_TIMER.end(e0, 2.0 * N * HW * C4 * P, ("dgrad", N, C4, H, W, P, 1, 1), "pwgemm_kernel",
                             _nb(dy, w2, dz, z))
@@ -848,7 +848,7 @@ class PwMlpFn(torch.autograd.Function):
             if want_dh:
                 dh = _empty(N, C, H, W, dy)
                 e0 = IGEMM_TIMER.begin()
-                call("dsgan_pw_dgrad_io", ptr(w1), ptr(dz), C4 * HW, 1, ptr(dh), C * HW, 0, None, 0, C, C4, HW,
+                call("dsgan_pw_dgrad_io", ptr(bf16_weight(w1)), 1, ptr(dz), C4 * HW, 1, ptr(dh), C * HW, 0, None, 0, C, C4, HW,
                      N, 0, stream())
                 IGEMM_TIMER.end(e0, 2.0 * N * HW * C4 * C, ("dgrad", N, C4, H, W, C, 1, 1), "pwgemm_kernel",
                                 _nb(dz, w1, dh))

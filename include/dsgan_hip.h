@@ -97,13 +97,14 @@ int dsgan_pw_wgrad_mixed(const void* A, long a_bs, int a_bf16, const void* B, lo
 /* forward with bf16 activations in and/or out (unfused ConvNeXt MLP blocks c4/c5/uc1/uc2,
  * MixConvNeXtML.py:221-240): Y (+)= act(W X + bias), X/Y fp32 or bf16; ypre (nullable) = fp32
  * pre-activation, or with ypre_grad_bf16 the bf16 act'(pre) the backward multiplies by */
-int dsgan_pw_fwd_io(const float* W, const void* X, long x_bs, int x_bf16, void* Y, long y_bs, int y_bf16,
-                    const void* ypre, long ypre_bs, int ypre_grad_bf16, const float* bias, int M, int K,
-                    int P, int nb, int act, int accumulate, float slope, hipStream_t stream);
+int dsgan_pw_fwd_io(const void* W, int w_bf16, const void* X, long x_bs, int x_bf16, void* Y, long y_bs, int y_bf16,
+                    const void* ypre, long ypre_bs, int ypre_grad_bf16, const float* bias, int M, int K, int P, int nb,
+                    int act, int accumulate, float slope, hipStream_t stream);
 /* DX (+)= (W^T DY) (* GP): DY fp32 or bf16, DX fp32 or bf16, GP (nullable) the bf16 act'(pre) of
  * dsgan_pw_fwd_io.  Unfused-block pwconv2 / pwconv1 data-grads. */
-int dsgan_pw_dgrad_io(const float* W, const void* DY, long dy_bs, int dy_bf16, void* DX, long dx_bs, int dx_bf16,
-                      const void* GP, long gp_bs, int M, int K, int P, int nb, int accumulate, hipStream_t stream);
+int dsgan_pw_dgrad_io(const void* W, int w_bf16, const void* DY, long dy_bs, int dy_bf16, void* DX, long dx_bs,
+                      int dx_bf16, const void* GP, long gp_bs, int M, int K, int P, int nb, int accumulate,
+                      hipStream_t stream);
 
 /* ---- fused ConvNeXt MLP (mlp.hip), replaces Block.pwconv1 -> GELU -> pwconv2 -------------------
  * DSGAN/models/model/MixConvNeXtML.py:221-223,236-240 (nn.Linear(C,4C) + GELU + nn.Linear(4C,P) on

@@ -215,9 +215,10 @@ def test_instnorm_bf16_output(N, C, HW):
     assert torch.equal(m, m32) and torch.equal(r, r32)
 
 
+@pytest.mark.parametrize("w_bf16", [0, 1])
 @pytest.mark.parametrize("dy_bf16,dx_bf16,gp", [(0, 1, True), (1, 0, False), (1, 1, True), (0, 0, False)])
 @pytest.mark.parametrize("N,M,K,P", [(2, 512, 128, 256), (1, 2048, 256, 128), (2, 96, 64, 384), (1, 1024, 1024, 256)])
-def test_pw_dgrad_io(dy_bf16, dx_bf16, gp, N, M, K, P):
+def test_pw_dgrad_io(w_bf16, dy_bf16, dx_bf16, gp, N, M, K, P):
     """dsgan_pw_dgrad_io: DX = (W^T DY) (* GP) with bf16 DY/DX options vs float64 torch on the
     bf16-rounded operands (the last shape takes the 256-row M tiles)."""
     from dsgan_hip._lib import call, ptr, stream
@@ -230,7 +231,8 @@ def test_pw_dgrad_io(dy_bf16, dx_bf16, gp, N, M, K, P):
         ref = ref * gpv.double()
     dyd = dy.to(DEV).to(torch.bfloat16) if dy_bf16 else dy.to(DEV)
     dx = torch.empty((N, M, P), device=DEV, dtype=torch.bfloat16 if dx_bf16 else torch.float32)
-    call("dsgan_pw_dgrad_io", ptr(w.to(DEV)), ptr(dyd), K * P, dy_bf16, ptr(dx), M * P, dx_bf16,
+    wd = w.to(DEV).to(torch.bfloat16) if w_bf16 else w.to(DEV)
+    call("dsgan_pw_dgrad_io", ptr(wd), w_bf16, ptr(dyd), K * P, dy_bf16, ptr(dx), M * P, dx_bf16,
          ptr(gpv.to(DEV)) if gp else None, M * P, M, K, P, N, 0, stream())
     torch.cuda.synchronize()
     got = dx.double().cpu()
@@ -784,8 +786,10 @@ def test_instance_norm_cat(shape):
     assert torch.equal(sd.grad.cpu(), sr.grad)
 
 
-@pytest.mark.parametrize("M,K,P,nb", [(2048, 512, 4096, 2), (1024, 256, 1024, 3), (256, 64, 256, 2), (4096, 1024, 1024, 1)])
-def test_pw_fwd_io_bf16_outputs(M, K, P, nb):
+@pytest.mark.parametrize("w_bf16,x_bf16", [(0, 0), (1, 1), (1, 0)])
+@pytest.mark.parametrize("M,K,P,nb", [(2048, 512, 4096, 2), (1024, 256, 1024, 3), (256, 64, 256, 2), (4096, 1024, 1024, 1),
+                                      (96, 40, 256, 2)])
+def test_pw_fwd_io_bf16_outputs(w_bf16, x_bf16, M, K, P, nb):
     """pwconv1 of the unfused MLP blocks (MixConvNeXtML.py:221-223): g = gelu(W x + b) and
     gp = gelu'(W x + b) written bf16 through the LDS-staged epilogue, vs torch on the same bf16
     operands (one bf16 ulp)."""
@@ -799,8 +803,9 @@ def test_pw_fwd_io_bf16_outputs(M, K, P, nb):
     b = torch.randn(M, generator=g).cuda()
     y = torch.empty(nb, M, P, device="cuda", dtype=torch.bfloat16)
     gp = torch.empty_like(y)
-    call("dsgan_pw_fwd_io", ptr(w), ptr(x), K * P, 0, ptr(y), M * P, 1, ptr(gp), M * P, 1, ptr(b), M, K, P, nb,
-         HF.ACT["gelu"], 0, 0.2, stream())
+    wd, xd = (w.bfloat16() if w_bf16 else w), (x.bfloat16() if x_bf16 else x)
+    call("dsgan_pw_fwd_io", ptr(wd), w_bf16, ptr(xd), K * P, x_bf16, ptr(y), M * P, 1, ptr(gp), M * P, 1, ptr(b), M, K,
+         P, nb, HF.ACT["gelu"], 0, 0.2, stream())
     z = torch.einsum("mk,bkp->bmp", w.bfloat16().double(), x.bfloat16().double()) + b.double().view(1, M, 1)
     zz = z.clone().requires_grad_(True)
     torch.nn.functional.gelu(zz).sum().backward()

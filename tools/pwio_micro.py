@@ -1,4 +1,4 @@
-"""Time dsgan_pw_fwd_io (pwconv1 of the unfused MLP blocks) epilogue variants at the c4/c5 shapes:
+"""Time dsgan_pw_fwd_io (bf16 weight and activation in, as in the training path) (pwconv1 of the unfused MLP blocks) epilogue variants at the c4/c5 shapes:
 gelu + bf16 g + bf16 gelu' (the training path), gelu + bf16 g only, no act bf16 out, no act fp32 out."""
 import os, sys
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -21,20 +21,20 @@ def timeit(fn, it=20):
 
 for N, K, H, M in [(16, 512, 64, 2048), (16, 1024, 32, 4096), (16, 256, 128, 1024)]:
     P = H * H
-    x = torch.randn(N, K, P, device="cuda")
-    w = torch.randn(M, K, device="cuda") * 0.05
+    x = torch.randn(N, K, P, device="cuda").bfloat16()
+    w = (torch.randn(M, K, device="cuda") * 0.05).bfloat16()
     b = torch.randn(M, device="cuda")
     g = torch.empty(N, M, P, device="cuda", dtype=torch.bfloat16)
     gp = torch.empty(N, M, P, device="cuda", dtype=torch.bfloat16)
     y32 = torch.empty(N, M, P, device="cuda")
     v = {
-        "gelu+g+gp": lambda: call("dsgan_pw_fwd_io", ptr(w), ptr(x), K * P, 0, ptr(g), M * P, 1, ptr(gp), M * P, 1,
+        "gelu+g+gp": lambda: call("dsgan_pw_fwd_io", ptr(w), 1, ptr(x), K * P, 1, ptr(g), M * P, 1, ptr(gp), M * P, 1,
                                   ptr(b), M, K, P, N, 1, 0, 0.2, stream()),
-        "gelu+g": lambda: call("dsgan_pw_fwd_io", ptr(w), ptr(x), K * P, 0, ptr(g), M * P, 1, None, 0, 0,
+        "gelu+g": lambda: call("dsgan_pw_fwd_io", ptr(w), 1, ptr(x), K * P, 1, ptr(g), M * P, 1, None, 0, 0,
                                ptr(b), M, K, P, N, 1, 0, 0.2, stream()),
-        "bf16 out": lambda: call("dsgan_pw_fwd_io", ptr(w), ptr(x), K * P, 0, ptr(g), M * P, 1, None, 0, 0,
+        "bf16 out": lambda: call("dsgan_pw_fwd_io", ptr(w), 1, ptr(x), K * P, 1, ptr(g), M * P, 1, None, 0, 0,
                                  ptr(b), M, K, P, N, 0, 0, 0.2, stream()),
-        "fp32 out": lambda: call("dsgan_pw_fwd_io", ptr(w), ptr(x), K * P, 0, ptr(y32), M * P, 0, None, 0, 0,
+        "fp32 out": lambda: call("dsgan_pw_fwd_io", ptr(w), 1, ptr(x), K * P, 1, ptr(y32), M * P, 0, None, 0, 0,
                                  ptr(b), M, K, P, N, 0, 0, 0.2, stream()),
     }
     fl = 2.0 * N * P * M * K
