@@ -337,18 +337,21 @@ __global__ __launch_bounds__(NW * 64, MINB) void mlp_fwd_kernel(MlpArgs g) {
 // ------------------------------------------------------------------------------------------
 // backward (data path): dh, g, dz, per-(tile, quarter) sums of dz
 // ------------------------------------------------------------------------------------------
-template <int C, int P, int BN, int HC, int NW>
-__global__ __launch_bounds__(NW * 64, 1) void mlp_bwd_kernel(MlpArgs g) {
+// GD: also write g and dz (bf16) and the b1 partial sums for the weight-grad GEMMs; without it the
+// kernel writes dh only (mlp_wgrad_kernel recomputes what the weight path needs), drops the g
+// chunk buffer and fits two workgroups per CU (MINB) where the tiles allow.
+template <int C, int P, int BN, int HC, int NW, bool GD, int MINB>
+__global__ __launch_bounds__(NW * 64, MINB) void mlp_bwd_kernel(MlpArgs g) {
   constexpr int NT = NW * 64;
   constexpr int C4 = 4 * C, NCH = C4 / HC;
   constexpr int HSTR = BN + 32, NSTR = HC + 8, W1STR = C + 8, W2STR = HC + 8;
   constexpr int H_SZ = C * HSTR, D_SZ = P * HSTR, N_SZ = BN * NSTR, W1_SZ = HC * W1STR, W2_SZ = P * W2STR;
-  __shared__ __attribute__((aligned(16))) __bf16 smem[H_SZ + D_SZ + 2 * N_SZ + W1_SZ + W2_SZ];
+  __shared__ __attribute__((aligned(16))) __bf16 smem[H_SZ + D_SZ + (GD ? 2 : 1) * N_SZ + W1_SZ + W2_SZ];
   __bf16* Hs = smem;
   __bf16* Ds = Hs + H_SZ;
-  __bf16* Zn = Ds + D_SZ;     // dz chunk, pixel-major [BN][NSTR]
-  __bf16* Gn = Zn + N_SZ;     // g chunk,  pixel-major [BN][NSTR]
-  __bf16* W1s = Gn + N_SZ;
+  __bf16* Zn = Ds + D_SZ;                 // dz chunk, pixel-major [BN][NSTR]
+  __bf16* Gn = Zn + (GD ? N_SZ : 0);      // g chunk,  pixel-major [BN][NSTR] (GD only)
+  __bf16* W1s = Zn + (GD ? 2 : 1) * N_SZ;
   __bf16* W2s = W1s + W1_SZ;
 
   using ZG = WGrid<HC, BN, NW>;   // z / t chunk [HC x BN]
@@ -448,7 +451,7 @@ __global__ __launch_bounds__(NW * 64, 1) void mlp_bwd_kernel(MlpArgs g) {
             dv4[e] = (__bf16)(tacc[i][t][4 * q + e] * gp);
           }
           const int m = wm * (HC / 2) + i * 32 + 8 * q + 4 * lh;
-          *reinterpret_cast<mbf16x4*>(Gn + n * NSTR + m) = gv4;
+          if constexpr (GD) *reinterpret_cast<mbf16x4*>(Gn + n * NSTR + m) = gv4;
           *reinterpret_cast<mbf16x4*>(Zn + n * NSTR + m) = dv4;
         }
       }
@@ -456,7 +459,7 @@ __global__ __launch_bounds__(NW * 64, 1) void mlp_bwd_kernel(MlpArgs g) {
     // ---- copy-out: 8 pixels of one hidden row per lane (transposing read) -> 16-byte stores;
     //      per-(tile, wave>>1) sums of dz for the b1 grad.  Skipped (g_out == NULL) when the
     //      weight-grads come from mlp_wgrad_kernel instead. ----
-    if (g.g_out) {
+    if constexpr (GD) {
       float bacc = 0.f;
 #pragma unroll
       for (int c = 0; c < CPW; ++c) {
@@ -471,7 +474,7 @@ __global__ __launch_bounds__(NW * 64, 1) void mlp_bwd_kernel(MlpArgs g) {
         for (int e = 0; e < 8; ++e) bacc += (float)dv[e];
       }
       bacc += __shfl_xor(bacc, 32, 64);
-      if (lh == 0) g.bsum[((long)tile * (NW / 2) + (wave >> 1)) * C4 + j * HC + chh + lr] = bacc;
+      if (lh == 0 && g.bsum) g.bsum[((long)tile * (NW / 2) + (wave >> 1)) * C4 + j * HC + chh + lr] = bacc;
     }
     // ---- dh += W1[chunk]^T dz ----
 #pragma unroll
@@ -555,14 +558,15 @@ struct WTiles {
   static_assert(T % NW == 0 || NW % T == 0, "weight-grad tile split");
 };
 
-template <int C, int P, int BN, int NW, bool HBF>
-__global__ __launch_bounds__(NW * 64, 1) void mlp_wgrad_kernel(MlpArgs g) {
+template <int C, int P, int BN, int NW, bool HBF, int MINB>
+__global__ __launch_bounds__(NW * 64, MINB) void mlp_wgrad_kernel(MlpArgs g) {
   constexpr int HC = 64;
   constexpr int NT = NW * 64;
   constexpr int C4 = 4 * C, NCH = C4 / HC;
   // Hs / Ds are read transposed (z, t: k = channel) and row-wise (dW: k = pixel): a row stride of
-  // 20 (mod 64) dwords keeps the row-wise 16-byte reads conflict-free
-  constexpr int HSTR = BN + 40, NSTR = HC + 8, W1STR = C + 8, W2STR = HC + 8;
+  // 4 (mod 16) 16-byte slots keeps the row-wise 16-byte reads conflict-free (the transposed reads
+  // are then 2-way at BN = 64, whose tight stride lets two workgroups share a CU)
+  constexpr int HSTR = BN + (BN == 64 ? 8 : 40), NSTR = HC + 8, W1STR = C + 8, W2STR = HC + 8;
   constexpr int H_SZ = C * HSTR, D_SZ = P * HSTR, N_SZ = BN * NSTR, W1_SZ = HC * W1STR, W2_SZ = P * W2STR;
   __shared__ __attribute__((aligned(16))) __bf16 smem[H_SZ + D_SZ + 2 * N_SZ + W1_SZ + W2_SZ];
   __bf16* Hs = smem;
@@ -808,17 +812,17 @@ static void fwd_launch(const MlpArgs& g, hipStream_t st) {
 }
 // backward: 8 waves x 128 pixels where the LDS tiles fit, else 4 waves x 64 pixels (same bsum
 // granularity: one partial row per 32 pixels)
-template <int C, int P, int BN, int NW>
+template <int C, int P, int BN, int NW, bool GD = true, int MINB = 1>
 static void bwd_launch(const MlpArgs& g, hipStream_t st) {
   static_assert(BN / (NW / 2) == 32, "bsum granularity");
   const unsigned tiles = (unsigned)((long)g.nb * (g.HW / BN));
-  hipLaunchKernelGGL((mlp_bwd_kernel<C, P, BN, 64, NW>), dim3(tiles), dim3(NW * 64), 0, st, g);
+  hipLaunchKernelGGL((mlp_bwd_kernel<C, P, BN, 64, NW, GD, MINB>), dim3(tiles), dim3(NW * 64), 0, st, g);
 }
 
 // weight-grad kernel: same pixel tile as the backward; splits so that NCH * S ~ 512 workgroups
 // (2 per CU), a multiple of 8 (whole split groups per XCD), at most one tile per split
 static int mlp_wgrad_splits(int C, int P, int HW, int nb) {
-  const int bn = (C == 64 || (C == 128 && P == 64)) ? 128 : 64;
+  const int bn = 64;
   const int nch = 4 * C / 64;
   const long ntiles = (long)nb * (HW / bn);
   long S = 512 / nch;
@@ -828,11 +832,11 @@ static int mlp_wgrad_splits(int C, int P, int HW, int nb) {
   return (int)S;
 }
 
-template <int C, int P, int BN, int NW>
+template <int C, int P, int BN, int NW, int MINB>
 static void wgrad_launch(const MlpArgs& g, hipStream_t st) {
   const unsigned wgs = (unsigned)((4 * C / 64) * g.splits);
-  if (g.h_bf16) hipLaunchKernelGGL((mlp_wgrad_kernel<C, P, BN, NW, true>), dim3(wgs), dim3(NW * 64), 0, st, g);
-  else hipLaunchKernelGGL((mlp_wgrad_kernel<C, P, BN, NW, false>), dim3(wgs), dim3(NW * 64), 0, st, g);
+  if (g.h_bf16) hipLaunchKernelGGL((mlp_wgrad_kernel<C, P, BN, NW, true, MINB>), dim3(wgs), dim3(NW * 64), 0, st, g);
+  else hipLaunchKernelGGL((mlp_wgrad_kernel<C, P, BN, NW, false, MINB>), dim3(wgs), dim3(NW * 64), 0, st, g);
 }
 
 }  // namespace dsg
@@ -870,8 +874,8 @@ int dsgan_mlp_fwd(const void* h, long h_bs, int h_bf16, const void* w1, const fl
 int dsgan_mlp_bwd(const void* h, long h_bs, int h_bf16, const float* dy, long dy_bs, const void* w1, const float* b1,
                   const void* w2, float* dh, long dh_bs, void* g_out, void* dz_out, float* bsum, int nb,
                   int C, int P, int HW, hipStream_t st) {
-  DSG_REQUIRE(h && dy && w1 && b1 && w2 && dh && nb > 0 && ((g_out && dz_out && bsum) || (!g_out && !dz_out && !bsum)),
-              "dsgan_mlp_bwd: bad args (g_out, dz_out, bsum: all or none)");
+  DSG_REQUIRE(h && dy && w1 && b1 && w2 && dh && nb > 0 && (g_out != nullptr) == (dz_out != nullptr) && (g_out || !bsum),
+              "dsgan_mlp_bwd: bad args (g_out and dz_out both or neither; bsum needs them)");
   DSG_REQUIRE(dsgan_mlp_supported(C, P, HW), "dsgan_mlp_bwd: unsupported shape C=%d P=%d HW=%d", C, P, HW);
   DSG_REQUIRE(((uintptr_t)h & 15) == 0 && ((uintptr_t)dy & 15) == 0 && (h_bs & 7) == 0 && (dy_bs & 3) == 0 &&
               ((uintptr_t)g_out & 15) == 0 && ((uintptr_t)dz_out & 15) == 0,
@@ -880,7 +884,12 @@ int dsgan_mlp_bwd(const void* h, long h_bs, int h_bf16, const float* dy, long dy
   g.h = h; g.h_bs = h_bs; g.dy = dy; g.dy_bs = dy_bs; g.w1 = (const __bf16*)w1; g.b1 = b1;
   g.w2 = (const __bf16*)w2; g.out = dh; g.out_bs = dh_bs; g.g_out = (__bf16*)g_out;
   g.dz_out = (__bf16*)dz_out; g.bsum = bsum; g.HW = HW; g.nb = nb; g.h_bf16 = h_bf16;
-  if (C == 64) bwd_launch<64, 128, 128, 8>(g, st);
+  if (!g_out) {   // dh only: 64-pixel tiles, two workgroups per CU where the LDS allows
+    if (C == 64) bwd_launch<64, 128, 64, 4, false, 2>(g, st);
+    else if (C == 128 && P == 64) bwd_launch<128, 64, 64, 4, false, 2>(g, st);
+    else if (C == 128) bwd_launch<128, 256, 64, 4, false, 1>(g, st);
+    else bwd_launch<256, 128, 64, 4, false, 1>(g, st);
+  } else if (C == 64) bwd_launch<64, 128, 128, 8>(g, st);
   else if (C == 128 && P == 64) bwd_launch<128, 64, 128, 8>(g, st);
   else if (C == 128) bwd_launch<128, 256, 64, 4>(g, st);
   else bwd_launch<256, 128, 64, 4>(g, st);
@@ -907,10 +916,10 @@ int dsgan_mlp_wgrad(const void* h, long h_bs, int h_bf16, const float* dy, long 
   g.w2 = (const __bf16*)w2; g.HW = HW; g.nb = nb; g.ws = ws;
   const int S = mlp_wgrad_splits(C, P, HW, nb);
   g.splits = S;
-  if (C == 64) wgrad_launch<64, 128, 128, 8>(g, st);
-  else if (C == 128 && P == 64) wgrad_launch<128, 64, 128, 8>(g, st);
-  else if (C == 128) wgrad_launch<128, 256, 64, 4>(g, st);
-  else wgrad_launch<256, 128, 64, 4>(g, st);
+  if (C == 64) wgrad_launch<64, 128, 64, 4, 2>(g, st);
+  else if (C == 128 && P == 64) wgrad_launch<128, 64, 64, 4, 2>(g, st);
+  else if (C == 128) wgrad_launch<128, 256, 64, 4, 1>(g, st);
+  else wgrad_launch<256, 128, 64, 4, 1>(g, st);
   DSG_CHECK_LAUNCH();
   const long n1 = 4L * C * C, n2 = (long)P * 4 * C;
   launch_split_reduce(ws, S, n1, dw1, st);

@@ -890,9 +890,11 @@ class PwMlpFn(torch.autograd.Function):
             dy, dybs = dy.contiguous(), P * HW
         gw2, gb2, gws, gw1, gb1 = (_grad_buf(t) for t in (w2, b2, ws_ref, w1, b1))
         dh = _empty(N, C, H, W, h)
-        if gw1 is not None and gb1 is not None and gw2 is not None:
+        if gw1 is not None and gb1 is not None and gw2 is not None and C < 256:
             # dh from the data-path kernel; dW1 / db1 / dW2 from the weight-path kernel, which
-            # recomputes z and dz per hidden chunk -- gelu(z) and dz never reach HBM
+            # recomputes z and dz per hidden chunk -- gelu(z) and dz never reach HBM.  (Both kernels
+            # are GELU/VALU-bound, so the recompute pays only where the bf16 g/dz round trip is the
+            # larger cost: measured at B=16, C=128 @256^2 1.98 -> 1.77 ms, C=256 @128^2 1.70 -> 1.94 ms.)
             w1b, w2b = bf16_weight(w1), bf16_weight(w2)
             e0 = IGEMM_TIMER.begin()
             call("dsgan_mlp_bwd", ptr(h), C * HW, ctx.hb, ptr(dy), dybs, ptr(w1b), ptr(b1), ptr(w2b), ptr(dh), C * HW,
@@ -911,33 +913,32 @@ class PwMlpFn(torch.autograd.Function):
                 conv_wgrad_raw(dy, x, gws, 1, 0)
             _params_done(*ctx.refs)
             return dh, PwMlpFn._dx(ctx, dy, ws, x)
-        ntiles = N * HW // ctx.tile
         g = torch.empty((N, C4, H, W), device=h.device, dtype=torch.bfloat16)
         dz = torch.empty_like(g)
-        bsum = torch.empty((ntiles, C4), device=h.device, dtype=torch.float32)
         e0 = IGEMM_TIMER.begin()
         call("dsgan_mlp_bwd", ptr(h), C * HW, ctx.hb, ptr(dy), dybs, ptr(bf16_weight(w1)), ptr(b1),
-             ptr(bf16_weight(w2)), ptr(dh), C * HW, ptr(g), ptr(dz), ptr(bsum), N, C, P, HW, stream())
+             ptr(bf16_weight(w2)), ptr(dh), C * HW, ptr(g), ptr(dz), None, N, C, P, HW, stream())
         IGEMM_TIMER.end(e0, _mlp_flops(N, C, P, HW), ("mlp_bwd", N, C, H, W, P, 1, 1), "mlp_bwd_kernel",
-                        _nb(h, dy, w1, b1, w2, dh, g, dz, bsum))
+                        _nb(h, dy, w1, b1, w2, dh, g, dz))
+        # bias grads from the weight-grads' staged A tiles: b2 = sum dy, b1 = sum of the bf16 dz
         if gw2 is not None:
             e0 = IGEMM_TIMER.begin()
-            call("dsgan_pw_wgrad_mixed", ptr(dy), dybs, 0, ptr(g), C4 * HW, 1, ptr(gw2), None, P, C4, HW, N,
+            call("dsgan_pw_wgrad_mixed", ptr(dy), dybs, 0, ptr(g), C4 * HW, 1, ptr(gw2), ptr(gb2), P, C4, HW, N,
                  ptr(_pw_ws(P, C4, HW, N, dy)), stream())
             IGEMM_TIMER.end(e0, 2.0 * N * HW * C4 * P, ("wgrad", N, C4, H, W, P, 1, 1), "pwgemm_kernel",
                             _nb(dy, g, gw2))
-        if gb2 is not None:
+        elif gb2 is not None:
             channel_sum_raw(dy, gb2)
         if gws is not None:
             conv_wgrad_raw(dy, x, gws, 1, 0)
         if gw1 is not None:
             e0 = IGEMM_TIMER.begin()
-            call("dsgan_pw_wgrad_mixed", ptr(dz), C4 * HW, 1, ptr(h), C * HW, ctx.hb, ptr(gw1), None, C4, C, HW, N,
-                 ptr(_pw_ws(C4, C, HW, N, dz)), stream())
+            call("dsgan_pw_wgrad_mixed", ptr(dz), C4 * HW, 1, ptr(h), C * HW, ctx.hb, ptr(gw1), ptr(gb1), C4, C, HW,
+                 N, ptr(_pw_ws(C4, C, HW, N, dz)), stream())
             IGEMM_TIMER.end(e0, 2.0 * N * HW * C4 * C, ("wgrad", N, C, H, W, C4, 1, 1), "pwgemm_kernel",
                             _nb(dz, h, gw1))
-        if gb1 is not None:
-            call("dsgan_colsum", ptr(bsum), ntiles, C4, ptr(gb1), stream())
+        elif gb1 is not None:
+            channel_sum_raw(dz.float(), gb1)
         _params_done(*ctx.refs)
         return dh, PwMlpFn._dx(ctx, dy, ws, x)
 

@@ -124,7 +124,8 @@ int dsgan_mlp_fwd(const void* h, long h_bs, int h_bf16, const void* w1, const fl
 int dsgan_mlp_bwd(const void* h, long h_bs, int h_bf16, const float* dy, long dy_bs, const void* w1,
                   const float* b1, const void* w2, float* dh, long dh_bs, void* g_out, void* dz_out,
                   float* bsum, int nb, int C, int P, int HW, hipStream_t stream);
-/* dsgan_mlp_bwd with g_out = dz_out = bsum = NULL writes dh only; the weight-grads then come from
+/* bsum may be NULL (the b1 grad then comes from dsgan_pw_wgrad_mixed's db on dz).
+ * dsgan_mlp_bwd with g_out = dz_out = bsum = NULL writes dh only; the weight-grads then come from
  * dsgan_mlp_wgrad: dw1 [4C][C] += dz h^T, dw2 [P][4C] += dy gelu(z)^T, db1 [4C] += sum dz, with z and
  * dz recomputed per (hidden chunk, pixel split) workgroup so neither reaches HBM.  ws:
  * dsgan_mlp_wgrad_workspace() floats of per-split partials, summed in a fixed order. */
