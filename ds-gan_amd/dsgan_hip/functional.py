@@ -99,6 +99,7 @@ class KernelTimer:
 
 
 IGEMM_TIMER = KernelTimer()
+AUX_TIMER = KernelTimer()   # the HBM-bound depthwise / InstanceNorm launches (tools/launch_table.py)
 
 
 def _nb(*ts):
@@ -734,8 +735,10 @@ class PwMlpFn(torch.autograd.Function):
                 mean = torch.empty(N * C, device=d.device, dtype=torch.float32)
                 rstd = torch.empty(N * C, device=d.device, dtype=torch.float32)
                 h = torch.empty((N, C, H, W), device=d.device, dtype=torch.bfloat16)
+                e0 = AUX_TIMER.begin()
                 call("dsgan_instnorm_fwd_bf16", ptr(d), dbs, ptr(h), C * HW, ptr(mean), ptr(rstd), N, C, HW, IN_EPS,
                      stream())
+                AUX_TIMER.end(e0, 0.0, ("in_fwd_bf16", N, C, H, W), "instnorm", _nb(d, h))
             else:
                 h, mean, rstd = instnorm_raw(d)
                 tile = tile if h.data_ptr() % 16 == 0 else 0
@@ -959,8 +962,11 @@ def dwconv_raw(x, w, b, flip=False, out=None, accumulate=False):
     K = w.shape[-1]
     y = out if out is not None else _empty(N, C, H, W, x)
     y4, ybs = nchw(y)
+    e0 = AUX_TIMER.begin()
     call("dsgan_dwconv_fwd", ptr(x), xbs, ptr(w), ptr(b), ptr(y4), ybs, N, C, H, W, K, int(flip), int(accumulate),
          stream())
+    AUX_TIMER.end(e0, 2.0 * N * C * H * W * K * K, ("dw_dgrad" if flip else "dw_fwd", N, C, H, W, K), "dwconv",
+                  (3 if accumulate else 2) * _nb(x))
     return y4
 
 
@@ -970,7 +976,9 @@ def _dw_wgrad(dy, x, gw, gb, K):
     N, C, H, W = x4.shape
     al = int(x4.data_ptr() % 16 == 0 and dy4.data_ptr() % 16 == 0 and xbs % 4 == 0 and dybs % 4 == 0)
     ws = torch.empty(_lib.load().dsgan_dwconv_wgrad_workspace(N, C, H, W, K, al), device=x4.device, dtype=torch.float32)
+    e0 = AUX_TIMER.begin()
     call("dsgan_dwconv_wgrad", ptr(dy4), dybs, ptr(x4), xbs, ptr(gw), ptr(gb), N, C, H, W, K, ptr(ws), stream())
+    AUX_TIMER.end(e0, 2.0 * N * C * H * W * K * K, ("dw_wgrad", N, C, H, W, K), "dwconv", 2 * _nb(x4))
 
 
 class DwConvFn(torch.autograd.Function):
@@ -1060,8 +1068,10 @@ def instnorm_raw(x, scale=None, res=None, act=None, out=None):
     y4, ybs = nchw(y)
     mean = torch.empty(N * C, device=x.device, dtype=torch.float32)
     rstd = torch.empty(N * C, device=x.device, dtype=torch.float32)
+    e0 = AUX_TIMER.begin()
     call("dsgan_instnorm_fwd", ptr(x), xbs, ptr(scale), ptr(res), rbs, ptr(y4), ybs, ptr(mean),
          ptr(rstd), N, C, H * W, ACT[act], LRELU_SLOPE, IN_EPS, stream())
+    AUX_TIMER.end(e0, 0.0, ("in_fwd", N, C, H, W, act, res is not None), "instnorm", (3 if res is not None else 2) * _nb(x))
     return y4, mean, rstd
 
 
@@ -1075,9 +1085,12 @@ def instnorm_bwd_raw(dy, x, scale, res, mean, rstd, act, want_dres, want_dscale)
     dx = _empty(N, C, H, W, x)
     dres = _empty(N, C, H, W, x) if want_dres else None
     dscale = torch.empty(N * C, device=x.device, dtype=torch.float32) if want_dscale else None
+    e0 = AUX_TIMER.begin()
     call("dsgan_instnorm_bwd", ptr(dy), dybs, ptr(x), xbs, ptr(scale), ptr(res), rbs, ptr(mean),
          ptr(rstd), ptr(dx), C * H * W, ptr(dres), C * H * W, ptr(dscale), N, C, H * W, ACT[act],
          LRELU_SLOPE, IN_EPS, stream())
+    AUX_TIMER.end(e0, 0.0, ("in_bwd", N, C, H, W, act, res is not None), "instnorm",
+                  (3 + (res is not None) + want_dres) * _nb(x))
     return dx, dres, dscale
 
 

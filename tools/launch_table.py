@@ -28,13 +28,13 @@ def main():
     for _ in range(3):
         m.optimize_parameters()
     torch.cuda.synchronize()
-    HF.IGEMM_TIMER.rec = []
-    HF.IGEMM_TIMER.on = True
+    HF.IGEMM_TIMER.rec, HF.AUX_TIMER.rec = [], []
+    HF.IGEMM_TIMER.on = HF.AUX_TIMER.on = True
     m.optimize_parameters()
     torch.cuda.synchronize()
-    HF.IGEMM_TIMER.on = False
+    HF.IGEMM_TIMER.on = HF.AUX_TIMER.on = False
     rows = []
-    for r in HF.IGEMM_TIMER.rec:
+    for r in HF.IGEMM_TIMER.rec + HF.AUX_TIMER.rec:
         ms = r[0].elapsed_time(r[1])
         if a.family and r[4] != a.family:
             continue
