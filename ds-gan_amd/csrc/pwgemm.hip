@@ -249,7 +249,10 @@ __global__ __launch_bounds__(256, 2) void pwgemm_kernel(PwArgs g) {
         int off;
         if (B_KMAJ) off = (it / (BN / 4)) * B_STR + (it % (BN / 4)) * 4;
         else off = (it >> 3) * B_STR + (it & 7) * 4;
-        *reinterpret_cast<pbf16x4*>(Bs + off) = cv(rb[i]);
+        // WGRAD rows past N (a thin operand, e.g. a 12-channel hidden) read 0: skip their
+        // conversion / activation-on-load (whole waves branch around it)
+        if (MODE == PW_WGRAD && n0 + (it >> 3) >= g.N) *reinterpret_cast<pbf16x4*>(Bs + off) = pbf16x4{};
+        else *reinterpret_cast<pbf16x4*>(Bs + off) = cv(rb[i]);
       }
     };
     if constexpr (BBF && MODE != PW_WGRAD) {
@@ -535,7 +538,11 @@ static int wgrad_plan(int M, int N, long K, int BM, int* k_split) {
   const long tiles = (long)((M + BM - 1) / BM) * ((N + 127) / 128);
   long splits = (640 + tiles - 1) / tiles;
   const long max_splits = (K + 8L * PBK - 1) / (8L * PBK);
-  const long byte_cap = ((long)(M + N) * K) / (4L * M * N);
+  // the byte cap yields to a one-workgroup-per-CU floor: a deep weight-grad over few tiles (e.g.
+  // 1024 x 2048 at 16^2, 128 tiles) is worth its extra partial traffic
+  long byte_cap = ((long)(M + N) * K) / (4L * M * N);
+  const long floor_splits = (256 + tiles - 1) / tiles;
+  if (byte_cap < floor_splits) byte_cap = floor_splits;
   if (splits > max_splits) splits = max_splits;
   if (splits > byte_cap) splits = byte_cap;
   if (splits < 1) splits = 1;
