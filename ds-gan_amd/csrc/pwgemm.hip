@@ -78,19 +78,23 @@ __device__ __forceinline__ pbf16x4 cvt4(float4 v, int bact, float slope) {
 // ABF (WGRAD only) / BBF: the A (dy) / B (x, dy) operand is bf16 in HBM -- the block activation h
 // (InstanceNorm bf16 output), gelu(z) and dz of the MLPs (mlp.hip and the unfused blocks) -- and
 // is copied to LDS unconverted.
-template <int MODE, int BM, int ABF = 0, int BBF = 0>
-__global__ __launch_bounds__(256, 2) void pwgemm_kernel(PwArgs g) {
-  constexpr int BN = 128;
-  constexpr int WM = 2, WN = 2;
+// BN x WN waves / BK: 128 x 2 / 32 (4 waves, two workgroups per CU), or the wide form 256 x 4 / 64
+// (8 waves, 256 x 256 tiles, 64-deep K steps: twice the MFMAs per staged byte and per barrier)
+// for the deep, wide GEMMs of the unfused blocks.
+template <int MODE, int BM, int ABF = 0, int BBF = 0, int BN = 128, int WN = 2, int BK = PBK>
+__global__ __launch_bounds__(128 * WN, WN == 2 ? 2 : 1) void pwgemm_kernel(PwArgs g) {
+  constexpr int WM = 2, NT = 64 * WM * WN;
   constexpr int TM = BM / WM / 32, TN = BN / WN / 32;
+  constexpr int RM_STR = BK + 8;        // row-major [rows][k] stride (odd 16-byte slot count)
+  constexpr int RF = BK / 4, RH = BK / 8;   // fp32 / bf16 16-byte items per row-major row
   // A tile: row-major [BM][RM_STR] (FWD, WGRAD) or k-major [PBK][BM+32] (DGRAD)
   // B tile: k-major [PBK][BN+32] (FWD, DGRAD) or row-major [BN][RM_STR] (WGRAD)
   constexpr bool A_KMAJ = (MODE == PW_DGRAD);
   constexpr bool B_KMAJ = (MODE != PW_WGRAD);
   constexpr int A_STR = A_KMAJ ? BM + 32 : RM_STR;
   constexpr int B_STR = B_KMAJ ? BN + 32 : RM_STR;
-  constexpr int A_SZ = A_KMAJ ? PBK * A_STR : BM * A_STR;
-  constexpr int B_SZ = B_KMAJ ? PBK * B_STR : BN * B_STR;
+  constexpr int A_SZ = A_KMAJ ? BK * A_STR : BM * A_STR;
+  constexpr int B_SZ = B_KMAJ ? BK * B_STR : BN * B_STR;
   __shared__ __attribute__((aligned(16))) __bf16 smem[2 * (A_SZ + B_SZ)];
 
   // wave index through readfirstlane: the compiler then knows it is uniform (SGPR), so
@@ -115,7 +119,7 @@ __global__ __launch_bounds__(256, 2) void pwgemm_kernel(PwArgs g) {
   int kbeg = 0, kend = g.K;
   if (MODE == PW_WGRAD) { kbeg = split * g.k_split; kend = min(g.K, kbeg + g.k_split); }
   if (kbeg >= kend) return;
-  const int nk = (kend - kbeg + PBK - 1) / PBK;
+  const int nk = (kend - kbeg + BK - 1) / BK;
 
   // FWD/DGRAD: the N tile lies inside one image (P % BN == 0)
   const int bimg = (MODE == PW_WGRAD) ? 0 : n0 / g.P;
@@ -124,8 +128,9 @@ __global__ __launch_bounds__(256, 2) void pwgemm_kernel(PwArgs g) {
   // ---- staging maps ----
   // row-major tiles: item = (row, c4) with c4 in [0,8): 8 float4 per 32-k row
   // k-major tiles  : item = (k, c4) with c4 in [0, C/4)
-  constexpr int A_ITEMS = ABF ? (A_KMAJ ? PBK * BM / 8 : BM * 4) / 256 : (A_KMAJ ? PBK * BM / 4 : BM * 8) / 256;
-  constexpr int B_ITEMS = BBF ? BN * 4 / 256 : (B_KMAJ ? PBK * BN / 4 : BN * 8) / 256;
+  constexpr int A_ITEMS = BK * BM / (ABF ? 8 : 4) / NT;
+  constexpr int B_ITEMS = BK * BN / (BBF ? 8 : 4) / NT;
+  static_assert(A_ITEMS * NT * (ABF ? 8 : 4) == BK * BM && B_ITEMS * NT * (BBF ? 8 : 4) == BK * BN, "staging split");
   float4 ra[ABF ? 1 : A_ITEMS], rb[BBF ? 1 : B_ITEMS];
   pu32x4 rha[ABF ? A_ITEMS : 1], rhb[BBF ? B_ITEMS : 1];
   float asr[A_ITEMS];   // WGRAD asum: this thread's running row sums of its A items (fixed order)
@@ -149,70 +154,70 @@ __global__ __launch_bounds__(256, 2) void pwgemm_kernel(PwArgs g) {
   };
 
   auto gload = [&](int kt) {
-    const int kb = kbeg + kt * PBK;
-    // WGRAD: a 32-pixel K step lies inside one image (P % 32 == 0): image index is uniform
+    const int kb = kbeg + kt * BK;
+    // WGRAD: a BK-pixel K step lies inside one image (P % BK == 0): image index is uniform
     const unsigned bw = (MODE == PW_WGRAD) ? (unsigned)(kb / g.P) : 0u;
     const unsigned pw = (MODE == PW_WGRAD) ? (unsigned)(kb - (int)bw * g.P) : 0u;
     if constexpr (ABF) {   // bf16 A, 8 elements per item
 #pragma unroll
       for (int i = 0; i < A_ITEMS; ++i) {
-        const int it = tid + i * 256;
+        const int it = tid + i * NT;
         unsigned off;
         if (MODE == PW_FWD) {                    // W[M][K] bf16, row m, k = kb + c8*8
-          const int m = m0 + (it >> 2), k = kb + (it & 3) * 8;
+          const int m = m0 + it / RH, k = kb + (it % RH) * 8;
           off = ((m < g.M) & (k < kend)) ? ((unsigned)m * g.K + k) * 2u : PW_OOB;
         } else if (MODE == PW_DGRAD) {           // W[K][M] bf16, row k (k >= K is past the range)
           const int k = kb + it / (BM / 8), m = m0 + (it % (BM / 8)) * 8;
           off = (m < g.M) ? ((unsigned)k * g.M + m) * 2u : PW_OOB;
         } else {                                 // DY[b][M][P] bf16, row m, 8 pixels per item
-          const int m = m0 + (it >> 2);
-          off = (m < g.M) ? (bw * (unsigned)g.a_bs + (unsigned)m * g.P + pw + (it & 3) * 8) * 2u : PW_OOB;
+          const int m = m0 + it / RH;
+          off = (m < g.M) ? (bw * (unsigned)g.a_bs + (unsigned)m * g.P + pw + (it % RH) * 8) * 2u : PW_OOB;
         }
         rha[i] = bldh(rA, off);
       }
     } else
 #pragma unroll
     for (int i = 0; i < A_ITEMS; ++i) {
-      const int it = tid + i * 256;
+      const int it = tid + i * NT;
       unsigned off;
       if (MODE == PW_FWD) {                      // W[M][K], row m, k = kb + c4*4
-        const int m = m0 + (it >> 3), k = kb + (it & 7) * 4;
+        const int m = m0 + it / RF, k = kb + (it % RF) * 4;
         off = ((m < g.M) & (k < kend)) ? ((unsigned)m * g.K + k) * 4u : PW_OOB;
       } else if (MODE == PW_DGRAD) {             // W[K][M], row k (k >= K is past the range)
         const int k = kb + it / (BM / 4), m = m0 + (it % (BM / 4)) * 4;
         off = (m < g.M) ? ((unsigned)k * g.M + m) * 4u : PW_OOB;
       } else {                                   // DY[b][M][P], row m
-        const int m = m0 + (it >> 3);
-        off = (m < g.M) ? (bw * (unsigned)g.a_bs + (unsigned)m * g.P + pw + (it & 7) * 4) * 4u : PW_OOB;
+        const int m = m0 + it / RF;
+        off = (m < g.M) ? (bw * (unsigned)g.a_bs + (unsigned)m * g.P + pw + (it % RF) * 4) * 4u : PW_OOB;
       }
       ra[i] = bld4(rA, off);
     }
     if constexpr (BBF && MODE != PW_WGRAD) {     // X/DY[b][K][P] bf16, k-major: row k, 8 pixels per item
 #pragma unroll
       for (int i = 0; i < B_ITEMS; ++i) {
-        const int it = tid + i * 256;
+        const int it = tid + i * NT;
         const int k = kb + it / (BN / 8);
         rhb[i] = bldh(rB, ((unsigned)k * g.P + p0 + (it % (BN / 8)) * 8) * 2u);
       }
     } else if constexpr (BBF) {                  // X[b][N][P] bf16, row n
 #pragma unroll
       for (int i = 0; i < B_ITEMS; ++i) {
-        const int it = tid + i * 256;
-        const int n = n0 + (it >> 2);
-        const unsigned off = (n < g.N) ? (bw * (unsigned)g.b_bs + (unsigned)n * g.P + pw + (it & 3) * 8) * 2u : PW_OOB;
+        const int it = tid + i * NT;
+        const int n = n0 + it / RH;
+        const unsigned off = (n < g.N) ? (bw * (unsigned)g.b_bs + (unsigned)n * g.P + pw + (it % RH) * 8) * 2u : PW_OOB;
         rhb[i] = bldh(rB, off);
       }
     } else
 #pragma unroll
     for (int i = 0; i < B_ITEMS; ++i) {
-      const int it = tid + i * 256;
+      const int it = tid + i * NT;
       unsigned off;
       if (MODE != PW_WGRAD) {                    // [K][P] k-major (k >= K is past the range)
         const int k = kb + it / (BN / 4);
         off = ((unsigned)k * g.P + p0 + (it % (BN / 4)) * 4) * 4u;
       } else {                                   // X[b][N][P], row n
-        const int n = n0 + (it >> 3);
-        off = (n < g.N) ? (bw * (unsigned)g.b_bs + (unsigned)n * g.P + pw + (it & 7) * 4) * 4u : PW_OOB;
+        const int n = n0 + it / RF;
+        off = (n < g.N) ? (bw * (unsigned)g.b_bs + (unsigned)n * g.P + pw + (it % RF) * 4) * 4u : PW_OOB;
       }
       rb[i] = bld4(rB, off);
     }
@@ -223,8 +228,8 @@ __global__ __launch_bounds__(256, 2) void pwgemm_kernel(PwArgs g) {
     if constexpr (ABF) {
 #pragma unroll
       for (int i = 0; i < A_ITEMS; ++i) {
-        const int it = tid + i * 256;
-        const int off = A_KMAJ ? (it / (BM / 8)) * A_STR + (it % (BM / 8)) * 8 : (it >> 2) * A_STR + (it & 3) * 8;
+        const int it = tid + i * NT;
+        const int off = A_KMAJ ? (it / (BM / 8)) * A_STR + (it % (BM / 8)) * 8 : (it / RH) * A_STR + (it % RH) * 8;
         *reinterpret_cast<pu32x4*>(As + off) = rha[i];
         if (MODE == PW_WGRAD && g.asum) {
           const pbf16x8 hv = __builtin_bit_cast(pbf16x8, rha[i]);
@@ -235,38 +240,38 @@ __global__ __launch_bounds__(256, 2) void pwgemm_kernel(PwArgs g) {
     } else
 #pragma unroll
     for (int i = 0; i < A_ITEMS; ++i) {
-      const int it = tid + i * 256;
+      const int it = tid + i * NT;
       int off;
       if (A_KMAJ) off = (it / (BM / 4)) * A_STR + (it % (BM / 4)) * 4;
-      else off = (it >> 3) * A_STR + (it & 7) * 4;
+      else off = (it / RF) * A_STR + (it % RF) * 4;
       *reinterpret_cast<pbf16x4*>(As + off) = cvt4(ra[i], 0, 0.f);
       if (MODE == PW_WGRAD && g.asum) asr[i] += (ra[i].x + ra[i].y) + (ra[i].z + ra[i].w);
     }
     auto bstore = [&](auto cv) {
 #pragma unroll
       for (int i = 0; i < B_ITEMS; ++i) {
-        const int it = tid + i * 256;
+        const int it = tid + i * NT;
         int off;
         if (B_KMAJ) off = (it / (BN / 4)) * B_STR + (it % (BN / 4)) * 4;
-        else off = (it >> 3) * B_STR + (it & 7) * 4;
+        else off = (it / RF) * B_STR + (it % RF) * 4;
         // WGRAD rows past N (a thin operand, e.g. a 12-channel hidden) read 0: skip their
         // conversion / activation-on-load (whole waves branch around it)
-        if (MODE == PW_WGRAD && n0 + (it >> 3) >= g.N) *reinterpret_cast<pbf16x4*>(Bs + off) = pbf16x4{};
+        if (MODE == PW_WGRAD && n0 + it / RF >= g.N) *reinterpret_cast<pbf16x4*>(Bs + off) = pbf16x4{};
         else *reinterpret_cast<pbf16x4*>(Bs + off) = cv(rb[i]);
       }
     };
     if constexpr (BBF && MODE != PW_WGRAD) {
 #pragma unroll
       for (int i = 0; i < B_ITEMS; ++i) {
-        const int it = tid + i * 256;
+        const int it = tid + i * NT;
         *reinterpret_cast<pu32x4*>(Bs + (it / (BN / 8)) * B_STR + (it % (BN / 8)) * 8) = rhb[i];
       }
       return;
     } else if constexpr (BBF) {
 #pragma unroll
       for (int i = 0; i < B_ITEMS; ++i) {
-        const int it = tid + i * 256;
-        *reinterpret_cast<pu32x4*>(Bs + (it >> 2) * B_STR + (it & 3) * 8) = rhb[i];
+        const int it = tid + i * NT;
+        *reinterpret_cast<pu32x4*>(Bs + (it / RH) * B_STR + (it % RH) * 8) = rhb[i];
       }
       return;
     }
@@ -315,7 +320,7 @@ __global__ __launch_bounds__(256, 2) void pwgemm_kernel(PwArgs g) {
     const __bf16* As = smem + buf * (A_SZ + B_SZ);
     const __bf16* Bs = As + A_SZ;
 #pragma unroll
-    for (int ks = 0; ks < PBK / 16; ++ks) {
+    for (int ks = 0; ks < BK / 16; ++ks) {
       pbf16x8 af[TM], bfr[TN];
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
@@ -348,13 +353,14 @@ __global__ __launch_bounds__(256, 2) void pwgemm_kernel(PwArgs g) {
     if (g.asum) {
       // the threads of one A row (4 bf16 / 8 fp32 items per 32-pixel row) are adjacent lanes:
       // butterfly over them; the n-tile-0 workgroup writes (its split's partial, or db += when unsplit)
-      constexpr int RT = ABF ? 4 : 8;
+      constexpr int RT = ABF ? RH : RF;
 #pragma unroll
       for (int i = 0; i < A_ITEMS; ++i) {
         float t = asr[i];
         t += __shfl_xor(t, 1, 64); t += __shfl_xor(t, 2, 64);
-        if (RT == 8) t += __shfl_xor(t, 4, 64);
-        const int it = tid + i * 256, m = m0 + it / RT;
+        if (RT >= 8) t += __shfl_xor(t, 4, 64);
+        if (RT >= 16) t += __shfl_xor(t, 8, 64);
+        const int it = tid + i * NT, m = m0 + it / RT;
         if (n_t == 0 && it % RT == 0 && m < g.M) {
           if (g.ws) g.ws[(long)gridDim.x / mt / nt * g.M * g.N + (long)split * g.M + m] = t;
           else g.asum[m] += t;
@@ -470,12 +476,15 @@ __global__ __launch_bounds__(256, 2) void pwgemm_kernel(PwArgs g) {
   }
 }
 
-template <int MODE, int BM, int ABF = 0, int BBF = 0>
+template <int MODE, int BM, int ABF = 0, int BBF = 0, int BN = 128, int WN = 2, int BK = PBK>
 static void pw_launch(const PwArgs& g, int splits, hipStream_t st) {
   const int mt = (g.M + BM - 1) / BM;
-  const int nt = (MODE == PW_WGRAD) ? (g.N + 127) / 128 : g.N / 128;
-  hipLaunchKernelGGL((pwgemm_kernel<MODE, BM, ABF, BBF>), dim3((unsigned)((long)mt * nt * splits)), dim3(256), 0, st, g);
+  const int nt = (MODE == PW_WGRAD) ? (g.N + BN - 1) / BN : g.N / BN;
+  hipLaunchKernelGGL((pwgemm_kernel<MODE, BM, ABF, BBF, BN, WN, BK>), dim3((unsigned)((long)mt * nt * splits)),
+                     dim3(128 * WN), 0, st, g);
 }
+
+constexpr int PW_WIDE = -1;   // tile selector: 256 x 256 tiles, 8 waves, 64-deep K steps
 
 // FWD / DGRAD launch over (tile rows, bf16 weight, bf16 activation)
 template <int MODE>
@@ -488,8 +497,16 @@ static void pw_launch_ab(const PwArgs& g, int bm, int abf, int bbf, hipStream_t 
     case 2: pw_launch<MODE, BM, 1, 0>(g, 1, st); break;                \
     default: pw_launch<MODE, BM, 1, 1>(g, 1, st); break;               \
   }
-  if (bm == 256) { PW_AB(256) } else if (bm == 128) { PW_AB(128) } else { PW_AB(64) }
+#define PW_ABW                                                                    \
+  switch (sel) {                                                                  \
+    case 0: pw_launch<MODE, 128, 0, 0>(g, 1, st); break;  /* (not selected) */  \
+    case 1: pw_launch<MODE, 256, 0, 1, 256, 4, 64>(g, 1, st); break;              \
+    case 2: pw_launch<MODE, 256, 1, 0, 256, 4, 64>(g, 1, st); break;              \
+    default: pw_launch<MODE, 256, 1, 1, 256, 4, 64>(g, 1, st); break;             \
+  }
+  if (bm == PW_WIDE) { PW_ABW } else if (bm == 256) { PW_AB(256) } else if (bm == 128) { PW_AB(128) } else { PW_AB(64) }
 #undef PW_AB
+#undef PW_ABW
 }
 
 // dw[e] += sum_s ws[s][e], s in a fixed order: thread (e, j) of a workgroup of EL elements x J
@@ -531,15 +548,15 @@ __global__ __launch_bounds__(256) void split_reduce_kernel(const float* __restri
   }
 }
 
-// K (pixel) split of a weight-grad launch: about 640 workgroups (2.5 per CU: enough bytes in
-// flight to stream HBM), >= 8 K steps each, and partials of at most a quarter of the operand
-// bytes (each split writes, and the reduce reads, an M x N fp32 tile).
-static int wgrad_plan(int M, int N, long K, int BM, int* k_split) {
-  const long tiles = (long)((M + BM - 1) / BM) * ((N + 127) / 128);
-  long splits = (640 + tiles - 1) / tiles;
-  const long max_splits = (K + 8L * PBK - 1) / (8L * PBK);
-  // the byte cap yields to a one-workgroup-per-CU floor: a deep weight-grad over few tiles (e.g.
-  // 1024 x 2048 at 16^2, 128 tiles) is worth its extra partial traffic
+// K (pixel) split of a weight-grad launch: about `target` workgroups (640 = 2.5 per CU for the
+// 4-wave tiles: enough bytes in flight to stream HBM; 256 = one per CU for the 8-wave wide
+// tiles), >= 8 K steps each, and partials of at most a quarter of the operand bytes (each split
+// writes, and the reduce reads, an M x N fp32 tile) -- that cap yielding to a one-workgroup-per-CU
+// floor: a deep weight-grad over few tiles (1024 x 2048 at 16^2, 128 tiles) is worth the traffic.
+static int wgrad_plan(int M, int N, long K, int BM, int BN, int BK, long target, int* k_split) {
+  const long tiles = (long)((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+  long splits = (target + tiles - 1) / tiles;
+  const long max_splits = (K + 8L * BK - 1) / (8L * BK);
   long byte_cap = ((long)(M + N) * K) / (4L * M * N);
   const long floor_splits = (256 + tiles - 1) / tiles;
   if (byte_cap < floor_splits) byte_cap = floor_splits;
@@ -547,12 +564,23 @@ static int wgrad_plan(int M, int N, long K, int BM, int* k_split) {
   if (splits > byte_cap) splits = byte_cap;
   if (splits < 1) splits = 1;
   long ks = (K + splits - 1) / splits;
-  ks = (ks + PBK - 1) / PBK * PBK;
+  ks = (ks + BK - 1) / BK * BK;
   splits = (K + ks - 1) / ks;
   *k_split = (int)ks;
   return (int)splits;
 }
-static int wgrad_split(PwArgs& g, int BM) { return wgrad_plan(g.M, g.N, g.K, BM, &g.k_split); }
+
+// Weight-grad tile choice: 256 x 256 x 64 (8 waves) for the wide, deep ones (both sides >= 256
+// channels), else 128 (64) x 128 x 32.
+static bool wgrad_wide(int M, int N, int P) {
+  return M >= 256 && N >= 256 && P % 64 == 0 && (M % 256 == 0 || M >= 1024) && (N % 256 == 0 || N >= 1024);
+}
+// (fp32-only operands stay on the 4-wave tiles: the wide tile's fp32 staging spills)
+static int wgrad_cfg(PwArgs& g, bool any_bf16, int* bm) {
+  if (any_bf16 && wgrad_wide(g.M, g.N, g.P)) { *bm = PW_WIDE; return wgrad_plan(g.M, g.N, g.K, 256, 256, 64, 256, &g.k_split); }
+  *bm = g.M > 64 ? 128 : 64;
+  return wgrad_plan(g.M, g.N, g.K, *bm, 128, PBK, 640, &g.k_split);
+}
 
 // Pre-pass for many splits over few elements: workgroup (element block, row group g) adds rows
 // [g*SC, (g+1)*SC) (64 elements x 4 row lanes, coalesced 256-B row reads, fixed order) and writes
@@ -609,6 +637,18 @@ static bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 static bool use_bm256(const PwArgs& g) {
   return g.M >= 1024 && g.M % 256 == 0 && g.K >= 1024 && (long)(g.M / 256) * (g.N / 128) >= 512;
 }
+// 256 x 256 x 64 tiles (8 waves, one workgroup per CU) for the wide FWD / DGRAD GEMMs of the
+// unfused blocks: 256-pixel tiles inside one image, M a multiple of 256, a grid of >= 256 tiles.
+static bool use_wide(const PwArgs& g) {
+  return g.M % 256 == 0 && g.P % 256 == 0 && g.K >= 128 && (long)(g.M / 256) * (g.N / 256) >= 256;
+}
+// (Only for plain epilogues: with the per-element bf16 act' side tensor -- the gelu-pair forward
+// and the gp-multiplied data-grad -- one 8-wave workgroup per CU leaves the epilogue's loads and
+// 2-byte stores exposed, measured 1.3-1.5x slower than the 4-wave tiles.)
+static int fd_tile(const PwArgs& g, bool any_bf16) {
+  const bool plain = !g.ypre && !g.gpre;
+  return any_bf16 && plain && use_wide(g) ? PW_WIDE : use_bm256(g) ? 256 : g.M > 64 ? 128 : 64;
+}
 
 }  // namespace dsg
 
@@ -647,13 +687,13 @@ extern "C" int dsgan_pw_gemm(int mode, const float* A, long a_bs, const float* B
     g.a_range = (unsigned)ar; g.b_range = (unsigned)br;
     DSG_REQUIRE(dsgan_pw_supported(mode, M, K, P, a_bs, b_bs, A, B), "dsgan_pw_gemm: unsupported WGRAD shape");
     g.M = M; g.N = N; g.K = nb * P;
-    const int BM = M > 64 ? 128 : 64;
-    const int splits = wgrad_split(g, BM);
+    int bm;
+    const int splits = wgrad_cfg(g, false, &bm);
     DSG_REQUIRE(splits == 1 || ws, "dsgan_pw_gemm: WGRAD needs the dsgan_pw_wgrad_workspace scratch");
     g.ws = splits > 1 ? ws : nullptr;
     g.asum = const_cast<float*>(bias);   // WGRAD: bias (nullable) receives the bias grad += sum_k A
     g.bias = nullptr;
-    if (BM == 128) pw_launch<PW_WGRAD, 128>(g, splits, st);
+    if (bm == 128) pw_launch<PW_WGRAD, 128>(g, splits, st);
     else pw_launch<PW_WGRAD, 64>(g, splits, st);
     wgrad_finish(g, splits, st);
   } else {
@@ -663,16 +703,8 @@ extern "C" int dsgan_pw_gemm(int mode, const float* A, long a_bs, const float* B
     DSG_REQUIRE((long)K * P * 4 < lim && (long)M * K * 4 < lim, "dsgan_pw_gemm: operand exceeds 4 GiB buffer range");
     g.a_range = (unsigned)((long)M * K * 4);
     g.b_range = (unsigned)((long)K * P * 4);
-    const bool big = M > 64;
-    if (mode == PW_FWD) {
-      if (use_bm256(g)) pw_launch<PW_FWD, 256>(g, 1, st);
-      else if (big) pw_launch<PW_FWD, 128>(g, 1, st);
-      else pw_launch<PW_FWD, 64>(g, 1, st);
-    } else {
-      if (use_bm256(g)) pw_launch<PW_DGRAD, 256>(g, 1, st);
-      else if (big) pw_launch<PW_DGRAD, 128>(g, 1, st);
-      else pw_launch<PW_DGRAD, 64>(g, 1, st);
-    }
+    if (mode == PW_FWD) pw_launch_ab<PW_FWD>(g, fd_tile(g, false), 0, 0, st);
+    else pw_launch_ab<PW_DGRAD>(g, fd_tile(g, false), 0, 0, st);
   }
   DSG_CHECK_LAUNCH();
   return 0;
@@ -698,8 +730,7 @@ extern "C" int dsgan_pw_fwd_io(const void* W, int w_bf16, const void* X, long x_
   g.P = P; g.M = M; g.N = nb * P; g.K = K;
   g.a_range = (unsigned)((long)M * K * (w_bf16 ? 2 : 4));
   g.b_range = (unsigned)((long)K * P * (x_bf16 ? 2 : 4));
-  const int bm = use_bm256(g) ? 256 : M > 64 ? 128 : 64;
-  pw_launch_ab<PW_FWD>(g, bm, w_bf16, x_bf16, st);
+  pw_launch_ab<PW_FWD>(g, fd_tile(g, w_bf16 || x_bf16), w_bf16, x_bf16, st);
   DSG_CHECK_LAUNCH();
   return 0;
 }
@@ -723,8 +754,7 @@ extern "C" int dsgan_pw_dgrad_io(const void* W, int w_bf16, const void* DY, long
   g.accumulate = accumulate; g.P = P; g.M = M; g.N = nb * P; g.K = K;
   g.a_range = (unsigned)((long)M * K * (w_bf16 ? 2 : 4));
   g.b_range = (unsigned)((long)K * P * (dy_bf16 ? 2 : 4));
-  const int bm = use_bm256(g) ? 256 : M > 64 ? 128 : 64;
-  pw_launch_ab<PW_DGRAD>(g, bm, w_bf16, dy_bf16, st);
+  pw_launch_ab<PW_DGRAD>(g, fd_tile(g, w_bf16 || dy_bf16), w_bf16, dy_bf16, st);
   DSG_CHECK_LAUNCH();
   return 0;
 }
@@ -734,8 +764,10 @@ extern "C" int dsgan_pw_dgrad_io(const void* W, int w_bf16, const void* DY, long
 // staged A tiles (the bf16 values when A is bf16).  P % 32 == 0, 16-byte aligned operands.
 // Scratch (floats) a weight-grad of M x N over nb*P pixels needs (0: no split).
 extern "C" long dsgan_pw_wgrad_workspace(int M, int N, int P, int nb) {
-  int ks;
-  const int splits = wgrad_plan(M, N, (long)nb * P, M > 64 ? 128 : 64, &ks);
+  PwArgs g{};
+  g.M = M; g.N = N; g.P = P; g.K = nb * P;
+  int bm;   // enough for either tile plan (the caller's operand dtypes pick one)
+  const int splits = max(wgrad_cfg(g, false, &bm), wgrad_cfg(g, true, &bm));
   return splits > 1 ? (long)splits * ((long)M * N + M) : 0;   // weight partials, then bias-sum partials
 }
 
@@ -752,12 +784,15 @@ extern "C" int dsgan_pw_wgrad_mixed(const void* A, long a_bs, int a_bf16, const 
   DSG_REQUIRE(ar < (long)PW_OOB && br < (long)PW_OOB, "dsgan_pw_wgrad_mixed: operands exceed 4 GiB buffer range");
   g.a_range = (unsigned)ar; g.b_range = (unsigned)br;
   g.M = M; g.N = N; g.K = nb * P;
-  const int BM = M > 64 ? 128 : 64;
-  const int splits = wgrad_split(g, BM);
+  int bm;
+  const int splits = wgrad_cfg(g, a_bf16 || b_bf16, &bm);
   DSG_REQUIRE(splits == 1 || ws, "dsgan_pw_wgrad_mixed: needs the dsgan_pw_wgrad_workspace scratch");
   g.ws = splits > 1 ? ws : nullptr;
-  const int sel = (a_bf16 ? 2 : 0) + (b_bf16 ? 1 : 0) + (BM == 128 ? 4 : 0);
+  const int sel = (a_bf16 ? 2 : 0) + (b_bf16 ? 1 : 0) + (bm == 128 ? 4 : bm == PW_WIDE ? 8 : 0);
   switch (sel) {
+    case 9: pw_launch<PW_WGRAD, 256, 0, 1, 256, 4, 64>(g, splits, st); break;
+    case 10: pw_launch<PW_WGRAD, 256, 1, 0, 256, 4, 64>(g, splits, st); break;
+    case 11: pw_launch<PW_WGRAD, 256, 1, 1, 256, 4, 64>(g, splits, st); break;
     case 0: pw_launch<PW_WGRAD, 64, 0, 0>(g, splits, st); break;
     case 1: pw_launch<PW_WGRAD, 64, 0, 1>(g, splits, st); break;
     case 2: pw_launch<PW_WGRAD, 64, 1, 0>(g, splits, st); break;

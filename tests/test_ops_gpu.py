@@ -242,6 +242,27 @@ def test_pw_dgrad_io(w_bf16, dy_bf16, dx_bf16, gp, N, M, K, P):
         assert rel(got, ref) < 1e-5
 
 
+@pytest.mark.parametrize("dy_bf16,gp", [(0, True), (1, False)])
+def test_pw_dgrad_io_wide_tiles(dy_bf16, gp):
+    """The 256 x 256 x 64 (8-wave) tiles of the bf16 data-grad: a grid of 256 tiles over one image
+    (M = 512 rows, 32768 pixels), vs float64 torch on the bf16 operands."""
+    from dsgan_hip._lib import call, ptr, stream
+    N, M, K, P = 1, 512, 256, 32768
+    g = torch.Generator().manual_seed(5)
+    w = torch.randn(K, M, generator=g) / math.sqrt(K)
+    dy = torch.randn(N, K, P, generator=g)
+    gpv = torch.rand(N, M, P, generator=g).to(torch.bfloat16)
+    ref = torch.einsum("km,nkp->nmp", _q(w, "bf16").double(), _q(dy, "bf16").double())
+    if gp:
+        ref = ref * gpv.double()
+    dyd = dy.to(DEV).to(torch.bfloat16) if dy_bf16 else dy.to(DEV)
+    dx = torch.empty((N, M, P), device=DEV)
+    call("dsgan_pw_dgrad_io", ptr(w.to(DEV).to(torch.bfloat16)), 1, ptr(dyd), K * P, dy_bf16, ptr(dx), M * P, 0,
+         ptr(gpv.to(DEV)) if gp else None, M * P, M, K, P, N, 0, stream())
+    torch.cuda.synchronize()
+    assert rel(dx.double().cpu(), ref) < 1e-5
+
+
 @pytest.mark.parametrize("a_bf16,b_bf16", [(0, 0), (1, 1), (1, 0), (0, 1)])
 @pytest.mark.parametrize("N,M,C,P", [(2, 512, 128, 4096), (16, 64, 512, 1024), (1, 96, 40, 256), (2, 2048, 512, 256)])
 def test_pw_wgrad_bias_sums(a_bf16, b_bf16, N, M, C, P):

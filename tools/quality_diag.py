@@ -46,6 +46,11 @@ def pin(mod, prec):
 
 
 def run(base, fp32_parts=()):
+    """base "bf16-nopin": bf16 everywhere, the MidMLKA 1x1 conv included (its shipped fp32 pin off)."""
+    from models.mixconvnext import MidMLKA
+    label = base
+    MidMLKA.conv_precision = "bf16" if base == "bf16-nopin" else "fp32"
+    base = "bf16" if base == "bf16-nopin" else base
     random.seed(20)
     torch.manual_seed(20)
     model = create_model(default_train_opt(gpu_ids=[0], pool_size=0, precision=base, batchSize=batch))
@@ -65,17 +70,17 @@ def run(base, fp32_parts=()):
     m = O.ms_ssim((fg + 1) / 2, tgt).item()
     sim = O.ms_ssim(((fg + 1) / 2).clamp(0, 1), ((ref.fake_B + 1) / 2).clamp(0, 1)).item()
     rel = ((fg - ref.fake_B).norm() / ref.fake_B.norm()).item()
-    print("%-40s delta %.6f  ms_ssim(gpu,ref) %.4f  rel-l2(fake) %.3e" % (base + " +fp32:" + ",".join(fp32_parts),
+    print("%-40s delta %.6f  ms_ssim(gpu,ref) %.4f  rel-l2(fake) %.3e" % (label + " +fp32:" + ",".join(fp32_parts),
                                                                         abs(m - m_ref), sim, rel), flush=True)
+    MidMLKA.conv_precision = "fp32"
 
 
 MID = ("netG.local.mid32", "netG.local.mid64", "netG.local.mid128", "netG.local.mid256")
 UPC = ("netG.local.upc1.1", "netG.local.upc2", "netG.local.upc3")
 UPS = ("netG.local.up1", "netG.local.up2", "netG.local.up3")
-variants = [("fp32", ()), ("bf16", ()),
-            ("bf16", ("netG.local",)), ("bf16", ("netG.local",)),
-            ("bf16", MID + UPC), ("bf16", MID), ("bf16", UPC), ("bf16", UPS),
-            ("bf16", ("netG.local.mid256", "netG.local.mid128")), ("bf16", ("netG.local.mid32", "netG.local.mid64"))]
+# "bf16" = the shipped policy (MidMLKA 1x1 pinned to fp32); "bf16-nopin" = everything bf16
+variants = [("fp32", ()), ("bf16", ()), ("bf16-nopin", ()),
+            ("bf16-nopin", MID + UPC), ("bf16-nopin", MID), ("bf16-nopin", UPC), ("bf16-nopin", UPS)]
 if len(sys.argv) > 2:
     variants = [("bf16", tuple(v.split(","))) for v in sys.argv[2:]]
 for base, parts in variants:
