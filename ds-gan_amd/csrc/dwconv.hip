@@ -218,18 +218,16 @@ __device__ __forceinline__ void dw_row(float (&v)[12], const float* row) {
   for (int i = 0; i < 4; ++i) { v[i] = a[i]; v[4 + i] = b[i]; v[8 + i] = c[i]; }
 }
 
+// One workgroup's output tile (bx) of plane `plane`; `tile` = LDS of DwTile<K,...>::LH * LW floats.
 template <int K, int TWT, int THT, int R>
-__global__ __launch_bounds__(256, 4) void dwconv_fwd_v2(const float* __restrict__ x, long x_bs,
-                                                     const float* __restrict__ w,
-                                                     const float* __restrict__ bias,
-                                                     float* __restrict__ y, long y_bs, int C, int H,
-                                                     int W, int flip, int accumulate, int tiles_w) {
+__device__ __forceinline__ void dw_fwd_body(const float* __restrict__ x, long x_bs, const float* __restrict__ w,
+                                            const float* __restrict__ bias, float* __restrict__ y, long y_bs, int C,
+                                            int H, int W, int flip, int accumulate, int tiles_w, int bx, int plane,
+                                            float* tile) {
   using T = DwTile<K, TWT, THT, R>;
-  __shared__ __attribute__((aligned(16))) float tile[T::LH][T::LW];
-  const int plane = blockIdx.y;
   const int n = plane / C, c = plane - n * C;
-  const int th0 = (blockIdx.x / tiles_w) * T::TH, tw0 = (blockIdx.x % tiles_w) * T::TW;
-  dw_stage<K, TWT, THT, R, true>(&tile[0][0], x + (long)n * x_bs + (long)c * H * W, H, W, th0, tw0);
+  const int th0 = (bx / tiles_w) * T::TH, tw0 = (bx % tiles_w) * T::TW;
+  dw_stage<K, TWT, THT, R, true>(tile, x + (long)n * x_bs + (long)c * H * W, H, W, th0, tw0);
   float wv[K * K];
 #pragma unroll
   for (int i = 0; i < K * K; ++i) wv[i] = w[c * K * K + (flip ? K * K - 1 - i : i)];
@@ -244,10 +242,10 @@ __global__ __launch_bounds__(256, 4) void dwconv_fwd_v2(const float* __restrict_
   // one input row in flight ahead of the FMAs; the scheduling barrier keeps the compiler from
   // hoisting every row load of the unrolled loop (which costs occupancy or spills)
   float cur[12], nxt[12];
-  dw_row<K>(cur, &tile[R * ty][4 * tx]);
+  dw_row<K>(cur, tile + (R * ty) * T::LW + 4 * tx);
 #pragma unroll
   for (int r = 0; r < R + K - 1; ++r) {
-    if (r + 1 < R + K - 1) dw_row<K>(nxt, &tile[R * ty + r + 1][4 * tx]);
+    if (r + 1 < R + K - 1) dw_row<K>(nxt, tile + (R * ty + r + 1) * T::LW + 4 * tx);
 #pragma unroll
     for (int s = 0; s < R; ++s) {
       const int kh = r - s;
@@ -276,20 +274,54 @@ __global__ __launch_bounds__(256, 4) void dwconv_fwd_v2(const float* __restrict_
   }
 }
 
+template <int K, int TWT, int THT, int R>
+__global__ __launch_bounds__(256, 4) void dwconv_fwd_v2(const float* __restrict__ x, long x_bs,
+                                                     const float* __restrict__ w,
+                                                     const float* __restrict__ bias,
+                                                     float* __restrict__ y, long y_bs, int C, int H,
+                                                     int W, int flip, int accumulate, int tiles_w) {
+  using T = DwTile<K, TWT, THT, R>;
+  __shared__ __attribute__((aligned(16))) float tile[T::LH * T::LW];
+  dw_fwd_body<K, TWT, THT, R>(x, x_bs, w, bias, y, y_bs, C, H, W, flip, accumulate, tiles_w, blockIdx.x, blockIdx.y,
+                              tile);
+}
+
+// MidMLKA's four channel quarters (X3/X5/X7/X9 depthwise, MixConvNeXtML.py:94-97,110-111) in one
+// launch: blockIdx.z = quarter (K = 3 + 2z), one tile configuration for all four (the 9x9-safe
+// rows per thread).  The quarters' launches are each too small to fill the chip on their own.
+struct DwQuad { const float* w[4]; const float* b[4]; float* ws[4]; float* dw[4]; float* db[4]; };
+
+template <int TWT, int THT, int R>
+__global__ __launch_bounds__(256, 3) void dwconv_multi_fwd(const float* __restrict__ x, long x_bs, DwQuad q4,
+                                                           float* __restrict__ y, long y_bs, int q, int H, int W,
+                                                           int flip, int accumulate, int tiles_w) {
+  using T = DwTile<9, TWT, THT, R>;
+  __shared__ __attribute__((aligned(16))) float tile[T::LH * T::LW];
+  const int qi = blockIdx.z;
+  const float* xq = x + (long)qi * q * H * W;
+  float* yq = y + (long)qi * q * H * W;
+  switch (qi) {
+    case 0: dw_fwd_body<3, TWT, THT, R>(xq, x_bs, q4.w[0], q4.b[0], yq, y_bs, q, H, W, flip, accumulate, tiles_w, blockIdx.x, blockIdx.y, tile); break;
+    case 1: dw_fwd_body<5, TWT, THT, R>(xq, x_bs, q4.w[1], q4.b[1], yq, y_bs, q, H, W, flip, accumulate, tiles_w, blockIdx.x, blockIdx.y, tile); break;
+    case 2: dw_fwd_body<7, TWT, THT, R>(xq, x_bs, q4.w[2], q4.b[2], yq, y_bs, q, H, W, flip, accumulate, tiles_w, blockIdx.x, blockIdx.y, tile); break;
+    default: dw_fwd_body<9, TWT, THT, R>(xq, x_bs, q4.w[3], q4.b[3], yq, y_bs, q, H, W, flip, accumulate, tiles_w, blockIdx.x, blockIdx.y, tile); break;
+  }
+}
+
 // dw[c] += sum over (images [n0, n0+nper), tile) of the 7x7 (KxK) correlation of dy with x;
 // db[c] += sum dy.  The dy block of a thread stays in registers; partial sums are reduced over
 // the workgroup once, after all of its images.
+// Weight-grad partials of channel c, tile bx, image split `split` (slot split * ntiles + bx).
+// `tile` = LH * LW floats of LDS, `red` = 4 * (K*K + 1) floats.
 template <int K, int TWT, int THT, int R>
-__global__ __launch_bounds__(256, 4) void dwconv_wgrad_v2(const float* __restrict__ dy, long dy_bs,
-                                                       const float* __restrict__ x, long x_bs,
-                                                       float* __restrict__ ws,
-                                                       int N, int C, int H, int W, int tiles_w, int nper) {
+__device__ __forceinline__ void dw_wgrad_body(const float* __restrict__ dy, long dy_bs, const float* __restrict__ x,
+                                              long x_bs, float* __restrict__ ws, int N, int C, int H, int W,
+                                              int tiles_w, int nper, int bx, int c, int split, int ntiles, float* tile,
+                                              float* red_) {
   using T = DwTile<K, TWT, THT, R>;
-  __shared__ __attribute__((aligned(16))) float tile[T::LH][T::LW];
-  __shared__ float red[4][K * K + 1];
-  const int c = blockIdx.y;
-  const int th0 = (blockIdx.x / tiles_w) * T::TH, tw0 = (blockIdx.x % tiles_w) * T::TW;
-  const int n0 = blockIdx.z * nper, n1 = min(N, n0 + nper);
+  float (*red)[K * K + 1] = reinterpret_cast<float (*)[K * K + 1]>(red_);
+  const int th0 = (bx / tiles_w) * T::TH, tw0 = (bx % tiles_w) * T::TW;
+  const int n0 = split * nper, n1 = min(N, n0 + nper);
   const int tx = threadIdx.x % TWT, ty = threadIdx.x / TWT;
   float acc[K * K];
 #pragma unroll
@@ -297,7 +329,7 @@ __global__ __launch_bounds__(256, 4) void dwconv_wgrad_v2(const float* __restric
   float bacc = 0.f;
   for (int n = n0; n < n1; ++n) {
     __syncthreads();
-    dw_stage<K, TWT, THT, R>(&tile[0][0], x + (long)n * x_bs + (long)c * H * W, H, W, th0, tw0);
+    dw_stage<K, TWT, THT, R>(tile, x + (long)n * x_bs + (long)c * H * W, H, W, th0, tw0);
     float g[R][4];
     const float* gp = dy + (long)n * dy_bs + (long)c * H * W + tw0 + 4 * tx;
 #pragma unroll
@@ -310,10 +342,10 @@ __global__ __launch_bounds__(256, 4) void dwconv_wgrad_v2(const float* __restric
     }
     __syncthreads();
     float cur[12], nxt[12];
-    dw_row<K>(cur, &tile[R * ty][4 * tx]);
+    dw_row<K>(cur, tile + (R * ty) * T::LW + 4 * tx);
 #pragma unroll
     for (int r = 0; r < R + K - 1; ++r) {
-      if (r + 1 < R + K - 1) dw_row<K>(nxt, &tile[R * ty + r + 1][4 * tx]);
+      if (r + 1 < R + K - 1) dw_row<K>(nxt, tile + (R * ty + r + 1) * T::LW + 4 * tx);
 #pragma unroll
       for (int s = 0; s < R; ++s) {
         const int kh = r - s;
@@ -342,8 +374,39 @@ __global__ __launch_bounds__(256, 4) void dwconv_wgrad_v2(const float* __restric
   __syncthreads();
   if (threadIdx.x < K * K + 1) {   // this workgroup's slot of ws (summed in order by dw_partial_reduce)
     const float v = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
-    const long g = (long)blockIdx.z * gridDim.x + blockIdx.x;   // slot layout [g][c][i]
+    const long g = (long)split * ntiles + bx;   // slot layout [g][c][i]
     ws[(g * C + c) * (K * K + 1) + threadIdx.x] = v;
+  }
+}
+
+template <int K, int TWT, int THT, int R>
+__global__ __launch_bounds__(256, 4) void dwconv_wgrad_v2(const float* __restrict__ dy, long dy_bs,
+                                                       const float* __restrict__ x, long x_bs,
+                                                       float* __restrict__ ws,
+                                                       int N, int C, int H, int W, int tiles_w, int nper) {
+  using T = DwTile<K, TWT, THT, R>;
+  __shared__ __attribute__((aligned(16))) float tile[T::LH * T::LW];
+  __shared__ float red[4 * (K * K + 1)];
+  dw_wgrad_body<K, TWT, THT, R>(dy, dy_bs, x, x_bs, ws, N, C, H, W, tiles_w, nper, blockIdx.x, blockIdx.y, blockIdx.z,
+                                gridDim.x, tile, red);
+}
+
+// The four MidMLKA quarters' weight-grads in one launch: blockIdx.z = quarter * nsplit + split.
+template <int TWT, int THT, int R>
+__global__ __launch_bounds__(256, 4) void dwconv_multi_wgrad(const float* __restrict__ dy, long dy_bs,
+                                                             const float* __restrict__ x, long x_bs, DwQuad q4,
+                                                             int N, int q, int H, int W, int tiles_w, int nper,
+                                                             int nsplit) {
+  using T = DwTile<9, TWT, THT, R>;
+  __shared__ __attribute__((aligned(16))) float tile[T::LH * T::LW];
+  __shared__ float red[4 * 82];
+  const int qi = blockIdx.z / nsplit, split = blockIdx.z - qi * nsplit;
+  const long co = (long)qi * q * H * W;
+  switch (qi) {
+    case 0: dw_wgrad_body<3, TWT, THT, R>(dy + co, dy_bs, x + co, x_bs, q4.ws[0], N, q, H, W, tiles_w, nper, blockIdx.x, blockIdx.y, split, gridDim.x, tile, red); break;
+    case 1: dw_wgrad_body<5, TWT, THT, R>(dy + co, dy_bs, x + co, x_bs, q4.ws[1], N, q, H, W, tiles_w, nper, blockIdx.x, blockIdx.y, split, gridDim.x, tile, red); break;
+    case 2: dw_wgrad_body<7, TWT, THT, R>(dy + co, dy_bs, x + co, x_bs, q4.ws[2], N, q, H, W, tiles_w, nper, blockIdx.x, blockIdx.y, split, gridDim.x, tile, red); break;
+    default: dw_wgrad_body<9, TWT, THT, R>(dy + co, dy_bs, x + co, x_bs, q4.ws[3], N, q, H, W, tiles_w, nper, blockIdx.x, blockIdx.y, split, gridDim.x, tile, red); break;
   }
 }
 
@@ -441,11 +504,105 @@ static bool dw_tiled_ok(int K, int cfg, const void* x, const void* dy, long x_bs
   return cfg && K >= 3 && ((uintptr_t)x & 15) == 0 && ((uintptr_t)dy & 15) == 0 && (x_bs & 3) == 0 && (dy_bs & 3) == 0;
 }
 
+// MidMLKA quarters: one tile configuration for all four kernel sizes (rows per thread safe for
+// 9x9: cfg 1 -> 32 x 8 threads x 2 rows, cfg 2 -> 16 x 16 x 2, cfg 3 -> 8 x 32 x 1)
+template <int TWT, int THT, int R>
+static void dw_multi_fwd_launch(const float* x, long x_bs, const DwQuad& q4, float* y, long y_bs, int N, int q, int H,
+                                int W, int flip, int accumulate, hipStream_t st) {
+  using T = DwTile<9, TWT, THT, R>;
+  const int tw = W / T::TW, th = (H + T::TH - 1) / T::TH;
+  hipLaunchKernelGGL((dwconv_multi_fwd<TWT, THT, R>), dim3(tw * th, N * q, 4), dim3(256), 0, st, x, x_bs, q4, y, y_bs,
+                     q, H, W, flip, accumulate, tw);
+}
+
+template <int TWT, int THT, int R>
+static long dw_multi_wgrad_run(const float* dy, long dy_bs, const float* x, long x_bs, const DwQuad* q4, int N, int q,
+                               int H, int W, hipStream_t st) {
+  using T = DwTile<9, TWT, THT, R>;
+  const int tw = W / T::TW, th = (H + T::TH - 1) / T::TH;
+  int nsplit, nper;
+  const long G = dw_wgrad_v2_plan<9, TWT, THT, R>(N, q, H, W, &nsplit, &nper);
+  if (q4)
+    hipLaunchKernelGGL((dwconv_multi_wgrad<TWT, THT, R>), dim3(tw * th, q, 4 * nsplit), dim3(256), 0, st, dy, dy_bs,
+                       x, x_bs, *q4, N, q, H, W, tw, nper, nsplit);
+  return G;
+}
+
+static long dw_multi_wgrad_any(int cfg, const float* dy, long dy_bs, const float* x, long x_bs, const DwQuad* q4,
+                               int N, int q, int H, int W, hipStream_t st) {
+  if (cfg == 1) return dw_multi_wgrad_run<32, 8, 2>(dy, dy_bs, x, x_bs, q4, N, q, H, W, st);
+  if (cfg == 2) return dw_multi_wgrad_run<16, 16, 2>(dy, dy_bs, x, x_bs, q4, N, q, H, W, st);
+  return dw_multi_wgrad_run<8, 32, 1>(dy, dy_bs, x, x_bs, q4, N, q, H, W, st);
+}
+
 }  // namespace dsg
 
 using namespace dsg;
 
 extern "C" {
+
+// MidMLKA chunk(4) -> X3/X5/X7/X9 depthwise (MixConvNeXtML.py:94-97,110-111) as one launch per
+// pass.  Supported when every quarter takes a tiled configuration: W % 4 == 0, W in {32, 64,
+// multiples of 128}, 16-byte aligned x / y (dy) with batch strides % 4 == 0.
+int dsgan_dwconv_multi_supported(int H, int W, const void* x, long x_bs, const void* y, long y_bs) {
+  return dw_cfg(H, W) != 0 && ((uintptr_t)x & 15) == 0 && ((uintptr_t)y & 15) == 0 && (x_bs & 3) == 0 &&
+         (y_bs & 3) == 0;
+}
+
+// y[:, 4 quarters] (+)= dwconv_{3,5,7,9}(x quarter) + bias (flip = 1, biases NULL: the data-grad)
+int dsgan_dwconv_multi_fwd(const float* x, long x_bs, const float* w3, const float* b3, const float* w5,
+                           const float* b5, const float* w7, const float* b7, const float* w9, const float* b9,
+                           float* y, long y_bs, int N, int q, int H, int W, int flip, int accumulate, hipStream_t st) {
+  DSG_REQUIRE(x && y && w3 && w5 && w7 && w9 && N > 0 && q > 0, "dsgan_dwconv_multi_fwd: bad args");
+  DSG_REQUIRE(dsgan_dwconv_multi_supported(H, W, x, x_bs, y, y_bs) && (long)N * q <= 65535,
+              "dsgan_dwconv_multi_fwd: unsupported H=%d W=%d / alignment", H, W);
+  DwQuad q4{};
+  q4.w[0] = w3; q4.w[1] = w5; q4.w[2] = w7; q4.w[3] = w9;
+  q4.b[0] = b3; q4.b[1] = b5; q4.b[2] = b7; q4.b[3] = b9;
+  const int cfg = dw_cfg(H, W);
+  if (cfg == 1) dw_multi_fwd_launch<32, 8, 2>(x, x_bs, q4, y, y_bs, N, q, H, W, flip, accumulate, st);
+  else if (cfg == 2) dw_multi_fwd_launch<16, 16, 2>(x, x_bs, q4, y, y_bs, N, q, H, W, flip, accumulate, st);
+  else dw_multi_fwd_launch<8, 32, 1>(x, x_bs, q4, y, y_bs, N, q, H, W, flip, accumulate, st);
+  DSG_CHECK_LAUNCH();
+  return 0;
+}
+
+// floats of scratch: the four quarters' slot partials, back to back (quarter K uses G*q*(K*K+1))
+long dsgan_dwconv_multi_wgrad_workspace(int N, int q, int H, int W) {
+  const int cfg = dw_cfg(H, W);
+  if (!cfg) return 0;
+  const long G = dw_multi_wgrad_any(cfg, nullptr, 0, nullptr, 0, nullptr, N, q, H, W, 0);
+  return G * q * (10 + 26 + 50 + 82);
+}
+
+// dw_K += sum dy * x, db_K += sum dy for the four quarters (fixed-order slot reduction)
+int dsgan_dwconv_multi_wgrad(const float* dy, long dy_bs, const float* x, long x_bs, float* dw3, float* db3,
+                             float* dw5, float* db5, float* dw7, float* db7, float* dw9, float* db9, int N, int q,
+                             int H, int W, float* ws, hipStream_t st) {
+  DSG_REQUIRE(dy && x && ws && dw3 && dw5 && dw7 && dw9 && N > 0 && q > 0 && q <= 65535,
+              "dsgan_dwconv_multi_wgrad: bad args");
+  DSG_REQUIRE(dsgan_dwconv_multi_supported(H, W, x, x_bs, dy, dy_bs), "dsgan_dwconv_multi_wgrad: unsupported H=%d W=%d",
+              H, W);
+  const int cfg = dw_cfg(H, W);
+  const long G = dw_multi_wgrad_any(cfg, nullptr, 0, nullptr, 0, nullptr, N, q, H, W, 0);
+  DwQuad q4{};
+  float* dws[4] = {dw3, dw5, dw7, dw9};
+  float* dbs[4] = {db3, db5, db7, db9};
+  long off = 0;
+  for (int i = 0; i < 4; ++i) {
+    const int K = 3 + 2 * i;
+    q4.ws[i] = ws + off;
+    off += G * q * (K * K + 1);
+  }
+  dw_multi_wgrad_any(cfg, dy, dy_bs, x, x_bs, &q4, N, q, H, W, st);
+  DSG_CHECK_LAUNCH();
+  for (int i = 0; i < 4; ++i) {
+    const int K = 3 + 2 * i;
+    launch_split_reduce_kk(q4.ws[i], (int)G, (long)q * (K * K + 1), dws[i], dbs[i], K * K + 1, st);
+  }
+  DSG_CHECK_LAUNCH();
+  return 0;
+}
 
 // y (+)= dwconv(x, w) + bias   (flip=1, bias=NULL gives the data-grad of dy; accumulate adds
 // into y -- the data-grad of a tensor that has another consumer)

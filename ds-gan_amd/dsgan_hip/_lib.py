@@ -72,6 +72,10 @@ SIGNATURES = {
     "dsgan_dwconv_fwd": [P, L, P, P, P, L, I, I, I, I, I, I, I, S],
     "dsgan_dwconv_wgrad_workspace": [I, I, I, I, I, I],
     "dsgan_dwconv_wgrad": [P, L, P, L, P, P, I, I, I, I, I, P, S],
+    "dsgan_dwconv_multi_supported": [I, I, P, L, P, L],
+    "dsgan_dwconv_multi_fwd": [P, L, P, P, P, P, P, P, P, P, P, L, I, I, I, I, I, I, S],
+    "dsgan_dwconv_multi_wgrad_workspace": [I, I, I, I],
+    "dsgan_dwconv_multi_wgrad": [P, L, P, L, P, P, P, P, P, P, P, P, I, I, I, I, P, S],
     # norm_pointwise.hip
     "dsgan_instnorm_fwd": [P, L, P, P, L, P, L, P, P, I, I, I, I, F, F, S],
     "dsgan_instnorm_fwd_bf16": [P, L, P, L, P, P, I, I, I, F, S],

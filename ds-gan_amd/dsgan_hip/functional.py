@@ -1012,16 +1012,29 @@ def dwconv(x, w, b):
 
 class MultiDwConvFn(torch.autograd.Function):
     """MidMLKA's chunk(4) -> X3/X5/X7/X9 depthwise -> cat (MixConvNeXtML.py:110-111), written
-    straight into one output buffer (no chunk/cat copies)."""
+    straight into one output buffer (no chunk/cat copies); one launch per pass over the four
+    quarters where the plane shape takes a tiled configuration (dsgan_dwconv_multi_*)."""
+
+    @staticmethod
+    def _multi_ok(x4, xbs, y, ybs):
+        N, C, H, W = x4.shape
+        return C % 4 == 0 and bool(_lib.load().dsgan_dwconv_multi_supported(H, W, ptr(x4), xbs, ptr(y), ybs))
 
     @staticmethod
     def forward(ctx, x, *wb):
-        x4, _ = nchw(x)
+        x4, xbs = nchw(x)
         N, C, H, W = x4.shape
         q = C // 4
         y = _empty(N, C, H, W, x4)
-        for i in range(4):
-            dwconv_raw(x4[:, i * q:(i + 1) * q], wb[2 * i], wb[2 * i + 1], out=y[:, i * q:(i + 1) * q])
+        if MultiDwConvFn._multi_ok(x4, xbs, y, C * H * W):
+            e0 = AUX_TIMER.begin()
+            call("dsgan_dwconv_multi_fwd", ptr(x4), xbs, *[ptr(t) for t in wb], ptr(y), C * H * W, N, q, H, W, 0, 0,
+                 stream())
+            AUX_TIMER.end(e0, 2.0 * N * q * H * W * (9 + 25 + 49 + 81), ("dw_multi_fwd", N, C, H, W, 0), "dwconv",
+                          2 * _nb(x4))
+        else:
+            for i in range(4):
+                dwconv_raw(x4[:, i * q:(i + 1) * q], wb[2 * i], wb[2 * i + 1], out=y[:, i * q:(i + 1) * q])
         ctx.save_for_backward(x4, *wb)
         ctx.refs = wb
         ctx.box = _box(x)
@@ -1032,19 +1045,39 @@ class MultiDwConvFn(torch.autograd.Function):
         x, *wb = ctx.saved_tensors
         N, C, H, W = x.shape
         q = C // 4
-        dy4, _ = nchw(dy)
+        dy4, dybs = nchw(dy)
         out, acc = _acc_target(ctx.box)
         dx = None
         if ctx.needs_input_grad[0]:
             dx = out if acc else _empty(N, C, H, W, x)
-        for i in range(4):
-            sl = slice(i * q, (i + 1) * q)
-            w = wb[2 * i]
+        grads = [_grad_buf(r) for r in ctx.refs]
+        xbs = x.stride(0) if N > 1 else C * H * W
+        multi = MultiDwConvFn._multi_ok(x, xbs, dy4, dybs) and (dx is None or dx.stride(0) == C * H * W or N == 1)
+        if multi:
             if dx is not None:
-                dwconv_raw(dy4[:, sl], w, None, flip=True, out=dx[:, sl], accumulate=acc)
-            gw, gb = _grad_buf(ctx.refs[2 * i]), _grad_buf(ctx.refs[2 * i + 1])
+                e0 = AUX_TIMER.begin()
+                call("dsgan_dwconv_multi_fwd", ptr(dy4), dybs, *[ptr(t) if i % 2 == 0 else None for i, t in enumerate(wb)],
+                     ptr(dx), C * H * W, N, q, H, W, 1, int(acc), stream())
+                AUX_TIMER.end(e0, 2.0 * N * q * H * W * 164, ("dw_multi_dgrad", N, C, H, W, 0), "dwconv",
+                              (3 if acc else 2) * _nb(x))
+            if all(g_ is not None for g_ in grads):
+                wsp = torch.empty(_lib.load().dsgan_dwconv_multi_wgrad_workspace(N, q, H, W), device=x.device,
+                                  dtype=torch.float32)
+                e0 = AUX_TIMER.begin()
+                call("dsgan_dwconv_multi_wgrad", ptr(dy4), dybs, ptr(x), xbs, *[ptr(g_) for g_ in grads], N, q, H, W,
+                     ptr(wsp), stream())
+                AUX_TIMER.end(e0, 2.0 * N * q * H * W * 164, ("dw_multi_wgrad", N, C, H, W, 0), "dwconv", 2 * _nb(x))
+                grads = [None] * 8
+        else:
+            for i in range(4):
+                sl = slice(i * q, (i + 1) * q)
+                if dx is not None:
+                    dwconv_raw(dy4[:, sl], wb[2 * i], None, flip=True, out=dx[:, sl], accumulate=acc)
+        for i in range(4):
+            gw, gb = grads[2 * i], grads[2 * i + 1]
             if gw is not None:
-                _dw_wgrad(dy4[:, sl], x[:, sl], gw, gb, w.shape[-1])
+                sl = slice(i * q, (i + 1) * q)
+                _dw_wgrad(dy4[:, sl], x[:, sl], gw, gb, wb[2 * i].shape[-1])
         dx = None if acc else _give(ctx.box, dx)
         _params_done(*ctx.refs)
         return (dx,) + (None,) * 8

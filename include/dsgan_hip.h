@@ -241,6 +241,20 @@ int dsgan_dwconv_fwd(const float* x, long x_bs, const float* w, const float* bia
 /* dw += sum dy*x (KxK), db += sum dy; per-workgroup partials in ws (dsgan_dwconv_wgrad_workspace
  * floats; aligned16 = x, dy 16-byte aligned with batch strides % 4 == 0) summed in a fixed order. */
 long dsgan_dwconv_wgrad_workspace(int N, int C, int H, int W, int K, int aligned16);
+/* MidMLKA's chunk(4) -> X3/X5/X7/X9 depthwise convs (MixConvNeXtML.py:94-97,110-111) as ONE launch
+ * per pass over the four channel quarters (q channels each, quarter i has K = 3 + 2i):
+ * dsgan_dwconv_multi_fwd: y (+)= dwconv_K(x) + b_K (flip = 1 with NULL biases: the data-grad);
+ * dsgan_dwconv_multi_wgrad: dw_K += sum dy*x, db_K += sum dy, deterministic slot reduction in ws
+ * (dsgan_dwconv_multi_wgrad_workspace floats).  Supported: dsgan_dwconv_multi_supported != 0. */
+int dsgan_dwconv_multi_supported(int H, int W, const void* x, long x_bs, const void* y, long y_bs);
+int dsgan_dwconv_multi_fwd(const float* x, long x_bs, const float* w3, const float* b3, const float* w5,
+                           const float* b5, const float* w7, const float* b7, const float* w9, const float* b9,
+                           float* y, long y_bs, int N, int q, int H, int W, int flip, int accumulate,
+                           hipStream_t stream);
+long dsgan_dwconv_multi_wgrad_workspace(int N, int q, int H, int W);
+int dsgan_dwconv_multi_wgrad(const float* dy, long dy_bs, const float* x, long x_bs, float* dw3, float* db3,
+                             float* dw5, float* db5, float* dw7, float* db7, float* dw9, float* db9, int N, int q,
+                             int H, int W, float* ws, hipStream_t stream);
 int dsgan_dwconv_wgrad(const float* dy, long dy_bs, const float* x, long x_bs, float* dw,
                        float* db, int N, int C, int H, int W, int K, float* ws, hipStream_t stream);
 

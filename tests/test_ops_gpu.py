@@ -518,16 +518,22 @@ def test_mid_tail(C, H):
         assert rel(pd.grad, pr.grad) <= max(2 * rel(p32.grad, pr.grad), 1e-5)
 
 
-def test_multi_dwconv():
+@pytest.mark.parametrize("N,C,H,W", [(2, 16, 12, 12),      # per-quarter generic kernels
+                                     (2, 32, 32, 32),      # one launch per pass, cfg 3 (W = 32)
+                                     (2, 64, 64, 64),      # cfg 2 (W = 64)
+                                     (1, 32, 20, 128)])    # cfg 1 (W % 128 == 0), ragged rows
+def test_multi_dwconv(N, C, H, W):
+    """MidMLKA's four depthwise quarters (X3/X5/X7/X9) fwd + data-grad + weight/bias grads vs torch."""
     from dsgan_hip import functional as HF
-    g = torch.Generator().manual_seed(5)
-    x = torch.randn(2, 16, 12, 12, generator=g)
+    g = torch.Generator().manual_seed(5 + C + W)
+    x = torch.randn(N, C, H, W, generator=g)
+    q = C // 4
     ws = []
     for k in (3, 5, 7, 9):
-        ws += [torch.randn(4, 1, k, k, generator=g) / k, torch.randn(4, generator=g)]
+        ws += [torch.randn(q, 1, k, k, generator=g) / k, torch.randn(q, generator=g)]
     T = [t.clone().requires_grad_() for t in [x] + ws]
     parts = torch.chunk(T[0], 4, 1)
-    y_ref = torch.cat([F.conv2d(parts[i], T[1 + 2 * i], T[2 + 2 * i], padding=k // 2, groups=4)
+    y_ref = torch.cat([F.conv2d(parts[i], T[1 + 2 * i], T[2 + 2 * i], padding=k // 2, groups=q)
                        for i, k in enumerate((3, 5, 7, 9))], 1)
     gy = torch.randn(y_ref.shape, generator=g)
     y_ref.backward(gy)
