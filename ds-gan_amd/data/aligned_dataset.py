@@ -4,7 +4,15 @@ The host side decodes (PIL ``.convert('RGB')``), draws the crop offsets and the 
 python ``random`` in the reference's order (w_offset, h_offset, then ``random.random() < 0.5``
 unless --no_flip, :61-62, :74) and crops the uint8 image.  ToTensor / Normalize(0.5, 0.5) /
 flip / RGB->gray then run as one HIP kernel on the uploaded uint8 batch (``dsgan_u8_to_image``,
-bit-exact with the torch CPU ops), so a batch crosses PCIe as uint8 (4x fewer bytes)."""
+bit-exact with the torch CPU ops), so a batch crosses PCIe as uint8 (4x fewer bytes).
+
+Seeded data order is parity-PINNED only for serial, unshuffled loading (nThreads=0,
+serial_batches; tests/test_eval_gpu.py checks that path bit-exactly).  With worker processes
+(nThreads > 0) each worker's ``random`` is reseeded from torch's CPU base seed, and shuffling
+draws from the torch CPU generator, whose state after create_model differs from the
+reference's: torchvision's vgg16() also initialises its classifier from the global generator,
+which this build (conv holders only, ImageNet weights or a private-generator init) does not.
+So under seed 20 the shuffled order and the crop/flip draws are valid but parity-UNPINNED."""
 import os
 import random
 
