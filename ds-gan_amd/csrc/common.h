@@ -46,20 +46,63 @@ __device__ __forceinline__ float gelu_g(float x) {
   return cdf + x * (kInvSqrt2Pi * __expf(-0.5f * x * x));
 }
 
-// gelu(z) and gelu'(z) together for bf16 outputs: erfc by Abramowitz & Stegun 7.1.26
-// (|err| <= 1.5e-7, far below bf16 rounding); exp(-z^2/2) is shared by both.
+// GELU for bf16 outputs: he = erfc(|z|/sqrt2)/2 by Abramowitz & Stegun 7.1.26 (|err| <= 1.5e-7,
+// far below bf16 rounding), with the 1/sqrt2 folded into p and the 1/2 into the coefficients:
+// he = t (a1 + t (a2 + ...)) e, t = 1/(1 + p|z|/sqrt2), e = exp(-z^2/2) -- e is also the factor
+// GELU's derivative needs.  Returns q = he - 1/2 (in [-1/2, 0]); one rcp + one exp + 9 VALU.
+__device__ __forceinline__ float gelu_q(float z, float& e) {
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f * kInvSqrt2, fabsf(z), 1.f));
+  float p = fmaf(t, 0.5f * 1.061405429f, 0.5f * -1.453152027f);
+  p = fmaf(t, p, 0.5f * 1.421413741f);
+  p = fmaf(t, p, 0.5f * -0.284496736f);
+  p = fmaf(t, p, 0.5f * 0.254829592f);
+  e = __builtin_amdgcn_exp2f((z * z) * -0.72134752044448170368f);   // -log2(e)/2
+  return fmaf(t * p, e, -0.5f);
+}
+// gelu(z) = z Phi(z) = z/2 - |z| q   (z >= 0: z (1 - he); z < 0: z he)
+__device__ __forceinline__ float gelu_fast(float z) {
+  float e;
+  const float q = gelu_q(z, e);
+  return fmaf(-fabsf(z), q, 0.5f * z);
+}
+// gelu(z) and gelu'(z) = Phi(z) + z phi(z) together; Phi(z) = 1/2 - sign(z) q
 __device__ __forceinline__ void gelu_pair_fast(float z, float& g, float& gp) {
-  const float u = fabsf(z) * kInvSqrt2;
-  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, u, 1.f));
-  float p = fmaf(t, 1.061405429f, -1.453152027f);
-  p = fmaf(t, p, 1.421413741f);
-  p = fmaf(t, p, -0.284496736f);
-  p = fmaf(t, p, 0.254829592f);
-  const float e = __expf(-u * u);
-  const float he = 0.5f * t * p * e;
-  const float cdf = z >= 0.f ? 1.f - he : he;
+  float e;
+  const float q = gelu_q(z, e);
+  const float cdf = 0.5f + copysignf(-q, z);
   g = z * cdf;
   gp = fmaf(z * kInvSqrt2Pi, e, cdf);
+}
+
+// Two-element forms of the above on packed fp32 (v_pk_fma_f32 / v_pk_mul_f32 / v_pk_add_f32: one
+// wave instruction does both elements, so outside MFMA gaps they halve the VALU issue time of
+// the polynomial; rcp and exp stay per element).  Same operations per element, same results.
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f32x2 pk_fma(f32x2 a, f32x2 b, f32x2 c) { return __builtin_elementwise_fma(a, b, c); }
+__device__ __forceinline__ f32x2 gelu_nq2(f32x2 z, f32x2 az, f32x2& e) {   // -q = 1/2 - he >= 0
+  const f32x2 d = pk_fma(az, f32x2(0.3275911f * kInvSqrt2), f32x2(1.f));
+  const f32x2 t = {__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
+  f32x2 p = pk_fma(t, f32x2(-0.5f * 1.061405429f), f32x2(-0.5f * -1.453152027f));   // -(polynomial): exact
+  p = pk_fma(t, p, f32x2(-0.5f * 1.421413741f));
+  p = pk_fma(t, p, f32x2(-0.5f * -0.284496736f));
+  p = pk_fma(t, p, f32x2(-0.5f * 0.254829592f));
+  const f32x2 w = (z * z) * f32x2(-0.72134752044448170368f);
+  e = f32x2{__builtin_amdgcn_exp2f(w.x), __builtin_amdgcn_exp2f(w.y)};
+  return pk_fma(t * p, e, f32x2(0.5f));
+}
+__device__ __forceinline__ f32x2 gelu_fast2(f32x2 z) {
+  const f32x2 az = {fabsf(z.x), fabsf(z.y)};
+  f32x2 e;
+  const f32x2 nq = gelu_nq2(z, az, e);
+  return pk_fma(az, nq, f32x2(0.5f) * z);
+}
+__device__ __forceinline__ void gelu_pair_fast2(f32x2 z, f32x2& g, f32x2& gp) {
+  const f32x2 az = {fabsf(z.x), fabsf(z.y)};
+  f32x2 e;
+  const f32x2 nq = gelu_nq2(z, az, e);
+  const f32x2 cdf = f32x2(0.5f) + f32x2{copysignf(nq.x, z.x), copysignf(nq.y, z.y)};
+  g = z * cdf;
+  gp = pk_fma(z * f32x2(kInvSqrt2Pi), e, cdf);
 }
 
 __device__ __forceinline__ float act_f(int act, float x, float slope) {

@@ -49,32 +49,8 @@ __device__ __forceinline__ mbf16x4 mcvt4(float4 v) {
   return r;
 }
 
-// GELU for the bf16 path: erfc by Abramowitz & Stegun 7.1.26 (|err| <= 1.5e-7, far below the
-// bf16 rounding of the result), t = 1/(1 + p*u).  Its exp(-u^2) = exp(-z^2/2) is the same factor
-// GELU's derivative needs, so the pair costs one rcp + one exp + ~14 FMA-class ops (the exact
-// branch-free erf of common.h costs ~40).
-__device__ __forceinline__ float half_erfc_e(float z, float& e) {
-  const float u = fabsf(z) * kInvSqrt2;
-  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, u, 1.f));
-  float p = fmaf(t, 1.061405429f, -1.453152027f);
-  p = fmaf(t, p, 1.421413741f);
-  p = fmaf(t, p, -0.284496736f);
-  p = fmaf(t, p, 0.254829592f);
-  e = __expf(-u * u);
-  return 0.5f * t * p * e;
-}
-__device__ __forceinline__ float gelu_fast(float z) {
-  float e;
-  const float he = half_erfc_e(z, e);
-  return z * (z >= 0.f ? 1.f - he : he);
-}
-__device__ __forceinline__ void gelu_and_grad(float z, float& g, float& gp) {
-  float e;
-  const float he = half_erfc_e(z, e);
-  const float cdf = z >= 0.f ? 1.f - he : he;
-  g = z * cdf;
-  gp = fmaf(z * kInvSqrt2Pi, e, cdf);
-}
+// GELU of the bf16 path: gelu_fast2 / gelu_pair_fast2 (common.h, A&S 7.1.26 erfc on packed fp32,
+// two elements per instruction; the exact branch-free erf of gelu_f costs ~40 VALU per element).
 
 struct MlpArgs {
   const void* h; long h_bs;         // [nb][C][HW]   block activation after InstanceNorm (fp32, or bf16 if h_bf16)
@@ -203,8 +179,183 @@ struct WGrid {
 // ------------------------------------------------------------------------------------------
 // forward
 // ------------------------------------------------------------------------------------------
+// Hidden-row order of the forward's W1 chunk: rows 16a + 4b + e with quads b = 1 and 2 swapped.
+// Lane half h of a 32x32 accumulator holds rows 8q + 4h + e; with this order the rows it holds for
+// q = 2kk, 2kk+1 are the LOGICAL hidden units 16kk + 8h + (0..7) -- exactly the k slice of a B
+// fragment -- so gelu(z) feeds the second GEMM straight from registers against W2 in its natural
+// layout.  (An involution: the same map takes logical rows back to physical ones.)
+__device__ __forceinline__ int qswap(int r) { return (r & ~12) | ((r & 4) << 1) | ((r & 8) >> 1); }
+
+// XOR swizzle of the 16-byte slots of an unpadded LDS row of S slots, conflict-free for both
+// readers of these tiles: ds_read_b128 of one logical slot by 16 consecutive rows (16 distinct bank
+// groups), and ds_read_b64_tr_b16 of 4 consecutive slots (4-aligned) by 4 consecutive rows
+// (4-aligned; the 32 lanes then cover the 64 banks once).  256-byte+ rows (S >= 16): rows 4i..4i+3
+// take XOR masks 4(r & 3) + ((r >> 2) & 3).  128-byte rows (S = 8; two rows per bank window): the
+// two rows of equal parity among 4 consecutive ones differ by mask bit 2.
+template <int S>
+__device__ __forceinline__ int slot_swz(int r) {
+  return S >= 16 ? (((r & 3) << 2) | ((r >> 2) & 3)) : ((((r >> 1) & 1) << 2) | ((r >> 2) & 3));
+}
+
+// One 16-byte-per-lane LDS-DMA (global_load_lds_dwordx4): lane l's 16 bytes land at LDS byte
+// address lds + 16 l.  Issued from asm so that hipcc neither counts it nor drains it with a
+// vmcnt(0) in front of every LDS read of the other buffer: completion is waited for by hand
+// (s_waitcnt vmcnt + barrier before the buffer is read).  M0 is written and restored in the same
+// statement (it is compiler-reserved).
+__device__ __forceinline__ void glds16(const void* gsrc, unsigned lds) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(gsrc), "s"(lds)
+               : "memory");
+}
+__device__ __forceinline__ unsigned lds_addr(const void* p) {   // LDS byte offset of a __shared__ pointer
+  return __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)p);
+}
+
+// Weight chunk j -> LDS by LDS-DMA (no register staging): W1 rows [j*64, +64) as [64][C] (in qswap
+// row order when QS), W2 columns [j*64, +64) as [P][64].  Every wave issues C/64 + P/64 wave-instructions
+// of 1 KB each; the LDS image of one instruction is lane-linear, the swizzle is applied on the
+// per-lane global source address.
+template <int C, int P, int NW, bool QS = true>
+__device__ __forceinline__ void glds_chunk(__bf16* W1d, __bf16* W2d, const __bf16* __restrict__ w1,
+                                           const __bf16* __restrict__ w2, int j, int wave, int lane) {
+  constexpr int S1 = C / 8, R1 = 64 / S1, N1 = C / 8 / NW;
+#pragma unroll
+  for (int i = 0; i < N1; ++i) {
+    const int inst = wave * N1 + i, r = inst * R1 + lane / S1, ps = lane % S1;
+    const __bf16* src = w1 + ((long)j * 64 + (QS ? qswap(r) : r)) * C + (ps ^ slot_swz<S1>(r)) * 8;
+    glds16(src, lds_addr(W1d + inst * 512));
+  }
+  constexpr int N2 = P / 8 / NW;
+#pragma unroll
+  for (int i = 0; i < N2; ++i) {
+    const int inst = wave * N2 + i, r = inst * 8 + lane / 8, ps = lane % 8;
+    const __bf16* src = w2 + (long)r * (4 * C) + j * 64 + (ps ^ slot_swz<8>(r)) * 8;
+    glds16(src, lds_addr(W2d + inst * 512));
+  }
+}
+
+// 8 waves = 2 (hidden half wm of the 64-row chunk) x 4 (32-pixel column wn of the 128-pixel tile).
+// Each wave keeps the B fragments of its h columns (all C channels) in registers for the whole
+// tile, so per chunk LDS serves only the weight A fragments: z (32 x 32 per wave) = W1[chunk]
+// h + b1 on MFMA, gelu in registers (packed fp32), out[:, wn cols] += W2[:, wave's 32 hidden]
+// gelu(z) (see qswap).  The two hidden halves' partial outputs meet once, through LDS, in a fixed
+// order (acc[wm 0] + acc[wm 1]: deterministic).  Weight chunks are double-buffered and filled by
+// LDS-DMA one chunk ahead: one barrier per chunk.
+template <int C, int P, int MINB>
+__global__ __launch_bounds__(512, MINB) void mlp_fwd_kernel(MlpArgs g) {
+  constexpr int NW = 8, NT = NW * 64, BN = 128, HC = 64;
+  constexpr int C4 = 4 * C, NCH = C4 / HC, KS = C / 16, PT = P / 32;
+  constexpr int HSTR = BN + 32;
+  constexpr int H_SZ = C * HSTR, W_SZ = HC * C + P * HC, R_SZ = 2 * 4 * PT * 16 * 64;   // bf16 elements
+  constexpr int SM = H_SZ > 2 * W_SZ ? (H_SZ > R_SZ ? H_SZ : R_SZ) : (2 * W_SZ > R_SZ ? 2 * W_SZ : R_SZ);
+  __shared__ __attribute__((aligned(16))) __bf16 smem[SM + 2 * (C4 + P)];
+  float* b1s = reinterpret_cast<float*>(smem + SM);   // b1 [C4], then b2 [P]: no global load is in
+  float* b2s = b1s + C4;                              // flight in the loop besides the LDS-DMA
+  static_assert(C % 64 == 0 && P % 64 == 0 && NCH >= 2, "tile shape");
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int lr = lane & 31, lh = lane >> 5;
+  const int tq = (lane >> 2) & 3, tp = lane & 3, tG = (lane >> 4) & 1;
+  const int wm = wave >> 2, wn = wave & 3;
+
+  const int tpi = g.HW / BN;
+  const int tile = xcd_tile(blockIdx.x, gridDim.x);
+  const int img = tile / tpi, p0 = (tile - img * tpi) * BN;
+
+  stage_h<C, BN, HSTR, NT>(smem, g, img, p0, tid);
+  for (int i = tid; i < C4; i += NT) b1s[i] = g.b1[i];
+  for (int i = tid; i < P; i += NT) b2s[i] = g.b2 ? g.b2[i] : 0.f;
+  __syncthreads();
+  mbf16x8 hb[KS];
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks)
+    hb[ks] = mtr_frag(smem + (ks * 16 + 8 * lh + tq) * HSTR + wn * 32 + 16 * tG + 4 * tp, HSTR);
+  mf32x16 oacc[PT];
+#pragma unroll
+  for (int pt = 0; pt < PT; ++pt)
+#pragma unroll
+    for (int r = 0; r < 16; ++r)
+      oacc[pt][r] = wm == 0 ? b2s[pt * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh] : 0.f;
+  __syncthreads();   // the h staging area becomes the weight double buffer
+  glds_chunk<C, P, NW>(smem, smem + HC * C, g.w1, g.w2, 0, wave, lane);
+  glds_chunk<C, P, NW>(smem + W_SZ, smem + W_SZ + HC * C, g.w1, g.w2, 1, wave, lane);
+  constexpr int NI = C / 8 / NW + P / 8 / NW;   // LDS-DMA instructions per wave per chunk
+  asm volatile("s_waitcnt vmcnt(%0)" ::"i"(NI) : "memory");   // chunk 0 landed (chunk 1 may still fly)
+  __builtin_amdgcn_s_barrier();
+
+  for (int j = 0; j < NCH; ++j) {
+    const __bf16* W1c = smem + (j & 1) * W_SZ;
+    const __bf16* W2c = W1c + HC * C;
+    mf32x16 zacc;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {   // bias of physical rows wm*32 + 8q + 4lh + e (qswap order)
+      const float4 bv = *reinterpret_cast<const float4*>(b1s + j * HC + qswap(wm * 32 + 8 * q + 4 * lh));
+      zacc[4 * q] = bv.x; zacc[4 * q + 1] = bv.y; zacc[4 * q + 2] = bv.z; zacc[4 * q + 3] = bv.w;
+    }
+    const int r1 = wm * 32 + lr;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const mbf16x8 a =
+          *reinterpret_cast<const mbf16x8*>(W1c + r1 * C + ((ks * 2 + lh) ^ slot_swz<C / 8>(r1)) * 8);
+      zacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, hb[ks], zacc, 0, 0, 0);
+    }
+    // gelu of k slice kk -> its GEMM2 MFMAs (the second slice's VALU overlaps the first's MFMAs)
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      mbf16x8 gb;
+#pragma unroll
+      for (int i = 0; i < 8; i += 2) {
+        const f32x2 v = gelu_fast2(f32x2{zacc[8 * kk + i], zacc[8 * kk + i + 1]});
+        gb[i] = (__bf16)v.x;
+        gb[i + 1] = (__bf16)v.y;
+      }
+#pragma unroll
+      for (int pt = 0; pt < PT; ++pt) {
+        const int r2 = pt * 32 + lr;
+        const mbf16x8 a = *reinterpret_cast<const mbf16x8*>(
+            W2c + r2 * HC + ((wm * 4 + kk * 2 + lh) ^ slot_swz<8>(r2)) * 8);
+        oacc[pt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, gb, oacc[pt], 0, 0, 0);
+      }
+    }
+    // chunk j+1 landed (each wave waits for its own DMA; the barrier makes all of it visible) and
+    // every wave is done reading buffer j&1 -> refill it with chunk j+2
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (j + 2 < NCH) {
+      __bf16* W1n = smem + (j & 1) * W_SZ;
+      glds_chunk<C, P, NW>(W1n, W1n + HC * C, g.w1, g.w2, j + 2, wave, lane);
+    }
+  }
+
+  // ---- epilogue: wave (wm, wn) finishes the tiles pt with pt % 2 == wm and parks the others ----
+  float* red = reinterpret_cast<float*>(smem);   // [wn][pt][16][64]
+#pragma unroll
+  for (int pt = 0; pt < PT; ++pt)
+    if ((pt & 1) != wm)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) red[((wn * PT + pt) * 16 + r) * 64 + lane] = oacc[pt][r];
+  __syncthreads();
+  float* ob = g.out + (long)img * g.out_bs + p0 + wn * 32 + lr;
+#pragma unroll
+  for (int pt = 0; pt < PT; ++pt)
+    if ((pt & 1) == wm)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float o = red[((wn * PT + pt) * 16 + r) * 64 + lane];
+        const float v = wm == 0 ? oacc[pt][r] + o : o + oacc[pt][r];   // acc[wm 0] + acc[wm 1]
+        float* d = ob + (long)(pt * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh) * g.HW;
+        *d = g.accumulate ? *d + v : v;
+      }
+}
+
+// Forward for small C (C = 64: only 4 hidden chunks per tile, where the register-resident h of
+// mlp_fwd_kernel costs the second workgroup per CU): h staged once into LDS and read by every
+// chunk's GEMM1; gelu(z) goes through an LDS chunk buffer (aliasing the W1 chunk) to GEMM2; weight
+// chunks register-prefetched one chunk ahead.
 template <int C, int P, int BN, int HC, int NW, int MINB>
-__global__ __launch_bounds__(NW * 64, MINB) void mlp_fwd_kernel(MlpArgs g) {
+__global__ __launch_bounds__(NW * 64, MINB) void mlp_fwd_lds_kernel(MlpArgs g) {
   constexpr int NT = NW * 64;
   constexpr int C4 = 4 * C, NCH = C4 / HC;
   constexpr int HSTR = BN + 32, GSTR = HC + 8, W1STR = C + 8, W2STR = HC + 8;
@@ -290,7 +441,11 @@ __global__ __launch_bounds__(NW * 64, MINB) void mlp_fwd_kernel(MlpArgs g) {
         for (int q = 0; q < 4; ++q) {
           mbf16x4 v;
 #pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] = (__bf16)gelu_fast(zacc[i][t][4 * q + e]);
+          for (int e = 0; e < 4; e += 2) {
+            const f32x2 gv = gelu_fast2(f32x2{zacc[i][t][4 * q + e], zacc[i][t][4 * q + e + 1]});
+            v[e] = (__bf16)gv.x;
+            v[e + 1] = (__bf16)gv.y;
+          }
           *reinterpret_cast<mbf16x4*>(Gs + n * GSTR + wm * (HC / 2) + i * 32 + 8 * q + 4 * lh) = v;
         }
       }
@@ -332,6 +487,168 @@ __global__ __launch_bounds__(NW * 64, MINB) void mlp_fwd_kernel(MlpArgs g) {
         *o = g.accumulate ? *o + oacc[i][t][r] : oacc[i][t][r];
       }
     }
+}
+
+
+// Transposed 32x32x16 operand fragment of a swizzled [rows][S*8] LDS tile (k = row): lane (c, h)
+// receives T[k0 + 4h + i][col0 + c] (i < 4) and T[k0 + 8 + 4h + i - 4][col0 + c] (i >= 4) -- the k
+// order in which a 32x32 accumulator lane half holds rows 16kk + {4h + e, 8 + 4h + e}, so that
+// accumulator, converted, is the matching B fragment (see mlp_dh_kernel).
+template <int S>
+__device__ __forceinline__ mbf16x8 mtr_frag_q(const __bf16* T, int k0, int col0, int lane) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const int tq = (lane >> 2) & 3, tp = lane & 3, tG = (lane >> 4) & 1, h = lane >> 5;
+  const int col = col0 + 16 * tG + 4 * tp;
+  const int rlo = k0 + 4 * h + tq, rhi = rlo + 8;
+  const __bf16* plo = T + rlo * (S * 8) + (((col >> 3) ^ slot_swz<S>(rlo)) << 3) + (col & 7);
+  const __bf16* phi = T + rhi * (S * 8) + (((col >> 3) ^ slot_swz<S>(rhi)) << 3) + (col & 7);
+  ms16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_ms16x4*)(plo));
+  ms16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_ms16x4*)(phi));
+  typedef __attribute__((ext_vector_type(8))) short s16x8;
+  s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(mbf16x8, v);
+#else
+  return mbf16x8{};
+#endif
+}
+// Same, plain k order: lane (c, h) receives T[k0 + 8h + i][col0 + c], i = 0..7.
+template <int S>
+__device__ __forceinline__ mbf16x8 mtr_frag_s(const __bf16* T, int k0, int col0, int lane) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const int tq = (lane >> 2) & 3, tp = lane & 3, tG = (lane >> 4) & 1, h = lane >> 5;
+  const int col = col0 + 16 * tG + 4 * tp;
+  const int rlo = k0 + 8 * h + tq, rhi = rlo + 4;
+  const __bf16* plo = T + rlo * (S * 8) + (((col >> 3) ^ slot_swz<S>(rlo)) << 3) + (col & 7);
+  const __bf16* phi = T + rhi * (S * 8) + (((col >> 3) ^ slot_swz<S>(rhi)) << 3) + (col & 7);
+  ms16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_ms16x4*)(plo));
+  ms16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_ms16x4*)(phi));
+  typedef __attribute__((ext_vector_type(8))) short s16x8;
+  s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(mbf16x8, v);
+#else
+  return mbf16x8{};
+#endif
+}
+
+// ------------------------------------------------------------------------------------------
+// backward, data path only: dh = W1^T (W2^T dy * gelu'(W1 h + b1))
+// ------------------------------------------------------------------------------------------
+// Same decomposition as mlp_fwd_kernel: 8 waves = 2 hidden halves (wm) x 4 pixel columns (wn) of a
+// 128-pixel tile.  Each wave holds the B fragments of its h AND dy columns in registers; per
+// 64-row hidden chunk (weights double-buffered in LDS by LDS-DMA, natural order):
+//   z = W1 h + b1, t = W2^T dy (A fragments by row / transposed LDS reads), dz = t gelu'(z) in
+//   registers (packed fp32), dh[:, wn cols] += W1^T dz with dz as the B operand straight from the
+//   accumulators (mtr_frag_q reads W1 in the accumulator's k order).
+// The two hidden halves' partial dh meet once, through LDS, in a fixed order (deterministic).
+template <int C, int P, int MINB>
+__global__ __launch_bounds__(512, MINB) void mlp_dh_kernel(MlpArgs g) {
+  constexpr int NW = 8, NT = NW * 64, BN = 128, HC = 64;
+  constexpr int C4 = 4 * C, NCH = C4 / HC, KS = C / 16, PS = P / 16, CT = C / 32;
+  constexpr int HSTR = BN + 32;
+  constexpr int ST_SZ = (C + P) * HSTR, W_SZ = HC * C + P * HC, R_SZ = 2 * 4 * CT * 16 * 64;   // bf16 elements
+  constexpr int SM = ST_SZ > 2 * W_SZ ? (ST_SZ > R_SZ ? ST_SZ : R_SZ) : (2 * W_SZ > R_SZ ? 2 * W_SZ : R_SZ);
+  __shared__ __attribute__((aligned(16))) __bf16 smem[SM + 2 * C4];
+  float* b1s = reinterpret_cast<float*>(smem + SM);
+  static_assert(C % 64 == 0 && P % 64 == 0 && NCH >= 2, "tile shape");
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int lr = lane & 31, lh = lane >> 5;
+  const int tq = (lane >> 2) & 3, tp = lane & 3, tG = (lane >> 4) & 1;
+  const int wm = wave >> 2, wn = wave & 3;
+
+  const int tpi = g.HW / BN;
+  const int tile = xcd_tile(blockIdx.x, gridDim.x);
+  const int img = tile / tpi, p0 = (tile - img * tpi) * BN;
+
+  __bf16* Hs = smem;
+  __bf16* Ds = smem + C * HSTR;
+  stage_h<C, BN, HSTR, NT>(Hs, g, img, p0, tid);
+  stage_rows<P, BN, HSTR, NT>(Ds, g.dy + (long)img * g.dy_bs + p0, g.HW, tid);
+  for (int i = tid; i < C4; i += NT) b1s[i] = g.b1[i];
+  __syncthreads();
+  mbf16x8 hb[KS], db[PS];
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks)
+    hb[ks] = mtr_frag(Hs + (ks * 16 + 8 * lh + tq) * HSTR + wn * 32 + 16 * tG + 4 * tp, HSTR);
+#pragma unroll
+  for (int ks = 0; ks < PS; ++ks)
+    db[ks] = mtr_frag(Ds + (ks * 16 + 8 * lh + tq) * HSTR + wn * 32 + 16 * tG + 4 * tp, HSTR);
+  mf32x16 hacc[CT];
+#pragma unroll
+  for (int ct = 0; ct < CT; ++ct)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) hacc[ct][r] = 0.f;
+  __syncthreads();   // the staging area becomes the weight double buffer
+  glds_chunk<C, P, NW, false>(smem, smem + HC * C, g.w1, g.w2, 0, wave, lane);
+  glds_chunk<C, P, NW, false>(smem + W_SZ, smem + W_SZ + HC * C, g.w1, g.w2, 1, wave, lane);
+  constexpr int NI = C / 8 / NW + P / 8 / NW;
+  asm volatile("s_waitcnt vmcnt(%0)" ::"i"(NI) : "memory");
+  __builtin_amdgcn_s_barrier();
+
+  for (int j = 0; j < NCH; ++j) {
+    const __bf16* W1c = smem + (j & 1) * W_SZ;
+    const __bf16* W2c = W1c + HC * C;
+    mf32x16 zacc, tacc;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float4 bv = *reinterpret_cast<const float4*>(b1s + j * HC + wm * 32 + 8 * q + 4 * lh);
+      zacc[4 * q] = bv.x; zacc[4 * q + 1] = bv.y; zacc[4 * q + 2] = bv.z; zacc[4 * q + 3] = bv.w;
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) tacc[r] = 0.f;
+    const int r1 = wm * 32 + lr;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const mbf16x8 a =
+          *reinterpret_cast<const mbf16x8*>(W1c + r1 * C + ((ks * 2 + lh) ^ slot_swz<C / 8>(r1)) * 8);
+      zacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, hb[ks], zacc, 0, 0, 0);
+    }
+#pragma unroll
+    for (int ks = 0; ks < PS; ++ks) {   // A[m = hidden][k = p] = W2[p][hidden]: transposed read of W2c
+      const mbf16x8 a = mtr_frag_s<8>(W2c, ks * 16, wm * 32, lane);
+      tacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, db[ks], tacc, 0, 0, 0);
+    }
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      mbf16x8 dzb;
+#pragma unroll
+      for (int i = 0; i < 8; i += 2) {
+        f32x2 gv, gp;
+        gelu_pair_fast2(f32x2{zacc[8 * kk + i], zacc[8 * kk + i + 1]}, gv, gp);
+        const f32x2 dz = f32x2{tacc[8 * kk + i], tacc[8 * kk + i + 1]} * gp;
+        dzb[i] = (__bf16)dz.x;
+        dzb[i + 1] = (__bf16)dz.y;
+      }
+#pragma unroll
+      for (int ct = 0; ct < CT; ++ct) {   // A[m = c][k = hidden] = W1[hidden][c], in dz's k order
+        const mbf16x8 a = mtr_frag_q<C / 8>(W1c, wm * 32 + 16 * kk, ct * 32, lane);
+        hacc[ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, dzb, hacc[ct], 0, 0, 0);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (j + 2 < NCH) {
+      __bf16* W1n = smem + (j & 1) * W_SZ;
+      glds_chunk<C, P, NW, false>(W1n, W1n + HC * C, g.w1, g.w2, j + 2, wave, lane);
+    }
+  }
+
+  float* red = reinterpret_cast<float*>(smem);   // [wn][ct][16][64]
+#pragma unroll
+  for (int ct = 0; ct < CT; ++ct)
+    if ((ct & 1) != wm)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) red[((wn * CT + ct) * 16 + r) * 64 + lane] = hacc[ct][r];
+  __syncthreads();
+  float* ob = g.out + (long)img * g.out_bs + p0 + wn * 32 + lr;
+#pragma unroll
+  for (int ct = 0; ct < CT; ++ct)
+    if ((ct & 1) == wm)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float o = red[((wn * CT + ct) * 16 + r) * 64 + lane];
+        ob[(long)(ct * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh) * g.HW] = wm == 0 ? hacc[ct][r] + o : o + hacc[ct][r];
+      }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -444,11 +761,12 @@ __global__ __launch_bounds__(NW * 64, MINB) void mlp_bwd_kernel(MlpArgs g) {
         for (int q = 0; q < 4; ++q) {
           mbf16x4 gv4, dv4;
 #pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            float gv, gp;
-            gelu_and_grad(zacc[i][t][4 * q + e], gv, gp);
-            gv4[e] = (__bf16)gv;
-            dv4[e] = (__bf16)(tacc[i][t][4 * q + e] * gp);
+          for (int e = 0; e < 4; e += 2) {
+            f32x2 gv, gp;
+            gelu_pair_fast2(f32x2{zacc[i][t][4 * q + e], zacc[i][t][4 * q + e + 1]}, gv, gp);
+            const f32x2 dz = f32x2{tacc[i][t][4 * q + e], tacc[i][t][4 * q + e + 1]} * gp;
+            gv4[e] = (__bf16)gv.x; gv4[e + 1] = (__bf16)gv.y;
+            dv4[e] = (__bf16)dz.x; dv4[e + 1] = (__bf16)dz.y;
           }
           const int m = wm * (HC / 2) + i * 32 + 8 * q + 4 * lh;
           if constexpr (GD) *reinterpret_cast<mbf16x4*>(Gn + n * NSTR + m) = gv4;
@@ -691,12 +1009,14 @@ __global__ __launch_bounds__(NW * 64, MINB) void mlp_wgrad_kernel(MlpArgs g) {
         for (int q = 0; q < 4; ++q) {
           mbf16x4 gv4, dv4;
 #pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            float gv, gp;
-            gelu_and_grad(zacc[i][t][4 * q + e], gv, gp);
-            gv4[e] = (__bf16)gv;
-            dv4[e] = (__bf16)(tacc[i][t][4 * q + e] * gp);
+          for (int e = 0; e < 4; e += 2) {
+            f32x2 gv, gp;
+            gelu_pair_fast2(f32x2{zacc[i][t][4 * q + e], zacc[i][t][4 * q + e + 1]}, gv, gp);
+            const f32x2 dz = f32x2{tacc[i][t][4 * q + e], tacc[i][t][4 * q + e + 1]} * gp;
+            gv4[e] = (__bf16)gv.x; gv4[e + 1] = (__bf16)gv.y;
+            dv4[e] = (__bf16)dz.x; dv4[e + 1] = (__bf16)dz.y;
             bacc[i][4 * q + e] += (float)dv4[e];
+            bacc[i][4 * q + e + 1] += (float)dv4[e + 1];
           }
           const int m = wm * (HC / 2) + i * 32 + 8 * q + 4 * lh;
           *reinterpret_cast<mbf16x4*>(Gn + n * NSTR + m) = gv4;
@@ -806,9 +1126,14 @@ static int mlp_bn(int C, int P) {
 constexpr int MLP_NW = 8;
 
 template <int C, int P, int BN, int MINB>
-static void fwd_launch(const MlpArgs& g, hipStream_t st) {
+static void fwd_lds_launch(const MlpArgs& g, hipStream_t st) {
   const unsigned tiles = (unsigned)((long)g.nb * (g.HW / BN));
-  hipLaunchKernelGGL((mlp_fwd_kernel<C, P, BN, 64, MLP_NW, MINB>), dim3(tiles), dim3(MLP_NW * 64), 0, st, g);
+  hipLaunchKernelGGL((mlp_fwd_lds_kernel<C, P, BN, 64, MLP_NW, MINB>), dim3(tiles), dim3(MLP_NW * 64), 0, st, g);
+}
+template <int C, int P, int MINB>
+static void fwd_launch(const MlpArgs& g, hipStream_t st) {
+  const unsigned tiles = (unsigned)((long)g.nb * (g.HW / 128));
+  hipLaunchKernelGGL((mlp_fwd_kernel<C, P, MINB>), dim3(tiles), dim3(512), 0, st, g);
 }
 // backward: 8 waves x 128 pixels where the LDS tiles fit, else 4 waves x 64 pixels (same bsum
 // granularity: one partial row per 32 pixels)
@@ -863,10 +1188,11 @@ int dsgan_mlp_fwd(const void* h, long h_bs, int h_bf16, const void* w1, const fl
   MlpArgs g{};
   g.h = h; g.h_bs = h_bs; g.w1 = (const __bf16*)w1; g.b1 = b1; g.w2 = (const __bf16*)w2; g.b2 = b2;
   g.out = out; g.out_bs = out_bs; g.HW = HW; g.nb = nb; g.accumulate = accumulate; g.h_bf16 = h_bf16;
-  if (C == 64) fwd_launch<64, 128, 128, 2>(g, st);
-  else if (C == 128 && P == 64) fwd_launch<128, 64, 128, 2>(g, st);
-  else if (C == 128) fwd_launch<128, 256, 128, 1>(g, st);
-  else fwd_launch<256, 128, 128, 1>(g, st);
+  // MINB = waves per SIMD: 4 (two workgroups per CU) where 128 registers hold
+  if (C == 64) fwd_lds_launch<64, 128, 128, 2>(g, st);
+  else if (C == 128 && P == 64) fwd_launch<128, 64, 4>(g, st);
+  else if (C == 128) fwd_launch<128, 256, 2>(g, st);
+  else fwd_launch<256, 128, 2>(g, st);
   DSG_CHECK_LAUNCH();
   return 0;
 }
@@ -884,9 +1210,10 @@ int dsgan_mlp_bwd(const void* h, long h_bs, int h_bf16, const float* dy, long dy
   g.h = h; g.h_bs = h_bs; g.dy = dy; g.dy_bs = dy_bs; g.w1 = (const __bf16*)w1; g.b1 = b1;
   g.w2 = (const __bf16*)w2; g.out = dh; g.out_bs = dh_bs; g.g_out = (__bf16*)g_out;
   g.dz_out = (__bf16*)dz_out; g.bsum = bsum; g.HW = HW; g.nb = nb; g.h_bf16 = h_bf16;
-  if (!g_out) {   // dh only: 64-pixel tiles, two workgroups per CU where the LDS allows
-    if (C == 64) bwd_launch<64, 128, 64, 4, false, 2>(g, st);
-    else if (C == 128 && P == 64) bwd_launch<128, 64, 64, 4, false, 2>(g, st);
+  if (!g_out) {   // dh only: the register-chained kernel where h, dy and dh fragments fit in registers
+    const unsigned tiles = (unsigned)((long)g.nb * (g.HW / 128));
+    if (C == 64) hipLaunchKernelGGL((mlp_dh_kernel<64, 128, 2>), dim3(tiles), dim3(512), 0, st, g);
+    else if (C == 128 && P == 64) hipLaunchKernelGGL((mlp_dh_kernel<128, 64, 2>), dim3(tiles), dim3(512), 0, st, g);
     else if (C == 128) bwd_launch<128, 256, 64, 4, false, 1>(g, st);
     else bwd_launch<256, 128, 64, 4, false, 1>(g, st);
   } else if (C == 64) bwd_launch<64, 128, 128, 8>(g, st);

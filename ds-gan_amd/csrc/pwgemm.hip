@@ -435,16 +435,27 @@ __global__ __launch_bounds__(128 * WN, WN == 2 ? 2 : 1) void pwgemm_kernel(PwArg
       }
       bool acted = false;
       if (g.ypre && g.gbf) {          // FWD: ypre <- bf16 act'(pre), v <- act(pre) (one GELU evaluation)
+        float apv[16];
+        if (g.act == ACT_GELU) {
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          float a, ap;
-          if (g.act == ACT_GELU) gelu_pair_fast(v[r], a, ap);
-          else { a = act_f(g.act, v[r], g.slope); ap = act_g(g.act, v[r], g.slope); }
-          v[r] = a;
-          __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(unsigned short, (__bf16)ap), rp,
+          for (int r = 0; r < 16; r += 2) {
+            f32x2 a, ap;
+            gelu_pair_fast2(f32x2{v[r], v[r + 1]}, a, ap);
+            v[r] = a.x; v[r + 1] = a.y;
+            apv[r] = ap.x; apv[r + 1] = ap.y;
+          }
+        } else {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            apv[r] = act_g(g.act, v[r], g.slope);
+            v[r] = act_f(g.act, v[r], g.slope);
+          }
+        }
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(unsigned short, (__bf16)apv[r]), rp,
                                                 vrow[r] == (int)PW_OOB ? (int)PW_OOB : vrow[r] / 2,
                                                 (mrow + (r & 3) + 8 * (r >> 2)) * (P4 / 2), 0);
-        }
         acted = true;
       } else if (g.ypre) {
 #pragma unroll

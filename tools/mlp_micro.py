@@ -1,15 +1,21 @@
-"""Time the fused MLP kernels (mlp.hip) and the bf16 weight-grads at the DS-GAN block shapes."""
+"""Time the fused MLP kernels (mlp.hip) at the DS-GAN block shapes, as the training step calls them
+(bf16 h from the block's InstanceNorm): forward, backward dh-only + weight-grad kernel, and the
+backward with bf16 g / dz written for the pwgemm weight-grads.
+
+    python tools/mlp_micro.py            # DSGAN_HIP_LIB=<other .so> to time another build
+"""
 import os, sys
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [REPO, os.path.join(REPO, "ds-gan_amd")]
 import torch
 from dsgan_hip._lib import call, ptr, stream
 import dsgan_hip
-from dsgan_hip import functional as HF
 
 dsgan_hip.require_gpu()
 N = 16
 SHAPES = [("uc4", 128, 64, 256), ("uc3", 256, 128, 128), ("c2", 64, 128, 128), ("c3", 128, 256, 64)]
+if os.environ.get("MLP_SHAPES"):
+    SHAPES = [s for s in SHAPES if s[0] in os.environ["MLP_SHAPES"].split(",")]
 
 
 def timeit(fn, it=20):
@@ -22,31 +28,38 @@ def timeit(fn, it=20):
     return e0.elapsed_time(e1) / it
 
 
+lib = dsgan_hip._lib.load()
+print("lib:", os.environ.get("DSGAN_HIP_LIB", "default"), flush=True)
 for name, C, P, H in SHAPES:
     HW = H * H
     C4 = 4 * C
-    h = torch.randn(N, C, H, H, device="cuda")
+    torch.manual_seed(0)
+    h = torch.randn(N, C, H, H, device="cuda").bfloat16()
     dy = torch.randn(N, P, H, H, device="cuda")
     out = torch.zeros(N, P, H, H, device="cuda")
     w1 = (torch.randn(C4, C, device="cuda") / C ** 0.5).bfloat16()
     w2 = (torch.randn(P, C4, device="cuda") / C4 ** 0.5).bfloat16()
     b1 = torch.randn(C4, device="cuda") * 0.1
     b2 = torch.randn(P, device="cuda") * 0.1
-    tile = dsgan_hip._lib.load().dsgan_mlp_supported(C, P, HW)
     g = torch.empty(N, C4, H, H, device="cuda", dtype=torch.bfloat16)
     dz = torch.empty_like(g)
-    bsum = torch.empty(N * HW // tile, C4, device="cuda")
-    dh = torch.empty_like(h)
-    gw2 = torch.zeros(P, C4, device="cuda")
-    gw1 = torch.zeros(C4, C, device="cuda")
-    f = lambda: call("dsgan_mlp_fwd", ptr(h), C * HW, 0, ptr(w1), ptr(b1), ptr(w2), ptr(b2), ptr(out), P * HW, N, C, P, HW, 1, stream())
-    b = lambda: call("dsgan_mlp_bwd", ptr(h), C * HW, 0, ptr(dy), P * HW, ptr(w1), ptr(b1), ptr(w2), ptr(dh), C * HW,
-                     ptr(g), ptr(dz), ptr(bsum), N, C, P, HW, stream())
-    w2g = lambda: call("dsgan_pw_wgrad_mixed", ptr(dy), P * HW, 0, ptr(g), C4 * HW, 1, ptr(gw2), P, C4, HW, N, ptr(HF._pw_ws(P, C4, HW, N, dy)), stream())
-    w1g = lambda: call("dsgan_pw_wgrad_mixed", ptr(dz), C4 * HW, 1, ptr(h), C * HW, 0, ptr(gw1), C4, C, HW, N, ptr(HF._pw_ws(C4, C, HW, N, dz)), stream())
-    tf, tb, t2, t1 = timeit(f), timeit(b), timeit(w2g), timeit(w1g)
+    dh = torch.empty(N, C, H, H, device="cuda")
+    gw1, gb1, gw2 = torch.zeros(C4, C, device="cuda"), torch.zeros(C4, device="cuda"), torch.zeros(P, C4, device="cuda")
+    wsp = torch.empty(lib.dsgan_mlp_wgrad_workspace(C, P, HW, N), device="cuda")
+    f = lambda: call("dsgan_mlp_fwd", ptr(h), C * HW, 1, ptr(w1), ptr(b1), ptr(w2), ptr(b2), ptr(out), P * HW, N, C, P,
+                     HW, 1, stream())
+    bd = lambda: call("dsgan_mlp_bwd", ptr(h), C * HW, 1, ptr(dy), P * HW, ptr(w1), ptr(b1), ptr(w2), ptr(dh), C * HW,
+                      None, None, None, N, C, P, HW, stream())
+    wg = lambda: call("dsgan_mlp_wgrad", ptr(h), C * HW, 1, ptr(dy), P * HW, ptr(w1), ptr(b1), ptr(w2), ptr(gw1),
+                      ptr(gb1), ptr(gw2), ptr(wsp), N, C, P, HW, stream())
+    bg = lambda: call("dsgan_mlp_bwd", ptr(h), C * HW, 1, ptr(dy), P * HW, ptr(w1), ptr(b1), ptr(w2), ptr(dh), C * HW,
+                      ptr(g), ptr(dz), None, N, C, P, HW, stream())
+    tf, tbd, twg, tbg = timeit(f), timeit(bd), timeit(wg), timeit(bg)
+    # checksums so that two builds can be compared for identical results
+    f(); bd(); wg(); torch.cuda.synchronize()
+    cs = (out.double().sum().item(), dh.double().sum().item(), gw1.double().abs().sum().item(),
+          gw2.double().abs().sum().item(), gb1.double().abs().sum().item())
     fl = 2.0 * N * HW * (C4 * C + C4 * P)
-    byf = N * HW * (C + 2 * P) * 4
-    byb = N * HW * ((C + P + C) * 4 + 2 * C4 * 2)
-    print("%-4s C=%4d P=%4d HW=%6d | fwd %.3f ms (%.0f TF/s, %.0f GB/s) | bwd %.3f ms (%.0f GB/s) | wg2 %.3f wg1 %.3f ms"
-          % (name, C, P, HW, tf, fl / tf / 1e9, byf / tf / 1e6, tb, byb / tb / 1e6, t2, t1), flush=True)
+    print("%-4s C=%4d P=%4d HW=%6d | fwd %.3f ms (%.0f TF/s) | bwd-dh %.3f | wgrad %.3f | bwd-g/dz %.3f ms | cs %s"
+          % (name, C, P, HW, tf, fl / tf / 1e9, tbd, twg, tbg, " ".join("%.6e" % c for c in cs)), flush=True)
+    del h, dy, out, g, dz, dh, wsp

@@ -13,12 +13,16 @@ Derived per family (per launch averages; MI355X_MICROARCH.md § rocprofv3 PMC sl
 """
 import collections
 import json
+import os
 import re
 import sqlite3
 import sys
 
 
 def fam(name):
+    if os.environ.get("PMC_BY") == "name":   # one row per template instance
+        m = re.search(r"dsg::(\w+?_kernel<[^(]*>)", name)
+        return m.group(1) if m else None
     m = re.search(r"dsg::(\w+?_kernel|\w+)(<|\()", name)
     return m.group(1) if m else None
 
@@ -56,6 +60,10 @@ def main():
             for k in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY"):
                 if k in r:
                     r[k.lower().replace("sq_", "") + "_frac"] = r[k] / w
+        if "SQ_ACTIVE_INST_VALU" in r and g:   # quad-cycles summed over waves -> share of SIMD-cycles
+            r["valu_busy"] = 4.0 * r["SQ_ACTIVE_INST_VALU"] / (1024.0 * g / 8.0)
+        if "SQ_VALU_MFMA_COEXEC_CYCLES" in r and g:
+            r["coexec"] = r["SQ_VALU_MFMA_COEXEC_CYCLES"] / (1024.0 * g / 8.0)
         if r.get("SQ_LDS_IDX_ACTIVE"):
             r["lds_conflict_frac"] = r.get("SQ_LDS_BANK_CONFLICT", 0.0) / r["SQ_LDS_IDX_ACTIVE"]
         res[f] = {k: (round(v, 4) if isinstance(v, float) else v) for k, v in sorted(r.items())}
@@ -64,9 +72,10 @@ def main():
     order = sorted(res, key=lambda f: -res[f]["dur_us"] * res[f]["launches"])
     for f in order[:20]:
         r = res[f]
-        print("%-26s n=%4d %8.1fus clk=%s mfma_busy=%s cyc/mfma=%s wait=%s inst=%s lds_cf=%s" % (
+        print("%-26s n=%4d %8.1fus clk=%s mfma_busy=%s cyc/mfma=%s wait=%s inst=%s lds_cf=%s valu=%s coexec=%s" % (
             f, r["launches"], r["dur_us"], r.get("clock_ghz"), r.get("mfma_busy"), r.get("mfma_cyc_per_inst"),
-            r.get("wait_any_frac"), r.get("wait_inst_any_frac"), r.get("lds_conflict_frac")))
+            r.get("wait_any_frac"), r.get("wait_inst_any_frac"), r.get("lds_conflict_frac"), r.get("valu_busy"),
+            r.get("coexec")))
 
 
 if __name__ == "__main__":
