@@ -24,7 +24,7 @@ FLAGS = ["-O3", "-fPIC", "-std=c++17", "--offload-arch=" + ARCH, "-munsafe-fp-at
 
 
 # per-source extra flags
-EXTRA = {"dwconv.hip": ["-fno-slp-vectorize"], "mlp.hip": ["-fno-slp-vectorize"]}
+EXTRA = {"dwconv.hip": ["-fno-slp-vectorize"], "mlp.hip": ["-fno-slp-vectorize"], "thin3.hip": ["-fno-slp-vectorize"]}
 
 
 def _newer(src, obj, headers):

@@ -68,6 +68,12 @@ SIGNATURES = {
     "dsgan_conv_small_in": [P, L, P, L, L, L, L, P, P, L] + [I] * 13 + [F, I, S],
     "dsgan_conv_wgrad_small_workspace": [I] * 7,
     "dsgan_conv_wgrad_small": [P, L, P, L, P] + [I] * 11 + [P, S],
+    # thin3.hip
+    "dsgan_thin3_supported": [I, I, I, L, L],
+    "dsgan_thin3_fwd": [P, L, P, P, P, L] + [I] * 6 + [S],
+    "dsgan_thin3_wgrad_workspace": [I] * 5,
+    "dsgan_thin3_wgrad": [P, L, P, L, P, P] + [I] * 5 + [S],
+    "dsgan_thin3_dgrad": [P, L, P, P, L] + [I] * 6 + [S],
     # dwconv.hip
     "dsgan_dwconv_fwd": [P, L, P, P, P, L, I, I, I, I, I, I, I, S],
     "dsgan_dwconv_wgrad_workspace": [I, I, I, I, I, I],

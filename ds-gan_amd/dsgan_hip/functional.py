@@ -249,6 +249,12 @@ def _pws_ok(K, M, P, xbs, ybs, x, y):
             and bool(_lib.load().dsgan_pw_small_supported(K, M, P, xbs, ybs)))
 
 
+def _thin3_ok(M, H, W, bs_small, bs_big, t_small, t_big):
+    """3x3 / s1 / p1 conv with <= 4 channels on one side at W % 256 == 0 (thin3.hip)."""
+    return (t_small.data_ptr() % 16 == 0 and t_big.data_ptr() % 16 == 0
+            and bool(_lib.load().dsgan_thin3_supported(M, H, W, bs_small, bs_big)))
+
+
 def _pconv_ok(K, KH, KW, stride):
     return _state["prec"] == "bf16" and bool(_lib.load().dsgan_pconv_supported(K, KH, KW, stride))
 
@@ -273,7 +279,13 @@ def conv_fwd_raw(x, w, b, stride, pad, act=None, out=None, pre=None, accumulate=
         pre, pbs = nchw(pre)
     e0 = IGEMM_TIMER.begin()
     fam = "igemm_kernel"
-    if KH == 1 and KW == 1 and stride == 1 and pad == 0 and pre is None and _pws_ok(Cin, Cout, H * W, xbs, ybs, x, y):
+    if (KH == 3 and KW == 3 and stride == 1 and pad == 1 and act is None and pre is None and xact is None
+            and w.is_contiguous() and _thin3_ok(Cout, H, W, ybs, xbs, y, x)):
+        # 3x3 into <= 4 channels at full resolution (the G head): row-strip fp32 stream
+        fam = "thin3_kernel"
+        call("dsgan_thin3_fwd", ptr(x), xbs, ptr(w), ptr(b), ptr(y), ybs, N, Cin, Cout, H, W, int(accumulate),
+             stream())
+    elif KH == 1 and KW == 1 and stride == 1 and pad == 0 and pre is None and _pws_ok(Cin, Cout, H * W, xbs, ybs, x, y):
         # 1x1 with <= 16 channels on one side (the 3/12-channel layers at 256^2): VALU stream
         fam = "pw_small_kernel"
         call("dsgan_pw_small", ptr(x), xbs, ptr(w), Cin, 1, ptr(b), ptr(y), ybs, None, 0, N, Cin, Cout, H * W,
@@ -331,7 +343,11 @@ def conv_dgrad_raw(dy, w, x_shape, stride, pad, bias=None, act=None, gpre=None, 
         gpre, gbs = nchw(gpre)
     e0 = IGEMM_TIMER.begin()
     fam = "igemm_kernel"
-    if (KH == 1 and KW == 1 and stride == 1 and pad == 0 and act is None and bias is None
+    if (KH == 3 and KW == 3 and stride == 1 and pad == 1 and act is None and bias is None and gpre is None
+            and w.is_contiguous() and _thin3_ok(Cout, H, W, dybs, dxbs, dy, dx)):
+        fam = "thin3_kernel"
+        call("dsgan_thin3_dgrad", ptr(dy), dybs, ptr(w), ptr(dx), dxbs, N, Cin, Cout, H, W, int(accumulate), stream())
+    elif (KH == 1 and KW == 1 and stride == 1 and pad == 0 and act is None and bias is None
             and _pws_ok(Cout, Cin, H * W, dybs, dxbs, dy, dx) and (gpre is None or (gbs % 4 == 0 and gpre.data_ptr() % 16 == 0))):
         fam = "pw_small_kernel"
         call("dsgan_pw_small", ptr(dy), dybs, ptr(w), 1, Cin, None, ptr(dx), dxbs, ptr(gpre), gbs, N, Cout, Cin, H * W,
@@ -412,7 +428,13 @@ def conv_wgrad_raw(dy, x, dw, stride, pad, xact=None, db=None):
     KH, KW = (dw.shape[2], dw.shape[3]) if dw.dim() == 4 else (1, 1)
     e0 = IGEMM_TIMER.begin()
     fam = "igemm_kernel"
-    if xact is None and KH * KW in (1, 9, 16) and (Cout <= 8 or (Cin <= 8 and KH * KW == 1)):
+    if (xact is None and KH == 3 and KW == 3 and stride == 1 and pad == 1 and dw.is_contiguous()
+            and _thin3_ok(Cout, H, W, dybs, xbs, dy, x)):
+        fam = "thin3_kernel"
+        ws = torch.empty(_lib.load().dsgan_thin3_wgrad_workspace(N, Cin, Cout, H, W), device=dy.device,
+                         dtype=torch.float32)
+        call("dsgan_thin3_wgrad", ptr(dy), dybs, ptr(x), xbs, ptr(dw), ptr(ws), N, Cin, Cout, H, W, stream())
+    elif xact is None and KH * KW in (1, 9, 16) and (Cout <= 8 or (Cin <= 8 and KH * KW == 1)):
         fam = "wgrad_small_kernel"
         nws = _lib.load().dsgan_conv_wgrad_small_workspace(N, Cin, Cout, KH, KW, dy.shape[2], dy.shape[3])
         ws = torch.empty(nws, device=dy.device, dtype=torch.float32) if nws > 0 else None

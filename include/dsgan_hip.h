@@ -167,6 +167,23 @@ int dsgan_conv_wgrad_small(const float* dy, long dy_bs, const float* x, long x_b
                            int Cin, int H, int W, int Cout, int KH, int KW, int stride, int pad, int Ho,
                            int Wo, float* ws, hipStream_t stream);
 
+/* ---- thin 3x3 / stride 1 / pad 1 convs at full resolution (thin3.hip, exact fp32) ----------
+ * The G head res = nn.Conv2d(64, 3, 3, padding=1) (DSGAN/models/model/MixConvNeXtML.py:459, applied
+ * at :492): forward, weight-grad and data-grad.  M (the small side) 1..4, H % 4 == 0, W % 256 == 0,
+ * 16-byte aligned planes (dsgan_thin3_supported).  w / dw are [M][K][3][3].
+ *   fwd  : y[nb][M][H][W] (+)= bias + conv(x[nb][K][H][W]);
+ *   wgrad: dw += sum over pixels (dy [nb][M][H][W], x [nb][K][H][W]); per-split partials in ws
+ *          (dsgan_thin3_wgrad_workspace floats) summed in a fixed order: deterministic;
+ *   dgrad: dx[nb][K][H][W] (+)= data-grad from dy [nb][M][H][W]. */
+int dsgan_thin3_supported(int M, int H, int W, long bs_small, long bs_big);
+int dsgan_thin3_fwd(const float* x, long x_bs, const float* w, const float* bias, float* y, long y_bs, int nb, int K,
+                    int M, int H, int W, int accumulate, hipStream_t stream);
+long dsgan_thin3_wgrad_workspace(int nb, int K, int M, int H, int W);
+int dsgan_thin3_wgrad(const float* dy, long dy_bs, const float* x, long x_bs, float* dw, float* ws, int nb, int K,
+                      int M, int H, int W, hipStream_t stream);
+int dsgan_thin3_dgrad(const float* dy, long dy_bs, const float* w, float* dx, long dx_bs, int nb, int K, int M, int H,
+                      int W, int accumulate, hipStream_t stream);
+
 /* ---- tap-major implicit-GEMM conv for channel counts % 32 == 0 (tconv.hip, bf16 MFMA) -------
  * out[b][m][dst(o)] = act(sum_{tap,k} Wt[tap][m][k] * X[b][k][o*stride + (dh,dw)[tap]] + bias[m])
  *                     (* gact'(gpre) if gpre); dst(o) = (oh*os+ph, ow*os+pw) in Hdst x Wdst.

@@ -65,6 +65,9 @@ def _q(t, prec):
     (2, 3, 64, 64, 32, 1, 1, 0),       # to32 (wgrad with Cin = 3)
     (2, 6, 66, 66, 64, 4, 2, 1),       # PatchGAN layer 0 (stride-2 data-grad into 6 channels)
     (2, 1024, 96, 96, 1024, 1, 1, 0),  # wide, deep 1x1 fwd + data-grad: 256-row M tiles (K >= 1024)
+    (2, 64, 8, 256, 3, 3, 1, 1),       # G head at full width: thin3.hip row strips (act=None)
+    (1, 33, 12, 512, 4, 3, 1, 1),      # thin3: two 256-column segments per row, M = 4, odd K
+    (2, 9, 4, 256, 1, 3, 1, 1),        # thin3: M = 1
 ])
 def test_conv2d(prec, N, Cin, H, W, Cout, K, s, p):
     from dsgan_hip import functional as HF
@@ -841,3 +844,33 @@ def test_pw_fwd_io_bf16_outputs(w_bf16, x_bf16, M, K, P, nb):
     for got, ref in ((y, ref_g), (gp, ref_gp)):
         got = got.double()
         assert ((got - ref.cuda()).abs() <= ref.cuda().abs() * 2 ** -7 + 1e-3).all()
+
+
+@pytest.mark.parametrize("N,K,M,H,W", [(2, 64, 3, 8, 256), (1, 20, 2, 4, 512)])
+def test_thin3_accumulate_and_strides(N, K, M, H, W):
+    """thin3.hip fwd / dgrad accumulate into (and read) channel slices of larger buffers."""
+    from dsgan_hip import functional as HF
+    HF.set_precision("fp32")
+    g = torch.Generator().manual_seed(K * 7 + M)
+    xb = torch.randn(N, K + 4, H, W, generator=g)          # x = channels 4.. of a bigger tensor
+    x = xb[:, 4:]
+    w = torch.randn(M, K, 3, 3, generator=g) / math.sqrt(9 * K)
+    b = torch.randn(M, generator=g)
+    y0 = torch.randn(N, M + 2, H, W, generator=g)
+    y = y0.to(DEV)
+    HF.conv_fwd_raw(xb.to(DEV)[:, 4:], w.to(DEV), b.to(DEV), 1, 1, out=y[:, 1:1 + M], accumulate=True)
+    ref = y0.clone()
+    ref[:, 1:1 + M] += F.conv2d(x, w, b, padding=1)
+    assert rel(y, ref) < 1e-5
+    dy = torch.randn(N, M, H, W, generator=g)
+    dx0 = torch.randn(N, K + 4, H, W, generator=g)
+    dx = dx0.to(DEV)
+    HF.conv_dgrad_raw(dy.to(DEV), w.to(DEV), (N, K, H, W), 1, 1, out=dx[:, 4:], accumulate=True)
+    refx = dx0.clone()
+    refx[:, 4:] += torch.nn.grad.conv2d_input((N, K, H, W), w, dy, padding=1)
+    assert rel(dx, refx) < 1e-5
+    dw = torch.randn(M, K, 3, 3, generator=g)
+    dwd = dw.to(DEV)
+    HF.conv_wgrad_raw(dy.to(DEV), xb.to(DEV)[:, 4:], dwd, 1, 1)
+    refw = dw + torch.nn.grad.conv2d_weight(x, (M, K, 3, 3), dy, padding=1)
+    assert rel(dwd, refw) < 1e-5
