@@ -326,6 +326,68 @@ __global__ __launch_bounds__(256) void wgrad_small_kernel(WsArgs a) {
   }
 }
 
+// 1x1 / stride 1 form of the above (the 3-channel-input 1x1 convs at 256^2: the c1 shortcut and
+// pwconv1, the local branch's to32; MixConvNeXtML.py:124,145,221): a thread walks pixel QUADS with
+// 16-byte loads (dy of the workgroup's channel once, the small side's <= S planes), four products
+// per FMA chain step -- a quarter of the load instructions of the pixel-per-thread walk.
+template <int S, bool SMALL_OUT>
+__global__ __launch_bounds__(256) void wgrad_small_pw4_kernel(WsArgs a) {
+  __shared__ float red[4][S];
+  const int c = blockIdx.x;
+  const int HW = a.Ho * a.Wo;
+  const long total = (long)a.nb * HW;
+  const long p0 = (long)blockIdx.y * a.pix_per_block;
+  const long p1 = min(total, p0 + a.pix_per_block);
+  const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc((void*)a.x, (short)0, a.x_range, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rg = __builtin_amdgcn_make_buffer_rsrc((void*)a.dy, (short)0, a.dy_range, 0x00020000);
+  auto ld4 = [](__amdgpu_buffer_rsrc_t r, unsigned off) {
+    return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 0));
+  };
+  float acc[S];
+#pragma unroll
+  for (int s = 0; s < S; ++s) acc[s] = 0.f;
+  // (b, r) of this thread's first quad, then advanced by 1024 pixels per step (HW % 4 == 0)
+  long p = p0 + 4 * threadIdx.x;
+  int b = (int)(p / HW), r = (int)(p - (long)b * HW);
+  for (; p < p1; p += 1024) {
+    const unsigned xb = (unsigned)((long)b * a.x_bs) + r, gb = (unsigned)((long)b * a.dy_bs) + r;
+    if (SMALL_OUT) {
+      const float4 xv = ld4(rx, (xb + (unsigned)c * HW) * 4u);
+#pragma unroll
+      for (int s = 0; s < S; ++s) {
+        if (s >= a.nsmall) break;
+        const float4 g = ld4(rg, (gb + (unsigned)s * HW) * 4u);
+        acc[s] = fmaf(g.x, xv.x, fmaf(g.y, xv.y, fmaf(g.z, xv.z, fmaf(g.w, xv.w, acc[s]))));
+      }
+    } else {
+      const float4 g = ld4(rg, (gb + (unsigned)c * HW) * 4u);
+#pragma unroll
+      for (int s = 0; s < S; ++s) {
+        if (s >= a.nsmall) break;
+        const float4 xv = ld4(rx, (xb + (unsigned)s * HW) * 4u);
+        acc[s] = fmaf(g.x, xv.x, fmaf(g.y, xv.y, fmaf(g.z, xv.z, fmaf(g.w, xv.w, acc[s]))));
+      }
+    }
+    r += 1024;
+    while (r >= HW) { r -= HW; ++b; }
+  }
+  const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
+#pragma unroll
+  for (int s = 0; s < S; ++s) {
+    if (s >= a.nsmall) break;
+    const float v = warp_sum(acc[s]);
+    if (ln == 0) red[wv][s] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x < a.nsmall) {
+    const int s = threadIdx.x;
+    const float v = red[0][s] + red[1][s] + red[2][s] + red[3][s];
+    const long o = SMALL_OUT ? (long)s * a.Cin + c : (long)c * a.Cin + s;
+    if (a.ws) a.ws[(long)blockIdx.y * a.Cout * a.Cin + o] = v;
+    else a.dw[o] += v;
+  }
+}
+
 // pixel chunks of a small weight-grad (gridDim.y): ~2048 workgroups, >= 16 pixels per thread
 static long ws_chunks(int big, long total, long* ppb_out) {
   long chunks = (2048 + big - 1) / big;
@@ -448,6 +510,22 @@ int dsgan_conv_wgrad_small(const float* dy, long dy_bs, const float* x, long x_b
   DSG_REQUIRE(chunks == 1 || ws, "dsgan_conv_wgrad_small: needs dsgan_conv_wgrad_small_workspace floats of scratch");
   a.ws = chunks > 1 ? ws : nullptr;
   const bool s4 = a.nsmall <= 4;
+  if (T == 1 && stride == 1 && pad == 0 && Ho == H && Wo == W && (Ho * Wo) % 4 == 0 && (x_bs & 3) == 0 &&
+      (dy_bs & 3) == 0 && ((uintptr_t)x & 15) == 0 && ((uintptr_t)dy & 15) == 0) {
+    // pixel-quad walk: chunks of whole 1024-pixel steps (never more chunks than the workspace has)
+    const long ppb4 = (ppb + 1023) / 1024 * 1024;
+    const long chunks4 = ((long)N * Ho * Wo + ppb4 - 1) / ppb4;
+    a.pix_per_block = ppb4;
+    a.ws = chunks4 > 1 ? ws : nullptr;
+    const dim3 grid((unsigned)big, (unsigned)chunks4);
+    if (so) { if (s4) hipLaunchKernelGGL((wgrad_small_pw4_kernel<4, true>), grid, dim3(256), 0, st, a);
+              else hipLaunchKernelGGL((wgrad_small_pw4_kernel<8, true>), grid, dim3(256), 0, st, a); }
+    else { if (s4) hipLaunchKernelGGL((wgrad_small_pw4_kernel<4, false>), grid, dim3(256), 0, st, a);
+           else hipLaunchKernelGGL((wgrad_small_pw4_kernel<8, false>), grid, dim3(256), 0, st, a); }
+    if (chunks4 > 1) launch_split_reduce(ws, (int)chunks4, (long)Cout * Cin, dw, st);
+    DSG_CHECK_LAUNCH();
+    return 0;
+  }
 #define WS_CASE(TT)                                                                    \
   if (T == TT) {                                                                       \
     if (so) { if (s4) ws_launch<4, TT, true>(a, big, (int)chunks, st); else ws_launch<8, TT, true>(a, big, (int)chunks, st); } \
