@@ -57,81 +57,88 @@ __global__ __launch_bounds__(256) void small_out_kernel(SkArgs a) {
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int HWo = a.Ho * a.Wo;
   const long total = (long)a.nb * HWo;
-  long q = (long)blockIdx.x * 64 + lane;
-  const bool qv = q < total;
-  if (!qv) q = 0;
-  const int b = (int)(q / HWo), r = (int)(q - (long)b * HWo);
-  const int oh = r / a.Wo, ow = r - (r / a.Wo) * a.Wo;
-  const int HWi = a.Hin * a.Win;
-  const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc((void*)a.x, (short)0, a.x_range, 0x00020000);
-  const unsigned xb = (unsigned)((long)b * a.x_bs);
+  // the staged weights serve a grid-stride run of 64-pixel blocks (staging them per block cost
+  // more L2 traffic than the activations when K*T*MS is large: 16 KB per 64 pixels for the
+  // PatchGAN conv-0 data-grad)
+  for (long blk = blockIdx.x; blk * 64 < total; blk += gridDim.x) {
+    long q = blk * 64 + lane;
+    const bool qv = q < total;
+    if (!qv) q = 0;
+    const int b = (int)(q / HWo), r = (int)(q - (long)b * HWo);
+    const int oh = r / a.Wo, ow = r - (r / a.Wo) * a.Wo;
+    const int HWi = a.Hin * a.Win;
+    const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc((void*)a.x, (short)0, a.x_range, 0x00020000);
+    const unsigned xb = (unsigned)((long)b * a.x_bs);
 
-  // per-tap in-plane offsets (or OOB), independent of k
-  constexpr int TMAX = PAR ? 4 : (KH_ ? KH_ * KW_ : 1);
-  unsigned toff[TMAX];
-  int tsel[TMAX];                               // weight tap of each slot (PAR: per lane)
-  auto tap_off = [&](int kh, int kw) -> unsigned {
-    int ih, iw; bool ok;
-    if (!a.transposed) {
-      ih = oh * a.stride - a.pad + kh; iw = ow * a.stride - a.pad + kw;
-      ok = ((unsigned)ih < (unsigned)a.Hin) & ((unsigned)iw < (unsigned)a.Win);
-    } else {
-      const int th = oh + a.pad - kh, tw = ow + a.pad - kw;
-      ih = a.stride == 1 ? th : (th >> 1); iw = a.stride == 1 ? tw : (tw >> 1);
-      ok = (th >= 0) & (tw >= 0) & ((a.stride == 1) | !((th | tw) & 1)) & (ih < a.Hin) & (iw < a.Win);
-    }
-    return ok ? (unsigned)(ih * a.Win + iw) : 0x3FFFFFF0u;
-  };
-  if (PAR) {
-    const int kh0 = (oh + a.pad) & 1, kw0 = (ow + a.pad) & 1;
+    // per-tap in-plane offsets (or OOB), independent of k
+    constexpr int TMAX = PAR ? 4 : (KH_ ? KH_ * KW_ : 1);
+    unsigned toff[TMAX];
+    int tsel[TMAX];                               // weight tap of each slot (PAR: per lane)
+    auto tap_off = [&](int kh, int kw) -> unsigned {
+      int ih, iw; bool ok;
+      if (!a.transposed) {
+        ih = oh * a.stride - a.pad + kh; iw = ow * a.stride - a.pad + kw;
+        ok = ((unsigned)ih < (unsigned)a.Hin) & ((unsigned)iw < (unsigned)a.Win);
+      } else {
+        const int th = oh + a.pad - kh, tw = ow + a.pad - kw;
+        ih = a.stride == 1 ? th : (th >> 1); iw = a.stride == 1 ? tw : (tw >> 1);
+        ok = (th >= 0) & (tw >= 0) & ((a.stride == 1) | !((th | tw) & 1)) & (ih < a.Hin) & (iw < a.Win);
+      }
+      return ok ? (unsigned)(ih * a.Win + iw) : 0x3FFFFFF0u;
+    };
+    if (PAR) {
+      const int kh0 = (oh + a.pad) & 1, kw0 = (ow + a.pad) & 1;
 #pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      const int kh = kh0 + 2 * (t >> 1), kw = kw0 + 2 * (t & 1);
-      toff[t] = tap_off(kh, kw);
-      tsel[t] = kh * KW_ + kw;
-    }
-  } else if (KH_) {
+      for (int t = 0; t < 4; ++t) {
+        const int kh = kh0 + 2 * (t >> 1), kw = kw0 + 2 * (t & 1);
+        toff[t] = tap_off(kh, kw);
+        tsel[t] = kh * KW_ + kw;
+      }
+    } else if (KH_) {
 #pragma unroll
-    for (int t = 0; t < TMAX; ++t) { toff[t] = tap_off(t / KW_, t % KW_); tsel[t] = t; }
-  }
+      for (int t = 0; t < TMAX; ++t) { toff[t] = tap_off(t / KW_, t % KW_); tsel[t] = t; }
+    }
 
-  float acc[MS];
+    float acc[MS];
 #pragma unroll
-  for (int m = 0; m < MS; ++m) acc[m] = 0.f;
-  for (int k = wave; k < a.K; k += 4) {
-    const unsigned xk = xb + (unsigned)k * HWi;
-    const float* wk = wsm + k * T * MS;
-    if (KH_) {
-      float xv[TMAX];
+    for (int m = 0; m < MS; ++m) acc[m] = 0.f;
+    for (int k = wave; k < a.K; k += 4) {
+      const unsigned xk = xb + (unsigned)k * HWi;
+      const float* wk = wsm + k * T * MS;
+      if (KH_) {
+        float xv[TMAX];
 #pragma unroll
-      for (int t = 0; t < TMAX; ++t) xv[t] = bld(rx, toff[t] >= 0x3FFFFFF0u ? SK_OOB : (xk + toff[t]) * 4u);
+        for (int t = 0; t < TMAX; ++t) xv[t] = bld(rx, toff[t] >= 0x3FFFFFF0u ? SK_OOB : (xk + toff[t]) * 4u);
 #pragma unroll
-      for (int t = 0; t < TMAX; ++t)
+        for (int t = 0; t < TMAX; ++t)
 #pragma unroll
-        for (int m = 0; m < MS; ++m) acc[m] = fmaf(wk[tsel[t] * MS + m], xv[t], acc[m]);
-    } else {
-      for (int t = 0; t < T; ++t) {
-        const unsigned o = tap_off(t / KW, t % KW);
-        const float xv = bld(rx, o >= 0x3FFFFFF0u ? SK_OOB : (xk + o) * 4u);
+          for (int m = 0; m < MS; ++m) acc[m] = fmaf(wk[tsel[t] * MS + m], xv[t], acc[m]);
+      } else {
+        for (int t = 0; t < T; ++t) {
+          const unsigned o = tap_off(t / KW, t % KW);
+          const float xv = bld(rx, o >= 0x3FFFFFF0u ? SK_OOB : (xk + o) * 4u);
 #pragma unroll
-        for (int m = 0; m < MS; ++m) acc[m] = fmaf(wk[t * MS + m], xv, acc[m]);
+          for (int m = 0; m < MS; ++m) acc[m] = fmaf(wk[t * MS + m], xv, acc[m]);
+        }
       }
     }
-  }
-  if (wave > 0) {
+    if (wave > 0) {
 #pragma unroll
-    for (int m = 0; m < MS; ++m) part[wave - 1][m][lane] = acc[m];
-  }
-  __syncthreads();
-  if (wave > 0 || !qv) return;
-  float* yp = a.y + (long)b * a.y_bs + r;
+      for (int m = 0; m < MS; ++m) part[wave - 1][m][lane] = acc[m];
+    }
+    __syncthreads();
+    if (wave == 0 && qv) {
+      float* yp = a.y + (long)b * a.y_bs + r;
 #pragma unroll
-  for (int m = 0; m < MS; ++m) {
-    if (m >= a.M) break;
-    float v = ((acc[m] + part[0][m][lane]) + part[1][m][lane]) + part[2][m][lane];
-    if (a.bias) v += a.bias[m];
-    if (a.accumulate) v += yp[(long)m * HWo];
-    yp[(long)m * HWo] = v;
+      for (int m = 0; m < MS; ++m) {
+        if (m >= a.M) break;
+        float v = ((acc[m] + part[0][m][lane]) + part[1][m][lane]) + part[2][m][lane];
+        if (a.bias) v += a.bias[m];
+        if (a.accumulate) v += yp[(long)m * HWo];
+        yp[(long)m * HWo] = v;
+      }
+    }
+    __syncthreads();   // part[] is rewritten by the next block
   }
 }
 
@@ -430,7 +437,7 @@ int dsgan_conv_small_out(const float* x, long x_bs, const float* w, long wm, lon
   a.accumulate = accumulate;
   const long pblocks = ((long)nb * Ho * Wo + 63) / 64;
   DSG_REQUIRE(pblocks < (1L << 31), "dsgan_conv_small_out: too many pixels");
-  const dim3 grid((unsigned)pblocks);
+  const dim3 grid((unsigned)(pblocks < 2048 ? pblocks : 2048));   // grid-stride over pixel blocks
   const int MSr = M == 1 ? 1 : (M <= 4 ? 4 : 8);
   const size_t lds = (size_t)K * KH * KW * MSr * 4;
   DSG_REQUIRE(lds <= 64 * 1024, "dsgan_conv_small_out: K*KH*KW*M too large for the LDS weight stage");
