@@ -60,8 +60,12 @@ __global__ __launch_bounds__(256) void small_out_kernel(SkArgs a) {
   // the staged weights serve a grid-stride run of 64-pixel blocks (staging them per block cost
   // more L2 traffic than the activations when K*T*MS is large: 16 KB per 64 pixels for the
   // PatchGAN conv-0 data-grad)
-  for (long blk = blockIdx.x; blk * 64 < total; blk += gridDim.x) {
-    long q = blk * 64 + lane;
+  // K <= 64: each wave owns its own 64 pixels over all K (no cross-wave combine or barrier per
+  // block); larger K: the four waves split the channels of one 64-pixel block.
+  const bool own = a.K <= 64;
+  const int PB = own ? 256 : 64;
+  for (long blk = blockIdx.x; blk * PB < total; blk += gridDim.x) {
+    long q = blk * PB + (own ? wave * 64 : 0) + lane;
     const bool qv = q < total;
     if (!qv) q = 0;
     const int b = (int)(q / HWo), r = (int)(q - (long)b * HWo);
@@ -102,7 +106,7 @@ __global__ __launch_bounds__(256) void small_out_kernel(SkArgs a) {
     float acc[MS];
 #pragma unroll
     for (int m = 0; m < MS; ++m) acc[m] = 0.f;
-    for (int k = wave; k < a.K; k += 4) {
+    for (int k = own ? 0 : wave; k < a.K; k += own ? 1 : 4) {
       const unsigned xk = xb + (unsigned)k * HWi;
       const float* wk = wsm + k * T * MS;
       if (KH_) {
@@ -121,6 +125,20 @@ __global__ __launch_bounds__(256) void small_out_kernel(SkArgs a) {
           for (int m = 0; m < MS; ++m) acc[m] = fmaf(wk[t * MS + m], xv, acc[m]);
         }
       }
+    }
+    if (own) {
+      if (qv) {
+        float* yp = a.y + (long)b * a.y_bs + r;
+#pragma unroll
+        for (int m = 0; m < MS; ++m) {
+          if (m >= a.M) break;
+          float v = acc[m];
+          if (a.bias) v += a.bias[m];
+          if (a.accumulate) v += yp[(long)m * HWo];
+          yp[(long)m * HWo] = v;
+        }
+      }
+      continue;   // (uniform over the workgroup)
     }
     if (wave > 0) {
 #pragma unroll
@@ -437,7 +455,8 @@ int dsgan_conv_small_out(const float* x, long x_bs, const float* w, long wm, lon
   a.accumulate = accumulate;
   const long pblocks = ((long)nb * Ho * Wo + 63) / 64;
   DSG_REQUIRE(pblocks < (1L << 31), "dsgan_conv_small_out: too many pixels");
-  const dim3 grid((unsigned)(pblocks < 2048 ? pblocks : 2048));   // grid-stride over pixel blocks
+  const long wblocks = K <= 64 ? (pblocks + 3) / 4 : pblocks;       // 256-pixel blocks when K <= 64
+  const dim3 grid((unsigned)(wblocks < 2048 ? wblocks : 2048));    // grid-stride over pixel blocks
   const int MSr = M == 1 ? 1 : (M <= 4 ? 4 : 8);
   const size_t lds = (size_t)K * KH * KW * MSr * 4;
   DSG_REQUIRE(lds <= 64 * 1024, "dsgan_conv_small_out: K*KH*KW*M too large for the LDS weight stage");
