@@ -86,7 +86,9 @@ __global__ __launch_bounds__(256) void pw_small_kernel(PsArgs a) {
 
 // K <= 16 input channels: the thread's 4 pixels x K inputs are loaded (and xact applied) once,
 // then every output channel is one K-term dot product stored immediately.
-template <int KC>
+// ACC / GP: accumulate into Y / multiply by gact'(G) (compile-time, so the plain forward carries
+// no registers for the preloaded operands of either).
+template <int KC, bool ACC, bool GP>
 __global__ __launch_bounds__(256) void pw_small_k_kernel(PsArgs a) {
   __shared__ __attribute__((aligned(16))) float wl[PS_MAXM * KC];   // [m][KC] (W then W2 columns)
   for (int e = threadIdx.x; e < a.M * KC; e += 256) {
@@ -100,7 +102,7 @@ __global__ __launch_bounds__(256) void pw_small_k_kernel(PsArgs a) {
     const int b = (int)(q / P4), p = (int)(q - (long)b * P4) * 4;
     const float* xb = a.X + (long)b * a.x_bs + p;
     float* yb = a.Y + (long)b * a.y_bs + p;
-    const float* gb = a.G ? a.G + (long)b * a.g_bs + p : nullptr;
+    const float* gb = GP ? a.G + (long)b * a.g_bs + p : nullptr;
     // inputs: K channels of X (xact applied when there is no X2), then K2 channels of X2 (xact)
     float4 xs[KC];
     const float* x2b = a.X2 ? a.X2 + (long)b * a.x2_bs + p : nullptr;
@@ -118,12 +120,12 @@ __global__ __launch_bounds__(256) void pw_small_k_kernel(PsArgs a) {
     // output channels in chunks of 8: the chunk's accumulate / act' operands are loaded up front
     // so their latencies overlap (a load after the previous channel's store could alias it)
     for (int m0 = 0; m0 < a.M; m0 += 8) {
-      float4 old[8], gv[8];
+      float4 old[ACC ? 8 : 1], gv[GP ? 8 : 1];
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
         const int m = m0 + i < a.M ? m0 + i : a.M - 1;
-        old[i] = a.accumulate ? *reinterpret_cast<const float4*>(yb + (long)m * a.P) : make_float4(0.f, 0.f, 0.f, 0.f);
-        gv[i] = gb ? *reinterpret_cast<const float4*>(gb + (long)m * a.P) : make_float4(0.f, 0.f, 0.f, 0.f);
+        if (ACC) old[i] = *reinterpret_cast<const float4*>(yb + (long)m * a.P);
+        if (GP) gv[i] = *reinterpret_cast<const float4*>(gb + (long)m * a.P);
       }
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
@@ -139,11 +141,11 @@ __global__ __launch_bounds__(256) void pw_small_k_kernel(PsArgs a) {
         }
         if (a.act) { v.x = act_f(a.act, v.x, a.slope); v.y = act_f(a.act, v.y, a.slope);
                      v.z = act_f(a.act, v.z, a.slope); v.w = act_f(a.act, v.w, a.slope); }
-        if (gb) {
+        if constexpr (GP) {
           v.x *= act_g(a.gact, gv[i].x, a.slope); v.y *= act_g(a.gact, gv[i].y, a.slope);
           v.z *= act_g(a.gact, gv[i].z, a.slope); v.w *= act_g(a.gact, gv[i].w, a.slope);
         }
-        v.x += old[i].x; v.y += old[i].y; v.z += old[i].z; v.w += old[i].w;
+        if constexpr (ACC) { v.x += old[i].x; v.y += old[i].y; v.z += old[i].z; v.w += old[i].w; }
         *reinterpret_cast<float4*>(yb + (long)m * a.P) = v;
       }
     }
@@ -194,8 +196,17 @@ int dsgan_pw_small2(const float* X, long x_bs, const float* W, int wm, int wk, c
   const long total = (long)nb * (P / 4);
   long blocks = (total + 255) / 256;
   if (blocks > 16384) blocks = 16384;
-  if (Kt <= 4) hipLaunchKernelGGL((pw_small_k_kernel<4>), dim3((unsigned)blocks), dim3(256), 0, st, a);
-  else if (Kt <= 16) hipLaunchKernelGGL((pw_small_k_kernel<16>), dim3((unsigned)blocks), dim3(256), 0, st, a);
+  const int sel = (accumulate ? 1 : 0) + (G ? 2 : 0);
+#define PSK(KC_)                                                                                        \
+  switch (sel) {                                                                                        \
+    case 0: hipLaunchKernelGGL((pw_small_k_kernel<KC_, false, false>), dim3((unsigned)blocks), dim3(256), 0, st, a); break; \
+    case 1: hipLaunchKernelGGL((pw_small_k_kernel<KC_, true, false>), dim3((unsigned)blocks), dim3(256), 0, st, a); break;  \
+    case 2: hipLaunchKernelGGL((pw_small_k_kernel<KC_, false, true>), dim3((unsigned)blocks), dim3(256), 0, st, a); break;  \
+    default: hipLaunchKernelGGL((pw_small_k_kernel<KC_, true, true>), dim3((unsigned)blocks), dim3(256), 0, st, a); break;  \
+  }
+  if (Kt <= 4) { PSK(4) }
+  else if (Kt <= 16) { PSK(16) }
+#undef PSK
   else if (M <= 4) hipLaunchKernelGGL((pw_small_kernel<4>), dim3((unsigned)blocks), dim3(256), 0, st, a);
   else hipLaunchKernelGGL((pw_small_kernel<16>), dim3((unsigned)blocks), dim3(256), 0, st, a);
   DSG_CHECK_LAUNCH();

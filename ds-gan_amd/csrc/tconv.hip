@@ -39,6 +39,7 @@ struct TcArgs {
   int dh[T_MAXTAPS], dw[T_MAXTAPS];   // input offset of each tap: ih = oh*stride + dh
   int Hdst, Wdst, os, ph, pw;          // dst pixel = (oh*os + ph, ow*os + pw)
   int act, gact; float slope;
+  float* ws; int kchunk;               // split-K (ws != NULL): raw partials [split][nb][M][Hout*Wout]
 };
 
 template <int BM>
@@ -65,7 +66,8 @@ __global__ __launch_bounds__(256, 2) void tconv_kernel(TcArgs g) {
     const int xcd = id & 7, q = nwg >> 3, r = nwg & 7;
     tile = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (id >> 3);
   }
-  const int m_t = tile % mt, rest = tile / mt;
+  const int m_t = tile % mt, rest0 = tile / mt;
+  const int nn = g.nb * ntpi, split = rest0 / nn, rest = rest0 - split * nn;
   const int bimg = rest / ntpi, nt_i = rest - bimg * ntpi;
   const int m0 = m_t * BM, q0 = nt_i * BN;
 
@@ -83,11 +85,14 @@ __global__ __launch_bounds__(256, 2) void tconv_kernel(TcArgs g) {
   const int ih0 = oh * g.stride, iw0 = ow * g.stride;
 
   const int ksteps_per_tap = g.K / TBK;
-  const int nk = g.ntaps * ksteps_per_tap;
+  const int nk_all = g.ntaps * ksteps_per_tap;
+  const int kb0 = g.ws ? split * g.kchunk : 0;
+  const int nk = g.ws ? min(g.kchunk, nk_all - kb0) : nk_all;   // K steps of this split
 
   float4 ra[A_ITEMS];
   float rb[16];
-  auto gload = [&](int kt) {
+  auto gload = [&](int kt0) {
+    const int kt = kb0 + kt0;
     const int tap = kt / ksteps_per_tap;
     const int k0 = (kt - tap * ksteps_per_tap) * TBK;
     // A rows past M get an offset past the resource range (reads 0, no branch)
@@ -127,7 +132,7 @@ __global__ __launch_bounds__(256, 2) void tconv_kernel(TcArgs g) {
   };
 
   tf32x16 acc[TM][TN];
-  const bool has_bias = g.bias != nullptr;
+  const bool has_bias = g.bias != nullptr && !g.ws;   // split-K: the bias is added by the reduce
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
     float bv[16];
@@ -174,6 +179,22 @@ __global__ __launch_bounds__(256, 2) void tconv_kernel(TcArgs g) {
     __syncthreads();
   }
 
+  if (g.ws) {   // split-K partial: rows m, pixel-contiguous along the lanes (coalesced)
+    float* wp = g.ws + ((long)split * g.nb + bimg) * g.M * Pout;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int qq = q0 + wn * TN * 32 + j * 32 + lr;
+      if (qq >= Pout) continue;
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int m = m0 + wm * TM * 32 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+          if (m < g.M) wp[(long)m * Pout + qq] = acc[i][j][r];
+        }
+    }
+    return;
+  }
   // ---- epilogue: dst pixel of this lane's column, channel rows via scalar offsets ----
   const int HWd = g.Hdst * g.Wdst;
   const unsigned range = (unsigned)((long)g.M * HWd * 4);
@@ -218,6 +239,36 @@ __global__ __launch_bounds__(256, 2) void tconv_kernel(TcArgs g) {
   }
 }
 
+// Split-K finish: y[b][m][dst(q)] = act( sum_s ws[s][b][m][q] + bias[m] ) (* gact'(gpre)),
+// splits added in a fixed order (deterministic).
+__global__ __launch_bounds__(256) void tconv_reduce_kernel(TcArgs g, int S) {
+  const int Pout = g.Hout * g.Wout, HWd = g.Hdst * g.Wdst;
+  const long per = (long)g.nb * g.M * Pout;
+  for (long e = blockIdx.x * 256L + threadIdx.x; e < per; e += (long)gridDim.x * 256) {
+    float v = 0.f;
+    for (int s = 0; s < S; ++s) v += g.ws[(long)s * per + e];
+    const int q = (int)(e % Pout);
+    const long bm = e / Pout;
+    const int m = (int)(bm % g.M), b = (int)(bm / g.M);
+    if (g.bias) v += g.bias[m];
+    const int oh = q / g.Wout, ow = q - oh * g.Wout;
+    const long d = (long)m * HWd + (long)(oh * g.os + g.ph) * g.Wdst + ow * g.os + g.pw;
+    if (g.gpre) v *= act_g(g.gact, g.gpre[(long)b * g.gpre_bs + d], g.slope);
+    g.Y[(long)b * g.y_bs + d] = act_f(g.act, v, g.slope);
+  }
+}
+
+// K split of a launch whose tiles leave the chip under-filled (the deep ConvT data-grads: 256
+// tiles of 144 K steps at 16^2): about 1024 workgroups, >= 16 K steps each.
+static int tc_splits(long tiles, int nk, int* kchunk) {
+  long S = (1024 + tiles - 1) / tiles;
+  if (S > nk / 16) S = nk / 16;
+  if (tiles >= 512 || S < 2) { *kchunk = nk; return 1; }
+  const int kc = (int)((nk + S - 1) / S);
+  *kchunk = kc;
+  return (nk + kc - 1) / kc;
+}
+
 // Wt[tap][m][k] from an OIHW weight W[Co][Ci][KH][KW].
 //   mode 0 (forward):      m = co, k = ci, tap = (kh, kw)
 //   mode 1 (data-grad s1): m = ci, k = co, tap = (kh', kw') with kh = KH-1-kh'
@@ -258,11 +309,37 @@ int dsgan_conv_wtrans(const float* W, float* Wt, int Co, int Ci, int KH, int KW,
   return 0;
 }
 
+static long tc_tiles(int nb, int M, int Hout, int Wout) {
+  return (long)nb * ((Hout * Wout + 127) / 128) * (M > 64 ? (M + 127) / 128 : (M + 63) / 64);
+}
+
+// fp32 scratch dsgan_tconv_ws needs (0: the launch is not split)
+long dsgan_tconv_workspace(int nb, int K, int M, int Hout, int Wout, int ntaps) {
+  if (K % TBK != 0 || K <= 0) return 0;
+  int kc;
+  const int S = tc_splits(tc_tiles(nb, M, Hout, Wout), ntaps * (K / TBK), &kc);
+  return S > 1 ? (long)S * nb * M * Hout * Wout : 0;
+}
+
+int dsgan_tconv_ws(const float* X, long x_bs, const float* Wt, const float* bias, float* Y, long y_bs,
+                   const float* gpre, long gpre_bs, int nb, int K, int M, int Hin, int Win, int Hout,
+                   int Wout, int stride, int ntaps, const int* dh, const int* dw, int Hdst, int Wdst,
+                   int os, int ph, int pw, int act, int gact, float slope, float* ws, hipStream_t st);
+
 // Generic launcher.  taps: ntaps pairs (dh, dw).  dst lattice: (oh*os+ph, ow*os+pw) in Hdst x Wdst.
 int dsgan_tconv(const float* X, long x_bs, const float* Wt, const float* bias, float* Y, long y_bs,
                 const float* gpre, long gpre_bs, int nb, int K, int M, int Hin, int Win, int Hout,
                 int Wout, int stride, int ntaps, const int* dh, const int* dw, int Hdst, int Wdst,
                 int os, int ph, int pw, int act, int gact, float slope, hipStream_t st) {
+  return dsgan_tconv_ws(X, x_bs, Wt, bias, Y, y_bs, gpre, gpre_bs, nb, K, M, Hin, Win, Hout, Wout, stride, ntaps,
+                        dh, dw, Hdst, Wdst, os, ph, pw, act, gact, slope, nullptr, st);
+}
+
+// Same, with the split-K scratch of dsgan_tconv_workspace (NULL: never split).
+int dsgan_tconv_ws(const float* X, long x_bs, const float* Wt, const float* bias, float* Y, long y_bs,
+                   const float* gpre, long gpre_bs, int nb, int K, int M, int Hin, int Win, int Hout,
+                   int Wout, int stride, int ntaps, const int* dh, const int* dw, int Hdst, int Wdst,
+                   int os, int ph, int pw, int act, int gact, float slope, float* ws, hipStream_t st) {
   DSG_REQUIRE(X && Wt && Y && nb > 0 && M > 0 && Hout > 0 && Wout > 0, "dsgan_tconv: bad args");
   DSG_REQUIRE(K % TBK == 0 && K > 0, "dsgan_tconv: K (input channels) must be a multiple of 32");
   DSG_REQUIRE(ntaps >= 1 && ntaps <= T_MAXTAPS, "dsgan_tconv: 1..16 taps");
@@ -277,13 +354,22 @@ int dsgan_tconv(const float* X, long x_bs, const float* Wt, const float* bias, f
   for (int t = 0; t < ntaps; ++t) { g.dh[t] = dh[t]; g.dw[t] = dw[t]; }
   g.Hdst = Hdst; g.Wdst = Wdst; g.os = os; g.ph = ph; g.pw = pw;
   g.act = act; g.gact = gact; g.slope = slope;
-  const long ntiles = (long)nb * ((Hout * Wout + 127) / 128);
-  if (M > 64) {
-    hipLaunchKernelGGL(tconv_kernel<128>, dim3((unsigned)(ntiles * ((M + 127) / 128))), dim3(256), 0, st, g);
-  } else {
-    hipLaunchKernelGGL(tconv_kernel<64>, dim3((unsigned)(ntiles * ((M + 63) / 64))), dim3(256), 0, st, g);
-  }
+  const long tiles = tc_tiles(nb, M, Hout, Wout);
+  int kc;
+  const int S = ws ? tc_splits(tiles, ntaps * (K / TBK), &kc) : 1;
+  g.ws = S > 1 ? ws : nullptr;
+  g.kchunk = S > 1 ? kc : 0;
+  DSG_REQUIRE(S == 1 || (long)S * nb * M * Hout * Wout < (1L << 31), "dsgan_tconv: split partials too large");
+  if (M > 64) hipLaunchKernelGGL(tconv_kernel<128>, dim3((unsigned)(tiles * S)), dim3(256), 0, st, g);
+  else hipLaunchKernelGGL(tconv_kernel<64>, dim3((unsigned)(tiles * S)), dim3(256), 0, st, g);
   DSG_CHECK_LAUNCH();
+  if (S > 1) {
+    const long per = (long)nb * M * Hout * Wout;
+    long blocks = (per + 255) / 256;
+    if (blocks > 8192) blocks = 8192;
+    hipLaunchKernelGGL(tconv_reduce_kernel, dim3((unsigned)blocks), dim3(256), 0, st, g, S);
+    DSG_CHECK_LAUNCH();
+  }
   return 0;
 }
 

@@ -166,10 +166,12 @@ def _tconv(X, xbs, Wt, bias, Y, ybs, gpre, gbs, nb, K, M, Hin, Win, Hout, Wout, 
     import ctypes
     dh = (ctypes.c_int * len(taps))(*[t[0] for t in taps])
     dw = (ctypes.c_int * len(taps))(*[t[1] for t in taps])
-    call("dsgan_tconv", ptr(X), xbs, ptr(Wt), ptr(bias), ptr(Y), ybs, ptr(gpre), gbs, nb, K, M, Hin,
+    nws = _lib.load().dsgan_tconv_workspace(nb, K, M, Hout, Wout, len(taps))
+    ws = torch.empty(nws, device=X.device, dtype=torch.float32) if nws > 0 else None
+    call("dsgan_tconv_ws", ptr(X), xbs, ptr(Wt), ptr(bias), ptr(Y), ybs, ptr(gpre), gbs, nb, K, M, Hin,
          Win, Hout, Wout, stride, len(taps), ctypes.cast(dh, ctypes.c_void_p),
          ctypes.cast(dw, ctypes.c_void_p), Hdst, Wdst, os_, ph, pw, ACT[act], ACT[gact],
-         LRELU_SLOPE, stream())
+         LRELU_SLOPE, ptr(ws), stream())
 
 
 # Transformed-weight cache: an entry is valid while the parameter's storage pointer and the

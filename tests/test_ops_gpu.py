@@ -100,7 +100,8 @@ def test_conv2d(prec, N, Cin, H, W, Cout, K, s, p):
 
 
 @pytest.mark.parametrize("prec", ["fp32", "bf16"])
-@pytest.mark.parametrize("N,Ci,Co,H", [(2, 64, 32, 8), (2, 128, 64, 5), (1, 256, 128, 16)])
+@pytest.mark.parametrize("N,Ci,Co,H", [(2, 64, 32, 8), (2, 128, 64, 5), (1, 256, 128, 16),
+                                       (2, 1024, 512, 16)])   # u1 shape: split-K tconv data-grad
 def test_conv_transpose(prec, N, Ci, Co, H):
     from dsgan_hip import functional as HF
     HF.set_precision(prec)
