@@ -42,13 +42,15 @@ struct TcArgs {
   float* ws; int kchunk;               // split-K (ws != NULL): raw partials [split][nb][M][Hout*Wout]
 };
 
-template <int BM>
+// ABF: Wt is bf16 (dsgan_conv_wtrans_bf16, cached per weight version): half the A bytes, copied to
+// LDS unconverted.
+template <int BM, bool ABF>
 __global__ __launch_bounds__(256, 2) void tconv_kernel(TcArgs g) {
   constexpr int BN = 128;
   constexpr int WM = 2, WN = 2;
   constexpr int TM = BM / WM / 32, TN = BN / WN / 32;
   constexpr int A_SZ = BM * T_STR, B_SZ = BN * T_STR;
-  constexpr int A_ITEMS = BM * 8 / 256;  // float4 items of the [BM][32] A tile
+  constexpr int A_ITEMS = ABF ? BM * 4 / 256 : BM * 8 / 256;  // 16-byte items of the [BM][32] A tile
   __shared__ __attribute__((aligned(16))) __bf16 smem[2 * (A_SZ + B_SZ)];
 
   // wave index through readfirstlane: the compiler then knows it is uniform (SGPR), so
@@ -73,7 +75,7 @@ __global__ __launch_bounds__(256, 2) void tconv_kernel(TcArgs g) {
 
   const int HWin = g.Hin * g.Win;
   const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)g.Wt, (short)0, (unsigned)((long)g.ntaps * g.M * g.K * 4), 0x00020000);
+      (void*)g.Wt, (short)0, (unsigned)((long)g.ntaps * g.M * g.K * (ABF ? 2 : 4)), 0x00020000);
   const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(g.X + (long)bimg * g.x_bs), (short)0, (unsigned)((long)g.K * HWin * 4), 0x00020000);
 
@@ -89,20 +91,28 @@ __global__ __launch_bounds__(256, 2) void tconv_kernel(TcArgs g) {
   const int kb0 = g.ws ? split * g.kchunk : 0;
   const int nk = g.ws ? min(g.kchunk, nk_all - kb0) : nk_all;   // K steps of this split
 
-  float4 ra[A_ITEMS];
+  typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
+  float4 ra[ABF ? 1 : A_ITEMS];
+  u32x4 rha[ABF ? A_ITEMS : 1];
   float rb[16];
   auto gload = [&](int kt0) {
     const int kt = kb0 + kt0;
     const int tap = kt / ksteps_per_tap;
     const int k0 = (kt - tap * ksteps_per_tap) * TBK;
     // A rows past M get an offset past the resource range (reads 0, no branch)
-    const unsigned wtap = (unsigned)tap * g.M * g.K * 4u;
+    const unsigned wtap = (unsigned)tap * g.M * g.K * (ABF ? 2u : 4u);
 #pragma unroll
     for (int i = 0; i < A_ITEMS; ++i) {
       const int it = tid + i * 256;
-      const int m = m0 + (it >> 3), kk = k0 + (it & 7) * 4;
-      const unsigned off = m < g.M ? ((unsigned)m * g.K + kk) * 4u : 0xFFFFFFF0u;
-      ra[i] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rw, (int)off, wtap, 0));
+      if constexpr (ABF) {   // 8 bf16 per item, 4 items per 32-deep row
+        const int m = m0 + (it >> 2), kk = k0 + (it & 3) * 8;
+        const unsigned off = m < g.M ? ((unsigned)m * g.K + kk) * 2u : 0xFFFFFFF0u;
+        rha[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rw, (int)off, wtap, 0));
+      } else {
+        const int m = m0 + (it >> 3), kk = k0 + (it & 7) * 4;
+        const unsigned off = m < g.M ? ((unsigned)m * g.K + kk) * 4u : 0xFFFFFFF0u;
+        ra[i] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rw, (int)off, wtap, 0));
+      }
     }
     const int ih = ih0 + g.dh[tap], iw = iw0 + g.dw[tap];
     const bool in = qv && (unsigned)ih < (unsigned)g.Hin && (unsigned)iw < (unsigned)g.Win;
@@ -118,6 +128,10 @@ __global__ __launch_bounds__(256, 2) void tconv_kernel(TcArgs g) {
 #pragma unroll
     for (int i = 0; i < A_ITEMS; ++i) {
       const int it = tid + i * 256;
+      if constexpr (ABF) {
+        *reinterpret_cast<u32x4*>(As + (it >> 2) * T_STR + (it & 3) * 8) = rha[i];
+        continue;
+      }
       typedef __attribute__((ext_vector_type(4))) __bf16 b4;
       b4 v;
       v[0] = (__bf16)ra[i].x; v[1] = (__bf16)ra[i].y; v[2] = (__bf16)ra[i].z; v[3] = (__bf16)ra[i].w;
@@ -324,7 +338,7 @@ long dsgan_tconv_workspace(int nb, int K, int M, int Hout, int Wout, int ntaps) 
 int dsgan_tconv_ws(const float* X, long x_bs, const float* Wt, const float* bias, float* Y, long y_bs,
                    const float* gpre, long gpre_bs, int nb, int K, int M, int Hin, int Win, int Hout,
                    int Wout, int stride, int ntaps, const int* dh, const int* dw, int Hdst, int Wdst,
-                   int os, int ph, int pw, int act, int gact, float slope, float* ws, hipStream_t st);
+                   int os, int ph, int pw, int act, int gact, float slope, int wt_bf16, float* ws, hipStream_t st);
 
 // Generic launcher.  taps: ntaps pairs (dh, dw).  dst lattice: (oh*os+ph, ow*os+pw) in Hdst x Wdst.
 int dsgan_tconv(const float* X, long x_bs, const float* Wt, const float* bias, float* Y, long y_bs,
@@ -332,14 +346,14 @@ int dsgan_tconv(const float* X, long x_bs, const float* Wt, const float* bias, f
                 int Wout, int stride, int ntaps, const int* dh, const int* dw, int Hdst, int Wdst,
                 int os, int ph, int pw, int act, int gact, float slope, hipStream_t st) {
   return dsgan_tconv_ws(X, x_bs, Wt, bias, Y, y_bs, gpre, gpre_bs, nb, K, M, Hin, Win, Hout, Wout, stride, ntaps,
-                        dh, dw, Hdst, Wdst, os, ph, pw, act, gact, slope, nullptr, st);
+                        dh, dw, Hdst, Wdst, os, ph, pw, act, gact, slope, 0, nullptr, st);
 }
 
 // Same, with the split-K scratch of dsgan_tconv_workspace (NULL: never split).
 int dsgan_tconv_ws(const float* X, long x_bs, const float* Wt, const float* bias, float* Y, long y_bs,
                    const float* gpre, long gpre_bs, int nb, int K, int M, int Hin, int Win, int Hout,
                    int Wout, int stride, int ntaps, const int* dh, const int* dw, int Hdst, int Wdst,
-                   int os, int ph, int pw, int act, int gact, float slope, float* ws, hipStream_t st) {
+                   int os, int ph, int pw, int act, int gact, float slope, int wt_bf16, float* ws, hipStream_t st) {
   DSG_REQUIRE(X && Wt && Y && nb > 0 && M > 0 && Hout > 0 && Wout > 0, "dsgan_tconv: bad args");
   DSG_REQUIRE(K % TBK == 0 && K > 0, "dsgan_tconv: K (input channels) must be a multiple of 32");
   DSG_REQUIRE(ntaps >= 1 && ntaps <= T_MAXTAPS, "dsgan_tconv: 1..16 taps");
@@ -347,6 +361,7 @@ int dsgan_tconv_ws(const float* X, long x_bs, const float* Wt, const float* bias
               "dsgan_tconv: tensor exceeds a 2 GiB buffer resource");
   DSG_REQUIRE(((uintptr_t)Wt & 15) == 0, "dsgan_tconv: Wt must be 16-byte aligned");
   DSG_REQUIRE((long)ntaps * M * K * 4 < 0xFFFFFFF0L, "dsgan_tconv: Wt exceeds a 4 GiB buffer resource");
+  DSG_REQUIRE(!wt_bf16 || K % 8 == 0, "dsgan_tconv: bf16 Wt needs K %% 8 == 0");
   TcArgs g{};
   g.X = X; g.x_bs = x_bs; g.Wt = Wt; g.Y = Y; g.y_bs = y_bs; g.bias = bias; g.gpre = gpre;
   g.gpre_bs = gpre_bs; g.nb = nb; g.K = K; g.M = M; g.Hin = Hin; g.Win = Win; g.Hout = Hout;
@@ -360,8 +375,14 @@ int dsgan_tconv_ws(const float* X, long x_bs, const float* Wt, const float* bias
   g.ws = S > 1 ? ws : nullptr;
   g.kchunk = S > 1 ? kc : 0;
   DSG_REQUIRE(S == 1 || (long)S * nb * M * Hout * Wout < (1L << 31), "dsgan_tconv: split partials too large");
-  if (M > 64) hipLaunchKernelGGL(tconv_kernel<128>, dim3((unsigned)(tiles * S)), dim3(256), 0, st, g);
-  else hipLaunchKernelGGL(tconv_kernel<64>, dim3((unsigned)(tiles * S)), dim3(256), 0, st, g);
+  const dim3 grid((unsigned)(tiles * S));
+  if (M > 64) {
+    if (wt_bf16) hipLaunchKernelGGL((tconv_kernel<128, true>), grid, dim3(256), 0, st, g);
+    else hipLaunchKernelGGL((tconv_kernel<128, false>), grid, dim3(256), 0, st, g);
+  } else {
+    if (wt_bf16) hipLaunchKernelGGL((tconv_kernel<64, true>), grid, dim3(256), 0, st, g);
+    else hipLaunchKernelGGL((tconv_kernel<64, false>), grid, dim3(256), 0, st, g);
+  }
   DSG_CHECK_LAUNCH();
   if (S > 1) {
     const long per = (long)nb * M * Hout * Wout;

@@ -64,7 +64,7 @@ SIGNATURES = {
     "dsgan_conv_wtrans": [P, P, I, I, I, I, I, I, I, I, I, S],
     "dsgan_tconv": [P, L, P, P, P, L, P, L] + [I] * 9 + [P, P] + [I] * 7 + [F, S],
     "dsgan_tconv_workspace": [I] * 6,
-    "dsgan_tconv_ws": [P, L, P, P, P, L, P, L] + [I] * 9 + [P, P] + [I] * 7 + [F, P, S],
+    "dsgan_tconv_ws": [P, L, P, P, P, L, P, L] + [I] * 9 + [P, P] + [I] * 7 + [F, I, P, S],
     # skinny.hip
     "dsgan_conv_small_out": [P, L, P, L, L, L, L, P, P, L] + [I] * 13 + [S],
     "dsgan_conv_small_in": [P, L, P, L, L, L, L, P, P, L] + [I] * 13 + [F, I, S],

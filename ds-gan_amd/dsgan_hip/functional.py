@@ -163,6 +163,7 @@ def _pw_ok(mode, M, K, P, a_bs, b_bs, a, b):
 
 def _tconv(X, xbs, Wt, bias, Y, ybs, gpre, gbs, nb, K, M, Hin, Win, Hout, Wout, stride, taps,
            Hdst, Wdst, os_, ph, pw, act, gact):
+    """Wt: fp32 tap-major weights (_wtrans) or their bf16 copy (_wtrans_bf16, mode 0)."""
     import ctypes
     dh = (ctypes.c_int * len(taps))(*[t[0] for t in taps])
     dw = (ctypes.c_int * len(taps))(*[t[1] for t in taps])
@@ -171,7 +172,7 @@ def _tconv(X, xbs, Wt, bias, Y, ybs, gpre, gbs, nb, K, M, Hin, Win, Hout, Wout, 
     call("dsgan_tconv_ws", ptr(X), xbs, ptr(Wt), ptr(bias), ptr(Y), ybs, ptr(gpre), gbs, nb, K, M, Hin,
          Win, Hout, Wout, stride, len(taps), ctypes.cast(dh, ctypes.c_void_p),
          ctypes.cast(dw, ctypes.c_void_p), Hdst, Wdst, os_, ph, pw, ACT[act], ACT[gact],
-         LRELU_SLOPE, ptr(ws), stream())
+         LRELU_SLOPE, int(Wt.dtype == torch.bfloat16), ptr(ws), stream())
 
 
 # Transformed-weight cache: an entry is valid while the parameter's storage pointer and the
@@ -318,7 +319,7 @@ def conv_fwd_raw(x, w, b, stride, pad, act=None, out=None, pre=None, accumulate=
     elif (_state["prec"] == "bf16" and w.dim() == 4 and (KH > 1 or KW > 1) and Cin % 32 == 0
           and pre is None and not accumulate and xact is None and KH * KW <= 16):
         fam = "tconv_kernel"
-        wt = _wtrans(w, 0)
+        wt = _wtrans_bf16(w, 0) if Cin % 8 == 0 else _wtrans(w, 0)
         taps = [(kh - pad, kw - pad) for kh in range(KH) for kw in range(KW)]
         _tconv(x, xbs, wt, b, y, ybs, None, 0, N, Cin, Cout, H, W, Ho, Wo, stride, taps, Ho, Wo, 1, 0, 0,
                act, None)

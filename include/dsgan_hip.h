@@ -198,12 +198,14 @@ int dsgan_tconv(const float* X, long x_bs, const float* Wt, const float* bias, f
 /* Split-K form: a launch whose tiles under-fill the chip (fewer than 512, e.g. the ConvTranspose
  * data-grads at 16^2 / 32^2, DSGAN/models/model/MixConvNeXtML.py:53) splits its K steps over
  * about 1024 workgroups; raw partials in ws (dsgan_tconv_workspace floats; 0 = not split, ws may
- * be NULL) are summed in a fixed order by a finishing pass that applies bias / act / gact'. */
+ * be NULL) are summed in a fixed order by a finishing pass that applies bias / act / gact'.
+ * wt_bf16: Wt is the bf16 copy of dsgan_conv_wtrans_bf16 (same [tap][M][K] layout, K % 8 == 0). */
 long dsgan_tconv_workspace(int nb, int K, int M, int Hout, int Wout, int ntaps);
 int dsgan_tconv_ws(const float* X, long x_bs, const float* Wt, const float* bias, float* Y, long y_bs,
                    const float* gpre, long gpre_bs, int nb, int K, int M, int Hin, int Win, int Hout,
                    int Wout, int stride, int ntaps, const int* dh, const int* dw, int Hdst, int Wdst,
-                   int os, int ph, int pw, int act, int gact, float slope, float* ws, hipStream_t stream);
+                   int os, int ph, int pw, int act, int gact, float slope, int wt_bf16, float* ws,
+                   hipStream_t stream);
 
 /* ---- patch-staged implicit-GEMM conv (pconv.hip): VGG16 3x3 s1 (DSGAN/models/vgg.py:15-24) fwd
  * and data-grad, PatchGAN 4x4 s2/s1 (DSGAN/models/networks.py:543-569) fwd and s1 data-grad ------
