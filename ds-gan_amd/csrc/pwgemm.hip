@@ -653,12 +653,16 @@ static bool use_bm256(const PwArgs& g) {
 static bool use_wide(const PwArgs& g) {
   return g.M % 256 == 0 && g.P % 256 == 0 && g.K >= 128 && (long)(g.M / 256) * (g.N / 256) >= 256;
 }
-// (Only for plain epilogues: with the per-element bf16 act' side tensor -- the gelu-pair forward
-// and the gp-multiplied data-grad -- one 8-wave workgroup per CU leaves the epilogue's loads and
-// 2-byte stores exposed, measured 1.3-1.5x slower than the 4-wave tiles.)
+// (Not for the gp-multiplied data-grad: there one 8-wave workgroup per CU leaves the epilogue's
+// 2-byte gp loads exposed.)
+// The gelu-pair forward (bf16 act(z) and act'(z) out, packed-fp32 GELU) now measures faster on the
+// wide tiles too (tools/pwio_micro.py, B=16: M=2048 K=512 at 64^2 0.455 -> 0.383 ms, M=4096 K=1024 at
+// 32^2 0.256 -> 0.227 ms); the gp-multiplied data-grad stays on 128-row tiles (wide: +5-20 %,
+// tools/pwdgrad_micro.py).
 static int fd_tile(const PwArgs& g, bool any_bf16) {
   const bool plain = !g.ypre && !g.gpre;
-  return any_bf16 && plain && use_wide(g) ? PW_WIDE : use_bm256(g) ? 256 : g.M > 64 ? 128 : 64;
+  const bool gelu_pair = g.ypre && g.gbf;
+  return any_bf16 && (plain || gelu_pair) && use_wide(g) ? PW_WIDE : use_bm256(g) ? 256 : g.M > 64 ? 128 : 64;
 }
 
 }  // namespace dsg
