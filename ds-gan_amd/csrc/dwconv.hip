@@ -430,14 +430,18 @@ static void dw_fwd_v2(const float* x, long x_bs, const float* w, const float* bi
                      y_bs, C, H, W, flip, accumulate, tw);
 }
 
-// images per workgroup of the tiled weight-grad: enough workgroups to fill the chip, as many
-// images each as that allows.  Returns the workgroups per channel (= partial slots).
+// images per workgroup of the tiled weight-grad: about `target` workgroups, as many images each as
+// that allows -- every workgroup ends in a block reduction of its K*K+1 sums, so a workgroup per
+// image tile over-fills the chip with reductions (tools/dw_wgrad_micro.py, B=16: the 7x7 launches
+// are fastest at ~1024 workgroups, the four-quarter MidMLKA launch at ~256 per quarter set:
+// 1024 ch @ 32^2 67 -> 55 us, C=128 @ 128^2 quarters 162 -> 99 us).  Returns the workgroups per
+// channel (= partial slots).
 template <int K, int TWT, int THT, int R>
-static long dw_wgrad_v2_plan(int N, int C, int H, int W, int* nsplit_out, int* nper_out) {
+static long dw_wgrad_v2_plan(int N, int C, int H, int W, int* nsplit_out, int* nper_out, long target = 1024) {
   using T = DwTile<K, TWT, THT, R>;
   const int tw = W / T::TW, th = (H + T::TH - 1) / T::TH;
   const long base = (long)tw * th * C;
-  int nsplit = (int)((2048 + base - 1) / base);
+  int nsplit = (int)((target + base - 1) / base);
   if (nsplit > N) nsplit = N;
   const int nper = (N + nsplit - 1) / nsplit;
   nsplit = (N + nper - 1) / nper;
@@ -521,7 +525,7 @@ static long dw_multi_wgrad_run(const float* dy, long dy_bs, const float* x, long
   using T = DwTile<9, TWT, THT, R>;
   const int tw = W / T::TW, th = (H + T::TH - 1) / T::TH;
   int nsplit, nper;
-  const long G = dw_wgrad_v2_plan<9, TWT, THT, R>(N, q, H, W, &nsplit, &nper);
+  const long G = dw_wgrad_v2_plan<9, TWT, THT, R>(N, q, H, W, &nsplit, &nper, 256);
   if (q4)
     hipLaunchKernelGGL((dwconv_multi_wgrad<TWT, THT, R>), dim3(tw * th, q, 4 * nsplit), dim3(256), 0, st, dy, dy_bs,
                        x, x_bs, *q4, N, q, H, W, tw, nper, nsplit);
