@@ -559,6 +559,42 @@ __global__ __launch_bounds__(256) void split_reduce_kernel(const float* __restri
   }
 }
 
+// The same reduction on 16-byte element groups (KK1 == 0, MN % 4 == 0, 16-byte aligned rows): a
+// lane sums four consecutive elements per load, so a wave reads 4 rows x 256 B instead of 4 rows x
+// 64 B per instruction; the per-element order of additions is the scalar kernel's (same bits).
+template <int J>
+__global__ __launch_bounds__(256) void split_reduce4_kernel(const float* __restrict__ ws, int S, long MN, long rs,
+                                                            float* __restrict__ dw) {
+  constexpr int EL = 256 / J;
+  __shared__ float4 sh[J][EL + 1];
+  const int el = threadIdx.x % EL, j = threadIdx.x / EL;
+  const long e = ((long)blockIdx.x * EL + el) * 4;
+  float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+  auto add = [](float4& x, const float4 v) { x.x += v.x; x.y += v.y; x.z += v.z; x.w += v.w; };
+  if (e < MN) {
+    int s = j;
+    for (; s + 3 * J < S; s += 4 * J) {
+      const float4 v0 = *reinterpret_cast<const float4*>(ws + (long)s * rs + e);
+      const float4 v1 = *reinterpret_cast<const float4*>(ws + (long)(s + J) * rs + e);
+      const float4 v2 = *reinterpret_cast<const float4*>(ws + (long)(s + 2 * J) * rs + e);
+      const float4 v3 = *reinterpret_cast<const float4*>(ws + (long)(s + 3 * J) * rs + e);
+      add(a, v0); add(a, v1); add(a, v2); add(a, v3);
+    }
+    for (; s < S; s += J) add(a, *reinterpret_cast<const float4*>(ws + (long)s * rs + e));
+  }
+  sh[j][el] = a;
+  __syncthreads();
+  if (j == 0 && e < MN) {
+    float4 t = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int q = 0; q < J; ++q) add(t, sh[q][el]);
+    float4* d = reinterpret_cast<float4*>(dw + e);
+    float4 o = *d;
+    add(o, t);
+    *d = o;
+  }
+}
+
 // K (pixel) split of a weight-grad launch: about `target` workgroups (640 = 2.5 per CU for the
 // 4-wave tiles: enough bytes in flight to stream HBM; 256 = one per CU for the 8-wave wide
 // tiles), >= 8 K steps each, and partials of at most a quarter of the operand bytes (each split
@@ -621,7 +657,12 @@ void launch_split_reduce_kk(const float* ws, int splits, long MN, float* dw, flo
     splits = groups;
     rs = MN * SPLIT_SC;
   }
-  if (splits <= 8)
+  const bool v4 = KK1 == 0 && (MN & 3) == 0 && (rs & 3) == 0 && (((uintptr_t)ws | (uintptr_t)dw) & 15) == 0;
+  if (v4 && splits <= 8)
+    hipLaunchKernelGGL(split_reduce4_kernel<4>, dim3((unsigned)((MN + 255) / 256)), dim3(256), 0, st, ws, splits, MN, rs, dw);
+  else if (v4)
+    hipLaunchKernelGGL(split_reduce4_kernel<16>, dim3((unsigned)((MN + 63) / 64)), dim3(256), 0, st, ws, splits, MN, rs, dw);
+  else if (splits <= 8)
     hipLaunchKernelGGL(split_reduce_kernel<4>, dim3((unsigned)((MN + 63) / 64)), dim3(256), 0, st, ws, splits, MN, rs, dw, db, KK1);
   else
     hipLaunchKernelGGL(split_reduce_kernel<16>, dim3((unsigned)((MN + 15) / 16)), dim3(256), 0, st, ws, splits, MN, rs, dw, db, KK1);
