@@ -646,14 +646,40 @@ __global__ __launch_bounds__(256) void split_prereduce_kernel(float* __restrict_
   if (j == 0 && e < MN) ws[(long)s0 * MN + e] = ((sh[0][el] + sh[1][el]) + sh[2][el]) + sh[3][el];
 }
 
+// 16-byte form of the pre-pass (MN % 4 == 0, 16-byte aligned rows): 64 float4 per row group lane.
+__global__ __launch_bounds__(256) void split_prereduce4_kernel(float* __restrict__ ws, int S, long MN) {
+  __shared__ float4 sh[4][65];
+  const int el = threadIdx.x & 63, j = threadIdx.x >> 6;
+  const long e = ((long)blockIdx.x * 64 + el) * 4;
+  const int s0 = blockIdx.y * SPLIT_SC, s1 = min(S, s0 + SPLIT_SC);
+  float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (e < MN)
+    for (int s = s0 + j; s < s1; s += 4) {
+      const float4 v = *reinterpret_cast<const float4*>(ws + (long)s * MN + e);
+      a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
+    }
+  sh[j][el] = a;
+  __syncthreads();
+  if (j == 0 && e < MN) {
+    const float4 p0 = sh[0][el], p1 = sh[1][el], p2 = sh[2][el], p3 = sh[3][el];
+    *reinterpret_cast<float4*>(ws + (long)s0 * MN + e) =
+        make_float4(((p0.x + p1.x) + p2.x) + p3.x, ((p0.y + p1.y) + p2.y) + p3.y, ((p0.z + p1.z) + p2.z) + p3.z,
+                    ((p0.w + p1.w) + p2.w) + p3.w);
+  }
+}
+
 // dw[e] += sum_s ws[s][e] (fixed order); every split reduction of the library goes through here.
 // (ws is consumed: the pre-pass overwrites some of its rows.)
 void launch_split_reduce_kk(const float* ws, int splits, long MN, float* dw, float* db, int KK1, hipStream_t st) {
   long rs = MN;
   if (splits > 64 && MN < 65536) {
     const int groups = (splits + SPLIT_SC - 1) / SPLIT_SC;
-    hipLaunchKernelGGL(split_prereduce_kernel, dim3((unsigned)((MN + 63) / 64), (unsigned)groups), dim3(256), 0, st,
-                       (float*)ws, splits, MN);
+    if ((MN & 3) == 0 && ((uintptr_t)ws & 15) == 0)
+      hipLaunchKernelGGL(split_prereduce4_kernel, dim3((unsigned)((MN + 255) / 256), (unsigned)groups), dim3(256), 0,
+                         st, (float*)ws, splits, MN);
+    else
+      hipLaunchKernelGGL(split_prereduce_kernel, dim3((unsigned)((MN + 63) / 64), (unsigned)groups), dim3(256), 0, st,
+                         (float*)ws, splits, MN);
     splits = groups;
     rs = MN * SPLIT_SC;
   }
