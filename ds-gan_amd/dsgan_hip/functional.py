@@ -838,7 +838,12 @@ class PwMlpFn(torch.autograd.Function):
     def _backward_unfused(ctx, dy):
         h, x, z, w1v, w2v, ws = ctx.saved_tensors
         w1, b1, w2, b2, ws_ref = ctx.refs
-        dy = dy.contiguous()
+        # dy may be a channel slice of a concat gradient (c1's output feeds the u4 concat): every
+        # consumer below takes a batch stride, so only a misaligned slice is copied
+        dy, dybs = nchw(dy)
+        if dy.data_ptr() % 16 or dybs % 8:
+            dy = dy.contiguous()
+            dybs = dy.shape[1] * dy.shape[2] * dy.shape[3]
         gw2, gb2, gws, gw1, gb1 = (_grad_buf(t) for t in (w2, b2, ws_ref, w1, b1))
         want_dh = ctx.needs_input_grad[0]
         if ctx.g is not None:
@@ -848,7 +853,7 @@ class PwMlpFn(torch.autograd.Function):
             HW, P, C = H * W, w2.shape[0], h.shape[1]
             dz = torch.empty((N, C4, H, W), device=dy.device, dtype=torch.bfloat16)
             e0 = IGEMM_TIMER.begin()
-            call("dsgan_pw_dgrad_io", ptr(bf16_weight(w2)), 1, ptr(dy), P * HW, 0, ptr(dz), C4 * HW, 1, ptr(z), C4 * HW,
+            call("dsgan_pw_dgrad_io", ptr(bf16_weight(w2)), 1, ptr(dy), dybs, 0, ptr(dz), C4 * HW, 1, ptr(z), C4 * HW,
                  C4, P, HW, N, 0, stream())
             IGEMM_TIMER.end(e0, 2.0 * N * HW * C4 * P, ("dgrad", N, C4, H, W, P, 1, 1), "pwgemm_kernel",
                             _nb(dy, w2, dz, z))
@@ -856,7 +861,7 @@ class PwMlpFn(torch.autograd.Function):
             # the bf16 dz (as the fused kernels sum it)
             if gw2 is not None:
                 e0 = IGEMM_TIMER.begin()
-                call("dsgan_pw_wgrad_mixed", ptr(dy), P * HW, 0, ptr(ctx.g), C4 * HW, 1, ptr(gw2), ptr(gb2), P, C4,
+                call("dsgan_pw_wgrad_mixed", ptr(dy), dybs, 0, ptr(ctx.g), C4 * HW, 1, ptr(gw2), ptr(gb2), P, C4,
                      HW, N, ptr(_pw_ws(P, C4, HW, N, dy)), stream())
                 IGEMM_TIMER.end(e0, 2.0 * N * HW * C4 * P, ("wgrad", N, C4, H, W, P, 1, 1), "pwgemm_kernel",
                                 _nb(dy, ctx.g, gw2))
