@@ -31,6 +31,7 @@ struct PcArgs {
   int tiles_w, tiles_h;
   int act, gact; float slope;
   int accumulate;
+  float* ws; int kchunk;              // split-K (ws != NULL): raw partials [split][nb][M][Ho*Wo], kchunk 32-channel blocks each
 };
 
 constexpr int PC_STR = 40;   // bf16 per staged pixel / weight row (32 + 8: conflict-free b128 reads)
@@ -60,8 +61,9 @@ __global__ __launch_bounds__(256, 2) void pconv_kernel(PcArgs g) {
     const int xcd = id & 7, q = nwg >> 3, r = nwg & 7;
     tile = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (id >> 3);
   }
-  const int m_t = tile % mt, rest = tile / mt;
+  const int m_t = tile % mt, rest0 = tile / mt;
   const int tpi = g.tiles_w * g.tiles_h;
+  const int split = rest0 / (g.nb * tpi), rest = rest0 - split * (g.nb * tpi);
   const int bimg = rest / tpi, t_i = rest - bimg * tpi;
   const int m0 = m_t * BM;
   const int oh0 = (t_i / g.tiles_w) * TH, ow0 = (t_i % g.tiles_w) * TW;
@@ -133,7 +135,7 @@ __global__ __launch_bounds__(256, 2) void pconv_kernel(PcArgs g) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int m = m0 + wm * TM * 32 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-      bv[r] = (g.bias && m < g.M) ? g.bias[m] : 0.f;
+      bv[r] = (g.bias && !g.ws && m < g.M) ? g.bias[m] : 0.f;   // split-K: the finishing pass adds it
     }
 #pragma unroll
     for (int j = 0; j < TN; ++j)
@@ -141,11 +143,12 @@ __global__ __launch_bounds__(256, 2) void pconv_kernel(PcArgs g) {
       for (int r = 0; r < 16; ++r) acc[i][j][r] = bv[r];
   }
 
-  const int nkb = g.K / 32;
+  const int kb0 = g.ws ? split * g.kchunk : 0;
+  const int nkb = g.ws ? min(g.K / 32, kb0 + g.kchunk) : g.K / 32;   // this split's channel blocks [kb0, nkb)
   int buf = 0;
-  aload(0, 0);
-  pload(0);
-  for (int kb = 0; kb < nkb; ++kb) {
+  aload(0, kb0 * 32);
+  pload(kb0 * 32);
+  for (int kb = kb0; kb < nkb; ++kb) {
     const int k0 = kb * 32;
     __syncthreads();                 // previous block's patch and A buffers are free
     pwrite();
@@ -184,6 +187,24 @@ __global__ __launch_bounds__(256, 2) void pconv_kernel(PcArgs g) {
 
   // ---- epilogue ----
   const int HWo = g.Ho * g.Wo;
+  if (g.ws) {   // split-K partial: raw sums, lanes along the pixels
+    float* wp = g.ws + ((long)split * g.nb + bimg) * g.M * HWo;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int n = wn * (BN / WN) + j * 32 + lr;
+      const int oh = oh0 + n / TW, ow = ow0 + n % TW;
+      if (oh >= g.Ho || ow >= g.Wo) continue;
+      const long pofs = (long)oh * g.Wo + ow;
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int m = m0 + wm * TM * 32 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+          if (m < g.M) wp[(long)m * HWo + pofs] = acc[i][j][r];
+        }
+    }
+    return;
+  }
   float* yb = g.Y + (long)bimg * g.y_bs;
   const float* gb = g.gpre ? g.gpre + (long)bimg * g.gpre_bs : nullptr;
 #pragma unroll
@@ -221,6 +242,36 @@ __global__ __launch_bounds__(256, 2) void pconv_kernel(PcArgs g) {
   }
 }
 
+// Split-K finish: y (+)= act( sum_s ws[s] + bias ) (* gact'(gpre)), splits in a fixed order.
+__global__ __launch_bounds__(256) void pconv_reduce_kernel(PcArgs g, int S) {
+  const int HWo = g.Ho * g.Wo;
+  const long per = (long)g.nb * g.M * HWo;
+  for (long e = blockIdx.x * 256L + threadIdx.x; e < per; e += (long)gridDim.x * 256) {
+    float v = 0.f;
+    for (int s = 0; s < S; ++s) v += g.ws[(long)s * per + e];
+    const int p = (int)(e % HWo);
+    const long bm = e / HWo;
+    const int m = (int)(bm % g.M), b = (int)(bm / g.M);
+    if (g.bias) v += g.bias[m];
+    if (g.gpre) v *= act_g(g.gact, g.gpre[(long)b * g.gpre_bs + (long)m * HWo + p], g.slope);
+    v = act_f(g.act, v, g.slope);
+    float* o = g.Y + (long)b * g.y_bs + (long)m * HWo + p;
+    *o = g.accumulate ? *o + v : v;
+  }
+}
+
+// K split of a launch whose tiles under-fill the chip (the PatchGAN stride-1 data-grad at 31^2:
+// 128 tiles of 8 channel blocks): about 1024 workgroups, >= 2 channel blocks each, only for
+// K >= 256 (tools/pconv_micro.py, B=16: K=256 70 -> 44 us; K=128 split in two measured 44 -> 49 us).
+static int pc_splits(long tiles, int nkb, int* kchunk) {
+  long S = (1024 + tiles - 1) / tiles;
+  if (S > nkb / 2) S = nkb / 2;
+  if (tiles >= 512 || nkb < 8 || S < 2) { *kchunk = nkb; return 1; }
+  const int kc = (int)((nkb + S - 1) / S);
+  *kchunk = kc;
+  return (nkb + kc - 1) / kc;
+}
+
 // bf16 tap-major weights (same modes as dsgan_conv_wtrans):
 //   mode 0 (forward):      Wb[tap][co][ci], tap = (kh, kw)
 //   mode 1 (data-grad s1): Wb[tap][ci][co], tap = (kh', kw') with kh = KH-1-kh', kw = KW-1-kw'
@@ -245,7 +296,17 @@ static void pc_launch(PcArgs& g, hipStream_t st) {
   g.tiles_w = (g.Wo + TW - 1) / TW;
   g.tiles_h = (g.Ho + TH - 1) / TH;
   const long tiles = (long)g.nb * g.tiles_w * g.tiles_h * ((g.M + BM - 1) / BM);
-  hipLaunchKernelGGL((pconv_kernel<BM, TH, TW, S, KH, KW>), dim3((unsigned)tiles), dim3(256), 0, st, g);
+  int kc = 0;
+  const int splits = g.ws ? pc_splits(tiles, g.K / 32, &kc) : 1;
+  if (splits == 1) g.ws = nullptr;
+  g.kchunk = kc;
+  hipLaunchKernelGGL((pconv_kernel<BM, TH, TW, S, KH, KW>), dim3((unsigned)(tiles * splits)), dim3(256), 0, st, g);
+  if (splits > 1) {
+    const long per = (long)g.nb * g.M * g.Ho * g.Wo;
+    long blocks = (per + 255) / 256;
+    if (blocks > 8192) blocks = 8192;
+    hipLaunchKernelGGL(pconv_reduce_kernel, dim3((unsigned)blocks), dim3(256), 0, st, g, splits);
+  }
 }
 
 template <int BM>
@@ -277,11 +338,43 @@ int dsgan_conv_wtrans_bf16(const float* W, void* Wb, int Co, int Ci, int KH, int
   return 0;
 }
 
+// BM = 256 for the wide layers (VGG conv3/conv4, 256/512 output channels): per tap twice the
+// MFMAs between barriers and half the patch traffic per MAC, only while the launch still has >= 2
+// workgroups per CU (at 32x32 it would have one)
+static int pc_bm(int nb, int M, int Ho, int Wo) {
+  const long ptiles = (long)nb * ((Ho + 7) / 8) * ((Wo + 15) / 16);
+  return M >= 256 && ptiles * ((M + 255) / 256) >= 512 ? 256 : M > 64 ? 128 : 64;
+}
+
+// fp32 scratch dsgan_pconv_ws needs (0: the launch is not split)
+long dsgan_pconv_workspace(int nb, int K, int M, int Ho, int Wo) {
+  if (K % 32 != 0 || K <= 0) return 0;
+  const int bm = pc_bm(nb, M, Ho, Wo);
+  const long tiles = (long)nb * ((Ho + 7) / 8) * ((Wo + 15) / 16) * ((M + bm - 1) / bm);
+  int kc;
+  const int S = pc_splits(tiles, K / 32, &kc);
+  return S > 1 ? (long)S * nb * M * Ho * Wo : 0;
+}
+
+int dsgan_pconv_ws(const float* X, long x_bs, const void* Wb, const float* bias, float* Y, long y_bs,
+                   const float* gpre, long gpre_bs, int nb, int K, int M, int H, int W, int Ho, int Wo,
+                   int KH, int KW, int stride, int pad, int act, int gact, float slope, int accumulate,
+                   float* ws, hipStream_t st);
+
 // y[b][m][oh][ow] (+)= act(bias[m] + sum W * x) (* gact'(gpre)); Wb from dsgan_conv_wtrans_bf16.
 int dsgan_pconv(const float* X, long x_bs, const void* Wb, const float* bias, float* Y, long y_bs,
                 const float* gpre, long gpre_bs, int nb, int K, int M, int H, int W, int Ho, int Wo,
                 int KH, int KW, int stride, int pad, int act, int gact, float slope, int accumulate,
                 hipStream_t st) {
+  return dsgan_pconv_ws(X, x_bs, Wb, bias, Y, y_bs, gpre, gpre_bs, nb, K, M, H, W, Ho, Wo, KH, KW, stride, pad, act,
+                        gact, slope, accumulate, nullptr, st);
+}
+
+// Same, with the split-K scratch of dsgan_pconv_workspace (NULL: never split).
+int dsgan_pconv_ws(const float* X, long x_bs, const void* Wb, const float* bias, float* Y, long y_bs,
+                   const float* gpre, long gpre_bs, int nb, int K, int M, int H, int W, int Ho, int Wo,
+                   int KH, int KW, int stride, int pad, int act, int gact, float slope, int accumulate,
+                   float* ws, hipStream_t st) {
   DSG_REQUIRE(X && Wb && Y && nb > 0 && M > 0 && Ho > 0 && Wo > 0, "dsgan_pconv: bad args");
   DSG_REQUIRE(dsgan_pconv_supported(K, KH, KW, stride), "dsgan_pconv: unsupported K=%d KH=%d KW=%d stride=%d", K, KH, KW, stride);
   DSG_REQUIRE(((uintptr_t)Wb & 15) == 0, "dsgan_pconv: Wb must be 16-byte aligned");
@@ -291,13 +384,11 @@ int dsgan_pconv(const float* X, long x_bs, const void* Wb, const float* bias, fl
   g.X = X; g.x_bs = x_bs; g.Wb = (const __bf16*)Wb; g.Y = Y; g.y_bs = y_bs; g.bias = bias;
   g.gpre = gpre; g.gpre_bs = gpre_bs; g.nb = nb; g.K = K; g.M = M; g.H = H; g.W = W; g.Ho = Ho;
   g.Wo = Wo; g.pad = pad; g.act = act; g.gact = gact; g.slope = slope; g.accumulate = accumulate;
-  // BM = 256 for the wide layers (VGG conv3/conv4, 256/512 output channels): per tap twice the
-  // MFMAs between barriers and half the patch traffic per MAC, only while the launch still has >= 2 workgroups per CU (at 32x32 it would have one)
-  const long ptiles = (long)nb * ((Ho + 7) / 8) * ((Wo + 15) / 16);
-  const bool use256 = M >= 256 && ptiles * ((M + 255) / 256) >= 512;
-  const int rc = use256 ? pc_dispatch<256>(g, KH, stride, st)
-                 : M > 64            ? pc_dispatch<128>(g, KH, stride, st)
-                                     : pc_dispatch<64>(g, KH, stride, st);
+  g.ws = ws;
+  const int bm = pc_bm(nb, M, Ho, Wo);
+  const int rc = bm == 256 ? pc_dispatch<256>(g, KH, stride, st)
+                 : bm == 128 ? pc_dispatch<128>(g, KH, stride, st)
+                             : pc_dispatch<64>(g, KH, stride, st);
   DSG_REQUIRE(rc == 0, "dsgan_pconv: no kernel for KH=%d stride=%d", KH, stride);
   DSG_CHECK_LAUNCH();
   return 0;

@@ -49,6 +49,8 @@ SIGNATURES = {
     "dsgan_pconv_supported": [I, I, I, I],
     "dsgan_conv_wtrans_bf16": [P, P, I, I, I, I, I, S],
     "dsgan_pconv": [P, L, P, P, P, L, P, L] + [I] * 13 + [F, I, S],
+    "dsgan_pconv_workspace": [I] * 5,
+    "dsgan_pconv_ws": [P, L, P, P, P, L, P, L] + [I] * 13 + [F, I, P, S],
     # pwsmall.hip
     "dsgan_pw_small_supported": [I, I, I, L, L],
     "dsgan_pw_small": [P, L, P, I, I, P, P, L, P, L] + [I] * 8 + [F, S],

@@ -263,8 +263,10 @@ def _pconv_ok(K, KH, KW, stride):
 
 
 def _pconv(x, xbs, wb, b, y, ybs, N, K, M, H, W, Ho, Wo, KH, KW, stride, pad, act, gpre, gbs, gact, accumulate):
-    call("dsgan_pconv", ptr(x), xbs, ptr(wb), ptr(b), ptr(y), ybs, ptr(gpre), gbs, N, K, M, H, W, Ho, Wo, KH, KW,
-         stride, pad, ACT[act], ACT[gact], LRELU_SLOPE, int(accumulate), stream())
+    nws = _lib.load().dsgan_pconv_workspace(N, K, M, Ho, Wo)
+    ws = torch.empty(nws, device=x.device, dtype=torch.float32) if nws > 0 else None
+    call("dsgan_pconv_ws", ptr(x), xbs, ptr(wb), ptr(b), ptr(y), ybs, ptr(gpre), gbs, N, K, M, H, W, Ho, Wo, KH, KW,
+         stride, pad, ACT[act], ACT[gact], LRELU_SLOPE, int(accumulate), ptr(ws), stream())
 
 
 def conv_fwd_raw(x, w, b, stride, pad, act=None, out=None, pre=None, accumulate=False, xact=None):

@@ -221,6 +221,15 @@ int dsgan_pconv(const float* X, long x_bs, const void* Wb, const float* bias, fl
                 const float* gpre, long gpre_bs, int nb, int K, int M, int H, int W, int Ho, int Wo,
                 int KH, int KW, int stride, int pad, int act, int gact, float slope, int accumulate,
                 hipStream_t stream);
+/* Split-K form of dsgan_pconv: a launch whose tiles under-fill the chip (the PatchGAN stride-1
+ * layers at 31^2, DSGAN/models/networks.py:560-569) splits its 32-channel blocks over about 1024
+ * workgroups; raw partials in ws (dsgan_pconv_workspace floats; 0 = not split, ws may be NULL)
+ * are summed in a fixed order by a finishing pass applying bias / gact' / act / accumulate. */
+long dsgan_pconv_workspace(int nb, int K, int M, int Ho, int Wo);
+int dsgan_pconv_ws(const float* X, long x_bs, const void* Wb, const float* bias, float* Y, long y_bs,
+                   const float* gpre, long gpre_bs, int nb, int K, int M, int H, int W, int Ho, int Wo,
+                   int KH, int KW, int stride, int pad, int act, int gact, float slope, int accumulate,
+                   float* ws, hipStream_t stream);
 
 /* ---- 1x1 contractions with <= 16 channels on one side (pwsmall.hip): the 3/12-channel layers
  * at 256^2 -- c1 pwconv1/pwconv2/shortcut, OriginMLKA.to32/shortcut (MixConvNeXtML.py:122,145,
