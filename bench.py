@@ -39,23 +39,63 @@ PEAK_F32_TFLOPS = 157.3
 PEAK_HBM_GBS = 8000.0       # MI355X HBM3E (MI355X_MICROARCH.md)
 
 
-def reference_legs(steps=10, batch=16, size=256, threads=16, timed=(2, 7)):
+def host_cpu():
+    """The host's CPU as BASELINE.md §3 asks for it: model name, physical cores of the CPUs this
+    process may run on (sched affinity, SMT siblings counted once), and the cgroup CPU quota; the
+    baseline uses every physical core it is allowed (min of the two)."""
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    cpus = sorted(os.sched_getaffinity(0))
+    phys = set()
+    for c in cpus:
+        try:
+            base = "/sys/devices/system/cpu/cpu%d/topology/" % c
+            with open(base + "physical_package_id") as f1, open(base + "core_id") as f2:
+                phys.add((f1.read().strip(), f2.read().strip()))
+        except OSError:
+            phys.add(("?", str(c)))
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+            if q != "max":
+                quota = max(1, int(int(q) // int(per)))
+    except (OSError, ValueError):
+        pass
+    threads = len(phys) if quota is None else min(len(phys), quota)
+    return {"cpu_model": model, "logical_cpus_allowed": len(cpus), "physical_cores_allowed": len(phys),
+            "cgroup_cpu_quota": quota, "threads": threads}
+
+
+def reference_legs(steps=10, batch=16, size=256, threads=None, timed=(2, 7)):
     """The two legs of the metric that need the reference's arithmetic, on ONE shared run:
 
     * quality -- 'MS-SSIM Δ vs ref': the GPU model (bench precision) and the CPU oracle
       (oracle/dsgan_cpu.py, the reference step restated in fp32 -- the checker, never the thing
       measured) train `steps` steps from identical weights (the reference's own N(0, 0.02) init
-      recipe) on identical synthetic 256^2 pairs at the bench batch (pool_size 0).  Δ =
+      recipe) on identical synthetic pairs at the bench batch (pool_size 0).  Δ =
       |MS-SSIM(fake_gpu, real_B) - MS-SSIM(fake_ref, real_B)| on the last step's fake_B,
       DSGAN/MS_SSIM.py:153 with data_range 1.
     * cpu_baseline -- the oracle's steps [timed[0], timed[1]) of that same run (BASELINE.md §3:
-      2 warm-up + 5 timed steps at B=16, 256^2, fp32) on `threads` host threads."""
+      2 warm-up + 5 timed steps, fp32), clamped to the steps run, on every physical core the
+      process may use (``host_cpu``; ``threads`` overrides).
+    Each leg reports its own error instead of hiding the other."""
     import random
     from oracle import dsgan_cpu as O
     from oracle.recipe import make_params, synth_pair
     from options.train_options import default_train_opt
     from models import create_model
     from dsgan_hip import functional as HF
+    host = host_cpu()
+    if threads is None:
+        threads = host["threads"]
     torch.set_num_threads(threads)
     prec = HF.get_precision()
     random.seed(20)
@@ -79,22 +119,34 @@ def reference_legs(steps=10, batch=16, size=256, threads=16, timed=(2, 7)):
         ref.step(A, B)
         cpu_s.append(time.perf_counter() - tc)
         print("[bench] reference leg step %d/%d: oracle %.1f s" % (i + 1, steps, cpu_s[-1]), file=sys.stderr, flush=True)
-    fg = model.fake_B.detach().float().cpu()
-    fo = ref.fake_B
-    tgt = (B + 1) / 2
-    m_gpu = O.ms_ssim((fg + 1) / 2, tgt).item()
-    m_ref = O.ms_ssim((fo + 1) / 2, tgt).item()
     HF.set_precision(prec)
-    quality = {"msssim_delta": round(abs(m_gpu - m_ref), 6), "msssim_gpu": round(m_gpu, 6), "msssim_ref": round(m_ref, 6),
-               "msssim_gpu_vs_ref": round(O.ms_ssim(((fg + 1) / 2).clamp(0, 1), ((fo + 1) / 2).clamp(0, 1)).item(), 6),
-               "steps": steps, "batch": batch, "size": size, "init": "reference N(0,0.02) recipe", "precision": prec,
-               "ref": "oracle/dsgan_cpu.py fp32 (%d threads)" % threads, "seconds": round(time.time() - t0, 1)}
-    a, b = timed
-    ts = sum(cpu_s[a:b])
-    cpu = dict(value=round(batch * (b - a) / ts, 4), unit="img/s", cores=threads, kind="port",
-               sample="oracle/dsgan_cpu.py OracleStep (a port of the reference step), fp32, %dx%d, batch %d: "
-                      "steps %d-%d of the quality leg's %d (%d warm-up + %d timed, %.1f s), %d host threads"
-                      % (size, size, batch, a + 1, b, steps, a, b - a, ts, threads))
+    try:
+        fg = model.fake_B.detach().float().cpu()
+        fo = ref.fake_B
+        tgt = (B + 1) / 2
+        m_gpu = O.ms_ssim((fg + 1) / 2, tgt).item()
+        m_ref = O.ms_ssim((fo + 1) / 2, tgt).item()
+        quality = {"msssim_delta": round(abs(m_gpu - m_ref), 6), "msssim_gpu": round(m_gpu, 6),
+                   "msssim_ref": round(m_ref, 6),
+                   "msssim_gpu_vs_ref": round(O.ms_ssim(((fg + 1) / 2).clamp(0, 1), ((fo + 1) / 2).clamp(0, 1)).item(), 6),
+                   "steps": steps, "batch": batch, "size": size, "init": "reference N(0,0.02) recipe",
+                   "precision": prec, "ref": "oracle/dsgan_cpu.py fp32 (%d threads)" % threads,
+                   "seconds": round(time.time() - t0, 1)}
+    except Exception as e:  # noqa: BLE001 -- reported in the line, never fatal
+        quality = {"error": repr(e)}
+    try:
+        b = min(timed[1], steps)
+        a = min(timed[0], max(0, b - 1))
+        ts = sum(cpu_s[a:b])
+        cpu = dict(value=round(batch * (b - a) / ts, 4), unit="img/s", cores=threads, kind="port",
+                   cpu_model=host["cpu_model"], physical_cores_allowed=host["physical_cores_allowed"],
+                   logical_cpus_allowed=host["logical_cpus_allowed"], cgroup_cpu_quota=host["cgroup_cpu_quota"],
+                   sample="oracle/dsgan_cpu.py OracleStep (a port of the reference step), fp32, %dx%d, batch %d: "
+                          "steps %d-%d of the quality leg's %d (%d warm-up + %d timed, %.1f s), %d host threads "
+                          "(every physical core this job may use)"
+                          % (size, size, batch, a + 1, b, steps, a, b - a, ts, threads))
+    except Exception as e:  # noqa: BLE001
+        cpu = {"error": repr(e)}
     return quality, cpu
 
 
@@ -120,7 +172,8 @@ def main():
     ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-quality", action="store_true", help="skip the MS-SSIM delta leg")
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=None,
+                    help="oracle threads for cpu_baseline (default: every physical core the job may use)")
     ap.add_argument("--quality-steps", type=int, default=10, help="steps of the shared quality / cpu_baseline leg")
     args = ap.parse_args()
 
@@ -241,7 +294,9 @@ def main():
                 if not args.no_cpu_baseline:
                     out["cpu_baseline"] = cpu
             except Exception as e:  # reported, never fatal to the GPU measurement
-                out["cpu_baseline" if not args.no_cpu_baseline else "quality"] = {"error": repr(e)}
+                for leg, skip in (("quality", args.no_quality), ("cpu_baseline", args.no_cpu_baseline)):
+                    if not skip:
+                        out[leg] = {"error": repr(e)}
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

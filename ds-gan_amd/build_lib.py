@@ -19,8 +19,7 @@ OBJ_DIR = os.path.join(HERE, "build", "obj")
 LIB = os.path.join(OUT_DIR, "libdsgan_hip.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
-FLAGS = ["-O3", "-fPIC", "-std=c++17", "--offload-arch=" + ARCH, "-munsafe-fp-atomics",
-         "-Wno-unused-result", "-I" + CSRC]
+FLAGS = ["-O3", "-fPIC", "-std=c++17", "--offload-arch=" + ARCH, "-Wno-unused-result", "-I" + CSRC]
 
 
 # per-source extra flags

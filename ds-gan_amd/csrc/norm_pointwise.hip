@@ -695,7 +695,8 @@ __global__ __launch_bounds__(256) void ca_fwd_kernel(const float* avg, const flo
   }
 }
 
-// Backward of CA for one sample per block.  Weight grads accumulate (atomics) into dw1/dw2/dpa.
+// Backward of CA for one sample per block.  Weight grads go to per-image partials in ws, summed
+// over images in a fixed order by launch_split_reduce (deterministic, no atomics).
 __global__ __launch_bounds__(256) void ca_bwd_kernel(const float* datt, const float* att,
                                                      const float* avg, const float* mx,
                                                      const float* hsave, const float* w1,

@@ -10,7 +10,8 @@
 //   * wgrad_small: weight-grads with <= 8 channels on one side -- the G head (Cout 3), the
 //     first 1x1 convs from the 3-channel input (to32 / shortcut, MixConvNeXtML.py:124,145) and
 //     the PatchGAN ends.  Workgroup = (big-side channel, pixel chunk); the small side x taps are
-//     register accumulators, reduced once per workgroup and added atomically.
+//     register accumulators, reduced once per workgroup into per-chunk partials that
+//     launch_split_reduce sums in a fixed order (deterministic, no atomics).
 #include "common.h"
 
 namespace dsg {

@@ -39,25 +39,46 @@ def _dist():
 class RankBatchSampler:
     """Global batches of ``sampler`` (batch_size each, the last one ragged), of which this rank
     yields its ``Tensor.chunk`` slice: chunk = ceil(n / world), rank r gets [r*chunk, (r+1)*chunk).
-    A global batch that would leave some rank empty (n <= (world-1)*chunk) is skipped on every
-    rank (the collectives of a step need all ranks).  ``sizes`` queues the global size of each
-    yielded chunk, in order."""
+    ``Tensor.chunk`` leaves trailing ranks EMPTY when n <= (world-1)*chunk (e.g. n=4 over 3 GPUs
+    gives chunks [2, 2]); a step's collectives need every rank, so such a ragged last batch is
+    skipped on every rank, and a batch_size that is itself not viable is refused up front.
+    The epoch's index list is drawn on every rank (same RNG consumption as the 1-process loader)
+    and rank 0's list is broadcast, so the ranks cannot drift apart.  ``sizes`` queues the global
+    size of each yielded chunk, in order."""
 
     def __init__(self, sampler, batch_size, rank, world):
         self.sampler, self.batch_size, self.rank, self.world = sampler, batch_size, rank, world
         self.sizes = collections.deque()
+        if not self.viable(batch_size):
+            raise ValueError(
+                "--batchSize %d (the global batch) cannot be split over %d ranks: Tensor.chunk would leave "
+                "rank(s) without samples (chunk %d); use a batchSize with ceil(B/W)*(W-1) < B, e.g. a multiple of %d"
+                % (batch_size, world, math.ceil(batch_size / world), world))
+
+    def viable(self, n):
+        """True when every rank gets at least one sample of an n-sample global batch."""
+        return n > (self.world - 1) * math.ceil(n / self.world)
 
     def _chunk(self, buf):
         n = len(buf)
-        c = math.ceil(n / self.world)
-        if n <= (self.world - 1) * c:
+        if not self.viable(n):
             return None
+        c = math.ceil(n / self.world)
         return buf[self.rank * c:(self.rank + 1) * c]
+
+    def _epoch_indices(self):
+        idx = list(self.sampler)
+        if self.world > 1 and dist.is_available() and dist.is_initialized():
+            dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend() == "nccl" else torch.device("cpu")
+            t = torch.tensor(idx, dtype=torch.int64, device=dev)
+            dist.broadcast(t, 0)
+            idx = t.cpu().tolist()
+        return idx
 
     def __iter__(self):
         self.sizes.clear()
         buf = []
-        for idx in self.sampler:
+        for idx in self._epoch_indices():
             buf.append(idx)
             if len(buf) == self.batch_size:
                 mine = self._chunk(buf)
@@ -72,9 +93,8 @@ class RankBatchSampler:
                 yield mine
 
     def __len__(self):
-        n = len(self.sampler)
-        full, tail = divmod(n, self.batch_size)
-        return full + (1 if tail and tail > (self.world - 1) * math.ceil(tail / self.world) else 0)
+        full, tail = divmod(len(self.sampler), self.batch_size)
+        return (full if self.viable(self.batch_size) else 0) + (1 if tail and self.viable(tail) else 0)
 
 
 def CreateDataset(opt):

@@ -54,10 +54,11 @@ def _post_scale(buf, W):
         _scale(buf, 1.0 / W)
 
 
-def allreduce_mean_(buf, bucket_mb=32):
-    """In-place mean of a flat fp32 buffer over all ranks (blocking for the caller's stream)."""
+def allreduce_mean_(buf, bucket_mb=32, force=False):
+    """In-place mean of a flat fp32 buffer over all ranks (blocking for the caller's stream).
+    One rank skips the collective unless ``force`` (the 1-rank RCCL test exercises it)."""
     W = world_size()
-    if W == 1:
+    if W == 1 and not force:
         return buf
     n = buf.numel()
     step = max(1, int(bucket_mb * (1 << 20) // 4))

@@ -80,6 +80,9 @@ class Pix2PixModel(BaseModel):
             order = self.netG.backward_order() if hasattr(self.netG, "backward_order") else None
             self.flatG = FlatParams(self.netG, self.device, order=order)
             self.flatD = FlatParams(self.netD, self.device)
+            # the two exchanges run whenever there is more than one rank (``exchange`` can force
+            # them on a 1-rank group: the RCCL stream-ordering test of tests/test_ddp_gpu.py)
+            self.exchange = W > 1
             self.g_buckets = hdist.GradBuckets(self.flatG.grad, self.flatG.layout) if W > 1 else None
             hdist.broadcast_params(self.flatG)
             hdist.broadcast_params(self.flatD)
@@ -172,7 +175,8 @@ class Pix2PixModel(BaseModel):
             self.set_requires_grad(self.netD, True)
             self.optimizer_D.zero_grad()
             self.backward_D()
-            hdist.allreduce_mean_(self.flatD.grad)
+            if self.exchange:
+                hdist.allreduce_mean_(self.flatD.grad, force=True)
             self.optimizer_D.step()
         else:
             self.loss_D_fake = 0

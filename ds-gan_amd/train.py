@@ -100,6 +100,9 @@ def main(argv=None, output_freq=100):
             with torch.no_grad():   # the reference runs this forward with autograd on; output is identical
                 model.get_img_gen(data)
             model.get_img_label(data)
+            # the reference scores image 0 of the GLOBAL batch only (DSGAN/train.py:110-124); under
+            # DDP that image is rank 0's fake_B[0] (Tensor.chunk order), so rank 0's accumulators
+            # are exactly the reference's metric and no cross-rank reduction is needed
             metrics.update(model.fake_B[0], model.real_B[0])
             if (i + 1) % output_freq == 0:
                 losses = global_losses(model.get_current_losses(), int(model.real_A.shape[0]),

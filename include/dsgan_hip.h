@@ -383,8 +383,8 @@ int dsgan_u8_to_image(const unsigned char* src, const int* flip, float* dst, int
  * conversion; part = 128 doubles of scratch.  No host sync. */
 int dsgan_img_metrics(const float* fake, const float* real, int C, int H, int W, double* part, float* acc,
                       hipStream_t stream);
-/* MS-SSIM evaluation of (a*real+b, a*fake+b), DSGAN/MS_SSIM.py:153-225 (ms_ssim; no gradient):
- * per scale the SSIM / contrast-structure plane means, then the padded 2x2 average pool;
+/* MS-SSIM evaluation of (a*real+b, a*fake+b), DSGAN/MS_SSIM.py:153-225 (ms_ssim, forward only;
+ * the differentiable form is dsgan_ms_ssim_fwd_train + dsgan_ms_ssim_bwd below): per scale the SSIM / contrast-structure plane means, then the padded 2x2 average pool;
  * weights_host = the level weights (host array, levels <= 8).  work: dsgan_ms_ssim_workspace
  * floats, stats: 2*levels*N*C floats, out: N+1 floats (per image, then the batch mean). */
 long dsgan_ms_ssim_workspace(int N, int C, int H, int W);

@@ -9,8 +9,18 @@ DSGAN/models/networks.py:74-77, computes every loss on the gathered global batch
     DSGAN/models/pix2pix_model.py:189-191: the per-rank TV coefficient carries the world size);
   * the post-step D (and G) parameters are identical on both ranks and equal the single run's --
     the G step reads the updated D, so an exchange that landed after optimizer_D.step would show.
-fp32 mode, pool_size 0, "fanin" weight recipe; bars are fp32 reassociation level (the batch sum
-of every weight-grad is split differently across the two runs).
+fp32 mode, pool_size 0, "fanin" weight recipe.  Gradients are compared PER TENSOR with the bars of
+test_model_gpu.py::test_full_step_fp32_vs_oracle (2e-3 of the tensor's norm, or 8x its measured
+fp32 conditioning): the batch sum of every weight-grad is split differently across the two runs,
+so they differ at fp32 reassociation level, but a bucket that fired before one of its tensors'
+grads landed would leave that tensor at half its value.
+
+``test_one_rank_rccl_exchange_is_bitwise_neutral`` runs the RCCL ("nccl") branch itself on the
+one GPU: a 1-rank group with the D all-reduce (ReduceOp.AVG) and the G buckets (async, started
+from the autograd thread during backward_G) forced on must give bitwise the flat gradients and
+post-step parameters of the same step without any exchange -- a bucket launched on RCCL's stream
+before its weight-grad kernels finished, or an optimizer step that did not wait for it, changes
+bits.
 """
 import os
 import random
@@ -23,7 +33,7 @@ pytestmark = pytest.mark.gpu
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def _model():
+def _model(precision="fp32"):
     import dsgan_hip
     from oracle import dsgan_cpu as O
     from oracle.recipe import make_params
@@ -32,7 +42,7 @@ def _model():
     dsgan_hip.require_gpu()
     random.seed(20)
     torch.manual_seed(20)
-    m = create_model(default_train_opt(gpu_ids=[0], pool_size=0, precision="fp32", batchSize=2))
+    m = create_model(default_train_opt(gpu_ids=[0], pool_size=0, precision=precision, batchSize=2))
     with torch.no_grad():
         for net, pr in ((m.netG, make_params(O.g_param_spec(), "fanin", 1000)),
                         (m.netD, make_params(O.d_param_spec(), "fanin", 5000)),
@@ -44,7 +54,9 @@ def _model():
 
 def _grads_and_params(m):
     torch.cuda.synchronize()
-    return {"gG": torch.cat([p.grad.detach().flatten() for p in m.netG.parameters()]).cpu(),
+    return {"tG": {k: p.grad.detach().cpu().clone() for k, p in m.netG.named_parameters()},
+            "tD": {k: p.grad.detach().cpu().clone() for k, p in m.netD.named_parameters()},
+            "gG": torch.cat([p.grad.detach().flatten() for p in m.netG.parameters()]).cpu(),
             "gD": torch.cat([p.grad.detach().flatten() for p in m.netD.parameters()]).cpu(),
             "pG": torch.cat([p.detach().flatten() for p in m.netG.parameters()]).cpu(),
             "pD": torch.cat([p.detach().flatten() for p in m.netD.parameters()]).cpu(),
@@ -100,9 +112,20 @@ def test_two_ranks_equal_one_process(tmp_path):
         assert torch.equal(r0[k], r1[k]), k
     # the mean of the per-rank losses is the global-batch loss
     assert abs(0.5 * (r0["loss_D"] + r1["loss_D"]) - one["loss_D"]) <= 1e-5 * abs(one["loss_D"])
-    # averaged gradients == one process on the whole batch (fp32 reassociation level)
+    # averaged gradients == one process on the whole batch, per tensor (fp32 reassociation level)
     assert _rel(r0["gD"], one["gD"]) < 2e-5, _rel(r0["gD"], one["gD"])
     assert _rel(r0["gG"], one["gG"]) < 1e-3, _rel(r0["gG"], one["gG"])
+    from oracle import dsgan_cpu as O
+    from oracle.recipe import make_params
+    from test_model_gpu import fp32_sensitivity
+    sens, _ = fp32_sensitivity(make_params(O.g_param_spec(), "fanin", 1000), make_params(O.d_param_spec(), "fanin", 5000),
+                               A, B)
+    for tag in ("G", "D"):
+        for k, g1 in one["t" + tag].items():
+            g2 = r0["t" + tag][k]
+            err = (g2.double() - g1.double()).norm().item()
+            bar = max(2e-3 * g1.double().norm().item(), 8 * sens[(tag, k)]) + 1e-6
+            assert err <= bar, (tag, k, err, bar)
     # post-step parameters: the D step used the exchanged gradient (Adam's first step is
     # lr * sign(g): equal wherever |g| is above fp32 noise)
     big = one["gD"].abs() > 1e-6
@@ -110,3 +133,48 @@ def test_two_ranks_equal_one_process(tmp_path):
     bigG = one["gG"].abs() > 1e-5
     frac = ((r0["pG"][bigG] - one["pG"][bigG]).abs() > 1e-6).double().mean().item()
     assert frac < 1e-3, frac
+
+
+def _nccl_worker(port, out_dir):
+    import sys
+    sys.path[:0] = [REPO, os.path.join(REPO, "ds-gan_amd")]
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    assert dist.get_backend() == "nccl"
+    from oracle.recipe import synth_pair
+    from dsgan_hip import dist as hdist
+    res = {}
+    for mode in ("plain", "exchange", "plain2"):
+        m = _model("bf16")
+        if mode == "exchange":
+            m.exchange = True
+            # small buckets: several async RCCL all-reduces start during backward_G
+            m.g_buckets = hdist.GradBuckets(m.flatG.grad, m.flatG.layout, bucket_mb=4)
+            assert len(m.g_buckets.buckets) >= 8
+        for it in range(2):
+            A, B = synth_pair(2, 64, seed=40 + it)
+            m.set_input({"A": A.cuda(), "B": B.cuda(), "A_paths": ["a"] * 2, "B_paths": ["b"] * 2})
+            m.optimize_parameters()
+            if mode == "exchange":
+                assert m.g_buckets.pending is None
+        torch.cuda.synchronize()
+        res[mode] = {"gG": m.flatG.grad.detach().cpu().clone(), "gD": m.flatD.grad.detach().cpu().clone(),
+                     "pG": m.flatG.data.detach().cpu().clone(), "pD": m.flatD.data.detach().cpu().clone()}
+    torch.save(res, os.path.join(out_dir, "nccl.pt"))
+    dist.destroy_process_group()
+
+
+def test_one_rank_rccl_exchange_is_bitwise_neutral(tmp_path):
+    import multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    port = 36000 + random.randint(0, 2000)
+    p = ctx.Process(target=_nccl_worker, args=(port, str(tmp_path)))
+    p.start()
+    p.join(timeout=240)
+    assert p.exitcode == 0, p.exitcode
+    r = torch.load(tmp_path / "nccl.pt", weights_only=True)
+    for k in ("gG", "gD", "pG", "pD"):
+        assert torch.equal(r["plain"][k], r["plain2"][k]), ("step not deterministic", k)
+        assert torch.equal(r["plain"][k], r["exchange"][k]), k

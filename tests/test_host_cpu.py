@@ -164,6 +164,11 @@ def test_rank_batch_sampler_matches_global_batches():
         assert per_rank[0][1] == [len(b) for b in kept]
         for b, chunks in zip(kept, zip(*[pr[0] for pr in per_rank])):
             assert [len(c) for c in chunks] == [len(t) for t in torch.arange(len(b)).chunk(W)] + [0] * (W - len(torch.arange(len(b)).chunk(W)))
+    # a global batch size that Tensor.chunk cannot spread over every rank is refused, not
+    # silently skipped every step (B=1 over 2 ranks is the reference default under torchrun)
+    for B, W in ((1, 2), (4, 3), (6, 4), (10, 8)):
+        with pytest.raises(ValueError):
+            RankBatchSampler(list(range(20)), B, 0, W)
 
 
 def _bucket_worker(rank, world, port, q):
