@@ -169,7 +169,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=16, help="per-GPU batch (BASELINE config 2: 16)")
     ap.add_argument("--size", type=int, default=256)
-    ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--precision", default="bf16", choices=["bf16", "fp16", "fp32"],
+                    help="MFMA operand type (fp32 accumulation); configs[4] names fp16")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-quality", action="store_true", help="skip the MS-SSIM delta leg")
     ap.add_argument("--cpu-threads", type=int, default=None,
@@ -224,7 +225,7 @@ def main():
     fams = HF.IGEMM_TIMER.families()
     if rank == 0:
         imgs = args.batch * args.steps * world
-        peak = PEAK_BF16_TFLOPS if args.precision == "bf16" else PEAK_F32_TFLOPS
+        peak = PEAK_F32_TFLOPS if args.precision == "fp32" else PEAK_BF16_TFLOPS   # dense fp16 = bf16 rate
         ach = ig["flops"] / (ig["total_ms"] * 1e-3) / 1e12 if ig["total_ms"] > 0 else 0.0
         # dominant kernel: the contraction family with the most time in the timed steps; its
         # roofline bound is whichever resource its algorithmic work needs longest at peak
@@ -280,7 +281,10 @@ def main():
                                            "configs[3] shape: 256x256, batch 32/GPU (VGG16 perceptual + SSIM; "
                                            "--ssim_loss ms_ssim is the MS-SSIM opt-in)"
                                            if (args.size, args.batch) == (256, 32) else
-                                           "configs[4] shape (512x512, batch 8/GPU) in bf16 -- NOT configs[4] as named (fp16 is not implemented)"
+                                           ("configs[4]: 512x512 upsampled, batch 8/GPU, fp16 MFMA operands (%dxMI355X)" % world
+                                            if args.precision == "fp16" else
+                                            "configs[4] shape (512x512, batch 8/GPU) in %s (configs[4] names fp16: "
+                                            "--precision fp16)" % args.precision)
                                            if (args.size, args.batch) == (512, 8) else
                                            "off-baseline shape %dx%d, batch %d" % (args.size, args.size, args.batch))},
             "roofline": roof,

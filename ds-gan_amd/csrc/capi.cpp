@@ -1,10 +1,17 @@
 // C-ABI plumbing shared by every entry point of libdsgan_hip.so: thread-local last error,
-// library version, and a device-count probe used by the host side to fail loudly.
+// library version, the process-wide 16-bit operand type (common.h HalfType), and a
+// device-count probe used by the host side to fail loudly.
 #include <hip/hip_runtime.h>
 #include <stdarg.h>
 #include <stdio.h>
+#include <atomic>
 
 static thread_local char g_err[512] = "";
+// The one piece of library state besides the error string: which 16-bit type the "bf16" operand
+// flags and the 16-bit MFMAs mean.  Set by the host when it selects a precision
+// (dsgan_hip.functional.set_precision) and read by every launcher when it picks a kernel
+// instantiation; launches are stream-ordered, so a change applies to launches issued after it.
+static std::atomic<int> g_half{0};
 
 void dsgan_set_error(const char* fmt, ...) {
   va_list ap;
@@ -13,7 +20,20 @@ void dsgan_set_error(const char* fmt, ...) {
   va_end(ap);
 }
 
+namespace dsg {
+int half_type() { return g_half.load(std::memory_order_relaxed); }
+}  // namespace dsg
+
 extern "C" {
 const char* dsgan_last_error_string(void) { return g_err; }
-int dsgan_abi_version(void) { return 1; }
+int dsgan_abi_version(void) { return 2; }
+int dsgan_set_half_type(int t) {
+  if (t != 0 && t != 1) {
+    dsgan_set_error("dsgan_set_half_type: %d is not 0 (bf16) or 1 (fp16)", t);
+    return -1;
+  }
+  g_half.store(t, std::memory_order_relaxed);
+  return 0;
+}
+int dsgan_get_half_type(void) { return g_half.load(std::memory_order_relaxed); }
 }

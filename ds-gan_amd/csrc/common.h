@@ -12,6 +12,37 @@ void launch_split_reduce(const float* ws, int splits, long MN, float* dw, hipStr
 void launch_split_reduce_kk(const float* ws, int splits, long MN, float* dw, float* db, int KK1, hipStream_t st);
 
 
+// ---- 16-bit MFMA operand type ------------------------------------------------------------
+// Every "bf16" operand / storage flag and every 16-bit MFMA of the library uses ONE 16-bit type
+// per process, the library's half type (dsgan_set_half_type): bf16 (default; --precision bf16) or
+// IEEE fp16 (--precision fp16, BASELINE configs[4]).  Kernels are templated on it (T16) and the
+// host launchers pick the instantiation from half_type(); both MFMA forms are the gfx950
+// v_mfma_f32_32x32x16_{bf16,f16} (8 operands per lane, fp32 accumulation), so tiles, LDS layouts
+// and the ds_read_b64_tr_b16 transposes are identical.  Conversions from fp32 are
+// round-to-nearest-even in both.
+enum HalfType : int { HALF_BF16 = 0, HALF_F16 = 1 };
+int half_type();   // capi.cpp
+
+template <typename T> using hx8 = T __attribute__((ext_vector_type(8)));
+template <typename T> using hx4 = T __attribute__((ext_vector_type(4)));
+typedef float f32x16_t __attribute__((ext_vector_type(16)));
+__device__ __forceinline__ f32x16_t mfma16(hx8<__bf16> a, hx8<__bf16> b, f32x16_t c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ f32x16_t mfma16(hx8<_Float16> a, hx8<_Float16> b, f32x16_t c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+}
+// a 16-bit value from its raw bits (2-byte buffer loads)
+template <typename T> __device__ __forceinline__ float h2f(unsigned short b) { return (float)__builtin_bit_cast(T, b); }
+template <typename T> __device__ __forceinline__ unsigned short f2h(float v) { return __builtin_bit_cast(unsigned short, (T)v); }
+
+// host dispatch: F(tag) with tag = (__bf16*)0 or (_Float16*)0, e.g.
+//   return with_half([&](auto* t) { using T16 = std::remove_pointer_t<decltype(t)>; ... });
+template <typename F> __host__ inline auto with_half(F&& f) {
+  if (half_type() == HALF_F16) return f((_Float16*)nullptr);
+  return f((__bf16*)nullptr);
+}
+
 enum Act : int { ACT_NONE = 0, ACT_GELU = 1, ACT_RELU = 2, ACT_LRELU = 3, ACT_SIGMOID = 4 };
 
 constexpr float kInvSqrt2 = 0.70710678118654752440f;

@@ -32,9 +32,8 @@
 namespace dsg {
 
 enum Mode : int { FWD = 0, DGRAD = 1, WGRAD = 2, DGRAD2 = 3 };
-enum Prec : int { PREC_F32 = 0, PREC_BF16 = 1 };
+enum Prec : int { PREC_F32 = 0, PREC_BF16 = 1, PREC_F16 = 2 };   // PREC_F16: internal (PREC_BF16 + HALF_F16)
 
-typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 typedef __attribute__((ext_vector_type(16))) float f32x16;
 
 struct GemmArgs {
@@ -59,6 +58,7 @@ struct GemmArgs {
 template <int PREC> struct PT;
 template <> struct PT<PREC_F32>  { using T = float;  static constexpr int BK = 16; };
 template <> struct PT<PREC_BF16> { using T = __bf16; static constexpr int BK = 32; };
+template <> struct PT<PREC_F16>  { using T = _Float16; static constexpr int BK = 32; };
 
 // ---------------------------------------------------------------------------------------
 // Per-thread row state.  Each thread owns fixed (row, k-chunk) items of the A and B tiles for
@@ -254,11 +254,11 @@ template <typename T, int CH>
 __device__ __forceinline__ void store_chunk(T* dst, const float* v) {
   if constexpr (sizeof(T) == 2) {
     // CH == 16 bf16 = 32 bytes -> two 16-byte LDS writes
-    bf16x8 lo, hi;
+    hx8<T> lo, hi;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) { lo[j] = (__bf16)v[j]; hi[j] = (__bf16)v[8 + j]; }
-    reinterpret_cast<bf16x8*>(dst)[0] = lo;
-    reinterpret_cast<bf16x8*>(dst)[1] = hi;
+    for (int j = 0; j < 8; ++j) { lo[j] = (T)v[j]; hi[j] = (T)v[8 + j]; }
+    reinterpret_cast<hx8<T>*>(dst)[0] = lo;
+    reinterpret_cast<hx8<T>*>(dst)[1] = hi;
   } else {
 #pragma unroll
     for (int j = 0; j < CH; j += 4)
@@ -393,21 +393,21 @@ __global__ __launch_bounds__(256) void igemm_kernel(GemmArgs g) {
     if (kt + 1 < nk) gload(kt + 1);
     const T* Ab = As + buf * BM * PADK;
     const T* Bb = Bs + buf * BN * PADK;
-    if constexpr (PREC == PREC_BF16) {
+    if constexpr (PREC != PREC_F32) {
 #pragma unroll
       for (int ks = 0; ks < BK / 16; ++ks) {
-        bf16x8 af[TM], bfr[TN];
+        hx8<T> af[TM], bfr[TN];
 #pragma unroll
         for (int i = 0; i < TM; ++i)
-          af[i] = *reinterpret_cast<const bf16x8*>(Ab + (wm * TM * 32 + i * 32 + lr) * PADK + ks * 16 + lh * 8);
+          af[i] = *reinterpret_cast<const hx8<T>*>(Ab + (wm * TM * 32 + i * 32 + lr) * PADK + ks * 16 + lh * 8);
 #pragma unroll
         for (int j = 0; j < TN; ++j)
-          bfr[j] = *reinterpret_cast<const bf16x8*>(Bb + (wn * TN * 32 + j * 32 + lr) * PADK + ks * 16 + lh * 8);
+          bfr[j] = *reinterpret_cast<const hx8<T>*>(Bb + (wn * TN * 32 + j * 32 + lr) * PADK + ks * 16 + lh * 8);
 #pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll
           for (int j = 0; j < TN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+            acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
       }
     } else {
       // k permuted inside the tile: lane-half h owns k = h*8 + s (s = MFMA sub-step)
@@ -541,7 +541,10 @@ static void launch_cfg(const GemmArgs& g, int splits, hipStream_t st) {
 template <int MODE>
 static void launch_mode(const GemmArgs& g, int prec, int splits, hipStream_t st) {
   const bool pw = MODE != DGRAD2 && g.KH == 1 && g.KW == 1 && g.stride == 1 && g.pad == 0;
-  if (prec == PREC_BF16) {
+  if (prec == PREC_BF16 && half_type() == HALF_F16) {
+    if (pw) launch_cfg<MODE, PREC_F16, true>(g, splits, st);
+    else launch_cfg<MODE, PREC_F16, false>(g, splits, st);
+  } else if (prec == PREC_BF16) {
     if (pw) launch_cfg<MODE, PREC_BF16, true>(g, splits, st);
     else launch_cfg<MODE, PREC_BF16, false>(g, splits, st);
   } else {

@@ -18,12 +18,11 @@
 // Weights are bf16 copies (w1 [4C][C] as nn.Linear stores it, w2 [P][4C]); the same two LDS
 // chunk layouts serve the transposed products of the backward through the transposing LDS read.
 #include "common.h"
+#include <type_traits>
 
 namespace dsg {
 
-typedef __attribute__((ext_vector_type(8))) __bf16 mbf16x8;
-typedef __attribute__((ext_vector_type(4))) __bf16 mbf16x4;
-typedef __attribute__((ext_vector_type(16))) float mf32x16;
+typedef f32x16_t mf32x16;
 typedef __attribute__((ext_vector_type(4))) short ms16x4;
 typedef __attribute__((address_space(3))) ms16x4 lds_ms16x4;
 typedef __attribute__((ext_vector_type(4))) unsigned int mu32x4;   // raw 16 bytes
@@ -31,21 +30,23 @@ typedef __attribute__((ext_vector_type(4))) unsigned int mu32x4;   // raw 16 byt
 // Fragment of a k-major LDS tile T[k][col] (row stride STR elements) for a 32x32x16 MFMA
 // operand: lane (h = lane>>5, c = lane&31) receives T[8h + i][c], i = 0..7, via two
 // ds_read_b64_tr_b16 (see pwgemm.hip).  `p` = T + (ks*16 + 8h + q)*STR + colbase + 16G + 4p.
-__device__ __forceinline__ mbf16x8 mtr_frag(const __bf16* p0, int stride) {
+template <typename T16>
+__device__ __forceinline__ hx8<T16> mtr_frag(const T16* p0, int stride) {
 #if defined(__HIP_DEVICE_COMPILE__)
   ms16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_ms16x4*)(p0));
   ms16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_ms16x4*)(p0 + 4 * stride));
   typedef __attribute__((ext_vector_type(8))) short s16x8;
   s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-  return __builtin_bit_cast(mbf16x8, v);
+  return __builtin_bit_cast(hx8<T16>, v);
 #else
-  return mbf16x8{};
+  return hx8<T16>{};
 #endif
 }
 
-__device__ __forceinline__ mbf16x4 mcvt4(float4 v) {
-  mbf16x4 r;
-  r[0] = (__bf16)v.x; r[1] = (__bf16)v.y; r[2] = (__bf16)v.z; r[3] = (__bf16)v.w;
+template <typename T16>
+__device__ __forceinline__ hx4<T16> mcvt4(float4 v) {
+  hx4<T16> r;
+  r[0] = (T16)v.x; r[1] = (T16)v.y; r[2] = (T16)v.z; r[3] = (T16)v.w;
   return r;
 }
 
@@ -55,13 +56,13 @@ __device__ __forceinline__ mbf16x4 mcvt4(float4 v) {
 struct MlpArgs {
   const void* h; long h_bs;         // [nb][C][HW]   block activation after InstanceNorm (fp32, or bf16 if h_bf16)
   const float* dy; long dy_bs;      // [nb][P][HW]   (backward) upstream grad of the block output
-  const __bf16* w1;                 // [4C][C]
+  const void* w1;                   // [4C][C]   (16-bit: the library's half type)
   const float* b1;                  // [4C]
-  const __bf16* w2;                 // [P][4C]
+  const void* w2;                   // [P][4C]
   const float* b2;                  // [P]           (forward; may be null)
   float* out; long out_bs;          // forward: out [nb][P][HW] (+= when accumulate); backward: dh [nb][C][HW]
-  __bf16* g_out;                    // (backward) gelu(z)  [nb][4C][HW]
-  __bf16* dz_out;                   // (backward) dz       [nb][4C][HW]
+  void* g_out;                      // (backward) gelu(z)  [nb][4C][HW]
+  void* dz_out;                     // (backward) dz       [nb][4C][HW]
   float* bsum;                      // (backward) [ntiles][4C] per-tile sums of dz
   int HW, nb, accumulate;
   int h_bf16;
@@ -76,8 +77,8 @@ __device__ __forceinline__ int xcd_tile(int id, int nwg) {
 }
 
 // Stage a [K][BN] fp32 tile (rows strided by HW) into a k-major bf16 LDS tile [K][STR].
-template <int K, int BN, int STR, int NT>
-__device__ __forceinline__ void stage_rows(__bf16* dst, const float* __restrict__ src, int HW, int tid) {
+template <int K, int BN, int STR, int NT, typename T16>
+__device__ __forceinline__ void stage_rows(T16* dst, const float* __restrict__ src, int HW, int tid) {
   constexpr int ITEMS = K * BN / 4;
   static_assert(ITEMS % NT == 0, "tile must split evenly over the workgroup");
   constexpr int PER = ITEMS / NT;
@@ -95,14 +96,14 @@ __device__ __forceinline__ void stage_rows(__bf16* dst, const float* __restrict_
     for (int i = 0; i < BATCH; ++i) {
       const int it = tid + (i0 + i) * NT;
       const int k = it / (BN / 4), c4 = it % (BN / 4);
-      *reinterpret_cast<mbf16x4*>(dst + k * STR + c4 * 4) = mcvt4(v[i]);
+      *reinterpret_cast<hx4<T16>*>(dst + k * STR + c4 * 4) = mcvt4<T16>(v[i]);
     }
   }
 }
 
 // Same, from a bf16 source (the InstanceNorm's bf16 output): 16-byte items copied unconverted.
-template <int K, int BN, int STR, int NT>
-__device__ __forceinline__ void stage_rows_h16(__bf16* dst, const __bf16* __restrict__ src, int HW, int tid) {
+template <int K, int BN, int STR, int NT, typename T16>
+__device__ __forceinline__ void stage_rows_h16(T16* dst, const T16* __restrict__ src, int HW, int tid) {
   constexpr int ITEMS = K * BN / 8;
   static_assert(ITEMS % NT == 0, "tile must split evenly over the workgroup");
   constexpr int PER = ITEMS / NT;
@@ -125,9 +126,9 @@ __device__ __forceinline__ void stage_rows_h16(__bf16* dst, const __bf16* __rest
   }
 }
 
-template <int K, int BN, int STR, int NT>
-__device__ __forceinline__ void stage_h(__bf16* dst, const MlpArgs& g, int img, int p0, int tid) {
-  if (g.h_bf16) stage_rows_h16<K, BN, STR, NT>(dst, (const __bf16*)g.h + (long)img * g.h_bs + p0, g.HW, tid);
+template <int K, int BN, int STR, int NT, typename T16>
+__device__ __forceinline__ void stage_h(T16* dst, const MlpArgs& g, int img, int p0, int tid) {
+  if (g.h_bf16) stage_rows_h16<K, BN, STR, NT>(dst, (const T16*)g.h + (long)img * g.h_bs + p0, g.HW, tid);
   else stage_rows<K, BN, STR, NT>(dst, (const float*)g.h + (long)img * g.h_bs + p0, g.HW, tid);
 }
 
@@ -141,8 +142,11 @@ struct WCh {
 };
 
 template <int C, int P, int HC, int NT, int N1, int N2>
-__device__ __forceinline__ void wch_load(mu32x4 (&r1)[N1], mu32x4 (&r2)[N2], const __bf16* __restrict__ w1,
-                                         const __bf16* __restrict__ w2, int j, int tid) {
+__device__ __forceinline__ void wch_load(mu32x4 (&r1)[N1], mu32x4 (&r2)[N2], const void* w1v, const void* w2v, int j,
+                                         int tid) {
+  // raw 16-bit elements: the loads move bits, the half type does not matter here
+  const unsigned short* __restrict__ w1 = (const unsigned short*)w1v;
+  const unsigned short* __restrict__ w2 = (const unsigned short*)w2v;
   const mu32x4* s1 = reinterpret_cast<const mu32x4*>(w1 + (long)j * HC * C);
 #pragma unroll
   for (int i = 0; i < N1; ++i) r1[i] = s1[tid + i * NT];
@@ -153,8 +157,8 @@ __device__ __forceinline__ void wch_load(mu32x4 (&r1)[N1], mu32x4 (&r2)[N2], con
   }
 }
 
-template <int C, int P, int HC, int NT, int W1STR, int W2STR, int N1, int N2>
-__device__ __forceinline__ void wch_store(const mu32x4 (&r1)[N1], const mu32x4 (&r2)[N2], __bf16* W1s, __bf16* W2s,
+template <int C, int P, int HC, int NT, int W1STR, int W2STR, int N1, int N2, typename T16>
+__device__ __forceinline__ void wch_store(const mu32x4 (&r1)[N1], const mu32x4 (&r2)[N2], T16* W1s, T16* W2s,
                                           int tid) {
 #pragma unroll
   for (int i = 0; i < N1; ++i) {
@@ -218,21 +222,25 @@ __device__ __forceinline__ unsigned lds_addr(const void* p) {   // LDS byte offs
 // of 1 KB each; the LDS image of one instruction is lane-linear, the swizzle is applied on the
 // per-lane global source address.
 template <int C, int P, int NW, bool QS = true>
-__device__ __forceinline__ void glds_chunk(__bf16* W1d, __bf16* W2d, const __bf16* __restrict__ w1,
-                                           const __bf16* __restrict__ w2, int j, int wave, int lane) {
+__device__ __forceinline__ void glds_chunk(void* W1d, void* W2d, const void* w1v, const void* w2v, int j, int wave,
+                                           int lane) {
+  const unsigned short* __restrict__ w1 = (const unsigned short*)w1v;   // raw 16-bit elements
+  const unsigned short* __restrict__ w2 = (const unsigned short*)w2v;
+  unsigned short* const W1h = (unsigned short*)W1d;
+  unsigned short* const W2h = (unsigned short*)W2d;
   constexpr int S1 = C / 8, R1 = 64 / S1, N1 = C / 8 / NW;
 #pragma unroll
   for (int i = 0; i < N1; ++i) {
     const int inst = wave * N1 + i, r = inst * R1 + lane / S1, ps = lane % S1;
-    const __bf16* src = w1 + ((long)j * 64 + (QS ? qswap(r) : r)) * C + (ps ^ slot_swz<S1>(r)) * 8;
-    glds16(src, lds_addr(W1d + inst * 512));
+    const unsigned short* src = w1 + ((long)j * 64 + (QS ? qswap(r) : r)) * C + (ps ^ slot_swz<S1>(r)) * 8;
+    glds16(src, lds_addr(W1h + inst * 512));
   }
   constexpr int N2 = P / 8 / NW;
 #pragma unroll
   for (int i = 0; i < N2; ++i) {
     const int inst = wave * N2 + i, r = inst * 8 + lane / 8, ps = lane % 8;
-    const __bf16* src = w2 + (long)r * (4 * C) + j * 64 + (ps ^ slot_swz<8>(r)) * 8;
-    glds16(src, lds_addr(W2d + inst * 512));
+    const unsigned short* src = w2 + (long)r * (4 * C) + j * 64 + (ps ^ slot_swz<8>(r)) * 8;
+    glds16(src, lds_addr(W2h + inst * 512));
   }
 }
 
@@ -243,14 +251,16 @@ __device__ __forceinline__ void glds_chunk(__bf16* W1d, __bf16* W2d, const __bf1
 // gelu(z) (see qswap).  The two hidden halves' partial outputs meet once, through LDS, in a fixed
 // order (acc[wm 0] + acc[wm 1]: deterministic).  Weight chunks are double-buffered and filled by
 // LDS-DMA one chunk ahead: one barrier per chunk.
-template <int C, int P, int MINB>
+template <typename T16, int C, int P, int MINB>
 __global__ __launch_bounds__(512, MINB) void mlp_fwd_kernel(MlpArgs g) {
+  typedef hx8<T16> mbf16x8;
+  typedef hx4<T16> mbf16x4;
   constexpr int NW = 8, NT = NW * 64, BN = 128, HC = 64;
   constexpr int C4 = 4 * C, NCH = C4 / HC, KS = C / 16, PT = P / 32;
   constexpr int HSTR = BN + 32;
   constexpr int H_SZ = C * HSTR, W_SZ = HC * C + P * HC, R_SZ = 2 * 4 * PT * 16 * 64;   // bf16 elements
   constexpr int SM = H_SZ > 2 * W_SZ ? (H_SZ > R_SZ ? H_SZ : R_SZ) : (2 * W_SZ > R_SZ ? 2 * W_SZ : R_SZ);
-  __shared__ __attribute__((aligned(16))) __bf16 smem[SM + 2 * (C4 + P)];
+  __shared__ __attribute__((aligned(16))) T16 smem[SM + 2 * (C4 + P)];
   float* b1s = reinterpret_cast<float*>(smem + SM);   // b1 [C4], then b2 [P]: no global load is in
   float* b2s = b1s + C4;                              // flight in the loop besides the LDS-DMA
   static_assert(C % 64 == 0 && P % 64 == 0 && NCH >= 2, "tile shape");
@@ -286,8 +296,8 @@ __global__ __launch_bounds__(512, MINB) void mlp_fwd_kernel(MlpArgs g) {
   __builtin_amdgcn_s_barrier();
 
   for (int j = 0; j < NCH; ++j) {
-    const __bf16* W1c = smem + (j & 1) * W_SZ;
-    const __bf16* W2c = W1c + HC * C;
+    const T16* W1c = smem + (j & 1) * W_SZ;
+    const T16* W2c = W1c + HC * C;
     mf32x16 zacc;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {   // bias of physical rows wm*32 + 8q + 4lh + e (qswap order)
@@ -299,7 +309,7 @@ __global__ __launch_bounds__(512, MINB) void mlp_fwd_kernel(MlpArgs g) {
     for (int ks = 0; ks < KS; ++ks) {
       const mbf16x8 a =
           *reinterpret_cast<const mbf16x8*>(W1c + r1 * C + ((ks * 2 + lh) ^ slot_swz<C / 8>(r1)) * 8);
-      zacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, hb[ks], zacc, 0, 0, 0);
+      zacc = mfma16(a, hb[ks], zacc);
     }
     // gelu of k slice kk -> its GEMM2 MFMAs (the second slice's VALU overlaps the first's MFMAs)
 #pragma unroll
@@ -308,15 +318,15 @@ __global__ __launch_bounds__(512, MINB) void mlp_fwd_kernel(MlpArgs g) {
 #pragma unroll
       for (int i = 0; i < 8; i += 2) {
         const f32x2 v = gelu_fast2(f32x2{zacc[8 * kk + i], zacc[8 * kk + i + 1]});
-        gb[i] = (__bf16)v.x;
-        gb[i + 1] = (__bf16)v.y;
+        gb[i] = (T16)v.x;
+        gb[i + 1] = (T16)v.y;
       }
 #pragma unroll
       for (int pt = 0; pt < PT; ++pt) {
         const int r2 = pt * 32 + lr;
         const mbf16x8 a = *reinterpret_cast<const mbf16x8*>(
             W2c + r2 * HC + ((wm * 4 + kk * 2 + lh) ^ slot_swz<8>(r2)) * 8);
-        oacc[pt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, gb, oacc[pt], 0, 0, 0);
+        oacc[pt] = mfma16(a, gb, oacc[pt]);
       }
     }
     // chunk j+1 landed (each wave waits for its own DMA; the barrier makes all of it visible) and
@@ -324,7 +334,7 @@ __global__ __launch_bounds__(512, MINB) void mlp_fwd_kernel(MlpArgs g) {
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     if (j + 2 < NCH) {
-      __bf16* W1n = smem + (j & 1) * W_SZ;
+      T16* W1n = smem + (j & 1) * W_SZ;
       glds_chunk<C, P, NW>(W1n, W1n + HC * C, g.w1, g.w2, j + 2, wave, lane);
     }
   }
@@ -354,19 +364,21 @@ __global__ __launch_bounds__(512, MINB) void mlp_fwd_kernel(MlpArgs g) {
 // mlp_fwd_kernel costs the second workgroup per CU): h staged once into LDS and read by every
 // chunk's GEMM1; gelu(z) goes through an LDS chunk buffer (aliasing the W1 chunk) to GEMM2; weight
 // chunks register-prefetched one chunk ahead.
-template <int C, int P, int BN, int HC, int NW, int MINB>
+template <typename T16, int C, int P, int BN, int HC, int NW, int MINB>
 __global__ __launch_bounds__(NW * 64, MINB) void mlp_fwd_lds_kernel(MlpArgs g) {
+  typedef hx8<T16> mbf16x8;
+  typedef hx4<T16> mbf16x4;
   constexpr int NT = NW * 64;
   constexpr int C4 = 4 * C, NCH = C4 / HC;
   constexpr int HSTR = BN + 32, GSTR = HC + 8, W1STR = C + 8, W2STR = HC + 8;
   constexpr int H_SZ = C * HSTR, G_SZ = BN * GSTR, W1_SZ = HC * W1STR, W2_SZ = P * W2STR;
   // the g chunk overwrites the W1 chunk once GEMM1 is done with it
   constexpr int GW_SZ = G_SZ > W1_SZ ? G_SZ : W1_SZ;
-  __shared__ __attribute__((aligned(16))) __bf16 smem[H_SZ + GW_SZ + W2_SZ];
-  __bf16* Hs = smem;
-  __bf16* Gs = Hs + H_SZ;
-  __bf16* W1s = Gs;
-  __bf16* W2s = Gs + GW_SZ;
+  __shared__ __attribute__((aligned(16))) T16 smem[H_SZ + GW_SZ + W2_SZ];
+  T16* Hs = smem;
+  T16* Gs = Hs + H_SZ;
+  T16* W1s = Gs;
+  T16* W2s = Gs + GW_SZ;
 
   using ZG = WGrid<HC, BN, NW>;   // z chunk [HC x BN]
   using OG = WGrid<P, BN, NW>;    // out tile [P x BN]
@@ -428,7 +440,7 @@ __global__ __launch_bounds__(NW * 64, MINB) void mlp_fwd_lds_kernel(MlpArgs g) {
       for (int i = 0; i < ZG::TM; ++i)
 #pragma unroll
         for (int t = 0; t < ZG::TN; ++t)
-          zacc[i][t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bf[t], zacc[i][t], 0, 0, 0);
+          zacc[i][t] = mfma16(af[i], bf[t], zacc[i][t]);
     }
     __syncthreads();   // every wave is done reading W1s (Gs aliases it)
     // ---- GELU -> Gs (pixel-major [BN][GSTR]) ----
@@ -443,8 +455,8 @@ __global__ __launch_bounds__(NW * 64, MINB) void mlp_fwd_lds_kernel(MlpArgs g) {
 #pragma unroll
           for (int e = 0; e < 4; e += 2) {
             const f32x2 gv = gelu_fast2(f32x2{zacc[i][t][4 * q + e], zacc[i][t][4 * q + e + 1]});
-            v[e] = (__bf16)gv.x;
-            v[e + 1] = (__bf16)gv.y;
+            v[e] = (T16)gv.x;
+            v[e + 1] = (T16)gv.y;
           }
           *reinterpret_cast<mbf16x4*>(Gs + n * GSTR + wm * (HC / 2) + i * 32 + 8 * q + 4 * lh) = v;
         }
@@ -464,7 +476,7 @@ __global__ __launch_bounds__(NW * 64, MINB) void mlp_fwd_lds_kernel(MlpArgs g) {
       for (int i = 0; i < OG::TM; ++i)
 #pragma unroll
         for (int t = 0; t < OG::TN; ++t)
-          oacc[i][t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bf[t], oacc[i][t], 0, 0, 0);
+          oacc[i][t] = mfma16(af[i], bf[t], oacc[i][t]);
     }
     __syncthreads();
     if (j + 1 < NCH) {
@@ -494,39 +506,39 @@ __global__ __launch_bounds__(NW * 64, MINB) void mlp_fwd_lds_kernel(MlpArgs g) {
 // receives T[k0 + 4h + i][col0 + c] (i < 4) and T[k0 + 8 + 4h + i - 4][col0 + c] (i >= 4) -- the k
 // order in which a 32x32 accumulator lane half holds rows 16kk + {4h + e, 8 + 4h + e}, so that
 // accumulator, converted, is the matching B fragment (see mlp_dh_kernel).
-template <int S>
-__device__ __forceinline__ mbf16x8 mtr_frag_q(const __bf16* T, int k0, int col0, int lane) {
+template <int S, typename T16>
+__device__ __forceinline__ hx8<T16> mtr_frag_q(const T16* T, int k0, int col0, int lane) {
 #if defined(__HIP_DEVICE_COMPILE__)
   const int tq = (lane >> 2) & 3, tp = lane & 3, tG = (lane >> 4) & 1, h = lane >> 5;
   const int col = col0 + 16 * tG + 4 * tp;
   const int rlo = k0 + 4 * h + tq, rhi = rlo + 8;
-  const __bf16* plo = T + rlo * (S * 8) + (((col >> 3) ^ slot_swz<S>(rlo)) << 3) + (col & 7);
-  const __bf16* phi = T + rhi * (S * 8) + (((col >> 3) ^ slot_swz<S>(rhi)) << 3) + (col & 7);
+  const T16* plo = T + rlo * (S * 8) + (((col >> 3) ^ slot_swz<S>(rlo)) << 3) + (col & 7);
+  const T16* phi = T + rhi * (S * 8) + (((col >> 3) ^ slot_swz<S>(rhi)) << 3) + (col & 7);
   ms16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_ms16x4*)(plo));
   ms16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_ms16x4*)(phi));
   typedef __attribute__((ext_vector_type(8))) short s16x8;
   s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-  return __builtin_bit_cast(mbf16x8, v);
+  return __builtin_bit_cast(hx8<T16>, v);
 #else
-  return mbf16x8{};
+  return hx8<T16>{};
 #endif
 }
 // Same, plain k order: lane (c, h) receives T[k0 + 8h + i][col0 + c], i = 0..7.
-template <int S>
-__device__ __forceinline__ mbf16x8 mtr_frag_s(const __bf16* T, int k0, int col0, int lane) {
+template <int S, typename T16>
+__device__ __forceinline__ hx8<T16> mtr_frag_s(const T16* T, int k0, int col0, int lane) {
 #if defined(__HIP_DEVICE_COMPILE__)
   const int tq = (lane >> 2) & 3, tp = lane & 3, tG = (lane >> 4) & 1, h = lane >> 5;
   const int col = col0 + 16 * tG + 4 * tp;
   const int rlo = k0 + 8 * h + tq, rhi = rlo + 4;
-  const __bf16* plo = T + rlo * (S * 8) + (((col >> 3) ^ slot_swz<S>(rlo)) << 3) + (col & 7);
-  const __bf16* phi = T + rhi * (S * 8) + (((col >> 3) ^ slot_swz<S>(rhi)) << 3) + (col & 7);
+  const T16* plo = T + rlo * (S * 8) + (((col >> 3) ^ slot_swz<S>(rlo)) << 3) + (col & 7);
+  const T16* phi = T + rhi * (S * 8) + (((col >> 3) ^ slot_swz<S>(rhi)) << 3) + (col & 7);
   ms16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_ms16x4*)(plo));
   ms16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_ms16x4*)(phi));
   typedef __attribute__((ext_vector_type(8))) short s16x8;
   s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-  return __builtin_bit_cast(mbf16x8, v);
+  return __builtin_bit_cast(hx8<T16>, v);
 #else
-  return mbf16x8{};
+  return hx8<T16>{};
 #endif
 }
 
@@ -540,14 +552,16 @@ __device__ __forceinline__ mbf16x8 mtr_frag_s(const __bf16* T, int k0, int col0,
 //   registers (packed fp32), dh[:, wn cols] += W1^T dz with dz as the B operand straight from the
 //   accumulators (mtr_frag_q reads W1 in the accumulator's k order).
 // The two hidden halves' partial dh meet once, through LDS, in a fixed order (deterministic).
-template <int C, int P, int MINB>
+template <typename T16, int C, int P, int MINB>
 __global__ __launch_bounds__(512, MINB) void mlp_dh_kernel(MlpArgs g) {
+  typedef hx8<T16> mbf16x8;
+  typedef hx4<T16> mbf16x4;
   constexpr int NW = 8, NT = NW * 64, BN = 128, HC = 64;
   constexpr int C4 = 4 * C, NCH = C4 / HC, KS = C / 16, PS = P / 16, CT = C / 32;
   constexpr int HSTR = BN + 32;
   constexpr int ST_SZ = (C + P) * HSTR, W_SZ = HC * C + P * HC, R_SZ = 2 * 4 * CT * 16 * 64;   // bf16 elements
   constexpr int SM = ST_SZ > 2 * W_SZ ? (ST_SZ > R_SZ ? ST_SZ : R_SZ) : (2 * W_SZ > R_SZ ? 2 * W_SZ : R_SZ);
-  __shared__ __attribute__((aligned(16))) __bf16 smem[SM + 2 * C4];
+  __shared__ __attribute__((aligned(16))) T16 smem[SM + 2 * C4];
   float* b1s = reinterpret_cast<float*>(smem + SM);
   static_assert(C % 64 == 0 && P % 64 == 0 && NCH >= 2, "tile shape");
 
@@ -560,8 +574,8 @@ __global__ __launch_bounds__(512, MINB) void mlp_dh_kernel(MlpArgs g) {
   const int tile = xcd_tile(blockIdx.x, gridDim.x);
   const int img = tile / tpi, p0 = (tile - img * tpi) * BN;
 
-  __bf16* Hs = smem;
-  __bf16* Ds = smem + C * HSTR;
+  T16* Hs = smem;
+  T16* Ds = smem + C * HSTR;
   stage_h<C, BN, HSTR, NT>(Hs, g, img, p0, tid);
   stage_rows<P, BN, HSTR, NT>(Ds, g.dy + (long)img * g.dy_bs + p0, g.HW, tid);
   for (int i = tid; i < C4; i += NT) b1s[i] = g.b1[i];
@@ -586,8 +600,8 @@ __global__ __launch_bounds__(512, MINB) void mlp_dh_kernel(MlpArgs g) {
   __builtin_amdgcn_s_barrier();
 
   for (int j = 0; j < NCH; ++j) {
-    const __bf16* W1c = smem + (j & 1) * W_SZ;
-    const __bf16* W2c = W1c + HC * C;
+    const T16* W1c = smem + (j & 1) * W_SZ;
+    const T16* W2c = W1c + HC * C;
     mf32x16 zacc, tacc;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
@@ -601,12 +615,12 @@ __global__ __launch_bounds__(512, MINB) void mlp_dh_kernel(MlpArgs g) {
     for (int ks = 0; ks < KS; ++ks) {
       const mbf16x8 a =
           *reinterpret_cast<const mbf16x8*>(W1c + r1 * C + ((ks * 2 + lh) ^ slot_swz<C / 8>(r1)) * 8);
-      zacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, hb[ks], zacc, 0, 0, 0);
+      zacc = mfma16(a, hb[ks], zacc);
     }
 #pragma unroll
     for (int ks = 0; ks < PS; ++ks) {   // A[m = hidden][k = p] = W2[p][hidden]: transposed read of W2c
       const mbf16x8 a = mtr_frag_s<8>(W2c, ks * 16, wm * 32, lane);
-      tacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, db[ks], tacc, 0, 0, 0);
+      tacc = mfma16(a, db[ks], tacc);
     }
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
@@ -616,19 +630,19 @@ __global__ __launch_bounds__(512, MINB) void mlp_dh_kernel(MlpArgs g) {
         f32x2 gv, gp;
         gelu_pair_fast2(f32x2{zacc[8 * kk + i], zacc[8 * kk + i + 1]}, gv, gp);
         const f32x2 dz = f32x2{tacc[8 * kk + i], tacc[8 * kk + i + 1]} * gp;
-        dzb[i] = (__bf16)dz.x;
-        dzb[i + 1] = (__bf16)dz.y;
+        dzb[i] = (T16)dz.x;
+        dzb[i + 1] = (T16)dz.y;
       }
 #pragma unroll
       for (int ct = 0; ct < CT; ++ct) {   // A[m = c][k = hidden] = W1[hidden][c], in dz's k order
         const mbf16x8 a = mtr_frag_q<C / 8>(W1c, wm * 32 + 16 * kk, ct * 32, lane);
-        hacc[ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, dzb, hacc[ct], 0, 0, 0);
+        hacc[ct] = mfma16(a, dzb, hacc[ct]);
       }
     }
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     if (j + 2 < NCH) {
-      __bf16* W1n = smem + (j & 1) * W_SZ;
+      T16* W1n = smem + (j & 1) * W_SZ;
       glds_chunk<C, P, NW, false>(W1n, W1n + HC * C, g.w1, g.w2, j + 2, wave, lane);
     }
   }
@@ -657,19 +671,21 @@ __global__ __launch_bounds__(512, MINB) void mlp_dh_kernel(MlpArgs g) {
 // GD: also write g and dz (bf16) and the b1 partial sums for the weight-grad GEMMs; without it the
 // kernel writes dh only (mlp_wgrad_kernel recomputes what the weight path needs), drops the g
 // chunk buffer and fits two workgroups per CU (MINB) where the tiles allow.
-template <int C, int P, int BN, int HC, int NW, bool GD, int MINB>
+template <typename T16, int C, int P, int BN, int HC, int NW, bool GD, int MINB>
 __global__ __launch_bounds__(NW * 64, MINB) void mlp_bwd_kernel(MlpArgs g) {
+  typedef hx8<T16> mbf16x8;
+  typedef hx4<T16> mbf16x4;
   constexpr int NT = NW * 64;
   constexpr int C4 = 4 * C, NCH = C4 / HC;
   constexpr int HSTR = BN + 32, NSTR = HC + 8, W1STR = C + 8, W2STR = HC + 8;
   constexpr int H_SZ = C * HSTR, D_SZ = P * HSTR, N_SZ = BN * NSTR, W1_SZ = HC * W1STR, W2_SZ = P * W2STR;
-  __shared__ __attribute__((aligned(16))) __bf16 smem[H_SZ + D_SZ + (GD ? 2 : 1) * N_SZ + W1_SZ + W2_SZ];
-  __bf16* Hs = smem;
-  __bf16* Ds = Hs + H_SZ;
-  __bf16* Zn = Ds + D_SZ;                 // dz chunk, pixel-major [BN][NSTR]
-  __bf16* Gn = Zn + (GD ? N_SZ : 0);      // g chunk,  pixel-major [BN][NSTR] (GD only)
-  __bf16* W1s = Zn + (GD ? 2 : 1) * N_SZ;
-  __bf16* W2s = W1s + W1_SZ;
+  __shared__ __attribute__((aligned(16))) T16 smem[H_SZ + D_SZ + (GD ? 2 : 1) * N_SZ + W1_SZ + W2_SZ];
+  T16* Hs = smem;
+  T16* Ds = Hs + H_SZ;
+  T16* Zn = Ds + D_SZ;                 // dz chunk, pixel-major [BN][NSTR]
+  T16* Gn = Zn + (GD ? N_SZ : 0);      // g chunk,  pixel-major [BN][NSTR] (GD only)
+  T16* W1s = Zn + (GD ? 2 : 1) * N_SZ;
+  T16* W2s = W1s + W1_SZ;
 
   using ZG = WGrid<HC, BN, NW>;   // z / t chunk [HC x BN]
   using HG = WGrid<C, BN, NW>;    // dh tile [C x BN]
@@ -734,7 +750,7 @@ __global__ __launch_bounds__(NW * 64, MINB) void mlp_bwd_kernel(MlpArgs g) {
       for (int i = 0; i < ZG::TM; ++i)
 #pragma unroll
         for (int t = 0; t < ZG::TN; ++t)
-          zacc[i][t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bf[t], zacc[i][t], 0, 0, 0);
+          zacc[i][t] = mfma16(af[i], bf[t], zacc[i][t]);
     }
 #pragma unroll 4
     for (int ks = 0; ks < P / 16; ++ks) {
@@ -749,7 +765,7 @@ __global__ __launch_bounds__(NW * 64, MINB) void mlp_bwd_kernel(MlpArgs g) {
       for (int i = 0; i < ZG::TM; ++i)
 #pragma unroll
         for (int t = 0; t < ZG::TN; ++t)
-          tacc[i][t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bf[t], tacc[i][t], 0, 0, 0);
+          tacc[i][t] = mfma16(af[i], bf[t], tacc[i][t]);
     }
     // ---- epilogue: g = gelu(z), dz = t * gelu'(z) -> LDS, pixel-major, 4 hidden per write ----
 #pragma unroll
@@ -765,8 +781,8 @@ __global__ __launch_bounds__(NW * 64, MINB) void mlp_bwd_kernel(MlpArgs g) {
             f32x2 gv, gp;
             gelu_pair_fast2(f32x2{zacc[i][t][4 * q + e], zacc[i][t][4 * q + e + 1]}, gv, gp);
             const f32x2 dz = f32x2{tacc[i][t][4 * q + e], tacc[i][t][4 * q + e + 1]} * gp;
-            gv4[e] = (__bf16)gv.x; gv4[e + 1] = (__bf16)gv.y;
-            dv4[e] = (__bf16)dz.x; dv4[e + 1] = (__bf16)dz.y;
+            gv4[e] = (T16)gv.x; gv4[e + 1] = (T16)gv.y;
+            dv4[e] = (T16)dz.x; dv4[e + 1] = (T16)dz.y;
           }
           const int m = wm * (HC / 2) + i * 32 + 8 * q + 4 * lh;
           if constexpr (GD) *reinterpret_cast<mbf16x4*>(Gn + n * NSTR + m) = gv4;
@@ -786,8 +802,8 @@ __global__ __launch_bounds__(NW * 64, MINB) void mlp_bwd_kernel(MlpArgs g) {
         const mbf16x8 gv = mtr_frag(Gn + off, NSTR);
         const mbf16x8 dv = mtr_frag(Zn + off, NSTR);
         const long o = gbase + (long)(j * HC + chh + lr) * g.HW + pb + 8 * lh;
-        *reinterpret_cast<mbf16x8*>(g.g_out + o) = gv;
-        *reinterpret_cast<mbf16x8*>(g.dz_out + o) = dv;
+        *reinterpret_cast<mbf16x8*>((T16*)g.g_out + o) = gv;
+        *reinterpret_cast<mbf16x8*>((T16*)g.dz_out + o) = dv;
 #pragma unroll
         for (int e = 0; e < 8; ++e) bacc += (float)dv[e];
       }
@@ -808,7 +824,7 @@ __global__ __launch_bounds__(NW * 64, MINB) void mlp_bwd_kernel(MlpArgs g) {
       for (int i = 0; i < HG::TM; ++i)
 #pragma unroll
         for (int t = 0; t < HG::TN; ++t)
-          hacc[i][t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bf[t], hacc[i][t], 0, 0, 0);
+          hacc[i][t] = mfma16(af[i], bf[t], hacc[i][t]);
     }
     __syncthreads();
     if (j + 1 < NCH) {
@@ -856,13 +872,13 @@ struct TileLd {   // a [K][BN] activation tile (rows strided by HW), fp32 or bf1
       v[i] = *reinterpret_cast<const mu32x4*>(p);
     }
   }
-  template <int STR>
-  __device__ __forceinline__ void store(__bf16* dst, int tid) const {
+  template <int STR, typename T16>
+  __device__ __forceinline__ void store(T16* dst, int tid) const {
 #pragma unroll
     for (int i = 0; i < N; ++i) {
       const int it = tid + i * NT, k = it / (BN / E), c = it % (BN / E);
       if constexpr (BF) *reinterpret_cast<mu32x4*>(dst + k * STR + c * E) = v[i];
-      else *reinterpret_cast<mbf16x4*>(dst + k * STR + c * E) = mcvt4(__builtin_bit_cast(float4, v[i]));
+      else *reinterpret_cast<hx4<T16>*>(dst + k * STR + c * E) = mcvt4<T16>(__builtin_bit_cast(float4, v[i]));
     }
   }
 };
@@ -876,8 +892,10 @@ struct WTiles {
   static_assert(T % NW == 0 || NW % T == 0, "weight-grad tile split");
 };
 
-template <int C, int P, int BN, int NW, bool HBF, int MINB>
+template <typename T16, int C, int P, int BN, int NW, bool HBF, int MINB>
 __global__ __launch_bounds__(NW * 64, MINB) void mlp_wgrad_kernel(MlpArgs g) {
+  typedef hx8<T16> mbf16x8;
+  typedef hx4<T16> mbf16x4;
   constexpr int HC = 64;
   constexpr int NT = NW * 64;
   constexpr int C4 = 4 * C, NCH = C4 / HC;
@@ -886,13 +904,13 @@ __global__ __launch_bounds__(NW * 64, MINB) void mlp_wgrad_kernel(MlpArgs g) {
   // are then 2-way at BN = 64, whose tight stride lets two workgroups share a CU)
   constexpr int HSTR = BN + (BN == 64 ? 8 : 40), NSTR = HC + 8, W1STR = C + 8, W2STR = HC + 8;
   constexpr int H_SZ = C * HSTR, D_SZ = P * HSTR, N_SZ = BN * NSTR, W1_SZ = HC * W1STR, W2_SZ = P * W2STR;
-  __shared__ __attribute__((aligned(16))) __bf16 smem[H_SZ + D_SZ + 2 * N_SZ + W1_SZ + W2_SZ];
-  __bf16* Hs = smem;
-  __bf16* Ds = Hs + H_SZ;
-  __bf16* Zn = Ds + D_SZ;     // dz, pixel-major [BN][NSTR]
-  __bf16* Gn = Zn + N_SZ;     // g,  pixel-major [BN][NSTR]
-  __bf16* W1s = Gn + N_SZ;
-  __bf16* W2s = W1s + W1_SZ;
+  __shared__ __attribute__((aligned(16))) T16 smem[H_SZ + D_SZ + 2 * N_SZ + W1_SZ + W2_SZ];
+  T16* Hs = smem;
+  T16* Ds = Hs + H_SZ;
+  T16* Zn = Ds + D_SZ;     // dz, pixel-major [BN][NSTR]
+  T16* Gn = Zn + N_SZ;     // g,  pixel-major [BN][NSTR]
+  T16* W1s = Gn + N_SZ;
+  T16* W2s = W1s + W1_SZ;
 
   using ZG = WGrid<HC, BN, NW>;    // z / t tile [HC x BN]
   using T1 = WTiles<HC, C, NW>;    // dW1[j]    [HC x C]
@@ -939,7 +957,7 @@ __global__ __launch_bounds__(NW * 64, MINB) void mlp_wgrad_kernel(MlpArgs g) {
   TileLd<P, BN, NT, false> dreg;
   auto tile_src = [&](int tt, const void*& hp, const float*& dp) {
     const int img = tt / tpi, p0 = (tt - img * tpi) * BN;
-    hp = HBF ? (const void*)((const __bf16*)g.h + (long)img * g.h_bs + p0)
+    hp = HBF ? (const void*)((const T16*)g.h + (long)img * g.h_bs + p0)
              : (const void*)((const float*)g.h + (long)img * g.h_bs + p0);
     dp = g.dy + (long)img * g.dy_bs + p0;
   };
@@ -982,7 +1000,7 @@ __global__ __launch_bounds__(NW * 64, MINB) void mlp_wgrad_kernel(MlpArgs g) {
       for (int i = 0; i < ZG::TM; ++i)
 #pragma unroll
         for (int t = 0; t < ZG::TN; ++t)
-          zacc[i][t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bf[t], zacc[i][t], 0, 0, 0);
+          zacc[i][t] = mfma16(af[i], bf[t], zacc[i][t]);
     }
 #pragma unroll 4
     for (int ks = 0; ks < P / 16; ++ks) {
@@ -997,7 +1015,7 @@ __global__ __launch_bounds__(NW * 64, MINB) void mlp_wgrad_kernel(MlpArgs g) {
       for (int i = 0; i < ZG::TM; ++i)
 #pragma unroll
         for (int t = 0; t < ZG::TN; ++t)
-          tacc[i][t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bf[t], tacc[i][t], 0, 0, 0);
+          tacc[i][t] = mfma16(af[i], bf[t], tacc[i][t]);
     }
     // ---- g = gelu(z), dz = t gelu'(z) -> LDS (bf16, pixel-major); b1 sums of the rounded dz ----
 #pragma unroll
@@ -1013,8 +1031,8 @@ __global__ __launch_bounds__(NW * 64, MINB) void mlp_wgrad_kernel(MlpArgs g) {
             f32x2 gv, gp;
             gelu_pair_fast2(f32x2{zacc[i][t][4 * q + e], zacc[i][t][4 * q + e + 1]}, gv, gp);
             const f32x2 dz = f32x2{tacc[i][t][4 * q + e], tacc[i][t][4 * q + e + 1]} * gp;
-            gv4[e] = (__bf16)gv.x; gv4[e + 1] = (__bf16)gv.y;
-            dv4[e] = (__bf16)dz.x; dv4[e + 1] = (__bf16)dz.y;
+            gv4[e] = (T16)gv.x; gv4[e + 1] = (T16)gv.y;
+            dv4[e] = (T16)dz.x; dv4[e + 1] = (T16)dz.y;
             bacc[i][4 * q + e] += (float)dv4[e];
             bacc[i][4 * q + e + 1] += (float)dv4[e + 1];
           }
@@ -1034,7 +1052,7 @@ __global__ __launch_bounds__(NW * 64, MINB) void mlp_wgrad_kernel(MlpArgs g) {
       for (int ks = kp * (BN / 16 / T1::KS); ks < (kp + 1) * (BN / 16 / T1::KS); ++ks) {
         const mbf16x8 af = mtr_frag(Zn + (ks * 16 + 8 * lh + tq) * NSTR + mt * 32 + 16 * tG + 4 * tp, NSTR);
         const mbf16x8 bf = *reinterpret_cast<const mbf16x8*>(Hs + (nt * 32 + lr) * HSTR + ks * 16 + lh * 8);
-        a1[q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bf, a1[q], 0, 0, 0);
+        a1[q] = mfma16(af, bf, a1[q]);
       }
     }
     // ---- dW2[:, j] += dy g^T  (A = dy row-wise from Ds, B = g^T transposed from Gn) ----
@@ -1047,7 +1065,7 @@ __global__ __launch_bounds__(NW * 64, MINB) void mlp_wgrad_kernel(MlpArgs g) {
       for (int ks = kp * (BN / 16 / T2::KS); ks < (kp + 1) * (BN / 16 / T2::KS); ++ks) {
         const mbf16x8 af = *reinterpret_cast<const mbf16x8*>(Ds + (mt * 32 + lr) * HSTR + ks * 16 + lh * 8);
         const mbf16x8 bf = mtr_frag(Gn + (ks * 16 + 8 * lh + tq) * NSTR + nt * 32 + 16 * tG + 4 * tp, NSTR);
-        a2[q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bf, a2[q], 0, 0, 0);
+        a2[q] = mfma16(af, bf, a2[q]);
       }
     }
   }
@@ -1114,8 +1132,9 @@ __global__ __launch_bounds__(NW * 64, MINB) void mlp_wgrad_kernel(MlpArgs g) {
   }
 }
 
-__global__ __launch_bounds__(256) void f32_to_bf16_kernel(const float* __restrict__ s, __bf16* __restrict__ d, long n) {
-  for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) d[i] = (__bf16)s[i];
+template <typename T16>
+__global__ __launch_bounds__(256) void f32_to_half_kernel(const float* __restrict__ s, T16* __restrict__ d, long n) {
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) d[i] = (T16)s[i];
 }
 
 // Supported (C, P) -> pixel tile (forward and backward use the same BN); HC = 64, 8 waves.
@@ -1125,23 +1144,23 @@ static int mlp_bn(int C, int P) {
 }
 constexpr int MLP_NW = 8;
 
-template <int C, int P, int BN, int MINB>
+template <typename T16, int C, int P, int BN, int MINB>
 static void fwd_lds_launch(const MlpArgs& g, hipStream_t st) {
   const unsigned tiles = (unsigned)((long)g.nb * (g.HW / BN));
-  hipLaunchKernelGGL((mlp_fwd_lds_kernel<C, P, BN, 64, MLP_NW, MINB>), dim3(tiles), dim3(MLP_NW * 64), 0, st, g);
+  hipLaunchKernelGGL((mlp_fwd_lds_kernel<T16, C, P, BN, 64, MLP_NW, MINB>), dim3(tiles), dim3(MLP_NW * 64), 0, st, g);
 }
-template <int C, int P, int MINB>
+template <typename T16, int C, int P, int MINB>
 static void fwd_launch(const MlpArgs& g, hipStream_t st) {
   const unsigned tiles = (unsigned)((long)g.nb * (g.HW / 128));
-  hipLaunchKernelGGL((mlp_fwd_kernel<C, P, MINB>), dim3(tiles), dim3(512), 0, st, g);
+  hipLaunchKernelGGL((mlp_fwd_kernel<T16, C, P, MINB>), dim3(tiles), dim3(512), 0, st, g);
 }
 // backward: 8 waves x 128 pixels where the LDS tiles fit, else 4 waves x 64 pixels (same bsum
 // granularity: one partial row per 32 pixels)
-template <int C, int P, int BN, int NW, bool GD = true, int MINB = 1>
+template <typename T16, int C, int P, int BN, int NW, bool GD = true, int MINB = 1>
 static void bwd_launch(const MlpArgs& g, hipStream_t st) {
   static_assert(BN / (NW / 2) == 32, "bsum granularity");
   const unsigned tiles = (unsigned)((long)g.nb * (g.HW / BN));
-  hipLaunchKernelGGL((mlp_bwd_kernel<C, P, BN, 64, NW, GD, MINB>), dim3(tiles), dim3(NW * 64), 0, st, g);
+  hipLaunchKernelGGL((mlp_bwd_kernel<T16, C, P, BN, 64, NW, GD, MINB>), dim3(tiles), dim3(NW * 64), 0, st, g);
 }
 
 // weight-grad kernel: same pixel tile as the backward; splits so that NCH * S ~ 512 workgroups
@@ -1157,11 +1176,11 @@ static int mlp_wgrad_splits(int C, int P, int HW, int nb) {
   return (int)S;
 }
 
-template <int C, int P, int BN, int NW, int MINB>
+template <typename T16, int C, int P, int BN, int NW, int MINB>
 static void wgrad_launch(const MlpArgs& g, hipStream_t st) {
   const unsigned wgs = (unsigned)((4 * C / 64) * g.splits);
-  if (g.h_bf16) hipLaunchKernelGGL((mlp_wgrad_kernel<C, P, BN, NW, true, MINB>), dim3(wgs), dim3(NW * 64), 0, st, g);
-  else hipLaunchKernelGGL((mlp_wgrad_kernel<C, P, BN, NW, false, MINB>), dim3(wgs), dim3(NW * 64), 0, st, g);
+  if (g.h_bf16) hipLaunchKernelGGL((mlp_wgrad_kernel<T16, C, P, BN, NW, true, MINB>), dim3(wgs), dim3(NW * 64), 0, st, g);
+  else hipLaunchKernelGGL((mlp_wgrad_kernel<T16, C, P, BN, NW, false, MINB>), dim3(wgs), dim3(NW * 64), 0, st, g);
 }
 
 }  // namespace dsg
@@ -1186,13 +1205,16 @@ int dsgan_mlp_fwd(const void* h, long h_bs, int h_bf16, const void* w1, const fl
   DSG_REQUIRE(((uintptr_t)h & 15) == 0 && (h_bs & 7) == 0 && ((uintptr_t)w1 & 15) == 0 && ((uintptr_t)w2 & 15) == 0,
               "dsgan_mlp_fwd: operands must be 16-byte aligned");
   MlpArgs g{};
-  g.h = h; g.h_bs = h_bs; g.w1 = (const __bf16*)w1; g.b1 = b1; g.w2 = (const __bf16*)w2; g.b2 = b2;
+  g.h = h; g.h_bs = h_bs; g.w1 = w1; g.b1 = b1; g.w2 = w2; g.b2 = b2;
   g.out = out; g.out_bs = out_bs; g.HW = HW; g.nb = nb; g.accumulate = accumulate; g.h_bf16 = h_bf16;
   // MINB = waves per SIMD: 4 (two workgroups per CU) where 128 registers hold
-  if (C == 64) fwd_lds_launch<64, 128, 128, 2>(g, st);
-  else if (C == 128 && P == 64) fwd_launch<128, 64, 4>(g, st);
-  else if (C == 128) fwd_launch<128, 256, 2>(g, st);
-  else fwd_launch<256, 128, 2>(g, st);
+  with_half([&](auto* t) {
+    using T16 = std::remove_pointer_t<decltype(t)>;
+    if (C == 64) fwd_lds_launch<T16, 64, 128, 128, 2>(g, st);
+    else if (C == 128 && P == 64) fwd_launch<T16, 128, 64, 4>(g, st);
+    else if (C == 128) fwd_launch<T16, 128, 256, 2>(g, st);
+    else fwd_launch<T16, 256, 128, 2>(g, st);
+  });
   DSG_CHECK_LAUNCH();
   return 0;
 }
@@ -1207,19 +1229,22 @@ int dsgan_mlp_bwd(const void* h, long h_bs, int h_bf16, const float* dy, long dy
               ((uintptr_t)g_out & 15) == 0 && ((uintptr_t)dz_out & 15) == 0,
               "dsgan_mlp_bwd: operands must be 16-byte aligned");
   MlpArgs g{};
-  g.h = h; g.h_bs = h_bs; g.dy = dy; g.dy_bs = dy_bs; g.w1 = (const __bf16*)w1; g.b1 = b1;
-  g.w2 = (const __bf16*)w2; g.out = dh; g.out_bs = dh_bs; g.g_out = (__bf16*)g_out;
-  g.dz_out = (__bf16*)dz_out; g.bsum = bsum; g.HW = HW; g.nb = nb; g.h_bf16 = h_bf16;
-  if (!g_out) {   // dh only: the register-chained kernel where h, dy and dh fragments fit in registers
-    const unsigned tiles = (unsigned)((long)g.nb * (g.HW / 128));
-    if (C == 64) hipLaunchKernelGGL((mlp_dh_kernel<64, 128, 2>), dim3(tiles), dim3(512), 0, st, g);
-    else if (C == 128 && P == 64) hipLaunchKernelGGL((mlp_dh_kernel<128, 64, 2>), dim3(tiles), dim3(512), 0, st, g);
-    else if (C == 128) bwd_launch<128, 256, 64, 4, false, 1>(g, st);
-    else bwd_launch<256, 128, 64, 4, false, 1>(g, st);
-  } else if (C == 64) bwd_launch<64, 128, 128, 8>(g, st);
-  else if (C == 128 && P == 64) bwd_launch<128, 64, 128, 8>(g, st);
-  else if (C == 128) bwd_launch<128, 256, 64, 4>(g, st);
-  else bwd_launch<256, 128, 64, 4>(g, st);
+  g.h = h; g.h_bs = h_bs; g.dy = dy; g.dy_bs = dy_bs; g.w1 = w1; g.b1 = b1;
+  g.w2 = w2; g.out = dh; g.out_bs = dh_bs; g.g_out = g_out;
+  g.dz_out = dz_out; g.bsum = bsum; g.HW = HW; g.nb = nb; g.h_bf16 = h_bf16;
+  with_half([&](auto* t) {
+    using T16 = std::remove_pointer_t<decltype(t)>;
+    if (!g_out) {   // dh only: the register-chained kernel where h, dy and dh fragments fit in registers
+      const unsigned tiles = (unsigned)((long)g.nb * (g.HW / 128));
+      if (C == 64) hipLaunchKernelGGL((mlp_dh_kernel<T16, 64, 128, 2>), dim3(tiles), dim3(512), 0, st, g);
+      else if (C == 128 && P == 64) hipLaunchKernelGGL((mlp_dh_kernel<T16, 128, 64, 2>), dim3(tiles), dim3(512), 0, st, g);
+      else if (C == 128) bwd_launch<T16, 128, 256, 64, 4, false, 1>(g, st);
+      else bwd_launch<T16, 256, 128, 64, 4, false, 1>(g, st);
+    } else if (C == 64) bwd_launch<T16, 64, 128, 128, 8>(g, st);
+    else if (C == 128 && P == 64) bwd_launch<T16, 128, 64, 128, 8>(g, st);
+    else if (C == 128) bwd_launch<T16, 128, 256, 64, 4>(g, st);
+    else bwd_launch<T16, 256, 128, 64, 4>(g, st);
+  });
   DSG_CHECK_LAUNCH();
   return 0;
 }
@@ -1239,14 +1264,17 @@ int dsgan_mlp_wgrad(const void* h, long h_bs, int h_bf16, const float* dy, long 
   DSG_REQUIRE(((uintptr_t)h & 15) == 0 && ((uintptr_t)dy & 15) == 0 && (h_bs & 7) == 0 && (dy_bs & 3) == 0,
               "dsgan_mlp_wgrad: operands must be 16-byte aligned");
   MlpArgs g{};
-  g.h = h; g.h_bs = h_bs; g.h_bf16 = h_bf16; g.dy = dy; g.dy_bs = dy_bs; g.w1 = (const __bf16*)w1; g.b1 = b1;
-  g.w2 = (const __bf16*)w2; g.HW = HW; g.nb = nb; g.ws = ws;
+  g.h = h; g.h_bs = h_bs; g.h_bf16 = h_bf16; g.dy = dy; g.dy_bs = dy_bs; g.w1 = w1; g.b1 = b1;
+  g.w2 = w2; g.HW = HW; g.nb = nb; g.ws = ws;
   const int S = mlp_wgrad_splits(C, P, HW, nb);
   g.splits = S;
-  if (C == 64) wgrad_launch<64, 128, 64, 4, 2>(g, st);
-  else if (C == 128 && P == 64) wgrad_launch<128, 64, 64, 4, 2>(g, st);
-  else if (C == 128) wgrad_launch<128, 256, 64, 4, 1>(g, st);
-  else wgrad_launch<256, 128, 64, 4, 1>(g, st);
+  with_half([&](auto* t) {
+    using T16 = std::remove_pointer_t<decltype(t)>;
+    if (C == 64) wgrad_launch<T16, 64, 128, 64, 4, 2>(g, st);
+    else if (C == 128 && P == 64) wgrad_launch<T16, 128, 64, 64, 4, 2>(g, st);
+    else if (C == 128) wgrad_launch<T16, 128, 256, 64, 4, 1>(g, st);
+    else wgrad_launch<T16, 256, 128, 64, 4, 1>(g, st);
+  });
   DSG_CHECK_LAUNCH();
   const long n1 = 4L * C * C, n2 = (long)P * 4 * C;
   launch_split_reduce(ws, S, n1, dw1, st);
@@ -1263,11 +1291,15 @@ int dsgan_colsum(float* part, int rows, int cols, float* out, hipStream_t st) {
   return 0;
 }
 
+// (dst has the library's half type: bf16, or fp16 in --precision fp16)
 int dsgan_f32_to_bf16(const float* src, void* dst, long n, hipStream_t st) {
   DSG_REQUIRE(src && dst && n > 0, "dsgan_f32_to_bf16: bad args");
   long blocks = (n + 255) / 256;
   if (blocks > 4096) blocks = 4096;
-  hipLaunchKernelGGL(f32_to_bf16_kernel, dim3((unsigned)blocks), dim3(256), 0, st, src, (__bf16*)dst, n);
+  with_half([&](auto* t) {
+    using T16 = std::remove_pointer_t<decltype(t)>;
+    hipLaunchKernelGGL((f32_to_half_kernel<T16>), dim3((unsigned)blocks), dim3(256), 0, st, src, (T16*)dst, n);
+  });
   DSG_CHECK_LAUNCH();
   return 0;
 }

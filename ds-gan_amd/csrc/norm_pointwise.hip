@@ -18,7 +18,7 @@ struct INArgs {
   float* y; long y_bs;
   float* mean; float* rstd;     // statistics of scale*x, [N*C]
   int N, C, HW, act; float slope, eps;
-  int y_bf16;                   // y is bf16 (y_bs in elements): the block activation h whose only
+  int y_bf16;                   // y is 16-bit (1 bf16, 2 fp16; y_bs in elements): the block activation h whose only
                                 // consumers are bf16-operand MFMA GEMMs (v4 kernels only)
 };
 
@@ -205,11 +205,12 @@ __global__ __launch_bounds__(NT == 64 ? 256 : NT) void instnorm_fwd_v4(INArgs a)
     if (r) { const float4 q = r[i]; v.x += q.x; v.y += q.y; v.z += q.z; v.w += q.w; }
     v.x = act_f(a.act, v.x, a.slope); v.y = act_f(a.act, v.y, a.slope);
     v.z = act_f(a.act, v.z, a.slope); v.w = act_f(a.act, v.w, a.slope);
-    if (a.y_bf16) {   // round-to-nearest-even, the same rounding the GEMMs apply to fp32 operands
-      typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4_t;
-      bf16x4_t hv;
-      hv[0] = (__bf16)v.x; hv[1] = (__bf16)v.y; hv[2] = (__bf16)v.z; hv[3] = (__bf16)v.w;
-      reinterpret_cast<bf16x4_t*>(reinterpret_cast<__bf16*>(a.y) + (long)n * a.y_bs + (long)c * a.HW)[i] = hv;
+    if (a.y_bf16 == 2) {   // fp16 (--precision fp16), round-to-nearest-even like the GEMMs' operand loads
+      hx4<_Float16> hv = {(_Float16)v.x, (_Float16)v.y, (_Float16)v.z, (_Float16)v.w};
+      reinterpret_cast<hx4<_Float16>*>(reinterpret_cast<_Float16*>(a.y) + (long)n * a.y_bs + (long)c * a.HW)[i] = hv;
+    } else if (a.y_bf16) {   // bf16, round-to-nearest-even, the same rounding the GEMMs apply to fp32 operands
+      hx4<__bf16> hv = {(__bf16)v.x, (__bf16)v.y, (__bf16)v.z, (__bf16)v.w};
+      reinterpret_cast<hx4<__bf16>*>(reinterpret_cast<__bf16*>(a.y) + (long)n * a.y_bs + (long)c * a.HW)[i] = hv;
     } else {
       y[i] = v;
     }
@@ -957,7 +958,9 @@ int dsgan_instnorm_fwd_bf16(const float* x, long x_bs, void* y, long y_bs, float
                             int HW, float eps, hipStream_t st) {
   DSG_REQUIRE(x && y && mean && rstd && N > 0 && C > 0 && HW > 0, "dsgan_instnorm_fwd_bf16: bad args");
   DSG_REQUIRE(in_v4_ok(HW, x, x_bs) && in_v4_ok(HW, y, y_bs), "dsgan_instnorm_fwd_bf16: HW %% 4 and 16-byte alignment");
-  INArgs a{x, x_bs, nullptr, nullptr, 0, (float*)y, y_bs, mean, rstd, N, C, HW, ACT_NONE, 0.f, eps, 1};
+  // (y has the library's half type: y_bf16 = 1 bf16, 2 fp16)
+  INArgs a{x, x_bs, nullptr, nullptr, 0, (float*)y, y_bs, mean, rstd, N, C, HW, ACT_NONE, 0.f, eps,
+           half_type() == HALF_F16 ? 2 : 1};
   const int planes = N * C;
   if (HW <= 64 * 16)
     hipLaunchKernelGGL((instnorm_fwd_v4<64, 4>), dim3(cdiv(planes, 4)), dim3(256), 0, st, a);

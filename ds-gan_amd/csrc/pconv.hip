@@ -13,17 +13,17 @@
 // Per tap the bf16 weight slice [BM][32] is register-prefetched one tap ahead into a double
 // buffer.  Weights are a bf16 tap-major copy (dsgan_conv_wtrans_bf16).
 #include "common.h"
+#include <type_traits>
 #include <stdlib.h>
 
 namespace dsg {
 
-typedef __attribute__((ext_vector_type(8))) __bf16 cbf16x8;
-typedef __attribute__((ext_vector_type(16))) float cf32x16;
+typedef f32x16_t cf32x16;
 typedef __attribute__((ext_vector_type(4))) unsigned int cu32x4;
 
 struct PcArgs {
   const float* X; long x_bs;          // [nb][K][H][W]
-  const __bf16* Wb;                   // [taps][M][K] bf16
+  const unsigned short* Wb;           // [taps][M][K] 16-bit (the half type; moved as raw bits)
   float* Y; long y_bs;                // [nb][M][Hdst][Wdst]
   const float* bias;
   const float* gpre; long gpre_bs;    // dst-shaped act' multiplier (data-grad of the producer's act)
@@ -36,8 +36,9 @@ struct PcArgs {
 
 constexpr int PC_STR = 40;   // bf16 per staged pixel / weight row (32 + 8: conflict-free b128 reads)
 
-template <int BM, int TH, int TW, int S, int KH, int KW>
+template <typename T16, int BM, int TH, int TW, int S, int KH, int KW>
 __global__ __launch_bounds__(256, 2) void pconv_kernel(PcArgs g) {
+  typedef hx8<T16> cbf16x8;
   constexpr int BN = TH * TW;
   static_assert(BN == 128, "128 output pixels per tile");
   constexpr int WM = 2, WN = 2, TM = BM / WM / 32, TN = BN / WN / 32;
@@ -46,8 +47,8 @@ __global__ __launch_bounds__(256, 2) void pconv_kernel(PcArgs g) {
   constexpr int A_SZ = BM * PC_STR, P_SZ = PPIX * PC_STR;
   constexpr int A_ITEMS = BM * 4 / 256;           // 16-byte items of a [BM][32] bf16 slice
   constexpr int P_ITEMS = (PPIX * 4 + 255) / 256; // (pixel, 8-channel group) items of the patch per thread
-  __shared__ __attribute__((aligned(16))) __bf16 smem[2 * A_SZ + P_SZ];
-  __bf16* Ps = smem + 2 * A_SZ;
+  __shared__ __attribute__((aligned(16))) T16 smem[2 * A_SZ + P_SZ];
+  T16* Ps = smem + 2 * A_SZ;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave / WN, wn = wave % WN;
@@ -90,7 +91,7 @@ __global__ __launch_bounds__(256, 2) void pconv_kernel(PcArgs g) {
     }
   };
   auto astore = [&](int buf) {
-    __bf16* As = smem + buf * A_SZ;
+    T16* As = smem + buf * A_SZ;
 #pragma unroll
     for (int i = 0; i < A_ITEMS; ++i) {
       const int it = tid + i * 256;
@@ -122,7 +123,7 @@ __global__ __launch_bounds__(256, 2) void pconv_kernel(PcArgs g) {
         const int cg = it / PPIX, pix = it - cg * PPIX;
         cbf16x8 v;
 #pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] = (__bf16)rp[i][e];
+        for (int e = 0; e < 8; ++e) v[e] = (T16)rp[i][e];
         *reinterpret_cast<cbf16x8*>(Ps + pix * PC_STR + cg * 8) = v;
       }
     }
@@ -159,7 +160,7 @@ __global__ __launch_bounds__(256, 2) void pconv_kernel(PcArgs g) {
     for (int tap = 0; tap < TAPS; ++tap) {
       if (tap + 1 < TAPS) aload(tap + 1, k0);
       else if (kb + 1 < nkb) aload(0, k0 + 32);
-      const __bf16* As = smem + buf * A_SZ;
+      const T16* As = smem + buf * A_SZ;
       const int kh = tap / KW, kw = tap - (tap / KW) * KW;
       const int toff = (kh * PW + kw) * PC_STR;
 #pragma unroll
@@ -175,7 +176,7 @@ __global__ __launch_bounds__(256, 2) void pconv_kernel(PcArgs g) {
         for (int i = 0; i < TM; ++i)
 #pragma unroll
           for (int j = 0; j < TN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+            acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
       }
       if (tap + 1 < TAPS) {
         astore(buf ^ 1);
@@ -276,7 +277,8 @@ static int pc_splits(long tiles, int nkb, int* kchunk) {
 //   mode 0 (forward):      Wb[tap][co][ci], tap = (kh, kw)
 //   mode 1 (data-grad s1): Wb[tap][ci][co], tap = (kh', kw') with kh = KH-1-kh', kw = KW-1-kw'
 //   mode 2 (stride-2 data-grad / ConvTranspose, pconvt.hip): Wb[tap][ci][co], tap = (kh, kw)
-__global__ void wtrans_bf16_kernel(const float* __restrict__ W, __bf16* __restrict__ Wb, int Co, int Ci, int KH,
+template <typename T16>
+__global__ void wtrans_bf16_kernel(const float* __restrict__ W, T16* __restrict__ Wb, int Co, int Ci, int KH,
                                    int KW, int mode) {
   const int M = mode == 0 ? Co : Ci, K = mode == 0 ? Ci : Co;
   const long total = (long)KH * KW * M * K;
@@ -287,11 +289,11 @@ __global__ void wtrans_bf16_kernel(const float* __restrict__ W, __bf16* __restri
     int kh = tap / KW, kw = tap % KW, co = m, ci = k;
     if (mode == 1) { kh = KH - 1 - kh; kw = KW - 1 - kw; co = k; ci = m; }
     if (mode == 2) { co = k; ci = m; }
-    Wb[e] = (__bf16)W[(((long)co * Ci + ci) * KH + kh) * KW + kw];
+    Wb[e] = (T16)W[(((long)co * Ci + ci) * KH + kh) * KW + kw];
   }
 }
 
-template <int BM, int TH, int TW, int S, int KH, int KW>
+template <typename T16, int BM, int TH, int TW, int S, int KH, int KW>
 static void pc_launch(PcArgs& g, hipStream_t st) {
   g.tiles_w = (g.Wo + TW - 1) / TW;
   g.tiles_h = (g.Ho + TH - 1) / TH;
@@ -300,7 +302,7 @@ static void pc_launch(PcArgs& g, hipStream_t st) {
   const int splits = g.ws ? pc_splits(tiles, g.K / 32, &kc) : 1;
   if (splits == 1) g.ws = nullptr;
   g.kchunk = kc;
-  hipLaunchKernelGGL((pconv_kernel<BM, TH, TW, S, KH, KW>), dim3((unsigned)(tiles * splits)), dim3(256), 0, st, g);
+  hipLaunchKernelGGL((pconv_kernel<T16, BM, TH, TW, S, KH, KW>), dim3((unsigned)(tiles * splits)), dim3(256), 0, st, g);
   if (splits > 1) {
     const long per = (long)g.nb * g.M * g.Ho * g.Wo;
     long blocks = (per + 255) / 256;
@@ -309,11 +311,11 @@ static void pc_launch(PcArgs& g, hipStream_t st) {
   }
 }
 
-template <int BM>
+template <typename T16, int BM>
 static int pc_dispatch(PcArgs& g, int KH, int S, hipStream_t st) {
-  if (KH == 3 && S == 1) { pc_launch<BM, 8, 16, 1, 3, 3>(g, st); return 0; }
-  if (KH == 4 && S == 1) { pc_launch<BM, 8, 16, 1, 4, 4>(g, st); return 0; }
-  if (KH == 4 && S == 2) { pc_launch<BM, 8, 16, 2, 4, 4>(g, st); return 0; }
+  if (KH == 3 && S == 1) { pc_launch<T16, BM, 8, 16, 1, 3, 3>(g, st); return 0; }
+  if (KH == 4 && S == 1) { pc_launch<T16, BM, 8, 16, 1, 4, 4>(g, st); return 0; }
+  if (KH == 4 && S == 2) { pc_launch<T16, BM, 8, 16, 2, 4, 4>(g, st); return 0; }
   return -1;
 }
 
@@ -333,7 +335,11 @@ int dsgan_conv_wtrans_bf16(const float* W, void* Wb, int Co, int Ci, int KH, int
   const long total = (long)KH * KW * Co * Ci;
   long blocks = (total + 255) / 256;
   if (blocks > 8192) blocks = 8192;
-  hipLaunchKernelGGL(wtrans_bf16_kernel, dim3((unsigned)blocks), dim3(256), 0, st, W, (__bf16*)Wb, Co, Ci, KH, KW, mode);
+  with_half([&](auto* t_) {
+    using T16 = std::remove_pointer_t<decltype(t_)>;
+    hipLaunchKernelGGL((wtrans_bf16_kernel<T16>), dim3((unsigned)blocks), dim3(256), 0, st, W, (T16*)Wb, Co, Ci, KH, KW,
+                       mode);
+  });
   DSG_CHECK_LAUNCH();
   return 0;
 }
@@ -381,14 +387,17 @@ int dsgan_pconv_ws(const float* X, long x_bs, const void* Wb, const float* bias,
   DSG_REQUIRE((Ho - 1) * stride - pad + KH <= H + pad && (Wo - 1) * stride - pad + KW <= W + pad,
               "dsgan_pconv: output size inconsistent with input/pad");
   PcArgs g{};
-  g.X = X; g.x_bs = x_bs; g.Wb = (const __bf16*)Wb; g.Y = Y; g.y_bs = y_bs; g.bias = bias;
+  g.X = X; g.x_bs = x_bs; g.Wb = (const unsigned short*)Wb; g.Y = Y; g.y_bs = y_bs; g.bias = bias;
   g.gpre = gpre; g.gpre_bs = gpre_bs; g.nb = nb; g.K = K; g.M = M; g.H = H; g.W = W; g.Ho = Ho;
   g.Wo = Wo; g.pad = pad; g.act = act; g.gact = gact; g.slope = slope; g.accumulate = accumulate;
   g.ws = ws;
   const int bm = pc_bm(nb, M, Ho, Wo);
-  const int rc = bm == 256 ? pc_dispatch<256>(g, KH, stride, st)
-                 : bm == 128 ? pc_dispatch<128>(g, KH, stride, st)
-                             : pc_dispatch<64>(g, KH, stride, st);
+  const int rc = with_half([&](auto* t_) {
+    using T16 = std::remove_pointer_t<decltype(t_)>;
+    return bm == 256 ? pc_dispatch<T16, 256>(g, KH, stride, st)
+           : bm == 128 ? pc_dispatch<T16, 128>(g, KH, stride, st)
+                       : pc_dispatch<T16, 64>(g, KH, stride, st);
+  });
   DSG_REQUIRE(rc == 0, "dsgan_pconv: no kernel for KH=%d stride=%d", KH, stride);
   DSG_CHECK_LAUNCH();
   return 0;

@@ -15,17 +15,17 @@
 //   * the epilogue writes the two column parities of an output row as one float2 per lane
 //     (adjacent lanes = adjacent grid columns: fully coalesced).
 #include "common.h"
+#include <type_traits>
 #include <stdlib.h>
 
 namespace dsg {
 
-typedef __attribute__((ext_vector_type(8))) __bf16 tbf16x8;
-typedef __attribute__((ext_vector_type(16))) float tf32x16;
+typedef f32x16_t tf32x16;
 typedef __attribute__((ext_vector_type(4))) unsigned int tu32x4;
 
 struct PtArgs {
   const float* X; long x_bs;          // [nb][K][Hi][Wi]   (grid = input)
-  const __bf16* Wb;                   // [KS*KS][M][K] bf16, tap = kh*KS + kw (unflipped)
+  const unsigned short* Wb;                   // [KS*KS][M][K] bf16, tap = kh*KS + kw (unflipped)
   float* Y; long y_bs;                // [nb][M][Ho][Wo], Ho <= 2*Hi, Wo <= 2*Wi
   const float* bias;
   const float* gpre; long gpre_bs;    // Y-shaped act' multiplier
@@ -57,8 +57,9 @@ struct PtGeo {
 static_assert(PtGeo<3, 1>::dmin == 0 && PtGeo<3, 1>::dmax == 1, "ConvT 3x3 shifts");
 static_assert(PtGeo<4, 1>::dmin == -1 && PtGeo<4, 1>::dmax == 1, "4x4 s2 data-grad shifts");
 
-template <int BM, int KS, bool PERSIST>
+template <typename T16, int BM, int KS, bool PERSIST>
 __global__ __launch_bounds__(256, BM == 32 ? 4 : 2) void pconvt_kernel(PtArgs g) {
+  typedef hx8<T16> tbf16x8;
   constexpr int PAD = 1;
   constexpr int TH = 8, TW = 16, BN = TH * TW;
   constexpr int T = KS * KS;
@@ -71,8 +72,8 @@ __global__ __launch_bounds__(256, BM == 32 ? 4 : 2) void pconvt_kernel(PtArgs g)
   constexpr int A_IT = (A_ITEMS + 255) / 256;
   constexpr int P_ITEMS = PPIX * 4;                // (pixel, 8-channel group)
   constexpr int P_IT = (P_ITEMS + 255) / 256;
-  __shared__ __attribute__((aligned(16))) __bf16 smem[T * A_SZ + PPIX * PT_STR];
-  __bf16* Ps = smem + T * A_SZ;
+  __shared__ __attribute__((aligned(16))) T16 smem[T * A_SZ + PPIX * PT_STR];
+  T16* Ps = smem + T * A_SZ;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave % WMW, wn = wave / WMW;
@@ -149,7 +150,7 @@ __global__ __launch_bounds__(256, BM == 32 ? 4 : 2) void pconvt_kernel(PtArgs g)
         const int cg = it / PPIX, pix = it - cg * PPIX;
         tbf16x8 v;
 #pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] = (__bf16)rp[i][e];
+        for (int e = 0; e < 8; ++e) v[e] = (T16)rp[i][e];
         *reinterpret_cast<tbf16x8*>(Ps + pix * PT_STR + cg * 8) = v;
       }
     }
@@ -198,8 +199,8 @@ __global__ __launch_bounds__(256, BM == 32 ? 4 : 2) void pconvt_kernel(PtArgs g)
                                                                  ks * 16 + lh * 8);
 #pragma unroll
             for (int j = 0; j < NT; ++j)
-              acc[ph * 2 + pw][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bfr[dh - DMIN][dw - DMIN][j],
-                                                                            acc[ph * 2 + pw][j], 0, 0, 0);
+              acc[ph * 2 + pw][j] = mfma16(af, bfr[dh - DMIN][dw - DMIN][j],
+                                                                            acc[ph * 2 + pw][j]);
           }
         }
       }
@@ -246,13 +247,13 @@ __global__ __launch_bounds__(256, BM == 32 ? 4 : 2) void pconvt_kernel(PtArgs g)
   }
 }
 
-template <int BM, int KS, bool PERSIST>
+template <typename T16, int BM, int KS, bool PERSIST>
 static void pt_launch(PtArgs& g, hipStream_t st) {
   g.tiles_w = (g.Wi + 15) / 16;
   g.tiles_h = (g.Hi + 7) / 8;
   const long tiles = (long)g.nb * g.tiles_w * g.tiles_h * ((g.M + BM - 1) / BM);
   const long grid = PERSIST && tiles > PT_WGS ? PT_WGS : tiles;
-  hipLaunchKernelGGL((pconvt_kernel<BM, KS, PERSIST>), dim3((unsigned)grid), dim3(256), 0, st, g);
+  hipLaunchKernelGGL((pconvt_kernel<T16, BM, KS, PERSIST>), dim3((unsigned)grid), dim3(256), 0, st, g);
 }
 
 }  // namespace dsg
@@ -279,11 +280,14 @@ int dsgan_pconvt(const float* X, long x_bs, const void* Wb, const float* bias, f
                   (!gpre || (((uintptr_t)gpre & 7) == 0 && (gpre_bs & 1) == 0)),
               "dsgan_pconvt: alignment (Wb 16 B, Y/gpre rows 8 B, even Wo)");
   PtArgs g{};
-  g.X = X; g.x_bs = x_bs; g.Wb = (const __bf16*)Wb; g.Y = Y; g.y_bs = y_bs; g.bias = bias;
+  g.X = X; g.x_bs = x_bs; g.Wb = (const unsigned short*)Wb; g.Y = Y; g.y_bs = y_bs; g.bias = bias;
   g.gpre = gpre; g.gpre_bs = gpre_bs; g.nb = nb; g.K = K; g.M = M; g.Hi = Hi; g.Wi = Wi; g.Ho = Ho; g.Wo = Wo;
   g.pad = pad; g.gact = gact; g.slope = slope; g.accumulate = accumulate;
-  if (KS == 3) pt_launch<64, 3, false>(g, st);
-  else pt_launch<32, 4, false>(g, st);
+  with_half([&](auto* t_) {
+    using T16 = std::remove_pointer_t<decltype(t_)>;
+    if (KS == 3) pt_launch<T16, 64, 3, false>(g, st);
+    else pt_launch<T16, 32, 4, false>(g, st);
+  });
   DSG_CHECK_LAUNCH();
   return 0;
 }

@@ -18,506 +18,22 @@
 //   WGRAD: DW[m][n]   += sum_{b,p} DY[b][m][p] * xact(X[b][n][p])     (split over pixels: each split
 //          writes its partial tile to a workspace, pw_wgrad_reduce_kernel adds the splits in a fixed
 //          order -- deterministic, and plain stores stream faster than float atomics)
-#include "common.h"
-#include <stdlib.h>
+#include "pw_impl.h"
 
 namespace dsg {
 
-typedef __attribute__((ext_vector_type(8))) __bf16 pbf16x8;
-typedef __attribute__((ext_vector_type(4))) __bf16 pbf16x4;
-typedef __attribute__((ext_vector_type(16))) float pf32x16;
-typedef __attribute__((ext_vector_type(4))) short s16x4;
-typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
-typedef __attribute__((ext_vector_type(4))) unsigned int pu32x4;   // 16 raw bytes (8 bf16)
+extern template void pw_fd_launch<_Float16>(int, const PwArgs&, int, int, int, hipStream_t);
+extern template void pw_wgrad_launch<_Float16>(const PwArgs&, int, int, int, int, hipStream_t);
+template void pw_fd_launch<__bf16>(int, const PwArgs&, int, int, int, hipStream_t);
+template void pw_wgrad_launch<__bf16>(const PwArgs&, int, int, int, int, hipStream_t);
 
-enum PwMode : int { PW_FWD = 0, PW_DGRAD = 1, PW_WGRAD = 2 };
-
-struct PwArgs {
-  const float* A; long a_bs;   // FWD: W[M][K]  DGRAD: W[K][M]  WGRAD: DY[b][M][P]
-  const float* B; long b_bs;   // FWD/DGRAD: X/DY [b][K][P]     WGRAD: X[b][N][P]
-  float* Y; long y_bs;         // FWD/DGRAD output [b][M][P];   WGRAD: DW[M][N] (+=)
-  const float* bias;
-  float* ypre; long ypre_bs;
-  const float* gpre; long gpre_bs;
-  int M, N, K, P;
-  int act, gact, bact, accumulate; float slope;
-  int k_split;
-  float* ws;                   // WGRAD with splits > 1: partials [split][M][N]
-  unsigned a_range, b_range;   // buffer-resource byte ranges of A and B (B: per image for FWD/DGRAD)
-  int y_bf16;  // FWD: Y is bf16 [b][M][P] (y_bs in elements)
-  int gbf;     // FWD: ypre is bf16 and receives act'(pre);  DGRAD: gpre is a bf16 multiplier (no act')
-  float* asum; // WGRAD (nullable): db[m] += sum_k A[m][k] -- the bias grad of the layer whose output
-               // grad is A, from the staged A tiles (split partials after the S*M*N weight partials)
-};
-
-constexpr int PBK = 32;                 // K per main-loop step
-constexpr int RM_STR = PBK + 8;         // row-major [rows][k] tile stride (80 B: conflict-free b128)
-
-__device__ __forceinline__ pbf16x8 tr_frag(const __bf16* p0, int stride) {
-  // two ds_read_b64_tr_b16: rows k..k+3 then k+4..k+7 of a k-major tile
-#if defined(__HIP_DEVICE_COMPILE__)
-  s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p0));
-  s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p0 + 4 * stride));
-  typedef __attribute__((ext_vector_type(8))) short s16x8;
-  s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-  return __builtin_bit_cast(pbf16x8, v);
-#else
-  return pbf16x8{};
-#endif
+static void fd_dispatch(int mode, const PwArgs& g, int bm, int abf, int bbf, hipStream_t st) {
+  if (half_type() == HALF_F16) pw_fd_launch<_Float16>(mode, g, bm, abf, bbf, st);
+  else pw_fd_launch<__bf16>(mode, g, bm, abf, bbf, st);
 }
-
-constexpr unsigned PW_OOB = 0xFFFFFFF0u;   // voffset past every resource range (ranges < PW_OOB)
-
-__device__ __forceinline__ pbf16x4 cvt4(float4 v, int bact, float slope) {
-  if (bact) { v.x = act_f(bact, v.x, slope); v.y = act_f(bact, v.y, slope); v.z = act_f(bact, v.z, slope); v.w = act_f(bact, v.w, slope); }
-  pbf16x4 r;
-  r[0] = (__bf16)v.x; r[1] = (__bf16)v.y; r[2] = (__bf16)v.z; r[3] = (__bf16)v.w;
-  return r;
-}
-
-// ABF (WGRAD only) / BBF: the A (dy) / B (x, dy) operand is bf16 in HBM -- the block activation h
-// (InstanceNorm bf16 output), gelu(z) and dz of the MLPs (mlp.hip and the unfused blocks) -- and
-// is copied to LDS unconverted.
-// BN x WN waves / BK: 128 x 2 / 32 (4 waves, two workgroups per CU), or the wide form 256 x 4 / 64
-// (8 waves, 256 x 256 tiles, 64-deep K steps: twice the MFMAs per staged byte and per barrier)
-// for the deep, wide GEMMs of the unfused blocks.
-template <int MODE, int BM, int ABF = 0, int BBF = 0, int BN = 128, int WN = 2, int BK = PBK>
-__global__ __launch_bounds__(128 * WN, WN == 2 ? 2 : 1) void pwgemm_kernel(PwArgs g) {
-  constexpr int WM = 2, NT = 64 * WM * WN;
-  constexpr int TM = BM / WM / 32, TN = BN / WN / 32;
-  constexpr int RM_STR = BK + 8;        // row-major [rows][k] stride (odd 16-byte slot count)
-  constexpr int RF = BK / 4, RH = BK / 8;   // fp32 / bf16 16-byte items per row-major row
-  // A tile: row-major [BM][RM_STR] (FWD, WGRAD) or k-major [PBK][BM+32] (DGRAD)
-  // B tile: k-major [PBK][BN+32] (FWD, DGRAD) or row-major [BN][RM_STR] (WGRAD)
-  constexpr bool A_KMAJ = (MODE == PW_DGRAD);
-  constexpr bool B_KMAJ = (MODE != PW_WGRAD);
-  constexpr int A_STR = A_KMAJ ? BM + 32 : RM_STR;
-  constexpr int B_STR = B_KMAJ ? BN + 32 : RM_STR;
-  constexpr int A_SZ = A_KMAJ ? BK * A_STR : BM * A_STR;
-  constexpr int B_SZ = B_KMAJ ? BK * B_STR : BN * B_STR;
-  __shared__ __attribute__((aligned(16))) __bf16 smem[2 * (A_SZ + B_SZ)];
-
-  // wave index through readfirstlane: the compiler then knows it is uniform (SGPR), so
-  // per-wave row offsets can be scalar soffsets instead of readfirstlane waterfall loops
-  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave / WN, wn = wave % WN;
-  const int lr = lane & 31, lh = lane >> 5;
-
-  // ---- tile decode (1-D grid, XCD-aware, M-tile fastest; see igemm.hip) ----
-  const int mt = (g.M + BM - 1) / BM;
-  const int nt = (MODE == PW_WGRAD) ? (g.N + BN - 1) / BN : g.N / BN;
-  int tile;
-  {
-    const int nwg = gridDim.x, id = blockIdx.x;
-    const int xcd = id & 7, q = nwg >> 3, r = nwg & 7;
-    tile = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (id >> 3);
-  }
-  const int m_t = tile % mt, rest = tile / mt;
-  const int n_t = rest % nt, split = rest / nt;
-  const int m0 = m_t * BM, n0 = n_t * BN;
-
-  int kbeg = 0, kend = g.K;
-  if (MODE == PW_WGRAD) { kbeg = split * g.k_split; kend = min(g.K, kbeg + g.k_split); }
-  if (kbeg >= kend) return;
-  const int nk = (kend - kbeg + BK - 1) / BK;
-
-  // FWD/DGRAD: the N tile lies inside one image (P % BN == 0)
-  const int bimg = (MODE == PW_WGRAD) ? 0 : n0 / g.P;
-  const int p0 = (MODE == PW_WGRAD) ? 0 : n0 - bimg * g.P;
-
-  // ---- staging maps ----
-  // row-major tiles: item = (row, c4) with c4 in [0,8): 8 float4 per 32-k row
-  // k-major tiles  : item = (k, c4) with c4 in [0, C/4)
-  constexpr int A_ITEMS = BK * BM / (ABF ? 8 : 4) / NT;
-  constexpr int B_ITEMS = BK * BN / (BBF ? 8 : 4) / NT;
-  static_assert(A_ITEMS * NT * (ABF ? 8 : 4) == BK * BM && B_ITEMS * NT * (BBF ? 8 : 4) == BK * BN, "staging split");
-  float4 ra[ABF ? 1 : A_ITEMS], rb[BBF ? 1 : B_ITEMS];
-  pu32x4 rha[ABF ? A_ITEMS : 1], rhb[BBF ? B_ITEMS : 1];
-  float asr[A_ITEMS];   // WGRAD asum: this thread's running row sums of its A items (fixed order)
-#pragma unroll
-  for (int i = 0; i < A_ITEMS; ++i) asr[i] = 0.f;
-
-  // Operand loads are 16-byte buffer loads: an element outside its tensor gets the offset
-  // PW_OOB, past every resource range, and reads 0 in hardware -- no branch, no mask VALU.
-  // (A select of the address followed by a select of the value is turned back into a branch
-  // around the load by the compiler; see igemm.hip ldsel.)
-  const int b_fix = (MODE == PW_WGRAD) ? 0 : bimg;
-  const __amdgpu_buffer_rsrc_t rA = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)g.A, (short)0, g.a_range, 0x00020000);
-  const __amdgpu_buffer_rsrc_t rB = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)((const char*)g.B + (long)b_fix * g.b_bs * (BBF ? 2 : 4)), (short)0, g.b_range, 0x00020000);
-  auto bld4 = [](__amdgpu_buffer_rsrc_t r, unsigned voff) {
-    return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)voff, 0, 0));
-  };
-  auto bldh = [](__amdgpu_buffer_rsrc_t r, unsigned voff) {
-    return __builtin_bit_cast(pu32x4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)voff, 0, 0));
-  };
-
-  auto gload = [&](int kt) {
-    const int kb = kbeg + kt * BK;
-    // WGRAD: a BK-pixel K step lies inside one image (P % BK == 0): image index is uniform
-    const unsigned bw = (MODE == PW_WGRAD) ? (unsigned)(kb / g.P) : 0u;
-    const unsigned pw = (MODE == PW_WGRAD) ? (unsigned)(kb - (int)bw * g.P) : 0u;
-    if constexpr (ABF) {   // bf16 A, 8 elements per item
-#pragma unroll
-      for (int i = 0; i < A_ITEMS; ++i) {
-        const int it = tid + i * NT;
-        unsigned off;
-        if (MODE == PW_FWD) {                    // W[M][K] bf16, row m, k = kb + c8*8
-          const int m = m0 + it / RH, k = kb + (it % RH) * 8;
-          off = ((m < g.M) & (k < kend)) ? ((unsigned)m * g.K + k) * 2u : PW_OOB;
-        } else if (MODE == PW_DGRAD) {           // W[K][M] bf16, row k (k >= K is past the range)
-          const int k = kb + it / (BM / 8), m = m0 + (it % (BM / 8)) * 8;
-          off = (m < g.M) ? ((unsigned)k * g.M + m) * 2u : PW_OOB;
-        } else {                                 // DY[b][M][P] bf16, row m, 8 pixels per item
-          const int m = m0 + it / RH;
-          off = (m < g.M) ? (bw * (unsigned)g.a_bs + (unsigned)m * g.P + pw + (it % RH) * 8) * 2u : PW_OOB;
-        }
-        rha[i] = bldh(rA, off);
-      }
-    } else
-#pragma unroll
-    for (int i = 0; i < A_ITEMS; ++i) {
-      const int it = tid + i * NT;
-      unsigned off;
-      if (MODE == PW_FWD) {                      // W[M][K], row m, k = kb + c4*4
-        const int m = m0 + it / RF, k = kb + (it % RF) * 4;
-        off = ((m < g.M) & (k < kend)) ? ((unsigned)m * g.K + k) * 4u : PW_OOB;
-      } else if (MODE == PW_DGRAD) {             // W[K][M], row k (k >= K is past the range)
-        const int k = kb + it / (BM / 4), m = m0 + (it % (BM / 4)) * 4;
-        off = (m < g.M) ? ((unsigned)k * g.M + m) * 4u : PW_OOB;
-      } else {                                   // DY[b][M][P], row m
-        const int m = m0 + it / RF;
-        off = (m < g.M) ? (bw * (unsigned)g.a_bs + (unsigned)m * g.P + pw + (it % RF) * 4) * 4u : PW_OOB;
-      }
-      ra[i] = bld4(rA, off);
-    }
-    if constexpr (BBF && MODE != PW_WGRAD) {     // X/DY[b][K][P] bf16, k-major: row k, 8 pixels per item
-#pragma unroll
-      for (int i = 0; i < B_ITEMS; ++i) {
-        const int it = tid + i * NT;
-        const int k = kb + it / (BN / 8);
-        rhb[i] = bldh(rB, ((unsigned)k * g.P + p0 + (it % (BN / 8)) * 8) * 2u);
-      }
-    } else if constexpr (BBF) {                  // X[b][N][P] bf16, row n
-#pragma unroll
-      for (int i = 0; i < B_ITEMS; ++i) {
-        const int it = tid + i * NT;
-        const int n = n0 + it / RH;
-        const unsigned off = (n < g.N) ? (bw * (unsigned)g.b_bs + (unsigned)n * g.P + pw + (it % RH) * 8) * 2u : PW_OOB;
-        rhb[i] = bldh(rB, off);
-      }
-    } else
-#pragma unroll
-    for (int i = 0; i < B_ITEMS; ++i) {
-      const int it = tid + i * NT;
-      unsigned off;
-      if (MODE != PW_WGRAD) {                    // [K][P] k-major (k >= K is past the range)
-        const int k = kb + it / (BN / 4);
-        off = ((unsigned)k * g.P + p0 + (it % (BN / 4)) * 4) * 4u;
-      } else {                                   // X[b][N][P], row n
-        const int n = n0 + it / RF;
-        off = (n < g.N) ? (bw * (unsigned)g.b_bs + (unsigned)n * g.P + pw + (it % RF) * 4) * 4u : PW_OOB;
-      }
-      rb[i] = bld4(rB, off);
-    }
-  };
-  auto sstore = [&](int buf) {
-    __bf16* As = smem + buf * (A_SZ + B_SZ);
-    __bf16* Bs = As + A_SZ;
-    if constexpr (ABF) {
-#pragma unroll
-      for (int i = 0; i < A_ITEMS; ++i) {
-        const int it = tid + i * NT;
-        const int off = A_KMAJ ? (it / (BM / 8)) * A_STR + (it % (BM / 8)) * 8 : (it / RH) * A_STR + (it % RH) * 8;
-        *reinterpret_cast<pu32x4*>(As + off) = rha[i];
-        if (MODE == PW_WGRAD && g.asum) {
-          const pbf16x8 hv = __builtin_bit_cast(pbf16x8, rha[i]);
-          asr[i] += (((float)hv[0] + (float)hv[1]) + ((float)hv[2] + (float)hv[3])) +
-                    (((float)hv[4] + (float)hv[5]) + ((float)hv[6] + (float)hv[7]));
-        }
-      }
-    } else
-#pragma unroll
-    for (int i = 0; i < A_ITEMS; ++i) {
-      const int it = tid + i * NT;
-      int off;
-      if (A_KMAJ) off = (it / (BM / 4)) * A_STR + (it % (BM / 4)) * 4;
-      else off = (it / RF) * A_STR + (it % RF) * 4;
-      *reinterpret_cast<pbf16x4*>(As + off) = cvt4(ra[i], 0, 0.f);
-      if (MODE == PW_WGRAD && g.asum) asr[i] += (ra[i].x + ra[i].y) + (ra[i].z + ra[i].w);
-    }
-    auto bstore = [&](auto cv) {
-#pragma unroll
-      for (int i = 0; i < B_ITEMS; ++i) {
-        const int it = tid + i * NT;
-        int off;
-        if (B_KMAJ) off = (it / (BN / 4)) * B_STR + (it % (BN / 4)) * 4;
-        else off = (it / RF) * B_STR + (it % RF) * 4;
-        // WGRAD rows past N (a thin operand, e.g. a 12-channel hidden) read 0: skip their
-        // conversion / activation-on-load (whole waves branch around it)
-        if (MODE == PW_WGRAD && n0 + it / RF >= g.N) *reinterpret_cast<pbf16x4*>(Bs + off) = pbf16x4{};
-        else *reinterpret_cast<pbf16x4*>(Bs + off) = cv(rb[i]);
-      }
-    };
-    if constexpr (BBF && MODE != PW_WGRAD) {
-#pragma unroll
-      for (int i = 0; i < B_ITEMS; ++i) {
-        const int it = tid + i * NT;
-        *reinterpret_cast<pu32x4*>(Bs + (it / (BN / 8)) * B_STR + (it % (BN / 8)) * 8) = rhb[i];
-      }
-      return;
-    } else if constexpr (BBF) {
-#pragma unroll
-      for (int i = 0; i < B_ITEMS; ++i) {
-        const int it = tid + i * NT;
-        *reinterpret_cast<pu32x4*>(Bs + (it / RH) * B_STR + (it % RH) * 8) = rhb[i];
-      }
-      return;
-    }
-    // activation-on-load switch hoisted out of the element loop (uniform)
-    if (g.bact == ACT_NONE) bstore([](float4 v) { return cvt4(v, 0, 0.f); });
-    else if (g.bact == ACT_GELU)
-      bstore([](float4 v) {
-        return cvt4(make_float4(gelu_f(v.x), gelu_f(v.y), gelu_f(v.z), gelu_f(v.w)), 0, 0.f);
-      });
-    else bstore([&](float4 v) { return cvt4(v, g.bact, g.slope); });
-  };
-
-  // ---- accumulators (bias folded into the init for FWD) ----
-  pf32x16 acc[TM][TN];
-  const bool has_bias = MODE == PW_FWD && g.bias != nullptr;
-#pragma unroll
-  for (int i = 0; i < TM; ++i) {
-    float bv[16];
-#pragma unroll
-    for (int r = 0; r < 16; ++r) bv[r] = 0.f;
-    if (has_bias) {   // one uniform branch; guarded loads are clamp + select (see igemm.hip ldsel)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int m = m0 + wm * TM * 32 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-        const float t = g.bias[m < g.M ? m : 0];
-        bv[r] = m < g.M ? t : 0.f;
-      }
-    }
-#pragma unroll
-    for (int j = 0; j < TN; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = bv[r];
-  }
-
-  gload(0);
-  sstore(0);
-  __syncthreads();
-
-  // per-lane fragment address parts for the transposed reads:
-  // lane = 32h + 16G + 4q + p supplies row (8h + q) and column 16G + 4p of its 16-column block
-  const int tq = (lane >> 2) & 3, tp = lane & 3, tG = (lane >> 4) & 1;
-
-  for (int kt = 0; kt < nk; ++kt) {
-    const int buf = kt & 1;
-    if (kt + 1 < nk) gload(kt + 1);
-    const __bf16* As = smem + buf * (A_SZ + B_SZ);
-    const __bf16* Bs = As + A_SZ;
-#pragma unroll
-    for (int ks = 0; ks < BK / 16; ++ks) {
-      pbf16x8 af[TM], bfr[TN];
-#pragma unroll
-      for (int i = 0; i < TM; ++i) {
-        const int mb = wm * TM * 32 + i * 32;
-        if (A_KMAJ)
-          af[i] = tr_frag(As + (ks * 16 + 8 * lh + tq) * A_STR + mb + 16 * tG + 4 * tp, A_STR);
-        else
-          af[i] = *reinterpret_cast<const pbf16x8*>(As + (mb + lr) * A_STR + ks * 16 + lh * 8);
-      }
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        const int nbb = wn * TN * 32 + j * 32;
-        if (B_KMAJ)
-          bfr[j] = tr_frag(Bs + (ks * 16 + 8 * lh + tq) * B_STR + nbb + 16 * tG + 4 * tp, B_STR);
-        else
-          bfr[j] = *reinterpret_cast<const pbf16x8*>(Bs + (nbb + lr) * B_STR + ks * 16 + lh * 8);
-      }
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
-    }
-    if (kt + 1 < nk) sstore(buf ^ 1);
-    __syncthreads();
-  }
-
-  // ---- epilogue ----
-  if (MODE == PW_WGRAD) {
-    if (g.asum) {
-      // the threads of one A row (4 bf16 / 8 fp32 items per 32-pixel row) are adjacent lanes:
-      // butterfly over them; the n-tile-0 workgroup writes (its split's partial, or db += when unsplit)
-      constexpr int RT = ABF ? RH : RF;
-#pragma unroll
-      for (int i = 0; i < A_ITEMS; ++i) {
-        float t = asr[i];
-        t += __shfl_xor(t, 1, 64); t += __shfl_xor(t, 2, 64);
-        if (RT >= 8) t += __shfl_xor(t, 4, 64);
-        if (RT >= 16) t += __shfl_xor(t, 8, 64);
-        const int it = tid + i * NT, m = m0 + it / RT;
-        if (n_t == 0 && it % RT == 0 && m < g.M) {
-          if (g.ws) g.ws[(long)gridDim.x / mt / nt * g.M * g.N + (long)split * g.M + m] = t;
-          else g.asum[m] += t;
-        }
-      }
-    }
-    // splits > 1: this split's partial tile (plain stores); one split: the only writer, +=
-    float* dst = g.ws ? g.ws + (long)split * g.M * g.N : g.Y;
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const int n = n0 + wn * TN * 32 + j * 32 + lr;
-      if (n >= g.N) continue;
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int m = m0 + wm * TM * 32 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-          if (m < g.M) {
-            float* o = dst + (long)m * g.N + n;
-            *o = g.ws ? acc[i][j][r] : *o + acc[i][j][r];
-          }
-        }
-    }
-    return;
-  }
-  // FWD / DGRAD: element (m, n0+col) of image bimg lives at base + m*P + col; buffer resources
-  // are based at pixel p0 of row 0, their range ends at row M (rows >= M are dropped/read 0).
-  const unsigned range = (unsigned)(((long)g.M * g.P - p0) * 4);
-  const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(g.Y + (long)bimg * g.y_bs + p0), (short)0, range, 0x00020000);
-  const __amdgpu_buffer_rsrc_t ryh = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)((__bf16*)g.Y + (long)bimg * g.y_bs + p0), (short)0, range / 2, 0x00020000);
-  __amdgpu_buffer_rsrc_t rp = ry, rg = ry;
-  // bf16 side tensors (gbf): same element offsets, byte offsets halved
-  const int esz = g.gbf ? 2 : 4;
-  if (g.ypre) rp = __builtin_amdgcn_make_buffer_rsrc((void*)((char*)g.ypre + ((long)bimg * g.ypre_bs + p0) * esz), (short)0,
-                                                     g.gbf ? range / 2 : range, 0x00020000);
-  if (g.gpre) rg = __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)g.gpre + ((long)bimg * g.gpre_bs + p0) * esz),
-                                                     (short)0, g.gbf ? range / 2 : range, 0x00020000);
-  const int P4 = g.P * 4;
-  const bool full = m0 + BM <= g.M;
-#pragma unroll
-  for (int j = 0; j < TN; ++j) {
-    const int col = wn * TN * 32 + j * 32 + lr;
-#pragma unroll
-    for (int i = 0; i < TM; ++i) {
-      const int mrow = m0 + wm * TM * 32 + i * 32;   // uniform
-      // lane part of the offset: rows 4h, column col.  In a partial M tile, rows >= M get an
-      // offset past the resource range so the hardware drops the store / returns 0.
-      const int vofs = (4 * lh * g.P + col) * 4;
-      const int mlim = full ? BM : g.M - mrow - 4 * lh;   // rows (r&3)+8(r>>2) < mlim are valid
-      int vrow[16];
-#pragma unroll
-      for (int r = 0; r < 16; ++r) vrow[r] = ((r & 3) + 8 * (r >> 2) < mlim) ? vofs : (int)PW_OOB;
-      float v[16];
-#pragma unroll
-      for (int r = 0; r < 16; ++r) v[r] = acc[i][j][r];
-      if (g.gpre && g.gbf) {          // DGRAD: v *= gp, gp = act'(pre) stored bf16 by the forward
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const unsigned short hb = __builtin_amdgcn_raw_buffer_load_b16(
-              rg, vrow[r] == (int)PW_OOB ? (int)PW_OOB : vrow[r] / 2, (mrow + (r & 3) + 8 * (r >> 2)) * (P4 / 2), 0);
-          v[r] *= (float)__builtin_bit_cast(__bf16, hb);
-        }
-      } else if (g.gpre) {
-        float gv[16];
-#pragma unroll
-        for (int r = 0; r < 16; ++r)
-          gv[r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
-                      rg, vrow[r], (mrow + (r & 3) + 8 * (r >> 2)) * P4, 0));
-        act_g_mul_arr(g.gact, v, gv, g.slope);
-      }
-      bool acted = false;
-      if (g.ypre && g.gbf) {          // FWD: ypre <- bf16 act'(pre), v <- act(pre) (one GELU evaluation)
-        float apv[16];
-        if (g.act == ACT_GELU) {
-#pragma unroll
-          for (int r = 0; r < 16; r += 2) {
-            f32x2 a, ap;
-            gelu_pair_fast2(f32x2{v[r], v[r + 1]}, a, ap);
-            v[r] = a.x; v[r + 1] = a.y;
-            apv[r] = ap.x; apv[r + 1] = ap.y;
-          }
-        } else {
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            apv[r] = act_g(g.act, v[r], g.slope);
-            v[r] = act_f(g.act, v[r], g.slope);
-          }
-        }
-#pragma unroll
-        for (int r = 0; r < 16; ++r)
-          __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(unsigned short, (__bf16)apv[r]), rp,
-                                                vrow[r] == (int)PW_OOB ? (int)PW_OOB : vrow[r] / 2,
-                                                (mrow + (r & 3) + 8 * (r >> 2)) * (P4 / 2), 0);
-        acted = true;
-      } else if (g.ypre) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r)
-          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v[r]), rp, vrow[r],
-                                                (mrow + (r & 3) + 8 * (r >> 2)) * P4, 0);
-      }
-      if (!acted) act_f_arr(g.act, v, g.slope);
-      if (g.accumulate) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r)
-          v[r] += __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
-                      ry, vrow[r], (mrow + (r & 3) + 8 * (r >> 2)) * P4, 0));
-      }
-      if (g.y_bf16) {   // bf16 output: same rows, half the byte offsets
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const unsigned short hb = __builtin_bit_cast(unsigned short, (__bf16)v[r]);
-          __builtin_amdgcn_raw_buffer_store_b16(hb, ryh, vrow[r] == (int)PW_OOB ? (int)PW_OOB : vrow[r] / 2,
-                                                (mrow + (r & 3) + 8 * (r >> 2)) * (P4 / 2), 0);
-        }
-        continue;
-      }
-#pragma unroll
-      for (int r = 0; r < 16; ++r)
-        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v[r]), ry, vrow[r],
-                                              (mrow + (r & 3) + 8 * (r >> 2)) * P4, 0);
-    }
-  }
-}
-
-template <int MODE, int BM, int ABF = 0, int BBF = 0, int BN = 128, int WN = 2, int BK = PBK>
-static void pw_launch(const PwArgs& g, int splits, hipStream_t st) {
-  const int mt = (g.M + BM - 1) / BM;
-  const int nt = (MODE == PW_WGRAD) ? (g.N + BN - 1) / BN : g.N / BN;
-  hipLaunchKernelGGL((pwgemm_kernel<MODE, BM, ABF, BBF, BN, WN, BK>), dim3((unsigned)((long)mt * nt * splits)),
-                     dim3(128 * WN), 0, st, g);
-}
-
-constexpr int PW_WIDE = -1;   // tile selector: 256 x 256 tiles, 8 waves, 64-deep K steps
-
-// FWD / DGRAD launch over (tile rows, bf16 weight, bf16 activation)
-template <int MODE>
-static void pw_launch_ab(const PwArgs& g, int bm, int abf, int bbf, hipStream_t st) {
-  const int sel = (abf ? 2 : 0) + (bbf ? 1 : 0);
-#define PW_AB(BM)                                                      \
-  switch (sel) {                                                       \
-    case 0: pw_launch<MODE, BM, 0, 0>(g, 1, st); break;                \
-    case 1: pw_launch<MODE, BM, 0, 1>(g, 1, st); break;                \
-    case 2: pw_launch<MODE, BM, 1, 0>(g, 1, st); break;                \
-    default: pw_launch<MODE, BM, 1, 1>(g, 1, st); break;               \
-  }
-#define PW_ABW                                                                    \
-  switch (sel) {                                                                  \
-    case 0: pw_launch<MODE, 128, 0, 0>(g, 1, st); break;  /* (not selected) */  \
-    case 1: pw_launch<MODE, 256, 0, 1, 256, 4, 64>(g, 1, st); break;              \
-    case 2: pw_launch<MODE, 256, 1, 0, 256, 4, 64>(g, 1, st); break;              \
-    default: pw_launch<MODE, 256, 1, 1, 256, 4, 64>(g, 1, st); break;             \
-  }
-  if (bm == PW_WIDE) { PW_ABW } else if (bm == 256) { PW_AB(256) } else if (bm == 128) { PW_AB(128) } else { PW_AB(64) }
-#undef PW_AB
-#undef PW_ABW
+static void wg_dispatch(const PwArgs& g, int bm, int abf, int bbf, int splits, hipStream_t st) {
+  if (half_type() == HALF_F16) pw_wgrad_launch<_Float16>(g, bm, abf, bbf, splits, st);
+  else pw_wgrad_launch<__bf16>(g, bm, abf, bbf, splits, st);
 }
 
 // dw[e] += sum_s ws[s][e], s in a fixed order: thread (e, j) of a workgroup of EL elements x J
@@ -595,40 +111,6 @@ __global__ __launch_bounds__(256) void split_reduce4_kernel(const float* __restr
   }
 }
 
-// K (pixel) split of a weight-grad launch: about `target` workgroups (640 = 2.5 per CU for the
-// 4-wave tiles: enough bytes in flight to stream HBM; 256 = one per CU for the 8-wave wide
-// tiles), >= 8 K steps each, and partials of at most a quarter of the operand bytes (each split
-// writes, and the reduce reads, an M x N fp32 tile) -- that cap yielding to a one-workgroup-per-CU
-// floor: a deep weight-grad over few tiles (1024 x 2048 at 16^2, 128 tiles) is worth the traffic.
-static int wgrad_plan(int M, int N, long K, int BM, int BN, int BK, long target, int* k_split) {
-  const long tiles = (long)((M + BM - 1) / BM) * ((N + BN - 1) / BN);
-  long splits = (target + tiles - 1) / tiles;
-  const long max_splits = (K + 8L * BK - 1) / (8L * BK);
-  long byte_cap = ((long)(M + N) * K) / (4L * M * N);
-  const long floor_splits = (256 + tiles - 1) / tiles;
-  if (byte_cap < floor_splits) byte_cap = floor_splits;
-  if (splits > max_splits) splits = max_splits;
-  if (splits > byte_cap) splits = byte_cap;
-  if (splits < 1) splits = 1;
-  long ks = (K + splits - 1) / splits;
-  ks = (ks + BK - 1) / BK * BK;
-  splits = (K + ks - 1) / ks;
-  *k_split = (int)ks;
-  return (int)splits;
-}
-
-// Weight-grad tile choice: 256 x 256 x 64 (8 waves) for the wide, deep ones (both sides >= 256
-// channels), else 128 (64) x 128 x 32.
-static bool wgrad_wide(int M, int N, int P) {
-  return M >= 256 && N >= 256 && P % 64 == 0 && (M % 256 == 0 || M >= 1024) && (N % 256 == 0 || N >= 1024);
-}
-// (fp32-only operands stay on the 4-wave tiles: the wide tile's fp32 staging spills)
-static int wgrad_cfg(PwArgs& g, bool any_bf16, int* bm) {
-  if (any_bf16 && wgrad_wide(g.M, g.N, g.P)) { *bm = PW_WIDE; return wgrad_plan(g.M, g.N, g.K, 256, 256, 64, 256, &g.k_split); }
-  *bm = g.M > 64 ? 128 : 64;
-  return wgrad_plan(g.M, g.N, g.K, *bm, 128, PBK, 640, &g.k_split);
-}
-
 // Pre-pass for many splits over few elements: workgroup (element block, row group g) adds rows
 // [g*SC, (g+1)*SC) (64 elements x 4 row lanes, coalesced 256-B row reads, fixed order) and writes
 // the sum over its own first row, which no other workgroup reads -- in place, no scratch.
@@ -704,34 +186,6 @@ static void wgrad_finish(const PwArgs& g, int splits, hipStream_t st) {
   }
 }
 
-static bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
-
-// 256-row M tiles for the wide, deep FWD / DGRAD GEMMs: each staged pixel tile feeds twice the
-// MFMAs, as long as the grid still keeps >= 2 workgroups per CU.  Isolated A/B at the step's
-// shapes (tools/gpu_pw256_micro.sh, B=16): K=4096 dgrad into 1024 ch 0.356 -> 0.264 ms, K=1024
-// fwd to 4096 ch 0.380 -> 0.342 ms; with K <= 512 the halved occupancy loses (K=256: +10 %),
-// hence K >= 1024.  (WGRAD keeps 128-row tiles: 256 rows measured 4-7 % slower on the step's
-// wide weight-grads, tools/gpu_pw256wg_micro.sh -- they already stream at ~5 TB/s.)
-static bool use_bm256(const PwArgs& g) {
-  return g.M >= 1024 && g.M % 256 == 0 && g.K >= 1024 && (long)(g.M / 256) * (g.N / 128) >= 512;
-}
-// 256 x 256 x 64 tiles (8 waves, one workgroup per CU) for the wide FWD / DGRAD GEMMs of the
-// unfused blocks: 256-pixel tiles inside one image, M a multiple of 256, a grid of >= 256 tiles.
-static bool use_wide(const PwArgs& g) {
-  return g.M % 256 == 0 && g.P % 256 == 0 && g.K >= 128 && (long)(g.M / 256) * (g.N / 256) >= 256;
-}
-// (Not for the gp-multiplied data-grad: there one 8-wave workgroup per CU leaves the epilogue's
-// 2-byte gp loads exposed.)
-// The gelu-pair forward (bf16 act(z) and act'(z) out, packed-fp32 GELU) now measures faster on the
-// wide tiles too (tools/pwio_micro.py, B=16: M=2048 K=512 at 64^2 0.455 -> 0.383 ms, M=4096 K=1024 at
-// 32^2 0.256 -> 0.227 ms); the gp-multiplied data-grad stays on 128-row tiles (wide: +5-20 %,
-// tools/pwdgrad_micro.py).
-static int fd_tile(const PwArgs& g, bool any_bf16) {
-  const bool plain = !g.ypre && !g.gpre;
-  const bool gelu_pair = g.ypre && g.gbf;
-  return any_bf16 && (plain || gelu_pair) && use_wide(g) ? PW_WIDE : use_bm256(g) ? 256 : g.M > 64 ? 128 : 64;
-}
-
 }  // namespace dsg
 
 using namespace dsg;
@@ -775,8 +229,7 @@ extern "C" int dsgan_pw_gemm(int mode, const float* A, long a_bs, const float* B
     g.ws = splits > 1 ? ws : nullptr;
     g.asum = const_cast<float*>(bias);   // WGRAD: bias (nullable) receives the bias grad += sum_k A
     g.bias = nullptr;
-    if (bm == 128) pw_launch<PW_WGRAD, 128>(g, splits, st);
-    else pw_launch<PW_WGRAD, 64>(g, splits, st);
+    wg_dispatch(g, bm, 0, 0, splits, st);
     wgrad_finish(g, splits, st);
   } else {
     DSG_REQUIRE(dsgan_pw_supported(mode, M, K, P, a_bs, b_bs, A, B), "dsgan_pw_gemm: unsupported shape");
@@ -785,8 +238,7 @@ extern "C" int dsgan_pw_gemm(int mode, const float* A, long a_bs, const float* B
     DSG_REQUIRE((long)K * P * 4 < lim && (long)M * K * 4 < lim, "dsgan_pw_gemm: operand exceeds 4 GiB buffer range");
     g.a_range = (unsigned)((long)M * K * 4);
     g.b_range = (unsigned)((long)K * P * 4);
-    if (mode == PW_FWD) pw_launch_ab<PW_FWD>(g, fd_tile(g, false), 0, 0, st);
-    else pw_launch_ab<PW_DGRAD>(g, fd_tile(g, false), 0, 0, st);
+    fd_dispatch(mode, g, fd_tile(g, false), 0, 0, st);
   }
   DSG_CHECK_LAUNCH();
   return 0;
@@ -812,7 +264,7 @@ extern "C" int dsgan_pw_fwd_io(const void* W, int w_bf16, const void* X, long x_
   g.P = P; g.M = M; g.N = nb * P; g.K = K;
   g.a_range = (unsigned)((long)M * K * (w_bf16 ? 2 : 4));
   g.b_range = (unsigned)((long)K * P * (x_bf16 ? 2 : 4));
-  pw_launch_ab<PW_FWD>(g, fd_tile(g, w_bf16 || x_bf16), w_bf16, x_bf16, st);
+  fd_dispatch(PW_FWD, g, fd_tile(g, w_bf16 || x_bf16), w_bf16, x_bf16, st);
   DSG_CHECK_LAUNCH();
   return 0;
 }
@@ -836,7 +288,7 @@ extern "C" int dsgan_pw_dgrad_io(const void* W, int w_bf16, const void* DY, long
   g.accumulate = accumulate; g.P = P; g.M = M; g.N = nb * P; g.K = K;
   g.a_range = (unsigned)((long)M * K * (w_bf16 ? 2 : 4));
   g.b_range = (unsigned)((long)K * P * (dy_bf16 ? 2 : 4));
-  pw_launch_ab<PW_DGRAD>(g, fd_tile(g, w_bf16 || dy_bf16), w_bf16, dy_bf16, st);
+  fd_dispatch(PW_DGRAD, g, fd_tile(g, w_bf16 || dy_bf16), w_bf16, dy_bf16, st);
   DSG_CHECK_LAUNCH();
   return 0;
 }
@@ -870,20 +322,7 @@ extern "C" int dsgan_pw_wgrad_mixed(const void* A, long a_bs, int a_bf16, const 
   const int splits = wgrad_cfg(g, a_bf16 || b_bf16, &bm);
   DSG_REQUIRE(splits == 1 || ws, "dsgan_pw_wgrad_mixed: needs the dsgan_pw_wgrad_workspace scratch");
   g.ws = splits > 1 ? ws : nullptr;
-  const int sel = (a_bf16 ? 2 : 0) + (b_bf16 ? 1 : 0) + (bm == 128 ? 4 : bm == PW_WIDE ? 8 : 0);
-  switch (sel) {
-    case 9: pw_launch<PW_WGRAD, 256, 0, 1, 256, 4, 64>(g, splits, st); break;
-    case 10: pw_launch<PW_WGRAD, 256, 1, 0, 256, 4, 64>(g, splits, st); break;
-    case 11: pw_launch<PW_WGRAD, 256, 1, 1, 256, 4, 64>(g, splits, st); break;
-    case 0: pw_launch<PW_WGRAD, 64, 0, 0>(g, splits, st); break;
-    case 1: pw_launch<PW_WGRAD, 64, 0, 1>(g, splits, st); break;
-    case 2: pw_launch<PW_WGRAD, 64, 1, 0>(g, splits, st); break;
-    case 3: pw_launch<PW_WGRAD, 64, 1, 1>(g, splits, st); break;
-    case 4: pw_launch<PW_WGRAD, 128, 0, 0>(g, splits, st); break;
-    case 5: pw_launch<PW_WGRAD, 128, 0, 1>(g, splits, st); break;
-    case 6: pw_launch<PW_WGRAD, 128, 1, 0>(g, splits, st); break;
-    default: pw_launch<PW_WGRAD, 128, 1, 1>(g, splits, st); break;
-  }
+  wg_dispatch(g, bm, a_bf16, b_bf16, splits, st);
   wgrad_finish(g, splits, st);
   DSG_CHECK_LAUNCH();
   return 0;

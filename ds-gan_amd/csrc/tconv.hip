@@ -18,11 +18,11 @@
 //   flipped/transposed kernel, stride 2 as four parity classes each a stride-1 conv whose
 //   outputs land on a stride-2 lattice of the destination.
 #include "common.h"
+#include <type_traits>
 
 namespace dsg {
 
-typedef __attribute__((ext_vector_type(8))) __bf16 tbf16x8;
-typedef __attribute__((ext_vector_type(16))) float tf32x16;
+typedef f32x16_t tf32x16;
 
 constexpr int TBK = 32;
 constexpr int T_STR = TBK + 8;  // [rows][k] bf16 tile stride, 80 B (conflict-free ds_read_b128)
@@ -44,14 +44,15 @@ struct TcArgs {
 
 // ABF: Wt is bf16 (dsgan_conv_wtrans_bf16, cached per weight version): half the A bytes, copied to
 // LDS unconverted.
-template <int BM, bool ABF>
+template <typename T16, int BM, bool ABF>
 __global__ __launch_bounds__(256, 2) void tconv_kernel(TcArgs g) {
+  typedef hx8<T16> tbf16x8;
   constexpr int BN = 128;
   constexpr int WM = 2, WN = 2;
   constexpr int TM = BM / WM / 32, TN = BN / WN / 32;
   constexpr int A_SZ = BM * T_STR, B_SZ = BN * T_STR;
   constexpr int A_ITEMS = ABF ? BM * 4 / 256 : BM * 8 / 256;  // 16-byte items of the [BM][32] A tile
-  __shared__ __attribute__((aligned(16))) __bf16 smem[2 * (A_SZ + B_SZ)];
+  __shared__ __attribute__((aligned(16))) T16 smem[2 * (A_SZ + B_SZ)];
 
   // wave index through readfirstlane: the compiler then knows it is uniform (SGPR), so
   // per-wave row offsets can be scalar soffsets instead of readfirstlane waterfall loops
@@ -123,8 +124,8 @@ __global__ __launch_bounds__(256, 2) void tconv_kernel(TcArgs g) {
       rb[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rx, voff, (kb + j) * HWin * 4, 0));
   };
   auto sstore = [&](int buf) {
-    __bf16* As = smem + buf * (A_SZ + B_SZ);
-    __bf16* Bs = As + A_SZ;
+    T16* As = smem + buf * (A_SZ + B_SZ);
+    T16* Bs = As + A_SZ;
 #pragma unroll
     for (int i = 0; i < A_ITEMS; ++i) {
       const int it = tid + i * 256;
@@ -132,14 +133,14 @@ __global__ __launch_bounds__(256, 2) void tconv_kernel(TcArgs g) {
         *reinterpret_cast<u32x4*>(As + (it >> 2) * T_STR + (it & 3) * 8) = rha[i];
         continue;
       }
-      typedef __attribute__((ext_vector_type(4))) __bf16 b4;
+      typedef __attribute__((ext_vector_type(4))) T16 b4;
       b4 v;
-      v[0] = (__bf16)ra[i].x; v[1] = (__bf16)ra[i].y; v[2] = (__bf16)ra[i].z; v[3] = (__bf16)ra[i].w;
+      v[0] = (T16)ra[i].x; v[1] = (T16)ra[i].y; v[2] = (T16)ra[i].z; v[3] = (T16)ra[i].w;
       *reinterpret_cast<b4*>(As + (it >> 3) * T_STR + (it & 7) * 4) = v;
     }
     tbf16x8 lo, hi;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) { lo[j] = (__bf16)rb[j]; hi[j] = (__bf16)rb[8 + j]; }
+    for (int j = 0; j < 8; ++j) { lo[j] = (T16)rb[j]; hi[j] = (T16)rb[8 + j]; }
     tbf16x8* dst = reinterpret_cast<tbf16x8*>(Bs + col * T_STR + 16 * kc);
     dst[0] = lo;
     dst[1] = hi;
@@ -172,8 +173,8 @@ __global__ __launch_bounds__(256, 2) void tconv_kernel(TcArgs g) {
   for (int kt = 0; kt < nk; ++kt) {
     const int buf = kt & 1;
     if (kt + 1 < nk) gload(kt + 1);
-    const __bf16* As = smem + buf * (A_SZ + B_SZ);
-    const __bf16* Bs = As + A_SZ;
+    const T16* As = smem + buf * (A_SZ + B_SZ);
+    const T16* Bs = As + A_SZ;
 #pragma unroll
     for (int ks = 0; ks < TBK / 16; ++ks) {
       tbf16x8 af[TM], bfr[TN];
@@ -187,7 +188,7 @@ __global__ __launch_bounds__(256, 2) void tconv_kernel(TcArgs g) {
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
     }
     if (kt + 1 < nk) sstore(buf ^ 1);
     __syncthreads();
@@ -376,13 +377,16 @@ int dsgan_tconv_ws(const float* X, long x_bs, const float* Wt, const float* bias
   g.kchunk = S > 1 ? kc : 0;
   DSG_REQUIRE(S == 1 || (long)S * nb * M * Hout * Wout < (1L << 31), "dsgan_tconv: split partials too large");
   const dim3 grid((unsigned)(tiles * S));
-  if (M > 64) {
-    if (wt_bf16) hipLaunchKernelGGL((tconv_kernel<128, true>), grid, dim3(256), 0, st, g);
-    else hipLaunchKernelGGL((tconv_kernel<128, false>), grid, dim3(256), 0, st, g);
-  } else {
-    if (wt_bf16) hipLaunchKernelGGL((tconv_kernel<64, true>), grid, dim3(256), 0, st, g);
-    else hipLaunchKernelGGL((tconv_kernel<64, false>), grid, dim3(256), 0, st, g);
-  }
+  with_half([&](auto* t_) {
+    using T16 = std::remove_pointer_t<decltype(t_)>;
+    if (M > 64) {
+      if (wt_bf16) hipLaunchKernelGGL((tconv_kernel<T16, 128, true>), grid, dim3(256), 0, st, g);
+      else hipLaunchKernelGGL((tconv_kernel<T16, 128, false>), grid, dim3(256), 0, st, g);
+    } else {
+      if (wt_bf16) hipLaunchKernelGGL((tconv_kernel<T16, 64, true>), grid, dim3(256), 0, st, g);
+      else hipLaunchKernelGGL((tconv_kernel<T16, 64, false>), grid, dim3(256), 0, st, g);
+    }
+  });
   DSG_CHECK_LAUNCH();
   if (S > 1) {
     const long per = (long)nb * M * Hout * Wout;

@@ -24,12 +24,11 @@
 //   cb16_maxpool      MaxPool2d(2) of a tapped fp32 feature -> bf16 + 2-bit window argmax.
 //   cb16_tap_bwd      (maxpool backward + L1 backward) x ReLU' at a tapped layer -> bf16.
 #include "common.h"
+#include <type_traits>
 
 namespace dsg {
 
-typedef __attribute__((ext_vector_type(8))) __bf16 vgb8;
-typedef __attribute__((ext_vector_type(4))) __bf16 vgb4;
-typedef __attribute__((ext_vector_type(16))) float vgf16;
+typedef f32x16_t vgf16;
 typedef __attribute__((ext_vector_type(4))) unsigned int vgu4;
 typedef __attribute__((ext_vector_type(4))) unsigned char vgc4;
 
@@ -37,19 +36,22 @@ __device__ __forceinline__ long cb16(int n, int c, int h, int w, int C, int H, i
   return ((((long)n * (C >> 4) + (c >> 4)) * H + h) * W + w) * 16 + (c & 15);
 }
 
+template <typename T16>
 struct VcArgs {
-  const __bf16* X;      // CB16 [N][K][H][W]
-  const __bf16* Wt;     // [M/BM][K/16][9][2][BM][8] (dsgan_vconv_wtrans)
+  const T16* X;      // CB16 [N][K][H][W]
+  const T16* Wt;     // [M/BM][K/16][9][2][BM][8] (dsgan_vconv_wtrans)
   const float* bias;    // [M] or null
-  const __bf16* mask;   // CB16 [N][M][H][W] or null: out *= (mask > 0)
+  const T16* mask;   // CB16 [N][M][H][W] or null: out *= (mask > 0)
   void* Y;              // CB16 [N][M][H][W], bf16 or fp32 (y_f32)
   int N, K, M, H, W;
   int tiles_w, tiles_h;
   int relu, y_f32;
 };
 
-template <int BM, int TH>
-__global__ __launch_bounds__(256, 2) void vconv3x3_kernel(VcArgs g) {
+template <typename T16, int BM, int TH>
+__global__ __launch_bounds__(256, 2) void vconv3x3_kernel(VcArgs<T16> g) {
+  typedef hx8<T16> vgb8;
+  typedef hx4<T16> vgb4;
   constexpr int TW = 32, BN = TH * TW;
   constexpr int WM = BM / 64, WN = 4 / WM;           // waves along M (64 rows each) and N
   constexpr int TM = 2, TN = BN / WN / 32;           // 32x32 MFMA tiles per wave
@@ -89,7 +91,7 @@ __global__ __launch_bounds__(256, 2) void vconv3x3_kernel(VcArgs g) {
       const int it = tid + i * 256;
       if (A_PIECES % 256 == 0 || it < A_PIECES) ra[i] = a[it];
     }
-    const __bf16* xb = g.X + (((long)img * nkc + kc) * g.H) * (long)g.W * 16;
+    const T16* xb = g.X + (((long)img * nkc + kc) * g.H) * (long)g.W * 16;
 #pragma unroll
     for (int i = 0; i < B_IT; ++i) {
       const int it = tid + i * 256;
@@ -126,8 +128,8 @@ __global__ __launch_bounds__(256, 2) void vconv3x3_kernel(VcArgs g) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-  const __bf16* Ab = reinterpret_cast<const __bf16*>(smem);
-  const __bf16* Bb = reinterpret_cast<const __bf16*>(smem + A_PIECES);
+  const T16* Ab = reinterpret_cast<const T16*>(smem);
+  const T16* Bb = reinterpret_cast<const T16*>(smem + A_PIECES);
   gload(0);
   for (int kc = 0; kc < nkc; ++kc) {
     __syncthreads();   // the previous chunk's fragments have been read
@@ -152,7 +154,7 @@ __global__ __launch_bounds__(256, 2) void vconv3x3_kernel(VcArgs g) {
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
     }
   }
 
@@ -189,8 +191,8 @@ __global__ __launch_bounds__(256, 2) void vconv3x3_kernel(VcArgs g) {
         } else {
           vgb4 b;
 #pragma unroll
-          for (int e = 0; e < 4; ++e) b[e] = (__bf16)v[e];
-          *reinterpret_cast<vgb4*>(reinterpret_cast<__bf16*>(g.Y) + o) = b;
+          for (int e = 0; e < 4; ++e) b[e] = (T16)v[e];
+          *reinterpret_cast<vgb4*>(reinterpret_cast<T16*>(g.Y) + o) = b;
         }
       }
   }
@@ -199,8 +201,11 @@ __global__ __launch_bounds__(256, 2) void vconv3x3_kernel(VcArgs g) {
 // Wt[mt][kc][tap][half][BM][8]: the LDS image of weight chunk kc of M tile mt.  Forward: row m =
 // output channel, k = input channel, tap (kh, kw).  Data-grad (dgrad=1): row m = input channel,
 // k = output channel, W flipped: value W[k][m][2-kh][2-kw].
-__global__ void vconv_wtrans_kernel(const float* __restrict__ W, __bf16* __restrict__ Wt, int Co, int Ci, int BM,
+template <typename T16>
+__global__ void vconv_wtrans_kernel(const float* __restrict__ W, T16* __restrict__ Wt, int Co, int Ci, int BM,
                                     int dgrad) {
+  typedef hx8<T16> vgb8;
+  typedef hx4<T16> vgb4;
   const int M = dgrad ? Ci : Co, K = dgrad ? Co : Ci;
   const long total = 9L * M * K;
   const int nkc = K >> 4;
@@ -216,16 +221,19 @@ __global__ void vconv_wtrans_kernel(const float* __restrict__ W, __bf16* __restr
     const int kh = tap / 3, kw = tap % 3;
     const int co = dgrad ? k : m, ci = dgrad ? m : k;
     const int fh = dgrad ? 2 - kh : kh, fw = dgrad ? 2 - kw : kw;
-    Wt[e] = (__bf16)W[(((long)co * Ci + ci) * 3 + fh) * 3 + fw];
+    Wt[e] = (T16)W[(((long)co * Ci + ci) * 3 + fh) * 3 + fw];
   }
 }
 
 // conv1_1 (DSGAN/models/vgg.py:17): y[n][c][h][w] = relu(b[c] + sum_{ci,kh,kw} w[c][ci][kh][kw] *
 // x[n][ci][h-1+kh][w-1+kw]), exact fp32 FMAs in (ci, kh, kw) order, stored CB16 bf16.  Thread =
 // (pixel, 16-channel block).
+template <typename T16>
 __global__ __launch_bounds__(256) void vgg_conv1_fwd_kernel(const float* __restrict__ x, long x_bs,
                                                             const float* __restrict__ w, const float* __restrict__ b,
-                                                            __bf16* __restrict__ y, int N, int H, int W) {
+                                                            T16* __restrict__ y, int N, int H, int W) {
+  typedef hx8<T16> vgb8;
+  typedef hx4<T16> vgb4;
   __shared__ float ws[64 * 27 + 64];
   for (int i = threadIdx.x; i < 64 * 27; i += 256) ws[i] = w[i];
   if (threadIdx.x < 64) ws[64 * 27 + threadIdx.x] = b[threadIdx.x];
@@ -254,7 +262,7 @@ __global__ __launch_bounds__(256) void vgg_conv1_fwd_kernel(const float* __restr
     float a = ws[64 * 27 + co];
 #pragma unroll
     for (int i = 0; i < 27; ++i) a = fmaf(ws[co * 27 + i], in[i], a);
-    o[c >> 3][c & 7] = (__bf16)fmaxf(a, 0.f);
+    o[c >> 3][c & 7] = (T16)fmaxf(a, 0.f);
   }
   vgb8* dst = reinterpret_cast<vgb8*>(y + cb16(n, cb * 16, h, wc, 64, H, W));
   dst[0] = o[0];
@@ -263,8 +271,11 @@ __global__ __launch_bounds__(256) void vgg_conv1_fwd_kernel(const float* __restr
 
 // conv1_1 data-grad: dx[n][ci][h][w] = sum_{co,kh,kw} w[co][ci][kh][kw] * d[n][co][h+1-kh][w+1-kw],
 // d = CB16 bf16 [N][64][H][W] (the grad at conv1_1's pre-activation), dx NCHW fp32.  Thread = pixel.
-__global__ __launch_bounds__(256) void vgg_conv1_dgrad_kernel(const __bf16* __restrict__ d, const float* __restrict__ w,
+template <typename T16>
+__global__ __launch_bounds__(256) void vgg_conv1_dgrad_kernel(const T16* __restrict__ d, const float* __restrict__ w,
                                                               float* __restrict__ dx, long dx_bs, int N, int H, int W) {
+  typedef hx8<T16> vgb8;
+  typedef hx4<T16> vgb4;
   __shared__ float ws[9 * 64 * 3];   // [tap][co][ci]
   for (int i = threadIdx.x; i < 9 * 64 * 3; i += 256) {
     const int ci = i % 3, co = (i / 3) % 64, tap = i / 192;
@@ -304,8 +315,11 @@ __global__ __launch_bounds__(256) void vgg_conv1_dgrad_kernel(const __bf16* __re
 
 // MaxPool2d(2) of an fp32 CB16 feature -> bf16 CB16 + window argmax (dh*2 + dw, first max wins as
 // in torch).  Thread = (output pixel, 4 channels).
-__global__ __launch_bounds__(256) void cb16_maxpool_kernel(const float* __restrict__ x, __bf16* __restrict__ y,
+template <typename T16>
+__global__ __launch_bounds__(256) void cb16_maxpool_kernel(const float* __restrict__ x, T16* __restrict__ y,
                                                            unsigned char* __restrict__ idx, int N, int C, int H, int W) {
+  typedef hx8<T16> vgb8;
+  typedef hx4<T16> vgb4;
   const int Ho = H >> 1, Wo = W >> 1;
   const long total = (long)N * (C >> 2) * Ho * Wo;
   const long t = blockIdx.x * 256L + threadIdx.x;
@@ -334,7 +348,7 @@ __global__ __launch_bounds__(256) void cb16_maxpool_kernel(const float* __restri
   vgb4 b;
   vgc4 ix;
 #pragma unroll
-  for (int e = 0; e < 4; ++e) { b[e] = (__bf16)best[e]; ix[e] = (unsigned char)bi[e]; }
+  for (int e = 0; e < 4; ++e) { b[e] = (T16)best[e]; ix[e] = (unsigned char)bi[e]; }
   *reinterpret_cast<vgb4*>(y + o) = b;
   *reinterpret_cast<vgc4*>(idx + o) = ix;
 }
@@ -342,11 +356,14 @@ __global__ __launch_bounds__(256) void cb16_maxpool_kernel(const float* __restri
 // Gradient at the pre-ReLU output of a tapped conv (f = its fp32 output, r = the real image's):
 //   d = (maxpool_bwd(dpool, idx) [dpool != NULL] + gout * coef * sign(f - r)) * (f > 0),  bf16 out.
 // Thread = (pooled pixel, 4 channels), covering the 2x2 window.
-__global__ __launch_bounds__(256) void cb16_tap_bwd_kernel(const __bf16* __restrict__ dpool,
+template <typename T16>
+__global__ __launch_bounds__(256) void cb16_tap_bwd_kernel(const T16* __restrict__ dpool,
                                                            const unsigned char* __restrict__ idx,
                                                            const float* __restrict__ f, const float* __restrict__ rr,
-                                                           __bf16* __restrict__ d, int N, int C, int H, int W,
+                                                           T16* __restrict__ d, int N, int C, int H, int W,
                                                            const float* __restrict__ gout, float coef) {
+  typedef hx8<T16> vgb8;
+  typedef hx4<T16> vgb4;
   const int Ho = H >> 1, Wo = W >> 1;
   const long total = (long)N * (C >> 2) * Ho * Wo;
   const long t = blockIdx.x * 256L + threadIdx.x;
@@ -381,18 +398,18 @@ __global__ __launch_bounds__(256) void cb16_tap_bwd_kernel(const __bf16* __restr
       const float df = fa[e] - ra[e];
       float v = df > 0.f ? g : (df < 0.f ? -g : 0.f);
       if (dpool && (int)ix[e] == k) v += up[e];
-      out[e] = (__bf16)(fa[e] > 0.f ? v : 0.f);
+      out[e] = (T16)(fa[e] > 0.f ? v : 0.f);
     }
     *reinterpret_cast<vgb4*>(d + o) = out;
   }
 }
 
-template <int BM, int TH>
-static void vc_launch(VcArgs& g, hipStream_t st) {
+template <typename T16, int BM, int TH>
+static void vc_launch(VcArgs<T16>& g, hipStream_t st) {
   g.tiles_w = g.W / 32;
   g.tiles_h = g.H / TH;
   const long tiles = (long)g.N * g.tiles_w * g.tiles_h * (g.M / BM);
-  hipLaunchKernelGGL((vconv3x3_kernel<BM, TH>), dim3((unsigned)tiles), dim3(256), 0, st, g);
+  hipLaunchKernelGGL((vconv3x3_kernel<T16, BM, TH>), dim3((unsigned)tiles), dim3(256), 0, st, g);
 }
 
 static int vc_bm(int M) { return (M % 128 == 0) ? 128 : 64; }
@@ -417,8 +434,11 @@ int dsgan_vconv_wtrans(const float* W, void* Wt, int Co, int Ci, int dgrad, hipS
   const long total = 9L * Co * Ci;
   long blocks = (total + 255) / 256;
   if (blocks > 8192) blocks = 8192;
-  hipLaunchKernelGGL(vconv_wtrans_kernel, dim3((unsigned)blocks), dim3(256), 0, st, W, (__bf16*)Wt, Co, Ci, vc_bm(M),
-                     dgrad);
+  with_half([&](auto* t_) {
+    using T16 = std::remove_pointer_t<decltype(t_)>;
+    hipLaunchKernelGGL((vconv_wtrans_kernel<T16>), dim3((unsigned)blocks), dim3(256), 0, st, W, (T16*)Wt, Co, Ci,
+                       vc_bm(M), dgrad);
+  });
   DSG_CHECK_LAUNCH();
   return 0;
 }
@@ -431,17 +451,20 @@ int dsgan_vconv3x3(const void* X, const void* Wt, const float* bias, const void*
   DSG_REQUIRE(dsgan_vconv_supported(K, M, H, W), "dsgan_vconv3x3: unsupported K=%d M=%d H=%d W=%d", K, M, H, W);
   DSG_REQUIRE((((uintptr_t)X | (uintptr_t)Wt | (uintptr_t)Y | (uintptr_t)bias | (uintptr_t)mask) & 15) == 0,
               "dsgan_vconv3x3: 16-byte aligned operands required");
-  VcArgs g{};
-  g.X = (const __bf16*)X; g.Wt = (const __bf16*)Wt; g.bias = bias; g.mask = (const __bf16*)mask; g.Y = Y;
-  g.N = N; g.K = K; g.M = M; g.H = H; g.W = W; g.relu = relu; g.y_f32 = y_f32;
-  const int BM = vc_bm(M);
-  // 8-row pixel tiles unless that leaves fewer than two workgroups per CU
-  const bool th8 = H % 8 == 0 && (long)N * (W / 32) * (H / 8) * (M / BM) >= 512;
-  if (BM == 128) {
-    if (th8) vc_launch<128, 8>(g, st); else vc_launch<128, 4>(g, st);
-  } else {
-    if (th8) vc_launch<64, 8>(g, st); else vc_launch<64, 4>(g, st);
-  }
+  with_half([&](auto* t_) {
+    using T16 = std::remove_pointer_t<decltype(t_)>;
+    VcArgs<T16> g{};
+    g.X = (const T16*)X; g.Wt = (const T16*)Wt; g.bias = bias; g.mask = (const T16*)mask; g.Y = Y;
+    g.N = N; g.K = K; g.M = M; g.H = H; g.W = W; g.relu = relu; g.y_f32 = y_f32;
+    const int BM = vc_bm(M);
+    // 8-row pixel tiles unless that leaves fewer than two workgroups per CU
+    const bool th8 = H % 8 == 0 && (long)N * (W / 32) * (H / 8) * (M / BM) >= 512;
+    if (BM == 128) {
+      if (th8) vc_launch<T16, 128, 8>(g, st); else vc_launch<T16, 128, 4>(g, st);
+    } else {
+      if (th8) vc_launch<T16, 64, 8>(g, st); else vc_launch<T16, 64, 4>(g, st);
+    }
+  });
   DSG_CHECK_LAUNCH();
   return 0;
 }
@@ -451,8 +474,11 @@ int dsgan_vgg_conv1_fwd(const float* x, long x_bs, const float* w, const float* 
                         hipStream_t st) {
   DSG_REQUIRE(x && w && b && y && N > 0 && H > 0 && W > 0 && (((uintptr_t)y) & 15) == 0, "dsgan_vgg_conv1_fwd: bad args");
   const long total = (long)N * 4 * H * W;
-  hipLaunchKernelGGL(vgg_conv1_fwd_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, x, x_bs, w, b,
-                     (__bf16*)y, N, H, W);
+  with_half([&](auto* t_) {
+    using T16 = std::remove_pointer_t<decltype(t_)>;
+    hipLaunchKernelGGL((vgg_conv1_fwd_kernel<T16>), dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, x, x_bs,
+                       w, b, (T16*)y, N, H, W);
+  });
   DSG_CHECK_LAUNCH();
   return 0;
 }
@@ -461,8 +487,11 @@ int dsgan_vgg_conv1_fwd(const float* x, long x_bs, const float* w, const float* 
 int dsgan_vgg_conv1_dgrad(const void* d, const float* w, float* dx, long dx_bs, int N, int H, int W, hipStream_t st) {
   DSG_REQUIRE(d && w && dx && N > 0 && (((uintptr_t)d) & 15) == 0, "dsgan_vgg_conv1_dgrad: bad args");
   const long total = (long)N * H * W;
-  hipLaunchKernelGGL(vgg_conv1_dgrad_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st,
-                     (const __bf16*)d, w, dx, dx_bs, N, H, W);
+  with_half([&](auto* t_) {
+    using T16 = std::remove_pointer_t<decltype(t_)>;
+    hipLaunchKernelGGL((vgg_conv1_dgrad_kernel<T16>), dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st,
+                       (const T16*)d, w, dx, dx_bs, N, H, W);
+  });
   DSG_CHECK_LAUNCH();
   return 0;
 }
@@ -471,8 +500,11 @@ int dsgan_vgg_conv1_dgrad(const void* d, const float* w, float* dx, long dx_bs, 
 int dsgan_cb16_maxpool(const float* x, void* y, void* idx, int N, int C, int H, int W, hipStream_t st) {
   DSG_REQUIRE(x && y && idx && C % 16 == 0 && H % 2 == 0 && W % 2 == 0, "dsgan_cb16_maxpool: bad args");
   const long total = (long)N * (C / 4) * (H / 2) * (W / 2);
-  hipLaunchKernelGGL(cb16_maxpool_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, x, (__bf16*)y,
-                     (unsigned char*)idx, N, C, H, W);
+  with_half([&](auto* t_) {
+    using T16 = std::remove_pointer_t<decltype(t_)>;
+    hipLaunchKernelGGL((cb16_maxpool_kernel<T16>), dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, x,
+                       (T16*)y, (unsigned char*)idx, N, C, H, W);
+  });
   DSG_CHECK_LAUNCH();
   return 0;
 }
@@ -485,8 +517,11 @@ int dsgan_cb16_tap_bwd(const void* dpool, const void* idx, const float* f, const
               "dsgan_cb16_tap_bwd: bad args");
   const long total = (long)N * (C / 4) * (H / 2) * (W / 2);
   const float coef = 1.f / ((float)N * C * H * W);
-  hipLaunchKernelGGL(cb16_tap_bwd_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st,
-                     (const __bf16*)dpool, (const unsigned char*)idx, f, r, (__bf16*)d, N, C, H, W, gout, coef);
+  with_half([&](auto* t_) {
+    using T16 = std::remove_pointer_t<decltype(t_)>;
+    hipLaunchKernelGGL((cb16_tap_bwd_kernel<T16>), dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st,
+                       (const T16*)dpool, (const unsigned char*)idx, f, r, (T16*)d, N, C, H, W, gout, coef);
+  });
   DSG_CHECK_LAUNCH();
   return 0;
 }

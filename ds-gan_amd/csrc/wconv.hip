@@ -26,10 +26,7 @@
 
 namespace dsg {
 
-typedef __attribute__((ext_vector_type(8))) __bf16 wbf16x8;
-typedef __attribute__((ext_vector_type(4))) __bf16 wbf16x4;
-typedef __attribute__((ext_vector_type(2))) __bf16 wbf16x2;
-typedef __attribute__((ext_vector_type(16))) float wf32x16;
+typedef f32x16_t wf32x16;
 typedef __attribute__((ext_vector_type(4))) unsigned int wu32x4;
 
 struct WcArgs {
@@ -62,8 +59,9 @@ template <> struct WcGeo<1> {
 };
 
 // 8 consecutive bf16 starting SH elements after the 16-byte aligned p.
-template <int SH>
-__device__ __forceinline__ wbf16x8 frag_at(const __bf16* p) {
+template <int SH, typename T16>
+__device__ __forceinline__ hx8<T16> frag_at(const T16* p) {
+  typedef hx8<T16> wbf16x8;
   if constexpr (SH == 0) {
     return *reinterpret_cast<const wbf16x8*>(p);
   } else {
@@ -79,8 +77,11 @@ __device__ __forceinline__ wbf16x8 frag_at(const __bf16* p) {
   }
 }
 
-template <int KH, int KW, int S>
+template <typename T16, int KH, int KW, int S>
 __global__ __launch_bounds__(256, 1) void wconv_kernel(WcArgs g) {
+  typedef hx8<T16> wbf16x8;
+  typedef hx4<T16> wbf16x4;
+  typedef T16 wbf16x2 __attribute__((ext_vector_type(2)));
   constexpr int T = KH * KW, NT4 = (T + 3) / 4;
   constexpr int PX = WC_TH * WC_TW;
   constexpr int PH = (WC_TH - 1) * S + KH;
@@ -94,8 +95,8 @@ __global__ __launch_bounds__(256, 1) void wconv_kernel(WcArgs g) {
   constexpr int B_ITEMS = WC_BC * PH * NQ;                // (c, patch row, float4) items
   constexpr int B_IT = (B_ITEMS + 255) / 256;
   static_assert(A_IT * 256 * 4 == WC_BM * PX, "A items");
-  __shared__ __attribute__((aligned(16))) __bf16 As[WC_BM * A_STR];
-  __shared__ __attribute__((aligned(16))) __bf16 Bs[WC_BC * C_STR];
+  __shared__ __attribute__((aligned(16))) T16 As[WC_BM * A_STR];
+  __shared__ __attribute__((aligned(16))) T16 Bs[WC_BC * C_STR];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int lr = lane & 31, lh = lane >> 5;
@@ -158,7 +159,7 @@ __global__ __launch_bounds__(256, 1) void wconv_kernel(WcArgs g) {
 #pragma unroll
     for (int i = 0; i < A_IT; ++i) {
       const int it = tid + i * 256, mm = it / (PX / 4), qq = it % (PX / 4);
-      const wbf16x4 v = {(__bf16)ra[i].x, (__bf16)ra[i].y, (__bf16)ra[i].z, (__bf16)ra[i].w};
+      const wbf16x4 v = {(T16)ra[i].x, (T16)ra[i].y, (T16)ra[i].z, (T16)ra[i].w};
       *reinterpret_cast<wbf16x4*>(As + mm * A_STR + qq * 4) = v;
     }
 #pragma unroll
@@ -167,14 +168,14 @@ __global__ __launch_bounds__(256, 1) void wconv_kernel(WcArgs g) {
       if (it < B_ITEMS) {
         const int q4 = it % NQ, rest = it / NQ;
         const int pr = rest % PH, c = rest / PH;
-        __bf16* row = Bs + c * C_STR + pr * (S * WC_JW);
+        T16* row = Bs + c * C_STR + pr * (S * WC_JW);
         if constexpr (S == 2) {
           // plane 1 <- (x, z) at j = 2q-2 (skip q = 0: j < 0); plane 0 <- (y, w) stored at 2q
-          if (q4 > 0) *reinterpret_cast<wbf16x2*>(row + WC_JW + 2 * q4 - 2) = wbf16x2{(__bf16)rb[i].x, (__bf16)rb[i].z};
-          *reinterpret_cast<wbf16x2*>(row + 2 * q4) = wbf16x2{(__bf16)rb[i].y, (__bf16)rb[i].w};
+          if (q4 > 0) *reinterpret_cast<wbf16x2*>(row + WC_JW + 2 * q4 - 2) = wbf16x2{(T16)rb[i].x, (T16)rb[i].z};
+          *reinterpret_cast<wbf16x2*>(row + 2 * q4) = wbf16x2{(T16)rb[i].y, (T16)rb[i].w};
         } else {
           *reinterpret_cast<wbf16x4*>(row + 4 * q4) =
-              wbf16x4{(__bf16)rb[i].x, (__bf16)rb[i].y, (__bf16)rb[i].z, (__bf16)rb[i].w};
+              wbf16x4{(T16)rb[i].x, (T16)rb[i].y, (T16)rb[i].z, (T16)rb[i].w};
         }
       }
     }
@@ -207,7 +208,7 @@ __global__ __launch_bounds__(256, 1) void wconv_kernel(WcArgs g) {
         for (int i = 0; i < NT4; ++i) {
           if (WV + 4 * i < T) {
             const int t = WV + 4 * i, kh = t / KW, kw = t % KW;
-            const __bf16* row = Bs + lr * C_STR + (S * r + kh) * (S * WC_JW) + (kw % S) * WC_JW + lh * 8;
+            const T16* row = Bs + lr * C_STR + (S * r + kh) * (S * WC_JW) + (kw % S) * WC_JW + lh * 8;
             wbf16x8 bf;
             switch (WcGeo<S>::shift(kw)) {   // folds: t, kw are compile-time after unrolling
               case 0: bf = frag_at<0>(row); break;
@@ -218,8 +219,8 @@ __global__ __launch_bounds__(256, 1) void wconv_kernel(WcArgs g) {
               case 5: bf = frag_at<5>(row); break;
               default: bf = frag_at<6>(row); break;
             }
-            acc[0][i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, bf, acc[0][i], 0, 0, 0);
-            acc[1][i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, bf, acc[1][i], 0, 0, 0);
+            acc[0][i] = mfma16(a0, bf, acc[0][i]);
+            acc[1][i] = mfma16(a1, bf, acc[1][i]);
           }
         }
       }
@@ -301,9 +302,9 @@ static WcPlan wc_plan(int nb, int C, int M, int Ho, int Wo) {
   return p;
 }
 
-template <int K, int S>
+template <typename T16, int K, int S>
 static void wc_launch(WcArgs& g, int grid, hipStream_t st) {
-  hipLaunchKernelGGL((wconv_kernel<K, K, S>), dim3((unsigned)grid), dim3(256), 0, st, g);
+  hipLaunchKernelGGL((wconv_kernel<T16, K, K, S>), dim3((unsigned)grid), dim3(256), 0, st, g);
 }
 
 }  // namespace dsg
@@ -341,10 +342,13 @@ int dsgan_wconv(const float* D, long d_bs, const float* X, long x_bs, float* dw,
   g.nbw = p.nbw; g.nbh = p.nbh; g.nblk = p.nblk; g.bps = p.bps; g.mt = p.mt; g.ct = p.ct;
   g.vec_d = ((uintptr_t)D % 16 == 0) && (d_bs % 4 == 0) && (Wo % 4 == 0);
   const int grid = p.splits * p.mt * p.ct;
-  if (KH == 3 && stride == 2) wc_launch<3, 2>(g, grid, st);
-  else if (KH == 3 && stride == 1) wc_launch<3, 1>(g, grid, st);
-  else if (KH == 4 && stride == 2) wc_launch<4, 2>(g, grid, st);
-  else wc_launch<4, 1>(g, grid, st);
+  with_half([&](auto* t_) {
+    using T16 = std::remove_pointer_t<decltype(t_)>;
+    if (KH == 3 && stride == 2) wc_launch<T16, 3, 2>(g, grid, st);
+    else if (KH == 3 && stride == 1) wc_launch<T16, 3, 1>(g, grid, st);
+    else if (KH == 4 && stride == 2) wc_launch<T16, 4, 2>(g, grid, st);
+    else wc_launch<T16, 4, 1>(g, grid, st);
+  });
   DSG_CHECK_LAUNCH();
   const long total4 = (long)KH * KW * M * C / 4;
   long blocks = (total4 + 255) / 256;

@@ -20,6 +20,11 @@ S = ctypes.c_void_p  # hipStream_t
 
 SIGNATURES = {
     "dsgan_abi_version": [],
+    "dsgan_set_half_type": [ctypes.c_int],
+    "dsgan_amp_parts": [],
+    "dsgan_amp_check": [P, L, P, P, F, F, I, S],
+    "dsgan_adam_amp": [P, P, P, P, L, F, F, F, F, P, S],
+    "dsgan_get_half_type": [],
     "dsgan_last_error_string": [],
     # igemm.hip
     "dsgan_conv_fwd": [P, L, P, P, P, L, P, L] + [I] * 12 + [F, I, I, I, S],

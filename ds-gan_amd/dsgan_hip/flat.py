@@ -64,9 +64,10 @@ class FlatAdam(torch.optim.Optimizer):
     DSGAN/models/networks.py:33-46) drives ``param_groups[0]['lr']`` exactly as before.
     """
 
-    def __init__(self, flat, lr=2e-4, betas=(0.9, 0.999), eps=1e-8):
+    def __init__(self, flat, lr=2e-4, betas=(0.9, 0.999), eps=1e-8, scaler=None):
         super().__init__(flat.params, dict(lr=lr, betas=betas, eps=eps))
         self.flat = flat
+        self.scaler = scaler   # dsgan_hip.amp.LossScaler (--precision fp16): unscale / skip on device
         self.m = torch.zeros_like(flat.data)
         self.v = torch.zeros_like(flat.data)
         self.step_count = 0
@@ -79,8 +80,15 @@ class FlatAdam(torch.optim.Optimizer):
         self.step_count += 1
         g = self.param_groups[0]
         b1, b2 = g["betas"]
-        call("dsgan_adam", ptr(self.flat.data), ptr(self.flat.grad), ptr(self.m), ptr(self.v),
-             self.flat.numel, float(g["lr"]), float(b1), float(b2), float(g["eps"]),
-             self.step_count, stream())
+        if self.scaler is not None:
+            # the scaler's check() has run on this gradient: g / scale, skipped on overflow, its
+            # own step count for the bias corrections (step_count here counts calls)
+            call("dsgan_adam_amp", ptr(self.flat.data), ptr(self.flat.grad), ptr(self.m), ptr(self.v),
+                 self.flat.numel, float(g["lr"]), float(b1), float(b2), float(g["eps"]), ptr(self.scaler.state),
+                 stream())
+        else:
+            call("dsgan_adam", ptr(self.flat.data), ptr(self.flat.grad), ptr(self.m), ptr(self.v),
+                 self.flat.numel, float(g["lr"]), float(b1), float(b2), float(g["eps"]),
+                 self.step_count, stream())
         bump_weight_generation(self.flat.params)
         return None

@@ -18,17 +18,24 @@ from . import _lib
 from ._lib import call, ptr, stream
 
 ACT = {None: 0, "none": 0, "gelu": 1, "relu": 2, "lrelu": 3, "sigmoid": 4}
-PREC = {"fp32": 0, "bf16": 1}
+PREC = {"fp32": 0, "bf16": 1, "fp16": 1}   # the C ABI's prec: 0 exact f32, 1 16-bit MFMA operands
 _state = {"prec": "fp32"}
 IN_EPS = 1e-5
 LRELU_SLOPE = 0.2
 
 
 def set_precision(p):
-    """'fp32' (exact f32 MFMA, parity mode) or 'bf16' (bf16 MFMA operands, fp32 accumulate)."""
+    """'fp32' (exact f32 MFMA, parity mode), 'bf16' (bf16 MFMA operands, fp32 accumulate) or
+    'fp16' (IEEE fp16 MFMA operands and 16-bit storage, fp32 accumulate; BASELINE configs[4]).
+    bf16 and fp16 run the same kernels: the library's half type (dsgan_set_half_type) selects
+    the 16-bit instantiation, so it follows the precision here."""
     if p not in PREC:
         raise ValueError(p)
     _state["prec"] = p
+    want = 1 if p == "fp16" else 0
+    lib = _lib.load()
+    if lib.dsgan_get_half_type() != want:
+        call("dsgan_set_half_type", want)
 
 
 def get_precision():
@@ -45,11 +52,21 @@ def precision(p):
     try:
         yield
     finally:
-        _state["prec"] = old
+        set_precision(old)
 
 
 def _prec():
     return PREC[_state["prec"]]
+
+
+def _is16():
+    """16-bit MFMA operands (bf16 or fp16 mode)."""
+    return _state["prec"] != "fp32"
+
+
+def half_dtype():
+    """torch dtype of the 16-bit operand / storage tensors of the current precision."""
+    return torch.float16 if _state["prec"] == "fp16" else torch.bfloat16
 
 
 class KernelTimer:
@@ -156,7 +173,7 @@ def _grad_buf(p):
 # ------------------------------------------------------------------------------------------
 
 def _pw_ok(mode, M, K, P, a_bs, b_bs, a, b):
-    if _state["prec"] != "bf16":
+    if not _is16():
         return False
     return bool(_lib.load().dsgan_pw_supported(mode, M, K, P, a_bs, b_bs, a, b))
 
@@ -172,7 +189,7 @@ def _tconv(X, xbs, Wt, bias, Y, ybs, gpre, gbs, nb, K, M, Hin, Win, Hout, Wout, 
     call("dsgan_tconv_ws", ptr(X), xbs, ptr(Wt), ptr(bias), ptr(Y), ybs, ptr(gpre), gbs, nb, K, M, Hin,
          Win, Hout, Wout, stride, len(taps), ctypes.cast(dh, ctypes.c_void_p),
          ctypes.cast(dw, ctypes.c_void_p), Hdst, Wdst, os_, ph, pw, ACT[act], ACT[gact],
-         LRELU_SLOPE, int(Wt.dtype == torch.bfloat16), ptr(ws), stream())
+         LRELU_SLOPE, int(Wt.dtype != torch.float32), ptr(ws), stream())
 
 
 # Transformed-weight cache: an entry is valid while the parameter's storage pointer and the
@@ -223,13 +240,13 @@ def _wtrans_build(w, mode, kh0=0, kw0=0, nth=0, ntw=0):
 def _wtrans_bf16(w, mode):
     """bf16 tap-major weights for pconv.hip / pconvt.hip (mode 0 forward, 1 stride-1 data-grad,
     2 stride-2 data-grad / ConvTranspose), cached."""
-    key = (id(w), w.data_ptr(), tuple(w.shape), "bf16", mode)
+    key = (id(w), w.data_ptr(), tuple(w.shape), half_dtype(), mode)
     ent = _WT_CACHE.get(key)
     gen = _wgen(w)
     if ent is not None and ent[0] == gen and ent[1] == w._version and ent[2] is w:
         return ent[3]
     Co, Ci, KH, KW = w.shape
-    wb = torch.empty(KH * KW * Co * Ci, device=w.device, dtype=torch.bfloat16)
+    wb = torch.empty(KH * KW * Co * Ci, device=w.device, dtype=half_dtype())
     call("dsgan_conv_wtrans_bf16", ptr(w), ptr(wb), Co, Ci, KH, KW, mode, stream())
     _WT_CACHE[key] = (gen, w._version, w, wb)
     return wb
@@ -259,7 +276,7 @@ def _thin3_ok(M, H, W, bs_small, bs_big, t_small, t_big):
 
 
 def _pconv_ok(K, KH, KW, stride):
-    return _state["prec"] == "bf16" and bool(_lib.load().dsgan_pconv_supported(K, KH, KW, stride))
+    return _is16() and bool(_lib.load().dsgan_pconv_supported(K, KH, KW, stride))
 
 
 def _pconv(x, xbs, wb, b, y, ybs, N, K, M, H, W, Ho, Wo, KH, KW, stride, pad, act, gpre, gbs, gact, accumulate):
@@ -318,7 +335,7 @@ def conv_fwd_raw(x, w, b, stride, pad, act=None, out=None, pre=None, accumulate=
         fam = "pconv_kernel"
         _pconv(x, xbs, _wtrans_bf16(w, 0), b, y, ybs, N, Cin, Cout, H, W, Ho, Wo, KH, KW, stride, pad, act,
                None, 0, None, accumulate)
-    elif (_state["prec"] == "bf16" and w.dim() == 4 and (KH > 1 or KW > 1) and Cin % 32 == 0
+    elif (_is16() and w.dim() == 4 and (KH > 1 or KW > 1) and Cin % 32 == 0
           and pre is None and not accumulate and xact is None and KH * KW <= 16):
         fam = "tconv_kernel"
         wt = _wtrans_bf16(w, 0) if Cin % 8 == 0 else _wtrans(w, 0)
@@ -383,14 +400,14 @@ def conv_dgrad_raw(dy, w, x_shape, stride, pad, bias=None, act=None, gpre=None, 
         fam = "pconv_kernel"
         _pconv(dy, dybs, _wtrans_bf16(w, 1), None, dx, dxbs, N, Cout, Cin, Ho, Wo, H, W, KH, KW, 1,
                KH - 1 - pad, None, gpre, gbs, gact, accumulate)
-    elif (_state["prec"] == "bf16" and w.dim() == 4 and stride == 2 and pad == 1 and KH == KW and act is None
+    elif (_is16() and w.dim() == 4 and stride == 2 and pad == 1 and KH == KW and act is None
           and H <= 2 * Ho and H > 2 * Ho - 2 and W <= 2 * Wo and W > 2 * Wo - 2 and W % 2 == 0 and dxbs % 2 == 0
           and (gpre is None or gbs % 2 == 0) and _lib.load().dsgan_pconvt_supported(Cout, KH, stride, pad)):
         # stride-2 data-grad / ConvTranspose: all four output parities in one launch
         fam = "pconvt_kernel"
         call("dsgan_pconvt", ptr(dy), dybs, ptr(_wtrans_bf16(w, 2)), ptr(bias), ptr(dx), dxbs, ptr(gpre), gbs, N,
              Cout, Cin, Ho, Wo, H, W, KH, stride, pad, ACT[gact], LRELU_SLOPE, int(accumulate), stream())
-    elif (_state["prec"] == "bf16" and w.dim() == 4 and (KH > 1 or KW > 1) and Cout % 32 == 0
+    elif (_is16() and w.dim() == 4 and (KH > 1 or KW > 1) and Cout % 32 == 0
           and act is None and not accumulate and stride in (1, 2) and KH * KW <= 16):
         fam = "tconv_kernel"
         if stride == 1:
@@ -458,7 +475,7 @@ def conv_wgrad_raw(dy, x, dw, stride, pad, xact=None, db=None):
         ws = torch.empty(nws, device=dy.device, dtype=torch.float32) if nws > 0 else None
         call("dsgan_pw_gemm_f32", 2, ptr(dy), dybs, ptr(x), xbs, ptr(dw), 0, None, None, 0, Cout, Cin, N * H * W,
              H * W, N, 0, 0, 0, LRELU_SLOPE, ptr(ws), stream())
-    elif (xact is None and _state["prec"] == "bf16" and dw.is_contiguous() and pad == 1 and W % 4 == 0
+    elif (xact is None and _is16() and dw.is_contiguous() and pad == 1 and W % 4 == 0
           and xbs % 4 == 0 and x.data_ptr() % 16 == 0 and _lib.load().dsgan_wconv_supported(Cin, KH, KW, stride)):
         fam = "wconv_kernel"
         Ho, Wo = dy.shape[2], dy.shape[3]
@@ -702,12 +719,12 @@ _BF16_CACHE = {}
 
 def bf16_weight(w):
     """bf16 copy of a parameter for the fused kernels, cached like _wtrans (same invalidation)."""
-    key = (id(w), w.data_ptr(), tuple(w.shape))
+    key = (id(w), w.data_ptr(), tuple(w.shape), half_dtype())
     ent = _BF16_CACHE.get(key)
     gen = _wgen(w)
     if ent is not None and ent[0] == gen and ent[1] == w._version and ent[2] is w:
         return ent[3]
-    out = torch.empty(w.shape, device=w.device, dtype=torch.bfloat16)
+    out = torch.empty(w.shape, device=w.device, dtype=half_dtype())
     call("dsgan_f32_to_bf16", ptr(w), ptr(out), w.numel(), stream())
     if len(_BF16_CACHE) > 8192:
         _BF16_CACHE.clear()
@@ -717,7 +734,7 @@ def bf16_weight(w):
 
 def _mlp_tile(C, P, HW, x):
     """Pixels per b1-grad partial row of the fused MLP kernels (mlp.hip), 0 if unsupported."""
-    if _state["prec"] != "bf16" or x.data_ptr() % 16:
+    if not _is16() or x.data_ptr() % 16:
         return 0
     return int(_lib.load().dsgan_mlp_supported(C, P, HW))
 
@@ -753,7 +770,7 @@ class PwMlpFn(torch.autograd.Function):
         ctx.box_h, ctx.box_x = _box(h), _box(x)
         h, hbs = nchw(h)
         tile = _mlp_tile(C, P, HW, x)
-        bigg = (not tile and _state["prec"] == "bf16" and HW % 128 == 0 and C % 8 == 0
+        bigg = (not tile and _is16() and HW % 128 == 0 and C % 8 == 0
                 and (norm or h.data_ptr() % 16 == 0))
         ctx.nrm = None
         if norm:
@@ -761,7 +778,7 @@ class PwMlpFn(torch.autograd.Function):
             if (tile or bigg) and d.data_ptr() % 16 == 0 and dbs % 4 == 0 and HW % 4 == 0:
                 mean = torch.empty(N * C, device=d.device, dtype=torch.float32)
                 rstd = torch.empty(N * C, device=d.device, dtype=torch.float32)
-                h = torch.empty((N, C, H, W), device=d.device, dtype=torch.bfloat16)
+                h = torch.empty((N, C, H, W), device=d.device, dtype=half_dtype())
                 e0 = AUX_TIMER.begin()
                 call("dsgan_instnorm_fwd_bf16", ptr(d), dbs, ptr(h), C * HW, ptr(mean), ptr(rstd), N, C, HW, IN_EPS,
                      stream())
@@ -773,7 +790,7 @@ class PwMlpFn(torch.autograd.Function):
             ctx.nrm = (d, mean, rstd)
         elif h.data_ptr() % 16:
             tile = 0
-        hb = int(h.dtype == torch.bfloat16)
+        hb = int(h.dtype != torch.float32)
         ctx.hb = hb
         ctx.tile = tile
         if tile:
@@ -791,8 +808,8 @@ class PwMlpFn(torch.autograd.Function):
         if bigg:
             # large blocks: pwconv1 evaluates GELU once and writes g = gelu(z) and gp = gelu'(z), both
             # bf16; pwconv2 and the W2 weight-grad stream g, the pwconv2 data-grad multiplies by gp
-            gp = torch.empty((N, C4, H, W), device=h.device, dtype=torch.bfloat16)   # gelu'(z), for dz
-            g = torch.empty((N, C4, H, W), device=h.device, dtype=torch.bfloat16)    # gelu(z)
+            gp = torch.empty((N, C4, H, W), device=h.device, dtype=half_dtype())   # gelu'(z), for dz
+            g = torch.empty((N, C4, H, W), device=h.device, dtype=half_dtype())    # gelu(z)
             e0 = IGEMM_TIMER.begin()
             call("dsgan_pw_fwd_io", ptr(bf16_weight(w1)), 1, ptr(h), hbs, hb, ptr(g), C4 * HW, 1, ptr(gp), C4 * HW, 1, ptr(b1), C4, C,
                  HW, N, ACT["gelu"], 0, LRELU_SLOPE, stream())
@@ -853,7 +870,7 @@ class PwMlpFn(torch.autograd.Function):
             # grad as fp32 partial row sums of the same epilogue
             N, C4, H, W = z.shape
             HW, P, C = H * W, w2.shape[0], h.shape[1]
-            dz = torch.empty((N, C4, H, W), device=dy.device, dtype=torch.bfloat16)
+            dz = torch.empty((N, C4, H, W), device=dy.device, dtype=half_dtype())
             e0 = IGEMM_TIMER.begin()
             call("dsgan_pw_dgrad_io", ptr(bf16_weight(w2)), 1, ptr(dy), dybs, 0, ptr(dz), C4 * HW, 1, ptr(z), C4 * HW,
                  C4, P, HW, N, 0, stream())
@@ -948,7 +965,7 @@ class PwMlpFn(torch.autograd.Function):
                 conv_wgrad_raw(dy, x, gws, 1, 0)
             _params_done(*ctx.refs)
             return dh, PwMlpFn._dx(ctx, dy, ws, x)
-        g = torch.empty((N, C4, H, W), device=h.device, dtype=torch.bfloat16)
+        g = torch.empty((N, C4, H, W), device=h.device, dtype=half_dtype())
         dz = torch.empty_like(g)
         e0 = IGEMM_TIMER.begin()
         call("dsgan_mlp_bwd", ptr(h), C * HW, ctx.hb, ptr(dy), dybs, ptr(bf16_weight(w1)), ptr(b1),
@@ -1292,7 +1309,7 @@ def vgg_features_raw(x, blocks):
 
 def vgg_cb16_ok(x):
     """bf16 mode and every VGG block resolution a multiple of 32 pixels wide (W % 256, H % 32)."""
-    return _state["prec"] == "bf16" and x.dim() == 4 and x.shape[3] % 256 == 0 and x.shape[2] % 32 == 0
+    return _is16() and x.dim() == 4 and x.shape[3] % 256 == 0 and x.shape[2] % 32 == 0
 
 
 def _cb16_empty(N, C, H, W, like, dtype):
@@ -1301,13 +1318,13 @@ def _cb16_empty(N, C, H, W, like, dtype):
 
 def _vgg_wt(w, dgrad):
     """bf16 weights of a VGG conv swizzled into vconv3x3's LDS image (dsgan_vconv_wtrans), cached."""
-    key = (id(w), w.data_ptr(), tuple(w.shape), "vconv", dgrad)
+    key = (id(w), w.data_ptr(), tuple(w.shape), "vconv", dgrad, half_dtype())
     ent = _WT_CACHE.get(key)
     gen = _wgen(w)
     if ent is not None and ent[0] == gen and ent[1] == w._version and ent[2] is w:
         return ent[3]
     Co, Ci = w.shape[0], w.shape[1]
-    wt = torch.empty(_lib.load().dsgan_vconv_wtrans_size(Co, Ci), device=w.device, dtype=torch.bfloat16)
+    wt = torch.empty(_lib.load().dsgan_vconv_wtrans_size(Co, Ci), device=w.device, dtype=half_dtype())
     call("dsgan_vconv_wtrans", ptr(w), ptr(wt), Co, Ci, int(dgrad), stream())
     _WT_CACHE[key] = (gen, w._version, w, wt)
     return wt
@@ -1335,14 +1352,14 @@ def vgg_features_cb16(x, blocks, keep=False):
             f = feats[-1]
             C = f.shape[1] * 16
             H, W = H // 2, W // 2
-            h = _cb16_empty(N, C, H, W, x, torch.bfloat16)
+            h = _cb16_empty(N, C, H, W, x, half_dtype())
             idx = torch.empty(h.shape, device=x.device, dtype=torch.uint8)
             call("dsgan_cb16_maxpool", ptr(f), ptr(h), ptr(idx), N, C, 2 * H, 2 * W, stream())
         acts = []
         for li, (w, b) in enumerate(convs):
             last = li == len(convs) - 1
             Co, Ci = w.shape[0], w.shape[1]
-            y = _cb16_empty(N, Co, H, W, x, torch.float32 if last else torch.bfloat16)
+            y = _cb16_empty(N, Co, H, W, x, torch.float32 if last else half_dtype())
             if bi == 0 and li == 0:   # conv1_1, 3 -> 64: exact fp32 FMAs from the NCHW image
                 call("dsgan_vgg_conv1_fwd", ptr(x), xbs, ptr(w), ptr(b), ptr(y), N, H, W, stream())
             else:
@@ -1365,7 +1382,7 @@ def _perceptual_bwd_cb16(ctx, g):
         idx, acts = ctx.saved[bi]
         f, r = ctx.feats[bi], ctx.real[bi]
         N, Cb, H, W, _ = f.shape
-        dpre = _cb16_empty(N, Cb * 16, H, W, f, torch.bfloat16)
+        dpre = _cb16_empty(N, Cb * 16, H, W, f, half_dtype())
         call("dsgan_cb16_tap_bwd", ptr(d), ptr(d_idx), ptr(f), ptr(r), ptr(dpre), N, Cb * 16, H, W, ptr(g), stream())
         for li in range(len(convs) - 1, -1, -1):
             w = convs[li][0]
@@ -1374,7 +1391,7 @@ def _perceptual_bwd_cb16(ctx, g):
                 dx = torch.empty(ctx.fake_shape, device=f.device, dtype=torch.float32)
                 call("dsgan_vgg_conv1_dgrad", ptr(dpre), ptr(w), ptr(dx), Ci * H * W, N, H, W, stream())
             else:
-                out = _cb16_empty(N, Ci, H, W, f, torch.bfloat16)
+                out = _cb16_empty(N, Ci, H, W, f, half_dtype())
                 _vconv(dpre, _vgg_wt(w, 1), None, acts[li - 1] if li > 0 else None, out, N, Co, Ci, H, W, False, "dgrad")
                 dpre = out
         d, d_idx = dpre, idx

@@ -18,7 +18,10 @@ Deliberate, documented deviations:
     *means* (BCE, L1, VGG-L1, SSIM) are weighted by world * n_rank / n_global (1 when the global
     batch divides evenly), the TV term -- a batch *sum*, :189-191 -- by the world size, and the
     gradients are averaged; the ImagePool is per rank (its python RNG seeded 20 + 1000 * rank);
-  * the unused VGG relu5_3 block is not computed (the loss never reads it, :182-186).
+  * the unused VGG relu5_3 block is not computed (the loss never reads it, :182-186);
+  * --precision fp16 (BASELINE configs[4]): both backward passes run on a dynamically scaled loss
+    (dsgan_hip.amp.LossScaler, GradScaler semantics on the device), the optimizers unscale, and
+    an overflowed step is skipped; the logged losses are the unscaled ones.
 """
 import random
 
@@ -27,6 +30,7 @@ import torch
 from dsgan_hip import functional as HF
 from dsgan_hip import dist as hdist
 from dsgan_hip.flat import FlatParams, FlatAdam
+from dsgan_hip.amp import LossScaler
 from util.image_pool import ImagePool
 from .base_model import BaseModel
 from . import networks
@@ -87,8 +91,11 @@ class Pix2PixModel(BaseModel):
             hdist.broadcast_params(self.flatG)
             hdist.broadcast_params(self.flatD)
             self.optimizers = []
-            self.optimizer_G = FlatAdam(self.flatG, lr=opt.lr, betas=(opt.beta1, 0.999))
-            self.optimizer_D = FlatAdam(self.flatD, lr=opt.lr, betas=(opt.beta1, 0.999))
+            fp16 = HF.get_precision() == "fp16"
+            self.scaler_G = LossScaler(self.device) if fp16 else None
+            self.scaler_D = LossScaler(self.device) if fp16 else None
+            self.optimizer_G = FlatAdam(self.flatG, lr=opt.lr, betas=(opt.beta1, 0.999), scaler=self.scaler_G)
+            self.optimizer_D = FlatAdam(self.flatD, lr=opt.lr, betas=(opt.beta1, 0.999), scaler=self.scaler_D)
             self.optimizers.append(self.optimizer_G)
             self.optimizers.append(self.optimizer_D)
             self.tv_scale = float(W)
@@ -120,7 +127,8 @@ class Pix2PixModel(BaseModel):
         pred_real = self.netD(real_AB)
         self.loss_D_real = self.criterionGAN(pred_real, True)
         self.loss_D = (self.loss_D_fake + self.loss_D_real) * 0.5
-        (self.loss_D if self.mean_w == 1.0 else self.loss_D * self.mean_w).backward()
+        loss = self.loss_D if self.mean_w == 1.0 else self.loss_D * self.mean_w
+        (loss if self.scaler_D is None else self.scaler_D.scale(loss)).backward()
 
     def backward_G(self):
         if self.use_gan == 1:
@@ -143,10 +151,11 @@ class Pix2PixModel(BaseModel):
         self.loss_G = (self.loss_G_GAN * self.w_gan + self.loss_G_L1 + self.loss_vgg * self.w_vgg
                        + self.tv_loss * self.w_tv + self.w_ss * self.loss_ssim)
         if self.mean_w == 1.0:
-            self.loss_G.backward()
+            loss = self.loss_G
         else:   # ragged global batch under DDP: reweight the batch means, not the TV sum
-            ((self.loss_G_GAN * self.w_gan + self.loss_G_L1 + self.loss_vgg * self.w_vgg + self.w_ss * self.loss_ssim)
-             * self.mean_w + self.tv_loss * self.w_tv).backward()
+            loss = ((self.loss_G_GAN * self.w_gan + self.loss_G_L1 + self.loss_vgg * self.w_vgg + self.w_ss * self.loss_ssim)
+                    * self.mean_w + self.tv_loss * self.w_tv)
+        (loss if self.scaler_G is None else self.scaler_G.scale(loss)).backward()
 
     def _launch_real_features(self):
         """vgg(real_B) (frozen, no grad) depends only on the input: run it on a side stream so it
@@ -177,6 +186,8 @@ class Pix2PixModel(BaseModel):
             self.backward_D()
             if self.exchange:
                 hdist.allreduce_mean_(self.flatD.grad, force=True)
+            if self.scaler_D is not None:
+                self.scaler_D.check(self.flatD.grad)
             self.optimizer_D.step()
         else:
             self.loss_D_fake = 0
@@ -188,6 +199,8 @@ class Pix2PixModel(BaseModel):
         self.backward_G()
         if self.g_buckets is not None:
             self.g_buckets.finish()
+        if self.scaler_G is not None:
+            self.scaler_G.check(self.flatG.grad)
         self.optimizer_G.step()
 
     # ---- train.py helpers (DSGAN/models/pix2pix_model.py:292-310) ----

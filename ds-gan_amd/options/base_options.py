@@ -73,7 +73,7 @@ class BaseOptions:
         parser.add_argument("--w_ss", default=1.25, help="weight of the ms-ssim loss")
         parser.add_argument("--use_condition", default=1, help="1 means add condition in discriminator")
         # ---- MI355X build flags ----
-        parser.add_argument("--precision", type=str, default="fp32", choices=["fp32", "bf16"],
+        parser.add_argument("--precision", type=str, default="fp32", choices=["fp32", "bf16", "fp16"],
                             help="operand precision of the MFMA contractions (accumulation is fp32)")
         parser.add_argument("--vgg_weights", type=str, default="",
                             help="local VGG16 weights (torchvision features.* or Vgg16 state dict)")

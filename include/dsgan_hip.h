@@ -16,8 +16,14 @@
  *   - Weight-gradient entry points ACCUMULATE (+=) into their outputs: the caller zeroes the
  *     flat gradient buffer once per optimizer step, exactly like autograd's accumulation.
  *   - act codes: 0 none, 1 GELU (erf), 2 ReLU, 3 LeakyReLU(slope), 4 sigmoid.
- *   - prec: 0 = exact f32 MFMA (v_mfma_f32_32x32x2_f32), 1 = bf16 MFMA operands with fp32
- *     accumulation (v_mfma_f32_32x32x16_bf16).
+ *   - prec: 0 = exact f32 MFMA (v_mfma_f32_32x32x2_f32), 1 = 16-bit MFMA operands with fp32
+ *     accumulation (v_mfma_f32_32x32x16_bf16 / _f16).
+ *   - 16-bit type: every "bf16" operand or storage flag, every 16-bit weight copy and every
+ *     16-bit MFMA below uses the library's HALF TYPE, set process-wide by dsgan_set_half_type:
+ *     0 = bf16 (default, --precision bf16), 1 = IEEE fp16 (--precision fp16, BASELINE configs[4]).
+ *     Names keep "bf16" for the default; in fp16 mode the same entry points read/write fp16.
+ *     The host selects it once per precision switch (dsgan_hip.functional.set_precision); calls
+ *     issued after a switch use the new type.
  */
 #ifndef DSGAN_HIP_H
 #define DSGAN_HIP_H
@@ -28,8 +34,11 @@
 extern "C" {
 #endif
 
-int dsgan_abi_version(void);
+int dsgan_abi_version(void);   /* 2: adds the half type and the fp16 mode */
 const char* dsgan_last_error_string(void);
+/* the 16-bit operand type (see Conventions): 0 bf16, 1 fp16; -1 for anything else */
+int dsgan_set_half_type(int t);
+int dsgan_get_half_type(void);
 
 /* ---- implicit-GEMM convolution (igemm.hip) ------------------------------------------------
  * Replaces nn.Conv2d / nn.Linear / nn.ConvTranspose2d forward+backward:
@@ -428,6 +437,17 @@ int dsgan_cb16_tap_bwd(const void* dpool, const void* idx, const float* f, const
 /* ---- fused Adam over a flat buffer (adam.hip): torch.optim.Adam pix2pix_model.py:122-125 -- */
 int dsgan_adam(float* p, const float* g, float* m, float* v, long n, float lr, float beta1,
                float beta2, float eps, int step, hipStream_t stream);
+/* fp16 mode (--precision fp16) dynamic loss scaling, device-resident (torch GradScaler semantics,
+ * no host sync).  state = fp32[5] {scale, skip, clean steps, 1/scale of this step, applied steps}.
+ * dsgan_amp_check: inf/nan scan of the flat gradient (16-byte aligned) + state update (skip the
+ * step and scale *= backoff on overflow; scale *= growth after `interval` clean steps);
+ * part = dsgan_amp_parts() ints of scratch.  dsgan_adam_amp: dsgan_adam on g * state[3] with the
+ * step count state[4]; no-op when state[1] != 0 (pix2pix_model.py:204-217 optimizer steps). */
+long dsgan_amp_parts(void);
+int dsgan_amp_check(const float* grad, long n, int* part, float* state, float backoff, float growth, int interval,
+                    hipStream_t stream);
+int dsgan_adam_amp(float* p, const float* g, float* m, float* v, long n, float lr, float beta1, float beta2,
+                   float eps, const float* state, hipStream_t stream);
 
 #ifdef __cplusplus
 }

@@ -39,7 +39,7 @@ def test_library_exports_every_symbol():
     lib = _lib.load()
     for name in _header_decls():
         assert hasattr(lib, name), name
-    assert lib.dsgan_abi_version() == 1
+    assert lib.dsgan_abi_version() == 2
     assert lib.dsgan_last_error_string() is not None
 
 

@@ -7,8 +7,11 @@
     loss (--ssim_loss ms_ssim, DSGAN/MS_SSIM.py:153-225): the terms that depend only on the
     step's inputs (fake_B, D_real, D_fake, G_L1, vgg, ms-ssim) vs the fp32 oracle, evaluated by
     the oracle in chunks (a batch mean of chunk means); the whole step fits in HBM and is finite.
-  * C5 shape (configs[4], per GPU): the same at 512x512, batch 8, single-scale SSIM.  (configs[4]
-    names fp16; the build's reduced-precision mode is bf16 -- DESIGN.md §3.)
+  * C5 (configs[4], per GPU) as named: one fp16 step at 512x512, batch 8 (fp16 MFMA operands and
+    16-bit storage, fp32 accumulation, device loss scaling) vs the fp32 oracle step on the same
+    batch (OracleStep.step_chunked: the 512^2 autograd graph is walked 2 samples at a time), with
+    the C2 bars, finite gradients and no overflow-skipped step; plus the same shape in bf16 (the
+    input-only terms).
 All at the reference's N(0, 0.02) init ("ref" weight recipe), pool_size 0.
 """
 import random
@@ -148,3 +151,37 @@ def test_c5_bf16_step_512_b8():
     m.optimize_parameters()
     torch.cuda.synchronize()
     _check_input_terms(m, gp, dp, A, B, 2, "ssim")
+
+
+@pytest.mark.timeout(1500)
+def test_c5_fp16_step_512_b8_vs_oracle():
+    torch.set_num_threads(16)
+    torch.cuda.reset_peak_memory_stats()
+    m, gp, dp = _model("fp16", 8)
+    A, B = synth_pair(8, 512, seed=51)
+    m.set_input({"A": A.cuda(), "B": B.cuda(), "A_paths": [""] * 8, "B_paths": [""] * 8})
+    m.optimize_parameters()
+    torch.cuda.synchronize()
+    got = _losses(m)
+    skipped = (m.scaler_G.skipped_last(), m.scaler_D.skipped_last())
+    gG = torch.cat([p.grad.detach().flatten() for p in m.netG.parameters()]).cpu()
+    gD = torch.cat([p.grad.detach().flatten() for p in m.netD.parameters()]).cpu()
+    fake = m.fake_B.detach().cpu()
+    finite_params = all(bool(torch.isfinite(p).all()) for net in (m.netG, m.netD) for p in net.parameters())
+    peak = torch.cuda.max_memory_allocated() / 2 ** 30
+    del m
+    torch.cuda.empty_cache()
+    assert skipped == (False, False), skipped
+    assert torch.isfinite(gG).all() and torch.isfinite(gD).all() and finite_params
+    st = O.OracleStep(gp, dp, _vp(), pool_size=0)
+    L = st.step_chunked(A, B, 2)
+    rG = torch.cat([v.grad.flatten() for v in st.gp.values()])
+    rD = torch.cat([v.grad.flatten() for v in st.dp.values()])
+    msg = {k: (v, L[k]) for k, v in got.items()}
+    s = _img_ssim(fake, st.fake_B)
+    cg, cd = _cos(gG, rG), _cos(gD, rD)   # (the flat grads hold the loss-scaled gradient: cosine is scale-free)
+    print("C5 fp16: peak HBM %.1f GiB, ssim(fake) %.6f  cos(gG) %.5f  cos(gD) %.5f  losses %s" % (peak, s, cg, cd, msg))
+    for k, v in got.items():
+        assert abs(v - L[k]) <= 2e-2 * abs(L[k]) + 1e-4, msg
+    assert s >= 0.999, s
+    assert cg >= 0.999 and cd >= 0.999, (cg, cd)

@@ -39,16 +39,26 @@ def _param(t):
     return p
 
 
-TOL = {"fp32": 2e-5, "bf16": 1.5e-2}
+TOL = {"fp32": 2e-5, "bf16": 1.5e-2, "fp16": 3e-3}   # fp16: 3 more mantissa bits than bf16
+HALVES = ["bf16", "fp16"]
+
+
+def _hdt(half):
+    return torch.float16 if half == "fp16" else torch.bfloat16
+
+
+def _ulp(half):
+    """relative rounding bound of one RNE conversion to the 16-bit type"""
+    return 2.0 ** -11 if half == "fp16" else 2.0 ** -8
 
 
 def _q(t, prec):
-    """bf16 mode rounds MFMA operands to bf16: the reference sees the same rounded operands, so
-    activation masks agree and the bar measures accumulation/rounding only."""
-    return t.bfloat16().float() if prec == "bf16" else t
+    """16-bit modes round MFMA operands to bf16 / fp16: the reference sees the same rounded
+    operands, so activation masks agree and the bar measures accumulation/rounding only."""
+    return t.to(_hdt(prec)).float() if prec in HALVES else t
 
 
-@pytest.mark.parametrize("prec", ["fp32", "bf16"])
+@pytest.mark.parametrize("prec", ["fp32", "bf16", "fp16"])
 @pytest.mark.parametrize("N,Cin,H,W,Cout,K,s,p", [
     (2, 3, 16, 16, 12, 1, 1, 0),       # c1.pwconv1 shape class (K tiny)
     (2, 64, 16, 16, 256, 1, 1, 0),
@@ -99,7 +109,7 @@ def test_conv2d(prec, N, Cin, H, W, Cout, K, s, p):
         assert rel(bd.grad, br.grad) < max(1e-5, tol), ("bgrad", act)
 
 
-@pytest.mark.parametrize("prec", ["fp32", "bf16"])
+@pytest.mark.parametrize("prec", ["fp32", "bf16", "fp16"])
 @pytest.mark.parametrize("N,Ci,Co,H", [(2, 64, 32, 8), (2, 128, 64, 5), (1, 256, 128, 16),
                                        (2, 1024, 512, 16)])   # u1 shape: split-K tconv data-grad
 def test_conv_transpose(prec, N, Ci, Co, H):
@@ -124,7 +134,7 @@ def test_conv_transpose(prec, N, Ci, Co, H):
     assert rel(bd.grad, br.grad) < 1e-5
 
 
-@pytest.mark.parametrize("prec", ["fp32", "bf16"])
+@pytest.mark.parametrize("prec", ["fp32", "bf16", "fp16"])
 @pytest.mark.parametrize("N,C,H,P", [(2, 3, 16, 64), (2, 64, 8, 128), (2, 128, 12, 64),
                                      (2, 256, 16, 512),    # unfused large block: bf16 g = gelu(z) path
                                      (2, 256, 96, 1024)])  # 4C = 1024 = K of the data-grad: 256-row M tiles
@@ -158,7 +168,7 @@ def test_pw_mlp(prec, N, C, H, P):
         assert rel(pd.grad, pr.grad) < 2 * tol
 
 
-@pytest.mark.parametrize("prec", ["fp32", "bf16"])
+@pytest.mark.parametrize("prec", ["fp32", "bf16", "fp16"])
 @pytest.mark.parametrize("N,C,H,P", [(2, 64, 16, 128),     # fused MLP kernels (mlp.hip)
                                      (2, 256, 16, 512),    # unfused bf16 g / gp / dz path
                                      (2, 3, 16, 64)])      # fp32-z path (tiny block)
@@ -203,65 +213,74 @@ def test_block_tail_norm(prec, N, C, H, P):
 
 
 @pytest.mark.parametrize("N,C,HW", [(2, 64, 256), (3, 128, 4096), (2, 256, 1024), (1, 32, 65536 + 1024)])
-def test_instnorm_bf16_output(N, C, HW):
+@pytest.mark.parametrize("half", HALVES)
+def test_instnorm_bf16_output(half, N, C, HW):
     """dsgan_instnorm_fwd_bf16 writes exactly the RNE bf16 rounding of the fp32 InstanceNorm output
     (same statistics, every plane-size kernel variant)."""
+    from dsgan_hip import functional as HF_
+    HF_.set_precision(half)
     from dsgan_hip import functional as HF
     from dsgan_hip._lib import call, ptr, stream
     g = torch.Generator().manual_seed(C + HW)
     d = (torch.randn(N, C, 1, HW, generator=g) * 3 - 1).to(DEV)
     y32, m32, r32 = HF.instnorm_raw(d)
-    yb = torch.empty((N, C, 1, HW), device=DEV, dtype=torch.bfloat16)
+    yb = torch.empty((N, C, 1, HW), device=DEV, dtype=_hdt(half))
     m, r = torch.empty(N * C, device=DEV), torch.empty(N * C, device=DEV)
     call("dsgan_instnorm_fwd_bf16", ptr(d), C * HW, ptr(yb), C * HW, ptr(m), ptr(r), N, C, HW, 1e-5, stream())
     torch.cuda.synchronize()
-    assert torch.equal(yb, y32.to(torch.bfloat16))
+    assert torch.equal(yb, y32.to(_hdt(half)))
     assert torch.equal(m, m32) and torch.equal(r, r32)
 
 
 @pytest.mark.parametrize("w_bf16", [0, 1])
 @pytest.mark.parametrize("dy_bf16,dx_bf16,gp", [(0, 1, True), (1, 0, False), (1, 1, True), (0, 0, False)])
 @pytest.mark.parametrize("N,M,K,P", [(2, 512, 128, 256), (1, 2048, 256, 128), (2, 96, 64, 384), (1, 1024, 1024, 256)])
-def test_pw_dgrad_io(w_bf16, dy_bf16, dx_bf16, gp, N, M, K, P):
+@pytest.mark.parametrize("half", HALVES)
+def test_pw_dgrad_io(half, w_bf16, dy_bf16, dx_bf16, gp, N, M, K, P):
     """dsgan_pw_dgrad_io: DX = (W^T DY) (* GP) with bf16 DY/DX options vs float64 torch on the
     bf16-rounded operands (the last shape takes the 256-row M tiles)."""
+    from dsgan_hip import functional as HF_
+    HF_.set_precision(half)
     from dsgan_hip._lib import call, ptr, stream
     g = torch.Generator().manual_seed(M + K + P)
     w = torch.randn(K, M, generator=g) / math.sqrt(K)
     dy = torch.randn(N, K, P, generator=g)
-    gpv = torch.rand(N, M, P, generator=g).to(torch.bfloat16)
-    ref = torch.einsum("km,nkp->nmp", _q(w, "bf16").double(), _q(dy, "bf16").double())
+    gpv = torch.rand(N, M, P, generator=g).to(_hdt(half))
+    ref = torch.einsum("km,nkp->nmp", _q(w, half).double(), _q(dy, half).double())
     if gp:
         ref = ref * gpv.double()
-    dyd = dy.to(DEV).to(torch.bfloat16) if dy_bf16 else dy.to(DEV)
-    dx = torch.empty((N, M, P), device=DEV, dtype=torch.bfloat16 if dx_bf16 else torch.float32)
-    wd = w.to(DEV).to(torch.bfloat16) if w_bf16 else w.to(DEV)
+    dyd = dy.to(DEV).to(_hdt(half)) if dy_bf16 else dy.to(DEV)
+    dx = torch.empty((N, M, P), device=DEV, dtype=_hdt(half) if dx_bf16 else torch.float32)
+    wd = w.to(DEV).to(_hdt(half)) if w_bf16 else w.to(DEV)
     call("dsgan_pw_dgrad_io", ptr(wd), w_bf16, ptr(dyd), K * P, dy_bf16, ptr(dx), M * P, dx_bf16,
          ptr(gpv.to(DEV)) if gp else None, M * P, M, K, P, N, 0, stream())
     torch.cuda.synchronize()
     got = dx.double().cpu()
     if dx_bf16:
-        assert ((got - ref).abs() <= ref.abs() * 2 ** -8 + 1e-6).all()
+        assert ((got - ref).abs() <= ref.abs() * _ulp(half) + 1e-6).all()
     else:
         assert rel(got, ref) < 1e-5
 
 
 @pytest.mark.parametrize("dy_bf16,gp", [(0, True), (1, False)])
-def test_pw_dgrad_io_wide_tiles(dy_bf16, gp):
+@pytest.mark.parametrize("half", HALVES)
+def test_pw_dgrad_io_wide_tiles(half, dy_bf16, gp):
     """The 256 x 256 x 64 (8-wave) tiles of the bf16 data-grad: a grid of 256 tiles over one image
     (M = 512 rows, 32768 pixels), vs float64 torch on the bf16 operands."""
+    from dsgan_hip import functional as HF_
+    HF_.set_precision(half)
     from dsgan_hip._lib import call, ptr, stream
     N, M, K, P = 1, 512, 256, 32768
     g = torch.Generator().manual_seed(5)
     w = torch.randn(K, M, generator=g) / math.sqrt(K)
     dy = torch.randn(N, K, P, generator=g)
-    gpv = torch.rand(N, M, P, generator=g).to(torch.bfloat16)
-    ref = torch.einsum("km,nkp->nmp", _q(w, "bf16").double(), _q(dy, "bf16").double())
+    gpv = torch.rand(N, M, P, generator=g).to(_hdt(half))
+    ref = torch.einsum("km,nkp->nmp", _q(w, half).double(), _q(dy, half).double())
     if gp:
         ref = ref * gpv.double()
-    dyd = dy.to(DEV).to(torch.bfloat16) if dy_bf16 else dy.to(DEV)
+    dyd = dy.to(DEV).to(_hdt(half)) if dy_bf16 else dy.to(DEV)
     dx = torch.empty((N, M, P), device=DEV)
-    call("dsgan_pw_dgrad_io", ptr(w.to(DEV).to(torch.bfloat16)), 1, ptr(dyd), K * P, dy_bf16, ptr(dx), M * P, 0,
+    call("dsgan_pw_dgrad_io", ptr(w.to(DEV).to(_hdt(half))), 1, ptr(dyd), K * P, dy_bf16, ptr(dx), M * P, 0,
          ptr(gpv.to(DEV)) if gp else None, M * P, M, K, P, N, 0, stream())
     torch.cuda.synchronize()
     assert rel(dx.double().cpu(), ref) < 1e-5
@@ -269,22 +288,25 @@ def test_pw_dgrad_io_wide_tiles(dy_bf16, gp):
 
 @pytest.mark.parametrize("a_bf16,b_bf16", [(0, 0), (1, 1), (1, 0), (0, 1)])
 @pytest.mark.parametrize("N,M,C,P", [(2, 512, 128, 4096), (16, 64, 512, 1024), (1, 96, 40, 256), (2, 2048, 512, 256)])
-def test_pw_wgrad_bias_sums(a_bf16, b_bf16, N, M, C, P):
+@pytest.mark.parametrize("half", HALVES)
+def test_pw_wgrad_bias_sums(half, a_bf16, b_bf16, N, M, C, P):
     """dsgan_pw_wgrad_mixed with db: dW += A B^T and db += row sums of A from the staged tiles, split or
     unsplit, fp32 or bf16 A; deterministic (two runs bitwise equal)."""
+    from dsgan_hip import functional as HF_
+    HF_.set_precision(half)
     from dsgan_hip import functional as HF
     from dsgan_hip._lib import call, ptr, stream
     g = torch.Generator().manual_seed(M + C + P)
     a = torch.randn(N, M, P, generator=g)
     b = torch.randn(N, C, P, generator=g)
-    aq, bq = (_q(a, "bf16") if a_bf16 else a), (_q(b, "bf16") if b_bf16 else b)
-    ref_w = torch.einsum("nmp,ncp->mc", _q(a, "bf16").double(), _q(b, "bf16").double())
+    aq, bq = (_q(a, half) if a_bf16 else a), (_q(b, half) if b_bf16 else b)
+    ref_w = torch.einsum("nmp,ncp->mc", _q(a, half).double(), _q(b, half).double())
     ref_b = aq.double().sum(dim=(0, 2))
     outs = []
     for _ in range(2):
         w0, b0 = torch.ones(M, C, device=DEV), torch.full((M,), 2.0, device=DEV)
-        ad = a.to(DEV).to(torch.bfloat16) if a_bf16 else a.to(DEV)
-        bd = b.to(DEV).to(torch.bfloat16) if b_bf16 else b.to(DEV)
+        ad = a.to(DEV).to(_hdt(half)) if a_bf16 else a.to(DEV)
+        bd = b.to(DEV).to(_hdt(half)) if b_bf16 else b.to(DEV)
         call("dsgan_pw_wgrad_mixed", ptr(ad), M * P, a_bf16, ptr(bd), C * P, b_bf16, ptr(w0), ptr(b0), M, C, P, N,
              ptr(HF._pw_ws(M, C, P, N, ad)), stream())
         torch.cuda.synchronize()
@@ -301,13 +323,14 @@ def test_pw_wgrad_bias_sums(a_bf16, b_bf16, N, M, C, P):
     (2, 128, 9, 11, 256, 4, 1, 1, None),         # PatchGAN s1 (output 8x10)
     (1, 256, 16, 16, 3 * 32, 3, 1, 1, "relu"),   # M not a multiple of the 128 tile
 ])
-def test_pconv_bf16(N, Cin, H, W, Cout, K, s, p, act):
+@pytest.mark.parametrize("half", HALVES)
+def test_pconv_bf16(half, N, Cin, H, W, Cout, K, s, p, act):
     """Patch-staged conv (pconv.hip): forward and stride-1 data-grad vs the bf16-rounded fp32 conv."""
     from dsgan_hip import functional as HF
-    HF.set_precision("bf16")
+    HF.set_precision(half)
     g = torch.Generator().manual_seed(Cin + Cout + K)
-    x = _q(torch.randn(N, Cin, H, W, generator=g), "bf16")
-    w = _q(torch.randn(Cout, Cin, K, K, generator=g) / math.sqrt(Cin * K * K), "bf16")
+    x = _q(torch.randn(N, Cin, H, W, generator=g), half)
+    w = _q(torch.randn(Cout, Cin, K, K, generator=g) / math.sqrt(Cin * K * K), half)
     b = torch.randn(Cout, generator=g) * 0.1
     y_ref = F.conv2d(x, w, b, stride=s, padding=p)
     if act == "relu":
@@ -316,15 +339,15 @@ def test_pconv_bf16(N, Cin, H, W, Cout, K, s, p, act):
         y_ref = F.leaky_relu(y_ref, 0.2)
     y = HF.conv_fwd_raw(x.to(DEV), w.to(DEV), b.to(DEV), s, p, act=act)
     assert y.shape == y_ref.shape
-    assert rel(y, y_ref) < TOL["bf16"]
+    assert rel(y, y_ref) < TOL[half]
     if s == 1:
-        gy = _q(torch.randn(y_ref.shape, generator=g), "bf16")
+        gy = _q(torch.randn(y_ref.shape, generator=g), half)
         dx_ref = torch.nn.grad.conv2d_input(x.shape, w, gy, stride=1, padding=p)
         dx = HF.conv_dgrad_raw(gy.to(DEV), w.to(DEV), tuple(x.shape), 1, p)
-        assert rel(dx, dx_ref) < TOL["bf16"]
+        assert rel(dx, dx_ref) < TOL[half]
         # fused act' epilogue: dx * relu'(x)
         dxg = HF.conv_dgrad_raw(gy.to(DEV), w.to(DEV), tuple(x.shape), 1, p, gpre=x.to(DEV), gact="relu")
-        assert rel(dxg, dx_ref * (x > 0)) < TOL["bf16"]
+        assert rel(dxg, dx_ref * (x > 0)) < TOL[half]
 
 
 @pytest.mark.parametrize("N,C,H,W,M,K,s,p", [
@@ -335,15 +358,16 @@ def test_pconv_bf16(N, Cin, H, W, Cout, K, s, p, act):
     (2, 128, 9, 12, 256, 4, 1, 1),      # PatchGAN 4x4 s1 (output 8x11)
     (2, 64, 12, 16, 64, 3, 1, 1),       # 3x3 s1
 ])
-def test_wconv_bf16(N, C, H, W, M, K, s, p):
+@pytest.mark.parametrize("half", HALVES)
+def test_wconv_bf16(half, N, C, H, W, M, K, s, p):
     """Patch-staged weight-grad (wconv.hip) vs torch's conv2d_weight on the bf16-rounded operands;
     accumulates into the existing gradient; deterministic (fixed-order split reduction)."""
     from dsgan_hip import functional as HF
-    HF.set_precision("bf16")
+    HF.set_precision(half)
     g = torch.Generator().manual_seed(C + M + K + H)
-    x = _q(torch.randn(N, C, H, W, generator=g), "bf16")
+    x = _q(torch.randn(N, C, H, W, generator=g), half)
     Ho, Wo = (H + 2 * p - K) // s + 1, (W + 2 * p - K) // s + 1
-    dy = _q(torch.randn(N, M, Ho, Wo, generator=g), "bf16")
+    dy = _q(torch.randn(N, M, Ho, Wo, generator=g), half)
     dw_ref = torch.nn.grad.conv2d_weight(x.double(), (M, C, K, K), dy.double(), stride=s, padding=p)
     w0 = torch.randn(M, C, K, K, generator=g)
     dw = w0.to(DEV)
@@ -363,20 +387,21 @@ def test_wconv_bf16(N, C, H, W, M, K, s, p):
 
 @pytest.mark.parametrize("N,C,H,P", [(2, 64, 16, 128), (2, 128, 16, 64), (3, 128, 16, 256), (2, 256, 16, 128),
                                      (1, 128, 32, 64)])
-def test_pw_mlp_fused(N, C, H, P):
+@pytest.mark.parametrize("half", HALVES)
+def test_pw_mlp_fused(half, N, C, H, P):
     """bf16 fused MLP kernels (mlp.hip) at every (C, P) they take: forward without the hidden z,
     backward recomputing z and feeding bf16 gelu(z)/dz to the weight-grads."""
     from dsgan_hip import functional as HF, _lib
-    HF.set_precision("bf16")
+    HF.set_precision(half)
     assert _lib.load().dsgan_mlp_supported(C, P, H * H) > 0
     g = torch.Generator().manual_seed(7 * C + P)
-    h = _q(torch.randn(N, C, H, H, generator=g), "bf16")
-    x = _q(torch.randn(N, C, H, H, generator=g), "bf16")
-    w1 = _q(torch.randn(4 * C, C, generator=g) / math.sqrt(C), "bf16")
+    h = _q(torch.randn(N, C, H, H, generator=g), half)
+    x = _q(torch.randn(N, C, H, H, generator=g), half)
+    w1 = _q(torch.randn(4 * C, C, generator=g) / math.sqrt(C), half)
     b1 = torch.randn(4 * C, generator=g) * 0.1
-    w2 = _q(torch.randn(P, 4 * C, generator=g) / math.sqrt(4 * C), "bf16")
+    w2 = _q(torch.randn(P, 4 * C, generator=g) / math.sqrt(4 * C), half)
     b2 = torch.randn(P, generator=g) * 0.1
-    ws = _q(torch.randn(P, C, 1, 1, generator=g) / math.sqrt(C), "bf16")
+    ws = _q(torch.randn(P, C, 1, 1, generator=g) / math.sqrt(C), half)
     R = [t.clone().requires_grad_() for t in (h, x, w1, b1, w2, b2, ws)]
     t = F.linear(R[0].permute(0, 2, 3, 1), R[2], R[3])
     t = F.linear(F.gelu(t), R[4], R[5]).permute(0, 3, 1, 2)
@@ -387,7 +412,7 @@ def test_pw_mlp_fused(N, C, H, P):
     P_ = [_param(t) for t in (w1, b1, w2, b2, ws)]
     y = HF.pw_mlp(hd, xd, *P_)
     y.backward(gy.to(DEV))
-    tol = TOL["bf16"]
+    tol = TOL[half]
     assert rel(y, y_ref) < tol
     assert rel(hd.grad, R[0].grad) < 2 * tol
     assert rel(xd.grad, R[1].grad) < 2 * tol
@@ -633,19 +658,20 @@ def test_adam_matches_torch():
 
 @pytest.mark.parametrize("N,Cin,H,Cout", [(2, 64, 16, 256), (2, 36, 16, 200), (3, 132, 32, 68),
                                           (2, 512, 8 * 4, 64), (1, 16, 128, 16)])
-def test_pw_gemm_fast_path(N, Cin, H, Cout):
+@pytest.mark.parametrize("half", HALVES)
+def test_pw_gemm_fast_path(half, N, Cin, H, Cout):
     """bf16 1x1 GEMM fast path (pwgemm.hip): fwd(+bias, xact=gelu, accumulate), dgrad(+gelu'
     epilogue), wgrad(+xact) incl. partial M tiles and K % 32 != 0, vs fp32 torch on bf16-rounded
     operands."""
     from dsgan_hip import functional as HF
     from dsgan_hip import _lib
-    HF.set_precision("bf16")
+    HF.set_precision(half)
     g = torch.Generator().manual_seed(Cin * 7 + Cout)
     x = torch.randn(N, Cin, H, H, generator=g)
     w = torch.randn(Cout, Cin, 1, 1, generator=g) / math.sqrt(Cin)
     b = torch.randn(Cout, generator=g) * 0.1
     y0 = torch.randn(N, Cout, H, H, generator=g)
-    xq, wq = _q(F.gelu(x), "bf16"), _q(w, "bf16")
+    xq, wq = _q(F.gelu(x), half), _q(w, half)
     xd, wd, bd = x.to(DEV), w.to(DEV), b.to(DEV)
     assert _lib.load().dsgan_pw_supported(0, Cout, Cin, H * H, 0, Cin * H * H, wd.data_ptr(), xd.data_ptr())
     # fwd with activation-on-load and accumulate
@@ -659,12 +685,12 @@ def test_pw_gemm_fast_path(N, Cin, H, Cout):
     dx = HF.conv_dgrad_raw(dy.to(DEV), wd, tuple(x.shape), 1, 0, gpre=z.to(DEV), gact="gelu")
     zr = z.clone().requires_grad_()
     gz = torch.autograd.grad(F.gelu(zr), zr, torch.ones_like(z))[0]
-    ref = F.conv_transpose2d(_q(dy, "bf16"), wq) * gz
+    ref = F.conv_transpose2d(_q(dy, half), wq) * gz
     assert rel(dx, ref) < 1e-2
     # wgrad with activation-on-load
     dw = torch.zeros_like(wd)
     HF.conv_wgrad_raw(dy.to(DEV), xd, dw, 1, 0, xact="gelu")
-    ref = torch.einsum("bmhw,bkhw->mk", _q(dy, "bf16"), xq).view_as(w)
+    ref = torch.einsum("bmhw,bkhw->mk", _q(dy, half), xq).view_as(w)
     assert rel(dw, ref) < 1e-2
     HF.set_precision("fp32")
 
@@ -676,19 +702,20 @@ def test_pw_gemm_fast_path(N, Cin, H, Cout):
     (2, 128, 9, 9, 256, 4, 1, 1),      # PatchGAN s1 (31x31-like odd outputs)
     (2, 64, 16, 16, 3, 3, 1, 1),       # G head (M = 3)
 ])
-def test_tap_conv_bf16(N, Cin, H, W, Cout, K, s, p):
+@pytest.mark.parametrize("half", HALVES)
+def test_tap_conv_bf16(half, N, Cin, H, W, Cout, K, s, p):
     """Tap-major bf16 conv (tconv.hip): fwd, stride-1 dgrad (flipped kernel) and stride-2 dgrad
     (parity classes) vs fp32 torch on bf16-rounded operands."""
     from dsgan_hip import functional as HF
-    HF.set_precision("bf16")
+    HF.set_precision(half)
     g = torch.Generator().manual_seed(Cin + Cout + K + H)
-    x = _q(torch.randn(N, Cin, H, W, generator=g), "bf16")
-    w = _q(torch.randn(Cout, Cin, K, K, generator=g) / math.sqrt(Cin * K * K), "bf16")
+    x = _q(torch.randn(N, Cin, H, W, generator=g), half)
+    w = _q(torch.randn(Cout, Cin, K, K, generator=g) / math.sqrt(Cin * K * K), half)
     b = torch.randn(Cout, generator=g) * 0.1
     y = HF.conv_fwd_raw(x.to(DEV), w.to(DEV), b.to(DEV), s, p, act="relu")
     assert rel(y, F.relu(F.conv2d(x, w, b, stride=s, padding=p))) < 1e-2
     Ho, Wo = y.shape[2], y.shape[3]
-    dy = _q(torch.randn(N, Cout, Ho, Wo, generator=g), "bf16")
+    dy = _q(torch.randn(N, Cout, Ho, Wo, generator=g), half)
     gp = torch.randn(N, Cin, H, W, generator=g)
     if Cout % 32 == 0:
         dx = HF.conv_dgrad_raw(dy.to(DEV), w.to(DEV), (N, Cin, H, W), s, p, gpre=gp.to(DEV), gact="lrelu")
@@ -699,7 +726,7 @@ def test_tap_conv_bf16(N, Cin, H, W, Cout, K, s, p):
     HF.set_precision("fp32")
 
 
-@pytest.mark.parametrize("prec", ["fp32", "bf16"])
+@pytest.mark.parametrize("prec", ["fp32", "bf16", "fp16"])
 def test_perceptual_l1_fused(prec):
     """VGG16 perceptual term as one node (PerceptualL1Fn): loss and d(loss)/d(fake) vs torch's
     conv2d/relu/max_pool2d/l1_loss chain (DSGAN/models/vgg.py:30-42, pix2pix_model.py:182-186)."""
@@ -755,14 +782,15 @@ def test_perceptual_l1_fused(prec):
     (2, 64, 32, 17, 18, 4, 34, 36),      # data-grad of the PatchGAN 4x4/s2 conv
     (2, 128, 64, 16, 16, 4, 32, 32),
 ])
-def test_pconvt_bf16(N, Cout, Cin, Hi, Wi, K, H, W):
+@pytest.mark.parametrize("half", HALVES)
+def test_pconvt_bf16(half, N, Cout, Cin, Hi, Wi, K, H, W):
     """pconvt.hip: the stride-2 data-grad / ConvTranspose with all four output parities in one
     launch, vs torch's conv2d_input on bf16-rounded operands; bias, act'(gpre) and accumulate."""
     from dsgan_hip import functional as HF
-    HF.set_precision("bf16")
+    HF.set_precision(half)
     g = torch.Generator().manual_seed(Cout + Cin + K + Hi)
-    dy = _q(torch.randn(N, Cout, Hi, Wi, generator=g), "bf16")
-    w = _q(torch.randn(Cout, Cin, K, K, generator=g) / math.sqrt(Cout * K * K / 4), "bf16")
+    dy = _q(torch.randn(N, Cout, Hi, Wi, generator=g), half)
+    w = _q(torch.randn(Cout, Cin, K, K, generator=g) / math.sqrt(Cout * K * K / 4), half)
     b = torch.randn(Cin, generator=g) * 0.1
     dx_ref = torch.nn.grad.conv2d_input((N, Cin, H, W), w.double(), dy.double(), stride=2, padding=1)
     HF.IGEMM_TIMER.rec, HF.IGEMM_TIMER.on = [], True
@@ -820,10 +848,13 @@ def test_instance_norm_cat(shape):
 @pytest.mark.parametrize("w_bf16,x_bf16", [(0, 0), (1, 1), (1, 0)])
 @pytest.mark.parametrize("M,K,P,nb", [(2048, 512, 4096, 2), (1024, 256, 1024, 3), (256, 64, 256, 2), (4096, 1024, 1024, 1),
                                       (96, 40, 256, 2)])
-def test_pw_fwd_io_bf16_outputs(w_bf16, x_bf16, M, K, P, nb):
+@pytest.mark.parametrize("half", HALVES)
+def test_pw_fwd_io_bf16_outputs(half, w_bf16, x_bf16, M, K, P, nb):
     """pwconv1 of the unfused MLP blocks (MixConvNeXtML.py:221-223): g = gelu(W x + b) and
     gp = gelu'(W x + b) written bf16 through the LDS-staged epilogue, vs torch on the same bf16
     operands (one bf16 ulp)."""
+    from dsgan_hip import functional as HF_
+    HF_.set_precision(half)
     import dsgan_hip
     from dsgan_hip._lib import call, ptr, stream
     from dsgan_hip import functional as HF
@@ -832,12 +863,12 @@ def test_pw_fwd_io_bf16_outputs(w_bf16, x_bf16, M, K, P, nb):
     x = torch.randn(nb, K, P, generator=g).cuda()
     w = (torch.randn(M, K, generator=g) / K ** 0.5).cuda()
     b = torch.randn(M, generator=g).cuda()
-    y = torch.empty(nb, M, P, device="cuda", dtype=torch.bfloat16)
+    y = torch.empty(nb, M, P, device="cuda", dtype=_hdt(half))
     gp = torch.empty_like(y)
-    wd, xd = (w.bfloat16() if w_bf16 else w), (x.bfloat16() if x_bf16 else x)
+    wd, xd = (w.to(_hdt(half)) if w_bf16 else w), (x.to(_hdt(half)) if x_bf16 else x)
     call("dsgan_pw_fwd_io", ptr(wd), w_bf16, ptr(xd), K * P, x_bf16, ptr(y), M * P, 1, ptr(gp), M * P, 1, ptr(b), M, K,
          P, nb, HF.ACT["gelu"], 0, 0.2, stream())
-    z = torch.einsum("mk,bkp->bmp", w.bfloat16().double(), x.bfloat16().double()) + b.double().view(1, M, 1)
+    z = torch.einsum("mk,bkp->bmp", w.to(_hdt(half)).double(), x.to(_hdt(half)).double()) + b.double().view(1, M, 1)
     zz = z.clone().requires_grad_(True)
     torch.nn.functional.gelu(zz).sum().backward()
     ref_g, ref_gp = torch.nn.functional.gelu(z), zz.grad

@@ -156,3 +156,29 @@ def test_oracle_msssim_grad_vs_reference():
     assert abs(gr.norm().item() - float(gv["MS_grad256_norm"])) < 1e-9 * float(gv["MS_grad256_norm"])
     for j in range(3):
         assert abs(float(gr @ probe(gr.numel(), 61000 + j)) - gv["MS_grad256_dot"][j]) < 1e-8 * float(gv["MS_grad256_norm"]) * 600
+
+
+def test_chunked_oracle_step_equals_full_step():
+    """OracleStep.step_chunked (used for the C5 512x512 parity test, whose full CPU graph is too
+    big) gives the full step's losses, gradients and post-Adam parameters (reassociation only;
+    the BCE terms go through fp32 constants, hence fp32-level bars)."""
+    import torch
+    from oracle import dsgan_cpu as O
+    from oracle.recipe import make_params, synth_pair
+    gp = {k: v.double() for k, v in make_params(O.g_param_spec(), "fanin", 1000).items()}
+    dp = {k: v.double() for k, v in make_params(O.d_param_spec(), "fanin", 5000).items()}
+    vp = {k: v.double() for k, v in make_params(O.vgg_param_spec(False), "vgg", 7000).items()}
+    A, B = synth_pair(4, 64, seed=3)
+    A, B = A.double(), B.double()
+    full = O.OracleStep(gp, dp, vp, pool_size=0)
+    Lf = full.step(A, B)
+    ch = O.OracleStep(gp, dp, vp, pool_size=0)
+    Lc = ch.step_chunked(A, B, 2)
+    for k in Lf:
+        assert abs(Lf[k] - Lc[k]) <= 1e-6 * max(1.0, abs(Lf[k])), (k, Lf[k], Lc[k])
+    assert torch.allclose(full.fake_B, ch.fake_B, rtol=0, atol=1e-12)
+    for a, b in ((full.gp, ch.gp), (full.dp, ch.dp)):
+        for k in a:
+            ga, gb = a[k].grad, b[k].grad
+            assert (ga - gb).norm() <= 1e-5 * max(ga.norm(), 1e-30) + 1e-12, k
+            assert torch.allclose(a[k], b[k], rtol=0, atol=1e-9), k

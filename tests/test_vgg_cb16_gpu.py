@@ -33,6 +33,17 @@ def bf(t):
     return t.to(torch.bfloat16).float()
 
 
+HALVES = ["bf16", "fp16"]
+
+
+def _hdt(half):
+    return torch.float16 if half == "fp16" else torch.bfloat16
+
+
+def _ulp(half):
+    return 2.0 ** -11 if half == "fp16" else 2.0 ** -8
+
+
 def rel(a, b):
     a, b = a.double(), b.double()
     return ((a - b).norm() / max(b.norm().item(), 1e-30)).item()
@@ -45,7 +56,12 @@ SHAPES = [(2, 64, 64, 64, 64), (2, 64, 128, 32, 64), (2, 128, 128, 32, 32), (2, 
 
 @pytest.mark.parametrize("shape", SHAPES)
 @pytest.mark.parametrize("out_f32", [True, False])
-def test_vconv_forward(shape, out_f32):
+@pytest.mark.parametrize("half", HALVES)
+def test_vconv_forward(half, shape, out_f32):
+    HT = _hdt(half)
+    bf = lambda v: v.to(HT).float()  # noqa: E731 -- this half type
+    from dsgan_hip import functional as HF_
+    HF_.set_precision(half)
     HF = _hf()
     from dsgan_hip._lib import call, ptr, stream
     N, Ci, Co, H, W = shape
@@ -54,22 +70,27 @@ def test_vconv_forward(shape, out_f32):
     w = torch.randn(Co, Ci, 3, 3, generator=g) * (2.0 / (9 * Ci)) ** 0.5
     b = torch.randn(Co, generator=g) * 0.1
     ref = torch.relu(F.conv2d(x.double(), bf(w).double(), b.double(), padding=1))
-    xd, wd, bd = to_cb16(x).cuda().to(torch.bfloat16), w.cuda(), b.cuda()
-    y = torch.empty((N, Co // 16, H, W, 16), device="cuda", dtype=torch.float32 if out_f32 else torch.bfloat16)
+    xd, wd, bd = to_cb16(x).cuda().to(HT), w.cuda(), b.cuda()
+    y = torch.empty((N, Co // 16, H, W, 16), device="cuda", dtype=torch.float32 if out_f32 else HT)
     HF._vconv(xd, HF._vgg_wt(wd, 0), bd, None, y, N, Ci, Co, H, W, True, "fwd")
     torch.cuda.synchronize()
     got = from_cb16(y.float().cpu())
     if out_f32:
         assert rel(got, ref) < 1e-5, rel(got, ref)
     else:
-        assert ((got.double() - ref).abs() <= ref.abs() * 2 ** -8 + 1e-6).all()
+        assert ((got.double() - ref).abs() <= ref.abs() * _ulp(half) + 1e-6).all()
 
 
 @pytest.mark.parametrize("shape", SHAPES[:6])
 @pytest.mark.parametrize("masked", [True, False])
-def test_vconv_dgrad(shape, masked):
+@pytest.mark.parametrize("half", HALVES)
+def test_vconv_dgrad(half, shape, masked):
     """The data-grad form: dx = conv_transpose(dy, W) [* (a_below > 0)] with the flipped /
     transposed weights of dsgan_vconv_wtrans(dgrad=1)."""
+    HT = _hdt(half)
+    bf = lambda v: v.to(HT).float()  # noqa: E731 -- this half type
+    from dsgan_hip import functional as HF_
+    HF_.set_precision(half)
     HF = _hf()
     N, Ci, Co, H, W = shape
     g = torch.Generator().manual_seed(7 + sum(shape))
@@ -79,15 +100,20 @@ def test_vconv_dgrad(shape, masked):
     ref = F.conv_transpose2d(dy.double(), bf(w).double(), padding=1)
     if masked:
         ref = ref * (below > 0)
-    out = torch.empty((N, Ci // 16, H, W, 16), device="cuda", dtype=torch.bfloat16)
-    HF._vconv(to_cb16(dy).cuda().to(torch.bfloat16), HF._vgg_wt(w.cuda(), 1), None,
-              to_cb16(below).cuda().to(torch.bfloat16) if masked else None, out, N, Co, Ci, H, W, False, "dgrad")
+    out = torch.empty((N, Ci // 16, H, W, 16), device="cuda", dtype=HT)
+    HF._vconv(to_cb16(dy).cuda().to(HT), HF._vgg_wt(w.cuda(), 1), None,
+              to_cb16(below).cuda().to(HT) if masked else None, out, N, Co, Ci, H, W, False, "dgrad")
     torch.cuda.synchronize()
     got = from_cb16(out.float().cpu())
-    assert ((got.double() - ref).abs() <= ref.abs() * 2 ** -8 + 1e-9).all()
+    assert ((got.double() - ref).abs() <= ref.abs() * _ulp(half) + 1e-9).all()
 
 
-def test_conv1_forward_and_dgrad():
+@pytest.mark.parametrize("half", HALVES)
+def test_conv1_forward_and_dgrad(half):
+    HT = _hdt(half)
+    bf = lambda v: v.to(HT).float()  # noqa: E731 -- this half type
+    from dsgan_hip import functional as HF_
+    HF_.set_precision(half)
     HF = _hf()
     from dsgan_hip._lib import call, ptr, stream
     g = torch.Generator().manual_seed(3)
@@ -96,22 +122,27 @@ def test_conv1_forward_and_dgrad():
     w = torch.randn(64, 3, 3, 3, generator=g) * 0.3
     b = torch.randn(64, generator=g) * 0.1
     ref = torch.relu(F.conv2d(x.double(), w.double(), b.double(), padding=1))
-    y = torch.empty((N, 4, H, W, 16), device="cuda", dtype=torch.bfloat16)
+    y = torch.empty((N, 4, H, W, 16), device="cuda", dtype=HT)
     call("dsgan_vgg_conv1_fwd", ptr(x.cuda()), 3 * H * W, ptr(w.cuda()), ptr(b.cuda()), ptr(y), N, H, W, stream())
     d = bf(torch.randn(N, 64, H, W, generator=g) * 1e-3)
     dx = torch.empty((N, 3, H, W), device="cuda")
-    call("dsgan_vgg_conv1_dgrad", ptr(to_cb16(d).cuda().to(torch.bfloat16)), ptr(w.cuda()), ptr(dx), 3 * H * W, N, H,
+    call("dsgan_vgg_conv1_dgrad", ptr(to_cb16(d).cuda().to(HT)), ptr(w.cuda()), ptr(dx), 3 * H * W, N, H,
          W, stream())
     torch.cuda.synchronize()
     got = from_cb16(y.float().cpu())
-    assert ((got.double() - ref).abs() <= ref.abs() * 2 ** -8 + 1e-6).all()
+    assert ((got.double() - ref).abs() <= ref.abs() * _ulp(half) + 1e-6).all()
     dref = F.conv_transpose2d(d.double(), w.double(), padding=1)
     assert rel(dx.cpu(), dref) < 1e-6
 
 
-def test_maxpool_and_tap_bwd():
+@pytest.mark.parametrize("half", HALVES)
+def test_maxpool_and_tap_bwd(half):
     """MaxPool2d(2) value + window argmax (first max wins, as torch) and the tapped-layer
     backward (maxpool backward + L1 backward) * ReLU' against torch autograd."""
+    HT = _hdt(half)
+    bf = lambda v: v.to(HT).float()  # noqa: E731 -- this half type
+    from dsgan_hip import functional as HF_
+    HF_.set_precision(half)
     _hf()
     from dsgan_hip._lib import call, ptr, stream
     g = torch.Generator().manual_seed(5)
@@ -120,7 +151,7 @@ def test_maxpool_and_tap_bwd():
     f[:, :, ::3, ::2] = 0.0                      # ties among zeros, as post-ReLU features have
     r = torch.relu(torch.randn(N, C, H, W, generator=g))
     fd, rd = to_cb16(f).cuda(), to_cb16(r).cuda()
-    y = torch.empty((N, C // 16, H // 2, W // 2, 16), device="cuda", dtype=torch.bfloat16)
+    y = torch.empty((N, C // 16, H // 2, W // 2, 16), device="cuda", dtype=HT)
     idx = torch.empty(y.shape, device="cuda", dtype=torch.uint8)
     call("dsgan_cb16_maxpool", ptr(fd), ptr(y), ptr(idx), N, C, H, W, stream())
     ref, ridx = F.max_pool2d(f, 2, return_indices=True)
@@ -131,18 +162,20 @@ def test_maxpool_and_tap_bwd():
     assert torch.equal(from_cb16(idx.cpu()), win)
     # backward: loss = gsc * L1(f, r) + <dpool, maxpool(f)>, grad at the pre-ReLU input
     dpool = bf(torch.randn(N, C, H // 2, W // 2, generator=g) * 1e-3)
-    gsc = torch.tensor([0.75])
+    # fp16: the loss-scaled magnitude the fp16 mode feeds this kernel (dsgan_hip.amp: x 2^16), so
+    # the gradients stay in the normal fp16 range
+    gsc = torch.tensor([0.75 * (2.0 ** 16 if half == "fp16" else 1.0)])
     pre = f.clone().requires_grad_(True)
     out = torch.relu(pre)
     loss = gsc * torch.mean(torch.abs(out - r)) + (F.max_pool2d(out, 2) * dpool).sum()
     loss.backward()
-    d = torch.empty(fd.shape, device="cuda", dtype=torch.bfloat16)
-    call("dsgan_cb16_tap_bwd", ptr(to_cb16(dpool).cuda().to(torch.bfloat16)), ptr(idx), ptr(fd), ptr(rd), ptr(d), N, C,
+    d = torch.empty(fd.shape, device="cuda", dtype=HT)
+    call("dsgan_cb16_tap_bwd", ptr(to_cb16(dpool).cuda().to(HT)), ptr(idx), ptr(fd), ptr(rd), ptr(d), N, C,
          H, W, ptr(gsc.cuda()), stream())
     torch.cuda.synchronize()
     got = from_cb16(d.float().cpu())
     refg = pre.grad * (f > 0)
-    assert ((got.double() - refg.double()).abs() <= refg.abs().double() * 2 ** -8 + 1e-12).all()
+    assert ((got.double() - refg.double()).abs() <= refg.abs().double() * _ulp(half) + 1e-12).all()
 
 
 def test_perceptual_cb16_matches_nchw_path():

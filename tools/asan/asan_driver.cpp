@@ -38,6 +38,8 @@ int dsgan_pw_small(const float* X, long x_bs, const float* W, int wm, int wk, co
                    int accumulate, float slope, hipStream_t st);
 }
 void dsgan_set_error(const char* fmt, ...);
+extern "C" int dsgan_set_half_type(int t);
+extern "C" int dsgan_get_half_type(void);
 
 static int fails = 0;
 #define CHECK(c)                                                        \
@@ -48,7 +50,12 @@ static int fails = 0;
 static bool err_has(const char* s) { return strstr(dsgan_last_error_string(), s) != nullptr; }
 
 int main() {
-  CHECK(dsgan_abi_version() == 1);
+  CHECK(dsgan_abi_version() == 2);
+  // the process-wide 16-bit operand type: 0 bf16 / 1 fp16, anything else refused with a message
+  CHECK(dsgan_get_half_type() == 0);
+  CHECK(dsgan_set_half_type(1) == 0 && dsgan_get_half_type() == 1);
+  CHECK(dsgan_set_half_type(7) == -1 && err_has("dsgan_set_half_type") && dsgan_get_half_type() == 1);
+  CHECK(dsgan_set_half_type(0) == 0 && dsgan_get_half_type() == 0);
   // error string: formatting and truncation at the buffer size
   char big[2048];
   memset(big, 'x', sizeof(big) - 1);
