@@ -819,6 +819,24 @@ __global__ __launch_bounds__(256) void copy4_kernel(const float* src, long src_b
   for (long e = blockIdx.x * 256L + threadIdx.x; e < E4; e += (long)gridDim.x * 256) d[e] = s[e];
 }
 
+// Up to COPY_MULTI (src, dst) pairs of E floats in one launch (blockIdx.y = pair): the ImagePool's
+// per-query gather / scatter (util/image_pool.py) instead of one copy launch per image.
+constexpr int COPY_MULTI = 32;
+struct CopyPairs {
+  const float* src[COPY_MULTI];
+  float* dst[COPY_MULTI];
+};
+__global__ __launch_bounds__(256) void copy_multi4_kernel(CopyPairs pr, long E4) {
+  const float4* s = reinterpret_cast<const float4*>(pr.src[blockIdx.y]);
+  float4* d = reinterpret_cast<float4*>(pr.dst[blockIdx.y]);
+  for (long e = blockIdx.x * 256L + threadIdx.x; e < E4; e += (long)gridDim.x * 256) d[e] = s[e];
+}
+__global__ __launch_bounds__(256) void copy_multi_kernel(CopyPairs pr, long E) {
+  const float* s = pr.src[blockIdx.y];
+  float* d = pr.dst[blockIdx.y];
+  for (long e = blockIdx.x * 256L + threadIdx.x; e < E; e += (long)gridDim.x * 256) d[e] = s[e];
+}
+
 static inline bool v4_ok(const void* p, long bs) { return (bs & 3) == 0 && (((uintptr_t)p) & 15) == 0; }
 static inline dim3 grid4(int N, long E4) {
   long gx = (E4 + 255) / 256;
@@ -1122,6 +1140,27 @@ int dsgan_copy_strided(const float* src, long src_bs, float* dst, long dst_bs, i
   }
   hipLaunchKernelGGL(copy_strided_kernel, dim3(grid_for((long)N * E)), dim3(256), 0, st, src, src_bs, dst, dst_bs, N, E);
   DSG_CHECK_LAUNCH();
+  return 0;
+}
+
+// dst[i][0..E) <- src[i][0..E) for i < count (host arrays of device pointers); pairs must not
+// overlap each other (the ImagePool orders its gather and scatter as two calls)
+int dsgan_copy_multi(const float* const* src, float* const* dst, int count, long E, hipStream_t st) {
+  DSG_REQUIRE(src && dst && count >= 0 && E >= 0, "dsgan_copy_multi: bad args");
+  for (int b = 0; b < count; b += COPY_MULTI) {
+    const int n = count - b < COPY_MULTI ? count - b : COPY_MULTI;
+    CopyPairs pr{};
+    bool v4 = (E & 3) == 0;
+    for (int i = 0; i < n; ++i) {
+      DSG_REQUIRE(src[b + i] && dst[b + i], "dsgan_copy_multi: null pointer in pair %d", b + i);
+      pr.src[i] = src[b + i];
+      pr.dst[i] = dst[b + i];
+      v4 = v4 && v4_ok(src[b + i], 0) && v4_ok(dst[b + i], 0);
+    }
+    if (v4) hipLaunchKernelGGL(copy_multi4_kernel, grid4(n, E / 4), dim3(256), 0, st, pr, E / 4);
+    else hipLaunchKernelGGL(copy_multi_kernel, grid4(n, E), dim3(256), 0, st, pr, E);
+    DSG_CHECK_LAUNCH();
+  }
   return 0;
 }
 

@@ -103,6 +103,7 @@ SIGNATURES = {
     "dsgan_ca_bwd": [P, P, P, P, P, P, P, P, P, P, P, P, P, I, I, I, P, S],
     "dsgan_add_n": [P, P, I, P, L, I, L, S],
     "dsgan_copy_strided": [P, L, P, L, I, L, S],
+    "dsgan_copy_multi": [P, P, I, L, S],
     "dsgan_fill": [P, F, L, S],
     "dsgan_scale": [P, F, L, S],
     "dsgan_act_bwd": [P, P, P, L, I, F, I, S],

@@ -519,6 +519,22 @@ def zeros(shape, like):
     return fill_(torch.empty(shape, device=like.device, dtype=torch.float32), 0.0)
 
 
+def copy_multi(pairs):
+    """dst <- src for a list of (dst, src) dense fp32 tensors of equal size, one launch per 32 pairs."""
+    import ctypes
+    if not pairs:
+        return
+    n = pairs[0][0].numel()
+    for d, s in pairs:
+        if d.numel() != n or s.numel() != n or not d.is_contiguous() or not s.is_contiguous() \
+                or d.dtype != torch.float32 or s.dtype != torch.float32:
+            raise ValueError("copy_multi: dense fp32 tensors of one size required")
+    srcs = (ctypes.c_void_p * len(pairs))(*[ptr(s) for _, s in pairs])
+    dsts = (ctypes.c_void_p * len(pairs))(*[ptr(d) for d, _ in pairs])
+    call("dsgan_copy_multi", ctypes.cast(srcs, ctypes.c_void_p), ctypes.cast(dsts, ctypes.c_void_p), len(pairs), n,
+         stream())
+
+
 def copy_into(dst, src):
     """dst[n] <- src[n] for per-sample dense blocks (used for channel concatenation)."""
     src, sbs = nchw(src)

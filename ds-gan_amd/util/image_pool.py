@@ -2,7 +2,11 @@
 
 Same decision rule and the same python-``random`` draws (``uniform(0,1) > 0.5`` then
 ``randint(0, size-1)``) per image, so a seeded run consumes the RNG exactly like the
-reference.  Images stay on the device; copies go through the HIP strided-copy kernel.
+reference.  The pool is ONE resident device tensor [pool_size, C, H, W]; a query resolves the
+reference's per-image loop on the host (which slot each output image comes from, which slots
+take which input image -- the same image may be swapped in and out of one slot twice within a
+batch), then runs two batched copies: the output gather (from the input or the pool's
+previous contents) and, after it, the scatter of the new images into their slots.
 """
 import random
 
@@ -17,36 +21,41 @@ class ImagePool:
         self.rng = rng if rng is not None else random
         if self.pool_size > 0:
             self.num_imgs = 0
-            self.images = []
+            self.store = None          # [pool_size, C, H, W], allocated at the first query
 
-    @staticmethod
-    def _clone(img):
-        out = torch.empty_like(img)
-        HF.copy_into(out, img)
-        return out
+    @property
+    def images(self):
+        """The stored images, reference order (views of the resident pool)."""
+        return [self.store[i:i + 1] for i in range(self.num_imgs)] if self.pool_size > 0 and self.store is not None else []
 
     def query(self, images):
         if self.pool_size == 0:
             return images
-        images = images.detach()
-        picks = []
+        images = images.detach().contiguous()
+        if self.store is None or self.store.shape[1:] != images.shape[1:]:
+            self.store = torch.empty((self.pool_size,) + tuple(images.shape[1:]), device=images.device,
+                                     dtype=images.dtype)
+        # slot -> where its CURRENT contents live: ("pool", slot) = unchanged this query, ("in", j)
+        cur = {}
+        src_of_out = []
         for i in range(images.shape[0]):
-            image = images[i:i + 1]
             if self.num_imgs < self.pool_size:
+                cur[self.num_imgs] = ("in", i)
                 self.num_imgs += 1
-                stored = self._clone(image)
-                self.images.append(stored)
-                picks.append(stored)
+                src_of_out.append(("in", i))
             else:
                 p = self.rng.uniform(0, 1)
                 if p > 0.5:
                     random_id = self.rng.randint(0, self.pool_size - 1)
-                    tmp = self.images[random_id]
-                    self.images[random_id] = self._clone(image)
-                    picks.append(tmp)
+                    src_of_out.append(cur.get(random_id, ("pool", random_id)))
+                    cur[random_id] = ("in", i)
                 else:
-                    picks.append(image)
+                    src_of_out.append(("in", i))
         out = torch.empty_like(images)
-        for i, t in enumerate(picks):
-            HF.copy_into(out[i:i + 1], t)
+
+        def t(src):
+            return images[src[1]] if src[0] == "in" else self.store[src[1]]
+        # gather first (it may read slots the scatter below overwrites), then scatter
+        HF.copy_multi([(out[i], t(s)) for i, s in enumerate(src_of_out)])
+        HF.copy_multi([(self.store[slot], images[j]) for slot, (_, j) in sorted(cur.items())])
         return out

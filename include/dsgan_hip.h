@@ -346,6 +346,10 @@ int dsgan_add_n(const float* const* ins, const long* in_bs, int nin, float* out,
                 int N, long E, hipStream_t stream);
 int dsgan_copy_strided(const float* src, long src_bs, float* dst, long dst_bs, int N, long E,
                        hipStream_t stream);
+/* dst[i][0..E) <- src[i][0..E), i < count; src / dst are HOST arrays of device pointers (packed into
+ * the launch, 32 pairs per launch): the ImagePool's per-query gather and scatter
+ * (DSGAN/util/image_pool.py:12-32) in one launch each instead of one copy per image */
+int dsgan_copy_multi(const float* const* src, float* const* dst, int count, long E, hipStream_t stream);
 int dsgan_fill(float* p, float v, long n, hipStream_t stream);
 int dsgan_scale(float* p, float a, long n, hipStream_t stream);
 int dsgan_act_bwd(const float* dy, const float* pre, float* dx, long n, int act, float slope,
