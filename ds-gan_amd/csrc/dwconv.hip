@@ -160,10 +160,23 @@ __global__ __launch_bounds__(256) void dwconv_wgrad_kernel(const float* __restri
 // of the tile, so each input row of a thread's window is three ds_read_b128 and serves
 // up to R*4*K FMAs.  The per-plane weights are wave-uniform (scalar loads).
 // ------------------------------------------------------------------------------------------
+// LDS row pitch (floats) of a tile whose loaded rows are lw floats: the window reads are
+// ds_read_b128 whose 16-lane groups span two thread rows (TWT = 16: rows ty, ty+1) or four (TWT = 8),
+// R tile rows apart; a pitch with R*LP = 0 (TWT 16) / 32 (TWT 8) mod 64 dwords puts them in disjoint
+// bank ranges (tools/lds_banks.py: 2-3-way -> conflict-free; the staging writes become 1.3-1.6-way)
+constexpr int dw_pitch(int twt, int r, int lw) {
+  if (twt != 16 && twt != 8) return lw;
+  const int tgt = twt == 16 ? 0 : 32;
+  int lp = lw;
+  while ((r * lp) % 64 != tgt) lp += 4;
+  return lp;
+}
+
 template <int K, int TWT, int THT, int R>
 struct DwTile {
   static constexpr int TW = 4 * TWT, TH = R * THT, P = K / 2;
   static constexpr int LW = TW + 8, LH = TH + K - 1, F4 = LW / 4;
+  static constexpr int LP = dw_pitch(TWT, R, LW);   // LDS pitch (LW loaded, LP apart)
   static constexpr int OFF = 4 - P;      // LDS column of input (out col - P) for i = kw = 0
   static_assert(TWT * THT == 256, "256 threads");
 };
@@ -189,7 +202,7 @@ __device__ __forceinline__ void dw_stage(float* tile, const float* __restrict__ 
     for (int j = 0; j < ITEMS; ++j) {
       const int i = threadIdx.x + j * 256;
       const int r = i / T::F4, q = i - r * T::F4;
-      if (i < T::LH * T::F4) *reinterpret_cast<float4*>(tile + r * T::LW + 4 * q) = v[j];
+      if (i < T::LH * T::F4) *reinterpret_cast<float4*>(tile + r * T::LP + 4 * q) = v[j];
     }
     return;
   }
@@ -199,7 +212,7 @@ __device__ __forceinline__ void dw_stage(float* tile, const float* __restrict__ 
     float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
     if ((unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W)
       v = *reinterpret_cast<const float4*>(xp + (long)ih * W + iw);
-    *reinterpret_cast<float4*>(tile + r * T::LW + 4 * q) = v;
+    *reinterpret_cast<float4*>(tile + r * T::LP + 4 * q) = v;
   }
 }
 
@@ -218,7 +231,7 @@ __device__ __forceinline__ void dw_row(float (&v)[12], const float* row) {
   for (int i = 0; i < 4; ++i) { v[i] = a[i]; v[4 + i] = b[i]; v[8 + i] = c[i]; }
 }
 
-// One workgroup's output tile (bx) of plane `plane`; `tile` = LDS of DwTile<K,...>::LH * LW floats.
+// One workgroup's output tile (bx) of plane `plane`; `tile` = LDS of DwTile<K,...>::LH * LP floats.
 template <int K, int TWT, int THT, int R>
 __device__ __forceinline__ void dw_fwd_body(const float* __restrict__ x, long x_bs, const float* __restrict__ w,
                                             const float* __restrict__ bias, float* __restrict__ y, long y_bs, int C,
@@ -242,10 +255,10 @@ __device__ __forceinline__ void dw_fwd_body(const float* __restrict__ x, long x_
   // one input row in flight ahead of the FMAs; the scheduling barrier keeps the compiler from
   // hoisting every row load of the unrolled loop (which costs occupancy or spills)
   float cur[12], nxt[12];
-  dw_row<K>(cur, tile + (R * ty) * T::LW + 4 * tx);
+  dw_row<K>(cur, tile + (R * ty) * T::LP + 4 * tx);
 #pragma unroll
   for (int r = 0; r < R + K - 1; ++r) {
-    if (r + 1 < R + K - 1) dw_row<K>(nxt, tile + (R * ty + r + 1) * T::LW + 4 * tx);
+    if (r + 1 < R + K - 1) dw_row<K>(nxt, tile + (R * ty + r + 1) * T::LP + 4 * tx);
 #pragma unroll
     for (int s = 0; s < R; ++s) {
       const int kh = r - s;
@@ -281,7 +294,7 @@ __global__ __launch_bounds__(256, 4) void dwconv_fwd_v2(const float* __restrict_
                                                      float* __restrict__ y, long y_bs, int C, int H,
                                                      int W, int flip, int accumulate, int tiles_w) {
   using T = DwTile<K, TWT, THT, R>;
-  __shared__ __attribute__((aligned(16))) float tile[T::LH * T::LW];
+  __shared__ __attribute__((aligned(16))) float tile[T::LH * T::LP];
   dw_fwd_body<K, TWT, THT, R>(x, x_bs, w, bias, y, y_bs, C, H, W, flip, accumulate, tiles_w, blockIdx.x, blockIdx.y,
                               tile);
 }
@@ -296,7 +309,7 @@ __global__ __launch_bounds__(256, 3) void dwconv_multi_fwd(const float* __restri
                                                            float* __restrict__ y, long y_bs, int q, int H, int W,
                                                            int flip, int accumulate, int tiles_w) {
   using T = DwTile<9, TWT, THT, R>;
-  __shared__ __attribute__((aligned(16))) float tile[T::LH * T::LW];
+  __shared__ __attribute__((aligned(16))) float tile[T::LH * T::LP];
   const int qi = blockIdx.z;
   const float* xq = x + (long)qi * q * H * W;
   float* yq = y + (long)qi * q * H * W;
@@ -312,7 +325,7 @@ __global__ __launch_bounds__(256, 3) void dwconv_multi_fwd(const float* __restri
 // db[c] += sum dy.  The dy block of a thread stays in registers; partial sums are reduced over
 // the workgroup once, after all of its images.
 // Weight-grad partials of channel c, tile bx, image split `split` (slot split * ntiles + bx).
-// `tile` = LH * LW floats of LDS, `red` = 4 * (K*K + 1) floats.
+// `tile` = LH * LP floats of LDS, `red` = 4 * (K*K + 1) floats.
 template <int K, int TWT, int THT, int R>
 __device__ __forceinline__ void dw_wgrad_body(const float* __restrict__ dy, long dy_bs, const float* __restrict__ x,
                                               long x_bs, float* __restrict__ ws, int N, int C, int H, int W,
@@ -342,10 +355,10 @@ __device__ __forceinline__ void dw_wgrad_body(const float* __restrict__ dy, long
     }
     __syncthreads();
     float cur[12], nxt[12];
-    dw_row<K>(cur, tile + (R * ty) * T::LW + 4 * tx);
+    dw_row<K>(cur, tile + (R * ty) * T::LP + 4 * tx);
 #pragma unroll
     for (int r = 0; r < R + K - 1; ++r) {
-      if (r + 1 < R + K - 1) dw_row<K>(nxt, tile + (R * ty + r + 1) * T::LW + 4 * tx);
+      if (r + 1 < R + K - 1) dw_row<K>(nxt, tile + (R * ty + r + 1) * T::LP + 4 * tx);
 #pragma unroll
       for (int s = 0; s < R; ++s) {
         const int kh = r - s;
@@ -385,7 +398,7 @@ __global__ __launch_bounds__(256, 4) void dwconv_wgrad_v2(const float* __restric
                                                        float* __restrict__ ws,
                                                        int N, int C, int H, int W, int tiles_w, int nper) {
   using T = DwTile<K, TWT, THT, R>;
-  __shared__ __attribute__((aligned(16))) float tile[T::LH * T::LW];
+  __shared__ __attribute__((aligned(16))) float tile[T::LH * T::LP];
   __shared__ float red[4 * (K * K + 1)];
   dw_wgrad_body<K, TWT, THT, R>(dy, dy_bs, x, x_bs, ws, N, C, H, W, tiles_w, nper, blockIdx.x, blockIdx.y, blockIdx.z,
                                 gridDim.x, tile, red);
@@ -398,7 +411,7 @@ __global__ __launch_bounds__(256, 4) void dwconv_multi_wgrad(const float* __rest
                                                              int N, int q, int H, int W, int tiles_w, int nper,
                                                              int nsplit) {
   using T = DwTile<9, TWT, THT, R>;
-  __shared__ __attribute__((aligned(16))) float tile[T::LH * T::LW];
+  __shared__ __attribute__((aligned(16))) float tile[T::LH * T::LP];
   __shared__ float red[4 * 82];
   const int qi = blockIdx.z / nsplit, split = blockIdx.z - qi * nsplit;
   const long co = (long)qi * q * H * W;

@@ -200,6 +200,29 @@ template <int S>
 __device__ __forceinline__ int slot_swz(int r) {
   return S >= 16 ? (((r & 3) << 2) | ((r >> 2) & 3)) : ((((r >> 1) & 1) << 2) | ((r >> 2) & 3));
 }
+// element offset of (row r, column c) in an unpadded [rows][S*8] tile with slot_swz'd 16-byte slots
+template <int S>
+__device__ __forceinline__ int swz_off(int r, int c) {
+  return r * (S * 8) + ((((c >> 3) ^ slot_swz<S>(r))) << 3) + (c & 7);
+}
+// wch_store into unpadded, swizzled chunk images: W1s [HC][C] (slots slot_swz<C/8>), W2s [P][HC]
+// (slot_swz<HC/8>): conflict-free for the row reads (ds_read_b128) AND the transposed reads
+// (ds_read_b64_tr_b16) both backward kernels make of them (tools/lds_banks.py; the padded images
+// were 2-4-way on the transposed reads)
+template <int C, int P, int HC, int NT, int N1, int N2, typename T16>
+__device__ __forceinline__ void wch_store_swz(const mu32x4 (&r1)[N1], const mu32x4 (&r2)[N2], T16* W1s, T16* W2s,
+                                              int tid) {
+#pragma unroll
+  for (int i = 0; i < N1; ++i) {
+    const int it = tid + i * NT, row = it / (C / 8), c8 = it % (C / 8);
+    *reinterpret_cast<mu32x4*>(W1s + row * C + ((c8 ^ slot_swz<C / 8>(row)) << 3)) = r1[i];
+  }
+#pragma unroll
+  for (int i = 0; i < N2; ++i) {
+    const int it = tid + i * NT, row = it / (HC / 8), c8 = it % (HC / 8);
+    *reinterpret_cast<mu32x4*>(W2s + row * HC + ((c8 ^ slot_swz<HC / 8>(row)) << 3)) = r2[i];
+  }
+}
 
 // One 16-byte-per-lane LDS-DMA (global_load_lds_dwordx4): lane l's 16 bytes land at LDS byte
 // address lds + 16 l.  Issued from asm so that hipcc neither counts it nor drains it with a
@@ -677,7 +700,8 @@ __global__ __launch_bounds__(NW * 64, MINB) void mlp_bwd_kernel(MlpArgs g) {
   typedef hx4<T16> mbf16x4;
   constexpr int NT = NW * 64;
   constexpr int C4 = 4 * C, NCH = C4 / HC;
-  constexpr int HSTR = BN + 32, NSTR = HC + 8, W1STR = C + 8, W2STR = HC + 8;
+  // Hs / Ds padded (transposed reads only); Zn / Gn and the weight chunks unpadded + slot-swizzled
+  constexpr int HSTR = BN + 32, NSTR = HC, W1STR = C, W2STR = HC;
   constexpr int H_SZ = C * HSTR, D_SZ = P * HSTR, N_SZ = BN * NSTR, W1_SZ = HC * W1STR, W2_SZ = P * W2STR;
   __shared__ __attribute__((aligned(16))) T16 smem[H_SZ + D_SZ + (GD ? 2 : 1) * N_SZ + W1_SZ + W2_SZ];
   T16* Hs = smem;
@@ -709,7 +733,7 @@ __global__ __launch_bounds__(NW * 64, MINB) void mlp_bwd_kernel(MlpArgs g) {
   wch_load<C, P, HC, NT>(wr1, wr2, g.w1, g.w2, 0, tid);
   stage_h<C, BN, HSTR, NT>(Hs, g, img, p0, tid);
   stage_rows<P, BN, HSTR, NT>(Ds, g.dy + (long)img * g.dy_bs + p0, g.HW, tid);
-  wch_store<C, P, HC, NT, W1STR, W2STR>(wr1, wr2, W1s, W2s, tid);
+  wch_store_swz<C, P, HC, NT>(wr1, wr2, W1s, W2s, tid);
 
   mf32x16 hacc[HG::TM][HG::TN];
 #pragma unroll
@@ -742,7 +766,7 @@ __global__ __launch_bounds__(NW * 64, MINB) void mlp_bwd_kernel(MlpArgs g) {
       mbf16x8 af[ZG::TM], bf[ZG::TN];
 #pragma unroll
       for (int i = 0; i < ZG::TM; ++i)
-        af[i] = *reinterpret_cast<const mbf16x8*>(W1s + (wm * (HC / 2) + i * 32 + lr) * W1STR + ks * 16 + lh * 8);
+        af[i] = *reinterpret_cast<const mbf16x8*>(W1s + swz_off<C / 8>(wm * (HC / 2) + i * 32 + lr, ks * 16 + lh * 8));
 #pragma unroll
       for (int t = 0; t < ZG::TN; ++t)
         bf[t] = mtr_frag(Hs + (ks * 16 + 8 * lh + tq) * HSTR + wn * (BN / ZG::WN) + t * 32 + 16 * tG + 4 * tp, HSTR);
@@ -757,7 +781,7 @@ __global__ __launch_bounds__(NW * 64, MINB) void mlp_bwd_kernel(MlpArgs g) {
       mbf16x8 af[ZG::TM], bf[ZG::TN];
 #pragma unroll
       for (int i = 0; i < ZG::TM; ++i)   // A[m][p] = W2[p][m]: W2s [P][W2STR] is k-major for this product
-        af[i] = mtr_frag(W2s + (ks * 16 + 8 * lh + tq) * W2STR + wm * (HC / 2) + i * 32 + 16 * tG + 4 * tp, W2STR);
+        af[i] = mtr_frag_s<HC / 8>(W2s, ks * 16, wm * (HC / 2) + i * 32, lane);
 #pragma unroll
       for (int t = 0; t < ZG::TN; ++t)
         bf[t] = mtr_frag(Ds + (ks * 16 + 8 * lh + tq) * HSTR + wn * (BN / ZG::WN) + t * 32 + 16 * tG + 4 * tp, HSTR);
@@ -785,8 +809,8 @@ __global__ __launch_bounds__(NW * 64, MINB) void mlp_bwd_kernel(MlpArgs g) {
             dv4[e] = (T16)dz.x; dv4[e + 1] = (T16)dz.y;
           }
           const int m = wm * (HC / 2) + i * 32 + 8 * q + 4 * lh;
-          if constexpr (GD) *reinterpret_cast<mbf16x4*>(Gn + n * NSTR + m) = gv4;
-          *reinterpret_cast<mbf16x4*>(Zn + n * NSTR + m) = dv4;
+          if constexpr (GD) *reinterpret_cast<mbf16x4*>(Gn + swz_off<HC / 8>(n, m)) = gv4;
+          *reinterpret_cast<mbf16x4*>(Zn + swz_off<HC / 8>(n, m)) = dv4;
         }
       }
     __syncthreads();
@@ -798,9 +822,8 @@ __global__ __launch_bounds__(NW * 64, MINB) void mlp_bwd_kernel(MlpArgs g) {
 #pragma unroll
       for (int c = 0; c < CPW; ++c) {
         const int pb = ((wave >> 1) * CPW + c) * 16;
-        const int off = (pb + 8 * lh + tq) * NSTR + chh + 16 * tG + 4 * tp;
-        const mbf16x8 gv = mtr_frag(Gn + off, NSTR);
-        const mbf16x8 dv = mtr_frag(Zn + off, NSTR);
+        const mbf16x8 gv = mtr_frag_s<HC / 8>(Gn, pb, chh, lane);
+        const mbf16x8 dv = mtr_frag_s<HC / 8>(Zn, pb, chh, lane);
         const long o = gbase + (long)(j * HC + chh + lr) * g.HW + pb + 8 * lh;
         *reinterpret_cast<mbf16x8*>((T16*)g.g_out + o) = gv;
         *reinterpret_cast<mbf16x8*>((T16*)g.dz_out + o) = dv;
@@ -816,10 +839,10 @@ __global__ __launch_bounds__(NW * 64, MINB) void mlp_bwd_kernel(MlpArgs g) {
       mbf16x8 af[HG::TM], bf[HG::TN];
 #pragma unroll
       for (int i = 0; i < HG::TM; ++i)   // A[c][m] = W1[m][c]: W1s [HC][W1STR] is k-major here
-        af[i] = mtr_frag(W1s + (ks * 16 + 8 * lh + tq) * W1STR + wm * (C / 2) + i * 32 + 16 * tG + 4 * tp, W1STR);
+        af[i] = mtr_frag_s<C / 8>(W1s, ks * 16, wm * (C / 2) + i * 32, lane);
 #pragma unroll
       for (int t = 0; t < HG::TN; ++t)
-        bf[t] = *reinterpret_cast<const mbf16x8*>(Zn + (wn * (BN / HG::WN) + t * 32 + lr) * NSTR + ks * 16 + lh * 8);
+        bf[t] = *reinterpret_cast<const mbf16x8*>(Zn + swz_off<HC / 8>(wn * (BN / HG::WN) + t * 32 + lr, ks * 16 + lh * 8));
 #pragma unroll
       for (int i = 0; i < HG::TM; ++i)
 #pragma unroll
@@ -828,7 +851,7 @@ __global__ __launch_bounds__(NW * 64, MINB) void mlp_bwd_kernel(MlpArgs g) {
     }
     __syncthreads();
     if (j + 1 < NCH) {
-      wch_store<C, P, HC, NT, W1STR, W2STR>(wr1, wr2, W1s, W2s, tid);
+      wch_store_swz<C, P, HC, NT>(wr1, wr2, W1s, W2s, tid);
       __syncthreads();
     }
   }
@@ -881,6 +904,17 @@ struct TileLd {   // a [K][BN] activation tile (rows strided by HW), fp32 or bf1
       else *reinterpret_cast<hx4<T16>*>(dst + k * STR + c * E) = mcvt4<T16>(__builtin_bit_cast(float4, v[i]));
     }
   }
+  // into an unpadded [K][BN] image with slot_swz<BN/8>'d 16-byte slots (a 4-element fp32 item
+  // stays inside its slot)
+  template <typename T16>
+  __device__ __forceinline__ void store_swz(T16* dst, int tid) const {
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      const int it = tid + i * NT, k = it / (BN / E), c = it % (BN / E);
+      if constexpr (BF) *reinterpret_cast<mu32x4*>(dst + swz_off<BN / 8>(k, c * E)) = v[i];
+      else *reinterpret_cast<hx4<T16>*>(dst + swz_off<BN / 8>(k, c * E)) = mcvt4<T16>(__builtin_bit_cast(float4, v[i]));
+    }
+  }
 };
 
 // wave -> (tile, k-part) split of an [M x N] weight-grad product over NW waves: TPW tiles per wave,
@@ -899,10 +933,10 @@ __global__ __launch_bounds__(NW * 64, MINB) void mlp_wgrad_kernel(MlpArgs g) {
   constexpr int HC = 64;
   constexpr int NT = NW * 64;
   constexpr int C4 = 4 * C, NCH = C4 / HC;
-  // Hs / Ds are read transposed (z, t: k = channel) and row-wise (dW: k = pixel): a row stride of
-  // 4 (mod 16) 16-byte slots keeps the row-wise 16-byte reads conflict-free (the transposed reads
-  // are then 2-way at BN = 64, whose tight stride lets two workgroups share a CU)
-  constexpr int HSTR = BN + (BN == 64 ? 8 : 40), NSTR = HC + 8, W1STR = C + 8, W2STR = HC + 8;
+  // Hs / Ds are read transposed (z, t: k = channel) and row-wise (dW: k = pixel); every LDS image
+  // here is unpadded with slot_swz'd 16-byte slots, conflict-free for both kinds of read and for
+  // the staging / epilogue writes except the 8-byte dz / g writes (2-way; tools/lds_banks.py)
+  constexpr int HSTR = BN, NSTR = HC, W1STR = C, W2STR = HC;
   constexpr int H_SZ = C * HSTR, D_SZ = P * HSTR, N_SZ = BN * NSTR, W1_SZ = HC * W1STR, W2_SZ = P * W2STR;
   __shared__ __attribute__((aligned(16))) T16 smem[H_SZ + D_SZ + 2 * N_SZ + W1_SZ + W2_SZ];
   T16* Hs = smem;
@@ -930,7 +964,7 @@ __global__ __launch_bounds__(NW * 64, MINB) void mlp_wgrad_kernel(MlpArgs g) {
     using WC = WCh<C, P, HC, NT>;
     mu32x4 wr1[WC::N1], wr2[WC::N2];
     wch_load<C, P, HC, NT>(wr1, wr2, g.w1, g.w2, j, tid);
-    wch_store<C, P, HC, NT, W1STR, W2STR>(wr1, wr2, W1s, W2s, tid);
+    wch_store_swz<C, P, HC, NT>(wr1, wr2, W1s, W2s, tid);
   }
   float bias[ZG::TM][16];
 #pragma unroll
@@ -970,8 +1004,8 @@ __global__ __launch_bounds__(NW * 64, MINB) void mlp_wgrad_kernel(MlpArgs g) {
 
   for (int tt = s; tt < ntiles; tt += S) {
     __syncthreads();   // every wave is done with the previous tile's Hs / Ds / Zn / Gn
-    hreg.template store<HSTR>(Hs, tid);
-    dreg.template store<HSTR>(Ds, tid);
+    hreg.store_swz(Hs, tid);
+    dreg.store_swz(Ds, tid);
     __syncthreads();
     if (tt + S < ntiles) {   // prefetch the next tile while this one computes
       const void* hp; const float* dp;
@@ -992,10 +1026,10 @@ __global__ __launch_bounds__(NW * 64, MINB) void mlp_wgrad_kernel(MlpArgs g) {
       mbf16x8 af[ZG::TM], bf[ZG::TN];
 #pragma unroll
       for (int i = 0; i < ZG::TM; ++i)
-        af[i] = *reinterpret_cast<const mbf16x8*>(W1s + (wm * (HC / 2) + i * 32 + lr) * W1STR + ks * 16 + lh * 8);
+        af[i] = *reinterpret_cast<const mbf16x8*>(W1s + swz_off<C / 8>(wm * (HC / 2) + i * 32 + lr, ks * 16 + lh * 8));
 #pragma unroll
       for (int t = 0; t < ZG::TN; ++t)
-        bf[t] = mtr_frag(Hs + (ks * 16 + 8 * lh + tq) * HSTR + wn * (BN / ZG::WN) + t * 32 + 16 * tG + 4 * tp, HSTR);
+        bf[t] = mtr_frag_s<BN / 8>(Hs, ks * 16, wn * (BN / ZG::WN) + t * 32, lane);
 #pragma unroll
       for (int i = 0; i < ZG::TM; ++i)
 #pragma unroll
@@ -1007,10 +1041,10 @@ __global__ __launch_bounds__(NW * 64, MINB) void mlp_wgrad_kernel(MlpArgs g) {
       mbf16x8 af[ZG::TM], bf[ZG::TN];
 #pragma unroll
       for (int i = 0; i < ZG::TM; ++i)
-        af[i] = mtr_frag(W2s + (ks * 16 + 8 * lh + tq) * W2STR + wm * (HC / 2) + i * 32 + 16 * tG + 4 * tp, W2STR);
+        af[i] = mtr_frag_s<HC / 8>(W2s, ks * 16, wm * (HC / 2) + i * 32, lane);
 #pragma unroll
       for (int t = 0; t < ZG::TN; ++t)
-        bf[t] = mtr_frag(Ds + (ks * 16 + 8 * lh + tq) * HSTR + wn * (BN / ZG::WN) + t * 32 + 16 * tG + 4 * tp, HSTR);
+        bf[t] = mtr_frag_s<BN / 8>(Ds, ks * 16, wn * (BN / ZG::WN) + t * 32, lane);
 #pragma unroll
       for (int i = 0; i < ZG::TM; ++i)
 #pragma unroll
@@ -1037,8 +1071,8 @@ __global__ __launch_bounds__(NW * 64, MINB) void mlp_wgrad_kernel(MlpArgs g) {
             bacc[i][4 * q + e + 1] += (float)dv4[e + 1];
           }
           const int m = wm * (HC / 2) + i * 32 + 8 * q + 4 * lh;
-          *reinterpret_cast<mbf16x4*>(Gn + n * NSTR + m) = gv4;
-          *reinterpret_cast<mbf16x4*>(Zn + n * NSTR + m) = dv4;
+          *reinterpret_cast<mbf16x4*>(Gn + swz_off<HC / 8>(n, m)) = gv4;
+          *reinterpret_cast<mbf16x4*>(Zn + swz_off<HC / 8>(n, m)) = dv4;
         }
       }
     __syncthreads();
@@ -1050,8 +1084,8 @@ __global__ __launch_bounds__(NW * 64, MINB) void mlp_wgrad_kernel(MlpArgs g) {
       const int mt = ti % T1::MT, nt = ti / T1::MT;
 #pragma unroll
       for (int ks = kp * (BN / 16 / T1::KS); ks < (kp + 1) * (BN / 16 / T1::KS); ++ks) {
-        const mbf16x8 af = mtr_frag(Zn + (ks * 16 + 8 * lh + tq) * NSTR + mt * 32 + 16 * tG + 4 * tp, NSTR);
-        const mbf16x8 bf = *reinterpret_cast<const mbf16x8*>(Hs + (nt * 32 + lr) * HSTR + ks * 16 + lh * 8);
+        const mbf16x8 af = mtr_frag_s<HC / 8>(Zn, ks * 16, mt * 32, lane);
+        const mbf16x8 bf = *reinterpret_cast<const mbf16x8*>(Hs + swz_off<BN / 8>(nt * 32 + lr, ks * 16 + lh * 8));
         a1[q] = mfma16(af, bf, a1[q]);
       }
     }
@@ -1063,8 +1097,8 @@ __global__ __launch_bounds__(NW * 64, MINB) void mlp_wgrad_kernel(MlpArgs g) {
       const int mt = ti % T2::MT, nt = ti / T2::MT;
 #pragma unroll
       for (int ks = kp * (BN / 16 / T2::KS); ks < (kp + 1) * (BN / 16 / T2::KS); ++ks) {
-        const mbf16x8 af = *reinterpret_cast<const mbf16x8*>(Ds + (mt * 32 + lr) * HSTR + ks * 16 + lh * 8);
-        const mbf16x8 bf = mtr_frag(Gn + (ks * 16 + 8 * lh + tq) * NSTR + nt * 32 + 16 * tG + 4 * tp, NSTR);
+        const mbf16x8 af = *reinterpret_cast<const mbf16x8*>(Ds + swz_off<BN / 8>(mt * 32 + lr, ks * 16 + lh * 8));
+        const mbf16x8 bf = mtr_frag_s<HC / 8>(Gn, ks * 16, nt * 32, lane);
         a2[q] = mfma16(af, bf, a2[q]);
       }
     }

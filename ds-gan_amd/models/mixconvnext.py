@@ -229,5 +229,11 @@ class MixConvNeXtML(nn.Module):
         O2 = self.uc2(self.u2(HF.add_n(O1, s64[2], s128[1], s256[0]), R3))
         O3 = self.uc3(self.u3(HF.add_n(O2, s64[1], s128[0]), R2))
         O4 = self.uc4(self.u4(HF.add_n(O3, s64[0]), R1))
-        Loc = self.local(x)
+        # --precision fp16 (configs[4]): the MLKA branch keeps bf16 16-bit operands (fp32 exponent
+        # range).  Its InstanceNorms see input variances far below eps at the reference init, so
+        # their backward multiplies gradients by up to ~1/sqrt(eps) per norm: under the fp16 mode's
+        # loss scale (2^16) the branch's fp16 data-grads overflow while every other tensor stays
+        # finite (tools/fp16_scale_probe.py; SURVEY.md §7 asks to keep this branch out of fp16).
+        with HF.precision("bf16" if HF.get_precision() == "fp16" else None):
+            Loc = self.local(x)
         return HF.conv2d(HF.add_n(O4, Loc), self.res.weight, self.res.bias, stride=1, pad=1)
