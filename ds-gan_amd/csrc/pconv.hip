@@ -43,8 +43,13 @@ __global__ __launch_bounds__(256, 2) void pconv_kernel(PcArgs g) {
   static_assert(BN == 128, "128 output pixels per tile");
   constexpr int WM = 2, WN = 2, TM = BM / WM / 32, TN = BN / WN / 32;
   constexpr int PH = (TH - 1) * S + KH, PW = (TW - 1) * S + KW, PPIX = PH * PW;
+  // LDS pitch of a patch row, in pixels: 32 for stride 1 puts the two grid rows a B read spans
+  // 32 pixels (= 0 mod 16 slots of 80 B) apart -> conflict-free ds_read_b128 (it was 2-way with
+  // the patch rows packed at PW; tools/lds_banks.py).  Stride 2 keeps PW (2-way either way).
+  constexpr int PWP = S == 1 ? 32 : PW;
+  static_assert(PWP >= PW, "patch pitch");
   constexpr int TAPS = KH * KW;
-  constexpr int A_SZ = BM * PC_STR, P_SZ = PPIX * PC_STR;
+  constexpr int A_SZ = BM * PC_STR, P_SZ = PH * PWP * PC_STR;
   constexpr int A_ITEMS = BM * 4 / 256;           // 16-byte items of a [BM][32] bf16 slice
   constexpr int P_ITEMS = (PPIX * 4 + 255) / 256; // (pixel, 8-channel group) items of the patch per thread
   __shared__ __attribute__((aligned(16))) T16 smem[2 * A_SZ + P_SZ];
@@ -77,7 +82,7 @@ __global__ __launch_bounds__(256, 2) void pconv_kernel(PcArgs g) {
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
     const int n = wn * (BN / WN) + j * 32 + lr;
-    pbase[j] = ((n / TW) * S * PW + (n % TW) * S) * PC_STR + lh * 8;
+    pbase[j] = ((n / TW) * S * PWP + (n % TW) * S) * PC_STR + lh * 8;
   }
 
   cu32x4 ra[A_ITEMS];
@@ -121,10 +126,11 @@ __global__ __launch_bounds__(256, 2) void pconv_kernel(PcArgs g) {
       const int it = tid + i * 256;
       if (it < PPIX * 4) {
         const int cg = it / PPIX, pix = it - cg * PPIX;
+        const int pr = pix / PW, pc = pix - pr * PW;
         cbf16x8 v;
 #pragma unroll
         for (int e = 0; e < 8; ++e) v[e] = (T16)rp[i][e];
-        *reinterpret_cast<cbf16x8*>(Ps + pix * PC_STR + cg * 8) = v;
+        *reinterpret_cast<cbf16x8*>(Ps + (pr * PWP + pc) * PC_STR + cg * 8) = v;
       }
     }
   };
@@ -162,7 +168,7 @@ __global__ __launch_bounds__(256, 2) void pconv_kernel(PcArgs g) {
       else if (kb + 1 < nkb) aload(0, k0 + 32);
       const T16* As = smem + buf * A_SZ;
       const int kh = tap / KW, kw = tap - (tap / KW) * KW;
-      const int toff = (kh * PW + kw) * PC_STR;
+      const int toff = (kh * PWP + kw) * PC_STR;
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
         cbf16x8 af[TM], bfr[TN];
@@ -313,8 +319,10 @@ static void pc_launch(PcArgs& g, hipStream_t st) {
 
 template <typename T16, int BM>
 static int pc_dispatch(PcArgs& g, int KH, int S, hipStream_t st) {
-  if (KH == 3 && S == 1) { pc_launch<T16, BM, 8, 16, 1, 3, 3>(g, st); return 0; }
-  if (KH == 4 && S == 1) { pc_launch<T16, BM, 8, 16, 1, 4, 4>(g, st); return 0; }
+  if constexpr (BM <= 128) {   // BM = 256 only for stride 2 (its stride-1 forms spill registers)
+    if (KH == 3 && S == 1) { pc_launch<T16, BM, 8, 16, 1, 3, 3>(g, st); return 0; }
+    if (KH == 4 && S == 1) { pc_launch<T16, BM, 8, 16, 1, 4, 4>(g, st); return 0; }
+  }
   if (KH == 4 && S == 2) { pc_launch<T16, BM, 8, 16, 2, 4, 4>(g, st); return 0; }
   return -1;
 }
@@ -346,7 +354,8 @@ int dsgan_conv_wtrans_bf16(const float* W, void* Wb, int Co, int Ci, int KH, int
 
 // BM = 256 for the wide layers (VGG conv3/conv4, 256/512 output channels): per tap twice the
 // MFMAs between barriers and half the patch traffic per MAC, only while the launch still has >= 2
-// workgroups per CU (at 32x32 it would have one)
+// workgroups per CU (at 32x32 it would have one); stride-1 launches take 128 instead (same
+// tile count >= 512, so neither form is K-split and dsgan_pconv_workspace needs no stride)
 static int pc_bm(int nb, int M, int Ho, int Wo) {
   const long ptiles = (long)nb * ((Ho + 7) / 8) * ((Wo + 15) / 16);
   return M >= 256 && ptiles * ((M + 255) / 256) >= 512 ? 256 : M > 64 ? 128 : 64;
@@ -394,7 +403,7 @@ int dsgan_pconv_ws(const float* X, long x_bs, const void* Wb, const float* bias,
   const int bm = pc_bm(nb, M, Ho, Wo);
   const int rc = with_half([&](auto* t_) {
     using T16 = std::remove_pointer_t<decltype(t_)>;
-    return bm == 256 ? pc_dispatch<T16, 256>(g, KH, stride, st)
+    return bm == 256 && stride == 2 ? pc_dispatch<T16, 256>(g, KH, stride, st)
            : bm == 128 ? pc_dispatch<T16, 128>(g, KH, stride, st)
                        : pc_dispatch<T16, 64>(g, KH, stride, st);
   });

@@ -66,13 +66,17 @@ __global__ __launch_bounds__(256, BM == 32 ? 4 : 2) void pconvt_kernel(PtArgs g)
   using G = PtGeo<KS, PAD>;
   constexpr int DMIN = G::dmin, NSH = G::NSH;
   constexpr int PH = TH + NSH - 1, PW = TW + NSH - 1, PPIX = PH * PW;
+  // LDS pitch of a patch row in pixels: 32 puts the two grid rows of a B read 32 pixels (0 mod 16
+  // slots of 80 B) apart -> conflict-free ds_read_b128 (2-way at the packed pitch PW)
+  constexpr int PWP = 32;
+  static_assert(PWP >= PW, "patch pitch");
   constexpr int WMW = BM / 32, WNW = 4 / WMW, NT = (BN / 32) / WNW;
   constexpr int A_SZ = BM * PT_STR;
   constexpr int A_ITEMS = T * BM * 4;             // 16-byte items of all taps' [BM][32] slices
   constexpr int A_IT = (A_ITEMS + 255) / 256;
   constexpr int P_ITEMS = PPIX * 4;                // (pixel, 8-channel group)
   constexpr int P_IT = (P_ITEMS + 255) / 256;
-  __shared__ __attribute__((aligned(16))) T16 smem[T * A_SZ + PPIX * PT_STR];
+  __shared__ __attribute__((aligned(16))) T16 smem[T * A_SZ + PH * PWP * PT_STR];
   T16* Ps = smem + T * A_SZ;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -104,7 +108,7 @@ __global__ __launch_bounds__(256, BM == 32 ? 4 : 2) void pconvt_kernel(PtArgs g)
 #pragma unroll
   for (int j = 0; j < NT; ++j) {
     const int n = (wn * NT + j) * 32 + lr;
-    pbase[j] = ((n / TW) * PW + (n % TW)) * PT_STR + lh * 8;
+    pbase[j] = ((n / TW) * PWP + (n % TW)) * PT_STR + lh * 8;
   }
 
   // global -> registers for K block kb of tile t (issued one block ahead of its use), -> LDS
@@ -148,10 +152,11 @@ __global__ __launch_bounds__(256, BM == 32 ? 4 : 2) void pconvt_kernel(PtArgs g)
       const int it = tid + i * 256;
       if (it < P_ITEMS) {
         const int cg = it / PPIX, pix = it - cg * PPIX;
+        const int pr = pix / PW, pc = pix - pr * PW;
         tbf16x8 v;
 #pragma unroll
         for (int e = 0; e < 8; ++e) v[e] = (T16)rp[i][e];
-        *reinterpret_cast<tbf16x8*>(Ps + pix * PT_STR + cg * 8) = v;
+        *reinterpret_cast<tbf16x8*>(Ps + (pr * PWP + pc) * PT_STR + cg * 8) = v;
       }
     }
   };
@@ -186,7 +191,7 @@ __global__ __launch_bounds__(256, BM == 32 ? 4 : 2) void pconvt_kernel(PtArgs g)
           for (int sw = 0; sw < NSH; ++sw)
 #pragma unroll
             for (int j = 0; j < NT; ++j)
-              bfr[sh][sw][j] = *reinterpret_cast<const tbf16x8*>(Ps + pbase[j] + (sh * PW + sw) * PT_STR + ks * 16);
+              bfr[sh][sw][j] = *reinterpret_cast<const tbf16x8*>(Ps + pbase[j] + (sh * PWP + sw) * PT_STR + ks * 16);
 #pragma unroll
         for (int kh = 0; kh < KS; ++kh) {
           const int ph = (kh + PAD) & 1;             // parity served by this tap row
