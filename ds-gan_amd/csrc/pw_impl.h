@@ -66,8 +66,14 @@ __device__ __forceinline__ hx4<T16> cvt4(float4 v, int bact, float slope) {
 // BN x WN waves / BK: 128 x 2 / 32 (4 waves, two workgroups per CU), or the wide form 256 x 4 / 64
 // (8 waves, 256 x 256 tiles, 64-deep K steps: twice the MFMAs per staged byte and per barrier)
 // for the deep, wide GEMMs of the unfused blocks.
-template <typename T16, int MODE, int BM, int ABF = 0, int BBF = 0, int BN = 128, int WN = 2, int BK = PBK>
+// SWP (FWD / DGRAD with a 16-bit output): the MFMA operands go in swapped, a pixel x channel tile,
+// so each lane ends with runs of 4 consecutive pixels of one channel and the epilogue writes
+// 16-byte stores (2 per 32x32 tile instead of 16 two-byte ones).  fp32 outputs keep the channel x
+// pixel tile, whose 4-byte stores fill two whole 128-byte rows per instruction (measured: the
+// swapped form's 16-byte row-strided fp32 stores are 10-15 % slower there).
+template <typename T16, int MODE, int BM, int ABF = 0, int BBF = 0, int BN = 128, int WN = 2, int BK = PBK, int SWP = 0>
 __global__ __launch_bounds__(128 * WN, WN == 2 ? 2 : 1) void pwgemm_kernel(PwArgs g) {
+  constexpr bool SW = MODE != PW_WGRAD && SWP;
   typedef hx8<T16> pbf16x8;
   typedef hx4<T16> pbf16x4;
   constexpr int WM = 2, NT = 64 * WM * WN;
@@ -281,8 +287,8 @@ __global__ __launch_bounds__(128 * WN, WN == 2 ? 2 : 1) void pwgemm_kernel(PwArg
     for (int r = 0; r < 16; ++r) bv[r] = 0.f;
     if (has_bias) {   // one uniform branch; guarded loads are clamp + select (see igemm.hip ldsel)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int m = m0 + wm * TM * 32 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+      for (int r = 0; r < 16; ++r) {   // SW: lane lr's channel; else row (r&3) + 8(r>>2) + 4lh
+        const int m = m0 + wm * TM * 32 + i * 32 + (SW ? lr : (r & 3) + 8 * (r >> 2) + 4 * lh);
         const float t = g.bias[m < g.M ? m : 0];
         bv[r] = m < g.M ? t : 0.f;
       }
@@ -329,7 +335,7 @@ __global__ __launch_bounds__(128 * WN, WN == 2 ? 2 : 1) void pwgemm_kernel(PwArg
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j)
-          acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
+          acc[i][j] = SW ? mfma16(bfr[j], af[i], acc[i][j]) : mfma16(af[i], bfr[j], acc[i][j]);
     }
     if (kt + 1 < nk) sstore(buf ^ 1);
     __syncthreads();
@@ -374,7 +380,11 @@ __global__ __launch_bounds__(128 * WN, WN == 2 ? 2 : 1) void pwgemm_kernel(PwArg
     return;
   }
   // FWD / DGRAD: element (m, n0+col) of image bimg lives at base + m*P + col; buffer resources
-  // are based at pixel p0 of row 0, their range ends at row M (rows >= M are dropped/read 0).
+  // are based at pixel p0 of row 0, their range ends at row M (a lane whose channel is >= M gets an
+  // offset past the range: its loads read 0, its stores are dropped).  Tile (i, j) is pixel x
+  // channel: lane lr holds channel mrow + lr, register 4q + e pixel col0 + 8q + 4lh + e -- fp32
+  // side tensors move as one 16-byte access per group q, 16-bit ones as 8-byte loads and, paired
+  // by v_permlane32_swap, two 16-byte stores per tile (cdna_hip_programming.md T21).
   const unsigned range = (unsigned)(((long)g.M * g.P - p0) * 4);
   const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(g.Y + (long)bimg * g.y_bs + p0), (short)0, range, 0x00020000);
@@ -387,124 +397,231 @@ __global__ __launch_bounds__(128 * WN, WN == 2 ? 2 : 1) void pwgemm_kernel(PwArg
                                                      g.gbf ? range / 2 : range, 0x00020000);
   if (g.gpre) rg = __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)g.gpre + ((long)bimg * g.gpre_bs + p0) * esz),
                                                      (short)0, g.gbf ? range / 2 : range, 0x00020000);
-  const int P4 = g.P * 4;
-  const bool full = m0 + BM <= g.M;
+  // 16-bit store of this lane's 16 values: groups (q, q+1) swap halves so lanes 0-31 hold pixels
+  // 8q..8q+7 and lanes 32-63 pixels 8q+8..8q+15 of their channel (byte offset +16)
+  auto store16 = [&](__amdgpu_buffer_rsrc_t r, const float* v, int vh, int srow) __attribute__((always_inline)) {
+    unsigned d[8];
 #pragma unroll
-  for (int j = 0; j < TN; ++j) {
-    const int col = wn * TN * 32 + j * 32 + lr;
+    for (int t = 0; t < 8; ++t) d[t] = (unsigned)f2h<T16>(v[2 * t]) | ((unsigned)f2h<T16>(v[2 * t + 1]) << 16);
 #pragma unroll
-    for (int i = 0; i < TM; ++i) {
-      const int mrow = m0 + wm * TM * 32 + i * 32;   // uniform
-      // lane part of the offset: rows 4h, column col.  In a partial M tile, rows >= M get an
-      // offset past the resource range so the hardware drops the store / returns 0.
-      const int vofs = (4 * lh * g.P + col) * 4;
-      const int mlim = full ? BM : g.M - mrow - 4 * lh;   // rows (r&3)+8(r>>2) < mlim are valid
-      int vrow[16];
+    for (int q = 0; q < 4; q += 2) {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) vrow[r] = ((r & 3) + 8 * (r >> 2) < mlim) ? vofs : (int)PW_OOB;
-      float v[16];
-#pragma unroll
-      for (int r = 0; r < 16; ++r) v[r] = acc[i][j][r];
-      if (g.gpre && g.gbf) {          // DGRAD: v *= gp, gp = act'(pre) stored bf16 by the forward
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const unsigned short hb = __builtin_amdgcn_raw_buffer_load_b16(
-              rg, vrow[r] == (int)PW_OOB ? (int)PW_OOB : vrow[r] / 2, (mrow + (r & 3) + 8 * (r >> 2)) * (P4 / 2), 0);
-          v[r] *= h2f<T16>(hb);
-        }
-      } else if (g.gpre) {
-        float gv[16];
-#pragma unroll
-        for (int r = 0; r < 16; ++r)
-          gv[r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
-                      rg, vrow[r], (mrow + (r & 3) + 8 * (r >> 2)) * P4, 0));
-        act_g_mul_arr(g.gact, v, gv, g.slope);
+      for (int w = 0; w < 2; ++w) {
+        const auto x = __builtin_amdgcn_permlane32_swap(d[2 * q + w], d[2 * q + 2 + w], false, false);
+        d[2 * q + w] = x[0];
+        d[2 * q + 2 + w] = x[1];
       }
-      bool acted = false;
-      if (g.ypre && g.gbf) {          // FWD: ypre <- bf16 act'(pre), v <- act(pre) (one GELU evaluation)
-        float apv[16];
-        if (g.act == ACT_GELU) {
+      const pu32x4 o = {d[2 * q], d[2 * q + 1], d[2 * q + 2], d[2 * q + 3]};
+      __builtin_amdgcn_raw_buffer_store_b128(o, r, vh, srow + 16 * q, 0);
+    }
+  };
+  if constexpr (SW) {
 #pragma unroll
-          for (int r = 0; r < 16; r += 2) {
-            f32x2 a, ap;
-            gelu_pair_fast2(f32x2{v[r], v[r + 1]}, a, ap);
-            v[r] = a.x; v[r + 1] = a.y;
-            apv[r] = ap.x; apv[r + 1] = ap.y;
+    for (int j = 0; j < TN; ++j) {
+      const int col0 = wn * TN * 32 + j * 32;
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int mrow = m0 + wm * TM * 32 + i * 32;   // uniform
+        const bool ok = mrow + lr < g.M;
+        const int e0 = lr * g.P + col0 + 4 * lh;       // lane part (elements)
+        const int v4 = ok ? e0 * 4 : (int)PW_OOB;      // fp32 byte offsets; + 32 q in soffset
+        const int v2 = ok ? e0 * 2 : (int)PW_OOB;      // 16-bit loads; + 16 q
+        const int vh = ok ? (e0 - 4 * lh) * 2 + 16 * lh : (int)PW_OOB;   // paired 16-bit stores
+        const int s4 = mrow * g.P * 4, s2 = mrow * g.P * 2;
+        float v[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) v[r] = acc[i][j][r];
+        if (g.gpre && g.gbf) {          // DGRAD: v *= gp, gp = act'(pre) stored 16-bit by the forward
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const auto u = __builtin_amdgcn_raw_buffer_load_b64(rg, v2, s2 + 16 * q, 0);
+            v[4 * q] *= h2f<T16>((unsigned short)(u[0] & 0xffffu));
+            v[4 * q + 1] *= h2f<T16>((unsigned short)(u[0] >> 16));
+            v[4 * q + 2] *= h2f<T16>((unsigned short)(u[1] & 0xffffu));
+            v[4 * q + 3] *= h2f<T16>((unsigned short)(u[1] >> 16));
           }
-        } else {
+        } else if (g.gpre) {
+          float gv[16];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const float4 u = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rg, v4, s4 + 32 * q, 0));
+            gv[4 * q] = u.x; gv[4 * q + 1] = u.y; gv[4 * q + 2] = u.z; gv[4 * q + 3] = u.w;
+          }
+          act_g_mul_arr(g.gact, v, gv, g.slope);
+        }
+        bool acted = false;
+        if (g.ypre && g.gbf) {          // FWD: ypre <- 16-bit act'(pre), v <- act(pre) (one GELU evaluation)
+          float apv[16];
+          if (g.act == ACT_GELU) {
+#pragma unroll
+            for (int r = 0; r < 16; r += 2) {
+              f32x2 a, ap;
+              gelu_pair_fast2(f32x2{v[r], v[r + 1]}, a, ap);
+              v[r] = a.x; v[r + 1] = a.y;
+              apv[r] = ap.x; apv[r + 1] = ap.y;
+            }
+          } else {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+              apv[r] = act_g(g.act, v[r], g.slope);
+              v[r] = act_f(g.act, v[r], g.slope);
+            }
+          }
+          store16(rp, apv, vh, s2);
+          acted = true;
+        } else if (g.ypre) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const pu32x4 o = {__builtin_bit_cast(unsigned, v[4 * q]), __builtin_bit_cast(unsigned, v[4 * q + 1]),
+                              __builtin_bit_cast(unsigned, v[4 * q + 2]), __builtin_bit_cast(unsigned, v[4 * q + 3])};
+            __builtin_amdgcn_raw_buffer_store_b128(o, rp, v4, s4 + 32 * q, 0);
+          }
+        }
+        if (!acted) act_f_arr(g.act, v, g.slope);
+        if (g.accumulate) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const float4 u = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(ry, v4, s4 + 32 * q, 0));
+            v[4 * q] += u.x; v[4 * q + 1] += u.y; v[4 * q + 2] += u.z; v[4 * q + 3] += u.w;
+          }
+        }
+        if (g.y_bf16) {   // 16-bit output: same rows, half the byte offsets
+          store16(ryh, v, vh, s2);
+          continue;
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const pu32x4 o = {__builtin_bit_cast(unsigned, v[4 * q]), __builtin_bit_cast(unsigned, v[4 * q + 1]),
+                            __builtin_bit_cast(unsigned, v[4 * q + 2]), __builtin_bit_cast(unsigned, v[4 * q + 3])};
+          __builtin_amdgcn_raw_buffer_store_b128(o, ry, v4, s4 + 32 * q, 0);
+        }
+      }
+    }
+  } else {
+    const int P4 = g.P * 4;
+    const bool full = m0 + BM <= g.M;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int col = wn * TN * 32 + j * 32 + lr;
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int mrow = m0 + wm * TM * 32 + i * 32;   // uniform
+        // lane part of the offset: rows 4h, column col.  In a partial M tile, rows >= M get an
+        // offset past the resource range so the hardware drops the store / returns 0.
+        const int vofs = (4 * lh * g.P + col) * 4;
+        const int mlim = full ? BM : g.M - mrow - 4 * lh;   // rows (r&3)+8(r>>2) < mlim are valid
+        int vrow[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) vrow[r] = ((r & 3) + 8 * (r >> 2) < mlim) ? vofs : (int)PW_OOB;
+        float v[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) v[r] = acc[i][j][r];
+        if (g.gpre && g.gbf) {          // DGRAD: v *= gp, gp = act'(pre) stored bf16 by the forward
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
-            apv[r] = act_g(g.act, v[r], g.slope);
-            v[r] = act_f(g.act, v[r], g.slope);
+            const unsigned short hb = __builtin_amdgcn_raw_buffer_load_b16(
+                rg, vrow[r] == (int)PW_OOB ? (int)PW_OOB : vrow[r] / 2, (mrow + (r & 3) + 8 * (r >> 2)) * (P4 / 2), 0);
+            v[r] *= h2f<T16>(hb);
           }
+        } else if (g.gpre) {
+          float gv[16];
+#pragma unroll
+          for (int r = 0; r < 16; ++r)
+            gv[r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                        rg, vrow[r], (mrow + (r & 3) + 8 * (r >> 2)) * P4, 0));
+          act_g_mul_arr(g.gact, v, gv, g.slope);
+        }
+        bool acted = false;
+        if (g.ypre && g.gbf) {          // FWD: ypre <- bf16 act'(pre), v <- act(pre) (one GELU evaluation)
+          float apv[16];
+          if (g.act == ACT_GELU) {
+#pragma unroll
+            for (int r = 0; r < 16; r += 2) {
+              f32x2 a, ap;
+              gelu_pair_fast2(f32x2{v[r], v[r + 1]}, a, ap);
+              v[r] = a.x; v[r + 1] = a.y;
+              apv[r] = ap.x; apv[r + 1] = ap.y;
+            }
+          } else {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+              apv[r] = act_g(g.act, v[r], g.slope);
+              v[r] = act_f(g.act, v[r], g.slope);
+            }
+          }
+#pragma unroll
+          for (int r = 0; r < 16; ++r)
+            __builtin_amdgcn_raw_buffer_store_b16(f2h<T16>(apv[r]), rp,
+                                                  vrow[r] == (int)PW_OOB ? (int)PW_OOB : vrow[r] / 2,
+                                                  (mrow + (r & 3) + 8 * (r >> 2)) * (P4 / 2), 0);
+          acted = true;
+        } else if (g.ypre) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r)
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v[r]), rp, vrow[r],
+                                                  (mrow + (r & 3) + 8 * (r >> 2)) * P4, 0);
+        }
+        if (!acted) act_f_arr(g.act, v, g.slope);
+        if (g.accumulate) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r)
+            v[r] += __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                        ry, vrow[r], (mrow + (r & 3) + 8 * (r >> 2)) * P4, 0));
+        }
+        if (g.y_bf16) {   // bf16 output: same rows, half the byte offsets
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const unsigned short hb = f2h<T16>(v[r]);
+            __builtin_amdgcn_raw_buffer_store_b16(hb, ryh, vrow[r] == (int)PW_OOB ? (int)PW_OOB : vrow[r] / 2,
+                                                  (mrow + (r & 3) + 8 * (r >> 2)) * (P4 / 2), 0);
+          }
+          continue;
         }
 #pragma unroll
         for (int r = 0; r < 16; ++r)
-          __builtin_amdgcn_raw_buffer_store_b16(f2h<T16>(apv[r]), rp,
-                                                vrow[r] == (int)PW_OOB ? (int)PW_OOB : vrow[r] / 2,
-                                                (mrow + (r & 3) + 8 * (r >> 2)) * (P4 / 2), 0);
-        acted = true;
-      } else if (g.ypre) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r)
-          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v[r]), rp, vrow[r],
+          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v[r]), ry, vrow[r],
                                                 (mrow + (r & 3) + 8 * (r >> 2)) * P4, 0);
       }
-      if (!acted) act_f_arr(g.act, v, g.slope);
-      if (g.accumulate) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r)
-          v[r] += __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
-                      ry, vrow[r], (mrow + (r & 3) + 8 * (r >> 2)) * P4, 0));
-      }
-      if (g.y_bf16) {   // bf16 output: same rows, half the byte offsets
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const unsigned short hb = f2h<T16>(v[r]);
-          __builtin_amdgcn_raw_buffer_store_b16(hb, ryh, vrow[r] == (int)PW_OOB ? (int)PW_OOB : vrow[r] / 2,
-                                                (mrow + (r & 3) + 8 * (r >> 2)) * (P4 / 2), 0);
-        }
-        continue;
-      }
-#pragma unroll
-      for (int r = 0; r < 16; ++r)
-        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v[r]), ry, vrow[r],
-                                              (mrow + (r & 3) + 8 * (r >> 2)) * P4, 0);
     }
   }
 }
 
-template <typename T16, int MODE, int BM, int ABF = 0, int BBF = 0, int BN = 128, int WN = 2, int BK = PBK>
+template <typename T16, int MODE, int BM, int ABF = 0, int BBF = 0, int BN = 128, int WN = 2, int BK = PBK, int SWP = 0>
 static void pw_launch(const PwArgs& g, int splits, hipStream_t st) {
   const int mt = (g.M + BM - 1) / BM;
   const int nt = (MODE == PW_WGRAD) ? (g.N + BN - 1) / BN : g.N / BN;
-  hipLaunchKernelGGL((pwgemm_kernel<T16, MODE, BM, ABF, BBF, BN, WN, BK>), dim3((unsigned)((long)mt * nt * splits)),
+  hipLaunchKernelGGL((pwgemm_kernel<T16, MODE, BM, ABF, BBF, BN, WN, BK, SWP>), dim3((unsigned)((long)mt * nt * splits)),
                      dim3(128 * WN), 0, st, g);
 }
 
 constexpr int PW_WIDE = -1;   // tile selector: 256 x 256 tiles, 8 waves, 64-deep K steps
 
-// FWD / DGRAD launch over (tile rows, bf16 weight, bf16 activation)
-template <typename T16, int MODE>
-static void pw_launch_ab(const PwArgs& g, int bm, int abf, int bbf, hipStream_t st) {
+// FWD / DGRAD launch over (tile rows, bf16 weight, bf16 activation, 16-bit output)
+template <typename T16, int MODE, int SWP>
+static void pw_launch_abs(const PwArgs& g, int bm, int abf, int bbf, hipStream_t st) {
   const int sel = (abf ? 2 : 0) + (bbf ? 1 : 0);
 #define PW_AB(BM)                                                      \
   switch (sel) {                                                       \
-    case 0: pw_launch<T16, MODE, BM, 0, 0>(g, 1, st); break;                \
-    case 1: pw_launch<T16, MODE, BM, 0, 1>(g, 1, st); break;                \
-    case 2: pw_launch<T16, MODE, BM, 1, 0>(g, 1, st); break;                \
-    default: pw_launch<T16, MODE, BM, 1, 1>(g, 1, st); break;               \
+    case 0: pw_launch<T16, MODE, BM, 0, 0, 128, 2, PBK, SWP>(g, 1, st); break;                \
+    case 1: pw_launch<T16, MODE, BM, 0, 1, 128, 2, PBK, SWP>(g, 1, st); break;                \
+    case 2: pw_launch<T16, MODE, BM, 1, 0, 128, 2, PBK, SWP>(g, 1, st); break;                \
+    default: pw_launch<T16, MODE, BM, 1, 1, 128, 2, PBK, SWP>(g, 1, st); break;               \
   }
 #define PW_ABW                                                                    \
   switch (sel) {                                                                  \
-    case 0: pw_launch<T16, MODE, 128, 0, 0>(g, 1, st); break;  /* (not selected) */  \
-    case 1: pw_launch<T16, MODE, 256, 0, 1, 256, 4, 64>(g, 1, st); break;              \
-    case 2: pw_launch<T16, MODE, 256, 1, 0, 256, 4, 64>(g, 1, st); break;              \
-    default: pw_launch<T16, MODE, 256, 1, 1, 256, 4, 64>(g, 1, st); break;             \
+    case 0: pw_launch<T16, MODE, 128, 0, 0, 128, 2, PBK, SWP>(g, 1, st); break;  /* (not selected) */  \
+    case 1: pw_launch<T16, MODE, 256, 0, 1, 256, 4, 64, SWP>(g, 1, st); break;              \
+    case 2: pw_launch<T16, MODE, 256, 1, 0, 256, 4, 64, SWP>(g, 1, st); break;              \
+    default: pw_launch<T16, MODE, 256, 1, 1, 256, 4, 64, SWP>(g, 1, st); break;             \
   }
   if (bm == PW_WIDE) { PW_ABW } else if (bm == 256) { PW_AB(256) } else if (bm == 128) { PW_AB(128) } else { PW_AB(64) }
 #undef PW_AB
 #undef PW_ABW
+}
+template <typename T16, int MODE>
+static void pw_launch_ab(const PwArgs& g, int bm, int abf, int bbf, hipStream_t st) {
+  if (g.y_bf16 || (g.ypre && g.gbf)) pw_launch_abs<T16, MODE, 1>(g, bm, abf, bbf, st);
+  else pw_launch_abs<T16, MODE, 0>(g, bm, abf, bbf, st);
 }
 
 // K (pixel) split of a weight-grad launch: about `target` workgroups (640 = 2.5 per CU for the

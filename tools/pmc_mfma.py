@@ -22,9 +22,13 @@ import sys
 def fam(name):
     if os.environ.get("PMC_BY") == "name":   # one row per template instance
         m = re.search(r"dsg::(\w+?_kernel<[^(]*>)", name)
-        return m.group(1) if m else None
+        return m.group(1) if m else (name if name.startswith("_ZN3dsg") else None)
     m = re.search(r"dsg::(\w+?_kernel|\w+)(<|\()", name)
-    return m.group(1) if m else None
+    if m:
+        return m.group(1)
+    # names c++filt leaves mangled (16-bit float template arguments, DF16b / DF16_)
+    m = re.match(r"_ZN3dsg(\d+)", name)
+    return name[m.end():m.end() + int(m.group(1))] if m else None
 
 
 def main():

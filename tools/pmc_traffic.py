@@ -8,7 +8,11 @@ import json, re, sqlite3, sys, collections
 
 def fam(name):
     m = re.search(r"dsg::(\w+?_kernel|\w+)(<|\()", name)
-    return m.group(1) if m else None
+    if m:
+        return m.group(1)
+    # names c++filt leaves mangled (16-bit float template arguments, DF16b / DF16_)
+    m = re.match(r"_ZN3dsg(\d+)", name)
+    return name[m.end():m.end() + int(m.group(1))] if m else None
 
 
 def per_family(db, counter):

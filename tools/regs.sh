@@ -2,6 +2,8 @@
 # Register / spill / occupancy table of every kernel in one HIP source (device-only compile).
 # usage: tools/regs.sh ds-gan_amd/csrc/<file>.hip [grep-filter]
 src=$1; flt=${2:-.}
+# the per-file flags of ds-gan_amd/build_lib.py (EXTRA)
+case "$(basename "$src")" in dwconv.hip|mlp.hip|thin3.hip) set -- "$1" "$flt" "$3 -fno-slp-vectorize";; esac
 /opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -I"$(dirname "$src")" --cuda-device-only -c "$src" \
   -o /tmp/regs_$$.o -Rpass-analysis=kernel-resource-usage $3 2>&1 |
 python3 -c '
