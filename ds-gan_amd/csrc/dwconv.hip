@@ -181,6 +181,15 @@ struct DwTile {
   static_assert(TWT * THT == 256, "256 threads");
 };
 
+// 1-D grid, XCD-aware: workgroup id -> logical index so that each XCD walks one contiguous range
+// (dispatch round-robins ids over the 8 XCDs): the tiles of a plane, which share halo rows and
+// columns, run on one XCD and re-read those halos from its L2 instead of HBM.
+__device__ __forceinline__ int dw_xcd_index() {
+  const int nwg = gridDim.x, id = blockIdx.x;
+  const int xcd = id & 7, q = nwg >> 3, r = nwg & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (id >> 3);
+}
+
 template <int K, int TWT, int THT, int R, bool BATCH = false>
 __device__ __forceinline__ void dw_stage(float* tile, const float* __restrict__ xp, int H, int W, int th0, int tw0) {
   using T = DwTile<K, TWT, THT, R>;
@@ -292,10 +301,11 @@ __global__ __launch_bounds__(256, 4) void dwconv_fwd_v2(const float* __restrict_
                                                      const float* __restrict__ w,
                                                      const float* __restrict__ bias,
                                                      float* __restrict__ y, long y_bs, int C, int H,
-                                                     int W, int flip, int accumulate, int tiles_w) {
+                                                     int W, int flip, int accumulate, int tiles_w, int tiles) {
   using T = DwTile<K, TWT, THT, R>;
   __shared__ __attribute__((aligned(16))) float tile[T::LH * T::LP];
-  dw_fwd_body<K, TWT, THT, R>(x, x_bs, w, bias, y, y_bs, C, H, W, flip, accumulate, tiles_w, blockIdx.x, blockIdx.y,
+  const int t = dw_xcd_index(), plane = t / tiles;
+  dw_fwd_body<K, TWT, THT, R>(x, x_bs, w, bias, y, y_bs, C, H, W, flip, accumulate, tiles_w, t - plane * tiles, plane,
                               tile);
 }
 
@@ -396,12 +406,13 @@ template <int K, int TWT, int THT, int R>
 __global__ __launch_bounds__(256, 4) void dwconv_wgrad_v2(const float* __restrict__ dy, long dy_bs,
                                                        const float* __restrict__ x, long x_bs,
                                                        float* __restrict__ ws,
-                                                       int N, int C, int H, int W, int tiles_w, int nper) {
+                                                       int N, int C, int H, int W, int tiles_w, int nper, int tiles) {
   using T = DwTile<K, TWT, THT, R>;
   __shared__ __attribute__((aligned(16))) float tile[T::LH * T::LP];
   __shared__ float red[4 * (K * K + 1)];
-  dw_wgrad_body<K, TWT, THT, R>(dy, dy_bs, x, x_bs, ws, N, C, H, W, tiles_w, nper, blockIdx.x, blockIdx.y, blockIdx.z,
-                                gridDim.x, tile, red);
+  const int t = dw_xcd_index(), cs = t / tiles, split = cs / C;   // t = (split * C + c) * tiles + tile
+  dw_wgrad_body<K, TWT, THT, R>(dy, dy_bs, x, x_bs, ws, N, C, H, W, tiles_w, nper, t - cs * tiles, cs - split * C, split,
+                                tiles, tile, red);
 }
 
 // The four MidMLKA quarters' weight-grads in one launch: blockIdx.z = quarter * nsplit + split.
@@ -439,8 +450,8 @@ static void dw_fwd_v2(const float* x, long x_bs, const float* w, const float* bi
                       int N, int C, int H, int W, int flip, int accumulate, hipStream_t st) {
   using T = DwTile<K, TWT, THT, R>;
   const int tw = W / T::TW, th = (H + T::TH - 1) / T::TH;
-  hipLaunchKernelGGL((dwconv_fwd_v2<K, TWT, THT, R>), dim3(tw * th, N * C), dim3(256), 0, st, x, x_bs, w, bias, y,
-                     y_bs, C, H, W, flip, accumulate, tw);
+  hipLaunchKernelGGL((dwconv_fwd_v2<K, TWT, THT, R>), dim3(tw * th * N * C), dim3(256), 0, st, x, x_bs, w, bias, y,
+                     y_bs, C, H, W, flip, accumulate, tw, tw * th);
 }
 
 // images per workgroup of the tiled weight-grad: about `target` workgroups, as many images each as
@@ -471,8 +482,8 @@ static long dw_wgrad_v2(const float* dy, long dy_bs, const float* x, long x_bs, 
   int nsplit, nper;
   const long G = dw_wgrad_v2_plan<K, TWT, THT, R>(N, C, H, W, &nsplit, &nper);
   if (ws)
-    hipLaunchKernelGGL((dwconv_wgrad_v2<K, TWT, THT, R>), dim3(tw * th, C, nsplit), dim3(256), 0, st, dy, dy_bs, x,
-                       x_bs, ws, N, C, H, W, tw, nper);
+    hipLaunchKernelGGL((dwconv_wgrad_v2<K, TWT, THT, R>), dim3(tw * th * C * nsplit), dim3(256), 0, st, dy, dy_bs, x,
+                       x_bs, ws, N, C, H, W, tw, nper, tw * th);
   return G;
 }
 

@@ -98,6 +98,9 @@ struct INBwdArgs {
   float* dres; long dres_bs;   // nullable
   float* dscale;               // nullable, [N*C] (written)
   int N, C, HW, act; float slope, eps;
+  void* dxh;                   // nullable: dx stored 16-bit (the library half type) here instead of dx
+  float* dxsum;                // nullable, [N*C]: per-plane sum of the fp32 dx (before rounding)
+  int half;                    // half type of dxh (HALF_BF16 / HALF_F16)
 };
 
 // y = act(xhat + res), xhat = (s*x - mean) * rstd
@@ -311,10 +314,27 @@ __global__ __launch_bounds__(NT == 64 ? 256 : NT) void instnorm_bwd_v4(INBwdArgs
     if (dres) dres[i] = g;
     return g;
   };
+  // 16-bit dx (dxh): its only readers are 16-bit-operand MFMA kernels, which round it the same way
+  unsigned short* dxh = a.dxh ? reinterpret_cast<unsigned short*>(a.dxh) + (long)n * a.dx_bs + po : nullptr;
+  float dsum = 0.f;
   auto fin = [&](int i, float4 g, float4 xh, float mg, float mgh) {
     const float k = s * rs;
-    dx[i] = make_float4(k * (g.x - mg - xh.x * mgh), k * (g.y - mg - xh.y * mgh), k * (g.z - mg - xh.z * mgh),
-                        k * (g.w - mg - xh.w * mgh));
+    const float4 v = make_float4(k * (g.x - mg - xh.x * mgh), k * (g.y - mg - xh.y * mgh), k * (g.z - mg - xh.z * mgh),
+                                 k * (g.w - mg - xh.w * mgh));
+    if (dxh) {
+      uint2 u;
+      if (a.half == HALF_F16) {
+        u.x = (unsigned)f2h<_Float16>(v.x) | ((unsigned)f2h<_Float16>(v.y) << 16);
+        u.y = (unsigned)f2h<_Float16>(v.z) | ((unsigned)f2h<_Float16>(v.w) << 16);
+      } else {
+        u.x = (unsigned)f2h<__bf16>(v.x) | ((unsigned)f2h<__bf16>(v.y) << 16);
+        u.y = (unsigned)f2h<__bf16>(v.z) | ((unsigned)f2h<__bf16>(v.w) << 16);
+      }
+      *reinterpret_cast<uint2*>(dxh + 4 * i) = u;
+      dsum += hsum4(v);
+    } else {
+      dx[i] = v;
+    }
   };
   float sg = 0.f, sgh = 0.f;
   float2 m;
@@ -383,6 +403,10 @@ __global__ __launch_bounds__(NT == 64 ? 256 : NT) void instnorm_bwd_v4(INBwdArgs
     }
   }
   if (a.dscale && t == 0) a.dscale[plane] = m.y * (float)a.HW * a.eps * rs * rs / s;
+  if (a.dxsum) {   // (uniform branch: every thread of the plane's block reaches the reduction)
+    const float2 ds = plane_sum2<NT>(dsum, 0.f, sh);
+    if (t == 0) a.dxsum[plane] = ds.x;
+  }
 }
 
 // ---------------------------------------------------------------------------------------
@@ -990,6 +1014,33 @@ int dsgan_instnorm_fwd_bf16(const float* x, long x_bs, void* y, long y_bs, float
     hipLaunchKernelGGL((instnorm_fwd_v4<1024, 16>), dim3(planes), dim3(1024), 0, st, a);
   else
     hipLaunchKernelGGL((instnorm_fwd_v4<1024, 0>), dim3(planes), dim3(1024), 0, st, a);
+  DSG_CHECK_LAUNCH();
+  return 0;
+}
+
+// Backward with dx stored in the library's 16-bit half type (dxh, batch stride dxh_bs elements)
+// plus the per-plane sums of the fp32 dx (dxsum [N*C]; nullable) -- the ConvTranspose backward's
+// operand (its data-/weight-grad kernels read it as 16-bit MFMA operands) and its bias grad.
+int dsgan_instnorm_bwd_h(const float* dy, long dy_bs, const float* x, long x_bs, const float* res, long res_bs,
+                         const float* mean, const float* rstd, void* dxh, long dxh_bs, float* dxsum, float* dres,
+                         long dres_bs, int N, int C, int HW, int act, float slope, float eps, hipStream_t st) {
+  DSG_REQUIRE(dy && x && mean && rstd && dxh && N > 0 && C > 0 && HW > 0, "dsgan_instnorm_bwd_h: bad args");
+  DSG_REQUIRE(in_v4_ok(HW, dy, dy_bs) && in_v4_ok(HW, x, x_bs) && (!res || in_v4_ok(HW, res, res_bs)) &&
+                  (!dres || in_v4_ok(HW, dres, dres_bs)) && ((uintptr_t)dxh & 7) == 0 && dxh_bs % 4 == 0,
+              "dsgan_instnorm_bwd_h: planes must be float4-aligned (HW %% 4 == 0) and dxh 8-byte aligned");
+  INBwdArgs a{dy, dy_bs, x, x_bs, nullptr, res, res_bs, mean, rstd, nullptr, dxh_bs, dres, dres_bs, nullptr,
+              N, C, HW, act, slope, eps, dxh, dxsum, half_type()};
+  const int planes = N * C;
+  if (HW <= 64 * 16)
+    hipLaunchKernelGGL((instnorm_bwd_v4<64, 4, true>), dim3(cdiv(planes, 4)), dim3(256), 0, st, a);
+  else if (HW <= 256 * 16)
+    hipLaunchKernelGGL((instnorm_bwd_v4<256, 4, true>), dim3(planes), dim3(256), 0, st, a);
+  else if (HW <= 256 * 64)
+    hipLaunchKernelGGL((instnorm_bwd_v4<256, 16, true>), dim3(planes), dim3(256), 0, st, a);
+  else if (HW <= 1024 * 64)
+    hipLaunchKernelGGL((instnorm_bwd_v4<1024, 16, false>), dim3(planes), dim3(1024), 0, st, a);
+  else
+    hipLaunchKernelGGL((instnorm_bwd_v4<1024, 0, false>), dim3(planes), dim3(1024), 0, st, a);
   DSG_CHECK_LAUNCH();
   return 0;
 }

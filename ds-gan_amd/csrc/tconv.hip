@@ -43,8 +43,9 @@ struct TcArgs {
 };
 
 // ABF: Wt is bf16 (dsgan_conv_wtrans_bf16, cached per weight version): half the A bytes, copied to
-// LDS unconverted.
-template <typename T16, int BM, bool ABF>
+// LDS unconverted.  XH: X is 16-bit (the half type; the ConvTranspose backward's output grad from
+// dsgan_instnorm_bwd_h): half the B bytes, no conversion.
+template <typename T16, int BM, bool ABF, bool XH = false>
 __global__ __launch_bounds__(256, 2) void tconv_kernel(TcArgs g) {
   typedef hx8<T16> tbf16x8;
   constexpr int BN = 128;
@@ -77,8 +78,9 @@ __global__ __launch_bounds__(256, 2) void tconv_kernel(TcArgs g) {
   const int HWin = g.Hin * g.Win;
   const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(
       (void*)g.Wt, (short)0, (unsigned)((long)g.ntaps * g.M * g.K * (ABF ? 2 : 4)), 0x00020000);
+  constexpr int XB = XH ? 2 : 4;   // bytes per X element
   const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(g.X + (long)bimg * g.x_bs), (short)0, (unsigned)((long)g.K * HWin * 4), 0x00020000);
+      (void*)((const char*)g.X + (long)bimg * g.x_bs * XB), (short)0, (unsigned)((long)g.K * HWin * XB), 0x00020000);
 
   // B staging: thread -> column c = tid % 128, channels 16*(tid/128) .. +15 of the step
   const int col = tid & 127, kc = wave >> 1;   // kc uniform per wave: channel rows are soffsets
@@ -95,7 +97,8 @@ __global__ __launch_bounds__(256, 2) void tconv_kernel(TcArgs g) {
   typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
   float4 ra[ABF ? 1 : A_ITEMS];
   u32x4 rha[ABF ? A_ITEMS : 1];
-  float rb[16];
+  float rb[XH ? 1 : 16];
+  unsigned short rh[XH ? 16 : 1];
   auto gload = [&](int kt0) {
     const int kt = kb0 + kt0;
     const int tap = kt / ksteps_per_tap;
@@ -117,11 +120,13 @@ __global__ __launch_bounds__(256, 2) void tconv_kernel(TcArgs g) {
     }
     const int ih = ih0 + g.dh[tap], iw = iw0 + g.dw[tap];
     const bool in = qv && (unsigned)ih < (unsigned)g.Hin && (unsigned)iw < (unsigned)g.Win;
-    const int voff = in ? (ih * g.Win + iw) * 4 : 0x7fffffff;
+    const int voff = in ? (ih * g.Win + iw) * XB : 0x7fffffff;
     const int kb = k0 + 16 * kc;
 #pragma unroll
-    for (int j = 0; j < 16; ++j)
-      rb[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rx, voff, (kb + j) * HWin * 4, 0));
+    for (int j = 0; j < 16; ++j) {
+      if constexpr (XH) rh[j] = __builtin_amdgcn_raw_buffer_load_b16(rx, voff, (kb + j) * HWin * 2, 0);
+      else rb[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rx, voff, (kb + j) * HWin * 4, 0));
+    }
   };
   auto sstore = [&](int buf) {
     T16* As = smem + buf * (A_SZ + B_SZ);
@@ -139,8 +144,13 @@ __global__ __launch_bounds__(256, 2) void tconv_kernel(TcArgs g) {
       *reinterpret_cast<b4*>(As + (it >> 3) * T_STR + (it & 7) * 4) = v;
     }
     tbf16x8 lo, hi;
+    if constexpr (XH) {
 #pragma unroll
-    for (int j = 0; j < 8; ++j) { lo[j] = (T16)rb[j]; hi[j] = (T16)rb[8 + j]; }
+      for (int j = 0; j < 8; ++j) { lo[j] = __builtin_bit_cast(T16, rh[j]); hi[j] = __builtin_bit_cast(T16, rh[8 + j]); }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { lo[j] = (T16)rb[j]; hi[j] = (T16)rb[8 + j]; }
+    }
     tbf16x8* dst = reinterpret_cast<tbf16x8*>(Bs + col * T_STR + 16 * kc);
     dst[0] = lo;
     dst[1] = hi;
@@ -350,11 +360,13 @@ int dsgan_tconv(const float* X, long x_bs, const float* Wt, const float* bias, f
                         dh, dw, Hdst, Wdst, os, ph, pw, act, gact, slope, 0, nullptr, st);
 }
 
-// Same, with the split-K scratch of dsgan_tconv_workspace (NULL: never split).
-int dsgan_tconv_ws(const float* X, long x_bs, const float* Wt, const float* bias, float* Y, long y_bs,
-                   const float* gpre, long gpre_bs, int nb, int K, int M, int Hin, int Win, int Hout,
-                   int Wout, int stride, int ntaps, const int* dh, const int* dw, int Hdst, int Wdst,
-                   int os, int ph, int pw, int act, int gact, float slope, int wt_bf16, float* ws, hipStream_t st) {
+}  // extern "C"
+
+static int tconv_impl(const float* X, long x_bs, const float* Wt, const float* bias, float* Y, long y_bs,
+                      const float* gpre, long gpre_bs, int nb, int K, int M, int Hin, int Win, int Hout,
+                      int Wout, int stride, int ntaps, const int* dh, const int* dw, int Hdst, int Wdst,
+                      int os, int ph, int pw, int act, int gact, float slope, int wt_bf16, int x_half, float* ws,
+                      hipStream_t st) {
   DSG_REQUIRE(X && Wt && Y && nb > 0 && M > 0 && Hout > 0 && Wout > 0, "dsgan_tconv: bad args");
   DSG_REQUIRE(K % TBK == 0 && K > 0, "dsgan_tconv: K (input channels) must be a multiple of 32");
   DSG_REQUIRE(ntaps >= 1 && ntaps <= T_MAXTAPS, "dsgan_tconv: 1..16 taps");
@@ -379,7 +391,10 @@ int dsgan_tconv_ws(const float* X, long x_bs, const float* Wt, const float* bias
   const dim3 grid((unsigned)(tiles * S));
   with_half([&](auto* t_) {
     using T16 = std::remove_pointer_t<decltype(t_)>;
-    if (M > 64) {
+    if (x_half) {   // (the ConvTranspose data-grads: bf16 weights)
+      if (M > 64) hipLaunchKernelGGL((tconv_kernel<T16, 128, true, true>), grid, dim3(256), 0, st, g);
+      else hipLaunchKernelGGL((tconv_kernel<T16, 64, true, true>), grid, dim3(256), 0, st, g);
+    } else if (M > 64) {
       if (wt_bf16) hipLaunchKernelGGL((tconv_kernel<T16, 128, true>), grid, dim3(256), 0, st, g);
       else hipLaunchKernelGGL((tconv_kernel<T16, 128, false>), grid, dim3(256), 0, st, g);
     } else {
@@ -396,6 +411,28 @@ int dsgan_tconv_ws(const float* X, long x_bs, const float* Wt, const float* bias
     DSG_CHECK_LAUNCH();
   }
   return 0;
+}
+
+extern "C" {
+
+// Same, with the split-K scratch of dsgan_tconv_workspace (NULL: never split).
+int dsgan_tconv_ws(const float* X, long x_bs, const float* Wt, const float* bias, float* Y, long y_bs,
+                   const float* gpre, long gpre_bs, int nb, int K, int M, int Hin, int Win, int Hout,
+                   int Wout, int stride, int ntaps, const int* dh, const int* dw, int Hdst, int Wdst,
+                   int os, int ph, int pw, int act, int gact, float slope, int wt_bf16, float* ws, hipStream_t st) {
+  return tconv_impl(X, x_bs, Wt, bias, Y, y_bs, gpre, gpre_bs, nb, K, M, Hin, Win, Hout, Wout, stride, ntaps, dh, dw,
+                    Hdst, Wdst, os, ph, pw, act, gact, slope, wt_bf16, 0, ws, st);
+}
+
+// Same with X in the library's 16-bit half type (x_bs in elements) and 16-bit Wt
+// (dsgan_conv_wtrans_bf16): the ConvTranspose backward on dsgan_instnorm_bwd_h's output.
+int dsgan_tconv_ws_xh(const void* Xh, long x_bs, const void* Wt, const float* bias, float* Y, long y_bs,
+                      const float* gpre, long gpre_bs, int nb, int K, int M, int Hin, int Win, int Hout,
+                      int Wout, int stride, int ntaps, const int* dh, const int* dw, int Hdst, int Wdst,
+                      int os, int ph, int pw, int act, int gact, float slope, float* ws, hipStream_t st) {
+  DSG_REQUIRE(K % 8 == 0, "dsgan_tconv_ws_xh: K %% 8 != 0");
+  return tconv_impl((const float*)Xh, x_bs, (const float*)Wt, bias, Y, y_bs, gpre, gpre_bs, nb, K, M, Hin, Win, Hout,
+                    Wout, stride, ntaps, dh, dw, Hdst, Wdst, os, ph, pw, act, gact, slope, 1, 1, ws, st);
 }
 
 }  // extern "C"

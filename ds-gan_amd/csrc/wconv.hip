@@ -77,8 +77,11 @@ __device__ __forceinline__ hx8<T16> frag_at(const T16* p) {
   }
 }
 
-template <typename T16, int KH, int KW, int S>
-__global__ __launch_bounds__(256, 1) void wconv_kernel(WcArgs g) {
+// XH: X is 16-bit (the half type; the ConvTranspose backward's output grad from
+// dsgan_instnorm_bwd_h): 8-byte loads of the same four columns, no conversion, half the staging
+// registers.
+template <typename T16, int KH, int KW, int S, bool XH = false>
+__global__ __launch_bounds__(256, XH ? 2 : 1) void wconv_kernel(WcArgs g) {
   typedef hx8<T16> wbf16x8;
   typedef hx4<T16> wbf16x4;
   typedef T16 wbf16x2 __attribute__((ext_vector_type(2)));
@@ -116,7 +119,8 @@ __global__ __launch_bounds__(256, 1) void wconv_kernel(WcArgs g) {
   const int HWo = g.Ho * g.Wo, HW = g.H * g.W;
   const int per_img = g.nbh * g.nbw;
 
-  float4 ra[A_IT], rb[B_IT];
+  float4 ra[A_IT], rb[XH ? 1 : B_IT];
+  uint2 rh[XH ? B_IT : 1];
 
   auto load = [&](int q) __attribute__((always_inline)) {
     const int b = q / per_img, rem = q - b * per_img;
@@ -141,7 +145,6 @@ __global__ __launch_bounds__(256, 1) void wconv_kernel(WcArgs g) {
       ra[i] = v;
     }
     // input patch rows: float4 q covers cols a0 + 4q .. a0 + 4q + 3, a0 = iw0 - 3 (16-byte aligned)
-    const float* xb = g.X + (long)b * g.x_bs;
     const int ih0 = oh0 * S - 1, a0 = ow0 * S - 4;
 #pragma unroll
     for (int i = 0; i < B_IT; ++i) {
@@ -149,10 +152,17 @@ __global__ __launch_bounds__(256, 1) void wconv_kernel(WcArgs g) {
       const int q4 = it % NQ, rest = it / NQ;
       const int pr = rest % PH, c = rest / PH;
       const int ih = ih0 + pr, col = a0 + 4 * q4;
-      float4 v = {0.f, 0.f, 0.f, 0.f};
-      if (it < B_ITEMS && (unsigned)ih < (unsigned)g.H && (unsigned)col < (unsigned)g.W)
-        v = *reinterpret_cast<const float4*>(xb + (long)(c0 + c) * HW + (long)ih * g.W + col);
-      rb[i] = v;
+      const bool ok = it < B_ITEMS && (unsigned)ih < (unsigned)g.H && (unsigned)col < (unsigned)g.W;
+      const long e = (long)b * g.x_bs + (long)(c0 + c) * HW + (long)ih * g.W + col;
+      if constexpr (XH) {
+        uint2 v = {0u, 0u};
+        if (ok) v = *reinterpret_cast<const uint2*>(reinterpret_cast<const unsigned short*>(g.X) + e);
+        rh[i] = v;
+      } else {
+        float4 v = {0.f, 0.f, 0.f, 0.f};
+        if (ok) v = *reinterpret_cast<const float4*>(g.X + e);
+        rb[i] = v;
+      }
     }
   };
   auto store = [&]() __attribute__((always_inline)) {
@@ -169,7 +179,15 @@ __global__ __launch_bounds__(256, 1) void wconv_kernel(WcArgs g) {
         const int q4 = it % NQ, rest = it / NQ;
         const int pr = rest % PH, c = rest / PH;
         T16* row = Bs + c * C_STR + pr * (S * WC_JW);
-        if constexpr (S == 2) {
+        if constexpr (XH) {   // elements e0..e3 = u.x lo, u.x hi, u.y lo, u.y hi
+          const uint2 u = rh[i];
+          if constexpr (S == 2) {
+            if (q4 > 0) *reinterpret_cast<unsigned*>(row + WC_JW + 2 * q4 - 2) = (u.x & 0xffffu) | (u.y << 16);
+            *reinterpret_cast<unsigned*>(row + 2 * q4) = (u.x >> 16) | (u.y & 0xffff0000u);
+          } else {
+            *reinterpret_cast<uint2*>(row + 4 * q4) = u;
+          }
+        } else if constexpr (S == 2) {
           // plane 1 <- (x, z) at j = 2q-2 (skip q = 0: j < 0); plane 0 <- (y, w) stored at 2q
           if (q4 > 0) *reinterpret_cast<wbf16x2*>(row + WC_JW + 2 * q4 - 2) = wbf16x2{(T16)rb[i].x, (T16)rb[i].z};
           *reinterpret_cast<wbf16x2*>(row + 2 * q4) = wbf16x2{(T16)rb[i].y, (T16)rb[i].w};
@@ -282,11 +300,13 @@ __global__ void wconv_reduce_kernel(const float* __restrict__ P, int splits, int
   }
 }
 
-constexpr int WC_TARGET_WG = 256;   // one resident workgroup per CU (next block prefetched into registers)
+// fp32 X: one resident workgroup per CU (next block prefetched into registers); 16-bit X (half the
+// staging registers): two, so one workgroup's MFMAs cover the other's block loads.
+constexpr int WC_TARGET_WG = 256, WC_TARGET_WG_XH = 512;
 
 struct WcPlan { int nbw, nbh, nblk, mt, ct, splits, bps; };
 
-static WcPlan wc_plan(int nb, int C, int M, int Ho, int Wo) {
+static WcPlan wc_plan(int nb, int C, int M, int Ho, int Wo, int target = WC_TARGET_WG) {
   WcPlan p;
   p.nbw = (Wo + WC_TW - 1) / WC_TW;
   p.nbh = (Ho + WC_TH - 1) / WC_TH;
@@ -294,7 +314,7 @@ static WcPlan wc_plan(int nb, int C, int M, int Ho, int Wo) {
   p.mt = (M + WC_BM - 1) / WC_BM;
   p.ct = C / WC_BC;
   const int tiles = p.mt * p.ct;
-  int splits = (WC_TARGET_WG + tiles - 1) / tiles;
+  int splits = (target + tiles - 1) / tiles;
   if (splits > p.nblk) splits = p.nblk;
   if (splits < 1) splits = 1;
   p.bps = (p.nblk + splits - 1) / splits;
@@ -303,7 +323,10 @@ static WcPlan wc_plan(int nb, int C, int M, int Ho, int Wo) {
 }
 
 template <typename T16, int K, int S>
-static void wc_launch(WcArgs& g, int grid, hipStream_t st) {
+static void wc_launch(WcArgs& g, int grid, bool xh, hipStream_t st) {
+  if constexpr (K == 3 && S == 2) {   // 16-bit X: the ConvTranspose 3x3/s2 weight-grads only
+    if (xh) { hipLaunchKernelGGL((wconv_kernel<T16, K, K, S, true>), dim3((unsigned)grid), dim3(256), 0, st, g); return; }
+  }
   hipLaunchKernelGGL((wconv_kernel<T16, K, K, S>), dim3((unsigned)grid), dim3(256), 0, st, g);
 }
 
@@ -320,34 +343,39 @@ int dsgan_wconv_supported(int C, int KH, int KW, int stride) {
 
 // fp32 workspace elements dsgan_wconv needs for this problem
 long dsgan_wconv_workspace(int nb, int C, int M, int Ho, int Wo, int KH, int KW) {
-  const WcPlan p = wc_plan(nb, C, M, Ho, Wo);
-  return (long)p.splits * KH * KW * M * C;
+  // (enough for either form: the 16-bit-X launches plan for twice the workgroups)
+  const WcPlan p = wc_plan(nb, C, M, Ho, Wo), q = wc_plan(nb, C, M, Ho, Wo, WC_TARGET_WG_XH);
+  return (long)(p.splits > q.splits ? p.splits : q.splits) * KH * KW * M * C;
 }
 
 // dw[M][C][KH][KW] += weight-grad of y = conv(x, w, stride, pad = 1): D = dy [nb][M][Ho][Wo],
 // X = x [nb][C][H][W] (batch strides d_bs / x_bs; X 16-byte aligned rows: W % 4 == 0);
 // ws: dsgan_wconv_workspace() floats.
-int dsgan_wconv(const float* D, long d_bs, const float* X, long x_bs, float* dw, float* ws, int nb, int C, int M,
-                int H, int W, int Ho, int Wo, int KH, int KW, int stride, int pad, hipStream_t st) {
+}  // extern "C"
+
+static int wconv_impl(const float* D, long d_bs, const void* X, long x_bs, bool xh, float* dw, float* ws, int nb,
+                      int C, int M, int H, int W, int Ho, int Wo, int KH, int KW, int stride, int pad, hipStream_t st) {
   DSG_REQUIRE(D && X && dw && ws && nb > 0 && M > 0 && Ho > 0 && Wo > 0, "dsgan_wconv: bad args");
   DSG_REQUIRE(dsgan_wconv_supported(C, KH, KW, stride) && pad == 1, "dsgan_wconv: unsupported C=%d K=%dx%d stride=%d pad=%d",
               C, KH, KW, stride, pad);
-  DSG_REQUIRE(W % 4 == 0 && x_bs % 4 == 0 && ((uintptr_t)X & 15) == 0, "dsgan_wconv: X rows must be 16-byte aligned");
+  DSG_REQUIRE(W % 4 == 0 && x_bs % 4 == 0 && ((uintptr_t)X & (xh ? 7 : 15)) == 0,
+              "dsgan_wconv: X rows must be 4-element aligned");
   DSG_REQUIRE((Ho - 1) * stride - pad + KH <= H + pad && (Wo - 1) * stride - pad + KW <= W + pad,
               "dsgan_wconv: output size inconsistent with input/pad");
-  const WcPlan p = wc_plan(nb, C, M, Ho, Wo);
+  DSG_REQUIRE(!xh || (KH == 3 && stride == 2), "dsgan_wconv_xh: 3x3 stride-2 only");
+  const WcPlan p = wc_plan(nb, C, M, Ho, Wo, xh ? WC_TARGET_WG_XH : WC_TARGET_WG);
   WcArgs g{};
-  g.D = D; g.d_bs = d_bs; g.X = X; g.x_bs = x_bs; g.P = ws;
+  g.D = D; g.d_bs = d_bs; g.X = (const float*)X; g.x_bs = x_bs; g.P = ws;
   g.nb = nb; g.M = M; g.C = C; g.H = H; g.W = W; g.Ho = Ho; g.Wo = Wo;
   g.nbw = p.nbw; g.nbh = p.nbh; g.nblk = p.nblk; g.bps = p.bps; g.mt = p.mt; g.ct = p.ct;
   g.vec_d = ((uintptr_t)D % 16 == 0) && (d_bs % 4 == 0) && (Wo % 4 == 0);
   const int grid = p.splits * p.mt * p.ct;
   with_half([&](auto* t_) {
     using T16 = std::remove_pointer_t<decltype(t_)>;
-    if (KH == 3 && stride == 2) wc_launch<T16, 3, 2>(g, grid, st);
-    else if (KH == 3 && stride == 1) wc_launch<T16, 3, 1>(g, grid, st);
-    else if (KH == 4 && stride == 2) wc_launch<T16, 4, 2>(g, grid, st);
-    else wc_launch<T16, 4, 1>(g, grid, st);
+    if (KH == 3 && stride == 2) wc_launch<T16, 3, 2>(g, grid, xh, st);
+    else if (KH == 3 && stride == 1) wc_launch<T16, 3, 1>(g, grid, xh, st);
+    else if (KH == 4 && stride == 2) wc_launch<T16, 4, 2>(g, grid, xh, st);
+    else wc_launch<T16, 4, 1>(g, grid, xh, st);
   });
   DSG_CHECK_LAUNCH();
   const long total4 = (long)KH * KW * M * C / 4;
@@ -356,6 +384,20 @@ int dsgan_wconv(const float* D, long d_bs, const float* X, long x_bs, float* dw,
   hipLaunchKernelGGL(wconv_reduce_kernel, dim3((unsigned)blocks), dim3(256), 0, st, ws, p.splits, KH * KW, M, C, dw);
   DSG_CHECK_LAUNCH();
   return 0;
+}
+
+extern "C" {
+
+int dsgan_wconv(const float* D, long d_bs, const float* X, long x_bs, float* dw, float* ws, int nb, int C, int M,
+                int H, int W, int Ho, int Wo, int KH, int KW, int stride, int pad, hipStream_t st) {
+  return wconv_impl(D, d_bs, X, x_bs, false, dw, ws, nb, C, M, H, W, Ho, Wo, KH, KW, stride, pad, st);
+}
+
+// Same with X in the library's 16-bit half type (x_bs in elements; rows 8-byte aligned): the
+// ConvTranspose weight-grad on dsgan_instnorm_bwd_h's output.
+int dsgan_wconv_xh(const float* D, long d_bs, const void* Xh, long x_bs, float* dw, float* ws, int nb, int C, int M,
+                   int H, int W, int Ho, int Wo, int KH, int KW, int stride, int pad, hipStream_t st) {
+  return wconv_impl(D, d_bs, Xh, x_bs, true, dw, ws, nb, C, M, H, W, Ho, Wo, KH, KW, stride, pad, st);
 }
 
 }  // extern "C"

@@ -67,11 +67,13 @@ SIGNATURES = {
     "dsgan_wconv_supported": [I, I, I, I],
     "dsgan_wconv_workspace": [I, I, I, I, I, I, I],
     "dsgan_wconv": [P, L, P, L, P, P] + [I] * 11 + [S],
+    "dsgan_wconv_xh": [P, L, P, L, P, P] + [I] * 11 + [S],
     # tconv.hip
     "dsgan_conv_wtrans": [P, P, I, I, I, I, I, I, I, I, I, S],
     "dsgan_tconv": [P, L, P, P, P, L, P, L] + [I] * 9 + [P, P] + [I] * 7 + [F, S],
     "dsgan_tconv_workspace": [I] * 6,
     "dsgan_tconv_ws": [P, L, P, P, P, L, P, L] + [I] * 9 + [P, P] + [I] * 7 + [F, I, P, S],
+    "dsgan_tconv_ws_xh": [P, L, P, P, P, L, P, L] + [I] * 9 + [P, P] + [I] * 7 + [F, P, S],
     # skinny.hip
     "dsgan_conv_small_out": [P, L, P, L, L, L, L, P, P, L] + [I] * 13 + [S],
     "dsgan_conv_small_in": [P, L, P, L, L, L, L, P, P, L] + [I] * 13 + [F, I, S],
@@ -95,6 +97,7 @@ SIGNATURES = {
     "dsgan_instnorm_fwd": [P, L, P, P, L, P, L, P, P, I, I, I, I, F, F, S],
     "dsgan_instnorm_fwd_bf16": [P, L, P, L, P, P, I, I, I, F, S],
     "dsgan_instnorm_bwd": [P, L, P, L, P, P, L, P, P, P, L, P, L, P, I, I, I, I, F, F, S],
+    "dsgan_instnorm_bwd_h": [P, L, P, L, P, L, P, P, P, L, P, P, L, I, I, I, I, F, F, S],
     "dsgan_maxpool_fwd": [P, L, P, L, P, I, I, I, I, I, S],
     "dsgan_maxpool_bwd": [P, L, P, P, L, I, I, I, I, I, I, S],
     "dsgan_plane_stats": [P, L, P, P, P, I, I, I, S],

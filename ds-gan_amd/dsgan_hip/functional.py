@@ -1242,6 +1242,114 @@ def instance_norm_cat(x, skip, act=None):
     return InstanceNormCatFn.apply(x, skip, act)
 
 
+class ConvTNormFn(torch.autograd.Function):
+    """ConvTranspose2d 3x3/s2 (pad 1, output_padding 1) feeding the decoder InstanceNorm:
+    cat(act(IN(convT(x))), skip) (upSample, MixConvNeXtML.py:48-66) or act(IN(convT(x)) + res)
+    (OriginMLKA tail, :150-152).  The forward is ConvT3s2Fn's then InstanceNorm(Cat)Fn's.  The
+    backward keeps the ConvT output grad off fp32: dsgan_instnorm_bwd_h stores it in the 16-bit
+    half type with its per-plane sums, the ConvT data-grad (dsgan_tconv_ws_xh) and weight-grad
+    (dsgan_wconv_xh) read those 16 bits as MFMA operands -- exactly the values the fp32-input forms
+    round to on load, so dx and dW are unchanged -- and the bias grad is the sum over images of
+    the plane sums (the fp32 values, as channel_sum of the fp32 grad would add them)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, other, act, cat):
+        N, Ci, Hi, Wi = x.shape
+        Co = w.shape[1]
+        t = conv_dgrad_raw(x, w, (N, Co, 2 * Hi, 2 * Wi), 2, 1, bias=b)
+        if cat:
+            out = _empty(N, Co + other.shape[1], 2 * Hi, 2 * Wi, t)
+            _, mean, rstd = instnorm_raw(t, None, None, act, out=out[:, :Co])
+            copy_into(out[:, Co:], other)
+            ctx.save_for_backward(x, w, t, mean, rstd)
+        else:
+            out, mean, rstd = instnorm_raw(t, None, other, act)
+            ctx.save_for_backward(x, w, t, mean, rstd, other)
+        ctx.prec, ctx.act, ctx.cat, ctx.has_b = _state["prec"], act, cat, b is not None
+        ctx.w_ref, ctx.b_ref = w, b
+        ctx.box_x, ctx.box_o = _box(x), _box(other)
+        return out
+
+    @staticmethod
+    def backward(ctx, dy):
+        with precision(ctx.prec):
+            return ConvTNormFn._backward(ctx, dy)
+
+    @staticmethod
+    def _backward(ctx, dy):
+        import ctypes
+        if ctx.cat:
+            x, w, t, mean, rstd = ctx.saved_tensors
+            res = None
+        else:
+            x, w, t, mean, rstd, res = ctx.saved_tensors
+        N, Ci, Hi, Wi = x.shape
+        Co, H, W = t.shape[1], t.shape[2], t.shape[3]
+        HW = H * W
+        dyt, dybs = nchw(dy[:, :Co] if ctx.cat else dy)
+        t4, tbs = nchw(t)
+        rbs = 0
+        if res is not None:
+            res, rbs = nchw(res)
+        want_dres = res is not None and ctx.needs_input_grad[3]
+        dres = _empty(N, Co, H, W, t) if want_dres else None
+        dth = torch.empty((N, Co, H, W), device=t.device, dtype=half_dtype())
+        psum = torch.empty(N * Co, device=t.device, dtype=torch.float32)
+        e0 = AUX_TIMER.begin()
+        call("dsgan_instnorm_bwd_h", ptr(dyt), dybs, ptr(t4), tbs, ptr(res), rbs, ptr(mean), ptr(rstd), ptr(dth),
+             Co * HW, ptr(psum), ptr(dres), Co * HW, N, Co, HW, ACT[ctx.act], LRELU_SLOPE, IN_EPS, stream())
+        AUX_TIMER.end(e0, 0.0, ("in_bwd_h", N, Co, H, W, ctx.act, res is not None), "instnorm",
+                      _nb(dyt, t4, res, dres) + _nb(dth))
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = _empty(N, Ci, Hi, Wi, x)
+            taps = [(kh - 1, kw - 1) for kh in range(3) for kw in range(3)]
+            dh = (ctypes.c_int * 9)(*[q[0] for q in taps])
+            dw = (ctypes.c_int * 9)(*[q[1] for q in taps])
+            nws = _lib.load().dsgan_tconv_workspace(N, Co, Ci, Hi, Wi, 9)
+            ws = torch.empty(nws, device=t.device, dtype=torch.float32) if nws > 0 else None
+            e0 = IGEMM_TIMER.begin()
+            call("dsgan_tconv_ws_xh", ptr(dth), Co * HW, ptr(_wtrans_bf16(w, 0)), None, ptr(dx), Ci * Hi * Wi, None,
+                 0, N, Co, Ci, H, W, Hi, Wi, 2, 9, ctypes.cast(dh, ctypes.c_void_p), ctypes.cast(dw, ctypes.c_void_p),
+                 Hi, Wi, 1, 0, 0, 0, 0, LRELU_SLOPE, ptr(ws), stream())
+            IGEMM_TIMER.end(e0, _conv_flops(N, Co, Ci, 3, 3, Hi, Wi), ("fwd", N, Co, H, W, Ci, 3, 2), "tconv_kernel",
+                            _nb(dth, dx) + 2.0 * w.numel())
+        gw = _grad_buf(ctx.w_ref) if ctx.needs_input_grad[1] else None
+        if gw is not None:
+            x4, xbs = nchw(x)
+            ws = torch.empty(_lib.load().dsgan_wconv_workspace(N, Co, Ci, Hi, Wi, 3, 3), device=t.device,
+                             dtype=torch.float32)
+            e0 = IGEMM_TIMER.begin()
+            call("dsgan_wconv_xh", ptr(x4), xbs, ptr(dth), Co * HW, ptr(gw), ptr(ws), N, Co, Ci, H, W, Hi, Wi, 3, 3,
+                 2, 1, stream())
+            IGEMM_TIMER.end(e0, _conv_flops(N, Co, Ci, 3, 3, Hi, Wi), ("wgrad", N, Co, H, W, Ci, 3, 2), "wconv_kernel",
+                            _nb(x4, dth, gw))
+        gb = _grad_buf(ctx.b_ref) if (ctx.has_b and ctx.needs_input_grad[2]) else None
+        if gb is not None:
+            channel_sum_raw(psum.view(N, Co, 1, 1), gb)
+        _params_done(ctx.w_ref, ctx.b_ref)
+        dother = _give(ctx.box_o, dy[:, Co:]) if ctx.cat else _give(ctx.box_o, dres)
+        return _give(ctx.box_x, dx), None, None, dother, None, None
+
+
+def _convt_norm_fused(x, w, other, cat):
+    """The fused ConvT + InstanceNorm backward's conditions: 16-bit operands (bf16 / fp16 mode),
+    K (ConvT output channels) % 32 for the 16-bit-operand kernels, float4-aligned planes."""
+    N, Ci, Hi, Wi = x.shape
+    Co = w.shape[1]
+    HW = 4 * Hi * Wi
+    return (_is16() and w.dim() == 4 and w.shape[2] == 3 and w.shape[3] == 3 and Co % 32 == 0 and Ci % 32 == 0
+            and HW % 4 == 0 and (2 * Wi) % 4 == 0 and bool(_lib.load().dsgan_wconv_supported(Co, 3, 3, 2)))
+
+
+def convt_norm(x, w, b, other, act=None, cat=False):
+    """cat(act(IN(ConvT3s2(x))), other) if cat else act(IN(ConvT3s2(x)) + other) (other may be None)."""
+    if _convt_norm_fused(x, w, other, cat):
+        return ConvTNormFn.apply(x, w, b, other, act, cat)
+    y = conv_transpose3s2(x, w, b)
+    return instance_norm_cat(y, other, act) if cat else instance_norm(y, act, other)
+
+
 # ------------------------------------------------------------------------------------------
 # MaxPool2d(k) with int32 plane-flat argmax
 # ------------------------------------------------------------------------------------------

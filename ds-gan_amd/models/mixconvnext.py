@@ -32,7 +32,7 @@ class upSample(nn.Module):
 
     def forward(self, x, feature_map):
         t = self.model[0]
-        return HF.instance_norm_cat(HF.conv_transpose3s2(x, t.weight, t.bias), feature_map, act="gelu")
+        return HF.convt_norm(x, t.weight, t.bias, feature_map, act="gelu", cat=True)
 
 
 class MidMLKA(nn.Module):
@@ -103,7 +103,7 @@ class OriginMLKA(nn.Module):
         sc = HF.instance_norm(HF.conv2d(x, self.shortcut[0].weight))
         t = self.up4[0]
         # GELU(IN(up4(u3)) + IN(shortcut(x))): the add and GELU are fused into the second IN
-        return HF.instance_norm(HF.conv_transpose3s2(u3, t.weight, t.bias), act="gelu", res=sc)
+        return HF.convt_norm(u3, t.weight, t.bias, sc, act="gelu")
 
 
 class Block(nn.Module):

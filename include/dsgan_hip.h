@@ -215,6 +215,13 @@ int dsgan_tconv_ws(const float* X, long x_bs, const float* Wt, const float* bias
                    int Wout, int stride, int ntaps, const int* dh, const int* dw, int Hdst, int Wdst,
                    int os, int ph, int pw, int act, int gact, float slope, int wt_bf16, float* ws,
                    hipStream_t stream);
+/* Same with X in the library's 16-bit half type (x_bs in elements) and the 16-bit Wt of
+ * dsgan_conv_wtrans_bf16: the ConvTranspose2d data-grad (MixConvNeXtML.py:53,149-152) on the
+ * 16-bit output grad of dsgan_instnorm_bwd_h -- the operand values the fp32 form rounds to on load. */
+int dsgan_tconv_ws_xh(const void* Xh, long x_bs, const void* Wt, const float* bias, float* Y, long y_bs,
+                      const float* gpre, long gpre_bs, int nb, int K, int M, int Hin, int Win, int Hout,
+                      int Wout, int stride, int ntaps, const int* dh, const int* dw, int Hdst, int Wdst,
+                      int os, int ph, int pw, int act, int gact, float slope, float* ws, hipStream_t stream);
 
 /* ---- patch-staged implicit-GEMM conv (pconv.hip): VGG16 3x3 s1 (DSGAN/models/vgg.py:15-24) fwd
  * and data-grad, PatchGAN 4x4 s2/s1 (DSGAN/models/networks.py:543-569) fwd and s1 data-grad ------
@@ -277,6 +284,12 @@ long dsgan_wconv_workspace(int nb, int C, int M, int Ho, int Wo, int KH, int KW)
 int dsgan_wconv(const float* D, long d_bs, const float* X, long x_bs, float* dw, float* ws, int nb,
                 int C, int M, int H, int W, int Ho, int Wo, int KH, int KW, int stride, int pad,
                 hipStream_t stream);
+/* Same with X in the library's 16-bit half type (x_bs in elements, rows 8-byte aligned), 3x3
+ * stride 2 only: the ConvTranspose2d weight-grad on dsgan_instnorm_bwd_h's output (two resident
+ * workgroups per CU; ws sized by dsgan_wconv_workspace, which covers both forms). */
+int dsgan_wconv_xh(const float* D, long d_bs, const void* Xh, long x_bs, float* dw, float* ws, int nb,
+                   int C, int M, int H, int W, int Ho, int Wo, int KH, int KW, int stride, int pad,
+                   hipStream_t stream);
 
 /* ---- depthwise conv (dwconv.hip): Block.dwconv :220, MidMLKA.X3..X9 :94-97 ----------------
  * y (+)= dwconv_KxK(x, w) + bias; flip = 1 with bias = NULL is the data-grad; accumulate adds into
@@ -314,6 +327,14 @@ int dsgan_instnorm_bwd(const float* dy, long dy_bs, const float* x, long x_bs, c
                        const float* res, long res_bs, const float* mean, const float* rstd,
                        float* dx, long dx_bs, float* dres, long dres_bs, float* dscale, int N,
                        int C, int HW, int act, float slope, float eps, hipStream_t stream);
+/* Backward with dx stored in the library's 16-bit half type (dxh, batch stride dxh_bs elements,
+ * 8-byte aligned) plus dxsum[n*C + c] = sum over the plane of the fp32 dx (nullable); no scale.
+ * The ConvTranspose2d that feeds each decoder InstanceNorm (upSample :61-66, OriginMLKA :150-152)
+ * reads dx only as 16-bit MFMA operands (dsgan_tconv_ws_xh, dsgan_wconv_xh) and its bias grad is
+ * sum_n dxsum.  HW % 4 == 0, float4-aligned planes. */
+int dsgan_instnorm_bwd_h(const float* dy, long dy_bs, const float* x, long x_bs, const float* res, long res_bs,
+                         const float* mean, const float* rstd, void* dxh, long dxh_bs, float* dxsum, float* dres,
+                         long dres_bs, int N, int C, int HW, int act, float slope, float eps, hipStream_t stream);
 /* y (bf16, round-to-nearest-even) = IN(x): Block.norm (MixConvNeXtML.py:221) whose only consumers
  * are the block's bf16-operand MLP GEMMs.  HW % 4 == 0, 16-byte aligned. */
 int dsgan_instnorm_fwd_bf16(const float* x, long x_bs, void* y, long y_bs, float* mean, float* rstd, int N,

@@ -845,6 +845,75 @@ def test_instance_norm_cat(shape):
     assert torch.equal(sd.grad.cpu(), sr.grad)
 
 
+@pytest.mark.parametrize("half", HALVES)
+@pytest.mark.parametrize("act,res", [("gelu", False), ("gelu", True), (None, True)])
+@pytest.mark.parametrize("N,C,H,W", [(2, 64, 16, 16), (1, 32, 64, 64), (2, 96, 32, 36), (1, 4, 256, 256)])
+def test_instnorm_bwd_h_is_rounded_fp32_backward(half, act, res, N, C, H, W):
+    """dsgan_instnorm_bwd_h: its 16-bit dx is the RNE rounding of dsgan_instnorm_bwd's fp32 dx
+    (bit for bit), dres is identical, dxsum the per-plane sum of the fp32 dx."""
+    from dsgan_hip import functional as HF
+    from dsgan_hip._lib import call, ptr, stream
+    HF.set_precision(half)
+    g = torch.Generator().manual_seed(C + H)
+    x = (torch.randn(N, C, H, W, generator=g) * 2 + 0.3).to(DEV)
+    dy = torch.randn(N, C, H, W, generator=g).to(DEV)
+    r = torch.randn(N, C, H, W, generator=g).to(DEV) if res else None
+    _, mean, rstd = HF.instnorm_raw(x, None, r, act)
+    dx32, dres32, _ = HF.instnorm_bwd_raw(dy, x, None, r, mean, rstd, act, res, False)
+    dxh = torch.empty((N, C, H, W), device=DEV, dtype=_hdt(half))
+    dsum = torch.empty(N * C, device=DEV)
+    dres = torch.empty_like(x) if res else None
+    HW = H * W
+    call("dsgan_instnorm_bwd_h", ptr(dy), C * HW, ptr(x), C * HW, ptr(r), C * HW, ptr(mean), ptr(rstd), ptr(dxh),
+         C * HW, ptr(dsum), ptr(dres), C * HW, N, C, HW, HF.ACT[act], 0.2, 1e-5, stream())
+    torch.cuda.synchronize()
+    assert torch.equal(dxh.cpu(), dx32.to(_hdt(half)).cpu())
+    if res:
+        assert torch.equal(dres.cpu(), dres32.cpu())
+    ref = dx32.double().sum((2, 3)).flatten()
+    scale = dx32.double().abs().sum((2, 3)).flatten()
+    assert ((dsum.double() - ref).abs() <= 1e-6 * scale + 1e-30).all()
+
+
+@pytest.mark.parametrize("half", HALVES)
+@pytest.mark.parametrize("cat", [True, False])
+@pytest.mark.parametrize("N,Ci,Co,H", [(2, 128, 64, 16), (2, 256, 128, 8), (1, 1024, 512, 16), (2, 64, 32, 24)])
+def test_convt_norm_fused_matches_unfused(half, cat, N, Ci, Co, H):
+    """ConvTNormFn (16-bit ConvT output grad from the IN backward, tconv / wconv reading it as
+    16-bit operands) vs conv_transpose3s2 + instance_norm(_cat) (fp32 grad, rounded on load):
+    the same output bits; dx bitwise (same tconv tiles and K order on the same operand values);
+    dW to fp32 summation order (the 16-bit-X wconv plans twice the pixel splits); the bias grad
+    (the ConvT output grad sums to ~0 under the InstanceNorm) to the fp32 rounding of its sum."""
+    from dsgan_hip import functional as HF
+    HF.set_precision(half)
+    g = torch.Generator().manual_seed(Ci + Co + H + int(cat))
+    x = torch.randn(N, Ci, H, H, generator=g)
+    w = torch.randn(Ci, Co, 3, 3, generator=g) / math.sqrt(Ci * 9)
+    b = torch.randn(Co, generator=g) * 0.1
+    o = torch.randn(N, 48 if cat else Co, 2 * H, 2 * H, generator=g)
+    gy = torch.randn(N, Co + (48 if cat else 0), 2 * H, 2 * H, generator=g).to(DEV)
+    outs = []
+    for fused in (True, False):
+        xd, od, wd, bd = _leaf(x), _leaf(o), _param(w), _param(b)
+        if fused:
+            assert HF._convt_norm_fused(xd, wd, od, cat)
+            y = HF.ConvTNormFn.apply(xd, wd, bd, od, "gelu", cat)
+        else:
+            t = HF.conv_transpose3s2(xd, wd, bd)
+            y = HF.instance_norm_cat(t, od, "gelu") if cat else HF.instance_norm(t, "gelu", od)
+        y.backward(gy)
+        torch.cuda.synchronize()
+        outs.append((y.detach().cpu(), xd.grad.cpu(), wd.grad.cpu(), bd.grad.cpu(), od.grad.cpu()))
+    (y1, dx1, dw1, db1, do1), (y2, dx2, dw2, db2, do2) = outs
+    assert torch.equal(y1, y2)
+    assert torch.equal(dx1, dx2)
+    assert torch.equal(do1, do2)
+    assert rel(dw1, dw2) < 1e-5
+    # |bias grad| ~ fp32 rounding of a near-cancelling sum: bar on the scale of the summands
+    t_scale = gy[:, :Co].abs().double().sum((0, 2, 3)).cpu()
+    assert ((db1.double() - db2.double()).abs() <= 1e-5 * t_scale).all()
+
+
 @pytest.mark.parametrize("w_bf16,x_bf16", [(0, 0), (1, 1), (1, 0)])
 @pytest.mark.parametrize("M,K,P,nb", [(2048, 512, 4096, 2), (1024, 256, 1024, 3), (256, 64, 256, 2), (4096, 1024, 1024, 1),
                                       (96, 40, 256, 2)])
