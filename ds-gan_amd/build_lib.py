@@ -26,6 +26,19 @@ FLAGS = ["-O3", "-fPIC", "-std=c++17", "--offload-arch=" + ARCH, "-Wno-unused-re
 EXTRA = {"dwconv.hip": ["-fno-slp-vectorize"], "mlp.hip": ["-fno-slp-vectorize"], "thin3.hip": ["-fno-slp-vectorize"]}
 
 
+def _includes(path, seen=None):
+    """The csrc headers a source pulls in (transitively, quoted includes only)."""
+    seen = set() if seen is None else seen
+    import re
+    with open(path) as f:
+        for m in re.finditer(r'^\s*#\s*include\s+"([^"]+)"', f.read(), re.M):
+            h = os.path.join(CSRC, m.group(1))
+            if os.path.exists(h) and h not in seen:
+                seen.add(h)
+                _includes(h, seen)
+    return seen
+
+
 def _newer(src, obj, headers):
     if not os.path.exists(obj):
         return True
@@ -44,13 +57,12 @@ def _compile(src, obj):
 def build(jobs=8, force=False, verbose=True):
     os.makedirs(OBJ_DIR, exist_ok=True)
     os.makedirs(OUT_DIR, exist_ok=True)
-    headers = glob.glob(os.path.join(CSRC, "*.h"))
     srcs = sorted(glob.glob(os.path.join(CSRC, "*.hip")) + glob.glob(os.path.join(CSRC, "*.cpp")))
     objs, todo = [], []
     for s in srcs:
         o = os.path.join(OBJ_DIR, os.path.basename(s) + ".o")
         objs.append(o)
-        if force or _newer(s, o, headers):
+        if force or _newer(s, o, _includes(s)):
             todo.append((s, o))
     if todo:
         with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:

@@ -24,11 +24,14 @@ struct PwArgs {
   const float* gpre; long gpre_bs;
   int M, N, K, P;
   int act, gact, bact, accumulate; float slope;
-  int k_split;
-  float* ws;                   // WGRAD with splits > 1: partials [split][M][N]
+  int k_split;                 // K per split (WGRAD: always; FWD/DGRAD: 0 = unsplit)
+  float* ws;                   // splits > 1: fp32 partials -- WGRAD [split][M][N]; FWD/DGRAD
+                               // [split][b][M][P] (raw accumulators, pw_split_finish_kernel applies
+                               // the epilogue)
   unsigned a_range, b_range;   // buffer-resource byte ranges of A and B (B: per image for FWD/DGRAD)
   int y_bf16;  // FWD: Y is bf16 [b][M][P] (y_bs in elements)
   int gbf;     // FWD: ypre is bf16 and receives act'(pre);  DGRAD: gpre is a bf16 multiplier (no act')
+  int bk64;    // host planner: 128 / 64-row tiles with 64-deep K steps (else 32)
   float* asum; // WGRAD (nullable): db[m] += sum_k A[m][k] -- the bias grad of the layer whose output
                // grad is A, from the staged A tiles (split partials after the S*M*N weight partials)
 };
@@ -110,7 +113,7 @@ __global__ __launch_bounds__(128 * WN, WN == 2 ? 2 : 1) void pwgemm_kernel(PwArg
   const int m0 = m_t * BM, n0 = n_t * BN;
 
   int kbeg = 0, kend = g.K;
-  if (MODE == PW_WGRAD) { kbeg = split * g.k_split; kend = min(g.K, kbeg + g.k_split); }
+  if (g.k_split > 0) { kbeg = split * g.k_split; kend = min(g.K, kbeg + g.k_split); }
   if (kbeg >= kend) return;
   const int nk = (kend - kbeg + BK - 1) / BK;
 
@@ -279,7 +282,7 @@ __global__ __launch_bounds__(128 * WN, WN == 2 ? 2 : 1) void pwgemm_kernel(PwArg
 
   // ---- accumulators (bias folded into the init for FWD) ----
   pf32x16 acc[TM][TN];
-  const bool has_bias = MODE == PW_FWD && g.bias != nullptr;
+  const bool has_bias = MODE == PW_FWD && g.bias != nullptr && g.ws == nullptr;
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
     float bv[16];
@@ -385,18 +388,26 @@ __global__ __launch_bounds__(128 * WN, WN == 2 ? 2 : 1) void pwgemm_kernel(PwArg
   // channel: lane lr holds channel mrow + lr, register 4q + e pixel col0 + 8q + 4lh + e -- fp32
   // side tensors move as one 16-byte access per group q, 16-bit ones as 8-byte loads and, paired
   // by v_permlane32_swap, two 16-byte stores per tile (cdna_hip_programming.md T21).
+  // A split-K partial (g.ws) stores the raw fp32 accumulator into its split's [b][M][P] slab; the
+  // bias, activation, side tensors and accumulation are pw_split_finish_kernel's.
+  const bool part = g.ws != nullptr;
+  float* const ybase = part ? g.ws + (long)split * g.M * g.N : g.Y;
+  const long ybs = part ? (long)g.M * g.P : g.y_bs;
+  const float* const gpre = part ? nullptr : g.gpre;
+  float* const ypre = part ? nullptr : g.ypre;
+  const int act = part ? 0 : g.act, accumulate = part ? 0 : g.accumulate, y_bf16 = part ? 0 : g.y_bf16;
   const unsigned range = (unsigned)(((long)g.M * g.P - p0) * 4);
   const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(g.Y + (long)bimg * g.y_bs + p0), (short)0, range, 0x00020000);
+      (void*)(ybase + (long)bimg * ybs + p0), (short)0, range, 0x00020000);
   const __amdgpu_buffer_rsrc_t ryh = __builtin_amdgcn_make_buffer_rsrc(
       (void*)((T16*)g.Y + (long)bimg * g.y_bs + p0), (short)0, range / 2, 0x00020000);
   __amdgpu_buffer_rsrc_t rp = ry, rg = ry;
   // bf16 side tensors (gbf): same element offsets, byte offsets halved
   const int esz = g.gbf ? 2 : 4;
-  if (g.ypre) rp = __builtin_amdgcn_make_buffer_rsrc((void*)((char*)g.ypre + ((long)bimg * g.ypre_bs + p0) * esz), (short)0,
-                                                     g.gbf ? range / 2 : range, 0x00020000);
-  if (g.gpre) rg = __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)g.gpre + ((long)bimg * g.gpre_bs + p0) * esz),
-                                                     (short)0, g.gbf ? range / 2 : range, 0x00020000);
+  if (ypre) rp = __builtin_amdgcn_make_buffer_rsrc((void*)((char*)ypre + ((long)bimg * g.ypre_bs + p0) * esz), (short)0,
+                                                   g.gbf ? range / 2 : range, 0x00020000);
+  if (gpre) rg = __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)gpre + ((long)bimg * g.gpre_bs + p0) * esz),
+                                                   (short)0, g.gbf ? range / 2 : range, 0x00020000);
   // 16-bit store of this lane's 16 values: groups (q, q+1) swap halves so lanes 0-31 hold pixels
   // 8q..8q+7 and lanes 32-63 pixels 8q+8..8q+15 of their channel (byte offset +16)
   auto store16 = [&](__amdgpu_buffer_rsrc_t r, const float* v, int vh, int srow) __attribute__((always_inline)) {
@@ -431,7 +442,7 @@ __global__ __launch_bounds__(128 * WN, WN == 2 ? 2 : 1) void pwgemm_kernel(PwArg
         float v[16];
 #pragma unroll
         for (int r = 0; r < 16; ++r) v[r] = acc[i][j][r];
-        if (g.gpre && g.gbf) {          // DGRAD: v *= gp, gp = act'(pre) stored 16-bit by the forward
+        if (gpre && g.gbf) {          // DGRAD: v *= gp, gp = act'(pre) stored 16-bit by the forward
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
             const auto u = __builtin_amdgcn_raw_buffer_load_b64(rg, v2, s2 + 16 * q, 0);
@@ -440,7 +451,7 @@ __global__ __launch_bounds__(128 * WN, WN == 2 ? 2 : 1) void pwgemm_kernel(PwArg
             v[4 * q + 2] *= h2f<T16>((unsigned short)(u[1] & 0xffffu));
             v[4 * q + 3] *= h2f<T16>((unsigned short)(u[1] >> 16));
           }
-        } else if (g.gpre) {
+        } else if (gpre) {
           float gv[16];
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
@@ -450,9 +461,9 @@ __global__ __launch_bounds__(128 * WN, WN == 2 ? 2 : 1) void pwgemm_kernel(PwArg
           act_g_mul_arr(g.gact, v, gv, g.slope);
         }
         bool acted = false;
-        if (g.ypre && g.gbf) {          // FWD: ypre <- 16-bit act'(pre), v <- act(pre) (one GELU evaluation)
+        if (ypre && g.gbf) {          // FWD: ypre <- 16-bit act'(pre), v <- act(pre) (one GELU evaluation)
           float apv[16];
-          if (g.act == ACT_GELU) {
+          if (act == ACT_GELU) {
 #pragma unroll
             for (int r = 0; r < 16; r += 2) {
               f32x2 a, ap;
@@ -463,13 +474,13 @@ __global__ __launch_bounds__(128 * WN, WN == 2 ? 2 : 1) void pwgemm_kernel(PwArg
           } else {
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
-              apv[r] = act_g(g.act, v[r], g.slope);
-              v[r] = act_f(g.act, v[r], g.slope);
+              apv[r] = act_g(act, v[r], g.slope);
+              v[r] = act_f(act, v[r], g.slope);
             }
           }
           store16(rp, apv, vh, s2);
           acted = true;
-        } else if (g.ypre) {
+        } else if (ypre) {
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
             const pu32x4 o = {__builtin_bit_cast(unsigned, v[4 * q]), __builtin_bit_cast(unsigned, v[4 * q + 1]),
@@ -477,15 +488,15 @@ __global__ __launch_bounds__(128 * WN, WN == 2 ? 2 : 1) void pwgemm_kernel(PwArg
             __builtin_amdgcn_raw_buffer_store_b128(o, rp, v4, s4 + 32 * q, 0);
           }
         }
-        if (!acted) act_f_arr(g.act, v, g.slope);
-        if (g.accumulate) {
+        if (!acted) act_f_arr(act, v, g.slope);
+        if (accumulate) {
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
             const float4 u = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(ry, v4, s4 + 32 * q, 0));
             v[4 * q] += u.x; v[4 * q + 1] += u.y; v[4 * q + 2] += u.z; v[4 * q + 3] += u.w;
           }
         }
-        if (g.y_bf16) {   // 16-bit output: same rows, half the byte offsets
+        if (y_bf16) {   // 16-bit output: same rows, half the byte offsets
           store16(ryh, v, vh, s2);
           continue;
         }
@@ -516,14 +527,14 @@ __global__ __launch_bounds__(128 * WN, WN == 2 ? 2 : 1) void pwgemm_kernel(PwArg
         float v[16];
 #pragma unroll
         for (int r = 0; r < 16; ++r) v[r] = acc[i][j][r];
-        if (g.gpre && g.gbf) {          // DGRAD: v *= gp, gp = act'(pre) stored bf16 by the forward
+        if (gpre && g.gbf) {          // DGRAD: v *= gp, gp = act'(pre) stored bf16 by the forward
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
             const unsigned short hb = __builtin_amdgcn_raw_buffer_load_b16(
                 rg, vrow[r] == (int)PW_OOB ? (int)PW_OOB : vrow[r] / 2, (mrow + (r & 3) + 8 * (r >> 2)) * (P4 / 2), 0);
             v[r] *= h2f<T16>(hb);
           }
-        } else if (g.gpre) {
+        } else if (gpre) {
           float gv[16];
 #pragma unroll
           for (int r = 0; r < 16; ++r)
@@ -532,9 +543,9 @@ __global__ __launch_bounds__(128 * WN, WN == 2 ? 2 : 1) void pwgemm_kernel(PwArg
           act_g_mul_arr(g.gact, v, gv, g.slope);
         }
         bool acted = false;
-        if (g.ypre && g.gbf) {          // FWD: ypre <- bf16 act'(pre), v <- act(pre) (one GELU evaluation)
+        if (ypre && g.gbf) {          // FWD: ypre <- bf16 act'(pre), v <- act(pre) (one GELU evaluation)
           float apv[16];
-          if (g.act == ACT_GELU) {
+          if (act == ACT_GELU) {
 #pragma unroll
             for (int r = 0; r < 16; r += 2) {
               f32x2 a, ap;
@@ -545,8 +556,8 @@ __global__ __launch_bounds__(128 * WN, WN == 2 ? 2 : 1) void pwgemm_kernel(PwArg
           } else {
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
-              apv[r] = act_g(g.act, v[r], g.slope);
-              v[r] = act_f(g.act, v[r], g.slope);
+              apv[r] = act_g(act, v[r], g.slope);
+              v[r] = act_f(act, v[r], g.slope);
             }
           }
 #pragma unroll
@@ -555,20 +566,20 @@ __global__ __launch_bounds__(128 * WN, WN == 2 ? 2 : 1) void pwgemm_kernel(PwArg
                                                   vrow[r] == (int)PW_OOB ? (int)PW_OOB : vrow[r] / 2,
                                                   (mrow + (r & 3) + 8 * (r >> 2)) * (P4 / 2), 0);
           acted = true;
-        } else if (g.ypre) {
+        } else if (ypre) {
 #pragma unroll
           for (int r = 0; r < 16; ++r)
             __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v[r]), rp, vrow[r],
                                                   (mrow + (r & 3) + 8 * (r >> 2)) * P4, 0);
         }
-        if (!acted) act_f_arr(g.act, v, g.slope);
-        if (g.accumulate) {
+        if (!acted) act_f_arr(act, v, g.slope);
+        if (accumulate) {
 #pragma unroll
           for (int r = 0; r < 16; ++r)
             v[r] += __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
                         ry, vrow[r], (mrow + (r & 3) + 8 * (r >> 2)) * P4, 0));
         }
-        if (g.y_bf16) {   // bf16 output: same rows, half the byte offsets
+        if (y_bf16) {   // bf16 output: same rows, half the byte offsets
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
             const unsigned short hb = f2h<T16>(v[r]);
@@ -598,15 +609,16 @@ constexpr int PW_WIDE = -1;   // tile selector: 256 x 256 tiles, 8 waves, 64-dee
 
 // FWD / DGRAD launch over (tile rows, bf16 weight, bf16 activation, 16-bit output)
 template <typename T16, int MODE, int SWP>
-static void pw_launch_abs(const PwArgs& g, int bm, int abf, int bbf, hipStream_t st) {
+static void pw_launch_abs(const PwArgs& g, int bm, int abf, int bbf, int splits, hipStream_t st) {
   const int sel = (abf ? 2 : 0) + (bbf ? 1 : 0);
-#define PW_AB(BM)                                                      \
+#define PW_AB_K(BM, BK)                                                \
   switch (sel) {                                                       \
-    case 0: pw_launch<T16, MODE, BM, 0, 0, 128, 2, PBK, SWP>(g, 1, st); break;                \
-    case 1: pw_launch<T16, MODE, BM, 0, 1, 128, 2, PBK, SWP>(g, 1, st); break;                \
-    case 2: pw_launch<T16, MODE, BM, 1, 0, 128, 2, PBK, SWP>(g, 1, st); break;                \
-    default: pw_launch<T16, MODE, BM, 1, 1, 128, 2, PBK, SWP>(g, 1, st); break;               \
+    case 0: pw_launch<T16, MODE, BM, 0, 0, 128, 2, BK, SWP>(g, splits, st); break;                \
+    case 1: pw_launch<T16, MODE, BM, 0, 1, 128, 2, BK, SWP>(g, splits, st); break;                \
+    case 2: pw_launch<T16, MODE, BM, 1, 0, 128, 2, BK, SWP>(g, splits, st); break;                \
+    default: pw_launch<T16, MODE, BM, 1, 1, 128, 2, BK, SWP>(g, splits, st); break;               \
   }
+#define PW_AB(BM) if (g.bk64 && BM <= 128) { PW_AB_K(BM, 64) } else { PW_AB_K(BM, PBK) }
 #define PW_ABW                                                                    \
   switch (sel) {                                                                  \
     case 0: pw_launch<T16, MODE, 128, 0, 0, 128, 2, PBK, SWP>(g, 1, st); break;  /* (not selected) */  \
@@ -616,12 +628,90 @@ static void pw_launch_abs(const PwArgs& g, int bm, int abf, int bbf, hipStream_t
   }
   if (bm == PW_WIDE) { PW_ABW } else if (bm == 256) { PW_AB(256) } else if (bm == 128) { PW_AB(128) } else { PW_AB(64) }
 #undef PW_AB
+#undef PW_AB_K
 #undef PW_ABW
 }
+
+// Finishing pass of a split-K FWD / DGRAD launch: y = epilogue(sum_s ws[s], s = 0..S-1 in order),
+// the kernel epilogue's operations in the same order (bias; DGRAD: * act'(gpre) or * 16-bit gp;
+// FWD: 16-bit act'(pre) / fp32 pre-activation to ypre, then act; accumulate; fp32 or 16-bit store),
+// four consecutive pixels of one (image, channel) row per thread (P % 4 == 0).
+template <typename T16>
+__global__ __launch_bounds__(256) void pw_split_finish_kernel(PwArgs g, int S, int mode) {
+  const long MN = (long)g.M * g.N, n4 = MN >> 2;
+  for (long q = blockIdx.x * 256L + threadIdx.x; q < n4; q += (long)gridDim.x * 256) {
+    const long e = q << 2;
+    float4 a = *reinterpret_cast<const float4*>(g.ws + e);
+    for (int s = 1; s < S; ++s) {
+      const float4 u = *reinterpret_cast<const float4*>(g.ws + (long)s * MN + e);
+      a.x += u.x; a.y += u.y; a.z += u.z; a.w += u.w;
+    }
+    float v[4] = {a.x, a.y, a.z, a.w};
+    const long bm = e / g.P;
+    const int p = (int)(e - bm * g.P), m = (int)(bm % g.M), b = (int)(bm / g.M);
+    const long off = (long)m * g.P + p;
+    if (mode == PW_FWD && g.bias) {
+      const float bv = g.bias[m];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] += bv;
+    }
+    if (mode == PW_DGRAD && g.gpre) {
+      if (g.gbf) {
+        const uint2 u = *reinterpret_cast<const uint2*>((const T16*)g.gpre + (long)b * g.gpre_bs + off);
+        v[0] *= h2f<T16>((unsigned short)(u.x & 0xffffu)); v[1] *= h2f<T16>((unsigned short)(u.x >> 16));
+        v[2] *= h2f<T16>((unsigned short)(u.y & 0xffffu)); v[3] *= h2f<T16>((unsigned short)(u.y >> 16));
+      } else {
+        const float4 u = *reinterpret_cast<const float4*>(g.gpre + (long)b * g.gpre_bs + off);
+        const float gv[4] = {u.x, u.y, u.z, u.w};
+        act_g_mul_arr(g.gact, v, gv, g.slope);
+      }
+    }
+    if (mode == PW_FWD) {
+      if (g.ypre && g.gbf) {
+        float apv[4];
+        if (g.act == ACT_GELU) {
+#pragma unroll
+          for (int r = 0; r < 4; r += 2) {
+            f32x2 ga, gpa;
+            gelu_pair_fast2(f32x2{v[r], v[r + 1]}, ga, gpa);
+            v[r] = ga.x; v[r + 1] = ga.y; apv[r] = gpa.x; apv[r + 1] = gpa.y;
+          }
+        } else {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) { apv[r] = act_g(g.act, v[r], g.slope); v[r] = act_f(g.act, v[r], g.slope); }
+        }
+        *reinterpret_cast<uint2*>((T16*)g.ypre + (long)b * g.ypre_bs + off) =
+            make_uint2((unsigned)f2h<T16>(apv[0]) | ((unsigned)f2h<T16>(apv[1]) << 16),
+                       (unsigned)f2h<T16>(apv[2]) | ((unsigned)f2h<T16>(apv[3]) << 16));
+      } else {
+        if (g.ypre) *reinterpret_cast<float4*>(g.ypre + (long)b * g.ypre_bs + off) = make_float4(v[0], v[1], v[2], v[3]);
+        act_f_arr(g.act, v, g.slope);
+      }
+    }
+    if (g.y_bf16) {
+      *reinterpret_cast<uint2*>((T16*)g.Y + (long)b * g.y_bs + off) =
+          make_uint2((unsigned)f2h<T16>(v[0]) | ((unsigned)f2h<T16>(v[1]) << 16),
+                     (unsigned)f2h<T16>(v[2]) | ((unsigned)f2h<T16>(v[3]) << 16));
+    } else {
+      float4* o = reinterpret_cast<float4*>(g.Y + (long)b * g.y_bs + off);
+      if (g.accumulate) { const float4 y = *o; v[0] += y.x; v[1] += y.y; v[2] += y.z; v[3] += y.w; }
+      *o = make_float4(v[0], v[1], v[2], v[3]);
+    }
+  }
+}
+
 template <typename T16, int MODE>
-static void pw_launch_ab(const PwArgs& g, int bm, int abf, int bbf, hipStream_t st) {
-  if (g.y_bf16 || (g.ypre && g.gbf)) pw_launch_abs<T16, MODE, 1>(g, bm, abf, bbf, st);
-  else pw_launch_abs<T16, MODE, 0>(g, bm, abf, bbf, st);
+static void pw_launch_ab(const PwArgs& g, int bm, int abf, int bbf, int splits, hipStream_t st) {
+  if (splits > 1) {   // raw fp32 partials (the channel x pixel tile), then the finishing pass
+    pw_launch_abs<T16, MODE, 0>(g, bm, abf, bbf, splits, st);
+    const long n4 = (long)g.M * g.N / 4;
+    long blocks = (n4 + 255) / 256;
+    if (blocks > 4096) blocks = 4096;
+    hipLaunchKernelGGL((pw_split_finish_kernel<T16>), dim3((unsigned)blocks), dim3(256), 0, st, g, splits, MODE);
+    return;
+  }
+  if (g.y_bf16 || (g.ypre && g.gbf)) pw_launch_abs<T16, MODE, 1>(g, bm, abf, bbf, 1, st);
+  else pw_launch_abs<T16, MODE, 0>(g, bm, abf, bbf, 1, st);
 }
 
 // K (pixel) split of a weight-grad launch: about `target` workgroups (640 = 2.5 per CU for the
@@ -687,15 +777,16 @@ static int fd_tile(const PwArgs& g, bool any_bf16) {
 }
 
 
-// The two launch entry points of one 16-bit operand type (explicitly instantiated per type).
-template <typename T16>
-void pw_fd_launch(int mode, const PwArgs& g, int bm, int abf, int bbf, hipStream_t st) {
-  if (mode == PW_FWD) pw_launch_ab<T16, PW_FWD>(g, bm, abf, bbf, st);
-  else pw_launch_ab<T16, PW_DGRAD>(g, bm, abf, bbf, st);
+// Launch entry points per (16-bit operand type, mode), each explicitly instantiated in a
+// translation unit of its own (pw_{fwd,dgrad,wgrad}_{bf16,f16}.hip) so the six kernel families
+// compile in parallel.
+template <typename T16, int MODE>
+void pw_fd_launch_m(const PwArgs& g, int bm, int abf, int bbf, int splits, hipStream_t st) {
+  pw_launch_ab<T16, MODE>(g, bm, abf, bbf, splits, st);
 }
 template <typename T16>
 void pw_wgrad_launch(const PwArgs& g, int bm, int abf, int bbf, int splits, hipStream_t st) {
-  const int sel = (abf ? 2 : 0) + (bbf ? 1 : 0) + (bm == 128 ? 4 : bm == PW_WIDE ? 8 : 0);
+  const int sel = (abf ? 2 : 0) + (bbf ? 1 : 0) + (bm == 128 ? 4 : bm == PW_WIDE ? 8 : 0) + (g.bk64 && bm == 128 ? 16 : 0);
   switch (sel) {
     case 9: pw_launch<T16, PW_WGRAD, 256, 0, 1, 256, 4, 64>(g, splits, st); break;
     case 10: pw_launch<T16, PW_WGRAD, 256, 1, 0, 256, 4, 64>(g, splits, st); break;
@@ -707,8 +798,16 @@ void pw_wgrad_launch(const PwArgs& g, int bm, int abf, int bbf, int splits, hipS
     case 4: pw_launch<T16, PW_WGRAD, 128, 0, 0>(g, splits, st); break;
     case 5: pw_launch<T16, PW_WGRAD, 128, 0, 1>(g, splits, st); break;
     case 6: pw_launch<T16, PW_WGRAD, 128, 1, 0>(g, splits, st); break;
-    default: pw_launch<T16, PW_WGRAD, 128, 1, 1>(g, splits, st); break;
+    case 7: pw_launch<T16, PW_WGRAD, 128, 1, 1>(g, splits, st); break;
+    case 16 + 4: pw_launch<T16, PW_WGRAD, 128, 0, 0, 128, 2, 64>(g, splits, st); break;
+    case 16 + 5: pw_launch<T16, PW_WGRAD, 128, 0, 1, 128, 2, 64>(g, splits, st); break;
+    case 16 + 6: pw_launch<T16, PW_WGRAD, 128, 1, 0, 128, 2, 64>(g, splits, st); break;
+    default: pw_launch<T16, PW_WGRAD, 128, 1, 1, 128, 2, 64>(g, splits, st); break;
   }
 }
+#define PW_EXTERN_LAUNCHERS(T16)                                                                            \
+  extern template void pw_fd_launch_m<T16, PW_FWD>(const PwArgs&, int, int, int, int, hipStream_t);         \
+  extern template void pw_fd_launch_m<T16, PW_DGRAD>(const PwArgs&, int, int, int, int, hipStream_t);       \
+  extern template void pw_wgrad_launch<T16>(const PwArgs&, int, int, int, int, hipStream_t);
 
 }  // namespace dsg

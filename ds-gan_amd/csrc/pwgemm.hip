@@ -22,14 +22,57 @@
 
 namespace dsg {
 
-extern template void pw_fd_launch<_Float16>(int, const PwArgs&, int, int, int, hipStream_t);
-extern template void pw_wgrad_launch<_Float16>(const PwArgs&, int, int, int, int, hipStream_t);
-template void pw_fd_launch<__bf16>(int, const PwArgs&, int, int, int, hipStream_t);
-template void pw_wgrad_launch<__bf16>(const PwArgs&, int, int, int, int, hipStream_t);
+// the kernel instantiations live in pw_{fwd,dgrad,wgrad}_{bf16,f16}.hip
+PW_EXTERN_LAUNCHERS(__bf16)
+PW_EXTERN_LAUNCHERS(_Float16)
+template <typename T16>
+static void pw_fd_launch(int mode, const PwArgs& g, int bm, int abf, int bbf, int splits, hipStream_t st) {
+  if (mode == PW_FWD) pw_fd_launch_m<T16, PW_FWD>(g, bm, abf, bbf, splits, st);
+  else pw_fd_launch_m<T16, PW_DGRAD>(g, bm, abf, bbf, splits, st);
+}
 
-static void fd_dispatch(int mode, const PwArgs& g, int bm, int abf, int bbf, hipStream_t st) {
-  if (half_type() == HALF_F16) pw_fd_launch<_Float16>(mode, g, bm, abf, bbf, st);
-  else pw_fd_launch<__bf16>(mode, g, bm, abf, bbf, st);
+// Planner knobs, read by the host launchers only (tools/pw_bench.py flips them for in-process A/B):
+//   [0] FWD/DGRAD split-K on/off, [1] its target workgroup count, [2] split only launches of fewer
+//   tiles than this, [3] minimum K steps per split, [4] 64-deep K steps for the 128 / 64-row FWD /
+//   DGRAD tiles, [5] the same for the 128-row WGRAD tiles.
+static int g_tune[8] = {1, 512, 256, 4, 0, 0, 0, 0};
+
+// K split of an under-filled FWD / DGRAD launch (the 16^2 bottleneck layers: e.g. the downSkip 1x1
+// data-grads, 32-128 tiles of 32-64 K steps each, ~40 us at 0.5 TB/s): about g_tune[1] workgroups,
+// >= g_tune[3] K steps per split; partials [split][b][M][P] in ws, pw_split_finish_kernel adds them
+// in split order and applies the epilogue (deterministic).  128 / 64-row tiles only (the wide and
+// 256-row forms are chosen only for launches that fill the chip).
+static int fd_splits(const PwArgs& g, int bm, int bk, int* k_split) {
+  *k_split = 0;
+  if (!g_tune[0] || bm == PW_WIDE || bm == 256) return 1;
+  const long tiles = (long)((g.M + bm - 1) / bm) * (g.N / 128);
+  if (tiles >= g_tune[2]) return 1;
+  const int nkb = (g.K + bk - 1) / bk;
+  long S = (g_tune[1] + tiles - 1) / tiles;
+  if (S > nkb / g_tune[3]) S = nkb / g_tune[3];
+  if (S < 2) return 1;
+  const int kc = (int)((nkb + S - 1) / S);
+  *k_split = kc * bk;
+  return (nkb + kc - 1) / kc;
+}
+// the finishing pass moves 16-byte fp32 / 8-byte 16-bit groups of 4 pixels
+static bool fd_split_ok(const PwArgs& g) {
+  auto a16 = [](const void* p, long bs) { return !p || ((((uintptr_t)p) & 15) == 0 && (bs & 3) == 0); };
+  return a16(g.Y, g.y_bs) && a16(g.ypre, g.ypre_bs) && a16(g.gpre, g.gpre_bs);
+}
+
+static void fd_dispatch(int mode, PwArgs& g, int bm, int abf, int bbf, float* ws, hipStream_t st) {
+  int splits = 1;
+  g.k_split = 0;
+  g.ws = nullptr;
+  g.bk64 = g_tune[4] && bm != PW_WIDE && bm != 256;
+  if (ws && fd_split_ok(g)) {
+    splits = fd_splits(g, bm, g.bk64 ? 64 : PBK, &g.k_split);
+    if (splits > 1) g.ws = ws;
+    else g.k_split = 0;
+  }
+  if (half_type() == HALF_F16) pw_fd_launch<_Float16>(mode, g, bm, abf, bbf, splits, st);
+  else pw_fd_launch<__bf16>(mode, g, bm, abf, bbf, splits, st);
 }
 static void wg_dispatch(const PwArgs& g, int bm, int abf, int bbf, int splits, hipStream_t st) {
   if (half_type() == HALF_F16) pw_wgrad_launch<_Float16>(g, bm, abf, bbf, splits, st);
@@ -179,6 +222,17 @@ void launch_split_reduce(const float* ws, int splits, long MN, float* dw, hipStr
   launch_split_reduce_kk(ws, splits, MN, dw, nullptr, 0, st);
 }
 
+// 64-deep K steps for the 128-row weight-grad tiles (knob 5): re-plan the pixel split on 64-pixel steps
+static int wgrad_cfg_k(PwArgs& g, bool any_bf16, int* bm) {
+  int splits = wgrad_cfg(g, any_bf16, bm);
+  g.bk64 = 0;
+  if (g_tune[5] && *bm == 128 && g.P % 64 == 0) {
+    g.bk64 = 1;
+    splits = wgrad_plan(g.M, g.N, g.K, 128, 128, 64, 640, &g.k_split);
+  }
+  return splits;
+}
+
 static void wgrad_finish(const PwArgs& g, int splits, hipStream_t st) {
   if (splits > 1) {
     launch_split_reduce(g.ws, splits, (long)g.M * g.N, g.Y, st);
@@ -224,7 +278,7 @@ extern "C" int dsgan_pw_gemm(int mode, const float* A, long a_bs, const float* B
     DSG_REQUIRE(dsgan_pw_supported(mode, M, K, P, a_bs, b_bs, A, B), "dsgan_pw_gemm: unsupported WGRAD shape");
     g.M = M; g.N = N; g.K = nb * P;
     int bm;
-    const int splits = wgrad_cfg(g, false, &bm);
+    const int splits = wgrad_cfg_k(g, false, &bm);
     DSG_REQUIRE(splits == 1 || ws, "dsgan_pw_gemm: WGRAD needs the dsgan_pw_wgrad_workspace scratch");
     g.ws = splits > 1 ? ws : nullptr;
     g.asum = const_cast<float*>(bias);   // WGRAD: bias (nullable) receives the bias grad += sum_k A
@@ -238,7 +292,7 @@ extern "C" int dsgan_pw_gemm(int mode, const float* A, long a_bs, const float* B
     DSG_REQUIRE((long)K * P * 4 < lim && (long)M * K * 4 < lim, "dsgan_pw_gemm: operand exceeds 4 GiB buffer range");
     g.a_range = (unsigned)((long)M * K * 4);
     g.b_range = (unsigned)((long)K * P * 4);
-    fd_dispatch(mode, g, fd_tile(g, false), 0, 0, st);
+    fd_dispatch(mode, g, fd_tile(g, false), 0, 0, ws, st);   // ws: dsgan_pw_fd_workspace (NULL: never split)
   }
   DSG_CHECK_LAUNCH();
   return 0;
@@ -248,9 +302,9 @@ extern "C" int dsgan_pw_gemm(int mode, const float* A, long a_bs, const float* B
 // act(W X + bias), X fp32 or bf16 (x_bf16), Y fp32 or bf16 (y_bf16; accumulate needs fp32 Y);
 // ypre (nullable): fp32 pre-activation, or (ypre_grad_bf16) bf16 act'(pre) for the backward.
 // P % 128 == 0, K % 8 == 0, 16-byte aligned.
-extern "C" int dsgan_pw_fwd_io(const void* W, int w_bf16, const void* X, long x_bs, int x_bf16, void* Y, long y_bs,
-                               int y_bf16, const void* ypre, long ypre_bs, int ypre_grad_bf16, const float* bias, int M,
-                               int K, int P, int nb, int act, int accumulate, float slope, hipStream_t st) {
+extern "C" int dsgan_pw_fwd_io_ws(const void* W, int w_bf16, const void* X, long x_bs, int x_bf16, void* Y, long y_bs,
+                                  int y_bf16, const void* ypre, long ypre_bs, int ypre_grad_bf16, const float* bias, int M,
+                                  int K, int P, int nb, int act, int accumulate, float slope, float* ws, hipStream_t st) {
   DSG_REQUIRE(W && X && Y && M >= 16 && K > 0 && P > 0 && nb > 0, "dsgan_pw_fwd_io: bad args");
   DSG_REQUIRE(P % 128 == 0 && K % 8 == 0 && al16(W) && al16(X) && al16(Y) && (x_bs & 7) == 0 && (y_bs & 7) == 0 &&
                   !(y_bf16 && accumulate),
@@ -264,18 +318,25 @@ extern "C" int dsgan_pw_fwd_io(const void* W, int w_bf16, const void* X, long x_
   g.P = P; g.M = M; g.N = nb * P; g.K = K;
   g.a_range = (unsigned)((long)M * K * (w_bf16 ? 2 : 4));
   g.b_range = (unsigned)((long)K * P * (x_bf16 ? 2 : 4));
-  fd_dispatch(PW_FWD, g, fd_tile(g, w_bf16 || x_bf16), w_bf16, x_bf16, st);
+  fd_dispatch(PW_FWD, g, fd_tile(g, w_bf16 || x_bf16), w_bf16, x_bf16, ws, st);
   DSG_CHECK_LAUNCH();
   return 0;
+}
+
+extern "C" int dsgan_pw_fwd_io(const void* W, int w_bf16, const void* X, long x_bs, int x_bf16, void* Y, long y_bs,
+                               int y_bf16, const void* ypre, long ypre_bs, int ypre_grad_bf16, const float* bias, int M,
+                               int K, int P, int nb, int act, int accumulate, float slope, hipStream_t st) {
+  return dsgan_pw_fwd_io_ws(W, w_bf16, X, x_bs, x_bf16, Y, y_bs, y_bf16, ypre, ypre_bs, ypre_grad_bf16, bias, M, K, P, nb,
+                            act, accumulate, slope, nullptr, st);
 }
 
 // Data-grad with bf16 operands/outputs (the unfused MLP blocks' backward):
 //   DX[b][M][p] (+)= (sum_k W[k][M] DY[b][k][p]) (* GP[b][M][p])
 // DY fp32 or bf16 (dy_bf16), DX fp32 or bf16 (dx_bf16; accumulate needs fp32), GP (nullable) the bf16
 // act'(pre) written by dsgan_pw_fwd_io (ypre_grad_bf16).  P % 128 == 0, 16-byte aligned.
-extern "C" int dsgan_pw_dgrad_io(const void* W, int w_bf16, const void* DY, long dy_bs, int dy_bf16, void* DX, long dx_bs,
-                                 int dx_bf16, const void* GP, long gp_bs, int M, int K, int P, int nb,
-                                 int accumulate, hipStream_t st) {
+extern "C" int dsgan_pw_dgrad_io_ws(const void* W, int w_bf16, const void* DY, long dy_bs, int dy_bf16, void* DX,
+                                    long dx_bs, int dx_bf16, const void* GP, long gp_bs, int M, int K, int P, int nb,
+                                    int accumulate, float* ws, hipStream_t st) {
   DSG_REQUIRE(W && DY && DX && M > 0 && K > 0 && nb > 0, "dsgan_pw_dgrad_io: bad args");
   DSG_REQUIRE(dsgan_pw_supported(PW_DGRAD, M, K, P, 0, dy_bs, W, DY) && al16(DX) && (dy_bs & 7) == 0 &&
                   (dx_bs & 7) == 0 && (!GP || (al16(GP) && (gp_bs & 7) == 0)) && !(dx_bf16 && accumulate),
@@ -288,9 +349,37 @@ extern "C" int dsgan_pw_dgrad_io(const void* W, int w_bf16, const void* DY, long
   g.accumulate = accumulate; g.P = P; g.M = M; g.N = nb * P; g.K = K;
   g.a_range = (unsigned)((long)M * K * (w_bf16 ? 2 : 4));
   g.b_range = (unsigned)((long)K * P * (dy_bf16 ? 2 : 4));
-  fd_dispatch(PW_DGRAD, g, fd_tile(g, w_bf16 || dy_bf16), w_bf16, dy_bf16, st);
+  fd_dispatch(PW_DGRAD, g, fd_tile(g, w_bf16 || dy_bf16), w_bf16, dy_bf16, ws, st);
   DSG_CHECK_LAUNCH();
   return 0;
+}
+
+extern "C" int dsgan_pw_dgrad_io(const void* W, int w_bf16, const void* DY, long dy_bs, int dy_bf16, void* DX, long dx_bs,
+                                 int dx_bf16, const void* GP, long gp_bs, int M, int K, int P, int nb,
+                                 int accumulate, hipStream_t st) {
+  return dsgan_pw_dgrad_io_ws(W, w_bf16, DY, dy_bs, dy_bf16, DX, dx_bs, dx_bf16, GP, gp_bs, M, K, P, nb, accumulate,
+                              nullptr, st);
+}
+
+// Scratch (floats) of a split-K FWD (mode 0) / DGRAD (1) launch of M output channels over K at nb
+// images of P pixels (0: never split).  An upper bound for either operand dtype and epilogue: the
+// wide / 256-row tile forms, which some of those pick, are never split.
+extern "C" long dsgan_pw_fd_workspace(int mode, int M, int K, int P, int nb) {
+  if ((mode != PW_FWD && mode != PW_DGRAD) || M <= 0 || K <= 0 || P <= 0 || nb <= 0 || P % 128) return 0;
+  PwArgs g{};
+  g.M = M; g.N = nb * P; g.K = K; g.P = P;
+  const int bm = use_bm256(g) ? 256 : M > 64 ? 128 : 64;
+  int ks;
+  const int splits = max(fd_splits(g, bm, PBK, &ks), fd_splits(g, bm, 64, &ks));
+  return splits > 1 ? (long)splits * M * nb * P : 0;
+}
+
+// Planner knob key <- val (val < 0: read only); returns the previous value.  Measurement tools only.
+extern "C" int dsgan_pw_tune(int key, int val) {
+  if (key < 0 || key >= 8) return -1;
+  const int old = g_tune[key];
+  if (val >= 0) g_tune[key] = val;
+  return old;
 }
 
 // Weight-grad with bf16 operand(s): DW[M][N] += sum_{b,p} A[b][M][P] * B[b][N][P], A/B fp32 or
@@ -319,7 +408,7 @@ extern "C" int dsgan_pw_wgrad_mixed(const void* A, long a_bs, int a_bf16, const 
   g.a_range = (unsigned)ar; g.b_range = (unsigned)br;
   g.M = M; g.N = N; g.K = nb * P;
   int bm;
-  const int splits = wgrad_cfg(g, a_bf16 || b_bf16, &bm);
+  const int splits = wgrad_cfg_k(g, a_bf16 || b_bf16, &bm);
   DSG_REQUIRE(splits == 1 || ws, "dsgan_pw_wgrad_mixed: needs the dsgan_pw_wgrad_workspace scratch");
   g.ws = splits > 1 ? ws : nullptr;
   wg_dispatch(g, bm, a_bf16, b_bf16, splits, st);

@@ -38,6 +38,10 @@ SIGNATURES = {
     "dsgan_pw_wgrad_mixed": [P, L, I, P, L, I, P, P, I, I, I, I, P, S],
     "dsgan_pw_fwd_io": [P, I, P, L, I, P, L, I, P, L, I, P, I, I, I, I, I, I, F, S],
     "dsgan_pw_dgrad_io": [P, I, P, L, I, P, L, I, P, L, I, I, I, I, I, S],
+    "dsgan_pw_fwd_io_ws": [P, I, P, L, I, P, L, I, P, L, I, P, I, I, I, I, I, I, F, P, S],
+    "dsgan_pw_dgrad_io_ws": [P, I, P, L, I, P, L, I, P, L, I, I, I, I, I, P, S],
+    "dsgan_pw_fd_workspace": [I, I, I, I, I],
+    "dsgan_pw_tune": [I, I],
     # pwf32.hip
     "dsgan_pw_f32_supported": [I, I, I, I, L, L, P, P],
     "dsgan_pw_f32_wgrad_workspace": [I, I, I, I],

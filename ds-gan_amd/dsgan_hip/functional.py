@@ -258,6 +258,12 @@ def _pw_ws(M, N, P, nb, like):
     return torch.empty(n, device=like.device, dtype=torch.float32) if n > 0 else None
 
 
+def _pw_fd_ws(mode, M, K, P, nb, like):
+    """Split-K scratch of an under-filled pointwise FWD (0) / DGRAD (1) (dsgan_pw_fd_workspace), or None."""
+    n = _lib.load().dsgan_pw_fd_workspace(mode, M, K, P, nb)
+    return torch.empty(n, device=like.device, dtype=torch.float32) if n > 0 else None
+
+
 def _pwf_ok(mode, M, K, P, a_bs, b_bs, a, b):
     """fp32 operands (the MidMLKA 1x1 conv, or every 1x1 in the fp32 parity mode): pwf32.hip."""
     return _state["prec"] == "fp32" and bool(_lib.load().dsgan_pw_f32_supported(mode, M, K, P, a_bs, b_bs, a, b))
@@ -325,7 +331,8 @@ def conv_fwd_raw(x, w, b, stride, pad, act=None, out=None, pre=None, accumulate=
     elif KH == 1 and KW == 1 and stride == 1 and pad == 0 and _pw_ok(0, Cout, Cin, H * W, 0, xbs, w.data_ptr(), x.data_ptr()):
         fam = "pwgemm_kernel"
         call("dsgan_pw_gemm", 0, ptr(w), 0, ptr(x), xbs, ptr(y), ybs, ptr(b), ptr(pre), pbs, None, 0,
-             Cout, N * H * W, Cin, H * W, N, ACT[act], 0, ACT[xact], int(accumulate), LRELU_SLOPE, None, stream())
+             Cout, N * H * W, Cin, H * W, N, ACT[act], 0, ACT[xact], int(accumulate), LRELU_SLOPE,
+             ptr(_pw_fd_ws(0, Cout, Cin, H * W, N, x)), stream())
     elif (KH == 1 and KW == 1 and stride == 1 and pad == 0 and pre is None and xact is None
           and _pwf_ok(0, Cout, Cin, H * W, 0, xbs, w.data_ptr(), x.data_ptr())):
         fam = "pwf32_kernel"
@@ -388,7 +395,8 @@ def conv_dgrad_raw(dy, w, x_shape, stride, pad, bias=None, act=None, gpre=None, 
             and _pw_ok(1, Cin, Cout, H * W, 0, dybs, w.data_ptr(), dy.data_ptr())):
         fam = "pwgemm_kernel"
         call("dsgan_pw_gemm", 1, ptr(w), 0, ptr(dy), dybs, ptr(dx), dxbs, None, None, 0, ptr(gpre), gbs,
-             Cin, N * H * W, Cout, H * W, N, 0, ACT[gact], 0, int(accumulate), LRELU_SLOPE, None, stream())
+             Cin, N * H * W, Cout, H * W, N, 0, ACT[gact], 0, int(accumulate), LRELU_SLOPE,
+             ptr(_pw_fd_ws(1, Cin, Cout, H * W, N, dy)), stream())
     elif (KH == 1 and KW == 1 and stride == 1 and pad == 0 and bias is None and act is None
             and _pwf_ok(1, Cin, Cout, H * W, 0, dybs, w.data_ptr(), dy.data_ptr())):
         fam = "pwf32_kernel"
@@ -827,14 +835,14 @@ class PwMlpFn(torch.autograd.Function):
             gp = torch.empty((N, C4, H, W), device=h.device, dtype=half_dtype())   # gelu'(z), for dz
             g = torch.empty((N, C4, H, W), device=h.device, dtype=half_dtype())    # gelu(z)
             e0 = IGEMM_TIMER.begin()
-            call("dsgan_pw_fwd_io", ptr(bf16_weight(w1)), 1, ptr(h), hbs, hb, ptr(g), C4 * HW, 1, ptr(gp), C4 * HW, 1, ptr(b1), C4, C,
-                 HW, N, ACT["gelu"], 0, LRELU_SLOPE, stream())
+            call("dsgan_pw_fwd_io_ws", ptr(bf16_weight(w1)), 1, ptr(h), hbs, hb, ptr(g), C4 * HW, 1, ptr(gp), C4 * HW, 1,
+                 ptr(b1), C4, C, HW, N, ACT["gelu"], 0, LRELU_SLOPE, ptr(_pw_fd_ws(0, C4, C, HW, N, h)), stream())
             IGEMM_TIMER.end(e0, 2.0 * N * HW * C4 * C, ("fwd", N, C, H, W, C4, 1, 1), "pwgemm_kernel",
                             _nb(h, w1, b1, g, gp))
             out = conv_fwd_raw(x, ws, None, 1, 0)
             e0 = IGEMM_TIMER.begin()
-            call("dsgan_pw_fwd_io", ptr(bf16_weight(w2)), 1, ptr(g), C4 * HW, 1, ptr(out), P * HW, 0, None, 0, 0, ptr(b2), P, C4,
-                 HW, N, 0, 1, LRELU_SLOPE, stream())
+            call("dsgan_pw_fwd_io_ws", ptr(bf16_weight(w2)), 1, ptr(g), C4 * HW, 1, ptr(out), P * HW, 0, None, 0, 0, ptr(b2),
+                 P, C4, HW, N, 0, 1, LRELU_SLOPE, ptr(_pw_fd_ws(0, P, C4, HW, N, g)), stream())
             IGEMM_TIMER.end(e0, 2.0 * N * HW * C4 * P, ("fwd", N, C4, H, W, P, 1, 1), "pwgemm_kernel",
                             _nb(g, w2, b2) + 2 * _nb(out))
             ctx.g = g
@@ -888,8 +896,8 @@ class PwMlpFn(torch.autograd.Function):
             HW, P, C = H * W, w2.shape[0], h.shape[1]
             dz = torch.empty((N, C4, H, W), device=dy.device, dtype=half_dtype())
             e0 = IGEMM_TIMER.begin()
-            call("dsgan_pw_dgrad_io", ptr(bf16_weight(w2)), 1, ptr(dy), dybs, 0, ptr(dz), C4 * HW, 1, ptr(z), C4 * HW,
-                 C4, P, HW, N, 0, stream())
+            call("dsgan_pw_dgrad_io_ws", ptr(bf16_weight(w2)), 1, ptr(dy), dybs, 0, ptr(dz), C4 * HW, 1, ptr(z), C4 * HW,
+                 C4, P, HW, N, 0, ptr(_pw_fd_ws(1, C4, P, HW, N, dy)), stream())
             IGEMM_TIMER.end(e0, 2.0 * N * HW * C4 * P, ("dgrad", N, C4, H, W, P, 1, 1), "pwgemm_kernel",
                             _nb(dy, w2, dz, z))
             # bias grads ride on the weight-grads' staged A tiles (db += sum_k A): b2 from dy, b1 from
@@ -916,8 +924,8 @@ class PwMlpFn(torch.autograd.Function):
             if want_dh:
                 dh = _empty(N, C, H, W, dy)
                 e0 = IGEMM_TIMER.begin()
-                call("dsgan_pw_dgrad_io", ptr(bf16_weight(w1)), 1, ptr(dz), C4 * HW, 1, ptr(dh), C * HW, 0, None, 0, C, C4, HW,
-                     N, 0, stream())
+                call("dsgan_pw_dgrad_io_ws", ptr(bf16_weight(w1)), 1, ptr(dz), C4 * HW, 1, ptr(dh), C * HW, 0, None, 0, C, C4,
+                     HW, N, 0, ptr(_pw_fd_ws(1, C, C4, HW, N, dz)), stream())
                 IGEMM_TIMER.end(e0, 2.0 * N * HW * C4 * C, ("dgrad", N, C4, H, W, C, 1, 1), "pwgemm_kernel",
                                 _nb(dz, w1, dh))
             _params_done(*ctx.refs)

@@ -78,6 +78,9 @@ int dsgan_conv_wgrad(const float* dy, long dy_bs, const float* x, long x_bs, flo
  *              floats; NULL allowed when that is 0), summed in a fixed order: deterministic.
  *              `bias` (nullable) is an OUTPUT here: bias[m] += sum_{b,p} DY[b][m][p] (the layer's
  *              bias grad, from the same staged tiles -- no separate channel-sum pass).
+ * FWD / DGRAD: ws (nullable) = dsgan_pw_fd_workspace(mode, M, K, P, nb) floats lets a launch whose
+ *              tiles under-fill the chip split K; the partials are added in split order by a
+ *              finishing pass that applies the epilogue (deterministic).
  * dsgan_pw_supported() reports whether a shape/alignment takes this path (else use igemm). */
 int dsgan_pw_supported(int mode, int M, int K, int P, long a_bs, long b_bs, const void* a,
                        const void* b);
@@ -86,6 +89,9 @@ int dsgan_pw_gemm(int mode, const float* A, long a_bs, const float* B, long b_bs
                   long gpre_bs, int M, int N, int K, int P, int nb, int act, int gact, int bact,
                   int accumulate, float slope, float* ws, hipStream_t stream);
 long dsgan_pw_wgrad_workspace(int M, int N, int P, int nb);
+long dsgan_pw_fd_workspace(int mode, int M, int K, int P, int nb);
+/* planner knob `key` <- val (val < 0: read only), returns the previous value (measurement tools) */
+int dsgan_pw_tune(int key, int val);
 
 /* ---- exact-fp32 pointwise GEMMs (pwf32.hip): v_mfma_f32_32x32x2_f32, same modes and argument
  * meaning as dsgan_pw_gemm (no ypre / activation-on-load); the MidMLKA 1x1 conv (fp32 by policy,
@@ -109,11 +115,19 @@ int dsgan_pw_wgrad_mixed(const void* A, long a_bs, int a_bf16, const void* B, lo
 int dsgan_pw_fwd_io(const void* W, int w_bf16, const void* X, long x_bs, int x_bf16, void* Y, long y_bs, int y_bf16,
                     const void* ypre, long ypre_bs, int ypre_grad_bf16, const float* bias, int M, int K, int P, int nb,
                     int act, int accumulate, float slope, hipStream_t stream);
+/* same, with the split-K scratch of dsgan_pw_fd_workspace(0, M, K, P, nb) (NULL: never split) */
+int dsgan_pw_fwd_io_ws(const void* W, int w_bf16, const void* X, long x_bs, int x_bf16, void* Y, long y_bs, int y_bf16,
+                       const void* ypre, long ypre_bs, int ypre_grad_bf16, const float* bias, int M, int K, int P,
+                       int nb, int act, int accumulate, float slope, float* ws, hipStream_t stream);
 /* DX (+)= (W^T DY) (* GP): DY fp32 or bf16, DX fp32 or bf16, GP (nullable) the bf16 act'(pre) of
  * dsgan_pw_fwd_io.  Unfused-block pwconv2 / pwconv1 data-grads. */
 int dsgan_pw_dgrad_io(const void* W, int w_bf16, const void* DY, long dy_bs, int dy_bf16, void* DX, long dx_bs,
                       int dx_bf16, const void* GP, long gp_bs, int M, int K, int P, int nb, int accumulate,
                       hipStream_t stream);
+/* same, with the split-K scratch of dsgan_pw_fd_workspace(1, M, K, P, nb) (NULL: never split) */
+int dsgan_pw_dgrad_io_ws(const void* W, int w_bf16, const void* DY, long dy_bs, int dy_bf16, void* DX, long dx_bs,
+                         int dx_bf16, const void* GP, long gp_bs, int M, int K, int P, int nb, int accumulate,
+                         float* ws, hipStream_t stream);
 
 /* ---- fused ConvNeXt MLP (mlp.hip), replaces Block.pwconv1 -> GELU -> pwconv2 -------------------
  * DSGAN/models/model/MixConvNeXtML.py:221-223,236-240 (nn.Linear(C,4C) + GELU + nn.Linear(4C,P) on

@@ -975,3 +975,87 @@ def test_thin3_accumulate_and_strides(N, K, M, H, W):
     HF.conv_wgrad_raw(dy.to(DEV), xb.to(DEV)[:, 4:], dwd, 1, 1)
     refw = dw + torch.nn.grad.conv2d_weight(x, (M, K, 3, 3), dy, padding=1)
     assert rel(dwd, refw) < 1e-5
+
+
+@pytest.mark.parametrize("half", HALVES)
+@pytest.mark.parametrize("N,M,K,P", [(16, 64, 1024, 256), (16, 512, 1024, 256), (4, 256, 512, 256), (2, 96, 640, 128)])
+def test_pw_split_k(half, N, M, K, P):
+    """Split-K of under-filled pointwise FWD / DGRAD launches (dsgan_pw_fd_workspace > 0): fp32
+    partials per K split, then the finishing pass with every epilogue form -- FWD bias + GELU +
+    fp32 pre-activation + accumulate, FWD GELU pair into 16-bit g / g', DGRAD gelu'(fp32 pre)
+    (+accumulate), DGRAD * 16-bit gp into a 16-bit dz -- vs float64 torch on the 16-bit operands,
+    and against the same launches with the split turned off (dsgan_pw_tune(0, 0))."""
+    from dsgan_hip import functional as HF
+    from dsgan_hip import _lib
+    from dsgan_hip._lib import call, ptr, stream
+    HF.set_precision(half)
+    lib = _lib.load()
+    assert lib.dsgan_pw_fd_workspace(0, M, K, P, N) > 0 and lib.dsgan_pw_fd_workspace(1, M, K, P, N) > 0
+    hd = _hdt(half)
+    g = torch.Generator().manual_seed(M * 3 + K + P)
+    x = torch.randn(N, K, P, generator=g)
+    w = torch.randn(M, K, generator=g) / math.sqrt(K)
+    b = torch.randn(M, generator=g) * 0.1
+    y0 = torch.randn(N, M, P, generator=g)
+    dy = torch.randn(N, K, P, generator=g)
+    z = torch.randn(N, M, P, generator=g)
+    gpv = torch.rand(N, M, P, generator=g).to(hd)
+    wT = w.t().contiguous()                                   # DGRAD: W[K'=M][M'=K] -> here [K][M]
+    # every device operand is held by a name for the whole test: a temporary freed right after ptr()
+    # would be handed to the next allocation on the stream before the kernel reads it
+    xd, wd, bd, dyd, zd = x.to(DEV), w.to(DEV), b.to(DEV), dy.to(DEV), z.to(DEV)
+    xh, wh, wTd, gpd = xd.to(hd), wd.to(hd), wT.to(DEV), gpv.to(DEV)
+    wTh = wTd.to(hd)
+    wss = {mode: torch.empty(lib.dsgan_pw_fd_workspace(mode, M, K, P, N), device=DEV) for mode in (0, 1)}
+
+    def ws(mode):
+        return wss[mode]
+
+    def runs():
+        out = {}
+        # FWD fp32 operands: y = gelu(W x + b) + y0, pre-activation to ypre
+        y, pre = y0.to(DEV), torch.empty(N, M, P, device=DEV)
+        call("dsgan_pw_gemm", 0, ptr(wd), 0, ptr(xd), K * P, ptr(y), M * P, ptr(bd), ptr(pre), M * P, None, 0,
+             M, N * P, K, P, N, HF.ACT["gelu"], 0, 0, 1, 0.2, ptr(ws(0)), stream())
+        out["fwd"], out["pre"] = y, pre
+        # FWD 16-bit in / GELU pair out
+        gg, gp = torch.empty(N, M, P, device=DEV, dtype=hd), torch.empty(N, M, P, device=DEV, dtype=hd)
+        call("dsgan_pw_fwd_io_ws", ptr(wh), 1, ptr(xh), K * P, 1, ptr(gg), M * P, 1, ptr(gp), M * P, 1,
+             ptr(bd), M, K, P, N, HF.ACT["gelu"], 0, 0.2, ptr(ws(0)), stream())
+        out["g"], out["gp"] = gg, gp
+        # DGRAD fp32: dx = (W^T dy) * gelu'(z) + y0  (W stored [K][M] as the layer's [out][in] weight)
+        dx = y0.to(DEV)
+        call("dsgan_pw_gemm", 1, ptr(wTd), 0, ptr(dyd), K * P, ptr(dx), M * P, None, None, 0, ptr(zd), M * P,
+             M, N * P, K, P, N, 0, HF.ACT["gelu"], 0, 1, 0.2, ptr(ws(1)), stream())
+        out["dgrad"] = dx
+        # DGRAD 16-bit: dz = (W^T dy) * gp, 16-bit out
+        dz = torch.empty(N, M, P, device=DEV, dtype=hd)
+        call("dsgan_pw_dgrad_io_ws", ptr(wTh), 1, ptr(dyd), K * P, 0, ptr(dz), M * P, 1, ptr(gpd),
+             M * P, M, K, P, N, 0, ptr(ws(1)), stream())
+        out["dz"] = dz
+        torch.cuda.synchronize()
+        return {k: v.double().cpu() for k, v in out.items()}
+
+    split = runs()
+    old = lib.dsgan_pw_tune(0, 0)
+    try:
+        whole = runs()
+    finally:
+        lib.dsgan_pw_tune(0, old)
+    qx, qw, qdy = _q(x, half).double(), _q(w, half).double(), _q(dy, half).double()
+    zr = torch.einsum("mk,nkp->nmp", qw, qx) + b.double().view(1, M, 1)
+    zz = zr.clone().requires_grad_(True)
+    F.gelu(zz).sum().backward()
+    ref = {"pre": zr, "fwd": F.gelu(zr) + y0.double(), "g": F.gelu(zr), "gp": zz.grad}
+    zg = z.double().clone().requires_grad_(True)
+    F.gelu(zg).sum().backward()
+    t = torch.einsum("mk,nkp->nmp", qw, qdy)
+    ref["dgrad"] = t * zg.grad + y0.double()
+    ref["dz"] = t * gpv.double()
+    for k in ("pre", "fwd", "dgrad"):
+        assert rel(split[k], ref[k]) < 1e-5, k
+    for k in ref:   # the unsplit launch sums K in another order: fp32 rounding, or a 16-bit ulp
+        assert rel(split[k], whole[k]) < (1e-5 if k in ("pre", "fwd", "dgrad") else 4 * _ulp(half)), k
+    for k in ("g", "gp", "dz"):
+        assert ((split[k] - ref[k]).abs() <= ref[k].abs() * 2 * _ulp(half) + 1e-3).all(), k
+    HF.set_precision("fp32")
