@@ -253,13 +253,21 @@ static void pf_launch_fd(const PfArgs& g, hipStream_t st) {
   else pf_launch<MODE, 64, 64>(g, 1, st);
 }
 
-// pixel split of a weight-grad: ~640 workgroups, >= 8 K steps each, partials <= 1/4 of operand bytes
+// Weight-grad tile and pixel split: 64 x 64 tiles when both sides have <= 64 channels (the MidMLKA(32)
+// / (64) 1x1s: a 64 x 128 tile over a 32 x 32 weight was 7/8 idle MFMA work), else 128 (64) x 128;
+// ~640 workgroups of >= 4 K steps each.  The f32 MFMA runs at 1/16 of the bf16 rate, so these
+// launches are MFMA-bound and the fp32 partials are cheap next to them: the partial bytes may exceed
+// a quarter of the operand bytes up to a floor of ~512 workgroups (the 256 x 256 weight at 16^2:
+// 8 -> 64 splits, 50 -> ~10 us; 128 x 128 at 32^2: 64 -> 256 splits).
+static int pf_wgrad_bn(int M, int N) { return M <= 64 && N <= 64 ? 64 : 128; }
 static int pf_wgrad_plan(int M, int N, long K, int* k_split) {
-  const int BM = M > 64 ? 128 : 64;
-  const long tiles = (long)((M + BM - 1) / BM) * ((N + 127) / 128);
+  const int BM = M > 64 ? 128 : 64, BN = pf_wgrad_bn(M, N);
+  const long tiles = (long)((M + BM - 1) / BM) * ((N + BN - 1) / BN);
   long splits = (640 + tiles - 1) / tiles;
-  const long max_splits = (K + 8L * FBK - 1) / (8L * FBK);
-  const long byte_cap = ((long)(M + N) * K) / (4L * M * N);
+  const long max_splits = (K + 4L * FBK - 1) / (4L * FBK);
+  long byte_cap = ((long)(M + N) * K) / (4L * M * N);
+  const long floor_splits = (512 + tiles - 1) / tiles;
+  if (byte_cap < floor_splits) byte_cap = floor_splits;
   if (splits > max_splits) splits = max_splits;
   if (splits > byte_cap) splits = byte_cap;
   if (splits < 1) splits = 1;
@@ -316,6 +324,7 @@ int dsgan_pw_gemm_f32(int mode, const float* A, long a_bs, const float* B, long 
     DSG_REQUIRE(splits == 1 || ws, "dsgan_pw_gemm_f32: WGRAD needs dsgan_pw_f32_wgrad_workspace floats of scratch");
     g.ws = splits > 1 ? ws : nullptr;
     if (M > 64) pf_launch<PF_WGRAD, 128>(g, splits, st);
+    else if (pf_wgrad_bn(M, N) == 64) pf_launch<PF_WGRAD, 64, 64>(g, splits, st);
     else pf_launch<PF_WGRAD, 64>(g, splits, st);
     if (splits > 1) launch_split_reduce(ws, splits, (long)M * N, Y, st);
   } else {

@@ -20,7 +20,9 @@ def rel(a, b):
     return ((a - b).norm() / max(b.norm().item(), 1e-30)).item()
 
 
-SHAPES = [(2, 128, 128, 32, 32), (3, 32, 32, 64, 64), (2, 256, 256, 16, 16), (1, 64, 96, 16, 24), (16, 128, 128, 8, 16)]
+SHAPES = [(2, 128, 128, 32, 32), (3, 32, 32, 64, 64), (2, 256, 256, 16, 16), (1, 64, 96, 16, 24), (16, 128, 128, 8, 16),
+          # the step's MidMLKA weight-grads (the 64 x 64 tile, the many-split plans)
+          (16, 256, 256, 16, 16), (16, 128, 128, 32, 32), (4, 32, 32, 128, 128), (8, 64, 64, 64, 64)]
 
 
 @pytest.mark.parametrize("shape", SHAPES)

@@ -23,14 +23,26 @@ B = 16
 GELU = 1
 
 
-def cases():
-    """(name, flops, bytes, fn) -- each fn allocates nothing inside the timed call."""
+def cases(arms):
+    """(name, flops, bytes, fn) -- each fn allocates nothing inside the timed call.  Scratch is sized
+    for the largest plan over every arm's knob settings (a split plan differs per arm)."""
     out = []
     hd = torch.bfloat16
     lib = _lib.load()
 
+    def most(q):
+        base = {k: lib.dsgan_pw_tune(k, -1) for k in range(8)}
+        n = 0
+        for kv in arms:
+            for k, v in kv.items():
+                lib.dsgan_pw_tune(k, v)
+            n = max(n, q())
+        for k, v in base.items():
+            lib.dsgan_pw_tune(k, v)
+        return n
+
     def ws_fd(mode, M, K, P):
-        n = lib.dsgan_pw_fd_workspace(mode, M, K, P, B)
+        n = most(lambda: lib.dsgan_pw_fd_workspace(mode, M, K, P, B))
         return torch.empty(max(n, 1), device="cuda")
 
     # unfused MLP blocks: (C, C4, P-out, HW)
@@ -51,8 +63,8 @@ def cases():
         wg1 = torch.zeros(C4, C, device="cuda")
         wg2 = torch.zeros(Pc, C4, device="cuda")
         gb1, gb2 = torch.zeros(C4, device="cuda"), torch.zeros(Pc, device="cuda")
-        wsw2 = torch.empty(max(1, lib.dsgan_pw_wgrad_workspace(Pc, C4, HW, B)), device="cuda")
-        wsw1 = torch.empty(max(1, lib.dsgan_pw_wgrad_workspace(C4, C, HW, B)), device="cuda")
+        wsw2 = torch.empty(max(1, most(lambda: lib.dsgan_pw_wgrad_workspace(Pc, C4, HW, B))), device="cuda")
+        wsw1 = torch.empty(max(1, most(lambda: lib.dsgan_pw_wgrad_workspace(C4, C, HW, B))), device="cuda")
         tag = "C%d@%d" % (C, H)
         f1 = 2.0 * B * HW * C4 * C
         f2 = 2.0 * B * HW * C4 * Pc
@@ -129,7 +141,7 @@ def main():
             k, v = t.split("=")
             kv[int(k)] = int(v)
         parsed.append(kv)
-    cs = [c for c in cases() if not a.only or a.only in c[0]]
+    cs = [c for c in cases(parsed) if not a.only or a.only in c[0]]
     res = {(c[0], i): [] for c in cs for i in range(len(parsed))}
     for _ in range(a.rounds):
         for i, kv in enumerate(parsed):
