@@ -32,6 +32,7 @@ struct PwArgs {
   int y_bf16;  // FWD: Y is bf16 [b][M][P] (y_bs in elements)
   int gbf;     // FWD: ypre is bf16 and receives act'(pre);  DGRAD: gpre is a bf16 multiplier (no act')
   int bk64;    // host planner: 128 / 64-row tiles with 64-deep K steps (else 32)
+  int gp_pref; // DGRAD with a 16-bit gp multiplier (SWP tiles): load gp before the K loop
   float* asum; // WGRAD (nullable): db[m] += sum_k A[m][k] -- the bias grad of the layer whose output
                // grad is A, from the staged A tiles (split partials after the S*M*N weight partials)
 };
@@ -310,6 +311,35 @@ __global__ __launch_bounds__(128 * WN, WN == 2 ? 2 : 1) void pwgemm_kernel(PwArg
   // lane = 32h + 16G + 4q + p supplies row (8h + q) and column 16G + 4p of its 16-column block
   const int tq = (lane >> 2) & 3, tp = lane & 3, tG = (lane >> 4) & 1;
 
+  // DGRAD * 16-bit gp (the unfused blocks' dz = (W2^T dy) gelu'(z)): this tile's gp values are
+  // loaded here, before the K loop, into TM*TN*4 8-byte registers -- their HBM latency then hides
+  // behind the whole loop instead of opening the epilogue (the short-K data-grads run 8-16 K steps).
+  // Same lanes / offsets as the SW epilogue below.  (TM*TN*8 VGPRs: 128 / 64-row 4-wave tiles only.)
+  constexpr bool GPF = SW && MODE == PW_DGRAD && WN == 2 && BM <= 128;   // (register room: 4-wave tiles)
+  const bool gpf_on = GPF && g.gp_pref && g.gpre && g.gbf && !g.ws;
+  uint2 gpf[GPF ? TM * TN * 4 : 1];
+  if constexpr (GPF) {
+    if (gpf_on) {
+      const unsigned grange = (unsigned)(((long)g.M * g.P - p0) * 2);
+      const __amdgpu_buffer_rsrc_t rgp = __builtin_amdgcn_make_buffer_rsrc(
+          (void*)((const char*)g.gpre + ((long)bimg * g.gpre_bs + p0) * 2), (short)0, grange, 0x00020000);
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          const int col0 = wn * TN * 32 + j * 32;
+          const int mrow = m0 + wm * TM * 32 + i * 32;
+          const bool ok = mrow + lr < g.M;
+          const int v2 = ok ? (lr * g.P + col0 + 4 * lh) * 2 : (int)PW_OOB;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const auto u = __builtin_amdgcn_raw_buffer_load_b64(rgp, v2, mrow * g.P * 2 + 16 * q, 0);
+            gpf[(j * TM + i) * 4 + q] = make_uint2(u[0], u[1]);
+          }
+        }
+    }
+  }
+
   for (int kt = 0; kt < nk; ++kt) {
     const int buf = kt & 1;
     if (kt + 1 < nk) gload(kt + 1);
@@ -445,11 +475,16 @@ __global__ __launch_bounds__(128 * WN, WN == 2 ? 2 : 1) void pwgemm_kernel(PwArg
         if (gpre && g.gbf) {          // DGRAD: v *= gp, gp = act'(pre) stored 16-bit by the forward
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
-            const auto u = __builtin_amdgcn_raw_buffer_load_b64(rg, v2, s2 + 16 * q, 0);
-            v[4 * q] *= h2f<T16>((unsigned short)(u[0] & 0xffffu));
-            v[4 * q + 1] *= h2f<T16>((unsigned short)(u[0] >> 16));
-            v[4 * q + 2] *= h2f<T16>((unsigned short)(u[1] & 0xffffu));
-            v[4 * q + 3] *= h2f<T16>((unsigned short)(u[1] >> 16));
+            uint2 u;
+            if (gpf_on) u = gpf[(GPF ? (j * TM + i) * 4 : 0) + (GPF ? q : 0)];
+            else {
+              const auto w2 = __builtin_amdgcn_raw_buffer_load_b64(rg, v2, s2 + 16 * q, 0);
+              u = make_uint2(w2[0], w2[1]);
+            }
+            v[4 * q] *= h2f<T16>((unsigned short)(u.x & 0xffffu));
+            v[4 * q + 1] *= h2f<T16>((unsigned short)(u.x >> 16));
+            v[4 * q + 2] *= h2f<T16>((unsigned short)(u.y & 0xffffu));
+            v[4 * q + 3] *= h2f<T16>((unsigned short)(u.y >> 16));
           }
         } else if (gpre) {
           float gv[16];

@@ -34,8 +34,21 @@ static void pw_fd_launch(int mode, const PwArgs& g, int bm, int abf, int bbf, in
 // Planner knobs, read by the host launchers only (tools/pw_bench.py flips them for in-process A/B):
 //   [0] FWD/DGRAD split-K on/off, [1] its target workgroup count, [2] split only launches of fewer
 //   tiles than this, [3] minimum K steps per split, [4] 64-deep K steps for the 128 / 64-row FWD /
-//   DGRAD tiles, [5] the same for the 128-row WGRAD tiles.
-static int g_tune[8] = {1, 512, 256, 4, 0, 0, 0, 0};
+//   DGRAD tiles, [5] the same for the 128-row WGRAD tiles, [6] gelu-pair forward tile (0 built-in,
+//   1 256 x 128, 2 128 x 128, 3 wide 256 x 256), [7] gp-multiplied data-grad tile (same codes),
+//   [8] gp loaded before the K loop (16-bit gp data-grads on 128 / 64-row tiles).
+static int g_tune[12] = {1, 512, 256, 4, 0, 0, 0, 0, 1, 0, 0, 0};
+
+// tile choice with the knob overrides of the two epilogue-heavy forms
+static int fd_tile_k(const PwArgs& g, bool any_bf16) {
+  const int bm = fd_tile(g, any_bf16);
+  const bool gelu_pair = g.ypre && g.gbf, gp_dgrad = g.gpre && g.gbf;
+  const int k = gelu_pair ? g_tune[6] : gp_dgrad ? g_tune[7] : 0;
+  if (k == 0 || !any_bf16) return bm;
+  if (k == 3 && use_wide(g)) return PW_WIDE;
+  if (k == 1 && g.M % 256 == 0) return 256;
+  return g.M > 64 ? 128 : 64;
+}
 
 // K split of an under-filled FWD / DGRAD launch (the 16^2 bottleneck layers: e.g. the downSkip 1x1
 // data-grads, 32-128 tiles of 32-64 K steps each, ~40 us at 0.5 TB/s): about g_tune[1] workgroups,
@@ -66,6 +79,7 @@ static void fd_dispatch(int mode, PwArgs& g, int bm, int abf, int bbf, float* ws
   g.k_split = 0;
   g.ws = nullptr;
   g.bk64 = g_tune[4] && bm != PW_WIDE && bm != 256;
+  g.gp_pref = g_tune[8];
   if (ws && fd_split_ok(g)) {
     splits = fd_splits(g, bm, g.bk64 ? 64 : PBK, &g.k_split);
     if (splits > 1) g.ws = ws;
@@ -318,7 +332,7 @@ extern "C" int dsgan_pw_fwd_io_ws(const void* W, int w_bf16, const void* X, long
   g.P = P; g.M = M; g.N = nb * P; g.K = K;
   g.a_range = (unsigned)((long)M * K * (w_bf16 ? 2 : 4));
   g.b_range = (unsigned)((long)K * P * (x_bf16 ? 2 : 4));
-  fd_dispatch(PW_FWD, g, fd_tile(g, w_bf16 || x_bf16), w_bf16, x_bf16, ws, st);
+  fd_dispatch(PW_FWD, g, fd_tile_k(g, w_bf16 || x_bf16), w_bf16, x_bf16, ws, st);
   DSG_CHECK_LAUNCH();
   return 0;
 }
@@ -349,7 +363,7 @@ extern "C" int dsgan_pw_dgrad_io_ws(const void* W, int w_bf16, const void* DY, l
   g.accumulate = accumulate; g.P = P; g.M = M; g.N = nb * P; g.K = K;
   g.a_range = (unsigned)((long)M * K * (w_bf16 ? 2 : 4));
   g.b_range = (unsigned)((long)K * P * (dy_bf16 ? 2 : 4));
-  fd_dispatch(PW_DGRAD, g, fd_tile(g, w_bf16 || dy_bf16), w_bf16, dy_bf16, ws, st);
+  fd_dispatch(PW_DGRAD, g, fd_tile_k(g, w_bf16 || dy_bf16), w_bf16, dy_bf16, ws, st);
   DSG_CHECK_LAUNCH();
   return 0;
 }
@@ -376,7 +390,7 @@ extern "C" long dsgan_pw_fd_workspace(int mode, int M, int K, int P, int nb) {
 
 // Planner knob key <- val (val < 0: read only); returns the previous value.  Measurement tools only.
 extern "C" int dsgan_pw_tune(int key, int val) {
-  if (key < 0 || key >= 8) return -1;
+  if (key < 0 || key >= 12) return -1;
   const int old = g_tune[key];
   if (val >= 0) g_tune[key] = val;
   return old;

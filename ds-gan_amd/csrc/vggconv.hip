@@ -228,21 +228,20 @@ __global__ void vconv_wtrans_kernel(const float* __restrict__ W, T16* __restrict
 // conv1_1 (DSGAN/models/vgg.py:17): y[n][c][h][w] = relu(b[c] + sum_{ci,kh,kw} w[c][ci][kh][kw] *
 // x[n][ci][h-1+kh][w-1+kw]), exact fp32 FMAs in (ci, kh, kw) order, stored CB16 bf16.  Thread =
 // (pixel, 16-channel block).
-template <typename T16>
+template <typename T16, bool UNI>
 __global__ __launch_bounds__(256) void vgg_conv1_fwd_kernel(const float* __restrict__ x, long x_bs,
                                                             const float* __restrict__ w, const float* __restrict__ b,
                                                             T16* __restrict__ y, int N, int H, int W) {
   typedef hx8<T16> vgb8;
   typedef hx4<T16> vgb4;
-  __shared__ float ws[64 * 27 + 64];
-  for (int i = threadIdx.x; i < 64 * 27; i += 256) ws[i] = w[i];
-  if (threadIdx.x < 64) ws[64 * 27 + threadIdx.x] = b[threadIdx.x];
-  __syncthreads();
+  // UNI (HW % 64 == 0): a wave's 64 pixels share (n, cb), so the channel block is wave-uniform and
+  // its 16 x 27 weights + biases come through the scalar cache (s_load), not one LDS read per FMA
   const long HW = (long)H * W;
   const long t = blockIdx.x * 256L + threadIdx.x;
   if (t >= (long)N * 4 * HW) return;
   const long pix = t % HW;
-  const int cb = (int)((t / HW) & 3), n = (int)(t / (HW * 4));
+  const int cb = UNI ? __builtin_amdgcn_readfirstlane((int)((t / HW) & 3)) : (int)((t / HW) & 3);
+  const int n = (int)(t / (HW * 4));
   const int h = (int)(pix / W), wc = (int)(pix - (long)h * W);
   float in[27];
 #pragma unroll
@@ -259,9 +258,9 @@ __global__ __launch_bounds__(256) void vgg_conv1_fwd_kernel(const float* __restr
 #pragma unroll
   for (int c = 0; c < 16; ++c) {
     const int co = cb * 16 + c;
-    float a = ws[64 * 27 + co];
+    float a = b[co];
 #pragma unroll
-    for (int i = 0; i < 27; ++i) a = fmaf(ws[co * 27 + i], in[i], a);
+    for (int i = 0; i < 27; ++i) a = fmaf(w[co * 27 + i], in[i], a);
     o[c >> 3][c & 7] = (T16)fmaxf(a, 0.f);
   }
   vgb8* dst = reinterpret_cast<vgb8*>(y + cb16(n, cb * 16, h, wc, 64, H, W));
@@ -282,8 +281,17 @@ __global__ __launch_bounds__(256) void vgg_conv1_dgrad_kernel(const T16* __restr
     ws[i] = w[(co * 3 + ci) * 9 + tap];
   }
   __syncthreads();
+  // XCD-aware row order: consecutive workgroups (neighbouring pixel rows, whose 3x3 windows read the
+  // same rows of d) run on one XCD and share its L2 -- dispatch round-robins workgroups over the 8
+  // XCDs, which made every row of d come from HBM ~9 times (FETCH_SIZE 1.22 GB for a 134 MB d)
   const long HW = (long)H * W;
-  const long t = blockIdx.x * 256L + threadIdx.x;
+  int blk;
+  {
+    const int nwg = gridDim.x, id = blockIdx.x;
+    const int xcd = id & 7, q = nwg >> 3, r = nwg & 7;
+    blk = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (id >> 3);
+  }
+  const long t = blk * 256L + threadIdx.x;
   if (t >= (long)N * HW) return;
   const int n = (int)(t / HW);
   const long pix = t - (long)n * HW;
@@ -476,8 +484,12 @@ int dsgan_vgg_conv1_fwd(const float* x, long x_bs, const float* w, const float* 
   const long total = (long)N * 4 * H * W;
   with_half([&](auto* t_) {
     using T16 = std::remove_pointer_t<decltype(t_)>;
-    hipLaunchKernelGGL((vgg_conv1_fwd_kernel<T16>), dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, x, x_bs,
-                       w, b, (T16*)y, N, H, W);
+    if ((H * W) % 64 == 0)
+      hipLaunchKernelGGL((vgg_conv1_fwd_kernel<T16, true>), dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, x,
+                         x_bs, w, b, (T16*)y, N, H, W);
+    else
+      hipLaunchKernelGGL((vgg_conv1_fwd_kernel<T16, false>), dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, x,
+                         x_bs, w, b, (T16*)y, N, H, W);
   });
   DSG_CHECK_LAUNCH();
   return 0;

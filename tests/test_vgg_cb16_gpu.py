@@ -111,25 +111,26 @@ def test_vconv_dgrad(half, shape, masked):
 
 
 @pytest.mark.parametrize("half", HALVES)
-def test_conv1_forward_and_dgrad(half):
+@pytest.mark.parametrize("N,H,W", [(2, 32, 64), (1, 9, 14), (3, 20, 36)])   # HW % 64 == 0 (scalar weights) or not
+def test_conv1_forward_and_dgrad(half, N, H, W):
     HT = _hdt(half)
     bf = lambda v: v.to(HT).float()  # noqa: E731 -- this half type
     from dsgan_hip import functional as HF_
     HF_.set_precision(half)
     HF = _hf()
     from dsgan_hip._lib import call, ptr, stream
-    g = torch.Generator().manual_seed(3)
-    N, H, W = 2, 32, 64
+    g = torch.Generator().manual_seed(3 + H * W)
     x = torch.rand(N, 3, H, W, generator=g) * 2 - 1
     w = torch.randn(64, 3, 3, 3, generator=g) * 0.3
     b = torch.randn(64, generator=g) * 0.1
     ref = torch.relu(F.conv2d(x.double(), w.double(), b.double(), padding=1))
     y = torch.empty((N, 4, H, W, 16), device="cuda", dtype=HT)
-    call("dsgan_vgg_conv1_fwd", ptr(x.cuda()), 3 * H * W, ptr(w.cuda()), ptr(b.cuda()), ptr(y), N, H, W, stream())
+    xd, wd, bd = x.cuda(), w.cuda(), b.cuda()   # named: a temporary freed after ptr() could be re-handed out
+    call("dsgan_vgg_conv1_fwd", ptr(xd), 3 * H * W, ptr(wd), ptr(bd), ptr(y), N, H, W, stream())
     d = bf(torch.randn(N, 64, H, W, generator=g) * 1e-3)
     dx = torch.empty((N, 3, H, W), device="cuda")
-    call("dsgan_vgg_conv1_dgrad", ptr(to_cb16(d).cuda().to(HT)), ptr(w.cuda()), ptr(dx), 3 * H * W, N, H,
-         W, stream())
+    dd = to_cb16(d).cuda().to(HT)
+    call("dsgan_vgg_conv1_dgrad", ptr(dd), ptr(wd), ptr(dx), 3 * H * W, N, H, W, stream())
     torch.cuda.synchronize()
     got = from_cb16(y.float().cpu())
     assert ((got.double() - ref).abs() <= ref.abs() * _ulp(half) + 1e-6).all()

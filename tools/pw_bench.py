@@ -31,7 +31,7 @@ def cases(arms):
     lib = _lib.load()
 
     def most(q):
-        base = {k: lib.dsgan_pw_tune(k, -1) for k in range(8)}
+        base = {k: lib.dsgan_pw_tune(k, -1) for k in range(12)}
         n = 0
         for kv in arms:
             for k, v in kv.items():
@@ -133,7 +133,7 @@ def main():
     HF.set_precision("bf16")
     lib = _lib.load()
     arms = a.arm or ["", "0=0"]
-    base = {k: lib.dsgan_pw_tune(k, -1) for k in range(8)}
+    base = {k: lib.dsgan_pw_tune(k, -1) for k in range(12)}
     parsed = []
     for s in arms:
         kv = dict(base)
