@@ -299,6 +299,36 @@ __global__ void wtrans_bf16_kernel(const float* __restrict__ W, T16* __restrict_
   }
 }
 
+// Batched refresh of the 16-bit weight copies after an optimizer step (dsgan_wtrans_multi): entry
+// blockIdx.y, grid-stride over its elements; mode -1 is a plain fp32 -> 16-bit cast of the
+// parameter (bf16_weight), modes 0-2 the tap-major transforms of wtrans_bf16_kernel.
+struct WtEnt { const float* W; void* Wb; long total; int Co, Ci, KH, KW, mode; };
+constexpr int WT_MAXE = 48;
+struct WtList { WtEnt e[WT_MAXE]; };
+
+template <typename T16>
+__global__ __launch_bounds__(256) void wtrans_multi_kernel(WtList L) {
+  const WtEnt en = L.e[blockIdx.y];
+  T16* __restrict__ Wb = (T16*)en.Wb;
+  const float* __restrict__ W = en.W;
+  const long stride = (long)gridDim.x * 256;
+  if (en.mode < 0) {
+    for (long e = blockIdx.x * 256L + threadIdx.x; e < en.total; e += stride) Wb[e] = (T16)W[e];
+    return;
+  }
+  const int Co = en.Co, Ci = en.Ci, KH = en.KH, KW = en.KW, mode = en.mode;
+  const int M = mode == 0 ? Co : Ci, K = mode == 0 ? Ci : Co;
+  for (long e = blockIdx.x * 256L + threadIdx.x; e < en.total; e += stride) {
+    const int k = e % K;
+    const long t = e / K;
+    const int m = t % M, tap = t / M;
+    int kh = tap / KW, kw = tap % KW, co = m, ci = k;
+    if (mode == 1) { kh = KH - 1 - kh; kw = KW - 1 - kw; co = k; ci = m; }
+    if (mode == 2) { co = k; ci = m; }
+    Wb[e] = (T16)W[(((long)co * Ci + ci) * KH + kh) * KW + kw];
+  }
+}
+
 template <typename T16, int BM, int TH, int TW, int S, int KH, int KW>
 static void pc_launch(PcArgs& g, hipStream_t st) {
   g.tiles_w = (g.Wo + TW - 1) / TW;
@@ -349,6 +379,35 @@ int dsgan_conv_wtrans_bf16(const float* W, void* Wb, int Co, int Ci, int KH, int
                        mode);
   });
   DSG_CHECK_LAUNCH();
+  return 0;
+}
+
+// n weight copies in as few launches as possible: W[i] (fp32 [Co][Ci][KH][KW]) -> Wb[i] (16-bit), desc[5i..5i+4]
+// = (Co, Ci, KH, KW, mode), mode 0-2 as dsgan_conv_wtrans_bf16, -1 a plain cast of the Co*Ci*KH*KW elements.
+int dsgan_wtrans_multi(const void* const* W, void* const* Wb, const int* desc, int n, hipStream_t st) {
+  DSG_REQUIRE(W && Wb && desc && n >= 0, "dsgan_wtrans_multi: bad args");
+  for (int i0 = 0; i0 < n; i0 += WT_MAXE) {
+    WtList L{};
+    const int ne = n - i0 < WT_MAXE ? n - i0 : WT_MAXE;
+    long most = 1;
+    for (int i = 0; i < ne; ++i) {
+      const int* d = desc + 5 * (i0 + i);
+      DSG_REQUIRE(W[i0 + i] && Wb[i0 + i] && d[0] > 0 && d[1] > 0 && d[2] > 0 && d[3] > 0 && d[4] >= -1 && d[4] <= 2,
+                  "dsgan_wtrans_multi: bad entry %d", i0 + i);
+      WtEnt& e = L.e[i];
+      e.W = (const float*)W[i0 + i]; e.Wb = Wb[i0 + i];
+      e.Co = d[0]; e.Ci = d[1]; e.KH = d[2]; e.KW = d[3]; e.mode = d[4];
+      e.total = (long)d[0] * d[1] * d[2] * d[3];
+      if (e.total > most) most = e.total;
+    }
+    long bx = (most + 256L * 8 - 1) / (256L * 8);   // ~8 elements per thread on the largest entry
+    if (bx > 1024) bx = 1024;
+    with_half([&](auto* t_) {
+      using T16 = std::remove_pointer_t<decltype(t_)>;
+      hipLaunchKernelGGL((wtrans_multi_kernel<T16>), dim3((unsigned)bx, (unsigned)ne), dim3(256), 0, st, L);
+    });
+    DSG_CHECK_LAUNCH();
+  }
   return 0;
 }
 

@@ -12,6 +12,8 @@ weight-grad launch at all.
 import contextlib
 import math
 
+import ctypes
+
 import torch
 
 from . import _lib
@@ -204,14 +206,51 @@ _PARAM_GEN = {}
 
 def bump_weight_generation(params=None):
     """Invalidate cached weight transforms: of ``params`` (the ones an optimizer just updated),
-    or of every weight.  Frozen weights (VGG16) keep their bf16 / tap-major copies across steps."""
+    or of every weight.  Frozen weights (VGG16) keep their bf16 / tap-major copies across steps.
+    With ``params``, the 16-bit copies cached for them (bf16_weight, _wtrans_bf16) are rebuilt
+    right away, in place, by one batched launch (dsgan_wtrans_multi) instead of one launch per
+    copy at its next use."""
     if params is None:
         WEIGHT_GEN[0] += 1
     else:
         for p in params:
             _PARAM_GEN[id(p)] = _PARAM_GEN.get(id(p), 0) + 1
+        _refresh_half_copies(params)
     if len(_WT_CACHE) > 8192:
         _WT_CACHE.clear()
+
+
+def _refresh_half_copies(params):
+    ids = {id(p) for p in params}
+    todo = []   # (cache, key, entry, mode)
+    for cache in (_WT_CACHE, _BF16_CACHE):
+        for key, ent in cache.items():
+            w = ent[2]
+            if id(w) not in ids or key[1] != w.data_ptr() or ent[3].dtype == torch.float32:
+                continue
+            if cache is _WT_CACHE and len(key) != 5:   # (fp32 _wtrans entries are rebuilt lazily)
+                continue
+            if ent[3].dtype != half_dtype():
+                continue
+            todo.append((cache, key, ent, key[4] if cache is _WT_CACHE else -1))
+    if not todo:
+        return
+    n = len(todo)
+    src = (ctypes.c_void_p * n)(*[e[2][2].data_ptr() for e in todo])
+    dst = (ctypes.c_void_p * n)(*[e[2][3].data_ptr() for e in todo])
+    desc = []
+    for _, _, ent, mode in todo:
+        w = ent[2]
+        Co, Ci, KH, KW = (tuple(w.shape) + (1, 1, 1))[:4] if w.dim() < 4 else tuple(w.shape)
+        if mode < 0:   # plain cast: any shape, as a flat run of numel elements
+            Co, Ci, KH, KW = w.numel(), 1, 1, 1
+        desc += [Co, Ci, KH, KW, mode]
+    dsc = (ctypes.c_int * len(desc))(*desc)
+    call("dsgan_wtrans_multi", ctypes.cast(src, ctypes.c_void_p), ctypes.cast(dst, ctypes.c_void_p),
+         ctypes.cast(dsc, ctypes.c_void_p), n, stream())
+    for cache, key, ent, _ in todo:
+        w = ent[2]
+        cache[key] = (_wgen(w), w._version, w, ent[3])
 
 
 def _wgen(w):

@@ -247,6 +247,10 @@ int dsgan_tconv_ws_xh(const void* Xh, long x_bs, const void* Wt, const float* bi
 int dsgan_pconv_supported(int K, int KH, int KW, int stride);
 int dsgan_conv_wtrans_bf16(const float* W, void* Wb, int Co, int Ci, int KH, int KW, int mode,
                            hipStream_t stream);
+/* n 16-bit weight copies in one launch (per 48): W[i] fp32 [Co][Ci][KH][KW] -> Wb[i], desc[5i..5i+4] =
+ * (Co, Ci, KH, KW, mode): mode 0-2 as dsgan_conv_wtrans_bf16, -1 a plain cast (dsgan_f32_to_bf16).
+ * The optimizer step refreshes every cached copy of the parameters it updated with one call. */
+int dsgan_wtrans_multi(const void* const* W, void* const* Wb, const int* desc, int n, hipStream_t stream);
 int dsgan_pconv(const float* X, long x_bs, const void* Wb, const float* bias, float* Y, long y_bs,
                 const float* gpre, long gpre_bs, int nb, int K, int M, int H, int W, int Ho, int Wo,
                 int KH, int KW, int stride, int pad, int act, int gact, float slope, int accumulate,

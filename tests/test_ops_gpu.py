@@ -1059,3 +1059,34 @@ def test_pw_split_k(half, N, M, K, P):
     for k in ("g", "gp", "dz"):
         assert ((split[k] - ref[k]).abs() <= ref[k].abs() * 2 * _ulp(half) + 1e-3).all(), k
     HF.set_precision("fp32")
+
+
+@pytest.mark.parametrize("half", HALVES)
+def test_weight_copy_refresh_batched(half):
+    """bump_weight_generation(params) rebuilds every cached 16-bit copy of those parameters
+    (tap-major modes 0-2, plain casts) in one dsgan_wtrans_multi launch: bitwise equal to the
+    per-copy launches, and the cache then hits without a rebuild."""
+    from dsgan_hip import functional as HF
+    from dsgan_hip._lib import call, ptr, stream
+    HF.set_precision(half)
+    g = torch.Generator().manual_seed(11)
+    w4 = torch.nn.Parameter(torch.randn(96, 40, 3, 3, generator=g).to(DEV))
+    w4b = torch.nn.Parameter(torch.randn(64, 128, 4, 4, generator=g).to(DEV))
+    w2 = torch.nn.Parameter(torch.randn(300, 77, generator=g).to(DEV))
+    copies = [HF._wtrans_bf16(w4, m) for m in (0, 1, 2)] + [HF._wtrans_bf16(w4b, 1), HF.bf16_weight(w2)]
+    with torch.no_grad():   # an in-place optimizer update (the fused Adam is invisible to torch's versions)
+        for p in (w4, w4b, w2):
+            p.copy_(torch.randn(p.shape, generator=g).to(DEV))
+    HF.bump_weight_generation([w4, w4b, w2])
+    again = [HF._wtrans_bf16(w4, m) for m in (0, 1, 2)] + [HF._wtrans_bf16(w4b, 1), HF.bf16_weight(w2)]
+    assert all(a.data_ptr() == b.data_ptr() for a, b in zip(copies, again))   # refreshed in place, cache hits
+    ref = []
+    for w, m in ((w4, 0), (w4, 1), (w4, 2), (w4b, 1)):
+        wb = torch.empty(w.numel(), device=DEV, dtype=_hdt(half))
+        call("dsgan_conv_wtrans_bf16", ptr(w), ptr(wb), *w.shape, m, stream())
+        ref.append(wb)
+    ref.append(w2.detach().to(_hdt(half)))
+    torch.cuda.synchronize()
+    for a, b in zip(again, ref):
+        assert torch.equal(a.view(-1).view(torch.int16), b.view(-1).view(torch.int16))
+    HF.set_precision("fp32")

@@ -2,7 +2,7 @@
 set -o pipefail
 mkdir -p gpurun_out
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-timeout -k 10 400 python -u -m pytest tests/test_vgg_cb16_gpu.py tests/test_ops_gpu.py tests/test_pwf32_gpu.py -m gpu -x -q --timeout 120 --timeout-method thread -k "conv1 or pw or vgg" > gpurun_out/r3j_tests.log 2>&1 || { tail -30 gpurun_out/r3j_tests.log; exit 1; }
+timeout -k 10 400 python -u -m pytest tests/test_vgg_cb16_gpu.py tests/test_ops_gpu.py tests/test_pwf32_gpu.py -m gpu -x -q --timeout 120 --timeout-method thread -k "conv1 or pw or vgg or refresh" > gpurun_out/r3j_tests.log 2>&1 || { tail -30 gpurun_out/r3j_tests.log; exit 1; }
 tail -2 gpurun_out/r3j_tests.log
 timeout -k 10 400 python -u tools/pw_bench.py --only gp --arm "" --arm "8=0" --arm "7=1" --arm "7=3" --arm "6=1" --arm "6=2" > gpurun_out/r3j_pwbench.log 2>&1 || { tail -30 gpurun_out/r3j_pwbench.log; exit 1; }
 cat gpurun_out/r3j_pwbench.log
