@@ -743,6 +743,17 @@ __global__ __launch_bounds__(NW * 64, MINB) void mlp_bwd_kernel(MlpArgs g) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) hacc[i][t][r] = 0.f;
   __syncthreads();
+  // The B fragments of this wave's pixel column of h (all C channels) and dy (all P) are the same for
+  // every hidden chunk: read them from LDS once, keep them in registers (the z / t GEMMs then read only
+  // their weight A fragments per MFMA; same operands, same order -- same bits)
+  static_assert(ZG::TN == 1 && ZG::TM == 1, "one 32 x 32 z / t tile per wave");
+  mbf16x8 hbr[C / 16], dbr[P / 16];
+#pragma unroll
+  for (int ks = 0; ks < C / 16; ++ks)
+    hbr[ks] = mtr_frag(Hs + (ks * 16 + 8 * lh + tq) * HSTR + wn * (BN / ZG::WN) + 16 * tG + 4 * tp, HSTR);
+#pragma unroll
+  for (int ks = 0; ks < P / 16; ++ks)
+    dbr[ks] = mtr_frag(Ds + (ks * 16 + 8 * lh + tq) * HSTR + wn * (BN / ZG::WN) + 16 * tG + 4 * tp, HSTR);
 
   // copy-out block of this wave: hidden half (wave & 1), pixel blocks (wave >> 1) * CPW + c
   const int chh = (wave & 1) * 32;
@@ -761,35 +772,15 @@ __global__ __launch_bounds__(NW * 64, MINB) void mlp_bwd_kernel(MlpArgs g) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) { zacc[i][t][r] = bv[r]; tacc[i][t][r] = 0.f; }
     }
-#pragma unroll 4
+#pragma unroll
     for (int ks = 0; ks < C / 16; ++ks) {
-      mbf16x8 af[ZG::TM], bf[ZG::TN];
-#pragma unroll
-      for (int i = 0; i < ZG::TM; ++i)
-        af[i] = *reinterpret_cast<const mbf16x8*>(W1s + swz_off<C / 8>(wm * (HC / 2) + i * 32 + lr, ks * 16 + lh * 8));
-#pragma unroll
-      for (int t = 0; t < ZG::TN; ++t)
-        bf[t] = mtr_frag(Hs + (ks * 16 + 8 * lh + tq) * HSTR + wn * (BN / ZG::WN) + t * 32 + 16 * tG + 4 * tp, HSTR);
-#pragma unroll
-      for (int i = 0; i < ZG::TM; ++i)
-#pragma unroll
-        for (int t = 0; t < ZG::TN; ++t)
-          zacc[i][t] = mfma16(af[i], bf[t], zacc[i][t]);
+      const mbf16x8 af = *reinterpret_cast<const mbf16x8*>(W1s + swz_off<C / 8>(wm * (HC / 2) + lr, ks * 16 + lh * 8));
+      zacc[0][0] = mfma16(af, hbr[ks], zacc[0][0]);
     }
-#pragma unroll 4
-    for (int ks = 0; ks < P / 16; ++ks) {
-      mbf16x8 af[ZG::TM], bf[ZG::TN];
 #pragma unroll
-      for (int i = 0; i < ZG::TM; ++i)   // A[m][p] = W2[p][m]: W2s [P][W2STR] is k-major for this product
-        af[i] = mtr_frag_s<HC / 8>(W2s, ks * 16, wm * (HC / 2) + i * 32, lane);
-#pragma unroll
-      for (int t = 0; t < ZG::TN; ++t)
-        bf[t] = mtr_frag(Ds + (ks * 16 + 8 * lh + tq) * HSTR + wn * (BN / ZG::WN) + t * 32 + 16 * tG + 4 * tp, HSTR);
-#pragma unroll
-      for (int i = 0; i < ZG::TM; ++i)
-#pragma unroll
-        for (int t = 0; t < ZG::TN; ++t)
-          tacc[i][t] = mfma16(af[i], bf[t], tacc[i][t]);
+    for (int ks = 0; ks < P / 16; ++ks) {   // A[m][p] = W2[p][m]: W2s [P][W2STR] is k-major for this product
+      const mbf16x8 af = mtr_frag_s<HC / 8>(W2s, ks * 16, wm * (HC / 2), lane);
+      tacc[0][0] = mfma16(af, dbr[ks], tacc[0][0]);
     }
     // ---- epilogue: g = gelu(z), dz = t * gelu'(z) -> LDS, pixel-major, 4 hidden per write ----
 #pragma unroll

@@ -785,6 +785,79 @@ __global__ __launch_bounds__(256) void ca_bwd_kernel(const float* datt, const fl
 }
 
 // dx[n,c,:] += davg/HW ; dx[n,c,argmax] += dmax
+// 16-byte forms (HW % 4 == 0, 16-byte aligned planes): each lane walks its float4 groups in increasing
+// index order (4 loads in flight), the max / first-argmax update is branch-free with the scalar
+// kernel's rule (strict >, NaN wins and sticks), and the cross-lane reduction is the same.
+template <int NT>
+__global__ __launch_bounds__(256) void plane_stats4_kernel(const float* __restrict__ x, long x_bs, float* avg, float* mx,
+                                                           int* amax, int N, int C, int HW) {
+  __shared__ float shv[4];
+  __shared__ int shi[4];
+  __shared__ float shs[4];
+  const int ppb = 256 / NT;
+  const int plane = blockIdx.x * ppb + (NT == 64 ? (threadIdx.x >> 6) : 0);
+  const int t = NT == 64 ? (threadIdx.x & 63) : threadIdx.x;
+  if (plane >= N * C) return;
+  const int n = plane / C, c = plane - n * C;
+  const float4* xp = reinterpret_cast<const float4*>(x + (long)n * x_bs + (long)c * HW);
+  const int HW4 = HW >> 2;
+  float s = 0.f, best = -INFINITY;
+  int bi = 0x7fffffff;
+  auto upd = [&](float v, int i) {
+    const bool take = v > best || (isnan(v) && !isnan(best));
+    best = take ? v : best;
+    bi = take ? i : bi;
+  };
+#pragma unroll 4
+  for (int i4 = t; i4 < HW4; i4 += NT) {
+    const float4 v = xp[i4];
+    s += (v.x + v.y) + (v.z + v.w);
+    upd(v.x, 4 * i4); upd(v.y, 4 * i4 + 1); upd(v.z, 4 * i4 + 2); upd(v.w, 4 * i4 + 3);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float ov = __shfl_xor(best, o, 64);
+    const int oi = __shfl_xor(bi, o, 64);
+    const bool take = (ov > best) || (ov == best && oi < bi) || (isnan(ov) && (!isnan(best) || oi < bi));
+    if (take) { best = ov; bi = oi; }
+  }
+  s = warp_sum(s);
+  if (NT == 256) {
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) { shv[w] = best; shi[w] = bi; shs[w] = s; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      best = shv[0]; bi = shi[0]; s = shs[0];
+      for (int i = 1; i < 4; ++i) {
+        const bool take = (shv[i] > best) || (shv[i] == best && shi[i] < bi) ||
+                          (isnan(shv[i]) && (!isnan(best) || shi[i] < bi));
+        if (take) { best = shv[i]; bi = shi[i]; }
+        s += shs[i];
+      }
+    }
+  }
+  if (t == 0) { avg[plane] = s / (float)HW; mx[plane] = best; amax[plane] = bi; }
+}
+
+// dx (+)= davg / HW + (i == amax) dmx, four pixels of one plane per thread (HW % 4 == 0, aligned)
+__global__ __launch_bounds__(256) void plane_stats_bwd4_kernel(const float* __restrict__ davg, const float* __restrict__ dmx,
+                                                               const int* __restrict__ amax, float* __restrict__ dx,
+                                                               long dx_bs, int N, int C, int HW) {
+  const int HW4 = HW >> 2;
+  const long total4 = (long)N * C * HW4;
+  for (long e = blockIdx.x * 256L + threadIdx.x; e < total4; e += (long)gridDim.x * 256) {
+    const long pl = e / HW4;
+    const int i4 = (int)(e - pl * HW4);
+    const int c = (int)(pl % C), n = (int)(pl / C);
+    const float a = davg[pl] / (float)HW, m = dmx[pl];
+    const int am = amax[pl] - 4 * i4;
+    float4* o = reinterpret_cast<float4*>(dx + (long)n * dx_bs + (long)c * HW) + i4;
+    float4 v = *o;
+    v.x += am == 0 ? a + m : a; v.y += am == 1 ? a + m : a; v.z += am == 2 ? a + m : a; v.w += am == 3 ? a + m : a;
+    *o = v;
+  }
+}
+
 __global__ void plane_stats_bwd_kernel(const float* davg, const float* dmx, const int* amax,
                                        float* dx, long dx_bs, int N, int C, int HW) {
   const long total = (long)N * C * HW;
@@ -1124,7 +1197,12 @@ int dsgan_plane_stats(const float* x, long x_bs, float* avg, float* mx, int* ama
                       int HW, hipStream_t st) {
   DSG_REQUIRE(x && avg && mx && amax && HW > 0, "dsgan_plane_stats: bad args");
   const int planes = N * C;
-  if (HW <= 4096)
+  const bool v4 = (HW & 3) == 0 && (x_bs & 3) == 0 && (((uintptr_t)x) & 15) == 0;
+  if (v4 && HW <= 4096)
+    hipLaunchKernelGGL(plane_stats4_kernel<64>, dim3(cdiv(planes, 4)), dim3(256), 0, st, x, x_bs, avg, mx, amax, N, C, HW);
+  else if (v4)
+    hipLaunchKernelGGL(plane_stats4_kernel<256>, dim3(planes), dim3(256), 0, st, x, x_bs, avg, mx, amax, N, C, HW);
+  else if (HW <= 4096)
     hipLaunchKernelGGL(plane_stats_kernel<64>, dim3(cdiv(planes, 4)), dim3(256), 0, st, x, x_bs, avg, mx, amax, N, C, HW);
   else
     hipLaunchKernelGGL(plane_stats_kernel<256>, dim3(planes), dim3(256), 0, st, x, x_bs, avg, mx, amax, N, C, HW);
@@ -1135,8 +1213,12 @@ int dsgan_plane_stats(const float* x, long x_bs, float* avg, float* mx, int* ama
 int dsgan_plane_stats_bwd(const float* davg, const float* dmx, const int* amax, float* dx,
                           long dx_bs, int N, int C, int HW, hipStream_t st) {
   const long total = (long)N * C * HW;
-  hipLaunchKernelGGL(plane_stats_bwd_kernel, dim3(grid_for(total)), dim3(256), 0, st, davg, dmx,
-                     amax, dx, dx_bs, N, C, HW);
+  if ((HW & 3) == 0 && (dx_bs & 3) == 0 && (((uintptr_t)dx) & 15) == 0)
+    hipLaunchKernelGGL(plane_stats_bwd4_kernel, dim3(grid_for(total / 4)), dim3(256), 0, st, davg, dmx, amax, dx, dx_bs,
+                       N, C, HW);
+  else
+    hipLaunchKernelGGL(plane_stats_bwd_kernel, dim3(grid_for(total)), dim3(256), 0, st, davg, dmx,
+                       amax, dx, dx_bs, N, C, HW);
   DSG_CHECK_LAUNCH();
   return 0;
 }

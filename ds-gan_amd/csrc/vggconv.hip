@@ -321,6 +321,66 @@ __global__ __launch_bounds__(256) void vgg_conv1_dgrad_kernel(const T16* __restr
   o[2 * HW] = a2;
 }
 
+// conv1_1 data-grad, row-sliding form: a thread owns one column and R consecutive output rows and walks
+// the R + 2 input rows of d that feed them once each, keeping the three output rows an input row
+// touches (kh = 0, 1, 2) in registers.  The 27 weights of one output channel co (w[co][ci][kh][kw], 27
+// contiguous floats) are wave-uniform: they come through the scalar cache as SGPR operands of the
+// FMAs (the per-pixel kernel spent one LDS read per FMA: 1728 per pixel).
+template <typename T16, int R>
+__global__ __launch_bounds__(256) void vgg_conv1_dgrad_rows_kernel(const T16* __restrict__ d, const float* __restrict__ w,
+                                                                   float* __restrict__ dx, long dx_bs, int N, int H, int W) {
+  typedef hx8<T16> vgb8;
+  const int wt = (W + 255) / 256, ht = (H + R - 1) / R;
+  int b = blockIdx.x;
+  const int wb = b % wt;
+  b /= wt;
+  const int hb = b % ht, n = b / ht;
+  const int wc = wb * 256 + threadIdx.x, h0 = hb * R;
+  if (wc >= W) return;
+  const long HW = (long)H * W;
+  float a0[3] = {0.f, 0.f, 0.f}, a1[3] = {0.f, 0.f, 0.f}, a2[3] = {0.f, 0.f, 0.f};   // rows ih-1, ih, ih+1
+  float* o = dx + (long)n * dx_bs + wc;
+  const bool lv = wc >= 1, rv = wc + 1 < W;   // iw = wc + 1 - kw in range for kw = 2 / kw = 0
+  for (int ih = h0 - 1; ih <= h0 + R; ++ih) {
+    if (ih >= 0 && ih < H) {
+#pragma unroll 1
+      for (int cb = 0; cb < 4; ++cb) {
+        vgb8 u[3][2];
+#pragma unroll
+        for (int kw = 0; kw < 3; ++kw) {
+          const int iw = wc + 1 - kw;
+          const bool ok = kw == 1 || (kw == 0 ? rv : lv);
+          const vgb8* p = reinterpret_cast<const vgb8*>(d + cb16(n, cb * 16, ih, ok ? iw : wc, 64, H, W));
+          u[kw][0] = p[0];
+          u[kw][1] = p[1];
+          if (!ok) { u[kw][0] = vgb8{}; u[kw][1] = vgb8{}; }
+        }
+        const float* wcb = w + cb * 16 * 27;   // w[co][ci][kh][kw], co = cb * 16 + c
+#pragma unroll
+        for (int c = 0; c < 16; ++c) {
+#pragma unroll
+          for (int kw = 0; kw < 3; ++kw) {
+            const float g = (float)(c < 8 ? u[kw][0][c] : u[kw][1][c - 8]);
+#pragma unroll
+            for (int ci = 0; ci < 3; ++ci) {
+              a0[ci] = fmaf(wcb[c * 27 + ci * 9 + 0 * 3 + kw], g, a0[ci]);   // kh = 0 -> output row ih - 1
+              a1[ci] = fmaf(wcb[c * 27 + ci * 9 + 1 * 3 + kw], g, a1[ci]);   // kh = 1 -> row ih
+              a2[ci] = fmaf(wcb[c * 27 + ci * 9 + 2 * 3 + kw], g, a2[ci]);   // kh = 2 -> row ih + 1
+            }
+          }
+        }
+      }
+    }
+    const int h = ih - 1;   // complete after input row ih
+    if (h >= h0 && h < H) {
+#pragma unroll
+      for (int ci = 0; ci < 3; ++ci) o[ci * HW + (long)h * W] = a0[ci];
+    }
+#pragma unroll
+    for (int ci = 0; ci < 3; ++ci) { a0[ci] = a1[ci]; a1[ci] = a2[ci]; a2[ci] = 0.f; }
+  }
+}
+
 // MaxPool2d(2) of an fp32 CB16 feature -> bf16 CB16 + window argmax (dh*2 + dw, first max wins as
 // in torch).  Thread = (output pixel, 4 channels).
 template <typename T16>
@@ -501,8 +561,11 @@ int dsgan_vgg_conv1_dgrad(const void* d, const float* w, float* dx, long dx_bs, 
   const long total = (long)N * H * W;
   with_half([&](auto* t_) {
     using T16 = std::remove_pointer_t<decltype(t_)>;
-    hipLaunchKernelGGL((vgg_conv1_dgrad_kernel<T16>), dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st,
-                       (const T16*)d, w, dx, dx_bs, N, H, W);
+    constexpr int R = 4;
+    const long blocks = (long)N * ((H + R - 1) / R) * ((W + 255) / 256);
+    hipLaunchKernelGGL((vgg_conv1_dgrad_rows_kernel<T16, R>), dim3((unsigned)blocks), dim3(256), 0, st, (const T16*)d, w,
+                       dx, dx_bs, N, H, W);
+    (void)total;
   });
   DSG_CHECK_LAUNCH();
   return 0;

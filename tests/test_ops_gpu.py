@@ -1090,3 +1090,41 @@ def test_weight_copy_refresh_batched(half):
     for a, b in zip(again, ref):
         assert torch.equal(a.view(-1).view(torch.int16), b.view(-1).view(torch.int16))
     HF.set_precision("fp32")
+
+
+@pytest.mark.parametrize("shape", [(2, 3, 80, 80), (2, 5, 7, 9), (2, 4, 64, 64), (3, 6, 16, 16)])
+def test_plane_stats_fwd_bwd(shape):
+    """Channel-attention plane statistics (CA avg/max pool, MixConvNeXtML.py:5-22): mean, max and the
+    FIRST argmax (torch's tie rule; a NaN wins and sticks) of every (n, c) plane, 16-byte and scalar
+    forms; the backward dx += davg/HW + (i == argmax) dmx."""
+    from dsgan_hip._lib import call, ptr, stream
+    N, C, H, W = shape
+    HW = H * W
+    g = torch.Generator().manual_seed(HW + C)
+    x = torch.randn(N, C, H, W, generator=g)
+    x[0, 0].view(-1)[[5, HW - 3]] = 7.0                  # tie: the first index wins
+    x[1, C - 1].view(-1)[[HW // 2, HW // 2 + 1]] = float("nan")
+    xd = x.to(DEV)
+    avg = torch.empty(N * C, device=DEV)
+    mx = torch.empty(N * C, device=DEV)
+    am = torch.empty(N * C, device=DEV, dtype=torch.int32)
+    call("dsgan_plane_stats", ptr(xd), C * HW, ptr(avg), ptr(mx), ptr(am), N, C, HW, stream())
+    davg = torch.randn(N * C, generator=g)
+    dmx = torch.randn(N * C, generator=g)
+    dx0 = torch.randn(N, C, H, W, generator=g)
+    dx = dx0.to(DEV)
+    dd, dm = davg.to(DEV), dmx.to(DEV)
+    call("dsgan_plane_stats_bwd", ptr(dd), ptr(dm), ptr(am), ptr(dx), C * HW, N, C, HW, stream())
+    torch.cuda.synchronize()
+    flat = x.view(N * C, HW)
+    ref_mx, ref_am = flat.max(dim=1)
+    nan_rows = torch.isnan(flat).any(dim=1)
+    assert torch.equal(am.cpu()[~nan_rows].long(), ref_am[~nan_rows])
+    assert torch.equal(mx.cpu()[~nan_rows], ref_mx[~nan_rows])
+    for r in torch.nonzero(nan_rows).view(-1).tolist():   # first NaN index, value NaN
+        assert torch.isnan(mx.cpu()[r]) and am.cpu()[r].item() == int(torch.nonzero(torch.isnan(flat[r]))[0])
+    ok = ~nan_rows
+    assert torch.allclose(avg.cpu()[ok], flat[ok].double().mean(dim=1).float(), rtol=1e-5, atol=1e-6)
+    ref_dx = dx0.view(N * C, HW) + (davg / HW).view(-1, 1)
+    ref_dx[torch.arange(N * C), am.cpu().long()] += dmx
+    assert torch.allclose(dx.cpu().view(N * C, HW), ref_dx, rtol=1e-6, atol=1e-6)
