@@ -1068,16 +1068,31 @@ __global__ __launch_bounds__(NW * 64, MINB) void mlp_wgrad_kernel(MlpArgs g) {
       }
     __syncthreads();
     // ---- dW1[j] += dz h^T  (A = dz [hidden][px] transposed from Zn, B = h^T row-wise from Hs) ----
+    if constexpr (T1::KS == 1 && NW % T1::MT == 0) {
+      // the wave's TPW tiles (wave + NW q) share one row tile mt: one A fragment per k step for all of them
+      const int mt = wave % T1::MT;
 #pragma unroll
-    for (int q = 0; q < T1::TPW; ++q) {
-      const int ti = T1::KS == 1 ? wave + NW * q : wave % T1::T;
-      const int kp = T1::KS == 1 ? 0 : wave / T1::T;
-      const int mt = ti % T1::MT, nt = ti / T1::MT;
-#pragma unroll
-      for (int ks = kp * (BN / 16 / T1::KS); ks < (kp + 1) * (BN / 16 / T1::KS); ++ks) {
+      for (int ks = 0; ks < BN / 16; ++ks) {
         const mbf16x8 af = mtr_frag_s<HC / 8>(Zn, ks * 16, mt * 32, lane);
-        const mbf16x8 bf = *reinterpret_cast<const mbf16x8*>(Hs + swz_off<BN / 8>(nt * 32 + lr, ks * 16 + lh * 8));
-        a1[q] = mfma16(af, bf, a1[q]);
+#pragma unroll
+        for (int q = 0; q < T1::TPW; ++q) {
+          const int nt = (wave + NW * q) / T1::MT;
+          const mbf16x8 bf = *reinterpret_cast<const mbf16x8*>(Hs + swz_off<BN / 8>(nt * 32 + lr, ks * 16 + lh * 8));
+          a1[q] = mfma16(af, bf, a1[q]);
+        }
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < T1::TPW; ++q) {
+        const int ti = T1::KS == 1 ? wave + NW * q : wave % T1::T;
+        const int kp = T1::KS == 1 ? 0 : wave / T1::T;
+        const int mt = ti % T1::MT, nt = ti / T1::MT;
+#pragma unroll
+        for (int ks = kp * (BN / 16 / T1::KS); ks < (kp + 1) * (BN / 16 / T1::KS); ++ks) {
+          const mbf16x8 af = mtr_frag_s<HC / 8>(Zn, ks * 16, mt * 32, lane);
+          const mbf16x8 bf = *reinterpret_cast<const mbf16x8*>(Hs + swz_off<BN / 8>(nt * 32 + lr, ks * 16 + lh * 8));
+          a1[q] = mfma16(af, bf, a1[q]);
+        }
       }
     }
     // ---- dW2[:, j] += dy g^T  (A = dy row-wise from Ds, B = g^T transposed from Gn) ----

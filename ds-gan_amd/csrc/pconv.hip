@@ -316,16 +316,22 @@ __global__ __launch_bounds__(256) void wtrans_multi_kernel(WtList L) {
     for (long e = blockIdx.x * 256L + threadIdx.x; e < en.total; e += stride) Wb[e] = (T16)W[e];
     return;
   }
+  // thread = one (m, k) pair, all taps: it reads the KH*KW contiguous source floats of (co, ci) and
+  // writes one element per tap plane -- adjacent lanes take adjacent k, so every tap's writes are
+  // coalesced and each lane's reads share one or two cache lines (per-element threads read one
+  // float per line)
   const int Co = en.Co, Ci = en.Ci, KH = en.KH, KW = en.KW, mode = en.mode;
-  const int M = mode == 0 ? Co : Ci, K = mode == 0 ? Ci : Co;
-  for (long e = blockIdx.x * 256L + threadIdx.x; e < en.total; e += stride) {
-    const int k = e % K;
-    const long t = e / K;
-    const int m = t % M, tap = t / M;
-    int kh = tap / KW, kw = tap % KW, co = m, ci = k;
-    if (mode == 1) { kh = KH - 1 - kh; kw = KW - 1 - kw; co = k; ci = m; }
-    if (mode == 2) { co = k; ci = m; }
-    Wb[e] = (T16)W[(((long)co * Ci + ci) * KH + kh) * KW + kw];
+  const int M = mode == 0 ? Co : Ci, K = mode == 0 ? Ci : Co, T = KH * KW;
+  const long pairs = (long)M * K, plane = pairs;
+  for (long e = blockIdx.x * 256L + threadIdx.x; e < pairs; e += stride) {
+    const int k = (int)(e % K), m = (int)(e / K);
+    const int co = mode == 0 ? m : k, ci = mode == 0 ? k : m;
+    const float* src = W + ((long)co * Ci + ci) * T;
+    for (int tap = 0; tap < T; ++tap) {
+      int kh = tap / KW, kw = tap - (tap / KW) * KW;
+      if (mode == 1) { kh = KH - 1 - kh; kw = KW - 1 - kw; }
+      Wb[(long)tap * plane + e] = (T16)src[kh * KW + kw];
+    }
   }
 }
 
@@ -400,7 +406,7 @@ int dsgan_wtrans_multi(const void* const* W, void* const* Wb, const int* desc, i
       e.total = (long)d[0] * d[1] * d[2] * d[3];
       if (e.total > most) most = e.total;
     }
-    long bx = (most + 256L * 8 - 1) / (256L * 8);   // ~8 elements per thread on the largest entry
+    long bx = (most + 256L * 8 - 1) / (256L * 8);   // ~8 elements (casts) / tap rows per thread at most
     if (bx > 1024) bx = 1024;
     with_half([&](auto* t_) {
       using T16 = std::remove_pointer_t<decltype(t_)>;
