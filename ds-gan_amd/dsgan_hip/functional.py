@@ -297,6 +297,12 @@ def _pw_ws(M, N, P, nb, like):
     return torch.empty(n, device=like.device, dtype=torch.float32) if n > 0 else None
 
 
+def _pw_io_ok(K, P, xbs, ybs, x, y, pre=None, pbs=0):
+    """dsgan_pw_fwd_io / dgrad_io alignment rules with fp32 activations (16-bit weight rows: K % 8)."""
+    return (K % 8 == 0 and P % 128 == 0 and xbs % 8 == 0 and ybs % 8 == 0 and x.data_ptr() % 16 == 0
+            and y.data_ptr() % 16 == 0 and (pre is None or (pbs % 4 == 0 and pre.data_ptr() % 16 == 0)))
+
+
 def _pw_fd_ws(mode, M, K, P, nb, like):
     """Split-K scratch of an under-filled pointwise FWD (0) / DGRAD (1) (dsgan_pw_fd_workspace), or None."""
     n = _lib.load().dsgan_pw_fd_workspace(mode, M, K, P, nb)
@@ -369,9 +375,16 @@ def conv_fwd_raw(x, w, b, stride, pad, act=None, out=None, pre=None, accumulate=
              N, Cin, Cout, H, W, Ho, Wo, KH, KW, stride, pad, 0, ACT[act], LRELU_SLOPE, int(accumulate), stream())
     elif KH == 1 and KW == 1 and stride == 1 and pad == 0 and _pw_ok(0, Cout, Cin, H * W, 0, xbs, w.data_ptr(), x.data_ptr()):
         fam = "pwgemm_kernel"
-        call("dsgan_pw_gemm", 0, ptr(w), 0, ptr(x), xbs, ptr(y), ybs, ptr(b), ptr(pre), pbs, None, 0,
-             Cout, N * H * W, Cin, H * W, N, ACT[act], 0, ACT[xact], int(accumulate), LRELU_SLOPE,
-             ptr(_pw_fd_ws(0, Cout, Cin, H * W, N, x)), stream())
+        if xact is None and _pw_io_ok(Cin, H * W, xbs, ybs, x, y, pre, pbs):
+            # the cached 16-bit weight copy instead of converting the fp32 weight tile in every
+            # workgroup (the same RNE rounding: the same bits)
+            call("dsgan_pw_fwd_io_ws", ptr(bf16_weight(w)), 1, ptr(x), xbs, 0, ptr(y), ybs, 0, ptr(pre), pbs, 0,
+                 ptr(b), Cout, Cin, H * W, N, ACT[act], int(accumulate), LRELU_SLOPE,
+                 ptr(_pw_fd_ws(0, Cout, Cin, H * W, N, x)), stream())
+        else:
+            call("dsgan_pw_gemm", 0, ptr(w), 0, ptr(x), xbs, ptr(y), ybs, ptr(b), ptr(pre), pbs, None, 0,
+                 Cout, N * H * W, Cin, H * W, N, ACT[act], 0, ACT[xact], int(accumulate), LRELU_SLOPE,
+                 ptr(_pw_fd_ws(0, Cout, Cin, H * W, N, x)), stream())
     elif (KH == 1 and KW == 1 and stride == 1 and pad == 0 and pre is None and xact is None
           and _pwf_ok(0, Cout, Cin, H * W, 0, xbs, w.data_ptr(), x.data_ptr())):
         fam = "pwf32_kernel"
@@ -433,9 +446,13 @@ def conv_dgrad_raw(dy, w, x_shape, stride, pad, bias=None, act=None, gpre=None, 
     elif (KH == 1 and KW == 1 and stride == 1 and pad == 0 and bias is None and act is None
             and _pw_ok(1, Cin, Cout, H * W, 0, dybs, w.data_ptr(), dy.data_ptr())):
         fam = "pwgemm_kernel"
-        call("dsgan_pw_gemm", 1, ptr(w), 0, ptr(dy), dybs, ptr(dx), dxbs, None, None, 0, ptr(gpre), gbs,
-             Cin, N * H * W, Cout, H * W, N, 0, ACT[gact], 0, int(accumulate), LRELU_SLOPE,
-             ptr(_pw_fd_ws(1, Cin, Cout, H * W, N, dy)), stream())
+        if gpre is None and Cin % 8 == 0 and _pw_io_ok(Cout, H * W, dybs, dxbs, dy, dx):
+            call("dsgan_pw_dgrad_io_ws", ptr(bf16_weight(w)), 1, ptr(dy), dybs, 0, ptr(dx), dxbs, 0, None, 0, Cin,
+                 Cout, H * W, N, int(accumulate), ptr(_pw_fd_ws(1, Cin, Cout, H * W, N, dy)), stream())
+        else:
+            call("dsgan_pw_gemm", 1, ptr(w), 0, ptr(dy), dybs, ptr(dx), dxbs, None, None, 0, ptr(gpre), gbs,
+                 Cin, N * H * W, Cout, H * W, N, 0, ACT[gact], 0, int(accumulate), LRELU_SLOPE,
+                 ptr(_pw_fd_ws(1, Cin, Cout, H * W, N, dy)), stream())
     elif (KH == 1 and KW == 1 and stride == 1 and pad == 0 and bias is None and act is None
             and _pwf_ok(1, Cin, Cout, H * W, 0, dybs, w.data_ptr(), dy.data_ptr())):
         fam = "pwf32_kernel"
