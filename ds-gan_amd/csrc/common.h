@@ -10,6 +10,9 @@ namespace dsg {
 void launch_split_reduce(const float* ws, int splits, long MN, float* dw, hipStream_t st);
 // ... with elements e = (c, i), i < KK1: i < KK1-1 -> dw[c*(KK1-1)+i], i == KK1-1 -> db[c]
 void launch_split_reduce_kk(const float* ws, int splits, long MN, float* dw, float* db, int KK1, hipStream_t st);
+// n (<= 4) independent reductions in one launch when none needs the many-split pre-pass (same bits)
+void launch_split_reduce_multi(int n, const float* const* ws, const int* splits, const long* MN, float* const* dw,
+                               hipStream_t st);
 
 
 // ---- 16-bit MFMA operand type ------------------------------------------------------------

@@ -1317,9 +1317,11 @@ int dsgan_mlp_wgrad(const void* h, long h_bs, int h_bf16, const float* dy, long 
   });
   DSG_CHECK_LAUNCH();
   const long n1 = 4L * C * C, n2 = (long)P * 4 * C;
-  launch_split_reduce(ws, S, n1, dw1, st);
-  launch_split_reduce(ws + S * n1, S, n2, dw2, st);
-  launch_split_reduce(ws + S * (n1 + n2), S, 4L * C, db1, st);
+  const float* wsv[3] = {ws, ws + S * n1, ws + S * (n1 + n2)};
+  const int sv[3] = {S, S, S};
+  const long mv[3] = {n1, n2, 4L * C};
+  float* dv[3] = {dw1, dw2, db1};
+  launch_split_reduce_multi(3, wsv, sv, mv, dv, st);
   DSG_CHECK_LAUNCH();
   return 0;
 }

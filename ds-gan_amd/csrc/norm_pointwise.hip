@@ -1241,9 +1241,17 @@ int dsgan_ca_bwd(const float* datt, const float* att, const float* avg, const fl
   const size_t shm = (C + 3 * R) * sizeof(float);
   hipLaunchKernelGGL(ca_bwd_kernel, dim3(N), dim3(256), shm, st, datt, att, avg, mx, hsave, w1, w2,
                      prelu_a, davg, dmx, ws, dw1 != nullptr, dw2 != nullptr, dprelu_a != nullptr, C, R);
-  if (dw1) launch_split_reduce(ws, N, (long)R * C, dw1, st);
-  if (dw2) launch_split_reduce(ws + (long)N * R * C, N, (long)C * R, dw2, st);
-  if (dprelu_a) launch_split_reduce(ws + 2L * N * R * C, N, 1, dprelu_a, st);
+  {   // the three parameter-grad reductions in one launch
+    const float* wsv[3];
+    int sv[3];
+    long mv[3];
+    float* dv[3];
+    int n = 0;
+    if (dw1) { wsv[n] = ws; sv[n] = N; mv[n] = (long)R * C; dv[n] = dw1; ++n; }
+    if (dw2) { wsv[n] = ws + (long)N * R * C; sv[n] = N; mv[n] = (long)C * R; dv[n] = dw2; ++n; }
+    if (dprelu_a) { wsv[n] = ws + 2L * N * R * C; sv[n] = N; mv[n] = 1; dv[n] = dprelu_a; ++n; }
+    if (n) launch_split_reduce_multi(n, wsv, sv, mv, dv, st);
+  }
   DSG_CHECK_LAUNCH();
   return 0;
 }

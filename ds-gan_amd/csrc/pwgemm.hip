@@ -100,12 +100,13 @@ static void wg_dispatch(const PwArgs& g, int bm, int abf, int bbf, int splits, h
 // (c, i) = (e / KK1, e % KK1) and goes to dw[c*(KK1-1) + i] (i < KK1-1) or db[c] (depthwise
 // weight + bias partial vectors, dwconv.hip).
 template <int J>
-__global__ __launch_bounds__(256) void split_reduce_kernel(const float* __restrict__ ws, int S, long MN, long rs,
-                                                           float* __restrict__ dw, float* __restrict__ db, int KK1) {
+__device__ __forceinline__ void split_reduce_body(const float* __restrict__ ws, int S, long MN, long rs,
+                                                  float* __restrict__ dw, float* __restrict__ db, int KK1, int blk,
+                                                  float* shm) {
   constexpr int EL = 256 / J;
-  __shared__ float sh[J][EL + 1];
+  float (*sh)[EL + 1] = reinterpret_cast<float (*)[EL + 1]>(shm);
   const int el = threadIdx.x % EL, j = threadIdx.x / EL;
-  const long e = (long)blockIdx.x * EL + el;
+  const long e = (long)blk * EL + el;
   float a = 0.f;
   if (e < MN) {
     int s = j;
@@ -131,17 +132,23 @@ __global__ __launch_bounds__(256) void split_reduce_kernel(const float* __restri
     }
   }
 }
+template <int J>
+__global__ __launch_bounds__(256) void split_reduce_kernel(const float* __restrict__ ws, int S, long MN, long rs,
+                                                           float* __restrict__ dw, float* __restrict__ db, int KK1) {
+  __shared__ float sh[J * (256 / J + 1)];
+  split_reduce_body<J>(ws, S, MN, rs, dw, db, KK1, blockIdx.x, sh);
+}
 
 // The same reduction on 16-byte element groups (KK1 == 0, MN % 4 == 0, 16-byte aligned rows): a
 // lane sums four consecutive elements per load, so a wave reads 4 rows x 256 B instead of 4 rows x
 // 64 B per instruction; the per-element order of additions is the scalar kernel's (same bits).
 template <int J>
-__global__ __launch_bounds__(256) void split_reduce4_kernel(const float* __restrict__ ws, int S, long MN, long rs,
-                                                            float* __restrict__ dw) {
+__device__ __forceinline__ void split_reduce4_body(const float* __restrict__ ws, int S, long MN, long rs,
+                                                   float* __restrict__ dw, int blk, float4* shm) {
   constexpr int EL = 256 / J;
-  __shared__ float4 sh[J][EL + 1];
+  float4 (*sh)[EL + 1] = reinterpret_cast<float4 (*)[EL + 1]>(shm);
   const int el = threadIdx.x % EL, j = threadIdx.x / EL;
-  const long e = ((long)blockIdx.x * EL + el) * 4;
+  const long e = ((long)blk * EL + el) * 4;
   float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
   auto add = [](float4& x, const float4 v) { x.x += v.x; x.y += v.y; x.z += v.z; x.w += v.w; };
   if (e < MN) {
@@ -165,6 +172,33 @@ __global__ __launch_bounds__(256) void split_reduce4_kernel(const float* __restr
     float4 o = *d;
     add(o, t);
     *d = o;
+  }
+}
+template <int J>
+__global__ __launch_bounds__(256) void split_reduce4_kernel(const float* __restrict__ ws, int S, long MN, long rs,
+                                                            float* __restrict__ dw) {
+  __shared__ float4 sh[J * (256 / J + 1)];
+  split_reduce4_body<J>(ws, S, MN, rs, dw, blockIdx.x, sh);
+}
+
+// Up to RS_MAX independent reductions (KK1 == 0, no pre-pass) in ONE launch: segment i owns blocks
+// [b0[i], b0[i+1]) and runs exactly the body (form and J) its own launch would (same bits).
+constexpr int RS_MAX = 4;
+struct RSeg { const float* ws; float* dw; long MN; int S; int form; int b0; };   // form: 0..3 = (v4, J=16)
+struct RSegs { RSeg s[RS_MAX + 1]; int n; };
+__global__ __launch_bounds__(256) void split_reduce_multi_kernel(RSegs R) {
+  __shared__ float4 sh[16 * (256 / 16 + 1)];
+  int i = 0;
+#pragma unroll
+  for (int q = 1; q < RS_MAX; ++q)
+    if (q < R.n && (int)blockIdx.x >= R.s[q].b0) i = q;
+  const RSeg g = R.s[i];
+  const int blk = blockIdx.x - g.b0;
+  switch (g.form) {
+    case 3: split_reduce4_body<16>(g.ws, g.S, g.MN, g.MN, g.dw, blk, sh); break;
+    case 2: split_reduce4_body<4>(g.ws, g.S, g.MN, g.MN, g.dw, blk, sh); break;
+    case 1: split_reduce_body<16>(g.ws, g.S, g.MN, g.MN, g.dw, nullptr, 0, blk, reinterpret_cast<float*>(sh)); break;
+    default: split_reduce_body<4>(g.ws, g.S, g.MN, g.MN, g.dw, nullptr, 0, blk, reinterpret_cast<float*>(sh)); break;
   }
 }
 
@@ -236,6 +270,30 @@ void launch_split_reduce(const float* ws, int splits, long MN, float* dw, hipStr
   launch_split_reduce_kk(ws, splits, MN, dw, nullptr, 0, st);
 }
 
+// n reductions dw_i[e] += sum_s ws_i[s][e] (fixed order) in one launch where none needs the pre-pass
+// (each is then exactly its launch_split_reduce body); otherwise one launch each.
+void launch_split_reduce_multi(int n, const float* const* ws, const int* splits, const long* MN, float* const* dw,
+                               hipStream_t st) {
+  RSegs R{};
+  bool ok = n >= 1 && n <= RS_MAX;
+  int b = 0;
+  for (int i = 0; ok && i < n; ++i) {
+    if (splits[i] > 64 && MN[i] < 65536) { ok = false; break; }
+    const bool v4 = (MN[i] & 3) == 0 && ((((uintptr_t)ws[i]) | ((uintptr_t)dw[i])) & 15) == 0;
+    const bool j16 = splits[i] > 8;
+    const int form = (v4 ? 2 : 0) + (j16 ? 1 : 0);
+    const long blocks = v4 ? (j16 ? (MN[i] + 63) / 64 : (MN[i] + 255) / 256) : (j16 ? (MN[i] + 15) / 16 : (MN[i] + 63) / 64);
+    R.s[i] = RSeg{ws[i], dw[i], MN[i], splits[i], form, b};
+    b += (int)blocks;
+  }
+  if (!ok) {
+    for (int i = 0; i < n; ++i) launch_split_reduce(ws[i], splits[i], MN[i], dw[i], st);
+    return;
+  }
+  R.n = n;
+  hipLaunchKernelGGL(split_reduce_multi_kernel, dim3((unsigned)b), dim3(256), 0, st, R);
+}
+
 // 64-deep K steps for the 128-row weight-grad tiles (knob 5): re-plan the pixel split on 64-pixel steps
 static int wgrad_cfg_k(PwArgs& g, bool any_bf16, int* bm) {
   int splits = wgrad_cfg(g, any_bf16, bm);
@@ -249,8 +307,12 @@ static int wgrad_cfg_k(PwArgs& g, bool any_bf16, int* bm) {
 
 static void wgrad_finish(const PwArgs& g, int splits, hipStream_t st) {
   if (splits > 1) {
-    launch_split_reduce(g.ws, splits, (long)g.M * g.N, g.Y, st);
-    if (g.asum) launch_split_reduce(g.ws + (long)splits * g.M * g.N, splits, g.M, g.asum, st);
+    // the weight and bias-sum partials in one launch
+    const float* wsv[2] = {g.ws, g.ws + (long)splits * g.M * g.N};
+    const int sv[2] = {splits, splits};
+    const long mv[2] = {(long)g.M * g.N, (long)g.M};
+    float* dv[2] = {g.Y, g.asum};
+    launch_split_reduce_multi(g.asum ? 2 : 1, wsv, sv, mv, dv, st);
   }
 }
 
