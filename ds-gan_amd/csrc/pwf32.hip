@@ -30,6 +30,8 @@ struct PfArgs {
   int k_split;
   float* ws;
   unsigned a_range, b_range;   // buffer-resource byte ranges (B: per image for FWD/DGRAD)
+  float* asum;                 // WGRAD (nullable): the bias grad asum[m] += sum_k DY[m][k], from the staged
+                               // A tiles (split partials after the S*M*N weight partials)
 };
 
 constexpr int FBK = 16;           // K per main-loop step (8 MFMA k-pairs)
@@ -78,6 +80,9 @@ __global__ __launch_bounds__(256, 2) void pwf32_kernel(PfArgs g) {
     return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 0));
   };
   float4 ra[A_ITEMS], rb[B_ITEMS];
+  float asr[A_ITEMS];   // WGRAD asum: this thread's running row sums of its A items (fixed order)
+#pragma unroll
+  for (int i = 0; i < A_ITEMS; ++i) asr[i] = 0.f;
   auto gload = [&](int kt) {
     const int kb = kbeg + kt * FBK;
     // WGRAD: a 16-pixel K step lies inside one image (P % 16 == 0)
@@ -126,6 +131,7 @@ __global__ __launch_bounds__(256, 2) void pwf32_kernel(PfArgs g) {
       } else {
         float* d = As + (it >> 2) * A_STR + (it & 3) * 4;
         d[0] = ra[i].x; d[1] = ra[i].y; d[2] = ra[i].z; d[3] = ra[i].w;
+        if (MODE == PF_WGRAD && g.asum) asr[i] += (ra[i].x + ra[i].y) + (ra[i].z + ra[i].w);
       }
     }
 #pragma unroll
@@ -182,6 +188,21 @@ __global__ __launch_bounds__(256, 2) void pwf32_kernel(PfArgs g) {
 
   // ---- epilogue: C layout col = lane & 31, row = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5) ----
   if (MODE == PF_WGRAD) {
+    if (g.asum) {
+      // a row's 4 items (16 pixels) are adjacent lanes: butterfly over them; the n-tile-0 workgroup
+      // writes (its split's partial, or asum += when unsplit)
+#pragma unroll
+      for (int i = 0; i < A_ITEMS; ++i) {
+        float t = asr[i];
+        t += __shfl_xor(t, 1, 64);
+        t += __shfl_xor(t, 2, 64);
+        const int it = tid + i * 256, m = m0 + (it >> 2);
+        if (n_t == 0 && (it & 3) == 0 && m < g.M) {
+          if (g.ws) g.ws[(long)gridDim.x / mt / nt * g.M * g.N + (long)split * g.M + m] = t;
+          else g.asum[m] += t;
+        }
+      }
+    }
     float* dst = g.ws ? g.ws + (long)split * g.M * g.N : g.Y;   // one split: the only writer, +=
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
@@ -295,7 +316,7 @@ int dsgan_pw_f32_supported(int mode, int M, int K, int P, long a_bs, long b_bs, 
 long dsgan_pw_f32_wgrad_workspace(int M, int N, int P, int nb) {
   int ks;
   const int splits = pf_wgrad_plan(M, N, (long)nb * P, &ks);
-  return splits > 1 ? (long)splits * M * N : 0;
+  return splits > 1 ? (long)splits * ((long)M * N + M) : 0;   // weight partials, then bias-sum partials
 }
 
 // Same argument meaning as dsgan_pw_gemm (mode 0 FWD / 1 DGRAD / 2 WGRAD), fp32 operands.
@@ -323,10 +344,18 @@ int dsgan_pw_gemm_f32(int mode, const float* A, long a_bs, const float* B, long 
     const int splits = pf_wgrad_plan(M, N, g.K, &g.k_split);
     DSG_REQUIRE(splits == 1 || ws, "dsgan_pw_gemm_f32: WGRAD needs dsgan_pw_f32_wgrad_workspace floats of scratch");
     g.ws = splits > 1 ? ws : nullptr;
+    g.asum = const_cast<float*>(bias);   // WGRAD: bias (nullable) receives the bias grad += sum_k DY
+    g.bias = nullptr;
     if (M > 64) pf_launch<PF_WGRAD, 128>(g, splits, st);
     else if (pf_wgrad_bn(M, N) == 64) pf_launch<PF_WGRAD, 64, 64>(g, splits, st);
     else pf_launch<PF_WGRAD, 64>(g, splits, st);
-    if (splits > 1) launch_split_reduce(ws, splits, (long)M * N, Y, st);
+    if (splits > 1) {
+      const float* wsv[2] = {ws, ws + (long)splits * M * N};
+      const int sv[2] = {splits, splits};
+      const long mv[2] = {(long)M * N, (long)M};
+      float* dv[2] = {Y, g.asum};
+      launch_split_reduce_multi(g.asum ? 2 : 1, wsv, sv, mv, dv, st);
+    }
   } else {
     DSG_REQUIRE(dsgan_pw_f32_supported(mode, M, K, P, a_bs, b_bs, A, B), "dsgan_pw_gemm_f32: unsupported shape");
     g.M = M; g.N = nb * P; g.K = K;

@@ -537,7 +537,8 @@ def conv_wgrad_raw(dy, x, dw, stride, pad, xact=None, db=None):
         fam = "pwf32_kernel"
         nws = _lib.load().dsgan_pw_f32_wgrad_workspace(Cout, Cin, H * W, N)
         ws = torch.empty(nws, device=dy.device, dtype=torch.float32) if nws > 0 else None
-        call("dsgan_pw_gemm_f32", 2, ptr(dy), dybs, ptr(x), xbs, ptr(dw), 0, None, None, 0, Cout, Cin, N * H * W,
+        did_db = db is not None
+        call("dsgan_pw_gemm_f32", 2, ptr(dy), dybs, ptr(x), xbs, ptr(dw), 0, ptr(db), None, 0, Cout, Cin, N * H * W,
              H * W, N, 0, 0, 0, LRELU_SLOPE, ptr(ws), stream())
     elif (xact is None and _is16() and dw.is_contiguous() and pad == 1 and W % 4 == 0
           and xbs % 4 == 0 and x.data_ptr() % 16 == 0 and _lib.load().dsgan_wconv_supported(Cin, KH, KW, stride)):

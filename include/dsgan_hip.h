@@ -96,7 +96,8 @@ int dsgan_pw_tune(int key, int val);
 /* ---- exact-fp32 pointwise GEMMs (pwf32.hip): v_mfma_f32_32x32x2_f32, same modes and argument
  * meaning as dsgan_pw_gemm (no ypre / activation-on-load); the MidMLKA 1x1 conv (fp32 by policy,
  * MixConvNeXtML.py:85,112) and every 1x1 conv in the fp32 parity mode.  WGRAD: ws =
- * dsgan_pw_f32_wgrad_workspace(M, N, P, nb) floats (deterministic split reduction). */
+ * dsgan_pw_f32_wgrad_workspace(M, N, P, nb) floats (deterministic split reduction); `bias`
+ * (nullable) is an OUTPUT there, as in dsgan_pw_gemm: bias[m] += sum_{b,p} DY[b][m][p]. */
 int dsgan_pw_f32_supported(int mode, int M, int K, int P, long a_bs, long b_bs, const void* a, const void* b);
 long dsgan_pw_f32_wgrad_workspace(int M, int N, int P, int nb);
 int dsgan_pw_gemm_f32(int mode, const float* A, long a_bs, const float* B, long b_bs, float* Y, long y_bs,

@@ -40,7 +40,8 @@ def test_pwf32_fwd_dgrad_wgrad(shape):
         y = HF.conv_fwd_raw(x, w, b, 1, 0)
         dx = HF.conv_dgrad_raw(dy, w, tuple(x.shape), 1, 0)
         dw = torch.zeros_like(w)
-        HF.conv_wgrad_raw(dy, x, dw, 1, 0)
+        db = torch.full((Co,), 0.5, device="cuda")
+        did_db = HF.conv_wgrad_raw(dy, x, dw, 1, 0, db=db)
         HF.IGEMM_TIMER.on = False
         fams = {r[4] for r in HF.IGEMM_TIMER.rec}
     torch.cuda.synchronize()
@@ -50,6 +51,8 @@ def test_pwf32_fwd_dgrad_wgrad(shape):
     dxr = torch.nn.functional.conv_transpose2d(dyd, wd)
     dwr = torch.einsum("nchw,nkhw->ck", dyd, xd).view(Co, Ci, 1, 1)
     assert rel(y, yr) < 1e-6 and rel(dx, dxr) < 1e-6 and rel(dw, dwr) < 1e-6, (rel(y, yr), rel(dx, dxr), rel(dw, dwr))
+    if Ci > 36:   # the bias grad rides on the weight-grad's staged dy tiles (+= into db)
+        assert did_db and rel(db, 0.5 + dyd.sum(dim=(0, 2, 3))) < 1e-6
 
 
 def test_pwf32_epilogues_and_slices():
