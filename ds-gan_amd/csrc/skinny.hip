@@ -45,12 +45,15 @@ __device__ __forceinline__ float bld(__amdgpu_buffer_rsrc_t r, unsigned off) {
 // PAR (transposed, stride 2, KH_ x KW_ = 4x4): only the 2x2 taps whose parity matches the output
 // pixel can land on an input pixel, so each lane walks its own four taps (kh = (oh+pad)&1 + 2i,
 // kw = (ow+pad)&1 + 2j) instead of issuing 16 loads of which 12 are out of range.
-template <int MS, int KH_, int KW_, bool PAR = false>
-__global__ __launch_bounds__(256) void small_out_kernel(SkArgs a) {
+// NWV = 16 (1024 threads, K > 64): the sixteen waves split the channels of one 64-pixel block --
+// for the under-filled launches (the PatchGAN last layer: 225 blocks of 64 pixels, K = 256), 16
+// channels per wave instead of 64 channel round trips in series.
+template <int MS, int KH_, int KW_, bool PAR = false, int NWV = 4>
+__global__ __launch_bounds__(64 * NWV) void small_out_kernel(SkArgs a) {
   extern __shared__ float wsm[];                 // [K][KH*KW][MS]
-  __shared__ float part[3][MS][64];
+  __shared__ float part[NWV - 1][MS][64];
   const int KH = KH_ ? KH_ : a.KH, KW = KW_ ? KW_ : a.KW, T = KH * KW;
-  for (int i = threadIdx.x; i < a.K * T * MS; i += 256) {
+  for (int i = threadIdx.x; i < a.K * T * MS; i += 64 * NWV) {
     const int m = i % MS, kt = i / MS, k = kt / T, t = kt - k * T;
     wsm[i] = m < a.M ? a.w[m * a.wm + k * a.wk + (t / KW) * a.wh + (t % KW) * a.ww] : 0.f;
   }
@@ -63,7 +66,7 @@ __global__ __launch_bounds__(256) void small_out_kernel(SkArgs a) {
   // PatchGAN conv-0 data-grad)
   // K <= 64: each wave owns its own 64 pixels over all K (no cross-wave combine or barrier per
   // block); larger K: the four waves split the channels of one 64-pixel block.
-  const bool own = a.K <= 64;
+  const bool own = NWV == 4 && a.K <= 64;
   const int PB = own ? 256 : 64;
   for (long blk = blockIdx.x; blk * PB < total; blk += gridDim.x) {
     long q = blk * PB + (own ? wave * 64 : 0) + lane;
@@ -107,7 +110,7 @@ __global__ __launch_bounds__(256) void small_out_kernel(SkArgs a) {
     float acc[MS];
 #pragma unroll
     for (int m = 0; m < MS; ++m) acc[m] = 0.f;
-    for (int k = own ? 0 : wave; k < a.K; k += own ? 1 : 4) {
+    for (int k = own ? 0 : wave; k < a.K; k += own ? 1 : NWV) {
       const unsigned xk = xb + (unsigned)k * HWi;
       const float* wk = wsm + k * T * MS;
       if (KH_) {
@@ -151,7 +154,9 @@ __global__ __launch_bounds__(256) void small_out_kernel(SkArgs a) {
 #pragma unroll
       for (int m = 0; m < MS; ++m) {
         if (m >= a.M) break;
-        float v = ((acc[m] + part[0][m][lane]) + part[1][m][lane]) + part[2][m][lane];
+        float v = acc[m];
+#pragma unroll
+        for (int w = 0; w < NWV - 1; ++w) v += part[w][m][lane];   // fixed order
         if (a.bias) v += a.bias[m];
         if (a.accumulate) v += yp[(long)m * HWo];
         yp[(long)m * HWo] = v;
@@ -458,6 +463,8 @@ int dsgan_conv_small_out(const float* x, long x_bs, const float* w, long wm, lon
   DSG_REQUIRE(pblocks < (1L << 31), "dsgan_conv_small_out: too many pixels");
   const long wblocks = K <= 64 ? (pblocks + 3) / 4 : pblocks;       // 256-pixel blocks when K <= 64
   const dim3 grid((unsigned)(wblocks < 2048 ? wblocks : 2048));    // grid-stride over pixel blocks
+  // few pixel blocks over many channels (PatchGAN last layer, 4x4 K = 256 -> 1 at 31^2): 16 waves
+  const bool wide = K >= 128 && pblocks < 1024 && KH == 4 && KW == 4 && M == 1 && !transposed;
   const int MSr = M == 1 ? 1 : (M <= 4 ? 4 : 8);
   const size_t lds = (size_t)K * KH * KW * MSr * 4;
   DSG_REQUIRE(lds <= 64 * 1024, "dsgan_conv_small_out: K*KH*KW*M too large for the LDS weight stage");
@@ -469,7 +476,8 @@ int dsgan_conv_small_out(const float* x, long x_bs, const float* w, long wm, lon
     hipLaunchKernelGGL((small_out_kernel<MS_, 4, 4, true>), grid, dim3(256), lds, st, a); \
   else if (KH == 4 && KW == 4) SO_LAUNCH(MS_, 4, 4);                        \
   else SO_LAUNCH(MS_, 0, 0);
-  if (MSr == 1) { SO_SHAPES(1) } else if (MSr == 4) { SO_SHAPES(4) } else { SO_SHAPES(8) }
+  if (wide) hipLaunchKernelGGL((small_out_kernel<1, 4, 4, false, 16>), grid, dim3(1024), lds, st, a);
+  else if (MSr == 1) { SO_SHAPES(1) } else if (MSr == 4) { SO_SHAPES(4) } else { SO_SHAPES(8) }
 #undef SO_SHAPES
 #undef SO_LAUNCH
   DSG_CHECK_LAUNCH();
