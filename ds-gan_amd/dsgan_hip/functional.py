@@ -546,8 +546,9 @@ def conv_wgrad_raw(dy, x, dw, stride, pad, xact=None, db=None):
         Ho, Wo = dy.shape[2], dy.shape[3]
         ws = torch.empty(_lib.load().dsgan_wconv_workspace(N, Cin, Cout, Ho, Wo, KH, KW), device=dy.device,
                          dtype=torch.float32)
-        call("dsgan_wconv", ptr(dy), dybs, ptr(x), xbs, ptr(dw), ptr(ws), N, Cin, Cout, H, W, Ho, Wo, KH, KW,
-             stride, pad, stream())
+        did_db = db is not None
+        call("dsgan_wconv_db", ptr(dy), dybs, ptr(x), xbs, ptr(dw), ptr(db), ptr(ws), N, Cin, Cout, H, W, Ho, Wo, KH,
+             KW, stride, pad, stream())
     else:
         nws = _lib.load().dsgan_conv_wgrad_workspace(N, Cin, Cout, KH, KW, dy.shape[2], dy.shape[3], _prec())
         ws = torch.empty(nws, device=dy.device, dtype=torch.float32) if nws > 0 else None
