@@ -7,41 +7,114 @@
 #include "common.h"
 
 namespace dsg {
-__global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
-                            float* __restrict__ v, long n, float w1, float b2, float step_size,
-                            float bc2_sqrt, float eps) {
-  const long i0 = (blockIdx.x * 256L + threadIdx.x) * 4;
-  for (long i = i0; i < n; i += (long)gridDim.x * 256 * 4) {
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const long e = i + j;
-      if (e >= n) break;
-      const float gr = g[e];
-      float mm = m[e];
-      // at::lerp: weight < 0.5 ? a + w*(b-a) : b - (b-a)*(1-w)
-      mm = w1 < 0.5f ? mm + w1 * (gr - mm) : gr - (gr - mm) * (1.f - w1);
-      const float vv = v[e] * b2 + (1.f - b2) * gr * gr;
-      m[e] = mm; v[e] = vv;
-      const float denom = sqrtf(vv) / bc2_sqrt + eps;
-      p[e] = p[e] - step_size * (mm / denom);
+// The optimizer's scalars as torch hands them to its fp32 kernels: python doubles, each rounded
+// to fp32 once (lerp weight 1 - b1, addcmul value 1 - b2, addcdiv value lr / (1 - b1^t), the
+// bias_correction2 sqrt divisor, eps).
+struct AdamScal {
+  float w1, b2, omb2, step_size, bc2s, eps;
+};
+
+static AdamScal adam_scal(double lr, double b1, double b2, double eps, double t) {
+  AdamScal a;
+  a.w1 = (float)(1.0 - b1);
+  a.b2 = (float)b2;
+  a.omb2 = (float)(1.0 - b2);
+  a.step_size = (float)(lr / (1.0 - pow(b1, t)));
+  a.bc2s = (float)sqrt(1.0 - pow(b2, t));
+  a.eps = (float)eps;
+  return a;
+}
+
+// One element (shared by the float4 body and the tail / unaligned body so both round identically):
+//   m.lerp_(g, w1); v.mul_(b2).addcmul_(g, g, 1 - b2); p.addcdiv_(m, sqrt(v) / bc2s + eps, -step_size)
+__device__ __forceinline__ void adam_elem(float& p, float gr, float& m, float& v, const AdamScal& a) {
+  float mm = m;
+  // at::lerp: weight < 0.5 ? a + w*(b-a) : b - (b-a)*(1-w)
+  mm = a.w1 < 0.5f ? mm + a.w1 * (gr - mm) : gr - (gr - mm) * (1.f - a.w1);
+  const float vv = v * a.b2 + a.omb2 * gr * gr;
+  m = mm; v = vv;
+  const float denom = sqrtf(vv) / a.bc2s + a.eps;
+  p = p - a.step_size * (mm / denom);
+}
+
+// VEC: p, g, m, v 16-byte aligned -- each lane moves float4s, the n % 4 tail elements go to the
+// first threads.  Otherwise one element per lane.
+// AMP: g is scaled by st[3] (1 / loss scale), the step count is st[4] (the scalars are formed here
+// from the doubles, as on the host for the plain form), and the whole update is skipped when
+// st[1] != 0.
+template <bool VEC, bool AMP>
+__global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const float* __restrict__ g,
+                                                   float* __restrict__ m, float* __restrict__ v, long n, AdamScal a,
+                                                   double lr, double b1, double b2, double eps,
+                                                   const float* __restrict__ st) {
+  float inv = 1.f;
+  if constexpr (AMP) {
+    if (st[1] != 0.f) return;   // overflowed step: parameters and moments untouched
+    inv = st[3];
+    const double t = (double)st[4];
+    a.w1 = (float)(1.0 - b1);
+    a.b2 = (float)b2;
+    a.omb2 = (float)(1.0 - b2);
+    a.step_size = (float)(lr / (1.0 - pow(b1, t)));
+    a.bc2s = (float)sqrt(1.0 - pow(b2, t));
+    a.eps = (float)eps;
+  }
+  const long tid = blockIdx.x * 256L + threadIdx.x, stride = (long)gridDim.x * 256;
+  if constexpr (VEC) {
+    const long n4 = n >> 2;
+    for (long i = tid; i < n4; i += stride) {
+      float4 pp = reinterpret_cast<const float4*>(p)[i];
+      float4 gg = reinterpret_cast<const float4*>(g)[i];
+      float4 mm = reinterpret_cast<const float4*>(m)[i];
+      float4 vv = reinterpret_cast<const float4*>(v)[i];
+      if constexpr (AMP) { gg.x *= inv; gg.y *= inv; gg.z *= inv; gg.w *= inv; }
+      adam_elem(pp.x, gg.x, mm.x, vv.x, a);
+      adam_elem(pp.y, gg.y, mm.y, vv.y, a);
+      adam_elem(pp.z, gg.z, mm.z, vv.z, a);
+      adam_elem(pp.w, gg.w, mm.w, vv.w, a);
+      reinterpret_cast<float4*>(m)[i] = mm;
+      reinterpret_cast<float4*>(v)[i] = vv;
+      reinterpret_cast<float4*>(p)[i] = pp;
+    }
+    const long e = (n4 << 2) + tid;
+    if (e < n) {
+      float gr = g[e];
+      if constexpr (AMP) gr *= inv;
+      adam_elem(p[e], gr, m[e], v[e], a);
+    }
+  } else {
+    for (long e = tid; e < n; e += stride) {
+      float gr = g[e];
+      if constexpr (AMP) gr *= inv;
+      adam_elem(p[e], gr, m[e], v[e], a);
     }
   }
+}
+
+static bool adam_vec_ok(const float* p, const float* g, const float* m, const float* v) {
+  return (((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) & 15) == 0;
+}
+
+template <bool AMP>
+static void adam_launch(float* p, const float* g, float* m, float* v, long n, const AdamScal& a, double lr, double b1,
+                        double b2, double eps, const float* state, hipStream_t st) {
+  long blocks = (n + 1023) / 1024;
+  if (blocks > 8192) blocks = 8192;
+  if (adam_vec_ok(p, g, m, v))
+    hipLaunchKernelGGL((adam_kernel<true, AMP>), dim3((unsigned)blocks), dim3(256), 0, st, p, g, m, v, n, a, lr, b1,
+                       b2, eps, state);
+  else
+    hipLaunchKernelGGL((adam_kernel<false, AMP>), dim3((unsigned)blocks), dim3(256), 0, st, p, g, m, v, n, a, lr, b1,
+                       b2, eps, state);
 }
 }  // namespace dsg
 
 using namespace dsg;
-extern "C" int dsgan_adam(float* p, const float* g, float* m, float* v, long n, float lr, float beta1,
-                          float beta2, float eps, int step, hipStream_t st) {
+extern "C" int dsgan_adam(float* p, const float* g, float* m, float* v, long n, double lr, double beta1,
+                          double beta2, double eps, int step, hipStream_t st) {
   DSG_REQUIRE(p && g && m && v && n >= 0 && step >= 1, "dsgan_adam: bad args");
   if (n == 0) return 0;
-  const double bc1 = 1.0 - pow((double)beta1, step);
-  const double bc2 = 1.0 - pow((double)beta2, step);
-  const float step_size = (float)(lr / bc1);
-  const float bc2s = (float)sqrt(bc2);
-  long blocks = (n + 1023) / 1024;
-  if (blocks > 8192) blocks = 8192;
-  hipLaunchKernelGGL(adam_kernel, dim3((unsigned)blocks), dim3(256), 0, st, p, g, m, v, n, 1.f - beta1,
-                     beta2, step_size, bc2s, eps);
+  adam_launch<false>(p, g, m, v, n, adam_scal(lr, beta1, beta2, eps, step), lr, beta1, beta2, eps, nullptr, st);
   DSG_CHECK_LAUNCH();
   return 0;
 }
@@ -94,32 +167,6 @@ __global__ __launch_bounds__(64) void amp_update_kernel(const int* __restrict__ 
     }
   }
 }
-__global__ void adam_amp_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
-                                float* __restrict__ v, long n, float lr, float beta1, float beta2, float eps,
-                                const float* __restrict__ st) {
-  if (st[1] != 0.f) return;   // overflowed step: parameters and moments untouched
-  const float inv = st[3];
-  const double t = (double)st[4];
-  // torch's bias corrections (python doubles), rounded to fp32 as torch hands them to the update
-  const float step_size = (float)((double)lr / (1.0 - pow((double)beta1, t)));
-  const float bc2s = (float)sqrt(1.0 - pow((double)beta2, t));
-  const float w1 = 1.f - beta1;
-  const long i0 = (blockIdx.x * 256L + threadIdx.x) * 4;
-  for (long i = i0; i < n; i += (long)gridDim.x * 256 * 4) {
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const long e = i + j;
-      if (e >= n) break;
-      const float gr = g[e] * inv;
-      float mm = m[e];
-      mm = w1 < 0.5f ? mm + w1 * (gr - mm) : gr - (gr - mm) * (1.f - w1);
-      const float vv = v[e] * beta2 + (1.f - beta2) * gr * gr;
-      m[e] = mm; v[e] = vv;
-      const float denom = sqrtf(vv) / bc2s + eps;
-      p[e] = p[e] - step_size * (mm / denom);
-    }
-  }
-}
 }  // namespace dsg
 
 extern "C" {
@@ -138,14 +185,11 @@ int dsgan_amp_check(const float* grad, long n, int* part, float* state, float ba
   return 0;
 }
 // Adam on the unscaled gradient g * state[3], skipped when state[1] != 0; step count = state[4]
-int dsgan_adam_amp(float* p, const float* g, float* m, float* v, long n, float lr, float beta1, float beta2, float eps,
-                   const float* state, hipStream_t st) {
+int dsgan_adam_amp(float* p, const float* g, float* m, float* v, long n, double lr, double beta1, double beta2,
+                   double eps, const float* state, hipStream_t st) {
   DSG_REQUIRE(p && g && m && v && state && n >= 0, "dsgan_adam_amp: bad args");
   if (n == 0) return 0;
-  long blocks = (n + 1023) / 1024;
-  if (blocks > 8192) blocks = 8192;
-  hipLaunchKernelGGL(adam_amp_kernel, dim3((unsigned)blocks), dim3(256), 0, st, p, g, m, v, n, lr, beta1, beta2, eps,
-                     state);
+  adam_launch<true>(p, g, m, v, n, AdamScal{}, lr, beta1, beta2, eps, state, st);
   DSG_CHECK_LAUNCH();
   return 0;
 }

@@ -522,11 +522,71 @@ __global__ __launch_bounds__(256) void ssim_bwd_kernel(SSIMArgs s, const float* 
   }
 }
 
+
+// The scalar loss combination of a training step in one launch (instead of one torch launch per
+// multiply / add, pix2pix_model.py:141-151, 193-199): out = scale * (t_0 + t_1 + ... ) summed left to
+// right, t_i = a_i * (b_i + c_i * x_i) with c_i in {1, -1} -- every product / sum rounded to fp32
+// once, as the chain of torch scalar ops rounds it (no contraction).
+constexpr int LOSS_TERMS = 8;
+struct LossTerms {
+  const float* x[LOSS_TERMS];
+  float a[LOSS_TERMS], b[LOSS_TERMS], c[LOSS_TERMS];
+  int n;
+  float scale;
+};
+__global__ void loss_combine_kernel(LossTerms t, float* __restrict__ out) {
+  if (threadIdx.x != 0) return;
+  float s = 0.f;
+  for (int i = 0; i < t.n; ++i) {
+    const float xi = t.x[i][0];
+    const float u = t.b[i] == 0.f ? (t.c[i] < 0.f ? -xi : xi) : __fadd_rn(t.b[i], t.c[i] < 0.f ? -xi : xi);
+    const float v = t.a[i] == 1.f ? u : __fmul_rn(t.a[i], u);
+    s = i == 0 ? v : __fadd_rn(s, v);
+  }
+  out[0] = t.scale == 1.f ? s : __fmul_rn(s, t.scale);
+}
+// gx[i] = ((gout * scale) * a_i) * c_i: the upstream grad of each term (torch's mul / rsub backward)
+__global__ void loss_combine_bwd_kernel(LossTerms t, const float* __restrict__ gout, float* __restrict__ gx) {
+  const int i = threadIdx.x;
+  if (i >= t.n) return;
+  float g = gout[0];
+  if (t.scale != 1.f) g = __fmul_rn(g, t.scale);
+  if (t.a[i] != 1.f) g = __fmul_rn(g, t.a[i]);
+  gx[i] = t.c[i] < 0.f ? -g : g;
+}
 }  // namespace dsg
 
 using namespace dsg;
 
 extern "C" {
+
+// out[0] = scale * sum_i a_i * (b_i + c_i * x_i[0]) (device scalars x_i; host arrays a, b, c; c_i = +-1)
+int dsgan_loss_combine(const float* const* x, const float* a, const float* b, const float* c, int n, float scale,
+                       float* out, hipStream_t st) {
+  DSG_REQUIRE(out && x && a && b && c && n >= 1 && n <= LOSS_TERMS, "dsgan_loss_combine: 1..%d terms", LOSS_TERMS);
+  LossTerms t{};
+  for (int i = 0; i < n; ++i) {
+    DSG_REQUIRE(x[i] != nullptr && (c[i] == 1.f || c[i] == -1.f), "dsgan_loss_combine: term %d", i);
+    t.x[i] = x[i]; t.a[i] = a[i]; t.b[i] = b[i]; t.c[i] = c[i];
+  }
+  t.n = n;
+  t.scale = scale;
+  hipLaunchKernelGGL(loss_combine_kernel, dim3(1), dim3(64), 0, st, t, out);
+  DSG_CHECK_LAUNCH();
+  return 0;
+}
+// gx[i] = gout[0] * scale * a_i * c_i (n floats), each product rounded in that order
+int dsgan_loss_combine_bwd(const float* gout, const float* a, const float* c, int n, float scale, float* gx,
+                           hipStream_t st) {
+  DSG_REQUIRE(gout && gx && a && c && n >= 1 && n <= LOSS_TERMS, "dsgan_loss_combine_bwd: bad args");
+  LossTerms t{};
+  for (int i = 0; i < n; ++i) { t.a[i] = a[i]; t.c[i] = c[i]; }
+  t.n = n;
+  t.scale = scale;
+  hipLaunchKernelGGL(loss_combine_bwd_kernel, dim3(1), dim3(64), 0, st, t, gout, gx);
+  DSG_CHECK_LAUNCH();
+  return 0;
+}
 
 // scratch floats the loss reductions below need for their block partials
 long dsgan_loss_parts(void) { return 4096; }

@@ -16,6 +16,7 @@ P = ctypes.c_void_p
 L = ctypes.c_long
 I = ctypes.c_int
 F = ctypes.c_float
+D = ctypes.c_double
 S = ctypes.c_void_p  # hipStream_t
 
 SIGNATURES = {
@@ -23,7 +24,7 @@ SIGNATURES = {
     "dsgan_set_half_type": [ctypes.c_int],
     "dsgan_amp_parts": [],
     "dsgan_amp_check": [P, L, P, P, F, F, I, S],
-    "dsgan_adam_amp": [P, P, P, P, L, F, F, F, F, P, S],
+    "dsgan_adam_amp": [P, P, P, P, L, D, D, D, D, P, S],
     "dsgan_get_half_type": [],
     "dsgan_last_error_string": [],
     # igemm.hip
@@ -119,6 +120,8 @@ SIGNATURES = {
     "dsgan_channel_sum": [P, L, P, I, I, I, P, S],
     # losses.hip
     "dsgan_loss_parts": [],
+    "dsgan_loss_combine": [P, P, P, P, I, F, P, S],
+    "dsgan_loss_combine_bwd": [P, P, P, I, F, P, S],
     "dsgan_ssim_parts": [I, I, I],
     "dsgan_bce_logits_fwd": [P, L, F, P, P, S],
     "dsgan_bce_logits_bwd": [P, L, F, P, P, I, S],
@@ -146,7 +149,7 @@ SIGNATURES = {
     "dsgan_cb16_maxpool": [P, P, P, I, I, I, I, S],
     "dsgan_cb16_tap_bwd": [P, P, P, P, P, I, I, I, I, P, S],
     # adam.hip
-    "dsgan_adam": [P, P, P, P, L, F, F, F, F, I, S],
+    "dsgan_adam": [P, P, P, P, L, D, D, D, D, I, S],
 }
 
 _lib = None

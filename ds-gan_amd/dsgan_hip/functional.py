@@ -1432,11 +1432,15 @@ class MaxPoolFn(torch.autograd.Function):
         ctx.k, ctx.shape = k, (N, C, H, W)
         ctx.save_for_backward(idx)
         ctx.mark_non_differentiable(idx)
+        # (no zero-filled int grad for idx per backward: autograd would materialise one)
+        ctx.set_materialize_grads(False)
         ctx.box = _box(x)
         return y, idx
 
     @staticmethod
     def backward(ctx, dy, _didx):
+        if dy is None:
+            return None, None
         (idx,) = ctx.saved_tensors
         N, C, H, W = ctx.shape
         dy4, dybs = nchw(dy)
@@ -1828,6 +1832,58 @@ class TVFn(torch.autograd.Function):
 
 def tv_loss(y, coef=1.0 / (320 * 256)):
     return TVFn.apply(y, coef)
+
+
+class LossSumFn(torch.autograd.Function):
+    """scale * sum_i a_i * (b_i + c_i * x_i) over 0-d fp32 losses in one launch each way
+    (dsgan_loss_combine): the same fp32 roundings as the torch scalar-op chain it replaces, which
+    costs one launch per multiply / add / rsub forward and per multiply backward."""
+
+    @staticmethod
+    def forward(ctx, coefs, scale, *xs):
+        import ctypes
+        n = len(xs)
+        fa = ctypes.c_float * n
+        ctx.a = fa(*[float(a) for a, _, _ in coefs])
+        ctx.c = fa(*[float(c) for _, _, c in coefs])
+        ctx.scale = float(scale)
+        b = fa(*[float(b) for _, b, _ in coefs])
+        xp = (ctypes.c_void_p * n)(*[ptr(x) for x in xs])
+        out = torch.empty((), device=xs[0].device, dtype=torch.float32)
+        call("dsgan_loss_combine", ctypes.cast(xp, ctypes.c_void_p), ctypes.cast(ctx.a, ctypes.c_void_p),
+             ctypes.cast(b, ctypes.c_void_p), ctypes.cast(ctx.c, ctypes.c_void_p), n, ctx.scale, ptr(out), stream())
+        ctx.n = n
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        import ctypes
+        gx = torch.empty(ctx.n, device=g.device, dtype=torch.float32)
+        call("dsgan_loss_combine_bwd", ptr(g.contiguous()), ctypes.cast(ctx.a, ctypes.c_void_p),
+             ctypes.cast(ctx.c, ctypes.c_void_p), ctx.n, ctx.scale, ptr(gx), stream())
+        return (None, None) + tuple(gx[i] for i in range(ctx.n))
+
+
+def loss_sum(terms, scale=1.0):
+    """scale * (t_0 + t_1 + ...), t_i = a * (b + c * x) for terms (x, a[, b, c]) with c = +-1, summed
+    left to right -- e.g. ``loss_sum([(gan, w_gan), (l1, 1), (ssim, w_ss, 1, -1)])`` is
+    ``gan * w_gan + l1 + w_ss * (1 - ssim)`` rounded as torch rounds that expression.  Terms whose x
+    is a python 0 (a disabled loss) are dropped, as ``0 * w + t`` is t."""
+    xs, coefs = [], []
+    for t in terms:
+        x, a = t[0], t[1]
+        b, c = (t[2], t[3]) if len(t) > 2 else (0.0, 1.0)
+        if not torch.is_tensor(x):
+            if x == 0 and b == 0:
+                continue
+            raise ValueError("loss_sum: non-tensor term %r" % (x,))
+        if x.dim() != 0 or x.dtype != torch.float32 or not x.is_cuda or c not in (1, -1, 1.0, -1.0):
+            raise ValueError("loss_sum: 0-d fp32 device losses and c = +-1 only")
+        xs.append(x)
+        coefs.append((a, b, c))
+    if not xs or len(xs) > 8:
+        raise ValueError("loss_sum: 1..8 tensor terms")
+    return LossSumFn.apply(tuple(coefs), scale, *xs)
 
 
 _WIN_CACHE = {}

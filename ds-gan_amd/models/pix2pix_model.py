@@ -34,6 +34,13 @@ from dsgan_hip.amp import LossScaler
 from util.image_pool import ImagePool
 from .base_model import BaseModel
 from . import networks
+
+
+def _fusable(*xs):
+    """Loss terms HF.loss_sum takes: 0-d fp32 device tensors (a disabled term may be a python 0)."""
+    ts = [x for x in xs if not (not torch.is_tensor(x) and x == 0)]
+    return bool(ts) and len(ts) <= 8 and all(torch.is_tensor(x) and x.dim() == 0 and x.dtype == torch.float32
+                                             and x.is_cuda for x in ts)
 from .vgg import Vgg16
 
 POOL_SEED = 20   # DSGAN/train.py:48 setup_seed(20): the ImagePool's RNG on ranks > 0 is offset from it
@@ -126,7 +133,10 @@ class Pix2PixModel(BaseModel):
         real_AB = HF.cat_channels(self.real_A, self.real_B) if self.use_condition == 1 else self.real_B
         pred_real = self.netD(real_AB)
         self.loss_D_real = self.criterionGAN(pred_real, True)
-        self.loss_D = (self.loss_D_fake + self.loss_D_real) * 0.5
+        if _fusable(self.loss_D_fake, self.loss_D_real):   # one launch each way (HF.loss_sum)
+            self.loss_D = HF.loss_sum([(self.loss_D_fake, 1.0), (self.loss_D_real, 1.0)], 0.5)
+        else:
+            self.loss_D = (self.loss_D_fake + self.loss_D_real) * 0.5
         loss = self.loss_D if self.mean_w == 1.0 else self.loss_D * self.mean_w
         (loss if self.scaler_D is None else self.scaler_D.scale(loss)).backward()
 
@@ -145,17 +155,28 @@ class Pix2PixModel(BaseModel):
         # 1 - ssim((real_B+1)/2, (fake_B+1)/2, data_range=1): the affine map is fused in-kernel
         # (--ssim_loss ms_ssim: the 5-level MS-SSIM of DSGAN/MS_SSIM.py:153-225 instead)
         if self.ssim_kind == "ms_ssim":
-            self.loss_ssim = 1 - HF.ms_ssim_loss_affine(self.real_B, self.fake_B, 0.5, 0.5, 1.0)
+            self._ssim_val = HF.ms_ssim_loss_affine(self.real_B, self.fake_B, 0.5, 0.5, 1.0)
         else:
-            self.loss_ssim = 1 - HF.ssim_affine(self.real_B, self.fake_B, 0.5, 0.5, 1.0)
-        self.loss_G = (self.loss_G_GAN * self.w_gan + self.loss_G_L1 + self.loss_vgg * self.w_vgg
-                       + self.tv_loss * self.w_tv + self.w_ss * self.loss_ssim)
+            self._ssim_val = HF.ssim_affine(self.real_B, self.fake_B, 0.5, 0.5, 1.0)
+        if self.mean_w == 1.0 and _fusable(self.loss_G_GAN, self.loss_G_L1, self.loss_vgg, self.tv_loss, self._ssim_val):
+            # the same sum in one launch each way: w_ss * (1 - ssim) is the (w_ss, 1, -1) term
+            self.loss_G = HF.loss_sum([(self.loss_G_GAN, self.w_gan), (self.loss_G_L1, 1.0),
+                                       (self.loss_vgg, self.w_vgg), (self.tv_loss, self.w_tv),
+                                       (self._ssim_val, self.w_ss, 1.0, -1.0)])
+        else:
+            self.loss_G = (self.loss_G_GAN * self.w_gan + self.loss_G_L1 + self.loss_vgg * self.w_vgg
+                           + self.tv_loss * self.w_tv + self.w_ss * self.loss_ssim)
         if self.mean_w == 1.0:
             loss = self.loss_G
         else:   # ragged global batch under DDP: reweight the batch means, not the TV sum
             loss = ((self.loss_G_GAN * self.w_gan + self.loss_G_L1 + self.loss_vgg * self.w_vgg + self.w_ss * self.loss_ssim)
                     * self.mean_w + self.tv_loss * self.w_tv)
         (loss if self.scaler_G is None else self.scaler_G.scale(loss)).backward()
+
+    @property
+    def loss_ssim(self):
+        """1 - ssim (the logged term; the step's loss_sum folds it into its (w_ss, 1, -1) term)."""
+        return 1 - self._ssim_val
 
     def _launch_real_features(self):
         """vgg(real_B) (frozen, no grad) depends only on the input: run it on a side stream so it

@@ -408,6 +408,14 @@ int dsgan_channel_sum(const float* dy, long dy_bs, float* out, int N, int C, int
  * Reductions are deterministic: block partials in `part` (dsgan_loss_parts() floats; ssim:
  * dsgan_ssim_parts(planes, H, W)) summed in a fixed order by one final workgroup. */
 long dsgan_loss_parts(void);
+/* The step's scalar loss combination in one launch (pix2pix_model.py:141-151 loss_G, :193-199
+ * loss_D): out[0] = scale * sum_i a_i * (b_i + c_i * x_i[0]), summed left to right, c_i = +-1, each
+ * product / sum rounded to fp32 once like the torch scalar-op chain it replaces (<= 8 terms; x_i
+ * device scalars, a/b/c host arrays).  _bwd: gx[i] = gout[0] * scale * a_i * c_i. */
+int dsgan_loss_combine(const float* const* x, const float* a, const float* b, const float* c, int n, float scale,
+                       float* out, hipStream_t stream);
+int dsgan_loss_combine_bwd(const float* gout, const float* a, const float* c, int n, float scale, float* gx,
+                           hipStream_t stream);
 long dsgan_ssim_parts(int planes, int H, int W);
 int dsgan_bce_logits_fwd(const float* x, long n, float target, float* out, float* part, hipStream_t stream);
 int dsgan_bce_logits_bwd(const float* x, long n, float target, const float* gout, float* dx,
@@ -483,8 +491,10 @@ int dsgan_cb16_tap_bwd(const void* dpool, const void* idx, const float* f, const
                        int H, int W, const float* gout, hipStream_t stream);
 
 /* ---- fused Adam over a flat buffer (adam.hip): torch.optim.Adam pix2pix_model.py:122-125 -- */
-int dsgan_adam(float* p, const float* g, float* m, float* v, long n, float lr, float beta1,
-               float beta2, float eps, int step, hipStream_t stream);
+/* lr, betas, eps are torch's python doubles; each scalar the update uses is formed in double and
+ * rounded to fp32 once, as torch's fp32 kernels receive them */
+int dsgan_adam(float* p, const float* g, float* m, float* v, long n, double lr, double beta1,
+               double beta2, double eps, int step, hipStream_t stream);
 /* fp16 mode (--precision fp16) dynamic loss scaling, device-resident (torch GradScaler semantics,
  * no host sync).  state = fp32[5] {scale, skip, clean steps, 1/scale of this step, applied steps}.
  * dsgan_amp_check: inf/nan scan of the flat gradient (16-byte aligned) + state update (skip the
@@ -494,8 +504,8 @@ int dsgan_adam(float* p, const float* g, float* m, float* v, long n, float lr, f
 long dsgan_amp_parts(void);
 int dsgan_amp_check(const float* grad, long n, int* part, float* state, float backoff, float growth, int interval,
                     hipStream_t stream);
-int dsgan_adam_amp(float* p, const float* g, float* m, float* v, long n, float lr, float beta1, float beta2,
-                   float eps, const float* state, hipStream_t stream);
+int dsgan_adam_amp(float* p, const float* g, float* m, float* v, long n, double lr, double beta1, double beta2,
+                   double eps, const float* state, hipStream_t stream);
 
 #ifdef __cplusplus
 }

@@ -660,6 +660,76 @@ def test_adam_matches_torch():
         assert torch.allclose(p.detach().cpu(), q.detach(), rtol=1e-6, atol=1e-7)
 
 
+def test_loss_sum_matches_torch_chain():
+    """HF.loss_sum (dsgan_loss_combine) is bit-identical to the torch scalar-op chains it replaces
+    in backward_G / backward_D (pix2pix_model.py), values and the grads of every term."""
+    from dsgan_hip import functional as HF
+    torch.manual_seed(5)
+    vals = [torch.rand((), device=DEV) * s for s in (3.0, 0.7, 12.0, 0.01, 1.0)]
+    w = (1.0, 100.0, 10.0, 0.37, 1.0)   # gan, (L1), vgg, tv, ss
+    for fused in (True, False):
+        xs = [v.clone().requires_grad_(True) for v in vals]
+        gan, l1, vgg, tv, ss = xs
+        if fused:
+            loss = HF.loss_sum([(gan, w[0]), (l1, 1.0), (vgg, w[2]), (tv, w[3]), (ss, w[4], 1.0, -1.0)])
+        else:
+            loss = gan * w[0] + l1 + vgg * w[2] + tv * w[3] + w[4] * (1 - ss)
+        (loss * 3.0).backward()
+        got = [loss.detach()] + [x.grad for x in xs]
+        if fused:
+            fused_res = got
+        else:
+            for a, b in zip(fused_res, got):
+                assert torch.equal(a, b), (a, b)
+    # the D form: (fake + real) * 0.5
+    f, r = (v.clone().requires_grad_(True) for v in vals[:2])
+    d = HF.loss_sum([(f, 1.0), (r, 1.0)], 0.5)
+    d.backward()
+    f2, r2 = (v.clone().requires_grad_(True) for v in vals[:2])
+    d2 = (f2 + r2) * 0.5
+    d2.backward()
+    assert torch.equal(d.detach(), d2.detach()) and torch.equal(f.grad, f2.grad) and torch.equal(r.grad, r2.grad)
+    # a disabled term (python 0) is dropped: 0 * w + l1 + ... == l1 + ...
+    x = vals[1].clone()
+    assert torch.equal(HF.loss_sum([(0, 5.0), (x, 1.0), (vals[2], 2.0)]), 0 * 5.0 + x + vals[2] * 2.0)
+
+
+@pytest.mark.parametrize("off", [0, 1])          # 0: float4 body + tail, 1: unaligned one-element body
+@pytest.mark.parametrize("amp", [False, True])
+def test_adam_kernel_paths(off, amp):
+    """dsgan_adam / dsgan_adam_amp on a flat buffer of n % 4 == 3 elements, against torch's
+    single-tensor Adam formula (fp32, same operation order); the AMP form unscales by state[3] and
+    skips the whole update when state[1] != 0."""
+    from dsgan_hip._lib import call, ptr, stream
+    torch.manual_seed(3)
+    n, lr, b1, b2, eps = 300_003, 2e-4, 0.5, 0.999, 1e-8
+    base = [torch.randn(n + 1, device=DEV) for _ in range(4)]
+    p, g, m, v = (t[off:off + n] for t in base)
+    v.abs_()
+    scale, step = 1024.0, 3
+    p0, m0, v0 = p.clone(), m.clone(), v.clone()
+    gr = g / scale if amp else g
+    m_ref = m0.lerp(gr, 1 - b1)
+    v_ref = v0 * b2 + (1 - b2) * gr * gr
+    bc1, bc2 = 1 - b1 ** step, 1 - b2 ** step
+    p_ref = p0 - (lr / bc1) * (m_ref / (v_ref.sqrt() / (bc2 ** 0.5) + eps))
+    if amp:
+        st = torch.tensor([scale, 0.0, 0.0, 1.0 / scale, float(step)], device=DEV)
+        call("dsgan_adam_amp", ptr(p), ptr(g), ptr(m), ptr(v), n, lr, b1, b2, eps, ptr(st), stream())
+    else:
+        call("dsgan_adam", ptr(p), ptr(g), ptr(m), ptr(v), n, lr, b1, b2, eps, step, stream())
+    torch.cuda.synchronize()
+    # (tolerances: one-ulp differences where the kernel contracts a multiply-add into an FMA)
+    assert torch.allclose(m, m_ref, rtol=1e-6, atol=1e-7) and torch.allclose(v, v_ref, rtol=1e-6, atol=1e-9)
+    assert torch.allclose(p, p_ref, rtol=0, atol=1e-7)
+    if amp:   # an overflowed step leaves everything untouched
+        st = torch.tensor([scale, 1.0, 0.0, 1.0 / scale, float(step)], device=DEV)
+        p1, m1, v1 = p.clone(), m.clone(), v.clone()
+        call("dsgan_adam_amp", ptr(p), ptr(g), ptr(m), ptr(v), n, lr, b1, b2, eps, ptr(st), stream())
+        torch.cuda.synchronize()
+        assert torch.equal(p, p1) and torch.equal(m, m1) and torch.equal(v, v1)
+
+
 @pytest.mark.parametrize("N,Cin,H,Cout", [(2, 64, 16, 256), (2, 36, 16, 200), (3, 132, 32, 68),
                                           (2, 512, 8 * 4, 64), (1, 16, 128, 16)])
 @pytest.mark.parametrize("half", HALVES)

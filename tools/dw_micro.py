@@ -18,7 +18,7 @@ def timeit(fn, it=20):
     return e0.elapsed_time(e1) / it
 
 
-for N, C, H, K in [(16, 128, 256, 7), (16, 256, 128, 7), (16, 64, 128, 7), (16, 512, 64, 7), (16, 1024, 32, 7),
+for N, C, H, K in [(16, 3, 256, 7), (16, 128, 256, 7), (16, 256, 128, 7), (16, 64, 128, 7), (16, 512, 64, 7), (16, 1024, 32, 7),
                    (16, 32, 128, 9), (16, 32, 128, 3), (16, 64, 64, 9)]:
     x = torch.randn(N, C, H, H, device="cuda")
     y = torch.empty_like(x)
