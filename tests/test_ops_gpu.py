@@ -721,7 +721,7 @@ def test_adam_kernel_paths(off, amp):
     torch.cuda.synchronize()
     # (tolerances: one-ulp differences where the kernel contracts a multiply-add into an FMA)
     assert torch.allclose(m, m_ref, rtol=1e-6, atol=1e-7) and torch.allclose(v, v_ref, rtol=1e-6, atol=1e-9)
-    assert torch.allclose(p, p_ref, rtol=0, atol=1e-7)
+    assert torch.allclose(p, p_ref, rtol=3e-7, atol=1e-7)   # ~2 ulp of p
     if amp:   # an overflowed step leaves everything untouched
         st = torch.tensor([scale, 1.0, 0.0, 1.0 / scale, float(step)], device=DEV)
         p1, m1, v1 = p.clone(), m.clone(), v.clone()
