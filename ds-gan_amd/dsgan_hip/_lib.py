@@ -43,7 +43,6 @@ SIGNATURES = {
     "dsgan_pw_dgrad_io_ws": [P, I, P, L, I, P, L, I, P, L, I, I, I, I, I, P, S],
     "dsgan_pw_fd_workspace": [I, I, I, I, I],
     "dsgan_wtrans_multi": [P, P, P, I, S],
-    "dsgan_wconv_db": [P, L, P, L, P, P, P] + [I] * 11 + [S],
     "dsgan_pw_tune": [I, I],
     # pwf32.hip
     "dsgan_pw_f32_supported": [I, I, I, I, L, L, P, P],

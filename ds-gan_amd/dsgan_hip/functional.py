@@ -546,9 +546,8 @@ def conv_wgrad_raw(dy, x, dw, stride, pad, xact=None, db=None):
         Ho, Wo = dy.shape[2], dy.shape[3]
         ws = torch.empty(_lib.load().dsgan_wconv_workspace(N, Cin, Cout, Ho, Wo, KH, KW), device=dy.device,
                          dtype=torch.float32)
-        did_db = db is not None
-        call("dsgan_wconv_db", ptr(dy), dybs, ptr(x), xbs, ptr(dw), ptr(db), ptr(ws), N, Cin, Cout, H, W, Ho, Wo, KH,
-             KW, stride, pad, stream())
+        call("dsgan_wconv", ptr(dy), dybs, ptr(x), xbs, ptr(dw), ptr(ws), N, Cin, Cout, H, W, Ho, Wo, KH, KW,
+             stride, pad, stream())
     else:
         nws = _lib.load().dsgan_conv_wgrad_workspace(N, Cin, Cout, KH, KW, dy.shape[2], dy.shape[3], _prec())
         ws = torch.empty(nws, device=dy.device, dtype=torch.float32) if nws > 0 else None
@@ -1592,6 +1591,18 @@ def _perceptual_bwd_cb16(ctx, g):
     return dx
 
 
+def _sum4_raw(outs):
+    """((L1(f1) + L1(f2)) + L1(f3)) + L1(f0) -- the reference's order -- in one dsgan_loss_combine
+    launch (the fp32 adds of the three torch adds it replaces)."""
+    import ctypes
+    xp = (ctypes.c_void_p * 4)(*[outs[i:].data_ptr() for i in (1, 2, 3, 0)])
+    ones, zeros = (ctypes.c_float * 4)(1, 1, 1, 1), (ctypes.c_float * 4)(0, 0, 0, 0)
+    out = torch.empty((), device=outs.device, dtype=torch.float32)
+    call("dsgan_loss_combine", ctypes.cast(xp, ctypes.c_void_p), ctypes.cast(ones, ctypes.c_void_p),
+         ctypes.cast(zeros, ctypes.c_void_p), ctypes.cast(ones, ctypes.c_void_p), 4, 1.0, ptr(out), stream())
+    return out
+
+
 class PerceptualL1Fn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, fake, blocks, real_feats):
@@ -1605,7 +1616,7 @@ class PerceptualL1Fn(torch.autograd.Function):
             ctx.blocks, ctx.saved, ctx.real, ctx.feats = blocks, saved, real_feats, feats
             ctx.fake_shape = tuple(fake.shape)
             ctx.prec = _state["prec"]
-            return ((outs[1] + outs[2]) + outs[3]) + outs[0]
+            return _sum4_raw(outs)
         feats, saved = vgg_features_raw(fake, blocks)
         outs = torch.empty(4, device=fake.device, dtype=torch.float32)
         for i, (f, r) in enumerate(zip(feats, real_feats)):
@@ -1613,8 +1624,7 @@ class PerceptualL1Fn(torch.autograd.Function):
         ctx.blocks, ctx.saved, ctx.real = blocks, saved, real_feats
         ctx.fake_shape = tuple(fake.shape)
         ctx.prec = _state["prec"]
-        # reference order: L1(f1) + L1(f2) + L1(f3) + L1(f0)
-        return ((outs[1] + outs[2]) + outs[3]) + outs[0]
+        return _sum4_raw(outs)
 
     @staticmethod
     def backward(ctx, g):

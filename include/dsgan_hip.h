@@ -303,10 +303,6 @@ long dsgan_wconv_workspace(int nb, int C, int M, int Ho, int Wo, int KH, int KW)
 int dsgan_wconv(const float* D, long d_bs, const float* X, long x_bs, float* dw, float* ws, int nb,
                 int C, int M, int H, int W, int Ho, int Wo, int KH, int KW, int stride, int pad,
                 hipStream_t stream);
-/* dsgan_wconv plus the conv's bias grad: db[m] += sum_{b,oh,ow} D[b][m][oh][ow] (fp32, fixed order),
- * from the staged D tiles (ws from dsgan_wconv_workspace, which includes the bias partials). */
-int dsgan_wconv_db(const float* D, long d_bs, const float* X, long x_bs, float* dw, float* db, float* ws, int nb,
-                   int C, int M, int H, int W, int Ho, int Wo, int KH, int KW, int stride, int pad, hipStream_t stream);
 /* Same with X in the library's 16-bit half type (x_bs in elements, rows 8-byte aligned), 3x3
  * stride 2 only: the ConvTranspose2d weight-grad on dsgan_instnorm_bwd_h's output (two resident
  * workgroups per CU; ws sized by dsgan_wconv_workspace, which covers both forms). */

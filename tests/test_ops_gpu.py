@@ -371,17 +371,13 @@ def test_wconv_bf16(half, N, C, H, W, M, K, s, p):
     dw_ref = torch.nn.grad.conv2d_weight(x.double(), (M, C, K, K), dy.double(), stride=s, padding=p)
     w0 = torch.randn(M, C, K, K, generator=g)
     dw = w0.to(DEV)
-    db0 = torch.randn(M, generator=g)
-    db = db0.to(DEV)
     HF.IGEMM_TIMER.rec, HF.IGEMM_TIMER.on = [], True
     try:
-        did_db = HF.conv_wgrad_raw(dy.to(DEV), x.to(DEV), dw, s, p, db=db)
+        HF.conv_wgrad_raw(dy.to(DEV), x.to(DEV), dw, s, p)
     finally:
         HF.IGEMM_TIMER.on = False
     assert HF.IGEMM_TIMER.rec[-1][4] == "wconv_kernel"
     assert rel(dw - w0.to(DEV), dw_ref) < 1e-5
-    # the bias grad summed from the staged dy tiles (fp32), += into db
-    assert did_db and rel(db - db0.to(DEV), dy.double().sum(dim=(0, 2, 3))) < 1e-6
     # channel-slice inputs (batch stride != C*H*W) and determinism
     xb = torch.cat([x, torch.randn(N, 32, H, W, generator=g)], 1).to(DEV)[:, :C]
     dw2 = w0.to(DEV)
