@@ -1606,6 +1606,7 @@ def _sum4_raw(outs):
 class PerceptualL1Fn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, fake, blocks, real_feats):
+        ctx.box = _box(fake)
         fake, _ = nchw(fake)
         ctx.cb16 = real_feats[0].dim() == 5
         if ctx.cb16:
@@ -1632,7 +1633,7 @@ class PerceptualL1Fn(torch.autograd.Function):
             with precision(ctx.prec):
                 dx = _perceptual_bwd_cb16(ctx, g.contiguous())
             ctx.saved = ctx.real = ctx.feats = None
-            return dx, None, None
+            return _give(ctx.box, dx), None, None
         with precision(ctx.prec):
             g = g.contiguous()
             d, d_idx = None, None   # grad at the pool output of the block above, and that pool's argmax
@@ -1656,7 +1657,7 @@ class PerceptualL1Fn(torch.autograd.Function):
                         dpre = conv_dgrad_raw(dpre, w, in_shape, 1, 1)
                 d, d_idx = dpre, idx
             ctx.saved = ctx.real = None
-            return d, None, None
+            return _give(ctx.box, d), None, None
 
 
 def perceptual_l1(fake, blocks, real_feats):
@@ -1791,9 +1792,24 @@ def bce_with_logits(x, target):
     return BCELogitsFn.apply(x, target)
 
 
+def _loss_grad(box, like, run):
+    """Input-grad of a loss w.r.t. a (possibly shared, HF.share) image: a shared input whose buffer
+    is owned and dense gets the grad accumulated in-kernel (run(buf, 1)); otherwise a fresh grad
+    (run(d, 0)) is handed to the box or returned.  Either way the grads of a shared tensor are
+    summed in arrival order, old + new, as autograd sums them."""
+    buf, acc = _acc_target(box)
+    if acc and buf.is_contiguous() and buf.shape == like.shape and buf.dtype == torch.float32:
+        run(buf, 1)
+        return None
+    d = torch.empty_like(like)
+    run(d, 0)
+    return _give(box, d)
+
+
 class L1Fn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, a, b):
+        ctx.box_a, ctx.box_b = _box(a), _box(b)
         a, b = a.contiguous(), b.contiguous()
         out = torch.empty((), device=a.device, dtype=torch.float32)
         call("dsgan_l1_fwd", ptr(a), ptr(b), a.numel(), ptr(out), ptr(_loss_part(a)), stream())
@@ -1806,11 +1822,11 @@ class L1Fn(torch.autograd.Function):
         g = g.contiguous()
         da = db = None
         if ctx.needs_input_grad[0]:
-            da = torch.empty_like(a)
-            call("dsgan_l1_bwd", ptr(a), ptr(b), a.numel(), ptr(g), ptr(da), 0, stream())
+            da = _loss_grad(ctx.box_a, a, lambda d, acc: call("dsgan_l1_bwd", ptr(a), ptr(b), a.numel(), ptr(g),
+                                                              ptr(d), acc, stream()))
         if ctx.needs_input_grad[1]:
-            db = torch.empty_like(b)
-            call("dsgan_l1_bwd", ptr(b), ptr(a), b.numel(), ptr(g), ptr(db), 0, stream())
+            db = _loss_grad(ctx.box_b, b, lambda d, acc: call("dsgan_l1_bwd", ptr(b), ptr(a), b.numel(), ptr(g),
+                                                              ptr(d), acc, stream()))
         return da, db
 
 
@@ -1823,6 +1839,7 @@ class TVFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, y, coef):
+        ctx.box = _box(y)
         y = y.contiguous()
         N, C, H, W = y.shape
         out = torch.empty((), device=y.device, dtype=torch.float32)
@@ -1835,8 +1852,9 @@ class TVFn(torch.autograd.Function):
     def backward(ctx, g):
         (y,) = ctx.saved_tensors
         N, C, H, W = y.shape
-        dy = torch.empty_like(y)
-        call("dsgan_tv_bwd", ptr(y), N * C, H, W, ctx.coef, ptr(g.contiguous()), ptr(dy), 0, stream())
+        g = g.contiguous()
+        dy = _loss_grad(ctx.box, y, lambda d, acc: call("dsgan_tv_bwd", ptr(y), N * C, H, W, ctx.coef, ptr(g), ptr(d),
+                                                        acc, stream()))
         return dy, None
 
 
@@ -1914,6 +1932,7 @@ class SSIMFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, real, fake, a, b, data_range):
+        ctx.box = _box(fake)
         real, fake = real.contiguous(), fake.contiguous()
         N, C, H, W = real.shape
         Ho, Wo = H - 10, W - 10
@@ -1934,9 +1953,10 @@ class SSIMFn(torch.autograd.Function):
     def backward(ctx, g):
         real, fake, coef = ctx.saved_tensors
         N, C, H, W = real.shape
-        dfake = torch.empty_like(fake)
-        call("dsgan_ssim_bwd", ptr(real), ptr(fake), ctx.ab[0], ctx.ab[1], N * C, H, W,
-             ptr(gauss_win(real.device)), ptr(coef), ptr(g.contiguous()), 1.0 / ctx.cnt, ptr(dfake), 0, stream())
+        g = g.contiguous()
+        dfake = _loss_grad(ctx.box, fake, lambda d, acc: call(
+            "dsgan_ssim_bwd", ptr(real), ptr(fake), ctx.ab[0], ctx.ab[1], N * C, H, W, ptr(gauss_win(real.device)),
+            ptr(coef), ptr(g), 1.0 / ctx.cnt, ptr(d), acc, stream()))
         return None, dfake, None, None, None
 
 

@@ -146,18 +146,21 @@ class Pix2PixModel(BaseModel):
             self.loss_G_GAN = self.criterionGAN(self.netD(fake_AB), True)
         else:
             self.loss_G_GAN = 0
-        self.loss_G_L1 = self.criterionL1(self.fake_B, self.real_B)
+        # the four image losses sum their fake_B grads in one buffer (HF.share: the L1 / TV / SSIM
+        # backward kernels accumulate in place) instead of through autograd adds; same order of sums
+        fB = HF.share(self.fake_B)
+        self.loss_G_L1 = self.criterionL1(fB, self.real_B)
         self.real_B_features = self._take_real_features()
         # L1(f1,r1) + L1(f2,r2) + L1(f3,r3) + L1(f0,r0) over vgg(fake_B): one fused node whose
         # backward is the hand-written VGG data-grad chain (vgg.py / functional.PerceptualL1Fn)
-        self.loss_vgg = self.vgg.perceptual_l1(self.fake_B, self.real_B_features)
-        self.tv_loss = HF.tv_loss(self.fake_B, self.tv_scale / (320 * 256))
+        self.loss_vgg = self.vgg.perceptual_l1(fB, self.real_B_features)
+        self.tv_loss = HF.tv_loss(fB, self.tv_scale / (320 * 256))
         # 1 - ssim((real_B+1)/2, (fake_B+1)/2, data_range=1): the affine map is fused in-kernel
         # (--ssim_loss ms_ssim: the 5-level MS-SSIM of DSGAN/MS_SSIM.py:153-225 instead)
         if self.ssim_kind == "ms_ssim":
-            self._ssim_val = HF.ms_ssim_loss_affine(self.real_B, self.fake_B, 0.5, 0.5, 1.0)
+            self._ssim_val = HF.ms_ssim_loss_affine(self.real_B, fB, 0.5, 0.5, 1.0)
         else:
-            self._ssim_val = HF.ssim_affine(self.real_B, self.fake_B, 0.5, 0.5, 1.0)
+            self._ssim_val = HF.ssim_affine(self.real_B, fB, 0.5, 0.5, 1.0)
         if self.mean_w == 1.0 and _fusable(self.loss_G_GAN, self.loss_G_L1, self.loss_vgg, self.tv_loss, self._ssim_val):
             # the same sum in one launch each way: w_ss * (1 - ssim) is the (w_ss, 1, -1) term
             self.loss_G = HF.loss_sum([(self.loss_G_GAN, self.w_gan), (self.loss_G_L1, 1.0),
