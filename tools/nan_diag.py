@@ -26,7 +26,7 @@ for arm in arms:
         for net, pr in ((model.netG, gp), (model.netD, dp), (model.vgg, make_params(O.vgg_param_spec(True), "vgg", 7000))):
             for k, v in net.state_dict().items():
                 v.copy_(pr[k])
-    for i in range(10):
+    for i in range(int(os.environ.get("NAN_DIAG_STEPS", "10"))):
         A, B = synth_pair(16, 256, seed=100 + i)
         model.set_input({"A": A.cuda(), "B": B.cuda(), "A_paths": [""] * 16, "B_paths": [""] * 16})
         model.optimize_parameters()
