@@ -37,6 +37,7 @@ PEAK_F32_TFLOPS = 157.3
 
 
 PEAK_HBM_GBS = 8000.0       # MI355X HBM3E (MI355X_MICROARCH.md)
+STEP_GFLOP_PER_IMG = 367.02  # algorithmic GFLOP per 256x256 image pair of one G+D step
 
 
 def host_cpu():
@@ -176,6 +177,8 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=None,
                     help="oracle threads for cpu_baseline (default: every physical core the job may use)")
     ap.add_argument("--quality-steps", type=int, default=10, help="steps of the shared quality / cpu_baseline leg")
+    ap.add_argument("--no-train-equiv", action="store_true",
+                    help="skip the train.py-equivalent iteration leg (profiling runs)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -221,6 +224,33 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = t.item()
     ig = HF.IGEMM_TIMER.summary()
+
+    # train.py-equivalent iteration (DSGAN/train.py:106-124): the step plus the post-step
+    # get_img_tir / get_img_gen forward / get_img_label and the per-iteration SSIM + PSNR of image 0
+    # (device-side, util/metrics.py) -- timed separately, never part of `value`
+    n_tp, dt_tp = 0, None
+    if not args.no_train_equiv:
+        from util.metrics import TrainMetrics
+        metrics = TrainMetrics(model.device)
+        n_tp = max(1, args.steps)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        for _ in range(n_tp):
+            model.set_input(data)
+            model.optimize_parameters()
+            model.get_img_tir(data)
+            with torch.no_grad():
+                model.get_img_gen(data)
+            model.get_img_label(data)
+            metrics.update(model.fake_B[0], model.real_B[0])
+        torch.cuda.synchronize()
+        dt_tp = time.perf_counter() - t1
+        if world > 1:
+            t = torch.tensor([dt_tp], device="cuda")
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            dt_tp = t.item()
 
     fams = HF.IGEMM_TIMER.families()
     if rank == 0:
@@ -288,7 +318,21 @@ def main():
                                            if (args.size, args.batch) == (512, 8) else
                                            "off-baseline shape %dx%d, batch %d" % (args.size, args.size, args.batch))},
             "roofline": roof,
+            # the whole step against the dense MFMA peak: SURVEY.md section 8(d)'s algorithmic work per
+            # image pair (367.02 GFLOP at 256^2: G fwd+bwd 244.5, D 13.0, VGG16 2 fwd + 1 data-grad 109.5)
+            "step_roofline": {"gflop_per_img": STEP_GFLOP_PER_IMG if args.size == 256 else None,
+                              "achieved_tflops": round(STEP_GFLOP_PER_IMG * imgs / dt / 1e3, 1) if args.size == 256 else None,
+                              "peak_tflops": peak,
+                              "frac": round(STEP_GFLOP_PER_IMG * imgs / dt / 1e3 / peak, 4) if args.size == 256 else None,
+                              "counted_conv_gflop_per_img": round(ig["flops"] / args.steps / 1e9 / args.batch, 2),
+                              "source": "SURVEY.md 8(d); counted = the conv launches IGEMM_TIMER saw"},
         }
+        if dt_tp:
+            out["train_py_equiv"] = {
+                "iters_per_s": round(n_tp / dt_tp, 3), "img_per_s": round(args.batch * world * n_tp / dt_tp, 3),
+                "ms_per_iter": round(dt_tp / n_tp * 1e3, 3), "iters": n_tp,
+                "what": "DSGAN/train.py:106-124 iteration: set_input + optimize_parameters + get_img_tir + "
+                        "get_img_gen (forward) + get_img_label + per-iteration SSIM/PSNR of image 0"}
         if world == 1 and not (args.no_cpu_baseline and args.no_quality):
             try:
                 q, cpu = reference_legs(steps=args.quality_steps, batch=args.batch, size=args.size,

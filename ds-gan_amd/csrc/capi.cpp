@@ -20,13 +20,26 @@ void dsgan_set_error(const char* fmt, ...) {
   va_end(ap);
 }
 
+// Plan-only mode (common.h DSG_WS): entry points validate, plan and check their scratch, then
+// return before any launch.  Thread-local, off by default; the CPU planner tests switch it on.
+static thread_local int g_plan_only = 0;
+static thread_local long g_ws_need = 0;
+
 namespace dsg {
 int half_type() { return g_half.load(std::memory_order_relaxed); }
+bool plan_only() { return g_plan_only != 0; }
+void note_ws_need(long n) { g_ws_need = n; }
 }  // namespace dsg
 
 extern "C" {
 const char* dsgan_last_error_string(void) { return g_err; }
-int dsgan_abi_version(void) { return 2; }
+int dsgan_abi_version(void) { return 3; }
+int dsgan_set_plan_only(int on) {
+  const int old = g_plan_only;
+  g_plan_only = on ? 1 : 0;
+  return old;
+}
+long dsgan_last_ws_need(void) { return g_ws_need; }
 int dsgan_set_half_type(int t) {
   if (t != 0 && t != 1) {
     dsgan_set_error("dsgan_set_half_type: %d is not 0 (bf16) or 1 (fp16)", t);

@@ -259,3 +259,25 @@ void dsgan_set_error(const char* fmt, ...);
   } while (0)
 
 static inline unsigned cdiv(long a, long b) { return (unsigned)((a + b - 1) / b); }
+
+// ---- scratch (workspace) contract -------------------------------------------------
+// Every entry point that takes a scratch buffer also takes its size `ws_elems` (fp32 elements, or
+// the buffer's own element type where stated).  The launcher plans the launch it is about to issue,
+// computes the scratch that plan writes (`need`) and refuses an undersized buffer with an error
+// code instead of writing past it.  In plan-only mode (dsgan_set_plan_only, thread-local; CPU
+// planner tests) the entry point returns 0 right after this check: no HIP call has been made by
+// then, so every planner runs without a GPU.
+namespace dsg {
+bool plan_only();           // capi.cpp
+void note_ws_need(long n);  // capi.cpp: dsgan_last_ws_need() reports it
+}  // namespace dsg
+#define DSG_WS(need, ws, ws_elems, name)                                                              \
+  do {                                                                                               \
+    const long n__ = (long)(need);                                                                   \
+    dsg::note_ws_need(n__);                                                                          \
+    if (n__ > 0 && ((ws) == nullptr || n__ > (long)(ws_elems))) {                                    \
+      dsgan_set_error("%s: scratch of %ld elements, this launch needs %ld", name, (long)(ws_elems), n__); \
+      return -1;                                                                                     \
+    }                                                                                                \
+    if (dsg::plan_only()) return 0;                                                                  \
+  } while (0)

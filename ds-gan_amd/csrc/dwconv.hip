@@ -606,13 +606,14 @@ long dsgan_dwconv_multi_wgrad_workspace(int N, int q, int H, int W) {
 // dw_K += sum dy * x, db_K += sum dy for the four quarters (fixed-order slot reduction)
 int dsgan_dwconv_multi_wgrad(const float* dy, long dy_bs, const float* x, long x_bs, float* dw3, float* db3,
                              float* dw5, float* db5, float* dw7, float* db7, float* dw9, float* db9, int N, int q,
-                             int H, int W, float* ws, hipStream_t st) {
-  DSG_REQUIRE(dy && x && ws && dw3 && dw5 && dw7 && dw9 && N > 0 && q > 0 && q <= 65535,
+                             int H, int W, float* ws, long ws_elems, hipStream_t st) {
+  DSG_REQUIRE(dy && x && dw3 && dw5 && dw7 && dw9 && N > 0 && q > 0 && q <= 65535,
               "dsgan_dwconv_multi_wgrad: bad args");
   DSG_REQUIRE(dsgan_dwconv_multi_supported(H, W, x, x_bs, dy, dy_bs), "dsgan_dwconv_multi_wgrad: unsupported H=%d W=%d",
               H, W);
   const int cfg = dw_cfg(H, W);
   const long G = dw_multi_wgrad_any(cfg, nullptr, 0, nullptr, 0, nullptr, N, q, H, W, 0);
+  DSG_WS(G * q * (10 + 26 + 50 + 82), ws, ws_elems, "dsgan_dwconv_multi_wgrad (dsgan_dwconv_multi_wgrad_workspace)");
   DwQuad q4{};
   float* dws[4] = {dw3, dw5, dw7, dw9};
   float* dbs[4] = {db3, db5, db7, db9};
@@ -679,16 +680,23 @@ long dsgan_dwconv_wgrad_workspace(int N, int C, int H, int W, int K, int aligned
 // dw[c] += sum dy * x (KxK correlation), db[c] += sum dy: every workgroup writes its partial
 // sums to ws, dw_partial_reduce_kernel adds them in a fixed order (deterministic).
 int dsgan_dwconv_wgrad(const float* dy, long dy_bs, const float* x, long x_bs, float* dw, float* db,
-                       int N, int C, int H, int W, int K, float* ws, hipStream_t st) {
-  DSG_REQUIRE(dy && x && dw && ws && K >= 1 && K <= DW_MAXK && (K & 1), "dsgan_dwconv_wgrad: bad args");
+                       int N, int C, int H, int W, int K, float* ws, long ws_elems, hipStream_t st) {
+  DSG_REQUIRE(dy && x && dw && K >= 1 && K <= DW_MAXK && (K & 1), "dsgan_dwconv_wgrad: bad args");
   const int cfg = dw_cfg(H, W);
   long G;
-  if (dw_tiled_ok(K, cfg, x, dy, x_bs, dy_bs)) {
-    G = dw_wgrad_any(K, cfg, dy, dy_bs, x, x_bs, ws, N, C, H, W, st);
+  const bool tiled = dw_tiled_ok(K, cfg, x, dy, x_bs, dy_bs);
+  int tpb = 0, groups = 0;
+  if (tiled) {
+    G = dw_wgrad_any(K, cfg, nullptr, 0, nullptr, 0, nullptr, N, C, H, W, st);   // (plan only)
   } else {
-    int tpb;
-    const int groups = dw_generic_groups(N, C, H, W, &tpb);
+    groups = dw_generic_groups(N, C, H, W, &tpb);
     DSG_REQUIRE((long)N * C < (1L << 31) && groups <= 65535, "dsgan_dwconv_wgrad: grid too large");
+    G = (long)N * groups;
+  }
+  DSG_WS(G * C * (K * K + 1), ws, ws_elems, "dsgan_dwconv_wgrad (dsgan_dwconv_wgrad_workspace)");
+  if (tiled) {
+    dw_wgrad_any(K, cfg, dy, dy_bs, x, x_bs, ws, N, C, H, W, st);
+  } else {
     const dim3 grid(N * C, groups);
     switch (K) {
       case 3: hipLaunchKernelGGL(dwconv_wgrad_kernel<3>, grid, dim3(256), 0, st, dy, dy_bs, x, x_bs, ws, C, H, W, tpb); break;
@@ -697,7 +705,6 @@ int dsgan_dwconv_wgrad(const float* dy, long dy_bs, const float* x, long x_bs, f
       case 9: hipLaunchKernelGGL(dwconv_wgrad_kernel<9>, grid, dim3(256), 0, st, dy, dy_bs, x, x_bs, ws, C, H, W, tpb); break;
       default: DSG_REQUIRE(false, "dsgan_dwconv_wgrad: K must be 3, 5, 7 or 9");
     }
-    G = (long)N * groups;
   }
   // dw[c][i] += sum_g ws[g][c][i] (i < K*K), db[c] += sum_g ws[g][c][K*K]; g in a fixed order
   launch_split_reduce_kk(ws, (int)G, (long)C * (K * K + 1), dw, db, K * K + 1, st);

@@ -665,7 +665,7 @@ long dsgan_conv_wgrad_workspace(int N, int Cin, int Cout, int KH, int KW, int Ho
 // per step; concurrent uses of one weight accumulate, as autograd would).
 int dsgan_conv_wgrad(const float* dy, long dy_bs, const float* x, long x_bs, float* dw, int N,
                      int Cin, int H, int W, int Cout, int KH, int KW, int stride, int pad, int Ho,
-                     int Wo, int xact, int prec, float* ws, hipStream_t st) {
+                     int Wo, int xact, int prec, float* ws, long ws_elems, hipStream_t st) {
   if (int e = check_geom(N, Cin, H, W, Cout, KH, KW, stride, pad, Ho, Wo, prec)) return e;
   DSG_REQUIRE(dy && x && dw, "dsgan_conv_wgrad: null pointer");
   GemmArgs g = base_args(N, Cin, H, W, Cout, KH, KW, stride, pad, Ho, Wo);
@@ -674,8 +674,8 @@ int dsgan_conv_wgrad(const float* dy, long dy_bs, const float* x, long x_bs, flo
   g.M = Cout; g.NN = Cin * KH * KW; g.K = N * Ho * Wo;
   const int BK = prec == PREC_BF16 ? PT<PREC_BF16>::BK : PT<PREC_F32>::BK;
   const int splits = igemm_wgrad_plan(g.M, g.NN, g.K, BK, &g.k_split);
-  DSG_REQUIRE(splits == 1 || ws, "dsgan_conv_wgrad: needs dsgan_conv_wgrad_workspace floats of scratch");
   g.ws = splits > 1 ? ws : nullptr;
+  DSG_WS(splits > 1 ? (long)splits * g.M * g.NN : 0, ws, ws_elems, "dsgan_conv_wgrad (dsgan_conv_wgrad_workspace)");
   launch_mode<WGRAD>(g, prec, splits, st);
   if (splits > 1) launch_split_reduce(ws, splits, (long)g.M * g.NN, dw, st);
   DSG_CHECK_LAUNCH();

@@ -698,12 +698,13 @@ long dsgan_ms_ssim_workspace(int N, int C, int H, int W) {
 // out[n] per image (size_average=False), out[N] the batch mean (size_average=True).
 int dsgan_ms_ssim(const float* real, const float* fake, float a, float b, int N, int C, int H, int W,
                   const float* win11, float C1, float C2, const float* weights_host, int levels, float* work,
-                  float* stats, float* out, hipStream_t st) {
-  DSG_REQUIRE(real && fake && win11 && weights_host && work && stats && out && N > 0 && C > 0 && levels >= 1 &&
+                  long work_elems, float* stats, float* out, hipStream_t st) {
+  DSG_REQUIRE(real && fake && win11 && weights_host && stats && out && N > 0 && C > 0 && levels >= 1 &&
                   levels <= 8 && N * C <= 65535,
               "dsgan_ms_ssim: bad args");
   DSG_REQUIRE(((H < W ? H : W) > (SS_K - 1) * (1 << (levels - 1))),
               "dsgan_ms_ssim: image smaller than the (win_size-1)*2^(levels-1) ms-ssim minimum");
+  DSG_WS(dsgan_ms_ssim_workspace(N, C, H, W), work, work_elems, "dsgan_ms_ssim (dsgan_ms_ssim_workspace)");
   const int planes = N * C;
   MsArgs m{};
   const float* xr = real;
@@ -775,12 +776,14 @@ static MsArgs ms_args(int levels, const int* hs, const int* ws, const float* wei
 // level in `work` for dsgan_ms_ssim_bwd.  stats: [levels][planes][2] map sums.
 int dsgan_ms_ssim_fwd_train(const float* real, const float* fake, float a, float b, int N, int C, int H, int W,
                             const float* win11, float C1, float C2, const float* weights_host, int levels, float* work,
-                            float* stats, float* out, hipStream_t st) {
-  DSG_REQUIRE(real && fake && win11 && weights_host && work && stats && out && N > 0 && C > 0 && levels >= 1 &&
+                            long work_elems, float* stats, float* out, hipStream_t st) {
+  DSG_REQUIRE(real && fake && win11 && weights_host && stats && out && N > 0 && C > 0 && levels >= 1 &&
                   levels <= 8 && N * C <= 65535,
               "dsgan_ms_ssim_fwd_train: bad args");
   DSG_REQUIRE(((H < W ? H : W) > (SS_K - 1) * (1 << (levels - 1))),
               "dsgan_ms_ssim_fwd_train: image smaller than the (win_size-1)*2^(levels-1) ms-ssim minimum");
+  DSG_WS(dsgan_ms_ssim_train_workspace(N, C, H, W, levels), work, work_elems,
+         "dsgan_ms_ssim_fwd_train (dsgan_ms_ssim_train_workspace)");
   const int planes = N * C;
   int hs[8], ws[8];
   ms_dims(H, W, levels, hs, ws);
@@ -820,10 +823,13 @@ int dsgan_ms_ssim_fwd_train(const float* real, const float* fake, float a, float
 // dfake (+)= d(gout[0] * batch-mean MS-SSIM)/d(fake); work/stats as left by dsgan_ms_ssim_fwd_train.
 int dsgan_ms_ssim_bwd(const float* real, const float* fake, float a, float b, int N, int C, int H, int W,
                       const float* win11, float C1, float C2, const float* weights_host, int levels, float* work,
-                      const float* stats, const float* gout, float* dfake, int accumulate, hipStream_t st) {
-  DSG_REQUIRE(real && fake && win11 && weights_host && work && stats && gout && dfake && N > 0 && C > 0 &&
+                      long work_elems, const float* stats, const float* gout, float* dfake, int accumulate,
+                      hipStream_t st) {
+  DSG_REQUIRE(real && fake && win11 && weights_host && stats && gout && dfake && N > 0 && C > 0 &&
                   levels >= 1 && levels <= 8 && N * C <= 65535,
               "dsgan_ms_ssim_bwd: bad args");
+  DSG_WS(dsgan_ms_ssim_train_workspace(N, C, H, W, levels), work, work_elems,
+         "dsgan_ms_ssim_bwd (dsgan_ms_ssim_train_workspace)");
   DSG_REQUIRE(!accumulate || levels == 1, "dsgan_ms_ssim_bwd: accumulate needs levels == 1 (dfake is staged)");
   const int planes = N * C;
   int hs[8], ws[8];

@@ -1297,9 +1297,9 @@ long dsgan_mlp_wgrad_workspace(int C, int P, int HW, int nb) {
 }
 
 int dsgan_mlp_wgrad(const void* h, long h_bs, int h_bf16, const float* dy, long dy_bs, const void* w1,
-                    const float* b1, const void* w2, float* dw1, float* db1, float* dw2, float* ws, int nb, int C,
-                    int P, int HW, hipStream_t st) {
-  DSG_REQUIRE(h && dy && w1 && b1 && w2 && dw1 && db1 && dw2 && ws && nb > 0, "dsgan_mlp_wgrad: bad args");
+                    const float* b1, const void* w2, float* dw1, float* db1, float* dw2, float* ws, long ws_elems,
+                    int nb, int C, int P, int HW, hipStream_t st) {
+  DSG_REQUIRE(h && dy && w1 && b1 && w2 && dw1 && db1 && dw2 && nb > 0, "dsgan_mlp_wgrad: bad args");
   DSG_REQUIRE(dsgan_mlp_supported(C, P, HW), "dsgan_mlp_wgrad: unsupported shape C=%d P=%d HW=%d", C, P, HW);
   DSG_REQUIRE(((uintptr_t)h & 15) == 0 && ((uintptr_t)dy & 15) == 0 && (h_bs & 7) == 0 && (dy_bs & 3) == 0,
               "dsgan_mlp_wgrad: operands must be 16-byte aligned");
@@ -1308,6 +1308,7 @@ int dsgan_mlp_wgrad(const void* h, long h_bs, int h_bf16, const float* dy, long 
   g.w2 = w2; g.HW = HW; g.nb = nb; g.ws = ws;
   const int S = mlp_wgrad_splits(C, P, HW, nb);
   g.splits = S;
+  DSG_WS((long)S * (4L * C * C + (long)P * 4 * C + 4L * C), ws, ws_elems, "dsgan_mlp_wgrad (dsgan_mlp_wgrad_workspace)");
   with_half([&](auto* t) {
     using T16 = std::remove_pointer_t<decltype(t)>;
     if (C == 64) wgrad_launch<T16, 64, 128, 64, 4, 2>(g, st);

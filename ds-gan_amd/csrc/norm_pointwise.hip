@@ -1236,8 +1236,9 @@ int dsgan_ca_fwd(const float* avg, const float* mx, const float* w1, const float
 int dsgan_ca_bwd(const float* datt, const float* att, const float* avg, const float* mx,
                  const float* hsave, const float* w1, const float* w2, const float* prelu_a,
                  float* davg, float* dmx, float* dw1, float* dw2, float* dprelu_a, int N, int C,
-                 int R, float* ws, hipStream_t st) {
-  DSG_REQUIRE(C > 0 && R > 0 && C <= 4096 && ws, "dsgan_ca_bwd: bad dims / ws (N*(2*R*C+1) floats)");
+                 int R, float* ws, long ws_elems, hipStream_t st) {
+  DSG_REQUIRE(N > 0 && C > 0 && R > 0 && C <= 4096, "dsgan_ca_bwd: bad dims");
+  DSG_WS((long)N * (2L * R * C + 1), ws, ws_elems, "dsgan_ca_bwd (N*(2*R*C+1) floats)");
   const size_t shm = (C + 3 * R) * sizeof(float);
   hipLaunchKernelGGL(ca_bwd_kernel, dim3(N), dim3(256), shm, st, datt, att, avg, mx, hsave, w1, w2,
                      prelu_a, davg, dmx, ws, dw1 != nullptr, dw2 != nullptr, dprelu_a != nullptr, C, R);
@@ -1335,8 +1336,10 @@ int dsgan_act_bwd(const float* dy, const float* pre, float* dx, long n, int act,
   return 0;
 }
 
-int dsgan_channel_sum(const float* dy, long dy_bs, float* out, int N, int C, int HW, float* ws, hipStream_t st) {
-  DSG_REQUIRE(dy && out && ws && N > 0 && C > 0 && HW > 0, "dsgan_channel_sum: bad args (ws: N*C floats)");
+int dsgan_channel_sum(const float* dy, long dy_bs, float* out, int N, int C, int HW, float* ws, long ws_elems,
+                      hipStream_t st) {
+  DSG_REQUIRE(dy && out && N > 0 && C > 0 && HW > 0, "dsgan_channel_sum: bad args");
+  DSG_WS((long)N * C, ws, ws_elems, "dsgan_channel_sum (N*C floats)");
   if (HW <= 8192)
     hipLaunchKernelGGL(channel_sum_kernel<64>, dim3(cdiv((long)N * C, 4)), dim3(256), 0, st, dy, dy_bs, ws, N, C, HW);
   else

@@ -335,15 +335,19 @@ __global__ __launch_bounds__(256) void wtrans_multi_kernel(WtList L) {
   }
 }
 
+// pixel tile of every pconv form
+constexpr int PC_TH = 8, PC_TW = 16;
+static long pc_tiles(int nb, int M, int Ho, int Wo, int BM) {
+  return (long)nb * ((Wo + PC_TW - 1) / PC_TW) * ((Ho + PC_TH - 1) / PC_TH) * ((M + BM - 1) / BM);
+}
+
+// (the split plan -- g.ws / g.kchunk, `splits` -- comes from the entry point, which checked its scratch)
 template <typename T16, int BM, int TH, int TW, int S, int KH, int KW>
-static void pc_launch(PcArgs& g, hipStream_t st) {
+static void pc_launch(PcArgs& g, int splits, hipStream_t st) {
+  static_assert(TH == PC_TH && TW == PC_TW, "pc_tiles");
   g.tiles_w = (g.Wo + TW - 1) / TW;
   g.tiles_h = (g.Ho + TH - 1) / TH;
-  const long tiles = (long)g.nb * g.tiles_w * g.tiles_h * ((g.M + BM - 1) / BM);
-  int kc = 0;
-  const int splits = g.ws ? pc_splits(tiles, g.K / 32, &kc) : 1;
-  if (splits == 1) g.ws = nullptr;
-  g.kchunk = kc;
+  const long tiles = pc_tiles(g.nb, g.M, g.Ho, g.Wo, BM);
   hipLaunchKernelGGL((pconv_kernel<T16, BM, TH, TW, S, KH, KW>), dim3((unsigned)(tiles * splits)), dim3(256), 0, st, g);
   if (splits > 1) {
     const long per = (long)g.nb * g.M * g.Ho * g.Wo;
@@ -354,12 +358,12 @@ static void pc_launch(PcArgs& g, hipStream_t st) {
 }
 
 template <typename T16, int BM>
-static int pc_dispatch(PcArgs& g, int KH, int S, hipStream_t st) {
+static int pc_dispatch(PcArgs& g, int KH, int S, int splits, hipStream_t st) {
   if constexpr (BM <= 128) {   // BM = 256 only for stride 2 (its stride-1 forms spill registers)
-    if (KH == 3 && S == 1) { pc_launch<T16, BM, 8, 16, 1, 3, 3>(g, st); return 0; }
-    if (KH == 4 && S == 1) { pc_launch<T16, BM, 8, 16, 1, 4, 4>(g, st); return 0; }
+    if (KH == 3 && S == 1) { pc_launch<T16, BM, PC_TH, PC_TW, 1, 3, 3>(g, splits, st); return 0; }
+    if (KH == 4 && S == 1) { pc_launch<T16, BM, PC_TH, PC_TW, 1, 4, 4>(g, splits, st); return 0; }
   }
-  if (KH == 4 && S == 2) { pc_launch<T16, BM, 8, 16, 2, 4, 4>(g, st); return 0; }
+  if (KH == 4 && S == 2) { pc_launch<T16, BM, PC_TH, PC_TW, 2, 4, 4>(g, splits, st); return 0; }
   return -1;
 }
 
@@ -427,19 +431,20 @@ static int pc_bm(int nb, int M, int Ho, int Wo) {
 }
 
 // fp32 scratch dsgan_pconv_ws needs (0: the launch is not split)
+// (an upper bound over the strides: a stride-1 launch runs the 256-row choice on 128-row tiles)
 long dsgan_pconv_workspace(int nb, int K, int M, int Ho, int Wo) {
   if (K % 32 != 0 || K <= 0) return 0;
   const int bm = pc_bm(nb, M, Ho, Wo);
-  const long tiles = (long)nb * ((Ho + 7) / 8) * ((Wo + 15) / 16) * ((M + bm - 1) / bm);
   int kc;
-  const int S = pc_splits(tiles, K / 32, &kc);
+  const int S = max(pc_splits(pc_tiles(nb, M, Ho, Wo, bm), K / 32, &kc),
+                    pc_splits(pc_tiles(nb, M, Ho, Wo, bm == 256 ? 128 : bm), K / 32, &kc));
   return S > 1 ? (long)S * nb * M * Ho * Wo : 0;
 }
 
 int dsgan_pconv_ws(const float* X, long x_bs, const void* Wb, const float* bias, float* Y, long y_bs,
                    const float* gpre, long gpre_bs, int nb, int K, int M, int H, int W, int Ho, int Wo,
                    int KH, int KW, int stride, int pad, int act, int gact, float slope, int accumulate,
-                   float* ws, hipStream_t st);
+                   float* ws, long ws_elems, hipStream_t st);
 
 // y[b][m][oh][ow] (+)= act(bias[m] + sum W * x) (* gact'(gpre)); Wb from dsgan_conv_wtrans_bf16.
 int dsgan_pconv(const float* X, long x_bs, const void* Wb, const float* bias, float* Y, long y_bs,
@@ -447,14 +452,14 @@ int dsgan_pconv(const float* X, long x_bs, const void* Wb, const float* bias, fl
                 int KH, int KW, int stride, int pad, int act, int gact, float slope, int accumulate,
                 hipStream_t st) {
   return dsgan_pconv_ws(X, x_bs, Wb, bias, Y, y_bs, gpre, gpre_bs, nb, K, M, H, W, Ho, Wo, KH, KW, stride, pad, act,
-                        gact, slope, accumulate, nullptr, st);
+                        gact, slope, accumulate, nullptr, 0, st);
 }
 
 // Same, with the split-K scratch of dsgan_pconv_workspace (NULL: never split).
 int dsgan_pconv_ws(const float* X, long x_bs, const void* Wb, const float* bias, float* Y, long y_bs,
                    const float* gpre, long gpre_bs, int nb, int K, int M, int H, int W, int Ho, int Wo,
                    int KH, int KW, int stride, int pad, int act, int gact, float slope, int accumulate,
-                   float* ws, hipStream_t st) {
+                   float* ws, long ws_elems, hipStream_t st) {
   DSG_REQUIRE(X && Wb && Y && nb > 0 && M > 0 && Ho > 0 && Wo > 0, "dsgan_pconv: bad args");
   DSG_REQUIRE(dsgan_pconv_supported(K, KH, KW, stride), "dsgan_pconv: unsupported K=%d KH=%d KW=%d stride=%d", K, KH, KW, stride);
   DSG_REQUIRE(((uintptr_t)Wb & 15) == 0, "dsgan_pconv: Wb must be 16-byte aligned");
@@ -464,13 +469,19 @@ int dsgan_pconv_ws(const float* X, long x_bs, const void* Wb, const float* bias,
   g.X = X; g.x_bs = x_bs; g.Wb = (const unsigned short*)Wb; g.Y = Y; g.y_bs = y_bs; g.bias = bias;
   g.gpre = gpre; g.gpre_bs = gpre_bs; g.nb = nb; g.K = K; g.M = M; g.H = H; g.W = W; g.Ho = Ho;
   g.Wo = Wo; g.pad = pad; g.act = act; g.gact = gact; g.slope = slope; g.accumulate = accumulate;
-  g.ws = ws;
-  const int bm = pc_bm(nb, M, Ho, Wo);
+  // tile rows: 256 only at stride 2 (the stride-1 forms spill), where the planner asks for 256
+  const int bm0 = pc_bm(nb, M, Ho, Wo);
+  const int bm = bm0 == 256 ? (stride == 2 ? 256 : 128) : bm0;
+  int kc = 0;
+  const int splits = ws ? pc_splits(pc_tiles(nb, M, Ho, Wo, bm), K / 32, &kc) : 1;
+  g.ws = splits > 1 ? ws : nullptr;
+  g.kchunk = kc;
+  DSG_WS(splits > 1 ? (long)splits * nb * M * Ho * Wo : 0, ws, ws_elems, "dsgan_pconv (dsgan_pconv_workspace)");
   const int rc = with_half([&](auto* t_) {
     using T16 = std::remove_pointer_t<decltype(t_)>;
-    return bm == 256 && stride == 2 ? pc_dispatch<T16, 256>(g, KH, stride, st)
-           : bm == 128 ? pc_dispatch<T16, 128>(g, KH, stride, st)
-                       : pc_dispatch<T16, 64>(g, KH, stride, st);
+    return bm == 256 ? pc_dispatch<T16, 256>(g, KH, stride, splits, st)
+           : bm == 128 ? pc_dispatch<T16, 128>(g, KH, stride, splits, st)
+                       : pc_dispatch<T16, 64>(g, KH, stride, splits, st);
   });
   DSG_REQUIRE(rc == 0, "dsgan_pconv: no kernel for KH=%d stride=%d", KH, stride);
   DSG_CHECK_LAUNCH();

@@ -322,7 +322,7 @@ long dsgan_pw_f32_wgrad_workspace(int M, int N, int P, int nb) {
 // Same argument meaning as dsgan_pw_gemm (mode 0 FWD / 1 DGRAD / 2 WGRAD), fp32 operands.
 int dsgan_pw_gemm_f32(int mode, const float* A, long a_bs, const float* B, long b_bs, float* Y, long y_bs,
                       const float* bias, const float* gpre, long gpre_bs, int M, int N, int K, int P, int nb, int act,
-                      int gact, int accumulate, float slope, float* ws, hipStream_t st) {
+                      int gact, int accumulate, float slope, float* ws, long ws_elems, hipStream_t st) {
   DSG_REQUIRE(A && B && Y && M > 0 && N > 0 && K > 0 && P > 0 && nb > 0, "dsgan_pw_gemm_f32: bad args");
   PfArgs g{};
   g.A = A; g.a_bs = a_bs; g.B = B; g.b_bs = b_bs; g.Y = Y; g.y_bs = y_bs; g.bias = bias;
@@ -342,10 +342,11 @@ int dsgan_pw_gemm_f32(int mode, const float* A, long a_bs, const float* B, long 
     DSG_REQUIRE(dsgan_pw_f32_supported(mode, M, K, P, a_bs, b_bs, A, B), "dsgan_pw_gemm_f32: unsupported WGRAD shape");
     g.M = M; g.N = N; g.K = nb * P;
     const int splits = pf_wgrad_plan(M, N, g.K, &g.k_split);
-    DSG_REQUIRE(splits == 1 || ws, "dsgan_pw_gemm_f32: WGRAD needs dsgan_pw_f32_wgrad_workspace floats of scratch");
     g.ws = splits > 1 ? ws : nullptr;
     g.asum = const_cast<float*>(bias);   // WGRAD: bias (nullable) receives the bias grad += sum_k DY
     g.bias = nullptr;
+    DSG_WS(splits > 1 ? (long)splits * ((long)M * N + (g.asum ? M : 0)) : 0, ws, ws_elems,
+           "dsgan_pw_gemm_f32 (WGRAD; dsgan_pw_f32_wgrad_workspace)");
     if (M > 64) pf_launch<PF_WGRAD, 128>(g, splits, st);
     else if (pf_wgrad_bn(M, N) == 64) pf_launch<PF_WGRAD, 64, 64>(g, splits, st);
     else pf_launch<PF_WGRAD, 64>(g, splits, st);
@@ -359,6 +360,7 @@ int dsgan_pw_gemm_f32(int mode, const float* A, long a_bs, const float* B, long 
   } else {
     DSG_REQUIRE(dsgan_pw_f32_supported(mode, M, K, P, a_bs, b_bs, A, B), "dsgan_pw_gemm_f32: unsupported shape");
     g.M = M; g.N = nb * P; g.K = K;
+    DSG_WS(0, ws, ws_elems, "dsgan_pw_gemm_f32");
     if (mode == PF_FWD) pf_launch_fd<PF_FWD>(g, st);
     else pf_launch_fd<PF_DGRAD>(g, st);
   }

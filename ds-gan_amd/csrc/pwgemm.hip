@@ -74,7 +74,9 @@ static bool fd_split_ok(const PwArgs& g) {
   return a16(g.Y, g.y_bs) && a16(g.ypre, g.ypre_bs) && a16(g.gpre, g.gpre_bs);
 }
 
-static void fd_dispatch(int mode, PwArgs& g, int bm, int abf, int bbf, float* ws, hipStream_t st) {
+// The split plan of a FWD / DGRAD launch on tile bm (ws: the caller's scratch, NULL = never split):
+// sets g.k_split / g.ws / the K-step variant and returns the split count.
+static int fd_plan(PwArgs& g, int bm, float* ws) {
   int splits = 1;
   g.k_split = 0;
   g.ws = nullptr;
@@ -85,6 +87,11 @@ static void fd_dispatch(int mode, PwArgs& g, int bm, int abf, int bbf, float* ws
     if (splits > 1) g.ws = ws;
     else g.k_split = 0;
   }
+  return splits;
+}
+// scratch that plan writes: partials [split][b][M][P]
+static long fd_need(const PwArgs& g, int splits) { return splits > 1 ? (long)splits * g.M * g.N : 0; }
+static void fd_launch(int mode, const PwArgs& g, int bm, int abf, int bbf, int splits, hipStream_t st) {
   if (half_type() == HALF_F16) pw_fd_launch<_Float16>(mode, g, bm, abf, bbf, splits, st);
   else pw_fd_launch<__bf16>(mode, g, bm, abf, bbf, splits, st);
 }
@@ -305,6 +312,11 @@ static int wgrad_cfg_k(PwArgs& g, bool any_bf16, int* bm) {
   return splits;
 }
 
+// scratch a weight-grad plan writes: weight partials [split][M][N], then bias-sum partials [split][M]
+static long wgrad_need(const PwArgs& g, int splits) {
+  return splits > 1 ? (long)splits * ((long)g.M * g.N + (g.asum ? g.M : 0)) : 0;
+}
+
 static void wgrad_finish(const PwArgs& g, int splits, hipStream_t st) {
   if (splits > 1) {
     // the weight and bias-sum partials in one launch
@@ -339,7 +351,7 @@ extern "C" int dsgan_pw_gemm(int mode, const float* A, long a_bs, const float* B
                              float* Y, long y_bs, const float* bias, float* ypre, long ypre_bs,
                              const float* gpre, long gpre_bs, int M, int N, int K, int P, int nb,
                              int act, int gact, int bact, int accumulate, float slope, float* ws,
-                             hipStream_t st) {
+                             long ws_elems, hipStream_t st) {
   DSG_REQUIRE(A && B && Y && M > 0 && N > 0 && K > 0 && P > 0 && nb > 0, "dsgan_pw_gemm: bad args");
   PwArgs g{};
   g.A = A; g.a_bs = a_bs; g.B = B; g.b_bs = b_bs; g.Y = Y; g.y_bs = y_bs; g.bias = bias;
@@ -355,10 +367,10 @@ extern "C" int dsgan_pw_gemm(int mode, const float* A, long a_bs, const float* B
     g.M = M; g.N = N; g.K = nb * P;
     int bm;
     const int splits = wgrad_cfg_k(g, false, &bm);
-    DSG_REQUIRE(splits == 1 || ws, "dsgan_pw_gemm: WGRAD needs the dsgan_pw_wgrad_workspace scratch");
     g.ws = splits > 1 ? ws : nullptr;
     g.asum = const_cast<float*>(bias);   // WGRAD: bias (nullable) receives the bias grad += sum_k A
     g.bias = nullptr;
+    DSG_WS(wgrad_need(g, splits), ws, ws_elems, "dsgan_pw_gemm (WGRAD; dsgan_pw_wgrad_workspace)");
     wg_dispatch(g, bm, 0, 0, splits, st);
     wgrad_finish(g, splits, st);
   } else {
@@ -368,7 +380,10 @@ extern "C" int dsgan_pw_gemm(int mode, const float* A, long a_bs, const float* B
     DSG_REQUIRE((long)K * P * 4 < lim && (long)M * K * 4 < lim, "dsgan_pw_gemm: operand exceeds 4 GiB buffer range");
     g.a_range = (unsigned)((long)M * K * 4);
     g.b_range = (unsigned)((long)K * P * 4);
-    fd_dispatch(mode, g, fd_tile(g, false), 0, 0, ws, st);   // ws: dsgan_pw_fd_workspace (NULL: never split)
+    const int bm = fd_tile(g, false);
+    const int splits = fd_plan(g, bm, ws);   // ws: dsgan_pw_fd_workspace (NULL: never split)
+    DSG_WS(fd_need(g, splits), ws, ws_elems, "dsgan_pw_gemm (dsgan_pw_fd_workspace)");
+    fd_launch(mode, g, bm, 0, 0, splits, st);
   }
   DSG_CHECK_LAUNCH();
   return 0;
@@ -380,7 +395,8 @@ extern "C" int dsgan_pw_gemm(int mode, const float* A, long a_bs, const float* B
 // P % 128 == 0, K % 8 == 0, 16-byte aligned.
 extern "C" int dsgan_pw_fwd_io_ws(const void* W, int w_bf16, const void* X, long x_bs, int x_bf16, void* Y, long y_bs,
                                   int y_bf16, const void* ypre, long ypre_bs, int ypre_grad_bf16, const float* bias, int M,
-                                  int K, int P, int nb, int act, int accumulate, float slope, float* ws, hipStream_t st) {
+                                  int K, int P, int nb, int act, int accumulate, float slope, float* ws, long ws_elems,
+                                  hipStream_t st) {
   DSG_REQUIRE(W && X && Y && M >= 16 && K > 0 && P > 0 && nb > 0, "dsgan_pw_fwd_io: bad args");
   DSG_REQUIRE(P % 128 == 0 && K % 8 == 0 && al16(W) && al16(X) && al16(Y) && (x_bs & 7) == 0 && (y_bs & 7) == 0 &&
                   !(y_bf16 && accumulate),
@@ -394,7 +410,10 @@ extern "C" int dsgan_pw_fwd_io_ws(const void* W, int w_bf16, const void* X, long
   g.P = P; g.M = M; g.N = nb * P; g.K = K;
   g.a_range = (unsigned)((long)M * K * (w_bf16 ? 2 : 4));
   g.b_range = (unsigned)((long)K * P * (x_bf16 ? 2 : 4));
-  fd_dispatch(PW_FWD, g, fd_tile_k(g, w_bf16 || x_bf16), w_bf16, x_bf16, ws, st);
+  const int bm = fd_tile_k(g, w_bf16 || x_bf16);
+  const int splits = fd_plan(g, bm, ws);
+  DSG_WS(fd_need(g, splits), ws, ws_elems, "dsgan_pw_fwd_io (dsgan_pw_fd_workspace)");
+  fd_launch(PW_FWD, g, bm, w_bf16, x_bf16, splits, st);
   DSG_CHECK_LAUNCH();
   return 0;
 }
@@ -403,7 +422,7 @@ extern "C" int dsgan_pw_fwd_io(const void* W, int w_bf16, const void* X, long x_
                                int y_bf16, const void* ypre, long ypre_bs, int ypre_grad_bf16, const float* bias, int M,
                                int K, int P, int nb, int act, int accumulate, float slope, hipStream_t st) {
   return dsgan_pw_fwd_io_ws(W, w_bf16, X, x_bs, x_bf16, Y, y_bs, y_bf16, ypre, ypre_bs, ypre_grad_bf16, bias, M, K, P, nb,
-                            act, accumulate, slope, nullptr, st);
+                            act, accumulate, slope, nullptr, 0, st);
 }
 
 // Data-grad with bf16 operands/outputs (the unfused MLP blocks' backward):
@@ -412,7 +431,7 @@ extern "C" int dsgan_pw_fwd_io(const void* W, int w_bf16, const void* X, long x_
 // act'(pre) written by dsgan_pw_fwd_io (ypre_grad_bf16).  P % 128 == 0, 16-byte aligned.
 extern "C" int dsgan_pw_dgrad_io_ws(const void* W, int w_bf16, const void* DY, long dy_bs, int dy_bf16, void* DX,
                                     long dx_bs, int dx_bf16, const void* GP, long gp_bs, int M, int K, int P, int nb,
-                                    int accumulate, float* ws, hipStream_t st) {
+                                    int accumulate, float* ws, long ws_elems, hipStream_t st) {
   DSG_REQUIRE(W && DY && DX && M > 0 && K > 0 && nb > 0, "dsgan_pw_dgrad_io: bad args");
   DSG_REQUIRE(dsgan_pw_supported(PW_DGRAD, M, K, P, 0, dy_bs, W, DY) && al16(DX) && (dy_bs & 7) == 0 &&
                   (dx_bs & 7) == 0 && (!GP || (al16(GP) && (gp_bs & 7) == 0)) && !(dx_bf16 && accumulate),
@@ -425,7 +444,10 @@ extern "C" int dsgan_pw_dgrad_io_ws(const void* W, int w_bf16, const void* DY, l
   g.accumulate = accumulate; g.P = P; g.M = M; g.N = nb * P; g.K = K;
   g.a_range = (unsigned)((long)M * K * (w_bf16 ? 2 : 4));
   g.b_range = (unsigned)((long)K * P * (dy_bf16 ? 2 : 4));
-  fd_dispatch(PW_DGRAD, g, fd_tile_k(g, w_bf16 || dy_bf16), w_bf16, dy_bf16, ws, st);
+  const int bm = fd_tile_k(g, w_bf16 || dy_bf16);
+  const int splits = fd_plan(g, bm, ws);
+  DSG_WS(fd_need(g, splits), ws, ws_elems, "dsgan_pw_dgrad_io (dsgan_pw_fd_workspace)");
+  fd_launch(PW_DGRAD, g, bm, w_bf16, dy_bf16, splits, st);
   DSG_CHECK_LAUNCH();
   return 0;
 }
@@ -434,7 +456,7 @@ extern "C" int dsgan_pw_dgrad_io(const void* W, int w_bf16, const void* DY, long
                                  int dx_bf16, const void* GP, long gp_bs, int M, int K, int P, int nb,
                                  int accumulate, hipStream_t st) {
   return dsgan_pw_dgrad_io_ws(W, w_bf16, DY, dy_bs, dy_bf16, DX, dx_bs, dx_bf16, GP, gp_bs, M, K, P, nb, accumulate,
-                              nullptr, st);
+                              nullptr, 0, st);
 }
 
 // Scratch (floats) of a split-K FWD (mode 0) / DGRAD (1) launch of M output channels over K at nb
@@ -444,7 +466,8 @@ extern "C" long dsgan_pw_fd_workspace(int mode, int M, int K, int P, int nb) {
   if ((mode != PW_FWD && mode != PW_DGRAD) || M <= 0 || K <= 0 || P <= 0 || nb <= 0 || P % 128) return 0;
   PwArgs g{};
   g.M = M; g.N = nb * P; g.K = K; g.P = P;
-  const int bm = use_bm256(g) ? 256 : M > 64 ? 128 : 64;
+  // the 128 / 64-row tile is the only one that splits (a knob may pick it where 256 rows would run)
+  const int bm = M > 64 ? 128 : 64;
   int ks;
   const int splits = max(fd_splits(g, bm, PBK, &ks), fd_splits(g, bm, 64, &ks));
   return splits > 1 ? (long)splits * M * nb * P : 0;
@@ -466,13 +489,13 @@ extern "C" long dsgan_pw_wgrad_workspace(int M, int N, int P, int nb) {
   PwArgs g{};
   g.M = M; g.N = N; g.P = P; g.K = nb * P;
   int bm;   // enough for either tile plan (the caller's operand dtypes pick one)
-  const int splits = max(wgrad_cfg(g, false, &bm), wgrad_cfg(g, true, &bm));
+  const int splits = max(wgrad_cfg_k(g, false, &bm), wgrad_cfg_k(g, true, &bm));
   return splits > 1 ? (long)splits * ((long)M * N + M) : 0;   // weight partials, then bias-sum partials
 }
 
 extern "C" int dsgan_pw_wgrad_mixed(const void* A, long a_bs, int a_bf16, const void* B, long b_bs,
                                     int b_bf16, float* DW, float* db, int M, int N, int P, int nb, float* ws,
-                                    hipStream_t st) {
+                                    long ws_elems, hipStream_t st) {
   DSG_REQUIRE(A && B && DW && M >= 16 && N > 0 && P > 0 && nb > 0, "dsgan_pw_wgrad_mixed: bad args");
   DSG_REQUIRE(P % 32 == 0 && al16(A) && al16(B) && (a_bs & 7) == 0 && (b_bs & 7) == 0,
               "dsgan_pw_wgrad_mixed: P %% 32 and 16-byte alignment required");
@@ -485,8 +508,8 @@ extern "C" int dsgan_pw_wgrad_mixed(const void* A, long a_bs, int a_bf16, const 
   g.M = M; g.N = N; g.K = nb * P;
   int bm;
   const int splits = wgrad_cfg_k(g, a_bf16 || b_bf16, &bm);
-  DSG_REQUIRE(splits == 1 || ws, "dsgan_pw_wgrad_mixed: needs the dsgan_pw_wgrad_workspace scratch");
   g.ws = splits > 1 ? ws : nullptr;
+  DSG_WS(wgrad_need(g, splits), ws, ws_elems, "dsgan_pw_wgrad_mixed (dsgan_pw_wgrad_workspace)");
   wg_dispatch(g, bm, a_bf16, b_bf16, splits, st);
   wgrad_finish(g, splits, st);
   DSG_CHECK_LAUNCH();

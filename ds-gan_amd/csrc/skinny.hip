@@ -522,7 +522,7 @@ long dsgan_conv_wgrad_small_workspace(int N, int Cin, int Cout, int KH, int KW, 
 
 int dsgan_conv_wgrad_small(const float* dy, long dy_bs, const float* x, long x_bs, float* dw, int N,
                            int Cin, int H, int W, int Cout, int KH, int KW, int stride, int pad, int Ho,
-                           int Wo, float* ws, hipStream_t st) {
+                           int Wo, float* ws, long ws_elems, hipStream_t st) {
   DSG_REQUIRE(dy && x && dw && N > 0 && Cin > 0 && Cout > 0 && Ho > 0 && Wo > 0, "dsgan_conv_wgrad_small: bad args");
   const int T = KH * KW;
   DSG_REQUIRE(T == 1 || T == 9 || T == 16, "dsgan_conv_wgrad_small: KH*KW must be 1, 9 or 16");
@@ -542,14 +542,16 @@ int dsgan_conv_wgrad_small(const float* dy, long dy_bs, const float* x, long x_b
   const long chunks = ws_chunks(big, (long)N * Ho * Wo, &ppb);
   a.pix_per_block = ppb;
   DSG_REQUIRE(chunks <= 65535, "dsgan_conv_wgrad_small: grid too large");
-  DSG_REQUIRE(chunks == 1 || ws, "dsgan_conv_wgrad_small: needs dsgan_conv_wgrad_small_workspace floats of scratch");
   a.ws = chunks > 1 ? ws : nullptr;
   const bool s4 = a.nsmall <= 4;
-  if (T == 1 && stride == 1 && pad == 0 && Ho == H && Wo == W && (Ho * Wo) % 4 == 0 && (x_bs & 3) == 0 &&
-      (dy_bs & 3) == 0 && ((uintptr_t)x & 15) == 0 && ((uintptr_t)dy & 15) == 0) {
-    // pixel-quad walk: chunks of whole 1024-pixel steps (never more chunks than the workspace has)
-    const long ppb4 = (ppb + 1023) / 1024 * 1024;
-    const long chunks4 = ((long)N * Ho * Wo + ppb4 - 1) / ppb4;
+  const bool quad = T == 1 && stride == 1 && pad == 0 && Ho == H && Wo == W && (Ho * Wo) % 4 == 0 && (x_bs & 3) == 0 &&
+                    (dy_bs & 3) == 0 && ((uintptr_t)x & 15) == 0 && ((uintptr_t)dy & 15) == 0;
+  // pixel-quad walk: chunks of whole 1024-pixel steps (never more chunks than the general plan)
+  const long ppb4 = (ppb + 1023) / 1024 * 1024;
+  const long chunks4 = ((long)N * Ho * Wo + ppb4 - 1) / ppb4;
+  const long used = quad ? chunks4 : chunks;
+  DSG_WS(used > 1 ? used * Cout * Cin * T : 0, ws, ws_elems, "dsgan_conv_wgrad_small (dsgan_conv_wgrad_small_workspace)");
+  if (quad) {
     a.pix_per_block = ppb4;
     a.ws = chunks4 > 1 ? ws : nullptr;
     const dim3 grid((unsigned)big, (unsigned)chunks4);

@@ -349,7 +349,8 @@ long dsgan_tconv_workspace(int nb, int K, int M, int Hout, int Wout, int ntaps) 
 int dsgan_tconv_ws(const float* X, long x_bs, const float* Wt, const float* bias, float* Y, long y_bs,
                    const float* gpre, long gpre_bs, int nb, int K, int M, int Hin, int Win, int Hout,
                    int Wout, int stride, int ntaps, const int* dh, const int* dw, int Hdst, int Wdst,
-                   int os, int ph, int pw, int act, int gact, float slope, int wt_bf16, float* ws, hipStream_t st);
+                   int os, int ph, int pw, int act, int gact, float slope, int wt_bf16, float* ws, long ws_elems,
+                   hipStream_t st);
 
 // Generic launcher.  taps: ntaps pairs (dh, dw).  dst lattice: (oh*os+ph, ow*os+pw) in Hdst x Wdst.
 int dsgan_tconv(const float* X, long x_bs, const float* Wt, const float* bias, float* Y, long y_bs,
@@ -357,7 +358,7 @@ int dsgan_tconv(const float* X, long x_bs, const float* Wt, const float* bias, f
                 int Wout, int stride, int ntaps, const int* dh, const int* dw, int Hdst, int Wdst,
                 int os, int ph, int pw, int act, int gact, float slope, hipStream_t st) {
   return dsgan_tconv_ws(X, x_bs, Wt, bias, Y, y_bs, gpre, gpre_bs, nb, K, M, Hin, Win, Hout, Wout, stride, ntaps,
-                        dh, dw, Hdst, Wdst, os, ph, pw, act, gact, slope, 0, nullptr, st);
+                        dh, dw, Hdst, Wdst, os, ph, pw, act, gact, slope, 0, nullptr, 0, st);
 }
 
 }  // extern "C"
@@ -366,7 +367,7 @@ static int tconv_impl(const float* X, long x_bs, const float* Wt, const float* b
                       const float* gpre, long gpre_bs, int nb, int K, int M, int Hin, int Win, int Hout,
                       int Wout, int stride, int ntaps, const int* dh, const int* dw, int Hdst, int Wdst,
                       int os, int ph, int pw, int act, int gact, float slope, int wt_bf16, int x_half, float* ws,
-                      hipStream_t st) {
+                      long ws_elems, hipStream_t st) {
   DSG_REQUIRE(X && Wt && Y && nb > 0 && M > 0 && Hout > 0 && Wout > 0, "dsgan_tconv: bad args");
   DSG_REQUIRE(K % TBK == 0 && K > 0, "dsgan_tconv: K (input channels) must be a multiple of 32");
   DSG_REQUIRE(ntaps >= 1 && ntaps <= T_MAXTAPS, "dsgan_tconv: 1..16 taps");
@@ -388,6 +389,7 @@ static int tconv_impl(const float* X, long x_bs, const float* Wt, const float* b
   g.ws = S > 1 ? ws : nullptr;
   g.kchunk = S > 1 ? kc : 0;
   DSG_REQUIRE(S == 1 || (long)S * nb * M * Hout * Wout < (1L << 31), "dsgan_tconv: split partials too large");
+  DSG_WS(S > 1 ? (long)S * nb * M * Hout * Wout : 0, ws, ws_elems, "dsgan_tconv (dsgan_tconv_workspace)");
   const dim3 grid((unsigned)(tiles * S));
   with_half([&](auto* t_) {
     using T16 = std::remove_pointer_t<decltype(t_)>;
@@ -419,9 +421,10 @@ extern "C" {
 int dsgan_tconv_ws(const float* X, long x_bs, const float* Wt, const float* bias, float* Y, long y_bs,
                    const float* gpre, long gpre_bs, int nb, int K, int M, int Hin, int Win, int Hout,
                    int Wout, int stride, int ntaps, const int* dh, const int* dw, int Hdst, int Wdst,
-                   int os, int ph, int pw, int act, int gact, float slope, int wt_bf16, float* ws, hipStream_t st) {
+                   int os, int ph, int pw, int act, int gact, float slope, int wt_bf16, float* ws, long ws_elems,
+                   hipStream_t st) {
   return tconv_impl(X, x_bs, Wt, bias, Y, y_bs, gpre, gpre_bs, nb, K, M, Hin, Win, Hout, Wout, stride, ntaps, dh, dw,
-                    Hdst, Wdst, os, ph, pw, act, gact, slope, wt_bf16, 0, ws, st);
+                    Hdst, Wdst, os, ph, pw, act, gact, slope, wt_bf16, 0, ws, ws_elems, st);
 }
 
 // Same with X in the library's 16-bit half type (x_bs in elements) and 16-bit Wt
@@ -429,10 +432,11 @@ int dsgan_tconv_ws(const float* X, long x_bs, const float* Wt, const float* bias
 int dsgan_tconv_ws_xh(const void* Xh, long x_bs, const void* Wt, const float* bias, float* Y, long y_bs,
                       const float* gpre, long gpre_bs, int nb, int K, int M, int Hin, int Win, int Hout,
                       int Wout, int stride, int ntaps, const int* dh, const int* dw, int Hdst, int Wdst,
-                      int os, int ph, int pw, int act, int gact, float slope, float* ws, hipStream_t st) {
+                      int os, int ph, int pw, int act, int gact, float slope, float* ws, long ws_elems,
+                      hipStream_t st) {
   DSG_REQUIRE(K % 8 == 0, "dsgan_tconv_ws_xh: K %% 8 != 0");
   return tconv_impl((const float*)Xh, x_bs, (const float*)Wt, bias, Y, y_bs, gpre, gpre_bs, nb, K, M, Hin, Win, Hout,
-                    Wout, stride, ntaps, dh, dw, Hdst, Wdst, os, ph, pw, act, gact, slope, 1, 1, ws, st);
+                    Wout, stride, ntaps, dh, dw, Hdst, Wdst, os, ph, pw, act, gact, slope, 1, 1, ws, ws_elems, st);
 }
 
 }  // extern "C"

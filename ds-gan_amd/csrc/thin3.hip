@@ -297,9 +297,9 @@ long dsgan_thin3_wgrad_workspace(int nb, int K, int M, int H, int W) {
 }
 
 // dw[M][K][3][3] += weight-grad (dy [nb][M][H][W], x [nb][K][H][W]); ws: dsgan_thin3_wgrad_workspace floats
-int dsgan_thin3_wgrad(const float* dy, long dy_bs, const float* x, long x_bs, float* dw, float* ws, int nb, int K,
-                      int M, int H, int W, hipStream_t st) {
-  DSG_REQUIRE(dy && x && dw && ws && nb > 0 && K > 0 && dsgan_thin3_supported(M, H, W, dy_bs, x_bs) &&
+int dsgan_thin3_wgrad(const float* dy, long dy_bs, const float* x, long x_bs, float* dw, float* ws, long ws_elems,
+                      int nb, int K, int M, int H, int W, hipStream_t st) {
+  DSG_REQUIRE(dy && x && dw && nb > 0 && K > 0 && dsgan_thin3_supported(M, H, W, dy_bs, x_bs) &&
                   ((uintptr_t)dy & 15) == 0,
               "dsgan_thin3_wgrad: unsupported shape/alignment");
   T3Args a{};
@@ -311,6 +311,7 @@ int dsgan_thin3_wgrad(const float* dy, long dy_bs, const float* x, long x_bs, fl
   int spw;
   const long splits = t3_wgrad_plan(nb, K, H, W, &spw);
   a.strips_per_wg = spw;
+  DSG_WS(splits * (long)M * K * 9, ws, ws_elems, "dsgan_thin3_wgrad (dsgan_thin3_wgrad_workspace)");
   const dim3 grid((unsigned)((K + 4 * T3_CW - 1) / (4 * T3_CW)), (unsigned)splits);
   if (M <= 1) hipLaunchKernelGGL((thin3_wgrad_kernel<1, T3_CW>), grid, dim3(256), 0, st, a);
   else if (M <= 2) hipLaunchKernelGGL((thin3_wgrad_kernel<2, T3_CW>), grid, dim3(256), 0, st, a);

@@ -37,6 +37,7 @@ struct WcArgs {
   int nbw, nbh, nblk, bps;     // pixel blocks per row / per column / total, blocks per split
   int mt, ct;                  // M tiles (64), C tiles (32)
   int vec_d;                   // D rows float4-loadable
+  float* dbp;                  // (nullable) bias-grad partials [splits][M] = sum over the split's pixels of D
 };
 
 constexpr int WC_TW = 16, WC_TH = 4;
@@ -121,6 +122,13 @@ __global__ __launch_bounds__(256, XH ? 2 : 1) void wconv_kernel(WcArgs g) {
 
   float4 ra[A_IT], rb[XH ? 1 : B_IT];
   uint2 rh[XH ? B_IT : 1];
+  // dbp: the c-tile-0 workgroups also sum their staged fp32 D rows (the conv's bias grad), per
+  // thread in block order, then over the 16 lanes of a row (fixed order: deterministic)
+  // (compiled out of the 16-bit-X ConvTranspose form, which never folds a bias: its codegen is tight)
+  float asr[XH ? 1 : A_IT];
+#pragma unroll
+  for (int i = 0; i < (XH ? 1 : A_IT); ++i) asr[i] = 0.f;
+  const bool want_db = !XH && g.dbp != nullptr && c_t == 0;
 
   auto load = [&](int q) __attribute__((always_inline)) {
     const int b = q / per_img, rem = q - b * per_img;
@@ -171,6 +179,8 @@ __global__ __launch_bounds__(256, XH ? 2 : 1) void wconv_kernel(WcArgs g) {
       const int it = tid + i * 256, mm = it / (PX / 4), qq = it % (PX / 4);
       const wbf16x4 v = {(T16)ra[i].x, (T16)ra[i].y, (T16)ra[i].z, (T16)ra[i].w};
       *reinterpret_cast<wbf16x4*>(As + mm * A_STR + qq * 4) = v;
+      if constexpr (!XH)
+        if (want_db) asr[i] += (ra[i].x + ra[i].y) + (ra[i].z + ra[i].w);
     }
 #pragma unroll
     for (int i = 0; i < B_IT; ++i) {
@@ -260,6 +270,16 @@ __global__ __launch_bounds__(256, XH ? 2 : 1) void wconv_kernel(WcArgs g) {
           }
       }
     }
+    if constexpr (!XH) if (want_db) {
+      static_assert(PX / 4 == 16, "a D row is 16 consecutive items");
+#pragma unroll
+      for (int i = 0; i < A_IT; ++i) {
+        float t = asr[i];
+        t += __shfl_xor(t, 1, 64); t += __shfl_xor(t, 2, 64); t += __shfl_xor(t, 4, 64); t += __shfl_xor(t, 8, 64);
+        const int it = tid + i * 256, m = m0 + it / (PX / 4);
+        if ((it & 15) == 0 && m < g.M) g.dbp[(long)split * g.M + m] = t;
+      }
+    }
   };
   switch (wave) {
     case 0: run(std::integral_constant<int, 0>{}); break;
@@ -345,7 +365,8 @@ int dsgan_wconv_supported(int C, int KH, int KW, int stride) {
 long dsgan_wconv_workspace(int nb, int C, int M, int Ho, int Wo, int KH, int KW) {
   // (enough for either form: the 16-bit-X launches plan for twice the workgroups)
   const WcPlan p = wc_plan(nb, C, M, Ho, Wo), q = wc_plan(nb, C, M, Ho, Wo, WC_TARGET_WG_XH);
-  return (long)(p.splits > q.splits ? p.splits : q.splits) * KH * KW * M * C;
+  // (+ splits * M: the bias-grad partials of dsgan_wconv_db)
+  return (long)(p.splits > q.splits ? p.splits : q.splits) * ((long)KH * KW * M * C + M);
 }
 
 // dw[M][C][KH][KW] += weight-grad of y = conv(x, w, stride, pad = 1): D = dy [nb][M][Ho][Wo],
@@ -353,9 +374,10 @@ long dsgan_wconv_workspace(int nb, int C, int M, int Ho, int Wo, int KH, int KW)
 // ws: dsgan_wconv_workspace() floats.
 }  // extern "C"
 
-static int wconv_impl(const float* D, long d_bs, const void* X, long x_bs, bool xh, float* dw, float* ws, int nb,
-                      int C, int M, int H, int W, int Ho, int Wo, int KH, int KW, int stride, int pad, hipStream_t st) {
-  DSG_REQUIRE(D && X && dw && ws && nb > 0 && M > 0 && Ho > 0 && Wo > 0, "dsgan_wconv: bad args");
+static int wconv_impl(const float* D, long d_bs, const void* X, long x_bs, bool xh, float* dw, float* db, float* ws,
+                      long ws_elems, int nb, int C, int M, int H, int W, int Ho, int Wo, int KH, int KW, int stride,
+                      int pad, hipStream_t st) {
+  DSG_REQUIRE(D && X && dw && nb > 0 && M > 0 && Ho > 0 && Wo > 0, "dsgan_wconv: bad args");
   DSG_REQUIRE(dsgan_wconv_supported(C, KH, KW, stride) && pad == 1, "dsgan_wconv: unsupported C=%d K=%dx%d stride=%d pad=%d",
               C, KH, KW, stride, pad);
   DSG_REQUIRE(W % 4 == 0 && x_bs % 4 == 0 && ((uintptr_t)X & (xh ? 7 : 15)) == 0,
@@ -364,11 +386,14 @@ static int wconv_impl(const float* D, long d_bs, const void* X, long x_bs, bool 
               "dsgan_wconv: output size inconsistent with input/pad");
   DSG_REQUIRE(!xh || (KH == 3 && stride == 2), "dsgan_wconv_xh: 3x3 stride-2 only");
   const WcPlan p = wc_plan(nb, C, M, Ho, Wo, xh ? WC_TARGET_WG_XH : WC_TARGET_WG);
+  // weight partials [splits][T][M][C], then (db) the bias partials [splits][M]
+  DSG_WS((long)p.splits * ((long)KH * KW * M * C + (db ? M : 0)), ws, ws_elems, "dsgan_wconv (dsgan_wconv_workspace)");
   WcArgs g{};
   g.D = D; g.d_bs = d_bs; g.X = (const float*)X; g.x_bs = x_bs; g.P = ws;
   g.nb = nb; g.M = M; g.C = C; g.H = H; g.W = W; g.Ho = Ho; g.Wo = Wo;
   g.nbw = p.nbw; g.nbh = p.nbh; g.nblk = p.nblk; g.bps = p.bps; g.mt = p.mt; g.ct = p.ct;
   g.vec_d = ((uintptr_t)D % 16 == 0) && (d_bs % 4 == 0) && (Wo % 4 == 0);
+  g.dbp = db ? ws + (long)p.splits * KH * KW * M * C : nullptr;
   const int grid = p.splits * p.mt * p.ct;
   with_half([&](auto* t_) {
     using T16 = std::remove_pointer_t<decltype(t_)>;
@@ -382,22 +407,32 @@ static int wconv_impl(const float* D, long d_bs, const void* X, long x_bs, bool 
   long blocks = (total4 + 255) / 256;
   if (blocks > 4096) blocks = 4096;
   hipLaunchKernelGGL(wconv_reduce_kernel, dim3((unsigned)blocks), dim3(256), 0, st, ws, p.splits, KH * KW, M, C, dw);
+  if (db) launch_split_reduce(g.dbp, p.splits, M, db, st);
   DSG_CHECK_LAUNCH();
   return 0;
 }
 
 extern "C" {
 
-int dsgan_wconv(const float* D, long d_bs, const float* X, long x_bs, float* dw, float* ws, int nb, int C, int M,
-                int H, int W, int Ho, int Wo, int KH, int KW, int stride, int pad, hipStream_t st) {
-  return wconv_impl(D, d_bs, X, x_bs, false, dw, ws, nb, C, M, H, W, Ho, Wo, KH, KW, stride, pad, st);
+int dsgan_wconv(const float* D, long d_bs, const float* X, long x_bs, float* dw, float* ws, long ws_elems, int nb, int C,
+                int M, int H, int W, int Ho, int Wo, int KH, int KW, int stride, int pad, hipStream_t st) {
+  return wconv_impl(D, d_bs, X, x_bs, false, dw, nullptr, ws, ws_elems, nb, C, M, H, W, Ho, Wo, KH, KW, stride, pad, st);
+}
+
+// Same, plus the conv's bias grad db[m] += sum_{b, oh, ow} D[b][m][oh][ow] from the staged D tiles
+// (fp32 values, fixed order) -- no separate channel-sum pass over D.
+int dsgan_wconv_db(const float* D, long d_bs, const float* X, long x_bs, float* dw, float* db, float* ws, long ws_elems,
+                   int nb, int C, int M, int H, int W, int Ho, int Wo, int KH, int KW, int stride, int pad,
+                   hipStream_t st) {
+  DSG_REQUIRE(db, "dsgan_wconv_db: db is NULL");
+  return wconv_impl(D, d_bs, X, x_bs, false, dw, db, ws, ws_elems, nb, C, M, H, W, Ho, Wo, KH, KW, stride, pad, st);
 }
 
 // Same with X in the library's 16-bit half type (x_bs in elements; rows 8-byte aligned): the
 // ConvTranspose weight-grad on dsgan_instnorm_bwd_h's output.
-int dsgan_wconv_xh(const float* D, long d_bs, const void* Xh, long x_bs, float* dw, float* ws, int nb, int C, int M,
-                   int H, int W, int Ho, int Wo, int KH, int KW, int stride, int pad, hipStream_t st) {
-  return wconv_impl(D, d_bs, Xh, x_bs, true, dw, ws, nb, C, M, H, W, Ho, Wo, KH, KW, stride, pad, st);
+int dsgan_wconv_xh(const float* D, long d_bs, const void* Xh, long x_bs, float* dw, float* ws, long ws_elems, int nb,
+                   int C, int M, int H, int W, int Ho, int Wo, int KH, int KW, int stride, int pad, hipStream_t st) {
+  return wconv_impl(D, d_bs, Xh, x_bs, true, dw, nullptr, ws, ws_elems, nb, C, M, H, W, Ho, Wo, KH, KW, stride, pad, st);
 }
 
 }  // extern "C"

@@ -27,33 +27,36 @@ SIGNATURES = {
     "dsgan_adam_amp": [P, P, P, P, L, D, D, D, D, P, S],
     "dsgan_get_half_type": [],
     "dsgan_last_error_string": [],
+    # scratch contract: plan-only mode and the scratch the last planned launch needs (CPU planner tests)
+    "dsgan_set_plan_only": [I],
+    "dsgan_last_ws_need": [],
     # igemm.hip
     "dsgan_conv_fwd": [P, L, P, P, P, L, P, L] + [I] * 12 + [F, I, I, I, S],
     "dsgan_conv_dgrad": [P, L, P, P, P, L, P, L, P, L, I, I, I, I, I, I, I, I, I, I, I, I, I, F, I, I, S],
-    "dsgan_conv_wgrad": [P, L, P, L, P] + [I] * 13 + [P, S],
+    "dsgan_conv_wgrad": [P, L, P, L, P] + [I] * 13 + [P, L, S],
     "dsgan_conv_wgrad_workspace": [I] * 8,
     # pwgemm.hip
     "dsgan_pw_supported": [I, I, I, I, L, L, P, P],
-    "dsgan_pw_gemm": [I, P, L, P, L, P, L, P, P, L, P, L, I, I, I, I, I, I, I, I, I, F, P, S],
+    "dsgan_pw_gemm": [I, P, L, P, L, P, L, P, P, L, P, L, I, I, I, I, I, I, I, I, I, F, P, L, S],
     "dsgan_pw_wgrad_workspace": [I, I, I, I],
-    "dsgan_pw_wgrad_mixed": [P, L, I, P, L, I, P, P, I, I, I, I, P, S],
+    "dsgan_pw_wgrad_mixed": [P, L, I, P, L, I, P, P, I, I, I, I, P, L, S],
     "dsgan_pw_fwd_io": [P, I, P, L, I, P, L, I, P, L, I, P, I, I, I, I, I, I, F, S],
     "dsgan_pw_dgrad_io": [P, I, P, L, I, P, L, I, P, L, I, I, I, I, I, S],
-    "dsgan_pw_fwd_io_ws": [P, I, P, L, I, P, L, I, P, L, I, P, I, I, I, I, I, I, F, P, S],
-    "dsgan_pw_dgrad_io_ws": [P, I, P, L, I, P, L, I, P, L, I, I, I, I, I, P, S],
+    "dsgan_pw_fwd_io_ws": [P, I, P, L, I, P, L, I, P, L, I, P, I, I, I, I, I, I, F, P, L, S],
+    "dsgan_pw_dgrad_io_ws": [P, I, P, L, I, P, L, I, P, L, I, I, I, I, I, P, L, S],
     "dsgan_pw_fd_workspace": [I, I, I, I, I],
     "dsgan_wtrans_multi": [P, P, P, I, S],
     "dsgan_pw_tune": [I, I],
     # pwf32.hip
     "dsgan_pw_f32_supported": [I, I, I, I, L, L, P, P],
     "dsgan_pw_f32_wgrad_workspace": [I, I, I, I],
-    "dsgan_pw_gemm_f32": [I, P, L, P, L, P, L, P, P, L, I, I, I, I, I, I, I, I, F, P, S],
+    "dsgan_pw_gemm_f32": [I, P, L, P, L, P, L, P, P, L, I, I, I, I, I, I, I, I, F, P, L, S],
     # mlp.hip
     "dsgan_mlp_supported": [I, I, I],
     "dsgan_mlp_fwd": [P, L, I, P, P, P, P, P, L, I, I, I, I, I, S],
     "dsgan_mlp_bwd": [P, L, I, P, L, P, P, P, P, L, P, P, P, I, I, I, I, S],
     "dsgan_mlp_wgrad_workspace": [I, I, I, I],
-    "dsgan_mlp_wgrad": [P, L, I, P, L, P, P, P, P, P, P, P, I, I, I, I, S],
+    "dsgan_mlp_wgrad": [P, L, I, P, L, P, P, P, P, P, P, P, L, I, I, I, I, S],
     "dsgan_colsum": [P, I, I, P, S],
     "dsgan_f32_to_bf16": [P, P, L, S],
     # pconv.hip
@@ -61,7 +64,7 @@ SIGNATURES = {
     "dsgan_conv_wtrans_bf16": [P, P, I, I, I, I, I, S],
     "dsgan_pconv": [P, L, P, P, P, L, P, L] + [I] * 13 + [F, I, S],
     "dsgan_pconv_workspace": [I] * 5,
-    "dsgan_pconv_ws": [P, L, P, P, P, L, P, L] + [I] * 13 + [F, I, P, S],
+    "dsgan_pconv_ws": [P, L, P, P, P, L, P, L] + [I] * 13 + [F, I, P, L, S],
     # pwsmall.hip
     "dsgan_pw_small_supported": [I, I, I, L, L],
     "dsgan_pw_small": [P, L, P, I, I, P, P, L, P, L] + [I] * 8 + [F, S],
@@ -72,33 +75,34 @@ SIGNATURES = {
     # wconv.hip
     "dsgan_wconv_supported": [I, I, I, I],
     "dsgan_wconv_workspace": [I, I, I, I, I, I, I],
-    "dsgan_wconv": [P, L, P, L, P, P] + [I] * 11 + [S],
-    "dsgan_wconv_xh": [P, L, P, L, P, P] + [I] * 11 + [S],
+    "dsgan_wconv": [P, L, P, L, P, P, L] + [I] * 11 + [S],
+    "dsgan_wconv_db": [P, L, P, L, P, P, P, L] + [I] * 11 + [S],
+    "dsgan_wconv_xh": [P, L, P, L, P, P, L] + [I] * 11 + [S],
     # tconv.hip
     "dsgan_conv_wtrans": [P, P, I, I, I, I, I, I, I, I, I, S],
     "dsgan_tconv": [P, L, P, P, P, L, P, L] + [I] * 9 + [P, P] + [I] * 7 + [F, S],
     "dsgan_tconv_workspace": [I] * 6,
-    "dsgan_tconv_ws": [P, L, P, P, P, L, P, L] + [I] * 9 + [P, P] + [I] * 7 + [F, I, P, S],
-    "dsgan_tconv_ws_xh": [P, L, P, P, P, L, P, L] + [I] * 9 + [P, P] + [I] * 7 + [F, P, S],
+    "dsgan_tconv_ws": [P, L, P, P, P, L, P, L] + [I] * 9 + [P, P] + [I] * 7 + [F, I, P, L, S],
+    "dsgan_tconv_ws_xh": [P, L, P, P, P, L, P, L] + [I] * 9 + [P, P] + [I] * 7 + [F, P, L, S],
     # skinny.hip
     "dsgan_conv_small_out": [P, L, P, L, L, L, L, P, P, L] + [I] * 13 + [S],
     "dsgan_conv_small_in": [P, L, P, L, L, L, L, P, P, L] + [I] * 13 + [F, I, S],
     "dsgan_conv_wgrad_small_workspace": [I] * 7,
-    "dsgan_conv_wgrad_small": [P, L, P, L, P] + [I] * 11 + [P, S],
+    "dsgan_conv_wgrad_small": [P, L, P, L, P] + [I] * 11 + [P, L, S],
     # thin3.hip
     "dsgan_thin3_supported": [I, I, I, L, L],
     "dsgan_thin3_fwd": [P, L, P, P, P, L] + [I] * 6 + [S],
     "dsgan_thin3_wgrad_workspace": [I] * 5,
-    "dsgan_thin3_wgrad": [P, L, P, L, P, P] + [I] * 5 + [S],
+    "dsgan_thin3_wgrad": [P, L, P, L, P, P, L] + [I] * 5 + [S],
     "dsgan_thin3_dgrad": [P, L, P, P, L] + [I] * 6 + [S],
     # dwconv.hip
     "dsgan_dwconv_fwd": [P, L, P, P, P, L, I, I, I, I, I, I, I, S],
     "dsgan_dwconv_wgrad_workspace": [I, I, I, I, I, I],
-    "dsgan_dwconv_wgrad": [P, L, P, L, P, P, I, I, I, I, I, P, S],
+    "dsgan_dwconv_wgrad": [P, L, P, L, P, P, I, I, I, I, I, P, L, S],
     "dsgan_dwconv_multi_supported": [I, I, P, L, P, L],
     "dsgan_dwconv_multi_fwd": [P, L, P, P, P, P, P, P, P, P, P, L, I, I, I, I, I, I, S],
     "dsgan_dwconv_multi_wgrad_workspace": [I, I, I, I],
-    "dsgan_dwconv_multi_wgrad": [P, L, P, L, P, P, P, P, P, P, P, P, I, I, I, I, P, S],
+    "dsgan_dwconv_multi_wgrad": [P, L, P, L, P, P, P, P, P, P, P, P, I, I, I, I, P, L, S],
     # norm_pointwise.hip
     "dsgan_instnorm_fwd": [P, L, P, P, L, P, L, P, P, I, I, I, I, F, F, S],
     "dsgan_instnorm_fwd_bf16": [P, L, P, L, P, P, I, I, I, F, S],
@@ -109,14 +113,14 @@ SIGNATURES = {
     "dsgan_plane_stats": [P, L, P, P, P, I, I, I, S],
     "dsgan_plane_stats_bwd": [P, P, P, P, L, I, I, I, S],
     "dsgan_ca_fwd": [P, P, P, P, P, P, P, I, I, I, S],
-    "dsgan_ca_bwd": [P, P, P, P, P, P, P, P, P, P, P, P, P, I, I, I, P, S],
+    "dsgan_ca_bwd": [P, P, P, P, P, P, P, P, P, P, P, P, P, I, I, I, P, L, S],
     "dsgan_add_n": [P, P, I, P, L, I, L, S],
     "dsgan_copy_strided": [P, L, P, L, I, L, S],
     "dsgan_copy_multi": [P, P, I, L, S],
     "dsgan_fill": [P, F, L, S],
     "dsgan_scale": [P, F, L, S],
     "dsgan_act_bwd": [P, P, P, L, I, F, I, S],
-    "dsgan_channel_sum": [P, L, P, I, I, I, P, S],
+    "dsgan_channel_sum": [P, L, P, I, I, I, P, L, S],
     # losses.hip
     "dsgan_loss_parts": [],
     "dsgan_loss_combine": [P, P, P, P, I, F, P, S],
@@ -133,10 +137,10 @@ SIGNATURES = {
     "dsgan_ms_ssim_workspace": [I, I, I, I],
     "dsgan_u8_to_image": [P, P, P, I, I, I, I, S],
     "dsgan_img_metrics": [P, P, I, I, I, P, P, S],
-    "dsgan_ms_ssim": [P, P, F, F, I, I, I, I, P, F, F, P, I, P, P, P, S],
+    "dsgan_ms_ssim": [P, P, F, F, I, I, I, I, P, F, F, P, I, P, L, P, P, S],
     "dsgan_ms_ssim_train_workspace": [I, I, I, I, I],
-    "dsgan_ms_ssim_fwd_train": [P, P, F, F, I, I, I, I, P, F, F, P, I, P, P, P, S],
-    "dsgan_ms_ssim_bwd": [P, P, F, F, I, I, I, I, P, F, F, P, I, P, P, P, P, I, S],
+    "dsgan_ms_ssim_fwd_train": [P, P, F, F, I, I, I, I, P, F, F, P, I, P, L, P, P, S],
+    "dsgan_ms_ssim_bwd": [P, P, F, F, I, I, I, I, P, F, F, P, I, P, L, P, P, P, I, S],
     "dsgan_ssim_bwd": [P, P, F, F, I, I, I, P, P, P, F, P, I, S],
     # vggconv.hip
     "dsgan_vconv_supported": [I, I, I, I],
@@ -168,7 +172,7 @@ def load():
         fn = getattr(lib, name)
         fn.argtypes = argtypes
         fn.restype = (ctypes.c_char_p if name == "dsgan_last_error_string"
-                      else ctypes.c_long if name.endswith(("_workspace", "_parts", "_size")) else ctypes.c_int)
+                      else ctypes.c_long if name.endswith(("_workspace", "_parts", "_size", "_need")) else ctypes.c_int)
     _lib = lib
     return lib
 

@@ -17,6 +17,10 @@ divided by it again.  Unlike GradScaler nothing here syncs with the host:
     GradScaler skips optimizer.step()).
 One scaler per network (D and G have their own backward and optimizer).  Defaults are
 GradScaler's (init 2^16, growth 2, backoff 0.5, interval 2000).
+
+``LossScaler.guard(device)`` is the unit-scale form (scale 1, never grown or backed off): the bf16
+mode's non-finite guard (``--nonfinite_guard``).  ``scale`` is then the identity, the check and the
+skip are the same kernels, and Adam multiplies the gradient by exactly 1.0.
 """
 import torch
 
@@ -31,9 +35,21 @@ class LossScaler:
         self.part = torch.empty(int(_lib.load().dsgan_amp_parts()), device=device, dtype=torch.int32)
         self.growth, self.backoff, self.interval = float(growth_factor), float(backoff_factor), int(growth_interval)
 
+    @classmethod
+    def guard(cls, device):
+        s = cls(device, init_scale=1.0, growth_factor=1.0, backoff_factor=1.0, growth_interval=1 << 30)
+        s.unit = True
+        return s
+
+    unit = False
+
     def scale(self, loss):
         """loss * scale (a power of two: exact); the scale is a device scalar, no host sync."""
-        return loss * self.state[0]
+        return loss if self.unit else loss * self.state[0]
+
+    def skipped_steps(self, calls):
+        """optimizer steps skipped so far out of `calls` (synchronises)"""
+        return calls - self.applied_steps()
 
     def check(self, flat_grad):
         call("dsgan_amp_check", ptr(flat_grad), flat_grad.numel(), ptr(self.part), ptr(self.state), self.backoff,

@@ -19,6 +19,17 @@ import torch
 from . import _lib
 from ._lib import call, ptr, stream
 
+
+def wsa(t):
+    """(pointer, element count) of a scratch tensor (None -> NULL, 0): every scratch-taking entry
+    point takes the buffer's size right after it and refuses an undersized one (include/dsgan_hip.h)."""
+    return (ptr(t), t.numel() if t is not None else 0)
+
+
+# PatchGAN 4x4 weight-grads also sum the conv's bias grad from their staged dy tiles
+# (dsgan_wconv_db) instead of a separate channel-sum pass; see DESIGN.md section 6.
+WCONV_DB_FOLD = False
+
 ACT = {None: 0, "none": 0, "gelu": 1, "relu": 2, "lrelu": 3, "sigmoid": 4}
 PREC = {"fp32": 0, "bf16": 1, "fp16": 1}   # the C ABI's prec: 0 exact f32, 1 16-bit MFMA operands
 _state = {"prec": "fp32"}
@@ -191,7 +202,7 @@ def _tconv(X, xbs, Wt, bias, Y, ybs, gpre, gbs, nb, K, M, Hin, Win, Hout, Wout, 
     call("dsgan_tconv_ws", ptr(X), xbs, ptr(Wt), ptr(bias), ptr(Y), ybs, ptr(gpre), gbs, nb, K, M, Hin,
          Win, Hout, Wout, stride, len(taps), ctypes.cast(dh, ctypes.c_void_p),
          ctypes.cast(dw, ctypes.c_void_p), Hdst, Wdst, os_, ph, pw, ACT[act], ACT[gact],
-         LRELU_SLOPE, int(Wt.dtype != torch.float32), ptr(ws), stream())
+         LRELU_SLOPE, int(Wt.dtype != torch.float32), *wsa(ws), stream())
 
 
 # Transformed-weight cache: an entry is valid while the parameter's storage pointer and the
@@ -334,7 +345,7 @@ def _pconv(x, xbs, wb, b, y, ybs, N, K, M, H, W, Ho, Wo, KH, KW, stride, pad, ac
     nws = _lib.load().dsgan_pconv_workspace(N, K, M, Ho, Wo)
     ws = torch.empty(nws, device=x.device, dtype=torch.float32) if nws > 0 else None
     call("dsgan_pconv_ws", ptr(x), xbs, ptr(wb), ptr(b), ptr(y), ybs, ptr(gpre), gbs, N, K, M, H, W, Ho, Wo, KH, KW,
-         stride, pad, ACT[act], ACT[gact], LRELU_SLOPE, int(accumulate), ptr(ws), stream())
+         stride, pad, ACT[act], ACT[gact], LRELU_SLOPE, int(accumulate), *wsa(ws), stream())
 
 
 def conv_fwd_raw(x, w, b, stride, pad, act=None, out=None, pre=None, accumulate=False, xact=None):
@@ -380,16 +391,16 @@ def conv_fwd_raw(x, w, b, stride, pad, act=None, out=None, pre=None, accumulate=
             # workgroup (the same RNE rounding: the same bits)
             call("dsgan_pw_fwd_io_ws", ptr(bf16_weight(w)), 1, ptr(x), xbs, 0, ptr(y), ybs, 0, ptr(pre), pbs, 0,
                  ptr(b), Cout, Cin, H * W, N, ACT[act], int(accumulate), LRELU_SLOPE,
-                 ptr(_pw_fd_ws(0, Cout, Cin, H * W, N, x)), stream())
+                 *wsa(_pw_fd_ws(0, Cout, Cin, H * W, N, x)), stream())
         else:
             call("dsgan_pw_gemm", 0, ptr(w), 0, ptr(x), xbs, ptr(y), ybs, ptr(b), ptr(pre), pbs, None, 0,
                  Cout, N * H * W, Cin, H * W, N, ACT[act], 0, ACT[xact], int(accumulate), LRELU_SLOPE,
-                 ptr(_pw_fd_ws(0, Cout, Cin, H * W, N, x)), stream())
+                 *wsa(_pw_fd_ws(0, Cout, Cin, H * W, N, x)), stream())
     elif (KH == 1 and KW == 1 and stride == 1 and pad == 0 and pre is None and xact is None
           and _pwf_ok(0, Cout, Cin, H * W, 0, xbs, w.data_ptr(), x.data_ptr())):
         fam = "pwf32_kernel"
         call("dsgan_pw_gemm_f32", 0, ptr(w), 0, ptr(x), xbs, ptr(y), ybs, ptr(b), None, 0, Cout, N * H * W, Cin,
-             H * W, N, ACT[act], 0, int(accumulate), LRELU_SLOPE, None, stream())
+             H * W, N, ACT[act], 0, int(accumulate), LRELU_SLOPE, None, 0, stream())
     elif w.dim() == 4 and pre is None and xact is None and _pconv_ok(Cin, KH, KW, stride):
         fam = "pconv_kernel"
         _pconv(x, xbs, _wtrans_bf16(w, 0), b, y, ybs, N, Cin, Cout, H, W, Ho, Wo, KH, KW, stride, pad, act,
@@ -448,16 +459,16 @@ def conv_dgrad_raw(dy, w, x_shape, stride, pad, bias=None, act=None, gpre=None, 
         fam = "pwgemm_kernel"
         if gpre is None and Cin % 8 == 0 and _pw_io_ok(Cout, H * W, dybs, dxbs, dy, dx):
             call("dsgan_pw_dgrad_io_ws", ptr(bf16_weight(w)), 1, ptr(dy), dybs, 0, ptr(dx), dxbs, 0, None, 0, Cin,
-                 Cout, H * W, N, int(accumulate), ptr(_pw_fd_ws(1, Cin, Cout, H * W, N, dy)), stream())
+                 Cout, H * W, N, int(accumulate), *wsa(_pw_fd_ws(1, Cin, Cout, H * W, N, dy)), stream())
         else:
             call("dsgan_pw_gemm", 1, ptr(w), 0, ptr(dy), dybs, ptr(dx), dxbs, None, None, 0, ptr(gpre), gbs,
                  Cin, N * H * W, Cout, H * W, N, 0, ACT[gact], 0, int(accumulate), LRELU_SLOPE,
-                 ptr(_pw_fd_ws(1, Cin, Cout, H * W, N, dy)), stream())
+                 *wsa(_pw_fd_ws(1, Cin, Cout, H * W, N, dy)), stream())
     elif (KH == 1 and KW == 1 and stride == 1 and pad == 0 and bias is None and act is None
             and _pwf_ok(1, Cin, Cout, H * W, 0, dybs, w.data_ptr(), dy.data_ptr())):
         fam = "pwf32_kernel"
         call("dsgan_pw_gemm_f32", 1, ptr(w), 0, ptr(dy), dybs, ptr(dx), dxbs, None, ptr(gpre), gbs, Cin, N * H * W,
-             Cout, H * W, N, 0, ACT[gact], int(accumulate), LRELU_SLOPE, None, stream())
+             Cout, H * W, N, 0, ACT[gact], int(accumulate), LRELU_SLOPE, None, 0, stream())
     elif (w.dim() == 4 and stride == 1 and act is None and bias is None and KH == KW
           and _pconv_ok(Cout, KH, KW, 1)):
         # stride-1 data-grad = forward conv of dy with the flipped, transposed kernel
@@ -519,18 +530,18 @@ def conv_wgrad_raw(dy, x, dw, stride, pad, xact=None, db=None):
         fam = "thin3_kernel"
         ws = torch.empty(_lib.load().dsgan_thin3_wgrad_workspace(N, Cin, Cout, H, W), device=dy.device,
                          dtype=torch.float32)
-        call("dsgan_thin3_wgrad", ptr(dy), dybs, ptr(x), xbs, ptr(dw), ptr(ws), N, Cin, Cout, H, W, stream())
+        call("dsgan_thin3_wgrad", ptr(dy), dybs, ptr(x), xbs, ptr(dw), *wsa(ws), N, Cin, Cout, H, W, stream())
     elif xact is None and KH * KW in (1, 9, 16) and (Cout <= 8 or (Cin <= 8 and KH * KW == 1)):
         fam = "wgrad_small_kernel"
         nws = _lib.load().dsgan_conv_wgrad_small_workspace(N, Cin, Cout, KH, KW, dy.shape[2], dy.shape[3])
         ws = torch.empty(nws, device=dy.device, dtype=torch.float32) if nws > 0 else None
         call("dsgan_conv_wgrad_small", ptr(dy), dybs, ptr(x), xbs, ptr(dw), N, Cin, H, W, Cout, KH, KW,
-             stride, pad, dy.shape[2], dy.shape[3], ptr(ws), stream())
+             stride, pad, dy.shape[2], dy.shape[3], *wsa(ws), stream())
     elif KH == 1 and KW == 1 and stride == 1 and pad == 0 and _pw_ok(2, Cout, N * H * W, H * W, dybs, xbs, dy.data_ptr(), x.data_ptr()):
         fam = "pwgemm_kernel"
         did_db = db is not None
         call("dsgan_pw_gemm", 2, ptr(dy), dybs, ptr(x), xbs, ptr(dw), 0, ptr(db), None, 0, None, 0,
-             Cout, Cin, N * H * W, H * W, N, 0, 0, ACT[xact], 0, LRELU_SLOPE, ptr(_pw_ws(Cout, Cin, H * W, N, dy)),
+             Cout, Cin, N * H * W, H * W, N, 0, 0, ACT[xact], 0, LRELU_SLOPE, *wsa(_pw_ws(Cout, Cin, H * W, N, dy)),
              stream())
     elif (KH == 1 and KW == 1 and stride == 1 and pad == 0 and xact is None
           and _pwf_ok(2, Cout, N * H * W, H * W, dybs, xbs, dy.data_ptr(), x.data_ptr())):
@@ -539,20 +550,25 @@ def conv_wgrad_raw(dy, x, dw, stride, pad, xact=None, db=None):
         ws = torch.empty(nws, device=dy.device, dtype=torch.float32) if nws > 0 else None
         did_db = db is not None
         call("dsgan_pw_gemm_f32", 2, ptr(dy), dybs, ptr(x), xbs, ptr(dw), 0, ptr(db), None, 0, Cout, Cin, N * H * W,
-             H * W, N, 0, 0, 0, LRELU_SLOPE, ptr(ws), stream())
+             H * W, N, 0, 0, 0, LRELU_SLOPE, *wsa(ws), stream())
     elif (xact is None and _is16() and dw.is_contiguous() and pad == 1 and W % 4 == 0
           and xbs % 4 == 0 and x.data_ptr() % 16 == 0 and _lib.load().dsgan_wconv_supported(Cin, KH, KW, stride)):
         fam = "wconv_kernel"
         Ho, Wo = dy.shape[2], dy.shape[3]
         ws = torch.empty(_lib.load().dsgan_wconv_workspace(N, Cin, Cout, Ho, Wo, KH, KW), device=dy.device,
                          dtype=torch.float32)
-        call("dsgan_wconv", ptr(dy), dybs, ptr(x), xbs, ptr(dw), ptr(ws), N, Cin, Cout, H, W, Ho, Wo, KH, KW,
-             stride, pad, stream())
+        if db is not None and WCONV_DB_FOLD:   # the bias grad from the staged dy tiles (no channel-sum pass)
+            did_db = True
+            call("dsgan_wconv_db", ptr(dy), dybs, ptr(x), xbs, ptr(dw), ptr(db), *wsa(ws), N, Cin, Cout, H, W, Ho, Wo,
+                 KH, KW, stride, pad, stream())
+        else:
+            call("dsgan_wconv", ptr(dy), dybs, ptr(x), xbs, ptr(dw), *wsa(ws), N, Cin, Cout, H, W, Ho, Wo, KH, KW,
+                 stride, pad, stream())
     else:
         nws = _lib.load().dsgan_conv_wgrad_workspace(N, Cin, Cout, KH, KW, dy.shape[2], dy.shape[3], _prec())
         ws = torch.empty(nws, device=dy.device, dtype=torch.float32) if nws > 0 else None
         call("dsgan_conv_wgrad", ptr(dy), dybs, ptr(x), xbs, ptr(dw), N, Cin, H, W, Cout, KH, KW,
-             stride, pad, dy.shape[2], dy.shape[3], ACT[xact], _prec(), ptr(ws), stream())
+             stride, pad, dy.shape[2], dy.shape[3], ACT[xact], _prec(), *wsa(ws), stream())
     IGEMM_TIMER.end(e0, _conv_flops(N, Cin, Cout, KH, KW, dy.shape[2], dy.shape[3]),
                     ("wgrad", N, Cin, H, W, Cout, KH, stride), fam, _nb(dy, x, dw))
     return did_db
@@ -562,7 +578,7 @@ def channel_sum_raw(dy, out):
     dy, dybs = nchw(dy)
     N, C, H, W = dy.shape
     ws = torch.empty(N * C, device=dy.device, dtype=torch.float32)
-    call("dsgan_channel_sum", ptr(dy), dybs, ptr(out), N, C, H * W, ptr(ws), stream())
+    call("dsgan_channel_sum", ptr(dy), dybs, ptr(out), N, C, H * W, *wsa(ws), stream())
 
 
 def act_bwd_raw(dy, pre, act, out=None):
@@ -893,13 +909,13 @@ class PwMlpFn(torch.autograd.Function):
             g = torch.empty((N, C4, H, W), device=h.device, dtype=half_dtype())    # gelu(z)
             e0 = IGEMM_TIMER.begin()
             call("dsgan_pw_fwd_io_ws", ptr(bf16_weight(w1)), 1, ptr(h), hbs, hb, ptr(g), C4 * HW, 1, ptr(gp), C4 * HW, 1,
-                 ptr(b1), C4, C, HW, N, ACT["gelu"], 0, LRELU_SLOPE, ptr(_pw_fd_ws(0, C4, C, HW, N, h)), stream())
+                 ptr(b1), C4, C, HW, N, ACT["gelu"], 0, LRELU_SLOPE, *wsa(_pw_fd_ws(0, C4, C, HW, N, h)), stream())
             IGEMM_TIMER.end(e0, 2.0 * N * HW * C4 * C, ("fwd", N, C, H, W, C4, 1, 1), "pwgemm_kernel",
                             _nb(h, w1, b1, g, gp))
             out = conv_fwd_raw(x, ws, None, 1, 0)
             e0 = IGEMM_TIMER.begin()
             call("dsgan_pw_fwd_io_ws", ptr(bf16_weight(w2)), 1, ptr(g), C4 * HW, 1, ptr(out), P * HW, 0, None, 0, 0, ptr(b2),
-                 P, C4, HW, N, 0, 1, LRELU_SLOPE, ptr(_pw_fd_ws(0, P, C4, HW, N, g)), stream())
+                 P, C4, HW, N, 0, 1, LRELU_SLOPE, *wsa(_pw_fd_ws(0, P, C4, HW, N, g)), stream())
             IGEMM_TIMER.end(e0, 2.0 * N * HW * C4 * P, ("fwd", N, C4, H, W, P, 1, 1), "pwgemm_kernel",
                             _nb(g, w2, b2) + 2 * _nb(out))
             ctx.g = g
@@ -954,7 +970,7 @@ class PwMlpFn(torch.autograd.Function):
             dz = torch.empty((N, C4, H, W), device=dy.device, dtype=half_dtype())
             e0 = IGEMM_TIMER.begin()
             call("dsgan_pw_dgrad_io_ws", ptr(bf16_weight(w2)), 1, ptr(dy), dybs, 0, ptr(dz), C4 * HW, 1, ptr(z), C4 * HW,
-                 C4, P, HW, N, 0, ptr(_pw_fd_ws(1, C4, P, HW, N, dy)), stream())
+                 C4, P, HW, N, 0, *wsa(_pw_fd_ws(1, C4, P, HW, N, dy)), stream())
             IGEMM_TIMER.end(e0, 2.0 * N * HW * C4 * P, ("dgrad", N, C4, H, W, P, 1, 1), "pwgemm_kernel",
                             _nb(dy, w2, dz, z))
             # bias grads ride on the weight-grads' staged A tiles (db += sum_k A): b2 from dy, b1 from
@@ -962,7 +978,7 @@ class PwMlpFn(torch.autograd.Function):
             if gw2 is not None:
                 e0 = IGEMM_TIMER.begin()
                 call("dsgan_pw_wgrad_mixed", ptr(dy), dybs, 0, ptr(ctx.g), C4 * HW, 1, ptr(gw2), ptr(gb2), P, C4,
-                     HW, N, ptr(_pw_ws(P, C4, HW, N, dy)), stream())
+                     HW, N, *wsa(_pw_ws(P, C4, HW, N, dy)), stream())
                 IGEMM_TIMER.end(e0, 2.0 * N * HW * C4 * P, ("wgrad", N, C4, H, W, P, 1, 1), "pwgemm_kernel",
                                 _nb(dy, ctx.g, gw2))
             elif gb2 is not None:
@@ -972,7 +988,7 @@ class PwMlpFn(torch.autograd.Function):
             if gw1 is not None:
                 e0 = IGEMM_TIMER.begin()
                 call("dsgan_pw_wgrad_mixed", ptr(dz), C4 * HW, 1, ptr(h), C * HW, ctx.hb, ptr(gw1), ptr(gb1), C4, C,
-                     HW, N, ptr(_pw_ws(C4, C, HW, N, dz)), stream())
+                     HW, N, *wsa(_pw_ws(C4, C, HW, N, dz)), stream())
                 IGEMM_TIMER.end(e0, 2.0 * N * HW * C4 * C, ("wgrad", N, C, H, W, C4, 1, 1), "pwgemm_kernel",
                                 _nb(dz, h, gw1))
             elif gb1 is not None:   # frozen pwconv1 weight, trainable bias (not on the train path)
@@ -982,7 +998,7 @@ class PwMlpFn(torch.autograd.Function):
                 dh = _empty(N, C, H, W, dy)
                 e0 = IGEMM_TIMER.begin()
                 call("dsgan_pw_dgrad_io_ws", ptr(bf16_weight(w1)), 1, ptr(dz), C4 * HW, 1, ptr(dh), C * HW, 0, None, 0, C, C4,
-                     HW, N, 0, ptr(_pw_fd_ws(1, C, C4, HW, N, dz)), stream())
+                     HW, N, 0, *wsa(_pw_fd_ws(1, C, C4, HW, N, dz)), stream())
                 IGEMM_TIMER.end(e0, 2.0 * N * HW * C4 * C, ("dgrad", N, C4, H, W, C, 1, 1), "pwgemm_kernel",
                                 _nb(dz, w1, dh))
             _params_done(*ctx.refs)
@@ -1037,7 +1053,7 @@ class PwMlpFn(torch.autograd.Function):
             wsp = torch.empty(_lib.load().dsgan_mlp_wgrad_workspace(C, P, HW, N), device=h.device, dtype=torch.float32)
             e0 = IGEMM_TIMER.begin()
             call("dsgan_mlp_wgrad", ptr(h), C * HW, ctx.hb, ptr(dy), dybs, ptr(w1b), ptr(b1), ptr(w2b), ptr(gw1),
-                 ptr(gb1), ptr(gw2), ptr(wsp), N, C, P, HW, stream())
+                 ptr(gb1), ptr(gw2), *wsa(wsp), N, C, P, HW, stream())
             IGEMM_TIMER.end(e0, 2.0 * N * HW * C4 * (2 * C + 2 * P), ("mlp_wgrad", N, C, H, W, P, 1, 1),
                             "mlp_wgrad_kernel", _nb(h, dy, w1, b1, w2, gw1, gb1, gw2))
             if gb2 is not None:
@@ -1057,7 +1073,7 @@ class PwMlpFn(torch.autograd.Function):
         if gw2 is not None:
             e0 = IGEMM_TIMER.begin()
             call("dsgan_pw_wgrad_mixed", ptr(dy), dybs, 0, ptr(g), C4 * HW, 1, ptr(gw2), ptr(gb2), P, C4, HW, N,
-                 ptr(_pw_ws(P, C4, HW, N, dy)), stream())
+                 *wsa(_pw_ws(P, C4, HW, N, dy)), stream())
             IGEMM_TIMER.end(e0, 2.0 * N * HW * C4 * P, ("wgrad", N, C4, H, W, P, 1, 1), "pwgemm_kernel",
                             _nb(dy, g, gw2))
         elif gb2 is not None:
@@ -1067,7 +1083,7 @@ class PwMlpFn(torch.autograd.Function):
         if gw1 is not None:
             e0 = IGEMM_TIMER.begin()
             call("dsgan_pw_wgrad_mixed", ptr(dz), C4 * HW, 1, ptr(h), C * HW, ctx.hb, ptr(gw1), ptr(gb1), C4, C, HW,
-                 N, ptr(_pw_ws(C4, C, HW, N, dz)), stream())
+                 N, *wsa(_pw_ws(C4, C, HW, N, dz)), stream())
             IGEMM_TIMER.end(e0, 2.0 * N * HW * C4 * C, ("wgrad", N, C, H, W, C4, 1, 1), "pwgemm_kernel",
                             _nb(dz, h, gw1))
         elif gb1 is not None:
@@ -1107,7 +1123,7 @@ def _dw_wgrad(dy, x, gw, gb, K):
     al = int(x4.data_ptr() % 16 == 0 and dy4.data_ptr() % 16 == 0 and xbs % 4 == 0 and dybs % 4 == 0)
     ws = torch.empty(_lib.load().dsgan_dwconv_wgrad_workspace(N, C, H, W, K, al), device=x4.device, dtype=torch.float32)
     e0 = AUX_TIMER.begin()
-    call("dsgan_dwconv_wgrad", ptr(dy4), dybs, ptr(x4), xbs, ptr(gw), ptr(gb), N, C, H, W, K, ptr(ws), stream())
+    call("dsgan_dwconv_wgrad", ptr(dy4), dybs, ptr(x4), xbs, ptr(gw), ptr(gb), N, C, H, W, K, *wsa(ws), stream())
     AUX_TIMER.end(e0, 2.0 * N * C * H * W * K * K, ("dw_wgrad", N, C, H, W, K), "dwconv", 2 * _nb(x4))
 
 
@@ -1195,7 +1211,7 @@ class MultiDwConvFn(torch.autograd.Function):
                                   dtype=torch.float32)
                 e0 = AUX_TIMER.begin()
                 call("dsgan_dwconv_multi_wgrad", ptr(dy4), dybs, ptr(x), xbs, *[ptr(g_) for g_ in grads], N, q, H, W,
-                     ptr(wsp), stream())
+                     *wsa(wsp), stream())
                 AUX_TIMER.end(e0, 2.0 * N * q * H * W * 164, ("dw_multi_wgrad", N, C, H, W, 0), "dwconv", 2 * _nb(x))
                 grads = [None] * 8
         else:
@@ -1376,7 +1392,7 @@ class ConvTNormFn(torch.autograd.Function):
             e0 = IGEMM_TIMER.begin()
             call("dsgan_tconv_ws_xh", ptr(dth), Co * HW, ptr(_wtrans_bf16(w, 0)), None, ptr(dx), Ci * Hi * Wi, None,
                  0, N, Co, Ci, H, W, Hi, Wi, 2, 9, ctypes.cast(dh, ctypes.c_void_p), ctypes.cast(dw, ctypes.c_void_p),
-                 Hi, Wi, 1, 0, 0, 0, 0, LRELU_SLOPE, ptr(ws), stream())
+                 Hi, Wi, 1, 0, 0, 0, 0, LRELU_SLOPE, *wsa(ws), stream())
             IGEMM_TIMER.end(e0, _conv_flops(N, Co, Ci, 3, 3, Hi, Wi), ("fwd", N, Co, H, W, Ci, 3, 2), "tconv_kernel",
                             _nb(dth, dx) + 2.0 * w.numel())
         gw = _grad_buf(ctx.w_ref) if ctx.needs_input_grad[1] else None
@@ -1385,7 +1401,7 @@ class ConvTNormFn(torch.autograd.Function):
             ws = torch.empty(_lib.load().dsgan_wconv_workspace(N, Co, Ci, Hi, Wi, 3, 3), device=t.device,
                              dtype=torch.float32)
             e0 = IGEMM_TIMER.begin()
-            call("dsgan_wconv_xh", ptr(x4), xbs, ptr(dth), Co * HW, ptr(gw), ptr(ws), N, Co, Ci, H, W, Hi, Wi, 3, 3,
+            call("dsgan_wconv_xh", ptr(x4), xbs, ptr(dth), Co * HW, ptr(gw), *wsa(ws), N, Co, Ci, H, W, Hi, Wi, 3, 3,
                  2, 1, stream())
             IGEMM_TIMER.end(e0, _conv_flops(N, Co, Ci, 3, 3, Hi, Wi), ("wgrad", N, Co, H, W, Ci, 3, 2), "wconv_kernel",
                             _nb(x4, dth, gw))
@@ -1698,7 +1714,7 @@ class MidTailFn(torch.autograd.Function):
         w1r, par, w2r = ctx.refs
         call("dsgan_ca_bwd", ptr(datt), ptr(att), ptr(avg), ptr(mx), ptr(hsave), ptr(w1), ptr(w2), ptr(pa),
              ptr(davg), ptr(dmx), ptr(_grad_buf(w1r)), ptr(_grad_buf(w2r)), ptr(_grad_buf(par)), N, C, R,
-             ptr(torch.empty(N * (2 * R * C + 1), device=v.device, dtype=torch.float32)), stream())
+             *wsa(torch.empty(N * (2 * R * C + 1), device=v.device, dtype=torch.float32)), stream())
         call("dsgan_plane_stats_bwd", ptr(davg), ptr(dmx), ptr(amax), ptr(dv), C * H * W, N, C, H * W, stream())
         _params_done(*ctx.refs)
         return _give(ctx.box_v, dv), _give(ctx.box_x, dx), None, None, None
@@ -1983,7 +1999,7 @@ def ms_ssim_affine(real, fake, a=1.0, b=0.0, data_range=1.0, weights=MS_SSIM_WEI
     C1 = (0.01 * data_range) ** 2
     C2 = (0.03 * data_range) ** 2
     call("dsgan_ms_ssim", ptr(real), ptr(fake), float(a), float(b), N, C, H, W, ptr(gauss_win(real.device)),
-         float(C1), float(C2), ctypes.cast(wh, ctypes.c_void_p), len(weights), ptr(work), ptr(stats), ptr(out),
+         float(C1), float(C2), ctypes.cast(wh, ctypes.c_void_p), len(weights), *wsa(work), ptr(stats), ptr(out),
          stream())
     return out[N] if size_average else out[:N]
 
@@ -2007,7 +2023,7 @@ class MSSSIMFn(torch.autograd.Function):
         wh = (ctypes.c_float * L)(*[float(w) for w in weights])
         C1, C2 = (0.01 * data_range) ** 2, (0.03 * data_range) ** 2
         call("dsgan_ms_ssim_fwd_train", ptr(real), ptr(fake), float(a), float(b), N, C, H, W,
-             ptr(gauss_win(real.device)), float(C1), float(C2), ctypes.cast(wh, ctypes.c_void_p), L, ptr(work),
+             ptr(gauss_win(real.device)), float(C1), float(C2), ctypes.cast(wh, ctypes.c_void_p), L, *wsa(work),
              ptr(stats), ptr(out), stream())
         ctx.save_for_backward(real, fake, work, stats)
         ctx.args = (float(a), float(b), float(C1), float(C2), tuple(float(w) for w in weights))
@@ -2022,7 +2038,7 @@ class MSSSIMFn(torch.autograd.Function):
         wh = (ctypes.c_float * len(weights))(*weights)
         dfake = torch.empty_like(fake)
         call("dsgan_ms_ssim_bwd", ptr(real), ptr(fake), a, b, N, C, H, W, ptr(gauss_win(real.device)), C1, C2,
-             ctypes.cast(wh, ctypes.c_void_p), len(weights), ptr(work), ptr(stats), ptr(g.contiguous()), ptr(dfake),
+             ctypes.cast(wh, ctypes.c_void_p), len(weights), *wsa(work), ptr(stats), ptr(g.contiguous()), ptr(dfake),
              0, stream())
         return None, dfake, None, None, None, None
 

@@ -21,7 +21,10 @@ Deliberate, documented deviations:
   * the unused VGG relu5_3 block is not computed (the loss never reads it, :182-186);
   * --precision fp16 (BASELINE configs[4]): both backward passes run on a dynamically scaled loss
     (dsgan_hip.amp.LossScaler, GradScaler semantics on the device), the optimizers unscale, and
-    an overflowed step is skipped; the logged losses are the unscaled ones.
+    an overflowed step is skipped; the logged losses are the unscaled ones;
+  * --nonfinite_guard (on by default in bf16): the same device-side check with a unit scale -- an
+    optimizer step whose flat gradient holds inf/nan is skipped (the reference would write NaN
+    into its weights and never recover); with finite gradients nothing changes.
 """
 import random
 
@@ -99,8 +102,14 @@ class Pix2PixModel(BaseModel):
             hdist.broadcast_params(self.flatD)
             self.optimizers = []
             fp16 = HF.get_precision() == "fp16"
-            self.scaler_G = LossScaler(self.device) if fp16 else None
-            self.scaler_D = LossScaler(self.device) if fp16 else None
+            guard = int(getattr(opt, "nonfinite_guard", -1))
+            guard = HF.get_precision() == "bf16" if guard < 0 else bool(guard)
+            if fp16:
+                self.scaler_G, self.scaler_D = LossScaler(self.device), LossScaler(self.device)
+            elif guard:   # unit-scale scalers: the inf/nan check + skip only
+                self.scaler_G, self.scaler_D = LossScaler.guard(self.device), LossScaler.guard(self.device)
+            else:
+                self.scaler_G = self.scaler_D = None
             self.optimizer_G = FlatAdam(self.flatG, lr=opt.lr, betas=(opt.beta1, 0.999), scaler=self.scaler_G)
             self.optimizer_D = FlatAdam(self.flatD, lr=opt.lr, betas=(opt.beta1, 0.999), scaler=self.scaler_D)
             self.optimizers.append(self.optimizer_G)

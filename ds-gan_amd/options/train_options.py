@@ -29,6 +29,12 @@ class TrainOptions(BaseOptions):
         # gaussian-pyramid MS-SSIM of DSGAN/MS_SSIM.py:153-225, which needs images > 160 px)
         parser.add_argument("--ssim_loss", type=str, default="ssim", choices=["ssim", "ms_ssim"],
                             help="structural loss term: ssim (reference) or ms_ssim (opt-in)")
+        # build extension: a device-side inf/nan scan of each network's flat gradient before its Adam
+        # step; a non-finite gradient skips that optimizer step (parameters and moments untouched)
+        # instead of writing NaN into the weights.  -1 = on for --precision bf16 (fp16 always has it
+        # through its loss scaler), off for the fp32 parity mode.
+        parser.add_argument("--nonfinite_guard", type=int, default=-1, choices=[-1, 0, 1],
+                            help="skip an optimizer step whose gradient has inf/nan (-1: on for bf16)")
         self.isTrain = True
         return parser
 

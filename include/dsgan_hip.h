@@ -34,8 +34,19 @@
 extern "C" {
 #endif
 
-int dsgan_abi_version(void);   /* 2: adds the half type and the fp16 mode */
+int dsgan_abi_version(void);   /* 3: every scratch-taking entry point takes the scratch size */
 const char* dsgan_last_error_string(void);
+/* Scratch contract.  Every entry point that takes a scratch buffer (ws / work) takes its size
+ * right after it (`ws_elems`, fp32 elements).  The launcher plans the launch it is about to issue,
+ * computes the scratch that plan writes and returns -1 (message in dsgan_last_error_string) if
+ * the buffer is NULL or smaller -- an undersized buffer is an error code, never an out-of-bounds
+ * write.  Size a buffer with the matching *_workspace query.
+ * dsgan_set_plan_only(1) (thread-local, returns the previous setting): scratch-taking entry points
+ * validate, plan and check, then return 0 before any HIP call -- the planners run without a GPU
+ * (tests/test_planner_cpu.py).  dsgan_last_ws_need(): the scratch the last planned launch of this
+ * thread needed (elements; 0 = none). */
+int dsgan_set_plan_only(int on);
+long dsgan_last_ws_need(void);
 /* the 16-bit operand type (see Conventions): 0 bf16, 1 fp16; -1 for anything else */
 int dsgan_set_half_type(int t);
 int dsgan_get_half_type(void);
@@ -68,7 +79,7 @@ int dsgan_conv_dgrad(const float* dy, long dy_bs, const float* w, const float* b
 long dsgan_conv_wgrad_workspace(int N, int Cin, int Cout, int KH, int KW, int Ho, int Wo, int prec);
 int dsgan_conv_wgrad(const float* dy, long dy_bs, const float* x, long x_bs, float* dw, int N,
                      int Cin, int H, int W, int Cout, int KH, int KW, int stride, int pad, int Ho,
-                     int Wo, int xact, int prec, float* ws, hipStream_t stream);
+                     int Wo, int xact, int prec, float* ws, long ws_elems, hipStream_t stream);
 
 /* ---- pointwise (1x1 / Linear) GEMM fast path (pwgemm.hip): bf16 MFMA, fp32 in HBM ----------
  * mode 0 FWD  : Y[b][M][P] = act(W[M][K] . xact(X[b][K][P]) + bias) (+Y), ypre = pre-act
@@ -87,7 +98,7 @@ int dsgan_pw_supported(int mode, int M, int K, int P, long a_bs, long b_bs, cons
 int dsgan_pw_gemm(int mode, const float* A, long a_bs, const float* B, long b_bs, float* Y,
                   long y_bs, const float* bias, float* ypre, long ypre_bs, const float* gpre,
                   long gpre_bs, int M, int N, int K, int P, int nb, int act, int gact, int bact,
-                  int accumulate, float slope, float* ws, hipStream_t stream);
+                  int accumulate, float slope, float* ws, long ws_elems, hipStream_t stream);
 long dsgan_pw_wgrad_workspace(int M, int N, int P, int nb);
 long dsgan_pw_fd_workspace(int mode, int M, int K, int P, int nb);
 /* planner knob `key` <- val (val < 0: read only), returns the previous value (measurement tools) */
@@ -102,14 +113,15 @@ int dsgan_pw_f32_supported(int mode, int M, int K, int P, long a_bs, long b_bs, 
 long dsgan_pw_f32_wgrad_workspace(int M, int N, int P, int nb);
 int dsgan_pw_gemm_f32(int mode, const float* A, long a_bs, const float* B, long b_bs, float* Y, long y_bs,
                       const float* bias, const float* gpre, long gpre_bs, int M, int N, int K, int P, int nb, int act,
-                      int gact, int accumulate, float slope, float* ws, hipStream_t stream);
+                      int gact, int accumulate, float slope, float* ws, long ws_elems, hipStream_t stream);
 
 /* Weight-grad with bf16 operand(s) (pwgemm.hip): DW[M][N] += sum_{b,p} A[b][M][p] * B[b][N][p];
  * a_bf16 / b_bf16 select bf16 storage (h, gelu(z), dz of the MLP blocks).  P % 32 == 0.
  * db (nullable): db[m] += sum_{b,p} A[b][m][p], the bias grad (of the bf16 values when A is bf16).
  * ws: dsgan_pw_wgrad_workspace(M, N, P, nb) floats (deterministic split reduction). */
 int dsgan_pw_wgrad_mixed(const void* A, long a_bs, int a_bf16, const void* B, long b_bs, int b_bf16,
-                         float* dw, float* db, int M, int N, int P, int nb, float* ws, hipStream_t stream);
+                         float* dw, float* db, int M, int N, int P, int nb, float* ws, long ws_elems,
+                         hipStream_t stream);
 /* forward with bf16 activations in and/or out (unfused ConvNeXt MLP blocks c4/c5/uc1/uc2,
  * MixConvNeXtML.py:221-240): Y (+)= act(W X + bias), X/Y fp32 or bf16; ypre (nullable) = fp32
  * pre-activation, or with ypre_grad_bf16 the bf16 act'(pre) the backward multiplies by */
@@ -119,7 +131,7 @@ int dsgan_pw_fwd_io(const void* W, int w_bf16, const void* X, long x_bs, int x_b
 /* same, with the split-K scratch of dsgan_pw_fd_workspace(0, M, K, P, nb) (NULL: never split) */
 int dsgan_pw_fwd_io_ws(const void* W, int w_bf16, const void* X, long x_bs, int x_bf16, void* Y, long y_bs, int y_bf16,
                        const void* ypre, long ypre_bs, int ypre_grad_bf16, const float* bias, int M, int K, int P,
-                       int nb, int act, int accumulate, float slope, float* ws, hipStream_t stream);
+                       int nb, int act, int accumulate, float slope, float* ws, long ws_elems, hipStream_t stream);
 /* DX (+)= (W^T DY) (* GP): DY fp32 or bf16, DX fp32 or bf16, GP (nullable) the bf16 act'(pre) of
  * dsgan_pw_fwd_io.  Unfused-block pwconv2 / pwconv1 data-grads. */
 int dsgan_pw_dgrad_io(const void* W, int w_bf16, const void* DY, long dy_bs, int dy_bf16, void* DX, long dx_bs,
@@ -128,7 +140,7 @@ int dsgan_pw_dgrad_io(const void* W, int w_bf16, const void* DY, long dy_bs, int
 /* same, with the split-K scratch of dsgan_pw_fd_workspace(1, M, K, P, nb) (NULL: never split) */
 int dsgan_pw_dgrad_io_ws(const void* W, int w_bf16, const void* DY, long dy_bs, int dy_bf16, void* DX, long dx_bs,
                          int dx_bf16, const void* GP, long gp_bs, int M, int K, int P, int nb, int accumulate,
-                         float* ws, hipStream_t stream);
+                         float* ws, long ws_elems, hipStream_t stream);
 
 /* ---- fused ConvNeXt MLP (mlp.hip), replaces Block.pwconv1 -> GELU -> pwconv2 -------------------
  * DSGAN/models/model/MixConvNeXtML.py:221-223,236-240 (nn.Linear(C,4C) + GELU + nn.Linear(4C,P) on
@@ -155,8 +167,8 @@ int dsgan_mlp_bwd(const void* h, long h_bs, int h_bf16, const float* dy, long dy
  * dsgan_mlp_wgrad_workspace() floats of per-split partials, summed in a fixed order. */
 long dsgan_mlp_wgrad_workspace(int C, int P, int HW, int nb);
 int dsgan_mlp_wgrad(const void* h, long h_bs, int h_bf16, const float* dy, long dy_bs, const void* w1,
-                    const float* b1, const void* w2, float* dw1, float* db1, float* dw2, float* ws, int nb, int C,
-                    int P, int HW, hipStream_t stream);
+                    const float* b1, const void* w2, float* dw1, float* db1, float* dw2, float* ws, long ws_elems,
+                    int nb, int C, int P, int HW, hipStream_t stream);
 /* out[c] += sum_r part[r][c], rows added in a fixed order (deterministic); part is scratch and
  * is overwritten (in-place pre-reduction of many rows). */
 int dsgan_colsum(float* part, int rows, int cols, float* out, hipStream_t stream);
@@ -189,7 +201,7 @@ int dsgan_conv_small_in(const float* x, long x_bs, const float* w, long wm, long
 long dsgan_conv_wgrad_small_workspace(int N, int Cin, int Cout, int KH, int KW, int Ho, int Wo);
 int dsgan_conv_wgrad_small(const float* dy, long dy_bs, const float* x, long x_bs, float* dw, int N,
                            int Cin, int H, int W, int Cout, int KH, int KW, int stride, int pad, int Ho,
-                           int Wo, float* ws, hipStream_t stream);
+                           int Wo, float* ws, long ws_elems, hipStream_t stream);
 
 /* ---- thin 3x3 / stride 1 / pad 1 convs at full resolution (thin3.hip, exact fp32) ----------
  * The G head res = nn.Conv2d(64, 3, 3, padding=1) (DSGAN/models/model/MixConvNeXtML.py:459, applied
@@ -203,8 +215,8 @@ int dsgan_thin3_supported(int M, int H, int W, long bs_small, long bs_big);
 int dsgan_thin3_fwd(const float* x, long x_bs, const float* w, const float* bias, float* y, long y_bs, int nb, int K,
                     int M, int H, int W, int accumulate, hipStream_t stream);
 long dsgan_thin3_wgrad_workspace(int nb, int K, int M, int H, int W);
-int dsgan_thin3_wgrad(const float* dy, long dy_bs, const float* x, long x_bs, float* dw, float* ws, int nb, int K,
-                      int M, int H, int W, hipStream_t stream);
+int dsgan_thin3_wgrad(const float* dy, long dy_bs, const float* x, long x_bs, float* dw, float* ws, long ws_elems,
+                      int nb, int K, int M, int H, int W, hipStream_t stream);
 int dsgan_thin3_dgrad(const float* dy, long dy_bs, const float* w, float* dx, long dx_bs, int nb, int K, int M, int H,
                       int W, int accumulate, hipStream_t stream);
 
@@ -229,14 +241,15 @@ int dsgan_tconv_ws(const float* X, long x_bs, const float* Wt, const float* bias
                    const float* gpre, long gpre_bs, int nb, int K, int M, int Hin, int Win, int Hout,
                    int Wout, int stride, int ntaps, const int* dh, const int* dw, int Hdst, int Wdst,
                    int os, int ph, int pw, int act, int gact, float slope, int wt_bf16, float* ws,
-                   hipStream_t stream);
+                   long ws_elems, hipStream_t stream);
 /* Same with X in the library's 16-bit half type (x_bs in elements) and the 16-bit Wt of
  * dsgan_conv_wtrans_bf16: the ConvTranspose2d data-grad (MixConvNeXtML.py:53,149-152) on the
  * 16-bit output grad of dsgan_instnorm_bwd_h -- the operand values the fp32 form rounds to on load. */
 int dsgan_tconv_ws_xh(const void* Xh, long x_bs, const void* Wt, const float* bias, float* Y, long y_bs,
                       const float* gpre, long gpre_bs, int nb, int K, int M, int Hin, int Win, int Hout,
                       int Wout, int stride, int ntaps, const int* dh, const int* dw, int Hdst, int Wdst,
-                      int os, int ph, int pw, int act, int gact, float slope, float* ws, hipStream_t stream);
+                      int os, int ph, int pw, int act, int gact, float slope, float* ws, long ws_elems,
+                      hipStream_t stream);
 
 /* ---- patch-staged implicit-GEMM conv (pconv.hip): VGG16 3x3 s1 (DSGAN/models/vgg.py:15-24) fwd
  * and data-grad, PatchGAN 4x4 s2/s1 (DSGAN/models/networks.py:543-569) fwd and s1 data-grad ------
@@ -264,7 +277,7 @@ long dsgan_pconv_workspace(int nb, int K, int M, int Ho, int Wo);
 int dsgan_pconv_ws(const float* X, long x_bs, const void* Wb, const float* bias, float* Y, long y_bs,
                    const float* gpre, long gpre_bs, int nb, int K, int M, int H, int W, int Ho, int Wo,
                    int KH, int KW, int stride, int pad, int act, int gact, float slope, int accumulate,
-                   float* ws, hipStream_t stream);
+                   float* ws, long ws_elems, hipStream_t stream);
 
 /* ---- 1x1 contractions with <= 16 channels on one side (pwsmall.hip): the 3/12-channel layers
  * at 256^2 -- c1 pwconv1/pwconv2/shortcut, OriginMLKA.to32/shortcut (MixConvNeXtML.py:122,145,
@@ -300,14 +313,19 @@ int dsgan_pconvt(const float* X, long x_bs, const void* Wb, const float* bias, f
  * order: deterministic). */
 int dsgan_wconv_supported(int C, int KH, int KW, int stride);
 long dsgan_wconv_workspace(int nb, int C, int M, int Ho, int Wo, int KH, int KW);
-int dsgan_wconv(const float* D, long d_bs, const float* X, long x_bs, float* dw, float* ws, int nb,
-                int C, int M, int H, int W, int Ho, int Wo, int KH, int KW, int stride, int pad,
+int dsgan_wconv(const float* D, long d_bs, const float* X, long x_bs, float* dw, float* ws, long ws_elems,
+                int nb, int C, int M, int H, int W, int Ho, int Wo, int KH, int KW, int stride, int pad,
                 hipStream_t stream);
+/* dsgan_wconv plus the conv's bias grad: db[m] += sum_{b,oh,ow} D[b][m][oh][ow] (fp32, fixed order),
+ * from the staged D tiles (ws from dsgan_wconv_workspace, which includes the bias partials). */
+int dsgan_wconv_db(const float* D, long d_bs, const float* X, long x_bs, float* dw, float* db, float* ws,
+                   long ws_elems, int nb, int C, int M, int H, int W, int Ho, int Wo, int KH, int KW, int stride,
+                   int pad, hipStream_t stream);
 /* Same with X in the library's 16-bit half type (x_bs in elements, rows 8-byte aligned), 3x3
  * stride 2 only: the ConvTranspose2d weight-grad on dsgan_instnorm_bwd_h's output (two resident
  * workgroups per CU; ws sized by dsgan_wconv_workspace, which covers both forms). */
-int dsgan_wconv_xh(const float* D, long d_bs, const void* Xh, long x_bs, float* dw, float* ws, int nb,
-                   int C, int M, int H, int W, int Ho, int Wo, int KH, int KW, int stride, int pad,
+int dsgan_wconv_xh(const float* D, long d_bs, const void* Xh, long x_bs, float* dw, float* ws, long ws_elems,
+                   int nb, int C, int M, int H, int W, int Ho, int Wo, int KH, int KW, int stride, int pad,
                    hipStream_t stream);
 
 /* ---- depthwise conv (dwconv.hip): Block.dwconv :220, MidMLKA.X3..X9 :94-97 ----------------
@@ -332,9 +350,10 @@ int dsgan_dwconv_multi_fwd(const float* x, long x_bs, const float* w3, const flo
 long dsgan_dwconv_multi_wgrad_workspace(int N, int q, int H, int W);
 int dsgan_dwconv_multi_wgrad(const float* dy, long dy_bs, const float* x, long x_bs, float* dw3, float* db3,
                              float* dw5, float* db5, float* dw7, float* db7, float* dw9, float* db9, int N, int q,
-                             int H, int W, float* ws, hipStream_t stream);
+                             int H, int W, float* ws, long ws_elems, hipStream_t stream);
 int dsgan_dwconv_wgrad(const float* dy, long dy_bs, const float* x, long x_bs, float* dw,
-                       float* db, int N, int C, int H, int W, int K, float* ws, hipStream_t stream);
+                       float* db, int N, int C, int H, int W, int K, float* ws, long ws_elems,
+                       hipStream_t stream);
 
 /* ---- InstanceNorm2d(affine=False, eps) fused with per-plane scale, residual and activation
  * (norm_pointwise.hip): nn.InstanceNorm2d at MixConvNeXtML.py:54,80,113-116,151,158,221,
@@ -377,7 +396,7 @@ int dsgan_ca_fwd(const float* avg, const float* mx, const float* w1, const float
 int dsgan_ca_bwd(const float* datt, const float* att, const float* avg, const float* mx,
                  const float* hsave, const float* w1, const float* w2, const float* prelu_a,
                  float* davg, float* dmx, float* dw1, float* dw2, float* dprelu_a, int N, int C,
-                 int R, float* ws, hipStream_t stream);   /* ws: N*(2*R*C+1) floats (per-image partials) */
+                 int R, float* ws, long ws_elems, hipStream_t stream);   /* ws: N*(2*R*C+1) floats (per-image partials) */
 
 /* ---- elementwise / reductions ------------------------------------------------------------
  * add_n: the decoder skip sums MixConvNeXtML.py:482-492; copy_strided: torch.cat :66;
@@ -396,7 +415,7 @@ int dsgan_act_bwd(const float* dy, const float* pre, float* dx, long n, int act,
                   int accumulate, hipStream_t stream);
 /* out[c] += sum_{n,p} dy[n][c][p]; ws: N*C floats (per-plane sums, added over n in a fixed order) */
 int dsgan_channel_sum(const float* dy, long dy_bs, float* out, int N, int C, int HW, float* ws,
-                      hipStream_t stream);
+                      long ws_elems, hipStream_t stream);
 
 /* ---- losses (losses.hip): scalars written to device memory, upstream grads read from it ----
  * GANLoss/BCEWithLogits networks.py:143-163; L1 pix2pix_model.py:177,182-186;
@@ -451,7 +470,7 @@ int dsgan_img_metrics(const float* fake, const float* real, int C, int H, int W,
 long dsgan_ms_ssim_workspace(int N, int C, int H, int W);
 int dsgan_ms_ssim(const float* real, const float* fake, float a, float b, int N, int C, int H, int W,
                   const float* win11, float C1, float C2, const float* weights_host, int levels,
-                  float* work, float* stats, float* out, hipStream_t stream);
+                  float* work, long work_elems, float* stats, float* out, hipStream_t stream);
 /* MS-SSIM as a differentiable loss (C4 opt-in, --ssim_loss ms_ssim): the same value with every
  * pyramid level kept in `work` (dsgan_ms_ssim_train_workspace floats), then the backward
  * dfake (+)= d(gout[0] * out[N])/d(fake) through the per-level SSIM / contrast-structure maps,
@@ -460,10 +479,11 @@ int dsgan_ms_ssim(const float* real, const float* fake, float a, float b, int N,
 long dsgan_ms_ssim_train_workspace(int N, int C, int H, int W, int levels);
 int dsgan_ms_ssim_fwd_train(const float* real, const float* fake, float a, float b, int N, int C, int H, int W,
                             const float* win11, float C1, float C2, const float* weights_host, int levels,
-                            float* work, float* stats, float* out, hipStream_t stream);
+                            float* work, long work_elems, float* stats, float* out, hipStream_t stream);
 int dsgan_ms_ssim_bwd(const float* real, const float* fake, float a, float b, int N, int C, int H, int W,
                       const float* win11, float C1, float C2, const float* weights_host, int levels, float* work,
-                      const float* stats, const float* gout, float* dfake, int accumulate, hipStream_t stream);
+                      long work_elems, const float* stats, const float* gout, float* dfake, int accumulate,
+                      hipStream_t stream);
 
 /* ---- VGG16 perceptual pass in channel-blocked bf16 (vggconv.hip): DSGAN/models/vgg.py:15-42 ----
  * Layout CB16 = [n][c/16][h][w][c%16].  vconv3x3: 3x3/pad 1/stride 1 implicit GEMM on bf16 MFMA,

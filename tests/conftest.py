@@ -27,3 +27,9 @@ def gpu_available():
 def golden():
     import numpy as np
     return np.load(os.path.join(REPO, "tests", "golden", "golden_v1.npz"))
+
+
+@pytest.fixture(scope="session")
+def golden_v3():
+    import numpy as np
+    return np.load(os.path.join(REPO, "tests", "golden", "golden_v3.npz"))

@@ -39,8 +39,25 @@ def test_library_exports_every_symbol():
     lib = _lib.load()
     for name in _header_decls():
         assert hasattr(lib, name), name
-    assert lib.dsgan_abi_version() == 2
+    assert lib.dsgan_abi_version() == 3
     assert lib.dsgan_last_error_string() is not None
+
+
+def test_every_scratch_argument_carries_its_size():
+    """The scratch contract of include/dsgan_hip.h: a `float* ws` / `float* work` parameter is always
+    followed by its element count, and the ctypes table passes a long there."""
+    from dsgan_hip._lib import SIGNATURES, L
+    txt = re.sub(r"/\*.*?\*/", "", open(HEADER).read(), flags=re.S)
+    seen = 0
+    for m in re.finditer(r"\b(?:int|long|const char\*)\s+(dsgan_\w+)\s*\(([^)]*)\)\s*;", txt):
+        args = [" ".join(a.split()) for a in m.group(2).split(",")]
+        for i, a in enumerate(args):
+            if a in ("float* ws", "float* work"):
+                seen += 1
+                nxt = args[i + 1] if i + 1 < len(args) else ""
+                assert nxt in ("long ws_elems", "long work_elems"), (m.group(1), a, nxt)
+                assert SIGNATURES[m.group(1)][i + 1] is L, m.group(1)
+    assert seen >= 20
 
 
 def test_bad_args_fail_loudly_without_gpu_work():

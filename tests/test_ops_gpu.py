@@ -308,7 +308,7 @@ def test_pw_wgrad_bias_sums(half, a_bf16, b_bf16, N, M, C, P):
         ad = a.to(DEV).to(_hdt(half)) if a_bf16 else a.to(DEV)
         bd = b.to(DEV).to(_hdt(half)) if b_bf16 else b.to(DEV)
         call("dsgan_pw_wgrad_mixed", ptr(ad), M * P, a_bf16, ptr(bd), C * P, b_bf16, ptr(w0), ptr(b0), M, C, P, N,
-             ptr(HF._pw_ws(M, C, P, N, ad)), stream())
+             *HF.wsa(HF._pw_ws(M, C, P, N, ad)), stream())
         torch.cuda.synchronize()
         outs.append((w0.cpu(), b0.cpu()))
     assert rel(outs[0][0] - 1.0, ref_w) < 1e-5
@@ -383,6 +383,17 @@ def test_wconv_bf16(half, N, C, H, W, M, K, s, p):
     dw2 = w0.to(DEV)
     HF.conv_wgrad_raw(dy.to(DEV), xb, dw2, s, p)
     assert torch.equal(dw, dw2)
+    # the bias-grad fold (dsgan_wconv_db): the same dw bits, db += sum of the staged fp32 dy tiles
+    db0 = torch.randn(M, generator=g)
+    dw3, db = w0.to(DEV), db0.to(DEV)
+    old = HF.WCONV_DB_FOLD
+    HF.WCONV_DB_FOLD = True
+    try:
+        did_db = HF.conv_wgrad_raw(dy.to(DEV), x.to(DEV), dw3, s, p, db=db)
+    finally:
+        HF.WCONV_DB_FOLD = old
+    assert did_db and torch.equal(dw3, dw)
+    assert rel(db - db0.to(DEV), dy.double().sum(dim=(0, 2, 3))) < 1e-6
 
 
 @pytest.mark.parametrize("N,C,H,P", [(2, 64, 16, 128), (2, 128, 16, 64), (3, 128, 16, 256), (2, 256, 16, 128),
@@ -1086,22 +1097,22 @@ def test_pw_split_k(half, N, M, K, P):
         # FWD fp32 operands: y = gelu(W x + b) + y0, pre-activation to ypre
         y, pre = y0.to(DEV), torch.empty(N, M, P, device=DEV)
         call("dsgan_pw_gemm", 0, ptr(wd), 0, ptr(xd), K * P, ptr(y), M * P, ptr(bd), ptr(pre), M * P, None, 0,
-             M, N * P, K, P, N, HF.ACT["gelu"], 0, 0, 1, 0.2, ptr(ws(0)), stream())
+             M, N * P, K, P, N, HF.ACT["gelu"], 0, 0, 1, 0.2, *HF.wsa(ws(0)), stream())
         out["fwd"], out["pre"] = y, pre
         # FWD 16-bit in / GELU pair out
         gg, gp = torch.empty(N, M, P, device=DEV, dtype=hd), torch.empty(N, M, P, device=DEV, dtype=hd)
         call("dsgan_pw_fwd_io_ws", ptr(wh), 1, ptr(xh), K * P, 1, ptr(gg), M * P, 1, ptr(gp), M * P, 1,
-             ptr(bd), M, K, P, N, HF.ACT["gelu"], 0, 0.2, ptr(ws(0)), stream())
+             ptr(bd), M, K, P, N, HF.ACT["gelu"], 0, 0.2, *HF.wsa(ws(0)), stream())
         out["g"], out["gp"] = gg, gp
         # DGRAD fp32: dx = (W^T dy) * gelu'(z) + y0  (W stored [K][M] as the layer's [out][in] weight)
         dx = y0.to(DEV)
         call("dsgan_pw_gemm", 1, ptr(wTd), 0, ptr(dyd), K * P, ptr(dx), M * P, None, None, 0, ptr(zd), M * P,
-             M, N * P, K, P, N, 0, HF.ACT["gelu"], 0, 1, 0.2, ptr(ws(1)), stream())
+             M, N * P, K, P, N, 0, HF.ACT["gelu"], 0, 1, 0.2, *HF.wsa(ws(1)), stream())
         out["dgrad"] = dx
         # DGRAD 16-bit: dz = (W^T dy) * gp, 16-bit out
         dz = torch.empty(N, M, P, device=DEV, dtype=hd)
         call("dsgan_pw_dgrad_io_ws", ptr(wTh), 1, ptr(dyd), K * P, 0, ptr(dz), M * P, 1, ptr(gpd),
-             M * P, M, K, P, N, 0, ptr(ws(1)), stream())
+             M * P, M, K, P, N, 0, *HF.wsa(ws(1)), stream())
         out["dz"] = dz
         torch.cuda.synchronize()
         return {k: v.double().cpu() for k, v in out.items()}

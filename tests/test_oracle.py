@@ -103,6 +103,32 @@ def test_trajectory_with_pool(golden):
         assert np.allclose(mine, golden["F5_traj"][it], rtol=5e-4, atol=1e-5), (it, mine)
 
 
+def test_c1_trajectory_spec(golden_v3):
+    """SURVEY 8c F5 as specified (BASELINE configs[0]): 10 iterations at 64^2, batch 2,
+    pool_size 50, python random seeded 20 -- the oracle vs the reference's own recorded
+    trajectory (tests/golden/gen_golden_v3.py), and the same RNG consumption (none: the pool of 50
+    never fills with 20 images, DSGAN/util/image_pool.py:17-21).  Over 10 Adam steps the
+    reference's own fp32 trajectory moves under 1-ulp weight perturbations (fake_B ~2 %, losses
+    ~1e-3: C1_*_spread), so the bar is the north-star 1e-3 or 8x that spread, whichever is larger."""
+    g = golden_v3
+    gp = make_params(O.g_param_spec(), "fanin", 1000)
+    dp = make_params(O.d_param_spec(), "fanin", 5000)
+    vp = make_params(O.vgg_param_spec(False), "vgg", 7000)
+    rng = random.Random(20)
+    st = O.OracleStep(gp, dp, vp, pool_size=50, rng=rng)
+    for it in range(10):
+        A, B = synth_pair(2, 64, 100 + it)
+        L = st.step(A, B)
+        mine = [L["G_GAN"], L["G_L1"], L["D_real"], L["D_fake"], L["vgg"], L["tv"], L["ssim"], L["G"], L["D"]]
+        # bar: the north-star 1e-3 relative, or 8x the reference's own 1-ulp spread at this step
+        bar = np.maximum(1e-3 * np.abs(g["C1_traj"][it]), 8 * g["C1_traj_spread"][it]) + 1e-6
+        assert (np.abs(np.array(mine) - g["C1_traj"][it]) <= bar).all(), (it, mine, g["C1_traj"][it])
+    assert len(st.pool.images) == int(g["C1_pool_num_imgs"]) == 20
+    assert rng.random() == float(g["C1_next_random"])
+    fake = st.fake_B.double().numpy()
+    assert np.linalg.norm(fake - g["C1_fake"]) <= max(1e-3, 8 * float(g["C1_fake_spread"])) * np.linalg.norm(g["C1_fake"])
+
+
 def test_lambda_lr(golden):
     mults = [O.lambda_rule(e) for e in range(21)]
     assert np.allclose(mults, golden["lr_mults"], atol=1e-12)

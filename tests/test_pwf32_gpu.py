@@ -68,14 +68,14 @@ def test_pwf32_epilogues_and_slices():
     y0 = torch.randn(N, Co, H, W, generator=g).cuda()
     y = y0.clone()
     call("dsgan_pw_gemm_f32", 0, ptr(w), 0, ptr(x), (Ci + 32) * H * W, ptr(y), Co * H * W, None, None, 0, Co,
-         N * H * W, Ci, H * W, N, HF.ACT["gelu"], 0, 1, 0.2, None, stream())
+         N * H * W, Ci, H * W, N, HF.ACT["gelu"], 0, 1, 0.2, None, 0, stream())
     pre = torch.einsum("kc,nchw->nkhw", w.double(), x.double())
     ref = y0.double() + torch.nn.functional.gelu(pre)
     gpre = torch.randn(N, Ci, H, W, generator=g).cuda()
     dy = torch.randn(N, Co, H, W, generator=g).cuda()
     dx = torch.empty(N, Ci, H, W, device="cuda")
     call("dsgan_pw_gemm_f32", 1, ptr(w), 0, ptr(dy), Co * H * W, ptr(dx), Ci * H * W, None, ptr(gpre), Ci * H * W,
-         Ci, N * H * W, Co, H * W, N, 0, HF.ACT["gelu"], 0, 0.2, None, stream())
+         Ci, N * H * W, Co, H * W, N, 0, HF.ACT["gelu"], 0, 0.2, None, 0, stream())
     gp = gpre.double().requires_grad_(True)
     torch.nn.functional.gelu(gp).sum().backward()
     dref = torch.einsum("kc,nkhw->nchw", w.double(), dy.double()) * gp.grad

@@ -31,7 +31,7 @@ int dsgan_conv_small_out(const float* x, long x_bs, const float* w, long wm, lon
                          int accumulate, hipStream_t st);
 int dsgan_conv_wgrad_small(const float* dy, long dy_bs, const float* x, long x_bs, float* dw, int N,
                            int Cin, int H, int W, int Cout, int KH, int KW, int stride, int pad, int Ho,
-                           int Wo, float* ws, hipStream_t st);
+                           int Wo, float* ws, long ws_elems, hipStream_t st);
 int dsgan_pw_small_supported(int K, int M, int P, long x_bs, long y_bs);
 int dsgan_pw_small(const float* X, long x_bs, const float* W, int wm, int wk, const float* bias, float* Y,
                    long y_bs, const float* G, long g_bs, int nb, int K, int M, int P, int act, int xact, int gact,
@@ -50,7 +50,7 @@ static int fails = 0;
 static bool err_has(const char* s) { return strstr(dsgan_last_error_string(), s) != nullptr; }
 
 int main() {
-  CHECK(dsgan_abi_version() == 2);
+  CHECK(dsgan_abi_version() == 3);
   // the process-wide 16-bit operand type: 0 bf16 / 1 fp16, anything else refused with a message
   CHECK(dsgan_get_half_type() == 0);
   CHECK(dsgan_set_half_type(1) == 0 && dsgan_get_half_type() == 1);
@@ -99,7 +99,7 @@ int main() {
   CHECK(dsgan_conv_small_out(dummy, 0, dummy, 1, 1, 1, 1, nullptr, dummy, 0, 1, 4, 9, 8, 8, 8, 8, 3, 3, 1, 1, 0, 0,
                              nullptr) == -1);
   CHECK(err_has("dsgan_conv_small_out"));
-  CHECK(dsgan_conv_wgrad_small(dummy, 0, dummy, 0, dummy, 1, 16, 8, 8, 16, 5, 5, 1, 2, 8, 8, nullptr, nullptr) == -1);
+  CHECK(dsgan_conv_wgrad_small(dummy, 0, dummy, 0, dummy, 1, 16, 8, 8, 16, 5, 5, 1, 2, 8, 8, nullptr, 0, nullptr) == -1);
   CHECK(err_has("KH*KW"));
 
   // pwsmall dispatch checks

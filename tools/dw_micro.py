@@ -29,7 +29,7 @@ for N, C, H, K in [(16, 3, 256, 7), (16, 128, 256, 7), (16, 256, 128, 7), (16, 6
     f = lambda: call("dsgan_dwconv_fwd", ptr(x), C * H * H, ptr(w), ptr(b), ptr(y), C * H * H, N, C, H, H, K, 0, 0, stream())
     dws = torch.empty(dsgan_hip._lib.load().dsgan_dwconv_wgrad_workspace(N, C, H, H, K, 1), device="cuda")
     wg = lambda: call("dsgan_dwconv_wgrad", ptr(y), C * H * H, ptr(x), C * H * H, ptr(dw), ptr(db), N, C, H, H, K,
-                      ptr(dws), stream())
+                      ptr(dws), dws.numel(), stream())
     tf, tw = timeit(f), timeit(wg)
     by = 2 * x.numel() * 4
     print("N=%d C=%4d H=%3d K=%d | fwd %.3f ms %5.0f GB/s | wgrad %.3f ms %5.0f GB/s" % (N, C, H, K, tf, by / tf / 1e6, tw, by / tw / 1e6), flush=True)

@@ -28,7 +28,7 @@ for N, C, H in [(16, 128, 128), (16, 32, 128), (16, 128, 64), (16, 64, 64), (16,
     bs = [torch.zeros(q, device="cuda") for _ in range(4)]
     wsp = torch.empty(L.dsgan_dwconv_multi_wgrad_workspace(N, q, H, H), device="cuda")
     f = lambda: call("dsgan_dwconv_multi_wgrad", ptr(dy), C * H * H, ptr(x), C * H * H, ptr(ws[0]), ptr(bs[0]), ptr(ws[1]),
-                     ptr(bs[1]), ptr(ws[2]), ptr(bs[2]), ptr(ws[3]), ptr(bs[3]), N, q, H, H, ptr(wsp), stream())
+                     ptr(bs[1]), ptr(ws[2]), ptr(bs[2]), ptr(ws[3]), ptr(bs[3]), N, q, H, H, ptr(wsp), wsp.numel(), stream())
     out.append("multi C=%d H=%d %.1f us" % (C, H, timeit(f) * 1e3))
 for N, C, H in [(16, 256, 32), (16, 128, 64), (16, 1024, 32), (16, 512, 64), (16, 64, 128), (16, 128, 256)]:
     K = 7
@@ -36,6 +36,6 @@ for N, C, H in [(16, 256, 32), (16, 128, 64), (16, 1024, 32), (16, 512, 64), (16
     dw = torch.zeros(C, 1, K, K, device="cuda"); db = torch.zeros(C, device="cuda")
     dws = torch.empty(L.dsgan_dwconv_wgrad_workspace(N, C, H, H, K, 1), device="cuda")
     f = lambda: call("dsgan_dwconv_wgrad", ptr(dy), C * H * H, ptr(x), C * H * H, ptr(dw), ptr(db), N, C, H, H, K,
-                     ptr(dws), stream())
+                     ptr(dws), dws.numel(), stream())
     out.append("dw7 C=%d H=%d %.1f us" % (C, H, timeit(f) * 1e3))
 print(" | ".join(out), flush=True)

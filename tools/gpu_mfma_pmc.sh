@@ -4,7 +4,7 @@
 set -o pipefail
 mkdir -p gpurun_out
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-B="python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-quality"
+B="python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-quality --no-train-equiv"
 timeout -s KILL 30 rocprofv3 -L > gpurun_out/rocprof_counters.txt 2>&1
 echo "list rc=$?"
 timeout -s KILL 240 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CU_CYCLES SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE GRBM_GUI_ACTIVE GRBM_COUNT --kernel-trace -d gpurun_out/mfma_pmc1 -o run -- $B > gpurun_out/mfma_pmc1.log 2>&1 &&

@@ -2,7 +2,7 @@
 set -o pipefail
 mkdir -p gpurun_out
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run -- python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-quality > gpurun_out/prof.log 2>&1; rc=$?
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run -- python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-quality --no-train-equiv > gpurun_out/prof.log 2>&1; rc=$?
 tail -1 gpurun_out/prof.log | cut -c1-300
 python3 tools/prof_stats.py gpurun_out/prof/run_results.db gpurun_out/prof_stats.csv --steps 13 > gpurun_out/prof_top.txt 2>&1
 python3 tools/prof_dispatch.py gpurun_out/prof/run_results.db gpurun_out/prof_dispatch.csv --last 786 || true

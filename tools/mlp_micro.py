@@ -51,7 +51,7 @@ for name, C, P, H in SHAPES:
     bd = lambda: call("dsgan_mlp_bwd", ptr(h), C * HW, 1, ptr(dy), P * HW, ptr(w1), ptr(b1), ptr(w2), ptr(dh), C * HW,
                       None, None, None, N, C, P, HW, stream())
     wg = lambda: call("dsgan_mlp_wgrad", ptr(h), C * HW, 1, ptr(dy), P * HW, ptr(w1), ptr(b1), ptr(w2), ptr(gw1),
-                      ptr(gb1), ptr(gw2), ptr(wsp), N, C, P, HW, stream())
+                      ptr(gb1), ptr(gw2), ptr(wsp), wsp.numel(), N, C, P, HW, stream())
     bg = lambda: call("dsgan_mlp_bwd", ptr(h), C * HW, 1, ptr(dy), P * HW, ptr(w1), ptr(b1), ptr(w2), ptr(dh), C * HW,
                       ptr(g), ptr(dz), None, N, C, P, HW, stream())
     tf, tbd, twg, tbg = timeit(f), timeit(bd), timeit(wg), timeit(bg)

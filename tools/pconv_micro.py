@@ -27,8 +27,8 @@ for N, K, M, H, s, pad in [(16, 128, 256, 32, 1, 1), (16, 256, 128, 31, 1, 2), (
     nws = L.dsgan_pconv_workspace(N, K, M, Ho, Ho)
     ws = torch.empty(max(nws, 1), device="cuda")
     a = lambda: call("dsgan_pconv_ws", ptr(x), K * H * H, ptr(wb), None, ptr(y), M * Ho * Ho, None, 0, N, K, M, H, H, Ho, Ho,
-                     4, 4, s, pad, 3, 0, 0.2, 0, None, stream())
+                     4, 4, s, pad, 3, 0, 0.2, 0, None, 0, stream())
     b = lambda: call("dsgan_pconv_ws", ptr(x), K * H * H, ptr(wb), None, ptr(y), M * Ho * Ho, None, 0, N, K, M, H, H, Ho, Ho,
-                     4, 4, s, pad, 3, 0, 0.2, 0, ptr(ws), stream())
+                     4, 4, s, pad, 3, 0, 0.2, 0, ptr(ws), ws.numel(), stream())
     print("K=%d M=%d H=%d s=%d ws=%d | unsplit %.1f us | split %.1f us" % (K, M, H, s, nws, timeit(a) * 1e3, timeit(b) * 1e3),
           flush=True)

@@ -72,27 +72,27 @@ def cases(arms):
             ("fwd1-gp " + tag, f1, B * HW * (C * 2 + C4 * 4),
              lambda h=h, w1=w1, b1=b1, g=g, gp=gp, C=C, C4=C4, HW=HW, ws=wsa: call(
                  "dsgan_pw_fwd_io_ws", ptr(w1), 1, ptr(h), C * HW, 1, ptr(g), C4 * HW, 1, ptr(gp), C4 * HW, 1, ptr(b1),
-                 C4, C, HW, B, GELU, 0, 0.2, ptr(ws), stream())),
+                 C4, C, HW, B, GELU, 0, 0.2, ptr(ws), ws.numel(), stream())),
             ("fwd2-acc " + tag, f2, B * HW * (C4 * 2 + Pc * 8),
              lambda g=g, w2=w2, b2=b2, o=out_, C4=C4, Pc=Pc, HW=HW, ws=wsb: call(
                  "dsgan_pw_fwd_io_ws", ptr(w2), 1, ptr(g), C4 * HW, 1, ptr(o), Pc * HW, 0, None, 0, 0, ptr(b2),
-                 Pc, C4, HW, B, 0, 1, 0.2, ptr(ws), stream())),
+                 Pc, C4, HW, B, 0, 1, 0.2, ptr(ws), ws.numel(), stream())),
             ("dgrad2-gp " + tag, f2, B * HW * (Pc * 4 + C4 * 4),
              lambda w2=w2, dy=dy, dz=dz, gp=gp, C4=C4, Pc=Pc, HW=HW, ws=wsc: call(
                  "dsgan_pw_dgrad_io_ws", ptr(w2), 1, ptr(dy), Pc * HW, 0, ptr(dz), C4 * HW, 1, ptr(gp), C4 * HW,
-                 C4, Pc, HW, B, 0, ptr(ws), stream())),
+                 C4, Pc, HW, B, 0, ptr(ws), ws.numel(), stream())),
             ("dgrad1 " + tag, f1, B * HW * (C4 * 2 + C * 4),
              lambda w1=w1, dz=dz, dh=dh, C=C, C4=C4, HW=HW, ws=wsd: call(
                  "dsgan_pw_dgrad_io_ws", ptr(w1), 1, ptr(dz), C4 * HW, 1, ptr(dh), C * HW, 0, None, 0, C, C4,
-                 HW, B, 0, ptr(ws), stream())),
+                 HW, B, 0, ptr(ws), ws.numel(), stream())),
             ("wgrad2 " + tag, f2, B * HW * (Pc * 4 + C4 * 2),
              lambda dy=dy, g=g, wg2=wg2, gb2=gb2, C4=C4, Pc=Pc, HW=HW, ws=wsw2: call(
                  "dsgan_pw_wgrad_mixed", ptr(dy), Pc * HW, 0, ptr(g), C4 * HW, 1, ptr(wg2), ptr(gb2), Pc, C4, HW, B,
-                 ptr(ws), stream())),
+                 ptr(ws), ws.numel(), stream())),
             ("wgrad1 " + tag, f1, B * HW * (C4 * 2 + C * 2),
              lambda dz=dz, h=h, wg1=wg1, gb1=gb1, C=C, C4=C4, HW=HW, ws=wsw1: call(
                  "dsgan_pw_wgrad_mixed", ptr(dz), C4 * HW, 1, ptr(h), C * HW, 1, ptr(wg1), ptr(gb1), C4, C, HW, B,
-                 ptr(ws), stream())),
+                 ptr(ws), ws.numel(), stream())),
         ]
     # fp32 generic path (downSkip / shortcut 1x1s): (mode, M, K, H)
     for mode, M, K, H in [(1, 64, 1024, 16), (1, 128, 1024, 16), (1, 256, 1024, 16), (1, 512, 1024, 16),
@@ -107,7 +107,7 @@ def cases(arms):
                     B * HW * (K + M) * 4,
                     lambda mode=mode, w=w, x=x, y=y, M=M, K=K, HW=HW, ws=ws: call(
                         "dsgan_pw_gemm", mode, ptr(w), 0, ptr(x), K * HW, ptr(y), M * HW, None, None, 0, None, 0,
-                        M, B * HW, K, HW, B, 0, 0, 0, 0, 0.2, ptr(ws), stream())))
+                        M, B * HW, K, HW, B, 0, 0, 0, 0, 0.2, ptr(ws), ws.numel(), stream())))
     return out
 
 
