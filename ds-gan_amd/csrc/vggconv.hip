@@ -24,6 +24,7 @@
 //   cb16_maxpool      MaxPool2d(2) of a tapped fp32 feature -> bf16 + 2-bit window argmax.
 //   cb16_tap_bwd      (maxpool backward + L1 backward) x ReLU' at a tapped layer -> bf16.
 #include "common.h"
+#include "lds_dma.h"
 #include <type_traits>
 
 namespace dsg {
@@ -46,6 +47,7 @@ struct VcArgs {
   int N, K, M, H, W;
   int tiles_w, tiles_h;
   int relu, y_f32;
+  const void* zero;     // 16 zero bytes in global memory (the LDS-DMA kernel's out-of-image source)
 };
 
 template <typename T16, int BM, int TH>
@@ -163,6 +165,158 @@ __global__ __launch_bounds__(256, 2) void vconv3x3_kernel(VcArgs<T16> g) {
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
     const int n = wn * (BN / WN) + j * 32 + lr;
+    const int oh = oh0 + n / TW, ow = ow0 + n % TW;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int m = m_t * BM + wm * 64 + i * 32 + q * 8 + 4 * lh;
+        float v[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = acc[i][j][4 * q + e];
+        if (g.bias) {
+          const float4 bv = *reinterpret_cast<const float4*>(g.bias + m);
+          v[0] += bv.x; v[1] += bv.y; v[2] += bv.z; v[3] += bv.w;
+        }
+        if (g.relu) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
+        }
+        const long o = cb16(img, m, oh, ow, g.M, g.H, g.W);
+        if (g.mask) {
+          const vgb4 mk = *reinterpret_cast<const vgb4*>(g.mask + o);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = (float)mk[e] > 0.f ? v[e] : 0.f;
+        }
+        if (g.y_f32) {
+          *reinterpret_cast<float4*>(reinterpret_cast<float*>(g.Y) + o) = make_float4(v[0], v[1], v[2], v[3]);
+        } else {
+          vgb4 b;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) b[e] = (T16)v[e];
+          *reinterpret_cast<vgb4*>(reinterpret_cast<T16*>(g.Y) + o) = b;
+        }
+      }
+  }
+}
+
+// The same 3x3 implicit GEMM as vconv3x3_kernel, restructured around an LDS-DMA ring: 8 waves
+// (2 per SIMD, one workgroup per CU) own BM channels x (TH x 32) pixels; the K chunk (16 input
+// channels: all 9 taps of the pre-swizzled weight image + the (TH+2) x 34 input patch) is copied
+// global -> LDS by global_load_lds_dwordx4 straight into one of two stage buffers -- no VGPR
+// staging, no ds_write pass -- while the MFMAs run on the other: ONE barrier per chunk.  The patch
+// is a gather (per-lane source address; lanes outside the image read a 16-byte zero block), its LDS
+// image lane-linear in [half][ph][pw] order as in vconv3x3_kernel.  Per tap the next tap's A / B
+// fragments are read while this tap's MFMAs issue.  Arithmetic (operand values, accumulation order
+// per output: chunks in order, taps in order within a chunk) is vconv3x3_kernel's: same bits.
+template <typename T16, int BM, int TH>
+__global__ __launch_bounds__(512, 1) void vconv3x3_dma_kernel(VcArgs<T16> g) {
+  typedef hx8<T16> vgb8;
+  typedef hx4<T16> vgb4;
+  constexpr int TW = 32, BN = TH * TW;
+  constexpr int WM = BM / 64, WN = 8 / WM;           // waves along M (64 rows each) and N
+  constexpr int TM = 2, TN = BN / WN / 32;           // 32x32 MFMA tiles per wave
+  constexpr int PH = TH + 2, PW = TW + 2;
+  constexpr int A_BYTES = 9 * 2 * BM * 16;           // weight image of one K chunk (1 KB multiple)
+  constexpr int B_SLOTS = 2 * PH * PW;               // 16-byte patch slots [half][ph][pw]
+  constexpr int B_PIECES = (B_SLOTS + 63) / 64;      // 1 KB LDS-DMA pieces (the tail slots read zeros)
+  constexpr int STAGE = A_BYTES + B_PIECES * 1024;
+  constexpr int A_PIECES = A_BYTES / 1024;
+  constexpr int NBW = (B_PIECES + 7) / 8;            // patch pieces per wave (at most)
+  static_assert(TN >= 1 && A_BYTES % 1024 == 0 && 2 * STAGE <= 160 * 1024, "tile");
+  __shared__ __attribute__((aligned(16))) vgu4 smem[2 * STAGE / 16];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / WN, wn = wave % WN;
+  const int lr = lane & 31, lh = lane >> 5;
+
+  const int npt = g.N * g.tiles_w * g.tiles_h;
+  int tile;
+  {
+    const int nwg = gridDim.x, id = blockIdx.x;
+    const int xcd = id & 7, q = nwg >> 3, r = nwg & 7;
+    tile = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (id >> 3);
+  }
+  const int m_t = tile / npt, pt = tile - m_t * npt;
+  const int tpi = g.tiles_w * g.tiles_h;
+  const int img = pt / tpi, ti = pt - img * tpi;
+  const int oh0 = (ti / g.tiles_w) * TH, ow0 = (ti % g.tiles_w) * TW;
+  const int nkc = g.K >> 4;
+  const long plane = (long)g.H * g.W * 16;           // elements of one 16-channel block of one image
+
+  // per-lane patch gather offsets (elements within a chunk plane; -1 = outside the image)
+  int boff[NBW];
+#pragma unroll
+  for (int q = 0; q < NBW; ++q) {
+    const int s = (wave + 8 * q) * 64 + lane;
+    int off = -1;
+    if (s < B_SLOTS) {
+      const int half = s / (PH * PW), rem = s - half * (PH * PW);
+      const int ph = rem / PW, pw = rem - ph * PW;
+      const int ih = oh0 - 1 + ph, iw = ow0 - 1 + pw;
+      if ((unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W) off = (ih * g.W + iw) * 16 + half * 8;
+    }
+    boff[q] = off;
+  }
+  const char* wsrc = reinterpret_cast<const char*>(g.Wt) + (long)m_t * nkc * A_BYTES;
+  const unsigned lbase = lds_off(smem);
+  auto issue = [&](int kc, int stage) __attribute__((always_inline)) {
+    const unsigned ls = lbase + stage * STAGE;
+    const char* a = wsrc + (long)kc * A_BYTES + lane * 16;
+#pragma unroll
+    for (int p0 = 0; p0 < A_PIECES; p0 += 8)
+      if (p0 + wave < A_PIECES) dma16(a + (p0 + wave) * 1024, ls + (p0 + wave) * 1024);
+    const T16* xb = g.X + ((long)img * nkc + kc) * plane;
+#pragma unroll
+    for (int q = 0; q < NBW; ++q) {
+      const int p = wave + 8 * q;
+      if (p < B_PIECES)
+        dma16(boff[q] >= 0 ? (const void*)(xb + boff[q]) : g.zero, ls + A_BYTES + p * 1024);
+    }
+  };
+
+  vgf16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  issue(0, 0);
+  for (int kc = 0; kc < nkc; ++kc) {
+    dma_wait_all();                 // this wave's pieces of chunk kc have landed
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();   // every wave's pieces landed; every wave is done with chunk kc-1
+    if (kc + 1 < nkc) issue(kc + 1, (kc + 1) & 1);
+    const T16* Ab = reinterpret_cast<const T16*>(reinterpret_cast<const char*>(smem) + (kc & 1) * STAGE);
+    const T16* Bb = Ab + A_BYTES / 2;
+    vgb8 af[2][TM], bfr[2][TN];
+    auto frags = [&](int tap, int b) __attribute__((always_inline)) {
+      const int kh = tap / 3, kw = tap - (tap / 3) * 3;
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+        af[b][i] = *reinterpret_cast<const vgb8*>(Ab + ((tap * 2 + lh) * BM + wm * 64 + i * 32 + lr) * 8);
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        bfr[b][j] = *reinterpret_cast<const vgb8*>(Bb + ((lh * PH + wn * TN + j + kh) * PW + lr + kw) * 8);
+    };
+    frags(0, 0);
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap) {
+      if (tap + 1 < 9) frags(tap + 1, (tap + 1) & 1);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = mfma16(af[tap & 1][i], bfr[tap & 1][j], acc[i][j]);
+    }
+  }
+
+  // ---- epilogue (vconv3x3_kernel's) ----
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int n = (wn * TN + j) * 32 + lr;
     const int oh = oh0 + n / TW, ow = ow0 + n % TW;
 #pragma unroll
     for (int i = 0; i < TM; ++i)
@@ -480,7 +634,30 @@ static void vc_launch(VcArgs<T16>& g, hipStream_t st) {
   hipLaunchKernelGGL((vconv3x3_kernel<T16, BM, TH>), dim3((unsigned)tiles), dim3(256), 0, st, g);
 }
 
+// device address of the 16-byte zero block (nullptr if it cannot be resolved: the register-staged
+// kernel runs instead)
+static const void* vc_zero() {
+  static const void* zero = nullptr;
+  if (!zero) {
+    void* p = nullptr;
+    if (hipGetSymbolAddress(&p, HIP_SYMBOL(g_dma_zero16)) == hipSuccess) zero = p;
+  }
+  return zero;
+}
+
+template <typename T16, int BM, int TH>
+static void vc_launch_dma(VcArgs<T16>& g, hipStream_t st) {
+  g.tiles_w = g.W / 32;
+  g.tiles_h = g.H / TH;
+  const long tiles = (long)g.N * g.tiles_w * g.tiles_h * (g.M / BM);
+  hipLaunchKernelGGL((vconv3x3_dma_kernel<T16, BM, TH>), dim3((unsigned)tiles), dim3(512), 0, st, g);
+}
+
 static int vc_bm(int M) { return (M % 128 == 0) ? 128 : 64; }
+
+// Planner knob (measurement tools): 0 = the LDS-DMA ring kernel where a launch fills the chip,
+// 1 = always the register-staged kernel (default until the ring kernel is measured on the step).
+static int g_vc_mode = 1;
 
 }  // namespace dsg
 
@@ -490,6 +667,15 @@ extern "C" {
 
 int dsgan_vconv_supported(int K, int M, int H, int W) {
   return K > 0 && M > 0 && K % 16 == 0 && M % 64 == 0 && W % 32 == 0 && H % 4 == 0;
+}
+
+// planner knob `key` <- val (val < 0: read only), returns the previous value (measurement tools):
+// key 0 = kernel form (0 LDS-DMA ring where it fills the chip, 1 register-staged)
+int dsgan_vconv_tune(int key, int val) {
+  if (key != 0) return -1;
+  const int old = g_vc_mode;
+  if (val >= 0) g_vc_mode = val;
+  return old;
 }
 
 // bf16 elements of the swizzled weights of a Co x Ci 3x3 conv (either mode)
@@ -525,6 +711,19 @@ int dsgan_vconv3x3(const void* X, const void* Wt, const float* bias, const void*
     g.X = (const T16*)X; g.Wt = (const T16*)Wt; g.bias = bias; g.mask = (const T16*)mask; g.Y = Y;
     g.N = N; g.K = K; g.M = M; g.H = H; g.W = W; g.relu = relu; g.y_f32 = y_f32;
     const int BM = vc_bm(M);
+    // LDS-DMA ring kernel (one 8-wave workgroup per CU): 16-row pixel tiles where they still give a
+    // workgroup per CU, else 8-row ones
+    const long pt16 = H % 16 == 0 ? (long)N * (W / 32) * (H / 16) * (M / BM) : 0;
+    const long pt8 = H % 8 == 0 ? (long)N * (W / 32) * (H / 8) * (M / BM) : 0;
+    g.zero = g_vc_mode == 0 && (pt16 >= 256 || pt8 >= 256) ? vc_zero() : nullptr;
+    if (g.zero) {
+      if (BM == 128) {
+        if (pt16 >= 256) vc_launch_dma<T16, 128, 16>(g, st); else vc_launch_dma<T16, 128, 8>(g, st);
+      } else {
+        if (pt16 >= 256) vc_launch_dma<T16, 64, 16>(g, st); else vc_launch_dma<T16, 64, 8>(g, st);
+      }
+      return;
+    }
     // 8-row pixel tiles unless that leaves fewer than two workgroups per CU
     const bool th8 = H % 8 == 0 && (long)N * (W / 32) * (H / 8) * (M / BM) >= 512;
     if (BM == 128) {

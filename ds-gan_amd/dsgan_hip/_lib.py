@@ -144,6 +144,7 @@ SIGNATURES = {
     "dsgan_ssim_bwd": [P, P, F, F, I, I, I, P, P, P, F, P, I, S],
     # vggconv.hip
     "dsgan_vconv_supported": [I, I, I, I],
+    "dsgan_vconv_tune": [I, I],
     "dsgan_vconv_wtrans_size": [I, I],
     "dsgan_vconv_wtrans": [P, P, I, I, I, S],
     "dsgan_vconv3x3": [P, P, P, P, P, I, I, I, I, I, I, I, S],

@@ -494,6 +494,10 @@ int dsgan_ms_ssim_bwd(const float* real, const float* fake, float a, float b, in
  * cb16_maxpool: MaxPool2d(2) fp32 -> bf16 + u8 window argmax; cb16_tap_bwd: (maxpool backward +
  * L1 backward of the tapped feature) * ReLU' -> bf16 (pix2pix_model.py:182-186). */
 int dsgan_vconv_supported(int K, int M, int H, int W);
+/* planner knob `key` <- val (val < 0: read only), returns the previous value (measurement tools):
+ * key 0 = kernel form, 0 the LDS-DMA ring kernel where a launch fills the chip, 1 the
+ * register-staged kernel everywhere */
+int dsgan_vconv_tune(int key, int val);
 long dsgan_vconv_wtrans_size(int Co, int Ci);
 int dsgan_vconv_wtrans(const float* W, void* Wt, int Co, int Ci, int dgrad, hipStream_t stream);
 int dsgan_vconv3x3(const void* X, const void* Wt, const float* bias, const void* mask, void* Y, int y_f32, int relu,
