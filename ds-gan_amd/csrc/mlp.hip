@@ -694,7 +694,11 @@ __global__ __launch_bounds__(512, MINB) void mlp_dh_kernel(MlpArgs g) {
 // GD: also write g and dz (bf16) and the b1 partial sums for the weight-grad GEMMs; without it the
 // kernel writes dh only (mlp_wgrad_kernel recomputes what the weight path needs), drops the g
 // chunk buffer and fits two workgroups per CU (MINB) where the tiles allow.
-template <typename T16, int C, int P, int BN, int HC, int NW, bool GD, int MINB>
+// DMA: the weight chunks arrive by LDS-DMA into a two-chunk ring (chunk j+1 lands while chunk j
+// computes; the h / dy staging area becomes the second ring slot once their fragments are in
+// registers), the b1 slice comes from LDS: one barrier fewer per chunk and no register staging of
+// the weights.  Same operands, same order of every sum: same bits as the register-staged form.
+template <typename T16, int C, int P, int BN, int HC, int NW, bool GD, int MINB, bool DMA = false>
 __global__ __launch_bounds__(NW * 64, MINB) void mlp_bwd_kernel(MlpArgs g) {
   typedef hx8<T16> mbf16x8;
   typedef hx4<T16> mbf16x4;
@@ -703,13 +707,19 @@ __global__ __launch_bounds__(NW * 64, MINB) void mlp_bwd_kernel(MlpArgs g) {
   // Hs / Ds padded (transposed reads only); Zn / Gn and the weight chunks unpadded + slot-swizzled
   constexpr int HSTR = BN + 32, NSTR = HC, W1STR = C, W2STR = HC;
   constexpr int H_SZ = C * HSTR, D_SZ = P * HSTR, N_SZ = BN * NSTR, W1_SZ = HC * W1STR, W2_SZ = P * W2STR;
-  __shared__ __attribute__((aligned(16))) T16 smem[H_SZ + D_SZ + (GD ? 2 : 1) * N_SZ + W1_SZ + W2_SZ];
+  constexpr int W_SZ = W1_SZ + W2_SZ;
+  static_assert(!DMA || (H_SZ + D_SZ >= W_SZ && HC == 64 && (C / 8) % NW == 0 && (P / 8) % NW == 0), "DMA ring");
+  constexpr int SM_SZ = DMA ? H_SZ + D_SZ + W_SZ + (GD ? 2 : 1) * N_SZ + 2 * C4
+                            : H_SZ + D_SZ + (GD ? 2 : 1) * N_SZ + W1_SZ + W2_SZ;
+  __shared__ __attribute__((aligned(16))) T16 smem[SM_SZ];
   T16* Hs = smem;
   T16* Ds = Hs + H_SZ;
-  T16* Zn = Ds + D_SZ;                 // dz chunk, pixel-major [BN][NSTR]
-  T16* Gn = Zn + (GD ? N_SZ : 0);      // g chunk,  pixel-major [BN][NSTR] (GD only)
-  T16* W1s = Zn + (GD ? 2 : 1) * N_SZ;
+  // DMA: ring slot 0 after the staging area, then Zn / Gn, then b1 (fp32); slot 1 = the staging area
+  T16* Zn = Ds + D_SZ + (DMA ? W_SZ : 0);   // dz chunk, pixel-major [BN][NSTR]
+  T16* Gn = Zn + (GD ? N_SZ : 0);           // g chunk,  pixel-major [BN][NSTR] (GD only)
+  T16* W1s = DMA ? Ds + D_SZ : Zn + (GD ? 2 : 1) * N_SZ;
   T16* W2s = W1s + W1_SZ;
+  float* b1s = reinterpret_cast<float*>(Zn + (GD ? 2 : 1) * N_SZ);   // (DMA only)
 
   using ZG = WGrid<HC, BN, NW>;   // z / t chunk [HC x BN]
   using HG = WGrid<C, BN, NW>;    // dh tile [C x BN]
@@ -729,11 +739,16 @@ __global__ __launch_bounds__(NW * 64, MINB) void mlp_bwd_kernel(MlpArgs g) {
   const int img = tile / tpi, p0 = (tile - img * tpi) * BN;
 
   using WC = WCh<C, P, HC, NT>;
-  mu32x4 wr1[WC::N1], wr2[WC::N2];
-  wch_load<C, P, HC, NT>(wr1, wr2, g.w1, g.w2, 0, tid);
+  mu32x4 wr1[DMA ? 1 : WC::N1], wr2[DMA ? 1 : WC::N2];
+  if constexpr (DMA) {
+    glds_chunk<C, P, NW, false>(W1s, W2s, g.w1, g.w2, 0, wave, lane);   // chunk 0 -> ring slot 0
+    for (int i = tid; i < C4; i += NT) b1s[i] = g.b1[i];
+  } else {
+    wch_load<C, P, HC, NT>(wr1, wr2, g.w1, g.w2, 0, tid);
+  }
   stage_h<C, BN, HSTR, NT>(Hs, g, img, p0, tid);
   stage_rows<P, BN, HSTR, NT>(Ds, g.dy + (long)img * g.dy_bs + p0, g.HW, tid);
-  wch_store_swz<C, P, HC, NT>(wr1, wr2, W1s, W2s, tid);
+  if constexpr (!DMA) wch_store_swz<C, P, HC, NT>(wr1, wr2, W1s, W2s, tid);
 
   mf32x16 hacc[HG::TM][HG::TN];
 #pragma unroll
@@ -759,14 +774,35 @@ __global__ __launch_bounds__(NW * 64, MINB) void mlp_bwd_kernel(MlpArgs g) {
   const int chh = (wave & 1) * 32;
   const long gbase = (long)img * C4 * g.HW + p0;
   for (int j = 0; j < NCH; ++j) {
-    if (j + 1 < NCH) wch_load<C, P, HC, NT>(wr1, wr2, g.w1, g.w2, j + 1, tid);
+    if constexpr (DMA) {
+      // chunk j has landed (this wave's pieces: the only LDS-DMA in flight) and every wave is done
+      // with chunk j-1 (its ring slot, Zn / Gn, and at j = 0 the h / dy staging area = slot 1)
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      if (j + 1 < NCH) {
+        T16* W1n = (j & 1) ? Ds + D_SZ : Hs;
+        glds_chunk<C, P, NW, false>(W1n, W1n + W1_SZ, g.w1, g.w2, j + 1, wave, lane);
+      }
+      W1s = (j & 1) ? Hs : Ds + D_SZ;
+      W2s = W1s + W1_SZ;
+    } else {
+      if (j + 1 < NCH) wch_load<C, P, HC, NT>(wr1, wr2, g.w1, g.w2, j + 1, tid);
+    }
     // ---- z = W1[chunk] h + b1 ;  t = W2[:, chunk]^T dy ----
     mf32x16 zacc[ZG::TM][ZG::TN], tacc[ZG::TM][ZG::TN];
 #pragma unroll
     for (int i = 0; i < ZG::TM; ++i) {
       float bv[16];
+      if constexpr (DMA) {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) bv[r] = g.b1[j * HC + wm * (HC / 2) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh];
+        for (int q = 0; q < 4; ++q) {
+          const float4 b4 = *reinterpret_cast<const float4*>(b1s + j * HC + wm * (HC / 2) + i * 32 + 8 * q + 4 * lh);
+          bv[4 * q] = b4.x; bv[4 * q + 1] = b4.y; bv[4 * q + 2] = b4.z; bv[4 * q + 3] = b4.w;
+        }
+      } else {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) bv[r] = g.b1[j * HC + wm * (HC / 2) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh];
+      }
 #pragma unroll
       for (int t = 0; t < ZG::TN; ++t)
 #pragma unroll
@@ -804,7 +840,12 @@ __global__ __launch_bounds__(NW * 64, MINB) void mlp_bwd_kernel(MlpArgs g) {
           *reinterpret_cast<mbf16x4*>(Zn + swz_off<HC / 8>(n, m)) = dv4;
         }
       }
-    __syncthreads();
+    if constexpr (DMA) {   // raw barrier: the next chunk's LDS-DMA stays in flight across it
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+    } else {
+      __syncthreads();
+    }
     // ---- copy-out: 8 pixels of one hidden row per lane (transposing read) -> 16-byte stores;
     //      per-(tile, wave>>1) sums of dz for the b1 grad.  Skipped (g_out == NULL) when the
     //      weight-grads come from mlp_wgrad_kernel instead. ----
@@ -840,10 +881,12 @@ __global__ __launch_bounds__(NW * 64, MINB) void mlp_bwd_kernel(MlpArgs g) {
         for (int t = 0; t < HG::TN; ++t)
           hacc[i][t] = mfma16(af[i], bf[t], hacc[i][t]);
     }
-    __syncthreads();
-    if (j + 1 < NCH) {
-      wch_store_swz<C, P, HC, NT>(wr1, wr2, W1s, W2s, tid);
+    if constexpr (!DMA) {
       __syncthreads();
+      if (j + 1 < NCH) {
+        wch_store_swz<C, P, HC, NT>(wr1, wr2, W1s, W2s, tid);
+        __syncthreads();
+      }
     }
   }
 
@@ -1196,11 +1239,15 @@ static void fwd_launch(const MlpArgs& g, hipStream_t st) {
 }
 // backward: 8 waves x 128 pixels where the LDS tiles fit, else 4 waves x 64 pixels (same bsum
 // granularity: one partial row per 32 pixels)
-template <typename T16, int C, int P, int BN, int NW, bool GD = true, int MINB = 1>
+// Planner knob (measurement tools): key 0 = the C = 256 backward with g / dz out, 0 the LDS-DMA
+// weight ring, 1 the register-staged weights (default until the ring is measured on the GPU).
+static int g_mlp_tune[4] = {1, 0, 0, 0};
+
+template <typename T16, int C, int P, int BN, int NW, bool GD = true, int MINB = 1, bool DMA = false>
 static void bwd_launch(const MlpArgs& g, hipStream_t st) {
   static_assert(BN / (NW / 2) == 32, "bsum granularity");
   const unsigned tiles = (unsigned)((long)g.nb * (g.HW / BN));
-  hipLaunchKernelGGL((mlp_bwd_kernel<T16, C, P, BN, 64, NW, GD, MINB>), dim3(tiles), dim3(NW * 64), 0, st, g);
+  hipLaunchKernelGGL((mlp_bwd_kernel<T16, C, P, BN, 64, NW, GD, MINB, DMA>), dim3(tiles), dim3(NW * 64), 0, st, g);
 }
 
 // weight-grad kernel: same pixel tile as the backward; splits so that NCH * S ~ 512 workgroups
@@ -1283,6 +1330,7 @@ int dsgan_mlp_bwd(const void* h, long h_bs, int h_bf16, const float* dy, long dy
     } else if (C == 64) bwd_launch<T16, 64, 128, 128, 8>(g, st);
     else if (C == 128 && P == 64) bwd_launch<T16, 128, 64, 128, 8>(g, st);
     else if (C == 128) bwd_launch<T16, 128, 256, 64, 4>(g, st);
+    else if (g_mlp_tune[0] == 0) bwd_launch<T16, 256, 128, 64, 4, true, 1, true>(g, st);
     else bwd_launch<T16, 256, 128, 64, 4>(g, st);
   });
   DSG_CHECK_LAUNCH();
@@ -1325,6 +1373,15 @@ int dsgan_mlp_wgrad(const void* h, long h_bs, int h_bf16, const float* dy, long 
   launch_split_reduce_multi(3, wsv, sv, mv, dv, st);
   DSG_CHECK_LAUNCH();
   return 0;
+}
+
+// planner knob `key` <- val (val < 0: read only), returns the previous value (measurement tools):
+// key 0 = the C = 256 backward with g / dz out: 0 LDS-DMA weight ring, 1 register-staged weights
+int dsgan_mlp_tune(int key, int val) {
+  if (key < 0 || key >= 4) return -1;
+  const int old = g_mlp_tune[key];
+  if (val >= 0) g_mlp_tune[key] = val;
+  return old;
 }
 
 int dsgan_colsum(float* part, int rows, int cols, float* out, hipStream_t st) {

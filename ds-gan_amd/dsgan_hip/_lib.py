@@ -57,6 +57,7 @@ SIGNATURES = {
     "dsgan_mlp_bwd": [P, L, I, P, L, P, P, P, P, L, P, P, P, I, I, I, I, S],
     "dsgan_mlp_wgrad_workspace": [I, I, I, I],
     "dsgan_mlp_wgrad": [P, L, I, P, L, P, P, P, P, P, P, P, L, I, I, I, I, S],
+    "dsgan_mlp_tune": [I, I],
     "dsgan_colsum": [P, I, I, P, S],
     "dsgan_f32_to_bf16": [P, P, L, S],
     # pconv.hip
