@@ -1,6 +1,6 @@
-// Pointwise GEMM kernel templates (pwgemm.hip), shared by the two translation units that
-// instantiate them: pwgemm.hip (bf16 operands + the C ABI) and pwgemm_f16.hip (fp16 operands),
-// compiled in parallel.  See pwgemm.hip for the design notes.
+// Pointwise GEMM kernel templates (pwgemm.hip), shared by the translation units that instantiate
+// them: pw_{fwd,dgrad,wgrad}_{bf16,f16}.hip (one mode x operand type each, compiled in parallel) and
+// pwgemm.hip (the planner + the C ABI).  See pwgemm.hip for the design notes.
 #pragma once
 #include "common.h"
 #include <stdlib.h>

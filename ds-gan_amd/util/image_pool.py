@@ -32,7 +32,15 @@ class ImagePool:
         if self.pool_size == 0:
             return images
         images = images.detach().contiguous()
-        if self.store is None or self.store.shape[1:] != images.shape[1:]:
+        if self.store is not None and (self.store.shape[1:] != images.shape[1:] or self.store.dtype != images.dtype
+                                       or self.store.device != images.device):
+            if self.num_imgs > 0:
+                # the reference's list would mix shapes and its torch.cat (image_pool.py:32) fail
+                raise ValueError("ImagePool.query: images of shape %s %s on %s, the pool holds %d of shape %s %s on %s"
+                                 % (tuple(images.shape[1:]), images.dtype, images.device, self.num_imgs,
+                                    tuple(self.store.shape[1:]), self.store.dtype, self.store.device))
+            self.store = None
+        if self.store is None:
             self.store = torch.empty((self.pool_size,) + tuple(images.shape[1:]), device=images.device,
                                      dtype=images.dtype)
         # slot -> where its CURRENT contents live: ("pool", slot) = unchanged this query, ("in", j)

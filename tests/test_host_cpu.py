@@ -215,3 +215,20 @@ def test_grad_buckets_gloo_world2():
         ok, nb, early, n_early, unhooked = out[r]
         assert ok and unhooked
         assert nb >= 3 and 1 <= early < nb and n_early == early
+
+
+def test_image_pool_refuses_a_shape_change():
+    """ImagePool keeps one resident [pool, C, H, W] tensor: images of another shape while it holds
+    images raise (the reference's list would mix shapes and its torch.cat, image_pool.py:32, fail);
+    an empty pool re-sizes.  Checked before any device copy, so it runs on CPU."""
+    import random
+    import sys
+    sys.path.insert(0, os.path.join(REPO, "ds-gan_amd"))
+    from util.image_pool import ImagePool
+    pool = ImagePool(3, rng=random.Random(0))
+    pool.store = torch.empty(3, 3, 4, 4)
+    pool.num_imgs = 1
+    with pytest.raises(ValueError, match="pool holds 1"):
+        pool.query(torch.zeros(1, 3, 8, 8))
+    with pytest.raises(ValueError):
+        pool.query(torch.zeros(1, 3, 4, 4, dtype=torch.float64))

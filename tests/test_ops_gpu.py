@@ -1209,3 +1209,65 @@ def test_plane_stats_fwd_bwd(shape):
     ref_dx = dx0.view(N * C, HW) + (davg / HW).view(-1, 1)
     ref_dx[torch.arange(N * C), am.cpu().long()] += dmx
     assert torch.allclose(dx.cpu().view(N * C, HW), ref_dx, rtol=1e-6, atol=1e-6)
+
+
+@pytest.mark.parametrize("n", [1027, 4 * 300000 + 2])   # a scalar tail (n % 4 != 0); many check blocks
+def test_loss_scaler_state_machine(n):
+    """dsgan_amp_check / amp_update (adam.hip:135-169) against GradScaler's rule
+    (torch/amp/grad_scaler.py _amp_update_scale_): overflow -> skip, scale x backoff, clean count
+    reset; `interval` clean steps -> scale x growth; applied-step count only on clean steps.  The
+    non-finite element sits in the scalar tail, in the vector body and is a nan; the skipped
+    optimizer step leaves params / moments untouched.  Also the unit-scale guard (bf16 mode)."""
+    from dsgan_hip.amp import LossScaler
+    from dsgan_hip.flat import FlatAdam
+    sc = LossScaler(DEV, init_scale=2.0 ** 10, growth_factor=2.0, backoff_factor=0.5, growth_interval=3)
+    g = torch.randn(n, device=DEV) * 1e-3
+    scale, clean, applied = 2.0 ** 10, 0, 0
+    bad_at = {1: n - 1, 4: n // 3, 5: 0}           # step -> poisoned index (tail, body, first)
+    for step in range(10):
+        gg = g.clone()
+        if step in bad_at:
+            gg[bad_at[step]] = float("nan") if step == 4 else float("inf")
+        sc.check(gg)
+        torch.cuda.synchronize()
+        st = sc.state.cpu().tolist()
+        skip = step in bad_at
+        assert st[1] == (1.0 if skip else 0.0), (step, st)
+        assert st[3] == 1.0 / scale, (step, st)
+        if skip:
+            scale, clean = scale * 0.5, 0
+        else:
+            applied += 1
+            clean += 1
+            if clean >= 3:
+                scale, clean = scale * 2.0, 0
+        assert st[0] == scale and st[2] == clean and st[4] == applied, (step, st, scale, clean, applied)
+
+    # the optimizer on a skipped step: nothing moves
+    class _Flat:
+        pass
+    fl = _Flat()
+    fl.data = torch.randn(4099, device=DEV)
+    fl.grad = torch.randn(4099, device=DEV)
+    fl.grad[4098] = float("inf")
+    fl.numel = 4099
+    fl.params = [torch.nn.Parameter(fl.data)]
+    gs = LossScaler.guard(DEV)
+    opt = FlatAdam(fl, scaler=gs)
+    p0 = fl.data.clone()
+    gs.check(fl.grad)
+    opt.step()
+    torch.cuda.synchronize()
+    assert torch.equal(fl.data, p0) and not opt.m.any() and not opt.v.any()
+    assert gs.skipped_last() and gs.get_scale() == 1.0 and gs.skipped_steps(1) == 1
+    # a clean step under the guard = plain Adam (scale exactly 1, step count 1)
+    fl.grad[4098] = 0.5
+    gs.check(fl.grad)
+    opt.step()
+    torch.cuda.synchronize()
+    ref = p0.clone()
+    call_adam = torch.optim.Adam([torch.nn.Parameter(ref)], lr=2e-4, betas=(0.9, 0.999), eps=1e-8)
+    call_adam.param_groups[0]["params"][0].grad = fl.grad.clone()
+    call_adam.step()
+    assert gs.get_scale() == 1.0 and gs.applied_steps() == 1
+    assert rel(fl.data, call_adam.param_groups[0]["params"][0].detach()) < 1e-6
