@@ -1271,3 +1271,51 @@ def test_loss_scaler_state_machine(n):
     call_adam.step()
     assert gs.get_scale() == 1.0 and gs.applied_steps() == 1
     assert rel(fl.data, call_adam.param_groups[0]["params"][0].detach()) < 1e-6
+
+
+@pytest.mark.parametrize("half", HALVES)
+@pytest.mark.parametrize("N,H", [(2, 16), (3, 32)])
+def test_mlp_bwd_c256_forms_bitwise(half, N, H):
+    """The three forms of the C = 256 MLP backward with g / dz out (mlp.hip: register-staged 4-wave,
+    LDS-DMA weight ring, 8-wave mlp_bwd8_kernel; dsgan_mlp_tune key 0) give the same bits for dh, g,
+    dz and the per-32-pixel dz sums -- and dh matches the fp32 chain within the 16-bit bar."""
+    import dsgan_hip
+    from dsgan_hip import _lib
+    from dsgan_hip._lib import call, ptr, stream
+    lib = _lib.load()
+    dsgan_hip.set_precision(half)
+    C, P, HW = 256, 128, H * H
+    C4 = 4 * C
+    hd = _hdt(half)
+    g0 = torch.Generator(device=DEV).manual_seed(11)
+    h = torch.randn(N, C, HW, device=DEV, generator=g0).to(hd)
+    dy = torch.randn(N, P, HW, device=DEV, generator=g0)
+    w1 = (torch.randn(C4, C, device=DEV, generator=g0) / C ** 0.5).to(hd)
+    w2 = (torch.randn(P, C4, device=DEV, generator=g0) / C4 ** 0.5).to(hd)
+    b1 = torch.randn(C4, device=DEV, generator=g0) * 0.1
+    old = lib.dsgan_mlp_tune(0, -1)
+    outs = {}
+    try:
+        for mode in (1, 0, 2):
+            lib.dsgan_mlp_tune(0, mode)
+            dh = torch.full((N, C, HW), float("nan"), device=DEV)
+            gg = torch.empty(N, C4, HW, device=DEV, dtype=hd)
+            dz = torch.empty_like(gg)
+            bs = torch.full((N * HW // 32, C4), float("nan"), device=DEV)
+            call("dsgan_mlp_bwd", ptr(h), C * HW, 1, ptr(dy), P * HW, ptr(w1), ptr(b1), ptr(w2), ptr(dh), C * HW,
+                 ptr(gg), ptr(dz), ptr(bs), N, C, P, HW, stream())
+            torch.cuda.synchronize()
+            outs[mode] = (dh, gg, dz, bs)
+    finally:
+        lib.dsgan_mlp_tune(0, old)
+    for mode in (0, 2):
+        for a, b in zip(outs[mode], outs[1]):
+            assert torch.equal(a, b), mode
+    # value check of dh against the fp32 chain on the same 16-bit operands
+    hf, w1f, w2f = h.float(), w1.float(), w2.float()
+    z = torch.einsum("kc,nch->nkh", w1f, hf) + b1[None, :, None]
+    t = torch.einsum("pk,nph->nkh", w2f, dy)
+    gp = 0.5 * (1 + torch.erf(z / math.sqrt(2))) + z * torch.exp(-0.5 * z * z) / math.sqrt(2 * math.pi)
+    dzr = (t * gp).to(hd).float()
+    dhr = torch.einsum("kc,nkh->nch", w1f, dzr)
+    assert rel(outs[1][0], dhr) < 3 * _ulp(half)
