@@ -921,17 +921,9 @@ __global__ __launch_bounds__(NW * 64, MINB) void mlp_bwd_kernel(MlpArgs g) {
 }
 
 // ------------------------------------------------------------------------------------------
-// backward with g / dz out, 8 waves (the C = 256 blocks): the 4-wave kernel above at C = 256 holds
-// one workgroup -- one wave per SIMD -- per CU (139 KB of LDS), so every LDS-read, barrier and load
-// latency of its chunk loop is exposed.  Here 8 waves share one 64-pixel tile with 128-row hidden
-// chunks: z / t as 4 hidden quarters x 2 pixel halves of 32 x 32, dh as 4 channel quarters x 2 pixel
-// halves of 64 x 32.  h's B fragments live in registers, dy stays in LDS (its fragments are re-read
-// per chunk), the weight chunk (96 KB) takes the h staging area once h is in registers: 156 KB of
-// LDS, two waves per SIMD in 256 registers.  Every LDS address is one XOR or one immediate offset
-// away from a per-lane base (the swizzles only touch the slot bits below the row pitch): the chunk
-// loop keeps a dozen address registers instead of ~90.  Every sum runs in the 4-wave kernel's order
-// (z, t over C / P; dh over the hidden units 0..4C-1 in 16-row steps; the dz sums per 32-pixel
-// group): the same bits.
+// LDS addressing with few live registers: every address of a slot-swizzled tile is one XOR or one
+// immediate offset away from a per-lane base (the swizzles only touch the slot bits below the row
+// pitch), so a loop keeps one base per operand instead of one address per fragment.
 // ------------------------------------------------------------------------------------------
 // byte offset of a lane's 16-byte row read (row, column 8 lh) of a slot-swizzled [rows][S*8] tile;
 // column ks*16 + 8 lh is then at (this ^ 32 ks) (ks < S / 2: the XOR stays inside the row)
@@ -961,148 +953,6 @@ __device__ __forceinline__ hx8<T16> tr_at(const T16* T, uint2 a, unsigned k_byte
 #else
   return hx8<T16>{};
 #endif
-}
-
-template <typename T16, int C, int P>
-__global__ __launch_bounds__(512, 1) void mlp_bwd8_kernel(MlpArgs g) {
-  typedef hx8<T16> mbf16x8;
-  typedef hx4<T16> mbf16x4;
-  constexpr int NT = 512, BN = 64, HC = 128;
-  constexpr int C4 = 4 * C, NCH = C4 / HC;
-  constexpr int HSTR = BN + 32;
-  constexpr int H_SZ = C * HSTR, D_SZ = P * HSTR, W1_SZ = HC * C, W2_SZ = P * HC, N_SZ = BN * HC;
-  constexpr int R_SZ = (H_SZ > W1_SZ + W2_SZ) ? H_SZ : W1_SZ + W2_SZ;
-  static_assert(C == 256 && P % 16 == 0 && (2 * (R_SZ + D_SZ) + 4 * N_SZ + 4 * C4) <= 160 * 1024, "tile shape");
-  __shared__ __attribute__((aligned(1024))) T16 smem[R_SZ + 2 * N_SZ + D_SZ + 2 * C4];
-  T16* Hs = smem;
-  T16* W1s = smem;                 // after h is in registers
-  T16* W2s = W1s + W1_SZ;
-  T16* Zn = smem + R_SZ;           // dz chunk, pixel-major [BN][HC], slot-swizzled
-  T16* Gn = Zn + N_SZ;             // g chunk
-  T16* Ds = Gn + N_SZ;             // dy tile, k-major [P][HSTR]
-  float* b1s = reinterpret_cast<float*>(Ds + D_SZ);
-
-  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int lr = lane & 31, lh = lane >> 5;
-  const int tq = (lane >> 2) & 3, tp = lane & 3, tG = (lane >> 4) & 1;
-  const int wq = wave >> 1, wn = wave & 1;   // hidden (z / t) or channel (dh) quarter, pixel half
-
-  const int tpi = g.HW / BN;
-  const int tile = xcd_tile(blockIdx.x, gridDim.x);
-  const int img = tile / tpi, p0 = (tile - img * tpi) * BN;
-
-  using WC = WCh<C, P, HC, NT>;
-  mu32x4 wr1[WC::N1], wr2[WC::N2];
-  const __amdgpu_buffer_rsrc_t rw1 = __builtin_amdgcn_make_buffer_rsrc((void*)g.w1, (short)0, C4 * C * 2, 0x00020000);
-  const __amdgpu_buffer_rsrc_t rw2 = __builtin_amdgcn_make_buffer_rsrc((void*)g.w2, (short)0, P * C4 * 2, 0x00020000);
-  wch_load_buf<C, P, HC, NT>(wr1, wr2, rw1, rw2, 0, tid);
-  stage_h<C, BN, HSTR, NT>(Hs, g, img, p0, tid);
-  stage_rows<P, BN, HSTR, NT>(Ds, g.dy + (long)img * g.dy_bs + p0, g.HW, tid);
-  for (int i = tid; i < C4; i += NT) b1s[i] = g.b1[i];
-  __syncthreads();
-  // per-lane LDS byte offsets (chunk-invariant)
-  const unsigned tr_hd = (unsigned)(((8 * lh + tq) * HSTR + wn * 32 + 16 * tG + 4 * tp) * 2);   // mtr_frag on Hs / Ds
-  mbf16x8 hbr[C / 16];
-#pragma unroll
-  for (int ks = 0; ks < C / 16; ++ks)
-    hbr[ks] = mtr_frag((const T16*)((const char*)Hs + tr_hd) + ks * 16 * HSTR, HSTR);
-  mf32x16 hacc[2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) hacc[i][r] = 0.f;
-  __syncthreads();   // the staging area becomes the weight chunk
-  wch_store_swz<C, P, HC, NT>(wr1, wr2, W1s, W2s, tid);
-  __syncthreads();
-
-  const unsigned a_z = swz_row_b<C / 8>(wq * 32 + lr, lh);        // W1s row reads (z)
-  const uint2 a_t = swz_tr_b<HC / 8>(wq * 32, lane);              // W2s transposed reads (t)
-  const uint2 a_d0 = swz_tr_b<C / 8>(wq * 64, lane);              // W1s transposed reads (dh)
-  const uint2 a_d1 = swz_tr_b<C / 8>(wq * 64 + 32, lane);
-  const unsigned a_n = swz_row_b<HC / 8>(wn * 32 + lr, lh);       // Zn row reads (dh B operand)
-  const int chq = (wave & 3) * 32;                                // copy-out: hidden quarter
-  const uint2 a_c = swz_tr_b<HC / 8>(chq, lane);                  // Gn / Zn transposed reads
-  // epilogue writes: (pixel wn*32 + lr, hidden wq*32 + 8q + 4lh) at a_e ^ 16 q
-  const unsigned a_e = (unsigned)((wn * 32 + lr) * HC * 2 + (((wq * 4) ^ slot_swz<HC / 8>(wn * 32 + lr)) << 4) + 8 * lh);
-  const long gbase = (long)img * C4 * g.HW + p0;
-  for (int j = 0; j < NCH; ++j) {
-    if (j + 1 < NCH) wch_load_buf<C, P, HC, NT>(wr1, wr2, rw1, rw2, j + 1, tid);
-    // ---- z = W1[chunk] h + b1 ;  t = W2[:, chunk]^T dy  (rows wq * 32 .. +32 of the chunk) ----
-    mf32x16 zacc, tacc;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const float4 b4 = *reinterpret_cast<const float4*>(b1s + j * HC + wq * 32 + 8 * q + 4 * lh);
-      zacc[4 * q] = b4.x; zacc[4 * q + 1] = b4.y; zacc[4 * q + 2] = b4.z; zacc[4 * q + 3] = b4.w;
-    }
-#pragma unroll
-    for (int r = 0; r < 16; ++r) tacc[r] = 0.f;
-#pragma unroll
-    for (int ks = 0; ks < C / 16; ++ks) {
-      const mbf16x8 af = *reinterpret_cast<const mbf16x8*>((const char*)W1s + (a_z ^ (unsigned)(32 * ks)));
-      zacc = mfma16(af, hbr[ks], zacc);
-    }
-#pragma unroll
-    for (int ks = 0; ks < P / 16; ++ks) {
-      const mbf16x8 af = tr_at(W2s, a_t, ks * 16 * HC * 2);
-      const mbf16x8 bf = mtr_frag((const T16*)((const char*)Ds + tr_hd) + ks * 16 * HSTR, HSTR);
-      tacc = mfma16(af, bf, tacc);
-    }
-    // ---- g = gelu(z), dz = t * gelu'(z) -> LDS, pixel-major, 4 hidden per write ----
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      mbf16x4 gv4, dv4;
-#pragma unroll
-      for (int e = 0; e < 4; e += 2) {
-        f32x2 gv, gp;
-        gelu_pair_fast2(f32x2{zacc[4 * q + e], zacc[4 * q + e + 1]}, gv, gp);
-        const f32x2 dz = f32x2{tacc[4 * q + e], tacc[4 * q + e + 1]} * gp;
-        gv4[e] = (T16)gv.x; gv4[e + 1] = (T16)gv.y;
-        dv4[e] = (T16)dz.x; dv4[e + 1] = (T16)dz.y;
-      }
-      const unsigned o = a_e ^ (unsigned)(16 * q);
-      *reinterpret_cast<mbf16x4*>((char*)Gn + o) = gv4;
-      *reinterpret_cast<mbf16x4*>((char*)Zn + o) = dv4;
-    }
-    __syncthreads();
-    // ---- copy-out (8 pixels of one hidden row per lane, 16-byte stores) + dz sums per 32 pixels ----
-    {
-      float bacc = 0.f;
-#pragma unroll
-      for (int c = 0; c < 2; ++c) {
-        const int pb = ((wave >> 2) * 2 + c) * 16;
-        const mbf16x8 gv = tr_at(Gn, a_c, pb * HC * 2);
-        const mbf16x8 dv = tr_at(Zn, a_c, pb * HC * 2);
-        const long o = gbase + (long)(j * HC + chq + lr) * g.HW + pb + 8 * lh;
-        *reinterpret_cast<mbf16x8*>((T16*)g.g_out + o) = gv;
-        *reinterpret_cast<mbf16x8*>((T16*)g.dz_out + o) = dv;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) bacc += (float)dv[e];
-      }
-      bacc += __shfl_xor(bacc, 32, 64);
-      if (lh == 0 && g.bsum) g.bsum[((long)tile * 2 + (wave >> 2)) * C4 + j * HC + chq + lr] = bacc;
-    }
-    // ---- dh[wq * 64 .. +64][wn * 32 .. +32] += W1[chunk]^T dz ----
-#pragma unroll
-    for (int ks = 0; ks < HC / 16; ++ks) {
-      const mbf16x8 bf = *reinterpret_cast<const mbf16x8*>((const char*)Zn + (a_n ^ (unsigned)(32 * ks)));
-      hacc[0] = mfma16(tr_at(W1s, a_d0, ks * 16 * C * 2), bf, hacc[0]);
-      hacc[1] = mfma16(tr_at(W1s, a_d1, ks * 16 * C * 2), bf, hacc[1]);
-    }
-    __syncthreads();
-    if (j + 1 < NCH) {
-      wch_store_swz<C, P, HC, NT>(wr1, wr2, W1s, W2s, tid);
-      __syncthreads();
-    }
-  }
-
-  float* ob = g.out + (long)img * g.out_bs + p0 + wn * 32 + lr;
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int c = wq * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-      ob[(long)c * g.HW] = hacc[i][r];
-    }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1441,9 +1291,10 @@ static void fwd_launch(const MlpArgs& g, hipStream_t st) {
 // backward: 8 waves x 128 pixels where the LDS tiles fit, else 4 waves x 64 pixels (same bsum
 // granularity: one partial row per 32 pixels)
 // Planner knob (measurement tools): key 0 = the C = 256 backward with g / dz out, 0 the LDS-DMA
-// weight ring, 1 the register-staged weights (default until the others are measured on the GPU),
-// 2 the 8-wave form (mlp_bwd8_kernel).
-static int g_mlp_tune[4] = {1, 0, 0, 0};
+// weight ring (default: 0.831 -> 0.717 ms at uc3, B = 16, same bits; profiles/r04/mlp_micro.txt),
+// 1 the register-staged weights.  (An 8-wave form -- two waves per SIMD, 128-row hidden chunks --
+// measured 0.977 ms: at 256 registers it spills, and it issues more VALU per MFMA.)
+static int g_mlp_tune[4] = {0, 0, 0, 0};
 
 template <typename T16, int C, int P, int BN, int NW, bool GD = true, int MINB = 1, bool DMA = false>
 static void bwd_launch(const MlpArgs& g, hipStream_t st) {
@@ -1533,8 +1384,6 @@ int dsgan_mlp_bwd(const void* h, long h_bs, int h_bf16, const float* dy, long dy
     else if (C == 128 && P == 64) bwd_launch<T16, 128, 64, 128, 8>(g, st);
     else if (C == 128) bwd_launch<T16, 128, 256, 64, 4>(g, st);
     else if (g_mlp_tune[0] == 0) bwd_launch<T16, 256, 128, 64, 4, true, 1, true>(g, st);
-    else if (g_mlp_tune[0] == 2 && P == 128)
-      hipLaunchKernelGGL((mlp_bwd8_kernel<T16, 256, 128>), dim3((unsigned)((long)g.nb * (g.HW / 64))), dim3(512), 0, st, g);
     else bwd_launch<T16, 256, 128, 64, 4>(g, st);
   });
   DSG_CHECK_LAUNCH();
@@ -1580,8 +1429,7 @@ int dsgan_mlp_wgrad(const void* h, long h_bs, int h_bf16, const float* dy, long 
 }
 
 // planner knob `key` <- val (val < 0: read only), returns the previous value (measurement tools):
-// key 0 = the C = 256 backward with g / dz out: 0 LDS-DMA weight ring, 1 register-staged weights,
-// 2 8 waves x 128-row hidden chunks
+// key 0 = the C = 256 backward with g / dz out: 0 LDS-DMA weight ring, 1 register-staged weights
 int dsgan_mlp_tune(int key, int val) {
   if (key < 0 || key >= 4) return -1;
   const int old = g_mlp_tune[key];

@@ -31,7 +31,6 @@ struct PwArgs {
   unsigned a_range, b_range;   // buffer-resource byte ranges of A and B (B: per image for FWD/DGRAD)
   int y_bf16;  // FWD: Y is bf16 [b][M][P] (y_bs in elements)
   int gbf;     // FWD: ypre is bf16 and receives act'(pre);  DGRAD: gpre is a bf16 multiplier (no act')
-  int bk64;    // host planner: 128 / 64-row tiles with 64-deep K steps (else 32)
   int gp_pref; // DGRAD with a 16-bit gp multiplier (SWP tiles): load gp before the K loop
   float* asum; // WGRAD (nullable): db[m] += sum_k A[m][k] -- the bias grad of the layer whose output
                // grad is A, from the staged A tiles (split partials after the S*M*N weight partials)
@@ -653,7 +652,7 @@ static void pw_launch_abs(const PwArgs& g, int bm, int abf, int bbf, int splits,
     case 2: pw_launch<T16, MODE, BM, 1, 0, 128, 2, BK, SWP>(g, splits, st); break;                \
     default: pw_launch<T16, MODE, BM, 1, 1, 128, 2, BK, SWP>(g, splits, st); break;               \
   }
-#define PW_AB(BM) if (g.bk64 && BM <= 128) { PW_AB_K(BM, 64) } else { PW_AB_K(BM, PBK) }
+#define PW_AB(BM) PW_AB_K(BM, PBK)
 #define PW_ABW                                                                    \
   switch (sel) {                                                                  \
     case 0: pw_launch<T16, MODE, 128, 0, 0, 128, 2, PBK, SWP>(g, 1, st); break;  /* (not selected) */  \
@@ -821,7 +820,7 @@ void pw_fd_launch_m(const PwArgs& g, int bm, int abf, int bbf, int splits, hipSt
 }
 template <typename T16>
 void pw_wgrad_launch(const PwArgs& g, int bm, int abf, int bbf, int splits, hipStream_t st) {
-  const int sel = (abf ? 2 : 0) + (bbf ? 1 : 0) + (bm == 128 ? 4 : bm == PW_WIDE ? 8 : 0) + (g.bk64 && bm == 128 ? 16 : 0);
+  const int sel = (abf ? 2 : 0) + (bbf ? 1 : 0) + (bm == 128 ? 4 : bm == PW_WIDE ? 8 : 0);
   switch (sel) {
     case 9: pw_launch<T16, PW_WGRAD, 256, 0, 1, 256, 4, 64>(g, splits, st); break;
     case 10: pw_launch<T16, PW_WGRAD, 256, 1, 0, 256, 4, 64>(g, splits, st); break;
@@ -833,11 +832,7 @@ void pw_wgrad_launch(const PwArgs& g, int bm, int abf, int bbf, int splits, hipS
     case 4: pw_launch<T16, PW_WGRAD, 128, 0, 0>(g, splits, st); break;
     case 5: pw_launch<T16, PW_WGRAD, 128, 0, 1>(g, splits, st); break;
     case 6: pw_launch<T16, PW_WGRAD, 128, 1, 0>(g, splits, st); break;
-    case 7: pw_launch<T16, PW_WGRAD, 128, 1, 1>(g, splits, st); break;
-    case 16 + 4: pw_launch<T16, PW_WGRAD, 128, 0, 0, 128, 2, 64>(g, splits, st); break;
-    case 16 + 5: pw_launch<T16, PW_WGRAD, 128, 0, 1, 128, 2, 64>(g, splits, st); break;
-    case 16 + 6: pw_launch<T16, PW_WGRAD, 128, 1, 0, 128, 2, 64>(g, splits, st); break;
-    default: pw_launch<T16, PW_WGRAD, 128, 1, 1, 128, 2, 64>(g, splits, st); break;
+    default: pw_launch<T16, PW_WGRAD, 128, 1, 1>(g, splits, st); break;
   }
 }
 #define PW_EXTERN_LAUNCHERS(T16)                                                                            \

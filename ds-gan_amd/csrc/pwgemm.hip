@@ -33,8 +33,9 @@ static void pw_fd_launch(int mode, const PwArgs& g, int bm, int abf, int bbf, in
 
 // Planner knobs, read by the host launchers only (tools/pw_bench.py flips them for in-process A/B):
 //   [0] FWD/DGRAD split-K on/off, [1] its target workgroup count, [2] split only launches of fewer
-//   tiles than this, [3] minimum K steps per split, [4] 64-deep K steps for the 128 / 64-row FWD /
-//   DGRAD tiles, [5] the same for the 128-row WGRAD tiles, [6] gelu-pair forward tile (0 built-in,
+//   tiles than this, [3] minimum K steps per split, [4] / [5] retired (64-deep K steps for the 128 /
+//   64-row tiles: +1 % / neutral over the step's shapes, profiles/r04/pw_bench_knobs.txt; the variants
+//   are gone, the keys are ignored), [6] gelu-pair forward tile (0 built-in,
 //   1 256 x 128, 2 128 x 128, 3 wide 256 x 256), [7] gp-multiplied data-grad tile (same codes),
 //   [8] gp loaded before the K loop (16-bit gp data-grads on 128 / 64-row tiles).
 static int g_tune[12] = {1, 512, 256, 4, 0, 0, 0, 0, 1, 0, 0, 0};
@@ -80,10 +81,9 @@ static int fd_plan(PwArgs& g, int bm, float* ws) {
   int splits = 1;
   g.k_split = 0;
   g.ws = nullptr;
-  g.bk64 = g_tune[4] && bm != PW_WIDE && bm != 256;
   g.gp_pref = g_tune[8];
   if (ws && fd_split_ok(g)) {
-    splits = fd_splits(g, bm, g.bk64 ? 64 : PBK, &g.k_split);
+    splits = fd_splits(g, bm, PBK, &g.k_split);
     if (splits > 1) g.ws = ws;
     else g.k_split = 0;
   }
@@ -301,16 +301,7 @@ void launch_split_reduce_multi(int n, const float* const* ws, const int* splits,
   hipLaunchKernelGGL(split_reduce_multi_kernel, dim3((unsigned)b), dim3(256), 0, st, R);
 }
 
-// 64-deep K steps for the 128-row weight-grad tiles (knob 5): re-plan the pixel split on 64-pixel steps
-static int wgrad_cfg_k(PwArgs& g, bool any_bf16, int* bm) {
-  int splits = wgrad_cfg(g, any_bf16, bm);
-  g.bk64 = 0;
-  if (g_tune[5] && *bm == 128 && g.P % 64 == 0) {
-    g.bk64 = 1;
-    splits = wgrad_plan(g.M, g.N, g.K, 128, 128, 64, 640, &g.k_split);
-  }
-  return splits;
-}
+static int wgrad_cfg_k(PwArgs& g, bool any_bf16, int* bm) { return wgrad_cfg(g, any_bf16, bm); }
 
 // scratch a weight-grad plan writes: weight partials [split][M][N], then bias-sum partials [split][M]
 static long wgrad_need(const PwArgs& g, int splits) {

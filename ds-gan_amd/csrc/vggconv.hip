@@ -655,9 +655,10 @@ static void vc_launch_dma(VcArgs<T16>& g, hipStream_t st) {
 
 static int vc_bm(int M) { return (M % 128 == 0) ? 128 : 64; }
 
-// Planner knob (measurement tools): 0 = the LDS-DMA ring kernel where a launch fills the chip,
-// 1 = always the register-staged kernel (default until the ring kernel is measured on the step).
-static int g_vc_mode = 1;
+// Planner knob (measurement tools): 0 = the LDS-DMA ring kernel where a launch fills the chip
+// (default: the step's 14 VGG launches 1014 -> 936 us at B = 16, same bits;
+// profiles/r04/vconv_micro.txt), 1 = always the register-staged kernel.
+static int g_vc_mode = 0;
 
 }  // namespace dsg
 

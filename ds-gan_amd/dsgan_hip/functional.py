@@ -27,8 +27,10 @@ def wsa(t):
 
 
 # PatchGAN 4x4 weight-grads also sum the conv's bias grad from their staged dy tiles
-# (dsgan_wconv_db) instead of a separate channel-sum pass; see DESIGN.md section 6.
-WCONV_DB_FOLD = False
+# (dsgan_wconv_db) instead of a separate channel-sum pass (78 launches per step fewer); the
+# round-3 non-finite replay with it does not reproduce on the round-4 tree (tools/nan_diag.py,
+# profiles/r04/nan_diag.txt); see DESIGN.md section 6.
+WCONV_DB_FOLD = True
 
 ACT = {None: 0, "none": 0, "gelu": 1, "relu": 2, "lrelu": 3, "sigmoid": 4}
 PREC = {"fp32": 0, "bf16": 1, "fp16": 1}   # the C ABI's prec: 0 exact f32, 1 16-bit MFMA operands
