@@ -3,6 +3,7 @@
 // pwgemm.hip (the planner + the C ABI).  See pwgemm.hip for the design notes.
 #pragma once
 #include "common.h"
+#include "lds_dma.h"
 #include <stdlib.h>
 
 namespace dsg {
@@ -32,6 +33,7 @@ struct PwArgs {
   int y_bf16;  // FWD: Y is bf16 [b][M][P] (y_bs in elements)
   int gbf;     // FWD: ypre is bf16 and receives act'(pre);  DGRAD: gpre is a bf16 multiplier (no act')
   int gp_pref; // DGRAD with a 16-bit gp multiplier (SWP tiles): load gp before the K loop
+  int dma;     // host planner: the wide 16-bit-operand launch runs the LDS-DMA ring form (NS = 4)
   float* asum; // WGRAD (nullable): db[m] += sum_k A[m][k] -- the bias grad of the layer whose output
                // grad is A, from the staged A tiles (split partials after the S*M*N weight partials)
 };
@@ -45,6 +47,39 @@ __device__ __forceinline__ hx8<T16> tr_frag(const T16* p0, int stride) {
 #if defined(__HIP_DEVICE_COMPILE__)
   s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p0));
   s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p0 + 4 * stride));
+  typedef __attribute__((ext_vector_type(8))) short s16x8;
+  s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(hx8<T16>, v);
+#else
+  return hx8<T16>{};
+#endif
+}
+
+// ---- LDS-DMA stage images (NS > 0 kernels): unpadded tiles with XOR-swizzled 16-byte slots ----
+// A DMA piece is lane-linear in LDS, so the swizzle goes on the global source address.
+//   row image [rows][32] (4 slots per 64-byte row; row reads, ds_read_b128): slot ^ ((row >> 2) & 3)
+//     -- 16 consecutive rows reading one logical slot touch 16 distinct 16-byte bank groups;
+//   k-major image [32][cols] (cols / 8 >= 16 slots; transposed reads, 2 x ds_read_b64_tr_b16):
+//     slot ^ (4 (k & 3) + ((k >> 2) & 3)) -- conflict-free for the 4-slot x 4-row transposed reads.
+__device__ __forceinline__ int pw_rswz(int r) { return (r >> 2) & 3; }
+__device__ __forceinline__ int pw_kswz(int k) { return ((k & 3) << 2) | ((k >> 2) & 3); }
+typedef __attribute__((address_space(3))) s16x4 pw_lds_s16x4;
+// transposed fragment of a k-major image [32][S*8] at rows k0 + (8h + tq, +4), cols col0 + 16 tG + 4 tp
+// (the tr_frag lane map); byte offsets of the two reads for k0 = 0 (k0 % 16 == 0 adds k0 * S * 16 bytes)
+template <int S>
+__device__ __forceinline__ uint2 pw_tr_addr(int col0, int lane) {
+  const int tq = (lane >> 2) & 3, tp = lane & 3, tG = (lane >> 4) & 1, h = lane >> 5;
+  const int col = col0 + 16 * tG + 4 * tp;
+  const int rlo = 8 * h + tq, rhi = rlo + 4;
+  return make_uint2((unsigned)(rlo * S * 8 + (((col >> 3) ^ pw_kswz(rlo)) << 3) + (col & 7)) * 2u,
+                    (unsigned)(rhi * S * 8 + (((col >> 3) ^ pw_kswz(rhi)) << 3) + (col & 7)) * 2u);
+}
+template <typename T16>
+__device__ __forceinline__ hx8<T16> pw_tr_at(const T16* T, uint2 a, unsigned kbytes) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const char* b = (const char*)T + kbytes;
+  s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((pw_lds_s16x4*)(b + a.x));
+  s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((pw_lds_s16x4*)(b + a.y));
   typedef __attribute__((ext_vector_type(8))) short s16x8;
   s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
   return __builtin_bit_cast(hx8<T16>, v);
@@ -74,7 +109,13 @@ __device__ __forceinline__ hx4<T16> cvt4(float4 v, int bact, float slope) {
 // 16-byte stores (2 per 32x32 tile instead of 16 two-byte ones).  fp32 outputs keep the channel x
 // pixel tile, whose 4-byte stores fill two whole 128-byte rows per instruction (measured: the
 // swapped form's 16-byte row-strided fp32 stores are 10-15 % slower there).
-template <typename T16, int MODE, int BM, int ABF = 0, int BBF = 0, int BN = 128, int WN = 2, int BK = PBK, int SWP = 0>
+// NS > 0 (16-bit A and B, full tiles, K per split % 32 == 0): the operand tiles arrive by LDS-DMA
+// into an NS-stage ring of unpadded swizzled images, NS - 1 K steps ahead of the MFMAs, one raw
+// barrier per K step and no register staging; the MFMAs, their order and the epilogue are the
+// register-staged kernel's (same bits for the products; WGRAD's row sums of A are read back from
+// the landed stage).
+template <typename T16, int MODE, int BM, int ABF = 0, int BBF = 0, int BN = 128, int WN = 2, int BK = PBK, int SWP = 0,
+          int NS = 0>
 __global__ __launch_bounds__(128 * WN, WN == 2 ? 2 : 1) void pwgemm_kernel(PwArgs g) {
   constexpr bool SW = MODE != PW_WGRAD && SWP;
   typedef hx8<T16> pbf16x8;
@@ -91,7 +132,10 @@ __global__ __launch_bounds__(128 * WN, WN == 2 ? 2 : 1) void pwgemm_kernel(PwArg
   constexpr int B_STR = B_KMAJ ? BN + 32 : RM_STR;
   constexpr int A_SZ = A_KMAJ ? BK * A_STR : BM * A_STR;
   constexpr int B_SZ = B_KMAJ ? BK * B_STR : BN * B_STR;
-  __shared__ __attribute__((aligned(16))) T16 smem[2 * (A_SZ + B_SZ)];
+  constexpr bool DM = NS > 0;
+  static_assert(!DM || (ABF && BBF && BK == 32 && NS >= 2), "LDS-DMA ring: 16-bit operands, 32-deep K steps");
+  constexpr int DA_SZ = BM * BK, DB_SZ = BK * BN;   // DMA stage images (elements)
+  __shared__ __attribute__((aligned(1024))) T16 smem[DM ? NS * (DA_SZ + DB_SZ) : 2 * (A_SZ + B_SZ)];
 
   // wave index through readfirstlane: the compiler then knows it is uniform (SGPR), so
   // per-wave row offsets can be scalar soffsets instead of readfirstlane waterfall loops
@@ -302,9 +346,11 @@ __global__ __launch_bounds__(128 * WN, WN == 2 ? 2 : 1) void pwgemm_kernel(PwArg
       for (int r = 0; r < 16; ++r) acc[i][j][r] = bv[r];
   }
 
-  gload(0);
-  sstore(0);
-  __syncthreads();
+  if constexpr (!DM) {
+    gload(0);
+    sstore(0);
+    __syncthreads();
+  }
 
   // per-lane fragment address parts for the transposed reads:
   // lane = 32h + 16G + 4q + p supplies row (8h + q) and column 16G + 4p of its 16-column block
@@ -339,6 +385,119 @@ __global__ __launch_bounds__(128 * WN, WN == 2 ? 2 : 1) void pwgemm_kernel(PwArg
     }
   }
 
+  if constexpr (DM) {
+    // ---- LDS-DMA ring ----
+    constexpr int NW = NT / 64;
+    constexpr int AP = DA_SZ / 8 / NT, BP = DB_SZ / 8 / NT;   // 16-byte pieces per lane per stage
+    constexpr int PI = AP + BP;                               // DMA instructions per wave per stage
+    static_assert(AP * 8 * NT == DA_SZ && BP * 8 * NT == DB_SZ, "DMA pieces");
+    // per-lane source offsets (elements, stage-invariant part) of this lane's pieces
+    unsigned aoff[AP], boff[BP];
+#pragma unroll
+    for (int i = 0; i < AP; ++i) {
+      const int pc = (i * NW + wave) * 64 + lane;
+      if constexpr (A_KMAJ) {          // DGRAD W[K][M]: k-major [32][BM]
+        const int k = pc / (BM / 8), ls = (pc % (BM / 8)) ^ pw_kswz(k);
+        aoff[i] = (unsigned)(k * g.M + m0 + 8 * ls);
+      } else {                         // FWD W[M][K] / WGRAD DY[b][M][P]: rows [BM][32]
+        const int r = pc >> 2, ls = (pc & 3) ^ pw_rswz(r);
+        aoff[i] = (unsigned)((m0 + r) * (MODE == PW_WGRAD ? g.P : g.K) + 8 * ls);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < BP; ++i) {
+      const int pc = (i * NW + wave) * 64 + lane;
+      if constexpr (B_KMAJ) {          // X / DY [b][K][P]: k-major [32][BN]
+        const int k = pc / (BN / 8), ls = (pc % (BN / 8)) ^ pw_kswz(k);
+        boff[i] = (unsigned)(k * g.P + p0 + 8 * ls);
+      } else {                         // WGRAD X[b][N][P]: rows [BN][32]
+        const int r = pc >> 2, ls = (pc & 3) ^ pw_rswz(r);
+        boff[i] = (unsigned)((n0 + r) * g.P + 8 * ls);
+      }
+    }
+    const T16* Ag = (const T16*)g.A;
+    const T16* Bg = (const T16*)g.B + (long)b_fix * g.b_bs;
+    auto issue = [&](int kt) __attribute__((always_inline)) {
+      const int kb = kbeg + kt * BK;
+      T16* As = smem + (kt % NS) * (DA_SZ + DB_SZ);
+      T16* Bs = As + DA_SZ;
+      unsigned ua, ub;                 // stage-dependent uniform element offsets
+      if constexpr (MODE == PW_WGRAD) {
+        const int bw = kb / g.P, pw = kb - bw * g.P;
+        ua = (unsigned)(bw * g.a_bs + pw);
+        ub = (unsigned)(bw * g.b_bs + pw);
+      } else {
+        ua = A_KMAJ ? (unsigned)kb * g.M : (unsigned)kb;
+        ub = (unsigned)kb * g.P;
+      }
+#pragma unroll
+      for (int i = 0; i < AP; ++i) dma16(Ag + (ua + aoff[i]), lds_off(As + (i * NW + wave) * 512));
+#pragma unroll
+      for (int i = 0; i < BP; ++i) dma16(Bg + (ub + boff[i]), lds_off(Bs + (i * NW + wave) * 512));
+    };
+    // fragment read offsets (bytes, K-step invariant)
+    unsigned ar[TM];
+    uint2 at[TM], bt[TN];
+    unsigned br[TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int mb = wm * TM * 32 + i * 32;
+      if constexpr (A_KMAJ) at[i] = pw_tr_addr<BM / 8>(mb, lane);
+      else ar[i] = (unsigned)((mb + lr) * 64 + ((lh ^ pw_rswz(mb + lr)) << 4));
+    }
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int nbb = wn * TN * 32 + j * 32;
+      if constexpr (B_KMAJ) bt[j] = pw_tr_addr<BN / 8>(nbb, lane);
+      else br[j] = (unsigned)((nbb + lr) * 64 + ((lh ^ pw_rswz(nbb + lr)) << 4));
+    }
+#pragma unroll
+    for (int s = 0; s < NS - 1; ++s)
+      if (s < nk) issue(s);
+    for (int kt = 0; kt < nk; ++kt) {
+      // stage kt landed: this wave's later stages (at most NS - 2) may stay in flight
+      const int later = min(NS - 2, nk - 1 - kt);
+      if (later >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"i"(2 * PI) : "memory");
+      else if (later == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"i"(PI) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      static_assert(NS <= 4, "vmcnt ladder covers <= 2 later stages");
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();   // every wave's pieces of stage kt landed; slot (kt-1) % NS is free
+      if (kt + NS - 1 < nk) issue(kt + NS - 1);
+      const T16* As = smem + (kt % NS) * (DA_SZ + DB_SZ);
+      const T16* Bs = As + DA_SZ;
+      if constexpr (MODE == PW_WGRAD) {
+        if (g.asum) {   // the register path's row sums: this thread's A items, read from the landed stage
+#pragma unroll
+          for (int i = 0; i < A_ITEMS; ++i) {
+            const int it = tid + i * NT, r = it / RH, c8 = it % RH;
+            const pbf16x8 hv = *reinterpret_cast<const pbf16x8*>(As + r * BK + ((c8 ^ pw_rswz(r)) << 3));
+            asr[i] += (((float)hv[0] + (float)hv[1]) + ((float)hv[2] + (float)hv[3])) +
+                      (((float)hv[4] + (float)hv[5]) + ((float)hv[6] + (float)hv[7]));
+          }
+        }
+      }
+#pragma unroll
+      for (int ks = 0; ks < BK / 16; ++ks) {
+        pbf16x8 af[TM], bfr[TN];
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          if constexpr (A_KMAJ) af[i] = pw_tr_at(As, at[i], ks * 16 * BM * 2);
+          else af[i] = *reinterpret_cast<const pbf16x8*>((const char*)As + (ar[i] ^ (unsigned)(32 * ks)));
+        }
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          if constexpr (B_KMAJ) bfr[j] = pw_tr_at(Bs, bt[j], ks * 16 * BN * 2);
+          else bfr[j] = *reinterpret_cast<const pbf16x8*>((const char*)Bs + (br[j] ^ (unsigned)(32 * ks)));
+        }
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] = SW ? mfma16(bfr[j], af[i], acc[i][j]) : mfma16(af[i], bfr[j], acc[i][j]);
+      }
+    }
+  } else
   for (int kt = 0; kt < nk; ++kt) {
     const int buf = kt & 1;
     if (kt + 1 < nk) gload(kt + 1);
@@ -631,12 +790,13 @@ __global__ __launch_bounds__(128 * WN, WN == 2 ? 2 : 1) void pwgemm_kernel(PwArg
   }
 }
 
-template <typename T16, int MODE, int BM, int ABF = 0, int BBF = 0, int BN = 128, int WN = 2, int BK = PBK, int SWP = 0>
+template <typename T16, int MODE, int BM, int ABF = 0, int BBF = 0, int BN = 128, int WN = 2, int BK = PBK, int SWP = 0,
+          int NS = 0>
 static void pw_launch(const PwArgs& g, int splits, hipStream_t st) {
   const int mt = (g.M + BM - 1) / BM;
   const int nt = (MODE == PW_WGRAD) ? (g.N + BN - 1) / BN : g.N / BN;
-  hipLaunchKernelGGL((pwgemm_kernel<T16, MODE, BM, ABF, BBF, BN, WN, BK, SWP>), dim3((unsigned)((long)mt * nt * splits)),
-                     dim3(128 * WN), 0, st, g);
+  hipLaunchKernelGGL((pwgemm_kernel<T16, MODE, BM, ABF, BBF, BN, WN, BK, SWP, NS>),
+                     dim3((unsigned)((long)mt * nt * splits)), dim3(128 * WN), 0, st, g);
 }
 
 constexpr int PW_WIDE = -1;   // tile selector: 256 x 256 tiles, 8 waves, 64-deep K steps
@@ -658,7 +818,10 @@ static void pw_launch_abs(const PwArgs& g, int bm, int abf, int bbf, int splits,
     case 0: pw_launch<T16, MODE, 128, 0, 0, 128, 2, PBK, SWP>(g, 1, st); break;  /* (not selected) */  \
     case 1: pw_launch<T16, MODE, 256, 0, 1, 256, 4, 64, SWP>(g, 1, st); break;              \
     case 2: pw_launch<T16, MODE, 256, 1, 0, 256, 4, 64, SWP>(g, 1, st); break;              \
-    default: pw_launch<T16, MODE, 256, 1, 1, 256, 4, 64, SWP>(g, 1, st); break;             \
+    default:                                                                      \
+      if (g.dma) pw_launch<T16, MODE, 256, 1, 1, 256, 4, 32, SWP, 4>(g, 1, st);        \
+      else pw_launch<T16, MODE, 256, 1, 1, 256, 4, 64, SWP>(g, 1, st);                 \
+      break;                                                                      \
   }
   if (bm == PW_WIDE) { PW_ABW } else if (bm == 256) { PW_AB(256) } else if (bm == 128) { PW_AB(128) } else { PW_AB(64) }
 #undef PW_AB
@@ -824,7 +987,10 @@ void pw_wgrad_launch(const PwArgs& g, int bm, int abf, int bbf, int splits, hipS
   switch (sel) {
     case 9: pw_launch<T16, PW_WGRAD, 256, 0, 1, 256, 4, 64>(g, splits, st); break;
     case 10: pw_launch<T16, PW_WGRAD, 256, 1, 0, 256, 4, 64>(g, splits, st); break;
-    case 11: pw_launch<T16, PW_WGRAD, 256, 1, 1, 256, 4, 64>(g, splits, st); break;
+    case 11:
+      if (g.dma) pw_launch<T16, PW_WGRAD, 256, 1, 1, 256, 4, 32, 0, 4>(g, splits, st);
+      else pw_launch<T16, PW_WGRAD, 256, 1, 1, 256, 4, 64>(g, splits, st);
+      break;
     case 0: pw_launch<T16, PW_WGRAD, 64, 0, 0>(g, splits, st); break;
     case 1: pw_launch<T16, PW_WGRAD, 64, 0, 1>(g, splits, st); break;
     case 2: pw_launch<T16, PW_WGRAD, 64, 1, 0>(g, splits, st); break;

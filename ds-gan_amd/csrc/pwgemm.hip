@@ -37,8 +37,17 @@ static void pw_fd_launch(int mode, const PwArgs& g, int bm, int abf, int bbf, in
 //   64-row tiles: +1 % / neutral over the step's shapes, profiles/r04/pw_bench_knobs.txt; the variants
 //   are gone, the keys are ignored), [6] gelu-pair forward tile (0 built-in,
 //   1 256 x 128, 2 128 x 128, 3 wide 256 x 256), [7] gp-multiplied data-grad tile (same codes),
-//   [8] gp loaded before the K loop (16-bit gp data-grads on 128 / 64-row tiles).
+//   [8] gp loaded before the K loop (16-bit gp data-grads on 128 / 64-row tiles), [9] the LDS-DMA
+//   ring form of the wide 16-bit-operand launches (pw_impl.h NS = 4; off until measured).
 static int g_tune[12] = {1, 512, 256, 4, 0, 0, 0, 0, 1, 0, 0, 0};
+
+// the LDS-DMA ring form's conditions (full 256 x 256 tiles, 32-deep K steps, 16-byte pieces)
+static int dma_ok(const PwArgs& g, int bm, int abf, int bbf, int mode) {
+  if (!g_tune[9] || bm != PW_WIDE || !abf || !bbf) return 0;
+  if (!al16(g.A) || !al16(g.B) || (g.a_bs & 7) || (g.b_bs & 7) || g.M % 256) return 0;
+  if (mode == PW_WGRAD) return g.N % 256 == 0 && g.P % 32 == 0 && (g.k_split % 32) == 0;
+  return g.K % 32 == 0 && g.P % 256 == 0 && g.k_split == 0;
+}
 
 // tile choice with the knob overrides of the two epilogue-heavy forms
 static int fd_tile_k(const PwArgs& g, bool any_bf16) {
@@ -91,11 +100,15 @@ static int fd_plan(PwArgs& g, int bm, float* ws) {
 }
 // scratch that plan writes: partials [split][b][M][P]
 static long fd_need(const PwArgs& g, int splits) { return splits > 1 ? (long)splits * g.M * g.N : 0; }
-static void fd_launch(int mode, const PwArgs& g, int bm, int abf, int bbf, int splits, hipStream_t st) {
+static void fd_launch(int mode, const PwArgs& g0, int bm, int abf, int bbf, int splits, hipStream_t st) {
+  PwArgs g = g0;
+  g.dma = dma_ok(g, bm, abf, bbf, mode);
   if (half_type() == HALF_F16) pw_fd_launch<_Float16>(mode, g, bm, abf, bbf, splits, st);
   else pw_fd_launch<__bf16>(mode, g, bm, abf, bbf, splits, st);
 }
-static void wg_dispatch(const PwArgs& g, int bm, int abf, int bbf, int splits, hipStream_t st) {
+static void wg_dispatch(const PwArgs& g0, int bm, int abf, int bbf, int splits, hipStream_t st) {
+  PwArgs g = g0;
+  g.dma = dma_ok(g, bm, abf, bbf, PW_WGRAD);
   if (half_type() == HALF_F16) pw_wgrad_launch<_Float16>(g, bm, abf, bbf, splits, st);
   else pw_wgrad_launch<__bf16>(g, bm, abf, bbf, splits, st);
 }

@@ -1318,3 +1318,67 @@ def test_mlp_bwd_c256_forms_bitwise(half, N, H):
     dzr = (t * gp).to(hd).float()
     dhr = torch.einsum("kc,nkh->nch", w1f, dzr)
     assert rel(outs[1][0], dhr) < 3 * _ulp(half)
+
+
+@pytest.mark.parametrize("half", HALVES)
+@pytest.mark.parametrize("form", ["fwd16", "fwd32", "fwd_gelu_pair", "dgrad32", "dgrad16", "wgrad"])
+def test_pw_wide_dma_ring_bitwise(half, form):
+    """The LDS-DMA ring form of the wide 16-bit-operand pointwise GEMMs (pw_impl.h NS = 4, planner
+    knob dsgan_pw_tune(9)) against the register-staged wide kernel: the same MFMAs in the same order,
+    so FWD / DGRAD outputs and WGRAD weight grads are bitwise equal; the WGRAD bias sums (row sums of
+    the staged A tiles) within 1e-6.  Full 256 x 256 tiles, >= 256 of them."""
+    import dsgan_hip
+    from dsgan_hip import _lib, functional as HF
+    from dsgan_hip._lib import call, ptr, stream
+    lib = _lib.load()
+    dsgan_hip.set_precision(half)
+    hd = _hdt(half)
+    g0 = torch.Generator(device=DEV).manual_seed(5)
+    NB, HW = 4, 128 * 128
+    M, K = (512, 256) if form != "wgrad" else (256, 512)
+    w = (torch.randn(M, K, device=DEV, generator=g0) / K ** 0.5).to(hd)
+    bias = torch.randn(M, device=DEV, generator=g0)
+    x = torch.randn(NB, K, HW, device=DEV, generator=g0).to(hd)
+    dy = torch.randn(NB, M, HW, device=DEV, generator=g0).to(hd)
+    old = lib.dsgan_pw_tune(9, -1)
+
+    def run(dma):
+        lib.dsgan_pw_tune(9, dma)
+        if form.startswith("fwd"):
+            y16 = form != "fwd32"
+            y = torch.empty(NB, M, HW, device=DEV, dtype=hd if y16 else torch.float32)
+            gp = torch.empty(NB, M, HW, device=DEV, dtype=hd) if form == "fwd_gelu_pair" else None
+            ws = torch.empty(max(1, lib.dsgan_pw_fd_workspace(0, M, K, HW, NB)), device=DEV)
+            call("dsgan_pw_fwd_io_ws", ptr(w), 1, ptr(x), K * HW, 1, ptr(y), M * HW, int(y16), ptr(gp),
+                 M * HW if gp is not None else 0, 1 if gp is not None else 0, ptr(bias), M, K, HW, NB,
+                 1 if gp is not None else 0, 0, 0.2, *HF.wsa(ws), stream())
+            return [y] + ([gp] if gp is not None else [])
+        if form.startswith("dgrad"):   # dx[K] = W^T dy[M]: W [M][K] is the [in][out] operand
+            y16 = form == "dgrad16"
+            dx = torch.empty(NB, K, HW, device=DEV, dtype=hd if y16 else torch.float32)
+            ws = torch.empty(max(1, lib.dsgan_pw_fd_workspace(1, K, M, HW, NB)), device=DEV)
+            call("dsgan_pw_dgrad_io_ws", ptr(w), 1, ptr(dy), M * HW, 1, ptr(dx), K * HW, int(y16), None, 0, K, M,
+                 HW, NB, 0, *HF.wsa(ws), stream())
+            return [dx]
+        dw = torch.zeros(M, K, device=DEV)
+        db = torch.zeros(M, device=DEV)
+        ws = torch.empty(max(1, lib.dsgan_pw_wgrad_workspace(M, K, HW, NB)), device=DEV)
+        call("dsgan_pw_wgrad_mixed", ptr(dy), M * HW, 1, ptr(x), K * HW, 1, ptr(dw), ptr(db), M, K, HW, NB,
+             *HF.wsa(ws), stream())
+        return [dw, db]
+    try:
+        ref = run(0)
+        got = run(1)
+        torch.cuda.synchronize()
+    finally:
+        lib.dsgan_pw_tune(9, old)
+    if form == "wgrad":
+        assert torch.equal(got[0], ref[0])
+        assert rel(got[1], ref[1]) < 1e-6
+    else:
+        for a, b in zip(got, ref):
+            assert torch.equal(a, b)
+    # and the values: fp32 chain on the same 16-bit operands
+    if form == "fwd32":
+        r = torch.einsum("mk,nkp->nmp", w.float(), x.float()) + bias[None, :, None]
+        assert rel(got[0], r) < 1e-5
