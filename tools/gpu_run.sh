@@ -14,6 +14,7 @@
 #   launches                  tools/launch_table.py per-launch HIP-event table -> launches_all.txt
 #   prof                      rocprofv3 kernel stats of a short bench run (tools/gpu_prof.sh)
 #   pmc                       PMC HBM traffic + MFMA/LDS counters (tools/gpu_pmc.sh, gpu_mfma_pmc.sh)
+#   pwpmc=<case>[/arm]        per-instance PMC of one pw_bench case ('+' for spaces), two arms (tools/gpu_pw_pmc.sh)
 #   py=<script>[+args]        any python tool under tools/ (limit 600 s)     -> <script>.txt
 set -o pipefail
 mkdir -p gpurun_out
@@ -81,6 +82,12 @@ for step in "$@"; do
       bash tools/gpu_pmc.sh || exit $?
       rm -rf gpurun_out/pmcf gpurun_out/pmcw
       bash tools/gpu_mfma_pmc.sh || exit $? ;;
+    pwpmc)
+      c=${arg%%/*}; arm="9=1"
+      [ "$c" != "$arg" ] && arm=${arg#*/}
+      c=${c//+/ }
+      timeout -k 10 900 bash tools/gpu_pw_pmc.sh "$c" "$arm" > gpurun_out/pw_pmc.txt 2>&1 || { tail -30 gpurun_out/pw_pmc.txt; exit 1; }
+      tail -12 gpurun_out/pw_pmc.txt ;;
     py)
       s=${arg%%+*}; rest=""
       [ "$s" != "$arg" ] && rest=${arg#*+}
