@@ -33,7 +33,9 @@ struct PwArgs {
   int y_bf16;  // FWD: Y is bf16 [b][M][P] (y_bs in elements)
   int gbf;     // FWD: ypre is bf16 and receives act'(pre);  DGRAD: gpre is a bf16 multiplier (no act')
   int gp_pref; // DGRAD with a 16-bit gp multiplier (SWP tiles): load gp before the K loop
-  int dma;     // host planner: the wide 16-bit-operand launch runs the LDS-DMA ring form (NS = 4)
+  int dma;     // host planner: the wide 16-bit-operand launch runs an LDS-DMA ring form: 1 = 256 x 256
+               // tiles (8 waves, 4 stages, one workgroup per CU), 2 = 256 x 128 tiles (4 waves, 3 stages,
+               // two workgroups per CU: one's epilogue runs beside the other's MFMAs)
   float* asum; // WGRAD (nullable): db[m] += sum_k A[m][k] -- the bias grad of the layer whose output
                // grad is A, from the staged A tiles (split partials after the S*M*N weight partials)
 };
@@ -819,7 +821,8 @@ static void pw_launch_abs(const PwArgs& g, int bm, int abf, int bbf, int splits,
     case 1: pw_launch<T16, MODE, 256, 0, 1, 256, 4, 64, SWP>(g, 1, st); break;              \
     case 2: pw_launch<T16, MODE, 256, 1, 0, 256, 4, 64, SWP>(g, 1, st); break;              \
     default:                                                                      \
-      if (g.dma) pw_launch<T16, MODE, 256, 1, 1, 256, 4, 32, SWP, 4>(g, 1, st);        \
+      if (g.dma == 2) pw_launch<T16, MODE, 256, 1, 1, 128, 2, 32, SWP, 3>(g, 1, st);   \
+      else if (g.dma) pw_launch<T16, MODE, 256, 1, 1, 256, 4, 32, SWP, 4>(g, 1, st);   \
       else pw_launch<T16, MODE, 256, 1, 1, 256, 4, 64, SWP>(g, 1, st);                 \
       break;                                                                      \
   }
@@ -988,7 +991,8 @@ void pw_wgrad_launch(const PwArgs& g, int bm, int abf, int bbf, int splits, hipS
     case 9: pw_launch<T16, PW_WGRAD, 256, 0, 1, 256, 4, 64>(g, splits, st); break;
     case 10: pw_launch<T16, PW_WGRAD, 256, 1, 0, 256, 4, 64>(g, splits, st); break;
     case 11:
-      if (g.dma) pw_launch<T16, PW_WGRAD, 256, 1, 1, 256, 4, 32, 0, 4>(g, splits, st);
+      if (g.dma == 2) pw_launch<T16, PW_WGRAD, 256, 1, 1, 128, 2, 32, 0, 3>(g, splits, st);
+      else if (g.dma) pw_launch<T16, PW_WGRAD, 256, 1, 1, 256, 4, 32, 0, 4>(g, splits, st);
       else pw_launch<T16, PW_WGRAD, 256, 1, 1, 256, 4, 64>(g, splits, st);
       break;
     case 0: pw_launch<T16, PW_WGRAD, 64, 0, 0>(g, splits, st); break;
