@@ -38,15 +38,19 @@ static void pw_fd_launch(int mode, const PwArgs& g, int bm, int abf, int bbf, in
 //   are gone, the keys are ignored), [6] gelu-pair forward tile (0 built-in,
 //   1 256 x 128, 2 128 x 128, 3 wide 256 x 256), [7] gp-multiplied data-grad tile (same codes),
 //   [8] gp loaded before the K loop (16-bit gp data-grads on 128 / 64-row tiles), [9] the LDS-DMA
-//   ring form of the wide 16-bit-operand launches (pw_impl.h NS > 0: 1 = 256 x 256 tiles, 4 stages;
-//   2 = 256 x 128 tiles, 3 stages, two workgroups per CU; 0 = off, until measured).
-static int g_tune[12] = {1, 512, 256, 4, 0, 0, 0, 0, 1, 0, 0, 0};
+//   ring form of the wide 16-bit-operand launches (pw_impl.h NS > 0): 1 = 256 x 256 tiles, 4 stages,
+//   FWD / DGRAD only (default: the gelu-pair forwards 271 -> 262 and 203 -> 186 us, the data-grads
+//   155 -> 149 and 138 -> 131 us, same bits; profiles/r04/pw_bench_dma.txt); 3 = the same plus the
+//   weight-grads (3-5 % slower there); 2 = 256 x 128 tiles, 3 stages, two workgroups per CU (slower:
+//   392 us for the 512-channel gelu-pair forward); 0 = register-staged everywhere.
+static int g_tune[12] = {1, 512, 256, 4, 0, 0, 0, 0, 1, 1, 0, 0};
 
 // the LDS-DMA ring form's conditions (full 256 x 256 tiles, 32-deep K steps, 16-byte pieces)
 static int dma_ok(const PwArgs& g, int bm, int abf, int bbf, int mode) {
   if (!g_tune[9] || bm != PW_WIDE || !abf || !bbf) return 0;
   if (!al16(g.A) || !al16(g.B) || (g.a_bs & 7) || (g.b_bs & 7) || g.M % 256) return 0;
-  const bool ok = mode == PW_WGRAD ? g.N % 256 == 0 && g.P % 32 == 0 && (g.k_split % 32) == 0
+  // (the weight-grads stay register-staged unless asked for: 3-5 % slower on the ring)
+  const bool ok = mode == PW_WGRAD ? g_tune[9] >= 3 && g.N % 256 == 0 && g.P % 32 == 0 && (g.k_split % 32) == 0
                                    : g.K % 32 == 0 && g.P % 256 == 0 && g.k_split == 0;
   return ok ? (g_tune[9] == 2 ? 2 : 1) : 0;
 }

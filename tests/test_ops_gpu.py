@@ -1322,7 +1322,7 @@ def test_mlp_bwd_c256_forms_bitwise(half, N, H):
 
 @pytest.mark.parametrize("half", HALVES)
 @pytest.mark.parametrize("form", ["fwd16", "fwd32", "fwd_gelu_pair", "dgrad32", "dgrad16", "wgrad"])
-@pytest.mark.parametrize("ring", [1, 2])
+@pytest.mark.parametrize("ring", [3, 2])
 def test_pw_wide_dma_ring_bitwise(half, form, ring):
     """The LDS-DMA ring form of the wide 16-bit-operand pointwise GEMMs (pw_impl.h NS = 4, planner
     knob dsgan_pw_tune(9)) against the register-staged wide kernel: the same MFMAs in the same order,
