@@ -956,6 +956,174 @@ __device__ __forceinline__ hx8<T16> tr_at(const T16* T, uint2 a, unsigned k_byte
 }
 
 // ------------------------------------------------------------------------------------------
+// backward with g / dz out at C = 256 (P = 128): the DMA form of mlp_bwd_kernel<.., GD, .., DMA>
+// with the addressing made cheap.  The chunk loop runs two chunks per iteration, one per weight
+// ring slot, so every LDS address is a per-lane base plus an XOR or immediate (swz_row_b,
+// swz_tr_b); the LDS-DMA sources of a chunk are per-lane offsets computed once plus the chunk's
+// uniform offset.  Same operands and sums in the same order: the same bits as mlp_bwd_kernel.
+// ------------------------------------------------------------------------------------------
+template <typename T16, int C, int P>
+__global__ __launch_bounds__(256, 1) void mlp_bwd_dma_kernel(MlpArgs g) {
+  typedef hx8<T16> mbf16x8;
+  typedef hx4<T16> mbf16x4;
+  constexpr int NW = 4, NT = 256, BN = 64, HC = 64;
+  constexpr int C4 = 4 * C, NCH = C4 / HC;
+  constexpr int HSTR = BN + 32;
+  constexpr int H_SZ = C * HSTR, D_SZ = P * HSTR, N_SZ = BN * HC, W1_SZ = HC * C, W2_SZ = P * HC;
+  constexpr int W_SZ = W1_SZ + W2_SZ;
+  static_assert(H_SZ + D_SZ >= W_SZ && NCH % 2 == 0 && (C / 8) % NW == 0 && (P / 8) % NW == 0, "shape");
+  __shared__ __attribute__((aligned(1024))) T16 smem[H_SZ + D_SZ + W_SZ + 2 * N_SZ + 2 * C4];
+  T16* const Hs = smem;
+  T16* const Ds = Hs + H_SZ;
+  T16* const Wslot0 = Ds + D_SZ;   // chunks 0, 2, 4, ...
+  T16* const Wslot1 = Hs;          // chunks 1, 3, ... (the h / dy staging area, once read)
+  T16* const Zn = Wslot0 + W_SZ;   // dz chunk, pixel-major [BN][HC]
+  T16* const Gn = Zn + N_SZ;       // g chunk
+  float* const b1s = reinterpret_cast<float*>(Gn + N_SZ);
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int lr = lane & 31, lh = lane >> 5;
+  const int tq = (lane >> 2) & 3, tp = lane & 3, tG = (lane >> 4) & 1;
+  const int wm = wave >> 1, wn = wave & 1;   // z / t: hidden half x pixel half; dh: channel half x pixel half
+
+  const int tpi = g.HW / BN;
+  const int tile = xcd_tile(blockIdx.x, gridDim.x);
+  const int img = tile / tpi, p0 = (tile - img * tpi) * BN;
+
+  // LDS-DMA sources of a weight chunk (glds_chunk<C, P, NW, false>'s pieces), chunk-invariant parts
+  constexpr int S1 = C / 8, R1 = 64 / S1, N1 = C / 8 / NW, N2 = P / 8 / NW;
+  const unsigned short* const w1 = (const unsigned short*)g.w1;
+  const unsigned short* const w2 = (const unsigned short*)g.w2;
+  unsigned o1[N1], o2[N2];
+#pragma unroll
+  for (int i = 0; i < N1; ++i) {
+    const int inst = wave * N1 + i, r = inst * R1 + lane / S1, ps = lane % S1;
+    o1[i] = (unsigned)(r * C + (ps ^ slot_swz<S1>(r)) * 8);
+  }
+#pragma unroll
+  for (int i = 0; i < N2; ++i) {
+    const int inst = wave * N2 + i, r = inst * 8 + lane / 8, ps = lane % 8;
+    o2[i] = (unsigned)(r * (4 * C) + (ps ^ slot_swz<8>(r)) * 8);
+  }
+  auto chunk_dma = [&](int j, T16* W1d) __attribute__((always_inline)) {
+    unsigned short* const W1h = (unsigned short*)W1d;
+    unsigned short* const W2h = W1h + W1_SZ;
+#pragma unroll
+    for (int i = 0; i < N1; ++i) glds16(w1 + ((unsigned)(j * 64 * C) + o1[i]), lds_addr(W1h + (wave * N1 + i) * 512));
+#pragma unroll
+    for (int i = 0; i < N2; ++i) glds16(w2 + ((unsigned)(j * 64) + o2[i]), lds_addr(W2h + (wave * N2 + i) * 512));
+  };
+
+  chunk_dma(0, Wslot0);
+  for (int i = tid; i < C4; i += NT) b1s[i] = g.b1[i];
+  stage_h<C, BN, HSTR, NT>(Hs, g, img, p0, tid);
+  stage_rows<P, BN, HSTR, NT>(Ds, g.dy + (long)img * g.dy_bs + p0, g.HW, tid);
+
+  mf32x16 hacc[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) hacc[i][r] = 0.f;
+  __syncthreads();
+  mbf16x8 hbr[C / 16], dbr[P / 16];
+#pragma unroll
+  for (int ks = 0; ks < C / 16; ++ks)
+    hbr[ks] = mtr_frag(Hs + (ks * 16 + 8 * lh + tq) * HSTR + wn * 32 + 16 * tG + 4 * tp, HSTR);
+#pragma unroll
+  for (int ks = 0; ks < P / 16; ++ks)
+    dbr[ks] = mtr_frag(Ds + (ks * 16 + 8 * lh + tq) * HSTR + wn * 32 + 16 * tG + 4 * tp, HSTR);
+
+  // per-lane LDS byte offsets (chunk-invariant)
+  const unsigned a_z = swz_row_b<C / 8>(wm * 32 + lr, lh);          // W1 rows (z)
+  const uint2 a_t = swz_tr_b<HC / 8>(wm * 32, lane);                 // W2 transposed (t)
+  uint2 a_d[4];                                                      // W1 transposed (dh)
+#pragma unroll
+  for (int i = 0; i < 4; ++i) a_d[i] = swz_tr_b<C / 8>(wm * (C / 2) + i * 32, lane);
+  const unsigned a_n = swz_row_b<HC / 8>(wn * 32 + lr, lh);         // Zn rows (dh B operand)
+  const int chh = (wave & 1) * 32;                                   // copy-out hidden half
+  const uint2 a_c = swz_tr_b<HC / 8>(chh, lane);                     // Gn / Zn transposed (copy-out)
+  const unsigned a_e = (unsigned)((wn * 32 + lr) * HC * 2 + (((wm * 4) ^ slot_swz<HC / 8>(wn * 32 + lr)) << 4) + 8 * lh);
+  const long gbase = (long)img * C4 * g.HW + p0;
+
+  auto chunk = [&](int j, const T16* W1s, T16* Wnext) __attribute__((always_inline)) {
+    // chunk j landed (this wave's pieces: the only LDS-DMA in flight) and every wave is done with
+    // chunk j-1 (its ring slot, Zn / Gn; at j = 0 the h / dy staging area = slot 1)
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (j + 1 < NCH) chunk_dma(j + 1, Wnext);
+    const T16* W2s = W1s + W1_SZ;
+    mf32x16 zacc, tacc;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float4 b4 = *reinterpret_cast<const float4*>(b1s + j * HC + wm * 32 + 8 * q + 4 * lh);
+      zacc[4 * q] = b4.x; zacc[4 * q + 1] = b4.y; zacc[4 * q + 2] = b4.z; zacc[4 * q + 3] = b4.w;
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) tacc[r] = 0.f;
+#pragma unroll
+    for (int ks = 0; ks < C / 16; ++ks)
+      zacc = mfma16(*reinterpret_cast<const mbf16x8*>((const char*)W1s + (a_z ^ (unsigned)(32 * ks))), hbr[ks], zacc);
+#pragma unroll
+    for (int ks = 0; ks < P / 16; ++ks) tacc = mfma16(tr_at(W2s, a_t, ks * 16 * HC * 2), dbr[ks], tacc);
+    // g = gelu(z), dz = t gelu'(z) -> LDS, pixel-major, 4 hidden per write
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      mbf16x4 gv4, dv4;
+#pragma unroll
+      for (int e = 0; e < 4; e += 2) {
+        f32x2 gv, gp;
+        gelu_pair_fast2(f32x2{zacc[4 * q + e], zacc[4 * q + e + 1]}, gv, gp);
+        const f32x2 dz = f32x2{tacc[4 * q + e], tacc[4 * q + e + 1]} * gp;
+        gv4[e] = (T16)gv.x; gv4[e + 1] = (T16)gv.y;
+        dv4[e] = (T16)dz.x; dv4[e + 1] = (T16)dz.y;
+      }
+      const unsigned o = a_e ^ (unsigned)(16 * q);
+      *reinterpret_cast<mbf16x4*>((char*)Gn + o) = gv4;
+      *reinterpret_cast<mbf16x4*>((char*)Zn + o) = dv4;
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // raw barrier: chunk j+1's DMA stays in flight
+    __builtin_amdgcn_s_barrier();
+    // copy-out: 8 pixels of one hidden row per lane -> 16-byte stores; dz sums per 32 pixels
+    {
+      float bacc = 0.f;
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        const int pb = ((wave >> 1) * 2 + c) * 16;
+        const mbf16x8 gv = tr_at(Gn, a_c, pb * HC * 2);
+        const mbf16x8 dv = tr_at(Zn, a_c, pb * HC * 2);
+        const long o = gbase + (long)(j * HC + chh + lr) * g.HW + pb + 8 * lh;
+        *reinterpret_cast<mbf16x8*>((T16*)g.g_out + o) = gv;
+        *reinterpret_cast<mbf16x8*>((T16*)g.dz_out + o) = dv;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) bacc += (float)dv[e];
+      }
+      bacc += __shfl_xor(bacc, 32, 64);
+      if (lh == 0 && g.bsum) g.bsum[((long)tile * (NW / 2) + (wave >> 1)) * C4 + j * HC + chh + lr] = bacc;
+    }
+    // dh += W1[chunk]^T dz
+#pragma unroll
+    for (int ks = 0; ks < HC / 16; ++ks) {
+      const mbf16x8 bf = *reinterpret_cast<const mbf16x8*>((const char*)Zn + (a_n ^ (unsigned)(32 * ks)));
+#pragma unroll
+      for (int i = 0; i < 4; ++i) hacc[i] = mfma16(tr_at(W1s, a_d[i], ks * 16 * C * 2), bf, hacc[i]);
+    }
+  };
+  for (int j = 0; j < NCH; j += 2) {
+    chunk(j, Wslot0, Wslot1);
+    chunk(j + 1, Wslot1, Wslot0);
+  }
+
+  float* ob = g.out + (long)img * g.out_bs + p0 + wn * 32 + lr;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int c = wm * (C / 2) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+      ob[(long)c * g.HW] = hacc[i][r];
+    }
+}
+
+// ------------------------------------------------------------------------------------------
 // backward (weight path): dW1 = dz h^T, dW2 = dy g^T, db1 = sum dz -- without g / dz in HBM.
 // Workgroup (hidden chunk j, pixel split s) holds chunk j's W1 rows / W2 columns in LDS for its
 // whole life and walks pixel tiles s, s+S, ...: per tile it recomputes z = W1[j] h + b1 and
@@ -1292,8 +1460,9 @@ static void fwd_launch(const MlpArgs& g, hipStream_t st) {
 // granularity: one partial row per 32 pixels)
 // Planner knob (measurement tools): key 0 = the C = 256 backward with g / dz out, 0 the LDS-DMA
 // weight ring (default: 0.831 -> 0.717 ms at uc3, B = 16, same bits; profiles/r04/mlp_micro.txt),
-// 1 the register-staged weights.  (An 8-wave form -- two waves per SIMD, 128-row hidden chunks --
-// measured 0.977 ms: at 256 registers it spills, and it issues more VALU per MFMA.)
+// 1 the register-staged weights, 2 the DMA ring with precomputed LDS / DMA addresses
+// (mlp_bwd_dma_kernel).  (An 8-wave form -- two waves per SIMD, 128-row hidden chunks -- measured
+// 0.977 ms: at 256 registers it spills, and it issues more VALU per MFMA.)
 static int g_mlp_tune[4] = {0, 0, 0, 0};
 
 template <typename T16, int C, int P, int BN, int NW, bool GD = true, int MINB = 1, bool DMA = false>
@@ -1383,6 +1552,9 @@ int dsgan_mlp_bwd(const void* h, long h_bs, int h_bf16, const float* dy, long dy
     } else if (C == 64) bwd_launch<T16, 64, 128, 128, 8>(g, st);
     else if (C == 128 && P == 64) bwd_launch<T16, 128, 64, 128, 8>(g, st);
     else if (C == 128) bwd_launch<T16, 128, 256, 64, 4>(g, st);
+    else if (g_mlp_tune[0] == 2 && P == 128)
+      hipLaunchKernelGGL((mlp_bwd_dma_kernel<T16, 256, 128>), dim3((unsigned)((long)g.nb * (g.HW / 64))), dim3(256), 0,
+                         st, g);
     else if (g_mlp_tune[0] == 0) bwd_launch<T16, 256, 128, 64, 4, true, 1, true>(g, st);
     else bwd_launch<T16, 256, 128, 64, 4>(g, st);
   });
@@ -1429,7 +1601,8 @@ int dsgan_mlp_wgrad(const void* h, long h_bs, int h_bf16, const float* dy, long 
 }
 
 // planner knob `key` <- val (val < 0: read only), returns the previous value (measurement tools):
-// key 0 = the C = 256 backward with g / dz out: 0 LDS-DMA weight ring, 1 register-staged weights
+// key 0 = the C = 256 backward with g / dz out: 0 LDS-DMA weight ring, 1 register-staged weights,
+// 2 the ring with precomputed addresses
 int dsgan_mlp_tune(int key, int val) {
   if (key < 0 || key >= 4) return -1;
   const int old = g_mlp_tune[key];

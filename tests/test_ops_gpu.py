@@ -1276,8 +1276,8 @@ def test_loss_scaler_state_machine(n):
 @pytest.mark.parametrize("half", HALVES)
 @pytest.mark.parametrize("N,H", [(2, 16), (3, 32)])
 def test_mlp_bwd_c256_forms_bitwise(half, N, H):
-    """The two forms of the C = 256 MLP backward with g / dz out (mlp.hip: register-staged weights,
-    LDS-DMA weight ring; dsgan_mlp_tune key 0) give the same bits for dh, g, dz and the per-32-pixel
+    """The three forms of the C = 256 MLP backward with g / dz out (mlp.hip: register-staged weights,
+    LDS-DMA weight ring, the ring with precomputed addresses; dsgan_mlp_tune key 0) give the same bits for dh, g, dz and the per-32-pixel
     dz sums -- and dh matches the fp32 chain within the 16-bit bar."""
     import dsgan_hip
     from dsgan_hip import _lib
@@ -1296,7 +1296,7 @@ def test_mlp_bwd_c256_forms_bitwise(half, N, H):
     old = lib.dsgan_mlp_tune(0, -1)
     outs = {}
     try:
-        for mode in (1, 0):
+        for mode in (1, 0, 2):
             lib.dsgan_mlp_tune(0, mode)
             dh = torch.full((N, C, HW), float("nan"), device=DEV)
             gg = torch.empty(N, C4, HW, device=DEV, dtype=hd)
@@ -1308,8 +1308,9 @@ def test_mlp_bwd_c256_forms_bitwise(half, N, H):
             outs[mode] = (dh, gg, dz, bs)
     finally:
         lib.dsgan_mlp_tune(0, old)
-    for a, b in zip(outs[0], outs[1]):
-        assert torch.equal(a, b)
+    for mode in (0, 2):
+        for a, b in zip(outs[mode], outs[1]):
+            assert torch.equal(a, b), mode
     # value check of dh against the fp32 chain on the same 16-bit operands
     hf, w1f, w2f = h.float(), w1.float(), w2.float()
     z = torch.einsum("kc,nch->nkh", w1f, hf) + b1[None, :, None]

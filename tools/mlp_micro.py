@@ -59,19 +59,21 @@ for name, C, P, H in SHAPES:
     f(); bd(); wg(); torch.cuda.synchronize()
     cs = (out.double().sum().item(), dh.double().sum().item(), gw1.double().abs().sum().item(),
           gw2.double().abs().sum().item(), gb1.double().abs().sum().item())
-    # knob A/B of the backward with g / dz out (dsgan_mlp_tune key 0: 0 LDS-DMA ring, 1 register-staged)
+    # knob A/B of the backward with g / dz out (dsgan_mlp_tune key 0: 0 LDS-DMA ring, 1 register-staged,
+    # 2 the ring with precomputed addresses)
     ab = ""
     if C == 256:
         old = lib.dsgan_mlp_tune(0, -1)
         res = {}
-        for mode in (1, 0):
+        for mode in (1, 0, 2):
             lib.dsgan_mlp_tune(0, mode)
             t = timeit(bg)
             bg(); torch.cuda.synchronize()
             res[mode] = (t, dh.clone(), g.clone(), dz.clone())
         lib.dsgan_mlp_tune(0, old)
-        same = all(torch.equal(a, b) for a, b in zip(res[0][1:], res[1][1:]))
-        ab = " | bwd-g/dz staged %.3f dma %.3f ms (bitwise %s)" % (res[1][0], res[0][0], same)
+        same = [all(torch.equal(a, b) for a, b in zip(res[m][1:], res[1][1:])) for m in (0, 2)]
+        ab = " | bwd-g/dz staged %.3f dma %.3f (bitwise %s) dma-addr %.3f ms (bitwise %s)" % (
+            res[1][0], res[0][0], same[0], res[2][0], same[1])
     fl = 2.0 * N * HW * (C4 * C + C4 * P)
     print("%-4s C=%4d P=%4d HW=%6d | fwd %.3f ms (%.0f TF/s) | bwd-dh %.3f | wgrad %.3f | bwd-g/dz %.3f ms | cs %s%s"
           % (name, C, P, HW, tf, fl / tf / 1e9, tbd, twg, tbg, " ".join("%.6e" % c for c in cs), ab), flush=True)
