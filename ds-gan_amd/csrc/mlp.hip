@@ -1459,11 +1459,11 @@ static void fwd_launch(const MlpArgs& g, hipStream_t st) {
 // backward: 8 waves x 128 pixels where the LDS tiles fit, else 4 waves x 64 pixels (same bsum
 // granularity: one partial row per 32 pixels)
 // Planner knob (measurement tools): key 0 = the C = 256 backward with g / dz out, 0 the LDS-DMA
-// weight ring (default: 0.831 -> 0.717 ms at uc3, B = 16, same bits; profiles/r04/mlp_micro.txt),
-// 1 the register-staged weights, 2 the DMA ring with precomputed LDS / DMA addresses
-// (mlp_bwd_dma_kernel).  (An 8-wave form -- two waves per SIMD, 128-row hidden chunks -- measured
+// weight ring (0.831 -> 0.717 ms at uc3, B = 16, same bits; profiles/r04/mlp_micro.txt), 1 the
+// register-staged weights, 2 the DMA ring with precomputed LDS / DMA addresses (mlp_bwd_dma_kernel,
+// default: 0.733 -> 0.704 ms, same bits; profiles/r04/mlp_micro_b.txt).  (An 8-wave form -- two waves per SIMD, 128-row hidden chunks -- measured
 // 0.977 ms: at 256 registers it spills, and it issues more VALU per MFMA.)
-static int g_mlp_tune[4] = {0, 0, 0, 0};
+static int g_mlp_tune[4] = {2, 0, 0, 0};
 
 template <typename T16, int C, int P, int BN, int NW, bool GD = true, int MINB = 1, bool DMA = false>
 static void bwd_launch(const MlpArgs& g, hipStream_t st) {

@@ -170,7 +170,8 @@ int dsgan_mlp_wgrad(const void* h, long h_bs, int h_bf16, const float* dy, long 
                     const float* b1, const void* w2, float* dw1, float* db1, float* dw2, float* ws, long ws_elems,
                     int nb, int C, int P, int HW, hipStream_t stream);
 /* planner knob `key` <- val (val < 0: read only), returns the previous value (measurement tools):
- * key 0 = the C = 256 backward with g / dz out, 0 LDS-DMA weight ring (default), 1 register-staged */
+ * key 0 = the C = 256 backward with g / dz out, 0 LDS-DMA weight ring, 1 register-staged, 2 the ring with
+ *         precomputed addresses (default) */
 int dsgan_mlp_tune(int key, int val);
 /* out[c] += sum_r part[r][c], rows added in a fixed order (deterministic); part is scratch and
  * is overwritten (in-place pre-reduction of many rows). */
