@@ -209,30 +209,26 @@ __global__ __launch_bounds__(256, 2) void vconv3x3_kernel(VcArgs<T16> g) {
 // image lane-linear in [half][ph][pw] order as in vconv3x3_kernel.  Per tap the next tap's A / B
 // fragments are read while this tap's MFMAs issue.  Arithmetic (operand values, accumulation order
 // per output: chunks in order, taps in order within a chunk) is vconv3x3_kernel's: same bits.
-// NWV = 4 (the "wide wave" form): 4 waves, one per SIMD, each owning ALL BM rows x a quarter of the
-// pixels -- 4 x 4 MFMA tiles per wave, so a tap's 8 fragment reads feed 16 MFMAs (0.5 per MFMA, vs
-// 0.75 for 8 waves of 2 x 4): the 8-wave form's LDS reads run at ~75 % of the LDS bandwidth.
-template <typename T16, int BM, int TH, int NWV = 8>
-__global__ __launch_bounds__(NWV * 64, 1) void vconv3x3_dma_kernel(VcArgs<T16> g) {
+template <typename T16, int BM, int TH>
+__global__ __launch_bounds__(512, 1) void vconv3x3_dma_kernel(VcArgs<T16> g) {
   typedef hx8<T16> vgb8;
   typedef hx4<T16> vgb4;
   constexpr int TW = 32, BN = TH * TW;
-  constexpr int WM = NWV == 8 ? BM / 64 : 1, WN = NWV / WM;   // waves along M and N
-  constexpr int TM = BM / WM / 32, TN = BN / WN / 32;         // 32x32 MFMA tiles per wave
+  constexpr int WM = BM / 64, WN = 8 / WM;           // waves along M (64 rows each) and N
+  constexpr int TM = 2, TN = BN / WN / 32;           // 32x32 MFMA tiles per wave
   constexpr int PH = TH + 2, PW = TW + 2;
   constexpr int A_BYTES = 9 * 2 * BM * 16;           // weight image of one K chunk (1 KB multiple)
   constexpr int B_SLOTS = 2 * PH * PW;               // 16-byte patch slots [half][ph][pw]
   constexpr int B_PIECES = (B_SLOTS + 63) / 64;      // 1 KB LDS-DMA pieces (the tail slots read zeros)
   constexpr int STAGE = A_BYTES + B_PIECES * 1024;
   constexpr int A_PIECES = A_BYTES / 1024;
-  constexpr int NBW = (B_PIECES + NWV - 1) / NWV;    // patch pieces per wave (at most)
+  constexpr int NBW = (B_PIECES + 7) / 8;            // patch pieces per wave (at most)
   static_assert(TN >= 1 && A_BYTES % 1024 == 0 && 2 * STAGE <= 160 * 1024, "tile");
   __shared__ __attribute__((aligned(16))) vgu4 smem[2 * STAGE / 16];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave / WN, wn = wave % WN;
   const int lr = lane & 31, lh = lane >> 5;
-  static_assert(TM * WM * 32 == BM && TN * WN * 32 == BN, "wave grid");
 
   const int npt = g.N * g.tiles_w * g.tiles_h;
   int tile;
@@ -252,7 +248,7 @@ __global__ __launch_bounds__(NWV * 64, 1) void vconv3x3_dma_kernel(VcArgs<T16> g
   int boff[NBW];
 #pragma unroll
   for (int q = 0; q < NBW; ++q) {
-    const int s = (wave + NWV * q) * 64 + lane;
+    const int s = (wave + 8 * q) * 64 + lane;
     int off = -1;
     if (s < B_SLOTS) {
       const int half = s / (PH * PW), rem = s - half * (PH * PW);
@@ -268,12 +264,12 @@ __global__ __launch_bounds__(NWV * 64, 1) void vconv3x3_dma_kernel(VcArgs<T16> g
     const unsigned ls = lbase + stage * STAGE;
     const char* a = wsrc + (long)kc * A_BYTES + lane * 16;
 #pragma unroll
-    for (int p0 = 0; p0 < A_PIECES; p0 += NWV)
+    for (int p0 = 0; p0 < A_PIECES; p0 += 8)
       if (p0 + wave < A_PIECES) dma16(a + (p0 + wave) * 1024, ls + (p0 + wave) * 1024);
     const T16* xb = g.X + ((long)img * nkc + kc) * plane;
 #pragma unroll
     for (int q = 0; q < NBW; ++q) {
-      const int p = wave + NWV * q;
+      const int p = wave + 8 * q;
       if (p < B_PIECES)
         dma16(boff[q] >= 0 ? (const void*)(xb + boff[q]) : g.zero, ls + A_BYTES + p * 1024);
     }
@@ -300,7 +296,7 @@ __global__ __launch_bounds__(NWV * 64, 1) void vconv3x3_dma_kernel(VcArgs<T16> g
       const int kh = tap / 3, kw = tap - (tap / 3) * 3;
 #pragma unroll
       for (int i = 0; i < TM; ++i)
-        af[b][i] = *reinterpret_cast<const vgb8*>(Ab + ((tap * 2 + lh) * BM + wm * (TM * 32) + i * 32 + lr) * 8);
+        af[b][i] = *reinterpret_cast<const vgb8*>(Ab + ((tap * 2 + lh) * BM + wm * 64 + i * 32 + lr) * 8);
 #pragma unroll
       for (int j = 0; j < TN; ++j)
         bfr[b][j] = *reinterpret_cast<const vgb8*>(Bb + ((lh * PH + wn * TN + j + kh) * PW + lr + kw) * 8);
@@ -326,7 +322,7 @@ __global__ __launch_bounds__(NWV * 64, 1) void vconv3x3_dma_kernel(VcArgs<T16> g
     for (int i = 0; i < TM; ++i)
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const int m = m_t * BM + wm * (TM * 32) + i * 32 + q * 8 + 4 * lh;
+        const int m = m_t * BM + wm * 64 + i * 32 + q * 8 + 4 * lh;
         float v[4];
 #pragma unroll
         for (int e = 0; e < 4; ++e) v[e] = acc[i][j][4 * q + e];
@@ -649,20 +645,19 @@ static const void* vc_zero() {
   return zero;
 }
 
-template <typename T16, int BM, int TH, int NWV = 8>
+template <typename T16, int BM, int TH>
 static void vc_launch_dma(VcArgs<T16>& g, hipStream_t st) {
   g.tiles_w = g.W / 32;
   g.tiles_h = g.H / TH;
   const long tiles = (long)g.N * g.tiles_w * g.tiles_h * (g.M / BM);
-  hipLaunchKernelGGL((vconv3x3_dma_kernel<T16, BM, TH, NWV>), dim3((unsigned)tiles), dim3(NWV * 64), 0, st, g);
+  hipLaunchKernelGGL((vconv3x3_dma_kernel<T16, BM, TH>), dim3((unsigned)tiles), dim3(512), 0, st, g);
 }
 
 static int vc_bm(int M) { return (M % 128 == 0) ? 128 : 64; }
 
 // Planner knob (measurement tools): 0 = the LDS-DMA ring kernel where a launch fills the chip
 // (default: the step's 14 VGG launches 1014 -> 936 us at B = 16, same bits;
-// profiles/r04/vconv_micro.txt), 1 = always the register-staged kernel, 2 = the ring with 4 waves of
-// 4 x 4 MFMA tiles for the 128-row M tiles (NWV = 4).
+// profiles/r04/vconv_micro.txt), 1 = always the register-staged kernel.
 static int g_vc_mode = 0;
 
 }  // namespace dsg
@@ -676,8 +671,7 @@ int dsgan_vconv_supported(int K, int M, int H, int W) {
 }
 
 // planner knob `key` <- val (val < 0: read only), returns the previous value (measurement tools):
-// key 0 = kernel form (0 LDS-DMA ring where it fills the chip, 1 register-staged, 2 the ring's 4-wave
-// wide-wave form for 128-channel M tiles)
+// key 0 = kernel form (0 LDS-DMA ring where it fills the chip, 1 register-staged)
 int dsgan_vconv_tune(int key, int val) {
   if (key != 0) return -1;
   const int old = g_vc_mode;
@@ -722,11 +716,9 @@ int dsgan_vconv3x3(const void* X, const void* Wt, const float* bias, const void*
     // workgroup per CU, else 8-row ones
     const long pt16 = H % 16 == 0 ? (long)N * (W / 32) * (H / 16) * (M / BM) : 0;
     const long pt8 = H % 8 == 0 ? (long)N * (W / 32) * (H / 8) * (M / BM) : 0;
-    g.zero = g_vc_mode != 1 && (pt16 >= 256 || pt8 >= 256) ? vc_zero() : nullptr;
+    g.zero = g_vc_mode == 0 && (pt16 >= 256 || pt8 >= 256) ? vc_zero() : nullptr;
     if (g.zero) {
-      if (BM == 128 && g_vc_mode == 2) {   // wide-wave form (4 waves x 4 x 4 tiles)
-        if (pt16 >= 256) vc_launch_dma<T16, 128, 16, 4>(g, st); else vc_launch_dma<T16, 128, 8, 4>(g, st);
-      } else if (BM == 128) {
+      if (BM == 128) {
         if (pt16 >= 256) vc_launch_dma<T16, 128, 16>(g, st); else vc_launch_dma<T16, 128, 8>(g, st);
       } else {
         if (pt16 >= 256) vc_launch_dma<T16, 64, 16>(g, st); else vc_launch_dma<T16, 64, 8>(g, st);
