@@ -657,7 +657,9 @@ static int vc_bm(int M) { return (M % 128 == 0) ? 128 : 64; }
 
 // Planner knob (measurement tools): 0 = the LDS-DMA ring kernel where a launch fills the chip
 // (default: the step's 14 VGG launches 1014 -> 936 us at B = 16, same bits;
-// profiles/r04/vconv_micro.txt), 1 = always the register-staged kernel.
+// profiles/r04/vconv_micro.txt), 1 = always the register-staged kernel.  (A 4-wave form, one wave
+// per SIMD owning 4 x 4 MFMA tiles -- half the fragment reads per MFMA -- measured 1103 us against
+// the 8-wave ring's 957 over the same launches: profiles/r04/vconv_micro_4wave.txt.)
 static int g_vc_mode = 0;
 
 }  // namespace dsg
