@@ -118,11 +118,29 @@ class Pix2PixModel(BaseModel):
             self.mean_w = 1.0   # world * n_rank / n_global, set per batch by set_input
             self._vgg_stream = torch.cuda.Stream(self.device)
             self._real_feats = None
+            self._feats_joined = False
+            # the step as two captured HIP graphs (see _graph_step): one process, optimizer step counts
+            # on the device (the fp16 scalers or the bf16 guard), no RCCL exchange inside the step
+            cg = int(getattr(opt, "cuda_graph", -1))
+            can = W == 1 and self.scaler_G is not None
+            if cg == 1 and not can:
+                raise ValueError("--cuda_graph 1 needs one process and device-side step counts "
+                                 "(--precision fp16, or bf16 with the non-finite guard)")
+            self.cuda_graph = can and cg != 0
+            self._graphs = None
+            self._graph_key = None
+            self._graph_warm = False
 
     def set_input(self, input):
         AtoB = self.opt.which_direction == "AtoB"
-        self.real_A = input["A" if AtoB else "B"].to(self.device, non_blocking=True)
-        self.real_B = input["B" if AtoB else "A"].to(self.device, non_blocking=True)
+        A = input["A" if AtoB else "B"].to(self.device, non_blocking=True)
+        B = input["B" if AtoB else "A"].to(self.device, non_blocking=True)
+        if self._graphs is not None and A.shape == self._static_A.shape and B.shape == self._static_B.shape:
+            # captured graphs read the static input buffers
+            self._static_A.copy_(A, non_blocking=True)
+            self._static_B.copy_(B, non_blocking=True)
+            A, B = self._static_A, self._static_B
+        self.real_A, self.real_B = A, B
         self.image_paths = input["A_paths" if AtoB else "B_paths"]
         if self.isTrain:
             W = hdist.world_size()
@@ -132,8 +150,10 @@ class Pix2PixModel(BaseModel):
     def forward(self):
         self.fake_B = self.netG(self.real_A)
 
-    def backward_D(self):
-        if self.use_condition == 1:
+    def backward_D(self, fake_AB=None):
+        if fake_AB is not None:   # (the graph step: the pool's output, queried between the two graphs)
+            pass
+        elif self.use_condition == 1:
             fake_AB = self.fake_AB_pool.query(HF.cat_channels(self.real_A, self.fake_B.detach()))
         else:
             fake_AB = self.fake_B
@@ -206,17 +226,73 @@ class Pix2PixModel(BaseModel):
     def _take_real_features(self):
         if self._real_feats is None:
             self._launch_real_features()
-        torch.cuda.current_stream(self.device).wait_stream(self._vgg_stream)
+        if not self._feats_joined:   # (the graph step joined the side stream inside its first graph)
+            torch.cuda.current_stream(self.device).wait_stream(self._vgg_stream)
         feats, self._real_feats = self._real_feats, None
         return feats
 
     def optimize_parameters(self):
+        if self.cuda_graph and not self.exchange and self.g_buckets is None:
+            return self._graph_step()
         self._launch_real_features()
         self.forward()
+        self._d_and_g_steps()
+
+    # ---- the step as two HIP graphs ----
+    # ~760 kernel launches per step leave ~1 ms/step of dispatch gaps between them.  Replayed from
+    # graphs they go back to back.  The ImagePool query draws python `random` per image
+    # (DSGAN/util/image_pool.py:17-31), so the step is split around it: graph A = the VGG16
+    # real-feature pass (side stream, joined inside A) + G forward + cat(real_A, fake_B); the pool
+    # query runs eagerly into a static buffer (the same draws, in the same order, as the reference);
+    # graph B = the D step and the G step (backward, scaler checks, both Adams).  Everything a replay
+    # needs from the host is fixed at capture: shapes, loss weights, the learning rates (a change
+    # re-captures) and the Adam step counts (device-side under the scalers / guard).
+    def _graph_step(self):
+        key = (tuple(self.real_A.shape), tuple(self.real_B.shape), self.mean_w,
+               tuple(float(o.param_groups[0]["lr"]) for o in self.optimizers))
+        if self._graphs is None or key != self._graph_key:
+            if not self._graph_warm:   # one eager step first (lazy allocations, cached weight copies)
+                self._graph_warm = True
+                self._launch_real_features()
+                self.forward()
+                self._d_and_g_steps()
+                return
+            self._capture(key)
+        gA, gB = self._graphs
+        gA.replay()
+        if self.use_gan == 1 and self.use_condition == 1:
+            self.fake_AB_pool.query(self._cat_fake, out=self._fake_AB_buf)
+        gB.replay()
+
+    def _capture(self, key):
+        self._graphs = None
+        self._static_A = self.real_A.clone()
+        self._static_B = self.real_B.clone()
+        self.real_A, self.real_B = self._static_A, self._static_B
+        torch.cuda.synchronize(self.device)
+        pool = torch.cuda.graph_pool_handle()
+        gA, gB = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+        cond = self.use_gan == 1 and self.use_condition == 1
+        with torch.cuda.graph(gA, pool=pool):
+            self._launch_real_features()
+            self.forward()
+            if cond:
+                self._cat_fake = HF.cat_channels(self.real_A, self.fake_B.detach())
+                self._fake_AB_buf = torch.empty_like(self._cat_fake)
+            torch.cuda.current_stream(self.device).wait_stream(self._vgg_stream)
+            self._feats_joined = True
+        try:
+            with torch.cuda.graph(gB, pool=pool):
+                self._d_and_g_steps(self._fake_AB_buf if cond else None)
+        finally:
+            self._feats_joined = False
+        self._graphs, self._graph_key = (gA, gB), key
+
+    def _d_and_g_steps(self, fake_AB=None):
         if self.use_gan == 1:
             self.set_requires_grad(self.netD, True)
             self.optimizer_D.zero_grad()
-            self.backward_D()
+            self.backward_D(fake_AB)
             if self.exchange:
                 hdist.allreduce_mean_(self.flatD.grad, force=True)
             if self.scaler_D is not None:

@@ -33,6 +33,9 @@ class TrainOptions(BaseOptions):
         # step; a non-finite gradient skips that optimizer step (parameters and moments untouched)
         # instead of writing NaN into the weights.  -1 = on for --precision bf16 (fp16 always has it
         # through its loss scaler), off for the fp32 parity mode.
+        parser.add_argument("--cuda_graph", type=int, default=-1, choices=[-1, 0, 1],
+                            help="replay optimize_parameters as two captured HIP graphs around the ImagePool "
+                                 "query (-1: on for one process with device-side loss scaling / guard)")
         parser.add_argument("--nonfinite_guard", type=int, default=-1, choices=[-1, 0, 1],
                             help="skip an optimizer step whose gradient has inf/nan (-1: on for bf16)")
         self.isTrain = True

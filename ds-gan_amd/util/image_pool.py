@@ -28,8 +28,13 @@ class ImagePool:
         """The stored images, reference order (views of the resident pool)."""
         return [self.store[i:i + 1] for i in range(self.num_imgs)] if self.pool_size > 0 and self.store is not None else []
 
-    def query(self, images):
+    def query(self, images, out=None):
+        """The reference's query; ``out`` (optional, images' shape): the result is written there (the
+        CUDA-graph step's static buffer between its two captured halves)."""
         if self.pool_size == 0:
+            if out is not None:
+                out.copy_(images)
+                return out
             return images
         images = images.detach().contiguous()
         if self.store is not None and (self.store.shape[1:] != images.shape[1:] or self.store.dtype != images.dtype
@@ -59,7 +64,8 @@ class ImagePool:
                     cur[random_id] = ("in", i)
                 else:
                     src_of_out.append(("in", i))
-        out = torch.empty_like(images)
+        if out is None:
+            out = torch.empty_like(images)
 
         def t(src):
             return images[src[1]] if src[0] == "in" else self.store[src[1]]

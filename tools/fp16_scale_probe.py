@@ -25,7 +25,7 @@ def main():
     for e in (16, 14, 12, 10, 8, 6):
         random.seed(20)
         torch.manual_seed(20)
-        m = create_model(default_train_opt(gpu_ids=[0], pool_size=0, precision="fp16", batchSize=batch))
+        m = create_model(default_train_opt(gpu_ids=[0], pool_size=0, precision="fp16", batchSize=batch, cuda_graph=0))
         with torch.no_grad():
             for net, pr in ((m.netG, make_params(O.g_param_spec(), "ref", 1000)),
                             (m.netD, make_params(O.d_param_spec(), "ref", 5000)),

@@ -10,7 +10,7 @@ from oracle.recipe import synth_pair
 
 prec = sys.argv[1] if len(sys.argv) > 1 else "bf16"
 B = int(sys.argv[2]) if len(sys.argv) > 2 else 16
-opt = default_train_opt(gpu_ids=[0], precision=prec)
+opt = default_train_opt(gpu_ids=[0], precision=prec, cuda_graph=0)
 m = create_model(opt)
 A, Bi = synth_pair(B, 256, 0)
 m.set_input({"A": A.cuda(), "B": Bi.cuda(), "A_paths": [""] * B, "B_paths": [""] * B})

@@ -22,7 +22,7 @@ def main():
     from models import create_model
     from oracle.recipe import synth_pair
     torch.manual_seed(20)
-    m = create_model(default_train_opt(gpu_ids=[0], precision="bf16", batchSize=a.batch))
+    m = create_model(default_train_opt(gpu_ids=[0], precision="bf16", batchSize=a.batch, cuda_graph=0))
     A, B = synth_pair(a.batch, a.size, seed=0)
     m.set_input({"A": A.cuda(), "B": B.cuda(), "A_paths": [""] * a.batch, "B_paths": [""] * a.batch})
     for _ in range(3):

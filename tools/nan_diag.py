@@ -113,7 +113,7 @@ def run_arm(arm, base_trace):
     random.seed(20)
     torch.manual_seed(20)
     opt = default_train_opt(gpu_ids=[0], pool_size=0, precision="bf16", batchSize=16,
-                            nonfinite_guard=1 if "guard" in arm else 0)
+                            nonfinite_guard=1 if "guard" in arm else 0, cuda_graph=0)
     model = create_model(opt)
     gp = make_params(O.g_param_spec(), "ref", 1000)
     dp = make_params(O.d_param_spec(), "ref", 5000)

@@ -53,7 +53,7 @@ def run(base, fp32_parts=()):
     base = "bf16" if base == "bf16-nopin" else base
     random.seed(20)
     torch.manual_seed(20)
-    model = create_model(default_train_opt(gpu_ids=[0], pool_size=0, precision=base, batchSize=batch))
+    model = create_model(default_train_opt(gpu_ids=[0], pool_size=0, precision=base, batchSize=batch, cuda_graph=0))
     with torch.no_grad():
         for net, pr in ((model.netG, gp), (model.netD, dp), (model.vgg, vp_full)):
             for k, v in net.state_dict().items():
