@@ -209,7 +209,11 @@ __global__ __launch_bounds__(256, 2) void vconv3x3_kernel(VcArgs<T16> g) {
 // image lane-linear in [half][ph][pw] order as in vconv3x3_kernel.  Per tap the next tap's A / B
 // fragments are read while this tap's MFMAs issue.  Arithmetic (operand values, accumulation order
 // per output: chunks in order, taps in order within a chunk) is vconv3x3_kernel's: same bits.
-template <typename T16, int BM, int TH>
+// KWM: taps in kw-major order so that one kw's B fragments serve all three kh: per kw the TN + 2
+// patch rows are read once (TN + 2 row fragments instead of 3 TN), 18 B reads per chunk instead of
+// 36.  The taps of an output are then summed (kw, kh) in kw-major order: the same products, another
+// order of the fp32 sums (not the register-staged kernel's bits).
+template <typename T16, int BM, int TH, bool KWM = false>
 __global__ __launch_bounds__(512, 1) void vconv3x3_dma_kernel(VcArgs<T16> g) {
   typedef hx8<T16> vgb8;
   typedef hx4<T16> vgb4;
@@ -291,6 +295,35 @@ __global__ __launch_bounds__(512, 1) void vconv3x3_dma_kernel(VcArgs<T16> g) {
     if (kc + 1 < nkc) issue(kc + 1, (kc + 1) & 1);
     const T16* Ab = reinterpret_cast<const T16*>(reinterpret_cast<const char*>(smem) + (kc & 1) * STAGE);
     const T16* Bb = Ab + A_BYTES / 2;
+    if constexpr (KWM) {
+      vgb8 af[2][TM], bq[2][TN + 2];
+      auto afr = [&](int tap, int b) __attribute__((always_inline)) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+          af[b][i] = *reinterpret_cast<const vgb8*>(Ab + ((tap * 2 + lh) * BM + wm * 64 + i * 32 + lr) * 8);
+      };
+      auto bro = [&](int kw, int b) __attribute__((always_inline)) {
+#pragma unroll
+        for (int r = 0; r < TN + 2; ++r)
+          bq[b][r] = *reinterpret_cast<const vgb8*>(Bb + ((lh * PH + wn * TN + r) * PW + lr + kw) * 8);
+      };
+      bro(0, 0);
+      afr(0, 0);
+#pragma unroll
+      for (int kw = 0; kw < 3; ++kw) {
+        if (kw + 1 < 3) bro(kw + 1, (kw + 1) & 1);
+#pragma unroll
+        for (int kh = 0; kh < 3; ++kh) {
+          const int s = kw * 3 + kh;   // step in kw-major order; tap = kh * 3 + kw
+          if (s + 1 < 9) afr(((s + 1) % 3) * 3 + (s + 1) / 3, (s + 1) & 1);
+#pragma unroll
+          for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+              acc[i][j] = mfma16(af[s & 1][i], bq[kw & 1][j + kh], acc[i][j]);
+        }
+      }
+    } else {
     vgb8 af[2][TM], bfr[2][TN];
     auto frags = [&](int tap, int b) __attribute__((always_inline)) {
       const int kh = tap / 3, kw = tap - (tap / 3) * 3;
@@ -310,6 +343,7 @@ __global__ __launch_bounds__(512, 1) void vconv3x3_dma_kernel(VcArgs<T16> g) {
 #pragma unroll
         for (int j = 0; j < TN; ++j)
           acc[i][j] = mfma16(af[tap & 1][i], bfr[tap & 1][j], acc[i][j]);
+    }
     }
   }
 
@@ -626,6 +660,13 @@ __global__ __launch_bounds__(256) void cb16_tap_bwd_kernel(const T16* __restrict
   }
 }
 
+// Planner knob (measurement tools): 0 = the LDS-DMA ring kernel where a launch fills the chip
+// (default: the step's 14 VGG launches 1014 -> 936 us at B = 16, same bits;
+// profiles/r04/vconv_micro.txt), 1 = always the register-staged kernel.  (A 4-wave form, one wave
+// per SIMD owning 4 x 4 MFMA tiles -- half the fragment reads per MFMA -- measured 1103 us against
+// the 8-wave ring's 957 over the same launches: profiles/r04/vconv_micro_4wave.txt.)
+static int g_vc_mode = 0;
+
 template <typename T16, int BM, int TH>
 static void vc_launch(VcArgs<T16>& g, hipStream_t st) {
   g.tiles_w = g.W / 32;
@@ -650,17 +691,15 @@ static void vc_launch_dma(VcArgs<T16>& g, hipStream_t st) {
   g.tiles_w = g.W / 32;
   g.tiles_h = g.H / TH;
   const long tiles = (long)g.N * g.tiles_w * g.tiles_h * (g.M / BM);
-  hipLaunchKernelGGL((vconv3x3_dma_kernel<T16, BM, TH>), dim3((unsigned)tiles), dim3(512), 0, st, g);
+  if (g_vc_mode == 3)
+    hipLaunchKernelGGL((vconv3x3_dma_kernel<T16, BM, TH, true>), dim3((unsigned)tiles), dim3(512), 0, st, g);
+  else
+    hipLaunchKernelGGL((vconv3x3_dma_kernel<T16, BM, TH>), dim3((unsigned)tiles), dim3(512), 0, st, g);
 }
 
 static int vc_bm(int M) { return (M % 128 == 0) ? 128 : 64; }
 
-// Planner knob (measurement tools): 0 = the LDS-DMA ring kernel where a launch fills the chip
-// (default: the step's 14 VGG launches 1014 -> 936 us at B = 16, same bits;
-// profiles/r04/vconv_micro.txt), 1 = always the register-staged kernel.  (A 4-wave form, one wave
-// per SIMD owning 4 x 4 MFMA tiles -- half the fragment reads per MFMA -- measured 1103 us against
-// the 8-wave ring's 957 over the same launches: profiles/r04/vconv_micro_4wave.txt.)
-static int g_vc_mode = 0;
+
 
 }  // namespace dsg
 
@@ -673,7 +712,8 @@ int dsgan_vconv_supported(int K, int M, int H, int W) {
 }
 
 // planner knob `key` <- val (val < 0: read only), returns the previous value (measurement tools):
-// key 0 = kernel form (0 LDS-DMA ring where it fills the chip, 1 register-staged)
+// key 0 = kernel form (0 LDS-DMA ring where it fills the chip, 1 register-staged, 3 the ring with
+// kw-major taps and B row reuse)
 int dsgan_vconv_tune(int key, int val) {
   if (key != 0) return -1;
   const int old = g_vc_mode;
@@ -718,7 +758,7 @@ int dsgan_vconv3x3(const void* X, const void* Wt, const float* bias, const void*
     // workgroup per CU, else 8-row ones
     const long pt16 = H % 16 == 0 ? (long)N * (W / 32) * (H / 16) * (M / BM) : 0;
     const long pt8 = H % 8 == 0 ? (long)N * (W / 32) * (H / 8) * (M / BM) : 0;
-    g.zero = g_vc_mode == 0 && (pt16 >= 256 || pt8 >= 256) ? vc_zero() : nullptr;
+    g.zero = g_vc_mode != 1 && (pt16 >= 256 || pt8 >= 256) ? vc_zero() : nullptr;
     if (g.zero) {
       if (BM == 128) {
         if (pt16 >= 256) vc_launch_dma<T16, 128, 16>(g, st); else vc_launch_dma<T16, 128, 8>(g, st);

@@ -1,5 +1,6 @@
 """In-process A/B of the VGG16 3x3 conv kernels (vggconv.hip) at the step's shapes (batch 16, 256^2
-input): the LDS-DMA ring kernel (dsgan_vconv_tune(0, 0)) vs the register-staged one (1).  Outputs of
+input): the LDS-DMA ring kernel (dsgan_vconv_tune(0, 0)) vs the register-staged one (1), and the ring with
+kw-major taps (3: another fp32 summation order, compared by relative error).  Outputs of
 the two forms must be bitwise equal (same operands, same per-output accumulation order).
 
     python tools/vconv_micro.py [--it 20]
@@ -45,8 +46,9 @@ def main():
     lib = _lib.load()
     old = lib.dsgan_vconv_tune(0, -1)
     g = torch.Generator(device="cuda").manual_seed(0)
-    tot = [0.0, 0.0]
-    print("%-6s %5s %5s %4s | %9s %9s | %7s %7s | bitwise" % ("layer", "K", "M", "H", "old us", "dma us", "old TF", "dma TF"))
+    tot = [0.0, 0.0, 0.0]
+    print("%-6s %5s %5s %4s | %9s %9s %9s | %7s %7s %7s | bitwise | kwm rel" % (
+        "layer", "K", "M", "H", "old us", "dma us", "kwm us", "old TF", "dma TF", "kwm TF"))
     for name, K, M, H, dgrad in LAYERS:
         Co, Ci = (K, M) if dgrad else (M, K)
         W = torch.randn(Co, Ci, 3, 3, device="cuda", generator=g) * 0.05
@@ -57,7 +59,7 @@ def main():
         mask = torch.randn(N * M * H * H, device="cuda", generator=g).to(torch.bfloat16) if dgrad else None
         ys = []
         ts = []
-        for mode in (1, 0):
+        for mode in (1, 0, 3):
             lib.dsgan_vconv_tune(0, mode)
             Y = torch.empty(N * M * H * H, device="cuda", dtype=torch.bfloat16)
             fn = lambda Y=Y: call("dsgan_vconv3x3", ptr(X), ptr(Wt), ptr(bias), ptr(mask), ptr(Y), 0, 0 if dgrad else 1,
@@ -68,12 +70,14 @@ def main():
             ts.append(timeit(fn, a.it))
         fl = 2.0 * N * M * K * 9 * H * H
         same = torch.equal(ys[0], ys[1])
-        tot[0] += ts[0]
-        tot[1] += ts[1]
-        print("%-6s %5d %5d %4d | %9.1f %9.1f | %7.1f %7.1f | %s" % (name, K, M, H, ts[0], ts[1], fl / ts[0] / 1e6,
-                                                                    fl / ts[1] / 1e6, same), flush=True)
+        d = (ys[2].float() - ys[0].float()).norm() / ys[0].float().norm().clamp_min(1e-30)
+        for q in range(3):
+            tot[q] += ts[q]
+        print("%-6s %5d %5d %4d | %9.1f %9.1f %9.1f | %7.1f %7.1f %7.1f | %s | %.2e" % (
+            name, K, M, H, ts[0], ts[1], ts[2], fl / ts[0] / 1e6, fl / ts[1] / 1e6, fl / ts[2] / 1e6, same, d.item()),
+            flush=True)
     lib.dsgan_vconv_tune(0, old)
-    print("total: old %.1f us, dma %.1f us" % tuple(tot))
+    print("total: old %.1f us, dma %.1f us, kwm %.1f us" % tuple(tot))
 
 
 if __name__ == "__main__":
