@@ -15,6 +15,7 @@
 #   prof                      rocprofv3 kernel stats of a short bench run (tools/gpu_prof.sh)
 #   pmc                       PMC HBM traffic + MFMA/LDS counters (tools/gpu_pmc.sh, gpu_mfma_pmc.sh)
 #   pwpmc=<case>[/arm]        per-instance PMC of one pw_bench case ('+' for spaces), two arms (tools/gpu_pw_pmc.sh)
+#   kpmc=<tag>:<script>[+args] per-kernel-instance PMC over a python tool (tools/gpu_kpmc.sh)
 #   py=<script>[+args]        any python tool under tools/ (limit 600 s)     -> <script>.txt
 set -o pipefail
 mkdir -p gpurun_out
@@ -88,6 +89,12 @@ for step in "$@"; do
       c=${c//+/ }
       timeout -k 10 900 bash tools/gpu_pw_pmc.sh "$c" "$arm" > gpurun_out/pw_pmc.txt 2>&1 || { tail -30 gpurun_out/pw_pmc.txt; exit 1; }
       tail -12 gpurun_out/pw_pmc.txt ;;
+    kpmc)
+      tag=${arg%%:*}; sc=${arg#*:}; s=${sc%%+*}; rest=""
+      [ "$s" != "$sc" ] && rest=${sc#*+}
+      # shellcheck disable=SC2086
+      timeout -k 10 900 bash tools/gpu_kpmc.sh "$tag" "tools/$s" ${rest//+/ } > gpurun_out/kpmc_run_$tag.txt 2>&1 || { tail -30 gpurun_out/kpmc_run_$tag.txt; exit 1; }
+      head -25 gpurun_out/kpmc_$tag.txt ;;
     py)
       s=${arg%%+*}; rest=""
       [ "$s" != "$arg" ] && rest=${arg#*+}
