@@ -33,6 +33,8 @@ struct PwArgs {
   int y_bf16;  // FWD: Y is bf16 [b][M][P] (y_bs in elements)
   int gbf;     // FWD: ypre is bf16 and receives act'(pre);  DGRAD: gpre is a bf16 multiplier (no act')
   int gp_pref; // DGRAD with a 16-bit gp multiplier (SWP tiles): load gp before the K loop
+  int dbg;     // measurement only (planner knob 10): bit 0 = drop the epilogue's output stores,
+               // bit 1 = the gelu pair without its GELU arithmetic
   int dma;     // host planner: the wide 16-bit-operand launch runs an LDS-DMA ring form: 1 = 256 x 256
                // tiles (8 waves, 4 stages, one workgroup per CU), 2 = 256 x 128 tiles (4 waves, 3 stages,
                // two workgroups per CU: one's epilogue runs beside the other's MFMAs)
@@ -586,7 +588,10 @@ __global__ __launch_bounds__(128 * WN, WN == 2 ? 2 : 1) void pwgemm_kernel(PwArg
   const float* const gpre = part ? nullptr : g.gpre;
   float* const ypre = part ? nullptr : g.ypre;
   const int act = part ? 0 : g.act, accumulate = part ? 0 : g.accumulate, y_bf16 = part ? 0 : g.y_bf16;
-  const unsigned range = (unsigned)(((long)g.M * g.P - p0) * 4);
+  const unsigned grange = (unsigned)(((long)g.M * g.P - p0) * 4);
+  // (g.dbg & 1: measurement builds only -- zero-range output descriptors drop every output store, so
+  // an A/B prices the epilogue's HBM writes; cdna_hip_programming.md T8)
+  const unsigned range = (g.dbg & 1) ? 0u : grange;
   const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(ybase + (long)bimg * ybs + p0), (short)0, range, 0x00020000);
   const __amdgpu_buffer_rsrc_t ryh = __builtin_amdgcn_make_buffer_rsrc(
@@ -597,7 +602,7 @@ __global__ __launch_bounds__(128 * WN, WN == 2 ? 2 : 1) void pwgemm_kernel(PwArg
   if (ypre) rp = __builtin_amdgcn_make_buffer_rsrc((void*)((char*)ypre + ((long)bimg * g.ypre_bs + p0) * esz), (short)0,
                                                    g.gbf ? range / 2 : range, 0x00020000);
   if (gpre) rg = __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)gpre + ((long)bimg * g.gpre_bs + p0) * esz),
-                                                   (short)0, g.gbf ? range / 2 : range, 0x00020000);
+                                                   (short)0, g.gbf ? grange / 2 : grange, 0x00020000);
   // 16-bit store of this lane's 16 values: groups (q, q+1) swap halves so lanes 0-31 hold pixels
   // 8q..8q+7 and lanes 32-63 pixels 8q+8..8q+15 of their channel (byte offset +16)
   auto store16 = [&](__amdgpu_buffer_rsrc_t r, const float* v, int vh, int srow) __attribute__((always_inline)) {
@@ -658,7 +663,10 @@ __global__ __launch_bounds__(128 * WN, WN == 2 ? 2 : 1) void pwgemm_kernel(PwArg
         bool acted = false;
         if (ypre && g.gbf) {          // FWD: ypre <- 16-bit act'(pre), v <- act(pre) (one GELU evaluation)
           float apv[16];
-          if (act == ACT_GELU) {
+          if (g.dbg & 2) {              // (measurement only: the pair without its GELU arithmetic)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) apv[r] = v[r];
+          } else if (act == ACT_GELU) {
 #pragma unroll
             for (int r = 0; r < 16; r += 2) {
               f32x2 a, ap;

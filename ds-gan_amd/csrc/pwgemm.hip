@@ -43,6 +43,8 @@ static void pw_fd_launch(int mode, const PwArgs& g, int bm, int abf, int bbf, in
 //   155 -> 149 and 138 -> 131 us, same bits; profiles/r04/pw_bench_dma.txt); 3 = the same plus the
 //   weight-grads (3-5 % slower there); 2 = 256 x 128 tiles, 3 stages, two workgroups per CU (slower:
 //   392 us for the 512-channel gelu-pair forward); 0 = register-staged everywhere.
+//   [10] measurement only: bit 0 = FWD / DGRAD epilogues drop their output stores (prices the writes),
+//   bit 1 = the gelu-pair epilogue skips its GELU arithmetic (prices the VALU).
 static int g_tune[12] = {1, 512, 256, 4, 0, 0, 0, 0, 1, 1, 0, 0};
 
 // the LDS-DMA ring form's conditions (full 256 x 256 tiles, 32-deep K steps, 16-byte pieces)
@@ -97,6 +99,7 @@ static int fd_plan(PwArgs& g, int bm, float* ws) {
   g.k_split = 0;
   g.ws = nullptr;
   g.gp_pref = g_tune[8];
+  g.dbg = g_tune[10];
   if (ws && fd_split_ok(g)) {
     splits = fd_splits(g, bm, PBK, &g.k_split);
     if (splits > 1) g.ws = ws;
