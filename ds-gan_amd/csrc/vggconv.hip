@@ -661,11 +661,12 @@ __global__ __launch_bounds__(256) void cb16_tap_bwd_kernel(const T16* __restrict
 }
 
 // Planner knob (measurement tools): 0 = the LDS-DMA ring kernel where a launch fills the chip
-// (default: the step's 14 VGG launches 1014 -> 936 us at B = 16, same bits;
-// profiles/r04/vconv_micro.txt), 1 = always the register-staged kernel.  (A 4-wave form, one wave
+// (the step's 14 VGG launches 1014 -> 936 us at B = 16, same bits; profiles/r04/vconv_micro.txt),
+// 1 = always the register-staged kernel, 3 = the ring with kw-major taps and B row reuse (default:
+// 940 -> 924 us, relative difference 2-4e-5 from the tap-order change; profiles/r04/vconv_micro_kwm.txt).  (A 4-wave form, one wave
 // per SIMD owning 4 x 4 MFMA tiles -- half the fragment reads per MFMA -- measured 1103 us against
 // the 8-wave ring's 957 over the same launches: profiles/r04/vconv_micro_4wave.txt.)
-static int g_vc_mode = 0;
+static int g_vc_mode = 3;
 
 template <typename T16, int BM, int TH>
 static void vc_launch(VcArgs<T16>& g, hipStream_t st) {
