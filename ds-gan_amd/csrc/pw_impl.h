@@ -5,7 +5,6 @@
 #include "common.h"
 #include "lds_dma.h"
 #include <stdlib.h>
-#include <type_traits>
 
 namespace dsg {
 
@@ -34,7 +33,6 @@ struct PwArgs {
   int y_bf16;  // FWD: Y is bf16 [b][M][P] (y_bs in elements)
   int gbf;     // FWD: ypre is bf16 and receives act'(pre);  DGRAD: gpre is a bf16 multiplier (no act')
   int gp_pref; // DGRAD with a 16-bit gp multiplier (SWP tiles): load gp before the K loop
-  int lds_out; // host planner (knob 11): DMA ring kernels stage 16-bit output tiles through LDS
   int dbg;     // measurement only (planner knob 10): bit 0 = drop the epilogue's output stores,
                // bit 1 = the gelu pair without its GELU arithmetic
   int dma;     // host planner: the wide 16-bit-operand launch runs an LDS-DMA ring form: 1 = 256 x 256
@@ -623,70 +621,6 @@ __global__ __launch_bounds__(128 * WN, WN == 2 ? 2 : 1) void pwgemm_kernel(PwArg
       __builtin_amdgcn_raw_buffer_store_b128(o, r, vh, srow + 16 * q, 0);
     }
   };
-  // LDS-staged 16-bit outputs (DMA ring kernels, planner knob 11): the direct SW stores write 32 B
-  // into each of 32 channel rows per instruction, and the epilogue's writes cost ~18 % of the
-  // unfused-block GEMMs (knob 10 pricing).  Here the finished 16-bit tile goes through the (now
-  // free) ring LDS -- rows = channels, 512 B each, 16-byte slots XOR (row & 31) -- and every store
-  // instruction then writes two whole 512-byte channel rows.  A gelu pair is two passes over the
-  // accumulators (act' first, then act: the GELU arithmetic twice, the stores once each).
-  if constexpr (DM && SW && BN == 256) {
-    if (g.lds_out && y_bf16 && !gpre && !accumulate && (!ypre || g.gbf) && !part) {
-      static_assert(BM * BN * 2 <= NS * (DA_SZ + DB_SZ) * 2, "staged tile fits the ring");
-      constexpr int NWV = NT / 64;
-      char* const stg = reinterpret_cast<char*>(smem);
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();   // every wave is done reading the ring
-      auto stage_pass = [&](auto PASS) __attribute__((always_inline)) {
-        constexpr int pass = decltype(PASS)::value;
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-#pragma unroll
-          for (int i = 0; i < TM; ++i) {
-            float v[16];
-#pragma unroll
-            for (int r = 0; r < 16; ++r) v[r] = acc[i][j][r];
-            if (ypre) {
-              if (act == ACT_GELU) {
-#pragma unroll
-                for (int r = 0; r < 16; r += 2) {
-                  f32x2 a, ap;
-                  gelu_pair_fast2(f32x2{v[r], v[r + 1]}, a, ap);
-                  v[r] = pass ? a.x : ap.x;
-                  v[r + 1] = pass ? a.y : ap.y;
-                }
-              } else {
-#pragma unroll
-                for (int r = 0; r < 16; ++r) v[r] = pass ? act_f(act, v[r], g.slope) : act_g(act, v[r], g.slope);
-              }
-            } else {
-              act_f_arr(act, v, g.slope);
-            }
-            const int row = wm * TM * 32 + i * 32 + lr;   // channel within the tile
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-              const int slot = wn * TN * 4 + j * 4 + q;   // 8-pixel group within the tile row
-              const uint2 w = make_uint2((unsigned)f2h<T16>(v[4 * q]) | ((unsigned)f2h<T16>(v[4 * q + 1]) << 16),
-                                         (unsigned)f2h<T16>(v[4 * q + 2]) | ((unsigned)f2h<T16>(v[4 * q + 3]) << 16));
-              *reinterpret_cast<uint2*>(stg + row * 512 + ((slot ^ (row & 31)) << 4) + 8 * lh) = w;
-            }
-          }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        const __amdgpu_buffer_rsrc_t ro = pass ? ryh : rp;
-#pragma unroll 4
-        for (int r0 = wave * 2; r0 < BM; r0 += NWV * 2) {
-          const int row = r0 + lh, slot = lr;
-          const pu32x4 d = *reinterpret_cast<const pu32x4*>(stg + row * 512 + ((slot ^ (row & 31)) << 4));
-          __builtin_amdgcn_raw_buffer_store_b128(d, ro, ((m0 + row) * g.P + 8 * slot) * 2, 0, 0);
-        }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();   // the staging area is reused by the next pass
-      };
-      if (ypre) stage_pass(std::integral_constant<int, 0>{});
-      stage_pass(std::integral_constant<int, 1>{});
-      return;
-    }
-  }
   if constexpr (SW) {
 #pragma unroll
     for (int j = 0; j < TN; ++j) {

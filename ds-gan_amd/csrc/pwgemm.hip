@@ -45,7 +45,6 @@ static void pw_fd_launch(int mode, const PwArgs& g, int bm, int abf, int bbf, in
 //   392 us for the 512-channel gelu-pair forward); 0 = register-staged everywhere.
 //   [10] measurement only: bit 0 = FWD / DGRAD epilogues drop their output stores (prices the writes),
 //   bit 1 = the gelu-pair epilogue skips its GELU arithmetic (prices the VALU).
-//   [11] the DMA ring FWD / DGRAD kernels stage 16-bit output tiles through LDS (whole-row stores).
 static int g_tune[12] = {1, 512, 256, 4, 0, 0, 0, 0, 1, 1, 0, 0};
 
 // the LDS-DMA ring form's conditions (full 256 x 256 tiles, 32-deep K steps, 16-byte pieces)
@@ -101,7 +100,6 @@ static int fd_plan(PwArgs& g, int bm, float* ws) {
   g.ws = nullptr;
   g.gp_pref = g_tune[8];
   g.dbg = g_tune[10];
-  g.lds_out = g_tune[11];
   if (ws && fd_split_ok(g)) {
     splits = fd_splits(g, bm, PBK, &g.k_split);
     if (splits > 1) g.ws = ws;

@@ -1384,41 +1384,3 @@ def test_pw_wide_dma_ring_bitwise(half, form, ring):
     if form == "fwd32":
         r = torch.einsum("mk,nkp->nmp", w.float(), x.float()) + bias[None, :, None]
         assert rel(got[0], r) < 1e-5
-
-
-@pytest.mark.parametrize("half", HALVES)
-@pytest.mark.parametrize("pair", [False, True])
-def test_pw_lds_staged_output_bitwise(half, pair):
-    """The DMA-ring pointwise forward with its 16-bit output tile staged through LDS (planner knob
-    11: whole-row stores) writes the same bits as the direct per-lane stores -- plain bf16 output and
-    the gelu pair (act'(z) then act(z), two passes over the accumulators)."""
-    import dsgan_hip
-    from dsgan_hip import _lib, functional as HF
-    from dsgan_hip._lib import call, ptr, stream
-    lib = _lib.load()
-    dsgan_hip.set_precision(half)
-    hd = _hdt(half)
-    g0 = torch.Generator(device=DEV).manual_seed(9)
-    NB, HW, M, K = 4, 128 * 128, 512, 256
-    w = (torch.randn(M, K, device=DEV, generator=g0) / K ** 0.5).to(hd)
-    bias = torch.randn(M, device=DEV, generator=g0)
-    x = torch.randn(NB, K, HW, device=DEV, generator=g0).to(hd)
-    old9, old11 = lib.dsgan_pw_tune(9, -1), lib.dsgan_pw_tune(11, -1)
-
-    def run(staged):
-        lib.dsgan_pw_tune(9, 1)
-        lib.dsgan_pw_tune(11, staged)
-        y = torch.full((NB, M, HW), float("nan"), device=DEV).to(hd)
-        gp = torch.full((NB, M, HW), float("nan"), device=DEV).to(hd) if pair else None
-        ws = torch.empty(max(1, lib.dsgan_pw_fd_workspace(0, M, K, HW, NB)), device=DEV)
-        call("dsgan_pw_fwd_io_ws", ptr(w), 1, ptr(x), K * HW, 1, ptr(y), M * HW, 1, ptr(gp), M * HW if pair else 0,
-             1 if pair else 0, ptr(bias), M, K, HW, NB, 1 if pair else 0, 0, 0.2, *HF.wsa(ws), stream())
-        torch.cuda.synchronize()
-        return [y] + ([gp] if pair else [])
-    try:
-        ref, got = run(0), run(1)
-    finally:
-        lib.dsgan_pw_tune(9, old9)
-        lib.dsgan_pw_tune(11, old11)
-    for a, b in zip(got, ref):
-        assert torch.equal(a, b)
