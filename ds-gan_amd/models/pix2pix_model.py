@@ -257,7 +257,16 @@ class Pix2PixModel(BaseModel):
                 self.forward()
                 self._d_and_g_steps()
                 return
-            self._capture(key)
+            try:
+                self._capture(key)
+            except Exception as e:   # noqa: BLE001 -- a capture failure must not end the run: eager from here on
+                print("[Pix2PixModel] HIP graph capture failed (%r): running the eager step" % (e,))
+                self._graphs, self.cuda_graph, self._feats_joined = None, False, False
+                torch.cuda.synchronize(self.device)
+                self._launch_real_features()
+                self.forward()
+                self._d_and_g_steps()
+                return
         gA, gB = self._graphs
         gA.replay()
         if self.use_gan == 1 and self.use_condition == 1:
