@@ -409,6 +409,146 @@ __global__ __launch_bounds__(NT == 64 ? 256 : NT) void instnorm_bwd_v4(INBwdArgs
   }
 }
 
+// ---- few-plane forms: one plane split over S workgroups ----
+// The generator's 3-channel block (MixConvNeXtML.py:220-221 at dim 3) normalises N*3 = 48 planes
+// of 64K pixels: a workgroup per plane keeps 48 of the 256 CUs busy (72.6 us at 0.35 TB/s,
+// profiles/r04/launches_c.txt).  Here each plane's S chunks (IN_SPLIT_F4 float4s, 4 per thread)
+// are separate workgroups; the plane statistics are summed from per-chunk partials in a fixed
+// order, so the result is deterministic (it is not the one-workgroup kernel's summation order).
+// fwd: partial sums -> partial squared deviations -> output; bwd: partial (sum g, sum g*xhat) -> dx.
+constexpr int IN_SPLIT_F4 = 1024;
+
+static inline int in_split_chunks(long planes, int HW) {
+  if ((HW & 3) || planes >= 128 || HW < 16384) return 0;
+  return (int)cdiv(HW >> 2, IN_SPLIT_F4);
+}
+
+__device__ __forceinline__ float in_split_total(const float* p, int S, int stride) {
+  float r = 0.f;
+  for (int k = 0; k < S; ++k) r += p[k * stride];
+  return r;
+}
+
+// PASS 0: ws[plane*S + k] = sum of s*x over chunk k;  PASS 1: ws[P*S + plane*S + k] = sum of (s*x - mean)^2
+template <int PASS>
+__global__ __launch_bounds__(256) void in_split_stat(INArgs a, float* __restrict__ ws, int S) {
+  __shared__ float sh[4];
+  const int k = blockIdx.x, plane = blockIdx.y, P = a.N * a.C;
+  const int n = plane / a.C, c = plane - n * a.C;
+  const int HW4 = a.HW >> 2;
+  const float4* x = reinterpret_cast<const float4*>(a.x + (long)n * a.x_bs + (long)c * a.HW);
+  const float s = a.scale ? a.scale[plane] : 1.f;
+  const float mean = PASS ? in_split_total(ws + (long)plane * S, S, 1) * (1.f / (float)a.HW) : 0.f;
+  float acc = 0.f;
+#pragma unroll
+  for (int j = 0; j < IN_SPLIT_F4 / 256; ++j) {
+    const int i = k * IN_SPLIT_F4 + j * 256 + threadIdx.x;
+    if (i < HW4) {
+      float4 v = x[i];
+      v.x *= s; v.y *= s; v.z *= s; v.w *= s;
+      if (PASS == 0) {
+        acc += hsum4(v);
+      } else {
+        const float dx = v.x - mean, dy = v.y - mean, dz = v.z - mean, dw = v.w - mean;
+        acc += (dx * dx + dy * dy) + (dz * dz + dw * dw);
+      }
+    }
+  }
+  acc = block_sum<256>(acc, sh);
+  if (threadIdx.x == 0) ws[(long)PASS * P * S + (long)plane * S + k] = acc;
+}
+
+__global__ __launch_bounds__(256) void in_split_out(INArgs a, const float* __restrict__ ws, int S) {
+  const int k = blockIdx.x, plane = blockIdx.y, P = a.N * a.C;
+  const int n = plane / a.C, c = plane - n * a.C;
+  const int HW4 = a.HW >> 2;
+  const long po = (long)c * a.HW;
+  const float inv = 1.f / (float)a.HW;
+  const float mean = in_split_total(ws + (long)plane * S, S, 1) * inv;
+  const float rs = 1.f / sqrtf(in_split_total(ws + (long)P * S + (long)plane * S, S, 1) * inv + a.eps);
+  if (k == 0 && threadIdx.x == 0) { a.mean[plane] = mean; a.rstd[plane] = rs; }
+  const float4* x = reinterpret_cast<const float4*>(a.x + (long)n * a.x_bs + po);
+  const float4* r = a.res ? reinterpret_cast<const float4*>(a.res + (long)n * a.res_bs + po) : nullptr;
+  const float s = a.scale ? a.scale[plane] : 1.f;
+#pragma unroll
+  for (int j = 0; j < IN_SPLIT_F4 / 256; ++j) {
+    const int i = k * IN_SPLIT_F4 + j * 256 + threadIdx.x;
+    if (i >= HW4) continue;
+    float4 v = x[i];
+    v.x = (v.x * s - mean) * rs; v.y = (v.y * s - mean) * rs; v.z = (v.z * s - mean) * rs; v.w = (v.w * s - mean) * rs;
+    if (r) { const float4 q = r[i]; v.x += q.x; v.y += q.y; v.z += q.z; v.w += q.w; }
+    v.x = act_f(a.act, v.x, a.slope); v.y = act_f(a.act, v.y, a.slope);
+    v.z = act_f(a.act, v.z, a.slope); v.w = act_f(a.act, v.w, a.slope);
+    if (a.y_bf16 == 2) {
+      hx4<_Float16> hv = {(_Float16)v.x, (_Float16)v.y, (_Float16)v.z, (_Float16)v.w};
+      reinterpret_cast<hx4<_Float16>*>(reinterpret_cast<_Float16*>(a.y) + (long)n * a.y_bs + po)[i] = hv;
+    } else if (a.y_bf16) {
+      hx4<__bf16> hv = {(__bf16)v.x, (__bf16)v.y, (__bf16)v.z, (__bf16)v.w};
+      reinterpret_cast<hx4<__bf16>*>(reinterpret_cast<__bf16*>(a.y) + (long)n * a.y_bs + po)[i] = hv;
+    } else {
+      reinterpret_cast<float4*>(a.y + (long)n * a.y_bs + po)[i] = v;
+    }
+  }
+}
+
+// g = dy * act'(xhat + res) (dres = g written here);  ws[(plane*S + k)*2 + {0,1}] = chunk sums of g, g*xhat
+__device__ __forceinline__ float4 in_split_g(const INBwdArgs& a, int n, long po, int i, float4 xh) {
+  float4 g = reinterpret_cast<const float4*>(a.dy + (long)n * a.dy_bs + po)[i];
+  if (a.act != ACT_NONE) {
+    float4 z = xh;
+    if (a.res) {
+      const float4 q = reinterpret_cast<const float4*>(a.res + (long)n * a.res_bs + po)[i];
+      z.x += q.x; z.y += q.y; z.z += q.z; z.w += q.w;
+    }
+    g.x *= act_g(a.act, z.x, a.slope); g.y *= act_g(a.act, z.y, a.slope);
+    g.z *= act_g(a.act, z.z, a.slope); g.w *= act_g(a.act, z.w, a.slope);
+  }
+  return g;
+}
+
+template <int PASS>   // 0: partial sums (+ dres);  1: dx (+ dscale)
+__global__ __launch_bounds__(256) void in_split_bwd(INBwdArgs a, float* __restrict__ ws, int S) {
+  __shared__ float sh[8];
+  const int k = blockIdx.x, plane = blockIdx.y;
+  const int n = plane / a.C, c = plane - n * a.C;
+  const int HW4 = a.HW >> 2;
+  const long po = (long)c * a.HW;
+  const float4* x = reinterpret_cast<const float4*>(a.x + (long)n * a.x_bs + po);
+  const float s = a.scale ? a.scale[plane] : 1.f;
+  const float mean = a.mean[plane], rs = a.rstd[plane];
+  const float inv = 1.f / (float)a.HW;
+  float mg = 0.f, mgh = 0.f;
+  if (PASS == 1) {
+    mg = in_split_total(ws + (long)plane * S * 2, S, 2) * inv;
+    mgh = in_split_total(ws + (long)plane * S * 2 + 1, S, 2) * inv;
+  }
+  float sg = 0.f, sgh = 0.f;
+#pragma unroll
+  for (int j = 0; j < IN_SPLIT_F4 / 256; ++j) {
+    const int i = k * IN_SPLIT_F4 + j * 256 + threadIdx.x;
+    if (i >= HW4) continue;
+    float4 xh = x[i];
+    xh.x = (xh.x * s - mean) * rs; xh.y = (xh.y * s - mean) * rs; xh.z = (xh.z * s - mean) * rs; xh.w = (xh.w * s - mean) * rs;
+    const float4 g = in_split_g(a, n, po, i, xh);
+    if (PASS == 0) {
+      if (a.dres) reinterpret_cast<float4*>(a.dres + (long)n * a.dres_bs + po)[i] = g;
+      sg += hsum4(g);
+      sgh += (g.x * xh.x + g.y * xh.y) + (g.z * xh.z + g.w * xh.w);
+    } else {
+      const float kk = s * rs;
+      reinterpret_cast<float4*>(a.dx + (long)n * a.dx_bs + po)[i] =
+          make_float4(kk * (g.x - mg - xh.x * mgh), kk * (g.y - mg - xh.y * mgh), kk * (g.z - mg - xh.z * mgh),
+                      kk * (g.w - mg - xh.w * mgh));
+    }
+  }
+  if (PASS == 0) {
+    const float2 m = plane_sum2<256>(sg, sgh, sh);
+    if (threadIdx.x == 0) { ws[((long)plane * S + k) * 2] = m.x; ws[((long)plane * S + k) * 2 + 1] = m.y; }
+  } else if (a.dscale && k == 0 && threadIdx.x == 0) {
+    a.dscale[plane] = mgh * (float)a.HW * a.eps * rs * rs / s;
+  }
+}
+
 // ---------------------------------------------------------------------------------------
 // MaxPool2d(k) (stride k, no padding, floor): DSGAN/models/model/MixConvNeXtML.py:71,194,333-417
 // Indices are the plane-flat argmax ih*W+iw, first maximum in row-major window order, NaN wins
@@ -1067,6 +1207,33 @@ int dsgan_instnorm_fwd(const float* x, long x_bs, const float* scale, const floa
   return 0;
 }
 
+// Scratch (fp32 elements) of dsgan_instnorm_{fwd,bwd}_ws for this shape: 0 when the one-workgroup-
+// per-plane kernels serve it (>= 128 planes or planes under 16K pixels), else the per-chunk partials
+// of the split forms.
+long dsgan_instnorm_workspace(int N, int C, int HW) {
+  const int S = in_split_chunks((long)N * C, HW);
+  return S ? 2L * N * C * S : 0;
+}
+
+// dsgan_instnorm_fwd with scratch: few large planes are split over several workgroups each.
+int dsgan_instnorm_fwd_ws(const float* x, long x_bs, const float* scale, const float* res, long res_bs,
+                          float* y, long y_bs, float* mean, float* rstd, int N, int C, int HW, int act,
+                          float slope, float eps, float* ws, long ws_elems, hipStream_t st) {
+  DSG_REQUIRE(x && y && mean && rstd && N > 0 && C > 0 && HW > 0, "dsgan_instnorm_fwd_ws: bad args");
+  const long planes = (long)N * C;
+  const int v4 = in_v4_ok(HW, x, x_bs) && in_v4_ok(HW, y, y_bs) && (!res || in_v4_ok(HW, res, res_bs));
+  const int S = v4 ? in_split_chunks(planes, HW) : 0;
+  DSG_WS(S ? 2 * planes * S : 0, ws, ws_elems, "dsgan_instnorm_fwd_ws");
+  if (!S) return dsgan_instnorm_fwd(x, x_bs, scale, res, res_bs, y, y_bs, mean, rstd, N, C, HW, act, slope, eps, st);
+  INArgs a{x, x_bs, scale, res, res_bs, y, y_bs, mean, rstd, N, C, HW, act, slope, eps, 0};
+  const dim3 g(S, (unsigned)planes);
+  hipLaunchKernelGGL(in_split_stat<0>, g, dim3(256), 0, st, a, ws, S);
+  hipLaunchKernelGGL(in_split_stat<1>, g, dim3(256), 0, st, a, ws, S);
+  hipLaunchKernelGGL(in_split_out, g, dim3(256), 0, st, a, ws, S);
+  DSG_CHECK_LAUNCH();
+  return 0;
+}
+
 // y (bf16) = IN(x): the plain InstanceNorm2d(affine=False) of a ConvNeXt block
 // (DSGAN/models/model/MixConvNeXtML.py:233), stored bf16 for the block's MLP GEMMs.
 int dsgan_instnorm_fwd_bf16(const float* x, long x_bs, void* y, long y_bs, float* mean, float* rstd, int N, int C,
@@ -1150,6 +1317,29 @@ int dsgan_instnorm_bwd(const float* dy, long dy_bs, const float* x, long x_bs, c
     hipLaunchKernelGGL((instnorm_bwd_kernel<1024, 16>), dim3(planes), dim3(1024), 0, st, a);
   else
     hipLaunchKernelGGL((instnorm_bwd_kernel<1024, 0>), dim3(planes), dim3(1024), 0, st, a);
+  DSG_CHECK_LAUNCH();
+  return 0;
+}
+
+// dsgan_instnorm_bwd with scratch (dsgan_instnorm_workspace): few large planes split as in the forward.
+int dsgan_instnorm_bwd_ws(const float* dy, long dy_bs, const float* x, long x_bs, const float* scale,
+                          const float* res, long res_bs, const float* mean, const float* rstd,
+                          float* dx, long dx_bs, float* dres, long dres_bs, float* dscale, int N,
+                          int C, int HW, int act, float slope, float eps, float* ws, long ws_elems, hipStream_t st) {
+  DSG_REQUIRE(dy && x && mean && rstd && dx && N > 0 && C > 0 && HW > 0, "dsgan_instnorm_bwd_ws: bad args");
+  const long planes = (long)N * C;
+  const int v4 = in_v4_ok(HW, dy, dy_bs) && in_v4_ok(HW, x, x_bs) && in_v4_ok(HW, dx, dx_bs) &&
+                 (!res || in_v4_ok(HW, res, res_bs)) && (!dres || in_v4_ok(HW, dres, dres_bs));
+  const int S = v4 ? in_split_chunks(planes, HW) : 0;
+  DSG_WS(S ? 2 * planes * S : 0, ws, ws_elems, "dsgan_instnorm_bwd_ws");
+  if (!S)
+    return dsgan_instnorm_bwd(dy, dy_bs, x, x_bs, scale, res, res_bs, mean, rstd, dx, dx_bs, dres, dres_bs, dscale,
+                              N, C, HW, act, slope, eps, st);
+  INBwdArgs a{dy, dy_bs, x, x_bs, scale, res, res_bs, mean, rstd, dx, dx_bs, dres, dres_bs, dscale,
+              N, C, HW, act, slope, eps};
+  const dim3 g(S, (unsigned)planes);
+  hipLaunchKernelGGL(in_split_bwd<0>, g, dim3(256), 0, st, a, ws, S);
+  hipLaunchKernelGGL(in_split_bwd<1>, g, dim3(256), 0, st, a, ws, S);
   DSG_CHECK_LAUNCH();
   return 0;
 }

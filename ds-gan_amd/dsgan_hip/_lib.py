@@ -109,6 +109,9 @@ SIGNATURES = {
     "dsgan_instnorm_fwd_bf16": [P, L, P, L, P, P, I, I, I, F, S],
     "dsgan_instnorm_bwd": [P, L, P, L, P, P, L, P, P, P, L, P, L, P, I, I, I, I, F, F, S],
     "dsgan_instnorm_bwd_h": [P, L, P, L, P, L, P, P, P, L, P, P, L, I, I, I, I, F, F, S],
+    "dsgan_instnorm_workspace": [I, I, I],
+    "dsgan_instnorm_fwd_ws": [P, L, P, P, L, P, L, P, P, I, I, I, I, F, F, P, L, S],
+    "dsgan_instnorm_bwd_ws": [P, L, P, L, P, P, L, P, P, P, L, P, L, P, I, I, I, I, F, F, P, L, S],
     "dsgan_maxpool_fwd": [P, L, P, L, P, I, I, I, I, I, S],
     "dsgan_maxpool_bwd": [P, L, P, P, L, I, I, I, I, I, I, S],
     "dsgan_plane_stats": [P, L, P, P, P, I, I, I, S],

@@ -1239,6 +1239,12 @@ def multi_dwconv(x, w3, b3, w5, b5, w7, b7, w9, b9):
 # InstanceNorm (+scale, +residual, +act)
 # ------------------------------------------------------------------------------------------
 
+def _in_ws(N, C, HW, like):
+    """Scratch of the split InstanceNorm forms (few large planes), None when the shape needs none."""
+    n = _lib.load().dsgan_instnorm_workspace(N, C, HW)
+    return torch.empty(n, device=like.device, dtype=torch.float32) if n > 0 else None
+
+
 def instnorm_raw(x, scale=None, res=None, act=None, out=None):
     x, xbs = nchw(x)
     N, C, H, W = x.shape
@@ -1250,8 +1256,8 @@ def instnorm_raw(x, scale=None, res=None, act=None, out=None):
     mean = torch.empty(N * C, device=x.device, dtype=torch.float32)
     rstd = torch.empty(N * C, device=x.device, dtype=torch.float32)
     e0 = AUX_TIMER.begin()
-    call("dsgan_instnorm_fwd", ptr(x), xbs, ptr(scale), ptr(res), rbs, ptr(y4), ybs, ptr(mean),
-         ptr(rstd), N, C, H * W, ACT[act], LRELU_SLOPE, IN_EPS, stream())
+    call("dsgan_instnorm_fwd_ws", ptr(x), xbs, ptr(scale), ptr(res), rbs, ptr(y4), ybs, ptr(mean),
+         ptr(rstd), N, C, H * W, ACT[act], LRELU_SLOPE, IN_EPS, *wsa(_in_ws(N, C, H * W, x)), stream())
     AUX_TIMER.end(e0, 0.0, ("in_fwd", N, C, H, W, act, res is not None), "instnorm", (3 if res is not None else 2) * _nb(x))
     return y4, mean, rstd
 
@@ -1267,9 +1273,9 @@ def instnorm_bwd_raw(dy, x, scale, res, mean, rstd, act, want_dres, want_dscale)
     dres = _empty(N, C, H, W, x) if want_dres else None
     dscale = torch.empty(N * C, device=x.device, dtype=torch.float32) if want_dscale else None
     e0 = AUX_TIMER.begin()
-    call("dsgan_instnorm_bwd", ptr(dy), dybs, ptr(x), xbs, ptr(scale), ptr(res), rbs, ptr(mean),
+    call("dsgan_instnorm_bwd_ws", ptr(dy), dybs, ptr(x), xbs, ptr(scale), ptr(res), rbs, ptr(mean),
          ptr(rstd), ptr(dx), C * H * W, ptr(dres), C * H * W, ptr(dscale), N, C, H * W, ACT[act],
-         LRELU_SLOPE, IN_EPS, stream())
+         LRELU_SLOPE, IN_EPS, *wsa(_in_ws(N, C, H * W, x)), stream())
     AUX_TIMER.end(e0, 0.0, ("in_bwd", N, C, H, W, act, res is not None), "instnorm",
                   (3 + (res is not None) + want_dres) * _nb(x))
     return dx, dres, dscale

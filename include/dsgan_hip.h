@@ -369,6 +369,19 @@ int dsgan_instnorm_bwd(const float* dy, long dy_bs, const float* x, long x_bs, c
                        const float* res, long res_bs, const float* mean, const float* rstd,
                        float* dx, long dx_bs, float* dres, long dres_bs, float* dscale, int N,
                        int C, int HW, int act, float slope, float eps, hipStream_t stream);
+/* The same two with scratch (ws_elems fp32 elements, at least dsgan_instnorm_workspace(N, C, HW)):
+ * fewer than 128 planes of >= 16K pixels (the 3-channel block at 256^2) are split over several
+ * workgroups per plane, with the plane statistics summed from per-chunk partials in a fixed order.
+ * Other shapes need no scratch and run the kernels above. */
+long dsgan_instnorm_workspace(int N, int C, int HW);
+int dsgan_instnorm_fwd_ws(const float* x, long x_bs, const float* scale, const float* res, long res_bs,
+                          float* y, long y_bs, float* mean, float* rstd, int N, int C, int HW, int act,
+                          float slope, float eps, float* ws, long ws_elems, hipStream_t stream);
+int dsgan_instnorm_bwd_ws(const float* dy, long dy_bs, const float* x, long x_bs, const float* scale,
+                          const float* res, long res_bs, const float* mean, const float* rstd,
+                          float* dx, long dx_bs, float* dres, long dres_bs, float* dscale, int N,
+                          int C, int HW, int act, float slope, float eps, float* ws, long ws_elems,
+                          hipStream_t stream);
 /* Backward with dx stored in the library's 16-bit half type (dxh, batch stride dxh_bs elements,
  * 8-byte aligned) plus dxsum[n*C + c] = sum over the plane of the fp32 dx (nullable); no scale.
  * The ConvTranspose2d that feeds each decoder InstanceNorm (upSample :61-66, OriginMLKA :150-152)

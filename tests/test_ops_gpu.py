@@ -223,7 +223,10 @@ def test_instnorm_bf16_output(half, N, C, HW):
     from dsgan_hip._lib import call, ptr, stream
     g = torch.Generator().manual_seed(C + HW)
     d = (torch.randn(N, C, 1, HW, generator=g) * 3 - 1).to(DEV)
-    y32, m32, r32 = HF.instnorm_raw(d)
+    # the one-workgroup-per-plane fp32 forward (dsgan_instnorm_fwd; instnorm_raw splits few planes)
+    y32, m32, r32 = torch.empty_like(d), torch.empty(N * C, device=DEV), torch.empty(N * C, device=DEV)
+    call("dsgan_instnorm_fwd", ptr(d), C * HW, None, None, 0, ptr(y32), C * HW, ptr(m32), ptr(r32), N, C, HW, 0, 0.2,
+         1e-5, stream())
     yb = torch.empty((N, C, 1, HW), device=DEV, dtype=_hdt(half))
     m, r = torch.empty(N * C, device=DEV), torch.empty(N * C, device=DEV)
     call("dsgan_instnorm_fwd_bf16", ptr(d), C * HW, ptr(yb), C * HW, ptr(m), ptr(r), N, C, HW, 1e-5, stream())
@@ -472,7 +475,10 @@ def test_dwconv_accumulate(K, H, W):
 @pytest.mark.parametrize("res", [False, True])
 # sizes cover every kernel variant: scalar (HW % 4 != 0), float4 wave-per-plane (<= 1K, ragged
 # tail), 256-thread cached (<= 4K, <= 16K), 1024-thread cached 64K planes, streaming (> 64K)
+# ... and the split forms for < 128 planes of >= 16K pixels (the last three shapes; their 128-plane
+# twins take the one-workgroup kernels)
 @pytest.mark.parametrize("N,C,H,W", [(2, 3, 4, 4), (2, 5, 33, 31), (1, 2, 80, 80), (2, 4, 16, 16), (2, 3, 36, 20),
+                                     (1, 128, 128, 128), (1, 128, 256, 256), (1, 128, 256, 260),
                                      (1, 2, 128, 128), (1, 2, 256, 256), (1, 1, 256, 260)])
 def test_instance_norm(act, res, N, C, H, W):
     from dsgan_hip import functional as HF
@@ -491,7 +497,14 @@ def test_instance_norm(act, res, N, C, H, W):
     assert rel(y, y_ref) < 1e-5
     assert rel(xd.grad, xr.grad) < 1e-4
     if res:
-        assert rel(rd.grad, rr.grad) < 1e-5
+        got, ref = rd.grad.cpu(), rr.grad
+        if act == "lrelu":
+            # LeakyReLU's slope switches at xhat + r = 0: elements within rounding of the kink may take
+            # the other slope in either implementation (the 8.5M-element shapes hit a few)
+            z = F.instance_norm(x.double(), eps=1e-5) + r.double()
+            keep = z.abs() > 1e-5
+            got, ref = got[keep], ref[keep]
+        assert rel(got, ref) < 1e-5
 
 
 @pytest.mark.parametrize("k,W", [(2, 48), (2, 50), (4, 48), (8, 48), (16, 48)])
@@ -940,11 +953,14 @@ def test_instnorm_bwd_h_is_rounded_fp32_backward(half, act, res, N, C, H, W):
     dy = torch.randn(N, C, H, W, generator=g).to(DEV)
     r = torch.randn(N, C, H, W, generator=g).to(DEV) if res else None
     _, mean, rstd = HF.instnorm_raw(x, None, r, act)
-    dx32, dres32, _ = HF.instnorm_bwd_raw(dy, x, None, r, mean, rstd, act, res, False)
+    # the one-workgroup-per-plane fp32 backward (dsgan_instnorm_bwd; instnorm_bwd_raw splits few planes)
+    HW = H * W
+    dx32, dres32 = torch.empty_like(x), (torch.empty_like(x) if res else None)
+    call("dsgan_instnorm_bwd", ptr(dy), C * HW, ptr(x), C * HW, None, ptr(r), C * HW, ptr(mean), ptr(rstd), ptr(dx32),
+         C * HW, ptr(dres32), C * HW, None, N, C, HW, HF.ACT[act], 0.2, 1e-5, stream())
     dxh = torch.empty((N, C, H, W), device=DEV, dtype=_hdt(half))
     dsum = torch.empty(N * C, device=DEV)
     dres = torch.empty_like(x) if res else None
-    HW = H * W
     call("dsgan_instnorm_bwd_h", ptr(dy), C * HW, ptr(x), C * HW, ptr(r), C * HW, ptr(mean), ptr(rstd), ptr(dxh),
          C * HW, ptr(dsum), ptr(dres), C * HW, N, C, HW, HF.ACT[act], 0.2, 1e-5, stream())
     torch.cuda.synchronize()

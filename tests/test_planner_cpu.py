@@ -255,6 +255,16 @@ def test_conv_family_needs_within_queries(lib):
         check(lib, lambda ws, n: lib.dsgan_dwconv_multi_wgrad(A, 4 * q4 * H * H, A, 4 * q4 * H * H, A, A, A, A, A, A,
                                                               A, A, N, q4, H, H, ws, n, None),
               q, (), (), ("dwconv_multi", N, q4, H))
+    n_split = 0
+    for (N, C, HW) in [(16, 3, 65536), (16, 64, 65536), (1, 2, 16384), (2, 5, 20000), (4, 8, 4096)]:
+        q = lib.dsgan_instnorm_workspace(N, C, HW)
+        n_split += check(lib, lambda ws, n: lib.dsgan_instnorm_fwd_ws(A, C * HW, None, A, C * HW, A, C * HW, A, A, N, C,
+                                                                      HW, 1, 0.2, 1e-5, ws, n, None),
+                         q, (), (), ("instnorm_fwd", N, C, HW)) > 0
+        check(lib, lambda ws, n: lib.dsgan_instnorm_bwd_ws(A, C * HW, A, C * HW, None, None, 0, A, A, A, C * HW, A,
+                                                           C * HW, None, N, C, HW, 1, 0.2, 1e-5, ws, n, None),
+              q, (), (), ("instnorm_bwd", N, C, HW))
+    assert n_split == 3
     check(lib, lambda ws, n: lib.dsgan_ca_bwd(A, A, A, A, A, A, A, A, A, A, A, A, A, 16, 256, 16, ws, n, None),
           16 * (2 * 16 * 256 + 1), (), (), "ca_bwd")
     check(lib, lambda ws, n: lib.dsgan_channel_sum(A, 64 * 1024, A, 16, 64, 1024, ws, n, None), 16 * 64, (), (),

@@ -3,9 +3,17 @@
 backward with bf16 g / dz written for the pwgemm weight-grads.
 
     python tools/mlp_micro.py            # DSGAN_HIP_LIB=<other .so> to time another build
+    python tools/mlp_micro.py --libs a.so,b.so,a.so   # builds interleaved, one process each
 """
-import os, sys
+import os, subprocess, sys
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if len(sys.argv) > 2 and sys.argv[1] == "--libs":
+    # A/B of builds: one child process per listed library, in order (this parent never touches the GPU)
+    rc = 0
+    for lib_path in sys.argv[2].split(","):
+        env = dict(os.environ, DSGAN_HIP_LIB=os.path.join(REPO, lib_path))
+        rc |= subprocess.run([sys.executable, "-u", os.path.abspath(__file__)], env=env).returncode
+    sys.exit(rc)
 sys.path[:0] = [REPO, os.path.join(REPO, "ds-gan_amd")]
 import torch
 from dsgan_hip._lib import call, ptr, stream
