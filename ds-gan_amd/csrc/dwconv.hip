@@ -278,6 +278,14 @@ __device__ __forceinline__ void dw_fwd_body(const float* __restrict__ x, long x_
         for (int i = 0; i < 4; ++i) acc[s][i] = fmaf(wv[kh * K + kw], cur[i + kw + T::OFF], acc[s][i]);
     }
     __builtin_amdgcn_sched_barrier(0);
+    // pin this row's FMAs here: otherwise the compiler sinks every FMA below the last row read and
+    // computes one output row at a time, which keeps all R + K - 1 window rows live (127 VGPRs,
+    // 4 waves per SIMD; pinned: 44 VGPRs, the LDS-bound 7 workgroups per CU).  Same FMA order per
+    // accumulator, same bits.
+#pragma unroll
+    for (int s = 0; s < R; ++s)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) asm volatile("" : "+v"(acc[s][i])::"memory");
 #pragma unroll
     for (int i = 0; i < 12; ++i) cur[i] = nxt[i];
   }

@@ -52,17 +52,20 @@ __device__ __forceinline__ hx4<T16> mcvt4(float4 v) {
 
 // GELU of the bf16 path: gelu_fast2 / gelu_pair_fast2 (common.h, A&S 7.1.26 erfc on packed fp32,
 // two elements per instruction; the exact branch-free erf of gelu_f costs ~40 VALU per element).
-// MLP_PK_GELU (build-time A/B): 1 = the packed forms, 0 = gelu_fast1x2 / gelu_pair_fast1x2 (unpacked,
-// same bits).  These GELUs sit between the chunk's MFMAs.
-#ifndef MLP_PK_GELU
-#define MLP_PK_GELU 1
-#endif
-__device__ __forceinline__ f32x2 mlp_gelu2(f32x2 z) { return MLP_PK_GELU ? gelu_fast2(z) : gelu_fast1x2(z); }
+// Packed (gelu_fast2 / gelu_pair_fast2) or unpacked (gelu_fast1x2 / gelu_pair_fast1x2) fp32 GELU:
+// the same operations and bits; which issues faster depends on the MFMAs around it.  In-process
+// build A/B (tools/mlp_micro.py --libs, profiles/r04/mlp_micro_pk.txt): the unpacked form is 8 % /
+// 4 % faster in the weight-grad kernel at (C, P) = (256, 128) / (128, 256), where each hidden
+// element's GELU sits between more MFMAs; every other kernel and shape is 1-3 % faster packed.
+template <bool PK>
+__device__ __forceinline__ f32x2 mlp_gelu2(f32x2 z) { return PK ? gelu_fast2(z) : gelu_fast1x2(z); }
+template <bool PK>
 __device__ __forceinline__ void mlp_gelu_pair2(f32x2 z, f32x2& g, f32x2& gp) {
-  if (MLP_PK_GELU) gelu_pair_fast2(z, g, gp);
+  if (PK) gelu_pair_fast2(z, g, gp);
   else gelu_pair_fast1x2(z, g, gp);
 }
-__device__ __forceinline__ f32x2 mlp_mul2(f32x2 a, f32x2 b) { return MLP_PK_GELU ? a * b : f32x2{a.x * b.x, a.y * b.y}; }
+template <bool PK>
+__device__ __forceinline__ f32x2 mlp_mul2(f32x2 a, f32x2 b) { return PK ? a * b : f32x2{a.x * b.x, a.y * b.y}; }
 
 struct MlpArgs {
   const void* h; long h_bs;         // [nb][C][HW]   block activation after InstanceNorm (fp32, or bf16 if h_bf16)
@@ -367,7 +370,7 @@ __global__ __launch_bounds__(512, MINB) void mlp_fwd_kernel(MlpArgs g) {
       mbf16x8 gb;
 #pragma unroll
       for (int i = 0; i < 8; i += 2) {
-        const f32x2 v = mlp_gelu2(f32x2{zacc[8 * kk + i], zacc[8 * kk + i + 1]});
+        const f32x2 v = mlp_gelu2<true>(f32x2{zacc[8 * kk + i], zacc[8 * kk + i + 1]});
         gb[i] = (T16)v.x;
         gb[i + 1] = (T16)v.y;
       }
@@ -504,7 +507,7 @@ __global__ __launch_bounds__(NW * 64, MINB) void mlp_fwd_lds_kernel(MlpArgs g) {
           mbf16x4 v;
 #pragma unroll
           for (int e = 0; e < 4; e += 2) {
-            const f32x2 gv = mlp_gelu2(f32x2{zacc[i][t][4 * q + e], zacc[i][t][4 * q + e + 1]});
+            const f32x2 gv = mlp_gelu2<true>(f32x2{zacc[i][t][4 * q + e], zacc[i][t][4 * q + e + 1]});
             v[e] = (T16)gv.x;
             v[e + 1] = (T16)gv.y;
           }
@@ -678,8 +681,8 @@ __global__ __launch_bounds__(512, MINB) void mlp_dh_kernel(MlpArgs g) {
 #pragma unroll
       for (int i = 0; i < 8; i += 2) {
         f32x2 gv, gp;
-        mlp_gelu_pair2(f32x2{zacc[8 * kk + i], zacc[8 * kk + i + 1]}, gv, gp);
-        const f32x2 dz = mlp_mul2(f32x2{tacc[8 * kk + i], tacc[8 * kk + i + 1]}, gp);
+        mlp_gelu_pair2<true>(f32x2{zacc[8 * kk + i], zacc[8 * kk + i + 1]}, gv, gp);
+        const f32x2 dz = mlp_mul2<true>(f32x2{tacc[8 * kk + i], tacc[8 * kk + i + 1]}, gp);
         dzb[i] = (T16)dz.x;
         dzb[i + 1] = (T16)dz.y;
       }
@@ -857,8 +860,8 @@ __global__ __launch_bounds__(NW * 64, MINB) void mlp_bwd_kernel(MlpArgs g) {
 #pragma unroll
           for (int e = 0; e < 4; e += 2) {
             f32x2 gv, gp;
-            mlp_gelu_pair2(f32x2{zacc[i][t][4 * q + e], zacc[i][t][4 * q + e + 1]}, gv, gp);
-            const f32x2 dz = mlp_mul2(f32x2{tacc[i][t][4 * q + e], tacc[i][t][4 * q + e + 1]}, gp);
+            mlp_gelu_pair2<true>(f32x2{zacc[i][t][4 * q + e], zacc[i][t][4 * q + e + 1]}, gv, gp);
+            const f32x2 dz = mlp_mul2<true>(f32x2{tacc[i][t][4 * q + e], tacc[i][t][4 * q + e + 1]}, gp);
             gv4[e] = (T16)gv.x; gv4[e + 1] = (T16)gv.y;
             dv4[e] = (T16)dz.x; dv4[e + 1] = (T16)dz.y;
           }
@@ -1083,8 +1086,8 @@ __global__ __launch_bounds__(256, 1) void mlp_bwd_dma_kernel(MlpArgs g) {
 #pragma unroll
       for (int e = 0; e < 4; e += 2) {
         f32x2 gv, gp;
-        mlp_gelu_pair2(f32x2{zacc[4 * q + e], zacc[4 * q + e + 1]}, gv, gp);
-        const f32x2 dz = mlp_mul2(f32x2{tacc[4 * q + e], tacc[4 * q + e + 1]}, gp);
+        mlp_gelu_pair2<true>(f32x2{zacc[4 * q + e], zacc[4 * q + e + 1]}, gv, gp);
+        const f32x2 dz = mlp_mul2<true>(f32x2{tacc[4 * q + e], tacc[4 * q + e + 1]}, gp);
         gv4[e] = (T16)gv.x; gv4[e + 1] = (T16)gv.y;
         dv4[e] = (T16)dz.x; dv4[e + 1] = (T16)dz.y;
       }
@@ -1327,8 +1330,8 @@ __global__ __launch_bounds__(NW * 64, MINB) void mlp_wgrad_kernel(MlpArgs g) {
 #pragma unroll
           for (int e = 0; e < 4; e += 2) {
             f32x2 gv, gp;
-            mlp_gelu_pair2(f32x2{zacc[i][t][4 * q + e], zacc[i][t][4 * q + e + 1]}, gv, gp);
-            const f32x2 dz = mlp_mul2(f32x2{tacc[i][t][4 * q + e], tacc[i][t][4 * q + e + 1]}, gp);
+            mlp_gelu_pair2<(C + P < 384)>(f32x2{zacc[i][t][4 * q + e], zacc[i][t][4 * q + e + 1]}, gv, gp);
+            const f32x2 dz = mlp_mul2<(C + P < 384)>(f32x2{tacc[i][t][4 * q + e], tacc[i][t][4 * q + e + 1]}, gp);
             gv4[e] = (T16)gv.x; gv4[e + 1] = (T16)gv.y;
             dv4[e] = (T16)dz.x; dv4[e + 1] = (T16)dz.y;
             bacc[i][4 * q + e] += (float)dv4[e];
