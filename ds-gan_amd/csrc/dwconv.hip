@@ -344,7 +344,7 @@ __global__ __launch_bounds__(256, 3) void dwconv_multi_fwd(const float* __restri
 // the workgroup once, after all of its images.
 // Weight-grad partials of channel c, tile bx, image split `split` (slot split * ntiles + bx).
 // `tile` = LH * LP floats of LDS, `red` = 4 * (K*K + 1) floats.
-template <int K, int TWT, int THT, int R>
+template <int K, int TWT, int THT, int R, bool PF = false>
 __device__ __forceinline__ void dw_wgrad_body(const float* __restrict__ dy, long dy_bs, const float* __restrict__ x,
                                               long x_bs, float* __restrict__ ws, int N, int C, int H, int W,
                                               int tiles_w, int nper, int bx, int c, int split, int ntiles, float* tile,
@@ -358,20 +358,64 @@ __device__ __forceinline__ void dw_wgrad_body(const float* __restrict__ dy, long
 #pragma unroll
   for (int i = 0; i < K * K; ++i) acc[i] = 0.f;
   float bacc = 0.f;
-  for (int n = n0; n < n1; ++n) {
-    __syncthreads();
-    dw_stage<K, TWT, THT, R>(tile, x + (long)n * x_bs + (long)c * H * W, H, W, th0, tw0);
-    float g[R][4];
+  // PF: the next image's halo tile and dy block are loaded into registers while this image's FMAs
+  // run (the loop otherwise waits one memory latency per image); same values, same bits
+  constexpr int ITEMS = (T::LH * T::F4 + 255) / 256;
+  float4 pv[PF ? ITEMS : 1], pg[PF ? R : 1];
+  auto issue = [&](int n) {
+    const float* xp = x + (long)n * x_bs + (long)c * H * W;
+#pragma unroll
+    for (int j = 0; j < ITEMS; ++j) {
+      const int i = threadIdx.x + j * 256;
+      const int r = i / T::F4, q = i - r * T::F4;
+      const int ih = th0 - T::P + r, iw = tw0 - 4 + 4 * q;
+      pv[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (i < T::LH * T::F4 && (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W)
+        pv[j] = *reinterpret_cast<const float4*>(xp + (long)ih * W + iw);
+    }
     const float* gp = dy + (long)n * dy_bs + (long)c * H * W + tw0 + 4 * tx;
 #pragma unroll
     for (int s = 0; s < R; ++s) {
       const int oh = th0 + R * ty + s;
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (oh < H) v = *reinterpret_cast<const float4*>(gp + (long)oh * W);
-      g[s][0] = v.x; g[s][1] = v.y; g[s][2] = v.z; g[s][3] = v.w;
-      bacc += (v.x + v.y) + (v.z + v.w);
+      pg[s] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (oh < H) pg[s] = *reinterpret_cast<const float4*>(gp + (long)oh * W);
+    }
+  };
+  if constexpr (PF) {
+    if (n0 < n1) issue(n0);
+  }
+  for (int n = n0; n < n1; ++n) {
+    __syncthreads();
+    float g[R][4];
+    if constexpr (PF) {
+#pragma unroll
+      for (int j = 0; j < ITEMS; ++j) {
+        const int i = threadIdx.x + j * 256;
+        const int r = i / T::F4, q = i - r * T::F4;
+        if (i < T::LH * T::F4) *reinterpret_cast<float4*>(tile + r * T::LP + 4 * q) = pv[j];
+      }
+#pragma unroll
+      for (int s = 0; s < R; ++s) {
+        const float4 v = pg[s];
+        g[s][0] = v.x; g[s][1] = v.y; g[s][2] = v.z; g[s][3] = v.w;
+        bacc += (v.x + v.y) + (v.z + v.w);
+      }
+    } else {
+      dw_stage<K, TWT, THT, R>(tile, x + (long)n * x_bs + (long)c * H * W, H, W, th0, tw0);
+      const float* gp = dy + (long)n * dy_bs + (long)c * H * W + tw0 + 4 * tx;
+#pragma unroll
+      for (int s = 0; s < R; ++s) {
+        const int oh = th0 + R * ty + s;
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (oh < H) v = *reinterpret_cast<const float4*>(gp + (long)oh * W);
+        g[s][0] = v.x; g[s][1] = v.y; g[s][2] = v.z; g[s][3] = v.w;
+        bacc += (v.x + v.y) + (v.z + v.w);
+      }
     }
     __syncthreads();
+    if constexpr (PF) {
+      if (n + 1 < n1) issue(n + 1);
+    }
     float cur[12], nxt[12];
     dw_row<K>(cur, tile + (R * ty) * T::LP + 4 * tx);
 #pragma unroll
@@ -410,8 +454,8 @@ __device__ __forceinline__ void dw_wgrad_body(const float* __restrict__ dy, long
   }
 }
 
-template <int K, int TWT, int THT, int R>
-__global__ __launch_bounds__(256, 4) void dwconv_wgrad_v2(const float* __restrict__ dy, long dy_bs,
+template <int K, int TWT, int THT, int R, bool PF = false>
+__global__ __launch_bounds__(256, PF ? 3 : 4) void dwconv_wgrad_v2(const float* __restrict__ dy, long dy_bs,
                                                        const float* __restrict__ x, long x_bs,
                                                        float* __restrict__ ws,
                                                        int N, int C, int H, int W, int tiles_w, int nper, int tiles) {
@@ -419,8 +463,8 @@ __global__ __launch_bounds__(256, 4) void dwconv_wgrad_v2(const float* __restric
   __shared__ __attribute__((aligned(16))) float tile[T::LH * T::LP];
   __shared__ float red[4 * (K * K + 1)];
   const int t = dw_xcd_index(), cs = t / tiles, split = cs / C;   // t = (split * C + c) * tiles + tile
-  dw_wgrad_body<K, TWT, THT, R>(dy, dy_bs, x, x_bs, ws, N, C, H, W, tiles_w, nper, t - cs * tiles, cs - split * C, split,
-                                tiles, tile, red);
+  dw_wgrad_body<K, TWT, THT, R, PF>(dy, dy_bs, x, x_bs, ws, N, C, H, W, tiles_w, nper, t - cs * tiles, cs - split * C,
+                                    split, tiles, tile, red);
 }
 
 // The four MidMLKA quarters' weight-grads in one launch: blockIdx.z = quarter * nsplit + split.
@@ -482,6 +526,12 @@ static long dw_wgrad_v2_plan(int N, int C, int H, int W, int* nsplit_out, int* n
   return (long)tw * th * nsplit;
 }
 
+#ifndef DW_WG_PF
+#define DW_WG_PF 0
+#endif
+#ifndef DW_WG_R7
+#define DW_WG_R7 8
+#endif
 template <int K, int TWT, int THT, int R>
 static long dw_wgrad_v2(const float* dy, long dy_bs, const float* x, long x_bs, float* ws, int N, int C, int H, int W,
                         hipStream_t st) {
@@ -490,7 +540,7 @@ static long dw_wgrad_v2(const float* dy, long dy_bs, const float* x, long x_bs, 
   int nsplit, nper;
   const long G = dw_wgrad_v2_plan<K, TWT, THT, R>(N, C, H, W, &nsplit, &nper);
   if (ws)
-    hipLaunchKernelGGL((dwconv_wgrad_v2<K, TWT, THT, R>), dim3(tw * th * C * nsplit), dim3(256), 0, st, dy, dy_bs, x,
+    hipLaunchKernelGGL((dwconv_wgrad_v2<K, TWT, THT, R, (bool)DW_WG_PF>), dim3(tw * th * C * nsplit), dim3(256), 0, st, dy, dy_bs, x,
                        x_bs, ws, N, C, H, W, tw, nper, tw * th);
   return G;
 }
@@ -509,7 +559,7 @@ static void dw_fwd_dispatch(int cfg, const float* x, long x_bs, const float* w, 
 template <int K>
 static long dw_wgrad_dispatch(int cfg, const float* dy, long dy_bs, const float* x, long x_bs, float* ws,
                               int N, int C, int H, int W, hipStream_t st) {
-  constexpr int R1 = K >= 9 ? 2 : 8, R2 = K >= 9 ? 2 : 4;
+  constexpr int R1 = K >= 9 ? 2 : K == 7 ? DW_WG_R7 : 8, R2 = K >= 9 ? 2 : 4;
   if (cfg == 1) return dw_wgrad_v2<K, 32, 8, R1>(dy, dy_bs, x, x_bs, ws, N, C, H, W, st);
   if (cfg == 2) return dw_wgrad_v2<K, 16, 16, R2>(dy, dy_bs, x, x_bs, ws, N, C, H, W, st);
   return dw_wgrad_v2<K, 8, 32, 1>(dy, dy_bs, x, x_bs, ws, N, C, H, W, st);
