@@ -289,6 +289,7 @@ __device__ __forceinline__ void dw_fwd_body(const float* __restrict__ x, long x_
 #pragma unroll
     for (int i = 0; i < 12; ++i) cur[i] = nxt[i];
   }
+  // (loading the accumulated values before the FMAs instead measured 2.5 % slower: dw_micro A/B)
   float* yp = y + (long)n * y_bs + (long)c * H * W + tw0 + 4 * tx;
 #pragma unroll
   for (int s = 0; s < R; ++s) {
@@ -526,13 +527,7 @@ static long dw_wgrad_v2_plan(int N, int C, int H, int W, int* nsplit_out, int* n
   return (long)tw * th * nsplit;
 }
 
-#ifndef DW_WG_PF
-#define DW_WG_PF 0
-#endif
-#ifndef DW_WG_R7
-#define DW_WG_R7 8
-#endif
-template <int K, int TWT, int THT, int R>
+template <int K, int TWT, int THT, int R, bool PF = false>
 static long dw_wgrad_v2(const float* dy, long dy_bs, const float* x, long x_bs, float* ws, int N, int C, int H, int W,
                         hipStream_t st) {
   using T = DwTile<K, TWT, THT, R>;
@@ -540,7 +535,7 @@ static long dw_wgrad_v2(const float* dy, long dy_bs, const float* x, long x_bs, 
   int nsplit, nper;
   const long G = dw_wgrad_v2_plan<K, TWT, THT, R>(N, C, H, W, &nsplit, &nper);
   if (ws)
-    hipLaunchKernelGGL((dwconv_wgrad_v2<K, TWT, THT, R, (bool)DW_WG_PF>), dim3(tw * th * C * nsplit), dim3(256), 0, st, dy, dy_bs, x,
+    hipLaunchKernelGGL((dwconv_wgrad_v2<K, TWT, THT, R, PF>), dim3(tw * th * C * nsplit), dim3(256), 0, st, dy, dy_bs, x,
                        x_bs, ws, N, C, H, W, tw, nper, tw * th);
   return G;
 }
@@ -556,10 +551,29 @@ static void dw_fwd_dispatch(int cfg, const float* x, long x_bs, const float* w, 
 }
 
 // ws == NULL: only the partial-slot count per channel is returned (workspace query)
+// Workgroups that walk >= 8 images prefetch the next image's tile and dy block under the FMAs
+// (dw_wgrad_body PF; the 7x7 128-wide tiles then take 4 rows per thread so the prefetch registers
+// fit).  Build A/B at the step's shapes (profiles/r04/dw_micro_wgpf.txt): 289 -> 252 us at
+// C=128 @ 256^2, 165 -> 144 at 256 @ 128^2, 54 -> 46 at 1024 @ 32^2; with 2-4 images per workgroup
+// the lower occupancy lost 8-12 %, so those keep the plain loop.
+constexpr int DW_PF_MIN_IMAGES = 8;
+template <int K, int TWT, int THT, int R, int RPF>
+static long dw_wgrad_pick(const float* dy, long dy_bs, const float* x, long x_bs, float* ws, int N, int C, int H,
+                          int W, hipStream_t st) {
+  int nsplit, nper;
+  dw_wgrad_v2_plan<K, TWT, THT, RPF>(N, C, H, W, &nsplit, &nper);
+  if (nper >= DW_PF_MIN_IMAGES) return dw_wgrad_v2<K, TWT, THT, RPF, true>(dy, dy_bs, x, x_bs, ws, N, C, H, W, st);
+  return dw_wgrad_v2<K, TWT, THT, R>(dy, dy_bs, x, x_bs, ws, N, C, H, W, st);
+}
 template <int K>
 static long dw_wgrad_dispatch(int cfg, const float* dy, long dy_bs, const float* x, long x_bs, float* ws,
                               int N, int C, int H, int W, hipStream_t st) {
-  constexpr int R1 = K >= 9 ? 2 : K == 7 ? DW_WG_R7 : 8, R2 = K >= 9 ? 2 : 4;
+  constexpr int R1 = K >= 9 ? 2 : 8, R2 = K >= 9 ? 2 : 4;
+  if constexpr (K == 7) {
+    if (cfg == 1) return dw_wgrad_pick<7, 32, 8, R1, 4>(dy, dy_bs, x, x_bs, ws, N, C, H, W, st);
+    if (cfg == 2) return dw_wgrad_pick<7, 16, 16, R2, R2>(dy, dy_bs, x, x_bs, ws, N, C, H, W, st);
+    return dw_wgrad_pick<7, 8, 32, 1, 1>(dy, dy_bs, x, x_bs, ws, N, C, H, W, st);
+  }
   if (cfg == 1) return dw_wgrad_v2<K, 32, 8, R1>(dy, dy_bs, x, x_bs, ws, N, C, H, W, st);
   if (cfg == 2) return dw_wgrad_v2<K, 16, 16, R2>(dy, dy_bs, x, x_bs, ws, N, C, H, W, st);
   return dw_wgrad_v2<K, 8, 32, 1>(dy, dy_bs, x, x_bs, ws, N, C, H, W, st);
