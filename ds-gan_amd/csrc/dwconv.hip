@@ -469,8 +469,8 @@ __global__ __launch_bounds__(256, PF ? 3 : 4) void dwconv_wgrad_v2(const float* 
 }
 
 // The four MidMLKA quarters' weight-grads in one launch: blockIdx.z = quarter * nsplit + split.
-template <int TWT, int THT, int R>
-__global__ __launch_bounds__(256, 4) void dwconv_multi_wgrad(const float* __restrict__ dy, long dy_bs,
+template <int TWT, int THT, int R, bool PF = false>
+__global__ __launch_bounds__(256, PF ? 3 : 4) void dwconv_multi_wgrad(const float* __restrict__ dy, long dy_bs,
                                                              const float* __restrict__ x, long x_bs, DwQuad q4,
                                                              int N, int q, int H, int W, int tiles_w, int nper,
                                                              int nsplit) {
@@ -480,10 +480,10 @@ __global__ __launch_bounds__(256, 4) void dwconv_multi_wgrad(const float* __rest
   const int qi = blockIdx.z / nsplit, split = blockIdx.z - qi * nsplit;
   const long co = (long)qi * q * H * W;
   switch (qi) {
-    case 0: dw_wgrad_body<3, TWT, THT, R>(dy + co, dy_bs, x + co, x_bs, q4.ws[0], N, q, H, W, tiles_w, nper, blockIdx.x, blockIdx.y, split, gridDim.x, tile, red); break;
-    case 1: dw_wgrad_body<5, TWT, THT, R>(dy + co, dy_bs, x + co, x_bs, q4.ws[1], N, q, H, W, tiles_w, nper, blockIdx.x, blockIdx.y, split, gridDim.x, tile, red); break;
-    case 2: dw_wgrad_body<7, TWT, THT, R>(dy + co, dy_bs, x + co, x_bs, q4.ws[2], N, q, H, W, tiles_w, nper, blockIdx.x, blockIdx.y, split, gridDim.x, tile, red); break;
-    default: dw_wgrad_body<9, TWT, THT, R>(dy + co, dy_bs, x + co, x_bs, q4.ws[3], N, q, H, W, tiles_w, nper, blockIdx.x, blockIdx.y, split, gridDim.x, tile, red); break;
+    case 0: dw_wgrad_body<3, TWT, THT, R, PF>(dy + co, dy_bs, x + co, x_bs, q4.ws[0], N, q, H, W, tiles_w, nper, blockIdx.x, blockIdx.y, split, gridDim.x, tile, red); break;
+    case 1: dw_wgrad_body<5, TWT, THT, R, PF>(dy + co, dy_bs, x + co, x_bs, q4.ws[1], N, q, H, W, tiles_w, nper, blockIdx.x, blockIdx.y, split, gridDim.x, tile, red); break;
+    case 2: dw_wgrad_body<7, TWT, THT, R, PF>(dy + co, dy_bs, x + co, x_bs, q4.ws[2], N, q, H, W, tiles_w, nper, blockIdx.x, blockIdx.y, split, gridDim.x, tile, red); break;
+    default: dw_wgrad_body<9, TWT, THT, R, PF>(dy + co, dy_bs, x + co, x_bs, q4.ws[3], N, q, H, W, tiles_w, nper, blockIdx.x, blockIdx.y, split, gridDim.x, tile, red); break;
   }
 }
 
@@ -622,9 +622,16 @@ static long dw_multi_wgrad_run(const float* dy, long dy_bs, const float* x, long
   const int tw = W / T::TW, th = (H + T::TH - 1) / T::TH;
   int nsplit, nper;
   const long G = dw_wgrad_v2_plan<9, TWT, THT, R>(N, q, H, W, &nsplit, &nper, 256);
-  if (q4)
-    hipLaunchKernelGGL((dwconv_multi_wgrad<TWT, THT, R>), dim3(tw * th, q, 4 * nsplit), dim3(256), 0, st, dy, dy_bs,
-                       x, x_bs, *q4, N, q, H, W, tw, nper, nsplit);
+  if (q4) {
+    // (the next-image prefetch where a workgroup walks >= 8 images: 101 -> 98 us at C = 128 @ 128^2,
+    // profiles/r04/dw_micro_multi_pf.txt; shorter loops lose 2-6 % to the lower occupancy)
+    if (nper >= DW_PF_MIN_IMAGES)
+      hipLaunchKernelGGL((dwconv_multi_wgrad<TWT, THT, R, true>), dim3(tw * th, q, 4 * nsplit), dim3(256), 0, st, dy,
+                         dy_bs, x, x_bs, *q4, N, q, H, W, tw, nper, nsplit);
+    else
+      hipLaunchKernelGGL((dwconv_multi_wgrad<TWT, THT, R, false>), dim3(tw * th, q, 4 * nsplit), dim3(256), 0, st, dy,
+                         dy_bs, x, x_bs, *q4, N, q, H, W, tw, nper, nsplit);
+  }
   return G;
 }
 

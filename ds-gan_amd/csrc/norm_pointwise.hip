@@ -281,9 +281,16 @@ __global__ __launch_bounds__(NT == 64 ? 256 : NT) void instnorm_fwd_v4(INArgs a)
   }
 }
 
-template <int NT, int C4, bool CX>
+// XL (> 0 only with !CX): the first XL of a thread's C4 xhat float4s are parked in LDS between the
+// statistics pass and the output pass instead of being recomputed from a second read of x.  The
+// 64K-pixel planes (NT = 1024, C4 = 16) cannot hold xhat in registers next to g, and a plane of x
+// (256 KB) does not stay in the CU's share of L2, so the second read went to HBM: XL = 8 keeps half
+// of it in 128 KB of LDS (the workgroup is alone on its CU either way).  Same values, same bits.
+template <int NT, int C4, bool CX, int XL = 0>
 __global__ __launch_bounds__(NT == 64 ? 256 : NT) void instnorm_bwd_v4(INBwdArgs a) {
+  static_assert(XL == 0 || (!CX && XL <= C4 && NT > 64), "XL: LDS-parked xhat of the uncached form");
   __shared__ float sh[32];
+  __shared__ float4 xl[XL > 0 ? XL * NT : 1];
   const int plane = blockIdx.x * (NT == 64 ? 4 : 1) + (NT == 64 ? (threadIdx.x >> 6) : 0);
   const int t = NT == 64 ? (threadIdx.x & 63) : threadIdx.x;
   if (plane >= a.N * a.C) return;
@@ -348,6 +355,9 @@ __global__ __launch_bounds__(NT == 64 ? 256 : NT) void instnorm_bwd_v4(INBwdArgs
       if (i < HW4) {
         const float4 xh = xhat(i);
         if constexpr (CX) xv[j] = xh;
+        if constexpr (XL > 0) {
+          if (j < XL) xl[j * NT + t] = xh;
+        }
         gv[j] = grad(i, xh);
         sg += hsum4(gv[j]);
         sgh += (gv[j].x * xh.x + gv[j].y * xh.y) + (gv[j].z * xh.z + gv[j].w * xh.w);
@@ -360,6 +370,7 @@ __global__ __launch_bounds__(NT == 64 ? 256 : NT) void instnorm_bwd_v4(INBwdArgs
       const int i = t + j * NT;
       if (i < HW4) {
         if constexpr (CX) fin(i, gv[j], xv[j], m.x, m.y);
+        else if (XL > 0 && j < XL) fin(i, gv[j], xl[j * NT + t], m.x, m.y);
         else fin(i, gv[j], xhat(i), m.x, m.y);
       }
     }
@@ -408,6 +419,10 @@ __global__ __launch_bounds__(NT == 64 ? 256 : NT) void instnorm_bwd_v4(INBwdArgs
     if (t == 0) a.dxsum[plane] = ds.x;
   }
 }
+
+#ifndef IN_BWD_XL
+#define IN_BWD_XL 8
+#endif
 
 // ---- few-plane forms: one plane split over S workgroups ----
 // The generator's 3-channel block (MixConvNeXtML.py:220-221 at dim 3) normalises N*3 = 48 planes
@@ -1278,7 +1293,7 @@ int dsgan_instnorm_bwd_h(const float* dy, long dy_bs, const float* x, long x_bs,
   else if (HW <= 256 * 64)
     hipLaunchKernelGGL((instnorm_bwd_v4<256, 16, true>), dim3(planes), dim3(256), 0, st, a);
   else if (HW <= 1024 * 64)
-    hipLaunchKernelGGL((instnorm_bwd_v4<1024, 16, false>), dim3(planes), dim3(1024), 0, st, a);
+    hipLaunchKernelGGL((instnorm_bwd_v4<1024, 16, false, IN_BWD_XL>), dim3(planes), dim3(1024), 0, st, a);
   else
     hipLaunchKernelGGL((instnorm_bwd_v4<1024, 0, false>), dim3(planes), dim3(1024), 0, st, a);
   DSG_CHECK_LAUNCH();
@@ -1303,7 +1318,7 @@ int dsgan_instnorm_bwd(const float* dy, long dy_bs, const float* x, long x_bs, c
     else if (HW <= 256 * 64)
       hipLaunchKernelGGL((instnorm_bwd_v4<256, 16, true>), dim3(planes), dim3(256), 0, st, a);
     else if (HW <= 1024 * 64)
-      hipLaunchKernelGGL((instnorm_bwd_v4<1024, 16, false>), dim3(planes), dim3(1024), 0, st, a);
+      hipLaunchKernelGGL((instnorm_bwd_v4<1024, 16, false, IN_BWD_XL>), dim3(planes), dim3(1024), 0, st, a);
     else
       hipLaunchKernelGGL((instnorm_bwd_v4<1024, 0, false>), dim3(planes), dim3(1024), 0, st, a);
     DSG_CHECK_LAUNCH();

@@ -44,7 +44,8 @@ def timeit(fn, it=20):
 def digest(*ts):
     h = hashlib.sha1()
     for t in ts:
-        h.update(t.detach().cpu().numpy().tobytes())
+        t = t.detach().cpu()
+        h.update((t.view(torch.int16) if t.dtype == torch.bfloat16 else t).numpy().tobytes())
     return h.hexdigest()[:10]
 
 
@@ -81,15 +82,25 @@ for N, C, H in [(16, 128, 256), (16, 256, 128), (16, 512, 64), (16, 1024, 32), (
     print("C=%4d H=%3d | fwd %7.1f  dgrad %7.1f  wgrad %7.1f us | %s" % (C, H, *t, digest(y, dx, dw, db)), flush=True)
 for N, C, H in [(16, 128, 128), (16, 32, 128), (16, 128, 64), (16, 64, 64), (16, 128, 32)]:
     q, HW = C // 4, H * H
+    torch.manual_seed(C + H)
     x = torch.randn(N, C, H, H, device="cuda")
     wq = [torch.randn(q, 1, k, k, device="cuda") * 0.1 for k in (3, 5, 7, 9)]
     bq = [torch.randn(q, device="cuda") for _ in range(4)]
     y = torch.empty_like(x)
     f = lambda: call("dsgan_dwconv_multi_fwd", ptr(x), C * HW, ptr(wq[0]), ptr(bq[0]), ptr(wq[1]), ptr(bq[1]),
                      ptr(wq[2]), ptr(bq[2]), ptr(wq[3]), ptr(bq[3]), ptr(y), C * HW, N, q, H, H, 0, 0, stream())
-    t = timeit(f)
+    dy = torch.randn(N, C, H, H, device="cuda")
+    gw = [torch.zeros(q, 1, k, k, device="cuda") for k in (3, 5, 7, 9)]
+    gb = [torch.zeros(q, device="cuda") for _ in range(4)]
+    wsp = torch.empty(max(1, L.dsgan_dwconv_multi_wgrad_workspace(N, q, H, H)), device="cuda")
+    fw = lambda: call("dsgan_dwconv_multi_wgrad", ptr(dy), C * HW, ptr(x), C * HW, ptr(gw[0]), ptr(gb[0]), ptr(gw[1]),
+                      ptr(gb[1]), ptr(gw[2]), ptr(gb[2]), ptr(gw[3]), ptr(gb[3]), N, q, H, H, ptr(wsp), wsp.numel(),
+                      stream())
+    t, tw = timeit(f), timeit(fw)
     tot["fwd"] += t
+    tot["wgrad"] += tw
     f()
+    fw()
     torch.cuda.synchronize()
-    print("multi C=%4d H=%3d | fwd %7.1f us | %s" % (C, H, t, digest(y)), flush=True)
+    print("multi C=%4d H=%3d | fwd %7.1f  wgrad %7.1f us | %s" % (C, H, t, tw, digest(y, *gw, *gb)), flush=True)
 print("totals: " + "  ".join("%s %.1f us" % kv for kv in tot.items()), flush=True)

@@ -4,7 +4,7 @@
 #
 # Steps run in order, each under its own time limit; the first failing step ends the call (a GPU
 # fault, abort or time limit leaves nothing else running on the card).  Outputs go to gpurun_out/.
-#   tests[=<pytest -k expr>]  the -m gpu suite, or the subset -k selects   -> gpu_tests.txt
+#   tests[=<pytest -k expr>]  the -m gpu suite, or the subset -k selects (+ for spaces) -> gpu_tests.txt
 #   testfile=<path>[::k]      one test file (optionally -k)                 -> gpu_tests_<name>.txt
 #   smoke                     __graft_entry__.smoke()                       -> smoke.txt
 #   bench[=<bench.py args>]   the bench line ('+' separates arguments)       -> bench.log
@@ -41,7 +41,7 @@ for step in "$@"; do
   case "$name" in
     tests)
       if [ -n "$arg" ]; then
-        run 1200 gpurun_out/gpu_tests.txt python -u -m pytest tests -m gpu -x -q --timeout 600 --timeout-method thread -k "$arg"
+        run 1200 gpurun_out/gpu_tests.txt python -u -m pytest tests -m gpu -x -q --timeout 600 --timeout-method thread -k "${arg//+/ }"
       else
         run 1200 gpurun_out/gpu_tests.txt python -u -m pytest tests -m gpu -x -q --timeout 600 --timeout-method thread
       fi
