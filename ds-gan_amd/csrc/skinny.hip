@@ -377,30 +377,43 @@ __global__ __launch_bounds__(256) void wgrad_small_pw4_kernel(WsArgs a) {
   float acc[S];
 #pragma unroll
   for (int s = 0; s < S; ++s) acc[s] = 0.f;
-  // (b, r) of this thread's first quad, then advanced by 1024 pixels per step (HW % 4 == 0)
+  // (b, r) of this thread's first quad, then advanced by 1024 pixels per quad (HW % 4 == 0).  U quads
+  // per step: all of their loads are issued before the FMAs (one memory latency per U quads instead
+  // of per quad); each accumulator still takes the quads in pixel order (same sums, same bits).
+  constexpr int U = S <= 4 ? 4 : 2;
   long p = p0 + 4 * threadIdx.x;
   int b = (int)(p / HW), r = (int)(p - (long)b * HW);
-  for (; p < p1; p += 1024) {
-    const unsigned xb = (unsigned)((long)b * a.x_bs) + r, gb = (unsigned)((long)b * a.dy_bs) + r;
-    if (SMALL_OUT) {
-      const float4 xv = ld4(rx, (xb + (unsigned)c * HW) * 4u);
+  for (; p < p1; p += 1024 * U) {
+    float4 one[U], many[U][S];
 #pragma unroll
-      for (int s = 0; s < S; ++s) {
-        if (s >= a.nsmall) break;
-        const float4 g = ld4(rg, (gb + (unsigned)s * HW) * 4u);
-        acc[s] = fmaf(g.x, xv.x, fmaf(g.y, xv.y, fmaf(g.z, xv.z, fmaf(g.w, xv.w, acc[s]))));
+    for (int u = 0; u < U; ++u) {
+      const bool ok = p + 1024 * u < p1;
+      const unsigned xb = (unsigned)((long)b * a.x_bs) + r, gb = (unsigned)((long)b * a.dy_bs) + r;
+      // (an out-of-range quad reads zeros through the buffer range check: offset SK_OOB)
+      if (SMALL_OUT) {
+        one[u] = ld4(rx, ok ? (xb + (unsigned)c * HW) * 4u : SK_OOB);
+#pragma unroll
+        for (int s = 0; s < S; ++s)
+          many[u][s] = s < a.nsmall ? ld4(rg, ok ? (gb + (unsigned)s * HW) * 4u : SK_OOB) : float4{0.f, 0.f, 0.f, 0.f};
+      } else {
+        one[u] = ld4(rg, ok ? (gb + (unsigned)c * HW) * 4u : SK_OOB);
+#pragma unroll
+        for (int s = 0; s < S; ++s)
+          many[u][s] = s < a.nsmall ? ld4(rx, ok ? (xb + (unsigned)s * HW) * 4u : SK_OOB) : float4{0.f, 0.f, 0.f, 0.f};
       }
-    } else {
-      const float4 g = ld4(rg, (gb + (unsigned)c * HW) * 4u);
+      r += 1024;
+      while (r >= HW) { r -= HW; ++b; }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (p + 1024 * u >= p1) break;
 #pragma unroll
       for (int s = 0; s < S; ++s) {
         if (s >= a.nsmall) break;
-        const float4 xv = ld4(rx, (xb + (unsigned)s * HW) * 4u);
+        const float4 g = SMALL_OUT ? many[u][s] : one[u], xv = SMALL_OUT ? one[u] : many[u][s];
         acc[s] = fmaf(g.x, xv.x, fmaf(g.y, xv.y, fmaf(g.z, xv.z, fmaf(g.w, xv.w, acc[s]))));
       }
     }
-    r += 1024;
-    while (r >= HW) { r -= HW; ++b; }
   }
   const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
 #pragma unroll
