@@ -1074,19 +1074,29 @@ __global__ __launch_bounds__(256, 1) void mlp_bwd_dma_kernel(MlpArgs g) {
     }
 #pragma unroll
     for (int r = 0; r < 16; ++r) tacc[r] = 0.f;
+    // every A fragment of the two products read before the first MFMA: one LDS latency per chunk
+    // instead of one per MFMA (the compiler otherwise waits on each fragment right before its use)
+    mbf16x8 za[C / 16], ta[P / 16];
 #pragma unroll
-    for (int ks = 0; ks < C / 16; ++ks)
-      zacc = mfma16(*reinterpret_cast<const mbf16x8*>((const char*)W1s + (a_z ^ (unsigned)(32 * ks))), hbr[ks], zacc);
+    for (int ks = 0; ks < C / 16; ++ks) za[ks] = *reinterpret_cast<const mbf16x8*>((const char*)W1s + (a_z ^ (unsigned)(32 * ks)));
 #pragma unroll
-    for (int ks = 0; ks < P / 16; ++ks) tacc = mfma16(tr_at(W2s, a_t, ks * 16 * HC * 2), dbr[ks], tacc);
+    for (int ks = 0; ks < P / 16; ++ks) ta[ks] = tr_at(W2s, a_t, ks * 16 * HC * 2);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int ks = 0; ks < C / 16; ++ks) zacc = mfma16(za[ks], hbr[ks], zacc);
+    // gelu(z) / gelu'(z) need only z: their VALU can issue beside the t MFMAs
+    f32x2 gvv[8], gpv[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) mlp_gelu_pair2<true>(f32x2{zacc[2 * i], zacc[2 * i + 1]}, gvv[i], gpv[i]);
+#pragma unroll
+    for (int ks = 0; ks < P / 16; ++ks) tacc = mfma16(ta[ks], dbr[ks], tacc);
     // g = gelu(z), dz = t gelu'(z) -> LDS, pixel-major, 4 hidden per write
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       mbf16x4 gv4, dv4;
 #pragma unroll
       for (int e = 0; e < 4; e += 2) {
-        f32x2 gv, gp;
-        mlp_gelu_pair2<true>(f32x2{zacc[4 * q + e], zacc[4 * q + e + 1]}, gv, gp);
+        const f32x2 gv = gvv[(4 * q + e) / 2], gp = gpv[(4 * q + e) / 2];
         const f32x2 dz = mlp_mul2<true>(f32x2{tacc[4 * q + e], tacc[4 * q + e + 1]}, gp);
         gv4[e] = (T16)gv.x; gv4[e + 1] = (T16)gv.y;
         dv4[e] = (T16)dz.x; dv4[e + 1] = (T16)dz.y;
@@ -1114,13 +1124,19 @@ __global__ __launch_bounds__(256, 1) void mlp_bwd_dma_kernel(MlpArgs g) {
       bacc += __shfl_xor(bacc, 32, 64);
       if (lh == 0 && g.bsum) g.bsum[((long)tile * (NW / 2) + (wave >> 1)) * C4 + j * HC + chh + lr] = bacc;
     }
-    // dh += W1[chunk]^T dz
+    // dh += W1[chunk]^T dz (fragments read ahead as above)
+    mbf16x8 dzb[HC / 16], w1t[HC / 16][4];
 #pragma unroll
     for (int ks = 0; ks < HC / 16; ++ks) {
-      const mbf16x8 bf = *reinterpret_cast<const mbf16x8*>((const char*)Zn + (a_n ^ (unsigned)(32 * ks)));
+      dzb[ks] = *reinterpret_cast<const mbf16x8*>((const char*)Zn + (a_n ^ (unsigned)(32 * ks)));
 #pragma unroll
-      for (int i = 0; i < 4; ++i) hacc[i] = mfma16(tr_at(W1s, a_d[i], ks * 16 * C * 2), bf, hacc[i]);
+      for (int i = 0; i < 4; ++i) w1t[ks][i] = tr_at(W1s, a_d[i], ks * 16 * C * 2);
     }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int ks = 0; ks < HC / 16; ++ks)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) hacc[i] = mfma16(w1t[ks][i], dzb[ks], hacc[i]);
   };
   for (int j = 0; j < NCH; j += 2) {
     chunk(j, Wslot0, Wslot1);
