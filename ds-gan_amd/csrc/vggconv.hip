@@ -162,10 +162,29 @@ __global__ __launch_bounds__(256, 2) void vconv3x3_kernel(VcArgs<T16> g) {
 
   // ---- epilogue: lane holds pixel lr of each 32-pixel tile, channels (r&3)+8(r>>2)+4lh: four
   // consecutive channels per register quad -> one 8-byte (bf16) or 16-byte (fp32) store ----
+  // bias quads of this lane's channels loaded once (re-read after every store otherwise: the compiler
+  // cannot prove Y and bias apart) and each j's mask quads before their first use -- the epilogue
+  // waited one memory latency per quad
+  float4 bias4[TM][4];
+  if (g.bias) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) bias4[i][q] = *reinterpret_cast<const float4*>(g.bias + m_t * BM + wm * 64 + i * 32 + q * 8 + 4 * lh);
+  }
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
     const int n = wn * (BN / WN) + j * 32 + lr;
     const int oh = oh0 + n / TW, ow = ow0 + n % TW;
+    vgb4 mks[TM][4];   // this j's mask quads, all loaded before the first use
+    if (g.mask) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          mks[i][q] = *reinterpret_cast<const vgb4*>(
+              g.mask + cb16(img, m_t * BM + wm * 64 + i * 32 + q * 8 + 4 * lh, oh, ow, g.M, g.H, g.W));
+    }
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -175,7 +194,7 @@ __global__ __launch_bounds__(256, 2) void vconv3x3_kernel(VcArgs<T16> g) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) v[e] = acc[i][j][4 * q + e];
         if (g.bias) {
-          const float4 bv = *reinterpret_cast<const float4*>(g.bias + m);
+          const float4 bv = bias4[i][q];
           v[0] += bv.x; v[1] += bv.y; v[2] += bv.z; v[3] += bv.w;
         }
         if (g.relu) {
@@ -184,7 +203,7 @@ __global__ __launch_bounds__(256, 2) void vconv3x3_kernel(VcArgs<T16> g) {
         }
         const long o = cb16(img, m, oh, ow, g.M, g.H, g.W);
         if (g.mask) {
-          const vgb4 mk = *reinterpret_cast<const vgb4*>(g.mask + o);
+          const vgb4 mk = mks[i][q];
 #pragma unroll
           for (int e = 0; e < 4; ++e) v[e] = (float)mk[e] > 0.f ? v[e] : 0.f;
         }
@@ -348,10 +367,29 @@ __global__ __launch_bounds__(512, 1) void vconv3x3_dma_kernel(VcArgs<T16> g) {
   }
 
   // ---- epilogue (vconv3x3_kernel's) ----
+  // bias quads of this lane's channels loaded once (re-read after every store otherwise: the compiler
+  // cannot prove Y and bias apart) and each j's mask quads before their first use -- the epilogue
+  // waited one memory latency per quad
+  float4 bias4[TM][4];
+  if (g.bias) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) bias4[i][q] = *reinterpret_cast<const float4*>(g.bias + m_t * BM + wm * 64 + i * 32 + q * 8 + 4 * lh);
+  }
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
     const int n = (wn * TN + j) * 32 + lr;
     const int oh = oh0 + n / TW, ow = ow0 + n % TW;
+    vgb4 mks[TM][4];   // this j's mask quads, all loaded before the first use
+    if (g.mask) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          mks[i][q] = *reinterpret_cast<const vgb4*>(
+              g.mask + cb16(img, m_t * BM + wm * 64 + i * 32 + q * 8 + 4 * lh, oh, ow, g.M, g.H, g.W));
+    }
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -361,7 +399,7 @@ __global__ __launch_bounds__(512, 1) void vconv3x3_dma_kernel(VcArgs<T16> g) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) v[e] = acc[i][j][4 * q + e];
         if (g.bias) {
-          const float4 bv = *reinterpret_cast<const float4*>(g.bias + m);
+          const float4 bv = bias4[i][q];
           v[0] += bv.x; v[1] += bv.y; v[2] += bv.z; v[3] += bv.w;
         }
         if (g.relu) {
@@ -370,7 +408,7 @@ __global__ __launch_bounds__(512, 1) void vconv3x3_dma_kernel(VcArgs<T16> g) {
         }
         const long o = cb16(img, m, oh, ow, g.M, g.H, g.W);
         if (g.mask) {
-          const vgb4 mk = *reinterpret_cast<const vgb4*>(g.mask + o);
+          const vgb4 mk = mks[i][q];
 #pragma unroll
           for (int e = 0; e < 4; ++e) v[e] = (float)mk[e] > 0.f ? v[e] : 0.f;
         }

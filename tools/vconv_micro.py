@@ -4,12 +4,21 @@ kw-major taps (3: another fp32 summation order, compared by relative error).  Ou
 the two forms must be bitwise equal (same operands, same per-output accumulation order).
 
     python tools/vconv_micro.py [--it 20]
+    python tools/vconv_micro.py --libs a.so,b.so,a.so [--it 20]   # builds interleaved, one process each
 """
 import argparse
 import os
+import subprocess
 import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if len(sys.argv) > 2 and sys.argv[1] == "--libs":
+    # A/B of builds: one child process per listed library, in order (this parent never touches the GPU)
+    rc = 0
+    for lib_path in sys.argv[2].split(","):
+        env = dict(os.environ, DSGAN_HIP_LIB=os.path.join(REPO, lib_path))
+        rc |= subprocess.run([sys.executable, "-u", os.path.abspath(__file__)] + sys.argv[3:], env=env).returncode
+    sys.exit(rc)
 sys.path[:0] = [REPO, os.path.join(REPO, "ds-gan_amd")]
 import torch  # noqa: E402
 import dsgan_hip  # noqa: E402
