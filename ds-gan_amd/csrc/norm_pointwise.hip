@@ -286,7 +286,9 @@ __global__ __launch_bounds__(NT == 64 ? 256 : NT) void instnorm_fwd_v4(INArgs a)
 // 64K-pixel planes (NT = 1024, C4 = 16) cannot hold xhat in registers next to g, and a plane of x
 // (256 KB) does not stay in the CU's share of L2, so the second read went to HBM: XL = 8 keeps half
 // of it in 128 KB of LDS (the workgroup is alone on its CU either way).  Same values, same bits.
-template <int NT, int C4, bool CX, int XL = 0>
+// ACTT >= 0: the activation fixed at compile time (the launcher dispatches on a.act), so the cached
+// form's loop body has no branches and the scheduler can keep several items' loads in flight.
+template <int NT, int C4, bool CX, int XL = 0, int ACTT = -1>
 __global__ __launch_bounds__(NT == 64 ? 256 : NT) void instnorm_bwd_v4(INBwdArgs a) {
   static_assert(XL == 0 || (!CX && XL <= C4 && NT > 64), "XL: LDS-parked xhat of the uncached form");
   __shared__ float sh[32];
@@ -345,16 +347,16 @@ __global__ __launch_bounds__(NT == 64 ? 256 : NT) void instnorm_bwd_v4(INBwdArgs
   };
   float sg = 0.f, sgh = 0.f;
   float2 m;
-  if constexpr (C4 > 0) {
+  if constexpr (C4 > 0 && NT == 1024) {
+    // (64K-pixel planes: the scheduled form below spills at this size's 128-register cap, so the
+    // item loop keeps its guarded per-item order; XL parks half of xhat in LDS instead)
     float4 gv[C4];
-    float4 xv[CX ? C4 : 1];
 #pragma unroll
     for (int j = 0; j < C4; ++j) {
       const int i = t + j * NT;
       gv[j] = make_float4(0.f, 0.f, 0.f, 0.f);
       if (i < HW4) {
         const float4 xh = xhat(i);
-        if constexpr (CX) xv[j] = xh;
         if constexpr (XL > 0) {
           if (j < XL) xl[j * NT + t] = xh;
         }
@@ -369,9 +371,80 @@ __global__ __launch_bounds__(NT == 64 ? 256 : NT) void instnorm_bwd_v4(INBwdArgs
     for (int j = 0; j < C4; ++j) {
       const int i = t + j * NT;
       if (i < HW4) {
-        if constexpr (CX) fin(i, gv[j], xv[j], m.x, m.y);
-        else if (XL > 0 && j < XL) fin(i, gv[j], xl[j * NT + t], m.x, m.y);
+        if (XL > 0 && j < XL) fin(i, gv[j], xl[j * NT + t], m.x, m.y);
         else fin(i, gv[j], xhat(i), m.x, m.y);
+      }
+    }
+  } else if constexpr (C4 > 0) {
+    // Loads through plane-sized buffer resources (an item past the plane reads 0: no guard, no
+    // branch), the activation fixed at compile time, and no global store inside the statistics loop
+    // (dres is written afterwards).  A guarded load sits in its own basic block, and a load after a
+    // store may not be hoisted above it: each item had waited one memory latency.  Same values and
+    // the same summation order (an out-of-plane item adds +0): same bits.
+    const int act = ACTT >= 0 ? ACTT : a.act;
+    const unsigned prange = (unsigned)a.HW * 4u;
+    const __amdgpu_buffer_rsrc_t bx = __builtin_amdgcn_make_buffer_rsrc((void*)x, (short)0, prange, 0x00020000);
+    const __amdgpu_buffer_rsrc_t bd = __builtin_amdgcn_make_buffer_rsrc((void*)dy, (short)0, prange, 0x00020000);
+    const __amdgpu_buffer_rsrc_t br =
+        __builtin_amdgcn_make_buffer_rsrc(r ? (void*)r : (void*)dy, (short)0, r ? prange : 0u, 0x00020000);
+    auto bld4 = [](__amdgpu_buffer_rsrc_t rc, int i) {
+      return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rc, i * 16, 0, 0));
+    };
+    auto bxhat = [&](int i) -> float4 {
+      float4 v = bld4(bx, i);
+      v.x = (v.x * s - mean) * rs; v.y = (v.y * s - mean) * rs; v.z = (v.z * s - mean) * rs; v.w = (v.w * s - mean) * rs;
+      return v;
+    };
+    float4 gv[C4];
+    float4 xv[CX ? C4 : 1];
+#pragma unroll
+    for (int j = 0; j < C4; ++j) {
+      const int i = t + j * NT;
+      const float4 xh = bxhat(i);
+      float4 g = bld4(bd, i);
+      if (act != ACT_NONE) {
+        float4 z = xh;
+        // (no residual: a zero-range buffer reads 0 and z stays xhat -- no branch, no traffic)
+        const float4 q = bld4(br, i);
+        z.x += q.x; z.y += q.y; z.z += q.z; z.w += q.w;
+        g.x *= act_g(act, z.x, a.slope); g.y *= act_g(act, z.y, a.slope);
+        g.z *= act_g(act, z.z, a.slope); g.w *= act_g(act, z.w, a.slope);
+      }
+      gv[j] = g;
+      if constexpr (CX) xv[j] = xh;
+      if constexpr (XL > 0) {
+        if (j < XL) xl[j * NT + t] = xh;
+      }
+      sg += hsum4(g);
+      sgh += (g.x * xh.x + g.y * xh.y) + (g.z * xh.z + g.w * xh.w);
+    }
+    if (dres) {
+#pragma unroll
+      for (int j = 0; j < C4; ++j)
+        if (t + j * NT < HW4) dres[t + j * NT] = gv[j];
+    }
+    m = plane_sum2<NT>(sg, sgh, sh);
+    m.x *= inv; m.y *= inv;
+    // the recomputed xhat of the uncached items, in groups of FG loaded before their stores
+    constexpr int FG = 4;
+#pragma unroll
+    for (int j0 = 0; j0 < C4; j0 += FG) {
+      float4 xq[FG];
+      if constexpr (!CX) {
+#pragma unroll
+        for (int u = 0; u < FG && j0 + u < C4; ++u) {
+          const int i = t + (j0 + u) * NT;
+          if (!(XL > 0 && j0 + u < XL)) xq[u] = bxhat(i);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < FG && j0 + u < C4; ++u) {
+        const int j = j0 + u, i = t + j * NT;
+        if (i < HW4) {
+          if constexpr (CX) fin(i, gv[j], xv[j], m.x, m.y);
+          else if (XL > 0 && j < XL) fin(i, gv[j], xl[j * NT + t], m.x, m.y);
+          else fin(i, gv[j], xq[u], m.x, m.y);
+        }
       }
     }
   } else {
@@ -1176,6 +1249,17 @@ static inline unsigned grid_for(long n, int bs = 256) {
   return (unsigned)g;
 }
 
+// the cached IN backward forms instantiated per activation (ACTT, see instnorm_bwd_v4)
+template <int NT, int C4, bool CX, int XL = 0>
+static void in_bwd_launch(const INBwdArgs& a, dim3 grid, dim3 block, hipStream_t st) {
+  switch (a.act) {
+    case ACT_NONE: hipLaunchKernelGGL((instnorm_bwd_v4<NT, C4, CX, XL, ACT_NONE>), grid, block, 0, st, a); break;
+    case ACT_GELU: hipLaunchKernelGGL((instnorm_bwd_v4<NT, C4, CX, XL, ACT_GELU>), grid, block, 0, st, a); break;
+    case ACT_LRELU: hipLaunchKernelGGL((instnorm_bwd_v4<NT, C4, CX, XL, ACT_LRELU>), grid, block, 0, st, a); break;
+    default: hipLaunchKernelGGL((instnorm_bwd_v4<NT, C4, CX, XL>), grid, block, 0, st, a); break;
+  }
+}
+
 }  // namespace dsg
 
 using namespace dsg;
@@ -1287,13 +1371,13 @@ int dsgan_instnorm_bwd_h(const float* dy, long dy_bs, const float* x, long x_bs,
               N, C, HW, act, slope, eps, dxh, dxsum, half_type()};
   const int planes = N * C;
   if (HW <= 64 * 16)
-    hipLaunchKernelGGL((instnorm_bwd_v4<64, 4, true>), dim3(cdiv(planes, 4)), dim3(256), 0, st, a);
+    in_bwd_launch<64, 4, true>(a, dim3(cdiv(planes, 4)), dim3(256), st);
   else if (HW <= 256 * 16)
-    hipLaunchKernelGGL((instnorm_bwd_v4<256, 4, true>), dim3(planes), dim3(256), 0, st, a);
+    in_bwd_launch<256, 4, true>(a, dim3(planes), dim3(256), st);
   else if (HW <= 256 * 64)
-    hipLaunchKernelGGL((instnorm_bwd_v4<256, 16, true>), dim3(planes), dim3(256), 0, st, a);
+    in_bwd_launch<256, 16, true>(a, dim3(planes), dim3(256), st);
   else if (HW <= 1024 * 64)
-    hipLaunchKernelGGL((instnorm_bwd_v4<1024, 16, false, IN_BWD_XL>), dim3(planes), dim3(1024), 0, st, a);
+    in_bwd_launch<1024, 16, false, IN_BWD_XL>(a, dim3(planes), dim3(1024), st);
   else
     hipLaunchKernelGGL((instnorm_bwd_v4<1024, 0, false>), dim3(planes), dim3(1024), 0, st, a);
   DSG_CHECK_LAUNCH();
@@ -1312,13 +1396,13 @@ int dsgan_instnorm_bwd(const float* dy, long dy_bs, const float* x, long x_bs, c
                  (!res || in_v4_ok(HW, res, res_bs)) && (!dres || in_v4_ok(HW, dres, dres_bs));
   if (v4) {
     if (HW <= 64 * 16)
-      hipLaunchKernelGGL((instnorm_bwd_v4<64, 4, true>), dim3(cdiv(planes, 4)), dim3(256), 0, st, a);
+      in_bwd_launch<64, 4, true>(a, dim3(cdiv(planes, 4)), dim3(256), st);
     else if (HW <= 256 * 16)
-      hipLaunchKernelGGL((instnorm_bwd_v4<256, 4, true>), dim3(planes), dim3(256), 0, st, a);
+      in_bwd_launch<256, 4, true>(a, dim3(planes), dim3(256), st);
     else if (HW <= 256 * 64)
-      hipLaunchKernelGGL((instnorm_bwd_v4<256, 16, true>), dim3(planes), dim3(256), 0, st, a);
+      in_bwd_launch<256, 16, true>(a, dim3(planes), dim3(256), st);
     else if (HW <= 1024 * 64)
-      hipLaunchKernelGGL((instnorm_bwd_v4<1024, 16, false, IN_BWD_XL>), dim3(planes), dim3(1024), 0, st, a);
+      in_bwd_launch<1024, 16, false, IN_BWD_XL>(a, dim3(planes), dim3(1024), st);
     else
       hipLaunchKernelGGL((instnorm_bwd_v4<1024, 0, false>), dim3(planes), dim3(1024), 0, st, a);
     DSG_CHECK_LAUNCH();

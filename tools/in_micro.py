@@ -51,7 +51,9 @@ def digest(*ts):
 print("lib:", os.environ.get("DSGAN_HIP_LIB", "default"), flush=True)
 tot = {"fwd": 0.0, "bwd": 0.0, "bwd_h": 0.0}
 for N, C, H, act, res in [(16, 128, 256, None, False), (16, 64, 256, None, False), (16, 64, 256, "gelu", True),
-                          (16, 64, 256, "gelu", False), (16, 256, 128, None, False), (16, 128, 128, "gelu", True)]:
+                          (16, 64, 256, "gelu", False), (16, 256, 128, None, False), (16, 128, 128, "gelu", True),
+                          (16, 512, 64, None, False), (16, 256, 64, "gelu", False), (16, 128, 64, "gelu", True),
+                          (16, 1024, 32, None, False), (16, 512, 32, "gelu", False)]:
     HW = H * H
     g = torch.Generator(device="cuda").manual_seed(C + H)
     x = torch.randn(N, C, H, H, device="cuda", generator=g) * 2 + 0.3
