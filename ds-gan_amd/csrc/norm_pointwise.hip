@@ -493,9 +493,9 @@ __global__ __launch_bounds__(NT == 64 ? 256 : NT) void instnorm_bwd_v4(INBwdArgs
   }
 }
 
-#ifndef IN_BWD_XL
-#define IN_BWD_XL 8
-#endif
+// xhat float4s per thread parked in LDS by the 64K-pixel backward (instnorm_bwd_v4 XL; A/B in
+// profiles/r04/in_micro_xl.txt: 8 of 16, 128 KB of LDS)
+constexpr int IN_BWD_XL = 8;
 
 // ---- few-plane forms: one plane split over S workgroups ----
 // The generator's 3-channel block (MixConvNeXtML.py:220-221 at dim 3) normalises N*3 = 48 planes
