@@ -456,6 +456,67 @@ def test_dwconv(K, N, C, H, W):
     assert rel(bd.grad, br.grad) < 1e-5
 
 
+@pytest.mark.parametrize("C,H,W", [(128, 128, 128), (512, 64, 64), (1024, 32, 32)])
+def test_dwconv_wgrad_prefetch_path(C, H, W):
+    """The depthwise weight-grad's next-image prefetch form (dw_wgrad_body PF) runs only where a
+    workgroup walks >= 8 images (B = 16 step shapes; the op tests above use N <= 3).  Its dw / db at
+    B = 16 against the sum of 16 single-image launches (the plain form, pinned to torch above), per
+    tile configuration (W % 128 == 0, W = 64, W = 32)."""
+    from dsgan_hip import functional as HF
+    N, K = 16, 7
+    g = torch.Generator(device=DEV).manual_seed(C + H)
+    x = torch.randn(N, C, H, W, device=DEV, generator=g)
+    dy = torch.randn(N, C, H, W, device=DEV, generator=g)
+    dw, db = torch.zeros(C, 1, K, K, device=DEV), torch.zeros(C, device=DEV)
+    HF._dw_wgrad(dy, x, dw, db, K)
+    rw, rb = torch.zeros(C, 1, K, K, device=DEV, dtype=torch.float64), torch.zeros(C, device=DEV, dtype=torch.float64)
+    for n in range(N):
+        w1, b1 = torch.zeros(C, 1, K, K, device=DEV), torch.zeros(C, device=DEV)
+        HF._dw_wgrad(dy[n:n + 1].contiguous(), x[n:n + 1].contiguous(), w1, b1, K)
+        rw += w1.double()
+        rb += b1.double()
+    assert rel(dw, rw) < 1e-5 and rel(db, rb) < 1e-5
+
+
+@pytest.mark.parametrize("N", [16, 2])
+def test_multi_dwconv_wgrad_prefetch_path(N):
+    """MidMLKA's four-quarter weight-grad at C = 128 @ 128^2: N = 16 takes the prefetch form (16 images
+    per workgroup), N = 2 the plain one; the B = 16 grads equal the sum of two B = 8 launches' within
+    fp32 summation error, and the N = 2 ones match torch (the four quarter convs)."""
+    from dsgan_hip import functional as HF
+    C, H = 128, 128
+    q = C // 4
+    g = torch.Generator(device=DEV).manual_seed(N)
+    x = torch.randn(N, C, H, H, device=DEV, generator=g)
+    dy = torch.randn(N, C, H, H, device=DEV, generator=g)
+    ks = (3, 5, 7, 9)
+
+    def grads(xs, dys):
+        ws = torch.empty(max(1, HF._lib.load().dsgan_dwconv_multi_wgrad_workspace(xs.shape[0], q, H, H)), device=DEV)
+        gw = [torch.zeros(q, 1, k, k, device=DEV) for k in ks]
+        gb = [torch.zeros(q, device=DEV) for _ in ks]
+        args = []
+        for a_, b_ in zip(gw, gb):
+            args += [HF.ptr(a_), HF.ptr(b_)]
+        HF.call("dsgan_dwconv_multi_wgrad", HF.ptr(dys), C * H * H, HF.ptr(xs), C * H * H, *args, xs.shape[0], q, H, H,
+                HF.ptr(ws), ws.numel(), HF.stream())
+        return gw + gb
+
+    got = grads(x, dy)
+    if N == 16:
+        a, b = grads(x[:8].contiguous(), dy[:8].contiguous()), grads(x[8:].contiguous(), dy[8:].contiguous())
+        for t, u, v in zip(got, a, b):
+            assert rel(t, u.double() + v.double()) < 1e-5
+    else:
+        for i, k in enumerate(ks):
+            xr = x[:, i * q:(i + 1) * q].detach().cpu().double()
+            dr = dy[:, i * q:(i + 1) * q].detach().cpu().double()
+            w = torch.zeros(q, 1, k, k, dtype=torch.float64, requires_grad=True)
+            b = torch.zeros(q, dtype=torch.float64, requires_grad=True)
+            F.conv2d(xr, w, b, padding=k // 2, groups=q).backward(dr)
+            assert rel(got[i], w.grad) < 1e-5 and rel(got[4 + i], b.grad) < 1e-5
+
+
 @pytest.mark.parametrize("K", [3, 7, 9])
 @pytest.mark.parametrize("H,W", [(64, 64), (40, 128), (32, 32)])
 def test_dwconv_accumulate(K, H, W):
