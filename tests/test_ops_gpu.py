@@ -73,6 +73,8 @@ def _q(t, prec):
     (3, 64, 40, 36, 3, 3, 1, 1),       # skinny direct kernels at larger planes
     (4, 256, 31, 31, 1, 4, 1, 1),      # PatchGAN last layer shape (K-split atomics)
     (2, 3, 64, 64, 32, 1, 1, 0),       # to32 (wgrad with Cin = 3)
+    (2, 12, 64, 64, 64, 1, 1, 0),      # c1 pwconv2-like: data-grad 64 -> 12 (pw_small, 4-channel load steps)
+    (2, 12, 32, 32, 70, 1, 1, 0),      # ... with a channel remainder after the load steps
     (2, 6, 66, 66, 64, 4, 2, 1),       # PatchGAN layer 0 (stride-2 data-grad into 6 channels)
     (2, 1024, 96, 96, 1024, 1, 1, 0),  # wide, deep 1x1 fwd + data-grad: 256-row M tiles (K >= 1024)
     (2, 64, 8, 256, 3, 3, 1, 1),       # G head at full width: thin3.hip row strips (act=None)
