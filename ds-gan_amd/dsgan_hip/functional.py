@@ -618,6 +618,39 @@ def copy_multi(pairs):
          stream())
 
 
+class CatSlot:
+    """The buffer of a channel concatenation cat(head, tail) [N, Ch+Ct, H, W], allocated before
+    either half exists.  The tail's producer writes straight into ``tail()`` (a Block output that
+    is a decoder skip, MixConvNeXtML.py:229-236), and the node that forms the concatenation
+    (ConvTNormFn / InstanceNormCatFn, upSample :61-66) finds the tail already in place and writes
+    only the head: the skip is never copied.  ``tail()`` / ``whole()`` alias the buffer's storage
+    without being autograd views of it (no kernel writes through torch in-place ops)."""
+
+    def __init__(self, N, Ch, Ct, H, W, like):
+        self.buf = _empty(N, Ch + Ct, H, W, like)
+        self.Ch, self.Ct = Ch, Ct
+
+    def _alias(self, c0, C):
+        b = self.buf
+        N, _, H, W = b.shape
+        return torch.empty(0, device=b.device, dtype=b.dtype).set_(
+            b.untyped_storage(), b.storage_offset() + c0 * H * W, (N, C, H, W), b.stride())
+
+    def tail(self):
+        return self._alias(self.Ch, self.Ct)
+
+    def whole(self):
+        return self._alias(0, self.Ch + self.Ct)
+
+    def holds(self, t, Ch):
+        """t is this slot's tail (behind a head of Ch channels)."""
+        b = self.buf
+        N, _, H, W = b.shape
+        return (t is not None and Ch == self.Ch and t.dim() == 4 and t.dtype == b.dtype and t.device == b.device
+                and tuple(t.shape) == (N, self.Ct, H, W) and tuple(t.stride()) == tuple(b.stride())
+                and t.data_ptr() == b.data_ptr() + self.Ch * H * W * b.element_size())
+
+
 def copy_into(dst, src):
     """dst[n] <- src[n] for per-sample dense blocks (used for channel concatenation)."""
     src, sbs = nchw(src)
@@ -861,9 +894,12 @@ class PwMlpFn(torch.autograd.Function):
         activation-on-load, and the data-grad of pwconv2 multiplies by gelu'(z) in its epilogue."""
 
     @staticmethod
-    def forward(ctx, h, x, w1, b1, w2, b2, ws, norm=False):
+    def forward(ctx, h, x, w1, b1, w2, b2, ws, norm=False, slot=None):
         N, C, H, W = h.shape
         P, HW, C4 = w2.shape[0], H * W, 4 * C
+        # out: the slot's tail when the block output is a decoder skip (written in place)
+        out0 = slot.tail() if slot is not None else None
+        obs = nchw(out0)[1] if out0 is not None else P * HW
         ctx.refs = (w1, b1, w2, b2, ws)
         ctx.prec = _state["prec"]
         ctx.box_h, ctx.box_x = _box(h), _box(x)
@@ -893,10 +929,10 @@ class PwMlpFn(torch.autograd.Function):
         ctx.hb = hb
         ctx.tile = tile
         if tile:
-            out = conv_fwd_raw(x, ws, None, 1, 0)
+            out = conv_fwd_raw(x, ws, None, 1, 0, out=out0)
             e0 = IGEMM_TIMER.begin()
             call("dsgan_mlp_fwd", ptr(h), hbs, hb, ptr(bf16_weight(w1)), ptr(b1), ptr(bf16_weight(w2)), ptr(b2),
-                 ptr(out), P * HW, N, C, P, HW, 1, stream())
+                 ptr(out), obs, N, C, P, HW, 1, stream())
             IGEMM_TIMER.end(e0, _mlp_flops(N, C, P, HW), ("mlp_fwd", N, C, H, W, P, 1, 1), "mlp_fwd_kernel",
                             _nb(h, w1, b1, w2, b2) + 2 * _nb(out))
             ctx.save_for_backward(h, x, ws)
@@ -914,9 +950,9 @@ class PwMlpFn(torch.autograd.Function):
                  ptr(b1), C4, C, HW, N, ACT["gelu"], 0, LRELU_SLOPE, *wsa(_pw_fd_ws(0, C4, C, HW, N, h)), stream())
             IGEMM_TIMER.end(e0, 2.0 * N * HW * C4 * C, ("fwd", N, C, H, W, C4, 1, 1), "pwgemm_kernel",
                             _nb(h, w1, b1, g, gp))
-            out = conv_fwd_raw(x, ws, None, 1, 0)
+            out = conv_fwd_raw(x, ws, None, 1, 0, out=out0)
             e0 = IGEMM_TIMER.begin()
-            call("dsgan_pw_fwd_io_ws", ptr(bf16_weight(w2)), 1, ptr(g), C4 * HW, 1, ptr(out), P * HW, 0, None, 0, 0, ptr(b2),
+            call("dsgan_pw_fwd_io_ws", ptr(bf16_weight(w2)), 1, ptr(g), C4 * HW, 1, ptr(out), obs, 0, None, 0, 0, ptr(b2),
                  P, C4, HW, N, 0, 1, LRELU_SLOPE, *wsa(_pw_fd_ws(0, P, C4, HW, N, g)), stream())
             IGEMM_TIMER.end(e0, 2.0 * N * HW * C4 * P, ("fwd", N, C4, H, W, P, 1, 1), "pwgemm_kernel",
                             _nb(g, w2, b2) + 2 * _nb(out))
@@ -925,16 +961,17 @@ class PwMlpFn(torch.autograd.Function):
             return out
         z = conv_fwd_raw(h, w1v, b1, 1, 0)
         x4, xbs = nchw(x)
-        if 5 * C <= 16 and _pws_ok(5 * C, P, HW, xbs, P * HW, x4, z) and z.data_ptr() % 16 == 0:
+        out = out0 if out0 is not None else _empty(N, P, H, W, h)
+        if 5 * C <= 16 and _pws_ok(5 * C, P, HW, xbs, obs, x4, z) and z.data_ptr() % 16 == 0 \
+                and out.data_ptr() % 16 == 0:
             # tiny blocks (c1: 3 -> 12 -> 64 at 256^2): shortcut + pwconv2 in one streaming pass
-            out = _empty(N, P, H, W, h)
             e0 = IGEMM_TIMER.begin()
             call("dsgan_pw_small2", ptr(x4), xbs, ptr(ws), C, 1, ptr(z), 4 * C * HW, ptr(w2), 4 * C, ptr(b2),
-                 ptr(out), P * HW, None, 0, N, C, P, HW, 0, ACT["gelu"], 0, 0, LRELU_SLOPE, stream())
+                 ptr(out), obs, None, 0, N, C, P, HW, 0, ACT["gelu"], 0, 0, LRELU_SLOPE, stream())
             IGEMM_TIMER.end(e0, 2.0 * N * HW * P * 5 * C, ("fwd", N, 5 * C, H, W, P, 1, 1), "pw_small_kernel",
                             _nb(x4, z, out, ws, w2, b2))
         else:
-            out = conv_fwd_raw(x, ws, None, 1, 0)
+            conv_fwd_raw(x, ws, None, 1, 0, out=out)
             conv_fwd_raw(z, w2v, b2, 1, 0, out=out, accumulate=True, xact="gelu")
         ctx.save_for_backward(h, x, z, w1v, w2v, ws)
         return out
@@ -950,7 +987,7 @@ class PwMlpFn(torch.autograd.Function):
                 d, mean, rstd = ctx.nrm
                 dh = instnorm_bwd_raw(dh, d, None, None, mean, rstd, None, False, False)[0]
             ctx.nrm = None
-        return _give(ctx.box_h, dh), dx, None, None, None, None, None, None
+        return _give(ctx.box_h, dh), dx, None, None, None, None, None, None, None
 
     @staticmethod
     def _backward_unfused(ctx, dy):
@@ -1094,10 +1131,11 @@ class PwMlpFn(torch.autograd.Function):
         return dh, PwMlpFn._dx(ctx, dy, ws, x)
 
 
-def pw_mlp(h, x, w1, b1, w2, b2, ws, norm=False):
+def pw_mlp(h, x, w1, b1, w2, b2, ws, norm=False, slot=None):
     """ConvNeXt block tail; with norm=True the first argument is the depthwise-conv output d and
-    the block's InstanceNorm h = IN(d) is applied inside (MixConvNeXtML.py:219-224)."""
-    return PwMlpFn.apply(h, x, w1, b1, w2, b2, ws, norm)
+    the block's InstanceNorm h = IN(d) is applied inside (MixConvNeXtML.py:219-224).  ``slot``
+    (CatSlot): the output is written into the slot's tail and returned as that alias."""
+    return PwMlpFn.apply(h, x, w1, b1, w2, b2, ws, norm, slot)
 
 
 # ------------------------------------------------------------------------------------------
@@ -1310,11 +1348,15 @@ class InstanceNormCatFn(torch.autograd.Function):
     is copied; the backward reads its slice of dy in place."""
 
     @staticmethod
-    def forward(ctx, x, skip, act):
+    def forward(ctx, x, skip, act, slot=None):
         N, Ca, H, W = x.shape
-        out = _empty(N, Ca + skip.shape[1], H, W, x)
-        _, mean, rstd = instnorm_raw(x, None, None, act, out=out[:, :Ca])
-        copy_into(out[:, Ca:], skip)
+        if slot is not None and slot.holds(skip, Ca):
+            out = slot.whole()   # the skip's producer already wrote it into the tail
+            _, mean, rstd = instnorm_raw(x, None, None, act, out=out[:, :Ca])
+        else:
+            out = _empty(N, Ca + skip.shape[1], H, W, x)
+            _, mean, rstd = instnorm_raw(x, None, None, act, out=out[:, :Ca])
+            copy_into(out[:, Ca:], skip)
         ctx.act, ctx.Ca = act, Ca
         ctx.save_for_backward(x, mean, rstd)
         ctx.box_x, ctx.box_s = _box(x), _box(skip)
@@ -1324,11 +1366,11 @@ class InstanceNormCatFn(torch.autograd.Function):
     def backward(ctx, dy):
         x, mean, rstd = ctx.saved_tensors
         dx, _, _ = instnorm_bwd_raw(dy[:, :ctx.Ca], x, None, None, mean, rstd, ctx.act, False, False)
-        return _give(ctx.box_x, dx), _give(ctx.box_s, dy[:, ctx.Ca:]), None
+        return _give(ctx.box_x, dx), _give(ctx.box_s, dy[:, ctx.Ca:]), None, None
 
 
-def instance_norm_cat(x, skip, act=None):
-    return InstanceNormCatFn.apply(x, skip, act)
+def instance_norm_cat(x, skip, act=None, slot=None):
+    return InstanceNormCatFn.apply(x, skip, act, slot)
 
 
 class ConvTNormFn(torch.autograd.Function):
@@ -1342,14 +1384,18 @@ class ConvTNormFn(torch.autograd.Function):
     the plane sums (the fp32 values, as channel_sum of the fp32 grad would add them)."""
 
     @staticmethod
-    def forward(ctx, x, w, b, other, act, cat):
+    def forward(ctx, x, w, b, other, act, cat, slot=None):
         N, Ci, Hi, Wi = x.shape
         Co = w.shape[1]
         t = conv_dgrad_raw(x, w, (N, Co, 2 * Hi, 2 * Wi), 2, 1, bias=b)
         if cat:
-            out = _empty(N, Co + other.shape[1], 2 * Hi, 2 * Wi, t)
-            _, mean, rstd = instnorm_raw(t, None, None, act, out=out[:, :Co])
-            copy_into(out[:, Co:], other)
+            if slot is not None and slot.holds(other, Co):
+                out = slot.whole()   # the skip's producer already wrote it into the tail
+                _, mean, rstd = instnorm_raw(t, None, None, act, out=out[:, :Co])
+            else:
+                out = _empty(N, Co + other.shape[1], 2 * Hi, 2 * Wi, t)
+                _, mean, rstd = instnorm_raw(t, None, None, act, out=out[:, :Co])
+                copy_into(out[:, Co:], other)
             ctx.save_for_backward(x, w, t, mean, rstd)
         else:
             out, mean, rstd = instnorm_raw(t, None, other, act)
@@ -1418,7 +1464,7 @@ class ConvTNormFn(torch.autograd.Function):
             channel_sum_raw(psum.view(N, Co, 1, 1), gb)
         _params_done(ctx.w_ref, ctx.b_ref)
         dother = _give(ctx.box_o, dy[:, Co:]) if ctx.cat else _give(ctx.box_o, dres)
-        return _give(ctx.box_x, dx), None, None, dother, None, None
+        return _give(ctx.box_x, dx), None, None, dother, None, None, None
 
 
 def _convt_norm_fused(x, w, other, cat):
@@ -1431,12 +1477,14 @@ def _convt_norm_fused(x, w, other, cat):
             and HW % 4 == 0 and (2 * Wi) % 4 == 0 and bool(_lib.load().dsgan_wconv_supported(Co, 3, 3, 2)))
 
 
-def convt_norm(x, w, b, other, act=None, cat=False):
-    """cat(act(IN(ConvT3s2(x))), other) if cat else act(IN(ConvT3s2(x)) + other) (other may be None)."""
+def convt_norm(x, w, b, other, act=None, cat=False, slot=None):
+    """cat(act(IN(ConvT3s2(x))), other) if cat else act(IN(ConvT3s2(x)) + other) (other may be None).
+    ``slot`` (CatSlot, cat only): when ``other`` is the slot's tail the concatenation is formed in
+    place and returned as ``slot.whole()``."""
     if _convt_norm_fused(x, w, other, cat):
-        return ConvTNormFn.apply(x, w, b, other, act, cat)
+        return ConvTNormFn.apply(x, w, b, other, act, cat, slot)
     y = conv_transpose3s2(x, w, b)
-    return instance_norm_cat(y, other, act) if cat else instance_norm(y, act, other)
+    return instance_norm_cat(y, other, act, slot) if cat else instance_norm(y, act, other)
 
 
 # ------------------------------------------------------------------------------------------

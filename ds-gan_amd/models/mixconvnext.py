@@ -30,9 +30,9 @@ class upSample(nn.Module):
         self.model = nn.Sequential(nn.ConvTranspose2d(in_channel, out_channel, kernel_size=3, stride=2,
                                                       padding=1, output_padding=1))
 
-    def forward(self, x, feature_map):
+    def forward(self, x, feature_map, slot=None):
         t = self.model[0]
-        return HF.convt_norm(x, t.weight, t.bias, feature_map, act="gelu", cat=True)
+        return HF.convt_norm(x, t.weight, t.bias, feature_map, act="gelu", cat=True, slot=slot)
 
 
 class MidMLKA(nn.Module):
@@ -117,12 +117,12 @@ class Block(nn.Module):
         self.pwconv1 = nn.Linear(dim, 4 * dim)
         self.pwconv2 = nn.Linear(4 * dim, plans)
 
-    def forward(self, x):
+    def forward(self, x, slot=None):
         x = HF.share(x)   # read by the depthwise conv and by the 1x1 shortcut
         # norm=True: the block's InstanceNorm runs inside the MLP node (bf16 h, see PwMlpFn)
         d = HF.dwconv(x, self.dwconv.weight, self.dwconv.bias)
         return HF.pw_mlp(d, x, self.pwconv1.weight, self.pwconv1.bias, self.pwconv2.weight,
-                         self.pwconv2.bias, self.shortcut.weight, norm=True)
+                         self.pwconv2.bias, self.shortcut.weight, norm=True, slot=slot)
 
 
 def _skip(cin, cout, k):
@@ -211,24 +211,29 @@ class MixConvNeXtML(nn.Module):
         # MaxPool(2) of R_i is computed once for the encoder and the pyramid's k=2 branch
         # (both are MaxPool2d(2) of the same tensor).  Shared tensors accumulate their grads in
         # one buffer (HF.share) instead of through autograd adds.
+        # The decoder concatenations cat(upSample head, R_i) are allocated up front: c_i writes R_i
+        # straight into its tail and u_i only fills the head (no copy of the skip, HF.CatSlot).
         sh, mp = HF.share, lambda t: HF.share(HF.max_pool2d(t, 2))
-        R1 = sh(self.c1(x))
+        N, _, H, W = x.shape
+        cs = [HF.CatSlot(N, c, c, H >> i, W >> i, x) for i, c in enumerate((64, 128, 256, 512))]
+        R1 = sh(self.c1(x, cs[0]))
         P1 = mp(R1)
-        R2 = sh(self.c2(P1))
+        R2 = sh(self.c2(P1, cs[1]))
         P2 = mp(R2)
-        R3 = sh(self.c3(P2))
+        R3 = sh(self.c3(P2, cs[2]))
         P3 = mp(R3)
-        R4 = sh(self.c4(P3))
+        R4 = sh(self.c4(P3, cs[3]))
         P4 = mp(R4)
         R5 = self.c5(P4)
         s64 = self.down64(R1, P1)
         s128 = self.down128(R2, P2)
         s256 = self.down256(R3, P3)
         s512 = self.down512(R4, P4)
-        O1 = self.uc1(self.u1(HF.add_n(R5, s64[3], s128[2], s256[1], s512[0]), R4))
-        O2 = self.uc2(self.u2(HF.add_n(O1, s64[2], s128[1], s256[0]), R3))
-        O3 = self.uc3(self.u3(HF.add_n(O2, s64[1], s128[0]), R2))
-        O4 = self.uc4(self.u4(HF.add_n(O3, s64[0]), R1))
+        O1 = self.uc1(self.u1(HF.add_n(R5, s64[3], s128[2], s256[1], s512[0]), R4, cs[3]))
+        O2 = self.uc2(self.u2(HF.add_n(O1, s64[2], s128[1], s256[0]), R3, cs[2]))
+        O3 = self.uc3(self.u3(HF.add_n(O2, s64[1], s128[0]), R2, cs[1]))
+        O4 = self.uc4(self.u4(HF.add_n(O3, s64[0]), R1, cs[0]))
+        del cs
         # --precision fp16 (configs[4]): the MLKA branch keeps bf16 16-bit operands (fp32 exponent
         # range).  Its InstanceNorms see input variances far below eps at the reference init, so
         # their backward multiplies gradients by up to ~1/sqrt(eps) per norm: under the fp16 mode's

@@ -1074,6 +1074,52 @@ def test_convt_norm_fused_matches_unfused(half, cat, N, Ci, Co, H):
     assert ((db1.double() - db2.double()).abs() <= 1e-5 * t_scale).all()
 
 
+@pytest.mark.parametrize("prec", ["fp32", "bf16"])
+@pytest.mark.parametrize("N,C,P,H,Ci", [(2, 64, 64, 32, 128),     # fused MLP kernels (mlp.hip)
+                                        (2, 256, 128, 16, 256),   # unfused bf16 g / gp path
+                                        (2, 3, 64, 32, 128)])     # tiny block (c1: pw_small2)
+def test_cat_slot_in_place(prec, N, C, P, H, Ci):
+    """HF.CatSlot (the decoder skip written in place, MixConvNeXtML.py:229-236): the Block tail
+    writes R into the slot's tail, the ConvT + IN node fills only the head and returns the whole
+    buffer.  Against the same graph with a freshly allocated R and a copied skip: every output and
+    gradient bitwise (the kernels see the same values, only R's batch stride differs)."""
+    from dsgan_hip import functional as HF
+    HF.set_precision(prec)
+    g = torch.Generator().manual_seed(C + P + H)
+    d = torch.randn(N, C, H, H, generator=g)
+    x = torch.randn(N, C, H, H, generator=g)
+    w1 = torch.randn(4 * C, C, generator=g) / math.sqrt(C)
+    b1 = torch.randn(4 * C, generator=g) * 0.1
+    w2 = torch.randn(P, 4 * C, generator=g) / math.sqrt(4 * C)
+    b2 = torch.randn(P, generator=g) * 0.1
+    ws = torch.randn(P, C, 1, 1, generator=g) / math.sqrt(C)
+    u = torch.randn(N, Ci, H // 2, H // 2, generator=g)
+    wt = torch.randn(Ci, P, 3, 3, generator=g) / math.sqrt(Ci * 9)
+    bt = torch.randn(P, generator=g) * 0.1
+    gy = torch.randn(N, 2 * P, H, H, generator=g).to(DEV)
+    gp = torch.randn(N, P, H // 2, H // 2, generator=g).to(DEV)
+    outs = []
+    for use_slot in (False, True):
+        dd, xd, ud = _leaf(d), _leaf(x), _leaf(u)
+        Q = [_param(t) for t in (w1, b1, w2, b2, ws, wt, bt)]
+        slot = HF.CatSlot(N, P, P, H, H, dd) if use_slot else None
+        R = HF.share(HF.pw_mlp(dd, xd, *Q[:5], norm=True, slot=slot))
+        if use_slot:
+            assert slot.holds(R, P) and R.stride(0) == 2 * P * H * H
+        pooled = HF.max_pool2d(R, 2)
+        y = HF.convt_norm(ud, Q[5], Q[6], R, act="gelu", cat=True, slot=slot)
+        if use_slot:
+            assert y.data_ptr() == slot.buf.data_ptr()
+        # fresh upstream grads per run: R's shared grad buffer adopts its slice of gy and the
+        # max-pool backward accumulates into it
+        torch.autograd.backward([y, pooled], [gy.clone(), gp.clone()])
+        torch.cuda.synchronize()
+        outs.append([y.detach().cpu(), pooled.detach().cpu(), dd.grad.cpu(), xd.grad.cpu(), ud.grad.cpu()]
+                    + [q.grad.cpu() for q in Q])
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+
+
 @pytest.mark.parametrize("w_bf16,x_bf16", [(0, 0), (1, 1), (1, 0)])
 @pytest.mark.parametrize("M,K,P,nb", [(2048, 512, 4096, 2), (1024, 256, 1024, 3), (256, 64, 256, 2), (4096, 1024, 1024, 1),
                                       (96, 40, 256, 2)])
