@@ -894,11 +894,20 @@ class PwMlpFn(torch.autograd.Function):
         activation-on-load, and the data-grad of pwconv2 multiplies by gelu'(z) in its epilogue."""
 
     @staticmethod
-    def forward(ctx, h, x, w1, b1, w2, b2, ws, norm=False, slot=None):
+    def forward(ctx, h, x, w1, b1, w2, b2, ws, norm=False, slot=None, acc=None):
         N, C, H, W = h.shape
         P, HW, C4 = w2.shape[0], H * W, 4 * C
-        # out: the slot's tail when the block output is a decoder skip (written in place)
-        out0 = slot.tail() if slot is not None else None
+        # out: the slot's tail when the block output is a decoder skip (written in place), or acc
+        # itself when the block output is summed into acc (out = acc + block; the first kernel
+        # accumulates, acc is returned dirty)
+        if acc is not None:
+            if (slot is not None or tuple(acc.shape) != (N, P, H, W) or acc.dtype != torch.float32
+                    or not acc.is_contiguous()):
+                raise ValueError("pw_mlp: acc must be a dense fp32 [%d,%d,%d,%d] tensor (no slot)" % (N, P, H, W))
+            ctx.mark_dirty(acc)
+        ctx.box_acc = _box(acc) if acc is not None else None
+        out0 = slot.tail() if slot is not None else acc
+        acc1 = acc is not None
         obs = nchw(out0)[1] if out0 is not None else P * HW
         ctx.refs = (w1, b1, w2, b2, ws)
         ctx.prec = _state["prec"]
@@ -929,14 +938,14 @@ class PwMlpFn(torch.autograd.Function):
         ctx.hb = hb
         ctx.tile = tile
         if tile:
-            out = conv_fwd_raw(x, ws, None, 1, 0, out=out0)
+            out = conv_fwd_raw(x, ws, None, 1, 0, out=out0, accumulate=acc1)
             e0 = IGEMM_TIMER.begin()
             call("dsgan_mlp_fwd", ptr(h), hbs, hb, ptr(bf16_weight(w1)), ptr(b1), ptr(bf16_weight(w2)), ptr(b2),
                  ptr(out), obs, N, C, P, HW, 1, stream())
             IGEMM_TIMER.end(e0, _mlp_flops(N, C, P, HW), ("mlp_fwd", N, C, H, W, P, 1, 1), "mlp_fwd_kernel",
                             _nb(h, w1, b1, w2, b2) + 2 * _nb(out))
             ctx.save_for_backward(h, x, ws)
-            return out
+            return acc if acc1 else out
         w1v = w1.view(w1.shape[0], w1.shape[1], 1, 1)
         w2v = w2.view(w2.shape[0], w2.shape[1], 1, 1)
         ctx.g = None
@@ -950,7 +959,7 @@ class PwMlpFn(torch.autograd.Function):
                  ptr(b1), C4, C, HW, N, ACT["gelu"], 0, LRELU_SLOPE, *wsa(_pw_fd_ws(0, C4, C, HW, N, h)), stream())
             IGEMM_TIMER.end(e0, 2.0 * N * HW * C4 * C, ("fwd", N, C, H, W, C4, 1, 1), "pwgemm_kernel",
                             _nb(h, w1, b1, g, gp))
-            out = conv_fwd_raw(x, ws, None, 1, 0, out=out0)
+            out = conv_fwd_raw(x, ws, None, 1, 0, out=out0, accumulate=acc1)
             e0 = IGEMM_TIMER.begin()
             call("dsgan_pw_fwd_io_ws", ptr(bf16_weight(w2)), 1, ptr(g), C4 * HW, 1, ptr(out), obs, 0, None, 0, 0, ptr(b2),
                  P, C4, HW, N, 0, 1, LRELU_SLOPE, *wsa(_pw_fd_ws(0, P, C4, HW, N, g)), stream())
@@ -958,7 +967,7 @@ class PwMlpFn(torch.autograd.Function):
                             _nb(g, w2, b2) + 2 * _nb(out))
             ctx.g = g
             ctx.save_for_backward(h, x, gp, w1v, w2v, ws)
-            return out
+            return acc if acc1 else out
         z = conv_fwd_raw(h, w1v, b1, 1, 0)
         x4, xbs = nchw(x)
         out = out0 if out0 is not None else _empty(N, P, H, W, h)
@@ -967,14 +976,14 @@ class PwMlpFn(torch.autograd.Function):
             # tiny blocks (c1: 3 -> 12 -> 64 at 256^2): shortcut + pwconv2 in one streaming pass
             e0 = IGEMM_TIMER.begin()
             call("dsgan_pw_small2", ptr(x4), xbs, ptr(ws), C, 1, ptr(z), 4 * C * HW, ptr(w2), 4 * C, ptr(b2),
-                 ptr(out), obs, None, 0, N, C, P, HW, 0, ACT["gelu"], 0, 0, LRELU_SLOPE, stream())
+                 ptr(out), obs, None, 0, N, C, P, HW, 0, ACT["gelu"], 0, int(acc1), LRELU_SLOPE, stream())
             IGEMM_TIMER.end(e0, 2.0 * N * HW * P * 5 * C, ("fwd", N, 5 * C, H, W, P, 1, 1), "pw_small_kernel",
                             _nb(x4, z, out, ws, w2, b2))
         else:
-            conv_fwd_raw(x, ws, None, 1, 0, out=out)
+            conv_fwd_raw(x, ws, None, 1, 0, out=out, accumulate=acc1)
             conv_fwd_raw(z, w2v, b2, 1, 0, out=out, accumulate=True, xact="gelu")
         ctx.save_for_backward(h, x, z, w1v, w2v, ws)
-        return out
+        return acc if acc1 else out
 
     @staticmethod
     def backward(ctx, dy):
@@ -987,7 +996,9 @@ class PwMlpFn(torch.autograd.Function):
                 d, mean, rstd = ctx.nrm
                 dh = instnorm_bwd_raw(dh, d, None, None, mean, rstd, None, False, False)[0]
             ctx.nrm = None
-        return _give(ctx.box_h, dh), dx, None, None, None, None, None, None, None
+        # out = acc + block: acc's grad is dy itself (borrowed, never adopted as a buffer)
+        dacc = _give(ctx.box_acc, dy, adopt=False) if ctx.needs_input_grad[9] else None
+        return _give(ctx.box_h, dh), dx, None, None, None, None, None, None, None, dacc
 
     @staticmethod
     def _backward_unfused(ctx, dy):
@@ -1131,11 +1142,13 @@ class PwMlpFn(torch.autograd.Function):
         return dh, PwMlpFn._dx(ctx, dy, ws, x)
 
 
-def pw_mlp(h, x, w1, b1, w2, b2, ws, norm=False, slot=None):
+def pw_mlp(h, x, w1, b1, w2, b2, ws, norm=False, slot=None, acc=None):
     """ConvNeXt block tail; with norm=True the first argument is the depthwise-conv output d and
     the block's InstanceNorm h = IN(d) is applied inside (MixConvNeXtML.py:219-224).  ``slot``
-    (CatSlot): the output is written into the slot's tail and returned as that alias."""
-    return PwMlpFn.apply(h, x, w1, b1, w2, b2, ws, norm, slot)
+    (CatSlot): the output is written into the slot's tail and returned as that alias.  ``acc``: the
+    output is summed into acc in place (acc + block, the shortcut GEMM's epilogue adds acc) and acc
+    is returned."""
+    return PwMlpFn.apply(h, x, w1, b1, w2, b2, ws, norm, slot, acc)
 
 
 # ------------------------------------------------------------------------------------------

@@ -117,12 +117,12 @@ class Block(nn.Module):
         self.pwconv1 = nn.Linear(dim, 4 * dim)
         self.pwconv2 = nn.Linear(4 * dim, plans)
 
-    def forward(self, x, slot=None):
+    def forward(self, x, slot=None, acc=None):
         x = HF.share(x)   # read by the depthwise conv and by the 1x1 shortcut
         # norm=True: the block's InstanceNorm runs inside the MLP node (bf16 h, see PwMlpFn)
         d = HF.dwconv(x, self.dwconv.weight, self.dwconv.bias)
         return HF.pw_mlp(d, x, self.pwconv1.weight, self.pwconv1.bias, self.pwconv2.weight,
-                         self.pwconv2.bias, self.shortcut.weight, norm=True, slot=slot)
+                         self.pwconv2.bias, self.shortcut.weight, norm=True, slot=slot, acc=acc)
 
 
 def _skip(cin, cout, k):
@@ -232,7 +232,7 @@ class MixConvNeXtML(nn.Module):
         O1 = self.uc1(self.u1(HF.add_n(R5, s64[3], s128[2], s256[1], s512[0]), R4, cs[3]))
         O2 = self.uc2(self.u2(HF.add_n(O1, s64[2], s128[1], s256[0]), R3, cs[2]))
         O3 = self.uc3(self.u3(HF.add_n(O2, s64[1], s128[0]), R2, cs[1]))
-        O4 = self.uc4(self.u4(HF.add_n(O3, s64[0]), R1, cs[0]))
+        U4 = self.u4(HF.add_n(O3, s64[0]), R1, cs[0])
         del cs
         # --precision fp16 (configs[4]): the MLKA branch keeps bf16 16-bit operands (fp32 exponent
         # range).  Its InstanceNorms see input variances far below eps at the reference init, so
@@ -241,4 +241,6 @@ class MixConvNeXtML(nn.Module):
         # finite (tools/fp16_scale_probe.py; SURVEY.md §7 asks to keep this branch out of fp16).
         with HF.precision("bf16" if HF.get_precision() == "fp16" else None):
             Loc = self.local(x)
-        return HF.conv2d(HF.add_n(O4, Loc), self.res.weight, self.res.bias, stride=1, pad=1)
+        # uc4(U4) + Loc: the block's shortcut GEMM adds Loc in its epilogue and the block sums into
+        # Loc in place (no separate add of two 64 x 256^2 tensors)
+        return HF.conv2d(self.uc4(U4, acc=Loc), self.res.weight, self.res.bias, stride=1, pad=1)

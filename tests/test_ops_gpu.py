@@ -1120,6 +1120,40 @@ def test_cat_slot_in_place(prec, N, C, P, H, Ci):
         assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize("prec", ["fp32", "bf16"])
+@pytest.mark.parametrize("N,C,P,H", [(2, 64, 64, 32), (2, 256, 128, 16), (2, 3, 64, 32)])
+def test_pw_mlp_acc_in_place(prec, N, C, P, H):
+    """pw_mlp(..., acc=A) (the G tail uc4(U4) + Loc, MixConvNeXtML.py:236-239): the block output
+    summed into A in place by the shortcut GEMM's epilogue, A returned dirty.  Against block + A as
+    a separate add: the forward to fp32 rounding (one add moved ahead of the MLP's), A's grad is the
+    upstream grad, every other grad bitwise (the backward never reads A)."""
+    from dsgan_hip import functional as HF
+    HF.set_precision(prec)
+    g = torch.Generator().manual_seed(C + P + H + 7)
+    ins = [torch.randn(N, C, H, H, generator=g) for _ in range(2)]
+    prm = [torch.randn(4 * C, C, generator=g) / math.sqrt(C), torch.randn(4 * C, generator=g) * 0.1,
+           torch.randn(P, 4 * C, generator=g) / math.sqrt(4 * C), torch.randn(P, generator=g) * 0.1,
+           torch.randn(P, C, 1, 1, generator=g) / math.sqrt(C)]
+    a0 = torch.randn(N, P, H, H, generator=g)
+    gy = torch.randn(N, P, H, H, generator=g).to(DEV)
+    outs = []
+    for fused in (False, True):
+        dd, xd, ad = _leaf(ins[0]), _leaf(ins[1]), _leaf(a0)
+        Q = [_param(t) for t in prm]
+        a = ad * 1.0   # a non-leaf A, as the local branch's output is
+        y = HF.pw_mlp(dd, xd, *Q, norm=True, acc=a) if fused else HF.add_n(HF.pw_mlp(dd, xd, *Q, norm=True), a)
+        if fused:
+            assert y.data_ptr() == a.data_ptr()
+        y.backward(gy.clone())
+        torch.cuda.synchronize()
+        outs.append([y.detach().cpu(), ad.grad.cpu(), dd.grad.cpu(), xd.grad.cpu()] + [q.grad.cpu() for q in Q])
+    (y1, da1, *r1), (y2, da2, *r2) = outs
+    assert rel(y2, y1) < 1e-6
+    assert torch.equal(da1, gy.cpu()) and torch.equal(da2, gy.cpu())
+    for a, b in zip(r1, r2):
+        assert torch.equal(a, b)
+
+
 @pytest.mark.parametrize("w_bf16,x_bf16", [(0, 0), (1, 1), (1, 0)])
 @pytest.mark.parametrize("M,K,P,nb", [(2048, 512, 4096, 2), (1024, 256, 1024, 3), (256, 64, 256, 2), (4096, 1024, 1024, 1),
                                       (96, 40, 256, 2)])
