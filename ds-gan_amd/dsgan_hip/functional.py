@@ -676,10 +676,12 @@ def copy_into(dst, src):
 # ------------------------------------------------------------------------------------------
 
 class _GradBox:
-    __slots__ = ("buf", "owned")
+    # outer: the box of the tensor this one aliases (share of a shared tensor, e.g. a Block's input
+    # P_i = share(maxpool(R_i))); merged: this box accumulates straight into outer's buffer
+    __slots__ = ("buf", "owned", "outer", "merged")
 
     def __init__(self):
-        self.buf, self.owned = None, False
+        self.buf, self.owned, self.outer, self.merged = None, False, None, False
 
 
 def _box(t):
@@ -698,8 +700,17 @@ def _add_n_raw(out, ts):
 
 
 def _acc_target(box):
-    """(buffer, True) when a kernel may accumulate its grad straight into the box."""
-    if box is not None and box.buf is not None and box.owned:
+    """(buffer, True) when a kernel may accumulate its grad straight into the box.  An empty box
+    whose outer box already owns a buffer merges into it: its consumers accumulate into the outer
+    buffer in-kernel, instead of filling a buffer of their own that ShareFn then adds to the outer
+    one (one add of the whole tensor per nested share)."""
+    if box is None:
+        return None, False
+    if box.buf is None and box.outer is not None:
+        ob, _ = _acc_target(box.outer)
+        if ob is not None:
+            box.buf, box.owned, box.merged = ob, True, True
+    if box.buf is not None and box.owned:
         return box.buf, True
     return None, False
 
@@ -724,13 +735,14 @@ class ShareFn(torch.autograd.Function):
     def forward(ctx, x, box):
         ctx.set_materialize_grads(False)
         ctx.box, ctx.outer = box, _box(x)
+        box.outer = ctx.outer
         return x.view_as(x)
 
     @staticmethod
     def backward(ctx, g):
         box = ctx.box
-        buf, own = box.buf, box.owned
-        box.buf = None
+        buf, own, merged = box.buf, box.owned, box.merged
+        box.buf, box.merged = None, False
         if g is not None:
             if buf is None:
                 buf, own = g, False
@@ -740,6 +752,8 @@ class ShareFn(torch.autograd.Function):
                 nb = _empty(*g.shape, g)
                 _add_n_raw(nb, [buf, g])
                 buf, own = nb, True
+        if merged:
+            return None, None   # every grad already sits in the outer box's buffer
         if ctx.outer is not None:
             _give(ctx.outer, buf, adopt=own)
             return None, None
