@@ -1,7 +1,8 @@
-"""CPU tests of HF.CatSlot, the decoder concatenation buffer whose tail the skip's producer writes
-in place (functional.py CatSlot; MixConvNeXtML.py:229-236 upSample cat).  No kernels run: only the
-aliasing and the holds() check that decides whether a concat node may skip the copy.  A false
-positive there would let a node overwrite a live tensor's head, so the negative cases matter most.
+"""CPU tests of the in-place paths (no kernels run): HF.CatSlot, the decoder concatenation buffer
+whose tail the skip's producer writes in place (functional.py CatSlot; MixConvNeXtML.py:229-236
+upSample cat) -- its aliasing and the holds() check that decides whether a concat node may skip the
+copy, where a false positive would let a node overwrite a live tensor's head; pw_mlp's acc
+validation; and the nested gradient-box merge rule (functional._acc_target).
 """
 import torch
 
@@ -59,3 +60,23 @@ def test_pw_mlp_refuses_a_bad_acc_before_any_launch():
             HF.pw_mlp(h, x, *prm, acc=bad)
     with pytest.raises(ValueError, match="acc"):
         HF.pw_mlp(h, x, *prm, slot=HF.CatSlot(N, P, P, H, H, h), acc=torch.zeros(N, P, H, H))
+
+
+def test_nested_grad_box_merges_only_into_an_owned_outer_buffer():
+    """_acc_target on a box nested in another (share of a shared tensor): it merges into the outer
+    box's buffer only when that buffer is owned (freshly computed, safe to accumulate into), never
+    into a borrowed one (a grad autograd handed over), and an inner box with a buffer of its own
+    keeps it."""
+    outer, inner = HF._GradBox(), HF._GradBox()
+    inner.outer = outer
+    assert HF._acc_target(inner) == (None, False)             # outer empty: nothing to merge into
+    g = torch.zeros(2, 3)
+    outer.buf, outer.owned = g, False
+    assert HF._acc_target(inner) == (None, False) and not inner.merged   # borrowed: no merge
+    outer.owned = True
+    buf, acc = HF._acc_target(inner)
+    assert buf is g and acc and inner.merged and inner.owned
+    own = HF._GradBox()
+    own.outer, own.buf, own.owned = outer, torch.ones(2, 3), True
+    buf, acc = HF._acc_target(own)
+    assert buf is own.buf and buf is not g and not own.merged
