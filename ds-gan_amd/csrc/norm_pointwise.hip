@@ -226,12 +226,24 @@ __global__ __launch_bounds__(NT == 64 ? 256 : NT) void instnorm_fwd_v4(INArgs a)
   if constexpr (C4 > 0) {
     float4 rv[C4];
     float sum = 0.f;
+    // a plane of exactly C4 = 4 float4s per thread takes unguarded loads and stores (the same values
+    // in the same order: same bits).  Build A/B on two boxes (profiles/r04/in_micro_full*.txt): the
+    // 4K-pixel planes of the 256 x 4 form 45 -> 42 us (1024 @ 32^2: 24 -> 22) on both; with C4 = 16
+    // the 16K-pixel planes went 108 -> 113 us on one box and the 64K-pixel ones -4 % on one box,
+    // +2.5 % on the other, so those keep the guarded loop.
+    const bool full = C4 <= 4 && HW4 == C4 * NT;
+    if (full) {
 #pragma unroll
-    for (int j = 0; j < C4; ++j) {
-      const int i = t + j * NT;
-      rv[j] = i < HW4 ? ld(i) : make_float4(0.f, 0.f, 0.f, 0.f);
-      sum += hsum4(rv[j]);
+      for (int j = 0; j < C4; ++j) rv[j] = ld(t + j * NT);
+    } else {
+#pragma unroll
+      for (int j = 0; j < C4; ++j) {
+        const int i = t + j * NT;
+        rv[j] = i < HW4 ? ld(i) : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
     }
+#pragma unroll
+    for (int j = 0; j < C4; ++j) sum += hsum4(rv[j]);
     const float mean = plane_sum<NT>(sum, sh) * inv;
     float sq = 0.f;
 #pragma unroll
@@ -243,10 +255,15 @@ __global__ __launch_bounds__(NT == 64 ? 256 : NT) void instnorm_fwd_v4(INArgs a)
     }
     const float rs = 1.f / sqrtf(plane_sum<NT>(sq, sh) * inv + a.eps);
     if (t == 0) { a.mean[plane] = mean; a.rstd[plane] = rs; }
+    if (full) {
 #pragma unroll
-    for (int j = 0; j < C4; ++j) {
-      const int i = t + j * NT;
-      if (i < HW4) out(i, rv[j], mean, rs);
+      for (int j = 0; j < C4; ++j) out(t + j * NT, rv[j], mean, rs);
+    } else {
+#pragma unroll
+      for (int j = 0; j < C4; ++j) {
+        const int i = t + j * NT;
+        if (i < HW4) out(i, rv[j], mean, rs);
+      }
     }
   } else {
     float sum = 0.f;
