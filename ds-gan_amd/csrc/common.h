@@ -29,6 +29,15 @@ int half_type();   // capi.cpp
 template <typename T> using hx8 = T __attribute__((ext_vector_type(8)));
 template <typename T> using hx4 = T __attribute__((ext_vector_type(4)));
 typedef float f32x16_t __attribute__((ext_vector_type(16)));
+// A raw workgroup barrier (no implicit s_waitcnt: the caller has issued the waits it needs, so
+// LDS-DMA of later stages stays in flight across it) followed by a compiler memory fence.  LLVM
+// models s_barrier as touching no memory, so without the fence the compiler could hoist the next
+// stage's ds_reads above the barrier, before the other waves' DMA into that stage is ordered.
+__device__ __forceinline__ void raw_barrier() {
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
 __device__ __forceinline__ f32x16_t mfma16(hx8<__bf16> a, hx8<__bf16> b, f32x16_t c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
 }

@@ -346,7 +346,7 @@ __global__ __launch_bounds__(512, MINB) void mlp_fwd_kernel(MlpArgs g) {
   glds_chunk<C, P, NW>(smem + W_SZ, smem + W_SZ + HC * C, g.w1, g.w2, 1, wave, lane);
   constexpr int NI = C / 8 / NW + P / 8 / NW;   // LDS-DMA instructions per wave per chunk
   asm volatile("s_waitcnt vmcnt(%0)" ::"i"(NI) : "memory");   // chunk 0 landed (chunk 1 may still fly)
-  __builtin_amdgcn_s_barrier();
+  raw_barrier();
 
   for (int j = 0; j < NCH; ++j) {
     const T16* W1c = smem + (j & 1) * W_SZ;
@@ -385,7 +385,7 @@ __global__ __launch_bounds__(512, MINB) void mlp_fwd_kernel(MlpArgs g) {
     // chunk j+1 landed (each wave waits for its own DMA; the barrier makes all of it visible) and
     // every wave is done reading buffer j&1 -> refill it with chunk j+2
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
+    raw_barrier();
     if (j + 2 < NCH) {
       T16* W1n = smem + (j & 1) * W_SZ;
       glds_chunk<C, P, NW>(W1n, W1n + HC * C, g.w1, g.w2, j + 2, wave, lane);
@@ -650,7 +650,7 @@ __global__ __launch_bounds__(512, MINB) void mlp_dh_kernel(MlpArgs g) {
   glds_chunk<C, P, NW, false>(smem + W_SZ, smem + W_SZ + HC * C, g.w1, g.w2, 1, wave, lane);
   constexpr int NI = C / 8 / NW + P / 8 / NW;
   asm volatile("s_waitcnt vmcnt(%0)" ::"i"(NI) : "memory");
-  __builtin_amdgcn_s_barrier();
+  raw_barrier();
 
   for (int j = 0; j < NCH; ++j) {
     const T16* W1c = smem + (j & 1) * W_SZ;
@@ -693,7 +693,7 @@ __global__ __launch_bounds__(512, MINB) void mlp_dh_kernel(MlpArgs g) {
       }
     }
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
+    raw_barrier();
     if (j + 2 < NCH) {
       T16* W1n = smem + (j & 1) * W_SZ;
       glds_chunk<C, P, NW, false>(W1n, W1n + HC * C, g.w1, g.w2, j + 2, wave, lane);
@@ -808,7 +808,7 @@ __global__ __launch_bounds__(NW * 64, MINB) void mlp_bwd_kernel(MlpArgs g) {
       // chunk j has landed (this wave's pieces: the only LDS-DMA in flight) and every wave is done
       // with chunk j-1 (its ring slot, Zn / Gn, and at j = 0 the h / dy staging area = slot 1)
       asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
+      raw_barrier();
       if (j + 1 < NCH) {
         T16* W1n = (j & 1) ? Ds + D_SZ : Hs;
         glds_chunk<C, P, NW, false>(W1n, W1n + W1_SZ, g.w1, g.w2, j + 1, wave, lane);
@@ -872,7 +872,7 @@ __global__ __launch_bounds__(NW * 64, MINB) void mlp_bwd_kernel(MlpArgs g) {
       }
     if constexpr (DMA) {   // raw barrier: the next chunk's LDS-DMA stays in flight across it
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
+      raw_barrier();
     } else {
       __syncthreads();
     }
@@ -1063,7 +1063,7 @@ __global__ __launch_bounds__(256, 1) void mlp_bwd_dma_kernel(MlpArgs g) {
     // chunk j landed (this wave's pieces: the only LDS-DMA in flight) and every wave is done with
     // chunk j-1 (its ring slot, Zn / Gn; at j = 0 the h / dy staging area = slot 1)
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
+    raw_barrier();
     if (j + 1 < NCH) chunk_dma(j + 1, Wnext);
     const T16* W2s = W1s + W1_SZ;
     mf32x16 zacc, tacc;
@@ -1106,7 +1106,7 @@ __global__ __launch_bounds__(256, 1) void mlp_bwd_dma_kernel(MlpArgs g) {
       *reinterpret_cast<mbf16x4*>((char*)Zn + o) = dv4;
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // raw barrier: chunk j+1's DMA stays in flight
-    __builtin_amdgcn_s_barrier();
+    raw_barrier();
     // copy-out: 8 pixels of one hidden row per lane -> 16-byte stores; dz sums per 32 pixels
     {
       float bacc = 0.f;

@@ -466,7 +466,7 @@ __global__ __launch_bounds__(128 * WN, WN == 2 ? 2 : 1) void pwgemm_kernel(PwArg
       else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       static_assert(NS <= 4, "vmcnt ladder covers <= 2 later stages");
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();   // every wave's pieces of stage kt landed; slot (kt-1) % NS is free
+      raw_barrier();   // every wave's pieces of stage kt landed; slot (kt-1) % NS is free
       if (kt + NS - 1 < nk) issue(kt + NS - 1);
       const T16* As = smem + (kt % NS) * (DA_SZ + DB_SZ);
       const T16* Bs = As + DA_SZ;

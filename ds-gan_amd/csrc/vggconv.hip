@@ -310,7 +310,7 @@ __global__ __launch_bounds__(512, 1) void vconv3x3_dma_kernel(VcArgs<T16> g) {
   for (int kc = 0; kc < nkc; ++kc) {
     dma_wait_all();                 // this wave's pieces of chunk kc have landed
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();   // every wave's pieces landed; every wave is done with chunk kc-1
+    raw_barrier();   // every wave's pieces landed; every wave is done with chunk kc-1
     if (kc + 1 < nkc) issue(kc + 1, (kc + 1) & 1);
     const T16* Ab = reinterpret_cast<const T16*>(reinterpret_cast<const char*>(smem) + (kc & 1) * STAGE);
     const T16* Bb = Ab + A_BYTES / 2;

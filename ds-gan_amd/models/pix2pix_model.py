@@ -130,6 +130,9 @@ class Pix2PixModel(BaseModel):
             self._graphs = None
             self._graph_key = None
             self._graph_warm = False
+            # optimizer-step calls per network: host counters, since a graph replay never enters
+            # FlatAdam.step (the scalers count the applied steps on the device)
+            self.step_calls = {"G": 0, "D": 0}
 
     def set_input(self, input):
         AtoB = self.opt.which_direction == "AtoB"
@@ -231,7 +234,21 @@ class Pix2PixModel(BaseModel):
         feats, self._real_feats = self._real_feats, None
         return feats
 
+    def nonfinite_report(self):
+        """{'G': (skipped, calls), 'D': (skipped, calls)}: optimizer steps the non-finite guard (or
+        the fp16 loss scaler) skipped so far, out of the steps called.  Empty without scalers.
+        Reads the scalers' device state, so it synchronises: call it at logging time only."""
+        out = {}
+        for net, sc in (("G", self.scaler_G), ("D", self.scaler_D)):
+            if sc is not None:
+                n = self.step_calls[net]
+                out[net] = (n - sc.applied_steps(), n)
+        return out
+
     def optimize_parameters(self):
+        self.step_calls["G"] += 1
+        if self.use_gan == 1:
+            self.step_calls["D"] += 1
         if self.cuda_graph and not self.exchange and self.g_buckets is None:
             return self._graph_step()
         self._launch_real_features()

@@ -63,6 +63,35 @@ def global_losses(losses, n_local, n_global):
     return type(losses)(zip(losses.keys(), t.tolist()))
 
 
+class NonfiniteMonitor:
+    """Reports the optimizer steps that the bf16 non-finite guard or the fp16 loss scaler skipped
+    (``Pix2PixModel.nonfinite_report``), so that a network that stops learning shows in the log.
+
+    ``poll()`` runs at logging time.  It returns the text appended to the loss line: empty while no
+    step was ever skipped, else the running counts, e.g. ``skipped G 3/400 D 0/400``.  When every
+    step of one network since the previous poll was skipped, and there were at least
+    ``abort_window`` of them, the network is no longer training: ``poll()`` raises RuntimeError."""
+
+    def __init__(self, model, abort_window=50):
+        self.model = model
+        self.abort_window = int(abort_window)
+        self.last = {}
+
+    def poll(self):
+        rep = self.model.nonfinite_report() if hasattr(self.model, "nonfinite_report") else {}
+        dead = []
+        for net, (skipped, calls) in rep.items():
+            s0, c0 = self.last.get(net, (0, 0))
+            if calls - c0 >= self.abort_window and skipped - s0 == calls - c0:
+                dead.append("%s skipped all of its last %d optimizer steps" % (net, calls - c0))
+        self.last = dict(rep)
+        if dead:
+            raise RuntimeError("non-finite gradients: " + "; ".join(dead) + " (--nonfinite_guard)")
+        if not any(s for s, _ in rep.values()):
+            return ""
+        return "skipped " + " ".join("%s %d/%d" % (k, s, c) for k, (s, c) in rep.items()) + " "
+
+
 def main(argv=None, output_freq=100):
     from data import CreateDataLoader
     from models import create_model
@@ -86,6 +115,7 @@ def main(argv=None, output_freq=100):
     model = create_model(opt)
     model.setup(opt)
     metrics = TrainMetrics(model.device)
+    guard = NonfiniteMonitor(model)
     history = []
     for epoch in range(opt.epoch_count, opt.niter + opt.niter_decay + 1):
         metrics.reset()
@@ -107,13 +137,14 @@ def main(argv=None, output_freq=100):
             if (i + 1) % output_freq == 0:
                 losses = global_losses(model.get_current_losses(), int(model.real_A.shape[0]),
                                        int(data.get("global_batch", model.real_A.shape[0])))
+                skipped = guard.poll()   # every rank: a network that stopped learning ends every rank
                 if rank != 0:
                     continue
                 ssim_avg, psnr_avg = metrics.averages()
                 t = (time.time() - iter_start_time) / opt.batchSize
                 message = "(epoch: %d, iters: %d, time: %.3f) " % (epoch, epoch_iter, t)
                 message += "".join("%s: %.3f " % (k, v) for k, v in losses.items())
-                print(message + "ssim: %.4f psnr: %.3f" % (ssim_avg, psnr_avg))
+                print(message + "ssim: %.4f psnr: %.3f" % (ssim_avg, psnr_avg) + (" " + skipped if skipped else ""))
                 with open(os.path.join(out, "result.csv"), "a", newline="") as f:
                     csv.writer(f).writerow([epoch, "".join("%s: %.3f " % (k, v) for k, v in losses.items()) + "  ",
                                             ssim_avg, psnr_avg])

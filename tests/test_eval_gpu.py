@@ -161,3 +161,27 @@ def test_train_loop_metrics_vs_oracle(tmp_path):
     assert abs(p - O.cal_psnr(lab, res)) < 1e-4, (p, O.cal_psnr(lab, res))
     assert os.path.exists(tmp_path / "out" / "each_epoch.csv")
     assert os.path.exists(tmp_path / "out" / "checkpoints" / model.opt.name / "1_useSE_net_G.pth")
+
+
+def test_nonfinite_skips_are_logged():
+    """a step the bf16 non-finite guard skips shows in train.py's loss line.  One batch
+    with a NaN pixel makes both networks' gradients non-finite: that step is skipped (graph replay
+    included), the steps around it apply, and NonfiniteMonitor reports the counts."""
+    import train as T
+    from options.train_options import default_train_opt
+    from models import create_model
+    torch.manual_seed(20)
+    model = create_model(default_train_opt(gpu_ids=[0], precision="bf16", batchSize=1, pool_size=0))
+    assert model.scaler_G is not None and model.scaler_D is not None   # the guard is on by default in bf16
+    mon = T.NonfiniteMonitor(model, abort_window=3)
+    A, B = synth_pair(1, 64, seed=4)
+    bad = A.clone()
+    bad[0, 0, 5, 7] = float("nan")
+    for i, a in enumerate((A, A, bad, A)):
+        model.set_input({"A": a.to(DEV), "B": B.to(DEV), "A_paths": [""], "B_paths": [""]})
+        model.optimize_parameters()
+        if i == 1:
+            assert mon.poll() == ""      # nothing skipped yet: the line is unchanged
+    assert model.nonfinite_report() == {"G": (1, 4), "D": (1, 4)}
+    assert mon.poll() == "skipped G 1/4 D 1/4 "
+    assert all(torch.isfinite(p).all() for p in (model.flatG.data, model.flatD.data))

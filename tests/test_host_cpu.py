@@ -232,3 +232,28 @@ def test_image_pool_refuses_a_shape_change():
         pool.query(torch.zeros(1, 3, 8, 8))
     with pytest.raises(ValueError):
         pool.query(torch.zeros(1, 3, 4, 4, dtype=torch.float64))
+
+
+def test_nonfinite_monitor_reports_and_aborts():
+    """train.NonfiniteMonitor: silent while nothing is skipped, running counts once a
+    step is skipped, and an error once a whole window of one network's steps was skipped."""
+    import train as T
+
+    class FakeModel:
+        rep = {"G": (0, 0), "D": (0, 0)}
+
+        def nonfinite_report(self):
+            return dict(self.rep)
+
+    m = FakeModel()
+    mon = T.NonfiniteMonitor(m, abort_window=4)
+    m.rep = {"G": (0, 10), "D": (0, 10)}
+    assert mon.poll() == ""
+    m.rep = {"G": (2, 20), "D": (0, 20)}
+    assert mon.poll() == "skipped G 2/20 D 0/20 "
+    m.rep = {"G": (3, 23), "D": (3, 23)}          # a window of 3 < abort_window: reported only
+    assert mon.poll() == "skipped G 3/23 D 3/23 "
+    m.rep = {"G": (3, 27), "D": (7, 27)}          # D skipped all 4 of its last steps
+    with pytest.raises(RuntimeError, match="D skipped all of its last 4"):
+        mon.poll()
+    assert T.NonfiniteMonitor(object()).poll() == ""   # a model without scalers
