@@ -33,3 +33,9 @@ def golden():
 def golden_v3():
     import numpy as np
     return np.load(os.path.join(REPO, "tests", "golden", "golden_v3.npz"))
+
+
+@pytest.fixture(scope="session")
+def golden_v4():
+    import numpy as np
+    return np.load(os.path.join(REPO, "tests", "golden", "golden_v4.npz"))

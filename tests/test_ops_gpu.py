@@ -401,6 +401,44 @@ def test_wconv_bf16(half, N, C, H, W, M, K, s, p):
     assert rel(db - db0.to(DEV), dy.double().sum(dim=(0, 2, 3))) < 1e-6
 
 
+@pytest.mark.parametrize("N,C,H,W,M,s", [
+    (16, 64, 128, 128, 128, 2),    # PatchGAN layer 1 at B = 16 (64 x 64 output)
+    (16, 128, 64, 64, 256, 2),     # layer 2 (32 x 32)
+    (16, 256, 32, 32, 512, 1),     # layer 3, stride 1 (31 x 31: ragged in both block dimensions)
+    (1, 256, 6, 8, 512, 1),        # one partial 16 x 4 pixel block per image: fewer blocks than the split target
+    (3, 64, 10, 40, 96, 2),        # 5 x 20 outputs, M not a multiple of the 64-row tile
+])
+def test_wconv_db_fold_vs_channel_sum(N, C, H, W, M, s):
+    """the PatchGAN 4x4 weight-grad's folded bias grad (dsgan_wconv_db) against the
+    separate channel-sum kernel, at the step's shapes and at ragged / under-filled ones, with the
+    caching allocator's free blocks poisoned with NaN first -- a read of scratch no workgroup
+    wrote, or of a D element outside the tensor, turns db non-finite here instead of in training."""
+    from dsgan_hip import functional as HF
+    HF.set_precision("bf16")
+    g = torch.Generator().manual_seed(N + C + H + M)
+    Ho, Wo = (H + 2 - 4) // s + 1, (W + 2 - 4) // s + 1
+    x = torch.randn(N, C, H, W, generator=g).to(DEV)
+    dy = torch.randn(N, M, Ho, Wo, generator=g).to(DEV)
+    ws_need = HF._lib.load().dsgan_wconv_workspace(N, C, M, Ho, Wo, 4, 4)
+    poison = torch.full((ws_need * 2 + (1 << 20),), float("nan"), device=DEV)
+    del poison   # its block returns to the allocator: the next scratch allocation starts as NaN
+    dw1, db1 = torch.zeros(M, C, 4, 4, device=DEV), torch.zeros(M, device=DEV)
+    old = HF.WCONV_DB_FOLD
+    HF.WCONV_DB_FOLD = True
+    try:
+        assert HF.conv_wgrad_raw(dy, x, dw1, s, 1, db=db1)
+    finally:
+        HF.WCONV_DB_FOLD = old
+    db2, dw2 = torch.zeros(M, device=DEV), torch.zeros(M, C, 4, 4, device=DEV)
+    HF.conv_wgrad_raw(dy, x, dw2, s, 1)
+    HF.channel_sum_raw(dy, db2)
+    torch.cuda.synchronize()
+    assert torch.isfinite(db1).all() and torch.isfinite(dw1).all()
+    assert torch.equal(dw1, dw2)
+    ref = dy.double().sum(dim=(0, 2, 3))
+    assert rel(db1, ref) < 1e-6 and rel(db2, ref) < 1e-6, (rel(db1, ref), rel(db2, ref))
+
+
 @pytest.mark.parametrize("N,C,H,P", [(2, 64, 16, 128), (2, 128, 16, 64), (3, 128, 16, 256), (2, 256, 16, 128),
                                      (1, 128, 32, 64)])
 @pytest.mark.parametrize("half", HALVES)

@@ -208,3 +208,31 @@ def test_chunked_oracle_step_equals_full_step():
             ga, gb = a[k].grad, b[k].grad
             assert (ga - gb).norm() <= 1e-5 * max(ga.norm(), 1e-30) + 1e-12, k
             assert torch.allclose(a[k], b[k], rtol=0, atol=1e-9), k
+
+
+def test_step_256_matches_reference(golden_v4):
+    """The oracle's fp32 step at the north-star shape (256x256, batch 2, pool 0, fanin recipe) vs the
+    reference's own step there (tests/golden/gen_golden_v4.py): the nine losses, the fake_B sample
+    and probe dots, and every gradient's norm and probe dot.  Bars: the reference's own fp32 error
+    (its fp32 vs fp64 run) and its 1-ulp conditioning (S4_*_spread_*), as in the 64^2 golden tests."""
+    g = golden_v4
+    A, B = synth_pair(2, 256, seed=int(g["S4_input_seed"]))
+    st = O.OracleStep(make_params(O.g_param_spec(), "fanin", 1000), make_params(O.d_param_spec(), "fanin", 5000),
+                      make_params(O.vgg_param_spec(False), "vgg", 7000), pool_size=0)
+    st.step(A, B)
+    L = st.losses
+    mine = np.array([L["G_GAN"], L["G_L1"], L["D_real"], L["D_fake"], L["vgg"], L["tv"], L["ssim"], L["G"], L["D"]])
+    ref = g["S4_fanin_f32_losses"]
+    assert np.allclose(mine, ref, rtol=2e-5, atol=1e-7), (mine, ref)
+    fake = st.fake_B.double()
+    assert np.allclose(fake[:, :, ::8, ::8].numpy(), g["S4_fanin_f32_fake_sub"], rtol=1e-4, atol=1e-5)
+    pd = np.array([float(probe(fake.numel(), 70000 + j) @ fake.flatten()) for j in range(4)])
+    assert np.allclose(pd, g["S4_fanin_f32_fake_pdot"], rtol=1e-4, atol=1e-4)
+    for params, nm in ((st.gp, "G"), (st.dp, "D")):
+        d32, d64 = g["S4_fanin_f32_%s_gdot" % nm], g["S4_fanin_f64_%s_gdot" % nm]
+        n64, spr = g["S4_fanin_f64_%s_gnorm" % nm], g["S4_fanin_spread_%s_gvec" % nm]
+        for i, (k, v) in enumerate(params.items()):
+            gr = v.grad.double().flatten()
+            bar = max(2 * abs(d32[i] - d64[i]), 1e-3 * n64[i], 8 * spr[i]) + 1e-6
+            assert abs(float(gr @ probe(gr.numel(), 90000 + i)) - d64[i]) <= bar, (nm, k)
+            assert abs(float(gr.norm()) - n64[i]) <= bar, (nm, k)
