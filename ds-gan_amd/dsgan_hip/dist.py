@@ -28,6 +28,21 @@ def rank():
     return dist.get_rank() if dist.is_available() and dist.is_initialized() else 0
 
 
+def backend():
+    """The process group's backend ("nccl" = RCCL on ROCm, "gloo"), or None without one."""
+    return dist.get_backend() if dist.is_available() and dist.is_initialized() else None
+
+
+def all_ranks_true(flag, device):
+    """True when ``flag`` holds on every rank (one tiny MIN all-reduce; the flag itself on one rank).
+    The graph step uses it so that every rank replays captured graphs, or none does."""
+    if world_size() == 1:
+        return bool(flag)
+    t = torch.tensor([1 if flag else 0], dtype=torch.int32, device=device if backend() == "nccl" else "cpu")
+    dist.all_reduce(t, op=dist.ReduceOp.MIN)
+    return bool(t.item())
+
+
 def broadcast_params(flat, src=0):
     if world_size() > 1:
         dist.broadcast(flat.data, src)

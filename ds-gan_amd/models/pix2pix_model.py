@@ -119,17 +119,17 @@ class Pix2PixModel(BaseModel):
             self._vgg_stream = torch.cuda.Stream(self.device)
             self._real_feats = None
             self._feats_joined = False
-            # the step as two captured HIP graphs (see _graph_step): one process, optimizer step counts
-            # on the device (the fp16 scalers or the bf16 guard), no RCCL exchange inside the step
+            # the step as two captured HIP graphs (see _graph_step): optimizer step counts on the
+            # device (the fp16 scalers or the bf16 guard); under DDP the RCCL exchanges are captured
+            # into the second graph, so the process group must be RCCL ("nccl"), not gloo
             cg = int(getattr(opt, "cuda_graph", -1))
-            can = W == 1 and self.scaler_G is not None
+            can = self.scaler_G is not None and (W == 1 or hdist.backend() == "nccl")
             if cg == 1 and not can:
-                raise ValueError("--cuda_graph 1 needs one process and device-side step counts "
-                                 "(--precision fp16, or bf16 with the non-finite guard)")
+                raise ValueError("--cuda_graph 1 needs device-side step counts (--precision fp16, or bf16 "
+                                 "with the non-finite guard) and, under DDP, the RCCL backend")
             self.cuda_graph = can and cg != 0
-            self._graphs = None
-            self._graph_key = None
-            self._graph_warm = False
+            self._graphs = {}          # (input shapes, mean_w) -> one captured graph pair (_capture)
+            self._graph_warm = set()   # the keys whose eager warm-up step has run
             # optimizer-step calls per network: host counters, since a graph replay never enters
             # FlatAdam.step (the scalers count the applied steps on the device)
             self.step_calls = {"G": 0, "D": 0}
@@ -138,17 +138,17 @@ class Pix2PixModel(BaseModel):
         AtoB = self.opt.which_direction == "AtoB"
         A = input["A" if AtoB else "B"].to(self.device, non_blocking=True)
         B = input["B" if AtoB else "A"].to(self.device, non_blocking=True)
-        if self._graphs is not None and A.shape == self._static_A.shape and B.shape == self._static_B.shape:
-            # captured graphs read the static input buffers
-            self._static_A.copy_(A, non_blocking=True)
-            self._static_B.copy_(B, non_blocking=True)
-            A, B = self._static_A, self._static_B
-        self.real_A, self.real_B = A, B
         self.image_paths = input["A_paths" if AtoB else "B_paths"]
         if self.isTrain:
             W = hdist.world_size()
-            n = int(self.real_A.shape[0])
+            n = int(A.shape[0])
             self.mean_w = float(W * n) / float(input.get("global_batch", W * n))
+            ent = self._graphs.get(self._graph_key(A, B, self.mean_w))
+            if ent is not None:   # a captured graph pair reads its static input buffers
+                ent["vars"]["real_A"].copy_(A, non_blocking=True)
+                ent["vars"]["real_B"].copy_(B, non_blocking=True)
+                A, B = ent["vars"]["real_A"], ent["vars"]["real_B"]
+        self.real_A, self.real_B = A, B
 
     def forward(self):
         self.fake_B = self.netG(self.real_A)
@@ -249,8 +249,11 @@ class Pix2PixModel(BaseModel):
         self.step_calls["G"] += 1
         if self.use_gan == 1:
             self.step_calls["D"] += 1
-        if self.cuda_graph and not self.exchange and self.g_buckets is None:
+        if self.cuda_graph:
             return self._graph_step()
+        self._eager_step()
+
+    def _eager_step(self):
         self._launch_real_features()
         self.forward()
         self._d_and_g_steps()
@@ -261,40 +264,59 @@ class Pix2PixModel(BaseModel):
     # (DSGAN/util/image_pool.py:17-31), so the step is split around it: graph A = the VGG16
     # real-feature pass (side stream, joined inside A) + G forward + cat(real_A, fake_B); the pool
     # query runs eagerly into a static buffer (the same draws, in the same order, as the reference);
-    # graph B = the D step and the G step (backward, scaler checks, both Adams).  Everything a replay
-    # needs from the host is fixed at capture: shapes, loss weights, the learning rates (a change
-    # re-captures) and the Adam step counts (device-side under the scalers / guard).
+    # graph B = the D step and the G step (backward, scaler checks, both Adams) and, under DDP, the
+    # RCCL exchanges: the D all-reduce before optimizer_D.step() and the G buckets, started from the
+    # autograd thread as their weight-grads are launched, exactly as in the eager step -- captured,
+    # they replay on RCCL's stream with the same dependencies (every rank captures the same
+    # collectives in the same order, as the eager step already requires).
+    # Everything a replay needs from the host is fixed at capture: shapes, loss weights, the
+    # learning rates and the Adam step counts (device-side under the scalers / guard).  One graph
+    # pair is kept per input shape and loss weight (with one process a ragged last batch gets its
+    # own, captured once, after one eager warm-up step of that shape); a learning-rate change
+    # re-captures that shape's pair.
+    @staticmethod
+    def _graph_key(A, B, mean_w):
+        return (tuple(A.shape), tuple(B.shape), mean_w)
+
     def _graph_step(self):
-        key = (tuple(self.real_A.shape), tuple(self.real_B.shape), self.mean_w,
-               tuple(float(o.param_groups[0]["lr"]) for o in self.optimizers))
-        if self._graphs is None or key != self._graph_key:
-            if not self._graph_warm:   # one eager step first (lazy allocations, cached weight copies)
-                self._graph_warm = True
-                self._launch_real_features()
-                self.forward()
-                self._d_and_g_steps()
-                return
+        if self.mean_w != 1.0 and hdist.world_size() > 1:
+            # a ragged global batch under DDP: the ranks' chunks differ in size, so their graph keys
+            # would too, and the capture / replay decisions (with the capture's one agreement
+            # all-reduce) must be the same on every rank -- those steps run eager.  mean_w is 1 on
+            # every rank or on none (W * n == the global batch only when all chunks are equal).
+            return self._eager_step()
+        key = self._graph_key(self.real_A, self.real_B, self.mean_w)
+        lrs = tuple(float(o.param_groups[0]["lr"]) for o in self.optimizers)
+        ent = self._graphs.get(key)
+        if ent is not None and ent["lr"] != lrs:
+            # a learning-rate change: re-capture (set_input copied the inputs into this pair's static
+            # buffers, which real_A / real_B point at; _capture clones them)
+            del self._graphs[key]
+            ent = None
+        if ent is None:
+            if key not in self._graph_warm:   # one eager step first (lazy allocations, cached weight copies)
+                self._graph_warm.add(key)
+                return self._eager_step()
+            err = None
             try:
-                self._capture(key)
+                ent = self._capture(lrs)
             except Exception as e:   # noqa: BLE001 -- a capture failure must not end the run: eager from here on
-                print("[Pix2PixModel] HIP graph capture failed (%r): running the eager step" % (e,))
-                self._graphs, self.cuda_graph, self._feats_joined = None, False, False
+                err = e
+            if not hdist.all_ranks_true(err is None, self.device):   # every rank replays, or none does
+                print("[Pix2PixModel] HIP graph capture failed (%r): running the eager step" % (err,))
+                self._graphs, self.cuda_graph, self._feats_joined = {}, False, False
+                HF.GRAD_READY[0] = None
                 torch.cuda.synchronize(self.device)
-                self._launch_real_features()
-                self.forward()
-                self._d_and_g_steps()
-                return
-        gA, gB = self._graphs
-        gA.replay()
+                return self._eager_step()
+            self._graphs[key] = ent
+        self.__dict__.update(ent["vars"])   # this pair's outputs / losses / static inputs
+        ent["gA"].replay()
         if self.use_gan == 1 and self.use_condition == 1:
             self.fake_AB_pool.query(self._cat_fake, out=self._fake_AB_buf)
-        gB.replay()
+        ent["gB"].replay()
 
-    def _capture(self, key):
-        self._graphs = None
-        self._static_A = self.real_A.clone()
-        self._static_B = self.real_B.clone()
-        self.real_A, self.real_B = self._static_A, self._static_B
+    def _capture(self, lrs):
+        self.real_A, self.real_B = self.real_A.clone(), self.real_B.clone()   # the static inputs
         torch.cuda.synchronize(self.device)
         pool = torch.cuda.graph_pool_handle()
         gA, gB = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
@@ -312,7 +334,11 @@ class Pix2PixModel(BaseModel):
                 self._d_and_g_steps(self._fake_AB_buf if cond else None)
         finally:
             self._feats_joined = False
-        self._graphs, self._graph_key = (gA, gB), key
+            HF.GRAD_READY[0] = None
+        # every tensor attribute the captured step left on the model (static inputs, fake_B, the
+        # losses, ...): restored before each replay of this pair
+        tvars = {k: v for k, v in self.__dict__.items() if torch.is_tensor(v)}
+        return {"gA": gA, "gB": gB, "lr": lrs, "vars": tvars}
 
     def _d_and_g_steps(self, fake_AB=None):
         if self.use_gan == 1:

@@ -20,7 +20,8 @@ one GPU: a 1-rank group with the D all-reduce (ReduceOp.AVG) and the G buckets (
 from the autograd thread during backward_G) forced on must give bitwise the flat gradients and
 post-step parameters of the same step without any exchange -- a bucket launched on RCCL's stream
 before its weight-grad kernels finished, or an optimizer step that did not wait for it, changes
-bits.
+bits.  The same holds with the step replayed from its HIP graphs, the exchanges captured into the
+second graph (the multi-GPU bench and train loop run that way).
 """
 import os
 import random
@@ -146,19 +147,22 @@ def _nccl_worker(port, out_dir):
     from oracle.recipe import synth_pair
     from dsgan_hip import dist as hdist
     res = {}
-    for mode in ("plain", "exchange", "plain2"):
+    for mode in ("plain", "exchange", "exchange_graph", "plain2"):
         m = _model("bf16")
-        if mode == "exchange":
+        m.cuda_graph = mode == "exchange_graph"
+        if mode.startswith("exchange"):
             m.exchange = True
             # small buckets: several async RCCL all-reduces start during backward_G
             m.g_buckets = hdist.GradBuckets(m.flatG.grad, m.flatG.layout, bucket_mb=4)
             assert len(m.g_buckets.buckets) >= 8
-        for it in range(2):
+        for it in range(4):   # graph mode: eager warm-up, capture + replay, two replays
             A, B = synth_pair(2, 64, seed=40 + it)
             m.set_input({"A": A.cuda(), "B": B.cuda(), "A_paths": ["a"] * 2, "B_paths": ["b"] * 2})
             m.optimize_parameters()
-            if mode == "exchange":
+            if mode.startswith("exchange"):
                 assert m.g_buckets.pending is None
+        if mode == "exchange_graph":   # the exchanges were captured: the step replayed from its graphs
+            assert m.cuda_graph and len(m._graphs) == 1
         torch.cuda.synchronize()
         res[mode] = {"gG": m.flatG.grad.detach().cpu().clone(), "gD": m.flatD.grad.detach().cpu().clone(),
                      "pG": m.flatG.data.detach().cpu().clone(), "pD": m.flatD.data.detach().cpu().clone()}
@@ -178,3 +182,4 @@ def test_one_rank_rccl_exchange_is_bitwise_neutral(tmp_path):
     for k in ("gG", "gD", "pG", "pD"):
         assert torch.equal(r["plain"][k], r["plain2"][k]), ("step not deterministic", k)
         assert torch.equal(r["plain"][k], r["exchange"][k]), k
+        assert torch.equal(r["plain"][k], r["exchange_graph"][k]), ("graph replay with captured RCCL exchanges", k)

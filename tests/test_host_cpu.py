@@ -83,7 +83,9 @@ def _ddp_worker(rank, world, port, q):
     from dsgan_hip import dist as hdist
     buf = torch.arange(10, dtype=torch.float32) * (rank + 1)
     hdist.allreduce_mean_(buf, bucket_mb=1e-5)   # many tiny buckets
-    q.put((rank, buf.tolist()))
+    # the graph step's capture agreement: every rank replays, or none does
+    agree = (hdist.all_ranks_true(True, "cpu"), hdist.all_ranks_true(rank == 0, "cpu"), hdist.backend())
+    q.put((rank, (buf.tolist(), agree)))
     dist.destroy_process_group()
 
 
@@ -100,7 +102,8 @@ def test_allreduce_mean_gloo_world2():
     for p in ps:
         p.join(timeout=60)
     expect = (torch.arange(10, dtype=torch.float32) * 1.5).tolist()
-    assert out[0] == expect and out[1] == expect
+    assert out[0][0] == expect and out[1][0] == expect
+    assert out[0][1] == out[1][1] == (True, False, "gloo")
 
 
 def _write_pairs(d, n, H, W, seed=0):
