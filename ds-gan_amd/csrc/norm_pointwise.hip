@@ -830,6 +830,154 @@ __global__ void maxpool_bwd_row_kernel(const float* __restrict__ dy, long dy_bs,
   }
 }
 
+// ---- multi-scale max-pool pyramid (the generator's skip pyramids, MixConvNeXtML.py:328-426) ----
+// MaxPool2d(2), (4), (8), (16) of one tensor from ONE read of it: R1 feeds the encoder's k = 2 pool
+// and downSkip's k = 4 / 8 / 16 branches, R2 k = 2 / 4 / 8, R3 k = 2 / 4.  A wave owns a 16-row x
+// 64-column tile of a plane; lane (r4 = lane / 16, c4 = lane % 16) holds the 4 x 4 input block at
+// rows 4 r4.., cols 4 c4.. (four 16-byte row loads).  k = 2 and k = 4 scan the lane's block in
+// row-major order with torch's rule (v > best || isnan(v), initial index = the window's first
+// element); k = 8 and k = 16 merge 2 x 2 neighbour lanes' results (shuffles), keeping what a
+// row-major scan of the whole window keeps: any NaN beats a number and the later NaN beats an
+// earlier one; otherwise the larger value, and of equal values the smaller flat index.  Each
+// sub-window's result is the first max / last NaN of its own row-major scan, and a rectangular
+// sub-window's elements keep their relative row-major order inside the window, so the merge is
+// exactly the window's scan: bit-exact values and int32 indices.
+__device__ __forceinline__ void mp_merge(float& bv, int& bi, float v, int i) {
+  if (isnan(bv)) {
+    if (isnan(v) && i > bi) { bv = v; bi = i; }
+  } else if (isnan(v) || v > bv || (v == bv && i < bi)) {
+    bv = v; bi = i;
+  }
+}
+struct PyrPtrs {
+  float* y[4]; int* idx[4];                // forward outputs (levels k = 2, 4, 8, 16), dense [N][C][H/k][W/k]
+  const float* dy[4]; long dy_bs[4];       // backward: output grads (nullable = no grad), batch strides
+};
+template <int L>
+__global__ __launch_bounds__(256) void maxpool_pyr_fwd_kernel(const float* __restrict__ x, long x_bs, PyrPtrs p,
+                                                             int C, int H, int W, long nwaves) {
+  const long g = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (g >= nwaves) return;   // whole waves exit; no barrier below
+  const int lane = threadIdx.x & 63, r4 = lane >> 4, c4 = lane & 15;
+  const int TW = W >> 6, TP = (H >> 4) * TW;
+  const int plane = (int)(g / TP), t = (int)(g - (long)plane * TP);
+  const int n = plane / C, c = plane - n * C;
+  const int bh = (t / TW) * 16 + 4 * r4, bw = (t % TW) * 64 + 4 * c4;
+  const float* xp = x + (long)n * x_bs + (long)c * H * W + (long)bh * W + bw;
+  float v[4][4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const float4 q = *reinterpret_cast<const float4*>(xp + (long)r * W);
+    v[r][0] = q.x; v[r][1] = q.y; v[r][2] = q.z; v[r][3] = q.w;
+  }
+  const int base = bh * W + bw;
+  {   // k = 2: four windows, two 8-byte value / index stores per lane
+    const int W2 = W >> 1;
+    const long o = (long)plane * (H >> 1) * W2 + (long)(bh >> 1) * W2 + (bw >> 1);
+#pragma unroll
+    for (int a = 0; a < 2; ++a) {
+      float bv[2]; int bi[2];
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        bv[b] = -INFINITY; bi[b] = base + 2 * a * W + 2 * b;
+#pragma unroll
+        for (int r = 2 * a; r < 2 * a + 2; ++r)
+#pragma unroll
+          for (int j = 2 * b; j < 2 * b + 2; ++j) mp_pick(v[r][j], base + r * W + j, bv[b], bi[b]);
+      }
+      *reinterpret_cast<float2*>(p.y[0] + o + a * W2) = make_float2(bv[0], bv[1]);
+      *reinterpret_cast<int2*>(p.idx[0] + o + a * W2) = make_int2(bi[0], bi[1]);
+    }
+  }
+  if constexpr (L >= 2) {   // k = 4: the lane's whole block
+    float bv = -INFINITY; int bi = base;
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) mp_pick(v[r][j], base + r * W + j, bv, bi);
+    const int W4 = W >> 2;
+    const long o4 = (long)plane * (H >> 2) * W4 + (long)(bh >> 2) * W4 + (bw >> 2);
+    p.y[1][o4] = bv;
+    p.idx[1][o4] = bi;
+    if constexpr (L >= 3) {   // k = 8: 2 x 2 lanes
+      mp_merge(bv, bi, __shfl_xor(bv, 1, 64), __shfl_xor(bi, 1, 64));
+      mp_merge(bv, bi, __shfl_xor(bv, 16, 64), __shfl_xor(bi, 16, 64));
+      if (((r4 | c4) & 1) == 0) {
+        const int W8 = W >> 3;
+        const long o8 = (long)plane * (H >> 3) * W8 + (long)(bh >> 3) * W8 + (bw >> 3);
+        p.y[2][o8] = bv;
+        p.idx[2][o8] = bi;
+      }
+      if constexpr (L >= 4) {   // k = 16: 4 x 4 lanes
+        mp_merge(bv, bi, __shfl_xor(bv, 2, 64), __shfl_xor(bi, 2, 64));
+        mp_merge(bv, bi, __shfl_xor(bv, 32, 64), __shfl_xor(bi, 32, 64));
+        if (((r4 | c4) & 3) == 0) {
+          const int W16 = W >> 4;
+          const long o16 = (long)plane * (H >> 4) * W16 + (long)(bh >> 4) * W16 + (bw >> 4);
+          p.y[3][o16] = bv;
+          p.idx[3][o16] = bi;
+        }
+      }
+    }
+  }
+}
+// The pyramid's backward in one pass: each lane owns its 4 x 4 block of dx and adds, per level with a
+// gradient, the output grad of the window whose argmax lies in the block -- a gather, no atomics.
+// Per element the order is fixed: dx (accumulate) + k=2 + k=4 + k=8 + k=16 (at most one term per level).
+template <int L>
+__global__ __launch_bounds__(256) void maxpool_pyr_bwd_kernel(PyrPtrs p, float* __restrict__ dx, long dx_bs, int C,
+                                                             int H, int W, long nwaves, int accumulate) {
+  const long g = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (g >= nwaves) return;
+  const int lane = threadIdx.x & 63, r4 = lane >> 4, c4 = lane & 15;
+  const int TW = W >> 6, TP = (H >> 4) * TW;
+  const int plane = (int)(g / TP), t = (int)(g - (long)plane * TP);
+  const int n = plane / C, c = plane - n * C;
+  const int bh = (t / TW) * 16 + 4 * r4, bw = (t % TW) * 64 + 4 * c4;
+  float* dp = dx + (long)n * dx_bs + (long)c * H * W + (long)bh * W + bw;
+  const int base = bh * W + bw;
+  float o[4][4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    float4 q = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (accumulate) q = *reinterpret_cast<const float4*>(dp + (long)r * W);
+    o[r][0] = q.x; o[r][1] = q.y; o[r][2] = q.z; o[r][3] = q.w;
+  }
+  // one window's (grad, argmax) into the block: rel = argmax - base, hit where rel == r * W + j
+  auto add1 = [&](float gv, int id, int r0, int r1, int j0, int j1) __attribute__((always_inline)) {
+    const int rel = id - base;
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (r >= r0 && r < r1 && j >= j0 && j < j1) o[r][j] += (rel == r * W + j) ? gv : 0.f;
+  };
+  if (p.dy[0]) {
+    const int W2 = W >> 1;
+    const long po = (long)(bh >> 1) * W2 + (bw >> 1);
+    const float* gy = p.dy[0] + (long)n * p.dy_bs[0] + (long)c * (H >> 1) * W2 + po;
+    const int* gi = p.idx[0] + (long)plane * (H >> 1) * W2 + po;
+#pragma unroll
+    for (int a = 0; a < 2; ++a) {
+      const float2 gv = *reinterpret_cast<const float2*>(gy + a * W2);
+      const int2 id = *reinterpret_cast<const int2*>(gi + a * W2);
+      add1(gv.x, id.x, 2 * a, 2 * a + 2, 0, 2);
+      add1(gv.y, id.y, 2 * a, 2 * a + 2, 2, 4);
+    }
+  }
+#pragma unroll
+  for (int l = 1; l < L; ++l) {
+    if (!p.dy[l]) continue;
+    const int k = 2 << l, Wk = W / k;
+    const long po = (long)(bh / k) * Wk + bw / k;
+    const float gv = p.dy[l][(long)n * p.dy_bs[l] + (long)c * (H / k) * Wk + po];
+    const int id = p.idx[l][(long)plane * (H / k) * Wk + po];
+    add1(gv, id, 0, 4, 0, 4);
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) *reinterpret_cast<float4*>(dp + (long)r * W) = make_float4(o[r][0], o[r][1], o[r][2], o[r][3]);
+}
+
 // Generic fallback (any H, W): element-parallel, zero fill beyond the floor windows.
 __global__ void maxpool_fwd_kernel(const float* __restrict__ x, long x_bs, float* __restrict__ y,
                                    long y_bs, int* __restrict__ idx, int N, int C, int H, int W,
@@ -1495,6 +1643,62 @@ int dsgan_maxpool_bwd(const float* dy, long dy_bs, const int* idx, float* dx, lo
   else if (fast && k == 16) hipLaunchKernelGGL(maxpool_bwd_row_kernel<16>, plane_grid((long)H * W / 4, (long)N * C), dim3(256), 0, st, dy, dy_bs, idx, dx, dx_bs, N, C, H, W, accumulate);
   else hipLaunchKernelGGL(maxpool_bwd_kernel, plane_grid((long)H * W, (long)N * C), dim3(256), 0, st, dy, dy_bs,
                           idx, dx, dx_bs, N, C, H, W, k, accumulate);
+  DSG_CHECK_LAUNCH();
+  return 0;
+}
+
+int dsgan_maxpool_pyr_supported(int H, int W, int levels) {
+  return levels >= 1 && levels <= 4 && H >= 16 && W >= 64 && H % 16 == 0 && W % 64 == 0;
+}
+
+int dsgan_maxpool_pyr_fwd(const float* x, long x_bs, int levels, float* y2, int* i2, float* y4, int* i4, float* y8, int* i8,
+                          float* y16, int* i16, int N, int C, int H, int W, hipStream_t st) {
+  DSG_REQUIRE(x && y2 && i2 && N > 0 && C > 0 && dsgan_maxpool_pyr_supported(H, W, levels),
+              "dsgan_maxpool_pyr_fwd: bad args (levels %d, %dx%d: H %% 16, W %% 64)", levels, H, W);
+  DSG_REQUIRE((levels < 2 || (y4 && i4)) && (levels < 3 || (y8 && i8)) && (levels < 4 || (y16 && i16)),
+              "dsgan_maxpool_pyr_fwd: an output of a requested level is NULL");
+  DSG_REQUIRE((x_bs & 3) == 0 && ((uintptr_t)x & 15) == 0 && (((uintptr_t)y2 | (uintptr_t)i2) & 7) == 0,
+              "dsgan_maxpool_pyr_fwd: x rows must be 16-byte aligned, k=2 outputs 8-byte aligned");
+  PyrPtrs p{};
+  p.y[0] = y2; p.y[1] = y4; p.y[2] = y8; p.y[3] = y16;
+  p.idx[0] = i2; p.idx[1] = i4; p.idx[2] = i8; p.idx[3] = i16;
+  const long nw = (long)N * C * (H / 16) * (W / 64);
+  const dim3 grid((unsigned)((nw + 3) / 4));
+  switch (levels) {
+    case 1: hipLaunchKernelGGL(maxpool_pyr_fwd_kernel<1>, grid, dim3(256), 0, st, x, x_bs, p, C, H, W, nw); break;
+    case 2: hipLaunchKernelGGL(maxpool_pyr_fwd_kernel<2>, grid, dim3(256), 0, st, x, x_bs, p, C, H, W, nw); break;
+    case 3: hipLaunchKernelGGL(maxpool_pyr_fwd_kernel<3>, grid, dim3(256), 0, st, x, x_bs, p, C, H, W, nw); break;
+    default: hipLaunchKernelGGL(maxpool_pyr_fwd_kernel<4>, grid, dim3(256), 0, st, x, x_bs, p, C, H, W, nw); break;
+  }
+  DSG_CHECK_LAUNCH();
+  return 0;
+}
+
+int dsgan_maxpool_pyr_bwd(const float* dy2, long dy2_bs, const int* i2, const float* dy4, long dy4_bs, const int* i4,
+                          const float* dy8, long dy8_bs, const int* i8, const float* dy16, long dy16_bs, const int* i16,
+                          float* dx, long dx_bs, int levels, int N, int C, int H, int W, int accumulate, hipStream_t st) {
+  DSG_REQUIRE(dx && N > 0 && C > 0 && dsgan_maxpool_pyr_supported(H, W, levels), "dsgan_maxpool_pyr_bwd: bad args");
+  DSG_REQUIRE((!dy2 || i2) && (!dy4 || i4) && (!dy8 || i8) && (!dy16 || i16),
+              "dsgan_maxpool_pyr_bwd: a level with a gradient needs its indices");
+  DSG_REQUIRE((dx_bs & 3) == 0 && ((uintptr_t)dx & 15) == 0 && (!dy2 || ((dy2_bs & 1) == 0 && (((uintptr_t)dy2 | (uintptr_t)i2) & 7) == 0)),
+              "dsgan_maxpool_pyr_bwd: dx rows must be 16-byte aligned, k=2 grads 8-byte aligned");
+  PyrPtrs p{};
+  const float* dys[4] = {dy2, dy4, dy8, dy16};
+  const long bss[4] = {dy2_bs, dy4_bs, dy8_bs, dy16_bs};
+  const int* ids[4] = {i2, i4, i8, i16};
+  for (int l = 0; l < 4; ++l) {
+    p.dy[l] = l < levels ? dys[l] : nullptr;
+    p.dy_bs[l] = bss[l];
+    p.idx[l] = const_cast<int*>(ids[l]);
+  }
+  const long nw = (long)N * C * (H / 16) * (W / 64);
+  const dim3 grid((unsigned)((nw + 3) / 4));
+  switch (levels) {
+    case 1: hipLaunchKernelGGL(maxpool_pyr_bwd_kernel<1>, grid, dim3(256), 0, st, p, dx, dx_bs, C, H, W, nw, accumulate); break;
+    case 2: hipLaunchKernelGGL(maxpool_pyr_bwd_kernel<2>, grid, dim3(256), 0, st, p, dx, dx_bs, C, H, W, nw, accumulate); break;
+    case 3: hipLaunchKernelGGL(maxpool_pyr_bwd_kernel<3>, grid, dim3(256), 0, st, p, dx, dx_bs, C, H, W, nw, accumulate); break;
+    default: hipLaunchKernelGGL(maxpool_pyr_bwd_kernel<4>, grid, dim3(256), 0, st, p, dx, dx_bs, C, H, W, nw, accumulate); break;
+  }
   DSG_CHECK_LAUNCH();
   return 0;
 }

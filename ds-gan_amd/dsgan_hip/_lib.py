@@ -114,6 +114,9 @@ SIGNATURES = {
     "dsgan_instnorm_bwd_ws": [P, L, P, L, P, P, L, P, P, P, L, P, L, P, I, I, I, I, F, F, P, L, S],
     "dsgan_maxpool_fwd": [P, L, P, L, P, I, I, I, I, I, S],
     "dsgan_maxpool_bwd": [P, L, P, P, L, I, I, I, I, I, I, S],
+    "dsgan_maxpool_pyr_supported": [I, I, I],
+    "dsgan_maxpool_pyr_fwd": [P, L, I] + [P] * 8 + [I, I, I, I, S],
+    "dsgan_maxpool_pyr_bwd": [P, L, P] * 4 + [P, L] + [I] * 6 + [S],
     "dsgan_plane_stats": [P, L, P, P, P, I, I, I, S],
     "dsgan_plane_stats_bwd": [P, P, P, P, L, I, I, I, S],
     "dsgan_ca_fwd": [P, P, P, P, P, P, P, I, I, I, S],

@@ -1551,6 +1551,65 @@ class MaxPoolFn(torch.autograd.Function):
         return (None if acc else _give(ctx.box, dx)), None
 
 
+class MaxPoolPyrFn(torch.autograd.Function):
+    """MaxPool2d(2), (4), ... (2^levels) of one tensor (the skip pyramids) in one launch each way
+    (dsgan_maxpool_pyr_*): one read of x instead of one per k, and one read-modify-write of its
+    gradient instead of one per k."""
+
+    @staticmethod
+    def forward(ctx, x, levels):
+        x4, xbs = nchw(x)
+        N, C, H, W = x4.shape
+        ys, ids = [], []
+        for lv in range(levels):
+            k = 2 << lv
+            ys.append(_empty(N, C, H // k, W // k, x4))
+            ids.append(torch.empty((N, C, H // k, W // k), device=x4.device, dtype=torch.int32))
+        args = []
+        for lv in range(4):
+            args += [ptr(ys[lv]), ptr(ids[lv])] if lv < levels else [None, None]
+        call("dsgan_maxpool_pyr_fwd", ptr(x4), xbs, levels, *args, N, C, H, W, stream())
+        ctx.levels, ctx.shape = levels, (N, C, H, W)
+        ctx.save_for_backward(*ids)
+        ctx.mark_non_differentiable(*ids)
+        ctx.set_materialize_grads(False)
+        ctx.box = _box(x)
+        return tuple(ys) + tuple(ids)
+
+    @staticmethod
+    def backward(ctx, *grads):
+        L = ctx.levels
+        dys = grads[:L]
+        if all(g is None for g in dys):
+            return None, None
+        ids = ctx.saved_tensors
+        N, C, H, W = ctx.shape
+        out, acc = _acc_target(ctx.box)
+        dx = out if acc else torch.empty((N, C, H, W), device=ids[0].device, dtype=torch.float32)
+        dx4, dxbs = nchw(dx)
+        if dx4.data_ptr() != dx.data_ptr():
+            raise RuntimeError("maxpool pyramid backward: gradient buffer must be per-sample dense")
+        args, keep = [], []
+        for lv in range(4):
+            if lv < L and dys[lv] is not None:
+                d4, dbs = nchw(dys[lv])
+                keep.append(d4)
+                args += [ptr(d4), dbs, ptr(ids[lv])]
+            else:
+                args += [None, 0, None]
+        call("dsgan_maxpool_pyr_bwd", *args, ptr(dx4), dxbs, L, N, C, H, W, int(acc), stream())
+        return (None if acc else _give(ctx.box, dx)), None
+
+
+def max_pool_pyramid(x, levels):
+    """[MaxPool2d(2)(x), MaxPool2d(4)(x), ..., MaxPool2d(2^levels)(x)]: one launch when the shape
+    allows (H % 16 == 0, W % 64 == 0), else one max_pool2d per level."""
+    N, C, H, W = x.shape
+    if _lib.load().dsgan_maxpool_pyr_supported(H, W, levels):
+        return list(MaxPoolPyrFn.apply(x, levels)[:levels])
+    return [max_pool2d(x, 2 << lv) for lv in range(levels)]
+
+
 def max_pool2d(x, k, return_indices=False):
     y, idx = MaxPoolFn.apply(x, k)
     return (y, idx) if return_indices else y

@@ -143,8 +143,8 @@ class downSkip(nn.Module):
         super().__init__()
         self.to2, self.to4, self.to8, self.to16 = _skip(64, 128, 2), _skip(64, 256, 4), _skip(64, 512, 8), _skip(64, 1024, 16)
 
-    def forward(self, x, pool2=None):
-        return [_skip_fwd(self.to2, x, pool2)] + [_skip_fwd(s, x) for s in (self.to4, self.to8, self.to16)]
+    def forward(self, x, pools=(None,) * 4):
+        return [_skip_fwd(s, x, p) for s, p in zip((self.to2, self.to4, self.to8, self.to16), pools)]
 
 
 class downSkip128(nn.Module):
@@ -152,8 +152,8 @@ class downSkip128(nn.Module):
         super().__init__()
         self.to4, self.to8, self.to16 = _skip(128, 256, 2), _skip(128, 512, 4), _skip(128, 1024, 8)
 
-    def forward(self, x, pool2=None):
-        return [_skip_fwd(self.to4, x, pool2)] + [_skip_fwd(s, x) for s in (self.to8, self.to16)]
+    def forward(self, x, pools=(None,) * 3):
+        return [_skip_fwd(s, x, p) for s, p in zip((self.to4, self.to8, self.to16), pools)]
 
 
 class downSkip256(nn.Module):
@@ -161,8 +161,8 @@ class downSkip256(nn.Module):
         super().__init__()
         self.to8, self.to16 = _skip(256, 512, 2), _skip(256, 1024, 4)
 
-    def forward(self, x, pool2=None):
-        return [_skip_fwd(self.to8, x, pool2), _skip_fwd(self.to16, x)]
+    def forward(self, x, pools=(None,) * 2):
+        return [_skip_fwd(s, x, p) for s, p in zip((self.to8, self.to16), pools)]
 
 
 class downSkip512(nn.Module):
@@ -170,8 +170,8 @@ class downSkip512(nn.Module):
         super().__init__()
         self.to16 = _skip(512, 1024, 2)
 
-    def forward(self, x, pool2=None):
-        return [_skip_fwd(self.to16, x, pool2)]
+    def forward(self, x, pools=(None,)):
+        return [_skip_fwd(self.to16, x, pools[0])]
 
 
 class MixConvNeXtML(nn.Module):
@@ -207,28 +207,34 @@ class MixConvNeXtML(nn.Module):
                 self.down512, self.down256, self.down128, self.down64, self.c5, self.c4, self.c3, self.c2, self.c1]
 
     def forward(self, x):
-        # R1..R4 feed the next stage's MaxPool(2), their skip pyramid and a decoder concat; the
-        # MaxPool(2) of R_i is computed once for the encoder and the pyramid's k=2 branch
-        # (both are MaxPool2d(2) of the same tensor).  Shared tensors accumulate their grads in
-        # one buffer (HF.share) instead of through autograd adds.
+        # R1..R4 feed the next stage's MaxPool(2), their skip pyramid and a decoder concat.  Every
+        # MaxPool of R_i -- the encoder's k=2 (also the pyramid's k=2 branch) and the skips' k=4/8/16 --
+        # comes from ONE pass over R_i (HF.max_pool_pyramid), whose backward adds all their grads
+        # into R_i's in one pass.  Shared tensors accumulate their grads in one buffer (HF.share)
+        # instead of through autograd adds.
         # The decoder concatenations cat(upSample head, R_i) are allocated up front: c_i writes R_i
         # straight into its tail and u_i only fills the head (no copy of the skip, HF.CatSlot).
-        sh, mp = HF.share, lambda t: HF.share(HF.max_pool2d(t, 2))
+        sh = HF.share
+
+        def pyr(t, levels):   # [share(MaxPool(2)(t)), MaxPool(4)(t), ...]
+            ps = HF.max_pool_pyramid(t, levels)
+            return [sh(ps[0])] + ps[1:]
+
         N, _, H, W = x.shape
         cs = [HF.CatSlot(N, c, c, H >> i, W >> i, x) for i, c in enumerate((64, 128, 256, 512))]
         R1 = sh(self.c1(x, cs[0]))
-        P1 = mp(R1)
-        R2 = sh(self.c2(P1, cs[1]))
-        P2 = mp(R2)
-        R3 = sh(self.c3(P2, cs[2]))
-        P3 = mp(R3)
-        R4 = sh(self.c4(P3, cs[3]))
-        P4 = mp(R4)
-        R5 = self.c5(P4)
-        s64 = self.down64(R1, P1)
-        s128 = self.down128(R2, P2)
-        s256 = self.down256(R3, P3)
-        s512 = self.down512(R4, P4)
+        Q1 = pyr(R1, 4)
+        R2 = sh(self.c2(Q1[0], cs[1]))
+        Q2 = pyr(R2, 3)
+        R3 = sh(self.c3(Q2[0], cs[2]))
+        Q3 = pyr(R3, 2)
+        R4 = sh(self.c4(Q3[0], cs[3]))
+        Q4 = [sh(HF.max_pool2d(R4, 2))]
+        R5 = self.c5(Q4[0])
+        s64 = self.down64(R1, Q1)
+        s128 = self.down128(R2, Q2)
+        s256 = self.down256(R3, Q3)
+        s512 = self.down512(R4, Q4)
         O1 = self.uc1(self.u1(HF.add_n(R5, s64[3], s128[2], s256[1], s512[0]), R4, cs[3]))
         O2 = self.uc2(self.u2(HF.add_n(O1, s64[2], s128[1], s256[0]), R3, cs[2]))
         O3 = self.uc3(self.u3(HF.add_n(O2, s64[1], s128[0]), R2, cs[1]))

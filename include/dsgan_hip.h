@@ -401,6 +401,18 @@ int dsgan_maxpool_fwd(const float* x, long x_bs, float* y, long y_bs, int* idx, 
                       int H, int W, int k, hipStream_t stream);
 int dsgan_maxpool_bwd(const float* dy, long dy_bs, const int* idx, float* dx, long dx_bs, int N,
                       int C, int H, int W, int k, int accumulate, hipStream_t stream);
+/* The generator's skip pyramids (MixConvNeXtML.py:328-426: R1 -> k 2/4/8/16, R2 -> 2/4/8, R3 -> 2/4)
+ * from one read of the source: levels 1-4 = MaxPool2d(2), (4), (8), (16), each output dense
+ * [N][C][H/k][W/k] with its int32 plane-flat argmax (the same bits as dsgan_maxpool_fwd per k).
+ * The backward adds every level's output grad (NULL = none) into dx in one pass (accumulate: dx +=).
+ * Needs H % 16 == 0, W % 64 == 0 (dsgan_maxpool_pyr_supported). */
+int dsgan_maxpool_pyr_supported(int H, int W, int levels);
+int dsgan_maxpool_pyr_fwd(const float* x, long x_bs, int levels, float* y2, int* i2, float* y4, int* i4, float* y8,
+                          int* i8, float* y16, int* i16, int N, int C, int H, int W, hipStream_t stream);
+int dsgan_maxpool_pyr_bwd(const float* dy2, long dy2_bs, const int* i2, const float* dy4, long dy4_bs, const int* i4,
+                          const float* dy8, long dy8_bs, const int* i8, const float* dy16, long dy16_bs,
+                          const int* i16, float* dx, long dx_bs, int levels, int N, int C, int H, int W,
+                          int accumulate, hipStream_t stream);
 
 /* ---- channel attention CA (MixConvNeXtML.py:5-22) --------------------------------------- */
 int dsgan_plane_stats(const float* x, long x_bs, float* avg, float* mx, int* amax, int N, int C,

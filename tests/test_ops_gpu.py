@@ -637,6 +637,55 @@ def test_maxpool_indices_bit_exact(k, W):
     assert torch.equal(dxa.cpu(), base + xr.grad)
 
 
+@pytest.mark.parametrize("levels,H,W", [(4, 32, 64), (4, 16, 128), (3, 48, 64), (2, 16, 64), (1, 16, 64)])
+def test_maxpool_pyramid_bit_exact(levels, H, W):
+    """The one-pass skip pyramid (dsgan_maxpool_pyr_*): MaxPool2d(2), (4), (8), (16) of one tensor
+    against torch's max_pool2d per k -- values and int32 indices bit-exact, with ties spanning the
+    sub-windows the k = 8 / 16 levels merge (a tie whose first row-major occurrence is in the
+    second sub-window), NaNs (the last NaN of a window wins), an all -inf window and many exact
+    ties from a coarse value grid; the backward (every level's grad added in one pass, plain and
+    accumulating) against torch's autograd through the separate pools."""
+    from dsgan_hip import functional as HF
+    from dsgan_hip._lib import call, ptr, stream
+    g = torch.Generator().manual_seed(levels * 100 + H + W)
+    x = torch.randint(-3, 4, (2, 3, H, W), generator=g).float() * 0.5   # coarse grid: ties everywhere
+    x[0, 1] = torch.randn(H, W, generator=g)
+    x[0, 0, 0, 3] = 9.0; x[0, 0, 1, 0] = 9.0       # same max in two 2x2 sub-windows: row-major picks (0, 3)
+    x[0, 0, 0, 12] = 9.0; x[0, 0, 5, 1] = 9.0      # across the 8x8 sub-windows of a 16x16 window
+    x[1, 2, 5, 7] = float("nan"); x[1, 2, 2, 1] = float("nan")   # two NaNs in one window: the later wins
+    x[1, 2, 3, 9] = float("nan")
+    x[1, 0, :16, :16] = float("-inf")              # all -inf: index = the window's first element
+    ks = [2 << lv for lv in range(levels)]
+    xr = x.clone().requires_grad_()
+    refs = [F.max_pool2d(xr, k, return_indices=True) for k in ks]
+    gys = [torch.randn(r[0].shape, generator=g) for r in refs]
+    sum((r[0] * gy).sum() for r, gy in zip(refs, gys)).backward()
+    xd = _leaf(x)
+    ys = HF.max_pool_pyramid(xd, levels)
+    outs = HF.MaxPoolPyrFn.apply(x.to(DEV), levels)
+    for lv, (y_ref, i_ref) in enumerate(refs):
+        assert torch.allclose(ys[lv].detach().cpu(), y_ref.detach(), rtol=0, atol=0, equal_nan=True), ks[lv]
+        assert torch.equal(outs[levels + lv].cpu().long(), i_ref), ks[lv]
+    sum((y * gy.to(DEV)).sum() for y, gy in zip(ys, gys)).backward()
+    assert torch.allclose(xd.grad.cpu().double(), xr.grad.double(), rtol=1e-6, atol=1e-6)
+    # accumulate form through the C ABI, with the k = 4 grad absent
+    N, C = x.shape[:2]
+    base = torch.randn(x.shape, generator=g)
+    dxa = base.to(DEV)
+    args = []
+    for lv in range(4):
+        if lv < levels and lv != 1:
+            gy = gys[lv].to(DEV).contiguous()
+            args += [gy, gy.shape[1] * gy.shape[2] * gy.shape[3], outs[levels + lv]]
+        else:
+            args += [None, 0, None]
+    call("dsgan_maxpool_pyr_bwd", *[ptr(a) if torch.is_tensor(a) or a is None else a for a in args], ptr(dxa),
+         C * H * W, levels, N, C, H, W, 1, stream())
+    xr2 = x.clone().requires_grad_()
+    sum((F.max_pool2d(xr2, ks[lv]) * gys[lv]).sum() for lv in range(levels) if lv != 1).backward()
+    assert torch.allclose(dxa.cpu().double(), (base + xr2.grad).double(), rtol=1e-6, atol=1e-6)
+
+
 @pytest.mark.parametrize("C,H", [(32, 16), (128, 8), (256, 4)])
 def test_mid_tail(C, H):
     """GELU(IN(v * CA(v)) + x) (MixConvNeXtML.py:112-116, CA :18-22) fwd + all grads."""
