@@ -13,6 +13,7 @@
 // Per tap the bf16 weight slice [BM][32] is register-prefetched one tap ahead into a double
 // buffer.  Weights are a bf16 tap-major copy (dsgan_conv_wtrans_bf16).
 #include "common.h"
+#include "lds_pitch.h"
 #include <type_traits>
 #include <stdlib.h>
 
@@ -89,7 +90,7 @@ __global__ __launch_bounds__(256, 2) void pconv_kernel(PcArgs g) {
   auto aload = [&](int tap, int k0) {
 #pragma unroll
     for (int i = 0; i < A_ITEMS; ++i) {
-      const int it = tid + i * 256, row = it >> 2, c8 = it & 3;
+      const int it = tid + i * 256, row = p80_row16(it), c8 = p80_slot16(it);
       const int m = m0 + row;
       ra[i] = m < g.M ? *reinterpret_cast<const cu32x4*>(g.Wb + ((long)tap * g.M + m) * g.K + k0 + c8 * 8)
                       : cu32x4{0u, 0u, 0u, 0u};
@@ -100,7 +101,7 @@ __global__ __launch_bounds__(256, 2) void pconv_kernel(PcArgs g) {
 #pragma unroll
     for (int i = 0; i < A_ITEMS; ++i) {
       const int it = tid + i * 256;
-      *reinterpret_cast<cu32x4*>(As + (it >> 2) * PC_STR + (it & 3) * 8) = ra[i];
+      *reinterpret_cast<cu32x4*>(As + p80_row16(it) * PC_STR + p80_slot16(it) * 8) = ra[i];
     }
   };
   // patch of channel block k0: item = (pixel, 8-channel group); lanes run along the pixels of

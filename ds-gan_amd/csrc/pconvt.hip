@@ -15,6 +15,7 @@
 //   * the epilogue writes the two column parities of an output row as one float2 per lane
 //     (adjacent lanes = adjacent grid columns: fully coalesced).
 #include "common.h"
+#include "lds_pitch.h"
 #include <type_traits>
 #include <stdlib.h>
 
@@ -73,6 +74,7 @@ __global__ __launch_bounds__(256, BM == 32 ? 4 : 2) void pconvt_kernel(PtArgs g)
   constexpr int WMW = BM / 32, WNW = 4 / WMW, NT = (BN / 32) / WNW;
   constexpr int A_SZ = BM * PT_STR;
   constexpr int A_ITEMS = T * BM * 4;             // 16-byte items of all taps' [BM][32] slices
+  static_assert(BM % 8 == 0, "lds_pitch.h maps pair rows r, r + 4 within 8-row blocks");
   constexpr int A_IT = (A_ITEMS + 255) / 256;
   constexpr int P_ITEMS = PPIX * 4;                // (pixel, 8-channel group)
   constexpr int P_IT = (P_ITEMS + 255) / 256;
@@ -119,7 +121,7 @@ __global__ __launch_bounds__(256, BM == 32 ? 4 : 2) void pconvt_kernel(PtArgs g)
 #pragma unroll
     for (int i = 0; i < A_IT; ++i) {
       const int it = tid + i * 256;
-      const int c8 = it & 3, row = (it >> 2) % BM, tap = (it >> 2) / BM;
+      const int r = p80_row16(it), c8 = p80_slot16(it), row = r % BM, tap = r / BM;
       const int m = t.m0 + row;
       ra[i] = (it < A_ITEMS && m < g.M)
                   ? *reinterpret_cast<const tu32x4*>(g.Wb + ((long)tap * g.M + m) * g.K + k0 + c8 * 8)
@@ -143,7 +145,7 @@ __global__ __launch_bounds__(256, BM == 32 ? 4 : 2) void pconvt_kernel(PtArgs g)
     for (int i = 0; i < A_IT; ++i) {
       const int it = tid + i * 256;
       if (it < A_ITEMS) {
-        const int c8 = it & 3, row = (it >> 2) % BM, tap = (it >> 2) / BM;
+        const int r = p80_row16(it), c8 = p80_slot16(it), row = r % BM, tap = r / BM;
         *reinterpret_cast<tu32x4*>(smem + tap * A_SZ + row * PT_STR + c8 * 8) = ra[i];
       }
     }

@@ -18,6 +18,7 @@
 //   flipped/transposed kernel, stride 2 as four parity classes each a stride-1 conv whose
 //   outputs land on a stride-2 lattice of the destination.
 #include "common.h"
+#include "lds_pitch.h"
 #include <type_traits>
 
 namespace dsg {
@@ -109,11 +110,11 @@ __global__ __launch_bounds__(256, 2) void tconv_kernel(TcArgs g) {
     for (int i = 0; i < A_ITEMS; ++i) {
       const int it = tid + i * 256;
       if constexpr (ABF) {   // 8 bf16 per item, 4 items per 32-deep row
-        const int m = m0 + (it >> 2), kk = k0 + (it & 3) * 8;
+        const int m = m0 + p80_row16(it), kk = k0 + p80_slot16(it) * 8;
         const unsigned off = m < g.M ? ((unsigned)m * g.K + kk) * 2u : 0xFFFFFFF0u;
         rha[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rw, (int)off, wtap, 0));
       } else {
-        const int m = m0 + (it >> 3), kk = k0 + (it & 7) * 4;
+        const int m = m0 + p80_row8(it), kk = k0 + p80_piece8(it) * 4;
         const unsigned off = m < g.M ? ((unsigned)m * g.K + kk) * 4u : 0xFFFFFFF0u;
         ra[i] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rw, (int)off, wtap, 0));
       }
@@ -135,13 +136,13 @@ __global__ __launch_bounds__(256, 2) void tconv_kernel(TcArgs g) {
     for (int i = 0; i < A_ITEMS; ++i) {
       const int it = tid + i * 256;
       if constexpr (ABF) {
-        *reinterpret_cast<u32x4*>(As + (it >> 2) * T_STR + (it & 3) * 8) = rha[i];
+        *reinterpret_cast<u32x4*>(As + p80_row16(it) * T_STR + p80_slot16(it) * 8) = rha[i];
         continue;
       }
       typedef __attribute__((ext_vector_type(4))) T16 b4;
       b4 v;
       v[0] = (T16)ra[i].x; v[1] = (T16)ra[i].y; v[2] = (T16)ra[i].z; v[3] = (T16)ra[i].w;
-      *reinterpret_cast<b4*>(As + (it >> 3) * T_STR + (it & 7) * 4) = v;
+      *reinterpret_cast<b4*>(As + p80_row8(it) * T_STR + p80_piece8(it) * 4) = v;
     }
     tbf16x8 lo, hi;
     if constexpr (XH) {
