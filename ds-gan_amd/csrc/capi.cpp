@@ -49,4 +49,8 @@ int dsgan_set_half_type(int t) {
   return 0;
 }
 int dsgan_get_half_type(void) { return g_half.load(std::memory_order_relaxed); }
+// Reads and clears the HIP runtime's last launch error (0 = none).  A stream capture that was
+// invalidated leaves its error pending; every entry point checks hipGetLastError() after its
+// launches, so the first eager launch after a failed capture would report it as its own.
+int dsgan_clear_launch_error(void) { return (int)hipGetLastError(); }
 }

@@ -54,8 +54,6 @@ static int dma_ok(const PwArgs& g, int bm, int abf, int bbf, int mode) {
   // (the weight-grads stay register-staged unless asked for: 3-5 % slower on the ring)
   const bool ok = mode == PW_WGRAD ? g_tune[9] >= 3 && g.N % 256 == 0 && g.P % 32 == 0 && (g.k_split % 32) == 0
                                    : g.K % 32 == 0 && g.P % 256 == 0 && g.k_split == 0;
-  // (knob 9: 1 = 256 x 256 ring, 2 = 256 x 128 two per CU, 4 = 128 x 256 two per CU: FWD / DGRAD only)
-  if (ok && g_tune[9] == 4 && mode != PW_WGRAD) return 3;
   return ok ? (g_tune[9] == 2 ? 2 : 1) : 0;
 }
 

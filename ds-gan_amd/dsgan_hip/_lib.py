@@ -26,6 +26,7 @@ SIGNATURES = {
     "dsgan_amp_check": [P, L, P, P, F, F, I, S],
     "dsgan_adam_amp": [P, P, P, P, L, D, D, D, D, P, S],
     "dsgan_get_half_type": [],
+    "dsgan_clear_launch_error": [],
     "dsgan_last_error_string": [],
     # scratch contract: plan-only mode and the scratch the last planned launch needs (CPU planner tests)
     "dsgan_set_plan_only": [I],

@@ -30,6 +30,7 @@ import random
 
 import torch
 
+from dsgan_hip import _lib
 from dsgan_hip import functional as HF
 from dsgan_hip import dist as hdist
 from dsgan_hip.flat import FlatParams, FlatAdam
@@ -302,6 +303,8 @@ class Pix2PixModel(BaseModel):
                 ent = self._capture(lrs)
             except Exception as e:   # noqa: BLE001 -- a capture failure must not end the run: eager from here on
                 err = e
+            if err is not None:   # the invalidated capture's error is still pending in the HIP runtime
+                _lib.load().dsgan_clear_launch_error()
             if not hdist.all_ranks_true(err is None, self.device):   # every rank replays, or none does
                 print("[Pix2PixModel] HIP graph capture failed (%r): running the eager step" % (err,))
                 self._graphs, self.cuda_graph, self._feats_joined = {}, False, False
@@ -321,7 +324,10 @@ class Pix2PixModel(BaseModel):
         pool = torch.cuda.graph_pool_handle()
         gA, gB = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
         cond = self.use_gan == 1 and self.use_condition == 1
-        with torch.cuda.graph(gA, pool=pool):
+        # thread_local capture mode: the RCCL process group's watchdog thread polls the events of
+        # earlier (eager) collectives; in the default global mode such a query from another thread
+        # invalidates the capture.  The capturing thread itself still may not make unsafe calls.
+        with torch.cuda.graph(gA, pool=pool, capture_error_mode="thread_local"):
             self._launch_real_features()
             self.forward()
             if cond:
@@ -330,7 +336,7 @@ class Pix2PixModel(BaseModel):
             torch.cuda.current_stream(self.device).wait_stream(self._vgg_stream)
             self._feats_joined = True
         try:
-            with torch.cuda.graph(gB, pool=pool):
+            with torch.cuda.graph(gB, pool=pool, capture_error_mode="thread_local"):
                 self._d_and_g_steps(self._fake_AB_buf if cond else None)
         finally:
             self._feats_joined = False

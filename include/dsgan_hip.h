@@ -50,6 +50,10 @@ long dsgan_last_ws_need(void);
 /* the 16-bit operand type (see Conventions): 0 bf16, 1 fp16; -1 for anything else */
 int dsgan_set_half_type(int t);
 int dsgan_get_half_type(void);
+/* Reads and clears the HIP runtime's pending launch error (0 = none): the host calls it after a
+ * failed HIP-graph capture, whose invalidation error would otherwise be reported by the next
+ * eager launch's check. */
+int dsgan_clear_launch_error(void);
 
 /* ---- implicit-GEMM convolution (igemm.hip) ------------------------------------------------
  * Replaces nn.Conv2d / nn.Linear / nn.ConvTranspose2d forward+backward:
