@@ -26,6 +26,8 @@ from dsgan_hip import _lib  # noqa: E402
 from dsgan_hip._lib import call, ptr, stream  # noqa: E402
 
 N = 16
+# the three kernel forms compared (dsgan_vconv_tune key 0); VCONV_MODES="3,4,5" compares the ring variants
+MODES = tuple(int(m) for m in os.environ.get("VCONV_MODES", "1,0,3").split(","))
 # (name, K in, M out, H, dgrad): the forward convs of vgg.py:15-24 and the data-grads of the backward walk
 LAYERS = [("c1_2", 64, 64, 256, 0), ("c2_1", 64, 128, 128, 0), ("c2_2", 128, 128, 128, 0), ("c3_1", 128, 256, 64, 0),
           ("c3_2", 256, 256, 64, 0), ("c4_1", 256, 512, 32, 0), ("c4_2", 512, 512, 32, 0),
@@ -68,7 +70,7 @@ def main():
         mask = torch.randn(N * M * H * H, device="cuda", generator=g).to(torch.bfloat16) if dgrad else None
         ys = []
         ts = []
-        for mode in (1, 0, 3):
+        for mode in MODES:
             lib.dsgan_vconv_tune(0, mode)
             Y = torch.empty(N * M * H * H, device="cuda", dtype=torch.bfloat16)
             fn = lambda Y=Y: call("dsgan_vconv3x3", ptr(X), ptr(Wt), ptr(bias), ptr(mask), ptr(Y), 0, 0 if dgrad else 1,
