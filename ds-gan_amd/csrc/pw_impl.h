@@ -1013,6 +1013,9 @@ void pw_wgrad_launch(const PwArgs& g, int bm, int abf, int bbf, int splits, hipS
     default: pw_launch<T16, PW_WGRAD, 128, 1, 1>(g, splits, st); break;
   }
 }
+// pwpp.hip: the persistent gelu-pair forward (16-bit W / X / outputs, M % 256, P % 128, K % 32)
+void pwpp_gelu_launch(const PwArgs& g, hipStream_t st);
+
 #define PW_EXTERN_LAUNCHERS(T16)                                                                            \
   extern template void pw_fd_launch_m<T16, PW_FWD>(const PwArgs&, int, int, int, int, hipStream_t);         \
   extern template void pw_fd_launch_m<T16, PW_DGRAD>(const PwArgs&, int, int, int, int, hipStream_t);       \

@@ -426,6 +426,15 @@ extern "C" int dsgan_pw_fwd_io_ws(const void* W, int w_bf16, const void* X, long
   const int bm = fd_tile_k(g, w_bf16 || x_bf16);
   const int splits = fd_plan(g, bm, ws);
   DSG_WS(fd_need(g, splits), ws, ws_elems, "dsgan_pw_fwd_io (dsgan_pw_fd_workspace)");
+  // the gelu-pair forward of the wide unfused blocks on the persistent form (pwpp.hip: the GELU
+  // pair of one tile beside the next tile's MFMAs), planner knob 11.  bf16 only: with fp16 operands
+  // 6e-5 of its outputs differ from the one-tile kernel's by one fp16 ulp (tools/probe/pp_diag.py)
+  if (g_tune[11] && half_type() != HALF_F16 && splits == 1 && w_bf16 && x_bf16 && y_bf16 && g.ypre && g.gbf && act == ACT_GELU &&
+      !accumulate && M % 256 == 0 && P % 128 == 0 && K % 32 == 0 && al16(g.ypre) && (ypre_bs & 7) == 0) {
+    pwpp_gelu_launch(g, st);
+    DSG_CHECK_LAUNCH();
+    return 0;
+  }
   fd_launch(PW_FWD, g, bm, w_bf16, x_bf16, splits, st);
   DSG_CHECK_LAUNCH();
   return 0;
