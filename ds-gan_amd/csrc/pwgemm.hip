@@ -44,7 +44,8 @@ static void pw_fd_launch(int mode, const PwArgs& g, int bm, int abf, int bbf, in
 //   weight-grads (3-5 % slower there); 2 = 256 x 128 tiles, 3 stages, two workgroups per CU (slower:
 //   392 us for the 512-channel gelu-pair forward); 0 = register-staged everywhere.
 //   [10] measurement only: bit 0 = FWD / DGRAD epilogues drop their output stores (prices the writes),
-//   bit 1 = the gelu-pair epilogue skips its GELU arithmetic (prices the VALU).
+//   bit 1 = the gelu-pair epilogue skips its GELU arithmetic (prices the VALU); on the LDS-DMA ring
+//   bit 2 = no DMA after the prologue stages (prices the feed), bit 3 = no fragment reads / MFMAs.
 static int g_tune[12] = {1, 512, 256, 4, 0, 0, 0, 0, 1, 1, 0, 0};
 
 // the LDS-DMA ring form's conditions (full 256 x 256 tiles, 32-deep K steps, 16-byte pieces)

@@ -93,6 +93,11 @@ SIGNATURES = {
     "dsgan_conv_wgrad_small": [P, L, P, L, P] + [I] * 11 + [P, L, S],
     # thin3.hip
     "dsgan_thin3_supported": [I, I, I, L, L],
+    "dsgan_pgstem_supported": [I] * 4,
+    "dsgan_pgstem_fwd": [P, L, P, P, P, L] + [I] * 5 + [F, S],
+    "dsgan_pgstem_wgrad_workspace": [I] * 5,
+    "dsgan_pgstem_wgrad": [P, L, P, L, P, L, P, P] + [I] * 5 + [F, P, L, S],
+    "dsgan_pgstem_dgrad": [P, L, P, L, P, P, L] + [I] * 5 + [F, I, S],
     "dsgan_thin3_fwd": [P, L, P, P, P, L] + [I] * 6 + [S],
     "dsgan_thin3_wgrad_workspace": [I] * 5,
     "dsgan_thin3_wgrad": [P, L, P, L, P, P, L] + [I] * 5 + [S],

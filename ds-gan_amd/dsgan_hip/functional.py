@@ -809,9 +809,87 @@ class Conv2dFn(torch.autograd.Function):
         return dx, None, None, None, None, None
 
 
+# NLayerDiscriminator layer 0 (networks.py:543-545) on the stem kernels (pgstem.hip); off routes it
+# through the generic conv + LeakyReLU backward + bias channel sum (tests, A/B)
+PGSTEM = [True]
+
+
+def _pgstem_ok(x, w, stride, pad, act):
+    if not PGSTEM[0] or act != "lrelu" or stride != 2 or pad != 1 or w.dim() != 4 or tuple(w.shape[2:]) != (4, 4):
+        return False
+    if x.dim() != 4 or not x.is_cuda or not w.is_contiguous() or w.shape[1] != x.shape[1]:
+        return False
+    N, Cin, H, W = x.shape
+    return bool(_lib.load().dsgan_pgstem_supported(Cin, w.shape[0], H, W))
+
+
+class PatchStemFn(torch.autograd.Function):
+    """Conv2d(Cin, ndf, 4, 2, 1) + bias + LeakyReLU(0.2, True), the PatchGAN stem: one kernel per
+    direction (dsgan_pgstem_*), exact fp32 in every precision mode.  The backward differentiates
+    the LeakyReLU through its saved output, as the reference's in-place activation does."""
+
+    @staticmethod
+    def forward(ctx, x, w, b):
+        ctx.box = _box(x)
+        x, xbs = nchw(x)
+        if xbs % 4 or x.data_ptr() % 16:
+            x, xbs = x.contiguous(), x[0].numel()
+        N, Cin, H, W = x.shape
+        Cout = w.shape[0]
+        y = _empty(N, Cout, H // 2, W // 2, x)
+        e0 = IGEMM_TIMER.begin()
+        call("dsgan_pgstem_fwd", ptr(x), xbs, ptr(w), ptr(b), ptr(y), y[0].numel(), N, Cin, Cout, H, W, LRELU_SLOPE,
+             stream())
+        IGEMM_TIMER.end(e0, _conv_flops(N, Cin, Cout, 4, 4, H // 2, W // 2), ("fwd", N, Cin, H, W, Cout, 4, 2),
+                        "pgstem_kernel", _nb(x, w, b, y))
+        ctx.save_for_backward(x, w, b, y)
+        ctx.xbs = xbs
+        ctx.w_ref, ctx.b_ref = w, b
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w, b, y = ctx.saved_tensors
+        dy, dybs = nchw(dy)
+        if dybs % 4 or dy.data_ptr() % 16:
+            dy, dybs = dy.contiguous(), dy[0].numel()
+        N, Cin, H, W = x.shape
+        Cout = w.shape[0]
+        flops = _conv_flops(N, Cin, Cout, 4, 4, H // 2, W // 2)
+        dx = None
+        if ctx.needs_input_grad[0]:
+            out, acc = _acc_target(ctx.box)
+            dx = out if out is not None else _empty(N, Cin, H, W, dy)
+            dx4, dxbs = nchw(dx)
+            if dx4.data_ptr() != dx.data_ptr():
+                raise RuntimeError("PatchStemFn: accumulation target is not NCHW-dense")
+            e0 = IGEMM_TIMER.begin()
+            call("dsgan_pgstem_dgrad", ptr(dy), dybs, ptr(y), y[0].numel(), ptr(w), ptr(dx), dxbs, N, Cin, Cout, H, W,
+                 LRELU_SLOPE, int(acc), stream())
+            IGEMM_TIMER.end(e0, flops, ("dgrad", N, Cin, H, W, Cout, 4, 2), "pgstem_kernel",
+                            _nb(dy, y, w, dx) + (_nb(dx) if acc else 0.0))
+            dx = None if acc else _give(ctx.box, dx)
+        gw = _grad_buf(ctx.w_ref) if ctx.needs_input_grad[1] else None
+        gb = _grad_buf(ctx.b_ref) if (b is not None and ctx.needs_input_grad[2]) else None
+        if gw is not None or gb is not None:
+            lib = _lib.load()
+            ws = torch.empty(max(lib.dsgan_pgstem_wgrad_workspace(N, Cin, Cout, H, W), 1), device=dy.device,
+                             dtype=torch.float32)
+            # a frozen weight with a live bias still runs the weight-grad kernel (into scratch)
+            dwt = gw if gw is not None else torch.zeros_like(w)
+            e0 = IGEMM_TIMER.begin()
+            call("dsgan_pgstem_wgrad", ptr(dy), dybs, ptr(y), y[0].numel(), ptr(x), ctx.xbs, ptr(dwt), ptr(gb), N, Cin,
+                 Cout, H, W, LRELU_SLOPE, *wsa(ws), stream())
+            IGEMM_TIMER.end(e0, flops, ("wgrad", N, Cin, H, W, Cout, 4, 2), "pgstem_kernel", _nb(dy, y, x, dwt))
+        _params_done(ctx.w_ref, ctx.b_ref)
+        return dx, None, None
+
+
 def conv2d(x, w, b=None, stride=1, pad=0, act=None):
     """w may be OIHW or a Linear [out, in] weight (== 1x1 conv); pass the Parameter itself so its
     gradient lands in param.grad."""
+    if _pgstem_ok(x, w, stride, pad, act):
+        return PatchStemFn.apply(x, w, b)
     return Conv2dFn.apply(x, w, b, stride, pad, act)
 
 

@@ -211,6 +211,27 @@ int dsgan_conv_wgrad_small(const float* dy, long dy_bs, const float* x, long x_b
                            int Cin, int H, int W, int Cout, int KH, int KW, int stride, int pad, int Ho,
                            int Wo, float* ws, long ws_elems, hipStream_t stream);
 
+/* ---- PatchGAN stem (pgstem.hip, exact fp32) -------------------------------------------------
+ * NLayerDiscriminator layer 0: Conv2d(input_nc, ndf, 4, stride 2, pad 1) + bias + LeakyReLU(0.2, True)
+ * (DSGAN/models/networks.py:543-545), one kernel per direction instead of the generic conv + the
+ * LeakyReLU backward + the bias channel sum.  Cin in {3, 6}, Cout in {32, 64}, H % 8 == 0,
+ * W % 64 == 0, W <= 512 (dsgan_pgstem_supported).  NCHW fp32, w OIHW [Cout][Cin][4][4].
+ *   fwd  : y = lrelu(bias + conv(x)) (bias nullable), y [N][Cout][H/2][W/2];
+ *   wgrad: dw += dW, db += dB (db nullable) from dy (grad of y) and y (the LeakyReLU slope is
+ *          taken where y <= 0); per-workgroup partials in ws (dsgan_pgstem_wgrad_workspace floats)
+ *          summed in a fixed order: deterministic;
+ *   dgrad: dx (+)= the input gradient from dy and y. */
+int dsgan_pgstem_supported(int Cin, int Cout, int H, int W);
+int dsgan_pgstem_fwd(const float* x, long x_bs, const float* w, const float* bias, float* y, long y_bs, int N,
+                     int Cin, int Cout, int H, int W, float slope, hipStream_t stream);
+long dsgan_pgstem_wgrad_workspace(int N, int Cin, int Cout, int H, int W);
+int dsgan_pgstem_wgrad(const float* dy, long dy_bs, const float* y, long y_bs, const float* x, long x_bs, float* dw,
+                       float* db, int N, int Cin, int Cout, int H, int W, float slope, float* ws, long ws_elems,
+                       hipStream_t stream);
+int dsgan_pgstem_dgrad(const float* dy, long dy_bs, const float* y, long y_bs, const float* w, float* dx,
+                       long dx_bs, int N, int Cin, int Cout, int H, int W, float slope, int accumulate,
+                       hipStream_t stream);
+
 /* ---- thin 3x3 / stride 1 / pad 1 convs at full resolution (thin3.hip, exact fp32) ----------
  * The G head res = nn.Conv2d(64, 3, 3, padding=1) (DSGAN/models/model/MixConvNeXtML.py:459, applied
  * at :492): forward, weight-grad and data-grad.  M (the small side) 1..4, H % 4 == 0, W % 256 == 0,
