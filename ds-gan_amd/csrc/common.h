@@ -55,7 +55,10 @@ template <typename F> __host__ inline auto with_half(F&& f) {
   return f((__bf16*)nullptr);
 }
 
-enum Act : int { ACT_NONE = 0, ACT_GELU = 1, ACT_RELU = 2, ACT_LRELU = 3, ACT_SIGMOID = 4 };
+// ACT_GELU_FAST: nn.GELU by the A&S 7.1.26 erfc below (|err| <= 1.5e-7), for the 16-bit modes'
+// InstanceNorm epilogues (functional._in_act): the exact erf form is ~40 VALU per element and bounds
+// those streaming kernels; fp32 mode keeps ACT_GELU.
+enum Act : int { ACT_NONE = 0, ACT_GELU = 1, ACT_RELU = 2, ACT_LRELU = 3, ACT_SIGMOID = 4, ACT_GELU_FAST = 5 };
 
 constexpr float kInvSqrt2 = 0.70710678118654752440f;
 constexpr float kInvSqrt2Pi = 0.39894228040143267794f;
@@ -181,6 +184,7 @@ __device__ __forceinline__ float act_f(int act, float x, float slope) {
     case ACT_RELU: return x > 0.f ? x : 0.f;
     case ACT_LRELU: return x > 0.f ? x : x * slope;
     case ACT_SIGMOID: return 1.f / (1.f + __expf(-x));
+    case ACT_GELU_FAST: return gelu_fast(x);
     default: return x;
   }
 }
@@ -191,6 +195,7 @@ __device__ __forceinline__ float act_g(int act, float x, float slope) {
     case ACT_RELU: return x > 0.f ? 1.f : 0.f;
     case ACT_LRELU: return x > 0.f ? 1.f : slope;
     case ACT_SIGMOID: { float s = 1.f / (1.f + __expf(-x)); return s * (1.f - s); }
+    case ACT_GELU_FAST: { float g, gp; gelu_pair_fast(x, g, gp); return gp; }
     default: return 1.f;
   }
 }

@@ -1421,6 +1421,9 @@ static void in_bwd_launch(const INBwdArgs& a, dim3 grid, dim3 block, hipStream_t
     case ACT_NONE: hipLaunchKernelGGL((instnorm_bwd_v4<NT, C4, CX, XL, ACT_NONE>), grid, block, 0, st, a); break;
     case ACT_GELU: hipLaunchKernelGGL((instnorm_bwd_v4<NT, C4, CX, XL, ACT_GELU>), grid, block, 0, st, a); break;
     case ACT_LRELU: hipLaunchKernelGGL((instnorm_bwd_v4<NT, C4, CX, XL, ACT_LRELU>), grid, block, 0, st, a); break;
+    case ACT_GELU_FAST:
+      hipLaunchKernelGGL((instnorm_bwd_v4<NT, C4, CX, XL, ACT_GELU_FAST>), grid, block, 0, st, a);
+      break;
     default: hipLaunchKernelGGL((instnorm_bwd_v4<NT, C4, CX, XL>), grid, block, 0, st, a); break;
   }
 }

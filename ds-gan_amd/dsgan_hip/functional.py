@@ -33,6 +33,7 @@ def wsa(t):
 WCONV_DB_FOLD = True
 
 ACT = {None: 0, "none": 0, "gelu": 1, "relu": 2, "lrelu": 3, "sigmoid": 4}
+ACT_GELU_FAST = 5   # common.h: GELU by A&S 7.1.26 (|err| <= 1.5e-7), the 16-bit modes' InstanceNorm epilogues
 PREC = {"fp32": 0, "bf16": 1, "fp16": 1}   # the C ABI's prec: 0 exact f32, 1 16-bit MFMA operands
 _state = {"prec": "fp32"}
 IN_EPS = 1e-5
@@ -142,6 +143,12 @@ def _nb(*ts):
 def _conv_flops(N, Cin, Cout, KH, KW, Ho, Wo):
     # algorithmic MACs of the conv (also for its dgrad/wgrad): every output pixel x every tap
     return 2.0 * N * Cout * Cin * KH * KW * Ho * Wo
+
+
+def _in_act(act):
+    """Activation code of an InstanceNorm launch: the 16-bit modes take the A&S GELU (the MLP
+    kernels' form); fp32 mode keeps the exact erf."""
+    return ACT_GELU_FAST if act == "gelu" and _state["prec"] != "fp32" else ACT[act]
 
 
 def nchw(t):
@@ -1400,7 +1407,7 @@ def instnorm_raw(x, scale=None, res=None, act=None, out=None):
     rstd = torch.empty(N * C, device=x.device, dtype=torch.float32)
     e0 = AUX_TIMER.begin()
     call("dsgan_instnorm_fwd_ws", ptr(x), xbs, ptr(scale), ptr(res), rbs, ptr(y4), ybs, ptr(mean),
-         ptr(rstd), N, C, H * W, ACT[act], LRELU_SLOPE, IN_EPS, *wsa(_in_ws(N, C, H * W, x)), stream())
+         ptr(rstd), N, C, H * W, _in_act(act), LRELU_SLOPE, IN_EPS, *wsa(_in_ws(N, C, H * W, x)), stream())
     AUX_TIMER.end(e0, 0.0, ("in_fwd", N, C, H, W, act, res is not None), "instnorm", (3 if res is not None else 2) * _nb(x))
     return y4, mean, rstd
 
@@ -1417,7 +1424,7 @@ def instnorm_bwd_raw(dy, x, scale, res, mean, rstd, act, want_dres, want_dscale)
     dscale = torch.empty(N * C, device=x.device, dtype=torch.float32) if want_dscale else None
     e0 = AUX_TIMER.begin()
     call("dsgan_instnorm_bwd_ws", ptr(dy), dybs, ptr(x), xbs, ptr(scale), ptr(res), rbs, ptr(mean),
-         ptr(rstd), ptr(dx), C * H * W, ptr(dres), C * H * W, ptr(dscale), N, C, H * W, ACT[act],
+         ptr(rstd), ptr(dx), C * H * W, ptr(dres), C * H * W, ptr(dscale), N, C, H * W, _in_act(act),
          LRELU_SLOPE, IN_EPS, *wsa(_in_ws(N, C, H * W, x)), stream())
     AUX_TIMER.end(e0, 0.0, ("in_bwd", N, C, H, W, act, res is not None), "instnorm",
                   (3 + (res is not None) + want_dres) * _nb(x))
@@ -1537,7 +1544,7 @@ class ConvTNormFn(torch.autograd.Function):
         psum = torch.empty(N * Co, device=t.device, dtype=torch.float32)
         e0 = AUX_TIMER.begin()
         call("dsgan_instnorm_bwd_h", ptr(dyt), dybs, ptr(t4), tbs, ptr(res), rbs, ptr(mean), ptr(rstd), ptr(dth),
-             Co * HW, ptr(psum), ptr(dres), Co * HW, N, Co, HW, ACT[ctx.act], LRELU_SLOPE, IN_EPS, stream())
+             Co * HW, ptr(psum), ptr(dres), Co * HW, N, Co, HW, _in_act(ctx.act), LRELU_SLOPE, IN_EPS, stream())
         AUX_TIMER.end(e0, 0.0, ("in_bwd_h", N, Co, H, W, ctx.act, res is not None), "instnorm",
                       _nb(dyt, t4, res, dres) + _nb(dth))
         dx = None
