@@ -98,6 +98,11 @@ SIGNATURES = {
     "dsgan_pgstem_wgrad_workspace": [I] * 5,
     "dsgan_pgstem_wgrad": [P, L, P, L, P, L, P, P] + [I] * 5 + [F, P, L, S],
     "dsgan_pgstem_dgrad": [P, L, P, L, P, P, L] + [I] * 5 + [F, I, S],
+    "dsgan_pglast_supported": [I] * 3,
+    "dsgan_pglast_workspace": [I] * 4,
+    "dsgan_pglast_fwd": [P, L, P, P, P, L] + [I] * 5 + [P, L, S],
+    "dsgan_pglast_wgrad": [P, L, P, L, P, P] + [I] * 4 + [P, L, S],
+    "dsgan_pglast_dgrad": [P, L, P, P, L] + [I] * 5 + [S],
     "dsgan_thin3_fwd": [P, L, P, P, P, L] + [I] * 6 + [S],
     "dsgan_thin3_wgrad_workspace": [I] * 5,
     "dsgan_thin3_wgrad": [P, L, P, L, P, P, L] + [I] * 5 + [S],

@@ -340,6 +340,15 @@ def _pws_ok(K, M, P, xbs, ybs, x, y):
             and bool(_lib.load().dsgan_pw_small_supported(K, M, P, xbs, ybs)))
 
 
+PGLAST = [True]   # the PatchGAN head on pglast.hip (off: the generic small-channel kernels; tests / A-B)
+
+
+def _pglast_ok(Cout, Cin, KH, KW, stride, pad, H, W, w):
+    """Conv(Cin -> 1, 4x4, stride 1, pad 1): the PatchGAN head (networks.py:567-568), pglast.hip."""
+    return (PGLAST[0] and Cout == 1 and KH == 4 and KW == 4 and stride == 1 and pad == 1 and w.dim() == 4
+            and w.is_contiguous() and bool(_lib.load().dsgan_pglast_supported(Cin, H, W)))
+
+
 def _thin3_ok(M, H, W, bs_small, bs_big, t_small, t_big):
     """3x3 / s1 / p1 conv with <= 4 channels on one side at W % 256 == 0 (thin3.hip)."""
     return (t_small.data_ptr() % 16 == 0 and t_big.data_ptr() % 16 == 0
@@ -383,6 +392,12 @@ def conv_fwd_raw(x, w, b, stride, pad, act=None, out=None, pre=None, accumulate=
         fam = "pw_small_kernel"
         call("dsgan_pw_small", ptr(x), xbs, ptr(w), Cin, 1, ptr(b), ptr(y), ybs, None, 0, N, Cin, Cout, H * W,
              ACT[act], ACT[xact], 0, int(accumulate), LRELU_SLOPE, stream())
+    elif _pglast_ok(Cout, Cin, KH, KW, stride, pad, H, W, w) and act is None and pre is None and xact is None:
+        # PatchGAN head 256 -> 1, 4x4 s1 (pglast.hip): channel chunks in LDS, partials summed in order
+        fam = "pglast_kernel"
+        ws = torch.empty(_lib.load().dsgan_pglast_workspace(N, Cin, H, W), device=x.device, dtype=torch.float32)
+        call("dsgan_pglast_fwd", ptr(x), xbs, ptr(w), ptr(b), ptr(y), ybs, N, Cin, H, W, int(accumulate), *wsa(ws),
+             stream())
     elif Cout <= 8 and act is None and pre is None and xact is None:
         # few output channels (G head, PatchGAN last layer): direct conv, not a GEMM tile
         fam = "small_out_kernel"
@@ -453,6 +468,9 @@ def conv_dgrad_raw(dy, w, x_shape, stride, pad, bias=None, act=None, gpre=None, 
         fam = "pw_small_kernel"
         call("dsgan_pw_small", ptr(dy), dybs, ptr(w), 1, Cin, None, ptr(dx), dxbs, ptr(gpre), gbs, N, Cout, Cin, H * W,
              0, 0, ACT[gact], int(accumulate), LRELU_SLOPE, stream())
+    elif _pglast_ok(Cout, Cin, KH, KW, stride, pad, H, W, w) and act is None and bias is None and gpre is None:
+        fam = "pglast_kernel"
+        call("dsgan_pglast_dgrad", ptr(dy), dybs, ptr(w), ptr(dx), dxbs, N, Cin, H, W, int(accumulate), stream())
     elif Cin <= 8 and act is None and gpre is None and stride in (1, 2):
         fam = "small_out_kernel"
         # data-grad into a 3/6-channel tensor: direct transposed gather, w(m=ci, k=co, kh, kw)
@@ -540,6 +558,11 @@ def conv_wgrad_raw(dy, x, dw, stride, pad, xact=None, db=None):
         ws = torch.empty(_lib.load().dsgan_thin3_wgrad_workspace(N, Cin, Cout, H, W), device=dy.device,
                          dtype=torch.float32)
         call("dsgan_thin3_wgrad", ptr(dy), dybs, ptr(x), xbs, ptr(dw), *wsa(ws), N, Cin, Cout, H, W, stream())
+    elif xact is None and dw.is_contiguous() and _pglast_ok(Cout, Cin, KH, KW, stride, pad, H, W, dw):
+        fam = "pglast_kernel"
+        ws = torch.empty(_lib.load().dsgan_pglast_workspace(N, Cin, H, W), device=dy.device, dtype=torch.float32)
+        did_db = db is not None
+        call("dsgan_pglast_wgrad", ptr(dy), dybs, ptr(x), xbs, ptr(dw), ptr(db), N, Cin, H, W, *wsa(ws), stream())
     elif xact is None and KH * KW in (1, 9, 16) and (Cout <= 8 or (Cin <= 8 and KH * KW == 1)):
         fam = "wgrad_small_kernel"
         nws = _lib.load().dsgan_conv_wgrad_small_workspace(N, Cin, Cout, KH, KW, dy.shape[2], dy.shape[3])

@@ -211,6 +211,22 @@ int dsgan_conv_wgrad_small(const float* dy, long dy_bs, const float* x, long x_b
                            int Cin, int H, int W, int Cout, int KH, int KW, int stride, int pad, int Ho,
                            int Wo, float* ws, long ws_elems, hipStream_t stream);
 
+/* ---- PatchGAN head (pglast.hip, exact fp32) --------------------------------------------------
+ * NLayerDiscriminator's last layer Conv2d(ndf * 8, 1, 4, stride 1, pad 1) -> raw logits
+ * (DSGAN/models/networks.py:567-568): x [N][K][H][W] -> y [N][1][H-1][W-1], w [1][K][4][4].
+ * dsgan_pglast_supported(K, H, W): a channel chunk of the planes stages in 40 KB of LDS.
+ *   fwd  : y (+)= bias + conv (bias nullable); per-chunk partials in ws (dsgan_pglast_workspace);
+ *   wgrad: dw += dW, db += dB (db nullable); per-image partials in ws summed in a fixed order;
+ *   dgrad: dx (+)= the input gradient. */
+int dsgan_pglast_supported(int K, int H, int W);
+long dsgan_pglast_workspace(int N, int K, int H, int W);
+int dsgan_pglast_fwd(const float* x, long x_bs, const float* w, const float* bias, float* y, long y_bs, int N, int K,
+                     int H, int W, int accumulate, float* ws, long ws_elems, hipStream_t stream);
+int dsgan_pglast_wgrad(const float* dy, long dy_bs, const float* x, long x_bs, float* dw, float* db, int N, int K,
+                       int H, int W, float* ws, long ws_elems, hipStream_t stream);
+int dsgan_pglast_dgrad(const float* dy, long dy_bs, const float* w, float* dx, long dx_bs, int N, int K, int H, int W,
+                       int accumulate, hipStream_t stream);
+
 /* ---- PatchGAN stem (pgstem.hip, exact fp32) -------------------------------------------------
  * NLayerDiscriminator layer 0: Conv2d(input_nc, ndf, 4, stride 2, pad 1) + bias + LeakyReLU(0.2, True)
  * (DSGAN/models/networks.py:543-545), one kernel per direction instead of the generic conv + the

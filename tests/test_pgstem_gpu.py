@@ -140,3 +140,61 @@ def test_stem_dgrad_accumulates_into_slices():
     assert rel(big, ref) < 1e-6
     assert not _lib.load().dsgan_pgstem_supported(6, 32, 60, 64)
     assert not _lib.load().dsgan_pgstem_supported(6, 48, 64, 64)
+
+
+# ---- PatchGAN head (csrc/pglast.hip): Conv2d(ndf * 8, 1, 4, stride 1, pad 1), networks.py:567-568 ----
+
+@pytest.mark.parametrize("N,K,H,W", [(16, 256, 31, 31), (2, 256, 63, 63), (3, 64, 7, 9), (2, 40, 15, 15)])
+def test_head_vs_float64(N, K, H, W):
+    from dsgan_hip import _lib
+    from dsgan_hip import functional as HF
+    assert _lib.load().dsgan_pglast_supported(K, H, W)
+    HF.set_precision("bf16")
+    g = torch.Generator().manual_seed(N * 1000 + K + H)
+    x = torch.randn(N, K, H, W, generator=g)
+    w = torch.randn(1, K, 4, 4, generator=g) * 0.05
+    b = torch.randn(1, generator=g)
+    dy = torch.randn(N, 1, H - 1, W - 1, generator=g)
+    xg = x.to(DEV).requires_grad_(True)
+    wp = torch.nn.Parameter(w.to(DEV))
+    bp = torch.nn.Parameter(b.to(DEV))
+    wp.grad = torch.zeros_like(wp)
+    bp.grad = torch.zeros_like(bp)
+    y = HF.conv2d(xg, wp, bp, stride=1, pad=1)
+    y.backward(dy.to(DEV))
+    torch.cuda.synchronize()
+    xd, wd, bd = (t.double().requires_grad_(True) for t in (x, w, b))
+    yr = F.conv2d(xd, wd, bd, stride=1, padding=1)
+    yr.backward(dy.double())
+    assert rel(y, yr) < 1e-6
+    assert rel(xg.grad, xd.grad) < 1e-6
+    assert rel(wp.grad, wd.grad) < 1e-5
+    assert rel(bp.grad, bd.grad) < 1e-6
+
+
+def test_head_matches_generic_path_and_is_deterministic():
+    """Same layer with HF.PGLAST off (small_out / implicit GEMM / wgrad_small): equal to the fp32
+    bar; two runs of the head kernels give the same bits."""
+    from dsgan_hip import functional as HF
+    HF.set_precision("fp32")
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(4, 256, 31, 31, generator=g)
+    w = torch.randn(1, 256, 4, 4, generator=g) * 0.05
+    b = torch.randn(1, generator=g)
+    dy = torch.randn(4, 1, 30, 30, generator=g)
+    res = []
+    for on in (True, True, False):
+        HF.PGLAST[0] = on
+        xg = x.to(DEV).requires_grad_(True)
+        wp = torch.nn.Parameter(w.to(DEV))
+        bp = torch.nn.Parameter(b.to(DEV))
+        wp.grad = torch.zeros_like(wp)
+        bp.grad = torch.zeros_like(bp)
+        y = HF.conv2d(xg, wp, bp, stride=1, pad=1)
+        y.backward(dy.to(DEV))
+        torch.cuda.synchronize()
+        res.append((y.detach(), xg.grad, wp.grad, bp.grad))
+    HF.PGLAST[0] = True
+    for u, v, r in zip(res[0], res[1], res[2]):
+        assert torch.equal(u, v)
+        assert rel(u, r) < 2e-6

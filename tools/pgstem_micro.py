@@ -69,6 +69,23 @@ def main():
     rows.append(("generic bias sum", tmed(lambda: HF.channel_sum_raw(dy, db)), mb(dy)))
     rows.append(("generic dgrad", tmed(lambda: HF.conv_dgrad_raw(dy, w, (N, Cin, H, W), 2, 1, out=dx)), mb(dy, dx)))
     HF.PGSTEM[0] = True
+    # PatchGAN head (pglast.hip) vs the generic small-channel kernels: 256 -> 1, 4x4 s1 at 31^2
+    K, Hh = 256, H // 8 - 1
+    xh = torch.randn(N, K, Hh, Hh, generator=g).cuda()
+    wh = (torch.randn(1, K, 4, 4, generator=g) * 0.05).cuda()
+    bh = torch.zeros(1, device="cuda")
+    dyh = torch.randn(N, 1, Hh - 1, Hh - 1, generator=g).cuda()
+    yh = torch.empty(N, 1, Hh - 1, Hh - 1, device="cuda")
+    dxh = torch.empty_like(xh)
+    dwh, dbh = torch.zeros_like(wh), torch.zeros_like(bh)
+    for on in (True, False):
+        HF.PGLAST[0] = on
+        tag = "head" if on else "generic head"
+        rows.append((tag + " fwd", tmed(lambda: HF.conv_fwd_raw(xh, wh, bh, 1, 1, out=yh)), mb(xh, yh)))
+        rows.append((tag + " dgrad", tmed(lambda: HF.conv_dgrad_raw(dyh, wh, tuple(xh.shape), 1, 1, out=dxh)),
+                     mb(dyh, dxh)))
+        rows.append((tag + " wgrad", tmed(lambda: HF.conv_wgrad_raw(dyh, xh, dwh, 1, 1, db=dbh)), mb(dyh, xh)))
+    HF.PGLAST[0] = True
     for name, us, m in rows:
         print("%-18s %8.1f us  %7.1f MB  %6.0f GB/s" % (name, us, m, m * 1e3 / us))
 
