@@ -42,19 +42,30 @@ __device__ __forceinline__ float t3_ld1(__amdgpu_buffer_rsrc_t r, unsigned off) 
   return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, (int)off, 0, 0));
 }
 
-// Row h of plane `plane` (element offset), columns c0-1 .. c0+4 of this lane (c0 = seg*256 + 4*lane).
-__device__ __forceinline__ void t3_row6(__amdgpu_buffer_rsrc_t r, unsigned plane, int h, int H, int W, int c0,
-                                        int lane, float (&v)[6]) {
+// Row h of plane `plane` (element offset), columns c0-1 .. c0+4 of this lane (c0 = seg*256 + 4*lane):
+// the loads (t3_row_ld: the lane's 16 bytes + the outer lanes' halo columns) and the assembly from
+// the neighbour lanes (t3_row_asm) are separate, so a loop can issue the next channel's loads first.
+struct T3Row { float4 q; float el, er; };
+__device__ __forceinline__ T3Row t3_row_ld(__amdgpu_buffer_rsrc_t r, unsigned plane, int h, int H, int W, int c0,
+                                           int lane) {
   const bool ok = (unsigned)h < (unsigned)H;
   const unsigned rowoff = plane + (unsigned)(h * W);
-  const float4 q = t3_ld4(r, ok ? (rowoff + (unsigned)c0) * 4u : T3_OOB);
+  T3Row o;
+  o.q = t3_ld4(r, ok ? (rowoff + (unsigned)c0) * 4u : T3_OOB);
   // halo columns of the segment's outer lanes (a neighbouring segment, or the zero padding)
-  const float el = t3_ld1(r, (ok && lane == 0 && c0 > 0) ? (rowoff + (unsigned)c0 - 1u) * 4u : T3_OOB);
-  const float er = t3_ld1(r, (ok && lane == 63 && c0 + 4 < W) ? (rowoff + (unsigned)c0 + 4u) * 4u : T3_OOB);
-  const float l = __shfl_up(q.w, 1, 64), rr = __shfl_down(q.x, 1, 64);
-  v[0] = lane == 0 ? el : l;
-  v[1] = q.x; v[2] = q.y; v[3] = q.z; v[4] = q.w;
-  v[5] = lane == 63 ? er : rr;
+  o.el = t3_ld1(r, (ok && lane == 0 && c0 > 0) ? (rowoff + (unsigned)c0 - 1u) * 4u : T3_OOB);
+  o.er = t3_ld1(r, (ok && lane == 63 && c0 + 4 < W) ? (rowoff + (unsigned)c0 + 4u) * 4u : T3_OOB);
+  return o;
+}
+__device__ __forceinline__ void t3_row_asm(const T3Row& o, int lane, float (&v)[6]) {
+  const float l = __shfl_up(o.q.w, 1, 64), rr = __shfl_down(o.q.x, 1, 64);
+  v[0] = lane == 0 ? o.el : l;
+  v[1] = o.q.x; v[2] = o.q.y; v[3] = o.q.z; v[4] = o.q.w;
+  v[5] = lane == 63 ? o.er : rr;
+}
+__device__ __forceinline__ void t3_row6(__amdgpu_buffer_rsrc_t r, unsigned plane, int h, int H, int W, int c0,
+                                        int lane, float (&v)[6]) {
+  t3_row_asm(t3_row_ld(r, plane, h, H, W, c0, lane), lane, v);
 }
 
 __device__ __forceinline__ void t3_strip(int id, int H, int W, int& b, int& h0, int& c0, int lane) {
@@ -81,16 +92,27 @@ __global__ __launch_bounds__(256) void thin3_fwd_kernel(T3Args a) {
     for (int p = 0; p < 4; ++p)
 #pragma unroll
       for (int m = 0; m < MS; ++m) acc[r][p][m] = 0.f;
+  // the next channel's 6 rows are loaded before this channel's FMAs (one channel in flight)
+  T3Row nx[6];
+  if (wave < a.K) {
+    const unsigned plane = (unsigned)((long)b * a.x_bs) + (unsigned)wave * HW;
+#pragma unroll
+    for (int i = 0; i < 6; ++i) nx[i] = t3_row_ld(rx, plane, h0 - 1 + i, a.H, a.W, c0, lane);
+  }
   for (int k = wave; k < a.K; k += 4) {
-    const unsigned plane = (unsigned)((long)b * a.x_bs) + (unsigned)k * HW;
     float in[6][6];
 #pragma unroll
-    for (int i = 0; i < 6; ++i) t3_row6(rx, plane, h0 - 1 + i, a.H, a.W, c0, lane, in[i]);
+    for (int i = 0; i < 6; ++i) t3_row_asm(nx[i], lane, in[i]);
+    if (k + 4 < a.K) {
+      const unsigned plane = (unsigned)((long)b * a.x_bs) + (unsigned)(k + 4) * HW;
+#pragma unroll
+      for (int i = 0; i < 6; ++i) nx[i] = t3_row_ld(rx, plane, h0 - 1 + i, a.H, a.W, c0, lane);
+    }
     float wv[MS][9];
 #pragma unroll
     for (int m = 0; m < MS; ++m)
 #pragma unroll
-      for (int t = 0; t < 9; ++t) wv[m][t] = m < a.M ? a.w[((long)m * a.K + k) * 9 + t] : 0.f;
+      for (int t = 0; t < 9; ++t) wv[m][t] = a.w[((long)m * a.K + k) * 9 + t];
 #pragma unroll
     for (int r = 0; r < 4; ++r)
 #pragma unroll
@@ -112,7 +134,6 @@ __global__ __launch_bounds__(256) void thin3_fwd_kernel(T3Args a) {
   if (wave > 0) return;
 #pragma unroll
   for (int m = 0; m < MS; ++m) {
-    if (m >= a.M) break;
     const float bv = a.bias ? a.bias[m] : 0.f;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -147,6 +168,7 @@ __global__ __launch_bounds__(256) void thin3_wgrad_kernel(T3Args a) {
     for (int m = 0; m < MS; ++m)
 #pragma unroll
       for (int t = 0; t < 9; ++t) acc[c][m][t] = 0.f;
+#pragma unroll 1
   for (int s = s0; s < s1; ++s) {
     int b, h0, c0;
     t3_strip(s, a.H, a.W, b, h0, c0, lane);
@@ -155,8 +177,7 @@ __global__ __launch_bounds__(256) void thin3_wgrad_kernel(T3Args a) {
     for (int m = 0; m < MS; ++m)
 #pragma unroll
       for (int r = 0; r < 4; ++r)
-        gv[m][r] = t3_ld4(rg, m < a.M ? ((unsigned)((long)b * a.g_bs) + (unsigned)m * HW + (unsigned)((h0 + r) * a.W + c0)) * 4u
-                                      : T3_OOB);
+        gv[m][r] = t3_ld4(rg, ((unsigned)((long)b * a.g_bs) + (unsigned)m * HW + (unsigned)((h0 + r) * a.W + c0)) * 4u);
 #pragma unroll
     for (int c = 0; c < CW; ++c) {
       const int k = kb + c;
@@ -186,7 +207,7 @@ __global__ __launch_bounds__(256) void thin3_wgrad_kernel(T3Args a) {
 #pragma unroll
       for (int t = 0; t < 9; ++t) {
         const float v = warp_sum(acc[c][m][t]);
-        if (lane == 0 && k < a.K && m < a.M) dst[((long)m * a.K + k) * 9 + t] = v;
+        if (lane == 0 && k < a.K) dst[((long)m * a.K + k) * 9 + t] = v;
       }
   }
 }
@@ -204,21 +225,16 @@ __global__ __launch_bounds__(256) void thin3_dgrad_kernel(T3Args a) {
   for (int m = 0; m < MS; ++m) {
     const unsigned plane = (unsigned)((long)b * a.x_bs) + (unsigned)m * HW;
 #pragma unroll
-    for (int i = 0; i < 6; ++i) {
-      if (m < a.M) t3_row6(rx, plane, h0 - 1 + i, a.H, a.W, c0, lane, in[m][i]);
-      else {
-#pragma unroll
-        for (int j = 0; j < 6; ++j) in[m][i][j] = 0.f;
-      }
-    }
+    for (int i = 0; i < 6; ++i) t3_row6(rx, plane, h0 - 1 + i, a.H, a.W, c0, lane, in[m][i]);
   }
+#pragma unroll 1
   for (int k = wave; k < a.K; k += 4) {
     // flipped taps: dx[h][w] += w[m][k][2-i][2-j] dy[h-1+i][w-1+j]
     float wv[MS][9];
 #pragma unroll
     for (int m = 0; m < MS; ++m)
 #pragma unroll
-      for (int t = 0; t < 9; ++t) wv[m][t] = m < a.M ? a.w[((long)m * a.K + k) * 9 + (8 - t)] : 0.f;
+      for (int t = 0; t < 9; ++t) wv[m][t] = a.w[((long)m * a.K + k) * 9 + (8 - t)];
     float* yk = a.y + (long)b * a.y_bs + ((long)k * a.H + h0) * a.W + c0;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -283,9 +299,9 @@ int dsgan_thin3_fwd(const float* x, long x_bs, const float* w, const float* bias
   a.w = w; a.bias = bias; a.y = y; a.y_bs = y_bs; a.nb = nb; a.K = K; a.M = M; a.H = H; a.W = W;
   a.accumulate = accumulate;
   const dim3 grid((unsigned)((long)nb * (H / 4) * (W / 256)));
-  if (M <= 1) hipLaunchKernelGGL(thin3_fwd_kernel<1>, grid, dim3(256), 0, st, a);
-  else if (M <= 2) hipLaunchKernelGGL(thin3_fwd_kernel<2>, grid, dim3(256), 0, st, a);
-  else if (M <= 3) hipLaunchKernelGGL(thin3_fwd_kernel<3>, grid, dim3(256), 0, st, a);
+  if (M == 1) hipLaunchKernelGGL(thin3_fwd_kernel<1>, grid, dim3(256), 0, st, a);
+  else if (M == 2) hipLaunchKernelGGL(thin3_fwd_kernel<2>, grid, dim3(256), 0, st, a);
+  else if (M == 3) hipLaunchKernelGGL(thin3_fwd_kernel<3>, grid, dim3(256), 0, st, a);
   else hipLaunchKernelGGL(thin3_fwd_kernel<4>, grid, dim3(256), 0, st, a);
   DSG_CHECK_LAUNCH();
   return 0;
@@ -313,9 +329,9 @@ int dsgan_thin3_wgrad(const float* dy, long dy_bs, const float* x, long x_bs, fl
   a.strips_per_wg = spw;
   DSG_WS(splits * (long)M * K * 9, ws, ws_elems, "dsgan_thin3_wgrad (dsgan_thin3_wgrad_workspace)");
   const dim3 grid((unsigned)((K + 4 * T3_CW - 1) / (4 * T3_CW)), (unsigned)splits);
-  if (M <= 1) hipLaunchKernelGGL((thin3_wgrad_kernel<1, T3_CW>), grid, dim3(256), 0, st, a);
-  else if (M <= 2) hipLaunchKernelGGL((thin3_wgrad_kernel<2, T3_CW>), grid, dim3(256), 0, st, a);
-  else if (M <= 3) hipLaunchKernelGGL((thin3_wgrad_kernel<3, T3_CW>), grid, dim3(256), 0, st, a);
+  if (M == 1) hipLaunchKernelGGL((thin3_wgrad_kernel<1, T3_CW>), grid, dim3(256), 0, st, a);
+  else if (M == 2) hipLaunchKernelGGL((thin3_wgrad_kernel<2, T3_CW>), grid, dim3(256), 0, st, a);
+  else if (M == 3) hipLaunchKernelGGL((thin3_wgrad_kernel<3, T3_CW>), grid, dim3(256), 0, st, a);
   else hipLaunchKernelGGL((thin3_wgrad_kernel<4, T3_CW>), grid, dim3(256), 0, st, a);
   DSG_CHECK_LAUNCH();
   launch_split_reduce(ws, (int)splits, (long)M * K * 9, dw, st);
@@ -333,9 +349,9 @@ int dsgan_thin3_dgrad(const float* dy, long dy_bs, const float* w, float* dx, lo
   DSG_REQUIRE(t3_args(a, dy, dy_bs, M, nb, H, W), "dsgan_thin3_dgrad: dy exceeds 4 GiB / unaligned");
   a.w = w; a.y = dx; a.y_bs = dx_bs; a.nb = nb; a.K = K; a.M = M; a.H = H; a.W = W; a.accumulate = accumulate;
   const dim3 grid((unsigned)((long)nb * (H / 4) * (W / 256)));
-  if (M <= 1) hipLaunchKernelGGL(thin3_dgrad_kernel<1>, grid, dim3(256), 0, st, a);
-  else if (M <= 2) hipLaunchKernelGGL(thin3_dgrad_kernel<2>, grid, dim3(256), 0, st, a);
-  else if (M <= 3) hipLaunchKernelGGL(thin3_dgrad_kernel<3>, grid, dim3(256), 0, st, a);
+  if (M == 1) hipLaunchKernelGGL(thin3_dgrad_kernel<1>, grid, dim3(256), 0, st, a);
+  else if (M == 2) hipLaunchKernelGGL(thin3_dgrad_kernel<2>, grid, dim3(256), 0, st, a);
+  else if (M == 3) hipLaunchKernelGGL(thin3_dgrad_kernel<3>, grid, dim3(256), 0, st, a);
   else hipLaunchKernelGGL(thin3_dgrad_kernel<4>, grid, dim3(256), 0, st, a);
   DSG_CHECK_LAUNCH();
   return 0;
