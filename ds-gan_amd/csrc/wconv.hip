@@ -289,34 +289,52 @@ __global__ __launch_bounds__(256, XH ? 2 : 1) void wconv_kernel(WcArgs g) {
   }
 }
 
-// dW[m][c][t] += sum_s P[s][t][m][c] for 4 consecutive c per thread (fixed split order:
-// deterministic); 4 independent partial sums keep several loads in flight.
-__global__ void wconv_reduce_kernel(const float* __restrict__ P, int splits, int T, int M, int C,
-                                    float* __restrict__ dw) {
-  const long total = (long)T * M * C, total4 = total / 4;
-  for (long e4 = blockIdx.x * 256L + threadIdx.x; e4 < total4; e4 += (long)gridDim.x * 256) {
-    const float4* p = reinterpret_cast<const float4*>(P) + e4;
-    float4 s[4] = {};
-    int sp = 0;
-    for (; sp + 4 <= splits; sp += 4) {
+// dW[m][c][t] += sum_s P[s][t][m][c] (fixed split order: deterministic). Workgroup = 4 rows m x 32
+// channels c: the partial rows are read coalesced along c, the sums go through LDS and leave as the
+// contiguous dw block [m][c0..c0+31][0..T-1] (coalesced read-modify-write, no T-strided scatter).
+// Per element, the order of additions: 4 running sums over splits s = u mod 4 (the tail splits on
+// sum 0), combined as (s0 + s1) + (s2 + s3).
+// (WCR_MB = 4 rows per workgroup for wide problems, 1 for the few-tile / many-split ones.)
+template <int WCR_MB>
+__global__ __launch_bounds__(256) void wconv_reduce_kernel(const float* __restrict__ P, int splits, int T, int M,
+                                                           int C, float* __restrict__ dw) {
+  __shared__ float sh[WCR_MB * 32 * 17];
+  const int cbs = C / WC_BC;
+  const int c0 = (blockIdx.x % cbs) * WC_BC, m0 = (blockIdx.x / cbs) * WCR_MB;
+  const long plane = (long)M * C, sstride = plane * T;
+  const int n = WCR_MB * 32 * T;
+  for (int q = threadIdx.x; q < n; q += 256) {
+    const int c = q & 31, mi = (q >> 5) & (WCR_MB - 1), t = q / (32 * WCR_MB);
+    const int m = m0 + mi;
+    float r = 0.f;
+    if (m < M) {
+      const float* p = P + (long)t * plane + (long)m * C + c0 + c;
+      float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+      int sp = 0;
+      for (; sp + 16 <= splits; sp += 16) {   // 16 loads in flight, added in the 4-sum order
+        float v[16];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const float4 v = p[(long)(sp + u) * total4];
-        s[u].x += v.x; s[u].y += v.y; s[u].z += v.z; s[u].w += v.w;
+        for (int u = 0; u < 16; ++u) v[u] = p[(long)(sp + u) * sstride];
+#pragma unroll
+        for (int u = 0; u < 16; u += 4) { s0 += v[u]; s1 += v[u + 1]; s2 += v[u + 2]; s3 += v[u + 3]; }
       }
+      for (; sp + 4 <= splits; sp += 4) {
+        s0 += p[(long)sp * sstride]; s1 += p[(long)(sp + 1) * sstride];
+        s2 += p[(long)(sp + 2) * sstride]; s3 += p[(long)(sp + 3) * sstride];
+      }
+      for (; sp < splits; ++sp) s0 += p[(long)sp * sstride];
+      r = (s0 + s1) + (s2 + s3);
     }
-    for (; sp < splits; ++sp) {
-      const float4 v = p[(long)sp * total4];
-      s[0].x += v.x; s[0].y += v.y; s[0].z += v.z; s[0].w += v.w;
-    }
-    const float r[4] = {(s[0].x + s[1].x) + (s[2].x + s[3].x), (s[0].y + s[1].y) + (s[2].y + s[3].y),
-                        (s[0].z + s[1].z) + (s[2].z + s[3].z), (s[0].w + s[1].w) + (s[2].w + s[3].w)};
-    const long e = e4 * 4;
-    const int c = e % C;
-    const long rr = e / C;
-    const int m = rr % M, t = rr / M;
-#pragma unroll
-    for (int u = 0; u < 4; ++u) dw[((long)m * C + c + u) * T + t] += r[u];
+    sh[(mi * 32 + c) * (T + 1) + t] = r;
+  }
+  __syncthreads();
+  const int blk = 32 * T;
+  for (int j = threadIdx.x; j < n; j += 256) {
+    const int mi = j / blk, rr = j - mi * blk;
+    if (m0 + mi >= M) break;
+    const int c = rr / T, t = rr - c * T;
+    float* d = dw + ((long)(m0 + mi) * C + c0) * T + rr;
+    *d += sh[(mi * 32 + c) * (T + 1) + t];
   }
 }
 
@@ -403,10 +421,12 @@ static int wconv_impl(const float* D, long d_bs, const void* X, long x_bs, bool 
     else wc_launch<T16, 4, 1>(g, grid, xh, st);
   });
   DSG_CHECK_LAUNCH();
-  const long total4 = (long)KH * KW * M * C / 4;
-  long blocks = (total4 + 255) / 256;
-  if (blocks > 4096) blocks = 4096;
-  hipLaunchKernelGGL(wconv_reduce_kernel, dim3((unsigned)blocks), dim3(256), 0, st, ws, p.splits, KH * KW, M, C, dw);
+  if ((long)M * (C / WC_BC) >= 4096)
+    hipLaunchKernelGGL(wconv_reduce_kernel<4>, dim3((unsigned)((long)((M + 3) / 4) * (C / WC_BC))), dim3(256), 0, st,
+                       ws, p.splits, KH * KW, M, C, dw);
+  else
+    hipLaunchKernelGGL(wconv_reduce_kernel<1>, dim3((unsigned)((long)M * (C / WC_BC))), dim3(256), 0, st, ws, p.splits,
+                       KH * KW, M, C, dw);
   if (db) launch_split_reduce(g.dbp, p.splits, M, db, st);
   DSG_CHECK_LAUNCH();
   return 0;
