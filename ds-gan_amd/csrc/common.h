@@ -5,12 +5,13 @@
 
 namespace dsg {
 
-// dw[e] += sum_s ws[s * MN + e] for s = 0..splits-1 in a fixed order (pwgemm.hip): the
+// dw[e] += sum_s ws[s * MN + e] for s = 0..splits-1 in a fixed order (split_reduce.hip): the
 // deterministic reduction every split weight-grad (pwgemm, igemm, skinny) finishes with.
 void launch_split_reduce(const float* ws, int splits, long MN, float* dw, hipStream_t st);
 // ... with elements e = (c, i), i < KK1: i < KK1-1 -> dw[c*(KK1-1)+i], i == KK1-1 -> db[c]
 void launch_split_reduce_kk(const float* ws, int splits, long MN, float* dw, float* db, int KK1, hipStream_t st);
-// n (<= 4) independent reductions in one launch when none needs the many-split pre-pass (same bits)
+// n independent reductions with disjoint outputs in one launch (split_reduce.hip: the fixed order,
+// and the deferred mode that queues them for one batched flush)
 void launch_split_reduce_multi(int n, const float* const* ws, const int* splits, const long* MN, float* const* dw,
                                hipStream_t st);
 

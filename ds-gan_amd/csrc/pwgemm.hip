@@ -123,206 +123,7 @@ static void wg_dispatch(const PwArgs& g0, int bm, int abf, int bbf, int splits, 
   else pw_wgrad_launch<__bf16>(g, bm, abf, bbf, splits, st);
 }
 
-// dw[e] += sum_s ws[s][e], s in a fixed order: thread (e, j) of a workgroup of EL elements x J
-// s-lanes sums s = j, j+J, j+2J, ... in order, then the J partial sums of an element are added
-// j = 0..J-1 -- the same tree on every run.  J grows with the split count so that a reduction of
-// many splits over few elements still spreads over many workgroups.  KK1 > 0: element e is
-// (c, i) = (e / KK1, e % KK1) and goes to dw[c*(KK1-1) + i] (i < KK1-1) or db[c] (depthwise
-// weight + bias partial vectors, dwconv.hip).
-template <int J>
-__device__ __forceinline__ void split_reduce_body(const float* __restrict__ ws, int S, long MN, long rs,
-                                                  float* __restrict__ dw, float* __restrict__ db, int KK1, int blk,
-                                                  float* shm) {
-  constexpr int EL = 256 / J;
-  float (*sh)[EL + 1] = reinterpret_cast<float (*)[EL + 1]>(shm);
-  const int el = threadIdx.x % EL, j = threadIdx.x / EL;
-  const long e = (long)blk * EL + el;
-  float a = 0.f;
-  if (e < MN) {
-    int s = j;
-    for (; s + 3 * J < S; s += 4 * J) {
-      const float v0 = ws[(long)s * rs + e], v1 = ws[(long)(s + J) * rs + e];
-      const float v2 = ws[(long)(s + 2 * J) * rs + e], v3 = ws[(long)(s + 3 * J) * rs + e];
-      a += v0; a += v1; a += v2; a += v3;
-    }
-    for (; s < S; s += J) a += ws[(long)s * rs + e];
-  }
-  sh[j][el] = a;
-  __syncthreads();
-  if (j == 0 && e < MN) {
-    float t = 0.f;
-#pragma unroll
-    for (int q = 0; q < J; ++q) t += sh[q][el];
-    if (KK1 == 0) dw[e] += t;
-    else {
-      const long c = e / KK1;
-      const int i = (int)(e - c * KK1);
-      if (i < KK1 - 1) dw[c * (KK1 - 1) + i] += t;
-      else if (db) db[c] += t;
-    }
-  }
-}
-template <int J>
-__global__ __launch_bounds__(256) void split_reduce_kernel(const float* __restrict__ ws, int S, long MN, long rs,
-                                                           float* __restrict__ dw, float* __restrict__ db, int KK1) {
-  __shared__ float sh[J * (256 / J + 1)];
-  split_reduce_body<J>(ws, S, MN, rs, dw, db, KK1, blockIdx.x, sh);
-}
-
-// The same reduction on 16-byte element groups (KK1 == 0, MN % 4 == 0, 16-byte aligned rows): a
-// lane sums four consecutive elements per load, so a wave reads 4 rows x 256 B instead of 4 rows x
-// 64 B per instruction; the per-element order of additions is the scalar kernel's (same bits).
-template <int J>
-__device__ __forceinline__ void split_reduce4_body(const float* __restrict__ ws, int S, long MN, long rs,
-                                                   float* __restrict__ dw, int blk, float4* shm) {
-  constexpr int EL = 256 / J;
-  float4 (*sh)[EL + 1] = reinterpret_cast<float4 (*)[EL + 1]>(shm);
-  const int el = threadIdx.x % EL, j = threadIdx.x / EL;
-  const long e = ((long)blk * EL + el) * 4;
-  float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
-  auto add = [](float4& x, const float4 v) { x.x += v.x; x.y += v.y; x.z += v.z; x.w += v.w; };
-  if (e < MN) {
-    int s = j;
-    for (; s + 3 * J < S; s += 4 * J) {
-      const float4 v0 = *reinterpret_cast<const float4*>(ws + (long)s * rs + e);
-      const float4 v1 = *reinterpret_cast<const float4*>(ws + (long)(s + J) * rs + e);
-      const float4 v2 = *reinterpret_cast<const float4*>(ws + (long)(s + 2 * J) * rs + e);
-      const float4 v3 = *reinterpret_cast<const float4*>(ws + (long)(s + 3 * J) * rs + e);
-      add(a, v0); add(a, v1); add(a, v2); add(a, v3);
-    }
-    for (; s < S; s += J) add(a, *reinterpret_cast<const float4*>(ws + (long)s * rs + e));
-  }
-  sh[j][el] = a;
-  __syncthreads();
-  if (j == 0 && e < MN) {
-    float4 t = make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-    for (int q = 0; q < J; ++q) add(t, sh[q][el]);
-    float4* d = reinterpret_cast<float4*>(dw + e);
-    float4 o = *d;
-    add(o, t);
-    *d = o;
-  }
-}
-template <int J>
-__global__ __launch_bounds__(256) void split_reduce4_kernel(const float* __restrict__ ws, int S, long MN, long rs,
-                                                            float* __restrict__ dw) {
-  __shared__ float4 sh[J * (256 / J + 1)];
-  split_reduce4_body<J>(ws, S, MN, rs, dw, blockIdx.x, sh);
-}
-
-// Up to RS_MAX independent reductions (KK1 == 0, no pre-pass) in ONE launch: segment i owns blocks
-// [b0[i], b0[i+1]) and runs exactly the body (form and J) its own launch would (same bits).
-constexpr int RS_MAX = 4;
-struct RSeg { const float* ws; float* dw; long MN; int S; int form; int b0; };   // form: 0..3 = (v4, J=16)
-struct RSegs { RSeg s[RS_MAX + 1]; int n; };
-__global__ __launch_bounds__(256) void split_reduce_multi_kernel(RSegs R) {
-  __shared__ float4 sh[16 * (256 / 16 + 1)];
-  int i = 0;
-#pragma unroll
-  for (int q = 1; q < RS_MAX; ++q)
-    if (q < R.n && (int)blockIdx.x >= R.s[q].b0) i = q;
-  const RSeg g = R.s[i];
-  const int blk = blockIdx.x - g.b0;
-  switch (g.form) {
-    case 3: split_reduce4_body<16>(g.ws, g.S, g.MN, g.MN, g.dw, blk, sh); break;
-    case 2: split_reduce4_body<4>(g.ws, g.S, g.MN, g.MN, g.dw, blk, sh); break;
-    case 1: split_reduce_body<16>(g.ws, g.S, g.MN, g.MN, g.dw, nullptr, 0, blk, reinterpret_cast<float*>(sh)); break;
-    default: split_reduce_body<4>(g.ws, g.S, g.MN, g.MN, g.dw, nullptr, 0, blk, reinterpret_cast<float*>(sh)); break;
-  }
-}
-
-// Pre-pass for many splits over few elements: workgroup (element block, row group g) adds rows
-// [g*SC, (g+1)*SC) (64 elements x 4 row lanes, coalesced 256-B row reads, fixed order) and writes
-// the sum over its own first row, which no other workgroup reads -- in place, no scratch.
-constexpr int SPLIT_SC = 16;
-__global__ __launch_bounds__(256) void split_prereduce_kernel(float* __restrict__ ws, int S, long MN) {
-  __shared__ float sh[4][65];
-  const int el = threadIdx.x & 63, j = threadIdx.x >> 6;
-  const long e = (long)blockIdx.x * 64 + el;
-  const int s0 = blockIdx.y * SPLIT_SC, s1 = min(S, s0 + SPLIT_SC);
-  float a = 0.f;
-  if (e < MN)
-    for (int s = s0 + j; s < s1; s += 4) a += ws[(long)s * MN + e];
-  sh[j][el] = a;
-  __syncthreads();
-  if (j == 0 && e < MN) ws[(long)s0 * MN + e] = ((sh[0][el] + sh[1][el]) + sh[2][el]) + sh[3][el];
-}
-
-// 16-byte form of the pre-pass (MN % 4 == 0, 16-byte aligned rows): 64 float4 per row group lane.
-__global__ __launch_bounds__(256) void split_prereduce4_kernel(float* __restrict__ ws, int S, long MN) {
-  __shared__ float4 sh[4][65];
-  const int el = threadIdx.x & 63, j = threadIdx.x >> 6;
-  const long e = ((long)blockIdx.x * 64 + el) * 4;
-  const int s0 = blockIdx.y * SPLIT_SC, s1 = min(S, s0 + SPLIT_SC);
-  float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
-  if (e < MN)
-    for (int s = s0 + j; s < s1; s += 4) {
-      const float4 v = *reinterpret_cast<const float4*>(ws + (long)s * MN + e);
-      a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
-    }
-  sh[j][el] = a;
-  __syncthreads();
-  if (j == 0 && e < MN) {
-    const float4 p0 = sh[0][el], p1 = sh[1][el], p2 = sh[2][el], p3 = sh[3][el];
-    *reinterpret_cast<float4*>(ws + (long)s0 * MN + e) =
-        make_float4(((p0.x + p1.x) + p2.x) + p3.x, ((p0.y + p1.y) + p2.y) + p3.y, ((p0.z + p1.z) + p2.z) + p3.z,
-                    ((p0.w + p1.w) + p2.w) + p3.w);
-  }
-}
-
-// dw[e] += sum_s ws[s][e] (fixed order); every split reduction of the library goes through here.
-// (ws is consumed: the pre-pass overwrites some of its rows.)
-void launch_split_reduce_kk(const float* ws, int splits, long MN, float* dw, float* db, int KK1, hipStream_t st) {
-  long rs = MN;
-  if (splits > 64 && MN < 65536) {
-    const int groups = (splits + SPLIT_SC - 1) / SPLIT_SC;
-    if ((MN & 3) == 0 && ((uintptr_t)ws & 15) == 0)
-      hipLaunchKernelGGL(split_prereduce4_kernel, dim3((unsigned)((MN + 255) / 256), (unsigned)groups), dim3(256), 0,
-                         st, (float*)ws, splits, MN);
-    else
-      hipLaunchKernelGGL(split_prereduce_kernel, dim3((unsigned)((MN + 63) / 64), (unsigned)groups), dim3(256), 0, st,
-                         (float*)ws, splits, MN);
-    splits = groups;
-    rs = MN * SPLIT_SC;
-  }
-  const bool v4 = KK1 == 0 && (MN & 3) == 0 && (rs & 3) == 0 && (((uintptr_t)ws | (uintptr_t)dw) & 15) == 0;
-  if (v4 && splits <= 8)
-    hipLaunchKernelGGL(split_reduce4_kernel<4>, dim3((unsigned)((MN + 255) / 256)), dim3(256), 0, st, ws, splits, MN, rs, dw);
-  else if (v4)
-    hipLaunchKernelGGL(split_reduce4_kernel<16>, dim3((unsigned)((MN + 63) / 64)), dim3(256), 0, st, ws, splits, MN, rs, dw);
-  else if (splits <= 8)
-    hipLaunchKernelGGL(split_reduce_kernel<4>, dim3((unsigned)((MN + 63) / 64)), dim3(256), 0, st, ws, splits, MN, rs, dw, db, KK1);
-  else
-    hipLaunchKernelGGL(split_reduce_kernel<16>, dim3((unsigned)((MN + 15) / 16)), dim3(256), 0, st, ws, splits, MN, rs, dw, db, KK1);
-}
-void launch_split_reduce(const float* ws, int splits, long MN, float* dw, hipStream_t st) {
-  launch_split_reduce_kk(ws, splits, MN, dw, nullptr, 0, st);
-}
-
-// n reductions dw_i[e] += sum_s ws_i[s][e] (fixed order) in one launch where none needs the pre-pass
-// (each is then exactly its launch_split_reduce body); otherwise one launch each.
-void launch_split_reduce_multi(int n, const float* const* ws, const int* splits, const long* MN, float* const* dw,
-                               hipStream_t st) {
-  RSegs R{};
-  bool ok = n >= 1 && n <= RS_MAX;
-  int b = 0;
-  for (int i = 0; ok && i < n; ++i) {
-    if (splits[i] > 64 && MN[i] < 65536) { ok = false; break; }
-    const bool v4 = (MN[i] & 3) == 0 && ((((uintptr_t)ws[i]) | ((uintptr_t)dw[i])) & 15) == 0;
-    const bool j16 = splits[i] > 8;
-    const int form = (v4 ? 2 : 0) + (j16 ? 1 : 0);
-    const long blocks = v4 ? (j16 ? (MN[i] + 63) / 64 : (MN[i] + 255) / 256) : (j16 ? (MN[i] + 15) / 16 : (MN[i] + 63) / 64);
-    R.s[i] = RSeg{ws[i], dw[i], MN[i], splits[i], form, b};
-    b += (int)blocks;
-  }
-  if (!ok) {
-    for (int i = 0; i < n; ++i) launch_split_reduce(ws[i], splits[i], MN[i], dw[i], st);
-    return;
-  }
-  R.n = n;
-  hipLaunchKernelGGL(split_reduce_multi_kernel, dim3((unsigned)b), dim3(256), 0, st, R);
-}
+// (the split reductions: split_reduce.hip)
 
 static int wgrad_cfg_k(PwArgs& g, bool any_bf16, int* bm) { return wgrad_cfg(g, any_bf16, bm); }
 

@@ -60,6 +60,10 @@ SIGNATURES = {
     "dsgan_mlp_wgrad": [P, L, I, P, L, P, P, P, P, P, P, P, L, I, I, I, I, S],
     "dsgan_mlp_tune": [I, I],
     "dsgan_colsum": [P, I, I, P, S],
+    # split_reduce.hip: deferred split reductions (one batched flush per backward pass)
+    "dsgan_split_defer": [I],
+    "dsgan_split_pending": [],
+    "dsgan_split_flush": [S],
     "dsgan_f32_to_bf16": [P, P, L, S],
     # pconv.hip
     "dsgan_pconv_supported": [I, I, I, I],

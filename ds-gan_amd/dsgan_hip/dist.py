@@ -121,6 +121,7 @@ class GradBuckets:
 
     def _launch(self, i):
         if not self.launched[i]:
+            HF.split_flush()   # the bucket's weight-grads may still sit in the deferred split reductions
             s, e = self.buckets[i][0], self.buckets[i][1]
             self.launched[i] = True
             self.works.append(_allreduce_avg(self.grad[s:e], True))

@@ -22,8 +22,58 @@ from ._lib import call, ptr, stream
 
 def wsa(t):
     """(pointer, element count) of a scratch tensor (None -> NULL, 0): every scratch-taking entry
-    point takes the buffer's size right after it and refuses an undersized one (include/dsgan_hip.h)."""
+    point takes the buffer's size right after it and refuses an undersized one (include/dsgan_hip.h).
+    Inside deferred_splits() the tensor stays referenced until split_flush(): a queued split
+    reduction reads it after the call has returned."""
+    if t is not None and _DEFER_KEEP[0] is not None:
+        _DEFER_KEEP[0].append(t)
     return (ptr(t), t.numel() if t is not None else 0)
+
+
+# Deferred split reductions (split_reduce.hip): inside deferred_splits() every weight-grad launcher
+# queues its fixed-order split reduction (dw += sum_s partials[s]) instead of launching it, and the
+# block's end issues the queue as a few batched launches -- ~160 small reduction launches per
+# training step become a handful.  Only parameter gradients go through these reductions, and they
+# are read only after the backward pass (the optimizer, the non-finite guard) or by the DDP bucket
+# all-reduce, which flushes first (dist.GradBuckets._launch).  The queued scratch buffers (wsa) and
+# scratch outputs (_keep) are held until the flush.
+DEFER_SPLITS = [True]
+_DEFER_KEEP = [None]
+
+
+def _keep(t):
+    if _DEFER_KEEP[0] is not None:
+        _DEFER_KEEP[0].append(t)
+    return t
+
+
+def split_flush():
+    """Launch the queued split reductions (no-op when none are queued)."""
+    lib = _lib.load()
+    if lib.dsgan_split_pending() > 0:
+        call("dsgan_split_flush", stream())
+    if _DEFER_KEEP[0] is not None:
+        _DEFER_KEEP[0] = []
+
+
+@contextlib.contextmanager
+def deferred_splits():
+    """Run a backward pass with its weight-grads' split reductions queued and flushed at the end
+    (nested use is a no-op; DEFER_SPLITS[0] = False turns the batching off)."""
+    if not DEFER_SPLITS[0] or _DEFER_KEEP[0] is not None:
+        yield
+        return
+    lib = _lib.load()
+    _DEFER_KEEP[0] = []
+    lib.dsgan_split_defer(1)
+    try:
+        yield
+    finally:
+        lib.dsgan_split_defer(0)
+        try:
+            split_flush()
+        finally:
+            _DEFER_KEEP[0] = None
 
 
 # PatchGAN 4x4 weight-grads also sum the conv's bias grad from their staged dy tiles
@@ -906,7 +956,7 @@ class PatchStemFn(torch.autograd.Function):
             ws = torch.empty(max(lib.dsgan_pgstem_wgrad_workspace(N, Cin, Cout, H, W), 1), device=dy.device,
                              dtype=torch.float32)
             # a frozen weight with a live bias still runs the weight-grad kernel (into scratch)
-            dwt = gw if gw is not None else torch.zeros_like(w)
+            dwt = gw if gw is not None else _keep(torch.zeros_like(w))
             e0 = IGEMM_TIMER.begin()
             call("dsgan_pgstem_wgrad", ptr(dy), dybs, ptr(y), y[0].numel(), ptr(x), ctx.xbs, ptr(dwt), ptr(gb), N, Cin,
                  Cout, H, W, LRELU_SLOPE, *wsa(ws), stream())

@@ -171,7 +171,8 @@ class Pix2PixModel(BaseModel):
         else:
             self.loss_D = (self.loss_D_fake + self.loss_D_real) * 0.5
         loss = self.loss_D if self.mean_w == 1.0 else self.loss_D * self.mean_w
-        (loss if self.scaler_D is None else self.scaler_D.scale(loss)).backward()
+        with HF.deferred_splits():   # the weight-grads' split reductions: one batched flush at the end
+            (loss if self.scaler_D is None else self.scaler_D.scale(loss)).backward()
 
     def backward_G(self):
         if self.use_gan == 1:
@@ -207,7 +208,8 @@ class Pix2PixModel(BaseModel):
         else:   # ragged global batch under DDP: reweight the batch means, not the TV sum
             loss = ((self.loss_G_GAN * self.w_gan + self.loss_G_L1 + self.loss_vgg * self.w_vgg + self.w_ss * self.loss_ssim)
                     * self.mean_w + self.tv_loss * self.w_tv)
-        (loss if self.scaler_G is None else self.scaler_G.scale(loss)).backward()
+        with HF.deferred_splits():
+            (loss if self.scaler_G is None else self.scaler_G.scale(loss)).backward()
 
     @property
     def loss_ssim(self):

@@ -177,9 +177,21 @@ int dsgan_mlp_wgrad(const void* h, long h_bs, int h_bf16, const float* dy, long 
  * key 0 = the C = 256 backward with g / dz out, 0 LDS-DMA weight ring, 1 register-staged, 2 the ring with
  *         precomputed addresses (default) */
 int dsgan_mlp_tune(int key, int val);
-/* out[c] += sum_r part[r][c], rows added in a fixed order (deterministic); part is scratch and
- * is overwritten (in-place pre-reduction of many rows). */
+/* out[c] += sum_r part[r][c], rows added in a fixed order (deterministic); part is read only. */
 int dsgan_colsum(float* part, int rows, int cols, float* out, hipStream_t stream);
+
+/* ---- deferred split reductions (split_reduce.hip) --------------------------------------------
+ * Every weight-grad entry point finishes with a fixed-order split reduction dw += sum_s partials[s]
+ * of its scratch.  With deferral on, those reductions are queued (scratch pointers and outputs
+ * recorded) instead of launched; dsgan_split_flush issues the queue as a few multi-segment launches
+ * on the stream the producers ran on (segments with overlapping outputs in separate launches, in
+ * queue order) -- the same per-element order of additions as the immediate form.  The caller keeps
+ * every scratch buffer and output of a queued reduction alive, and reads no such output, until the
+ * flush.  Training-loop replacement for the reference's per-layer autograd weight-grad sums
+ * (DSGAN/models/pix2pix_model.py:201-217, loss.backward()). */
+int dsgan_split_defer(int on);        /* returns the previous setting; turning off does not flush */
+int dsgan_split_pending(void);        /* reductions queued */
+int dsgan_split_flush(hipStream_t stream);
 /* dst (bf16) = src (fp32), round to nearest even */
 int dsgan_f32_to_bf16(const float* src, void* dst, long n, hipStream_t stream);
 
