@@ -10,6 +10,7 @@ False (the frozen VGG16, or D during the G step, DSGAN/models/base_model.py:171-
 weight-grad launch at all.
 """
 import contextlib
+import os
 import math
 
 import ctypes
@@ -37,7 +38,7 @@ def wsa(t):
 # are read only after the backward pass (the optimizer, the non-finite guard) or by the DDP bucket
 # all-reduce, which flushes first (dist.GradBuckets._launch).  The queued scratch buffers (wsa) and
 # scratch outputs (_keep) are held until the flush.
-DEFER_SPLITS = [True]
+DEFER_SPLITS = [os.environ.get("DSGAN_DEFER_SPLITS", "1") != "0"]   # (=0: immediate, for A/B runs)
 _DEFER_KEEP = [None]
 
 
