@@ -14,6 +14,8 @@ void launch_split_reduce_kk(const float* ws, int splits, long MN, float* dw, flo
 // and the deferred mode that queues them for one batched flush)
 void launch_split_reduce_multi(int n, const float* const* ws, const int* splits, const long* MN, float* const* dw,
                                hipStream_t st);
+// wconv.hip's weight-grad partials [splits][T][M][C] -> dw[M][C][T] (+=), C % 32 == 0, T <= 16
+void launch_split_reduce_wconv(const float* ws, int splits, int T, int M, int C, float* dw, hipStream_t st);
 
 
 // ---- 16-bit MFMA operand type ------------------------------------------------------------

@@ -31,7 +31,9 @@ struct RSeg {
   float* dw;
   float* db;
   long MN;
-  int S, KK1, form, b0;   // form: bit 0 = 16 lanes (else 4), bit 1 = float4 elements, bit 2 = group rows
+  int S, KK1, form, b0;   // form: bit 0 = 16 lanes (else 4), bit 1 = float4 elements, bit 2 = group rows,
+                          //       bit 3 = wconv layout (bit 4: 4 rows m per workgroup, else 1)
+  int T, M, C;            // wconv layout: partials [S][T][M][C] -> dw [M][C][T]
 };
 constexpr int RS_MAX = 20;
 struct RSegs { RSeg s[RS_MAX]; int n; };
@@ -115,14 +117,67 @@ __device__ __forceinline__ void canon_body(const RSeg& g, int blk, float4* shm) 
   }
 }
 
+// The weight-grad partials of wconv.hip (ConvTranspose 3x3 and PatchGAN 4x4 weight-grads):
+// dW[m][c][t] += sum_s P[s][t][m][c].  Workgroup = MB rows m x 32 channels c: the partial rows are
+// read coalesced along c, the sums go through LDS and leave as the contiguous dw block
+// [m][c0..c0+31][0..T-1] (coalesced read-modify-write, no T-strided scatter).  Per element, the
+// order of additions: 4 running sums over splits s = u mod 4 (the tail splits on sum 0), combined as
+// (s0 + s1) + (s2 + s3).
+template <int MB>
+__device__ __forceinline__ void wc_body(const RSeg& g, int blk, float* sh) {
+  const int T = g.T, M = g.M, C = g.C, splits = g.S;
+  const int cbs = C / 32;
+  const int c0 = (blk % cbs) * 32, m0 = (blk / cbs) * MB;
+  const long plane = (long)M * C, sstride = plane * T;
+  const int n = MB * 32 * T;
+  for (int q = threadIdx.x; q < n; q += 256) {
+    const int c = q & 31, mi = (q >> 5) & (MB - 1), t = q / (32 * MB);
+    const int m = m0 + mi;
+    float r = 0.f;
+    if (m < M) {
+      const float* p = g.ws + (long)t * plane + (long)m * C + c0 + c;
+      float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+      int sp = 0;
+      for (; sp + 16 <= splits; sp += 16) {   // 16 loads in flight, added in the 4-sum order
+        float v[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) v[u] = p[(long)(sp + u) * sstride];
+#pragma unroll
+        for (int u = 0; u < 16; u += 4) { s0 += v[u]; s1 += v[u + 1]; s2 += v[u + 2]; s3 += v[u + 3]; }
+      }
+      for (; sp + 4 <= splits; sp += 4) {
+        s0 += p[(long)sp * sstride]; s1 += p[(long)(sp + 1) * sstride];
+        s2 += p[(long)(sp + 2) * sstride]; s3 += p[(long)(sp + 3) * sstride];
+      }
+      for (; sp < splits; ++sp) s0 += p[(long)sp * sstride];
+      r = (s0 + s1) + (s2 + s3);
+    }
+    sh[(mi * 32 + c) * (T + 1) + t] = r;
+  }
+  __syncthreads();
+  const int rowlen = 32 * T;
+  for (int j = threadIdx.x; j < n; j += 256) {
+    const int mi = j / rowlen, rr = j - mi * rowlen;
+    if (m0 + mi >= M) break;
+    const int c = rr / T, t = rr - c * T;
+    g.dw[((long)(m0 + mi) * C + c0) * T + rr] += sh[(mi * 32 + c) * (T + 1) + t];
+  }
+}
+
 // up to RS_MAX reductions with disjoint outputs: segment i owns blocks [b0[i], b0[i+1])
 __global__ __launch_bounds__(256) void split_canon_kernel(RSegs R) {
-  __shared__ float4 sh[16 * 17];   // >= J * (256 / J + 1) elements of the widest form
+  // >= J * (256 / J + 1) float4 of the widest lane form, 4 x 32 x 17 floats of the wconv form
+  __shared__ float4 sh[4 * 32 * 17 / 4];
   int i = 0;
   for (int q = 1; q < RS_MAX; ++q)
     if (q < R.n && (int)blockIdx.x >= R.s[q].b0) i = q;
   const RSeg g = R.s[i];
   const int blk = blockIdx.x - g.b0;
+  if (g.form & 8) {
+    if (g.form & 16) wc_body<4>(g, blk, reinterpret_cast<float*>(sh));
+    else wc_body<1>(g, blk, reinterpret_cast<float*>(sh));
+    return;
+  }
   switch (g.form & 3) {
     case 3: canon_body<16, true>(g, blk, sh); break;
     case 2: canon_body<4, true>(g, blk, sh); break;
@@ -141,6 +196,7 @@ static RSeg make_seg(const float* ws, int S, long MN, float* dw, float* db, int 
   return s;
 }
 static long seg_blocks(const RSeg& s) {
+  if (s.form & 8) return (long)((s.M + ((s.form & 16) ? 3 : 0)) / ((s.form & 16) ? 4 : 1)) * (s.C / 32);
   const long per = (long)(256 / ((s.form & 1) ? 16 : 4)) * ((s.form & 2) ? 4 : 1);
   return (s.MN + per - 1) / per;
 }
@@ -214,6 +270,14 @@ static void submit(const RSeg* v, int n, hipStream_t st) {
 
 void launch_split_reduce_kk(const float* ws, int splits, long MN, float* dw, float* db, int KK1, hipStream_t st) {
   const RSeg s = make_seg(ws, splits, MN, dw, db, KK1);
+  submit(&s, 1, st);
+}
+// wconv.hip's partial layout [splits][T][M][C] -> dw[M][C][T] (+=), C % 32 == 0, T <= 16
+void launch_split_reduce_wconv(const float* ws, int splits, int T, int M, int C, float* dw, hipStream_t st) {
+  RSeg s{};
+  s.ws = ws; s.dw = dw; s.db = nullptr; s.MN = (long)T * M * C; s.S = splits; s.KK1 = 0;
+  s.T = T; s.M = M; s.C = C;
+  s.form = 8 | ((long)M * (C / 32) >= 4096 ? 16 : 0);
   submit(&s, 1, st);
 }
 void launch_split_reduce(const float* ws, int splits, long MN, float* dw, hipStream_t st) {

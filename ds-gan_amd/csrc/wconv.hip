@@ -19,8 +19,8 @@
 // (kh, kw) of output row r reads plane kw % S of patch row S*r + kh at element shift
 // kw / S + OFF: shift 0 is one aligned 16-byte LDS read, other shifts two reads and a
 // v_alignbit funnel (shifts are compile-time: wave w owns taps w, w+4, ...).
-// Partial sums per split -> workspace [splits][T][M][C]; wconv_reduce sums the splits in a
-// fixed order and accumulates into dW (deterministic, no atomics).
+// Partial sums per split -> workspace [splits][T][M][C]; launch_split_reduce_wconv (split_reduce.hip)
+// sums the splits in a fixed order into dW (deterministic, no atomics; queued in deferred mode).
 #include "common.h"
 #include <type_traits>
 
@@ -289,55 +289,6 @@ __global__ __launch_bounds__(256, XH ? 2 : 1) void wconv_kernel(WcArgs g) {
   }
 }
 
-// dW[m][c][t] += sum_s P[s][t][m][c] (fixed split order: deterministic). Workgroup = 4 rows m x 32
-// channels c: the partial rows are read coalesced along c, the sums go through LDS and leave as the
-// contiguous dw block [m][c0..c0+31][0..T-1] (coalesced read-modify-write, no T-strided scatter).
-// Per element, the order of additions: 4 running sums over splits s = u mod 4 (the tail splits on
-// sum 0), combined as (s0 + s1) + (s2 + s3).
-// (WCR_MB = 4 rows per workgroup for wide problems, 1 for the few-tile / many-split ones.)
-template <int WCR_MB>
-__global__ __launch_bounds__(256) void wconv_reduce_kernel(const float* __restrict__ P, int splits, int T, int M,
-                                                           int C, float* __restrict__ dw) {
-  __shared__ float sh[WCR_MB * 32 * 17];
-  const int cbs = C / WC_BC;
-  const int c0 = (blockIdx.x % cbs) * WC_BC, m0 = (blockIdx.x / cbs) * WCR_MB;
-  const long plane = (long)M * C, sstride = plane * T;
-  const int n = WCR_MB * 32 * T;
-  for (int q = threadIdx.x; q < n; q += 256) {
-    const int c = q & 31, mi = (q >> 5) & (WCR_MB - 1), t = q / (32 * WCR_MB);
-    const int m = m0 + mi;
-    float r = 0.f;
-    if (m < M) {
-      const float* p = P + (long)t * plane + (long)m * C + c0 + c;
-      float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
-      int sp = 0;
-      for (; sp + 16 <= splits; sp += 16) {   // 16 loads in flight, added in the 4-sum order
-        float v[16];
-#pragma unroll
-        for (int u = 0; u < 16; ++u) v[u] = p[(long)(sp + u) * sstride];
-#pragma unroll
-        for (int u = 0; u < 16; u += 4) { s0 += v[u]; s1 += v[u + 1]; s2 += v[u + 2]; s3 += v[u + 3]; }
-      }
-      for (; sp + 4 <= splits; sp += 4) {
-        s0 += p[(long)sp * sstride]; s1 += p[(long)(sp + 1) * sstride];
-        s2 += p[(long)(sp + 2) * sstride]; s3 += p[(long)(sp + 3) * sstride];
-      }
-      for (; sp < splits; ++sp) s0 += p[(long)sp * sstride];
-      r = (s0 + s1) + (s2 + s3);
-    }
-    sh[(mi * 32 + c) * (T + 1) + t] = r;
-  }
-  __syncthreads();
-  const int blk = 32 * T;
-  for (int j = threadIdx.x; j < n; j += 256) {
-    const int mi = j / blk, rr = j - mi * blk;
-    if (m0 + mi >= M) break;
-    const int c = rr / T, t = rr - c * T;
-    float* d = dw + ((long)(m0 + mi) * C + c0) * T + rr;
-    *d += sh[(mi * 32 + c) * (T + 1) + t];
-  }
-}
-
 // fp32 X: one resident workgroup per CU (next block prefetched into registers); 16-bit X (half the
 // staging registers): two, so one workgroup's MFMAs cover the other's block loads.
 constexpr int WC_TARGET_WG = 256, WC_TARGET_WG_XH = 512;
@@ -421,12 +372,8 @@ static int wconv_impl(const float* D, long d_bs, const void* X, long x_bs, bool 
     else wc_launch<T16, 4, 1>(g, grid, xh, st);
   });
   DSG_CHECK_LAUNCH();
-  if ((long)M * (C / WC_BC) >= 4096)
-    hipLaunchKernelGGL(wconv_reduce_kernel<4>, dim3((unsigned)((long)((M + 3) / 4) * (C / WC_BC))), dim3(256), 0, st,
-                       ws, p.splits, KH * KW, M, C, dw);
-  else
-    hipLaunchKernelGGL(wconv_reduce_kernel<1>, dim3((unsigned)((long)M * (C / WC_BC))), dim3(256), 0, st, ws, p.splits,
-                       KH * KW, M, C, dw);
+  // dw[m][c][t] += sum_s P[s][t][m][c] in a fixed order (split_reduce.hip; queued in deferred mode)
+  launch_split_reduce_wconv(ws, p.splits, KH * KW, M, C, dw, st);
   if (db) launch_split_reduce(g.dbp, p.splits, M, db, st);
   DSG_CHECK_LAUNCH();
   return 0;
