@@ -34,7 +34,8 @@ struct PwArgs {
   int gbf;     // FWD: ypre is bf16 and receives act'(pre);  DGRAD: gpre is a bf16 multiplier (no act')
   int gp_pref; // DGRAD with a 16-bit gp multiplier (SWP tiles): load gp before the K loop
   int dbg;     // measurement only (planner knob 10): bit 0 = drop the epilogue's output stores,
-               // bit 1 = the gelu pair without its GELU arithmetic
+               // bit 1 = the gelu pair without its GELU arithmetic; DMA-ring kernels: 4 = no DMA after
+               // the prologue, 8 = no fragment reads / MFMAs, 16 = no epilogue, 32 = no prologue DMA
   int dma;     // host planner: the wide 16-bit-operand launch runs an LDS-DMA ring form: 1 = 256 x 256
                // tiles (8 waves, 4 stages, one workgroup per CU), 2 = 256 x 128 tiles (4 waves, 3 stages,
                // two workgroups per CU: one's epilogue runs beside the other's MFMAs)
