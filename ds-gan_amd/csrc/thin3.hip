@@ -86,12 +86,6 @@ __global__ __launch_bounds__(256) void thin3_fwd_kernel(T3Args a) {
   const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc((void*)a.x, (short)0, a.x_range, 0x00020000);
   const unsigned HW = (unsigned)(a.H * a.W);
   float acc[4][4][MS];
-#pragma unroll
-  for (int r = 0; r < 4; ++r)
-#pragma unroll
-    for (int p = 0; p < 4; ++p)
-#pragma unroll
-      for (int m = 0; m < MS; ++m) acc[r][p][m] = 0.f;
   // the next channel's 6 rows are loaded before this channel's FMAs (one channel in flight)
   T3Row nx[6];
   if (wave < a.K) {
@@ -99,6 +93,15 @@ __global__ __launch_bounds__(256) void thin3_fwd_kernel(T3Args a) {
 #pragma unroll
     for (int i = 0; i < 6; ++i) nx[i] = t3_row_ld(rx, plane, h0 - 1 + i, a.H, a.W, c0, lane);
   }
+  // output rows (r, r + 1) as the two halves of packed FMAs (v_pk_fma_f32, the weight broadcast):
+  // half the FMA instructions, each half the same fmaf chain as the scalar form (same bits)
+  f32x2 acc2[2][4][MS];
+#pragma unroll
+  for (int q = 0; q < 2; ++q)
+#pragma unroll
+    for (int p = 0; p < 4; ++p)
+#pragma unroll
+      for (int m = 0; m < MS; ++m) acc2[q][p][m] = f32x2{0.f, 0.f};
   for (int k = wave; k < a.K; k += 4) {
     float in[6][6];
 #pragma unroll
@@ -108,20 +111,35 @@ __global__ __launch_bounds__(256) void thin3_fwd_kernel(T3Args a) {
 #pragma unroll
       for (int i = 0; i < 6; ++i) nx[i] = t3_row_ld(rx, plane, h0 - 1 + i, a.H, a.W, c0, lane);
     }
+    f32x2 in2[5][6];   // rows (i, i + 1) of each column
+#pragma unroll
+    for (int i = 0; i < 5; ++i)
+#pragma unroll
+      for (int j = 0; j < 6; ++j) in2[i][j] = f32x2{in[i][j], in[i + 1][j]};
     float wv[MS][9];
 #pragma unroll
     for (int m = 0; m < MS; ++m)
 #pragma unroll
       for (int t = 0; t < 9; ++t) wv[m][t] = a.w[((long)m * a.K + k) * 9 + t];
 #pragma unroll
-    for (int r = 0; r < 4; ++r)
+    for (int q = 0; q < 2; ++q)
 #pragma unroll
       for (int p = 0; p < 4; ++p)
 #pragma unroll
         for (int t = 0; t < 9; ++t)
 #pragma unroll
-          for (int m = 0; m < MS; ++m) acc[r][p][m] = fmaf(wv[m][t], in[r + t / 3][p + t % 3], acc[r][p][m]);
+          for (int m = 0; m < MS; ++m)
+            acc2[q][p][m] = pk_fma(f32x2{wv[m][t], wv[m][t]}, in2[2 * q + t / 3][p + t % 3], acc2[q][p][m]);
   }
+#pragma unroll
+  for (int q = 0; q < 2; ++q)
+#pragma unroll
+    for (int p = 0; p < 4; ++p)
+#pragma unroll
+      for (int m = 0; m < MS; ++m) {
+        acc[2 * q][p][m] = acc2[q][p][m].x;
+        acc[2 * q + 1][p][m] = acc2[q][p][m].y;
+      }
   if (wave > 0) {
 #pragma unroll
     for (int r = 0; r < 4; ++r)
