@@ -14,6 +14,8 @@ void launch_split_reduce_kk(const float* ws, int splits, long MN, float* dw, flo
 // and the deferred mode that queues them for one batched flush)
 void launch_split_reduce_multi(int n, const float* const* ws, const int* splits, const long* MN, float* const* dw,
                                hipStream_t st);
+// out[0] = coef * sum_i part[i], i = 0..n-1 in a fixed order (losses.hip: the loss reductions' last pass)
+void launch_final_sum(const float* part, int n, float coef, float* out, hipStream_t st);
 // wconv.hip's weight-grad partials [splits][T][M][C] -> dw[M][C][T] (+=), C % 32 == 0, T <= 16
 void launch_split_reduce_wconv(const float* ws, int splits, int T, int M, int C, float* dw, hipStream_t st);
 

@@ -98,6 +98,10 @@ __global__ __launch_bounds__(256) void final_sum_kernel(const float* __restrict_
   if (threadIdx.x == 0) out[0] = s * coef;
 }
 
+void launch_final_sum(const float* part, int n, float coef, float* out, hipStream_t st) {
+  hipLaunchKernelGGL(final_sum_kernel, dim3(1), dim3(256), 0, st, part, n, coef, out);
+}
+
 // stats[p][j] = sum over the tiles t of part[p][t][j], j in {0, 1} (fixed order)
 __global__ void plane_tile_sum_kernel(const float* __restrict__ part, int planes, int tiles, float* __restrict__ stats) {
   const int t = blockIdx.x * 256 + threadIdx.x;

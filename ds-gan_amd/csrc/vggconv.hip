@@ -609,15 +609,26 @@ __global__ __launch_bounds__(256) void vgg_conv1_dgrad_rows_kernel(const T16* __
 
 // MaxPool2d(2) of an fp32 CB16 feature -> bf16 CB16 + window argmax (dh*2 + dw, first max wins as
 // in torch).  Thread = (output pixel, 4 channels).
-template <typename T16>
+// L1: also the perceptual L1 of the pooled feature against the real image's feature rf (same CB16
+// fp32 layout) from the same read of x: per workgroup sum of |x - rf| over its threads' 2 x 2 x 4
+// values (in window order) -> part[blockIdx.x], summed in order by final_sum_kernel.
+template <typename T16, bool L1 = false>
 __global__ __launch_bounds__(256) void cb16_maxpool_kernel(const float* __restrict__ x, T16* __restrict__ y,
-                                                           unsigned char* __restrict__ idx, int N, int C, int H, int W) {
+                                                           unsigned char* __restrict__ idx, int N, int C, int H, int W,
+                                                           const float* __restrict__ rf = nullptr,
+                                                           float* __restrict__ part = nullptr) {
   typedef hx8<T16> vgb8;
   typedef hx4<T16> vgb4;
   const int Ho = H >> 1, Wo = W >> 1;
   const long total = (long)N * (C >> 2) * Ho * Wo;
-  const long t = blockIdx.x * 256L + threadIdx.x;
-  if (t >= total) return;
+  long t = blockIdx.x * 256L + threadIdx.x;
+  float l1 = 0.f;
+  if constexpr (L1) {
+    if (t >= total) t = -1;   // (every thread reaches the block sum)
+  } else if (t >= total) {
+    return;
+  }
+  if (t >= 0) {
   // t -> (n, cblock, c4 (0..3), oh, ow) with ow fastest after c4 groups of one block
   const int q = (int)(t & 3);                 // 4-channel group inside the 16-channel block
   long r = t >> 2;
@@ -631,8 +642,13 @@ __global__ __launch_bounds__(256) void cb16_maxpool_kernel(const float* __restri
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     const int dh = k >> 1, dw = k & 1;
-    const float4 v = *reinterpret_cast<const float4*>(x + cb16(n, c, 2 * oh + dh, 2 * ow + dw, C, H, W));
+    const long xo = cb16(n, c, 2 * oh + dh, 2 * ow + dw, C, H, W);
+    const float4 v = *reinterpret_cast<const float4*>(x + xo);
     const float a[4] = {v.x, v.y, v.z, v.w};
+    if constexpr (L1) {
+      const float4 u = *reinterpret_cast<const float4*>(rf + xo);
+      l1 += ((fabsf(v.x - u.x) + fabsf(v.y - u.y)) + (fabsf(v.z - u.z) + fabsf(v.w - u.w)));
+    }
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       if (k == 0 || a[e] > best[e]) { best[e] = a[e]; bi[e] = k; }
@@ -645,6 +661,12 @@ __global__ __launch_bounds__(256) void cb16_maxpool_kernel(const float* __restri
   for (int e = 0; e < 4; ++e) { b[e] = (T16)best[e]; ix[e] = (unsigned char)bi[e]; }
   *reinterpret_cast<vgb4*>(y + o) = b;
   *reinterpret_cast<vgc4*>(idx + o) = ix;
+  }
+  if constexpr (L1) {
+    __shared__ float sh[4];
+    const float s = block_sum<256>(l1, sh);
+    if (threadIdx.x == 0) part[blockIdx.x] = s;
+  }
 }
 
 // Gradient at the pre-ReLU output of a tapped conv (f = its fp32 output, r = the real image's):
@@ -861,6 +883,32 @@ int dsgan_cb16_maxpool(const float* x, void* y, void* idx, int N, int C, int H, 
     hipLaunchKernelGGL((cb16_maxpool_kernel<T16>), dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, x,
                        (T16*)y, (unsigned char*)idx, N, C, H, W);
   });
+  DSG_CHECK_LAUNCH();
+  return 0;
+}
+
+// workgroup partials of dsgan_cb16_maxpool_l1 (floats of its `part` scratch)
+long dsgan_cb16_maxpool_l1_parts(int N, int C, int H, int W) {
+  return ((long)N * (C / 4) * (H / 2) * (W / 2) + 255) / 256;
+}
+
+// dsgan_cb16_maxpool, plus out[0] = mean |x - r| over the whole feature (the perceptual L1 of that
+// tap, DSGAN/models/pix2pix_model.py:182-186 over vgg.py's relu features) from the same read of x;
+// r = the real image's feature, same CB16 fp32 layout.  Deterministic: workgroup partials summed in
+// a fixed order.
+int dsgan_cb16_maxpool_l1(const float* x, const float* r, void* y, void* idx, float* out, float* part, long part_elems,
+                          int N, int C, int H, int W, hipStream_t st) {
+  DSG_REQUIRE(x && r && y && idx && out && C % 16 == 0 && H % 2 == 0 && W % 2 == 0, "dsgan_cb16_maxpool_l1: bad args");
+  const long blocks = dsgan_cb16_maxpool_l1_parts(N, C, H, W);
+  DSG_WS(blocks, part, part_elems, "dsgan_cb16_maxpool_l1 (dsgan_cb16_maxpool_l1_parts)");
+  DSG_REQUIRE(blocks < (1L << 31), "dsgan_cb16_maxpool_l1: feature too large");
+  with_half([&](auto* t_) {
+    using T16 = std::remove_pointer_t<decltype(t_)>;
+    hipLaunchKernelGGL((cb16_maxpool_kernel<T16, true>), dim3((unsigned)blocks), dim3(256), 0, st, x, (T16*)y,
+                       (unsigned char*)idx, N, C, H, W, r, part);
+  });
+  DSG_CHECK_LAUNCH();
+  launch_final_sum(part, (int)blocks, 1.f / ((float)N * C * H * W), out, st);
   DSG_CHECK_LAUNCH();
   return 0;
 }

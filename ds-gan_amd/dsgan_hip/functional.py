@@ -1849,9 +1849,11 @@ def _vconv(x, wt, bias, mask, y, N, K, M, H, W, relu, tag):
     return y
 
 
-def vgg_features_cb16(x, blocks, keep=False):
+def vgg_features_cb16(x, blocks, keep=False, real=None, outs=None):
     """relu1_2..relu4_3 of x (NCHW fp32) as fp32 CB16 tensors; with keep, also per block (pool
-    argmax or None, [bf16 CB16 outputs of the block's convs below the tapped one]) for the backward."""
+    argmax or None, [bf16 CB16 outputs of the block's convs below the tapped one]) for the backward.
+    real / outs: the real image's features -- every tap that is max-pooled also gets its perceptual
+    L1 mean |f - real| into outs[tap] from the pool's read of f (dsgan_cb16_maxpool_l1)."""
     x, xbs = nchw(x)
     N, _, H, W = x.shape
     feats, saved = [], []
@@ -1864,7 +1866,14 @@ def vgg_features_cb16(x, blocks, keep=False):
             H, W = H // 2, W // 2
             h = _cb16_empty(N, C, H, W, x, half_dtype())
             idx = torch.empty(h.shape, device=x.device, dtype=torch.uint8)
-            call("dsgan_cb16_maxpool", ptr(f), ptr(h), ptr(idx), N, C, 2 * H, 2 * W, stream())
+            if real is not None:
+                tap = len(feats) - 1
+                part = torch.empty(_lib.load().dsgan_cb16_maxpool_l1_parts(N, C, 2 * H, 2 * W), device=x.device,
+                                   dtype=torch.float32)
+                call("dsgan_cb16_maxpool_l1", ptr(f), ptr(real[tap]), ptr(h), ptr(idx), ptr(outs[tap:]), *wsa(part),
+                     N, C, 2 * H, 2 * W, stream())
+            else:
+                call("dsgan_cb16_maxpool", ptr(f), ptr(h), ptr(idx), N, C, 2 * H, 2 * W, stream())
         acts = []
         for li, (w, b) in enumerate(convs):
             last = li == len(convs) - 1
@@ -1920,6 +1929,11 @@ def _sum4_raw(outs):
     return out
 
 
+# the perceptual L1 of each max-pooled VGG tap from the pool's read of it (dsgan_cb16_maxpool_l1);
+# DSGAN_VGG_POOL_L1=0: the separate L1 pass (A/B runs)
+VGG_POOL_L1 = [os.environ.get("DSGAN_VGG_POOL_L1", "1") != "0"]
+
+
 class PerceptualL1Fn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, fake, blocks, real_feats):
@@ -1927,9 +1941,13 @@ class PerceptualL1Fn(torch.autograd.Function):
         fake, _ = nchw(fake)
         ctx.cb16 = real_feats[0].dim() == 5
         if ctx.cb16:
-            feats, saved = vgg_features_cb16(fake, blocks, keep=True)
+            # the L1 of every tap that is max-pooled comes from the pool's read of it; the others here
             outs = torch.empty(4, device=fake.device, dtype=torch.float32)
+            fuse = VGG_POOL_L1[0]
+            feats, saved = vgg_features_cb16(fake, blocks, keep=True, real=real_feats if fuse else None, outs=outs)
             for i, (f, r) in enumerate(zip(feats, real_feats)):
+                if fuse and i + 1 < len(blocks) and blocks[i + 1][0]:
+                    continue
                 call("dsgan_l1_fwd", ptr(f), ptr(r), f.numel(), ptr(outs[i:]), ptr(_loss_part(f)), stream())
             ctx.blocks, ctx.saved, ctx.real, ctx.feats = blocks, saved, real_feats, feats
             ctx.fake_shape = tuple(fake.shape)

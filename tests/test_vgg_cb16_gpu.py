@@ -139,6 +139,41 @@ def test_conv1_forward_and_dgrad(half, N, H, W):
 
 
 @pytest.mark.parametrize("half", HALVES)
+@pytest.mark.parametrize("shape", [(2, 32, 16, 24), (3, 48, 34, 18), (1, 16, 2, 2)])
+def test_maxpool_l1_fused(half, shape):
+    """dsgan_cb16_maxpool_l1: the same pooled values and argmax bits as dsgan_cb16_maxpool, and the
+    tap's perceptual L1 mean |f - r| (from the pool's read of f) against float64; a ragged last
+    workgroup (thread count not a multiple of 256) included."""
+    HT = _hdt(half)
+    from dsgan_hip import functional as HF_
+    HF_.set_precision(half)
+    _hf()
+    from dsgan_hip._lib import call, ptr, stream, load
+    g = torch.Generator().manual_seed(11)
+    N, C, H, W = shape
+    f = torch.relu(torch.randn(N, C, H, W, generator=g))
+    f[:, :, ::3, ::2] = 0.0
+    r = torch.relu(torch.randn(N, C, H, W, generator=g))
+    fd, rd = to_cb16(f).cuda(), to_cb16(r).cuda()
+    y0 = torch.empty((N, C // 16, H // 2, W // 2, 16), device="cuda", dtype=HT)
+    i0 = torch.empty(y0.shape, device="cuda", dtype=torch.uint8)
+    call("dsgan_cb16_maxpool", ptr(fd), ptr(y0), ptr(i0), N, C, H, W, stream())
+    y1, i1 = torch.empty_like(y0), torch.empty_like(i0)
+    part = torch.empty(load().dsgan_cb16_maxpool_l1_parts(N, C, H, W), device="cuda")
+    out = torch.full((2,), -1.0, device="cuda")
+    call("dsgan_cb16_maxpool_l1", ptr(fd), ptr(rd), ptr(y1), ptr(i1), ptr(out), ptr(part), part.numel(), N, C, H, W,
+         stream())
+    torch.cuda.synchronize()
+    assert torch.equal(y0.cpu(), y1.cpu()) and torch.equal(i0.cpu(), i1.cpu())
+    ref = (f.double() - r.double()).abs().mean().item()
+    assert abs(out[0].item() - ref) <= 2e-6 * ref, (out[0].item(), ref)
+    assert out[1].item() == -1.0   # one scalar written
+    with pytest.raises(RuntimeError):   # undersized partial scratch is refused
+        call("dsgan_cb16_maxpool_l1", ptr(fd), ptr(rd), ptr(y1), ptr(i1), ptr(out), ptr(part), part.numel() - 1, N,
+             C, H, W, stream())
+
+
+@pytest.mark.parametrize("half", HALVES)
 def test_maxpool_and_tap_bwd(half):
     """MaxPool2d(2) value + window argmax (first max wins, as torch) and the tapped-layer
     backward (maxpool backward + L1 backward) * ReLU' against torch autograd."""
