@@ -612,11 +612,14 @@ __global__ __launch_bounds__(256) void vgg_conv1_dgrad_rows_kernel(const T16* __
 // L1: also the perceptual L1 of the pooled feature against the real image's feature rf (same CB16
 // fp32 layout) from the same read of x: per workgroup sum of |x - rf| over its threads' 2 x 2 x 4
 // values (in window order) -> part[blockIdx.x], summed in order by final_sum_kernel.
+// codes (L1 form, nullable): per element of x one byte, bit 0 = (x > 0), bit 1 = (x > rf),
+// bit 2 = (x < rf) -- all the tap's backward needs of x and rf (cb16_tap_bwd_code_kernel).
 template <typename T16, bool L1 = false>
 __global__ __launch_bounds__(256) void cb16_maxpool_kernel(const float* __restrict__ x, T16* __restrict__ y,
                                                            unsigned char* __restrict__ idx, int N, int C, int H, int W,
                                                            const float* __restrict__ rf = nullptr,
-                                                           float* __restrict__ part = nullptr) {
+                                                           float* __restrict__ part = nullptr,
+                                                           unsigned char* __restrict__ codes = nullptr) {
   typedef hx8<T16> vgb8;
   typedef hx4<T16> vgb4;
   const int Ho = H >> 1, Wo = W >> 1;
@@ -648,6 +651,14 @@ __global__ __launch_bounds__(256) void cb16_maxpool_kernel(const float* __restri
     if constexpr (L1) {
       const float4 u = *reinterpret_cast<const float4*>(rf + xo);
       l1 += ((fabsf(v.x - u.x) + fabsf(v.y - u.y)) + (fabsf(v.z - u.z) + fabsf(v.w - u.w)));
+      if (codes) {
+        const float ua[4] = {u.x, u.y, u.z, u.w};
+        vgc4 cd;
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          cd[e] = (unsigned char)((a[e] > 0.f ? 1 : 0) | (a[e] > ua[e] ? 2 : 0) | (a[e] < ua[e] ? 4 : 0));
+        *reinterpret_cast<vgc4*>(codes + xo) = cd;
+      }
     }
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
@@ -717,6 +728,47 @@ __global__ __launch_bounds__(256) void cb16_tap_bwd_kernel(const T16* __restrict
       out[e] = (T16)(fa[e] > 0.f ? v : 0.f);
     }
     *reinterpret_cast<vgb4*>(d + o) = out;
+  }
+}
+
+// The same gradient from the forward's per-element codes (cb16_maxpool_kernel L1 form) instead of
+// f and r: 1 byte per element read instead of 8.  Same values: the codes hold exactly the sign of
+// f - r and the ReLU mask f > 0.
+template <typename T16>
+__global__ __launch_bounds__(256) void cb16_tap_bwd_code_kernel(const T16* __restrict__ dpool,
+                                                                const unsigned char* __restrict__ idx,
+                                                                const unsigned char* __restrict__ codes,
+                                                                T16* __restrict__ d, int N, int C, int H, int W,
+                                                                const float* __restrict__ gout, float coef) {
+  typedef hx4<T16> vgb4;
+  const int Ho = H >> 1, Wo = W >> 1;
+  const long total = (long)N * (C >> 2) * Ho * Wo;
+  const long t = blockIdx.x * 256L + threadIdx.x;
+  if (t >= total) return;
+  const int q = (int)(t & 3);
+  long r = t >> 2;
+  const int ow = (int)(r % Wo); r /= Wo;
+  const int oh = (int)(r % Ho); r /= Ho;
+  const int cbk = (int)(r % (C >> 4));
+  const int n = (int)(r / (C >> 4));
+  const int c = cbk * 16 + q * 4;
+  const float g = gout[0] * coef;
+  const long o = cb16(n, c, oh, ow, C, Ho, Wo);
+  const vgb4 u = *reinterpret_cast<const vgb4*>(dpool + o);
+  const vgc4 ix = *reinterpret_cast<const vgc4*>(idx + o);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int h = 2 * oh + (k >> 1), w = 2 * ow + (k & 1);
+    const long p = cb16(n, c, h, w, C, H, W);
+    const vgc4 cd = *reinterpret_cast<const vgc4*>(codes + p);
+    vgb4 out;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float v = (cd[e] & 2) ? g : ((cd[e] & 4) ? -g : 0.f);
+      if ((int)ix[e] == k) v += (float)u[e];
+      out[e] = (T16)((cd[e] & 1) ? v : 0.f);
+    }
+    *reinterpret_cast<vgb4*>(d + p) = out;
   }
 }
 
@@ -895,9 +947,10 @@ long dsgan_cb16_maxpool_l1_parts(int N, int C, int H, int W) {
 // dsgan_cb16_maxpool, plus out[0] = mean |x - r| over the whole feature (the perceptual L1 of that
 // tap, DSGAN/models/pix2pix_model.py:182-186 over vgg.py's relu features) from the same read of x;
 // r = the real image's feature, same CB16 fp32 layout.  Deterministic: workgroup partials summed in
-// a fixed order.
-int dsgan_cb16_maxpool_l1(const float* x, const float* r, void* y, void* idx, float* out, float* part, long part_elems,
-                          int N, int C, int H, int W, hipStream_t st) {
+// a fixed order.  codes (nullable, 1 byte per element of x, CB16): what dsgan_cb16_tap_bwd_codes
+// needs of x and r.
+int dsgan_cb16_maxpool_l1(const float* x, const float* r, void* y, void* idx, void* codes, float* out, float* part,
+                          long part_elems, int N, int C, int H, int W, hipStream_t st) {
   DSG_REQUIRE(x && r && y && idx && out && C % 16 == 0 && H % 2 == 0 && W % 2 == 0, "dsgan_cb16_maxpool_l1: bad args");
   const long blocks = dsgan_cb16_maxpool_l1_parts(N, C, H, W);
   DSG_WS(blocks, part, part_elems, "dsgan_cb16_maxpool_l1 (dsgan_cb16_maxpool_l1_parts)");
@@ -905,10 +958,27 @@ int dsgan_cb16_maxpool_l1(const float* x, const float* r, void* y, void* idx, fl
   with_half([&](auto* t_) {
     using T16 = std::remove_pointer_t<decltype(t_)>;
     hipLaunchKernelGGL((cb16_maxpool_kernel<T16, true>), dim3((unsigned)blocks), dim3(256), 0, st, x, (T16*)y,
-                       (unsigned char*)idx, N, C, H, W, r, part);
+                       (unsigned char*)idx, N, C, H, W, r, part, (unsigned char*)codes);
   });
   DSG_CHECK_LAUNCH();
   launch_final_sum(part, (int)blocks, 1.f / ((float)N * C * H * W), out, st);
+  DSG_CHECK_LAUNCH();
+  return 0;
+}
+
+// dsgan_cb16_tap_bwd of a pooled tap from dsgan_cb16_maxpool_l1's codes instead of f and r
+int dsgan_cb16_tap_bwd_codes(const void* dpool, const void* idx, const void* codes, void* d, int N, int C, int H, int W,
+                             const float* gout, hipStream_t st) {
+  DSG_REQUIRE(dpool && idx && codes && d && gout && C % 16 == 0 && H % 2 == 0 && W % 2 == 0,
+              "dsgan_cb16_tap_bwd_codes: bad args");
+  const long total = (long)N * (C / 4) * (H / 2) * (W / 2);
+  const float coef = 1.f / ((float)N * C * H * W);
+  with_half([&](auto* t_) {
+    using T16 = std::remove_pointer_t<decltype(t_)>;
+    hipLaunchKernelGGL((cb16_tap_bwd_code_kernel<T16>), dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st,
+                       (const T16*)dpool, (const unsigned char*)idx, (const unsigned char*)codes, (T16*)d, N, C, H, W,
+                       gout, coef);
+  });
   DSG_CHECK_LAUNCH();
   return 0;
 }

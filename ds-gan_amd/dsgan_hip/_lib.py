@@ -173,7 +173,8 @@ SIGNATURES = {
     "dsgan_vgg_conv1_fwd": [P, L, P, P, P, I, I, I, S],
     "dsgan_vgg_conv1_dgrad": [P, P, P, L, I, I, I, S],
     "dsgan_cb16_maxpool": [P, P, P, I, I, I, I, S],
-    "dsgan_cb16_maxpool_l1": [P, P, P, P, P, P, L, I, I, I, I, S],
+    "dsgan_cb16_maxpool_l1": [P, P, P, P, P, P, P, L, I, I, I, I, S],
+    "dsgan_cb16_tap_bwd_codes": [P, P, P, P, I, I, I, I, P, S],
     "dsgan_cb16_maxpool_l1_parts": [I, I, I, I],
     "dsgan_cb16_tap_bwd": [P, P, P, P, P, I, I, I, I, P, S],
     # adam.hip

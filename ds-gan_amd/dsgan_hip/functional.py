@@ -1849,11 +1849,12 @@ def _vconv(x, wt, bias, mask, y, N, K, M, H, W, relu, tag):
     return y
 
 
-def vgg_features_cb16(x, blocks, keep=False, real=None, outs=None):
+def vgg_features_cb16(x, blocks, keep=False, real=None, outs=None, codes=None):
     """relu1_2..relu4_3 of x (NCHW fp32) as fp32 CB16 tensors; with keep, also per block (pool
     argmax or None, [bf16 CB16 outputs of the block's convs below the tapped one]) for the backward.
     real / outs: the real image's features -- every tap that is max-pooled also gets its perceptual
-    L1 mean |f - real| into outs[tap] from the pool's read of f (dsgan_cb16_maxpool_l1)."""
+    L1 mean |f - real| into outs[tap] from the pool's read of f (dsgan_cb16_maxpool_l1), and with a
+    `codes` dict its backward's per-element codes (sign(f - real), f > 0) in codes[tap]."""
     x, xbs = nchw(x)
     N, _, H, W = x.shape
     feats, saved = [], []
@@ -1870,8 +1871,12 @@ def vgg_features_cb16(x, blocks, keep=False, real=None, outs=None):
                 tap = len(feats) - 1
                 part = torch.empty(_lib.load().dsgan_cb16_maxpool_l1_parts(N, C, 2 * H, 2 * W), device=x.device,
                                    dtype=torch.float32)
-                call("dsgan_cb16_maxpool_l1", ptr(f), ptr(real[tap]), ptr(h), ptr(idx), ptr(outs[tap:]), *wsa(part),
-                     N, C, 2 * H, 2 * W, stream())
+                cd = None
+                if codes is not None:
+                    cd = torch.empty(f.shape, device=x.device, dtype=torch.uint8)
+                    codes[tap] = cd
+                call("dsgan_cb16_maxpool_l1", ptr(f), ptr(real[tap]), ptr(h), ptr(idx), ptr(cd), ptr(outs[tap:]),
+                     *wsa(part), N, C, 2 * H, 2 * W, stream())
             else:
                 call("dsgan_cb16_maxpool", ptr(f), ptr(h), ptr(idx), N, C, 2 * H, 2 * W, stream())
         acts = []
@@ -1900,17 +1905,22 @@ def _perceptual_bwd_cb16(ctx, g):
         pool, convs = ctx.blocks[bi]
         idx, acts = ctx.saved[bi]
         f, r = ctx.feats[bi], ctx.real[bi]
-        N, Cb, H, W, _ = f.shape
-        dpre = _cb16_empty(N, Cb * 16, H, W, f, half_dtype())
-        call("dsgan_cb16_tap_bwd", ptr(d), ptr(d_idx), ptr(f), ptr(r), ptr(dpre), N, Cb * 16, H, W, ptr(g), stream())
+        N, Cb, H, W, _ = r.shape
+        dpre = _cb16_empty(N, Cb * 16, H, W, r, half_dtype())
+        if bi in ctx.codes:
+            call("dsgan_cb16_tap_bwd_codes", ptr(d), ptr(d_idx), ptr(ctx.codes[bi]), ptr(dpre), N, Cb * 16, H, W, ptr(g),
+                 stream())
+        else:
+            call("dsgan_cb16_tap_bwd", ptr(d), ptr(d_idx), ptr(f), ptr(r), ptr(dpre), N, Cb * 16, H, W, ptr(g),
+                 stream())
         for li in range(len(convs) - 1, -1, -1):
             w = convs[li][0]
             Co, Ci = w.shape[0], w.shape[1]
             if bi == 0 and li == 0:
-                dx = torch.empty(ctx.fake_shape, device=f.device, dtype=torch.float32)
+                dx = torch.empty(ctx.fake_shape, device=r.device, dtype=torch.float32)
                 call("dsgan_vgg_conv1_dgrad", ptr(dpre), ptr(w), ptr(dx), Ci * H * W, N, H, W, stream())
             else:
-                out = _cb16_empty(N, Ci, H, W, f, half_dtype())
+                out = _cb16_empty(N, Ci, H, W, r, half_dtype())
                 _vconv(dpre, _vgg_wt(w, 1), None, acts[li - 1] if li > 0 else None, out, N, Co, Ci, H, W, False, "dgrad")
                 dpre = out
         d, d_idx = dpre, idx
@@ -1944,12 +1954,16 @@ class PerceptualL1Fn(torch.autograd.Function):
             # the L1 of every tap that is max-pooled comes from the pool's read of it; the others here
             outs = torch.empty(4, device=fake.device, dtype=torch.float32)
             fuse = VGG_POOL_L1[0]
-            feats, saved = vgg_features_cb16(fake, blocks, keep=True, real=real_feats if fuse else None, outs=outs)
+            codes = {}
+            feats, saved = vgg_features_cb16(fake, blocks, keep=True, real=real_feats if fuse else None, outs=outs,
+                                             codes=codes)
             for i, (f, r) in enumerate(zip(feats, real_feats)):
-                if fuse and i + 1 < len(blocks) and blocks[i + 1][0]:
+                if i in codes:
                     continue
                 call("dsgan_l1_fwd", ptr(f), ptr(r), f.numel(), ptr(outs[i:]), ptr(_loss_part(f)), stream())
-            ctx.blocks, ctx.saved, ctx.real, ctx.feats = blocks, saved, real_feats, feats
+            # a tap with codes needs neither its feature nor the real one in the backward
+            feats = [None if i in codes else t for i, t in enumerate(feats)]
+            ctx.blocks, ctx.saved, ctx.real, ctx.feats, ctx.codes = blocks, saved, real_feats, feats, codes
             ctx.fake_shape = tuple(fake.shape)
             ctx.prec = _state["prec"]
             return _sum4_raw(outs)
@@ -1967,7 +1981,7 @@ class PerceptualL1Fn(torch.autograd.Function):
         if ctx.cb16:
             with precision(ctx.prec):
                 dx = _perceptual_bwd_cb16(ctx, g.contiguous())
-            ctx.saved = ctx.real = ctx.feats = None
+            ctx.saved = ctx.real = ctx.feats = ctx.codes = None
             return _give(ctx.box, dx), None, None
         with precision(ctx.prec):
             g = g.contiguous()

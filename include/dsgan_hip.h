@@ -591,10 +591,14 @@ int dsgan_vgg_conv1_dgrad(const void* d, const float* w, float* dx, long dx_bs, 
 int dsgan_cb16_maxpool(const float* x, void* y, void* idx, int N, int C, int H, int W, hipStream_t stream);
 /* dsgan_cb16_maxpool plus out[0] = mean |x - r| over the whole feature (the perceptual L1 of that
  * tap, DSGAN/models/pix2pix_model.py:182-186) from the same read of x; r = the real image's feature
- * (same CB16 fp32 layout); part: >= dsgan_cb16_maxpool_l1_parts floats of scratch */
+ * (same CB16 fp32 layout); part: >= dsgan_cb16_maxpool_l1_parts floats of scratch; codes (nullable):
+ * one byte per element of x (bit 0 = x > 0, bit 1 = x > r, bit 2 = x < r) for dsgan_cb16_tap_bwd_codes */
 long dsgan_cb16_maxpool_l1_parts(int N, int C, int H, int W);
-int dsgan_cb16_maxpool_l1(const float* x, const float* r, void* y, void* idx, float* out, float* part,
+int dsgan_cb16_maxpool_l1(const float* x, const float* r, void* y, void* idx, void* codes, float* out, float* part,
                           long part_elems, int N, int C, int H, int W, hipStream_t stream);
+/* dsgan_cb16_tap_bwd of a pooled tap (dpool, idx required) from those codes instead of f and r */
+int dsgan_cb16_tap_bwd_codes(const void* dpool, const void* idx, const void* codes, void* d, int N, int C, int H,
+                             int W, const float* gout, hipStream_t stream);
 int dsgan_cb16_tap_bwd(const void* dpool, const void* idx, const float* f, const float* r, void* d, int N, int C,
                        int H, int W, const float* gout, hipStream_t stream);
 

@@ -161,16 +161,27 @@ def test_maxpool_l1_fused(half, shape):
     y1, i1 = torch.empty_like(y0), torch.empty_like(i0)
     part = torch.empty(load().dsgan_cb16_maxpool_l1_parts(N, C, H, W), device="cuda")
     out = torch.full((2,), -1.0, device="cuda")
-    call("dsgan_cb16_maxpool_l1", ptr(fd), ptr(rd), ptr(y1), ptr(i1), ptr(out), ptr(part), part.numel(), N, C, H, W,
-         stream())
+    codes = torch.empty(fd.shape, device="cuda", dtype=torch.uint8)
+    call("dsgan_cb16_maxpool_l1", ptr(fd), ptr(rd), ptr(y1), ptr(i1), ptr(codes), ptr(out), ptr(part), part.numel(),
+         N, C, H, W, stream())
     torch.cuda.synchronize()
     assert torch.equal(y0.cpu(), y1.cpu()) and torch.equal(i0.cpu(), i1.cpu())
     ref = (f.double() - r.double()).abs().mean().item()
     assert abs(out[0].item() - ref) <= 2e-6 * ref, (out[0].item(), ref)
     assert out[1].item() == -1.0   # one scalar written
     with pytest.raises(RuntimeError):   # undersized partial scratch is refused
-        call("dsgan_cb16_maxpool_l1", ptr(fd), ptr(rd), ptr(y1), ptr(i1), ptr(out), ptr(part), part.numel() - 1, N,
-             C, H, W, stream())
+        call("dsgan_cb16_maxpool_l1", ptr(fd), ptr(rd), ptr(y1), ptr(i1), None, ptr(out), ptr(part), part.numel() - 1,
+             N, C, H, W, stream())
+    # the tap backward from the codes = the one from f and r, bit for bit
+    dpool = (torch.randn(N, C, H // 2, W // 2, generator=g) * 1e-3)
+    dpd = to_cb16(dpool).cuda().to(HT)
+    gsc = torch.tensor([0.75], device="cuda")
+    d0 = torch.empty(fd.shape, device="cuda", dtype=HT)
+    d1 = torch.empty_like(d0)
+    call("dsgan_cb16_tap_bwd", ptr(dpd), ptr(i0), ptr(fd), ptr(rd), ptr(d0), N, C, H, W, ptr(gsc), stream())
+    call("dsgan_cb16_tap_bwd_codes", ptr(dpd), ptr(i0), ptr(codes), ptr(d1), N, C, H, W, ptr(gsc), stream())
+    torch.cuda.synchronize()
+    assert torch.equal(d0.view(torch.int16).cpu(), d1.view(torch.int16).cpu())
 
 
 @pytest.mark.parametrize("half", HALVES)
