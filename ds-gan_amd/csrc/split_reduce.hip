@@ -315,7 +315,8 @@ int dsgan_split_pending(void) { return (int)g_queue.size(); }
 // Launch every queued reduction (on the stream its producers ran on; `st` is used only to check
 // that they agree) and empty the queue.  Returns 0, or an error code.
 int dsgan_split_flush(hipStream_t st) {
-  if (!g_queue.empty() && st != g_queue_st) {
+  if (g_queue.empty()) return 0;   // (no HIP call at all)
+  if (st != g_queue_st) {
     dsgan_set_error("dsgan_split_flush: queued reductions belong to another stream");
     return -1;
   }
