@@ -21,6 +21,8 @@
 // buffer and output alive until the flush (dsgan_hip/functional.py: wsa / deferred_splits).
 #include "common.h"
 
+#include <stdlib.h>
+
 #include <type_traits>
 #include <vector>
 
@@ -257,6 +259,18 @@ static int flush_queue() {
   return n;
 }
 
+// Deferred mode keeps a reduction in the queue only when its partials are at most this many MB:
+// larger ones run at once, while their partials are still cache-resident (DSGAN_SPLIT_DEFER_MAX_MB;
+// unset = every reduction deferred).
+static long defer_max_bytes() {
+  static long v = -2;
+  if (v == -2) {
+    const char* e = getenv("DSGAN_SPLIT_DEFER_MAX_MB");
+    v = (e && *e) ? (long)(atof(e) * 1048576.0) : -1;
+  }
+  return v;
+}
+
 static void submit(const RSeg* v, int n, hipStream_t st) {
   if (!g_defer) {
     launch_segs(v, n, st);
@@ -264,7 +278,17 @@ static void submit(const RSeg* v, int n, hipStream_t st) {
   }
   if (!g_queue.empty() && st != g_queue_st) flush_queue();
   g_queue_st = st;
-  for (int i = 0; i < n; ++i) g_queue.push_back(v[i]);
+  const long lim = defer_max_bytes();
+  for (int i = 0; i < n; ++i) {
+    if (lim >= 0 && (long)v[i].S * v[i].MN * 4 > lim) {
+      // run now; a queued reduction into the same output goes first (queue order = addition order)
+      for (const RSeg& q : g_queue)
+        if (overlaps(q, v[i])) { flush_queue(); break; }
+      launch_segs(&v[i], 1, st);
+    } else {
+      g_queue.push_back(v[i]);
+    }
+  }
   if (g_queue.size() >= 4096) flush_queue();
 }
 
