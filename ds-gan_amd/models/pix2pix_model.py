@@ -26,6 +26,7 @@ Deliberate, documented deviations:
     optimizer step whose flat gradient holds inf/nan is skipped (the reference would write NaN
     into its weights and never recover); with finite gradients nothing changes.
 """
+import os
 import random
 
 import torch
@@ -38,6 +39,10 @@ from dsgan_hip.amp import LossScaler
 from util.image_pool import ImagePool
 from .base_model import BaseModel
 from . import networks
+
+# backward_D runs D once on the fake and real batches stacked (DSGAN_D_BATCH=0: two passes, as the
+# reference's code reads: DSGAN/models/pix2pix_model.py:141-160)
+D_BATCH = os.environ.get("DSGAN_D_BATCH", "1") != "0"
 
 
 def _fusable(*xs):
@@ -161,10 +166,26 @@ class Pix2PixModel(BaseModel):
             fake_AB = self.fake_AB_pool.query(HF.cat_channels(self.real_A, self.fake_B.detach()))
         else:
             fake_AB = self.fake_B
-        pred_fake = self.netD(fake_AB.detach())
+        fake_AB = fake_AB.detach()
+        if D_BATCH and fake_AB.dim() == 4 and fake_AB.dtype == torch.float32:
+            # the fake and real passes as ONE batch-2N pass of D (D's ops are per-sample: the same
+            # outputs, half the launches); neither half needs an input grad
+            N, C, H, W = fake_AB.shape
+            AB = torch.empty((2 * N, C, H, W), device=fake_AB.device, dtype=torch.float32)
+            HF.copy_into(AB[:N], fake_AB)
+            if self.use_condition == 1:
+                Ca = self.real_A.shape[1]
+                HF.copy_into(AB[N:, :Ca], self.real_A)
+                HF.copy_into(AB[N:, Ca:], self.real_B)
+            else:
+                HF.copy_into(AB[N:], self.real_B)
+            pred = self.netD(AB)
+            pred_fake, pred_real = pred[:N], pred[N:]
+        else:
+            pred_fake = self.netD(fake_AB)
+            real_AB = HF.cat_channels(self.real_A, self.real_B) if self.use_condition == 1 else self.real_B
+            pred_real = self.netD(real_AB)
         self.loss_D_fake = self.criterionGAN(pred_fake, False)
-        real_AB = HF.cat_channels(self.real_A, self.real_B) if self.use_condition == 1 else self.real_B
-        pred_real = self.netD(real_AB)
         self.loss_D_real = self.criterionGAN(pred_real, True)
         if _fusable(self.loss_D_fake, self.loss_D_real):   # one launch each way (HF.loss_sum)
             self.loss_D = HF.loss_sum([(self.loss_D_fake, 1.0), (self.loss_D_real, 1.0)], 0.5)
