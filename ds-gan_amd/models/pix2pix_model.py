@@ -41,7 +41,9 @@ from .base_model import BaseModel
 from . import networks
 
 # backward_D runs D once on the fake and real batches stacked (DSGAN_D_BATCH=0: two passes, as the
-# reference's code reads: DSGAN/models/pix2pix_model.py:141-160)
+# reference's code reads: DSGAN/models/pix2pix_model.py:141-160).  Not in --precision fp16: there the
+# stacked pass moved the 10-step MS-SSIM delta vs the oracle from 2e-6 to 1.5e-3 at 512^2, batch 8
+# (cause not found yet: profiles/r05/bench_c5_*.json)
 D_BATCH = os.environ.get("DSGAN_D_BATCH", "1") != "0"
 
 
@@ -167,7 +169,7 @@ class Pix2PixModel(BaseModel):
         else:
             fake_AB = self.fake_B
         fake_AB = fake_AB.detach()
-        if D_BATCH and fake_AB.dim() == 4 and fake_AB.dtype == torch.float32:
+        if D_BATCH and HF.get_precision() != "fp16" and fake_AB.dim() == 4 and fake_AB.dtype == torch.float32:
             # the fake and real passes as ONE batch-2N pass of D (D's ops are per-sample: the same
             # outputs, half the launches); neither half needs an input grad
             N, C, H, W = fake_AB.shape
