@@ -243,8 +243,8 @@ __global__ __launch_bounds__(256) void ssim_fwd_kernel(SSIMArgs s, int tiles_w) 
     const float s11 = v[2] - mu1 * mu1, s22 = v[3] - mu2 * mu2, s12 = v[4] - mu1 * mu2;
     const float A1 = 2.f * mu1 * mu2 + s.C1, A2 = 2.f * s12 + s.C2;
     const float B1 = mu1 * mu1 + mu2 * mu2 + s.C1, B2 = s11 + s22 + s.C2;
-    const float cs = A2 / B2;
-    const float S = (A1 / B1) * cs;
+    const float cs = A2 / B2, l = A1 / B1;
+    const float S = l * cs;
     ssum += S;
     const long o = (long)plane * plane_out + (long)oh * Wo + ow;
     const long stride = (long)s.planes * plane_out;
@@ -255,9 +255,12 @@ __global__ __launch_bounds__(256) void ssim_fwd_kernel(SSIMArgs s, int tiles_w) 
       s.coef[o + 2 * stride] = k * (2.f / B2);
     } else {
       const float k = s.kscale ? s.kscale[plane] : 1.f;
-      s.coef[o] = k * (S * (2.f * mu1 / A1 - 2.f * mu1 / A2 - 2.f * mu2 / B1 + 2.f * mu2 / B2));
+      // S / A1 = cs / B1 and S / A2 = l / B2, written without the division by A1 or A2: those
+      // cross zero (a negative local mean of fake, a covariance of -C2/2), where S * (1/A) is 0 * inf
+      // = NaN although the derivative is finite -- the reference's autograd of A/B never divides by A
+      s.coef[o] = k * (2.f * mu1 * (cs / B1 - l / B2) + 2.f * mu2 * (S / B2 - S / B1));
       s.coef[o + stride] = k * (-S / B2);
-      s.coef[o + 2 * stride] = k * (2.f * S / A2);
+      s.coef[o + 2 * stride] = k * (2.f * l / B2);
     }
   }
   if (s.out) {   // per-tile partial sum of S (final_sum_kernel)

@@ -41,9 +41,9 @@ from .base_model import BaseModel
 from . import networks
 
 # backward_D runs D once on the fake and real batches stacked (DSGAN_D_BATCH=0: two passes, as the
-# reference's code reads: DSGAN/models/pix2pix_model.py:141-160).  Not in --precision fp16: there the
-# stacked pass moved the 10-step MS-SSIM delta vs the oracle from 2e-6 to 1.5e-3 at 512^2, batch 8
-# (cause not found yet: profiles/r05/bench_c5_*.json)
+# reference's code reads: DSGAN/models/pix2pix_model.py:141-160); same logits, the weight-grads to fp32
+# reassociation (tests/test_dbatch_gpu.py).  (Round 5 had it off in fp16 after a configs[4] run drifted:
+# the cause was a NaN in the SSIM backward, not the stacked pass -- losses.hip ssim_fwd_kernel.)
 D_BATCH = os.environ.get("DSGAN_D_BATCH", "1") != "0"
 
 
@@ -141,6 +141,8 @@ class Pix2PixModel(BaseModel):
             # optimizer-step calls per network: host counters, since a graph replay never enters
             # FlatAdam.step (the scalers count the applied steps on the device)
             self.step_calls = {"G": 0, "D": 0}
+            # backward_D's stacked batch-2N D pass (D_BATCH); an attribute so tests can compare the two forms
+            self.d_batch = D_BATCH
 
     def set_input(self, input):
         AtoB = self.opt.which_direction == "AtoB"
@@ -169,7 +171,7 @@ class Pix2PixModel(BaseModel):
         else:
             fake_AB = self.fake_B
         fake_AB = fake_AB.detach()
-        if D_BATCH and HF.get_precision() != "fp16" and fake_AB.dim() == 4 and fake_AB.dtype == torch.float32:
+        if self.d_batch and fake_AB.dim() == 4 and fake_AB.dtype == torch.float32:
             # the fake and real passes as ONE batch-2N pass of D (D's ops are per-sample: the same
             # outputs, half the launches); neither half needs an input grad
             N, C, H, W = fake_AB.shape
@@ -187,6 +189,7 @@ class Pix2PixModel(BaseModel):
             pred_fake = self.netD(fake_AB)
             real_AB = HF.cat_channels(self.real_A, self.real_B) if self.use_condition == 1 else self.real_B
             pred_real = self.netD(real_AB)
+        self.pred_fake, self.pred_real = pred_fake, pred_real
         self.loss_D_fake = self.criterionGAN(pred_fake, False)
         self.loss_D_real = self.criterionGAN(pred_real, True)
         if _fusable(self.loss_D_fake, self.loss_D_real):   # one launch each way (HF.loss_sum)

@@ -808,6 +808,60 @@ def test_ssim_fwd_bwd(shape):
     assert rel(fd.grad, fr.grad) < 1e-3
 
 
+def test_ssim_bwd_on_round5_nan_patches():
+    """The SSIM backward at the output pixels where round 5's kernel wrote NaN coefficients (configs[4],
+    fp16, step 4 of the quality leg: 121 NaN elements of the SSIM input-grad, so the G step was skipped
+    and the run drifted from the reference by an MS-SSIM delta of 1.5e-3).  The coefficient maps were
+    S * (1 / A1), S * (1 / A2): at an exact zero of A2 = 2 sigma12 + C2, 0 * inf = NaN, although the
+    derivative -- the reference's autograd of A / B, DSGAN/MS_SSIM.py:76-88 -- is finite there.  The
+    patches (tests/golden/ssim_nan_patch.npz, gen_ssim_nan_patch.py) hold those pixels' 11 x 11 input
+    windows; the current kernel must give a finite input-grad that matches float64 autograd."""
+    import os
+    import numpy as np
+    from dsgan_hip import functional as HF
+    from oracle import dsgan_cpu as O
+    z = np.load(os.path.join(os.path.dirname(__file__), "golden", "ssim_nan_patch.npz"))
+    real, fake = torch.from_numpy(z["real"]), torch.from_numpy(z["fake"])
+    assert real.shape[0] >= 1 and real.shape[1:] == (1, 16, 16)
+    for i in range(real.shape[0]):
+        r, f = real[i:i + 1], fake[i:i + 1]
+        fr = f.double().requires_grad_()
+        s_ref = O.ssim((r.double() + 1) / 2, (fr + 1) / 2)
+        s_ref.backward()
+        fd = _leaf(f)
+        s = HF.ssim_affine(r.to(DEV), fd, 0.5, 0.5, 1.0)
+        s.backward()
+        assert torch.isfinite(fd.grad).all(), i
+        assert abs(s.item() - s_ref.item()) < 2e-5
+        assert rel(fd.grad, fr.grad) < 1e-3, (i, rel(fd.grad, fr.grad))
+
+
+def test_ssim_bwd_finite_where_covariance_crosses_minus_c2():
+    """Accuracy of the SSIM backward where A2 = 2 sigma12 + C2 and A1 = 2 mu1 mu2 + C1 pass through zero
+    (see test_ssim_bwd_on_round5_nan_patches): anti-correlated fields whose local variance sweeps through
+    C2 / 2 along W, and a negative fake mean around -C1 / (2 mu1)."""
+    from dsgan_hip import functional as HF
+    from oracle import dsgan_cpu as O
+    g = torch.Generator().manual_seed(77)
+    N, C, H, W = 4, 3, 256, 256
+    amp = torch.linspace(0.005, 0.05, W).view(1, 1, 1, W)
+    noise = F.avg_pool2d(torch.randn(N, C, H + 2, W + 2, generator=g), 3, 1) * 3
+    X = 0.75 + amp * noise
+    Y = 0.75 - amp * noise + 0.002 * torch.randn(N, C, H, W, generator=g)
+    Y[:, 2] = Y[:, 2] - 0.75 - 0.02 * torch.linspace(-1, 1, H).view(H, 1)   # mu2 around -C1 / (2 mu1)
+    real, fake = X * 2 - 1, Y * 2 - 1
+    fr = fake.clone().double().requires_grad_()
+    s_ref = O.ssim((real.double() + 1) / 2, (fr + 1) / 2)
+    s_ref.backward()
+    fd = _leaf(fake)
+    s = HF.ssim_affine(real.to(DEV), fd, 0.5, 0.5, 1.0)
+    s.backward()
+    bad = int((~torch.isfinite(fd.grad)).sum())
+    assert bad == 0, "%d non-finite SSIM input-grad elements" % bad
+    assert abs(s.item() - s_ref.item()) < 2e-5
+    assert rel(fd.grad, fr.grad) < 1e-3
+
+
 def test_adam_matches_torch():
     from dsgan_hip.flat import FlatParams, FlatAdam
     torch.manual_seed(0)

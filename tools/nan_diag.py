@@ -85,8 +85,8 @@ def _wrap_functions():
 def _wrap_model(model):
     bD, bG, oD, oG = model.backward_D, model.backward_G, model.optimizer_D.step, model.optimizer_G.step
 
-    def backward_D():
-        bD()
+    def backward_D(*a):
+        bD(*a)
         PR.note("flatD.grad after backward_D", model.flatD.grad)
 
     def backward_G():
