@@ -163,7 +163,21 @@ def _profile_json(name):
     return {}, None
 
 
-def roofline_block(ig, fams, timing_steps, peak, roof_src, pmc_t=None, pmc_t_src=None, pmc_m=None, pmc_m_src=None):
+def rocprof_family_avg_us(csv_path, family):
+    """(average us, calls) of every kernel whose name contains ``family`` in a rocprofv3 --stats
+    style CSV (tools/prof_stats.py): the figure the line's ``avg_launch_us`` must agree with."""
+    import csv
+    calls, ns = 0, 0.0
+    with open(csv_path, newline="") as f:
+        for row in csv.DictReader(f):
+            if family in row["Name"]:
+                calls += int(row["Calls"])
+                ns += float(row["TotalDurationNs"])
+    return (ns / calls / 1e3 if calls else None), calls
+
+
+def roofline_block(ig, fams, timing_steps, peak, roof_src, pmc_t=None, pmc_t_src=None, pmc_m=None, pmc_m_src=None,
+                   pw_ms=None):
     """The line's ``roofline`` object from the kernel timer's records.
 
     ``ig`` = KernelTimer.summary() and ``fams`` = KernelTimer.families() over the launches of
@@ -171,11 +185,21 @@ def roofline_block(ig, fams, timing_steps, peak, roof_src, pmc_t=None, pmc_t_src
     steps timed after it when events recorded by graph nodes are unreadable.  Every per-step
     figure divides by ``timing_steps`` -- never by the bench's --steps, which the timer may not
     have seen.  The dominant kernel is the contraction family with the most time; its bound is
-    whichever resource its algorithmic work needs longest at peak."""
+    whichever resource its algorithmic work needs longest at peak.
+
+    ``pw_ms`` = per-launch ms of the pointwise GEMM kernels alone (``KernelTimer.pw_kernel_ms``: the
+    library's events around the GEMM kernel launch, without the split-K finishing pass the C-ABI
+    call may add).  When the dominant family is ``pwgemm_kernel`` and those cover the same launches,
+    ``achieved`` / ``frac`` / ``avg_launch_us`` are the kernel's own (the figure rocprofv3 reports);
+    the C-ABI bracket stays beside it as ``bracket_avg_launch_us``."""
     pmc_t, pmc_m = pmc_t or {}, pmc_m or {}
     ts = max(1, int(timing_steps))
     ach = ig["flops"] / (ig["total_ms"] * 1e-3) / 1e12 if ig["total_ms"] > 0 else 0.0
     dom, (dn, dms, dfl, dby) = max(fams.items(), key=lambda kv: kv[1][1])
+    bracket_ms = dms
+    kernel_only = bool(dom == "pwgemm_kernel" and pw_ms and len(pw_ms) == dn)
+    if kernel_only:
+        dms = float(sum(pw_ms))
     t_avg = dms / max(1, dn) * 1e-3
     fl_l, by_l = dfl / max(1, dn), dby / max(1, dn)
     mfma_ach, hbm_ach = fl_l / t_avg / 1e12, by_l / t_avg / 1e9
@@ -194,6 +218,12 @@ def roofline_block(ig, fams, timing_steps, peak, roof_src, pmc_t=None, pmc_t_src
             "hbm": {"achieved_gbs": round(hbm_ach, 1), "frac": round(hbm_ach / PEAK_HBM_GBS, 4)},
             "launches_per_step": round(dn / ts, 2), "kernel_ms_per_step": round(dms / ts, 3),
             "avg_launch_us": round(dms / max(1, dn) * 1e3, 1),
+            "avg_launch_timing": ("kernel-only events around the GEMM kernel launch (dsgan_ktimer)" if kernel_only else
+                                  "HIP events around the C-ABI call (kernel-only events unavailable: %s)"
+                                  % ("not the pointwise family" if dom != "pwgemm_kernel" else
+                                     "unreadable" if pw_ms is None else
+                                     "%d kernel pairs for %d calls" % (len(pw_ms), dn))),
+            "bracket_avg_launch_us": round(bracket_ms / max(1, dn) * 1e3, 1),
             "all_contractions": {"achieved": round(ach, 2), "frac": round(ach / peak, 4),
                                  "ms_per_step": round(ig["total_ms"] / ts, 3),
                                  "gflop_per_step": round(ig["flops"] / ts / 1e9, 1),
@@ -253,13 +283,13 @@ def main():
             # the per-launch HIP events of the roofline leg are recorded INSIDE the captured graphs
             # (the capture happens in this call): every replay re-records them, and the leg reads the
             # last timed replay's
-            HF.IGEMM_TIMER.rec = []
+            HF.IGEMM_TIMER.reset()
             HF.IGEMM_TIMER.on = True
         model.optimize_parameters()
     torch.cuda.synchronize()
 
     if not graphed:
-        HF.IGEMM_TIMER.rec = []
+        HF.IGEMM_TIMER.reset()
     HF.IGEMM_TIMER.on = True
     if world > 1:
         dist.barrier()
@@ -285,7 +315,7 @@ def main():
             raise RuntimeError("no timer records")
     except Exception:   # noqa: BLE001 -- events recorded by graph nodes unreadable: time eager steps
         torch.cuda.synchronize()
-        HF.IGEMM_TIMER.rec = []
+        HF.IGEMM_TIMER.reset()
         HF.IGEMM_TIMER.on = True
         model.cuda_graph = False
         for _ in range(EAGER_TIMING_STEPS):
@@ -325,12 +355,13 @@ def main():
             dt_tp = t.item()
 
     fams = HF.IGEMM_TIMER.families()
+    pw_ms = HF.IGEMM_TIMER.pw_kernel_ms()   # the pointwise GEMM kernels alone (no split-K finishing pass)
     if rank == 0:
         imgs = args.batch * args.steps * world
         peak = PEAK_F32_TFLOPS if args.precision == "fp32" else PEAK_BF16_TFLOPS   # dense fp16 = bf16 rate
         pmc_t, pmc_t_src = _profile_json("pmc_traffic.json")
         pmc_m, pmc_m_src = _profile_json("mfma_pmc.json")
-        roof = roofline_block(ig, fams, timing_steps, peak, roof_src, pmc_t, pmc_t_src, pmc_m, pmc_m_src)
+        roof = roofline_block(ig, fams, timing_steps, peak, roof_src, pmc_t, pmc_t_src, pmc_m, pmc_m_src, pw_ms=pw_ms)
         out = {
             "metric": METRIC,
             "value": round(imgs / dt, 3),

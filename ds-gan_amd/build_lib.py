@@ -1,9 +1,12 @@
 """Build libdsgan_hip.so in-tree: hipcc --offload-arch=gfx950, one object per source, then link.
 
-    python ds-gan_amd/build_lib.py [-j N] [--force]
+    python ds-gan_amd/build_lib.py [-j N] [--force] [--measure]
 
 The library lands at ds-gan_amd/dsgan_hip/libdsgan_hip.so (git-ignored, but it travels to the
 GPU box with the gpurun snapshot).  Objects are rebuilt only when a source or header is newer.
+--measure builds the measurement variant (-DDSG_MEASURE: the pricing branches of planner knob 10,
+e.g. epilogues that drop their stores) as libdsgan_hip_measure.so from its own objects; tools load
+it with DSGAN_HIP_LIB=.../libdsgan_hip_measure.so.  The product library never carries them.
 """
 import argparse
 import concurrent.futures as cf
@@ -46,44 +49,48 @@ def _newer(src, obj, headers):
     return os.path.getmtime(src) > t or any(os.path.getmtime(h) > t for h in headers)
 
 
-def _compile(src, obj):
-    cmd = [HIPCC] + FLAGS + EXTRA.get(os.path.basename(src), []) + ["-c", src, "-o", obj]
+def _compile(src, obj, defs=()):
+    cmd = [HIPCC] + FLAGS + list(defs) + EXTRA.get(os.path.basename(src), []) + ["-c", src, "-o", obj]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError("compile failed: %s\n%s\n%s" % (" ".join(cmd), r.stdout, r.stderr))
     return obj
 
 
-def build(jobs=8, force=False, verbose=True):
-    os.makedirs(OBJ_DIR, exist_ok=True)
+def build(jobs=8, force=False, verbose=True, measure=False):
+    obj_dir = OBJ_DIR + ("_measure" if measure else "")
+    lib = LIB.replace(".so", "_measure.so") if measure else LIB
+    defs = ["-DDSG_MEASURE"] if measure else []
+    os.makedirs(obj_dir, exist_ok=True)
     os.makedirs(OUT_DIR, exist_ok=True)
     srcs = sorted(glob.glob(os.path.join(CSRC, "*.hip")) + glob.glob(os.path.join(CSRC, "*.cpp")))
     objs, todo = [], []
     for s in srcs:
-        o = os.path.join(OBJ_DIR, os.path.basename(s) + ".o")
+        o = os.path.join(obj_dir, os.path.basename(s) + ".o")
         objs.append(o)
         if force or _newer(s, o, _includes(s)):
             todo.append((s, o))
     if todo:
         with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
-            futs = [ex.submit(_compile, s, o) for s, o in todo]
+            futs = [ex.submit(_compile, s, o, defs) for s, o in todo]
             for f in cf.as_completed(futs):
                 o = f.result()
                 if verbose:
                     print("  built", os.path.relpath(o, HERE), flush=True)
-    if todo or not os.path.exists(LIB) or any(os.path.getmtime(o) > os.path.getmtime(LIB) for o in objs):
-        cmd = [HIPCC, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", LIB] + objs
+    if todo or not os.path.exists(lib) or any(os.path.getmtime(o) > os.path.getmtime(lib) for o in objs):
+        cmd = [HIPCC, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", lib] + objs
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError("link failed:\n%s\n%s" % (r.stdout, r.stderr))
         if verbose:
-            print("  linked", os.path.relpath(LIB, HERE), flush=True)
-    return LIB
+            print("  linked", os.path.relpath(lib, HERE), flush=True)
+    return lib
 
 
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("-j", type=int, default=min(8, os.cpu_count() or 4))
     ap.add_argument("--force", action="store_true")
+    ap.add_argument("--measure", action="store_true", help="the DSG_MEASURE variant (libdsgan_hip_measure.so)")
     a = ap.parse_args()
-    build(a.j, a.force)
+    build(a.j, a.force, measure=a.measure)

@@ -316,6 +316,10 @@ static inline unsigned cdiv(long a, long b) { return (unsigned)((a + b - 1) / b)
 namespace dsg {
 bool plan_only();           // capi.cpp
 void note_ws_need(long n);  // capi.cpp: dsgan_last_ws_need() reports it
+// Kernel-only timer (dsgan_ktimer, capi.cpp): a launcher brackets ONE kernel launch -- not the split
+// reductions or finishing passes its entry point also issues -- with ktimer_mark(st, 0) / (st, 1).
+// Off by default (no HIP call then); bench.py's roofline leg turns it on.
+void ktimer_mark(hipStream_t st, int end);
 }  // namespace dsg
 #define DSG_WS(need, ws, ws_elems, name)                                                              \
   do {                                                                                               \

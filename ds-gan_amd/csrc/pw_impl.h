@@ -33,9 +33,10 @@ struct PwArgs {
   int y_bf16;  // FWD: Y is bf16 [b][M][P] (y_bs in elements)
   int gbf;     // FWD: ypre is bf16 and receives act'(pre);  DGRAD: gpre is a bf16 multiplier (no act')
   int gp_pref; // DGRAD with a 16-bit gp multiplier (SWP tiles): load gp before the K loop
-  int dbg;     // measurement only (planner knob 10): bit 0 = drop the epilogue's output stores,
-               // bit 1 = the gelu pair without its GELU arithmetic; DMA-ring kernels: 4 = no DMA after
-               // the prologue, 8 = no fragment reads / MFMAs, 16 = no epilogue, 32 = no prologue DMA
+#ifdef DSG_MEASURE
+  int dbg;     // measurement builds only (build_lib.py --measure; planner knob 10): bit 0 = drop the
+               // epilogue's output stores, bit 1 = the gelu pair without its GELU arithmetic
+#endif
   int dma;     // host planner: the wide 16-bit-operand launch runs an LDS-DMA ring form: 1 = 256 x 256
                // tiles (8 waves, 4 stages, one workgroup per CU), 2 = 256 x 128 tiles (4 waves, 3 stages,
                // two workgroups per CU: one's epilogue runs beside the other's MFMAs)
@@ -590,9 +591,13 @@ __global__ __launch_bounds__(128 * WN, WN == 2 ? 2 : 1) void pwgemm_kernel(PwArg
   float* const ypre = part ? nullptr : g.ypre;
   const int act = part ? 0 : g.act, accumulate = part ? 0 : g.accumulate, y_bf16 = part ? 0 : g.y_bf16;
   const unsigned grange = (unsigned)(((long)g.M * g.P - p0) * 4);
+#ifdef DSG_MEASURE
   // (g.dbg & 1: measurement builds only -- zero-range output descriptors drop every output store, so
   // an A/B prices the epilogue's HBM writes; cdna_hip_programming.md T8)
   const unsigned range = (g.dbg & 1) ? 0u : grange;
+#else
+  const unsigned range = grange;
+#endif
   const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(ybase + (long)bimg * ybs + p0), (short)0, range, 0x00020000);
   const __amdgpu_buffer_rsrc_t ryh = __builtin_amdgcn_make_buffer_rsrc(
@@ -664,10 +669,13 @@ __global__ __launch_bounds__(128 * WN, WN == 2 ? 2 : 1) void pwgemm_kernel(PwArg
         bool acted = false;
         if (ypre && g.gbf) {          // FWD: ypre <- 16-bit act'(pre), v <- act(pre) (one GELU evaluation)
           float apv[16];
-          if (g.dbg & 2) {              // (measurement only: the pair without its GELU arithmetic)
+#ifdef DSG_MEASURE
+          if (g.dbg & 2) {              // (measurement builds only: the pair without its GELU arithmetic)
 #pragma unroll
             for (int r = 0; r < 16; ++r) apv[r] = v[r];
-          } else if (act == ACT_GELU) {
+          } else
+#endif
+          if (act == ACT_GELU) {
 #pragma unroll
             for (int r = 0; r < 16; r += 2) {
               f32x2 a, ap;
@@ -806,8 +814,10 @@ template <typename T16, int MODE, int BM, int ABF = 0, int BBF = 0, int BN = 128
 static void pw_launch(const PwArgs& g, int splits, hipStream_t st) {
   const int mt = (g.M + BM - 1) / BM;
   const int nt = (MODE == PW_WGRAD) ? (g.N + BN - 1) / BN : g.N / BN;
+  ktimer_mark(st, 0);
   hipLaunchKernelGGL((pwgemm_kernel<T16, MODE, BM, ABF, BBF, BN, WN, BK, SWP, NS>),
                      dim3((unsigned)((long)mt * nt * splits)), dim3(128 * WN), 0, st, g);
+  ktimer_mark(st, 1);
 }
 
 constexpr int PW_WIDE = -1;   // tile selector: 256 x 256 tiles, 8 waves, 64-deep K steps
@@ -1014,9 +1024,6 @@ void pw_wgrad_launch(const PwArgs& g, int bm, int abf, int bbf, int splits, hipS
     default: pw_launch<T16, PW_WGRAD, 128, 1, 1>(g, splits, st); break;
   }
 }
-// pwpp.hip: the persistent gelu-pair forward (16-bit W / X / outputs, M % 256, P % 128, K % 32)
-void pwpp_gelu_launch(const PwArgs& g, hipStream_t st);
-
 #define PW_EXTERN_LAUNCHERS(T16)                                                                            \
   extern template void pw_fd_launch_m<T16, PW_FWD>(const PwArgs&, int, int, int, int, hipStream_t);         \
   extern template void pw_fd_launch_m<T16, PW_DGRAD>(const PwArgs&, int, int, int, int, hipStream_t);       \

@@ -43,9 +43,10 @@ static void pw_fd_launch(int mode, const PwArgs& g, int bm, int abf, int bbf, in
 //   155 -> 149 and 138 -> 131 us, same bits; profiles/r04/pw_bench_dma.txt); 3 = the same plus the
 //   weight-grads (3-5 % slower there); 2 = 256 x 128 tiles, 3 stages, two workgroups per CU (slower:
 //   392 us for the 512-channel gelu-pair forward); 0 = register-staged everywhere.
-//   [10] measurement only: bit 0 = FWD / DGRAD epilogues drop their output stores (prices the writes),
-//   bit 1 = the gelu-pair epilogue skips its GELU arithmetic (prices the VALU); on the LDS-DMA ring
-//   bit 2 = no DMA after the prologue stages (prices the feed), bit 3 = no fragment reads / MFMAs.
+//   [10] measurement builds only (build_lib.py --measure, DSG_MEASURE; ignored otherwise): bit 0 =
+//   FWD / DGRAD epilogues drop their output stores (prices the writes), bit 1 = the gelu-pair
+//   epilogue skips its GELU arithmetic (prices the VALU).  [11] retired (the persistent gelu-pair
+//   forward, 1.8x slower, removed).
 static int g_tune[12] = {1, 512, 256, 4, 0, 0, 0, 0, 1, 1, 0, 0};
 
 // the LDS-DMA ring form's conditions (full 256 x 256 tiles, 32-deep K steps, 16-byte pieces)
@@ -100,7 +101,9 @@ static int fd_plan(PwArgs& g, int bm, float* ws) {
   g.k_split = 0;
   g.ws = nullptr;
   g.gp_pref = g_tune[8];
+#ifdef DSG_MEASURE
   g.dbg = g_tune[10];
+#endif
   if (ws && fd_split_ok(g)) {
     splits = fd_splits(g, bm, PBK, &g.k_split);
     if (splits > 1) g.ws = ws;
@@ -228,15 +231,6 @@ extern "C" int dsgan_pw_fwd_io_ws(const void* W, int w_bf16, const void* X, long
   const int bm = fd_tile_k(g, w_bf16 || x_bf16);
   const int splits = fd_plan(g, bm, ws);
   DSG_WS(fd_need(g, splits), ws, ws_elems, "dsgan_pw_fwd_io (dsgan_pw_fd_workspace)");
-  // the gelu-pair forward of the wide unfused blocks on the persistent form (pwpp.hip: the GELU
-  // pair of one tile beside the next tile's MFMAs), planner knob 11.  bf16 only: with fp16 operands
-  // 6e-5 of its outputs differ from the one-tile kernel's by one fp16 ulp (tools/probe/pp_diag.py)
-  if (g_tune[11] && half_type() != HALF_F16 && splits == 1 && w_bf16 && x_bf16 && y_bf16 && g.ypre && g.gbf && act == ACT_GELU &&
-      !accumulate && M % 256 == 0 && P % 128 == 0 && K % 32 == 0 && al16(g.ypre) && (ypre_bs & 7) == 0) {
-    pwpp_gelu_launch(g, st);
-    DSG_CHECK_LAUNCH();
-    return 0;
-  }
   fd_launch(PW_FWD, g, bm, w_bf16, x_bf16, splits, st);
   DSG_CHECK_LAUNCH();
   return 0;

@@ -27,6 +27,8 @@ SIGNATURES = {
     "dsgan_adam_amp": [P, P, P, P, L, D, D, D, D, P, S],
     "dsgan_get_half_type": [],
     "dsgan_clear_launch_error": [],
+    "dsgan_ktimer": [I],
+    "dsgan_ktimer_read": [P, I],
     "dsgan_last_error_string": [],
     # scratch contract: plan-only mode and the scratch the last planned launch needs (CPU planner tests)
     "dsgan_set_plan_only": [I],

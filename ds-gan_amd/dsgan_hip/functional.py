@@ -138,11 +138,47 @@ def half_dtype():
 
 class KernelTimer:
     """Brackets every implicit-GEMM launch with HIP events on the launch stream (bench.py's
-    roofline leg).  Off by default; when on, records (start, end, algorithmic_flops)."""
+    roofline leg).  Off by default; when on, records (start, end, algorithmic_flops).
 
-    def __init__(self):
-        self.on = False
+    ``kernel_only=True`` (IGEMM_TIMER) also switches the library's kernel-only timer
+    (``dsgan_ktimer``) with it: the pointwise GEMM launchers then record an event pair around the
+    GEMM kernel itself, without the split-K finishing pass the same C-ABI call may issue --
+    ``pw_kernel_ms()`` reads those, the figure rocprofv3 reports for ``pwgemm_kernel``."""
+
+    def __init__(self, kernel_only=False):
+        self._on = False
         self.rec = []
+        self.kernel_only = kernel_only
+
+    @property
+    def on(self):
+        return self._on
+
+    @on.setter
+    def on(self, v):
+        self._on = bool(v)
+        if self.kernel_only:
+            _lib.load().dsgan_ktimer(1 if v else 0)
+
+    def reset(self):
+        """Drop the records (and the library's kernel-only pairs)."""
+        self.rec = []
+        if self.kernel_only:
+            _lib.load().dsgan_ktimer(-1)
+
+    def pw_kernel_ms(self):
+        """Per-launch ms of the pointwise GEMM kernels recorded since reset() (kernel-only timer),
+        or None when the library could not read them (events recorded by graph nodes)."""
+        lib = _lib.load()
+        torch.cuda.synchronize()
+        n = lib.dsgan_ktimer(1 if self._on else 0)
+        if n <= 0:
+            return []
+        buf = (ctypes.c_float * n)()
+        got = lib.dsgan_ktimer_read(buf, n)
+        if got != n:
+            return None
+        return list(buf)
 
     def begin(self):
         if not self.on:
@@ -182,7 +218,7 @@ class KernelTimer:
         return [(r[0].elapsed_time(r[1]), r[2], r[3] + (r[4],)) for r in self.rec]
 
 
-IGEMM_TIMER = KernelTimer()
+IGEMM_TIMER = KernelTimer(kernel_only=True)
 AUX_TIMER = KernelTimer()   # the HBM-bound depthwise / InstanceNorm launches (tools/launch_table.py)
 
 

@@ -47,6 +47,15 @@ from . import networks
 D_BATCH = os.environ.get("DSGAN_D_BATCH", "1") != "0"
 
 
+class GraphCaptureError(RuntimeError):
+    """Under DDP, graph B's capture (the step with its RCCL exchanges) failed: not recoverable by
+    an eager fallback, the run ends."""
+
+
+class _CaptureDeclined(RuntimeError):
+    """Graph A's capture failed on some rank; every rank raises this together (one agreement)."""
+
+
 def _fusable(*xs):
     """Loss terms HF.loss_sum takes: 0-d fp32 device tensors (a disabled term may be a python 0)."""
     ts = [x for x in xs if not (not torch.is_tensor(x) and x == 0)]
@@ -329,11 +338,14 @@ class Pix2PixModel(BaseModel):
             err = None
             try:
                 ent = self._capture(lrs)
+            except GraphCaptureError:   # DDP: graph B's capture failed after collectives were recorded
+                raise
             except Exception as e:   # noqa: BLE001 -- a capture failure must not end the run: eager from here on
                 err = e
-            if err is not None:   # the invalidated capture's error is still pending in the HIP runtime
+            if err is not None:
+                # one process, or every rank declined graph A together (_capture's agreement): the
+                # invalidated capture's error is still pending in the HIP runtime
                 _lib.load().dsgan_clear_launch_error()
-            if not hdist.all_ranks_true(err is None, self.device):   # every rank replays, or none does
                 print("[Pix2PixModel] HIP graph capture failed (%r): running the eager step" % (err,))
                 self._graphs, self.cuda_graph, self._feats_joined = {}, False, False
                 HF.GRAD_READY[0] = None
@@ -347,6 +359,12 @@ class Pix2PixModel(BaseModel):
         ent["gB"].replay()
 
     def _capture(self, lrs):
+        """Capture this shape's graph pair.  Graph A (VGG real features, G forward) holds no
+        collective: if its capture fails on any rank, every rank learns it from one MIN all-reduce
+        and raises _CaptureDeclined together (the caller runs eager from then on, the ranks still in
+        step).  Graph B holds the RCCL exchanges: a rank whose capture of B fails may have recorded a
+        different sequence of collectives than the others, so under DDP that ends the run
+        (GraphCaptureError) instead of an eager fallback whose collectives could pair up wrongly."""
         self.real_A, self.real_B = self.real_A.clone(), self.real_B.clone()   # the static inputs
         torch.cuda.synchronize(self.device)
         pool = torch.cuda.graph_pool_handle()
@@ -355,17 +373,36 @@ class Pix2PixModel(BaseModel):
         # thread_local capture mode: the RCCL process group's watchdog thread polls the events of
         # earlier (eager) collectives; in the default global mode such a query from another thread
         # invalidates the capture.  The capturing thread itself still may not make unsafe calls.
-        with torch.cuda.graph(gA, pool=pool, capture_error_mode="thread_local"):
-            self._launch_real_features()
-            self.forward()
-            if cond:
-                self._cat_fake = HF.cat_channels(self.real_A, self.fake_B.detach())
-                self._fake_AB_buf = torch.empty_like(self._cat_fake)
-            torch.cuda.current_stream(self.device).wait_stream(self._vgg_stream)
-            self._feats_joined = True
+        err_a = None
+        try:
+            with torch.cuda.graph(gA, pool=pool, capture_error_mode="thread_local"):
+                try:
+                    self._launch_real_features()
+                    self.forward()
+                    if cond:
+                        self._cat_fake = HF.cat_channels(self.real_A, self.fake_B.detach())
+                        self._fake_AB_buf = torch.empty_like(self._cat_fake)
+                finally:
+                    # the VGG side stream joins the capture stream even when the forward raised: an
+                    # unjoined forked stream makes the capture's end fail and leaves the capture
+                    # stream current (and capturing) for the eager step that follows
+                    torch.cuda.current_stream(self.device).wait_stream(self._vgg_stream)
+                self._feats_joined = True
+        except Exception as e:   # noqa: BLE001 -- agreed on below, before anything is re-raised
+            err_a = e
+            _lib.load().dsgan_clear_launch_error()
+            self._feats_joined = False
+        if not hdist.all_ranks_true(err_a is None, self.device):   # every rank captures B, or none does
+            raise _CaptureDeclined(err_a if err_a is not None else "graph A capture failed on another rank")
         try:
             with torch.cuda.graph(gB, pool=pool, capture_error_mode="thread_local"):
                 self._d_and_g_steps(self._fake_AB_buf if cond else None)
+        except Exception as e:
+            if hdist.world_size() > 1:
+                raise GraphCaptureError("HIP graph capture of the D / G step (with its RCCL exchanges) failed on "
+                                        "rank %d: %r -- ending the run (the ranks' recorded collectives may "
+                                        "differ)" % (hdist.rank(), e)) from e
+            raise
         finally:
             self._feats_joined = False
             HF.GRAD_READY[0] = None

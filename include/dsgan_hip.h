@@ -54,6 +54,15 @@ int dsgan_get_half_type(void);
  * failed HIP-graph capture, whose invalidation error would otherwise be reported by the next
  * eager launch's check. */
 int dsgan_clear_launch_error(void);
+/* Kernel-only timer (bench.py's roofline leg; no reference counterpart -- measurement plumbing):
+ * while on, the pointwise GEMM launchers record a HIP event pair around the GEMM kernel launch
+ * itself, not around the split-K finishing pass or split reduction the same entry point issues, so
+ * the figure is the kernel's own duration as rocprofv3 reports it.  dsgan_ktimer(1) on, (0) off,
+ * (-1) reset the pair count; returns the count.  dsgan_ktimer_read fills ms[] with the first
+ * min(count, max) pairs' elapsed ms (synchronise first) and returns how many, or -1 when an event
+ * could not be recorded or read (e.g. events recorded by a replayed HIP graph's nodes). */
+int dsgan_ktimer(int on);
+int dsgan_ktimer_read(float* ms, int max);
 
 /* ---- implicit-GEMM convolution (igemm.hip) ------------------------------------------------
  * Replaces nn.Conv2d / nn.Linear / nn.ConvTranspose2d forward+backward:

@@ -61,3 +61,30 @@ def test_pmc_traffic_feeds_waste_ratio():
     assert r["traffic"] == 185.3e6
     assert abs(r["waste_ratio"] - 185.3 / 161.95) < 1e-3
     assert r["mfma"]["pmc_mfma_busy"] == 0.14
+
+
+def test_kernel_only_timing_replaces_the_bracket():
+    """The dominant pointwise family's per-launch time comes from the library's kernel-only events
+    (dsgan_ktimer: the GEMM kernel alone, no split-K finishing pass) when they cover the same
+    launches; the C-ABI bracket stays beside it."""
+    t = FakeTimer(2)
+    pw_ms = [0.0593] * (92 * 2)          # the kernel alone: 59.3 us against the 61-us bracket
+    r = bench.roofline_block(t.summary(), t.families(), 2, bench.PEAK_BF16_TFLOPS, "fake", pw_ms=pw_ms)
+    assert abs(r["avg_launch_us"] - 59.3) < 0.05 and abs(r["bracket_avg_launch_us"] - 61.0) < 0.05
+    assert r["avg_launch_timing"].startswith("kernel-only")
+    assert abs(r["achieved"] - 161.95e6 / 59.3e-6 / 1e9) < 1.0
+    assert abs(r["kernel_ms_per_step"] - 92 * 0.0593) < 1e-3
+    # a pair count that does not match the family's calls, or unreadable pairs: the bracket
+    for bad in (pw_ms[:-1], None, []):
+        r = bench.roofline_block(t.summary(), t.families(), 2, bench.PEAK_BF16_TFLOPS, "fake", pw_ms=bad)
+        assert abs(r["avg_launch_us"] - 61.0) < 0.05 and r["avg_launch_timing"].startswith("HIP events around")
+
+
+def test_rocprof_family_average(tmp_path):
+    p = tmp_path / "s.csv"
+    p.write_text('"Name","Calls","TotalDurationNs","AverageNs","Percentage","MinNs","MaxNs"\n'
+                 '"_ZN3dsg13pwgemm_kernelIDF16bLi2EEEvNS_6PwArgsE",30,1800000,60000.0,1.0,1,1\n'
+                 '"void dsg::pwgemm_kernel<bool _Accum, int>(dsg::PwArgs)",10,580000,58000.0,1.0,1,1\n'
+                 '"dsg::split_canon_kernel(dsg::RSegs)",5,50000,10000.0,1.0,1,1\n')
+    avg, calls = bench.rocprof_family_avg_us(str(p), "pwgemm_kernel")
+    assert calls == 40 and abs(avg - 59.5) < 1e-6

@@ -1621,48 +1621,6 @@ def test_mlp_bwd_c256_forms_bitwise(half, N, H):
     assert rel(outs[1][0], dhr) < 3 * _ulp(half)
 
 
-@pytest.mark.parametrize("half", ["bf16"])   # (the planner keeps fp16 on the one-tile kernel: pwgemm.hip)
-@pytest.mark.parametrize("M,K,HW,NB,bias", [(512, 256, 128 * 128, 4, True),    # 1024 tiles: 4 per CU
-                                             (2048, 512, 64 * 64, 2, True),     # C512@64 block shape, nb 2
-                                             (1024, 96, 64 * 64, 4, False),     # 3 K steps: the short-K flush
-                                             (256, 1024, 32 * 32, 3, True)])    # 24 tiles < 256 CUs, 32 K steps
-def test_pw_gelu_pair_persistent_bitwise(half, M, K, HW, NB, bias):
-    """The persistent gelu-pair forward (pwpp.hip, planner knob dsgan_pw_tune(11)): one workgroup per CU
-    walks 256 x 128 tiles and finishes the previous tile's GELU pair beside the current tile's MFMAs.
-    Same accumulation order (bias, then 16-deep K chunks in order) and the same GELU-pair operations as
-    the one-tile kernel: y = gelu(z) and gp = gelu'(z) bitwise equal to it, at full / under-filled
-    grids, short K (fewer K steps than blocks to finish) and without bias."""
-    import dsgan_hip
-    from dsgan_hip import _lib, functional as HF
-    from dsgan_hip._lib import call, ptr, stream
-    lib = _lib.load()
-    dsgan_hip.set_precision(half)
-    hd = _hdt(half)
-    g0 = torch.Generator(device=DEV).manual_seed(M + K)
-    w = (torch.randn(M, K, device=DEV, generator=g0) / K ** 0.5).to(hd)
-    b = torch.randn(M, device=DEV, generator=g0) if bias else None
-    x = torch.randn(NB, K, HW, device=DEV, generator=g0).to(hd)
-    old = lib.dsgan_pw_tune(11, -1)
-
-    def run(pp):
-        lib.dsgan_pw_tune(11, pp)
-        y = torch.full((NB, M, HW), float("nan"), device=DEV).to(hd)
-        gp = torch.full((NB, M, HW), float("nan"), device=DEV).to(hd)
-        ws = torch.empty(max(1, lib.dsgan_pw_fd_workspace(0, M, K, HW, NB)), device=DEV)
-        call("dsgan_pw_fwd_io_ws", ptr(w), 1, ptr(x), K * HW, 1, ptr(y), M * HW, 1, ptr(gp), M * HW, 1, ptr(b), M, K,
-             HW, NB, 1, 0, 0.2, *HF.wsa(ws), stream())
-        return y, gp
-    try:
-        y0, g0_ = run(0)
-        y1, g1 = run(1)
-        torch.cuda.synchronize()
-    finally:
-        lib.dsgan_pw_tune(11, old)
-    assert torch.equal(y1, y0) and torch.equal(g1, g0_)
-    zr = torch.einsum("mk,nkp->nmp", w.float(), x.float()) + (b.view(1, M, 1) if bias else 0)
-    assert rel(y1.float(), torch.nn.functional.gelu(zr)) < 1e-2
-
-
 @pytest.mark.parametrize("half", HALVES)
 @pytest.mark.parametrize("form", ["fwd16", "fwd32", "fwd_gelu_pair", "dgrad32", "dgrad16", "wgrad"])
 @pytest.mark.parametrize("ring", [3, 2])

@@ -48,7 +48,7 @@ for step in "$@"; do
       tail -2 gpurun_out/gpu_tests.txt ;;
     testfile)
       f=${arg%%::*}; k=""
-      [ "$f" != "$arg" ] && k=${arg#*::}
+      [ "$f" != "$arg" ] && k=${arg#*::} && k=${k//+/ }
       log=gpurun_out/gpu_tests_$(basename "$f" .py).txt
       if [ -n "$k" ]; then
         run 1200 "$log" python -u -m pytest "$f" -m gpu -x -v -s --timeout 1100 --timeout-method thread -k "$k"
