@@ -98,7 +98,36 @@ __global__ __launch_bounds__(256) void final_sum_kernel(const float* __restrict_
   if (threadIdx.x == 0) out[0] = s * coef;
 }
 
+// Two-level form for many partials (the 512^2 VGG pool-L1 taps have tens of thousands,
+// a long serial tail for one workgroup): chunk c = part[c * ch .. c * ch + ch) is summed by workgroup
+// c in a fixed order and written back over its first element; then one workgroup sums the chunk
+// sums (stride ch) in order.  In place: no scratch beyond the partials themselves.
+__global__ __launch_bounds__(256) void chunk_sum_kernel(float* __restrict__ part, int n, int ch) {
+  __shared__ float sh[4];
+  const long b0 = (long)blockIdx.x * ch;
+  const int m = (int)min((long)ch, (long)n - b0);
+  float s = 0.f;
+  for (int i = threadIdx.x; i < m; i += 256) s += part[b0 + i];
+  s = block_sum<256>(s, sh);   // (every read of the chunk precedes the block's barriers)
+  if (threadIdx.x == 0) part[b0] = s;
+}
+__global__ __launch_bounds__(256) void strided_sum_kernel(const float* __restrict__ part, int nc, int ch, float coef,
+                                                          float* __restrict__ out) {
+  __shared__ float sh[4];
+  float s = 0.f;
+  for (int i = threadIdx.x; i < nc; i += 256) s += part[(long)i * ch];
+  s = block_sum<256>(s, sh);
+  if (threadIdx.x == 0) out[0] = s * coef;
+}
+
+constexpr int FS_TWO_LEVEL = 16384, FS_CHUNK = 1024;
 void launch_final_sum(const float* part, int n, float coef, float* out, hipStream_t st) {
+  if (n > FS_TWO_LEVEL) {   // (the partials are the caller's scratch: overwritten in place)
+    const int nc = (n + FS_CHUNK - 1) / FS_CHUNK;
+    hipLaunchKernelGGL(chunk_sum_kernel, dim3((unsigned)nc), dim3(256), 0, st, const_cast<float*>(part), n, FS_CHUNK);
+    hipLaunchKernelGGL(strided_sum_kernel, dim3(1), dim3(256), 0, st, part, nc, FS_CHUNK, coef, out);
+    return;
+  }
   hipLaunchKernelGGL(final_sum_kernel, dim3(1), dim3(256), 0, st, part, n, coef, out);
 }
 

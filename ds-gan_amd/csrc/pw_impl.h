@@ -104,6 +104,271 @@ __device__ __forceinline__ hx4<T16> cvt4(float4 v, int bact, float slope) {
   return r;
 }
 
+// 16-byte buffer store followed by its wait states.  A VALU write to a VGPR that still holds the
+// data of a preceding store of more than 8 bytes needs a wait state (the store reads its data after
+// issue).  hipcc models that hazard only for buffer stores whose soffset is not a register, and ours
+// always have one: in the persistent ring kernel it scheduled "buffer_store_dwordx4 v[138:141], ...,
+// s1; v_or_b32 v138, ..." and some lanes stored the new v138 (tests/test_ops_gpu.py
+// test_pw_persistent_ring_bitwise, tools/probe/ring_diff.py).  So the store is inline asm with the
+// pad inside the string (cdna_hip_programming.md section 5.7 item 2); hipcc does not count it in
+// its own vmcnt waits, which only makes those waits conservative.
+__device__ __forceinline__ void pw_st128(pu32x4 v, __amdgpu_buffer_rsrc_t r, int voff, int soff) {
+  asm volatile("buffer_store_dwordx4 %0, %1, %2, %3 offen\n\ts_nop 1" ::"v"(v), "v"(voff), "s"(r), "s"(soff) : "memory");
+}
+
+// FWD / DGRAD epilogue of one output tile (the one-tile kernel and the persistent ring kernel):
+// bias already in the accumulators; side tensors, activation, accumulation and the stores.
+// EPI: PW_EPI_ANY reads every epilogue option from g at run time; the persistent ring kernel
+// compiles the two forms it serves with the options fixed (less code, fewer live registers):
+// PW_EPI_GELU_PAIR = 16-bit y = gelu(z) and 16-bit act'(z) to ypre, no side input, no accumulate;
+// PW_EPI_PLAIN = y = z (no ypre / gpre / activation; accumulate and the output type from g).
+enum PwEpi : int { PW_EPI_ANY = 0, PW_EPI_GELU_PAIR = 1, PW_EPI_PLAIN = 2 };
+template <typename T16, int BM, int TM, int TN, bool SW, bool GPF, int EPI = PW_EPI_ANY>
+__device__ __forceinline__ void pw_fd_epi(const PwArgs& g, pf32x16 (&acc)[TM][TN], int m0, int bimg, int p0, int split,
+                                          int wm, int wn, int lr, int lh, bool gpf_on, const uint2* gpf) {
+  // FWD / DGRAD: element (m, n0+col) of image bimg lives at base + m*P + col; buffer resources
+  // are based at pixel p0 of row 0, their range ends at row M (a lane whose channel is >= M gets an
+  // offset past the range: its loads read 0, its stores are dropped).  Tile (i, j) is pixel x
+  // channel: lane lr holds channel mrow + lr, register 4q + e pixel col0 + 8q + 4lh + e -- fp32
+  // side tensors move as one 16-byte access per group q, 16-bit ones as 8-byte loads and, paired
+  // by v_permlane32_swap, two 16-byte stores per tile (cdna_hip_programming.md T21).
+  // A split-K partial (g.ws) stores the raw fp32 accumulator into its split's [b][M][P] slab; the
+  // bias, activation, side tensors and accumulation are pw_split_finish_kernel's.
+  const bool part = EPI == PW_EPI_ANY && g.ws != nullptr;
+  float* const ybase = part ? g.ws + (long)split * g.M * g.N : g.Y;
+  const long ybs = part ? (long)g.M * g.P : g.y_bs;
+  const float* const gpre = (part || EPI != PW_EPI_ANY) ? nullptr : g.gpre;
+  float* const ypre = (part || EPI == PW_EPI_PLAIN) ? nullptr : g.ypre;
+  const int act = part ? 0 : EPI == PW_EPI_GELU_PAIR ? ACT_GELU : EPI == PW_EPI_PLAIN ? ACT_NONE : g.act;
+  const int accumulate = (part || EPI == PW_EPI_GELU_PAIR) ? 0 : g.accumulate;
+  const int y_bf16 = part ? 0 : EPI == PW_EPI_GELU_PAIR ? 1 : g.y_bf16;
+  const int gbf = EPI == PW_EPI_GELU_PAIR ? 1 : g.gbf;
+  const unsigned grange = (unsigned)(((long)g.M * g.P - p0) * 4);
+#ifdef DSG_MEASURE
+  // (g.dbg & 1: measurement builds only -- zero-range output descriptors drop every output store, so
+  // an A/B prices the epilogue's HBM writes; cdna_hip_programming.md T8)
+  const unsigned range = (g.dbg & 1) ? 0u : grange;
+#else
+  const unsigned range = grange;
+#endif
+  const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(ybase + (long)bimg * ybs + p0), (short)0, range, 0x00020000);
+  const __amdgpu_buffer_rsrc_t ryh = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)((T16*)g.Y + (long)bimg * g.y_bs + p0), (short)0, range / 2, 0x00020000);
+  __amdgpu_buffer_rsrc_t rp = ry, rg = ry;
+  // bf16 side tensors (gbf): same element offsets, byte offsets halved
+  const int esz = gbf ? 2 : 4;
+  if (ypre) rp = __builtin_amdgcn_make_buffer_rsrc((void*)((char*)ypre + ((long)bimg * g.ypre_bs + p0) * esz), (short)0,
+                                                   gbf ? range / 2 : range, 0x00020000);
+  if (gpre) rg = __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)gpre + ((long)bimg * g.gpre_bs + p0) * esz),
+                                                   (short)0, gbf ? grange / 2 : grange, 0x00020000);
+  // 16-bit store of this lane's 16 values: groups (q, q+1) swap halves so lanes 0-31 hold pixels
+  // 8q..8q+7 and lanes 32-63 pixels 8q+8..8q+15 of their channel (byte offset +16)
+  auto store16 = [&](__amdgpu_buffer_rsrc_t r, const float* v, int vh, int srow) __attribute__((always_inline)) {
+    unsigned d[8];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) d[t] = (unsigned)f2h<T16>(v[2 * t]) | ((unsigned)f2h<T16>(v[2 * t + 1]) << 16);
+#pragma unroll
+    for (int q = 0; q < 4; q += 2) {
+#pragma unroll
+      for (int w = 0; w < 2; ++w) {
+        const auto x = __builtin_amdgcn_permlane32_swap(d[2 * q + w], d[2 * q + 2 + w], false, false);
+        d[2 * q + w] = x[0];
+        d[2 * q + 2 + w] = x[1];
+      }
+      const pu32x4 o = {d[2 * q], d[2 * q + 1], d[2 * q + 2], d[2 * q + 3]};
+      pw_st128(o, r, vh, srow + 16 * q);
+    }
+  };
+  if constexpr (SW) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int col0 = wn * TN * 32 + j * 32;
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int mrow = m0 + wm * TM * 32 + i * 32;   // uniform
+        const bool ok = mrow + lr < g.M;
+        const int e0 = lr * g.P + col0 + 4 * lh;       // lane part (elements)
+        const int v4 = ok ? e0 * 4 : (int)PW_OOB;      // fp32 byte offsets; + 32 q in soffset
+        const int v2 = ok ? e0 * 2 : (int)PW_OOB;      // 16-bit loads; + 16 q
+        const int vh = ok ? (e0 - 4 * lh) * 2 + 16 * lh : (int)PW_OOB;   // paired 16-bit stores
+        const int s4 = mrow * g.P * 4, s2 = mrow * g.P * 2;
+        float v[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) v[r] = acc[i][j][r];
+        if (gpre && gbf) {          // DGRAD: v *= gp, gp = act'(pre) stored 16-bit by the forward
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            uint2 u;
+            if (gpf_on) u = gpf[(GPF ? (j * TM + i) * 4 : 0) + (GPF ? q : 0)];
+            else {
+              const auto w2 = __builtin_amdgcn_raw_buffer_load_b64(rg, v2, s2 + 16 * q, 0);
+              u = make_uint2(w2[0], w2[1]);
+            }
+            v[4 * q] *= h2f<T16>((unsigned short)(u.x & 0xffffu));
+            v[4 * q + 1] *= h2f<T16>((unsigned short)(u.x >> 16));
+            v[4 * q + 2] *= h2f<T16>((unsigned short)(u.y & 0xffffu));
+            v[4 * q + 3] *= h2f<T16>((unsigned short)(u.y >> 16));
+          }
+        } else if (gpre) {
+          float gv[16];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const float4 u = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rg, v4, s4 + 32 * q, 0));
+            gv[4 * q] = u.x; gv[4 * q + 1] = u.y; gv[4 * q + 2] = u.z; gv[4 * q + 3] = u.w;
+          }
+          act_g_mul_arr(g.gact, v, gv, g.slope);
+        }
+        bool acted = false;
+        if (ypre && gbf) {          // FWD: ypre <- 16-bit act'(pre), v <- act(pre) (one GELU evaluation)
+          float apv[16];
+#ifdef DSG_MEASURE
+          if (g.dbg & 2) {              // (measurement builds only: the pair without its GELU arithmetic)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) apv[r] = v[r];
+          } else
+#endif
+          if (act == ACT_GELU) {
+#pragma unroll
+            for (int r = 0; r < 16; r += 2) {
+              f32x2 a, ap;
+              gelu_pair_fast2(f32x2{v[r], v[r + 1]}, a, ap);
+              v[r] = a.x; v[r + 1] = a.y;
+              apv[r] = ap.x; apv[r + 1] = ap.y;
+            }
+          } else {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+              apv[r] = act_g(act, v[r], g.slope);
+              v[r] = act_f(act, v[r], g.slope);
+            }
+          }
+          store16(rp, apv, vh, s2);
+          acted = true;
+        } else if (ypre) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const pu32x4 o = {__builtin_bit_cast(unsigned, v[4 * q]), __builtin_bit_cast(unsigned, v[4 * q + 1]),
+                              __builtin_bit_cast(unsigned, v[4 * q + 2]), __builtin_bit_cast(unsigned, v[4 * q + 3])};
+            pw_st128(o, rp, v4, s4 + 32 * q);
+          }
+        }
+        if (!acted) act_f_arr(act, v, g.slope);
+        if (accumulate) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const float4 u = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(ry, v4, s4 + 32 * q, 0));
+            v[4 * q] += u.x; v[4 * q + 1] += u.y; v[4 * q + 2] += u.z; v[4 * q + 3] += u.w;
+          }
+        }
+        if (y_bf16) {   // 16-bit output: same rows, half the byte offsets
+          store16(ryh, v, vh, s2);
+          continue;
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const pu32x4 o = {__builtin_bit_cast(unsigned, v[4 * q]), __builtin_bit_cast(unsigned, v[4 * q + 1]),
+                            __builtin_bit_cast(unsigned, v[4 * q + 2]), __builtin_bit_cast(unsigned, v[4 * q + 3])};
+          pw_st128(o, ry, v4, s4 + 32 * q);
+        }
+      }
+    }
+  } else {
+    const int P4 = g.P * 4;
+    const bool full = m0 + BM <= g.M;
+    constexpr bool VROW = EPI != PW_EPI_ANY;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int col = wn * TN * 32 + j * 32 + lr;
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int mrow = m0 + wm * TM * 32 + i * 32;   // uniform
+        // lane part of the offset: rows 4h, column col.  In a partial M tile, rows >= M get an
+        // offset past the resource range so the hardware drops the store / returns 0.
+        const int vofs = (4 * lh * g.P + col) * 4;
+        const int mlim = full ? BM : g.M - mrow - 4 * lh;   // rows (r&3)+8(r>>2) < mlim are valid
+        int vrow[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          vrow[r] = ((r & 3) + 8 * (r >> 2) < mlim) ? vofs + (VROW ? ((r & 3) + 8 * (r >> 2)) * P4 : 0) : (int)PW_OOB;
+        // the row of register r as a scalar offset (mrow + its row) * P4 -- or, in the ring kernel's fixed
+        // forms, in the lane's vector offset beside the column: 16 fewer scalars live across its loop
+        auto so = [&](int r, int div) __attribute__((always_inline)) {
+          return VROW ? mrow * (P4 / div) : (mrow + (r & 3) + 8 * (r >> 2)) * (P4 / div);
+        };
+        float v[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) v[r] = acc[i][j][r];
+        if (gpre && gbf) {          // DGRAD: v *= gp, gp = act'(pre) stored bf16 by the forward
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const unsigned short hb = __builtin_amdgcn_raw_buffer_load_b16(
+                rg, vrow[r] == (int)PW_OOB ? (int)PW_OOB : vrow[r] / 2, so(r, 2), 0);
+            v[r] *= h2f<T16>(hb);
+          }
+        } else if (gpre) {
+          float gv[16];
+#pragma unroll
+          for (int r = 0; r < 16; ++r)
+            gv[r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                        rg, vrow[r], so(r, 1), 0));
+          act_g_mul_arr(g.gact, v, gv, g.slope);
+        }
+        bool acted = false;
+        if (ypre && gbf) {          // FWD: ypre <- bf16 act'(pre), v <- act(pre) (one GELU evaluation)
+          float apv[16];
+          if (act == ACT_GELU) {
+#pragma unroll
+            for (int r = 0; r < 16; r += 2) {
+              f32x2 a, ap;
+              gelu_pair_fast2(f32x2{v[r], v[r + 1]}, a, ap);
+              v[r] = a.x; v[r + 1] = a.y;
+              apv[r] = ap.x; apv[r + 1] = ap.y;
+            }
+          } else {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+              apv[r] = act_g(act, v[r], g.slope);
+              v[r] = act_f(act, v[r], g.slope);
+            }
+          }
+#pragma unroll
+          for (int r = 0; r < 16; ++r)
+            __builtin_amdgcn_raw_buffer_store_b16(f2h<T16>(apv[r]), rp,
+                                                  vrow[r] == (int)PW_OOB ? (int)PW_OOB : vrow[r] / 2,
+                                                  so(r, 2), 0);
+          acted = true;
+        } else if (ypre) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r)
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v[r]), rp, vrow[r],
+                                                  so(r, 1), 0);
+        }
+        if (!acted) act_f_arr(act, v, g.slope);
+        if (accumulate) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r)
+            v[r] += __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                        ry, vrow[r], so(r, 1), 0));
+        }
+        if (y_bf16) {   // bf16 output: same rows, half the byte offsets
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const unsigned short hb = f2h<T16>(v[r]);
+            __builtin_amdgcn_raw_buffer_store_b16(hb, ryh, vrow[r] == (int)PW_OOB ? (int)PW_OOB : vrow[r] / 2,
+                                                  so(r, 2), 0);
+          }
+          continue;
+        }
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v[r]), ry, vrow[r],
+                                                so(r, 1), 0);
+      }
+    }
+  }
+}
+
 // ABF (WGRAD only) / BBF: the A (dy) / B (x, dy) operand is bf16 in HBM -- the block activation h
 // (InstanceNorm bf16 output), gelu(z) and dz of the MLPs (mlp.hip and the unfused blocks) -- and
 // is copied to LDS unconverted.
@@ -576,237 +841,7 @@ __global__ __launch_bounds__(128 * WN, WN == 2 ? 2 : 1) void pwgemm_kernel(PwArg
     }
     return;
   }
-  // FWD / DGRAD: element (m, n0+col) of image bimg lives at base + m*P + col; buffer resources
-  // are based at pixel p0 of row 0, their range ends at row M (a lane whose channel is >= M gets an
-  // offset past the range: its loads read 0, its stores are dropped).  Tile (i, j) is pixel x
-  // channel: lane lr holds channel mrow + lr, register 4q + e pixel col0 + 8q + 4lh + e -- fp32
-  // side tensors move as one 16-byte access per group q, 16-bit ones as 8-byte loads and, paired
-  // by v_permlane32_swap, two 16-byte stores per tile (cdna_hip_programming.md T21).
-  // A split-K partial (g.ws) stores the raw fp32 accumulator into its split's [b][M][P] slab; the
-  // bias, activation, side tensors and accumulation are pw_split_finish_kernel's.
-  const bool part = g.ws != nullptr;
-  float* const ybase = part ? g.ws + (long)split * g.M * g.N : g.Y;
-  const long ybs = part ? (long)g.M * g.P : g.y_bs;
-  const float* const gpre = part ? nullptr : g.gpre;
-  float* const ypre = part ? nullptr : g.ypre;
-  const int act = part ? 0 : g.act, accumulate = part ? 0 : g.accumulate, y_bf16 = part ? 0 : g.y_bf16;
-  const unsigned grange = (unsigned)(((long)g.M * g.P - p0) * 4);
-#ifdef DSG_MEASURE
-  // (g.dbg & 1: measurement builds only -- zero-range output descriptors drop every output store, so
-  // an A/B prices the epilogue's HBM writes; cdna_hip_programming.md T8)
-  const unsigned range = (g.dbg & 1) ? 0u : grange;
-#else
-  const unsigned range = grange;
-#endif
-  const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(ybase + (long)bimg * ybs + p0), (short)0, range, 0x00020000);
-  const __amdgpu_buffer_rsrc_t ryh = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)((T16*)g.Y + (long)bimg * g.y_bs + p0), (short)0, range / 2, 0x00020000);
-  __amdgpu_buffer_rsrc_t rp = ry, rg = ry;
-  // bf16 side tensors (gbf): same element offsets, byte offsets halved
-  const int esz = g.gbf ? 2 : 4;
-  if (ypre) rp = __builtin_amdgcn_make_buffer_rsrc((void*)((char*)ypre + ((long)bimg * g.ypre_bs + p0) * esz), (short)0,
-                                                   g.gbf ? range / 2 : range, 0x00020000);
-  if (gpre) rg = __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)gpre + ((long)bimg * g.gpre_bs + p0) * esz),
-                                                   (short)0, g.gbf ? grange / 2 : grange, 0x00020000);
-  // 16-bit store of this lane's 16 values: groups (q, q+1) swap halves so lanes 0-31 hold pixels
-  // 8q..8q+7 and lanes 32-63 pixels 8q+8..8q+15 of their channel (byte offset +16)
-  auto store16 = [&](__amdgpu_buffer_rsrc_t r, const float* v, int vh, int srow) __attribute__((always_inline)) {
-    unsigned d[8];
-#pragma unroll
-    for (int t = 0; t < 8; ++t) d[t] = (unsigned)f2h<T16>(v[2 * t]) | ((unsigned)f2h<T16>(v[2 * t + 1]) << 16);
-#pragma unroll
-    for (int q = 0; q < 4; q += 2) {
-#pragma unroll
-      for (int w = 0; w < 2; ++w) {
-        const auto x = __builtin_amdgcn_permlane32_swap(d[2 * q + w], d[2 * q + 2 + w], false, false);
-        d[2 * q + w] = x[0];
-        d[2 * q + 2 + w] = x[1];
-      }
-      const pu32x4 o = {d[2 * q], d[2 * q + 1], d[2 * q + 2], d[2 * q + 3]};
-      __builtin_amdgcn_raw_buffer_store_b128(o, r, vh, srow + 16 * q, 0);
-    }
-  };
-  if constexpr (SW) {
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const int col0 = wn * TN * 32 + j * 32;
-#pragma unroll
-      for (int i = 0; i < TM; ++i) {
-        const int mrow = m0 + wm * TM * 32 + i * 32;   // uniform
-        const bool ok = mrow + lr < g.M;
-        const int e0 = lr * g.P + col0 + 4 * lh;       // lane part (elements)
-        const int v4 = ok ? e0 * 4 : (int)PW_OOB;      // fp32 byte offsets; + 32 q in soffset
-        const int v2 = ok ? e0 * 2 : (int)PW_OOB;      // 16-bit loads; + 16 q
-        const int vh = ok ? (e0 - 4 * lh) * 2 + 16 * lh : (int)PW_OOB;   // paired 16-bit stores
-        const int s4 = mrow * g.P * 4, s2 = mrow * g.P * 2;
-        float v[16];
-#pragma unroll
-        for (int r = 0; r < 16; ++r) v[r] = acc[i][j][r];
-        if (gpre && g.gbf) {          // DGRAD: v *= gp, gp = act'(pre) stored 16-bit by the forward
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            uint2 u;
-            if (gpf_on) u = gpf[(GPF ? (j * TM + i) * 4 : 0) + (GPF ? q : 0)];
-            else {
-              const auto w2 = __builtin_amdgcn_raw_buffer_load_b64(rg, v2, s2 + 16 * q, 0);
-              u = make_uint2(w2[0], w2[1]);
-            }
-            v[4 * q] *= h2f<T16>((unsigned short)(u.x & 0xffffu));
-            v[4 * q + 1] *= h2f<T16>((unsigned short)(u.x >> 16));
-            v[4 * q + 2] *= h2f<T16>((unsigned short)(u.y & 0xffffu));
-            v[4 * q + 3] *= h2f<T16>((unsigned short)(u.y >> 16));
-          }
-        } else if (gpre) {
-          float gv[16];
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const float4 u = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rg, v4, s4 + 32 * q, 0));
-            gv[4 * q] = u.x; gv[4 * q + 1] = u.y; gv[4 * q + 2] = u.z; gv[4 * q + 3] = u.w;
-          }
-          act_g_mul_arr(g.gact, v, gv, g.slope);
-        }
-        bool acted = false;
-        if (ypre && g.gbf) {          // FWD: ypre <- 16-bit act'(pre), v <- act(pre) (one GELU evaluation)
-          float apv[16];
-#ifdef DSG_MEASURE
-          if (g.dbg & 2) {              // (measurement builds only: the pair without its GELU arithmetic)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) apv[r] = v[r];
-          } else
-#endif
-          if (act == ACT_GELU) {
-#pragma unroll
-            for (int r = 0; r < 16; r += 2) {
-              f32x2 a, ap;
-              gelu_pair_fast2(f32x2{v[r], v[r + 1]}, a, ap);
-              v[r] = a.x; v[r + 1] = a.y;
-              apv[r] = ap.x; apv[r + 1] = ap.y;
-            }
-          } else {
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-              apv[r] = act_g(act, v[r], g.slope);
-              v[r] = act_f(act, v[r], g.slope);
-            }
-          }
-          store16(rp, apv, vh, s2);
-          acted = true;
-        } else if (ypre) {
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const pu32x4 o = {__builtin_bit_cast(unsigned, v[4 * q]), __builtin_bit_cast(unsigned, v[4 * q + 1]),
-                              __builtin_bit_cast(unsigned, v[4 * q + 2]), __builtin_bit_cast(unsigned, v[4 * q + 3])};
-            __builtin_amdgcn_raw_buffer_store_b128(o, rp, v4, s4 + 32 * q, 0);
-          }
-        }
-        if (!acted) act_f_arr(act, v, g.slope);
-        if (accumulate) {
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const float4 u = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(ry, v4, s4 + 32 * q, 0));
-            v[4 * q] += u.x; v[4 * q + 1] += u.y; v[4 * q + 2] += u.z; v[4 * q + 3] += u.w;
-          }
-        }
-        if (y_bf16) {   // 16-bit output: same rows, half the byte offsets
-          store16(ryh, v, vh, s2);
-          continue;
-        }
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const pu32x4 o = {__builtin_bit_cast(unsigned, v[4 * q]), __builtin_bit_cast(unsigned, v[4 * q + 1]),
-                            __builtin_bit_cast(unsigned, v[4 * q + 2]), __builtin_bit_cast(unsigned, v[4 * q + 3])};
-          __builtin_amdgcn_raw_buffer_store_b128(o, ry, v4, s4 + 32 * q, 0);
-        }
-      }
-    }
-  } else {
-    const int P4 = g.P * 4;
-    const bool full = m0 + BM <= g.M;
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const int col = wn * TN * 32 + j * 32 + lr;
-#pragma unroll
-      for (int i = 0; i < TM; ++i) {
-        const int mrow = m0 + wm * TM * 32 + i * 32;   // uniform
-        // lane part of the offset: rows 4h, column col.  In a partial M tile, rows >= M get an
-        // offset past the resource range so the hardware drops the store / returns 0.
-        const int vofs = (4 * lh * g.P + col) * 4;
-        const int mlim = full ? BM : g.M - mrow - 4 * lh;   // rows (r&3)+8(r>>2) < mlim are valid
-        int vrow[16];
-#pragma unroll
-        for (int r = 0; r < 16; ++r) vrow[r] = ((r & 3) + 8 * (r >> 2) < mlim) ? vofs : (int)PW_OOB;
-        float v[16];
-#pragma unroll
-        for (int r = 0; r < 16; ++r) v[r] = acc[i][j][r];
-        if (gpre && g.gbf) {          // DGRAD: v *= gp, gp = act'(pre) stored bf16 by the forward
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const unsigned short hb = __builtin_amdgcn_raw_buffer_load_b16(
-                rg, vrow[r] == (int)PW_OOB ? (int)PW_OOB : vrow[r] / 2, (mrow + (r & 3) + 8 * (r >> 2)) * (P4 / 2), 0);
-            v[r] *= h2f<T16>(hb);
-          }
-        } else if (gpre) {
-          float gv[16];
-#pragma unroll
-          for (int r = 0; r < 16; ++r)
-            gv[r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
-                        rg, vrow[r], (mrow + (r & 3) + 8 * (r >> 2)) * P4, 0));
-          act_g_mul_arr(g.gact, v, gv, g.slope);
-        }
-        bool acted = false;
-        if (ypre && g.gbf) {          // FWD: ypre <- bf16 act'(pre), v <- act(pre) (one GELU evaluation)
-          float apv[16];
-          if (act == ACT_GELU) {
-#pragma unroll
-            for (int r = 0; r < 16; r += 2) {
-              f32x2 a, ap;
-              gelu_pair_fast2(f32x2{v[r], v[r + 1]}, a, ap);
-              v[r] = a.x; v[r + 1] = a.y;
-              apv[r] = ap.x; apv[r + 1] = ap.y;
-            }
-          } else {
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-              apv[r] = act_g(act, v[r], g.slope);
-              v[r] = act_f(act, v[r], g.slope);
-            }
-          }
-#pragma unroll
-          for (int r = 0; r < 16; ++r)
-            __builtin_amdgcn_raw_buffer_store_b16(f2h<T16>(apv[r]), rp,
-                                                  vrow[r] == (int)PW_OOB ? (int)PW_OOB : vrow[r] / 2,
-                                                  (mrow + (r & 3) + 8 * (r >> 2)) * (P4 / 2), 0);
-          acted = true;
-        } else if (ypre) {
-#pragma unroll
-          for (int r = 0; r < 16; ++r)
-            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v[r]), rp, vrow[r],
-                                                  (mrow + (r & 3) + 8 * (r >> 2)) * P4, 0);
-        }
-        if (!acted) act_f_arr(act, v, g.slope);
-        if (accumulate) {
-#pragma unroll
-          for (int r = 0; r < 16; ++r)
-            v[r] += __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
-                        ry, vrow[r], (mrow + (r & 3) + 8 * (r >> 2)) * P4, 0));
-        }
-        if (y_bf16) {   // bf16 output: same rows, half the byte offsets
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const unsigned short hb = f2h<T16>(v[r]);
-            __builtin_amdgcn_raw_buffer_store_b16(hb, ryh, vrow[r] == (int)PW_OOB ? (int)PW_OOB : vrow[r] / 2,
-                                                  (mrow + (r & 3) + 8 * (r >> 2)) * (P4 / 2), 0);
-          }
-          continue;
-        }
-#pragma unroll
-        for (int r = 0; r < 16; ++r)
-          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v[r]), ry, vrow[r],
-                                                (mrow + (r & 3) + 8 * (r >> 2)) * P4, 0);
-      }
-    }
-  }
+  pw_fd_epi<T16, BM, TM, TN, SW, GPF>(g, acc, m0, bimg, p0, split, wm, wn, lr, lh, gpf_on, gpf);
 }
 
 template <typename T16, int MODE, int BM, int ABF = 0, int BBF = 0, int BN = 128, int WN = 2, int BK = PBK, int SWP = 0,
@@ -819,6 +854,11 @@ static void pw_launch(const PwArgs& g, int splits, hipStream_t st) {
                      dim3((unsigned)((long)mt * nt * splits)), dim3(128 * WN), 0, st, g);
   ktimer_mark(st, 1);
 }
+
+// the persistent LDS-DMA ring form of the wide 16-bit FWD / DGRAD (pw_ring.h; instantiated in
+// pw_ring_{bf16,f16}.hip, so that editing it rebuilds two small units, not the six large ones)
+template <typename T16, int MODE, int SWP>
+bool pw_ring_launch(const PwArgs& g, hipStream_t st);
 
 constexpr int PW_WIDE = -1;   // tile selector: 256 x 256 tiles, 8 waves, 64-deep K steps
 
@@ -840,7 +880,8 @@ static void pw_launch_abs(const PwArgs& g, int bm, int abf, int bbf, int splits,
     case 1: pw_launch<T16, MODE, 256, 0, 1, 256, 4, 64, SWP>(g, 1, st); break;              \
     case 2: pw_launch<T16, MODE, 256, 1, 0, 256, 4, 64, SWP>(g, 1, st); break;              \
     default:                                                                      \
-      if (g.dma == 2) pw_launch<T16, MODE, 256, 1, 1, 128, 2, 32, SWP, 3>(g, 1, st);   \
+      if (g.dma == 3 && pw_ring_launch<T16, MODE, SWP>(g, st)) {                      \
+      } else if (g.dma == 2) pw_launch<T16, MODE, 256, 1, 1, 128, 2, 32, SWP, 3>(g, 1, st);   \
       else if (g.dma) pw_launch<T16, MODE, 256, 1, 1, 256, 4, 32, SWP, 4>(g, 1, st);   \
       else pw_launch<T16, MODE, 256, 1, 1, 256, 4, 64, SWP>(g, 1, st);                 \
       break;                                                                      \
@@ -1025,6 +1066,10 @@ void pw_wgrad_launch(const PwArgs& g, int bm, int abf, int bbf, int splits, hipS
   }
 }
 #define PW_EXTERN_LAUNCHERS(T16)                                                                            \
+  extern template bool pw_ring_launch<T16, PW_FWD, 0>(const PwArgs&, hipStream_t);                          \
+  extern template bool pw_ring_launch<T16, PW_FWD, 1>(const PwArgs&, hipStream_t);                          \
+  extern template bool pw_ring_launch<T16, PW_DGRAD, 0>(const PwArgs&, hipStream_t);                        \
+  extern template bool pw_ring_launch<T16, PW_DGRAD, 1>(const PwArgs&, hipStream_t);                        \
   extern template void pw_fd_launch_m<T16, PW_FWD>(const PwArgs&, int, int, int, int, hipStream_t);         \
   extern template void pw_fd_launch_m<T16, PW_DGRAD>(const PwArgs&, int, int, int, int, hipStream_t);       \
   extern template void pw_wgrad_launch<T16>(const PwArgs&, int, int, int, int, hipStream_t);

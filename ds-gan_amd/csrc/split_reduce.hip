@@ -19,6 +19,7 @@
 // runs each backward pass deferred and flushes at its end (and before every DDP bucket hook), so
 // ~160 small reduction launches per step become a handful; the caller keeps every queued scratch
 // buffer and output alive until the flush (dsgan_hip/functional.py: wsa / deferred_splits).
+#include <mutex>
 #include "common.h"
 
 #include <stdlib.h>
@@ -221,9 +222,12 @@ static void launch_segs(const RSeg* v, int n, hipStream_t st) {
 }
 
 // ---- deferred mode ----------------------------------------------------------------------
+// The queue is process state shared by the host threads that launch (the main thread and autograd's
+// backward thread, which flushes before a DDP bucket's all-reduce): every access holds g_qmu.
 static std::vector<RSeg> g_queue;
 static hipStream_t g_queue_st = nullptr;
 static int g_defer = 0;
+static std::mutex g_qmu;
 
 // output byte ranges of a segment: dw (and db)
 static void seg_ranges(const RSeg& s, uintptr_t r[4]) {
@@ -272,6 +276,7 @@ static long defer_max_bytes() {
 }
 
 static void submit(const RSeg* v, int n, hipStream_t st) {
+  std::lock_guard<std::mutex> lk(g_qmu);
   if (!g_defer) {
     launch_segs(v, n, st);
     return;
@@ -328,24 +333,42 @@ extern "C" {
 // Deferred split reductions on (1) / off (0); returns the previous setting.  Turning it off does not
 // flush: call dsgan_split_flush.
 int dsgan_split_defer(int on) {
+  std::lock_guard<std::mutex> lk(g_qmu);
   const int old = g_defer;
   g_defer = on ? 1 : 0;
   return old;
 }
 
 // Reductions queued and not yet launched.
-int dsgan_split_pending(void) { return (int)g_queue.size(); }
+int dsgan_split_pending(void) {
+  std::lock_guard<std::mutex> lk(g_qmu);
+  return (int)g_queue.size();
+}
 
-// Launch every queued reduction (on the stream its producers ran on; `st` is used only to check
-// that they agree) and empty the queue.  Returns 0, or an error code.
+// Launch every queued reduction on the stream its producers ran on and empty the queue.  When `st`
+// is another stream, it is made to wait for those launches (an event), so whatever `st` runs next
+// sees the reduced gradients.  Returns 0, or an error code (the queue is empty either way: a
+// reduction is never left queued to read scratch its caller has since released).
 int dsgan_split_flush(hipStream_t st) {
+  std::lock_guard<std::mutex> lk(g_qmu);
   if (g_queue.empty()) return 0;   // (no HIP call at all)
-  if (st != g_queue_st) {
-    dsgan_set_error("dsgan_split_flush: queued reductions belong to another stream");
-    return -1;
-  }
+  const hipStream_t qst = g_queue_st;
   flush_queue();
   DSG_CHECK_LAUNCH();
+  if (st != qst) {
+    static hipEvent_t ev = nullptr;
+    if (!ev && hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) {
+      ev = nullptr;
+      dsgan_set_error("dsgan_split_flush: no event to order stream %p after the reductions on %p", (void*)st,
+                      (void*)qst);
+      return -1;
+    }
+    if (hipEventRecord(ev, qst) != hipSuccess || hipStreamWaitEvent(st, ev, 0) != hipSuccess) {
+      dsgan_set_error("dsgan_split_flush: could not order stream %p after the reductions on %p", (void*)st,
+                      (void*)qst);
+      return -1;
+    }
+  }
   return 0;
 }
 

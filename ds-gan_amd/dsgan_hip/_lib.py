@@ -205,9 +205,19 @@ def load():
     return lib
 
 
+# Set by functional.deferred_splits(): called after every entry point with whether that call queued
+# a deferred split reduction (dsgan_split_pending rose), so that only the scratch of a call that
+# queued one is kept alive until the flush.
+DEFER_HOOK = [None]
+
+
 def call(name, *args):
     lib = load()
+    hook = DEFER_HOOK[0]
+    n0 = lib.dsgan_split_pending() if hook is not None else 0
     rc = getattr(lib, name)(*args)
+    if hook is not None:
+        hook(lib.dsgan_split_pending() > n0)
     if rc != 0:
         msg = lib.dsgan_last_error_string()
         raise RuntimeError("%s failed (rc=%d): %s" % (name, rc, msg.decode() if msg else ""))

@@ -89,9 +89,15 @@ class GradBuckets:
 
     ``layout`` = [(param, offset, numel)] in buffer order.  Buckets are contiguous ranges of about
     ``bucket_mb`` cut at parameter boundaries; ``arm()`` before the backward, ``ready(params)``
-    from functional.GRAD_READY as weight-grads are launched (a bucket starts when its last
-    parameter is reported), ``finish()`` after the backward: launches the buckets that are not
-    complete (parameters never reported) and waits for all of them."""
+    from functional.GRAD_READY as weight-grads are launched, ``finish()`` after the backward:
+    launches the buckets that are not complete (parameters never reported) and waits for all of them.
+
+    Buckets are launched strictly in index order: bucket i starts once it and every bucket before it
+    are complete.  Collectives pair up across ranks by issue order, so the sequence must not depend
+    on the order in which one rank's backward happens to report its parameters -- it is 0, 1, 2, ...
+    on every rank (tests/test_host_cpu.py::test_grad_buckets_same_sequence_under_perturbed_order).
+    The flat buffer is laid out in backward order, so in the step bucket 0 completes first and the
+    in-order rule costs no overlap."""
 
     def __init__(self, grad, layout, bucket_mb=24):
         self.grad = grad
@@ -112,11 +118,15 @@ class GradBuckets:
         self.pending = None
         self.works = None
         self.launched = None
+        self.next = 0              # the next bucket to launch (in index order)
+        self.sequence = []         # bucket indices in launch order (this step)
 
     def arm(self):
         self.pending = [set(b[2]) for b in self.buckets]
         self.works = []
         self.launched = [False] * len(self.buckets)
+        self.next = 0
+        self.sequence = []
         HF.GRAD_READY[0] = self.ready
 
     def _launch(self, i):
@@ -124,6 +134,7 @@ class GradBuckets:
             HF.split_flush()   # the bucket's weight-grads may still sit in the deferred split reductions
             s, e = self.buckets[i][0], self.buckets[i][1]
             self.launched[i] = True
+            self.sequence.append(i)
             self.works.append(_allreduce_avg(self.grad[s:e], True))
 
     def ready(self, params):
@@ -132,13 +143,15 @@ class GradBuckets:
             if i is None or self.launched[i]:
                 continue
             self.pending[i].discard(id(p))
-            if not self.pending[i]:
-                self._launch(i)
+        while self.next < len(self.buckets) and not self.pending[self.next]:
+            self._launch(self.next)
+            self.next += 1
 
     def finish(self):
         HF.GRAD_READY[0] = None
-        for i in range(len(self.buckets)):
+        for i in range(self.next, len(self.buckets)):
             self._launch(i)
+        self.next = len(self.buckets)
         for w in self.works:
             w.wait()
         _post_scale(self.grad, world_size())

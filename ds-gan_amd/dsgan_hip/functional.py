@@ -24,10 +24,12 @@ from ._lib import call, ptr, stream
 def wsa(t):
     """(pointer, element count) of a scratch tensor (None -> NULL, 0): every scratch-taking entry
     point takes the buffer's size right after it and refuses an undersized one (include/dsgan_hip.h).
-    Inside deferred_splits() the tensor stays referenced until split_flush(): a queued split
-    reduction reads it after the call has returned."""
+    Inside deferred_splits() the tensor is a keep-alive candidate of the call it is passed to: held
+    until split_flush() when that call queued a split reduction (which reads it after the call has
+    returned), dropped otherwise (InstanceNorm workspaces, forward scratch and the like
+    are not held for the whole backward pass)."""
     if t is not None and _DEFER_KEEP[0] is not None:
-        _DEFER_KEEP[0].append(t)
+        _DEFER_CAND.append(t)
     return (ptr(t), t.numel() if t is not None else 0)
 
 
@@ -36,15 +38,23 @@ def wsa(t):
 # block's end issues the queue as a few batched launches -- ~160 small reduction launches per
 # training step become a handful.  Only parameter gradients go through these reductions, and they
 # are read only after the backward pass (the optimizer, the non-finite guard) or by the DDP bucket
-# all-reduce, which flushes first (dist.GradBuckets._launch).  The queued scratch buffers (wsa) and
-# scratch outputs (_keep) are held until the flush.
+# all-reduce, which flushes first (dist.GradBuckets._launch).  The scratch of a call that queued a
+# reduction (wsa, _keep) is held until the flush.
 DEFER_SPLITS = [os.environ.get("DSGAN_DEFER_SPLITS", "1") != "0"]   # (=0: immediate, for A/B runs)
 _DEFER_KEEP = [None]
+_DEFER_CAND = []
+
+
+def _defer_hook(queued):
+    """_lib.call's report after each entry point: keep that call's candidates if it queued a reduction."""
+    if queued and _DEFER_KEEP[0] is not None:
+        _DEFER_KEEP[0].extend(_DEFER_CAND)
+    _DEFER_CAND.clear()
 
 
 def _keep(t):
     if _DEFER_KEEP[0] is not None:
-        _DEFER_KEEP[0].append(t)
+        _DEFER_CAND.append(t)
     return t
 
 
@@ -55,6 +65,7 @@ def split_flush():
         call("dsgan_split_flush", stream())
     if _DEFER_KEEP[0] is not None:
         _DEFER_KEEP[0] = []
+    _DEFER_CAND.clear()
 
 
 @contextlib.contextmanager
@@ -66,15 +77,19 @@ def deferred_splits():
         return
     lib = _lib.load()
     _DEFER_KEEP[0] = []
+    _DEFER_CAND.clear()
+    _lib.DEFER_HOOK[0] = _defer_hook
     lib.dsgan_split_defer(1)
     try:
         yield
     finally:
         lib.dsgan_split_defer(0)
+        _lib.DEFER_HOOK[0] = None
         try:
             split_flush()
         finally:
             _DEFER_KEEP[0] = None
+            _DEFER_CAND.clear()
 
 
 # PatchGAN 4x4 weight-grads also sum the conv's bias grad from their staged dy tiles

@@ -34,7 +34,7 @@ pytestmark = pytest.mark.gpu
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def _model(precision="fp32"):
+def _model(precision="fp32", batch=2):
     import dsgan_hip
     from oracle import dsgan_cpu as O
     from oracle.recipe import make_params
@@ -43,7 +43,7 @@ def _model(precision="fp32"):
     dsgan_hip.require_gpu()
     random.seed(20)
     torch.manual_seed(20)
-    m = create_model(default_train_opt(gpu_ids=[0], pool_size=0, precision=precision, batchSize=2))
+    m = create_model(default_train_opt(gpu_ids=[0], pool_size=0, precision=precision, batchSize=batch))
     with torch.no_grad():
         for net, pr in ((m.netG, make_params(O.g_param_spec(), "fanin", 1000)),
                         (m.netD, make_params(O.d_param_spec(), "fanin", 5000)),
@@ -64,7 +64,7 @@ def _grads_and_params(m):
             "loss_G": float(m.loss_G), "loss_D": float(m.loss_D)}
 
 
-def _worker(rank, world, port, out_dir):
+def _worker(rank, world, port, out_dir, precision="fp32", size=64, per_rank=1):
     import sys
     sys.path[:0] = [REPO, os.path.join(REPO, "ds-gan_amd")]
     import torch.distributed as dist
@@ -72,11 +72,11 @@ def _worker(rank, world, port, out_dir):
     torch.cuda.set_device(0)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from oracle.recipe import synth_pair
-    m = _model()
+    m = _model(precision, world * per_rank)
     assert m.g_buckets is not None and len(m.g_buckets.buckets) >= 3
-    A, B = synth_pair(2, 64, seed=4)
-    sl = slice(rank, rank + 1)
-    m.set_input({"A": A[sl].cuda(), "B": B[sl].cuda(), "A_paths": ["a"], "B_paths": ["b"]})
+    A, B = synth_pair(world * per_rank, size, seed=4)
+    sl = slice(rank * per_rank, (rank + 1) * per_rank)
+    m.set_input({"A": A[sl].cuda(), "B": B[sl].cuda(), "A_paths": ["a"] * per_rank, "B_paths": ["b"] * per_rank})
     m.optimize_parameters()
     res = _grads_and_params(m)
     torch.save(res, os.path.join(out_dir, "rank%d.pt" % rank))
@@ -86,6 +86,45 @@ def _worker(rank, world, port, out_dir):
 
 def _rel(a, b):
     return ((a.double() - b.double()).norm() / max(b.double().norm().item(), 1e-30)).item()
+
+
+def _two_ranks(tmp_path, precision="fp32", size=64, per_rank=1):
+    import multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    port = 33500 + random.randint(0, 2000)
+    ps = [ctx.Process(target=_worker, args=(r, 2, port, str(tmp_path), precision, size, per_rank)) for r in range(2)]
+    for p in ps:
+        p.start()
+    for p in ps:
+        p.join(timeout=300)
+    assert all(p.exitcode == 0 for p in ps), [p.exitcode for p in ps]
+    return (torch.load(tmp_path / "rank0.pt", weights_only=True), torch.load(tmp_path / "rank1.pt", weights_only=True))
+
+
+def test_two_ranks_equal_one_process_bf16_256(tmp_path):
+    """the same equivalence in the bench's mode -- bf16 MFMA operands, the
+    stacked batch-2N D pass (pix2pix_model.D_BATCH), the bf16 non-finite guard -- at 256^2 with two
+    images per rank: both ranks bitwise equal, and the averaged gradients equal one process training
+    all four images to fp32 reassociation (every per-sample operand, bf16 rounding included, is the
+    same in both runs; only the batch sums of the weight-grads split differently)."""
+    from oracle.recipe import synth_pair
+    from models import pix2pix_model as PM
+    assert PM.D_BATCH
+    r0, r1 = _two_ranks(tmp_path, "bf16", 256, 2)
+    m = _model("bf16", 4)
+    assert m.d_batch
+    A, B = synth_pair(4, 256, seed=4)
+    m.set_input({"A": A.cuda(), "B": B.cuda(), "A_paths": ["a"] * 4, "B_paths": ["b"] * 4})
+    m.optimize_parameters()
+    one = _grads_and_params(m)
+    for k in ("gG", "gD", "pG", "pD"):
+        assert torch.equal(r0[k], r1[k]), k
+    assert abs(0.5 * (r0["loss_D"] + r1["loss_D"]) - one["loss_D"]) <= 1e-5 * abs(one["loss_D"])
+    assert torch.isfinite(r0["gG"]).all() and torch.isfinite(r0["gD"]).all()
+    assert _rel(r0["gD"], one["gD"]) < 1e-4, _rel(r0["gD"], one["gD"])
+    assert _rel(r0["gG"], one["gG"]) < 2e-3, _rel(r0["gG"], one["gG"])
+    big = one["gD"].abs() > 1e-6
+    assert (r0["pD"][big] - one["pD"][big]).abs().max().item() < 1e-6
 
 
 def test_two_ranks_equal_one_process(tmp_path):

@@ -23,14 +23,20 @@ def test_deferred_splits_keeps_scratch_alive_and_restores_state():
     lib = _lib.load()
     assert HF._DEFER_KEEP[0] is None
     t = torch.empty(8)   # (wsa only reads the pointer and size of a device tensor; a CPU one stands in)
+    u = torch.empty(4)
     with HF.deferred_splits():
         assert HF._DEFER_KEEP[0] == []
+        assert _lib.DEFER_HOOK[0] is not None     # _lib.call reports whether each call queued a reduction
         assert lib.dsgan_split_defer(1) == 1   # the C queue is on inside the block
         HF._keep(t)
+        _lib.DEFER_HOOK[0](True)             # that call queued a reduction: its scratch is held
         assert HF._DEFER_KEEP[0][-1] is t
+        HF._keep(u)
+        _lib.DEFER_HOOK[0](False)            # this one queued nothing: its scratch is not held
+        assert all(x is not u for x in HF._DEFER_KEEP[0]) and not HF._DEFER_CAND
         with HF.deferred_splits():          # nested: a no-op, the outer block owns the flush
             assert HF._DEFER_KEEP[0] and HF._DEFER_KEEP[0][-1] is t
-    assert HF._DEFER_KEEP[0] is None
+    assert HF._DEFER_KEEP[0] is None and _lib.DEFER_HOOK[0] is None
     assert lib.dsgan_split_defer(0) == 0       # turned off again at the block's end
     assert lib.dsgan_split_pending() == 0
 

@@ -190,14 +190,72 @@ def _bucket_worker(rank, world, port, q):
     grad = torch.arange(off, dtype=torch.float32) * (rank + 1)
     gb = hdist.GradBuckets(grad, layout, bucket_mb=2)     # ~524k floats per bucket
     gb.arm()
-    # backward reports parameters (as the Functions do), in reverse layout order, one skipped
-    for p in reversed(params[1:]):
+    # backward reports parameters (as the Functions do) in layout order -- the flat buffer is laid
+    # out in backward order -- with the last one never reported
+    for p in params[:-1]:
         HF.GRAD_READY[0]([p])
     early = sum(gb.launched)
     n_early = gb.finish()
     q.put((rank, grad.tolist() == (torch.arange(off, dtype=torch.float32) * 1.5).tolist(), len(gb.buckets), early,
            n_early, HF.GRAD_READY[0] is None))
     dist.destroy_process_group()
+
+
+def _bucket_order_worker(rank, world, port, q):
+    import random as _r
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from dsgan_hip import dist as hdist
+    from dsgan_hip import functional as HF
+    sizes = [300000, 7, 400000, 64, 250000, 1000, 600000, 5, 123, 300000, 77]
+    params = [torch.nn.Parameter(torch.zeros(k)) for k in sizes]
+    layout, off = [], 0
+    for p in params:
+        layout.append((p, off, p.numel()))
+        off += (p.numel() + 63) // 64 * 64
+    grad = torch.arange(off, dtype=torch.float32) * (rank + 1)
+    gb = hdist.GradBuckets(grad, layout, bucket_mb=1)     # ~262k floats per bucket: most params alone
+    seqs = []
+    for trial in range(4):
+        grad.copy_(torch.arange(off, dtype=torch.float32) * (rank + 1))
+        gb.arm()
+        order = list(range(len(params)))
+        _r.Random(1000 * rank + trial).shuffle(order)      # each rank's backward reports in its own order
+        for k in order[:-2]:
+            HF.GRAD_READY[0]([params[k]])
+        HF.GRAD_READY[0]([params[order[-2]], params[order[-1]]])
+        gb.finish()
+        seqs.append(list(gb.sequence))
+        assert grad.tolist() == (torch.arange(off, dtype=torch.float32) * 1.5).tolist()
+    q.put((rank, seqs, len(gb.buckets)))
+    dist.destroy_process_group()
+
+
+def test_grad_buckets_same_sequence_under_perturbed_order():
+    """collectives pair up across ranks by issue order, so GradBuckets must issue
+    the same bucket sequence on every rank even when the ranks' backward passes report their
+    parameters in different orders.  Two gloo ranks, four steps, each rank reporting in its own
+    random order: the launch sequences are identical (0, 1, 2, ... -- buckets go out in index order
+    as they complete) and every step's result is the mean of the two ranks' gradients."""
+    import multiprocessing as mp
+    import random as _r
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29500 + _r.randint(0, 1500)
+    ps = [ctx.Process(target=_bucket_order_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    out = dict((v[0], v[1:]) for v in (q.get(timeout=120) for _ in ps))
+    for p in ps:
+        p.join(timeout=60)
+    assert all(p.exitcode == 0 for p in ps), [p.exitcode for p in ps]
+    (s0, nb0), (s1, nb1) = out[0], out[1]
+    assert nb0 == nb1 and nb0 >= 5
+    assert s0 == s1
+    for seq in s0:
+        assert seq == list(range(nb0))
 
 
 def test_grad_buckets_gloo_world2():

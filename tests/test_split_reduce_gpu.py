@@ -103,7 +103,10 @@ def test_deferred_queue_overlap_and_order():
         assert np.array_equal(t.cpu().numpy().view(np.uint32), canon_sum(parts[i]).view(np.uint32)), i
 
 
-def test_flush_refuses_foreign_stream():
+def test_flush_from_a_foreign_stream_orders_it():
+    """a flush called with another stream than the queued reductions' launches them on
+    their own stream and makes the caller's stream wait for them (an event): the queue is empty
+    afterwards and work on the caller's stream reads the reduced values."""
     L = _lib()
     lib = L.load()
     part = torch.randn(9, 64, device="cuda")
@@ -113,12 +116,15 @@ def test_flush_refuses_foreign_stream():
         L.call("dsgan_colsum", L.ptr(part), 9, 64, L.ptr(out), L.stream())
     finally:
         lib.dsgan_split_defer(old)
+    assert lib.dsgan_split_pending() == 1
     side = torch.cuda.Stream()
-    with pytest.raises(RuntimeError, match="another stream"):
-        L.call("dsgan_split_flush", side.cuda_stream)
-    L.call("dsgan_split_flush", L.stream())
+    side.wait_stream(torch.cuda.current_stream())
+    L.call("dsgan_split_flush", side.cuda_stream)
+    assert lib.dsgan_split_pending() == 0
+    with torch.cuda.stream(side):
+        copy = out.clone()          # ordered after the reduction by the flush's event
     torch.cuda.synchronize()
-    assert torch.equal(out.cpu(), torch.from_numpy(canon_sum(part.cpu().numpy())))
+    assert torch.equal(copy.cpu(), torch.from_numpy(canon_sum(part.cpu().numpy())))
 
 
 @pytest.mark.parametrize("prec,size", [("bf16", 256), ("fp32", 64), ("fp16", 128)])
