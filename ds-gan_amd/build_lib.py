@@ -27,6 +27,14 @@ FLAGS = ["-O3", "-fPIC", "-std=c++17", "--offload-arch=" + ARCH, "-Wno-unused-re
 
 # per-source extra flags
 EXTRA = {"dwconv.hip": ["-fno-slp-vectorize"], "mlp.hip": ["-fno-slp-vectorize"], "thin3.hip": ["-fno-slp-vectorize"]}
+# The pointwise GEMM units: their epilogue loops (8 accumulator blocks, every epilogue option) must
+# unroll fully -- the accumulators and the prefetched gp registers are indexed by the loop counters --
+# and LLVM's default budget for a #pragma unroll (16K instructions) refused them once the 16-byte
+# stores carried their hazard pad (pw_impl.h pw_st128): "loop not unrolled", the arrays went to
+# scratch and the gp-multiplied data-grad ran 8x slower.
+for _f in ("pw_fwd_bf16.hip", "pw_fwd_f16.hip", "pw_dgrad_bf16.hip", "pw_dgrad_f16.hip", "pw_wgrad_bf16.hip",
+           "pw_wgrad_f16.hip", "pw_ring_bf16.hip", "pw_ring_f16.hip", "pwgemm.hip"):
+    EXTRA[_f] = ["-mllvm", "-pragma-unroll-threshold=200000", "-Werror=pass-failed"]
 
 
 def _includes(path, seen=None):

@@ -109,11 +109,13 @@ __device__ __forceinline__ hx4<T16> cvt4(float4 v, int bact, float slope) {
 // issue).  hipcc models that hazard only for buffer stores whose soffset is not a register, and ours
 // always have one: in the persistent ring kernel it scheduled "buffer_store_dwordx4 v[138:141], ...,
 // s1; v_or_b32 v138, ..." and some lanes stored the new v138 (tests/test_ops_gpu.py
-// test_pw_persistent_ring_bitwise, tools/probe/ring_diff.py).  So the store is inline asm with the
-// pad inside the string (cdna_hip_programming.md section 5.7 item 2); hipcc does not count it in
-// its own vmcnt waits, which only makes those waits conservative.
+// test_pw_persistent_ring_bitwise, tools/probe/ring_diff.py).  The store stays the builtin (hipcc
+// counts it in its vmcnt waits: an inline-asm store it cannot see made every later load wait for all
+// earlier stores -- the gp-multiplied data-grad ran 8x slower), and an s_nop that reads the data
+// registers follows it: they stay allocated until two wait states after the store.
 __device__ __forceinline__ void pw_st128(pu32x4 v, __amdgpu_buffer_rsrc_t r, int voff, int soff) {
-  asm volatile("buffer_store_dwordx4 %0, %1, %2, %3 offen\n\ts_nop 1" ::"v"(v), "v"(voff), "s"(r), "s"(soff) : "memory");
+  __builtin_amdgcn_raw_buffer_store_b128(v, r, voff, soff, 0);
+  asm volatile("s_nop 1" ::"v"(v));
 }
 
 // FWD / DGRAD epilogue of one output tile (the one-tile kernel and the persistent ring kernel):
