@@ -33,7 +33,7 @@ EXTRA = {"dwconv.hip": ["-fno-slp-vectorize"], "mlp.hip": ["-fno-slp-vectorize"]
 # stores carried their hazard pad (pw_impl.h pw_st128): "loop not unrolled", the arrays went to
 # scratch and the gp-multiplied data-grad ran 8x slower.
 for _f in ("pw_fwd_bf16.hip", "pw_fwd_f16.hip", "pw_dgrad_bf16.hip", "pw_dgrad_f16.hip", "pw_wgrad_bf16.hip",
-           "pw_wgrad_f16.hip", "pw_ring_bf16.hip", "pw_ring_f16.hip", "pwgemm.hip"):
+           "pw_wgrad_f16.hip", "pwgemm.hip"):
     EXTRA[_f] = ["-mllvm", "-pragma-unroll-threshold=200000", "-Werror=pass-failed"]
 
 

@@ -107,9 +107,9 @@ __device__ __forceinline__ hx4<T16> cvt4(float4 v, int bact, float slope) {
 // 16-byte buffer store followed by its wait states.  A VALU write to a VGPR that still holds the
 // data of a preceding store of more than 8 bytes needs a wait state (the store reads its data after
 // issue).  hipcc models that hazard only for buffer stores whose soffset is not a register, and ours
-// always have one: in the persistent ring kernel it scheduled "buffer_store_dwordx4 v[138:141], ...,
-// s1; v_or_b32 v138, ..." and some lanes stored the new v138 (tests/test_ops_gpu.py
-// test_pw_persistent_ring_bitwise, tools/probe/ring_diff.py).  The store stays the builtin (hipcc
+// always have one: in round 6's persistent ring kernel (measured, removed) it scheduled
+// "buffer_store_dwordx4 v[138:141], ..., s1; v_or_b32 v138, ..." and some lanes stored the new v138
+// (1.4e-4 of one output's elements, bitwise test vs the one-tile kernel).  The store stays the builtin (hipcc
 // counts it in its vmcnt waits: an inline-asm store it cannot see made every later load wait for all
 // earlier stores -- the gp-multiplied data-grad ran 8x slower), and an s_nop that reads the data
 // registers follows it: they stay allocated until two wait states after the store.
@@ -118,14 +118,9 @@ __device__ __forceinline__ void pw_st128(pu32x4 v, __amdgpu_buffer_rsrc_t r, int
   asm volatile("s_nop 1" ::"v"(v));
 }
 
-// FWD / DGRAD epilogue of one output tile (the one-tile kernel and the persistent ring kernel):
-// bias already in the accumulators; side tensors, activation, accumulation and the stores.
-// EPI: PW_EPI_ANY reads every epilogue option from g at run time; the persistent ring kernel
-// compiles the two forms it serves with the options fixed (less code, fewer live registers):
-// PW_EPI_GELU_PAIR = 16-bit y = gelu(z) and 16-bit act'(z) to ypre, no side input, no accumulate;
-// PW_EPI_PLAIN = y = z (no ypre / gpre / activation; accumulate and the output type from g).
-enum PwEpi : int { PW_EPI_ANY = 0, PW_EPI_GELU_PAIR = 1, PW_EPI_PLAIN = 2 };
-template <typename T16, int BM, int TM, int TN, bool SW, bool GPF, int EPI = PW_EPI_ANY>
+// FWD / DGRAD epilogue of one output tile: bias already in the accumulators; side tensors,
+// activation, accumulation and the stores.
+template <typename T16, int BM, int TM, int TN, bool SW, bool GPF>
 __device__ __forceinline__ void pw_fd_epi(const PwArgs& g, pf32x16 (&acc)[TM][TN], int m0, int bimg, int p0, int split,
                                           int wm, int wn, int lr, int lh, bool gpf_on, const uint2* gpf) {
   // FWD / DGRAD: element (m, n0+col) of image bimg lives at base + m*P + col; buffer resources
@@ -136,15 +131,13 @@ __device__ __forceinline__ void pw_fd_epi(const PwArgs& g, pf32x16 (&acc)[TM][TN
   // by v_permlane32_swap, two 16-byte stores per tile (cdna_hip_programming.md T21).
   // A split-K partial (g.ws) stores the raw fp32 accumulator into its split's [b][M][P] slab; the
   // bias, activation, side tensors and accumulation are pw_split_finish_kernel's.
-  const bool part = EPI == PW_EPI_ANY && g.ws != nullptr;
+  const bool part = g.ws != nullptr;
   float* const ybase = part ? g.ws + (long)split * g.M * g.N : g.Y;
   const long ybs = part ? (long)g.M * g.P : g.y_bs;
-  const float* const gpre = (part || EPI != PW_EPI_ANY) ? nullptr : g.gpre;
-  float* const ypre = (part || EPI == PW_EPI_PLAIN) ? nullptr : g.ypre;
-  const int act = part ? 0 : EPI == PW_EPI_GELU_PAIR ? ACT_GELU : EPI == PW_EPI_PLAIN ? ACT_NONE : g.act;
-  const int accumulate = (part || EPI == PW_EPI_GELU_PAIR) ? 0 : g.accumulate;
-  const int y_bf16 = part ? 0 : EPI == PW_EPI_GELU_PAIR ? 1 : g.y_bf16;
-  const int gbf = EPI == PW_EPI_GELU_PAIR ? 1 : g.gbf;
+  const float* const gpre = part ? nullptr : g.gpre;
+  float* const ypre = part ? nullptr : g.ypre;
+  const int act = part ? 0 : g.act, accumulate = part ? 0 : g.accumulate, y_bf16 = part ? 0 : g.y_bf16;
+  const int gbf = g.gbf;
   const unsigned grange = (unsigned)(((long)g.M * g.P - p0) * 4);
 #ifdef DSG_MEASURE
   // (g.dbg & 1: measurement builds only -- zero-range output descriptors drop every output store, so
@@ -278,7 +271,6 @@ __device__ __forceinline__ void pw_fd_epi(const PwArgs& g, pf32x16 (&acc)[TM][TN
   } else {
     const int P4 = g.P * 4;
     const bool full = m0 + BM <= g.M;
-    constexpr bool VROW = EPI != PW_EPI_ANY;
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
       const int col = wn * TN * 32 + j * 32 + lr;
@@ -291,13 +283,9 @@ __device__ __forceinline__ void pw_fd_epi(const PwArgs& g, pf32x16 (&acc)[TM][TN
         const int mlim = full ? BM : g.M - mrow - 4 * lh;   // rows (r&3)+8(r>>2) < mlim are valid
         int vrow[16];
 #pragma unroll
-        for (int r = 0; r < 16; ++r)
-          vrow[r] = ((r & 3) + 8 * (r >> 2) < mlim) ? vofs + (VROW ? ((r & 3) + 8 * (r >> 2)) * P4 : 0) : (int)PW_OOB;
-        // the row of register r as a scalar offset (mrow + its row) * P4 -- or, in the ring kernel's fixed
-        // forms, in the lane's vector offset beside the column: 16 fewer scalars live across its loop
-        auto so = [&](int r, int div) __attribute__((always_inline)) {
-          return VROW ? mrow * (P4 / div) : (mrow + (r & 3) + 8 * (r >> 2)) * (P4 / div);
-        };
+        for (int r = 0; r < 16; ++r) vrow[r] = ((r & 3) + 8 * (r >> 2) < mlim) ? vofs : (int)PW_OOB;
+        // the row of register r as a scalar offset
+        auto so = [&](int r, int div) __attribute__((always_inline)) { return (mrow + (r & 3) + 8 * (r >> 2)) * (P4 / div); };
         float v[16];
 #pragma unroll
         for (int r = 0; r < 16; ++r) v[r] = acc[i][j][r];
@@ -857,11 +845,6 @@ static void pw_launch(const PwArgs& g, int splits, hipStream_t st) {
   ktimer_mark(st, 1);
 }
 
-// the persistent LDS-DMA ring form of the wide 16-bit FWD / DGRAD (pw_ring.h; instantiated in
-// pw_ring_{bf16,f16}.hip, so that editing it rebuilds two small units, not the six large ones)
-template <typename T16, int MODE, int SWP>
-bool pw_ring_launch(const PwArgs& g, hipStream_t st);
-
 constexpr int PW_WIDE = -1;   // tile selector: 256 x 256 tiles, 8 waves, 64-deep K steps
 
 // FWD / DGRAD launch over (tile rows, bf16 weight, bf16 activation, 16-bit output)
@@ -882,8 +865,7 @@ static void pw_launch_abs(const PwArgs& g, int bm, int abf, int bbf, int splits,
     case 1: pw_launch<T16, MODE, 256, 0, 1, 256, 4, 64, SWP>(g, 1, st); break;              \
     case 2: pw_launch<T16, MODE, 256, 1, 0, 256, 4, 64, SWP>(g, 1, st); break;              \
     default:                                                                      \
-      if (g.dma == 3 && pw_ring_launch<T16, MODE, SWP>(g, st)) {                      \
-      } else if (g.dma == 2) pw_launch<T16, MODE, 256, 1, 1, 128, 2, 32, SWP, 3>(g, 1, st);   \
+      if (g.dma == 2) pw_launch<T16, MODE, 256, 1, 1, 128, 2, 32, SWP, 3>(g, 1, st);   \
       else if (g.dma) pw_launch<T16, MODE, 256, 1, 1, 256, 4, 32, SWP, 4>(g, 1, st);   \
       else pw_launch<T16, MODE, 256, 1, 1, 256, 4, 64, SWP>(g, 1, st);                 \
       break;                                                                      \
@@ -1068,10 +1050,6 @@ void pw_wgrad_launch(const PwArgs& g, int bm, int abf, int bbf, int splits, hipS
   }
 }
 #define PW_EXTERN_LAUNCHERS(T16)                                                                            \
-  extern template bool pw_ring_launch<T16, PW_FWD, 0>(const PwArgs&, hipStream_t);                          \
-  extern template bool pw_ring_launch<T16, PW_FWD, 1>(const PwArgs&, hipStream_t);                          \
-  extern template bool pw_ring_launch<T16, PW_DGRAD, 0>(const PwArgs&, hipStream_t);                        \
-  extern template bool pw_ring_launch<T16, PW_DGRAD, 1>(const PwArgs&, hipStream_t);                        \
   extern template void pw_fd_launch_m<T16, PW_FWD>(const PwArgs&, int, int, int, int, hipStream_t);         \
   extern template void pw_fd_launch_m<T16, PW_DGRAD>(const PwArgs&, int, int, int, int, hipStream_t);       \
   extern template void pw_wgrad_launch<T16>(const PwArgs&, int, int, int, int, hipStream_t);

@@ -45,9 +45,11 @@ static void pw_fd_launch(int mode, const PwArgs& g, int bm, int abf, int bbf, in
 //   392 us for the 512-channel gelu-pair forward); 0 = register-staged everywhere.
 //   [10] measurement builds only (build_lib.py --measure, DSG_MEASURE; ignored otherwise): bit 0 =
 //   FWD / DGRAD epilogues drop their output stores (prices the writes), bit 1 = the gelu-pair
-//   epilogue skips its GELU arithmetic (prices the VALU).  [11] the LDS-DMA ring FWD / DGRAD as the
-//   persistent 8-wave kernel (pw_impl.h pwgemm_ring_kernel: one workgroup per CU walks its tiles,
-//   the ring runs on across tiles, the epilogue stores drain under the next tile's K loop).
+//   epilogue skips its GELU arithmetic (prices the VALU).  [11] retired: the persistent forms of the
+//   gelu-pair forward (round 5, one wave per SIMD: 1.8x slower) and of the whole 8-wave LDS-DMA ring
+//   (round 6: bitwise equal, 259.6 vs 267.9 us on the 512 -> 2048 gelu-pair forward, +3 % on the
+//   1024 -> 4096 one, the step's pointwise launches 2958 vs 2960 us) were measured and removed
+//   (DESIGN.md section 9).
 static int g_tune[12] = {1, 512, 256, 4, 0, 0, 0, 0, 1, 1, 0, 0};
 
 // the LDS-DMA ring form's conditions (full 256 x 256 tiles, 32-deep K steps, 16-byte pieces)
@@ -58,22 +60,7 @@ static int dma_ok(const PwArgs& g, int bm, int abf, int bbf, int mode) {
   const bool ok = mode == PW_WGRAD ? g_tune[9] >= 3 && g.N % 256 == 0 && g.P % 32 == 0 && (g.k_split % 32) == 0
                                    : g.K % 32 == 0 && g.P % 256 == 0 && g.k_split == 0;
   if (!ok) return 0;
-  if (g_tune[9] == 2) return 2;
-  // the persistent ring (pw_impl.h pwgemm_ring_kernel): FWD / DGRAD with >= 4 K steps (its bias slots)
-  if (g_tune[11] && mode != PW_WGRAD && g.K >= 128) return 3;
-  return 1;
-}
-
-int pw_cu_count() {
-  static int n = 0;
-  if (n == 0) {
-    int dev = 0, v = 0;
-    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-        v <= 0)
-      v = 256;
-    n = v;
-  }
-  return n;
+  return g_tune[9] == 2 ? 2 : 1;
 }
 
 // tile choice with the knob overrides of the two epilogue-heavy forms

@@ -1622,66 +1622,6 @@ def test_mlp_bwd_c256_forms_bitwise(half, N, H):
 
 
 @pytest.mark.parametrize("half", HALVES)
-@pytest.mark.parametrize("form", ["fwd16", "fwd32", "fwd_gelu_pair", "fwd_nobias", "dgrad32", "dgrad16"])
-@pytest.mark.parametrize("M,K,HW,NB", [(512, 256, 128 * 128, 4),     # 512 tiles: 2 per workgroup
-                                       (768, 128, 64 * 64, 25),      # 1200 tiles, uneven over XCDs / CUs; 4 K steps
-                                       (256, 1024, 64 * 64, 16)])    # 256 tiles: one each; 32 K steps
-def test_pw_persistent_ring_bitwise(half, form, M, K, HW, NB):
-    """The persistent LDS-DMA ring (pw_impl.h pwgemm_ring_kernel, planner knob dsgan_pw_tune(11)):
-    one workgroup per CU walks its tiles, the ring runs on across tiles and the stage waits are
-    counted so the epilogue stores drain under the next tile's K loop.  The same MFMAs in the same
-    order as the one-tile ring kernel (the bias rides in by LDS-DMA and starts the accumulators), so
-    every output is bitwise equal to it -- at several tiles per workgroup, an uneven tile count, the
-    shortest K it takes (4 steps) and a long one; outputs pre-filled with NaN."""
-    import dsgan_hip
-    from dsgan_hip import _lib, functional as HF
-    from dsgan_hip._lib import call, ptr, stream
-    lib = _lib.load()
-    dsgan_hip.set_precision(half)
-    hd = _hdt(half)
-    g0 = torch.Generator(device=DEV).manual_seed(M + K + NB)
-    fwd = form.startswith("fwd")
-    # FWD: W [M][K], x [NB][K][HW] -> y [NB][M][HW];  DGRAD: W [K][M] (the [in][out] operand), dy [NB][K][HW] -> dx [NB][M][HW]
-    w = (torch.randn(M, K, device=DEV, generator=g0) / K ** 0.5).to(hd) if fwd else \
-        (torch.randn(K, M, device=DEV, generator=g0) / K ** 0.5).to(hd)
-    bias = torch.randn(M, device=DEV, generator=g0) if form in ("fwd16", "fwd32", "fwd_gelu_pair") else None
-    x = torch.randn(NB, K, HW, device=DEV, generator=g0).to(hd)
-    old9, old11 = lib.dsgan_pw_tune(9, -1), lib.dsgan_pw_tune(11, -1)
-
-    def run(pers):
-        lib.dsgan_pw_tune(9, 1)
-        lib.dsgan_pw_tune(11, pers)
-        y16 = form in ("fwd16", "fwd_gelu_pair", "fwd_nobias", "dgrad16")
-        y = torch.full((NB, M, HW), float("nan"), device=DEV, dtype=hd if y16 else torch.float32)
-        if fwd:
-            gp = torch.full((NB, M, HW), float("nan"), device=DEV, dtype=hd) if form == "fwd_gelu_pair" else None
-            ws = torch.empty(max(1, lib.dsgan_pw_fd_workspace(0, M, K, HW, NB)), device=DEV)
-            call("dsgan_pw_fwd_io_ws", ptr(w), 1, ptr(x), K * HW, 1, ptr(y), M * HW, int(y16), ptr(gp),
-                 M * HW if gp is not None else 0, 1 if gp is not None else 0, ptr(bias), M, K, HW, NB,
-                 1 if gp is not None else 0, 0, 0.2, *HF.wsa(ws), stream())
-            return [y] + ([gp] if gp is not None else [])
-        ws = torch.empty(max(1, lib.dsgan_pw_fd_workspace(1, M, K, HW, NB)), device=DEV)
-        call("dsgan_pw_dgrad_io_ws", ptr(w), 1, ptr(x), K * HW, 1, ptr(y), M * HW, int(y16), None, 0, M, K,
-             HW, NB, 0, *HF.wsa(ws), stream())
-        return [y]
-    try:
-        ref = run(0)
-        got = run(1)
-        torch.cuda.synchronize()
-    finally:
-        lib.dsgan_pw_tune(9, old9)
-        lib.dsgan_pw_tune(11, old11)
-    for a, b in zip(got, ref):
-        assert torch.equal(a, b)
-    z = torch.einsum("mk,nkp->nmp", w.float(), x.float()) if fwd else torch.einsum("km,nkp->nmp", w.float(), x.float())
-    if bias is not None:
-        z = z + bias[None, :, None]
-    if form == "fwd_gelu_pair":
-        z = torch.nn.functional.gelu(z)
-    assert rel(got[0].float(), z) < (2e-5 if got[0].dtype == torch.float32 else 1e-2)
-
-
-@pytest.mark.parametrize("half", HALVES)
 @pytest.mark.parametrize("form", ["fwd16", "fwd32", "fwd_gelu_pair", "dgrad32", "dgrad16", "wgrad"])
 @pytest.mark.parametrize("ring", [3, 2])
 def test_pw_wide_dma_ring_bitwise(half, form, ring):
