@@ -1995,9 +1995,31 @@ def _sum4_raw(outs):
 VGG_POOL_L1 = [os.environ.get("DSGAN_VGG_POOL_L1", "1") != "0"]
 
 
+def _record_all(obj, stream):
+    """record_stream(stream) on every tensor in a nest of lists / tuples / dicts."""
+    if torch.is_tensor(obj):
+        obj.record_stream(stream)
+    elif isinstance(obj, (list, tuple)):
+        for o in obj:
+            _record_all(o, stream)
+    elif isinstance(obj, dict):
+        for o in obj.values():
+            _record_all(o, stream)
+
+
 class PerceptualL1Fn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, fake, blocks, real_feats):
+    def forward(ctx, fake, blocks, real_feats, side=None):
+        if side is not None:
+            # the forward's kernels on the side stream (the caller joins it before reading the loss);
+            # the autograd node was created on the current stream, so the backward runs there, and
+            # every tensor it or the caller reads is handed over to that stream
+            main = torch.cuda.current_stream()
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                out = PerceptualL1Fn.forward(ctx, fake, blocks, real_feats)
+            _record_all([out, ctx.saved, getattr(ctx, "feats", None), getattr(ctx, "codes", None)], main)
+            return out
         ctx.box = _box(fake)
         fake, _ = nchw(fake)
         ctx.cb16 = real_feats[0].dim() == 5
@@ -2033,7 +2055,7 @@ class PerceptualL1Fn(torch.autograd.Function):
             with precision(ctx.prec):
                 dx = _perceptual_bwd_cb16(ctx, g.contiguous())
             ctx.saved = ctx.real = ctx.feats = ctx.codes = None
-            return _give(ctx.box, dx), None, None
+            return _give(ctx.box, dx), None, None, None
         with precision(ctx.prec):
             g = g.contiguous()
             d, d_idx = None, None   # grad at the pool output of the block above, and that pool's argmax
@@ -2057,11 +2079,13 @@ class PerceptualL1Fn(torch.autograd.Function):
                         dpre = conv_dgrad_raw(dpre, w, in_shape, 1, 1)
                 d, d_idx = dpre, idx
             ctx.saved = ctx.real = None
-            return _give(ctx.box, d), None, None
+            return _give(ctx.box, d), None, None, None
 
 
-def perceptual_l1(fake, blocks, real_feats):
-    return PerceptualL1Fn.apply(fake, blocks, real_feats)
+def perceptual_l1(fake, blocks, real_feats, side=None):
+    """side (nullable torch.cuda.Stream): run the forward's kernels there -- the caller joins it before
+    reading the loss -- while the backward stays on the current stream."""
+    return PerceptualL1Fn.apply(fake, blocks, real_feats, side)
 
 
 # ------------------------------------------------------------------------------------------

@@ -46,6 +46,13 @@ from . import networks
 # the cause was a NaN in the SSIM backward, not the stacked pass -- losses.hip ssim_fwd_kernel.)
 D_BATCH = os.environ.get("DSGAN_D_BATCH", "1") != "0"
 
+# The G step's perceptual forward (VGG16 over fake_B and its four L1s) depends only on the generator's
+# output, not on the D step: it runs on the VGG side stream while the D step runs on the main stream,
+# and the G step joins the side stream before it reads the loss (DSGAN_VGG_OVERLAP=0: in program
+# order, as the reference's code reads: DSGAN/models/pix2pix_model.py:164-199).  The autograd node is
+# created on the main stream, so its backward (the VGG data-grad chain) stays there.
+VGG_OVERLAP = os.environ.get("DSGAN_VGG_OVERLAP", "1") != "0"
+
 
 class GraphCaptureError(RuntimeError):
     """Under DDP, graph B's capture (the step with its RCCL exchanges) failed: not recoverable by
@@ -152,6 +159,8 @@ class Pix2PixModel(BaseModel):
             self.step_calls = {"G": 0, "D": 0}
             # backward_D's stacked batch-2N D pass (D_BATCH); an attribute so tests can compare the two forms
             self.d_batch = D_BATCH
+            self.vgg_overlap = VGG_OVERLAP
+            self._pre_perc = None
 
     def set_input(self, input):
         AtoB = self.opt.which_direction == "AtoB"
@@ -217,12 +226,18 @@ class Pix2PixModel(BaseModel):
             self.loss_G_GAN = 0
         # the four image losses sum their fake_B grads in one buffer (HF.share: the L1 / TV / SSIM
         # backward kernels accumulate in place) instead of through autograd adds; same order of sums
-        fB = HF.share(self.fake_B)
-        self.loss_G_L1 = self.criterionL1(fB, self.real_B)
-        self.real_B_features = self._take_real_features()
-        # L1(f1,r1) + L1(f2,r2) + L1(f3,r3) + L1(f0,r0) over vgg(fake_B): one fused node whose
-        # backward is the hand-written VGG data-grad chain (vgg.py / functional.PerceptualL1Fn)
-        self.loss_vgg = self.vgg.perceptual_l1(fB, self.real_B_features)
+        pre, self._pre_perc = self._pre_perc, None
+        if pre is not None:   # the perceptual forward already ran on the side stream (VGG_OVERLAP)
+            fB, self.real_B_features, self.loss_vgg = pre
+            self.loss_G_L1 = self.criterionL1(fB, self.real_B)
+            torch.cuda.current_stream(self.device).wait_stream(self._vgg_stream)
+        else:
+            fB = HF.share(self.fake_B)
+            self.loss_G_L1 = self.criterionL1(fB, self.real_B)
+            self.real_B_features = self._take_real_features()
+            # L1(f1,r1) + L1(f2,r2) + L1(f3,r3) + L1(f0,r0) over vgg(fake_B): one fused node whose
+            # backward is the hand-written VGG data-grad chain (vgg.py / functional.PerceptualL1Fn)
+            self.loss_vgg = self.vgg.perceptual_l1(fB, self.real_B_features)
         self.tv_loss = HF.tv_loss(fB, self.tv_scale / (320 * 256))
         # 1 - ssim((real_B+1)/2, (fake_B+1)/2, data_range=1): the affine map is fused in-kernel
         # (--ssim_loss ms_ssim: the 5-level MS-SSIM of DSGAN/MS_SSIM.py:153-225 instead)
@@ -263,6 +278,17 @@ class Pix2PixModel(BaseModel):
         for f in feats:
             f.record_stream(main)
         self._real_feats = feats
+
+    def _launch_fake_perceptual(self):
+        """The G step's perceptual forward on the VGG side stream, ahead of the D step (VGG_OVERLAP):
+        it follows the real-feature pass on that stream, so it needs no join of its own; backward_G
+        joins the stream before reading the loss."""
+        if self._real_feats is None:
+            self._launch_real_features()
+        feats, self._real_feats = self._real_feats, None
+        fB = HF.share(self.fake_B)
+        loss = self.vgg.perceptual_l1(fB, feats, side=self._vgg_stream)
+        self._pre_perc = (fB, feats, loss)
 
     def _take_real_features(self):
         if self._real_feats is None:
@@ -412,6 +438,8 @@ class Pix2PixModel(BaseModel):
         return {"gA": gA, "gB": gB, "lr": lrs, "vars": tvars}
 
     def _d_and_g_steps(self, fake_AB=None):
+        if self.vgg_overlap and self.use_gan == 1:
+            self._launch_fake_perceptual()
         if self.use_gan == 1:
             self.set_requires_grad(self.netD, True)
             self.optimizer_D.zero_grad()

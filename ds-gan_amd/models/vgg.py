@@ -96,8 +96,9 @@ class Vgg16(nn.Module):
             return HF.vgg_features_cb16(x, self.loss_blocks())[0]
         return HF.vgg_features_raw(x, self.loss_blocks())[0]
 
-    def perceptual_l1(self, fake, real_feats):
+    def perceptual_l1(self, fake, real_feats, side=None):
         """L1(f1,r1) + L1(f2,r2) + L1(f3,r3) + L1(f0,r0) of f = self(fake), r = real_feats
-        (DSGAN/models/pix2pix_model.py:180-186) as one fused autograd node."""
-        return HF.perceptual_l1(fake, self.loss_blocks(), list(real_feats))
+        (DSGAN/models/pix2pix_model.py:180-186) as one fused autograd node; side (nullable stream):
+        where its forward's kernels run (functional.perceptual_l1)."""
+        return HF.perceptual_l1(fake, self.loss_blocks(), list(real_feats), side)
 
