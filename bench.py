@@ -153,7 +153,7 @@ def reference_legs(steps=10, batch=16, size=256, threads=None, timed=(2, 7)):
 
 def _profile_json(name):
     """A committed rocprofv3 summary over this same bench command (the newest round that has it)."""
-    for rnd in ("r05", "r04", "r03", "r02", "r01"):
+    for rnd in ("r06", "r05", "r04", "r03", "r02", "r01"):
         path = os.path.join(REPO, "profiles", rnd, name)
         try:
             with open(path) as f:
