@@ -53,6 +53,7 @@ SPLIT_ASYNC = [os.environ.get("DSGAN_SPLIT_ASYNC", "0") != "0"]
 SPLIT_ASYNC_MIN = 20          # one batched launch's worth of segments (split_reduce.hip RS_MAX)
 _SPLIT_SIDE = {}              # device index -> side stream
 _ASYNC_OUT = [None]           # the side stream while reductions launched on it are not yet joined
+_ASYNC_KEEP = []              # what those reductions read or write, held until the join
 
 
 def _split_side():
@@ -70,8 +71,10 @@ def _flush_async():
     rc = lib.dsgan_split_flush_to(side.cuda_stream)
     if rc != 0:
         raise RuntimeError("dsgan_split_flush_to failed (rc=%d): %s" % (rc, lib.dsgan_last_error_string().decode()))
-    for t in _DEFER_KEEP[0] or ():   # the partials are read on the side stream now
-        t.record_stream(side)
+    # the partials (and scratch outputs) are read on the side stream now: held until it is joined --
+    # not handed over with record_stream, which a graph capture's private pool does not honour (a
+    # captured step reused them under the side stream's reads: NaN gradients)
+    _ASYNC_KEEP.extend(_DEFER_KEEP[0] or ())
     _DEFER_KEEP[0] = []
     _ASYNC_OUT[0] = side
 
@@ -80,6 +83,7 @@ def _join_async():
     if _ASYNC_OUT[0] is not None:
         torch.cuda.current_stream().wait_stream(_ASYNC_OUT[0])
         _ASYNC_OUT[0] = None
+    _ASYNC_KEEP.clear()   # freed after the join: any reuse on this stream is ordered after the reads
 
 
 def _defer_hook(queued):
