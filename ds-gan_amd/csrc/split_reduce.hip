@@ -345,18 +345,6 @@ int dsgan_split_pending(void) {
   return (int)g_queue.size();
 }
 
-// Launch every queued reduction on `st` and empty the queue: the caller has ordered `st` after the
-// stream the producers ran on (the host's asynchronous flush: a side stream that waits on the
-// compute stream, so the reductions run beside the rest of the backward pass).
-int dsgan_split_flush_to(hipStream_t st) {
-  std::lock_guard<std::mutex> lk(g_qmu);
-  if (g_queue.empty()) return 0;
-  g_queue_st = st;
-  flush_queue();
-  DSG_CHECK_LAUNCH();
-  return 0;
-}
-
 // Launch every queued reduction on the stream its producers ran on and empty the queue.  When `st`
 // is another stream, it is made to wait for those launches (an event), so whatever `st` runs next
 // sees the reduced gradients.  Returns 0, or an error code (the queue is empty either way: a

@@ -66,7 +66,6 @@ SIGNATURES = {
     "dsgan_split_defer": [I],
     "dsgan_split_pending": [],
     "dsgan_split_flush": [S],
-    "dsgan_split_flush_to": [S],
     "dsgan_f32_to_bf16": [P, P, L, S],
     # pconv.hip
     "dsgan_pconv_supported": [I, I, I, I],

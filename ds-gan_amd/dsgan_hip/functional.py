@@ -45,55 +45,11 @@ _DEFER_KEEP = [None]
 _DEFER_CAND = []
 
 
-# Asynchronous flush: once SPLIT_ASYNC_MIN reductions are queued, they are launched on a side stream
-# that waits on the compute stream, so they run beside the rest of the backward pass instead of as a
-# burst at its end; split_flush() joins the side stream before anything reads a gradient
-# (DSGAN_SPLIT_ASYNC=0: every reduction at the final flush, on the compute stream).
-SPLIT_ASYNC = [os.environ.get("DSGAN_SPLIT_ASYNC", "0") != "0"]
-SPLIT_ASYNC_MIN = 20          # one batched launch's worth of segments (split_reduce.hip RS_MAX)
-_SPLIT_SIDE = {}              # device index -> side stream
-_ASYNC_OUT = [None]           # the side stream while reductions launched on it are not yet joined
-_ASYNC_KEEP = []              # what those reductions read or write, held until the join
-
-
-def _split_side():
-    d = torch.cuda.current_device()
-    st = _SPLIT_SIDE.get(d)
-    if st is None:
-        st = _SPLIT_SIDE[d] = torch.cuda.Stream(d)
-    return st
-
-
-def _flush_async():
-    lib = _lib.load()
-    main, side = torch.cuda.current_stream(), _split_side()
-    side.wait_stream(main)
-    rc = lib.dsgan_split_flush_to(side.cuda_stream)
-    if rc != 0:
-        raise RuntimeError("dsgan_split_flush_to failed (rc=%d): %s" % (rc, lib.dsgan_last_error_string().decode()))
-    # the partials (and scratch outputs) are read on the side stream now: held until it is joined --
-    # not handed over with record_stream, which a graph capture's private pool does not honour (a
-    # captured step reused them under the side stream's reads: NaN gradients)
-    _ASYNC_KEEP.extend(_DEFER_KEEP[0] or ())
-    _DEFER_KEEP[0] = []
-    _ASYNC_OUT[0] = side
-
-
-def _join_async():
-    if _ASYNC_OUT[0] is not None:
-        torch.cuda.current_stream().wait_stream(_ASYNC_OUT[0])
-        _ASYNC_OUT[0] = None
-    _ASYNC_KEEP.clear()   # freed after the join: any reuse on this stream is ordered after the reads
-
-
 def _defer_hook(queued):
-    """_lib.call's report after each entry point: keep that call's candidates if it queued a
-    reduction; launch the queue asynchronously once it holds SPLIT_ASYNC_MIN reductions."""
+    """_lib.call's report after each entry point: keep that call's candidates if it queued a reduction."""
     if queued and _DEFER_KEEP[0] is not None:
         _DEFER_KEEP[0].extend(_DEFER_CAND)
     _DEFER_CAND.clear()
-    if queued and SPLIT_ASYNC[0] and _DEFER_KEEP[0] is not None and _lib.load().dsgan_split_pending() >= SPLIT_ASYNC_MIN:
-        _flush_async()
 
 
 def _keep(t):
@@ -103,10 +59,8 @@ def _keep(t):
 
 
 def split_flush():
-    """Launch the queued split reductions (no-op when none are queued) and join the asynchronous
-    ones: every reduced gradient is ordered before what the current stream runs next."""
+    """Launch the queued split reductions (no-op when none are queued)."""
     lib = _lib.load()
-    _join_async()   # first: a queued reduction may add into an output one in flight also adds into
     if lib.dsgan_split_pending() > 0:
         call("dsgan_split_flush", stream())
     if _DEFER_KEEP[0] is not None:

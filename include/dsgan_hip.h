@@ -201,9 +201,6 @@ int dsgan_colsum(float* part, int rows, int cols, float* out, hipStream_t stream
 int dsgan_split_defer(int on);        /* returns the previous setting; turning off does not flush */
 int dsgan_split_pending(void);        /* reductions queued */
 int dsgan_split_flush(hipStream_t stream);  /* on the producers' stream; `stream` waits for them */
-/* launch the queue on `stream`, which the caller has ordered after the producers' stream (the
- * asynchronous flush: reductions on a side stream beside the rest of the backward pass) */
-int dsgan_split_flush_to(hipStream_t stream);
 /* dst (bf16) = src (fp32), round to nearest even */
 int dsgan_f32_to_bf16(const float* src, void* dst, long n, hipStream_t stream);
 
