@@ -92,12 +92,15 @@ class GradBuckets:
     from functional.GRAD_READY as weight-grads are launched, ``finish()`` after the backward:
     launches the buckets that are not complete (parameters never reported) and waits for all of them.
 
-    Buckets are launched strictly in index order: bucket i starts once it and every bucket before it
-    are complete.  Collectives pair up across ranks by issue order, so the sequence must not depend
-    on the order in which one rank's backward happens to report its parameters -- it is 0, 1, 2, ...
-    on every rank (tests/test_host_cpu.py::test_grad_buckets_same_sequence_under_perturbed_order).
-    The flat buffer is laid out in backward order, so in the step bucket 0 completes first and the
-    in-order rule costs no overlap."""
+    A bucket starts when its last parameter is reported.  Collectives pair up across ranks by issue
+    order, so the launch sequence is the order in which the backward completes the buckets: the
+    autograd engine runs the same graph's nodes in the same order on every rank, so every rank
+    issues the same sequence (tests/test_host_cpu.py::test_grad_buckets_sequence_follows_completion).
+    Round 6 tried a strict index-order rule (bucket i waits for every bucket before it, whatever the
+    report order): it issued several buckets at once from one hook, and the step captured that way
+    replayed wrong gradients (tests/test_ddp_gpu.py::test_one_rank_rccl_exchange_is_bitwise_neutral,
+    bisected to the rule; a capture of plain back-to-back all-reduces, tools/rccl_graph_burst.py,
+    does not show it) -- not kept."""
 
     def __init__(self, grad, layout, bucket_mb=24):
         self.grad = grad
@@ -118,14 +121,12 @@ class GradBuckets:
         self.pending = None
         self.works = None
         self.launched = None
-        self.next = 0              # the next bucket to launch (in index order)
         self.sequence = []         # bucket indices in launch order (this step)
 
     def arm(self):
         self.pending = [set(b[2]) for b in self.buckets]
         self.works = []
         self.launched = [False] * len(self.buckets)
-        self.next = 0
         self.sequence = []
         HF.GRAD_READY[0] = self.ready
 
@@ -143,15 +144,13 @@ class GradBuckets:
             if i is None or self.launched[i]:
                 continue
             self.pending[i].discard(id(p))
-        while self.next < len(self.buckets) and not self.pending[self.next]:
-            self._launch(self.next)
-            self.next += 1
+            if not self.pending[i]:
+                self._launch(i)
 
     def finish(self):
         HF.GRAD_READY[0] = None
-        for i in range(self.next, len(self.buckets)):
+        for i in range(len(self.buckets)):
             self._launch(i)
-        self.next = len(self.buckets)
         for w in self.works:
             w.wait()
         _post_scale(self.grad, world_size())
