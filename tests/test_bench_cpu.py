@@ -3,6 +3,8 @@ divides by the steps the timer actually recorded, not by --steps (VERDICT r04 we
 import os
 import sys
 
+import pytest
+
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 import bench  # noqa: E402
@@ -90,16 +92,18 @@ def test_rocprof_family_average(tmp_path):
     assert calls == 40 and abs(avg - 59.5) < 1e-6
 
 
-def test_committed_bench_line_agrees_with_its_rocprof_summary():
+@pytest.mark.parametrize("tag", ["a", "final"])
+def test_committed_bench_line_agrees_with_its_rocprof_summary(tag):
     """the committed round-6 bench line's avg_launch_us for the dominant family
     (kernel-only events) is within 5 % of the average of the same family in the committed rocprofv3
-    summary of the bench command on the same tree (profiles/r06: bench_a.log with rocprof_stats_a.csv)."""
+    summary of the bench command on the same tree (profiles/r06: bench_<tag>.log with rocprof_stats_<tag>.csv;
+    "final" = the round's last tree)."""
     import json
     d = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles", "r06")
-    with open(os.path.join(d, "bench_a.log")) as f:
+    with open(os.path.join(d, "bench_%s.log" % tag)) as f:
         line = json.loads([x for x in f if x.startswith("{")][-1])
     r = line["roofline"]
     assert r["avg_launch_timing"].startswith("kernel-only")
-    avg, calls = bench.rocprof_family_avg_us(os.path.join(d, "rocprof_stats_a.csv"), r["kernel"])
+    avg, calls = bench.rocprof_family_avg_us(os.path.join(d, "rocprof_stats_%s.csv" % tag), r["kernel"])
     assert calls > 0
     assert abs(r["avg_launch_us"] - avg) <= 0.05 * avg, (r["avg_launch_us"], avg)
