@@ -97,10 +97,10 @@ class GradBuckets:
     autograd engine runs the same graph's nodes in the same order on every rank, so every rank
     issues the same sequence (tests/test_host_cpu.py::test_grad_buckets_sequence_follows_completion).
     Round 6 tried a strict index-order rule (bucket i waits for every bucket before it, whatever the
-    report order): it issued several buckets at once from one hook, and the step captured that way
-    replayed wrong gradients (tests/test_ddp_gpu.py::test_one_rank_rccl_exchange_is_bitwise_neutral,
-    bisected to the rule; a capture of plain back-to-back all-reduces, tools/rccl_graph_burst.py,
-    does not show it) -- not kept."""
+    report order): it launched some buckets from a later hook than the one that completed them, and
+    the step captured that way replayed wrong gradients (bisected to the rule on
+    tests/test_ddp_gpu.py::test_one_rank_rccl_exchange_is_bitwise_neutral; a capture of plain
+    back-to-back all-reduces, tools/rccl_graph_burst.py, does not show it) -- not kept."""
 
     def __init__(self, grad, layout, bucket_mb=24):
         self.grad = grad

@@ -1,8 +1,9 @@
 """Captured RCCL all-reduces back to back vs interleaved with compute (1-rank "nccl" group).
 
 Round-6 bisection of tests/test_ddp_gpu.py::test_one_rank_rccl_exchange_is_bitwise_neutral: the
-G-bucket all-reduces issued several at a time from one autograd hook (in-order launch) replayed
-wrong values from the HIP graph; issued one per hook (completion order) they did not.  This tool
+G-bucket all-reduces launched in strict index order (some from a later hook than the one that
+completed them, several per hook) replayed wrong values from the HIP graph; launched at completion
+they did not (that order also issues several per hook, so the burst alone is not it).  This tool
 captures K async in-place AVG all-reduces of disjoint slices of one buffer -- a 1-rank AVG is the
 identity -- issued (a) back to back, (b) with a small kernel on the capture stream between them,
 from the capturing thread or from a second thread (the autograd engine's), replays the graph a few
